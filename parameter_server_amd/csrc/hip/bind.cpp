@@ -1,0 +1,463 @@
+// Python bindings (torch tensors in, kernels on the current HIP stream).
+// Every op validates device / dtype / contiguity and sizes on the host BEFORE
+// launching, so a malformed call raises instead of faulting the GPU.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "common.cuh"
+
+namespace psamd {
+// kv_table.hip
+void kv_init(void*, int64_t, hipStream_t);
+void kv_resolve(void*, int64_t, const uint64_t*, int64_t, const int32_t*, int64_t*, float*, bool,
+                int, float, float, uint64_t, int32_t*, int32_t*, hipStream_t);
+void kv_gather(const void*, const int64_t*, int64_t, const int32_t*, float*, int, hipStream_t);
+void kv_set(void*, const int64_t*, int64_t, const float*, const float*, const float*, hipStream_t);
+void kv_update(void*, const int64_t*, const float*, int64_t, const int32_t*, int, int, float, float,
+               float, float, float, float, double*, hipStream_t);
+void kv_accumulate(void*, const int64_t*, const float*, int64_t, const int32_t*, int64_t*, int32_t*,
+                   hipStream_t);
+void kv_apply_accumulated(void*, const int64_t*, const int32_t*, int64_t, int, int, float, float,
+                          float, float, float, float, double*, hipStream_t);
+void kv_census(const void*, int64_t, unsigned long long*, hipStream_t);
+// localize.hip
+void mix_iota(const uint64_t*, int64_t, KeyMix, uint64_t*, int32_t*, hipStream_t);
+void mix_keys(const uint64_t*, int64_t, KeyMix, uint64_t*, bool, hipStream_t);
+size_t sort_pairs_temp_bytes(int64_t, int);
+void sort_pairs(void*, size_t, const uint64_t*, uint64_t*, const int32_t*, int32_t*, int64_t, int,
+                hipStream_t);
+size_t scan_temp_bytes(int64_t);
+void inclusive_scan_i32(void*, size_t, const int32_t*, int32_t*, int64_t, hipStream_t);
+void rle(const uint64_t*, const int32_t*, int64_t, int32_t*, int32_t*, void*, size_t, uint64_t*,
+         int32_t*, int32_t*, int32_t*, float*, float*, hipStream_t);
+void seg_counts(const int32_t*, const int32_t*, int64_t, uint8_t*, int, hipStream_t);
+void owner_split(const uint64_t*, const int32_t*, int64_t, const uint64_t*, int, int64_t*,
+                 hipStream_t);
+void owner_of(const uint64_t*, int64_t, const uint64_t*, int, int32_t*, hipStream_t);
+// linear.hip
+void linear_fwd(const int64_t*, int64_t, int, const int32_t*, const float*, const float*,
+                const float*, int, float*, float*, float*, double*, uint32_t*, int, hipStream_t);
+void linear_bwd(const int32_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
+                const float*, const float*, float*, float*, hipStream_t);
+void auc_from_hist(uint32_t*, int, double*, hipStream_t);
+void csr_rows(const int64_t*, int64_t, int32_t*, hipStream_t);
+void criteo_set_cards(const uint32_t*);
+void criteo_gen(uint64_t, int64_t, const int64_t*, int64_t, uint64_t, float, uint64_t*, float*,
+                hipStream_t);
+void add_i64(int64_t*, int64_t, hipStream_t);
+// filters.hip
+void cm_insert(uint32_t*, uint64_t, int, uint32_t, const uint64_t*, const uint8_t*, int64_t,
+               const int32_t*, hipStream_t);
+void cm_query(const uint32_t*, uint64_t, int, uint32_t, const uint64_t*, int64_t, const int32_t*,
+              int, int32_t*, uint8_t*, hipStream_t);
+void compact_kept(const int32_t*, const int32_t*, int64_t, const int32_t*, int32_t*, int32_t*,
+                  int32_t*, hipStream_t);
+void ff_minmax(const float*, int64_t, float*, hipStream_t);
+void ff_encode(const float*, int64_t, const float*, int, uint64_t, uint8_t*, hipStream_t);
+void ff_decode(const uint8_t*, int64_t, const float*, int, float*, hipStream_t);
+void key_signature(const uint64_t*, int64_t, unsigned long long*, hipStream_t);
+}  // namespace psamd
+
+using at::Tensor;
+using c10::optional;
+namespace py = pybind11;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(bool ok, const std::string& msg) {
+  if (!ok) throw std::invalid_argument(msg);
+}
+
+void chk(const Tensor& t, at::ScalarType dt, const char* name) {
+  check(t.is_cuda(), std::string(name) + ": must be a GPU tensor");
+  check(t.is_contiguous(), std::string(name) + ": must be contiguous");
+  check(t.scalar_type() == dt, std::string(name) + ": wrong dtype " +
+                                   std::string(c10::toString(t.scalar_type())));
+}
+
+template <typename T>
+T* ptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+
+template <typename T>
+T* optr(const optional<Tensor>& t, at::ScalarType dt, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  chk(*t, dt, name);
+  return reinterpret_cast<T*>(t->data_ptr());
+}
+
+uint64_t inv_mod64(uint64_t a) {  // a odd; Newton iteration for a^-1 mod 2^64
+  uint64_t x = a;
+  for (int i = 0; i < 6; ++i) x *= 2 - a * x;
+  return x;
+}
+
+psamd::KeyMix make_keymix(int bits) {
+  check(bits >= 2 && bits <= 64, "key bits must be in [2, 64]");
+  psamd::KeyMix m;
+  m.bits = bits;
+  m.mask = bits == 64 ? ~0ull : ((1ull << bits) - 1);
+  m.a = 0xbf58476d1ce4e5b9ull & m.mask;
+  m.b = 0x94d049bb133111ebull & m.mask;
+  m.a |= 1;
+  m.b |= 1;
+  m.ai = inv_mod64(m.a) & m.mask;
+  m.bi = inv_mod64(m.b) & m.mask;
+  m.s = (bits + 1) / 2;
+  return m;
+}
+
+int64_t slot_capacity(const Tensor& slots) {
+  chk(slots, at::kLong, "slots");
+  check(slots.dim() == 2 && slots.size(1) == 4, "slots must be [capacity, 4] int64 (32-B slots)");
+  const int64_t cap = slots.size(0);
+  check(cap > 0 && (cap & (cap - 1)) == 0, "slot capacity must be a power of two");
+  return cap;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hipops, m) {
+  m.doc() = "parameter_server_amd HIP kernels (gfx950)";
+
+  m.def("keymix_params", [](int bits) {
+    auto k = make_keymix(bits);
+    return py::make_tuple(k.mask, k.a, k.b, k.ai, k.bi, k.s, k.bits);
+  });
+
+  // ---------------- KV table ----------------
+  m.def("kv_init", [](Tensor slots) {
+    psamd::kv_init(slots.data_ptr(), slot_capacity(slots), cur_stream());
+  });
+  m.def("kv_resolve", [](Tensor slots, Tensor keys, optional<Tensor> n_dev, Tensor out_slot,
+                         optional<Tensor> out_w, bool insert, int init_type, double init_v,
+                         double init_s, uint64_t seed, optional<Tensor> err,
+                         optional<Tensor> inserted) {
+    const int64_t cap = slot_capacity(slots);
+    chk(keys, at::kLong, "keys");
+    chk(out_slot, at::kLong, "out_slot");
+    const int64_t n = keys.numel();
+    check(out_slot.numel() >= n, "out_slot too small");
+    float* w = optr<float>(out_w, at::kFloat, "out_w");
+    if (w) check(out_w->numel() >= n, "out_w too small");
+    psamd::kv_resolve(slots.data_ptr(), cap, ptr<uint64_t>(keys), n,
+                      optr<int32_t>(n_dev, at::kInt, "n_dev"), ptr<int64_t>(out_slot), w, insert,
+                      init_type, (float)init_v, (float)init_s, seed,
+                      optr<int32_t>(err, at::kInt, "err"),
+                      optr<int32_t>(inserted, at::kInt, "inserted"), cur_stream());
+  });
+  m.def("kv_gather", [](Tensor slots, Tensor slot_idx, optional<Tensor> n_dev, Tensor out,
+                        int field) {
+    slot_capacity(slots);
+    chk(slot_idx, at::kLong, "slot_idx");
+    chk(out, at::kFloat, "out");
+    check(field >= 0 && field < 4, "field in [0,4): w,z,n,acc");
+    check(out.numel() >= slot_idx.numel(), "out too small");
+    psamd::kv_gather(slots.data_ptr(), ptr<int64_t>(slot_idx), slot_idx.numel(),
+                     optr<int32_t>(n_dev, at::kInt, "n_dev"), ptr<float>(out), field,
+                     cur_stream());
+  });
+  m.def("kv_set", [](Tensor slots, Tensor slot_idx, optional<Tensor> w, optional<Tensor> z,
+                     optional<Tensor> nn) {
+    slot_capacity(slots);
+    chk(slot_idx, at::kLong, "slot_idx");
+    const int64_t n = slot_idx.numel();
+    for (auto* t : {&w, &z, &nn})
+      if (t->has_value()) check((*t)->numel() >= n, "value array too small");
+    psamd::kv_set(slots.data_ptr(), ptr<int64_t>(slot_idx), n, optr<float>(w, at::kFloat, "w"),
+                  optr<float>(z, at::kFloat, "z"), optr<float>(nn, at::kFloat, "n"),
+                  cur_stream());
+  });
+  m.def("kv_update", [](Tensor slots, Tensor slot_idx, Tensor grad, optional<Tensor> n_dev,
+                        int algo, int lr_type, double alpha, double beta, double l1, double l2,
+                        double grad_scale, double max_delta, optional<Tensor> stats) {
+    slot_capacity(slots);
+    chk(slot_idx, at::kLong, "slot_idx");
+    chk(grad, at::kFloat, "grad");
+    check(grad.numel() >= slot_idx.numel(), "grad too small");
+    check(alpha > 0, "learning rate alpha must be > 0");
+    psamd::kv_update(slots.data_ptr(), ptr<int64_t>(slot_idx), ptr<float>(grad),
+                     slot_idx.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"), algo, lr_type,
+                     (float)alpha, (float)beta, (float)l1, (float)l2, (float)grad_scale,
+                     (float)max_delta, optr<double>(stats, at::kDouble, "stats"), cur_stream());
+  });
+  m.def("kv_accumulate", [](Tensor slots, Tensor slot_idx, Tensor grad, optional<Tensor> n_dev,
+                            Tensor touched, Tensor n_touched) {
+    const int64_t cap = slot_capacity(slots);
+    chk(slot_idx, at::kLong, "slot_idx");
+    chk(grad, at::kFloat, "grad");
+    chk(touched, at::kLong, "touched");
+    chk(n_touched, at::kInt, "n_touched");
+    check(touched.numel() >= std::min<int64_t>(cap, slot_idx.numel()) || touched.numel() >= cap,
+          "touched buffer too small");
+    psamd::kv_accumulate(slots.data_ptr(), ptr<int64_t>(slot_idx), ptr<float>(grad),
+                         slot_idx.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"),
+                         ptr<int64_t>(touched), ptr<int32_t>(n_touched), cur_stream());
+  });
+  m.def("kv_apply_accumulated", [](Tensor slots, Tensor touched, Tensor n_touched, int algo,
+                                   int lr_type, double alpha, double beta, double l1, double l2,
+                                   double grad_scale, double max_delta, optional<Tensor> stats) {
+    slot_capacity(slots);
+    chk(touched, at::kLong, "touched");
+    chk(n_touched, at::kInt, "n_touched");
+    psamd::kv_apply_accumulated(slots.data_ptr(), ptr<int64_t>(touched), ptr<int32_t>(n_touched),
+                                touched.numel(), algo, lr_type, (float)alpha, (float)beta,
+                                (float)l1, (float)l2, (float)grad_scale, (float)max_delta,
+                                optr<double>(stats, at::kDouble, "stats"), cur_stream());
+  });
+  m.def("kv_census", [](Tensor slots) {
+    const int64_t cap = slot_capacity(slots);
+    auto out = torch::zeros({2}, slots.options().dtype(at::kLong));
+    psamd::kv_census(slots.data_ptr(), cap, ptr<unsigned long long>(out), cur_stream());
+    return out;
+  });
+
+  // ---------------- localisation ----------------
+  m.def("mix_iota", [](Tensor keys, int bits, Tensor h, Tensor pos) {
+    chk(keys, at::kLong, "keys");
+    chk(h, at::kLong, "h");
+    chk(pos, at::kInt, "pos");
+    const int64_t n = keys.numel();
+    check(h.numel() >= n && pos.numel() >= n, "outputs too small");
+    psamd::mix_iota(ptr<uint64_t>(keys), n, make_keymix(bits), ptr<uint64_t>(h), ptr<int32_t>(pos),
+                    cur_stream());
+  });
+  m.def("mix_keys", [](Tensor keys, int bits, Tensor out, bool inverse) {
+    chk(keys, at::kLong, "keys");
+    chk(out, at::kLong, "out");
+    check(out.numel() >= keys.numel(), "out too small");
+    psamd::mix_keys(ptr<uint64_t>(keys), keys.numel(), make_keymix(bits), ptr<uint64_t>(out),
+                    inverse, cur_stream());
+  });
+  m.def("sort_pairs_temp_bytes", [](int64_t n, int end_bit) {
+    return (int64_t)psamd::sort_pairs_temp_bytes(n, end_bit);
+  });
+  m.def("sort_pairs", [](Tensor temp, Tensor k_in, Tensor k_out, Tensor v_in, Tensor v_out,
+                         int64_t n, int end_bit) {
+    chk(temp, at::kByte, "temp");
+    chk(k_in, at::kLong, "k_in");
+    chk(k_out, at::kLong, "k_out");
+    chk(v_in, at::kInt, "v_in");
+    chk(v_out, at::kInt, "v_out");
+    check(n >= 0 && k_in.numel() >= n && k_out.numel() >= n && v_in.numel() >= n &&
+              v_out.numel() >= n, "sort buffers too small");
+    check(n < (int64_t)INT32_MAX, "sort size must fit int32");
+    check(end_bit >= 1 && end_bit <= 64, "end_bit in [1,64]");
+    const size_t need = psamd::sort_pairs_temp_bytes(n, end_bit);
+    check((size_t)temp.numel() >= need, "sort temp storage too small");
+    psamd::sort_pairs(temp.data_ptr(), (size_t)temp.numel(), ptr<uint64_t>(k_in),
+                      ptr<uint64_t>(k_out), ptr<int32_t>(v_in), ptr<int32_t>(v_out), n, end_bit,
+                      cur_stream());
+  });
+  m.def("scan_temp_bytes", [](int64_t n) { return (int64_t)psamd::scan_temp_bytes(n); });
+  m.def("inclusive_scan_i32", [](Tensor temp, Tensor in, Tensor out, int64_t n) {
+    chk(temp, at::kByte, "temp");
+    chk(in, at::kInt, "in");
+    chk(out, at::kInt, "out");
+    check(in.numel() >= n && out.numel() >= n, "scan buffers too small");
+    check((size_t)temp.numel() >= psamd::scan_temp_bytes(n), "scan temp too small");
+    psamd::inclusive_scan_i32(temp.data_ptr(), (size_t)temp.numel(), ptr<int32_t>(in),
+                              ptr<int32_t>(out), n, cur_stream());
+  });
+  m.def("rle", [](Tensor hs, Tensor pos_s, int64_t n, Tensor flags, Tensor segid, Tensor scan_temp,
+                  Tensor uniq, Tensor seg_start, Tensor local_col, Tensor n_uniq,
+                  optional<Tensor> zero_a, optional<Tensor> zero_b) {
+    chk(hs, at::kLong, "hs");
+    chk(pos_s, at::kInt, "pos_s");
+    chk(flags, at::kInt, "flags");
+    chk(segid, at::kInt, "segid");
+    chk(scan_temp, at::kByte, "scan_temp");
+    chk(uniq, at::kLong, "uniq");
+    chk(seg_start, at::kInt, "seg_start");
+    chk(local_col, at::kInt, "local_col");
+    chk(n_uniq, at::kInt, "n_uniq");
+    check(n >= 1, "rle needs n >= 1");
+    check(hs.numel() >= n && pos_s.numel() >= n && flags.numel() >= n && segid.numel() >= n &&
+              uniq.numel() >= n && seg_start.numel() >= n + 1 && local_col.numel() >= n,
+          "rle buffers too small");
+    float* za = optr<float>(zero_a, at::kFloat, "zero_a");
+    float* zb = optr<float>(zero_b, at::kFloat, "zero_b");
+    if (za) check(zero_a->numel() >= n, "zero_a too small");
+    if (zb) check(zero_b->numel() >= n, "zero_b too small");
+    check((size_t)scan_temp.numel() >= psamd::scan_temp_bytes(n), "scan temp too small");
+    psamd::rle(ptr<uint64_t>(hs), ptr<int32_t>(pos_s), n, ptr<int32_t>(flags), ptr<int32_t>(segid),
+               scan_temp.data_ptr(), (size_t)scan_temp.numel(), ptr<uint64_t>(uniq),
+               ptr<int32_t>(seg_start), ptr<int32_t>(local_col), ptr<int32_t>(n_uniq), za, zb,
+               cur_stream());
+  });
+  m.def("seg_counts", [](Tensor seg_start, Tensor n_uniq, Tensor counts, int sat) {
+    chk(seg_start, at::kInt, "seg_start");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(counts, at::kByte, "counts");
+    check(seg_start.numel() >= counts.numel() + 1, "seg_start too small");
+    psamd::seg_counts(ptr<int32_t>(seg_start), ptr<int32_t>(n_uniq), counts.numel(),
+                      ptr<uint8_t>(counts), sat, cur_stream());
+  });
+  m.def("owner_split", [](Tensor uniq, optional<Tensor> n_uniq, Tensor bounds, Tensor offsets) {
+    chk(uniq, at::kLong, "uniq");
+    chk(bounds, at::kLong, "bounds");
+    chk(offsets, at::kLong, "offsets");
+    const int G = (int)bounds.numel() - 1;
+    check(G >= 1 && offsets.numel() >= G + 1, "bounds/offsets size mismatch");
+    psamd::owner_split(ptr<uint64_t>(uniq), optr<int32_t>(n_uniq, at::kInt, "n_uniq"),
+                       uniq.numel(), ptr<uint64_t>(bounds), G, ptr<int64_t>(offsets),
+                       cur_stream());
+  });
+  m.def("owner_of", [](Tensor h, Tensor bounds, Tensor owner) {
+    chk(h, at::kLong, "h");
+    chk(bounds, at::kLong, "bounds");
+    chk(owner, at::kInt, "owner");
+    const int G = (int)bounds.numel() - 1;
+    check(G >= 1 && owner.numel() >= h.numel(), "owner_of sizes");
+    psamd::owner_of(ptr<uint64_t>(h), h.numel(), ptr<uint64_t>(bounds), G, ptr<int32_t>(owner),
+                    cur_stream());
+  });
+
+  // ---------------- linear model ----------------
+  m.def("linear_fwd", [](optional<Tensor> row_ptr, int64_t B, int width, Tensor local_col,
+                         optional<Tensor> vals, Tensor w_local, Tensor labels, int loss_type,
+                         optional<Tensor> xw, Tensor coef, optional<Tensor> coef2,
+                         optional<Tensor> metrics, optional<Tensor> hist, int nbins) {
+    chk(local_col, at::kInt, "local_col");
+    chk(w_local, at::kFloat, "w_local");
+    chk(labels, at::kFloat, "labels");
+    chk(coef, at::kFloat, "coef");
+    check(labels.numel() >= B && coef.numel() >= B, "labels/coef too small");
+    const int64_t* rp = optr<int64_t>(row_ptr, at::kLong, "row_ptr");
+    if (rp) check(row_ptr->numel() >= B + 1, "row_ptr too small");
+    else check(width > 0 && local_col.numel() >= B * width, "fixed width layout too small");
+    const float* v = optr<float>(vals, at::kFloat, "vals");
+    if (v) check(vals->numel() >= local_col.numel(), "vals too small");
+    uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
+    if (hp) check(nbins > 0 && nbins <= 8192 && hist->numel() >= 2 * nbins, "hist size");
+    float* xp = optr<float>(xw, at::kFloat, "xw");
+    if (xp) check(xw->numel() >= B, "xw too small");
+    float* c2 = optr<float>(coef2, at::kFloat, "coef2");
+    if (c2) check(coef2->numel() >= B, "coef2 too small");
+    double* mp = optr<double>(metrics, at::kDouble, "metrics");
+    if (mp) check(metrics->numel() >= 5, "metrics needs >= 5 slots");
+    psamd::linear_fwd(rp, B, width, ptr<int32_t>(local_col), v, ptr<float>(w_local),
+                      ptr<float>(labels), loss_type, xp, ptr<float>(coef), c2, mp, hp, nbins,
+                      cur_stream());
+  });
+  m.def("linear_bwd", [](Tensor pos_s, Tensor segid, int64_t n, optional<Tensor> rows, int width,
+                         optional<Tensor> vals, Tensor coef, optional<Tensor> coef2, Tensor grad,
+                         optional<Tensor> hess) {
+    chk(pos_s, at::kInt, "pos_s");
+    chk(segid, at::kInt, "segid");
+    chk(coef, at::kFloat, "coef");
+    chk(grad, at::kFloat, "grad");
+    check(pos_s.numel() >= n && segid.numel() >= n, "bwd inputs too small");
+    const int32_t* r = optr<int32_t>(rows, at::kInt, "rows");
+    if (r) check(rows->numel() >= n, "rows too small");
+    else check(width > 0, "need rows or a fixed width");
+    float* h = optr<float>(hess, at::kFloat, "hess");
+    const float* c2 = optr<float>(coef2, at::kFloat, "coef2");
+    check(!h || c2, "hess requires coef2");
+    psamd::linear_bwd(ptr<int32_t>(pos_s), ptr<int32_t>(segid), n, r, width,
+                      optr<float>(vals, at::kFloat, "vals"), ptr<float>(coef), c2,
+                      ptr<float>(grad), h, cur_stream());
+  });
+  m.def("auc_from_hist", [](Tensor hist, int nbins, Tensor metrics) {
+    chk(hist, at::kInt, "hist");
+    chk(metrics, at::kDouble, "metrics");
+    check(hist.numel() >= 2 * nbins && metrics.numel() >= 5, "auc sizes");
+    psamd::auc_from_hist(ptr<uint32_t>(hist), nbins, ptr<double>(metrics), cur_stream());
+  });
+  m.def("csr_rows", [](Tensor row_ptr, Tensor rows) {
+    chk(row_ptr, at::kLong, "row_ptr");
+    chk(rows, at::kInt, "rows");
+    psamd::csr_rows(ptr<int64_t>(row_ptr), row_ptr.numel() - 1, ptr<int32_t>(rows),
+                    cur_stream());
+  });
+  m.def("criteo_set_cards", [](std::vector<uint32_t> cards) {
+    check(cards.size() == 26, "need 26 cardinalities");
+    psamd::criteo_set_cards(cards.data());
+  });
+  m.def("add_i64", [](Tensor p, int64_t v) {
+    chk(p, at::kLong, "p");
+    psamd::add_i64(ptr<int64_t>(p), v, cur_stream());
+  });
+  m.def("criteo_gen", [](uint64_t seed, int64_t row0, int64_t B, uint64_t num_features,
+                         double alpha, Tensor keys, Tensor labels, optional<Tensor> row0_dev) {
+    chk(keys, at::kLong, "keys");
+    chk(labels, at::kFloat, "labels");
+    check(keys.numel() >= B * 39 && labels.numel() >= B, "criteo_gen buffers too small");
+    check(alpha > 1.0, "power-law alpha must be > 1");
+    psamd::criteo_gen(seed, row0, optr<int64_t>(row0_dev, at::kLong, "row0_dev"), B,
+                      num_features, (float)alpha, ptr<uint64_t>(keys), ptr<float>(labels),
+                      cur_stream());
+  });
+
+  // ---------------- filters ----------------
+  m.def("cm_insert", [](Tensor table, int k, int vmax, Tensor keys, optional<Tensor> counts,
+                        optional<Tensor> n_dev) {
+    chk(table, at::kInt, "table");
+    chk(keys, at::kLong, "keys");
+    check(k >= 1 && k <= 30 && vmax >= 1 && vmax <= 255, "countmin k/vmax");
+    const uint8_t* c = optr<uint8_t>(counts, at::kByte, "counts");
+    if (c) check(counts->numel() >= keys.numel(), "counts too small");
+    psamd::cm_insert(ptr<uint32_t>(table), (uint64_t)table.numel() * 4, k, (uint32_t)vmax,
+                     ptr<uint64_t>(keys), c, keys.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"),
+                     cur_stream());
+  });
+  m.def("cm_query", [](Tensor table, int k, int vmax, Tensor keys, optional<Tensor> n_dev,
+                       int freq, optional<Tensor> keep, optional<Tensor> out_count) {
+    chk(table, at::kInt, "table");
+    chk(keys, at::kLong, "keys");
+    int32_t* kp = optr<int32_t>(keep, at::kInt, "keep");
+    uint8_t* cp = optr<uint8_t>(out_count, at::kByte, "out_count");
+    if (kp) check(keep->numel() >= keys.numel(), "keep too small");
+    if (cp) check(out_count->numel() >= keys.numel(), "out_count too small");
+    psamd::cm_query(ptr<uint32_t>(table), (uint64_t)table.numel() * 4, k, (uint32_t)vmax,
+                    ptr<uint64_t>(keys), keys.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"),
+                    freq, kp, cp, cur_stream());
+  });
+  m.def("compact_kept", [](Tensor keep, Tensor incl, optional<Tensor> n_dev, Tensor kept_idx,
+                           Tensor n_kept, optional<Tensor> remap) {
+    chk(keep, at::kInt, "keep");
+    chk(incl, at::kInt, "incl");
+    chk(kept_idx, at::kInt, "kept_idx");
+    chk(n_kept, at::kInt, "n_kept");
+    check(kept_idx.numel() >= keep.numel() && incl.numel() >= keep.numel(), "compact sizes");
+    psamd::compact_kept(ptr<int32_t>(keep), ptr<int32_t>(incl), keep.numel(),
+                        optr<int32_t>(n_dev, at::kInt, "n_dev"), ptr<int32_t>(kept_idx),
+                        ptr<int32_t>(n_kept), optr<int32_t>(remap, at::kInt, "remap"),
+                        cur_stream());
+  });
+  m.def("ff_minmax", [](Tensor x, Tensor mm) {
+    chk(x, at::kFloat, "x");
+    chk(mm, at::kFloat, "mm");
+    check(mm.numel() >= 2, "mm needs 2 floats");
+    psamd::ff_minmax(ptr<float>(x), x.numel(), ptr<float>(mm), cur_stream());
+  });
+  m.def("ff_encode", [](Tensor x, Tensor mm, int nbytes, uint64_t seed, Tensor out) {
+    chk(x, at::kFloat, "x");
+    chk(mm, at::kFloat, "mm");
+    chk(out, at::kByte, "out");
+    check(nbytes >= 1 && nbytes <= 7, "nbytes in [1,7]");
+    check(out.numel() >= x.numel() * nbytes, "out too small");
+    psamd::ff_encode(ptr<float>(x), x.numel(), ptr<float>(mm), nbytes, seed, ptr<uint8_t>(out),
+                     cur_stream());
+  });
+  m.def("ff_decode", [](Tensor code, Tensor mm, int nbytes, Tensor out) {
+    chk(code, at::kByte, "code");
+    chk(mm, at::kFloat, "mm");
+    chk(out, at::kFloat, "out");
+    check(nbytes >= 1 && nbytes <= 7, "nbytes in [1,7]");
+    check(code.numel() >= out.numel() * nbytes, "code too small");
+    psamd::ff_decode(ptr<uint8_t>(code), out.numel(), ptr<float>(mm), nbytes, ptr<float>(out),
+                     cur_stream());
+  });
+  m.def("key_signature", [](Tensor keys, Tensor sig) {
+    chk(keys, at::kLong, "keys");
+    chk(sig, at::kLong, "sig");
+    psamd::key_signature(ptr<uint64_t>(keys), keys.numel(), ptr<unsigned long long>(sig),
+                         cur_stream());
+  });
+}

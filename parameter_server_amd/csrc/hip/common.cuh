@@ -1,0 +1,136 @@
+// Shared device helpers for the parameter-server HIP kernels (gfx950 / CDNA4).
+//
+// Design notes (MI355X-first):
+//  * wave64 everywhere: block sizes are multiples of 64, cross-lane reductions
+//    use 64-lane shuffles, ballots are 64-bit.
+//  * all sparse kernels are HBM/latency bound; they use grid-stride loops with
+//    grids capped at ~8 blocks per CU (256 CUs) and read their valid length from
+//    a device counter when the host does not know it (graph-capturable steps).
+//  * keys are 64-bit; the "mixed" key space is a bijection of the raw key space
+//    so that deduplication on mixed keys == deduplication on raw keys, and range
+//    partitioning on mixed keys balances shards even for small integer ids
+//    (reference partitions raw keys by range: src/system/postmaster.cc:17-31).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace psamd {
+
+constexpr uint64_t kEmptyKey = ~0ull;
+constexpr int kWave = 64;
+
+#define PSAMD_HIP_CHECK(expr)                                                   \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess) {                                                     \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + \
+                               " at " __FILE__ ":" + std::to_string(__LINE__)); \
+    }                                                                           \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// 64-bit finaliser (murmur3 fmix64) — used for table slot placement.
+__host__ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// Bijective key mixer on [0, 2^bits): two rounds of (odd multiply mod 2^bits,
+// xorshift by s >= bits/2). xorshift by s >= bits/2 is an involution, and an odd
+// multiply is invertible mod 2^bits, so unmix() exists (host computes inverses).
+struct KeyMix {
+  uint64_t mask;   // 2^bits - 1 (all ones for bits == 64)
+  uint64_t a, b;   // odd multipliers (mod 2^bits)
+  uint64_t ai, bi; // their inverses mod 2^bits
+  int s;           // shift, >= ceil(bits/2)
+  int bits;
+};
+
+__host__ __device__ __forceinline__ uint64_t mix_key(uint64_t x, const KeyMix& m) {
+  x = (x * m.a) & m.mask;
+  x ^= x >> m.s;
+  x = (x * m.b) & m.mask;
+  x ^= x >> m.s;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint64_t unmix_key(uint64_t x, const KeyMix& m) {
+  x ^= x >> m.s;
+  x = (x * m.bi) & m.mask;
+  x ^= x >> m.s;
+  x = (x * m.ai) & m.mask;
+  return x;
+}
+
+// Grid helpers ---------------------------------------------------------------
+inline int grid_for(int64_t n, int block, int max_blocks = 2048) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > max_blocks) g = max_blocks;
+  return (int)g;
+}
+
+// Valid length: from a device counter if given, else the host-provided n.
+__device__ __forceinline__ int64_t dev_len(const int32_t* n_dev, int64_t n_host) {
+  return n_dev ? (int64_t)(*n_dev) : n_host;
+}
+
+// Wave-level reductions (64 lanes) -------------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    T o = __shfl_down(v, off, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    T o = __shfl_down(v, off, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// Block reduction of a double, result valid in thread 0. Block size <= 1024.
+__device__ __forceinline__ double block_sum_f64(double v, double* lds /*[16]*/) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) lds[wid] = v;
+  __syncthreads();
+  double r = 0;
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int i = 0; i < nw; ++i) r += lds[i];
+  }
+  __syncthreads();
+  return r;
+}
+
+// Counter-based RNG (splitmix64 of (seed, index)) — deterministic per element.
+__host__ __device__ __forceinline__ uint64_t rng64(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9e3779b97f4a7c15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ __forceinline__ float u01(uint64_t r) {  // (0,1]
+  return ((float)(r >> 40) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+}  // namespace psamd

@@ -1,0 +1,374 @@
+// HBM-resident sharded key/value store for scalar linear models.
+//
+// Replaces the reference's per-server CPU hash map `KVStore<K,V,E,S>`
+// (src/parameter/kv_store.h:28-80) whose entries implement the optimizer
+// (FTRLEntry / SGDEntry / AdaGradEntry, src/app/linear_method/async_sgd.h:71-124).
+//
+// Layout: open addressing, linear probing, one 32-byte slot per key
+//   { u64 key(mixed) | f32 w | f32 z | f32 n | f32 acc | u32 cnt | u32 flags }
+// so a lookup that hits on its first probe touches exactly one 32-B sector and
+// the optimizer read-modify-write touches the same sector again. Probe index =
+// fmix64(key) & mask. 10^9 keys at load 0.5 = 64 GB: fits one MI355X's 288 GB.
+//
+// Concurrency: a key transitions EMPTY -> key exactly once via 64-bit CAS, so
+// a stale plain load can only return EMPTY (then the CAS is authoritative) or
+// the final key. Payload updates to distinct slots are race free (callers
+// dedupe keys per launch); cross-source duplicates are applied by sequential
+// launches (reference semantics: every push message is one optimizer step)
+// or by the accumulate/apply pair (synchronous / BSP aggregation).
+#include "common.cuh"
+#include <stdexcept>
+#include <string>
+
+namespace psamd {
+
+struct alignas(32) Slot {
+  uint64_t key;
+  float w, z, n, acc;
+  uint32_t cnt, flags;
+};
+static_assert(sizeof(Slot) == 32, "slot must be 32 bytes");
+
+enum InitType : int { kInitZero = 0, kInitConstant = 1, kInitGaussian = 2, kInitUniform = 3 };
+enum Algo : int { kSGD = 0, kAdaGrad = 1, kFTRL = 2 };
+enum LrType : int { kLrConstant = 1, kLrDecay = 2 };
+
+struct UpdateParams {
+  int algo;
+  int lr_type;
+  float alpha, beta;
+  float l1, l2;
+  float grad_scale;  // multiply incoming gradient (e.g. 1/minibatch)
+  float max_delta;   // optional clip of |w_new - w_old| (<=0: off)
+};
+
+__device__ __forceinline__ float init_value(uint64_t key, int init_type, float v, float s,
+                                            uint64_t seed) {
+  switch (init_type) {
+    case kInitConstant: return v;
+    case kInitGaussian: {
+      uint64_t r1 = rng64(seed, key * 2), r2 = rng64(seed, key * 2 + 1);
+      float u1 = u01(r1), u2 = u01(r2);
+      return v + s * sqrtf(-2.f * logf(u1)) * cosf(6.283185307f * u2);
+    }
+    case kInitUniform: return v + s * (2.f * u01(rng64(seed, key)) - 1.f);
+    default: return 0.f;
+  }
+}
+
+__global__ void kv_init_kernel(Slot* __restrict__ slots, int64_t cap) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cap;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    Slot s;
+    s.key = kEmptyKey;
+    s.w = s.z = s.n = s.acc = 0.f;
+    s.cnt = s.flags = 0;
+    slots[i] = s;
+  }
+}
+
+// Lookup (optionally insert) every key; write its slot index (-1 if absent or
+// table full) and optionally its weight. Fused gather is exact for zero init;
+// for non-zero init the caller uses a separate gather launch (the inserting
+// lane writes w after its CAS, a same-launch reader could see the old 0).
+__global__ void kv_resolve_kernel(Slot* __restrict__ slots, uint64_t mask,
+                                  const uint64_t* __restrict__ keys, int64_t n_host,
+                                  const int32_t* __restrict__ n_dev,
+                                  int64_t* __restrict__ out_slot, float* __restrict__ out_w,
+                                  int insert, int init_type, float init_v, float init_s,
+                                  uint64_t seed, int32_t* __restrict__ err,
+                                  int32_t* __restrict__ inserted) {
+  const int64_t n = dev_len(n_dev, n_host);
+  int local_ins = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = keys[i];
+    uint64_t idx = fmix64(h) & mask;
+    int64_t found = -1;
+    float w = 0.f;
+    for (uint64_t probe = 0; probe <= mask; ++probe) {
+      uint64_t k = slots[idx].key;
+      if (k == h) {
+        found = (int64_t)idx;
+        w = slots[idx].w;
+        break;
+      }
+      if (k == kEmptyKey) {
+        if (!insert) break;
+        unsigned long long prev = atomicCAS((unsigned long long*)&slots[idx].key,
+                                            (unsigned long long)kEmptyKey,
+                                            (unsigned long long)h);
+        if (prev == kEmptyKey) {
+          found = (int64_t)idx;
+          if (init_type != kInitZero) {
+            w = init_value(h, init_type, init_v, init_s, seed);
+            slots[idx].w = w;
+          }
+          ++local_ins;
+          break;
+        }
+        if (prev == h) {
+          found = (int64_t)idx;
+          w = slots[idx].w;
+          break;
+        }
+      }
+      idx = (idx + 1) & mask;
+    }
+    if (found < 0 && insert && err) atomicOr(err, 1);  // table full
+    out_slot[i] = found;
+    if (out_w) out_w[i] = w;
+  }
+  if (inserted) {
+    int tot = wave_sum(local_ins);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(inserted, tot);
+  }
+}
+
+// out[i] = slot.w (0 for missing), gathered by cached slot index.
+__global__ void kv_gather_kernel(const Slot* __restrict__ slots,
+                                 const int64_t* __restrict__ slot_idx, int64_t n_host,
+                                 const int32_t* __restrict__ n_dev, float* __restrict__ out,
+                                 int field) {
+  const int64_t n = dev_len(n_dev, n_host);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = slot_idx[i];
+    float v = 0.f;
+    if (s >= 0) {
+      const float* f = &slots[s].w;
+      v = f[field];
+    }
+    out[i] = v;
+  }
+}
+
+// Set fields (checkpoint restore / explicit assignment).
+__global__ void kv_set_kernel(Slot* __restrict__ slots, const int64_t* __restrict__ slot_idx,
+                              int64_t n, const float* __restrict__ w,
+                              const float* __restrict__ z, const float* __restrict__ nn) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = slot_idx[i];
+    if (s < 0) continue;
+    if (w) slots[s].w = w[i];
+    if (z) slots[s].z = z[i];
+    if (nn) slots[s].n = nn[i];
+  }
+}
+
+__device__ __forceinline__ float soft_threshold_prox(float zz, float eta, float l1, float l2) {
+  // argmin_w 1/(2 eta) (w - zz)^2 + l1 |w| + l2/2 ... (reference ElasticNet::proximal,
+  // src/app/linear_method/penalty.h:38-43): shrink by l1*eta, scale by 1/(1+l2*eta).
+  const float leta = l1 * eta;
+  if (zz <= leta && zz >= -leta) return 0.f;
+  return (zz > 0.f ? zz - leta : zz + leta) / (1.f + l2 * eta);
+}
+
+__device__ __forceinline__ float apply_update(Slot& s, float g, const UpdateParams& p) {
+  const float w_old = s.w;
+  float w_new;
+  if (p.algo == kFTRL) {
+    // FTRL-proximal (reference FTRLEntry::get, async_sgd.h:107-119).
+    const float n_new = sqrtf(s.n * s.n + g * g);
+    const float sigma = (n_new - s.n) / p.alpha;
+    s.z += g - sigma * w_old;
+    s.n = n_new;
+    const float eta = p.lr_type == kLrConstant ? p.alpha : p.alpha / (n_new + p.beta);
+    w_new = soft_threshold_prox(-s.z * eta, eta, p.l1, p.l2);
+  } else if (p.algo == kAdaGrad) {
+    // Proximal AdaGrad (the reference leaves this as a TODO, async_sgd.h:73-79).
+    s.n += g * g;
+    const float eta = p.alpha / (p.beta + sqrtf(s.n));
+    w_new = soft_threshold_prox(w_old - eta * g, eta, p.l1, p.l2);
+  } else {
+    // Proximal SGD with per-key step count (reference stub: async_sgd.h:89-94).
+    s.cnt += 1;
+    const float eta = p.lr_type == kLrConstant ? p.alpha
+                                                : p.alpha / (p.beta + sqrtf((float)s.cnt));
+    w_new = soft_threshold_prox(w_old - eta * g, eta, p.l1, p.l2);
+  }
+  if (p.max_delta > 0.f) {
+    const float d = w_new - w_old;
+    if (d > p.max_delta) w_new = w_old + p.max_delta;
+    if (d < -p.max_delta) w_new = w_old - p.max_delta;
+  }
+  s.w = w_new;
+  return w_old;
+}
+
+// Apply one pushed gradient per (unique within this launch) slot.
+// stats: [0] nnz delta (as double), [1] sum w_new^2, [2] sum (w_new-w_old)^2.
+__global__ void kv_update_kernel(Slot* __restrict__ slots, const int64_t* __restrict__ slot_idx,
+                                 const float* __restrict__ grad, int64_t n_host,
+                                 const int32_t* __restrict__ n_dev, UpdateParams p,
+                                 double* __restrict__ stats) {
+  __shared__ double lds[16];
+  const int64_t n = dev_len(n_dev, n_host);
+  double dnnz = 0, wsum = 0, dsum = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t si = slot_idx[i];
+    if (si < 0) continue;
+    const float g = grad[i] * p.grad_scale;
+    if (g != g) continue;  // NaN mark = filtered entry (reference SparseFilter)
+    Slot s = slots[si];
+    const float w_old = apply_update(s, g, p);
+    slots[si] = s;
+    dnnz += (double)((s.w != 0.f) - (w_old != 0.f));
+    wsum += (double)s.w * s.w;
+    const double d = (double)s.w - w_old;
+    dsum += d * d;
+  }
+  if (stats) {
+    double a = block_sum_f64(dnnz, lds);
+    double b = block_sum_f64(wsum, lds);
+    double c = block_sum_f64(dsum, lds);
+    if (threadIdx.x == 0) {
+      if (a != 0) atomicAdd(&stats[0], a);
+      if (b != 0) atomicAdd(&stats[1], b);
+      if (c != 0) atomicAdd(&stats[2], c);
+    }
+  }
+}
+
+// Synchronous aggregation: acc += g; first toucher appends the slot to a list.
+__global__ void kv_accumulate_kernel(Slot* __restrict__ slots, const int64_t* __restrict__ slot_idx,
+                                     const float* __restrict__ grad, int64_t n_host,
+                                     const int32_t* __restrict__ n_dev,
+                                     int64_t* __restrict__ touched, int32_t* __restrict__ n_touched) {
+  const int64_t n = dev_len(n_dev, n_host);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t si = slot_idx[i];
+    if (si < 0) continue;
+    const float g = grad[i];
+    if (g != g) continue;
+    atomicAdd(&slots[si].acc, g);
+    if (atomicOr(&slots[si].flags, 1u) == 0u) {
+      int pos = atomicAdd(n_touched, 1);
+      touched[pos] = si;
+    }
+  }
+}
+
+__global__ void kv_apply_accumulated_kernel(Slot* __restrict__ slots,
+                                            const int64_t* __restrict__ touched,
+                                            const int32_t* __restrict__ n_touched, UpdateParams p,
+                                            double* __restrict__ stats) {
+  __shared__ double lds[16];
+  const int64_t n = *n_touched;
+  double dnnz = 0, wsum = 0, dsum = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t si = touched[i];
+    Slot s = slots[si];
+    const float g = s.acc * p.grad_scale;
+    s.acc = 0.f;
+    s.flags = 0u;
+    const float w_old = apply_update(s, g, p);
+    slots[si] = s;
+    dnnz += (double)((s.w != 0.f) - (w_old != 0.f));
+    wsum += (double)s.w * s.w;
+    const double d = (double)s.w - w_old;
+    dsum += d * d;
+  }
+  if (stats) {
+    double a = block_sum_f64(dnnz, lds);
+    double b = block_sum_f64(wsum, lds);
+    double c = block_sum_f64(dsum, lds);
+    if (threadIdx.x == 0) {
+      if (a != 0) atomicAdd(&stats[0], a);
+      if (b != 0) atomicAdd(&stats[1], b);
+      if (c != 0) atomicAdd(&stats[2], c);
+    }
+  }
+}
+
+// Occupancy / sparsity census: out[0] = occupied slots, out[1] = nonzero w.
+__global__ void kv_census_kernel(const Slot* __restrict__ slots, int64_t cap,
+                                 unsigned long long* __restrict__ out) {
+  unsigned long long occ = 0, nz = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < cap;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = slots[i].key;
+    if (k != kEmptyKey) {
+      ++occ;
+      nz += slots[i].w != 0.f;
+    }
+  }
+  occ = wave_sum(occ);
+  nz = wave_sum(nz);
+  if ((threadIdx.x & 63) == 0) {
+    if (occ) atomicAdd(&out[0], occ);
+    if (nz) atomicAdd(&out[1], nz);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers
+void kv_init(void* slots, int64_t cap, hipStream_t st) {
+  kv_init_kernel<<<grid_for(cap, 256, 8192), 256, 0, st>>>((Slot*)slots, cap);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void kv_resolve(void* slots, int64_t cap, const uint64_t* keys, int64_t n, const int32_t* n_dev,
+                int64_t* out_slot, float* out_w, bool insert, int init_type, float init_v,
+                float init_s, uint64_t seed, int32_t* err, int32_t* inserted, hipStream_t st) {
+  const bool fused_w = out_w && init_type == kInitZero;
+  kv_resolve_kernel<<<grid_for(n, 256), 256, 0, st>>>(
+      (Slot*)slots, (uint64_t)(cap - 1), keys, n, n_dev, out_slot, fused_w ? out_w : nullptr,
+      insert ? 1 : 0, init_type, init_v, init_s, seed, err, inserted);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  if (out_w && !fused_w) {
+    kv_gather_kernel<<<grid_for(n, 256), 256, 0, st>>>((const Slot*)slots, out_slot, n, n_dev,
+                                                       out_w, 0);
+    PSAMD_HIP_CHECK(hipGetLastError());
+  }
+}
+
+void kv_gather(const void* slots, const int64_t* slot_idx, int64_t n, const int32_t* n_dev,
+               float* out, int field, hipStream_t st) {
+  kv_gather_kernel<<<grid_for(n, 256), 256, 0, st>>>((const Slot*)slots, slot_idx, n, n_dev, out,
+                                                     field);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void kv_set(void* slots, const int64_t* slot_idx, int64_t n, const float* w, const float* z,
+            const float* nn, hipStream_t st) {
+  kv_set_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, slot_idx, n, w, z, nn);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void kv_update(void* slots, const int64_t* slot_idx, const float* grad, int64_t n,
+               const int32_t* n_dev, int algo, int lr_type, float alpha, float beta, float l1,
+               float l2, float grad_scale, float max_delta, double* stats, hipStream_t st) {
+  UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
+  kv_update_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, slot_idx, grad, n, n_dev, p,
+                                                     stats);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void kv_accumulate(void* slots, const int64_t* slot_idx, const float* grad, int64_t n,
+                   const int32_t* n_dev, int64_t* touched, int32_t* n_touched, hipStream_t st) {
+  kv_accumulate_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, slot_idx, grad, n, n_dev,
+                                                         touched, n_touched);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void kv_apply_accumulated(void* slots, const int64_t* touched, const int32_t* n_touched,
+                          int64_t max_n, int algo, int lr_type, float alpha, float beta, float l1,
+                          float l2, float grad_scale, float max_delta, double* stats,
+                          hipStream_t st) {
+  UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
+  kv_apply_accumulated_kernel<<<grid_for(max_n, 256), 256, 0, st>>>((Slot*)slots, touched,
+                                                                    n_touched, p, stats);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void kv_census(const void* slots, int64_t cap, unsigned long long* out, hipStream_t st) {
+  kv_census_kernel<<<grid_for(cap, 256, 4096), 256, 0, st>>>((const Slot*)slots, cap, out);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace psamd

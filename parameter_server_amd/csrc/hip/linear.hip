@@ -1,0 +1,320 @@
+// Fused sparse linear-model kernels on localized minibatches.
+//
+// Reference hot loops (CPU, Eigen + thread pool):
+//   Xw = X*w           SparseMatrix::times        src/util/sparse_matrix.h:73-107
+//   loss/tau/objective LogitLoss::evaluate/compute src/app/linear_method/loss.h:75-97
+//   grad = X^T(-y*tau) SparseMatrix::transTimes   src/util/matrix.h:57-59
+//   AUC / accuracy     Evaluation::auc/accuracy   src/util/evaluation.h:22-63
+// Here the forward pass computes Xw, the loss, dL/d(Xw), accuracy and a
+// bucketed-AUC histogram in ONE launch (lane per example, w_local is the small
+// pulled vector and stays L2 resident). The backward pass needs no atomics for
+// segments that live inside a wavefront: it walks the key-sorted order from
+// localisation (that order IS the CSC layout, so no CSR->CSC transpose,
+// reference alterStorage sparse_matrix.h:186-241, is ever materialised) and
+// does a 64-lane segmented scan; only segments that cross a wave boundary
+// issue one float atomic per wave piece.
+#include "common.cuh"
+#include <stdexcept>
+#include <string>
+
+namespace psamd {
+
+enum LossType : int { kSquare = 1, kLogit = 2, kHinge = 3, kSquareHinge = 4 };
+
+__device__ __forceinline__ float softplus(float x) {
+  return x > 20.f ? x : (x < -20.f ? expf(x) : log1pf(expf(x)));
+}
+
+template <bool kHasRowPtr>
+__global__ void __launch_bounds__(256)
+linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
+                  const int32_t* __restrict__ local_col, const float* __restrict__ vals,
+                  const float* __restrict__ w_local, const float* __restrict__ labels,
+                  int loss_type, float* __restrict__ xw_out, float* __restrict__ coef_out,
+                  float* __restrict__ coef2_out, double* __restrict__ metrics,
+                  uint32_t* __restrict__ hist, int nbins) {
+  extern __shared__ uint32_t lhist[];  // [2*nbins] when hist != nullptr
+  __shared__ double lds[16];
+  if (hist) {
+    for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) lhist[i] = 0;
+    __syncthreads();
+  }
+  double loss_acc = 0, corr_acc = 0, cnt = 0;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < B;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    int64_t b, e;
+    if (kHasRowPtr) { b = row_ptr[r]; e = row_ptr[r + 1]; }
+    else { b = r * width; e = b + width; }
+    float m = 0.f;
+    if (vals) {
+      for (int64_t k = b; k < e; ++k) {
+        const int32_t c = local_col[k];
+        if (c >= 0) m += w_local[c] * vals[k];
+      }
+    } else {
+      for (int64_t k = b; k < e; ++k) {
+        const int32_t c = local_col[k];
+        if (c >= 0) m += w_local[c];
+      }
+    }
+    const float y = labels[r] > 0.f ? 1.f : -1.f;
+    const float ym = y * m;
+    float loss, coef, coef2;
+    switch (loss_type) {
+      case kSquare: {
+        const float d = m - labels[r];
+        loss = 0.5f * d * d; coef = d; coef2 = 1.f;
+        break;
+      }
+      case kHinge:
+        loss = fmaxf(0.f, 1.f - ym); coef = ym < 1.f ? -y : 0.f; coef2 = 0.f;
+        break;
+      case kSquareHinge: {
+        const float h = fmaxf(0.f, 1.f - ym);
+        loss = h * h; coef = -2.f * y * h; coef2 = ym < 1.f ? 2.f : 0.f;
+        break;
+      }
+      default: {  // logit: tau = 1/(1+exp(y m))
+        loss = softplus(-ym);
+        const float tau = 1.f / (1.f + expf(ym));
+        coef = -y * tau; coef2 = tau * (1.f - tau);
+        break;
+      }
+    }
+    if (xw_out) xw_out[r] = m;
+    coef_out[r] = coef;
+    if (coef2_out) coef2_out[r] = coef2;
+    loss_acc += loss;
+    corr_acc += (ym > 0.f) ? 1.0 : 0.0;
+    cnt += 1.0;
+    if (hist) {
+      const float p = 1.f / (1.f + expf(-m));
+      int bin = (int)(p * nbins);
+      bin = bin < 0 ? 0 : (bin >= nbins ? nbins - 1 : bin);
+      atomicAdd(&lhist[(y > 0.f ? nbins : 0) + bin], 1u);
+    }
+  }
+  if (metrics) {
+    double a = block_sum_f64(loss_acc, lds);
+    double c = block_sum_f64(corr_acc, lds);
+    double n = block_sum_f64(cnt, lds);
+    if (threadIdx.x == 0 && n > 0) {
+      atomicAdd(&metrics[0], a);
+      atomicAdd(&metrics[1], c);
+      atomicAdd(&metrics[2], n);
+    }
+  }
+  if (hist) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x)
+      if (lhist[i]) atomicAdd(&hist[i], lhist[i]);
+  }
+}
+
+// grad[u] = sum_{i in seg u} coef[row(pos_s[i])] * val[pos_s[i]]   (and hess with val^2)
+__global__ void __launch_bounds__(256)
+linear_bwd_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ segid,
+                  int64_t n, const int32_t* __restrict__ rows, int width,
+                  const float* __restrict__ vals, const float* __restrict__ coef,
+                  const float* __restrict__ coef2, float* __restrict__ grad,
+                  float* __restrict__ hess) {
+  const int lane = threadIdx.x & 63;
+  // One element per lane; each wavefront is one segmented-scan unit.
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); i0 < n;
+       i0 += stride) {
+    const int64_t i = i0 + lane;
+    const bool valid = i < n;
+    int32_t s = -1;
+    float v = 0.f, v2 = 0.f;
+    if (valid) {
+      s = segid[i];
+      const int32_t p = pos_s[i];
+      const int32_t r = rows ? rows[p] : p / width;
+      const float x = vals ? vals[p] : 1.f;
+      v = coef[r] * x;
+      if (hess) v2 = coef2[r] * x * x;
+    }
+    // segmented inclusive scan (Hillis-Steele) over 64 lanes
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const float vo = __shfl_up(v, off, 64);
+      const float v2o = __shfl_up(v2, off, 64);
+      const int32_t so = __shfl_up(s, off, 64);
+      if (lane >= off && so == s) { v += vo; v2 += v2o; }
+    }
+    const int32_t s_next = __shfl_down(s, 1, 64);
+    const int32_t s_lane0 = __shfl(s, 0, 64);
+    int32_t prev_of_lane0 = -2;
+    if (lane == 0 && i0 > 0) prev_of_lane0 = segid[i0 - 1];
+    prev_of_lane0 = __shfl(prev_of_lane0, 0, 64);
+    const bool tail = valid && (lane == 63 || s_next != s || i + 1 >= n);
+    if (tail) {
+      const bool starts_inside = (s != s_lane0) || (prev_of_lane0 != s);
+      bool ends_inside = true;
+      if (lane == 63 && i + 1 < n) ends_inside = segid[i + 1] != s;
+      const int32_t u = s - 1;
+      if (starts_inside && ends_inside) {
+        grad[u] = v;
+        if (hess) hess[u] = v2;
+      } else {
+        atomicAdd(&grad[u], v);
+        if (hess) atomicAdd(&hess[u], v2);
+      }
+    }
+  }
+}
+
+// Bucketed AUC of one minibatch from its histogram; metrics[3] += auc, metrics[4] += 1.
+// Resets the histogram (so the next step starts clean inside a captured graph).
+__global__ void auc_from_hist_kernel(uint32_t* __restrict__ hist, int nbins,
+                                     double* __restrict__ metrics) {
+  __shared__ double s_neg[256], s_pos[256], s_area[256];
+  const int t = threadIdx.x;  // blockDim.x == 256
+  const int per = (nbins + 255) / 256;
+  const int lo = min(nbins, t * per), hi = min(nbins, lo + per);
+  double neg = 0, pos = 0;
+  for (int b = lo; b < hi; ++b) { neg += hist[b]; pos += hist[nbins + b]; }
+  s_neg[t] = neg;
+  s_pos[t] = pos;
+  __syncthreads();
+  if (t == 0) {  // exclusive prefix over 256 partials; totals in slot 255 of s_area/s_pos
+    double run = 0, ptot = 0;
+    for (int k = 0; k < 256; ++k) { const double x = s_neg[k]; s_neg[k] = run; run += x; ptot += s_pos[k]; }
+    s_area[0] = run;
+    s_pos[0] = ptot;
+  }
+  __syncthreads();
+  const double Ntot = s_area[0], Ptot = s_pos[0];
+  __syncthreads();
+  double below = s_neg[t], area = 0;
+  for (int b = lo; b < hi; ++b) {
+    const double nb = hist[b], pb = hist[nbins + b];
+    area += pb * (below + 0.5 * nb);
+    below += nb;
+    hist[b] = 0;
+    hist[nbins + b] = 0;
+  }
+  s_area[t] = area;
+  __syncthreads();
+  if (t == 0) {
+    double A = 0;
+    for (int k = 0; k < 256; ++k) A += s_area[k];
+    if (Ptot > 0 && Ntot > 0) {
+      metrics[3] += A / (Ptot * Ntot);
+      metrics[4] += 1.0;
+    }
+  }
+}
+
+// Expand a CSR row pointer into a per-nnz row index (COO rows).
+__global__ void csr_rows_kernel(const int64_t* __restrict__ row_ptr, int64_t B,
+                                int32_t* __restrict__ rows) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < B;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t k = row_ptr[r]; k < row_ptr[r + 1]; ++k) rows[k] = (int32_t)r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Criteo-shaped synthetic minibatch: 13 integer slots (log-bucketised) + 26
+// categorical slots with the Criteo-Kaggle cardinalities and power-law ids,
+// hashed into [0, num_features). Labels from a planted sparse logistic model.
+__constant__ uint32_t c_cards[26];
+
+__device__ __forceinline__ float planted_w(uint64_t key, uint64_t seed) {
+  const uint64_t r = rng64(seed ^ 0x5bd1e995ull, key);
+  if ((r & 0xff) >= 51) return 0.f;  // ~20% of features carry signal
+  const float u1 = u01(rng64(seed, key * 2 + 7)), u2 = u01(r);
+  return 0.6f * sqrtf(-2.f * logf(u1)) * cosf(6.283185307f * u2);
+}
+
+__global__ void __launch_bounds__(256)
+criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_dev, int64_t B,
+                  uint64_t num_features, float alpha, uint64_t* __restrict__ keys,
+                  float* __restrict__ labels) {
+  if (row0_dev) row0 += *row0_dev;
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < B;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t gr = (uint64_t)(row0 + r);
+    float logit = -1.2f;
+    for (int j = 0; j < 39; ++j) {
+      const float u = u01(rng64(seed + (uint64_t)j * 0x632be59bd9b4e019ull, gr));
+      uint64_t id;
+      if (j < 13) {
+        // integer feature: heavy tailed count, log2 bucketised (~<= 40 buckets)
+        const float x = expf(u * 12.f) - 1.f;
+        id = (uint64_t)(2.f * log2f(1.f + x));
+      } else {
+        const float C = (float)c_cards[j - 13];
+        const float oma = 1.f - alpha;
+        const float x = powf((powf(C, oma) - 1.f) * u + 1.f, 1.f / oma);
+        uint64_t v = (uint64_t)x;
+        id = v >= 1 ? v - 1 : 0;
+      }
+      const uint64_t key = fmix64(((uint64_t)(j + 1) << 48) ^ id) % num_features;
+      keys[r * 39 + j] = key;
+      logit += planted_w(key, seed);
+    }
+    const float p = 1.f / (1.f + expf(-logit));
+    const float u = u01(rng64(seed ^ 0xabcdefull, gr));
+    labels[r] = u < p ? 1.f : -1.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+void linear_fwd(const int64_t* row_ptr, int64_t B, int width, const int32_t* local_col,
+                const float* vals, const float* w_local, const float* labels, int loss_type,
+                float* xw, float* coef, float* coef2, double* metrics, uint32_t* hist, int nbins,
+                hipStream_t st) {
+  const size_t lds = hist ? (size_t)2 * nbins * sizeof(uint32_t) : 0;
+  const int g = grid_for(B, 256, 4096);
+  if (row_ptr)
+    linear_fwd_kernel<true><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
+                                                 labels, loss_type, xw, coef, coef2, metrics,
+                                                 hist, nbins);
+  else
+    linear_fwd_kernel<false><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
+                                                  labels, loss_type, xw, coef, coef2, metrics,
+                                                  hist, nbins);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void linear_bwd(const int32_t* pos_s, const int32_t* segid, int64_t n, const int32_t* rows,
+                int width, const float* vals, const float* coef, const float* coef2, float* grad,
+                float* hess, hipStream_t st) {
+  linear_bwd_kernel<<<grid_for(n, 256, 8192), 256, 0, st>>>(pos_s, segid, n, rows, width, vals,
+                                                            coef, coef2, grad, hess);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void auc_from_hist(uint32_t* hist, int nbins, double* metrics, hipStream_t st) {
+  auc_from_hist_kernel<<<1, 256, 0, st>>>(hist, nbins, metrics);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void csr_rows(const int64_t* row_ptr, int64_t B, int32_t* rows, hipStream_t st) {
+  csr_rows_kernel<<<grid_for(B, 256), 256, 0, st>>>(row_ptr, B, rows);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void criteo_set_cards(const uint32_t* cards26) {
+  PSAMD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_cards), cards26, 26 * sizeof(uint32_t)));
+}
+
+void criteo_gen(uint64_t seed, int64_t row0, const int64_t* row0_dev, int64_t B,
+                uint64_t num_features, float alpha, uint64_t* keys, float* labels,
+                hipStream_t st) {
+  criteo_gen_kernel<<<grid_for(B, 256, 4096), 256, 0, st>>>(seed, row0, row0_dev, B,
+                                                            num_features, alpha, keys, labels);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void add_i64_kernel(int64_t* p, int64_t v) { *p += v; }
+
+void add_i64(int64_t* p, int64_t v, hipStream_t st) {
+  add_i64_kernel<<<1, 1, 0, st>>>(p, v);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace psamd

@@ -1,0 +1,284 @@
+"""Sparse logistic regression trained through the sharded HBM parameter server.
+
+This is the MI355X-native counterpart of the reference's async-SGD linear
+method (src/app/linear_method/async_sgd.h: AsyncSGDWorker::computeGradient
+:241-289 and AsyncSGDServer with FTRL/SGD/AdaGrad entries :101-178,
+MinibatchReader::read src/learner/sgd.h:131-150). One process per GPU; every
+rank is a colocated worker (data shard ``rank``) and server shard (key range
+``rank`` of the mixed key space).
+
+One training step on a rank (all on the GPU, no host round trip when G == 1):
+  localise      mix -> radix sort -> RLE  (unique keys, local cols, CSC order)
+  [tail filter] CountMin insert/query of per-key counts, drop rare keys
+  pull          G == 1: lookup-or-insert in the local HBM table;
+                G  > 1: keys are already sorted by owner -> count exchange ->
+                all-to-all-v of keys -> owner lookup -> all-to-all-v of weights
+  forward       Xw, loss, dL/dXw, accuracy, AUC histogram (one kernel)
+  backward      segmented reduction over the CSC order -> grad per unique key
+  push          G == 1: optimizer update at the cached slots (key caching: the
+                push never re-sends or re-hashes keys);
+                G  > 1: all-to-all-v of gradients [FixingFloat-compressed] ->
+                owner applies one optimizer step per source segment in rank
+                order (reference semantics: one FTRL step per push message) or
+                sums them first (``push_mode='aggregate'``, synchronous SGD).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from ..ops import fixing_float as ff
+from ..ops.countmin import CountMinSketch
+from ..ops.keymix import key_bits_for, unmix
+from ..ops.kv_table import InitRule, KVTable, UpdateRule, next_pow2
+from ..ops.linear import AUC_BINS, auc_from_hist, linear_backward, linear_forward
+from ..ops.localize import Localizer
+from ..ops.native import hipops
+from ..parallel.comm import Comm, LocalComm
+from ..parallel.consistency import VectorClock, parse_consistency
+from ..parallel.partition import KeyPartition
+
+
+@dataclass
+class SparseLRConfig:
+    num_features: int = 10 ** 9          # hashed feature space (keys in [0, N)); 0 = raw u64
+    minibatch: int = 10000               # examples per worker step (reference SGDConfig.minibatch)
+    max_nnz_per_example: int = 39
+    loss: str = "logit"
+    algo: str = "ftrl"                   # ftrl | adagrad | sgd
+    lr_type: str = "decay"               # constant | decay
+    alpha: float = 0.01
+    beta: float = 10.0
+    l1: float = 10.0
+    l2: float = 1.0
+    grad_scale: float = 1.0
+    table_capacity: int = 0              # slots per shard (power of 2); 0 = auto
+    table_load: float = 0.5              # auto capacity = num_features / G / load
+    max_table_bytes: int = 96 << 30      # cap for the auto size (per GPU)
+    init: InitRule = field(default_factory=InitRule)
+    tail_feature_freq: int = 0           # keep keys seen > freq times (0 = off)
+    countmin_n: float = 1e8
+    countmin_k: int = 2
+    consistency: str = "bsp"             # bsp | ssp:<tau> | asp
+    push_mode: str = "sequential"        # sequential | aggregate
+    fixing_float_bytes: int = 0          # 0 = off, else 1..7 bytes per pushed gradient
+    seed: int = 0
+
+    def update_rule(self) -> UpdateRule:
+        return UpdateRule(self.algo, self.lr_type, self.alpha, self.beta, self.l1, self.l2,
+                          self.grad_scale)
+
+
+class SparseLRTrainer:
+    def __init__(self, cfg: SparseLRConfig, comm: Comm | None = None, device="cpu"):
+        self.cfg = cfg
+        self.comm = comm or LocalComm(device)
+        self.G, self.rank = self.comm.world, self.comm.rank
+        self.device = torch.device(device)
+        self.gpu = self.device.type == "cuda"
+        self.bits = key_bits_for(cfg.num_features)
+        self.part = KeyPartition(self.bits, self.G)
+        self.rule = cfg.update_rule()
+        self.tau = parse_consistency(cfg.consistency)
+        self.clock = VectorClock(self.G, self.tau)
+        cap = cfg.table_capacity or self.auto_capacity(cfg, self.G, self.bits)
+        self.table = KVTable(cap, self.device, cfg.init)
+        self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
+        self.localizer = Localizer(self.max_nnz, self.bits, self.device)
+        self.filter = (CountMinSketch(int(cfg.countmin_n), cfg.countmin_k, self.device)
+                       if cfg.tail_feature_freq > 0 else None)
+        dev = self.device
+        self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
+        self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.hist = torch.zeros(2 * AUC_BINS, dtype=torch.int32, device=dev)
+        self.coef = torch.empty(cfg.minibatch, dtype=torch.float32, device=dev)
+        if self.gpu:
+            self.slot_buf = torch.empty(self.max_nnz, dtype=torch.int64, device=dev)
+            self.w_buf = torch.empty(self.max_nnz, dtype=torch.float32, device=dev)
+            self.touched = None
+        self.step_count = 0
+        self.examples = 0
+        self.comm_bytes = 0
+        self.t0 = time.time()
+
+    @staticmethod
+    def auto_capacity(cfg: SparseLRConfig, G: int, bits: int) -> int:
+        n = cfg.num_features if cfg.num_features else (1 << 27)
+        want = next_pow2(int(math.ceil(n / G / cfg.table_load)))
+        cap_max = 1 << max(6, (cfg.max_table_bytes // 32).bit_length() - 1)
+        return max(1024, min(want, cap_max))
+
+    # ------------------------------------------------------------------ step
+    def step(self, keys: torch.Tensor, labels: torch.Tensor, *, width: int | None = None,
+             row_ptr: torch.Tensor | None = None, vals: torch.Tensor | None = None,
+             rows: torch.Tensor | None = None):
+        """One minibatch: pull, forward, backward, push. ``keys`` are raw feature ids
+        in CSR order (fixed ``width`` per row, or ``row_ptr``)."""
+        B = labels.numel()
+        if width is None and row_ptr is None:
+            width = self.cfg.max_nnz_per_example
+        if row_ptr is not None and rows is None and self.gpu:
+            rows = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
+            hipops().csr_rows(row_ptr, rows)
+        loc = self.localizer(keys)
+        if self.filter is not None:
+            w_local, push = self._pull_filtered(loc)
+        elif self.G == 1 and self.gpu:
+            slot, w_local = self.slot_buf, self.w_buf
+            it, iv, isd, seed = self.table.init.args()
+            hipops().kv_resolve(self.table.slots, loc.uniq, loc.n_uniq, slot, w_local, True, it,
+                                iv, isd, seed, self.table._err, self.table._inserted)
+            push = ("local", slot, loc.n_uniq)
+        else:
+            w_local, push = self._pull(loc.uniq, loc.n_uniq)
+        _, coef, _ = linear_forward(loc.local_col, w_local, labels, B=B, width=width or 0,
+                                    row_ptr=row_ptr, vals=vals, loss=self.cfg.loss,
+                                    coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
+        grad, _ = linear_backward(loc, coef, B=B, width=width or 0, rows=rows, vals=vals)
+        self._push(grad, push)
+        auc_from_hist(self.hist, self.metrics)
+        self.clock.tick(self.rank, self.step_count)
+        self.step_count += 1
+        self.examples += B
+
+    # ---------------------------------------------------------------- pull/push
+    def _pull(self, uniq: torch.Tensor, n_uniq: torch.Tensor):
+        """Pull weights of sorted unique mixed keys; returns (w_local, push handle)."""
+        if self.G == 1:
+            U = int(n_uniq.item())
+            keys = uniq[:U]
+            slot, w = self.table.resolve(keys, insert=True)
+            return w, ("local", slot, None)
+        off = self.part.split_sorted(uniq, n_uniq).cpu()
+        U = int(off[-1])
+        send_counts = (off[1:] - off[:-1])
+        recv_counts = self.comm.exchange_counts(send_counts).cpu()
+        req = self.comm.all_to_all_v(uniq[:U], send_counts.tolist(), recv_counts.tolist())
+        slot, w = self.table.resolve(req, insert=True)
+        w_back = self.comm.all_to_all_v(w, recv_counts.tolist(), send_counts.tolist())
+        return w_back, ("dist", slot, send_counts, recv_counts, U)
+
+    def _pull_filtered(self, loc):
+        """Tail-feature filter (reference MinibatchReader::read, sgd.h:140-148):
+        insert per-key counts into the worker's CountMin, pull only keys whose
+        estimated count > tail_feature_freq; filtered keys get w = 0, no push."""
+        U = loc.num_unique()
+        uniq = loc.uniq[:U]
+        cnt = (loc.seg_start[1:U + 1] - loc.seg_start[:U]).clamp(max=255).to(torch.uint8)
+        self.filter.insert(uniq, cnt)
+        keep, _ = self.filter.query(uniq, self.cfg.tail_feature_freq)
+        kept_idx = torch.nonzero(keep, as_tuple=False).flatten()
+        w_kept, push = self._pull(uniq[kept_idx].contiguous(),
+                                  torch.tensor([kept_idx.numel()], dtype=torch.int32,
+                                               device=uniq.device))
+        w_local = torch.zeros(loc.grad.numel(), dtype=torch.float32, device=uniq.device)
+        w_local[kept_idx] = w_kept
+        return w_local, ("filtered", kept_idx, push)
+
+    def _push(self, grad: torch.Tensor, push):
+        kind = push[0]
+        if kind == "filtered":
+            kept_idx, inner = push[1], push[2]
+            g = grad[kept_idx].contiguous()
+            return self._push(g, inner)
+        if kind == "local":
+            slot, n_dev = push[1], push[2]
+            if n_dev is None:
+                self.table.update(slot, grad[:slot.numel()], self.rule, self.stats)
+            else:
+                hipops().kv_update(self.table.slots, slot, grad, n_dev, *self.rule.args(),
+                                   self.stats)
+            return
+        _, slot, send_counts, recv_counts, U = push
+        g = grad[:U].contiguous()
+        nb = self.cfg.fixing_float_bytes
+        if nb:
+            code, mm = ff.encode(g, nb, seed=self.cfg.seed * 7919 + self.step_count)
+            mm_all = self.comm.all_to_all_v(mm.repeat(self.G), [2] * self.G, [2] * self.G)
+            code_in = self.comm.all_to_all_v(code, (send_counts * nb).tolist(),
+                                             (recv_counts * nb).tolist())
+            parts, a = [], 0
+            for s in range(self.G):
+                n = int(recv_counts[s])
+                parts.append(ff.decode(code_in[a * nb:(a + n) * nb], nb, mm_all[2 * s:2 * s + 2], n))
+                a += n
+            g_in = torch.cat(parts) if parts else torch.empty(0, device=g.device)
+        else:
+            g_in = self.comm.all_to_all_v(g, send_counts.tolist(), recv_counts.tolist())
+        if self.cfg.push_mode == "aggregate":
+            self._apply_aggregated(slot, g_in)
+            return
+        a = 0
+        for s in range(self.G):  # one optimizer step per push message, in rank order
+            n = int(recv_counts[s])
+            if n:
+                self.table.update(slot[a:a + n], g_in[a:a + n], self.rule, self.stats)
+            a += n
+
+    def _apply_aggregated(self, slot: torch.Tensor, g_in: torch.Tensor):
+        if self.gpu:
+            if self.touched is None or self.touched.numel() < slot.numel():
+                self.touched = torch.empty(max(slot.numel(), 1024), dtype=torch.int64,
+                                           device=self.device)
+                self.n_touched = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self.n_touched.zero_()
+            H = hipops()
+            H.kv_accumulate(self.table.slots, slot, g_in, None, self.touched, self.n_touched)
+            H.kv_apply_accumulated(self.table.slots, self.touched[:slot.numel()], self.n_touched,
+                                   *self.rule.args(), self.stats)
+            return
+        valid = slot >= 0
+        s, inv = torch.unique(slot[valid], return_inverse=True)
+        g = torch.zeros(s.numel(), dtype=torch.float32).index_add_(0, inv, g_in[valid])
+        self.table.update(s, g, self.rule, self.stats)
+
+    # ------------------------------------------------------------ reporting
+    def progress(self, reset: bool = True) -> dict:
+        """Merged progress across ranks (reference ISGDScheduler::showProgress, sgd.h:45-80)."""
+        m = torch.cat([self.metrics, self.stats]).clone()
+        if self.G > 1:
+            m = self.comm.all_reduce_(m.to(self.comm.device) if self.comm.backend == "nccl"
+                                      else m.cpu())
+        m = m.cpu()
+        n = max(float(m[2]), 1.0)
+        out = {
+            "examples": float(m[2]),
+            "loss": float(m[0]) / n,
+            "accuracy": float(m[1]) / n,
+            "auc": float(m[3]) / max(float(m[4]), 1.0),
+            "nnz_w": float(m[8]),
+            "updt_ratio": math.sqrt(float(m[10])) / math.sqrt(max(float(m[9]), 1e-20)),
+        }
+        if reset:
+            self.metrics.zero_()
+            self.stats[1:].zero_()
+        return out
+
+    # ------------------------------------------------------------ checkpoint
+    def save_model(self, prefix: str, node_id: str | None = None) -> str:
+        """Reference checkpoint layout: ``<prefix>_<NodeID>`` with one ``key\\tweight``
+        line per non-zero weight (src/parameter/kv_store.h:63-73)."""
+        from ..utils.checkpoint import write_text_model
+
+        keys, w, _, _ = self.table.occupied()
+        raw = unmix(keys, self.bits)
+        path = f"{prefix}_{node_id or f'S{self.rank}'}"
+        write_text_model(path, raw.cpu(), w.cpu())
+        return path
+
+    def state_dict(self) -> dict:
+        keys, w, z, n = self.table.occupied()
+        return {"keys": unmix(keys, self.bits).cpu(), "w": w.cpu(), "z": z.cpu(), "n": n.cpu(),
+                "step": self.step_count, "bits": self.bits, "rank": self.rank, "world": self.G}
+
+    def load_state_dict(self, sd: dict):
+        from ..ops.keymix import mix
+
+        keys = mix(sd["keys"].to(self.device), self.bits)
+        own = self.part.owner_of(keys) == self.rank
+        self.table.load(keys[own], sd["w"].to(self.device)[own], sd["z"].to(self.device)[own],
+                        sd["n"].to(self.device)[own])
+        self.step_count = int(sd.get("step", 0))

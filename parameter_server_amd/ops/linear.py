@@ -1,0 +1,144 @@
+"""Sparse linear-model forward / backward on localized minibatches.
+
+GPU: ``linear_fwd`` (Xw + loss + dL/dXw + accuracy + AUC histogram in one
+launch) and ``linear_bwd`` (segmented reduction in CSC order), see
+csrc/hip/linear.hip. CPU: the same math with plain PyTorch ops, which is also the
+fp32 reference the HIP kernels are tested against.
+
+Loss types follow the reference ``LossConfig`` enum
+(src/app/linear_method/proto/linear.proto: SQUARE=1, LOGIT=2, HINGE=3,
+SQUARE_HINGE=4); labels are +1 / -1 (>0 is positive).
+"""
+from __future__ import annotations
+
+import torch
+
+from .native import hipops, is_gpu
+
+LOSS_TYPES = {"square": 1, "logit": 2, "hinge": 3, "square_hinge": 4}
+AUC_BINS = 2048
+
+
+def loss_id(loss) -> int:
+    return loss if isinstance(loss, int) else LOSS_TYPES[str(loss).lower()]
+
+
+def _rows_of(B: int, width: int, row_ptr, device):
+    if row_ptr is None:
+        return torch.arange(B, device=device).repeat_interleave(width)
+    counts = row_ptr[1:] - row_ptr[:-1]
+    return torch.repeat_interleave(torch.arange(B, device=device), counts)
+
+
+def loss_terms_torch(m: torch.Tensor, labels: torch.Tensor, loss: int):
+    """(loss, coef = dL/dm, coef2 = d2L/dm2) elementwise, fp32."""
+    y = torch.where(labels > 0, 1.0, -1.0).to(m.dtype)
+    ym = y * m
+    if loss == 1:
+        d = m - labels
+        return 0.5 * d * d, d, torch.ones_like(m)
+    if loss == 3:
+        return torch.clamp(1 - ym, min=0), torch.where(ym < 1, -y, torch.zeros_like(y)), torch.zeros_like(m)
+    if loss == 4:
+        h = torch.clamp(1 - ym, min=0)
+        return h * h, -2 * y * h, torch.where(ym < 1, 2.0, 0.0).to(m.dtype)
+    tau = torch.sigmoid(-ym)
+    return torch.nn.functional.softplus(-ym), -y * tau, tau * (1 - tau)
+
+
+def linear_forward(local_col, w_local, labels, *, B: int, width: int = 0, row_ptr=None,
+                   vals=None, loss="logit", xw=None, coef=None, coef2=None, metrics=None,
+                   hist=None):
+    """Returns (xw, coef, coef2). ``metrics`` (float64[>=5]) += [loss, correct, n, ...];
+    ``hist`` (int32[2*AUC_BINS]) accumulates the bucketed-AUC histogram."""
+    L = loss_id(loss)
+    dev = local_col.device
+    if is_gpu(local_col):
+        coef = torch.empty(B, dtype=torch.float32, device=dev) if coef is None else coef
+        hipops().linear_fwd(row_ptr, B, width, local_col, vals, w_local, labels, L, xw, coef,
+                            coef2, metrics, hist, AUC_BINS)
+        return xw, coef, coef2
+    rows = _rows_of(B, width, row_ptr, dev)
+    col = local_col.long()
+    valid = col >= 0
+    contrib = torch.where(valid, w_local[col.clamp(min=0)], torch.zeros((), device=dev))
+    if vals is not None:
+        contrib = contrib * vals
+    m = torch.zeros(B, dtype=torch.float32, device=dev).index_add_(0, rows, contrib.float())
+    lo, c, c2 = loss_terms_torch(m, labels[:B].float(), L)
+    if xw is not None:
+        xw.copy_(m)
+    if coef is not None:
+        coef.copy_(c)
+    else:
+        coef = c
+    if coef2 is not None:
+        coef2.copy_(c2)
+    if metrics is not None:
+        y = torch.where(labels[:B] > 0, 1.0, -1.0)
+        metrics[0] += float(lo.double().sum())
+        metrics[1] += float(((y * m) > 0).double().sum())
+        metrics[2] += float(B)
+    if hist is not None:
+        p = torch.sigmoid(m)
+        b = torch.clamp((p * AUC_BINS).long(), 0, AUC_BINS - 1)
+        off = torch.where(labels[:B] > 0, AUC_BINS, 0)
+        hist += torch.bincount(b + off, minlength=2 * AUC_BINS).to(hist.dtype)
+    return (xw if xw is not None else m), coef, (coef2 if coef2 is not None else c2)
+
+
+def linear_backward(loc, coef, *, B: int, width: int = 0, rows=None, vals=None, coef2=None):
+    """grad[u] (and hess[u] if coef2 given) into loc.grad / loc.hess."""
+    if is_gpu(coef):
+        hipops().linear_bwd(loc.pos_s, loc.segid, loc.nnz, rows, width, vals, coef,
+                            coef2 if loc.hess is not None else None, loc.grad,
+                            loc.hess if coef2 is not None else None)
+        return loc.grad, loc.hess
+    dev = coef.device
+    if rows is None:
+        rows = torch.arange(B, device=dev).repeat_interleave(width) if width else None
+    r = rows.long()
+    x = vals.float() if vals is not None else torch.ones(r.numel(), device=dev)
+    col = loc.local_col.long()
+    U = loc.grad.numel()
+    g = torch.zeros(U, dtype=torch.float32, device=dev).index_add_(0, col, coef[r] * x)
+    loc.grad.copy_(g)
+    if coef2 is not None and loc.hess is not None:
+        h = torch.zeros(U, dtype=torch.float32, device=dev).index_add_(0, col, coef2[r] * x * x)
+        loc.hess.copy_(h)
+    return loc.grad, loc.hess
+
+
+def auc_from_hist(hist: torch.Tensor, metrics: torch.Tensor):
+    """metrics[3] += AUC of the histogram, metrics[4] += 1; zeroes hist."""
+    if is_gpu(hist):
+        hipops().auc_from_hist(hist, AUC_BINS, metrics)
+        return
+    neg = hist[:AUC_BINS].double()
+    pos = hist[AUC_BINS:].double()
+    P, N = float(pos.sum()), float(neg.sum())
+    if P > 0 and N > 0:
+        below = torch.cumsum(neg, 0) - neg
+        area = float((pos * (below + 0.5 * neg)).sum())
+        metrics[3] += area / (P * N)
+        metrics[4] += 1
+    hist.zero_()
+
+
+def exact_auc(scores: torch.Tensor, labels: torch.Tensor) -> float:
+    """Exact ROC AUC by sorting (reference Evaluation::auc, src/util/evaluation.h:22-45)."""
+    s = scores.double().cpu()
+    y = labels.cpu() > 0
+    order = torch.argsort(s)
+    ranks = torch.empty_like(s)
+    # average ranks for ties
+    ss = s[order]
+    uniq, inv, cnt = torch.unique_consecutive(ss, return_inverse=True, return_counts=True)
+    ends = torch.cumsum(cnt, 0).double()
+    avg = ends - (cnt.double() - 1) / 2
+    ranks[order] = avg[inv]
+    P = int(y.sum())
+    N = y.numel() - P
+    if P == 0 or N == 0:
+        return float("nan")
+    return float((ranks[y].sum() - P * (P + 1) / 2) / (P * N))

@@ -1,0 +1,111 @@
+"""Minibatch key localisation: unique keys + local column ids + CSC order.
+
+Reference: ``Localizer::countUniqIndex`` / ``remapIndex`` (src/util/localizer.h:69-191)
+which sort (key, pos) pairs on the CPU and rebuild a CSR with uint32 columns.
+On the GPU (``csrc/hip/localize.hip``): mix -> radix sort over ``bits`` key bits ->
+run-length encode, all into a preallocated workspace so a training step can be
+captured into a HIP graph (the unique count stays on the device).
+
+Outputs (``Localized``):
+  uniq[0:U]      sorted unique *mixed* keys (grouped by owner shard)
+  seg_start[0:U+1] start of each key's run in the sorted order
+  pos_s[0:nnz]   nnz index of each element in key-sorted (= CSC) order
+  segid[0:nnz]   1-based run id of each sorted element
+  local_col[0:nnz] local column (run id) of every nnz in original (CSR) order
+  n_uniq         int32[1] device counter U
+  grad / hess    float[cap] buffers zeroed for the segments (backward targets)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from .keymix import mix, to_unsigned_order
+from .native import hipops, is_gpu
+
+
+@dataclass
+class Localized:
+    uniq: torch.Tensor
+    seg_start: torch.Tensor
+    pos_s: torch.Tensor
+    segid: torch.Tensor
+    local_col: torch.Tensor
+    n_uniq: torch.Tensor  # int32[1] (device)
+    grad: torch.Tensor
+    hess: torch.Tensor | None
+    nnz: int
+
+    def num_unique(self) -> int:  # host sync
+        return int(self.n_uniq.item())
+
+
+class Localizer:
+    """Reusable localisation workspace for up to ``max_nnz`` keys per call."""
+
+    def __init__(self, max_nnz: int, bits: int, device="cpu", with_hess: bool = False):
+        self.max_nnz = int(max_nnz)
+        self.bits = int(bits)
+        self.device = torch.device(device)
+        self.with_hess = with_hess
+        n = self.max_nnz
+        dev = self.device
+        self.gpu = dev.type == "cuda"
+        if self.gpu:
+            H = hipops()
+            self.h = torch.empty(n, dtype=torch.int64, device=dev)
+            self.hs = torch.empty(n, dtype=torch.int64, device=dev)
+            self.pos = torch.empty(n, dtype=torch.int32, device=dev)
+            self.pos_s = torch.empty(n, dtype=torch.int32, device=dev)
+            self.flags = torch.empty(n, dtype=torch.int32, device=dev)
+            self.segid = torch.empty(n, dtype=torch.int32, device=dev)
+            self.uniq = torch.empty(n, dtype=torch.int64, device=dev)
+            self.seg_start = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            self.local_col = torch.empty(n, dtype=torch.int32, device=dev)
+            self.n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.grad = torch.empty(n, dtype=torch.float32, device=dev)
+            self.hess = torch.empty(n, dtype=torch.float32, device=dev) if with_hess else None
+            self.sort_temp = torch.empty(max(1, H.sort_pairs_temp_bytes(n, self.bits)),
+                                         dtype=torch.uint8, device=dev)
+            self.scan_temp = torch.empty(max(1, H.scan_temp_bytes(n)), dtype=torch.uint8,
+                                         device=dev)
+
+    def __call__(self, keys: torch.Tensor) -> Localized:
+        n = keys.numel()
+        if n > self.max_nnz:
+            raise ValueError(f"minibatch has {n} keys > workspace {self.max_nnz}")
+        if n == 0:
+            raise ValueError("empty minibatch")
+        if self.gpu and is_gpu(keys):
+            return self._gpu(keys.contiguous(), n)
+        return localize_torch(keys, self.bits, self.with_hess)
+
+    def _gpu(self, keys, n) -> Localized:
+        H = hipops()
+        H.mix_iota(keys, self.bits, self.h, self.pos)
+        H.sort_pairs(self.sort_temp, self.h, self.hs, self.pos, self.pos_s, n, self.bits)
+        H.rle(self.hs, self.pos_s, n, self.flags, self.segid, self.scan_temp, self.uniq,
+              self.seg_start, self.local_col, self.n_uniq, self.grad, self.hess)
+        return Localized(self.uniq, self.seg_start, self.pos_s[:n], self.segid[:n],
+                         self.local_col[:n], self.n_uniq, self.grad, self.hess, n)
+
+
+def localize_torch(keys: torch.Tensor, bits: int, with_hess: bool = False) -> Localized:
+    """Plain-PyTorch localisation (CPU path and numerics reference)."""
+    h = mix(keys.contiguous(), bits)
+    order_key = to_unsigned_order(h) if bits == 64 else h
+    sk, perm = torch.sort(order_key, stable=True)
+    hs = h[perm]
+    uniq, counts = torch.unique_consecutive(hs, return_counts=True)
+    U = uniq.numel()
+    seg = torch.repeat_interleave(torch.arange(U, device=keys.device), counts)
+    local_col = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
+    local_col[perm] = seg.to(torch.int32)
+    seg_start = torch.zeros(U + 1, dtype=torch.int32, device=keys.device)
+    seg_start[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    return Localized(uniq, seg_start, perm.to(torch.int32), (seg + 1).to(torch.int32), local_col,
+                     torch.tensor([U], dtype=torch.int32, device=keys.device),
+                     torch.zeros(U, dtype=torch.float32, device=keys.device),
+                     torch.zeros(U, dtype=torch.float32, device=keys.device) if with_hess else None,
+                     keys.numel())

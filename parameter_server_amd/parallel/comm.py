@@ -1,0 +1,117 @@
+"""Data-plane communicator: variable-size all-to-all over RCCL (xGMI) or gloo.
+
+The reference moves every push/pull as ZeroMQ point-to-point messages through
+per-process send/recv threads (src/system/van.cc:117-223). On an MI355X node
+every rank is a colocated worker + server shard and a push or pull step is ONE
+grouped all-to-all-v (``torch.distributed.all_to_all_single`` -> RCCL
+``ncclSend/ncclRecv`` in a group, one direct xGMI link per peer pair), preceded by
+a tiny all-to-all of the per-peer element counts.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    rank = 0
+    world = 1
+
+    def exchange_counts(self, send_counts: torch.Tensor) -> torch.Tensor:
+        return send_counts.clone()
+
+    def all_to_all_v(self, send: torch.Tensor, send_counts, recv_counts) -> torch.Tensor:
+        return send
+
+    def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
+        return t
+
+    def all_gather_obj(self, obj):
+        return [obj]
+
+    def barrier(self):
+        pass
+
+    def bytes_moved(self) -> int:
+        return 0
+
+
+class LocalComm(Comm):
+    """Single rank: identity exchanges."""
+
+    def __init__(self, device="cpu"):
+        self.device = torch.device(device)
+
+
+class DistComm(Comm):
+    """torch.distributed process group (nccl = RCCL on ROCm, or gloo on CPU)."""
+
+    def __init__(self, device=None, group=None):
+        assert dist.is_initialized(), "init_process_group first"
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self._sent = 0
+
+    def exchange_counts(self, send_counts: torch.Tensor) -> torch.Tensor:
+        sc = send_counts.to(torch.int64)
+        if self.backend == "nccl" and not sc.is_cuda:
+            sc = sc.to(self.device)
+        elif self.backend == "gloo" and sc.is_cuda:
+            sc = sc.cpu()
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc.contiguous(), group=self.group)
+        return rc
+
+    def all_to_all_v(self, send: torch.Tensor, send_counts, recv_counts) -> torch.Tensor:
+        sc = [int(x) for x in send_counts]
+        rc = [int(x) for x in recv_counts]
+        out = torch.empty((sum(rc),) + tuple(send.shape[1:]), dtype=send.dtype,
+                          device=send.device)
+        dist.all_to_all_single(out, send.contiguous(), output_split_sizes=rc,
+                               input_split_sizes=sc, group=self.group)
+        self._sent += send.element_size() * (sum(sc) - sc[self.rank]) * max(1, send[0:1].numel())
+        return out
+
+    def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
+        ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+        dist.all_reduce(t, op=ops[op], group=self.group)
+        return t
+
+    def all_gather_obj(self, obj):
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def barrier(self):
+        if self.backend == "nccl":
+            dist.barrier(group=self.group, device_ids=[self.device.index or 0])
+        else:
+            dist.barrier(group=self.group)
+
+    def bytes_moved(self) -> int:
+        return self._sent
+
+
+def init_from_env(device_type: str = "cuda", backend: str | None = None):
+    """Initialise torch.distributed from torchrun env vars; returns (Comm, device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if device_type == "cuda":
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+    if world <= 1:
+        return LocalComm(device), device
+    if not dist.is_initialized():
+        backend = backend or ("nccl" if device_type == "cuda" else "gloo")
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(backend=backend, **kw)
+    return DistComm(device), device

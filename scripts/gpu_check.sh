@@ -1,0 +1,21 @@
+#!/bin/bash
+# GPU round: tests, smoke, bench, kernel profile. Each GPU step has its own time
+# limit; a fault / abort / timeout stops the script (test failures do not).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
+timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+ok $rc || exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-50} --warmup 10 > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
+[ $rc -eq 0 ] || exit $rc
+if [ "${PROFILE:-1}" = "1" ]; then
+  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --graph 0 > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1
+  rc=$?; echo "prof rc=$rc"
+fi
+exit 0

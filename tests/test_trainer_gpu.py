@@ -1,0 +1,63 @@
+import pytest
+import torch
+
+from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+from parameter_server_amd.ops.synthetic import criteo_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("algo", ["ftrl", "adagrad", "sgd"])
+def test_trainer_gpu_matches_cpu(algo):
+    cfg = SparseLRConfig(num_features=10 ** 7, minibatch=2048, table_capacity=1 << 18, algo=algo,
+                         alpha=0.05, beta=1.0, l1=1.0, l2=0.1)
+    trs = [SparseLRTrainer(cfg, device=d) for d in ("cpu", "cuda")]
+    for s in range(6):
+        k, l = criteo_batch(2048, seed=3, row0=s * 2048, num_features=cfg.num_features,
+                            cards=[1000] * 26, device="cuda")
+        for tr in trs:
+            tr.step(k.to(tr.device), l.to(tr.device), width=39)
+    p = [tr.progress() for tr in trs]
+    assert abs(p[0]["loss"] - p[1]["loss"]) < 1e-4
+    assert abs(p[0]["accuracy"] - p[1]["accuracy"]) < 1e-3
+    assert abs(p[0]["nnz_w"] - p[1]["nnz_w"]) <= 2
+    sd = [tr.state_dict() for tr in trs]
+    a = dict(zip(sd[0]["keys"].tolist(), sd[0]["w"].tolist()))
+    b = dict(zip(sd[1]["keys"].tolist(), sd[1]["w"].tolist()))
+    assert a.keys() == b.keys()
+    worst = max(abs(a[k] - b[k]) for k in a)
+    assert worst < 1e-4
+
+
+def test_trainer_gpu_loss_decreases_and_graph_capture():
+    cfg = SparseLRConfig(num_features=10 ** 9, minibatch=8192, table_capacity=1 << 22)
+    tr = SparseLRTrainer(cfg, device="cuda")
+    keys = torch.empty(8192 * 39, dtype=torch.int64, device="cuda")
+    labels = torch.empty(8192, device="cuda")
+    row0 = torch.zeros(1, dtype=torch.int64, device="cuda")
+    from parameter_server_amd.ops.native import hipops
+
+    def step():
+        criteo_batch(8192, seed=9, row0=0, num_features=cfg.num_features, device="cuda",
+                     keys=keys, labels=labels, row0_dev=row0)
+        tr.step(keys, labels, width=39)
+        hipops().add_i64(row0, 8192)
+
+    step()
+    first = tr.progress()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for _ in range(40):
+        g.replay()
+    torch.cuda.synchronize()
+    assert int(row0.item()) == 8192 * 43
+    last = tr.progress()
+    assert last["examples"] == 41 * 8192
+    assert last["loss"] < first["loss"]
+    tr.table.check_ok()
