@@ -91,4 +91,6 @@ PYBIND11_MODULE(_pscore, m) {
   });
 
   register_util(m);
+  register_data(m);
+  register_runtime(m);
 }

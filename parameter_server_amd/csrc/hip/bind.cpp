@@ -15,21 +15,26 @@ namespace psamd {
 void kv_init(void*, int64_t, hipStream_t);
 void kv_resolve(void*, int64_t, const uint64_t*, int64_t, const int32_t*, int64_t*, float*, bool,
                 int, float, float, uint64_t, int32_t*, int32_t*, hipStream_t);
-void kv_gather(const void*, const int64_t*, int64_t, const int32_t*, float*, int, hipStream_t);
-void kv_set(void*, const int64_t*, int64_t, const float*, const float*, const float*, hipStream_t);
-void kv_update(void*, const int64_t*, const float*, int64_t, const int32_t*, int, int, float, float,
-               float, float, float, float, double*, hipStream_t);
-void kv_accumulate(void*, const int64_t*, const float*, int64_t, const int32_t*, int64_t*, int32_t*,
-                   hipStream_t);
-void kv_apply_accumulated(void*, const int64_t*, const int32_t*, int64_t, int, int, float, float,
-                          float, float, float, float, double*, hipStream_t);
+void kv_gather(const void*, int64_t, const int64_t*, int64_t, const int32_t*, float*, int,
+               hipStream_t);
+void kv_set(void*, int64_t, const int64_t*, int64_t, const float*, const float*, const float*,
+            hipStream_t);
+void kv_update(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int, int,
+               float, float, float, float, float, float, double*, hipStream_t);
+void kv_accumulate(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int64_t*,
+                   int32_t*, hipStream_t);
+void kv_apply_accumulated(void*, int64_t, const int64_t*, const int32_t*, int64_t, int, int, float,
+                          float, float, float, float, float, double*, hipStream_t);
 void kv_census(const void*, int64_t, unsigned long long*, hipStream_t);
 // localize.hip
 void mix_iota(const uint64_t*, int64_t, KeyMix, uint64_t*, int32_t*, hipStream_t);
 void mix_keys(const uint64_t*, int64_t, KeyMix, uint64_t*, bool, hipStream_t);
-size_t sort_pairs_temp_bytes(int64_t, int);
-void sort_pairs(void*, size_t, const uint64_t*, uint64_t*, const int32_t*, int32_t*, int64_t, int,
-                hipStream_t);
+size_t rocprim_sort_temp_bytes(int64_t, int);
+void rocprim_sort_pairs(void*, size_t, const uint64_t*, uint64_t*, const int32_t*, int32_t*,
+                        int64_t, int, hipStream_t);
+size_t radix_sort_temp_bytes(int64_t);
+void radix_sort_pairs(void*, size_t, const uint64_t*, uint64_t*, const int32_t*, int32_t*, int64_t,
+                      int, hipStream_t);
 size_t scan_temp_bytes(int64_t);
 void inclusive_scan_i32(void*, size_t, const int32_t*, int32_t*, int64_t, hipStream_t);
 void rle(const uint64_t*, const int32_t*, int64_t, int32_t*, int32_t*, void*, size_t, uint64_t*,
@@ -39,10 +44,10 @@ void owner_split(const uint64_t*, const int32_t*, int64_t, const uint64_t*, int,
                  hipStream_t);
 void owner_of(const uint64_t*, int64_t, const uint64_t*, int, int32_t*, hipStream_t);
 // linear.hip
-void linear_fwd(const int64_t*, int64_t, int, const int32_t*, const float*, const float*,
+void linear_fwd(const int64_t*, int64_t, int, const int32_t*, const float*, const float*, int64_t,
                 const float*, int, float*, float*, float*, double*, uint32_t*, int, hipStream_t);
 void linear_bwd(const int32_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
-                const float*, const float*, float*, float*, hipStream_t);
+                const float*, int64_t, const float*, float*, float*, int64_t, hipStream_t);
 void auc_from_hist(uint32_t*, int, double*, hipStream_t);
 void csr_rows(const int64_t*, int64_t, int32_t*, hipStream_t);
 void criteo_set_cards(const uint32_t*);
@@ -153,35 +158,35 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("kv_gather", [](Tensor slots, Tensor slot_idx, optional<Tensor> n_dev, Tensor out,
                         int field) {
-    slot_capacity(slots);
+    const int64_t cap = slot_capacity(slots);
     chk(slot_idx, at::kLong, "slot_idx");
     chk(out, at::kFloat, "out");
     check(field >= 0 && field < 4, "field in [0,4): w,z,n,acc");
     check(out.numel() >= slot_idx.numel(), "out too small");
-    psamd::kv_gather(slots.data_ptr(), ptr<int64_t>(slot_idx), slot_idx.numel(),
+    psamd::kv_gather(slots.data_ptr(), cap, ptr<int64_t>(slot_idx), slot_idx.numel(),
                      optr<int32_t>(n_dev, at::kInt, "n_dev"), ptr<float>(out), field,
                      cur_stream());
   });
   m.def("kv_set", [](Tensor slots, Tensor slot_idx, optional<Tensor> w, optional<Tensor> z,
                      optional<Tensor> nn) {
-    slot_capacity(slots);
+    const int64_t cap = slot_capacity(slots);
     chk(slot_idx, at::kLong, "slot_idx");
     const int64_t n = slot_idx.numel();
     for (auto* t : {&w, &z, &nn})
       if (t->has_value()) check((*t)->numel() >= n, "value array too small");
-    psamd::kv_set(slots.data_ptr(), ptr<int64_t>(slot_idx), n, optr<float>(w, at::kFloat, "w"),
+    psamd::kv_set(slots.data_ptr(), cap, ptr<int64_t>(slot_idx), n, optr<float>(w, at::kFloat, "w"),
                   optr<float>(z, at::kFloat, "z"), optr<float>(nn, at::kFloat, "n"),
                   cur_stream());
   });
   m.def("kv_update", [](Tensor slots, Tensor slot_idx, Tensor grad, optional<Tensor> n_dev,
                         int algo, int lr_type, double alpha, double beta, double l1, double l2,
                         double grad_scale, double max_delta, optional<Tensor> stats) {
-    slot_capacity(slots);
+    const int64_t cap = slot_capacity(slots);
     chk(slot_idx, at::kLong, "slot_idx");
     chk(grad, at::kFloat, "grad");
     check(grad.numel() >= slot_idx.numel(), "grad too small");
     check(alpha > 0, "learning rate alpha must be > 0");
-    psamd::kv_update(slots.data_ptr(), ptr<int64_t>(slot_idx), ptr<float>(grad),
+    psamd::kv_update(slots.data_ptr(), cap, ptr<int64_t>(slot_idx), ptr<float>(grad),
                      slot_idx.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"), algo, lr_type,
                      (float)alpha, (float)beta, (float)l1, (float)l2, (float)grad_scale,
                      (float)max_delta, optr<double>(stats, at::kDouble, "stats"), cur_stream());
@@ -193,19 +198,18 @@ PYBIND11_MODULE(_hipops, m) {
     chk(grad, at::kFloat, "grad");
     chk(touched, at::kLong, "touched");
     chk(n_touched, at::kInt, "n_touched");
-    check(touched.numel() >= std::min<int64_t>(cap, slot_idx.numel()) || touched.numel() >= cap,
-          "touched buffer too small");
-    psamd::kv_accumulate(slots.data_ptr(), ptr<int64_t>(slot_idx), ptr<float>(grad),
+    check(touched.numel() >= slot_idx.numel(), "touched buffer too small");
+    psamd::kv_accumulate(slots.data_ptr(), cap, ptr<int64_t>(slot_idx), ptr<float>(grad),
                          slot_idx.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"),
                          ptr<int64_t>(touched), ptr<int32_t>(n_touched), cur_stream());
   });
   m.def("kv_apply_accumulated", [](Tensor slots, Tensor touched, Tensor n_touched, int algo,
                                    int lr_type, double alpha, double beta, double l1, double l2,
                                    double grad_scale, double max_delta, optional<Tensor> stats) {
-    slot_capacity(slots);
+    const int64_t cap = slot_capacity(slots);
     chk(touched, at::kLong, "touched");
     chk(n_touched, at::kInt, "n_touched");
-    psamd::kv_apply_accumulated(slots.data_ptr(), ptr<int64_t>(touched), ptr<int32_t>(n_touched),
+    psamd::kv_apply_accumulated(slots.data_ptr(), cap, ptr<int64_t>(touched), ptr<int32_t>(n_touched),
                                 touched.numel(), algo, lr_type, (float)alpha, (float)beta,
                                 (float)l1, (float)l2, (float)grad_scale, (float)max_delta,
                                 optr<double>(stats, at::kDouble, "stats"), cur_stream());
@@ -234,11 +238,12 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::mix_keys(ptr<uint64_t>(keys), keys.numel(), make_keymix(bits), ptr<uint64_t>(out),
                     inverse, cur_stream());
   });
-  m.def("sort_pairs_temp_bytes", [](int64_t n, int end_bit) {
-    return (int64_t)psamd::sort_pairs_temp_bytes(n, end_bit);
-  });
+  m.def("sort_pairs_temp_bytes", [](int64_t n, int end_bit, bool rocprim) {
+    return (int64_t)(rocprim ? psamd::rocprim_sort_temp_bytes(n, end_bit)
+                             : psamd::radix_sort_temp_bytes(n));
+  }, py::arg("n"), py::arg("end_bit"), py::arg("rocprim") = false);
   m.def("sort_pairs", [](Tensor temp, Tensor k_in, Tensor k_out, Tensor v_in, Tensor v_out,
-                         int64_t n, int end_bit) {
+                         int64_t n, int end_bit, bool rocprim) {
     chk(temp, at::kByte, "temp");
     chk(k_in, at::kLong, "k_in");
     chk(k_out, at::kLong, "k_out");
@@ -248,12 +253,21 @@ PYBIND11_MODULE(_hipops, m) {
               v_out.numel() >= n, "sort buffers too small");
     check(n < (int64_t)INT32_MAX, "sort size must fit int32");
     check(end_bit >= 1 && end_bit <= 64, "end_bit in [1,64]");
-    const size_t need = psamd::sort_pairs_temp_bytes(n, end_bit);
+    check(k_in.data_ptr() != k_out.data_ptr() && v_in.data_ptr() != v_out.data_ptr(),
+          "sort input and output must not alias");
+    const size_t need = rocprim ? psamd::rocprim_sort_temp_bytes(n, end_bit)
+                                : psamd::radix_sort_temp_bytes(n);
     check((size_t)temp.numel() >= need, "sort temp storage too small");
-    psamd::sort_pairs(temp.data_ptr(), (size_t)temp.numel(), ptr<uint64_t>(k_in),
-                      ptr<uint64_t>(k_out), ptr<int32_t>(v_in), ptr<int32_t>(v_out), n, end_bit,
-                      cur_stream());
-  });
+    if (rocprim)
+      psamd::rocprim_sort_pairs(temp.data_ptr(), (size_t)temp.numel(), ptr<uint64_t>(k_in),
+                                ptr<uint64_t>(k_out), ptr<int32_t>(v_in), ptr<int32_t>(v_out), n,
+                                end_bit, cur_stream());
+    else
+      psamd::radix_sort_pairs(temp.data_ptr(), (size_t)temp.numel(), ptr<uint64_t>(k_in),
+                              ptr<uint64_t>(k_out), ptr<int32_t>(v_in), ptr<int32_t>(v_out), n,
+                              end_bit, cur_stream());
+  }, py::arg("temp"), py::arg("k_in"), py::arg("k_out"), py::arg("v_in"), py::arg("v_out"),
+     py::arg("n"), py::arg("end_bit"), py::arg("rocprim") = false);
   m.def("scan_temp_bytes", [](int64_t n) { return (int64_t)psamd::scan_temp_bytes(n); });
   m.def("inclusive_scan_i32", [](Tensor temp, Tensor in, Tensor out, int64_t n) {
     chk(temp, at::kByte, "temp");
@@ -342,7 +356,7 @@ PYBIND11_MODULE(_hipops, m) {
     double* mp = optr<double>(metrics, at::kDouble, "metrics");
     if (mp) check(metrics->numel() >= 5, "metrics needs >= 5 slots");
     psamd::linear_fwd(rp, B, width, ptr<int32_t>(local_col), v, ptr<float>(w_local),
-                      ptr<float>(labels), loss_type, xp, ptr<float>(coef), c2, mp, hp, nbins,
+                      w_local.numel(), ptr<float>(labels), loss_type, xp, ptr<float>(coef), c2, mp, hp, nbins,
                       cur_stream());
   });
   m.def("linear_bwd", [](Tensor pos_s, Tensor segid, int64_t n, optional<Tensor> rows, int width,
@@ -359,9 +373,10 @@ PYBIND11_MODULE(_hipops, m) {
     float* h = optr<float>(hess, at::kFloat, "hess");
     const float* c2 = optr<float>(coef2, at::kFloat, "coef2");
     check(!h || c2, "hess requires coef2");
+    if (h) check(hess->numel() >= grad.numel(), "hess smaller than grad");
     psamd::linear_bwd(ptr<int32_t>(pos_s), ptr<int32_t>(segid), n, r, width,
-                      optr<float>(vals, at::kFloat, "vals"), ptr<float>(coef), c2,
-                      ptr<float>(grad), h, cur_stream());
+                      optr<float>(vals, at::kFloat, "vals"), ptr<float>(coef), coef.numel(), c2,
+                      ptr<float>(grad), h, grad.numel(), cur_stream());
   });
   m.def("auc_from_hist", [](Tensor hist, int nbins, Tensor metrics) {
     chk(hist, at::kInt, "hist");

@@ -74,9 +74,17 @@ inline int grid_for(int64_t n, int block, int max_blocks = 2048) {
   return (int)g;
 }
 
-// Valid length: from a device counter if given, else the host-provided n.
+// Valid length: from a device counter if given (clamped to the host capacity so a
+// corrupted counter can never drive an out-of-bounds access), else the host n.
 __device__ __forceinline__ int64_t dev_len(const int32_t* n_dev, int64_t n_host) {
-  return n_dev ? (int64_t)(*n_dev) : n_host;
+  if (!n_dev) return n_host;
+  const int64_t d = (int64_t)(*n_dev);
+  return d < 0 ? 0 : (d > n_host ? n_host : d);
+}
+
+// Index guard for gathered / scattered indices.
+__device__ __forceinline__ bool in_range(int64_t i, int64_t cap) {
+  return (uint64_t)i < (uint64_t)cap;
 }
 
 // Wave-level reductions (64 lanes) -------------------------------------------

@@ -126,7 +126,7 @@ __global__ void kv_resolve_kernel(Slot* __restrict__ slots, uint64_t mask,
 }
 
 // out[i] = slot.w (0 for missing), gathered by cached slot index.
-__global__ void kv_gather_kernel(const Slot* __restrict__ slots,
+__global__ void kv_gather_kernel(const Slot* __restrict__ slots, int64_t cap,
                                  const int64_t* __restrict__ slot_idx, int64_t n_host,
                                  const int32_t* __restrict__ n_dev, float* __restrict__ out,
                                  int field) {
@@ -135,7 +135,7 @@ __global__ void kv_gather_kernel(const Slot* __restrict__ slots,
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = slot_idx[i];
     float v = 0.f;
-    if (s >= 0) {
+    if (in_range(s, cap)) {
       const float* f = &slots[s].w;
       v = f[field];
     }
@@ -144,13 +144,14 @@ __global__ void kv_gather_kernel(const Slot* __restrict__ slots,
 }
 
 // Set fields (checkpoint restore / explicit assignment).
-__global__ void kv_set_kernel(Slot* __restrict__ slots, const int64_t* __restrict__ slot_idx,
+__global__ void kv_set_kernel(Slot* __restrict__ slots, int64_t cap,
+                              const int64_t* __restrict__ slot_idx,
                               int64_t n, const float* __restrict__ w,
                               const float* __restrict__ z, const float* __restrict__ nn) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = slot_idx[i];
-    if (s < 0) continue;
+    if (!in_range(s, cap)) continue;
     if (w) slots[s].w = w[i];
     if (z) slots[s].z = z[i];
     if (nn) slots[s].n = nn[i];
@@ -199,7 +200,8 @@ __device__ __forceinline__ float apply_update(Slot& s, float g, const UpdatePara
 
 // Apply one pushed gradient per (unique within this launch) slot.
 // stats: [0] nnz delta (as double), [1] sum w_new^2, [2] sum (w_new-w_old)^2.
-__global__ void kv_update_kernel(Slot* __restrict__ slots, const int64_t* __restrict__ slot_idx,
+__global__ void kv_update_kernel(Slot* __restrict__ slots, int64_t cap,
+                                 const int64_t* __restrict__ slot_idx,
                                  const float* __restrict__ grad, int64_t n_host,
                                  const int32_t* __restrict__ n_dev, UpdateParams p,
                                  double* __restrict__ stats) {
@@ -209,7 +211,7 @@ __global__ void kv_update_kernel(Slot* __restrict__ slots, const int64_t* __rest
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t si = slot_idx[i];
-    if (si < 0) continue;
+    if (!in_range(si, cap)) continue;
     const float g = grad[i] * p.grad_scale;
     if (g != g) continue;  // NaN mark = filtered entry (reference SparseFilter)
     Slot s = slots[si];
@@ -233,7 +235,8 @@ __global__ void kv_update_kernel(Slot* __restrict__ slots, const int64_t* __rest
 }
 
 // Synchronous aggregation: acc += g; first toucher appends the slot to a list.
-__global__ void kv_accumulate_kernel(Slot* __restrict__ slots, const int64_t* __restrict__ slot_idx,
+__global__ void kv_accumulate_kernel(Slot* __restrict__ slots, int64_t cap,
+                                     const int64_t* __restrict__ slot_idx,
                                      const float* __restrict__ grad, int64_t n_host,
                                      const int32_t* __restrict__ n_dev,
                                      int64_t* __restrict__ touched, int32_t* __restrict__ n_touched) {
@@ -241,27 +244,28 @@ __global__ void kv_accumulate_kernel(Slot* __restrict__ slots, const int64_t* __
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t si = slot_idx[i];
-    if (si < 0) continue;
+    if (!in_range(si, cap)) continue;
     const float g = grad[i];
     if (g != g) continue;
     atomicAdd(&slots[si].acc, g);
     if (atomicOr(&slots[si].flags, 1u) == 0u) {
       int pos = atomicAdd(n_touched, 1);
-      touched[pos] = si;
+      if (pos < n_host) touched[pos] = si;
     }
   }
 }
 
-__global__ void kv_apply_accumulated_kernel(Slot* __restrict__ slots,
+__global__ void kv_apply_accumulated_kernel(Slot* __restrict__ slots, int64_t cap,
                                             const int64_t* __restrict__ touched,
-                                            const int32_t* __restrict__ n_touched, UpdateParams p,
-                                            double* __restrict__ stats) {
+                                            const int32_t* __restrict__ n_touched, int64_t max_n,
+                                            UpdateParams p, double* __restrict__ stats) {
   __shared__ double lds[16];
-  const int64_t n = *n_touched;
+  const int64_t n = dev_len(n_touched, max_n);
   double dnnz = 0, wsum = 0, dsum = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t si = touched[i];
+    if (!in_range(si, cap)) continue;
     Slot s = slots[si];
     const float g = s.acc * p.grad_scale;
     s.acc = 0.f;
@@ -321,48 +325,49 @@ void kv_resolve(void* slots, int64_t cap, const uint64_t* keys, int64_t n, const
       insert ? 1 : 0, init_type, init_v, init_s, seed, err, inserted);
   PSAMD_HIP_CHECK(hipGetLastError());
   if (out_w && !fused_w) {
-    kv_gather_kernel<<<grid_for(n, 256), 256, 0, st>>>((const Slot*)slots, out_slot, n, n_dev,
-                                                       out_w, 0);
+    kv_gather_kernel<<<grid_for(n, 256), 256, 0, st>>>((const Slot*)slots, cap, out_slot, n,
+                                                       n_dev, out_w, 0);
     PSAMD_HIP_CHECK(hipGetLastError());
   }
 }
 
-void kv_gather(const void* slots, const int64_t* slot_idx, int64_t n, const int32_t* n_dev,
-               float* out, int field, hipStream_t st) {
-  kv_gather_kernel<<<grid_for(n, 256), 256, 0, st>>>((const Slot*)slots, slot_idx, n, n_dev, out,
-                                                     field);
+void kv_gather(const void* slots, int64_t cap, const int64_t* slot_idx, int64_t n,
+               const int32_t* n_dev, float* out, int field, hipStream_t st) {
+  kv_gather_kernel<<<grid_for(n, 256), 256, 0, st>>>((const Slot*)slots, cap, slot_idx, n, n_dev,
+                                                     out, field);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void kv_set(void* slots, const int64_t* slot_idx, int64_t n, const float* w, const float* z,
-            const float* nn, hipStream_t st) {
-  kv_set_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, slot_idx, n, w, z, nn);
+void kv_set(void* slots, int64_t cap, const int64_t* slot_idx, int64_t n, const float* w,
+            const float* z, const float* nn, hipStream_t st) {
+  kv_set_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, cap, slot_idx, n, w, z, nn);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void kv_update(void* slots, const int64_t* slot_idx, const float* grad, int64_t n,
+void kv_update(void* slots, int64_t cap, const int64_t* slot_idx, const float* grad, int64_t n,
                const int32_t* n_dev, int algo, int lr_type, float alpha, float beta, float l1,
                float l2, float grad_scale, float max_delta, double* stats, hipStream_t st) {
   UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
-  kv_update_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, slot_idx, grad, n, n_dev, p,
-                                                     stats);
+  kv_update_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, cap, slot_idx, grad, n, n_dev,
+                                                     p, stats);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void kv_accumulate(void* slots, const int64_t* slot_idx, const float* grad, int64_t n,
-                   const int32_t* n_dev, int64_t* touched, int32_t* n_touched, hipStream_t st) {
-  kv_accumulate_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, slot_idx, grad, n, n_dev,
-                                                         touched, n_touched);
+void kv_accumulate(void* slots, int64_t cap, const int64_t* slot_idx, const float* grad,
+                   int64_t n, const int32_t* n_dev, int64_t* touched, int32_t* n_touched,
+                   hipStream_t st) {
+  kv_accumulate_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, cap, slot_idx, grad, n,
+                                                         n_dev, touched, n_touched);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void kv_apply_accumulated(void* slots, const int64_t* touched, const int32_t* n_touched,
+void kv_apply_accumulated(void* slots, int64_t cap, const int64_t* touched, const int32_t* n_touched,
                           int64_t max_n, int algo, int lr_type, float alpha, float beta, float l1,
                           float l2, float grad_scale, float max_delta, double* stats,
                           hipStream_t st) {
   UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
-  kv_apply_accumulated_kernel<<<grid_for(max_n, 256), 256, 0, st>>>((Slot*)slots, touched,
-                                                                    n_touched, p, stats);
+  kv_apply_accumulated_kernel<<<grid_for(max_n, 256), 256, 0, st>>>((Slot*)slots, cap, touched,
+                                                                    n_touched, max_n, p, stats);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

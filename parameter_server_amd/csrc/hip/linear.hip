@@ -29,7 +29,8 @@ template <bool kHasRowPtr>
 __global__ void __launch_bounds__(256)
 linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
                   const int32_t* __restrict__ local_col, const float* __restrict__ vals,
-                  const float* __restrict__ w_local, const float* __restrict__ labels,
+                  const float* __restrict__ w_local, int64_t w_cap,
+                  const float* __restrict__ labels,
                   int loss_type, float* __restrict__ xw_out, float* __restrict__ coef_out,
                   float* __restrict__ coef2_out, double* __restrict__ metrics,
                   uint32_t* __restrict__ hist, int nbins) {
@@ -49,12 +50,12 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
     if (vals) {
       for (int64_t k = b; k < e; ++k) {
         const int32_t c = local_col[k];
-        if (c >= 0) m += w_local[c] * vals[k];
+        if (in_range(c, w_cap)) m += w_local[c] * vals[k];
       }
     } else {
       for (int64_t k = b; k < e; ++k) {
         const int32_t c = local_col[k];
-        if (c >= 0) m += w_local[c];
+        if (in_range(c, w_cap)) m += w_local[c];
       }
     }
     const float y = labels[r] > 0.f ? 1.f : -1.f;
@@ -89,8 +90,8 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
     cnt += 1.0;
     if (hist) {
       const float p = 1.f / (1.f + expf(-m));
-      int bin = (int)(p * nbins);
-      bin = bin < 0 ? 0 : (bin >= nbins ? nbins - 1 : bin);
+      const float pb = p == p ? fminf(fmaxf(p * nbins, 0.f), (float)(nbins - 1)) : 0.f;
+      const int bin = (int)pb;
       atomicAdd(&lhist[(y > 0.f ? nbins : 0) + bin], 1u);
     }
   }
@@ -115,9 +116,9 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
 __global__ void __launch_bounds__(256)
 linear_bwd_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ segid,
                   int64_t n, const int32_t* __restrict__ rows, int width,
-                  const float* __restrict__ vals, const float* __restrict__ coef,
+                  const float* __restrict__ vals, const float* __restrict__ coef, int64_t B,
                   const float* __restrict__ coef2, float* __restrict__ grad,
-                  float* __restrict__ hess) {
+                  float* __restrict__ hess, int64_t grad_cap) {
   const int lane = threadIdx.x & 63;
   // One element per lane; each wavefront is one segmented-scan unit.
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -130,10 +131,14 @@ linear_bwd_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__
     if (valid) {
       s = segid[i];
       const int32_t p = pos_s[i];
-      const int32_t r = rows ? rows[p] : p / width;
-      const float x = vals ? vals[p] : 1.f;
-      v = coef[r] * x;
-      if (hess) v2 = coef2[r] * x * x;
+      if (in_range(p, n)) {
+        const int32_t r = rows ? rows[p] : p / width;
+        if (in_range(r, B)) {
+          const float x = vals ? vals[p] : 1.f;
+          v = coef[r] * x;
+          if (hess) v2 = coef2[r] * x * x;
+        }
+      }
     }
     // segmented inclusive scan (Hillis-Steele) over 64 lanes
 #pragma unroll
@@ -154,7 +159,9 @@ linear_bwd_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__
       bool ends_inside = true;
       if (lane == 63 && i + 1 < n) ends_inside = segid[i + 1] != s;
       const int32_t u = s - 1;
-      if (starts_inside && ends_inside) {
+      if (!in_range(u, grad_cap)) {
+        // corrupted segment id: drop (never write out of bounds)
+      } else if (starts_inside && ends_inside) {
         grad[u] = v;
         if (hess) hess[u] = v2;
       } else {
@@ -264,27 +271,28 @@ criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_
 
 // ---------------------------------------------------------------------------
 void linear_fwd(const int64_t* row_ptr, int64_t B, int width, const int32_t* local_col,
-                const float* vals, const float* w_local, const float* labels, int loss_type,
+                const float* vals, const float* w_local, int64_t w_cap, const float* labels,
+                int loss_type,
                 float* xw, float* coef, float* coef2, double* metrics, uint32_t* hist, int nbins,
                 hipStream_t st) {
   const size_t lds = hist ? (size_t)2 * nbins * sizeof(uint32_t) : 0;
   const int g = grid_for(B, 256, 4096);
   if (row_ptr)
     linear_fwd_kernel<true><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
-                                                 labels, loss_type, xw, coef, coef2, metrics,
+                                                 w_cap, labels, loss_type, xw, coef, coef2, metrics,
                                                  hist, nbins);
   else
     linear_fwd_kernel<false><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
-                                                  labels, loss_type, xw, coef, coef2, metrics,
+                                                  w_cap, labels, loss_type, xw, coef, coef2, metrics,
                                                   hist, nbins);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
 void linear_bwd(const int32_t* pos_s, const int32_t* segid, int64_t n, const int32_t* rows,
-                int width, const float* vals, const float* coef, const float* coef2, float* grad,
-                float* hess, hipStream_t st) {
+                int width, const float* vals, const float* coef, int64_t B, const float* coef2,
+                float* grad, float* hess, int64_t grad_cap, hipStream_t st) {
   linear_bwd_kernel<<<grid_for(n, 256, 8192), 256, 0, st>>>(pos_s, segid, n, rows, width, vals,
-                                                            coef, coef2, grad, hess);
+                                                            coef, B, coef2, grad, hess, grad_cap);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -55,7 +55,9 @@ __global__ void rle_scatter_kernel(const uint64_t* __restrict__ hs,
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t s = segid[i] - 1;
-    local_col[pos_s[i]] = s;
+    const int32_t p = pos_s[i];
+    if (!in_range(s, n)) continue;  // corrupted scan/sort output: never write OOB
+    if (in_range(p, n)) local_col[p] = s;
     const bool head = (i == 0) || (segid[i - 1] != segid[i]);
     if (head) {
       uniq[s] = hs[i];
@@ -75,7 +77,7 @@ __global__ void rle_scatter_kernel(const uint64_t* __restrict__ hs,
 __global__ void seg_counts_kernel(const int32_t* __restrict__ seg_start,
                                   const int32_t* __restrict__ n_uniq, int64_t cap,
                                   uint8_t* __restrict__ counts, int sat) {
-  const int64_t u_n = *n_uniq;
+  const int64_t u_n = dev_len(n_uniq, cap);
   for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < u_n;
        u += (int64_t)gridDim.x * blockDim.x) {
     int c = seg_start[u + 1] - seg_start[u];
@@ -90,7 +92,7 @@ __global__ void owner_split_kernel(const uint64_t* __restrict__ uniq,
                                    int64_t* __restrict__ offsets) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g > G) return;
-  const int64_t U = n_uniq ? (int64_t)*n_uniq : n_host;
+  const int64_t U = dev_len(n_uniq, n_host);
   if (g == 0) { offsets[0] = 0; return; }
   if (g == G) { offsets[G] = U; return; }
   const uint64_t b = bounds[g];
@@ -131,7 +133,8 @@ void mix_keys(const uint64_t* keys, int64_t n, KeyMix m, uint64_t* h, bool inver
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-size_t sort_pairs_temp_bytes(int64_t n, int end_bit) {
+// rocPRIM reference path (kept for A/B benchmarking; not used by the trainer).
+size_t rocprim_sort_temp_bytes(int64_t n, int end_bit) {
   size_t bytes = 0;
   PSAMD_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(
       nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const int32_t*)nullptr,
@@ -139,22 +142,23 @@ size_t sort_pairs_temp_bytes(int64_t n, int end_bit) {
   return bytes;
 }
 
-void sort_pairs(void* temp, size_t temp_bytes, const uint64_t* k_in, uint64_t* k_out,
-                const int32_t* v_in, int32_t* v_out, int64_t n, int end_bit, hipStream_t st) {
+void rocprim_sort_pairs(void* temp, size_t temp_bytes, const uint64_t* k_in, uint64_t* k_out,
+                        const int32_t* v_in, int32_t* v_out, int64_t n, int end_bit,
+                        hipStream_t st) {
   PSAMD_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, k_in, k_out, v_in, v_out,
                                                      (int)n, 0, end_bit, st));
 }
 
-size_t scan_temp_bytes(int64_t n) {
-  size_t bytes = 0;
-  PSAMD_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, (const int32_t*)nullptr,
-                                                   (int32_t*)nullptr, (int)n, (hipStream_t)0));
-  return bytes;
-}
+size_t scan_i32_temp_bytes(int64_t n);
+void scan_i32(const int32_t* in, int32_t* out, int64_t n, void* temp, bool inclusive,
+              hipStream_t st);
+
+size_t scan_temp_bytes(int64_t n) { return scan_i32_temp_bytes(n); }
 
 void inclusive_scan_i32(void* temp, size_t temp_bytes, const int32_t* in, int32_t* out,
                         int64_t n, hipStream_t st) {
-  PSAMD_HIP_CHECK(hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, in, out, (int)n, st));
+  if (temp_bytes < scan_i32_temp_bytes(n)) throw std::runtime_error("scan temp too small");
+  scan_i32(in, out, n, temp, true, st);
 }
 
 void rle(const uint64_t* hs, const int32_t* pos_s, int64_t n, int32_t* flags, int32_t* segid,

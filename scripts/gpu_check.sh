@@ -4,14 +4,15 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+export PYTHONUNBUFFERED=1
 ok() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
-timeout -k 10 600 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+PYTHONUNBUFFERED=1 timeout -k 10 900 python -m pytest tests -m gpu -x -v --timeout 240 -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
-ok $rc || exit $rc
+[ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-50} --warmup 10 > gpurun_out/bench.log 2>&1
+timeout -k 10 300 python bench.py --steps ${BENCH_STEPS:-50} --warmup 10 --progress > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
 [ $rc -eq 0 ] || exit $rc
 if [ "${PROFILE:-1}" = "1" ]; then

@@ -61,3 +61,46 @@ def test_trainer_gpu_loss_decreases_and_graph_capture():
     assert last["examples"] == 41 * 8192
     assert last["loss"] < first["loss"]
     tr.table.check_ok()
+
+
+def test_graph_replay_matches_eager():
+    """The captured HIP-graph step must produce exactly the eager result."""
+    from parameter_server_amd.ops.native import hipops
+
+    B = 70000  # > 1M keys: the multi-tile sort path
+    outs = []
+    for use_graph in (False, True):
+        cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, table_capacity=1 << 25)
+        tr = SparseLRTrainer(cfg, device="cuda")
+        keys = torch.empty(B * 39, dtype=torch.int64, device="cuda")
+        labels = torch.empty(B, device="cuda")
+        row0 = torch.zeros(1, dtype=torch.int64, device="cuda")
+
+        def step():
+            criteo_batch(B, seed=5, row0=0, num_features=cfg.num_features, device="cuda",
+                         keys=keys, labels=labels, row0_dev=row0)
+            tr.step(keys, labels, width=39)
+            hipops().add_i64(row0, B)
+
+        step()
+        if use_graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                step()
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+            for _ in range(6):
+                g.replay()
+        else:
+            for _ in range(7):
+                step()
+        torch.cuda.synchronize()
+        tr.table.check_ok()
+        outs.append((tr.progress(), tr.table.census(), int(row0.item())))
+    (pe, ce, re_), (pg, cg, rg) = outs
+    assert re_ == rg == 8 * B
+    assert ce == cg
+    assert abs(pe["loss"] - pg["loss"]) < 1e-9 * max(1.0, pe["loss"]) + 1e-7
