@@ -56,7 +56,7 @@ def test_trainer_gpu_loss_decreases_and_graph_capture():
     for _ in range(40):
         g.replay()
     torch.cuda.synchronize()
-    assert int(row0.item()) == 8192 * 43
+    assert int(row0.item()) == 8192 * 42  # capture itself does not execute
     last = tr.progress()
     assert last["examples"] == 41 * 8192
     assert last["loss"] < first["loss"]
