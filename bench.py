@@ -60,20 +60,19 @@ def main():
     tr = SparseLRTrainer(cfg, comm, device)
     keys = torch.empty(B * 39, dtype=torch.int64, device=device)
     labels = torch.empty(B, dtype=torch.float32, device=device)
-    row0 = torch.zeros(1, dtype=torch.int64, device=device)
     seed = 1000003 * (rank + 1)
     gpu = device.type == "cuda"
 
     def one_step():
-        criteo_batch(B, seed=seed, row0=0, num_features=N, device=device, keys=keys,
-                     labels=labels, row0_dev=row0 if gpu else None)
-        tr.step(keys, labels, width=39)
+        # fresh rows every step: row0 = device step clock * B (advanced by the
+        # trainer's epilogue kernel, so graph replays generate new data)
         if gpu:
-            from parameter_server_amd.ops.native import hipops
-
-            hipops().add_i64(row0, B)
+            criteo_batch(B, seed=seed, row0=0, num_features=N, device=device, keys=keys,
+                         labels=labels, row0_dev=tr.step_dev, row_scale=B)
         else:
-            row0.add_(B)
+            criteo_batch(B, seed=seed, row0=tr.step_count * B, num_features=N, device=device,
+                         keys=keys, labels=labels)
+        tr.step(keys, labels, width=39)
 
     run = one_step
     graph_used = False

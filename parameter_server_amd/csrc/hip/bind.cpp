@@ -43,16 +43,20 @@ void seg_counts(const int32_t*, const int32_t*, int64_t, uint8_t*, int, hipStrea
 void owner_split(const uint64_t*, const int32_t*, int64_t, const uint64_t*, int, int64_t*,
                  hipStream_t);
 void owner_of(const uint64_t*, int64_t, const uint64_t*, int, int32_t*, hipStream_t);
+// sort32.hip
+size_t localize32_temp_bytes(int64_t);
+void localize32(const uint64_t*, int64_t, KeyMix, void*, size_t, uint32_t*, int32_t*, int32_t*,
+                uint64_t*, int32_t*, int32_t*, int32_t*, float*, float*, hipStream_t);
 // linear.hip
 void linear_fwd(const int64_t*, int64_t, int, const int32_t*, const float*, const float*, int64_t,
                 const float*, int, float*, float*, float*, double*, uint32_t*, int, hipStream_t);
 void linear_bwd(const int32_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
                 const float*, int64_t, const float*, float*, float*, int64_t, hipStream_t);
-void auc_from_hist(uint32_t*, int, double*, hipStream_t);
+void auc_from_hist(uint32_t*, int, double*, int64_t*, hipStream_t);
 void csr_rows(const int64_t*, int64_t, int32_t*, hipStream_t);
 void criteo_set_cards(const uint32_t*);
-void criteo_gen(uint64_t, int64_t, const int64_t*, int64_t, uint64_t, float, uint64_t*, float*,
-                hipStream_t);
+void criteo_gen(uint64_t, int64_t, const int64_t*, int64_t, int64_t, uint64_t, float, uint64_t*,
+                float*, hipStream_t);
 void add_i64(int64_t*, int64_t, hipStream_t);
 // filters.hip
 void cm_insert(uint32_t*, uint64_t, int, uint32_t, const uint64_t*, const uint8_t*, int64_t,
@@ -304,6 +308,34 @@ PYBIND11_MODULE(_hipops, m) {
                ptr<int32_t>(seg_start), ptr<int32_t>(local_col), ptr<int32_t>(n_uniq), za, zb,
                cur_stream());
   });
+  m.def("localize32_temp_bytes", [](int64_t n) { return (int64_t)psamd::localize32_temp_bytes(n); });
+  m.def("localize32", [](Tensor keys, int bits, Tensor temp, Tensor hs, Tensor pos_s, Tensor segid,
+                         Tensor uniq, Tensor seg_start, Tensor local_col, Tensor n_uniq,
+                         optional<Tensor> zero_a, optional<Tensor> zero_b) {
+    chk(keys, at::kLong, "keys");
+    chk(temp, at::kByte, "temp");
+    chk(hs, at::kInt, "hs");
+    chk(pos_s, at::kInt, "pos_s");
+    chk(segid, at::kInt, "segid");
+    chk(uniq, at::kLong, "uniq");
+    chk(seg_start, at::kInt, "seg_start");
+    chk(local_col, at::kInt, "local_col");
+    chk(n_uniq, at::kInt, "n_uniq");
+    const int64_t n = keys.numel();
+    check(n >= 1 && n < (int64_t)INT32_MAX, "localize32: 1 <= n < 2^31");
+    check(bits >= 2 && bits <= 32, "localize32 needs key bits <= 32");
+    check(hs.numel() >= n && pos_s.numel() >= n && segid.numel() >= n && uniq.numel() >= n &&
+              seg_start.numel() >= n + 1 && local_col.numel() >= n, "localize32 buffers too small");
+    check((size_t)temp.numel() >= psamd::localize32_temp_bytes(n), "localize32 temp too small");
+    float* za = optr<float>(zero_a, at::kFloat, "zero_a");
+    float* zb = optr<float>(zero_b, at::kFloat, "zero_b");
+    if (za) check(zero_a->numel() >= n, "zero_a too small");
+    if (zb) check(zero_b->numel() >= n, "zero_b too small");
+    psamd::localize32(ptr<uint64_t>(keys), n, make_keymix(bits), temp.data_ptr(),
+                      (size_t)temp.numel(), ptr<uint32_t>(hs), ptr<int32_t>(pos_s),
+                      ptr<int32_t>(segid), ptr<uint64_t>(uniq), ptr<int32_t>(seg_start),
+                      ptr<int32_t>(local_col), ptr<int32_t>(n_uniq), za, zb, cur_stream());
+  });
   m.def("seg_counts", [](Tensor seg_start, Tensor n_uniq, Tensor counts, int sat) {
     chk(seg_start, at::kInt, "seg_start");
     chk(n_uniq, at::kInt, "n_uniq");
@@ -378,12 +410,15 @@ PYBIND11_MODULE(_hipops, m) {
                       optr<float>(vals, at::kFloat, "vals"), ptr<float>(coef), coef.numel(), c2,
                       ptr<float>(grad), h, grad.numel(), cur_stream());
   });
-  m.def("auc_from_hist", [](Tensor hist, int nbins, Tensor metrics) {
+  m.def("auc_from_hist", [](Tensor hist, int nbins, Tensor metrics,
+                            optional<Tensor> step_counter) {
     chk(hist, at::kInt, "hist");
     chk(metrics, at::kDouble, "metrics");
     check(hist.numel() >= 2 * nbins && metrics.numel() >= 5, "auc sizes");
-    psamd::auc_from_hist(ptr<uint32_t>(hist), nbins, ptr<double>(metrics), cur_stream());
-  });
+    psamd::auc_from_hist(ptr<uint32_t>(hist), nbins, ptr<double>(metrics),
+                         optr<int64_t>(step_counter, at::kLong, "step_counter"), cur_stream());
+  }, py::arg("hist"), py::arg("nbins"), py::arg("metrics"),
+     py::arg("step_counter") = py::none());
   m.def("csr_rows", [](Tensor row_ptr, Tensor rows) {
     chk(row_ptr, at::kLong, "row_ptr");
     chk(rows, at::kInt, "rows");
@@ -399,12 +434,14 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::add_i64(ptr<int64_t>(p), v, cur_stream());
   });
   m.def("criteo_gen", [](uint64_t seed, int64_t row0, int64_t B, uint64_t num_features,
-                         double alpha, Tensor keys, Tensor labels, optional<Tensor> row0_dev) {
+                         double alpha, Tensor keys, Tensor labels, optional<Tensor> row0_dev,
+                         int64_t row_scale) {
     chk(keys, at::kLong, "keys");
     chk(labels, at::kFloat, "labels");
     check(keys.numel() >= B * 39 && labels.numel() >= B, "criteo_gen buffers too small");
     check(alpha > 1.0, "power-law alpha must be > 1");
-    psamd::criteo_gen(seed, row0, optr<int64_t>(row0_dev, at::kLong, "row0_dev"), B,
+    check(num_features > 0, "num_features > 0");
+    psamd::criteo_gen(seed, row0, optr<int64_t>(row0_dev, at::kLong, "row0_dev"), row_scale, B,
                       num_features, (float)alpha, ptr<uint64_t>(keys), ptr<float>(labels),
                       cur_stream());
   });

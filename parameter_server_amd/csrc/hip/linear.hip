@@ -25,7 +25,7 @@ __device__ __forceinline__ float softplus(float x) {
   return x > 20.f ? x : (x < -20.f ? expf(x) : log1pf(expf(x)));
 }
 
-template <bool kHasRowPtr>
+template <bool kHasRowPtr, int kLPR>
 __global__ void __launch_bounds__(256)
 linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
                   const int32_t* __restrict__ local_col, const float* __restrict__ vals,
@@ -34,30 +34,33 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
                   int loss_type, float* __restrict__ xw_out, float* __restrict__ coef_out,
                   float* __restrict__ coef2_out, double* __restrict__ metrics,
                   uint32_t* __restrict__ hist, int nbins) {
+  // kLPR lanes cooperate on one example (strided over its nnz, then a shuffle
+  // reduction), so B = 65536 rows launch 8x more waves than lane-per-row.
   extern __shared__ uint32_t lhist[];  // [2*nbins] when hist != nullptr
   __shared__ double lds[16];
   if (hist) {
     for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) lhist[i] = 0;
     __syncthreads();
   }
+  const int sub = threadIdx.x % kLPR;
   double loss_acc = 0, corr_acc = 0, cnt = 0;
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < B;
-       r += (int64_t)gridDim.x * blockDim.x) {
-    int64_t b, e;
-    if (kHasRowPtr) { b = row_ptr[r]; e = row_ptr[r + 1]; }
-    else { b = r * width; e = b + width; }
-    float m = 0.f;
-    if (vals) {
-      for (int64_t k = b; k < e; ++k) {
-        const int32_t c = local_col[k];
-        if (in_range(c, w_cap)) m += w_local[c] * vals[k];
-      }
-    } else {
-      for (int64_t k = b; k < e; ++k) {
-        const int32_t c = local_col[k];
-        if (in_range(c, w_cap)) m += w_local[c];
-      }
+  const int64_t groups_per_grid = ((int64_t)gridDim.x * blockDim.x) / kLPR;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kLPR;
+       r < ((B + groups_per_grid - 1) / groups_per_grid) * groups_per_grid; r += groups_per_grid) {
+    const bool row_ok = r < B;
+    int64_t b = 0, e = 0;
+    if (row_ok) {
+      if (kHasRowPtr) { b = row_ptr[r]; e = row_ptr[r + 1]; }
+      else { b = r * width; e = b + width; }
     }
+    float m = 0.f;
+    for (int64_t k = b + sub; k < e; k += kLPR) {
+      const int32_t c = local_col[k];
+      if (in_range(c, w_cap)) m += vals ? w_local[c] * vals[k] : w_local[c];
+    }
+#pragma unroll
+    for (int off = kLPR / 2; off > 0; off >>= 1) m += __shfl_xor(m, off, 64);
+    if (!row_ok || sub != 0) continue;
     const float y = labels[r] > 0.f ? 1.f : -1.f;
     const float ym = y * m;
     float loss, coef, coef2;
@@ -91,8 +94,7 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
     if (hist) {
       const float p = 1.f / (1.f + expf(-m));
       const float pb = p == p ? fminf(fmaxf(p * nbins, 0.f), (float)(nbins - 1)) : 0.f;
-      const int bin = (int)pb;
-      atomicAdd(&lhist[(y > 0.f ? nbins : 0) + bin], 1u);
+      atomicAdd(&lhist[(y > 0.f ? nbins : 0) + (int)pb], 1u);
     }
   }
   if (metrics) {
@@ -175,7 +177,8 @@ linear_bwd_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__
 // Bucketed AUC of one minibatch from its histogram; metrics[3] += auc, metrics[4] += 1.
 // Resets the histogram (so the next step starts clean inside a captured graph).
 __global__ void auc_from_hist_kernel(uint32_t* __restrict__ hist, int nbins,
-                                     double* __restrict__ metrics) {
+                                     double* __restrict__ metrics,
+                                     int64_t* __restrict__ step_counter) {
   __shared__ double s_neg[256], s_pos[256], s_area[256];
   const int t = threadIdx.x;  // blockDim.x == 256
   const int per = (nbins + 255) / 256;
@@ -211,6 +214,7 @@ __global__ void auc_from_hist_kernel(uint32_t* __restrict__ hist, int nbins,
       metrics[3] += A / (Ptot * Ntot);
       metrics[4] += 1.0;
     }
+    if (step_counter) *step_counter += 1;  // device step clock (graph-replay safe)
   }
 }
 
@@ -236,36 +240,54 @@ __device__ __forceinline__ float planted_w(uint64_t key, uint64_t seed) {
   return 0.6f * sqrtf(-2.f * logf(u1)) * cosf(6.283185307f * u2);
 }
 
+__device__ __forceinline__ uint64_t criteo_key(uint64_t seed, uint64_t gr, int j,
+                                               uint64_t num_features, float alpha) {
+  const float u = u01(rng64(seed + (uint64_t)j * 0x632be59bd9b4e019ull, gr));
+  uint64_t id;
+  if (j < 13) {
+    // integer feature: heavy tailed count, log2 bucketised (~<= 40 buckets)
+    const float x = expf(u * 12.f) - 1.f;
+    id = (uint64_t)(2.f * log2f(1.f + x));
+  } else {
+    const float C = (float)c_cards[j - 13];
+    const float oma = 1.f - alpha;
+    const float x = powf((powf(C, oma) - 1.f) * u + 1.f, 1.f / oma);
+    uint64_t v = (uint64_t)x;
+    id = v >= 1 ? v - 1 : 0;
+  }
+  return fmix64(((uint64_t)(j + 1) << 48) ^ id) % num_features;
+}
+
+// One thread per (row, slot): a 256-thread block generates 6 rows (234 features);
+// per-row planted logits are summed in LDS, then 6 lanes draw the labels.
+constexpr int kGenRows = 6;
 __global__ void __launch_bounds__(256)
-criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_dev, int64_t B,
-                  uint64_t num_features, float alpha, uint64_t* __restrict__ keys,
-                  float* __restrict__ labels) {
-  if (row0_dev) row0 += *row0_dev;
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < B;
-       r += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t gr = (uint64_t)(row0 + r);
-    float logit = -1.2f;
-    for (int j = 0; j < 39; ++j) {
-      const float u = u01(rng64(seed + (uint64_t)j * 0x632be59bd9b4e019ull, gr));
-      uint64_t id;
-      if (j < 13) {
-        // integer feature: heavy tailed count, log2 bucketised (~<= 40 buckets)
-        const float x = expf(u * 12.f) - 1.f;
-        id = (uint64_t)(2.f * log2f(1.f + x));
-      } else {
-        const float C = (float)c_cards[j - 13];
-        const float oma = 1.f - alpha;
-        const float x = powf((powf(C, oma) - 1.f) * u + 1.f, 1.f / oma);
-        uint64_t v = (uint64_t)x;
-        id = v >= 1 ? v - 1 : 0;
-      }
-      const uint64_t key = fmix64(((uint64_t)(j + 1) << 48) ^ id) % num_features;
+criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_dev,
+                  int64_t row_scale, int64_t B, uint64_t num_features, float alpha,
+                  uint64_t* __restrict__ keys, float* __restrict__ labels) {
+  __shared__ float logit[kGenRows];
+  if (row0_dev) row0 += (*row0_dev) * row_scale;
+  const int t = threadIdx.x;
+  if (t < kGenRows) logit[t] = -1.2f;
+  __syncthreads();
+  for (int64_t rb = (int64_t)blockIdx.x * kGenRows; rb < B; rb += (int64_t)gridDim.x * kGenRows) {
+    const int lr = t / 39, j = t % 39;
+    const int64_t r = rb + lr;
+    if (lr < kGenRows && r < B) {
+      const uint64_t key = criteo_key(seed, (uint64_t)(row0 + r), j, num_features, alpha);
       keys[r * 39 + j] = key;
-      logit += planted_w(key, seed);
+      const float pw = planted_w(key, seed);
+      if (pw != 0.f) atomicAdd(&logit[lr], pw);
     }
-    const float p = 1.f / (1.f + expf(-logit));
-    const float u = u01(rng64(seed ^ 0xabcdefull, gr));
-    labels[r] = u < p ? 1.f : -1.f;
+    __syncthreads();
+    if (t < kGenRows && rb + t < B) {
+      const int64_t r2 = rb + t;
+      const float p = 1.f / (1.f + expf(-logit[t]));
+      const float u = u01(rng64(seed ^ 0xabcdefull, (uint64_t)(row0 + r2)));
+      labels[r2] = u < p ? 1.f : -1.f;
+      logit[t] = -1.2f;
+    }
+    __syncthreads();
   }
 }
 
@@ -276,13 +298,14 @@ void linear_fwd(const int64_t* row_ptr, int64_t B, int width, const int32_t* loc
                 float* xw, float* coef, float* coef2, double* metrics, uint32_t* hist, int nbins,
                 hipStream_t st) {
   const size_t lds = hist ? (size_t)2 * nbins * sizeof(uint32_t) : 0;
-  const int g = grid_for(B, 256, 4096);
+  constexpr int kLPR = 8;
+  const int g = grid_for(B * kLPR, 256, 8192);
   if (row_ptr)
-    linear_fwd_kernel<true><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
+    linear_fwd_kernel<true, kLPR><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
                                                  w_cap, labels, loss_type, xw, coef, coef2, metrics,
                                                  hist, nbins);
   else
-    linear_fwd_kernel<false><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
+    linear_fwd_kernel<false, kLPR><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
                                                   w_cap, labels, loss_type, xw, coef, coef2, metrics,
                                                   hist, nbins);
   PSAMD_HIP_CHECK(hipGetLastError());
@@ -296,8 +319,9 @@ void linear_bwd(const int32_t* pos_s, const int32_t* segid, int64_t n, const int
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void auc_from_hist(uint32_t* hist, int nbins, double* metrics, hipStream_t st) {
-  auc_from_hist_kernel<<<1, 256, 0, st>>>(hist, nbins, metrics);
+void auc_from_hist(uint32_t* hist, int nbins, double* metrics, int64_t* step_counter,
+                   hipStream_t st) {
+  auc_from_hist_kernel<<<1, 256, 0, st>>>(hist, nbins, metrics, step_counter);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
@@ -310,11 +334,12 @@ void criteo_set_cards(const uint32_t* cards26) {
   PSAMD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_cards), cards26, 26 * sizeof(uint32_t)));
 }
 
-void criteo_gen(uint64_t seed, int64_t row0, const int64_t* row0_dev, int64_t B,
-                uint64_t num_features, float alpha, uint64_t* keys, float* labels,
+void criteo_gen(uint64_t seed, int64_t row0, const int64_t* row0_dev, int64_t row_scale,
+                int64_t B, uint64_t num_features, float alpha, uint64_t* keys, float* labels,
                 hipStream_t st) {
-  criteo_gen_kernel<<<grid_for(B, 256, 4096), 256, 0, st>>>(seed, row0, row0_dev, B,
-                                                            num_features, alpha, keys, labels);
+  const int64_t blocks = (B + kGenRows - 1) / kGenRows;
+  criteo_gen_kernel<<<(unsigned)(blocks < 65535 ? blocks : 65535), 256, 0, st>>>(
+      seed, row0, row0_dev, row_scale, B, num_features, alpha, keys, labels);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -1,0 +1,323 @@
+// Localisation fast path for key spaces of <= 32 bits (e.g. 10^9 hashed features).
+//
+// Stable LSD radix sort of (mixed u32 key, i32 position) with 8-bit digits:
+//   pass 0 histogram kernel reads the RAW u64 keys, mixes them and writes the u32
+//   mixed keys (so the separate mix pass disappears) and the positions are an
+//   implicit iota (never read from memory in pass 0).
+//   per pass: hist (LDS atomics) -> single-launch scan of the digit-major
+//   histogram -> scatter.
+// Scatter ranking is wave64-native: each wave owns 1024 consecutive tile
+// elements, processed in 16 rounds of 64; lanes with equal digits are found with
+// 8 __ballot()s (a 64-bit "match-any"), ranked with popcount, and a per-wave
+// per-digit counter in LDS carries the rank across rounds. A 256-thread digit
+// scan turns (digit, wave) counts into tile offsets; the tile is reordered in LDS
+// and stored digit-run contiguous.
+// RLE (unique keys, segment ids, local columns) is fused into 2 kernels + scan.
+// All global indices are bounds-checked.
+#include "common.cuh"
+#include <stdexcept>
+#include <string>
+
+namespace psamd {
+
+namespace s32 {
+constexpr int kBlk = 256;
+constexpr int kWaves = kBlk / 64;
+constexpr int kItems = 16;
+constexpr int kTile = kBlk * kItems;  // 4096
+constexpr int kBits = 8;
+constexpr int kDigits = 1 << kBits;
+constexpr int kScanThreads = 1024;
+}  // namespace s32
+using namespace s32;
+
+__device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* lds, uint32_t* total,
+                                                        int nwaves) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int w = 0; w < nwaves; ++w) {
+      uint32_t t = lds[w];
+      lds[w] = run;
+      run += t;
+    }
+    lds[nwaves] = run;
+  }
+  __syncthreads();
+  const uint32_t r = x - v + lds[wid];
+  *total = lds[nwaves];
+  __syncthreads();
+  return r;
+}
+
+// ---------------------------------------------------------------- histogram
+template <bool kMix>
+__global__ void __launch_bounds__(kBlk)
+hist32_kernel(const uint64_t* __restrict__ raw, const uint32_t* __restrict__ keys, int64_t n,
+              KeyMix m, uint32_t* __restrict__ mixed_out, int shift, uint32_t* __restrict__ hist,
+              int64_t T) {
+  __shared__ uint32_t cnt[kDigits];
+  cnt[threadIdx.x] = 0;  // kBlk == kDigits
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+#pragma unroll 4
+  for (int j = 0; j < kItems; ++j) {
+    const int64_t i = base + j * kBlk + threadIdx.x;
+    if (i < n) {
+      uint32_t k;
+      if (kMix) {
+        k = (uint32_t)mix_key(raw[i], m);
+        mixed_out[i] = k;
+      } else {
+        k = keys[i];
+      }
+      atomicAdd(&cnt[(k >> shift) & (kDigits - 1)], 1u);
+    }
+  }
+  __syncthreads();
+  hist[(int64_t)threadIdx.x * T + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// ------------------------------------------------------- single-launch scan
+// Exclusive scan of a[0:n] in place by one 1024-thread workgroup: each thread
+// owns a contiguous chunk; chunk sums are block-scanned, then chunks rewritten.
+__global__ void __launch_bounds__(kScanThreads) scan_single_kernel(uint32_t* __restrict__ a,
+                                                                   int64_t n) {
+  __shared__ uint32_t lds[kScanThreads / 64 + 1];
+  const int64_t per = (n + kScanThreads - 1) / kScanThreads;
+  const int64_t lo = min(n, (int64_t)threadIdx.x * per), hi = min(n, lo + per);
+  uint32_t s = 0;
+  for (int64_t i = lo; i < hi; ++i) s += a[i];
+  uint32_t tot;
+  uint32_t run = block_excl_scan_u32(s, lds, &tot, kScanThreads / 64);
+  for (int64_t i = lo; i < hi; ++i) {
+    const uint32_t x = a[i];
+    a[i] = run;
+    run += x;
+  }
+}
+
+// ------------------------------------------------------------------ scatter
+__global__ void __launch_bounds__(kBlk)
+scatter32_kernel(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in,
+                 uint32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t n,
+                 int shift, const uint32_t* __restrict__ offs, int64_t T) {
+  __shared__ uint32_t skeys[kTile];
+  __shared__ int32_t svals[kTile];
+  __shared__ uint32_t wcnt[kWaves * kDigits];  // [wave][digit]
+  __shared__ uint32_t dstart[kDigits];
+  __shared__ uint32_t lds[kWaves + 1];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int tile_n = (int)min((int64_t)kTile, n - base);
+  for (int f = t; f < kWaves * kDigits; f += kBlk) wcnt[f] = 0;
+  __syncthreads();
+  uint32_t k[kItems];
+  int32_t v[kItems];
+  uint32_t rank[kItems];
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int r = 0; r < kItems; ++r) {
+    const int li = w * (kTile / kWaves) + r * 64 + lane;  // wave-owned 1024-element segment
+    const bool valid = li < tile_n;
+    uint32_t d = kDigits;  // sentinel for invalid lanes
+    if (valid) {
+      k[r] = keys_in[base + li];
+      v[r] = vals_in ? vals_in[base + li] : (int32_t)(base + li);
+      d = (k[r] >> shift) & (kDigits - 1);
+    }
+    // 64-lane match-any on the 8-bit digit
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < kBits; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bal = __ballot(bit);
+      peers &= bit ? bal : ~bal;
+    }
+    uint32_t base_cnt = 0;
+    if (valid) base_cnt = wcnt[w * kDigits + d];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && (peers & lt_mask) == 0ull)
+      wcnt[w * kDigits + d] = base_cnt + (uint32_t)__popcll(peers);
+    __builtin_amdgcn_wave_barrier();
+    rank[r] = base_cnt + (uint32_t)__popcll(peers & lt_mask);
+  }
+  __syncthreads();
+  // digit-major offsets: thread t handles digit t
+  {
+    uint32_t c[kWaves], tot_d = 0;
+#pragma unroll
+    for (int q = 0; q < kWaves; ++q) { c[q] = wcnt[q * kDigits + t]; tot_d += c[q]; }
+    uint32_t total;
+    const uint32_t ds = block_excl_scan_u32(tot_d, lds, &total, kWaves);
+    dstart[t] = ds;
+    uint32_t run = ds;
+#pragma unroll
+    for (int q = 0; q < kWaves; ++q) { wcnt[q * kDigits + t] = run; run += c[q]; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kItems; ++r) {
+    const int li = w * (kTile / kWaves) + r * 64 + lane;
+    if (li < tile_n) {
+      const uint32_t d = (k[r] >> shift) & (kDigits - 1);
+      const uint32_t pos = wcnt[w * kDigits + d] + rank[r];
+      if (pos < (uint32_t)kTile) {
+        skeys[pos] = k[r];
+        svals[pos] = v[r];
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int j = 0; j < kItems; ++j) {
+    const int li = j * kBlk + t;
+    if (li < tile_n) {
+      const uint32_t key = skeys[li];
+      const uint32_t d = (key >> shift) & (kDigits - 1);
+      const int64_t g = (int64_t)offs[(int64_t)d * T + blockIdx.x] + (li - (int)dstart[d]);
+      if (in_range(g, n)) {
+        keys_out[g] = key;
+        vals_out[g] = svals[li];
+      }
+    }
+  }
+}
+
+// -------------------------------------------------------------- fused RLE
+__global__ void __launch_bounds__(kBlk) rle32_count_kernel(const uint32_t* __restrict__ hs,
+                                                           int64_t n, uint32_t* __restrict__ part) {
+  __shared__ uint32_t lds[kWaves + 1];
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  uint32_t c = 0;
+#pragma unroll 4
+  for (int j = 0; j < kItems; ++j) {
+    const int64_t i = base + j * kBlk + threadIdx.x;
+    if (i < n) c += (i == 0 || hs[i] != hs[i - 1]) ? 1u : 0u;
+  }
+  uint32_t tot;
+  block_excl_scan_u32(c, lds, &tot, kWaves);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// part[] holds the exclusive prefix of head counts per tile (scan_single_kernel).
+__global__ void __launch_bounds__(kBlk)
+rle32_write_kernel(const uint32_t* __restrict__ hs, const int32_t* __restrict__ pos_s, int64_t n,
+                   const uint32_t* __restrict__ part, int32_t* __restrict__ segid,
+                   uint64_t* __restrict__ uniq, int32_t* __restrict__ seg_start,
+                   int32_t* __restrict__ local_col, int32_t* __restrict__ n_uniq,
+                   float* __restrict__ zero_a, float* __restrict__ zero_b) {
+  __shared__ uint32_t flag[kTile + 1];
+  __shared__ uint32_t lds[kWaves + 1];
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int tile_n = (int)min((int64_t)kTile, n - base);
+#pragma unroll 4
+  for (int j = 0; j < kItems; ++j) {  // coalesced flag computation into LDS
+    const int li = j * kBlk + t;
+    const int64_t i = base + li;
+    flag[li] = (li < tile_n) ? ((i == 0 || hs[i] != hs[i - 1]) ? 1u : 0u) : 0u;
+  }
+  __syncthreads();
+  // blocked: thread t owns tile elements [t*16, t*16+16)
+  uint32_t s = 0;
+#pragma unroll
+  for (int q = 0; q < kItems; ++q) s += flag[t * kItems + q];
+  uint32_t tot;
+  uint32_t run = block_excl_scan_u32(s, lds, &tot, kWaves) + part[blockIdx.x];
+#pragma unroll
+  for (int q = 0; q < kItems; ++q) {
+    run += flag[t * kItems + q];
+    flag[t * kItems + q] = run;  // inclusive 1-based segment id
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int j = 0; j < kItems; ++j) {
+    const int li = j * kBlk + t;
+    if (li >= tile_n) continue;
+    const int64_t i = base + li;
+    const uint32_t sid = flag[li];
+    const int32_t s0 = (int32_t)sid - 1;
+    segid[i] = (int32_t)sid;
+    if (!in_range(s0, n)) continue;
+    const int32_t p = pos_s[i];
+    if (in_range(p, n)) local_col[p] = s0;
+    const bool head = (i == 0) || hs[i] != hs[i - 1];
+    if (head) {
+      uniq[s0] = hs[i];
+      seg_start[s0] = (int32_t)i;
+      if (zero_a) zero_a[s0] = 0.f;
+      if (zero_b) zero_b[s0] = 0.f;
+    }
+    if (i == n - 1) {
+      *n_uniq = s0 + 1;
+      seg_start[s0 + 1] = (int32_t)n;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Workspace: [mixed keys n*4][keys tmp n*4][vals tmp n*4][hist 256*T*4][part T*4]
+size_t localize32_temp_bytes(int64_t n) {
+  const int64_t T = (n + kTile - 1) / kTile;
+  return (size_t)n * 12 + (size_t)kDigits * T * 4 + (size_t)T * 4 + 256;
+}
+
+// keys (raw u64) -> hs (mixed u32 sorted), pos_s; then RLE outputs.
+void localize32(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
+                uint32_t* hs, int32_t* pos_s, int32_t* segid, uint64_t* uniq, int32_t* seg_start,
+                int32_t* local_col, int32_t* n_uniq, float* zero_a, float* zero_b,
+                hipStream_t st) {
+  if (n <= 0) return;
+  if (m.bits > 32) throw std::runtime_error("localize32 needs key bits <= 32");
+  if (temp_bytes < localize32_temp_bytes(n)) throw std::runtime_error("localize32 temp too small");
+  const int64_t T = (n + kTile - 1) / kTile;
+  char* p = (char*)temp;
+  uint32_t* mixed = (uint32_t*)p;
+  p += (size_t)n * 4;
+  uint32_t* kt = (uint32_t*)p;
+  p += (size_t)n * 4;
+  int32_t* vt = (int32_t*)p;
+  p += (size_t)n * 4;
+  uint32_t* hist = (uint32_t*)p;
+  p += (size_t)kDigits * T * 4;
+  uint32_t* part = (uint32_t*)p;
+  const int passes = (m.bits + kBits - 1) / kBits;
+  const uint32_t* src_k = mixed;
+  const int32_t* src_v = nullptr;  // iota
+  for (int pass = 0; pass < passes; ++pass) {
+    const bool to_out = ((passes - 1 - pass) % 2) == 0;
+    uint32_t* dk = to_out ? hs : kt;
+    int32_t* dv = to_out ? pos_s : vt;
+    const int shift = pass * kBits;
+    if (pass == 0)
+      hist32_kernel<true><<<(unsigned)T, kBlk, 0, st>>>(raw, nullptr, n, m, mixed, shift, hist, T);
+    else
+      hist32_kernel<false><<<(unsigned)T, kBlk, 0, st>>>(nullptr, src_k, n, m, nullptr, shift,
+                                                         hist, T);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    scan_single_kernel<<<1, kScanThreads, 0, st>>>(hist, (int64_t)kDigits * T);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    scatter32_kernel<<<(unsigned)T, kBlk, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    src_k = dk;
+    src_v = dv;
+  }
+  rle32_count_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, n, part);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  scan_single_kernel<<<1, kScanThreads, 0, st>>>(part, T);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  rle32_write_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, pos_s, n, part, segid, uniq, seg_start,
+                                                   local_col, n_uniq, zero_a, zero_b);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace psamd

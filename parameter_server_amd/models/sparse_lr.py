@@ -95,6 +95,7 @@ class SparseLRTrainer:
         self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
         self.hist = torch.zeros(2 * AUC_BINS, dtype=torch.int32, device=dev)
         self.coef = torch.empty(cfg.minibatch, dtype=torch.float32, device=dev)
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)  # device step clock
         if self.gpu:
             self.slot_buf = torch.empty(self.max_nnz, dtype=torch.int64, device=dev)
             self.w_buf = torch.empty(self.max_nnz, dtype=torch.float32, device=dev)
@@ -139,7 +140,7 @@ class SparseLRTrainer:
                                     coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
         grad, _ = linear_backward(loc, coef, B=B, width=width or 0, rows=rows, vals=vals)
         self._push(grad, push)
-        auc_from_hist(self.hist, self.metrics)
+        auc_from_hist(self.hist, self.metrics, self.step_dev)
         self.clock.tick(self.rank, self.step_count)
         self.step_count += 1
         self.examples += B

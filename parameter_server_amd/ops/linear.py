@@ -109,10 +109,11 @@ def linear_backward(loc, coef, *, B: int, width: int = 0, rows=None, vals=None, 
     return loc.grad, loc.hess
 
 
-def auc_from_hist(hist: torch.Tensor, metrics: torch.Tensor):
-    """metrics[3] += AUC of the histogram, metrics[4] += 1; zeroes hist."""
+def auc_from_hist(hist: torch.Tensor, metrics: torch.Tensor, step_counter=None):
+    """metrics[3] += AUC of the histogram, metrics[4] += 1; zeroes hist; optionally
+    increments a device step counter (one epilogue kernel per step)."""
     if is_gpu(hist):
-        hipops().auc_from_hist(hist, AUC_BINS, metrics)
+        hipops().auc_from_hist(hist, AUC_BINS, metrics, step_counter)
         return
     neg = hist[:AUC_BINS].double()
     pos = hist[AUC_BINS:].double()
@@ -123,6 +124,8 @@ def auc_from_hist(hist: torch.Tensor, metrics: torch.Tensor):
         metrics[3] += area / (P * N)
         metrics[4] += 1
     hist.zero_()
+    if step_counter is not None:
+        step_counter += 1
 
 
 def exact_auc(scores: torch.Tensor, labels: torch.Tensor) -> float:

@@ -66,8 +66,14 @@ class Localizer:
             self.n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
             self.grad = torch.empty(n, dtype=torch.float32, device=dev)
             self.hess = torch.empty(n, dtype=torch.float32, device=dev) if with_hess else None
-            self.sort_temp = torch.empty(max(1, H.sort_pairs_temp_bytes(n, self.bits)),
-                                         dtype=torch.uint8, device=dev)
+            self.fast32 = self.bits <= 32
+            if self.fast32:  # fused mix + u32 8-bit-digit sort + fused RLE (csrc/hip/sort32.hip)
+                self.hs32 = torch.empty(n, dtype=torch.int32, device=dev)
+                self.sort_temp = torch.empty(H.localize32_temp_bytes(n), dtype=torch.uint8,
+                                             device=dev)
+            else:
+                self.sort_temp = torch.empty(max(1, H.sort_pairs_temp_bytes(n, self.bits)),
+                                             dtype=torch.uint8, device=dev)
             self.scan_temp = torch.empty(max(1, H.scan_temp_bytes(n)), dtype=torch.uint8,
                                          device=dev)
 
@@ -83,6 +89,12 @@ class Localizer:
 
     def _gpu(self, keys, n) -> Localized:
         H = hipops()
+        if self.fast32:
+            H.localize32(keys, self.bits, self.sort_temp, self.hs32, self.pos_s, self.segid,
+                         self.uniq, self.seg_start, self.local_col, self.n_uniq, self.grad,
+                         self.hess)
+            return Localized(self.uniq, self.seg_start, self.pos_s[:n], self.segid[:n],
+                             self.local_col[:n], self.n_uniq, self.grad, self.hess, n)
         H.mix_iota(keys, self.bits, self.h, self.pos)
         H.sort_pairs(self.sort_temp, self.h, self.hs, self.pos, self.pos_s, n, self.bits)
         H.rle(self.hs, self.pos_s, n, self.flags, self.segid, self.scan_temp, self.uniq,

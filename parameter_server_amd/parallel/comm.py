@@ -70,15 +70,24 @@ class DistComm(Comm):
     def all_to_all_v(self, send: torch.Tensor, send_counts, recv_counts) -> torch.Tensor:
         sc = [int(x) for x in send_counts]
         rc = [int(x) for x in recv_counts]
+        staged = self.backend == "gloo" and send.is_cuda  # rehearsal mode: GPU ranks over gloo
+        src = send.cpu() if staged else send
         out = torch.empty((sum(rc),) + tuple(send.shape[1:]), dtype=send.dtype,
-                          device=send.device)
-        dist.all_to_all_single(out, send.contiguous(), output_split_sizes=rc,
+                          device=src.device)
+        dist.all_to_all_single(out, src.contiguous(), output_split_sizes=rc,
                                input_split_sizes=sc, group=self.group)
+        if staged:
+            out = out.to(send.device)
         self._sent += send.element_size() * (sum(sc) - sc[self.rank]) * max(1, send[0:1].numel())
         return out
 
     def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
         ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+        if self.backend == "gloo" and t.is_cuda:
+            h = t.cpu()
+            dist.all_reduce(h, op=ops[op], group=self.group)
+            t.copy_(h)
+            return t
         dist.all_reduce(t, op=ops[op], group=self.group)
         return t
 
@@ -102,14 +111,18 @@ def init_from_env(device_type: str = "cuda", backend: str | None = None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if device_type == "cuda":
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        # PSAMD_DIST_BACKEND=gloo + more ranks than GPUs = rehearsal of the multi-rank
+        # GPU protocol on a 1-GPU box (exchanges staged through host memory).
+        ndev = max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local_rank % ndev)
+        device = torch.device("cuda", local_rank % ndev)
     else:
         device = torch.device("cpu")
     if world <= 1:
         return LocalComm(device), device
     if not dist.is_initialized():
-        backend = backend or ("nccl" if device_type == "cuda" else "gloo")
+        backend = backend or os.environ.get("PSAMD_DIST_BACKEND") or (
+            "nccl" if device_type == "cuda" else "gloo")
         kw = {}
         if backend == "nccl":
             kw["device_id"] = device

@@ -39,9 +39,9 @@ def test_trainer_gpu_loss_decreases_and_graph_capture():
 
     def step():
         criteo_batch(8192, seed=9, row0=0, num_features=cfg.num_features, device="cuda",
-                     keys=keys, labels=labels, row0_dev=row0)
+                     keys=keys, labels=labels, row0_dev=row0, row_scale=8192)
         tr.step(keys, labels, width=39)
-        hipops().add_i64(row0, 8192)
+        hipops().add_i64(row0, 1)
 
     step()
     first = tr.progress()
@@ -56,7 +56,8 @@ def test_trainer_gpu_loss_decreases_and_graph_capture():
     for _ in range(40):
         g.replay()
     torch.cuda.synchronize()
-    assert int(row0.item()) == 8192 * 42  # capture itself does not execute
+    assert int(row0.item()) == 42  # capture itself does not execute
+    assert int(tr.step_dev.item()) == 42
     last = tr.progress()
     assert last["examples"] == 41 * 8192
     assert last["loss"] < first["loss"]
@@ -78,9 +79,8 @@ def test_graph_replay_matches_eager():
 
         def step():
             criteo_batch(B, seed=5, row0=0, num_features=cfg.num_features, device="cuda",
-                         keys=keys, labels=labels, row0_dev=row0)
+                         keys=keys, labels=labels, row0_dev=tr.step_dev, row_scale=B)
             tr.step(keys, labels, width=39)
-            hipops().add_i64(row0, B)
 
         step()
         if use_graph:
@@ -99,8 +99,8 @@ def test_graph_replay_matches_eager():
                 step()
         torch.cuda.synchronize()
         tr.table.check_ok()
-        outs.append((tr.progress(), tr.table.census(), int(row0.item())))
+        outs.append((tr.progress(), tr.table.census(), int(tr.step_dev.item())))
     (pe, ce, re_), (pg, cg, rg) = outs
-    assert re_ == rg == 8 * B
+    assert re_ == rg == 8
     assert ce == cg
     assert abs(pe["loss"] - pg["loss"]) < 1e-9 * max(1.0, pe["loss"]) + 1e-7
