@@ -299,7 +299,8 @@ void linear_fwd(const int64_t* row_ptr, int64_t B, int width, const int32_t* loc
                 hipStream_t st) {
   const size_t lds = hist ? (size_t)2 * nbins * sizeof(uint32_t) : 0;
   constexpr int kLPR = 8;
-  const int g = grid_for(B * kLPR, 256, 8192);
+  // cap the grid: each block zeroes and flushes a 2*nbins LDS histogram
+  const int g = grid_for(B * kLPR, 256, 512);
   if (row_ptr)
     linear_fwd_kernel<true, kLPR><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
                                                  w_cap, labels, loss_type, xw, coef, coef2, metrics,

@@ -27,7 +27,6 @@ constexpr int kItems = 16;
 constexpr int kTile = kBlk * kItems;  // 4096
 constexpr int kBits = 8;
 constexpr int kDigits = 1 << kBits;
-constexpr int kScanThreads = 1024;
 }  // namespace s32
 using namespace s32;
 
@@ -68,41 +67,96 @@ hist32_kernel(const uint64_t* __restrict__ raw, const uint32_t* __restrict__ key
   cnt[threadIdx.x] = 0;  // kBlk == kDigits
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kTile;
+  if (!kMix && base + kTile <= n) {
+    // full tile: 16-byte loads, 4 keys per load, 4 loads per thread
+    const uint4* kv = reinterpret_cast<const uint4*>(keys + base);
+#pragma unroll
+    for (int j = 0; j < kItems / 4; ++j) {
+      const uint4 q = kv[j * kBlk + threadIdx.x];
+      atomicAdd(&cnt[(q.x >> shift) & (kDigits - 1)], 1u);
+      atomicAdd(&cnt[(q.y >> shift) & (kDigits - 1)], 1u);
+      atomicAdd(&cnt[(q.z >> shift) & (kDigits - 1)], 1u);
+      atomicAdd(&cnt[(q.w >> shift) & (kDigits - 1)], 1u);
+    }
+  } else {
 #pragma unroll 4
-  for (int j = 0; j < kItems; ++j) {
-    const int64_t i = base + j * kBlk + threadIdx.x;
-    if (i < n) {
-      uint32_t k;
-      if (kMix) {
-        k = (uint32_t)mix_key(raw[i], m);
-        mixed_out[i] = k;
-      } else {
-        k = keys[i];
+    for (int j = 0; j < kItems; ++j) {
+      const int64_t i = base + j * kBlk + threadIdx.x;
+      if (i < n) {
+        uint32_t k;
+        if (kMix) {
+          k = (uint32_t)mix_key(raw[i], m);
+          mixed_out[i] = k;
+        } else {
+          k = keys[i];
+        }
+        atomicAdd(&cnt[(k >> shift) & (kDigits - 1)], 1u);
       }
-      atomicAdd(&cnt[(k >> shift) & (kDigits - 1)], 1u);
     }
   }
   __syncthreads();
   hist[(int64_t)threadIdx.x * T + blockIdx.x] = cnt[threadIdx.x];
 }
 
-// ------------------------------------------------------- single-launch scan
-// Exclusive scan of a[0:n] in place by one 1024-thread workgroup: each thread
-// owns a contiguous chunk; chunk sums are block-scanned, then chunks rewritten.
-__global__ void __launch_bounds__(kScanThreads) scan_single_kernel(uint32_t* __restrict__ a,
-                                                                   int64_t n) {
-  __shared__ uint32_t lds[kScanThreads / 64 + 1];
-  const int64_t per = (n + kScanThreads - 1) / kScanThreads;
-  const int64_t lo = min(n, (int64_t)threadIdx.x * per), hi = min(n, lo + per);
+// ------------------------------------------------------------ 2-launch scan
+// Exclusive scan of a[0:n] in place: (1) per-2048-chunk sums, (2) each chunk
+// block sums the partials of all earlier chunks itself (few hundred L2-resident
+// values), then scans its chunk. No single-block serial phase, no spinning.
+constexpr int kScanChunk = 2048;
+
+__global__ void __launch_bounds__(kBlk) chunk_sum_kernel(const uint32_t* __restrict__ a,
+                                                         int64_t n, uint32_t* __restrict__ part) {
+  __shared__ uint32_t lds[kWaves + 1];
+  const int64_t base = (int64_t)blockIdx.x * kScanChunk;
   uint32_t s = 0;
-  for (int64_t i = lo; i < hi; ++i) s += a[i];
-  uint32_t tot;
-  uint32_t run = block_excl_scan_u32(s, lds, &tot, kScanThreads / 64);
-  for (int64_t i = lo; i < hi; ++i) {
-    const uint32_t x = a[i];
-    a[i] = run;
-    run += x;
+#pragma unroll
+  for (int j = 0; j < kScanChunk / kBlk; ++j) {
+    const int64_t i = base + j * kBlk + threadIdx.x;
+    if (i < n) s += a[i];
   }
+  uint32_t tot;
+  block_excl_scan_u32(s, lds, &tot, kWaves);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kBlk) chunk_scan_kernel(uint32_t* __restrict__ a, int64_t n,
+                                                          const uint32_t* __restrict__ part) {
+  __shared__ uint32_t tile[kScanChunk];
+  __shared__ uint32_t lds[kWaves + 1];
+  // prefix of earlier chunks
+  uint32_t pre = 0;
+  for (int64_t i = threadIdx.x; i < (int64_t)blockIdx.x; i += kBlk) pre += part[i];
+  uint32_t tot;
+  block_excl_scan_u32(pre, lds, &tot, kWaves);
+  const uint32_t offset = tot;
+  const int64_t base = (int64_t)blockIdx.x * kScanChunk;
+  constexpr int kPer = kScanChunk / kBlk;  // 8
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t i = base + j * kBlk + threadIdx.x;
+    tile[j * kBlk + threadIdx.x] = i < n ? a[i] : 0u;
+  }
+  __syncthreads();
+  uint32_t v[kPer], s = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) { v[q] = tile[threadIdx.x * kPer + q]; s += v[q]; }
+  uint32_t run = block_excl_scan_u32(s, lds, &tot, kWaves) + offset;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) { tile[threadIdx.x * kPer + q] = run; run += v[q]; }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t i = base + j * kBlk + threadIdx.x;
+    if (i < n) a[i] = tile[j * kBlk + threadIdx.x];
+  }
+}
+
+void scan2_u32(uint32_t* a, int64_t n, uint32_t* part, hipStream_t st) {
+  const int64_t chunks = (n + kScanChunk - 1) / kScanChunk;
+  chunk_sum_kernel<<<(unsigned)chunks, kBlk, 0, st>>>(a, n, part);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  chunk_scan_kernel<<<(unsigned)chunks, kBlk, 0, st>>>(a, n, part);
+  PSAMD_HIP_CHECK(hipGetLastError());
 }
 
 // ------------------------------------------------------------------ scatter
@@ -268,7 +322,8 @@ rle32_write_kernel(const uint32_t* __restrict__ hs, const int32_t* __restrict__ 
 // Workspace: [mixed keys n*4][keys tmp n*4][vals tmp n*4][hist 256*T*4][part T*4]
 size_t localize32_temp_bytes(int64_t n) {
   const int64_t T = (n + kTile - 1) / kTile;
-  return (size_t)n * 12 + (size_t)kDigits * T * 4 + (size_t)T * 4 + 256;
+  const int64_t chunks = ((int64_t)kDigits * T + kScanChunk - 1) / kScanChunk + T;
+  return (size_t)n * 12 + (size_t)kDigits * T * 4 + (size_t)T * 4 + (size_t)chunks * 4 + 512;
 }
 
 // keys (raw u64) -> hs (mixed u32 sorted), pos_s; then RLE outputs.
@@ -290,6 +345,8 @@ void localize32(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t tem
   uint32_t* hist = (uint32_t*)p;
   p += (size_t)kDigits * T * 4;
   uint32_t* part = (uint32_t*)p;
+  p += (size_t)T * 4;
+  uint32_t* spart = (uint32_t*)p;  // chunk partials for scan2
   const int passes = (m.bits + kBits - 1) / kBits;
   const uint32_t* src_k = mixed;
   const int32_t* src_v = nullptr;  // iota
@@ -304,8 +361,7 @@ void localize32(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t tem
       hist32_kernel<false><<<(unsigned)T, kBlk, 0, st>>>(nullptr, src_k, n, m, nullptr, shift,
                                                          hist, T);
     PSAMD_HIP_CHECK(hipGetLastError());
-    scan_single_kernel<<<1, kScanThreads, 0, st>>>(hist, (int64_t)kDigits * T);
-    PSAMD_HIP_CHECK(hipGetLastError());
+    scan2_u32(hist, (int64_t)kDigits * T, spart, st);
     scatter32_kernel<<<(unsigned)T, kBlk, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T);
     PSAMD_HIP_CHECK(hipGetLastError());
     src_k = dk;
@@ -313,8 +369,7 @@ void localize32(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t tem
   }
   rle32_count_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, n, part);
   PSAMD_HIP_CHECK(hipGetLastError());
-  scan_single_kernel<<<1, kScanThreads, 0, st>>>(part, T);
-  PSAMD_HIP_CHECK(hipGetLastError());
+  scan2_u32(part, T, spart, st);
   rle32_write_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, pos_s, n, part, segid, uniq, seg_start,
                                                    local_col, n_uniq, zero_a, zero_b);
   PSAMD_HIP_CHECK(hipGetLastError());
