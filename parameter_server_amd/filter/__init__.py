@@ -49,7 +49,7 @@ class KeyCachingFilter(Filter):
         return (not task.get("request")) or task.get("shared_para", {}).get("cmd") == "PUSH"
 
     def _ck(self, msg):
-        return (msg.task.get("key_channel", 0), tuple(msg.task.get("key_range", [0, 1 << 64])))
+        return (msg.task.get("key_channel", 0), tuple(msg.task.get("key_range", [0, (1 << 64) - 1])))
 
     def encode(self, msg):
         conf = msg.find_filter("KEY_CACHING")

@@ -108,18 +108,16 @@ class MinibatchReader:
 
     def __iter__(self):
         for b in self.reader:
-            keys = torch.from_numpy(b.keys.view(np.int64).copy())
-            loc = localize_torch(keys, 64)
-            # localize_torch works in the mixed space; the wire uses raw sorted keys
-            uniq_raw = torch.from_numpy(np.unique(b.keys).view(np.int64).copy())
-            _, inv = np.unique(b.keys, return_inverse=True)
+            # the wire carries raw keys sorted (key-ordered slicing over servers);
+            # countUniqIndex + remapIndex (localizer.h:69-191) as one np.unique
+            u, inv = np.unique(b.keys, return_inverse=True)
+            uniq_raw = torch.from_numpy(u.view(np.int64).copy())
             counts = np.bincount(inv, minlength=uniq_raw.numel())
             keep = np.ones(uniq_raw.numel(), bool)
             if self.filter is not None:
                 self.filter.insert(uniq_raw, torch.from_numpy(np.minimum(counts, 255).astype(np.uint8)))
                 k, _ = self.filter.query(uniq_raw, self.freq)
                 keep = k.numpy().astype(bool)
-            del loc
             remap = np.full(uniq_raw.numel(), -1, np.int64)
             remap[keep] = np.arange(int(keep.sum()))
             local_col = remap[inv].astype(np.int32)

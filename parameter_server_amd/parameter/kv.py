@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from ..ops.kv_table import KVTable, UpdateRule
+from ..system.message import KEY_MAX
 from .shared_parameter import SharedParameter, comp_ass_op
 
 
@@ -153,10 +154,10 @@ class KVBufferedVector(KVVector):
                 self.vals[chl] = np.zeros(0, self.dtype)
                 return
             t = msg.task["time"]
-            lo, hi = msg.task.get("key_range", [0, 1 << 64])
+            lo, hi = msg.task.get("key_range", [0, KEY_MAX])
             ukey = mk.astype(np.uint64)
             a = int(np.searchsorted(ukey, np.uint64(lo)))
-            b = int(np.searchsorted(ukey, np.uint64(min(hi, (1 << 64) - 1)))) if hi < (1 << 64) else ukey.size
+            b = int(np.searchsorted(ukey, np.uint64(hi))) if hi < KEY_MAX else ukey.size
             seg = mk[a:b]
             rng, bufs = self.recved.setdefault(t, ((a, b), []))
             for i, v in enumerate(msg.value):

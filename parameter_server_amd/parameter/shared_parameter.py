@@ -15,7 +15,7 @@ import numpy as np
 
 from ..ops.countmin import CountMinSketch
 from ..system.customer import KeyOrderedCustomer
-from ..system.message import CALL_CUSTOMER, Message, slice_key_ordered
+from ..system.message import CALL_CUSTOMER, KEY_MAX, Message, slice_key_ordered
 
 OPS = {
     "PLUS": np.add, "MINUS": np.subtract, "TIMES": np.multiply, "DIVIDE": np.divide,
@@ -66,7 +66,7 @@ class SharedParameter(KeyOrderedCustomer):
     # ------------------------------------------------------------ API
     def sync(self, msg: Message) -> int:
         msg.task["type"] = CALL_CUSTOMER
-        msg.task.setdefault("key_range", [0, 1 << 64])
+        msg.task.setdefault("key_range", [0, KEY_MAX])
         return self.port(msg.recver).submit(msg)
 
     def push(self, msg: Message) -> int:

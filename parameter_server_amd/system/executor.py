@@ -15,7 +15,7 @@ import threading
 import traceback
 
 from ..ops.native import core as core_mod
-from .message import (COMP_GROUP, GROUPS, INVALID_TIME, LIVE_GROUP, REPLY, SERVER_GROUP,
+from .message import (COMP_GROUP, GROUPS, INVALID_TIME, KEY_MAX, LIVE_GROUP, REPLY, SERVER_GROUP,
                       WORKER_GROUP, Message, new_task)
 
 
@@ -37,7 +37,7 @@ class RNode:
 
     def key_range(self):
         if self.node is None:
-            return (0, 1 << 64)
+            return (0, KEY_MAX)
         return (self.node.key_begin, self.node.key_end)
 
     # ----------------------------------------------------------- submit

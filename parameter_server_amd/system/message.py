@@ -19,6 +19,7 @@ import msgpack
 import numpy as np
 
 INVALID_TIME = -1
+KEY_MAX = (1 << 64) - 1  # exclusive end of the key space (2^64-1 itself is reserved)
 
 # Task.type
 TERMINATE, TERMINATE_CONFIRM, REPLY, MANAGE, CALL_CUSTOMER, HEARTBEATING = 1, 2, 3, 4, 5, 6
@@ -144,8 +145,8 @@ def slice_key_ordered(msg: Message, key_ranges: list[tuple[int, int]]) -> list[M
             continue
         ukey = key.astype(np.uint64, copy=False)
         a = int(np.searchsorted(ukey, np.uint64(lo), side="left"))
-        b = int(np.searchsorted(ukey, np.uint64(min(hi, (1 << 64) - 1)), side="left")) \
-            if hi < (1 << 64) else ukey.size
+        b = int(np.searchsorted(ukey, np.uint64(hi), side="left")) \
+            if hi < KEY_MAX else ukey.size
         if a >= b:
             m.valid = False
             m.key = key[0:0]

@@ -23,7 +23,7 @@ from ..ops.native import core
 from .message import (CALL_CUSTOMER, HEARTBEATING, MANAGE, REPLY, TERMINATE, Message,
                       new_task)
 
-KEY_MAX = 1 << 64
+from .message import KEY_MAX  # noqa: E402
 
 
 @dataclass
@@ -125,6 +125,9 @@ class Postoffice:
         self.verbose = verbose
         self.app_factory = app_factory
         self.van = core().Van(my_node.id)
+        import atexit
+
+        atexit.register(self.stop)  # never leave transport threads running at exit
         bind_host = "*"
         my_node.port = self.van.bind(bind_host, my_node.port)
         if print_van:
@@ -200,6 +203,8 @@ class Postoffice:
             self.hb.stop()
         for c in list(self.yp.customers.values()):
             c.executor.stop()
+        if self._recv_thread is not None and threading.current_thread() is not self._recv_thread:
+            self._recv_thread.join(timeout=5)
         if self.van:
             self.van.stop()
 
@@ -233,8 +238,12 @@ class Postoffice:
         self.van.send(msg.recver, msg.encode())
 
     def reply(self, req: Message, rep: Message | None = None):
-        rep = rep or Message()
-        rep.task.update({"type": REPLY, "request": False, "customer": req.task.get("customer", ""),
+        """Answer a request. With no payload this is the empty REPLY ack (reference
+        Postoffice::reply); a data reply (e.g. a pull answer) keeps CALL_CUSTOMER so the
+        requester's customer processes it (shared_parameter.h:105-109)."""
+        if rep is None:
+            rep = Message(task=new_task(type=REPLY))
+        rep.task.update({"request": False, "customer": req.task.get("customer", ""),
                          "time": req.task.get("time", -1), "key_channel": req.task.get("key_channel", 0)})
         rep.recver = req.sender
         req.replied = True
