@@ -100,6 +100,9 @@ class SparseLRTrainer:
             self.slot_buf = torch.empty(self.max_nnz, dtype=torch.int64, device=dev)
             self.w_buf = torch.empty(self.max_nnz, dtype=torch.float32, device=dev)
             self.touched = None
+        # multi-GPU: fuse push(t-1) into the pull exchange of step t (2 all-to-alls/step)
+        self.fused = self.G > 1 and self.filter is None and cfg.fixing_float_bytes == 0
+        self.pending = None
         self.step_count = 0
         self.examples = 0
         self.comm_bytes = 0
@@ -133,17 +136,110 @@ class SparseLRTrainer:
             hipops().kv_resolve(self.table.slots, loc.uniq, loc.n_uniq, slot, w_local, True, it,
                                 iv, isd, seed, self.table._err, self.table._inserted)
             push = ("local", slot, loc.n_uniq)
+        elif self.fused:
+            w_local, push = self._exchange_fused(loc.uniq, loc.n_uniq)
         else:
             w_local, push = self._pull(loc.uniq, loc.n_uniq)
         _, coef, _ = linear_forward(loc.local_col, w_local, labels, B=B, width=width or 0,
                                     row_ptr=row_ptr, vals=vals, loss=self.cfg.loss,
                                     coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
         grad, _ = linear_backward(loc, coef, B=B, width=width or 0, rows=rows, vals=vals)
-        self._push(grad, push)
+        if push[0] == "fused":
+            # deferred: travels with the next step's pull exchange (see _exchange_fused)
+            _, slot, send_c, recv_c, U = push
+            self.pending = (slot, send_c, recv_c, grad[:U].clone())
+        else:
+            self._push(grad, push)
         auc_from_hist(self.hist, self.metrics, self.step_dev)
         self.clock.tick(self.rank, self.step_count)
         self.step_count += 1
         self.examples += B
+
+    # ------------------------------------------------------- fused exchange (G > 1)
+    def _exchange_fused(self, uniq: torch.Tensor, n_uniq: torch.Tensor):
+        """One step of the multi-GPU data plane with 2 all-to-alls instead of 3:
+
+        A: per peer [keys(t) | grads(t-1)] packed as int32 words (keys are u32 when
+           the mixed key space has <= 32 bits, else 2 words) -> the owner first
+           applies the pushes of step t-1 (one optimizer step per source, rank
+           order), THEN resolves the pulls of step t, so every pull sees all pushes
+           up to t-1 (same order of operations as the unfused path: BSP results);
+        B: weights back.
+        The per-peer counts of both directions come from ONE all-gather of the
+        G x G count matrix (the only host synchronisation of the step)."""
+        G, dev = self.G, uniq.device
+        kw = 1 if self.bits <= 32 else 2
+        off = self.part.split_sorted(uniq, n_uniq)
+        send_t = (off[1:] - off[:-1]).to(torch.int64)
+        M = self.comm.all_gather_counts(send_t)          # [G src, G dst], host
+        send_t = M[self.rank].tolist()
+        recv_t = M[:, self.rank].tolist()
+        U = int(sum(send_t))
+        if self.pending is not None:
+            slot_p, send_p, recv_p, g_p = self.pending
+        else:
+            slot_p, send_p, recv_p, g_p = None, [0] * G, [0] * G, None
+        keys = uniq[:U]
+        k32 = keys.to(torch.int32) if kw == 1 else keys.contiguous().view(torch.int32)
+        g32 = g_p.view(torch.int32) if g_p is not None else None
+        pieces, ks, gs = [], 0, 0
+        for p in range(G):
+            pieces.append(k32[ks * kw:(ks + send_t[p]) * kw])
+            ks += send_t[p]
+            if g32 is not None:
+                pieces.append(g32[gs:gs + send_p[p]])
+                gs += send_p[p]
+        sendbuf = torch.cat(pieces) if pieces else torch.empty(0, dtype=torch.int32, device=dev)
+        ssz = [kw * send_t[p] + send_p[p] for p in range(G)]
+        rsz = [kw * recv_t[s] + recv_p[s] for s in range(G)]
+        recv = self.comm.all_to_all_v(sendbuf, ssz, rsz)
+        kparts, gparts, a = [], [], 0
+        for s in range(G):
+            kparts.append(recv[a:a + kw * recv_t[s]])
+            a += kw * recv_t[s]
+            n = recv_p[s]
+            if n and slot_p is not None:
+                gparts.append((slot_p[s], recv[a:a + n].view(torch.float32)))
+            a += n
+        self._apply_pushes(gparts)  # pushes of step t-1 first ...
+        rk = torch.cat(kparts)
+        if kw == 1:
+            req = rk.to(torch.int64) & 0xFFFFFFFF
+        else:
+            req = rk.view(torch.int64)
+        slot, w = self.table.resolve(req, insert=True)  # ... then the pulls of step t
+        slots_by_src, a = [], 0
+        for s in range(G):
+            slots_by_src.append(slot[a:a + recv_t[s]])
+            a += recv_t[s]
+        w_back = self.comm.all_to_all_v(w, recv_t, send_t)
+        return w_back, ("fused", slots_by_src, send_t, recv_t, U)
+
+    def _apply_pushes(self, parts):
+        """parts: [(slots, grads)] per source in rank order."""
+        if not parts:
+            return
+        if self.cfg.push_mode == "aggregate":
+            self._apply_aggregated(torch.cat([p[0] for p in parts]),
+                                   torch.cat([p[1] for p in parts]).contiguous())
+            return
+        for slot, g in parts:  # one optimizer step per push message, in rank order
+            self.table.update(slot, g.contiguous(), self.rule, self.stats)
+
+    def flush(self):
+        """Apply the deferred pushes of the last step (fused multi-GPU mode). Collective."""
+        if not self.fused or self.pending is None:
+            return
+        slot_p, send_p, recv_p, g_p = self.pending
+        self.pending = None
+        g_in = self.comm.all_to_all_v(g_p, send_p, recv_p)
+        parts, a = [], 0
+        for s in range(self.G):
+            n = recv_p[s]
+            if n:
+                parts.append((slot_p[s], g_in[a:a + n]))
+            a += n
+        self._apply_pushes(parts)
 
     # ---------------------------------------------------------------- pull/push
     def _pull(self, uniq: torch.Tensor, n_uniq: torch.Tensor):
@@ -238,7 +334,9 @@ class SparseLRTrainer:
 
     # ------------------------------------------------------------ reporting
     def progress(self, reset: bool = True) -> dict:
-        """Merged progress across ranks (reference ISGDScheduler::showProgress, sgd.h:45-80)."""
+        """Merged progress across ranks (reference ISGDScheduler::showProgress, sgd.h:45-80).
+        Collective when G > 1 (also applies deferred pushes)."""
+        self.flush()
         m = torch.cat([self.metrics, self.stats]).clone()
         if self.G > 1:
             m = self.comm.all_reduce_(m.to(self.comm.device) if self.comm.backend == "nccl"
@@ -264,6 +362,8 @@ class SparseLRTrainer:
         line per non-zero weight (src/parameter/kv_store.h:63-73)."""
         from ..utils.checkpoint import write_text_model
 
+        self.flush()
+
         keys, w, _, _ = self.table.occupied()
         raw = unmix(keys, self.bits)
         path = f"{prefix}_{node_id or f'S{self.rank}'}"
@@ -271,6 +371,7 @@ class SparseLRTrainer:
         return path
 
     def state_dict(self) -> dict:
+        self.flush()
         keys, w, z, n = self.table.occupied()
         return {"keys": unmix(keys, self.bits).cpu(), "w": w.cpu(), "z": z.cpu(), "n": n.cpu(),
                 "step": self.step_count, "bits": self.bits, "rank": self.rank, "world": self.G}

@@ -25,6 +25,10 @@ class Comm:
     def all_to_all_v(self, send: torch.Tensor, send_counts, recv_counts) -> torch.Tensor:
         return send
 
+    def all_gather_counts(self, counts: torch.Tensor) -> torch.Tensor:
+        """[world, world] int64 host matrix: row r = counts sent by rank r."""
+        return counts.reshape(1, -1).cpu()
+
     def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
         return t
 
@@ -80,6 +84,16 @@ class DistComm(Comm):
             out = out.to(send.device)
         self._sent += send.element_size() * (sum(sc) - sc[self.rank]) * max(1, send[0:1].numel())
         return out
+
+    def all_gather_counts(self, counts: torch.Tensor) -> torch.Tensor:
+        c = counts.to(torch.int64).reshape(-1).contiguous()
+        if self.backend == "nccl":
+            c = c.to(self.device)
+        elif c.is_cuda:
+            c = c.cpu()
+        out = torch.empty(self.world * c.numel(), dtype=torch.int64, device=c.device)
+        dist.all_gather_into_tensor(out, c, group=self.group)
+        return out.reshape(self.world, -1).cpu()
 
     def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
         ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
