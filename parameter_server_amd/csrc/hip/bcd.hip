@@ -1,0 +1,258 @@
+// Darlin block coordinate descent (L1-regularised logistic regression) on CDNA4.
+//
+// Reference hot loops (CPU, std::thread pools) this file replaces:
+//   K11 worker block gradient G_j, U_j       src/app/linear_method/darlin.h:381-427
+//   K13 server coordinate update + KKT filter + trust region
+//                                             src/app/linear_method/darlin.h:206-246
+//   K12 worker dual update dual_i *= exp(y_i dw_j x_ij)
+//                                             src/app/linear_method/darlin.h:472-502
+//   objective sum log(1 + 1/dual_i)           src/app/linear_method/darlin.h:504-511
+//
+// MI355X design:
+//  * the training matrix of a rank is one CSC over the GLOBAL column space of a
+//    feature group (columns = filtered keys, sorted); a feature block is a
+//    contiguous column range [c0, c1) == contiguous nnz range [p0, p1).
+//  * the reference keeps dual_i = exp(y_i x_i.w) and multiplies it; here the
+//    margin ym_i = y_i x_i.w is kept in fp64 and updated additively with the
+//    hardware fp64 global atomic add (log-space version of the same update; no
+//    overflow of exp for large margins). tau_i = 1 / (1 + exp(ym_i)).
+//  * the gradient is an nnz-parallel segmented reduction by column inside each
+//    wave64 (Hillis-Steele over 64 lanes, fp64): columns that start and end
+//    inside a wave are written with a plain store, only wave-spanning (head)
+//    columns use atomics -> no per-column wave imbalance for power-law columns.
+//  * every rank applies the (deterministic) server update to a replicated copy
+//    of the block after an all-reduce of (G, U); there is no pull phase.
+#include "common.cuh"
+
+#include <cmath>
+
+namespace psamd {
+
+namespace {
+
+__device__ __forceinline__ double softplus_neg(double m) {  // log(1 + exp(-m))
+  return m > 0 ? log1p(exp(-m)) : -m + log1p(exp(m));
+}
+
+__device__ __forceinline__ double shfl_up_d(double v, int off) {
+  return __shfl_up(v, off, 64);
+}
+
+// K11 -------------------------------------------------------------------------
+// G[c - c0] = -sum_i y_i tau_i x_ic
+// U[c - c0] =  sum_i min(tau_i (1 - tau_i) exp(|x_ic| delta_c), .25) x_ic^2
+// (binary: x = 1 and the exp factor is exp(delta_c), darlin.h:408-418).
+__global__ void __launch_bounds__(256)
+bcd_grad_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row,
+                const float* __restrict__ val, int64_t p0, int64_t p1, int64_t c0, int64_t ncols,
+                const double* __restrict__ ym, const float* __restrict__ y, int64_t nrows,
+                const double* __restrict__ delta, const uint8_t* __restrict__ active,
+                double* __restrict__ G, double* __restrict__ U) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = p0 + blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); i0 < p1;
+       i0 += stride) {
+    const int64_t i = i0 + lane;
+    const bool valid = i < p1;
+    int64_t c = -1;
+    double g = 0, u = 0;
+    if (valid) {
+      c = (int64_t)col[i] - c0;
+      if (c >= 0 && c < ncols && active[c0 + c]) {
+        const int32_t r = row[i];
+        if (in_range(r, nrows)) {
+          const double tau = 1.0 / (1.0 + exp(ym[r]));
+          const double yr = (double)y[r];
+          const double t2 = tau * (1.0 - tau);
+          const double dl = delta[c0 + c];
+          if (val) {
+            const double v = (double)val[i];
+            g = -yr * tau * v;
+            u = fmin(t2 * exp(fabs(v) * dl), 0.25) * v * v;
+          } else {
+            g = -yr * tau;
+            u = fmin(t2 * exp(dl), 0.25);
+          }
+        }
+      } else if (c < 0 || c >= ncols) {
+        c = -1;  // out-of-block element (corrupt input): contributes nothing
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double go = shfl_up_d(g, off);
+      const double uo = shfl_up_d(u, off);
+      const int64_t co = __shfl_up(c, off, 64);
+      if (lane >= off && co == c) { g += go; u += uo; }
+    }
+    const int64_t c_next = __shfl_down(c, 1, 64);
+    const int64_t c_lane0 = __shfl(c, 0, 64);
+    int64_t prev0 = -2;
+    if (lane == 0 && i0 > p0) prev0 = (int64_t)col[i0 - 1] - c0;
+    prev0 = __shfl(prev0, 0, 64);
+    const bool tail = valid && c >= 0 && (lane == 63 || c_next != c || i + 1 >= p1);
+    if (tail) {
+      const bool starts_inside = (c != c_lane0) || (prev0 != c);
+      bool ends_inside = true;
+      if (lane == 63 && i + 1 < p1) ends_inside = ((int64_t)col[i + 1] - c0) != c;
+      if (starts_inside && ends_inside) {
+        G[c] = g;
+        U[c] = u;
+      } else {
+        unsafeAtomicAdd(&G[c], g);
+        unsafeAtomicAdd(&U[c], u);
+      }
+    }
+  }
+}
+
+// K13 -------------------------------------------------------------------------
+// Per-coordinate proximal Newton step with trust region and KKT filter
+// (darlin.h:206-246). dw receives the applied change (0 if inactive / filtered).
+// Violation is max-reduced as the bit pattern of a non-negative double.
+__global__ void __launch_bounds__(256)
+bcd_update_kernel(int64_t c0, int64_t ncols, const double* __restrict__ G,
+                  const double* __restrict__ U, double* __restrict__ w, double* __restrict__ delta,
+                  uint8_t* __restrict__ active, double* __restrict__ dw, double eta, double lambda,
+                  double delta_max, double kkt_thr, unsigned long long* __restrict__ vio_bits) {
+  double vmax = 0;
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < ncols;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = c0 + j;
+    double d = 0;
+    if (active[k]) {
+      const double g = G[j], u = U[j] / eta + 1e-10;
+      const double gp = g + lambda, gn = g - lambda;
+      const double wk = w[k];
+      double vio = 0;
+      bool filtered = false;
+      if (wk == 0) {
+        if (gp < 0) vio = -gp;
+        else if (gn > 0) vio = gn;
+        else if (gp > kkt_thr && gn < -kkt_thr) filtered = true;
+      }
+      if (filtered) {
+        active[k] = 0;
+      } else {
+        vmax = fmax(vmax, vio);
+        d = -wk;
+        if (gp <= u * wk) d = -gp / u;
+        else if (gn >= u * wk) d = -gn / u;
+        const double dk = delta[k];
+        d = fmin(dk, fmax(-dk, d));
+        delta[k] = fmin(delta_max, 2 * fabs(d) + .1);
+        w[k] = wk + d;
+      }
+    }
+    dw[j] = d;
+  }
+  // wave max -> one atomic per wave
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, off, 64));
+  if ((threadIdx.x & 63) == 0 && vmax > 0)
+    atomicMax(vio_bits, (unsigned long long)__double_as_longlong(vmax));
+}
+
+// K12 -------------------------------------------------------------------------
+// ym_i += y_i * dw_c * x_ic for every nnz of the block with dw_c != 0.
+// scale_by_y = false is the plain SpMV  ym_i += w_c x_ic  used at init.
+__global__ void __launch_bounds__(256)
+bcd_dual_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row,
+                const float* __restrict__ val, int64_t p0, int64_t p1, int64_t c0, int64_t ncols,
+                const double* __restrict__ dw, const float* __restrict__ y, double* __restrict__ ym,
+                int64_t nrows) {
+  for (int64_t i = p0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < p1;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = (int64_t)col[i] - c0;
+    if (c < 0 || c >= ncols) continue;
+    const double d = dw[c];
+    if (d == 0) continue;
+    const int32_t r = row[i];
+    if (!in_range(r, nrows)) continue;
+    const double x = val ? (double)val[i] : 1.0;
+    unsafeAtomicAdd(&ym[r], (double)y[r] * d * x);
+  }
+}
+
+// objective: out[0] += sum_i log(1 + exp(-ym_i))
+__global__ void __launch_bounds__(256)
+bcd_objective_kernel(const double* __restrict__ ym, int64_t n, double* __restrict__ out) {
+  __shared__ double lds[4];
+  double s = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    s += softplus_neg(ym[i]);
+  const double t = block_sum_f64(s, lds);
+  if (threadIdx.x == 0) unsafeAtomicAdd(out, t);
+}
+
+// server stats over [c0, c1): out[0] += sum |w| (w != 0), out[1] += nnz(w),
+// out[2] += |active set|
+__global__ void __launch_bounds__(256)
+bcd_server_stats_kernel(const double* __restrict__ w, const uint8_t* __restrict__ active,
+                        int64_t c0, int64_t c1, double* __restrict__ out) {
+  __shared__ double lds[4];
+  double a = 0, nz = 0, na = 0;
+  for (int64_t k = c0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < c1;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const double wk = w[k];
+    if (wk != 0 && wk == wk) { a += fabs(wk); nz += 1; }
+    na += active[k] ? 1 : 0;
+  }
+  a = block_sum_f64(a, lds);
+  __syncthreads();
+  nz = block_sum_f64(nz, lds);
+  __syncthreads();
+  na = block_sum_f64(na, lds);
+  if (threadIdx.x == 0) {
+    unsafeAtomicAdd(&out[0], a);
+    unsafeAtomicAdd(&out[1], nz);
+    unsafeAtomicAdd(&out[2], na);
+  }
+}
+
+}  // namespace
+
+void bcd_grad(const int32_t* col, const int32_t* row, const float* val, int64_t p0, int64_t p1,
+              int64_t c0, int64_t ncols, const double* ym, const float* y, int64_t nrows,
+              const double* delta, const uint8_t* active, double* G, double* U, hipStream_t st) {
+  PSAMD_HIP_CHECK(hipMemsetAsync(G, 0, ncols * sizeof(double), st));
+  PSAMD_HIP_CHECK(hipMemsetAsync(U, 0, ncols * sizeof(double), st));
+  if (p1 <= p0) return;
+  bcd_grad_kernel<<<grid_for(p1 - p0, 256, 4096), 256, 0, st>>>(
+      col, row, val, p0, p1, c0, ncols, ym, y, nrows, delta, active, G, U);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void bcd_update(int64_t c0, int64_t ncols, const double* G, const double* U, double* w,
+                double* delta, uint8_t* active, double* dw, double eta, double lambda,
+                double delta_max, double kkt_thr, unsigned long long* vio_bits, hipStream_t st) {
+  if (ncols <= 0) return;
+  bcd_update_kernel<<<grid_for(ncols, 256, 4096), 256, 0, st>>>(
+      c0, ncols, G, U, w, delta, active, dw, eta, lambda, delta_max, kkt_thr, vio_bits);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void bcd_dual(const int32_t* col, const int32_t* row, const float* val, int64_t p0, int64_t p1,
+              int64_t c0, int64_t ncols, const double* dw, const float* y, double* ym,
+              int64_t nrows, hipStream_t st) {
+  if (p1 <= p0) return;
+  bcd_dual_kernel<<<grid_for(p1 - p0, 256, 4096), 256, 0, st>>>(col, row, val, p0, p1, c0, ncols,
+                                                                 dw, y, ym, nrows);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void bcd_objective(const double* ym, int64_t n, double* out, hipStream_t st) {
+  if (n <= 0) return;
+  bcd_objective_kernel<<<grid_for(n, 256, 1024), 256, 0, st>>>(ym, n, out);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void bcd_server_stats(const double* w, const uint8_t* active, int64_t c0, int64_t c1, double* out,
+                      hipStream_t st) {
+  if (c1 <= c0) return;
+  bcd_server_stats_kernel<<<grid_for(c1 - c0, 256, 1024), 256, 0, st>>>(w, active, c0, c1, out);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace psamd

@@ -69,6 +69,16 @@ void ff_minmax(const float*, int64_t, float*, hipStream_t);
 void ff_encode(const float*, int64_t, const float*, int, uint64_t, uint8_t*, hipStream_t);
 void ff_decode(const uint8_t*, int64_t, const float*, int, float*, hipStream_t);
 void key_signature(const uint64_t*, int64_t, unsigned long long*, hipStream_t);
+// bcd.hip
+void bcd_grad(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
+              const double*, const float*, int64_t, const double*, const uint8_t*, double*,
+              double*, hipStream_t);
+void bcd_update(int64_t, int64_t, const double*, const double*, double*, double*, uint8_t*,
+                double*, double, double, double, double, unsigned long long*, hipStream_t);
+void bcd_dual(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
+              const double*, const float*, double*, int64_t, hipStream_t);
+void bcd_objective(const double*, int64_t, double*, hipStream_t);
+void bcd_server_stats(const double*, const uint8_t*, int64_t, int64_t, double*, hipStream_t);
 }  // namespace psamd
 
 using at::Tensor;
@@ -511,5 +521,85 @@ PYBIND11_MODULE(_hipops, m) {
     chk(sig, at::kLong, "sig");
     psamd::key_signature(ptr<uint64_t>(keys), keys.numel(), ptr<unsigned long long>(sig),
                          cur_stream());
+  });
+
+  // ---------------------------------------------------------------- Darlin BCD
+  // CSC of one rank: col/row int32 per nnz (sorted by col), val f32 per nnz or None
+  // (binary). Block = nnz range [p0, p1) holding global columns [c0, c0 + ncols).
+  auto csc_check = [](const Tensor& col, const Tensor& row, const optional<Tensor>& val,
+                      int64_t p0, int64_t p1) {
+    chk(col, at::kInt, "col");
+    chk(row, at::kInt, "row");
+    check(col.numel() == row.numel(), "col/row size mismatch");
+    check(0 <= p0 && p0 <= p1 && p1 <= col.numel(), "nnz range outside the matrix");
+    if (val.has_value() && val->defined()) {
+      chk(*val, at::kFloat, "val");
+      check(val->numel() == col.numel(), "val size mismatch");
+    }
+  };
+  m.def("bcd_grad", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
+                                int64_t p1, int64_t c0, int64_t ncols, Tensor ym, Tensor y,
+                                Tensor delta, Tensor active, Tensor G, Tensor U) {
+    csc_check(col, row, val, p0, p1);
+    chk(ym, at::kDouble, "ym");
+    chk(y, at::kFloat, "y");
+    chk(delta, at::kDouble, "delta");
+    chk(active, at::kByte, "active");
+    chk(G, at::kDouble, "G");
+    chk(U, at::kDouble, "U");
+    check(y.numel() == ym.numel(), "y/ym size mismatch");
+    check(delta.numel() == active.numel(), "delta/active size mismatch");
+    check(c0 >= 0 && ncols >= 0 && c0 + ncols <= delta.numel(), "column block outside model");
+    check(G.numel() >= ncols && U.numel() >= ncols, "G/U too small");
+    psamd::bcd_grad(ptr<int32_t>(col), ptr<int32_t>(row), optr<float>(val, at::kFloat, "val"), p0,
+                    p1, c0, ncols, ptr<double>(ym), ptr<float>(y), ym.numel(), ptr<double>(delta),
+                    ptr<uint8_t>(active), ptr<double>(G), ptr<double>(U), cur_stream());
+  });
+  m.def("bcd_update", [](int64_t c0, int64_t ncols, Tensor G, Tensor U, Tensor w, Tensor delta,
+                         Tensor active, Tensor dw, double eta, double lambda, double delta_max,
+                         double kkt_thr, Tensor vio_bits) {
+    chk(G, at::kDouble, "G");
+    chk(U, at::kDouble, "U");
+    chk(w, at::kDouble, "w");
+    chk(delta, at::kDouble, "delta");
+    chk(active, at::kByte, "active");
+    chk(dw, at::kDouble, "dw");
+    chk(vio_bits, at::kLong, "vio_bits");
+    check(w.numel() == delta.numel() && w.numel() == active.numel(), "model arrays mismatch");
+    check(c0 >= 0 && ncols >= 0 && c0 + ncols <= w.numel(), "column block outside model");
+    check(G.numel() >= ncols && U.numel() >= ncols && dw.numel() >= ncols, "G/U/dw too small");
+    check(eta > 0, "eta must be > 0");
+    psamd::bcd_update(c0, ncols, ptr<double>(G), ptr<double>(U), ptr<double>(w),
+                      ptr<double>(delta), ptr<uint8_t>(active), ptr<double>(dw), eta, lambda,
+                      delta_max, kkt_thr, ptr<unsigned long long>(vio_bits), cur_stream());
+  });
+  m.def("bcd_dual", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
+                                int64_t p1, int64_t c0, int64_t ncols, Tensor dw, Tensor y,
+                                Tensor ym) {
+    csc_check(col, row, val, p0, p1);
+    chk(dw, at::kDouble, "dw");
+    chk(y, at::kFloat, "y");
+    chk(ym, at::kDouble, "ym");
+    check(y.numel() == ym.numel(), "y/ym size mismatch");
+    check(ncols >= 0 && dw.numel() >= ncols, "dw too small");
+    psamd::bcd_dual(ptr<int32_t>(col), ptr<int32_t>(row), optr<float>(val, at::kFloat, "val"), p0,
+                    p1, c0, ncols, ptr<double>(dw), ptr<float>(y), ptr<double>(ym), ym.numel(),
+                    cur_stream());
+  });
+  m.def("bcd_objective", [](Tensor ym, Tensor out) {
+    chk(ym, at::kDouble, "ym");
+    chk(out, at::kDouble, "out");
+    check(out.numel() >= 1, "out needs 1 double");
+    psamd::bcd_objective(ptr<double>(ym), ym.numel(), ptr<double>(out), cur_stream());
+  });
+  m.def("bcd_server_stats", [](Tensor w, Tensor active, int64_t c0, int64_t c1, Tensor out) {
+    chk(w, at::kDouble, "w");
+    chk(active, at::kByte, "active");
+    chk(out, at::kDouble, "out");
+    check(w.numel() == active.numel(), "w/active mismatch");
+    check(0 <= c0 && c0 <= c1 && c1 <= w.numel(), "range outside model");
+    check(out.numel() >= 3, "out needs 3 doubles");
+    psamd::bcd_server_stats(ptr<double>(w), ptr<uint8_t>(active), c0, c1, ptr<double>(out),
+                            cur_stream());
   });
 }

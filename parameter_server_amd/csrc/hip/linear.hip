@@ -89,7 +89,7 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
     coef_out[r] = coef;
     if (coef2_out) coef2_out[r] = coef2;
     loss_acc += loss;
-    corr_acc += (ym > 0.f) ? 1.0 : 0.0;
+    corr_acc += ((y > 0.f) == (m > 0.f)) ? 1.0 : 0.0;  // evaluation.h:55-57
     cnt += 1.0;
     if (hist) {
       const float p = 1.f / (1.f + expf(-m));

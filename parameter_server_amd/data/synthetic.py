@@ -1,0 +1,85 @@
+"""Deterministic synthetic datasets for batch (Darlin) training and tests.
+
+* ``sparse_classification`` — multi-group sparse data with a planted sparse
+  logistic model (power-law key popularity per group, optional real values).
+* ``criteo_slots`` — Criteo-shaped slots from the streaming generator
+  (``ops.synthetic.criteo_batch``): 39 groups with one key per example each.
+* ``write_text`` — dump as PS text (``label; grp k[:v] ...``) / LIBSVM files so the
+  runtime apps can read them through the normal parsers.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .slot_reader import SlotData
+
+
+def sparse_classification(rows: int, groups=(1, 2, 3), keys_per_group: int = 1000,
+                          nnz_per_row=(1, 3, 5), binary: bool = True, seed: int = 0,
+                          w_density: float = 0.1, alpha: float = 1.2, noise: float = 0.5,
+                          key_offset: int = 0) -> SlotData:
+    rng = np.random.default_rng(seed)
+    labels_margin = np.zeros(rows)
+    sd = SlotData(labels=np.zeros(rows, np.float32))
+    for gi, g in enumerate(groups):
+        k = nnz_per_row[gi % len(nnz_per_row)]
+        # power-law popularity: rank r drawn with p ~ 1/(r+1)^alpha
+        p = 1.0 / np.arange(1, keys_per_group + 1) ** alpha
+        p /= p.sum()
+        ids = rng.choice(keys_per_group, size=(rows, k), p=p)
+        keys = np.sort(ids, axis=1).reshape(-1).astype(np.uint64) * np.uint64(7) \
+            + np.uint64(key_offset + g * 1_000_003)
+        wg = np.where(rng.random(keys_per_group) < w_density, rng.normal(0, 2, keys_per_group), 0)
+        vals = None if binary else rng.uniform(0.2, 1.5, rows * k).astype(np.float32)
+        contrib = wg[ids.reshape(-1)] * (1.0 if vals is None else vals)
+        labels_margin += contrib.reshape(rows, k).sum(1)
+        off = np.arange(rows + 1, dtype=np.int64) * k
+        sd.groups[g] = (off, keys, vals)
+    pr = 1 / (1 + np.exp(-(labels_margin + rng.normal(0, noise, rows))))
+    sd.labels = np.where(rng.random(rows) < pr, 1.0, -1.0).astype(np.float32)
+    return sd
+
+
+def criteo_slots(rows: int, *, seed: int = 0, row0: int = 0, num_features: int = 10 ** 9,
+                 alpha: float = 1.1, device="cpu") -> SlotData:
+    """Criteo-shaped slot data: group s+1 holds slot s (one key per example)."""
+    from ..ops.synthetic import NUM_SLOTS, criteo_batch
+
+    keys, labels = criteo_batch(rows, seed=seed, row0=row0, num_features=num_features,
+                                alpha=alpha, device=device)
+    k = keys.view(rows, NUM_SLOTS).cpu().numpy().view(np.uint64)
+    sd = SlotData(labels=labels.cpu().numpy().astype(np.float32))
+    off = np.arange(rows + 1, dtype=np.int64)
+    for s in range(NUM_SLOTS):
+        sd.groups[s + 1] = (off, np.ascontiguousarray(k[:, s]), None)
+    return sd
+
+
+def write_text(sd: SlotData, path: str, fmt: str = "SPARSE_BINARY"):
+    """PS text format (reference text_parser.cc:200-250): ``label; g k[:v] k ...; ...``
+    or LIBSVM ``label k:v ...`` (groups merged)."""
+    gids = sorted(sd.groups)
+    with open(path, "w") as f:
+        for i in range(sd.rows):
+            y = 1 if sd.labels[i] > 0 else 0 if fmt != "LIBSVM" else -1
+            parts = [str(y)]
+            if fmt == "LIBSVM":
+                items = []
+                for g in gids:
+                    off, keys, vals = sd.groups[g]
+                    for j in range(off[i], off[i + 1]):
+                        items.append((int(keys[j]), 1.0 if vals is None else float(vals[j])))
+                items.sort()
+                f.write(" ".join([str(y if y > 0 else -1)] + [f"{k}:{v:g}" for k, v in items]) + "\n")
+                continue
+            for g in gids:
+                off, keys, vals = sd.groups[g]
+                if off[i + 1] == off[i]:
+                    continue
+                if vals is None:
+                    toks = [str(int(k)) for k in keys[off[i]:off[i + 1]]]
+                else:
+                    toks = [f"{int(k)}:{float(v):g}" for k, v in
+                            zip(keys[off[i]:off[i + 1]], vals[off[i]:off[i + 1]])]
+                parts.append(f"{g} " + " ".join(toks))
+            f.write("; ".join(parts) + "\n")

@@ -1,0 +1,412 @@
+"""Darlin: L1-regularised logistic regression by block coordinate descent, MI355X-native.
+
+Reference algorithm (PS v1 "Darlin"):
+* scheduler  src/app/linear_method/darlin.h:32-132 — passes over shuffled
+  feature blocks (prior groups first in pass 0), bounded block delay tau, KKT
+  filter threshold ``violation / num_ex * ratio``, convergence when the relative
+  objective <= epsilon twice with a KKT reset in between;
+* worker     darlin.h:297-502 — block gradient (G, U), dual update;
+* server     darlin.h:175-265 — aggregates G, U of all workers, proximal Newton
+  coordinate step with trust region + KKT filter, evaluation;
+* framework  src/learner/bcd.h — data loading, tail-feature filtering and key
+  localisation (preprocessData :324-465), block division (:78-122).
+
+MI355X design (one process per GPU, every rank = worker + server):
+* preprocessing builds, per feature group, the GLOBAL sorted list of kept keys
+  (tail filter with exact counts summed at owner ranks, then an all-gather), so
+  every rank's training matrix is ONE CSC over a global column space and a
+  feature block is a contiguous column range;
+* per block: HIP gradient kernel -> ONE fp64 all-reduce of [G; U] over RCCL
+  (replaces the push to servers and their ``KVBufferedVector`` sum) -> every
+  rank applies the identical coordinate update to its replica of the block
+  (replaces the server update AND the weight pull) -> HIP margin update;
+* bounded delay: the gradient of block i only waits for the dual updates of
+  blocks <= i - tau - 1, so with tau >= 1 the all-reduce of block i-1 is in
+  flight (on RCCL's stream) while block i's gradient runs;
+* state in HBM: w, delta (fp64) and the active set (uint8) per global column,
+  margins ym (fp64) per local example.
+
+Semantic differences (documented): tail filtering uses exact counts instead of a
+CountMin sketch (the sketch only over-counts, so the reference keeps a superset);
+a KKT-filtered weight stays 0 and is re-activated by a KKT reset (the reference
+server leaves it NaN forever, darlin.h:228-231 + 223-246).
+"""
+from __future__ import annotations
+
+import math
+import random
+import sys
+import time
+from collections import deque
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..data.slot_reader import SlotData, merge_slot_info
+from ..ops import bcd
+from ..parallel.comm import Comm, LocalComm
+from ..parallel.partition import even_divide
+
+SIGN = -(1 << 63)
+
+
+def _flip(keys_u64: np.ndarray) -> np.ndarray:
+    """uint64 -> int64 whose signed order is the unsigned order."""
+    return (keys_u64.astype(np.uint64) ^ np.uint64(1 << 63)).view(np.int64)
+
+
+def _unflip(k: np.ndarray) -> np.ndarray:
+    return k.view(np.uint64) ^ np.uint64(1 << 63)
+
+
+@dataclass
+class DarlinConfig:
+    l1: float = 1.0                 # penalty.lambda(0)
+    eta: float = 1.0                # learning_rate.alpha
+    delta_init: float = 1.0         # [PS.LM.delta_init_value]
+    delta_max: float = 5.0          # [PS.LM.delta_max_value]
+    kkt_ratio: float = 10.0         # [PS.LM.kkt_filter_threshold_ratio]
+    block_ratio: float = 4.0        # feature_block_ratio
+    random_order: bool = True       # random_feature_block_order
+    prior_groups: tuple = ()        # prior_fea_group
+    prior_iters: int = 5            # num_iter_for_prior_fea_group
+    tau: int = 0                    # max_block_delay
+    max_pass: int = 10              # max_pass_of_data
+    epsilon: float = 1e-4
+    tail_freq: int = 0              # tail_feature_freq
+    init_w: float = 0.0             # init_w (ZERO / CONSTANT)
+    seed: int = 0
+
+    @classmethod
+    def from_lm(cls, lm, seed: int = 0) -> "DarlinConfig":
+        d = lm.darlin
+        lam = list(lm.penalty.__getattr__("lambda")) or [1.0]
+        init = 0.0
+        if d.has("init_w") and d.init_w.type == "CONSTANT":
+            init = float(d.init_w.constant)
+        return cls(l1=float(lam[0]), eta=float(lm.learning_rate.alpha),
+                   delta_init=float(d.ext("delta_init_value")),
+                   delta_max=float(d.ext("delta_max_value")),
+                   kkt_ratio=float(d.ext("kkt_filter_threshold_ratio")),
+                   block_ratio=float(d.feature_block_ratio),
+                   random_order=bool(d.random_feature_block_order),
+                   prior_groups=tuple(d.prior_fea_group), prior_iters=int(d.num_iter_for_prior_fea_group),
+                   tau=int(d.max_block_delay), max_pass=int(d.max_pass_of_data),
+                   epsilon=float(d.epsilon), tail_freq=int(d.tail_feature_freq), init_w=init,
+                   seed=seed)
+
+
+def divide_feature_blocks(info: dict, ratio: float) -> list[tuple[int, int, int]]:
+    """[(group, key_begin, key_end)] — reference BCDScheduler::divideFeatureBlocks
+    (src/learner/bcd.h:78-106): a group with nnz_per_row > 1 is split into
+    ceil(nnz_per_row * ratio) even key ranges of [min_key, max_key)."""
+    out = []
+    for g in sorted(info["slots"]):
+        if g == 0:
+            continue
+        s = info["slots"][g]
+        npr = s["nnz_ele"] / max(s["nnz_ex"], 1)
+        n = max(int(math.ceil(npr * ratio)), 1) if npr > 1 + 1e-6 else 1
+        for i in range(n):
+            a, b = even_divide(s["min_key"], s["max_key"], n, i)
+            if b > a:
+                out.append((g, a, b))
+    return out
+
+
+def block_orders(blocks, cfg: DarlinConfig, rng: random.Random):
+    """(blk_order, prior_blk_order) — bcd.h:108-121."""
+    blk = list(range(len(blocks)))
+    prior = []
+    for g in cfg.prior_groups:
+        tmp = [k for k, b in enumerate(blocks) if b.group == g]
+        if not tmp:
+            continue
+        for _ in range(cfg.prior_iters):
+            if cfg.random_order:
+                rng.shuffle(tmp)
+            prior.extend(tmp)
+    return blk, prior
+
+
+@dataclass
+class Block:
+    group: int
+    key_begin: int
+    key_end: int
+    c0: int
+    c1: int
+    p0: int
+    p1: int
+
+    @property
+    def ncols(self):
+        return self.c1 - self.c0
+
+
+@dataclass
+class BCDProgress:
+    objective: float = 0.0
+    relative_obj: float = 0.0
+    nnz_w: int = 0
+    violation: float = 0.0
+    nnz_active_set: int = 0
+    total_time: float = 0.0
+    busy_time: list = field(default_factory=list)
+
+
+class DarlinTrainer:
+    """Darlin BCD on one rank (GPU or CPU tensors); ``comm`` spans all ranks."""
+
+    def __init__(self, data: SlotData, cfg: DarlinConfig, comm: Comm | None = None,
+                 device="cpu", verbose: bool = False):
+        self.cfg = cfg
+        self.comm = comm or LocalComm(device)
+        self.G = self.comm.world
+        self.rank = self.comm.rank
+        self.device = torch.device(device)
+        self.verbose = verbose
+        self.rng = random.Random(cfg.seed)
+        t0 = time.time()
+        self._preprocess(data)
+        self.preprocess_time = time.time() - t0
+        self.progress: list[BCDProgress] = []
+        self.kkt_thr = 1e20
+
+    # ------------------------------------------------------------ preprocess
+    def _global_info(self, data: SlotData) -> dict:
+        infos = self.comm.all_gather_obj(data.info()) if self.G > 1 else [data.info()]
+        return merge_slot_info(infos)
+
+    def _group_keys(self, gid: int, uniq: np.ndarray, cnt: np.ndarray, info_g) -> np.ndarray:
+        """Global sorted (flipped) key list of group ``gid`` after the tail filter."""
+        freq = self.cfg.tail_freq
+        if self.G == 1:
+            return uniq[cnt > freq] if freq > 0 else uniq
+        # owner = even split of the group's (flipped) key range; counts summed at owners
+        lo = int(_flip(np.array([info_g["min_key"]], np.uint64))[0])
+        hi = int(_flip(np.array([info_g["max_key"] - 1], np.uint64))[0]) + 1
+        bounds = np.array([even_divide(lo, hi, self.G, r)[0] for r in range(1, self.G)], np.int64)
+        owner = np.searchsorted(bounds, uniq, side="right")
+        sc = np.bincount(owner, minlength=self.G).astype(np.int64)
+        comm = self.comm
+        rc = comm.exchange_counts(torch.from_numpy(sc)).cpu().numpy()
+        rk = self._a2a(uniq, sc, rc)
+        rn = self._a2a(cnt.astype(np.int64), sc, rc)
+        if rk.size:
+            u, inv = np.unique(rk, return_inverse=True)
+            tot = np.bincount(inv, weights=rn.astype(np.float64)).astype(np.int64)
+            kept = u[tot > freq] if freq > 0 else u
+        else:
+            kept = np.zeros(0, np.int64)
+        # all-gather of the owners' kept lists (owner ranges are ordered -> sorted)
+        n = np.array([kept.size] * self.G, np.int64)
+        rcnt = comm.exchange_counts(torch.from_numpy(n)).cpu().numpy()
+        return self._a2a(np.tile(kept, self.G), n, rcnt)
+
+    def _a2a(self, x: np.ndarray, sc, rc) -> np.ndarray:
+        t = torch.from_numpy(np.ascontiguousarray(x))
+        if getattr(self.comm, "backend", "") == "nccl":
+            t = t.to(self.comm.device)
+        return self.comm.all_to_all_v(t, sc, rc).cpu().numpy()
+
+    def _preprocess(self, data: SlotData):
+        cfg = self.cfg
+        self.info = self._global_info(data)
+        self.num_ex = int(self.info["num_ex"])
+        rows = data.rows
+        if rows >= (1 << 31):
+            raise ValueError("a rank holds at most 2^31-1 examples")
+        self.rows = rows
+        gids = sorted(g for g in self.info["slots"] if g != 0)
+        cols, rws, vals = [], [], []
+        self.group_keys: dict[int, np.ndarray] = {}   # flipped, sorted
+        self.group_base: dict[int, int] = {}
+        base = 0
+        valued = any(data.groups.get(g, (None, None, None))[2] is not None for g in gids)
+        for g in gids:
+            if g in data.groups:
+                off, keys, v = data.groups[g]
+            else:
+                off, keys, v = np.zeros(rows + 1, np.int64), np.zeros(0, np.uint64), None
+            kf = _flip(keys)
+            uniq, inv, cnt = np.unique(kf, return_inverse=True, return_counts=True)
+            gk = self._group_keys(g, uniq, cnt, self.info["slots"][g])
+            self.group_keys[g] = gk
+            self.group_base[g] = base
+            # local nnz -> global column (drop tail-filtered keys)
+            pos = np.searchsorted(gk, uniq)
+            hit = (pos < gk.size) & (gk[np.minimum(pos, max(gk.size - 1, 0))] == uniq) \
+                if gk.size else np.zeros(uniq.size, bool)
+            ucol = np.where(hit, pos + base, -1)
+            c = ucol[inv]
+            r = np.repeat(np.arange(rows, dtype=np.int64), np.diff(off))
+            keep = c >= 0
+            cols.append(c[keep])
+            rws.append(r[keep])
+            if valued:
+                vals.append((np.ones(keys.size, np.float32) if v is None else v)[keep])
+            base += gk.size
+        self.num_cols = base
+        if base >= (1 << 31):
+            raise ValueError("at most 2^31-1 global columns")
+        col = np.concatenate(cols) if cols else np.zeros(0, np.int64)
+        row = np.concatenate(rws) if rws else np.zeros(0, np.int64)
+        order = np.argsort(col, kind="stable")  # CSR -> CSC (reference toColMajor)
+        col, row = col[order], row[order]
+        val = np.concatenate(vals)[order] if valued else None
+        colptr = np.zeros(base + 1, np.int64)
+        np.cumsum(np.bincount(col, minlength=base), out=colptr[1:])
+        self.colptr = colptr
+        dev = self.device
+        self.col = torch.from_numpy(col.astype(np.int32)).to(dev)
+        self.row = torch.from_numpy(row.astype(np.int32)).to(dev)
+        self.val = None if val is None else torch.from_numpy(val.astype(np.float32)).to(dev)
+        self.y = torch.from_numpy(np.where(data.labels > 0, 1.0, -1.0).astype(np.float32)).to(dev)
+        self.nnz = int(col.size)
+        # blocks: key ranges -> global column ranges
+        self.blocks: list[Block] = []
+        for g, a, b in divide_feature_blocks(self.info, cfg.block_ratio):
+            gk = self.group_keys[g]
+            fa = int(_flip(np.array([a], np.uint64))[0])
+            fb = int(_flip(np.array([b - 1], np.uint64))[0])
+            c0 = self.group_base[g] + int(np.searchsorted(gk, fa, side="left"))
+            c1 = self.group_base[g] + int(np.searchsorted(gk, fb, side="right"))
+            self.blocks.append(Block(g, a, b, c0, c1, int(colptr[c0]), int(colptr[c1])))
+        self.blk_order, self.prior_order = block_orders(self.blocks, cfg, self.rng)
+        # model state (replicated per rank) and margins
+        f64 = torch.float64
+        self.w = torch.full((base,), float(cfg.init_w), dtype=f64, device=dev)
+        self.delta = torch.full((base,), float(cfg.delta_init), dtype=f64, device=dev)
+        self.active = torch.ones(base, dtype=torch.uint8, device=dev)
+        self.ym = torch.zeros(rows, dtype=f64, device=dev)
+        if cfg.init_w != 0 and base:
+            bcd.dual(self.col, self.row, self.val, 0, self.nnz, 0, base, self.w, self.y, self.ym)
+        self.vio = torch.zeros(1, dtype=torch.int64, device=dev)
+        # owned column share for the server-side statistics
+        self.own = even_divide(0, base, self.G, self.rank)
+        if self.verbose and self.rank == 0:
+            print(f"Darlin: {self.num_ex} examples, {base} features in {len(gids)} groups, "
+                  f"{len(self.blocks)} blocks", file=sys.stderr)
+
+    # -------------------------------------------------------------- one pass
+    def _launch(self, b: Block):
+        GU = torch.empty(2 * b.ncols, dtype=torch.float64, device=self.device)
+        G, U = GU[:b.ncols], GU[b.ncols:]
+        bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
+                 self.delta, self.active, G, U)
+        work = self.comm.all_reduce_async(GU) if self.G > 1 else None
+        return (b, GU, work)
+
+    def _finish(self, item):
+        b, GU, work = item
+        if work is not None:
+            work.wait()
+        G, U = GU[:b.ncols], GU[b.ncols:]
+        c = self.cfg
+        dw, _ = bcd.update(b.c0, b.ncols, G, U, self.w, self.delta, self.active, c.eta, c.l1,
+                           c.delta_max, self.kkt_thr, vio=self.vio)
+        bcd.dual(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, dw, self.y, self.ym)
+
+    def run_pass(self, it: int, reset_kkt: bool = False) -> BCDProgress:
+        cfg = self.cfg
+        order = list(self.blk_order)
+        if cfg.random_order:
+            self.rng.shuffle(order)
+        nprior = 0
+        if it == 0:
+            order = list(self.prior_order) + order
+            nprior = len(self.prior_order)
+        if reset_kkt:
+            self.active.fill_(1)
+        self.vio.zero_()  # kkt threshold set at the first block of the pass: violation_ = 0
+        t0 = time.time()
+        inflight: deque = deque()
+        for i, k in enumerate(order):
+            tau = 0 if i < nprior else cfg.tau  # prior blocks: zero delay (darlin.h:86-88)
+            while inflight and inflight[0][0] <= i - tau - 1:
+                self._finish(inflight.popleft()[1])
+            inflight.append((i, self._launch(self.blocks[k])))
+        while inflight:
+            self._finish(inflight.popleft()[1])
+        prog = self.evaluate()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        busy = time.time() - t0
+        prog.busy_time = [busy]
+        prev = self.progress[-1].objective if self.progress else None
+        prog.relative_obj = 1.0 if prev is None else prev / prog.objective - 1
+        prog.total_time = (self.progress[-1].total_time if self.progress else 0.0) + busy
+        self.progress.append(prog)
+        return prog
+
+    def evaluate(self) -> BCDProgress:
+        """Objective = sum_i log(1+exp(-ym_i)) + l1 * ||w||_1 (darlin.h:248-265, 504-511)."""
+        obj = bcd.objective(self.ym)
+        st = bcd.server_stats(self.w, self.active, self.own[0], self.own[1])
+        vio = self.vio.view(torch.float64)
+        if self.G > 1:
+            buf = torch.cat([obj, st])
+            self.comm.all_reduce_(buf)
+            v = vio.clone()
+            self.comm.all_reduce_(v, op="max")
+            obj, st, vio = buf[:1], buf[1:], v
+        h = torch.cat([obj, st, vio]).cpu().tolist()
+        return BCDProgress(objective=h[0] + self.cfg.l1 * h[1], nnz_w=int(h[2]),
+                           nnz_active_set=int(h[3]), violation=h[4])
+
+    def train(self, printer=None) -> list[BCDProgress]:
+        """The scheduler loop of darlin.h:50-126."""
+        cfg = self.cfg
+        reset = False
+        for it in range(cfg.max_pass):
+            prog = self.run_pass(it, reset_kkt=reset)
+            if printer is not None:
+                printer(it, prog, self)
+            self.kkt_thr = prog.violation / max(self.num_ex, 1) * cfg.kkt_ratio
+            rel = prog.relative_obj
+            if 0 < rel <= cfg.epsilon:
+                if reset:
+                    break
+                reset = True
+            else:
+                reset = False
+        return self.progress
+
+    # ------------------------------------------------------------ model I/O
+    def model(self) -> tuple[np.ndarray, np.ndarray]:
+        """(raw uint64 keys, fp64 weights) of all global columns, group by group."""
+        keys = np.concatenate([_unflip(self.group_keys[g]) for g in sorted(self.group_keys)]) \
+            if self.group_keys else np.zeros(0, np.uint64)
+        return keys, self.w.cpu().numpy()
+
+    def save_model(self, prefix: str, node_id: str | None = None) -> str:
+        """Text ``key\\tw`` of the non-zero weights in this rank's server key range
+        (reference BCDServer::saveModel, src/learner/bcd.h:251-272; server s owns
+        Range::all().evenDivide(S, s), src/system/postmaster.cc:17-31)."""
+        from ..utils.checkpoint import write_text_model
+
+        keys, w = self.model()
+        lo, hi = even_divide(0, 1 << 64, self.G, self.rank)
+        ku = keys.astype(np.uint64)
+        m = (ku >= np.uint64(lo)) & ((ku < np.uint64(hi)) if hi < (1 << 64) else True)
+        m &= (w != 0) & ~np.isnan(w)
+        path = f"{prefix}_{node_id or f'S{self.rank}'}"
+        write_text_model(path, ku[m], w[m])
+        return path
+
+
+# ----------------------------------------------------------------- printing
+def show_progress(it: int, prog: BCDProgress, trainer: DarlinTrainer, out=sys.stderr):
+    """The three tables of darlin.h:136-156 / bcd.h:146-178."""
+    if it == 0:
+        out.write("     |        training        |  sparsity |      KKT filter     |    time (sec.)\n")
+        out.write("iter |  objective    relative |     |w|_0 | threshold  #activet |(app:min max) total\n")
+        out.write(" ----+------------------------+-----------+---------------------+-----------------\n")
+    bt = prog.busy_time or [0.0]
+    dt = prog.total_time - (trainer.progress[-2].total_time if len(trainer.progress) > 1 else 0)
+    out.write(f"{it:4d} | {prog.objective:.5e}  {prog.relative_obj:.3e} |{prog.nnz_w:10d} "
+              f"| {trainer.kkt_thr:.1e} {prog.nnz_active_set:11d} "
+              f"|{min(bt):6.1f}{max(bt):6.1f}{dt:6.1f}\n")
+    out.flush()

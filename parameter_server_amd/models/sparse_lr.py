@@ -346,7 +346,8 @@ class SparseLRTrainer:
         out = {
             "examples": float(m[2]),
             "loss": float(m[0]) / n,
-            "accuracy": float(m[1]) / n,
+            # reference Evaluation::accuracy folds to max(acc, 1-acc) (evaluation.h:61)
+            "accuracy": max(float(m[1]) / n, 1.0 - float(m[1]) / n) if m[2] > 0 else 0.0,
             "auc": float(m[3]) / max(float(m[4]), 1.0),
             "nnz_w": float(m[8]),
             "updt_ratio": math.sqrt(float(m[10])) / math.sqrt(max(float(m[9]), 1e-20)),

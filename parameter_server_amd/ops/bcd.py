@@ -1,0 +1,141 @@
+"""Darlin block-coordinate-descent ops (L1 logistic regression).
+
+GPU: ``csrc/hip/bcd.hip`` (K11 block gradient, K13 coordinate update with KKT
+filter + trust region, K12 margin update, objective / server statistics).
+CPU: the same math in plain fp64 PyTorch, which is both the host path of the
+runtime apps and the reference the HIP kernels are tested against.
+
+Conventions (shared with the kernels):
+* a rank's training matrix is ONE CSC over the global column space: ``col`` and
+  ``row`` int32 per nnz sorted by column, ``val`` f32 per nnz or ``None``
+  (binary). A feature block is a column range ``[c0, c0+ncols)`` stored in the
+  nnz range ``[p0, p1)``.
+* ``ym`` (fp64, per row) is the margin ``y_i * x_i.w``; the reference keeps
+  ``dual_i = exp(ym_i)`` instead (src/app/linear_method/darlin.h:288-293) and
+  uses ``tau_i = 1 / (1 + dual_i)``.
+* ``w``, ``delta`` (fp64) and ``active`` (uint8) are indexed by global column.
+
+Reference math: gradient darlin.h:381-427, update darlin.h:206-246, dual update
+darlin.h:472-502, objective darlin.h:504-511, server evaluate darlin.h:248-265.
+"""
+from __future__ import annotations
+
+import torch
+
+from .native import hipops, is_gpu
+
+
+def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, active,
+         G=None, U=None):
+    """Block gradient: returns (G, U) fp64[ncols] (inactive columns contribute 0)."""
+    dev = ym.device
+    if G is None:
+        G = torch.empty(ncols, dtype=torch.float64, device=dev)
+    if U is None:
+        U = torch.empty(ncols, dtype=torch.float64, device=dev)
+    if is_gpu(ym):
+        hipops().bcd_grad(col, row, val, p0, p1, c0, ncols, ym, y, delta, active, G, U)
+        return G, U
+    G.zero_()
+    U.zero_()
+    c = col[p0:p1].long() - c0
+    r = row[p0:p1].long()
+    keep = active[c0 + c].bool()
+    c, r = c[keep], r[keep]
+    tau = 1.0 / (1.0 + torch.exp(ym[r]))
+    yr = y[r].double()
+    t2 = tau * (1 - tau)
+    dl = delta[c0 + c]
+    if val is None:
+        g = -yr * tau
+        u = torch.clamp(t2 * torch.exp(dl), max=0.25)
+    else:
+        v = val[p0:p1][keep].double()
+        g = -yr * tau * v
+        u = torch.clamp(t2 * torch.exp(v.abs() * dl), max=0.25) * v * v
+    G.index_add_(0, c, g)
+    U.index_add_(0, c, u)
+    return G, U
+
+
+def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
+           delta_max: float, kkt_thr: float, dw=None, vio=None):
+    """Coordinate update of block [c0, c0+ncols). Returns (dw fp64[ncols], vio) where
+    ``vio`` is an int64[1] tensor holding the max KKT violation as fp64 bits
+    (max-accumulated across calls; see ``violation``)."""
+    dev = w.device
+    if dw is None:
+        dw = torch.empty(ncols, dtype=torch.float64, device=dev)
+    if vio is None:
+        vio = torch.zeros(1, dtype=torch.int64, device=dev)
+    if is_gpu(w):
+        hipops().bcd_update(c0, ncols, G, U, w, delta, active, dw, eta, lam, delta_max, kkt_thr,
+                            vio)
+        return dw, vio
+    sl = slice(c0, c0 + ncols)
+    act = active[sl].bool()
+    g, u = G[:ncols], U[:ncols] / eta + 1e-10
+    gp, gn = g + lam, g - lam
+    wk = w[sl].clone()
+    zero = wk == 0
+    v = torch.zeros_like(g)
+    v = torch.where(zero & (gp < 0), -gp, v)
+    v = torch.where(zero & ~(gp < 0) & (gn > 0), gn, v)
+    filt = zero & ~(gp < 0) & ~(gn > 0) & (gp > kkt_thr) & (gn < -kkt_thr) & act
+    upd = act & ~filt
+    d = -wk
+    d = torch.where(gp <= u * wk, -gp / u, torch.where(gn >= u * wk, -gn / u, d))
+    dk = delta[sl]
+    d = torch.minimum(dk, torch.maximum(-dk, d))
+    d = torch.where(upd, d, torch.zeros_like(d))
+    delta[sl] = torch.where(upd, torch.clamp(2 * d.abs() + .1, max=delta_max), dk)
+    w[sl] = wk + d
+    active[sl] = torch.where(filt, torch.zeros_like(active[sl]), active[sl])
+    dw[:ncols] = d
+    vm = float(torch.where(upd, v, torch.zeros_like(v)).max()) if ncols else 0.0
+    cur = violation(vio)
+    if vm > cur:
+        vio.copy_(torch.tensor([vm], dtype=torch.float64).view(torch.int64))
+    return dw, vio
+
+
+def violation(vio) -> float:
+    """fp64 value of the violation accumulator written by ``update``."""
+    return float(vio.detach().cpu().view(torch.float64)[0])
+
+
+def dual(col, row, val, p0: int, p1: int, c0: int, ncols: int, dw, y, ym):
+    """ym_i += y_i * dw_c * x_ic over the block (in place)."""
+    if is_gpu(ym):
+        hipops().bcd_dual(col, row, val, p0, p1, c0, ncols, dw, y, ym)
+        return ym
+    c = col[p0:p1].long() - c0
+    r = row[p0:p1].long()
+    d = dw[c]
+    x = torch.ones_like(d) if val is None else val[p0:p1].double()
+    ym.index_add_(0, r, y[r].double() * d * x)
+    return ym
+
+
+def objective(ym) -> torch.Tensor:
+    """fp64[1] tensor: sum_i log(1 + exp(-ym_i)) (stays on device)."""
+    out = torch.zeros(1, dtype=torch.float64, device=ym.device)
+    if is_gpu(ym):
+        hipops().bcd_objective(ym, out)
+        return out
+    out[0] = torch.nn.functional.softplus(-ym).sum()
+    return out
+
+
+def server_stats(w, active, c0: int, c1: int) -> torch.Tensor:
+    """fp64[3] tensor: [sum |w| over nonzero, nnz(w), |active set|] over [c0, c1)."""
+    out = torch.zeros(3, dtype=torch.float64, device=w.device)
+    if is_gpu(w):
+        hipops().bcd_server_stats(w, active, c0, c1, out)
+        return out
+    ws = w[c0:c1]
+    nz = (ws != 0) & ~torch.isnan(ws)
+    out[0] = ws[nz].abs().sum()
+    out[1] = nz.sum()
+    out[2] = active[c0:c1].double().sum()
+    return out

@@ -77,7 +77,7 @@ def linear_forward(local_col, w_local, labels, *, B: int, width: int = 0, row_pt
     if metrics is not None:
         y = torch.where(labels[:B] > 0, 1.0, -1.0)
         metrics[0] += float(lo.double().sum())
-        metrics[1] += float(((y * m) > 0).double().sum())
+        metrics[1] += float(((y > 0) == (m > 0)).double().sum())
         metrics[2] += float(B)
     if hist is not None:
         p = torch.sigmoid(m)

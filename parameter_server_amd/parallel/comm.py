@@ -15,6 +15,11 @@ import torch
 import torch.distributed as dist
 
 
+class _Done:
+    def wait(self):
+        return True
+
+
 class Comm:
     rank = 0
     world = 1
@@ -31,6 +36,11 @@ class Comm:
 
     def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
         return t
+
+    def all_reduce_async(self, t: torch.Tensor, op="sum"):
+        """Start an in-place all-reduce; returns a handle whose ``wait()`` orders the
+        current stream after it (RCCL runs it on its own stream meanwhile)."""
+        return _Done()
 
     def all_gather_obj(self, obj):
         return [obj]
@@ -104,6 +114,13 @@ class DistComm(Comm):
             return t
         dist.all_reduce(t, op=ops[op], group=self.group)
         return t
+
+    def all_reduce_async(self, t: torch.Tensor, op="sum"):
+        if self.backend == "gloo" and t.is_cuda:  # rehearsal mode: synchronous, staged
+            self.all_reduce_(t, op)
+            return _Done()
+        ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+        return dist.all_reduce(t, op=ops[op], group=self.group, async_op=True)
 
     def all_gather_obj(self, obj):
         out = [None] * self.world

@@ -129,38 +129,31 @@ class Message:
 
 
 def slice_key_ordered(msg: Message, key_ranges: list[tuple[int, int]]) -> list[Message]:
-    """Split a message with a sorted key array into one piece per key range.
-    Values carry k entries per key. Pieces with no key overlap are marked invalid
-    (they are answered locally instead of being sent)."""
+    """Split a message with a sorted key array into one piece per key range
+    (reference sliceKeyOrderedMsg, src/system/message.h:120-159). Every piece keeps
+    the message's own ``key_range`` (receivers align buffers to it); a piece is
+    invalid (answered locally instead of sent) iff the receiver's range does not
+    intersect the message range. Values carry k entries per key."""
     out = []
     key = msg.key
+    mlo, mhi = msg.task.get("key_range", [0, KEY_MAX])
+    ukey = None if key is None else key.astype(np.uint64, copy=False)
     for lo, hi in key_ranges:
         m = msg.copy_header()
-        m.task["key_range"] = [lo, hi]
         m.fin_handle, m.recv_handle, m.wait = msg.fin_handle, msg.recv_handle, msg.wait
-        if key is None:
-            m.valid = True
+        m.valid = max(lo, mlo) < min(hi, mhi)
+        if ukey is None:
             m.value = list(msg.value)
             out.append(m)
             continue
-        ukey = key.astype(np.uint64, copy=False)
-        a = int(np.searchsorted(ukey, np.uint64(lo), side="left"))
-        b = int(np.searchsorted(ukey, np.uint64(hi), side="left")) \
-            if hi < KEY_MAX else ukey.size
-        if a >= b:
-            m.valid = False
-            m.key = key[0:0]
-            m.task["has_key"] = True
-            m.value = [v[0:0] for v in msg.value]
-            out.append(m)
-            continue
+        plo, phi = min(max(lo, mlo), mhi), min(max(hi, mlo), mhi)  # Range::project
+        a = int(np.searchsorted(ukey, np.uint64(plo), side="left"))
+        b = int(np.searchsorted(ukey, np.uint64(phi), side="left")) \
+            if phi < KEY_MAX else ukey.size
+        b = max(a, b)
         m.key = key[a:b]
         m.task["has_key"] = True
         n = key.size
-        vals = []
-        for v in msg.value:
-            k = v.size // n if n else 0
-            vals.append(v[a * k:b * k])
-        m.value = vals
+        m.value = [v[a * (v.size // n):b * (v.size // n)] if n else v[0:0] for v in msg.value]
         out.append(m)
     return out

@@ -16,14 +16,18 @@ import numpy as np
 import torch
 
 
-def write_text_model(path: str, keys: torch.Tensor, w: torch.Tensor) -> int:
+def write_text_model(path: str, keys, w) -> int:
+    """``keys``: uint64 (or int64 bit pattern) tensor / array; ``w``: float tensor / array."""
     d = os.path.dirname(path)
     if d:
         os.makedirs(d, exist_ok=True)
-    w = w.float().cpu()
-    keep = (w != 0) & ~torch.isnan(w)
-    k = keys.cpu()[keep].numpy().view(np.uint64)
-    v = w[keep].numpy()
+    k = keys.cpu().numpy() if isinstance(keys, torch.Tensor) else np.asarray(keys)
+    v = w.cpu().numpy() if isinstance(w, torch.Tensor) else np.asarray(w)
+    if v.dtype not in (np.float32, np.float64):
+        v = v.astype(np.float32)
+    keep = (v != 0) & ~np.isnan(v)
+    k = k[keep].view(np.uint64) if k.dtype.itemsize == 8 else k[keep].astype(np.uint64)
+    v = v[keep]
     order = np.argsort(k, kind="stable")
     with open(path, "w") as f:
         for kk, vv in zip(k[order], v[order]):

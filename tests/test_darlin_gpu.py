@@ -1,0 +1,91 @@
+"""Darlin BCD HIP kernels (csrc/hip/bcd.hip) vs the fp64 PyTorch reference, and the
+GPU trainer vs the CPU trainer."""
+import numpy as np
+import pytest
+import torch
+
+from parameter_server_amd.data.synthetic import criteo_slots, sparse_classification
+from parameter_server_amd.models.darlin import DarlinConfig, DarlinTrainer
+from parameter_server_amd.ops import bcd
+
+pytestmark = pytest.mark.gpu
+
+
+def _csc(ncols, rows, seed, valued, head=5000):
+    rng = np.random.default_rng(seed)
+    cols, rws = [], []
+    for c in range(ncols):
+        n = int(rng.integers(0, 12))
+        if c % 97 == 0:
+            n = min(head, rows)  # head columns span many wave64 chunks (atomic path)
+        r = np.sort(rng.choice(rows, size=n, replace=False))
+        cols.append(np.full(r.size, c))
+        rws.append(r)
+    col = np.concatenate(cols).astype(np.int32)
+    row = np.concatenate(rws).astype(np.int32)
+    val = rng.uniform(0.1, 2.0, col.size).astype(np.float32) if valued else None
+    colptr = np.zeros(ncols + 1, np.int64)
+    np.cumsum(np.bincount(col, minlength=ncols), out=colptr[1:])
+    return col, row, val, colptr
+
+
+@pytest.mark.parametrize("valued", [False, True])
+def test_bcd_kernels_match_torch(valued):
+    ncols, rows = 3000, 20000
+    col, row, val, colptr = _csc(ncols, rows, 0, valued)
+    rng = np.random.default_rng(1)
+    y = np.where(rng.random(rows) < 0.5, 1.0, -1.0).astype(np.float32)
+    ym = rng.normal(0, 2, rows)
+    delta = rng.uniform(0.1, 2, ncols)
+    active = (rng.random(ncols) < 0.9).astype(np.uint8)
+    w = np.where(rng.random(ncols) < 0.6, 0.0, rng.normal(0, 1, ncols))
+    T = lambda a: None if a is None else torch.from_numpy(a)  # noqa: E731
+    D = lambda a: None if a is None else torch.from_numpy(a).cuda()  # noqa: E731
+    for c0, c1 in [(0, ncols), (97, 1234), (1500, 1501), (2000, 2000)]:
+        p0, p1 = int(colptr[c0]), int(colptr[c1])
+        Gc, Uc = bcd.grad(T(col), T(row), T(val), p0, p1, c0, c1 - c0, T(ym), T(y), T(delta),
+                          T(active))
+        Gg, Ug = bcd.grad(D(col), D(row), D(val), p0, p1, c0, c1 - c0, D(ym), D(y), D(delta),
+                          D(active))
+        torch.testing.assert_close(Gg.cpu(), Gc, rtol=1e-10, atol=1e-10)
+        torch.testing.assert_close(Ug.cpu(), Uc, rtol=1e-10, atol=1e-10)
+        for thr in (1e20, 0.05):
+            wc, dc, ac = T(w.copy()), T(delta.copy()), T(active.copy())
+            wg, dg, ag = D(w.copy()), D(delta.copy()), D(active.copy())
+            dwc, vc = bcd.update(c0, c1 - c0, Gc, Uc, wc, dc, ac, 1.0, 0.5, 5.0, thr)
+            dwg, vg = bcd.update(c0, c1 - c0, Gg, Ug, wg, dg, ag, 1.0, 0.5, 5.0, thr)
+            torch.testing.assert_close(wg.cpu(), wc, rtol=1e-9, atol=1e-12)
+            torch.testing.assert_close(dg.cpu(), dc, rtol=1e-9, atol=1e-12)
+            assert torch.equal(ag.cpu(), ac)
+            torch.testing.assert_close(dwg.cpu(), dwc, rtol=1e-9, atol=1e-12)
+            assert abs(bcd.violation(vg) - bcd.violation(vc)) <= 1e-9 * max(1, bcd.violation(vc))
+        ymc, ymg = T(ym.copy()), D(ym.copy())
+        bcd.dual(T(col), T(row), T(val), p0, p1, c0, c1 - c0, dwc, T(y), ymc)
+        bcd.dual(D(col), D(row), D(val), p0, p1, c0, c1 - c0, dwg, D(y), ymg)
+        torch.testing.assert_close(ymg.cpu(), ymc, rtol=1e-10, atol=1e-10)
+        oc, og = bcd.objective(ymc), bcd.objective(ymg)
+        torch.testing.assert_close(og.cpu(), oc, rtol=1e-11, atol=0)
+        sc, sg = bcd.server_stats(wc, ac, 10, ncols - 10), bcd.server_stats(wg, ag, 10, ncols - 10)
+        torch.testing.assert_close(sg.cpu(), sc, rtol=1e-11, atol=0)
+
+
+def test_darlin_gpu_trainer_matches_cpu():
+    sd = sparse_classification(6000, groups=(1, 2, 3, 4), keys_per_group=2000,
+                               nnz_per_row=(1, 3, 5, 2), binary=False, seed=7)
+    cfg = DarlinConfig(l1=1.0, max_pass=8, epsilon=1e-12, tail_freq=1, seed=1)
+    pc = DarlinTrainer(sd, cfg, device="cpu").train()
+    tg = DarlinTrainer(sd, cfg, device="cuda")
+    pg = tg.train()
+    np.testing.assert_allclose([p.objective for p in pg], [p.objective for p in pc], rtol=1e-8)
+    assert [p.nnz_w for p in pg] == [p.nnz_w for p in pc]
+    assert pg[-1].objective < pg[0].objective
+
+
+def test_darlin_gpu_criteo_shaped_with_delay():
+    sd = criteo_slots(200_000, seed=3, num_features=10 ** 6, device="cuda")
+    tr = DarlinTrainer(sd, DarlinConfig(l1=4.0, max_pass=3, tail_freq=2, tau=4, seed=0),
+                       device="cuda")
+    assert len(tr.blocks) == 39 and tr.nnz > 0
+    prog = tr.train()
+    assert prog[-1].objective < prog[0].objective
+    assert np.isfinite(prog[-1].objective)

@@ -61,11 +61,15 @@ def test_message_encode_decode_and_slice():
     m.add_value(np.arange(10, dtype=np.float32))  # 2 values per key
     m2 = Message.decode("W0", [f if isinstance(f, bytes) else f.tobytes() for f in m.encode()])
     assert np.array_equal(m2.key, m.key) and np.array_equal(m2.value[0], m.value[0])
+    # reference sliceKeyOrderedMsg: pieces keep the message key_range; a piece is
+    # invalid iff the receiver range misses the message range (message.h:120-159)
+    m.task["key_range"] = [0, 13]
     parts = slice_key_ordered(m, [(0, 6), (6, 10), (10, 15), (15, 16)])
     assert [p.key.tolist() for p in parts] == [[1, 5], [9], [12], []]
     assert parts[0].value[0].tolist() == [0, 1, 2, 3]
     assert parts[2].value[0].tolist() == [6, 7]
     assert [p.valid for p in parts] == [True, True, True, False]
+    assert all(p.task["key_range"] == [0, 13] for p in parts)
 
 
 def test_partition_key_space():
