@@ -115,6 +115,7 @@ class Postoffice:
         self._lifecycle = {}
         self._manage_time = 0
         self.hb = None
+        self._terminated = False
 
     # ----------------------------------------------------------- start
     def start(self, my_node: Node, scheduler: Node, *, num_servers: int = 0, num_workers: int = 0,
@@ -173,13 +174,15 @@ class Postoffice:
     def run(self, timeout: float = 3600.0):
         """Scheduler drives INIT/RUN; other nodes block until TERMINATE."""
         if self.my_node.role == "SCHEDULER":
-            t = self._manage_all("INIT")
-            self.app.init()
-            self._wait_replies(t, timeout)
-            t = self._manage_all("RUN")
-            self.app.run()
-            self._wait_replies(t, timeout)
-            self.stop()
+            try:
+                t = self._manage_all("INIT")
+                self.app.init()
+                self._wait_replies(t, timeout)
+                t = self._manage_all("RUN")
+                self.app.run()
+                self._wait_replies(t, timeout)
+            finally:
+                self.stop()  # TERMINATE every node, also when the job failed
         else:
             while not self._stopped.wait(0.2):
                 if self._error:
@@ -188,7 +191,8 @@ class Postoffice:
             raise self._error
 
     def stop(self):
-        if self.my_node and self.my_node.role == "SCHEDULER" and not self._stopped.is_set():
+        if self.my_node and self.my_node.role == "SCHEDULER" and not self._terminated:
+            self._terminated = True
             for n in list(self.yp.nodes.values()):
                 if n.id != self.my_node.id:
                     m = Message(task=new_task(type=TERMINATE))

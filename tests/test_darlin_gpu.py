@@ -83,9 +83,10 @@ def test_darlin_gpu_trainer_matches_cpu():
 
 def test_darlin_gpu_criteo_shaped_with_delay():
     sd = criteo_slots(200_000, seed=3, num_features=10 ** 6, device="cuda")
-    tr = DarlinTrainer(sd, DarlinConfig(l1=4.0, max_pass=3, tail_freq=2, tau=4, seed=0),
+    # 39 one-block groups: a delay of 1 block is still stable (large tau needs many blocks)
+    tr = DarlinTrainer(sd, DarlinConfig(l1=4.0, max_pass=3, tail_freq=2, tau=1, seed=0),
                        device="cuda")
     assert len(tr.blocks) == 39 and tr.nnz > 0
     prog = tr.train()
     assert prog[-1].objective < prog[0].objective
-    assert np.isfinite(prog[-1].objective)
+    assert prog[-1].objective < sd.rows * np.log(2)  # better than the zero model

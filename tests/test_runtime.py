@@ -73,3 +73,37 @@ model_input {{ format: TEXT file: "{model}_.*" }}
     line = [l for l in out.splitlines() if l.startswith("evaluation:")][0]
     auc = float(line.split()[2])
     assert auc > 0.75, line
+
+
+def test_heartbeat_detects_dead_worker_and_terminates_job():
+    """Fault injection: W1 crashes; the scheduler's heartbeat watchdog fails the job and
+    TERMINATEs the survivors well before the 60 s job timeout (reference: hangs)."""
+    import time
+
+    t0 = time.time()
+    rc, out = _launch(1, 3, ["parameter_server_amd.app.fault_injection", "-timeout", "60",
+                             "-heartbeat_interval", "0.2", "-kill_rank", "1"], timeout=90)
+    assert rc != 0, out
+    assert "W1: injected crash" in out
+    assert "node W1 missed heartbeats" in out
+    assert time.time() - t0 < 30, out
+
+
+def test_heartbeat_dashboard_in_darlin_run(tmp_path):
+    from parameter_server_amd.data.synthetic import sparse_classification, write_text
+
+    sd = sparse_classification(600, groups=(1, 2), keys_per_group=100, nnz_per_row=(1, 3), seed=0)
+    write_text(sd, str(tmp_path / "part-0"), "SPARSE_BINARY")
+    conf = tmp_path / "b.conf"
+    conf.write_text(f"""linear_method {{
+training_data {{ format: TEXT text: SPARSE_BINARY file: "{tmp_path}/part-0" }}
+loss {{ type: LOGIT }} penalty {{ type: L1 lambda: 1 }}
+learning_rate {{ type: CONSTANT alpha: 1 }}
+darlin {{ max_pass_of_data: 40 epsilon: 1e-12 }}
+}}""")
+    rc, out = _launch(1, 1, ["parameter_server_amd.app.main", "-app_file", str(conf),
+                             "-timeout", "90", "-heartbeat_interval", "0.1", "-verbose"])
+    assert rc == 0, out
+    assert "Dashboard" in out and "MyRSS(M)" in out
+    rows = [l.split()[0] for l in out.splitlines() if l.startswith(("S0 ", "W0 "))]
+    assert "S0" in rows and "W0" in rows

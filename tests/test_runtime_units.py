@@ -168,3 +168,29 @@ def test_gzip_file_and_concat(tmp_path):
     b2 = parse_text(b"-1 2:1 3:1\n", "LIBSVM")
     c = ExampleBatch.concat([b1, b2])
     assert c.row_ptr.tolist() == [0, 1, 3]
+
+
+def test_heartbeat_info_and_dashboard():
+    import time
+
+    from parameter_server_amd.system.heartbeat import Dashboard, HeartbeatInfo
+
+    hb = HeartbeatInfo()
+    x = 0
+    for i in range(200000):  # burn a little CPU so the rates are non-trivial
+        x += i * i
+    rep = hb.get()
+    for k in ("process_cpu_usage", "host_cpu_usage", "process_rss_mb", "host_in_use_mb",
+              "host_net_in_mb_s", "host_net_out_mb_s"):
+        assert k in rep and rep[k] >= 0
+    assert rep["process_rss_mb"] > 10
+    d = Dashboard()
+    d.add_report("W10", rep)
+    d.add_report("W2", rep)
+    d.add_report("S0", rep)
+    out = d.render().splitlines()
+    assert "Dashboard" in out[0] and out[1].startswith("Node")
+    assert [l.split()[0] for l in out[2:]] == ["S0", "W2", "W10"]
+    assert d.stale(10.0) == []
+    time.sleep(0.05)
+    assert sorted(d.stale(0.01)) == ["S0", "W10", "W2"]
