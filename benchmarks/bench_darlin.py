@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Darlin BCD (L1 logistic regression) throughput on Criteo-shaped data.
+
+Reference workload: example/linear/ctr/batch_l1lr.conf (lambda 10, tau 8, block
+ratio 4, tail feature freq 4). Metric: examples x passes / second for the whole
+node (every pass touches every nnz twice: block gradient + margin update).
+
+    python benchmarks/bench_darlin.py --rows 4000000 --passes 5
+    torchrun --nproc-per-node N benchmarks/bench_darlin.py ...   (N > 1, RCCL all-reduce)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=2_000_000, help="examples per GPU")
+    ap.add_argument("--passes", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--num-features", type=float, default=1e9)
+    ap.add_argument("--tau", type=int, default=1)
+    ap.add_argument("--l1", type=float, default=10.0)
+    ap.add_argument("--tail-freq", type=int, default=4)
+    ap.add_argument("--cpu", action="store_true")
+    args = ap.parse_args()
+
+    from parameter_server_amd.data.synthetic import criteo_slots
+    from parameter_server_amd.models.darlin import DarlinConfig, DarlinTrainer
+    from parameter_server_amd.parallel.comm import init_from_env
+
+    comm, device = init_from_env("cpu" if args.cpu else "cuda")
+    G, rank = comm.world, comm.rank
+    t0 = time.time()
+    sd = criteo_slots(args.rows, seed=17, row0=rank * args.rows,
+                      num_features=int(args.num_features), device=device)
+    cfg = DarlinConfig(l1=args.l1, tau=args.tau, tail_freq=args.tail_freq,
+                       max_pass=args.passes + args.warmup, epsilon=0.0, seed=0)
+    tr = DarlinTrainer(sd, cfg, comm=comm, device=device)
+    prep = time.time() - t0
+    for it in range(args.warmup):
+        tr.run_pass(it)
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for it in range(args.warmup, args.warmup + args.passes):
+        tr.run_pass(it)
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    dt = time.perf_counter() - t1
+    t = torch.tensor([dt], dtype=torch.float64,
+                     device=device if (G > 1 and device.type == "cuda") else "cpu")
+    comm.all_reduce_(t, op="max")
+    dt = float(t.item())
+    if rank == 0:
+        p = tr.progress[-1]
+        print(json.dumps({
+            "metric": "examples x passes / sec (whole node), Darlin L1-LR BCD, Criteo-shaped",
+            "value": G * args.rows * args.passes / dt, "unit": "examples/sec",
+            "n_gpus": G, "passes": args.passes, "warmup": args.warmup,
+            "ms_per_pass": dt / args.passes * 1e3, "dtype": "fp64 (margins, G/U, w)",
+            "config": {"rows_per_gpu": args.rows, "num_features": int(args.num_features),
+                       "kept_features": tr.num_cols, "nnz_per_gpu": tr.nnz,
+                       "blocks": len(tr.blocks), "tau": args.tau, "l1": args.l1,
+                       "tail_freq": args.tail_freq},
+            "preprocess_sec": prep,
+            "train": {"objective": p.objective, "relative_obj": p.relative_obj,
+                      "nnz_w": p.nnz_w, "active_set": p.nnz_active_set},
+        }), flush=True)
+    if G > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
