@@ -76,6 +76,32 @@ def main():
 
     run = one_step
     graph_used = False
+    if gpu and G > 1:
+        # multi-GPU: double-buffered minibatches; minibatch t+1 is generated and
+        # localised on a side stream while step t waits for its exchange counts
+        side = torch.cuda.Stream(device)
+        bufs = [(keys, labels), (torch.empty_like(keys), torch.empty_like(labels))]
+        state = {"t": 0, "loc": None}
+
+        def produce(t):
+            k, lab = bufs[t % 2]
+            side.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(side):
+                criteo_batch(B, seed=seed, row0=t * B, num_features=N, device=device, keys=k,
+                             labels=lab)
+                return tr.localize(k, buf=t % 2)
+
+        def pipelined_step():
+            t = state["t"]
+            loc = state["loc"] if state["loc"] is not None else produce(t)
+            torch.cuda.current_stream(device).wait_stream(side)
+            nxt = {}
+            k, lab = bufs[t % 2]
+            tr.step(k, lab, width=39, loc=loc, prefetch=lambda: nxt.setdefault("loc", produce(t + 1)))
+            state["loc"] = nxt.get("loc")
+            state["t"] = t + 1
+
+        run = pipelined_step
     for _ in range(max(1, args.warmup)):
         run()
     if gpu and G == 1 and args.graph:

@@ -88,6 +88,7 @@ class SparseLRTrainer:
         self.table = KVTable(cap, self.device, cfg.init)
         self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
         self.localizer = Localizer(self.max_nnz, self.bits, self.device)
+        self._localizers = [self.localizer]  # + a second buffer set for prefetching (G > 1)
         self.filter = (CountMinSketch(int(cfg.countmin_n), cfg.countmin_k, self.device)
                        if cfg.tail_feature_freq > 0 else None)
         dev = self.device
@@ -103,6 +104,7 @@ class SparseLRTrainer:
         # multi-GPU: fuse push(t-1) into the pull exchange of step t (2 all-to-alls/step)
         self.fused = self.G > 1 and self.filter is None and cfg.fixing_float_bytes == 0
         self.pending = None
+        self._prefetch = None
         self.step_count = 0
         self.examples = 0
         self.comm_bytes = 0
@@ -116,18 +118,31 @@ class SparseLRTrainer:
         return max(1024, min(want, cap_max))
 
     # ------------------------------------------------------------------ step
+    def localize(self, keys: torch.Tensor, buf: int = 0):
+        """Localise a minibatch into buffer set ``buf`` (0 or 1). Used to prefetch the
+        next minibatch on a side stream while the current step waits for its
+        exchange (``step(..., loc=..., prefetch=...)``)."""
+        while len(self._localizers) <= buf:
+            self._localizers.append(Localizer(self.max_nnz, self.bits, self.device))
+        return self._localizers[buf](keys)
+
     def step(self, keys: torch.Tensor, labels: torch.Tensor, *, width: int | None = None,
              row_ptr: torch.Tensor | None = None, vals: torch.Tensor | None = None,
-             rows: torch.Tensor | None = None):
+             rows: torch.Tensor | None = None, loc=None, prefetch=None):
         """One minibatch: pull, forward, backward, push. ``keys`` are raw feature ids
-        in CSR order (fixed ``width`` per row, or ``row_ptr``)."""
+        in CSR order (fixed ``width`` per row, or ``row_ptr``). ``loc``: an already
+        localised minibatch (``localize``); ``prefetch``: called once the step's
+        exchange counts are in flight and before the step blocks on them (multi-GPU),
+        so the caller can enqueue the next minibatch's work on another stream."""
         B = labels.numel()
         if width is None and row_ptr is None:
             width = self.cfg.max_nnz_per_example
         if row_ptr is not None and rows is None and self.gpu:
             rows = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
             hipops().csr_rows(row_ptr, rows)
-        loc = self.localizer(keys)
+        if loc is None:
+            loc = self.localizer(keys)
+        self._prefetch = prefetch
         if self.filter is not None:
             w_local, push = self._pull_filtered(loc)
         elif self.G == 1 and self.gpu:
@@ -140,6 +155,9 @@ class SparseLRTrainer:
             w_local, push = self._exchange_fused(loc.uniq, loc.n_uniq)
         else:
             w_local, push = self._pull(loc.uniq, loc.n_uniq)
+        if self._prefetch is not None:  # single-GPU / non-fused paths: no blocking point
+            self._prefetch()
+            self._prefetch = None
         _, coef, _ = linear_forward(loc.local_col, w_local, labels, B=B, width=width or 0,
                                     row_ptr=row_ptr, vals=vals, loss=self.cfg.loss,
                                     coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
@@ -171,7 +189,11 @@ class SparseLRTrainer:
         kw = 1 if self.bits <= 32 else 2
         off = self.part.split_sorted(uniq, n_uniq)
         send_t = (off[1:] - off[:-1]).to(torch.int64)
-        M = self.comm.all_gather_counts(send_t)          # [G src, G dst], host
+        M_dev = self.comm.all_gather_counts(send_t, to_host=False)
+        if self._prefetch is not None:  # overlap the next minibatch with this sync
+            self._prefetch()
+            self._prefetch = None
+        M = M_dev.cpu()                                  # [G src, G dst], host
         send_t = M[self.rank].tolist()
         recv_t = M[:, self.rank].tolist()
         U = int(sum(send_t))

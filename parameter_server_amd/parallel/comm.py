@@ -30,9 +30,11 @@ class Comm:
     def all_to_all_v(self, send: torch.Tensor, send_counts, recv_counts) -> torch.Tensor:
         return send
 
-    def all_gather_counts(self, counts: torch.Tensor) -> torch.Tensor:
-        """[world, world] int64 host matrix: row r = counts sent by rank r."""
-        return counts.reshape(1, -1).cpu()
+    def all_gather_counts(self, counts: torch.Tensor, to_host: bool = True) -> torch.Tensor:
+        """[world, world] int64 matrix (row r = counts sent by rank r); on the host
+        unless ``to_host=False`` (then the caller syncs when it needs the values)."""
+        m = counts.reshape(1, -1)
+        return m.cpu() if to_host else m
 
     def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
         return t
@@ -95,7 +97,7 @@ class DistComm(Comm):
         self._sent += send.element_size() * (sum(sc) - sc[self.rank]) * max(1, send[0:1].numel())
         return out
 
-    def all_gather_counts(self, counts: torch.Tensor) -> torch.Tensor:
+    def all_gather_counts(self, counts: torch.Tensor, to_host: bool = True) -> torch.Tensor:
         c = counts.to(torch.int64).reshape(-1).contiguous()
         if self.backend == "nccl":
             c = c.to(self.device)
@@ -103,7 +105,8 @@ class DistComm(Comm):
             c = c.cpu()
         out = torch.empty(self.world * c.numel(), dtype=torch.int64, device=c.device)
         dist.all_gather_into_tensor(out, c, group=self.group)
-        return out.reshape(self.world, -1).cpu()
+        out = out.reshape(self.world, -1)
+        return out.cpu() if to_host else out
 
     def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
         ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}

@@ -16,7 +16,7 @@ from test_dist_gloo import _free_port, _reference
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_worker(rank, world, port, out_dir, cfg_kw, steps):
+def _gpu_worker(rank, world, port, out_dir, cfg_kw, steps, pipelined=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), PSAMD_DIST_BACKEND="gloo")
     import torch.distributed as dist
@@ -29,10 +29,27 @@ def _gpu_worker(rank, world, port, out_dir, cfg_kw, steps):
     cfg = SparseLRConfig(**cfg_kw)
     tr = SparseLRTrainer(cfg, comm, dev)
     B = cfg.minibatch
-    for s in range(steps):
-        k, l = criteo_batch(B, seed=100 + rank, row0=s * B, num_features=cfg.num_features,
-                            cards=[200] * 26)
-        tr.step(k.to(dev), l.to(dev))
+    batches = [criteo_batch(B, seed=100 + rank, row0=s * B, num_features=cfg.num_features,
+                            cards=[200] * 26) for s in range(steps)]
+    batches = [(k.to(dev), l.to(dev)) for k, l in batches]
+    if not pipelined:
+        for k, l in batches:
+            tr.step(k, l)
+    else:  # bench.py's multi-GPU loop: localise t+1 on a side stream during step t
+        side = torch.cuda.Stream(dev)
+
+        def produce(t):
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                return tr.localize(batches[t][0], buf=t % 2)
+
+        loc = produce(0)
+        for t in range(steps):
+            torch.cuda.current_stream(dev).wait_stream(side)
+            nxt = {}
+            pf = (lambda t=t: nxt.setdefault("loc", produce(t + 1))) if t + 1 < steps else None
+            tr.step(batches[t][0], batches[t][1], loc=loc, prefetch=pf)
+            loc = nxt.get("loc")
     torch.cuda.synchronize()
     p = tr.progress()
     tr.table.check_ok()
@@ -40,12 +57,13 @@ def _gpu_worker(rank, world, port, out_dir, cfg_kw, steps):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ff_bytes", [0, 3])
-def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes):
+@pytest.mark.parametrize("ff_bytes,pipelined", [(0, False), (3, False), (0, True)])
+def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes, pipelined):
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
                   fixing_float_bytes=ff_bytes)
     port = _free_port()
-    mp.spawn(_gpu_worker, args=(2, port, str(tmp_path), cfg_kw, 4), nprocs=2, join=True)
+    mp.spawn(_gpu_worker, args=(2, port, str(tmp_path), cfg_kw, 4, pipelined), nprocs=2,
+             join=True)
     res = [torch.load(tmp_path / f"g{r}.pt", weights_only=False) for r in range(2)]
     merged = {}
     for r in res:
@@ -56,3 +74,23 @@ def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes):
     assert merged.keys() == ref.keys()
     tol = 1e-5 if ff_bytes == 0 else 2e-3
     assert max(abs(merged[k] - ref[k]) for k in ref) < tol
+
+
+def test_bench_two_rank_rehearsal_json(tmp_path):
+    """bench.py's multi-GPU path (pipelined fused exchange) under torchrun, 2 ranks on
+    one GPU over gloo; checks the one-line JSON contract."""
+    import json
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PSAMD_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus",
+           "2", "--steps", "4", "--warmup", "2", "--minibatch", "4096", "--num-features", "1e8"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 4 and out["config"]["global_batch"] == 8192
+    assert out["value"] > 0 and 0.3 < out["train"]["loss"] < 1.0
