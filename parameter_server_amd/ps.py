@@ -49,11 +49,31 @@ class _WorkerApp(App):
         self.ret = self.main(self.argv) or 0
 
 
+def assemble_my_node(flags: Flags, scheduler: Node) -> Node:
+    """Role, id, IP and port from ``-my_rank`` (reference Van::assembleMyNode,
+    src/system/van.cc:235-272): rank 0 is the scheduler, ranks 1..W the workers
+    W0.., then the servers S0..; IP of ``-interface`` (or the first non-loopback
+    interface) and a free port. Used by MPI launches (scripts/mpi_node.sh)."""
+    from .ops.native import core
+
+    r, W, S = flags.my_rank, flags.num_workers, flags.num_servers
+    if r == 0:
+        return scheduler
+    if r <= W:
+        role, nid = "WORKER", f"W{r - 1}"
+    elif r <= W + S:
+        role, nid = "SERVER", f"S{r - W - 1}"
+    else:
+        role, nid = "UNUSED", f"U{r - W - S - 1}"
+    ip = core().interface_ip(flags.interface) or "127.0.0.1"
+    return Node(role, nid, hostname=ip, port=core().free_port())
+
+
 def start_node(flags: Flags, app_factory=None) -> Postoffice:
-    if not flags.my_node or not flags.scheduler:
-        raise SystemExit("need -my_node and -scheduler (see scripts/local.sh)")
-    me = Node.parse(flags.my_node)
+    if not flags.scheduler or not (flags.my_node or flags.my_rank >= 0):
+        raise SystemExit("need -scheduler and -my_node (or -my_rank); see scripts/local.sh")
     sch = Node.parse(flags.scheduler)
+    me = Node.parse(flags.my_node) if flags.my_node else assemble_my_node(flags, sch)
     conf = ""
     if flags.app_file:
         with open(flags.app_file) as f:

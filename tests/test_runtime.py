@@ -107,3 +107,32 @@ darlin {{ max_pass_of_data: 40 epsilon: 1e-12 }}
     assert "Dashboard" in out and "MyRSS(M)" in out
     rows = [l.split()[0] for l in out.splitlines() if l.startswith(("S0 ", "W0 "))]
     assert "S0" in rows and "W0" in rows
+
+
+def test_my_rank_auto_addressing_like_mpi():
+    """Reference Van::assembleMyNode: -my_rank 0 = scheduler, 1..W workers, then servers;
+    launched through scripts/mpi_node.sh with the rank in PMI_RANK."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PS_SCHEDULER=f"role:SCHEDULER,hostname:'127.0.0.1',port:{port},id:'H'",
+               PS_INTERFACE="lo", OMP_NUM_THREADS="1")
+    procs = []
+    for r in range(1 + 2 + 3):  # 2 workers (ranks 1-2), 3 servers (ranks 3-5)
+        e = dict(env, PMI_RANK=str(r))
+        procs.append(subprocess.Popen(
+            ["bash", "scripts/mpi_node.sh", "3", "2", sys.executable, "-u", "-m",
+             "parameter_server_amd.app.hello_world", "-timeout", "60"],
+            cwd=ROOT, env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        out, _ = p.communicate(timeout=90)
+        assert p.returncode == 0, out
+        outs.append(out)
+    out = "".join(outs)
+    assert "W0: key: [4]: 0 2 4 5 ; value: [4]: 0 0.2 0.4 0.5" in out
+    assert "W1: key: [4]: 0 1 3 4 ; value: [4]: 0 0.1 0.3 0.4" in out
+    assert "S2, this is server 2" in out
