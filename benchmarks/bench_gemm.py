@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""TFLOP/s of the hand-written bf16 MFMA GEMM (csrc/hip/gemm.hip) on the wide & deep
+MLP shapes and a square reference shape, vs torch.matmul (hipBLASLt) for context."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from parameter_server_amd.ops import gemm as G  # noqa: E402
+
+
+def t(fn, it=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it * 1e-3
+
+
+rows = []
+for name, (M, N, K, ak, bk) in {
+    "fwd 16384x1024x4992": (16384, 1024, 4992, True, True),
+    "dX 16384x4992x1024": (16384, 4992, 1024, True, False),
+    "dW 1024x4992x16384": (1024, 4992, 16384, False, False),
+    "fwd 16384x512x1024": (16384, 512, 1024, True, True),
+    "square 4096": (4096, 4096, 4096, True, True),
+    "square 8192": (8192, 8192, 8192, True, True),
+}.items():
+    A = (torch.rand((M, K) if ak else (K, M), device="cuda") * 2 - 1).to(torch.bfloat16)
+    B = (torch.rand((N, K) if bk else (K, N), device="cuda") * 2 - 1).to(torch.bfloat16)
+    ours = t(lambda: G.gemm(A, ak, B, bk, M, N, K))
+    a = A if ak else A.t()
+    b = B if bk else B.t()
+    ref = t(lambda: a @ b.t())
+    fl = 2.0 * M * N * K
+    rows.append({"shape": name, "ours_tflops": fl / ours / 1e12, "torch_tflops": fl / ref / 1e12})
+    print(json.dumps(rows[-1]), flush=True)

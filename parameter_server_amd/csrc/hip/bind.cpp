@@ -79,6 +79,9 @@ void bcd_dual(const int32_t*, const int32_t*, const float*, int64_t, int64_t, in
               const double*, const float*, double*, int64_t, hipStream_t);
 void bcd_objective(const double*, int64_t, double*, hipStream_t);
 void bcd_server_stats(const double*, const uint8_t*, int64_t, int64_t, double*, hipStream_t);
+// gemm.hip
+void gemm_bf16(bool, bool, const void*, int, const void*, int, int, int, int, int, const float*,
+               const void*, int, void*, int, float*, int, float, hipStream_t);
 }  // namespace psamd
 
 using at::Tensor;
@@ -601,5 +604,53 @@ PYBIND11_MODULE(_hipops, m) {
     check(out.numel() >= 3, "out needs 3 doubles");
     psamd::bcd_server_stats(ptr<double>(w), ptr<uint8_t>(active), c0, c1, ptr<double>(out),
                             cur_stream());
+  });
+
+  // ------------------------------------------------------------------ bf16 GEMM
+  // C[m,n] = sum_k A(m,k) B(n,k); A(m,k) = A[m*lda+k] if a_kmajor else A[k*lda+m] (B alike)
+  m.def("gemm_bf16", [](Tensor A, bool a_kmajor, int64_t lda, Tensor B, bool b_kmajor,
+                        int64_t ldb, int64_t M, int64_t N, int64_t K, int epi,
+                        optional<Tensor> bias, optional<Tensor> aux, int64_t ldaux,
+                        optional<Tensor> C, int64_t ldc, optional<Tensor> Cf, int64_t ldcf,
+                        double beta) {
+    chk(A, at::kBFloat16, "A");
+    chk(B, at::kBFloat16, "B");
+    check(M > 0 && N > 0 && K > 0 && M < INT32_MAX && N < INT32_MAX && K < INT32_MAX,
+          "bad GEMM shape");
+    auto need = [&](const Tensor& t, bool kmaj, int64_t ld, int64_t rows, const char* nm) {
+      check(ld % 8 == 0, std::string(nm) + ": leading dimension must be a multiple of 8");
+      check(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+            std::string(nm) + ": must be 16-byte aligned");
+      if (kmaj) {
+        check(K % 8 == 0 && ld >= K, std::string(nm) + ": K-major needs K % 8 == 0, ld >= K");
+        check(t.numel() >= (rows - 1) * ld + K, std::string(nm) + ": too small");
+      } else {
+        check(rows % 8 == 0 && ld >= rows, std::string(nm) + ": MN-major needs rows % 8 == 0");
+        check(t.numel() >= (K - 1) * ld + rows, std::string(nm) + ": too small");
+      }
+    };
+    need(A, a_kmajor, lda, M, "A");
+    need(B, b_kmajor, ldb, N, "B");
+    const float* bp = optr<float>(bias, at::kFloat, "bias");
+    if (epi & 1) check(bp && bias->numel() >= N, "EPI_BIAS needs bias[N]");
+    const void* xp = nullptr;
+    if (epi & 4) {
+      check(aux.has_value() && aux->defined(), "EPI_MASK needs aux");
+      chk(*aux, at::kBFloat16, "aux");
+      check(aux->numel() >= (M - 1) * ldaux + N, "aux too small");
+      xp = aux->data_ptr();
+    }
+    void* cp = nullptr;
+    if (C.has_value() && C->defined()) {
+      chk(*C, at::kBFloat16, "C");
+      check(ldc >= N && C->numel() >= (M - 1) * ldc + N, "C too small");
+      cp = C->data_ptr();
+    }
+    float* cfp = optr<float>(Cf, at::kFloat, "Cf");
+    if (cfp) check(ldcf >= N && Cf->numel() >= (M - 1) * ldcf + N, "Cf too small");
+    check(cp || cfp, "GEMM needs an output");
+    psamd::gemm_bf16(a_kmajor, b_kmajor, A.data_ptr(), (int)lda, B.data_ptr(), (int)ldb, (int)M,
+                     (int)N, (int)K, epi, bp, xp, (int)ldaux, cp, (int)ldc, cfp, (int)ldcf,
+                     (float)beta, cur_stream());
   });
 }

@@ -1,0 +1,216 @@
+// bf16 MFMA GEMM for the dense (MLP) blocks of the wide & deep model.
+//
+//   C[m, n] = sum_k A(m, k) * B(n, k)           (fp32 accumulation)
+//   A(m, k) = A[m * lda + k]  (A_KMAJOR)  or  A[k * lda + m]
+//   B(n, k) = B[n * ldb + k]  (B_KMAJOR)  or  B[k * ldb + n]
+//
+// The three products of a Linear layer with weights W[N_out, K_in] (bf16, the
+// torch layout) and activations X[B, K_in] all map onto it without any
+// transposed copy: forward X.W^T (A, B K-major), input gradient dZ.W (A
+// K-major, B MN-major), weight gradient dZ^T.X (both MN-major).
+//
+// CDNA4 design: 256 threads = 4 wave64 in 2x2, a 128x128 block tile, BK = 64;
+// each wave owns 64x64 = 4x4 tiles of v_mfma_f32_16x16x32_bf16 (lane l holds
+// A[row l&15][k 8(l>>4)..+7], B[k 8(l>>4)..+7][col l&15]; C col = l&15,
+// row = 4(l>>4)+j). Operands are staged global -> registers -> LDS as
+// [rows][BK+8] K-contiguous images (144-B row stride: the 16 lanes of a
+// ds_read_b128 group hit 16 distinct 16-B bank slots); an MN-major operand is
+// transposed during the LDS write (4 k-rows x 8 elements per thread ->
+// 8 x ds_write_b64). Double-buffered LDS with the next tile's global loads in
+// flight during the current tile's MFMAs (one barrier per K-step). The block
+// index is remapped so consecutive tiles of one A panel share an XCD's L2.
+//
+// Fused epilogues: + bias[n], ReLU, multiply by the ReLU mask of an auxiliary
+// bf16 tensor (backward through an activation), bf16 and/or fp32 stores.
+#include "common.cuh"
+
+#include <hip/hip_bf16.h>
+
+namespace psamd {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, BK = 64, LDS_K = BK + 8;  // padded row (elements)
+constexpr int THREADS = 256;
+
+enum Epi : int {
+  EPI_NONE = 0,      // C = acc
+  EPI_BIAS = 1,      // + bias[n]
+  EPI_RELU = 2,      // max(., 0)
+  EPI_MASK = 4,      // * (aux[m, n] > 0)   (backward through ReLU)
+};
+
+__device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
+  // bijective remap: the blocks that land on one XCD (bid % 8) get a contiguous range
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + bid / 8;
+}
+
+// Stage one operand tile [rows r0.., k k0..] into registers.
+template <bool KMAJOR>
+struct Stage {
+  uint4 v[4];
+  __device__ __forceinline__ void load(const __bf16* __restrict__ p, int ld, int rows, int K,
+                                       int r0, int k0, int tid) {
+    if (KMAJOR) {
+      // 128 rows x 8 chunks of 8 k -> 4 chunks per thread
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = tid + i * THREADS;
+        const int row = c >> 3, kc = (c & 7) * 8;
+        const int gr = r0 + row, gk = k0 + kc;
+        if (gr < rows && gk < K)
+          v[i] = *reinterpret_cast<const uint4*>(p + (int64_t)gr * ld + gk);
+        else
+          v[i] = make_uint4(0, 0, 0, 0);
+      }
+    } else {
+      // 16 k-quads x 16 row-octets: thread owns k 4kq..4kq+3, rows 8rc..8rc+7
+      const int kq = tid >> 4, rc = tid & 15;
+      const int gr = r0 + rc * 8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int gk = k0 + kq * 4 + i;
+        if (gr < rows && gk < K)
+          v[i] = *reinterpret_cast<const uint4*>(p + (int64_t)gk * ld + gr);
+        else
+          v[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(__bf16* __restrict__ lds, int tid) const {
+    if (KMAJOR) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = tid + i * THREADS;
+        const int row = c >> 3, kc = (c & 7) * 8;
+        *reinterpret_cast<uint4*>(lds + row * LDS_K + kc) = v[i];
+      }
+    } else {
+      const int kq = tid >> 4, rc = tid & 15;
+      const unsigned short* e0 = reinterpret_cast<const unsigned short*>(&v[0]);
+      const unsigned short* e1 = reinterpret_cast<const unsigned short*>(&v[1]);
+      const unsigned short* e2 = reinterpret_cast<const unsigned short*>(&v[2]);
+      const unsigned short* e3 = reinterpret_cast<const unsigned short*>(&v[3]);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        uint2 w;
+        w.x = (uint32_t)e0[r] | ((uint32_t)e1[r] << 16);
+        w.y = (uint32_t)e2[r] | ((uint32_t)e3[r] << 16);
+        *reinterpret_cast<uint2*>(lds + (rc * 8 + r) * LDS_K + kq * 4) = w;
+      }
+    }
+  }
+};
+
+template <bool A_KMAJOR, bool B_KMAJOR>
+__global__ void __launch_bounds__(THREADS)
+gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ B, int ldb,
+                 int M, int N, int K, int epi, const float* __restrict__ bias,
+                 const __bf16* __restrict__ aux, int ldaux, __bf16* __restrict__ C, int ldc,
+                 float* __restrict__ Cf, int ldcf, float beta) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][BM * LDS_K];  // [buf][A|B]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int bid = xcd_swizzle(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM, n0 = (bid % tiles_n) * BN;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stage<A_KMAJOR> sa;
+  Stage<B_KMAJOR> sb;
+  const int nk = (K + BK - 1) / BK;
+  sa.load(A, lda, M, K, m0, 0, tid);
+  sb.load(B, ldb, N, K, n0, 0, tid);
+  sa.store(lds[0][0], tid);
+  sb.store(lds[0][1], tid);
+  __syncthreads();
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) {  // next tile's global loads stay in flight during the MFMAs below
+      sa.load(A, lda, M, K, m0, (kt + 1) * BK, tid);
+      sb.load(B, ldb, N, K, n0, (kt + 1) * BK, tid);
+    }
+    const __bf16* As = lds[cur][0] + (wm * 64 + (lane & 15)) * LDS_K + 8 * (lane >> 4);
+    const __bf16* Bs = lds[cur][1] + (wn * 64 + (lane & 15)) * LDS_K + 8 * (lane >> 4);
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 32) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        a[i] = *reinterpret_cast<const bf16x8*>(As + i * 16 * LDS_K + ks);
+        b[i] = *reinterpret_cast<const bf16x8*>(Bs + i * 16 * LDS_K + ks);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      sa.store(lds[cur ^ 1][0], tid);
+      sb.store(lds[cur ^ 1][1], tid);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  // epilogue: lane holds rows 4(l>>4)+r, col l&15 of every 16x16 tile
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+    if (n >= N) continue;
+    const float bn = (epi & EPI_BIAS) ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= M) continue;
+        float x = acc[i][j][r] + bn;
+        if (epi & EPI_RELU) x = fmaxf(x, 0.f);
+        if (epi & EPI_MASK) x = ((float)aux[(int64_t)m * ldaux + n] > 0.f) ? x : 0.f;
+        if (C) C[(int64_t)m * ldc + n] = (__bf16)x;
+        if (Cf) {
+          float* p = Cf + (int64_t)m * ldcf + n;
+          *p = beta != 0.f ? x + beta * *p : x;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+void gemm_bf16(bool a_kmajor, bool b_kmajor, const void* A, int lda, const void* B, int ldb,
+               int M, int N, int K, int epi, const float* bias, const void* aux, int ldaux,
+               void* C, int ldc, float* Cf, int ldcf, float beta, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  auto a = reinterpret_cast<const __bf16*>(A);
+  auto b = reinterpret_cast<const __bf16*>(B);
+  auto x = reinterpret_cast<const __bf16*>(aux);
+  auto c = reinterpret_cast<__bf16*>(C);
+#define PSAMD_GEMM(AK, BKM)                                                               \
+  gemm_bf16_kernel<AK, BKM><<<tiles, THREADS, 0, st>>>(a, lda, b, ldb, M, N, K, epi, bias, x, \
+                                                       ldaux, c, ldc, Cf, ldcf, beta)
+  if (a_kmajor && b_kmajor) PSAMD_GEMM(true, true);
+  else if (a_kmajor) PSAMD_GEMM(true, false);
+  else if (b_kmajor) PSAMD_GEMM(false, true);
+  else PSAMD_GEMM(false, false);
+#undef PSAMD_GEMM
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace psamd

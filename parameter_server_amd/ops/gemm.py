@@ -1,0 +1,74 @@
+"""bf16 MFMA GEMM (csrc/hip/gemm.hip) and the Linear-layer products built on it.
+
+``gemm(A, a_kmajor, B, b_kmajor, M, N, K)``: C[m, n] = sum_k A(m, k) B(n, k) with
+A(m, k) = A[m, k] (K-major, row-major [M, K]) or A[k, m] (MN-major, row-major
+[K, M]); B likewise. fp32 accumulation; fused epilogues (bias, ReLU, ReLU-mask
+of an auxiliary tensor); bf16 and / or fp32 outputs.
+
+For a layer with weights ``W [N_out, K_in]`` (bf16) and input ``X [B, K_in]``:
+* forward      ``Z = X W^T``      -> A = X (K-major), B = W (K-major)
+* input grad   ``dX = dZ W``      -> A = dZ (K-major), B = W (MN-major)
+* weight grad  ``dW = dZ^T X``    -> A = dZ (MN-major), B = X (MN-major)
+CPU tensors use the same math in fp32 PyTorch (the numerics reference).
+"""
+from __future__ import annotations
+
+import torch
+
+from .native import hipops, is_gpu
+
+EPI_BIAS, EPI_RELU, EPI_MASK = 1, 2, 4
+
+
+def _view(t: torch.Tensor, kmajor: bool, rows: int, K: int) -> torch.Tensor:
+    return t.reshape(rows, K) if kmajor else t.reshape(K, rows).t()
+
+
+def gemm(A, a_kmajor: bool, B, b_kmajor: bool, M: int, N: int, K: int, *, bias=None,
+         relu: bool = False, mask=None, out_bf16: bool = True, out_f32=None, beta: float = 0.0):
+    """Returns the bf16 output (or None when ``out_bf16`` is False and ``out_f32`` given)."""
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0) | \
+        (EPI_MASK if mask is not None else 0)
+    if is_gpu(A):
+        C = torch.empty(M, N, dtype=torch.bfloat16, device=A.device) if out_bf16 else None
+        lda = K if a_kmajor else M
+        ldb = K if b_kmajor else N
+        hipops().gemm_bf16(A, a_kmajor, lda, B, b_kmajor, ldb, M, N, K, epi, bias, mask, N, C, N,
+                           out_f32, N, beta)
+        return C
+    a = _view(A, a_kmajor, M, K).float()
+    b = _view(B, b_kmajor, N, K).float()
+    x = a @ b.t()
+    if bias is not None:
+        x = x + bias.float()
+    if relu:
+        x = x.clamp_min(0)
+    if mask is not None:
+        x = x * (mask.reshape(M, N).float() > 0)
+    if out_f32 is not None:
+        o = out_f32.view(M, N)
+        o.copy_(x + beta * o if beta != 0.0 else x)
+    return x.to(torch.bfloat16) if out_bf16 else None
+
+
+def linear_forward(X, W, bias=None, relu=False):
+    """X [B, K] bf16, W [N, K] bf16 -> act(X W^T + b) [B, N] bf16."""
+    Bn, K = X.shape
+    N = W.shape[0]
+    return gemm(X, True, W, True, Bn, N, K, bias=bias, relu=relu)
+
+
+def linear_input_grad(dZ, W, mask=None):
+    """dZ [B, N], W [N, K] -> dZ W [B, K] (times the ReLU mask of ``mask`` [B, K])."""
+    Bn, N = dZ.shape
+    K = W.shape[1]
+    return gemm(dZ, True, W, False, Bn, K, N, mask=mask)
+
+
+def linear_weight_grad(dZ, X, out=None, beta: float = 0.0):
+    """dZ [B, N], X [B, K] -> dW = dZ^T X [N, K] fp32 (``out`` accumulates with ``beta``)."""
+    Bn, N = dZ.shape
+    K = X.shape[1]
+    out = torch.empty(N, K, dtype=torch.float32, device=dZ.device) if out is None else out
+    gemm(dZ, False, X, False, N, K, Bn, out_bf16=False, out_f32=out, beta=beta)
+    return out

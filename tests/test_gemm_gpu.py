@@ -1,0 +1,58 @@
+"""bf16 MFMA GEMM (csrc/hip/gemm.hip) vs fp32 PyTorch of the same bf16 inputs."""
+import pytest
+import torch
+
+from parameter_server_amd.ops import gemm as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(A, ak, B, bk, M, N, K):
+    a = (A.reshape(M, K) if ak else A.reshape(K, M).t()).float()
+    b = (B.reshape(N, K) if bk else B.reshape(K, N).t()).float()
+    return a @ b.t()
+
+
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False), (False, True)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 72), (1024, 512, 4992),
+                                   (8, 8, 8), (4096, 1024, 256)])
+def test_gemm_layouts_match_fp32(ak, bk, M, N, K):
+    torch.manual_seed(M + N + K)
+    A = torch.randn((M, K) if ak else (K, M), device="cuda").to(torch.bfloat16)
+    B = torch.randn((N, K) if bk else (K, N), device="cuda").to(torch.bfloat16)
+    C = G.gemm(A, ak, B, bk, M, N, K)
+    ref = _ref(A, ak, B, bk, M, N, K)
+    torch.testing.assert_close(C.float(), ref, rtol=1e-2, atol=2e-2 * K ** 0.5)
+    Cf = torch.full((M, N), 3.0, device="cuda")
+    G.gemm(A, ak, B, bk, M, N, K, out_bf16=False, out_f32=Cf, beta=0.5)
+    torch.testing.assert_close(Cf, ref + 1.5, rtol=1e-4, atol=1e-3 * K ** 0.5)
+
+
+def test_gemm_asymmetric_identity():
+    """A = I with an asymmetric B catches a transposed C-write (guide §3)."""
+    M = N = K = 128
+    A = torch.eye(M, device="cuda").to(torch.bfloat16)
+    B = (torch.arange(N * K, device="cuda").reshape(N, K) % 97).to(torch.bfloat16)
+    C = G.gemm(A, True, B, True, M, N, K)
+    assert torch.equal(C.float(), B.float().t())
+
+
+def test_linear_layer_products_and_epilogues():
+    torch.manual_seed(0)
+    Bn, K, N = 384, 4992, 1024
+    X = torch.randn(Bn, K, device="cuda").to(torch.bfloat16)
+    W = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda")
+    H = G.linear_forward(X, W, b, relu=True)
+    ref = torch.relu(X.float() @ W.float().t() + b)
+    torch.testing.assert_close(H.float(), ref, rtol=2e-2, atol=2e-2)
+    dH = torch.randn(Bn, N, device="cuda").to(torch.bfloat16)
+    dZ = G.gemm(dH, True, torch.eye(N, device="cuda").to(torch.bfloat16), True, Bn, N, N, mask=H)
+    torch.testing.assert_close(dZ.float(), dH.float() * (H.float() > 0), rtol=0, atol=0)
+    dX = G.linear_input_grad(dZ, W)
+    torch.testing.assert_close(dX.float(), dZ.float() @ W.float(), rtol=2e-2, atol=2e-2)
+    dW = G.linear_weight_grad(dZ, X)
+    torch.testing.assert_close(dW, dZ.float().t() @ X.float(), rtol=1e-2, atol=5e-2)
+    # CPU path = same math
+    Hc = G.linear_forward(X.cpu(), W.cpu(), b.cpu(), relu=True)
+    torch.testing.assert_close(Hc.float(), H.cpu().float(), rtol=2e-2, atol=2e-2)
