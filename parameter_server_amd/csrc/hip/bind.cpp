@@ -4,6 +4,7 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
+#include <cmath>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -79,9 +80,25 @@ void bcd_dual(const int32_t*, const int32_t*, const float*, int64_t, int64_t, in
               const double*, const float*, double*, int64_t, hipStream_t);
 void bcd_objective(const double*, int64_t, double*, hipStream_t);
 void bcd_server_stats(const double*, const uint8_t*, int64_t, int64_t, double*, hipStream_t);
+// embedding.hip
+void emb_init_rows(const int64_t*, const uint64_t*, int64_t, const int32_t*, int64_t, void*,
+                   uint8_t*, int, uint64_t, float, hipStream_t);
+void emb_gather_rows(const int64_t*, int64_t, int64_t, const void*, int, void*, hipStream_t);
+void emb_expand(const int32_t*, int64_t, const int64_t*, int64_t, const void*, int64_t, int, void*,
+                hipStream_t);
+void emb_grad_reduce(const int32_t*, const int32_t*, const int32_t*, int64_t, int64_t, const void*,
+                     int, float*, hipStream_t);
+void emb_update(const int64_t*, int64_t, const int32_t*, int64_t, const float*, const void*, void*,
+                float*, int, float, float, hipStream_t);
+void wd_head(const void*, int64_t, int, const float*, const float*, const float*, int64_t,
+             const int32_t*, int, const float*, float*, void*, float*, float*, double*, uint32_t*,
+             int, hipStream_t);
+void colsum_bf16(const void*, int64_t, int, float*, hipStream_t);
+void adam_update(float*, const float*, float*, float*, int64_t, float, float, float, float, float,
+                 float, float, void*, hipStream_t);
 // gemm.hip
 void gemm_bf16(bool, bool, const void*, int, const void*, int, int, int, int, int, const float*,
-               const void*, int, void*, int, float*, int, float, hipStream_t);
+               const void*, int, void*, int, float*, int, float, int, hipStream_t);
 }  // namespace psamd
 
 using at::Tensor;
@@ -612,7 +629,7 @@ PYBIND11_MODULE(_hipops, m) {
                         int64_t ldb, int64_t M, int64_t N, int64_t K, int epi,
                         optional<Tensor> bias, optional<Tensor> aux, int64_t ldaux,
                         optional<Tensor> C, int64_t ldc, optional<Tensor> Cf, int64_t ldcf,
-                        double beta) {
+                        double beta, int splitk) {
     chk(A, at::kBFloat16, "A");
     chk(B, at::kBFloat16, "B");
     check(M > 0 && N > 0 && K > 0 && M < INT32_MAX && N < INT32_MAX && K < INT32_MAX,
@@ -649,8 +666,141 @@ PYBIND11_MODULE(_hipops, m) {
     float* cfp = optr<float>(Cf, at::kFloat, "Cf");
     if (cfp) check(ldcf >= N && Cf->numel() >= (M - 1) * ldcf + N, "Cf too small");
     check(cp || cfp, "GEMM needs an output");
+    if (splitk > 1)
+      check(!cp && cfp && epi == 0 && (beta == 0.0 || beta == 1.0),
+            "split-K: fp32 output only, no epilogue, beta 0 or 1");
     psamd::gemm_bf16(a_kmajor, b_kmajor, A.data_ptr(), (int)lda, B.data_ptr(), (int)ldb, (int)M,
                      (int)N, (int)K, epi, bp, xp, (int)ldaux, cp, (int)ldc, cfp, (int)ldcf,
-                     (float)beta, cur_stream());
+                     (float)beta, splitk, cur_stream());
+  });
+
+  // ------------------------------------------------------------- embeddings
+  auto rows_check = [](const Tensor& rows, int64_t cap, int D) {
+    chk(rows, at::kBFloat16, "rows");
+    check(D > 0 && D % 8 == 0 && D <= 128, "embedding dim must be a multiple of 8, <= 128");
+    check(rows.dim() == 2 && rows.size(0) == cap && rows.size(1) == D, "rows must be [cap, D]");
+  };
+  m.def("emb_init_rows", [rows_check](Tensor slot, Tensor keys, optional<Tensor> n_dev,
+                                      Tensor rows, Tensor inited, uint64_t seed, double scale) {
+    chk(slot, at::kLong, "slot");
+    chk(keys, at::kLong, "keys");
+    chk(inited, at::kByte, "inited");
+    const int64_t cap = inited.numel();
+    rows_check(rows, cap, (int)rows.size(1));
+    check(keys.numel() >= slot.numel(), "keys shorter than slot");
+    psamd::emb_init_rows(ptr<int64_t>(slot), ptr<uint64_t>(keys), slot.numel(),
+                         optr<int32_t>(n_dev, at::kInt, "n_dev"), cap, rows.data_ptr(),
+                         ptr<uint8_t>(inited), (int)rows.size(1), seed, (float)scale,
+                         cur_stream());
+  });
+  m.def("emb_gather_rows", [rows_check](Tensor slot, Tensor rows, Tensor out) {
+    chk(slot, at::kLong, "slot");
+    rows_check(rows, rows.size(0), (int)rows.size(1));
+    chk(out, at::kBFloat16, "out");
+    check(out.numel() >= slot.numel() * rows.size(1), "out too small");
+    psamd::emb_gather_rows(ptr<int64_t>(slot), slot.numel(), rows.size(0), rows.data_ptr(),
+                           (int)rows.size(1), out.data_ptr(), cur_stream());
+  });
+  m.def("emb_expand", [](Tensor local_col, int64_t nnz, optional<Tensor> idx, Tensor src,
+                         Tensor X0) {
+    chk(local_col, at::kInt, "local_col");
+    chk(src, at::kBFloat16, "src");
+    chk(X0, at::kBFloat16, "X0");
+    check(src.dim() == 2 && src.size(1) % 8 == 0, "src must be [rows, D], D % 8 == 0");
+    const int D = (int)src.size(1);
+    check(local_col.numel() >= nnz && X0.numel() >= nnz * D, "expand buffers too small");
+    const int64_t* ip = optr<int64_t>(idx, at::kLong, "idx");
+    psamd::emb_expand(ptr<int32_t>(local_col), nnz, ip, ip ? idx->numel() : 0, src.data_ptr(),
+                      src.size(0), D, X0.data_ptr(), cur_stream());
+  });
+  m.def("emb_grad_reduce", [](Tensor pos_s, Tensor seg_start, Tensor n_uniq, int64_t u_cap,
+                              int64_t nnz, Tensor dX0, int D, Tensor dE) {
+    chk(pos_s, at::kInt, "pos_s");
+    chk(seg_start, at::kInt, "seg_start");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(dX0, at::kBFloat16, "dX0");
+    chk(dE, at::kFloat, "dE");
+    check(D > 0 && D % 8 == 0, "D % 8 == 0");
+    check(seg_start.numel() >= u_cap + 1 && pos_s.numel() >= nnz, "segment arrays too small");
+    check(dX0.numel() >= nnz * D && dE.numel() >= u_cap * D, "gradient buffers too small");
+    psamd::emb_grad_reduce(ptr<int32_t>(pos_s), ptr<int32_t>(seg_start), ptr<int32_t>(n_uniq),
+                           u_cap, nnz, dX0.data_ptr(), D, ptr<float>(dE), cur_stream());
+  });
+  m.def("emb_update", [rows_check](Tensor slot, optional<Tensor> n_dev, optional<Tensor> grad,
+                                   optional<Tensor> grad16, Tensor rows, Tensor acc, double lr,
+                                   double eps) {
+    chk(slot, at::kLong, "slot");
+    chk(acc, at::kFloat, "acc");
+    const int64_t cap = acc.numel();
+    const int D = (int)rows.size(1);
+    rows_check(rows, cap, D);
+    const float* gp = optr<float>(grad, at::kFloat, "grad");
+    const void* g16 = nullptr;
+    if (!gp) {
+      check(grad16.has_value() && grad16->defined(), "emb_update needs grad or grad16");
+      chk(*grad16, at::kBFloat16, "grad16");
+      check(grad16->numel() >= slot.numel() * D, "grad16 too small");
+      g16 = grad16->data_ptr();
+    } else {
+      check(grad->numel() >= slot.numel() * D, "grad too small");
+    }
+    psamd::emb_update(ptr<int64_t>(slot), slot.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"),
+                      cap, gp, g16, rows.data_ptr(), ptr<float>(acc), D, (float)lr, (float)eps,
+                      cur_stream());
+  });
+  m.def("wd_head", [](Tensor h, Tensor w, Tensor b, Tensor wide_w, Tensor local_col, int S,
+                      Tensor labels, Tensor coef, Tensor dh, Tensor dw, Tensor db, Tensor metrics,
+                      Tensor hist, int nbins) {
+    chk(h, at::kBFloat16, "h");
+    chk(w, at::kFloat, "w");
+    chk(b, at::kFloat, "b");
+    chk(wide_w, at::kFloat, "wide_w");
+    chk(local_col, at::kInt, "local_col");
+    chk(labels, at::kFloat, "labels");
+    chk(coef, at::kFloat, "coef");
+    chk(dh, at::kBFloat16, "dh");
+    chk(dw, at::kFloat, "dw");
+    chk(db, at::kFloat, "db");
+    chk(metrics, at::kDouble, "metrics");
+    chk(hist, at::kInt, "hist");
+    check(h.dim() == 2, "h must be [B, H]");
+    const int64_t B = h.size(0);
+    const int H = (int)h.size(1);
+    check(H > 0 && H <= 512 && w.numel() == H && dw.numel() == H, "head width H in (0, 512]");
+    check(S > 0 && S <= 64 && local_col.numel() >= B * S, "S in (0, 64], local_col [B*S]");
+    check(labels.numel() >= B && coef.numel() >= B && dh.numel() >= B * H, "head buffers small");
+    check(metrics.numel() >= 3 && hist.numel() >= 2 * nbins && nbins > 0, "metrics / hist");
+    psamd::wd_head(h.data_ptr(), B, H, ptr<float>(w), ptr<float>(b), ptr<float>(wide_w),
+                   wide_w.numel(), ptr<int32_t>(local_col), S, ptr<float>(labels),
+                   ptr<float>(coef), dh.data_ptr(), ptr<float>(dw), ptr<float>(db),
+                   ptr<double>(metrics), reinterpret_cast<uint32_t*>(hist.data_ptr()), nbins,
+                   cur_stream());
+  });
+  m.def("colsum_bf16", [](Tensor x, Tensor out) {
+    chk(x, at::kBFloat16, "x");
+    chk(out, at::kFloat, "out");
+    check(x.dim() == 2 && out.numel() >= x.size(1), "colsum: x [B, N], out [N]");
+    psamd::colsum_bf16(x.data_ptr(), x.size(0), (int)x.size(1), ptr<float>(out), cur_stream());
+  });
+  m.def("adam_update", [](Tensor p, Tensor g, Tensor m_, Tensor v, double lr, double b1,
+                          double b2, double eps, int64_t step, double gscale,
+                          optional<Tensor> p16) {
+    chk(p, at::kFloat, "p");
+    chk(g, at::kFloat, "g");
+    chk(m_, at::kFloat, "m");
+    chk(v, at::kFloat, "v");
+    const int64_t n = p.numel();
+    check(g.numel() == n && m_.numel() == n && v.numel() == n, "adam buffers mismatch");
+    void* p16p = nullptr;
+    if (p16.has_value() && p16->defined()) {
+      chk(*p16, at::kBFloat16, "p16");
+      check(p16->numel() == n, "p16 mismatch");
+      p16p = p16->data_ptr();
+    }
+    check(step >= 1, "adam step >= 1");
+    const double bc1 = 1.0 - std::pow(b1, (double)step), bc2 = 1.0 - std::pow(b2, (double)step);
+    psamd::adam_update(ptr<float>(p), ptr<float>(g), ptr<float>(m_), ptr<float>(v), n, (float)lr,
+                       (float)b1, (float)b2, (float)eps, (float)bc1, (float)bc2, (float)gscale,
+                       p16p, cur_stream());
   });
 }

@@ -1,0 +1,348 @@
+// Embedding-table (dense value block) kernels for the wide & deep model.
+//
+// A shard's table = the scalar KV table (32-B slots: key | wide w, z, n ...;
+// csrc/hip/kv_table.hip) + a row block rows[capacity, D] (bf16) addressed by
+// the SAME slot index, + a per-row AdaGrad accumulator and an init flag.
+// D = 128 bf16 = 256 B = 16 lanes x 16 B: every kernel maps one key / row to a
+// 16-lane group (4 groups per wave64) doing 16-byte vector loads and stores.
+//
+//   emb_init_rows    first touch of a slot -> deterministic N(0, s) row from its key
+//   emb_gather_rows  rows[slot[i]] -> out[i]          (pull replies, G > 1)
+//   emb_expand       X0[p] = src[idx[p]], p = b*S + s (the [B, S*D] MLP input)
+//   emb_grad_reduce  dE[u] = sum of dX0 rows of u's occurrences (CSC order of the
+//                    localiser: no atomics, fp32 accumulation)
+//   emb_update       row-wise AdaGrad: acc += mean(g^2); row -= lr g / sqrt(acc + eps)
+//   wd_head          deep logit (h.w + b) + wide margin, logistic loss, metrics,
+//                    AUC histogram, dL/dlogit, dh = coef w * relu'(h), dw, db
+//   colsum_bf16      bias gradients
+//   adam_update      fp32 master weights + bf16 copy for the GEMMs
+#include "common.cuh"
+
+#include <hip/hip_bf16.h>
+
+namespace psamd {
+
+namespace {
+
+constexpr int kGroup = 16;  // lanes per row
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even, NaN kept
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = kGroup / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------- init / gather
+__global__ void __launch_bounds__(256)
+emb_init_rows_kernel(const int64_t* __restrict__ slot, const uint64_t* __restrict__ keys, int64_t n,
+                     const int32_t* __restrict__ n_dev, int64_t cap, uint16_t* __restrict__ rows,
+                     uint8_t* __restrict__ inited, int D, uint64_t seed, float scale) {
+  const int64_t nn = dev_len(n_dev, n);
+  const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; i < nn;
+       i += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
+    const int64_t s = slot[i];
+    if (!in_range(s, cap) || inited[s]) continue;
+    const uint64_t key = keys[i];
+    for (int d = l; d < D; d += kGroup) {  // Box-Muller on a counter-based stream
+      const uint64_t r = rng64(seed ^ key, (uint64_t)d);
+      const float u1 = ((r >> 40) + 1) * (1.f / 16777217.f);
+      const float u2 = ((r >> 16) & 0xffffff) * (1.f / 16777216.f);
+      const float z = sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+      rows[s * D + d] = f2bf(z * scale);
+    }
+    __threadfence_block();
+    if (l == 0) inited[s] = 1;  // racing duplicates write identical rows
+  }
+}
+
+__global__ void __launch_bounds__(256)
+emb_gather_rows_kernel(const int64_t* __restrict__ slot, int64_t n, int64_t cap,
+                       const uint16_t* __restrict__ rows, int D, uint16_t* __restrict__ out) {
+  const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  const int vec = D / 8;  // 16-B vectors per row
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; i < n;
+       i += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
+    const int64_t s = slot[i];
+    uint4* o = reinterpret_cast<uint4*>(out + i * D);
+    if (!in_range(s, cap)) {
+      for (int v = l; v < vec; v += kGroup) o[v] = make_uint4(0, 0, 0, 0);
+      continue;
+    }
+    const uint4* r = reinterpret_cast<const uint4*>(rows + s * D);
+    for (int v = l; v < vec; v += kGroup) o[v] = r[v];
+  }
+}
+
+// X0[p, :] = src[idx ? idx[local_col[p]] : local_col[p], :]
+__global__ void __launch_bounds__(256)
+emb_expand_kernel(const int32_t* __restrict__ local_col, int64_t nnz,
+                  const int64_t* __restrict__ idx, int64_t idx_cap,
+                  const uint16_t* __restrict__ src, int64_t src_rows, int D,
+                  uint16_t* __restrict__ X0) {
+  const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  const int vec = D / 8;
+  for (int64_t p = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; p < nnz;
+       p += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
+    int64_t r = local_col[p];
+    if (idx) r = in_range(r, idx_cap) ? idx[r] : -1;
+    uint4* o = reinterpret_cast<uint4*>(X0 + p * D);
+    if (!in_range(r, src_rows)) {
+      for (int v = l; v < vec; v += kGroup) o[v] = make_uint4(0, 0, 0, 0);
+      continue;
+    }
+    const uint4* s = reinterpret_cast<const uint4*>(src + r * D);
+    for (int v = l; v < vec; v += kGroup) o[v] = s[v];
+  }
+}
+
+// dE[u, :] = sum_{k in [seg_start[u], seg_start[u+1])} dX0[pos_s[k], :]
+__global__ void __launch_bounds__(256)
+emb_grad_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ seg_start,
+                       const int32_t* __restrict__ n_uniq, int64_t u_cap, int64_t nnz,
+                       const uint16_t* __restrict__ dX0, int D, float* __restrict__ dE) {
+  const int64_t U = dev_len(n_uniq, u_cap);
+  const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  for (int64_t u = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; u < U;
+       u += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
+    const int64_t a = seg_start[u], b = seg_start[u + 1];
+    for (int d0 = l * 8; d0 < D; d0 += kGroup * 8) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int64_t k = a; k < b; ++k) {
+        const int32_t p = pos_s[k];
+        if (!in_range(p, nnz)) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(dX0 + (int64_t)p * D + d0);
+        const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f(h[j]);
+      }
+      float4* o = reinterpret_cast<float4*>(dE + u * D + d0);
+      o[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+  }
+}
+
+// Row-wise AdaGrad (one accumulator per row, DLRM-style) on bf16 rows, fp32 math.
+__global__ void __launch_bounds__(256)
+emb_update_kernel(const int64_t* __restrict__ slot, int64_t n, const int32_t* __restrict__ n_dev,
+                  int64_t cap, const float* __restrict__ grad, const uint16_t* __restrict__ grad16,
+                  uint16_t* __restrict__ rows, float* __restrict__ acc, int D, float lr,
+                  float eps) {
+  const int64_t nn = dev_len(n_dev, n);
+  const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; i < nn;
+       i += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
+    const int64_t s = slot[i];
+    const bool ok = in_range(s, cap);
+    float gv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float sq = 0.f;
+    const int d0 = l * 8;  // D == 128: one 8-element chunk per lane
+    if (ok && d0 < D) {
+      if (grad) {
+        const float4* p = reinterpret_cast<const float4*>(grad + i * D + d0);
+        const float4 x = p[0], y = p[1];
+        gv[0] = x.x; gv[1] = x.y; gv[2] = x.z; gv[3] = x.w;
+        gv[4] = y.x; gv[5] = y.y; gv[6] = y.z; gv[7] = y.w;
+      } else {
+        const uint4 v = *reinterpret_cast<const uint4*>(grad16 + i * D + d0);
+        const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv[j] = bf2f(h[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sq += gv[j] * gv[j];
+    }
+    sq = group_sum(sq);
+    if (!ok) continue;
+    float a = acc[s] + sq / D;
+    if (l == 0) acc[s] = a;
+    const float step = lr / (sqrtf(a) + eps);
+    if (d0 < D) {
+      uint4* rp = reinterpret_cast<uint4*>(rows + s * D + d0);
+      uint4 v = *rp;
+      uint16_t* h = reinterpret_cast<uint16_t*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) h[j] = f2bf(bf2f(h[j]) - step * gv[j]);
+      *rp = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- head
+// One wave per example. h [B, H] bf16 (H <= 512), w [H] fp32.
+__global__ void __launch_bounds__(256)
+wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __restrict__ w,
+               const float* __restrict__ b, const float* __restrict__ wide_w, int64_t wide_cap,
+               const int32_t* __restrict__ local_col, int S, const float* __restrict__ labels,
+               float* __restrict__ coef_out, uint16_t* __restrict__ dh, float* __restrict__ dw,
+               float* __restrict__ db, double* __restrict__ metrics, uint32_t* __restrict__ hist,
+               int nbins) {
+  extern __shared__ uint32_t lhist[];  // [2 * nbins]
+  __shared__ float s_dw[512];
+  __shared__ double red[16];
+  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) lhist[i] = 0;
+  for (int i = threadIdx.x; i < H; i += blockDim.x) s_dw[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  double loss_acc = 0, corr = 0, cnt = 0, dbsum = 0;
+  for (int64_t r = (int64_t)blockIdx.x * nw + wid; r < B; r += (int64_t)gridDim.x * nw) {
+    float m = 0.f;
+    for (int k = lane; k < H; k += 64) m += bf2f(h[r * H + k]) * w[k];
+    if (lane < S) {
+      const int32_t c = local_col[r * S + lane];
+      if (in_range(c, wide_cap)) m += wide_w[c];
+    }
+    m = wave_sum(m) + b[0];
+    const float y = labels[r] > 0.f ? 1.f : -1.f;
+    const float ym = y * m;
+    const float loss = ym > 0 ? log1pf(expf(-ym)) : -ym + log1pf(expf(ym));
+    const float coef = -y / (1.f + expf(ym));
+    for (int k = lane; k < H; k += 64) {
+      const float hv = bf2f(h[r * H + k]);
+      dh[r * H + k] = f2bf(hv > 0.f ? coef * w[k] : 0.f);
+      atomicAdd(&s_dw[k], coef * hv);
+    }
+    if (lane == 0) {
+      coef_out[r] = coef;
+      loss_acc += loss;
+      corr += ((y > 0.f) == (m > 0.f)) ? 1.0 : 0.0;
+      cnt += 1.0;
+      dbsum += coef;
+      const float p = 1.f / (1.f + expf(-m));
+      const float pb = p == p ? fminf(fmaxf(p * nbins, 0.f), (float)(nbins - 1)) : 0.f;
+      atomicAdd(&lhist[(y > 0.f ? nbins : 0) + (int)pb], 1u);
+    }
+  }
+  const double a = block_sum_f64(loss_acc, red);
+  const double c = block_sum_f64(corr, red);
+  const double n = block_sum_f64(cnt, red);
+  const double d = block_sum_f64(dbsum, red);
+  if (threadIdx.x == 0 && n > 0) {
+    atomicAdd(&metrics[0], a);
+    atomicAdd(&metrics[1], c);
+    atomicAdd(&metrics[2], n);
+    atomicAdd(db, (float)d);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < H; i += blockDim.x) atomicAdd(&dw[i], s_dw[i]);
+  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x)
+    if (lhist[i]) atomicAdd(&hist[i], lhist[i]);
+}
+
+// out[n] = sum_b x[b, n] (bf16 in, fp32 out); a 256-thread block owns 64 columns x all rows
+__global__ void __launch_bounds__(256)
+colsum_bf16_kernel(const uint16_t* __restrict__ x, int64_t B, int N, float* __restrict__ out) {
+  __shared__ float part[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < N)
+    for (int64_t r = q; r < B; r += 4) s += bf2f(x[r * N + c]);
+  part[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && c < N) out[c] = part[0][threadIdx.x] + part[1][threadIdx.x] +
+                                part[2][threadIdx.x] + part[3][threadIdx.x];
+}
+
+// Adam with fp32 master weights; writes the bf16 copy used by the GEMMs.
+__global__ void __launch_bounds__(256)
+adam_update_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                   float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
+                   float bc1, float bc2, float gscale, uint16_t* __restrict__ p16) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * gscale;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float pi = p[i] - lr * (mi / bc1) / (sqrtf(vi / bc2) + eps);
+    p[i] = pi;
+    if (p16) p16[i] = f2bf(pi);
+  }
+}
+
+}  // namespace
+
+void emb_init_rows(const int64_t* slot, const uint64_t* keys, int64_t n, const int32_t* n_dev,
+                   int64_t cap, void* rows, uint8_t* inited, int D, uint64_t seed, float scale,
+                   hipStream_t st) {
+  if (n <= 0) return;
+  emb_init_rows_kernel<<<grid_for(n, 16, 4096), 256, 0, st>>>(
+      slot, keys, n, n_dev, cap, reinterpret_cast<uint16_t*>(rows), inited, D, seed, scale);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void emb_gather_rows(const int64_t* slot, int64_t n, int64_t cap, const void* rows, int D,
+                     void* out, hipStream_t st) {
+  if (n <= 0) return;
+  emb_gather_rows_kernel<<<grid_for(n, 16, 8192), 256, 0, st>>>(
+      slot, n, cap, reinterpret_cast<const uint16_t*>(rows), D, reinterpret_cast<uint16_t*>(out));
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void emb_expand(const int32_t* local_col, int64_t nnz, const int64_t* idx, int64_t idx_cap,
+                const void* src, int64_t src_rows, int D, void* X0, hipStream_t st) {
+  if (nnz <= 0) return;
+  emb_expand_kernel<<<grid_for(nnz, 16, 8192), 256, 0, st>>>(
+      local_col, nnz, idx, idx_cap, reinterpret_cast<const uint16_t*>(src), src_rows, D,
+      reinterpret_cast<uint16_t*>(X0));
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void emb_grad_reduce(const int32_t* pos_s, const int32_t* seg_start, const int32_t* n_uniq,
+                     int64_t u_cap, int64_t nnz, const void* dX0, int D, float* dE,
+                     hipStream_t st) {
+  if (u_cap <= 0) return;
+  emb_grad_reduce_kernel<<<grid_for(u_cap, 16, 8192), 256, 0, st>>>(
+      pos_s, seg_start, n_uniq, u_cap, nnz, reinterpret_cast<const uint16_t*>(dX0), D, dE);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void emb_update(const int64_t* slot, int64_t n, const int32_t* n_dev, int64_t cap,
+                const float* grad, const void* grad16, void* rows, float* acc, int D, float lr,
+                float eps, hipStream_t st) {
+  if (n <= 0) return;
+  emb_update_kernel<<<grid_for(n, 16, 8192), 256, 0, st>>>(
+      slot, n, n_dev, cap, grad, reinterpret_cast<const uint16_t*>(grad16),
+      reinterpret_cast<uint16_t*>(rows), acc, D, lr, eps);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void wd_head(const void* h, int64_t B, int H, const float* w, const float* b, const float* wide_w,
+             int64_t wide_cap, const int32_t* local_col, int S, const float* labels,
+             float* coef, void* dh, float* dw, float* db, double* metrics, uint32_t* hist,
+             int nbins, hipStream_t st) {
+  if (B <= 0) return;
+  const int blocks = (int)std::min<int64_t>((B + 3) / 4, 1024);
+  wd_head_kernel<<<blocks, 256, 2 * nbins * sizeof(uint32_t), st>>>(
+      reinterpret_cast<const uint16_t*>(h), B, H, w, b, wide_w, wide_cap, local_col, S, labels,
+      coef, reinterpret_cast<uint16_t*>(dh), dw, db, metrics, hist, nbins);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void colsum_bf16(const void* x, int64_t B, int N, float* out, hipStream_t st) {
+  if (N <= 0) return;
+  colsum_bf16_kernel<<<(N + 63) / 64, 256, 0, st>>>(reinterpret_cast<const uint16_t*>(x), B, N,
+                                                     out);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void adam_update(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
+                 float b2, float eps, float bc1, float bc2, float gscale, void* p16,
+                 hipStream_t st) {
+  if (n <= 0) return;
+  adam_update_kernel<<<grid_for(n, 256, 4096), 256, 0, st>>>(
+      p, g, m, v, n, lr, b1, b2, eps, bc1, bc2, gscale, reinterpret_cast<uint16_t*>(p16));
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace psamd

@@ -70,8 +70,10 @@ struct Stage {
           v[i] = make_uint4(0, 0, 0, 0);
       }
     } else {
-      // 16 k-quads x 16 row-octets: thread owns k 4kq..4kq+3, rows 8rc..8rc+7
-      const int kq = tid >> 4, rc = tid & 15;
+      // 16 k-quads x 16 row-octets: thread owns k 4kq..4kq+3, rows 8rc..8rc+7.
+      // kq varies fastest across lanes so the transposed LDS writes of a 16-lane
+      // group land on one row, 16 consecutive 8-B slots (conflict-free).
+      const int kq = tid & 15, rc = tid >> 4;
       const int gr = r0 + rc * 8;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -92,7 +94,7 @@ struct Stage {
         *reinterpret_cast<uint4*>(lds + row * LDS_K + kc) = v[i];
       }
     } else {
-      const int kq = tid >> 4, rc = tid & 15;
+      const int kq = tid & 15, rc = tid >> 4;
       const unsigned short* e0 = reinterpret_cast<const unsigned short*>(&v[0]);
       const unsigned short* e1 = reinterpret_cast<const unsigned short*>(&v[1]);
       const unsigned short* e2 = reinterpret_cast<const unsigned short*>(&v[2]);
@@ -113,7 +115,7 @@ __global__ void __launch_bounds__(THREADS)
 gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ B, int ldb,
                  int M, int N, int K, int epi, const float* __restrict__ bias,
                  const __bf16* __restrict__ aux, int ldaux, __bf16* __restrict__ C, int ldc,
-                 float* __restrict__ Cf, int ldcf, float beta) {
+                 float* __restrict__ Cf, int ldcf, float beta, int kchunk) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][BM * LDS_K];  // [buf][A|B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -129,9 +131,13 @@ gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict
 
   Stage<A_KMAJOR> sa;
   Stage<B_KMAJOR> sb;
-  const int nk = (K + BK - 1) / BK;
-  sa.load(A, lda, M, K, m0, 0, tid);
-  sb.load(B, ldb, N, K, n0, 0, tid);
+  // split-K: blockIdx.y owns k in [kbeg, kend); partial sums are added atomically
+  const int kbeg = blockIdx.y * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const bool split = gridDim.y > 1;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  sa.load(A, lda, M, kend, m0, kbeg, tid);
+  sb.load(B, ldb, N, kend, n0, kbeg, tid);
   sa.store(lds[0][0], tid);
   sb.store(lds[0][1], tid);
   __syncthreads();
@@ -139,8 +145,8 @@ gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) {  // next tile's global loads stay in flight during the MFMAs below
-      sa.load(A, lda, M, K, m0, (kt + 1) * BK, tid);
-      sb.load(B, ldb, N, K, n0, (kt + 1) * BK, tid);
+      sa.load(A, lda, M, kend, m0, kbeg + (kt + 1) * BK, tid);
+      sb.load(B, ldb, N, kend, n0, kbeg + (kt + 1) * BK, tid);
     }
     const __bf16* As = lds[cur][0] + (wm * 64 + (lane & 15)) * LDS_K + 8 * (lane >> 4);
     const __bf16* Bs = lds[cur][1] + (wn * 64 + (lane & 15)) * LDS_K + 8 * (lane >> 4);
@@ -181,6 +187,10 @@ gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict
         float x = acc[i][j][r] + bn;
         if (epi & EPI_RELU) x = fmaxf(x, 0.f);
         if (epi & EPI_MASK) x = ((float)aux[(int64_t)m * ldaux + n] > 0.f) ? x : 0.f;
+        if (split) {  // fp32 output only (host pre-scales Cf by beta)
+          unsafeAtomicAdd(Cf + (int64_t)m * ldcf + n, x);
+          continue;
+        }
         if (C) C[(int64_t)m * ldc + n] = (__bf16)x;
         if (Cf) {
           float* p = Cf + (int64_t)m * ldcf + n;
@@ -195,16 +205,27 @@ gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict
 
 void gemm_bf16(bool a_kmajor, bool b_kmajor, const void* A, int lda, const void* B, int ldb,
                int M, int N, int K, int epi, const float* bias, const void* aux, int ldaux,
-               void* C, int ldc, float* Cf, int ldcf, float beta, hipStream_t st) {
+               void* C, int ldc, float* Cf, int ldcf, float beta, int splitk, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (splitk < 1) splitk = 1;
+  // k chunks are whole BK tiles; a split GEMM accumulates fp32 partials atomically
+  const int kchunk = ((K + splitk * BK - 1) / (splitk * BK)) * BK;
+  splitk = (K + kchunk - 1) / kchunk;
+  if (splitk > 1) {
+    if (beta == 0.f)
+      PSAMD_HIP_CHECK(hipMemset2DAsync(Cf, (size_t)ldcf * 4, 0, (size_t)N * 4, M, st));
+    else if (beta != 1.f)
+      throw std::runtime_error("split-K GEMM supports beta 0 or 1");
+  }
+  const dim3 grid(tiles, splitk);
   auto a = reinterpret_cast<const __bf16*>(A);
   auto b = reinterpret_cast<const __bf16*>(B);
   auto x = reinterpret_cast<const __bf16*>(aux);
   auto c = reinterpret_cast<__bf16*>(C);
 #define PSAMD_GEMM(AK, BKM)                                                               \
-  gemm_bf16_kernel<AK, BKM><<<tiles, THREADS, 0, st>>>(a, lda, b, ldb, M, N, K, epi, bias, x, \
-                                                       ldaux, c, ldc, Cf, ldcf, beta)
+  gemm_bf16_kernel<AK, BKM><<<grid, THREADS, 0, st>>>(a, lda, b, ldb, M, N, K, epi, bias, x, \
+                                                      ldaux, c, ldc, Cf, ldcf, beta, kchunk)
   if (a_kmajor && b_kmajor) PSAMD_GEMM(true, true);
   else if (a_kmajor) PSAMD_GEMM(true, false);
   else if (b_kmajor) PSAMD_GEMM(false, true);

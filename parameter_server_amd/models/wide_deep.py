@@ -1,0 +1,258 @@
+"""Wide & deep CTR model on a sharded embedding table (BASELINE.json config 5).
+
+Not a reference model: the reference only *declares* dense value blocks
+(KVVector with k values per key, src/parameter/kv_vector.h:13-100; SArray
+segments); BASELINE.json names "embedding table 10^9 x 128 sharded across
+8 x 288 GB HBM, dense-block push/pull + MFMA GEMM" as a target workload.
+
+Per rank (one process per GPU):
+* embedding shard (model parallel): key -> 32-B KV slot (wide weight w + FTRL
+  state, the sparse-LR table) and a bf16 row of D at the same slot index, with
+  row-wise AdaGrad (``ops.embedding.EmbeddingShard``); keys are mixed and
+  range-partitioned like the sparse-LR keys;
+* minibatch: localise the B x S keys (sort / RLE kernels), pull [row | w] for
+  the unique keys (G > 1: ONE all-to-all of packed 65-word records each way),
+  expand to X0 [B, S*D] (bf16), MLP (S*D -> hidden... -> 1, ReLU) on the bf16
+  MFMA GEMM with fused bias/ReLU epilogues, wide margin + deep logit in one head
+  kernel (logistic loss, accuracy, AUC histogram, head gradients);
+* backward: input / weight gradients on the same GEMM (ReLU masks fused, split-K
+  weight gradients), embedding gradients reduced per unique key in CSC order,
+  wide gradients by the sparse-LR segmented reduction; push [bf16 grad row |
+  wide grad] to the owners, which apply AdaGrad rows + FTRL wide weights;
+* dense MLP (data parallel): fp32 master weights in one flat buffer, ONE RCCL
+  all-reduce of the flat gradient per step, fused Adam writing the bf16 copy.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from ..ops import embedding as E
+from ..ops import gemm as GM
+from ..ops.keymix import key_bits_for
+from ..ops.kv_table import UpdateRule, next_pow2
+from ..ops.linear import AUC_BINS, auc_from_hist, linear_backward
+from ..ops.localize import Localizer
+from ..ops.native import hipops
+from ..parallel.comm import Comm, LocalComm
+from ..parallel.partition import KeyPartition
+
+
+@dataclass
+class WideDeepConfig:
+    num_features: int = 10 ** 9          # hashed key space (whole job)
+    embedding_dim: int = 128
+    slots: int = 39                      # keys per example (Criteo: 13 int + 26 categorical)
+    hidden: tuple = (1024, 512, 256)
+    minibatch: int = 16384               # per rank
+    emb_lr: float = 0.05                 # row-wise AdaGrad
+    emb_init_scale: float = 0.01
+    mlp_lr: float = 1e-3                 # Adam
+    wide: UpdateRule = field(default_factory=lambda: UpdateRule("ftrl", "decay", 0.05, 1.0,
+                                                                 0.5, 1.0))
+    table_capacity: int = 0              # slots per rank (0 = auto)
+    table_load: float = 0.5
+    max_table_bytes: int = 160 << 30     # HBM budget of one shard (slots + rows)
+    seed: int = 0
+
+
+class WideDeepTrainer:
+    def __init__(self, cfg: WideDeepConfig, comm: Comm | None = None, device="cpu"):
+        self.cfg = cfg
+        self.comm = comm or LocalComm(device)
+        self.G, self.rank = self.comm.world, self.comm.rank
+        self.device = dev = torch.device(device)
+        self.gpu = dev.type == "cuda"
+        self.bits = key_bits_for(cfg.num_features)
+        self.part = KeyPartition(self.bits, self.G)
+        D, S, B = cfg.embedding_dim, cfg.slots, cfg.minibatch
+        if D % 8 or D > 128:
+            raise ValueError("embedding_dim must be a multiple of 8 and <= 128")
+        per_slot = 32 + 2 * D + 5
+        cap = cfg.table_capacity or next_pow2(int(math.ceil(cfg.num_features / self.G /
+                                                            cfg.table_load)))
+        cap = max(1024, min(cap, 1 << max(10, (cfg.max_table_bytes // per_slot).bit_length() - 1)))
+        self.shard = E.EmbeddingShard(cap, D, dev, init_scale=cfg.emb_init_scale,
+                                      seed=cfg.seed * 7919 + 17)
+        self.max_nnz = B * S
+        self.localizer = Localizer(self.max_nnz, self.bits, dev)
+        # ---- dense MLP: flat fp32 params / grads / Adam state, bf16 copy for the GEMMs
+        dims = [S * D] + list(cfg.hidden)
+        shapes = []
+        for i in range(len(cfg.hidden)):
+            shapes += [(dims[i + 1], dims[i]), (dims[i + 1],)]
+        shapes += [(dims[-1],), (1,)]  # head w, b
+        sizes = [math.prod(s) for s in shapes]
+        P = sum(sizes)
+        self.param = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.m = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(P, dtype=torch.float32, device=dev)
+        self.param16 = torch.zeros(P, dtype=torch.bfloat16, device=dev)
+        gen = torch.Generator().manual_seed(cfg.seed + 1)  # identical on every rank
+        views, gviews, v16, off = [], [], [], 0
+        for s, n in zip(shapes, sizes):
+            views.append(self.param[off:off + n].view(s))
+            gviews.append(self.grad[off:off + n].view(s))
+            v16.append(self.param16[off:off + n].view(s))
+            off += n
+        for i in range(len(cfg.hidden)):
+            views[2 * i].copy_(E.xavier(dims[i + 1], dims[i], gen).to(dev))
+        views[-2].copy_((torch.rand(dims[-1], generator=gen) * 2 - 1).to(dev) / math.sqrt(dims[-1]))
+        self.param16.copy_(self.param.to(torch.bfloat16))
+        nl = len(cfg.hidden)
+        self.W = [views[2 * i] for i in range(nl)]
+        self.b = [views[2 * i + 1] for i in range(nl)]
+        self.W16 = [v16[2 * i] for i in range(nl)]
+        self.dW = [gviews[2 * i] for i in range(nl)]
+        self.db = [gviews[2 * i + 1] for i in range(nl)]
+        self.w_head, self.b_head = views[-2], views[-1]
+        self.dw_head, self.db_head = gviews[-2], gviews[-1]
+        self.dims = dims
+        self.num_params = P
+        # ---- buffers / metrics
+        self.coef = torch.empty(B, dtype=torch.float32, device=dev)
+        self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
+        self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.hist = torch.zeros(2 * AUC_BINS, dtype=torch.int32, device=dev)
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        if self.gpu:
+            self.slot_buf = torch.empty(self.max_nnz, dtype=torch.int64, device=dev)
+            self.w_buf = torch.empty(self.max_nnz, dtype=torch.float32, device=dev)
+            self.dE = torch.empty(self.max_nnz, D, dtype=torch.float32, device=dev)
+        self.step_count = 0
+        self.examples = 0
+        self.t0 = time.time()
+
+    # ------------------------------------------------------------------ step
+    def step(self, keys: torch.Tensor, labels: torch.Tensor):
+        """One minibatch (``keys`` [B*S] raw feature ids, row-major; ``labels`` [B])."""
+        cfg, dev = self.cfg, self.device
+        S, D = cfg.slots, cfg.embedding_dim
+        B = labels.numel()
+        nnz = B * S
+        if keys.numel() != nnz:
+            raise ValueError(f"expected {nnz} keys, got {keys.numel()}")
+        loc = self.localizer(keys)
+        # ---------------- pull rows + wide weights of the unique keys
+        if self.G == 1:
+            if self.gpu:
+                slot, w_wide = self.shard.resolve(loc.uniq, loc.n_uniq, self.slot_buf, self.w_buf)
+            else:
+                slot, w_wide = self.shard.resolve(loc.uniq[:loc.num_unique()])
+            X0 = E.expand(loc.local_col, nnz, self.shard.rows, idx=slot)
+            push = ("local", slot)
+        else:
+            rows_u, w_wide, push = self._pull(loc)
+            X0 = E.expand(loc.local_col, nnz, rows_u)
+        X0 = X0.view(B, S * D)
+        # ---------------- MLP forward
+        acts = [X0]
+        for i in range(len(cfg.hidden)):
+            acts.append(GM.linear_forward(acts[-1], self.W16[i], self.b[i], relu=True))
+        # ---------------- head (wide + deep), loss, metrics, head grads
+        self.grad.zero_()
+        H = acts[-1]
+        dH = torch.empty_like(H)
+        E.head(H, self.w_head, self.b_head, w_wide, loc.local_col, S, labels, self.coef, dH,
+               self.dw_head, self.db_head, self.metrics, self.hist, AUC_BINS)
+        # ---------------- MLP backward (ReLU masks fused into the dX GEMMs)
+        for i in reversed(range(len(cfg.hidden))):
+            GM.linear_weight_grad(dH, acts[i], out=self.dW[i])
+            E.colsum(dH, self.db[i])
+            mask = acts[i] if i > 0 else None
+            dH = GM.linear_input_grad(dH, self.W16[i], mask=mask)
+        dX0 = dH  # [B, S*D]
+        # ---------------- sparse gradients
+        u_cap = nnz
+        if self.gpu:
+            dE = E.grad_reduce(loc, dX0, D, u_cap, out=self.dE)
+        else:
+            dE = E.grad_reduce(loc, dX0, D, loc.num_unique())
+        g_wide, _ = linear_backward(loc, self.coef[:B], B=B, width=S)
+        self._push(loc, push, dE, g_wide)
+        # ---------------- dense update: one all-reduce, fused Adam
+        if self.G > 1:
+            self.comm.all_reduce_(self.grad)
+        self.step_count += 1
+        E.adam(self.param, self.grad, self.m, self.v, lr=cfg.mlp_lr, step=self.step_count,
+               gscale=1.0 / (B * self.G), p16=self.param16)
+        auc_from_hist(self.hist, self.metrics, self.step_dev)
+        self.examples += B
+
+    # ------------------------------------------------------------ exchange (G > 1)
+    def _pull(self, loc):
+        """Owner split -> keys all-to-all -> resolve + gather [row | w] -> records back."""
+        D = self.cfg.embedding_dim
+        U = loc.num_unique()
+        off = self.part.split_sorted(loc.uniq, loc.n_uniq).cpu()
+        send = (off[1:] - off[:-1]).tolist()
+        recv = self.comm.exchange_counts(torch.tensor(send, dtype=torch.int64)).cpu().tolist()
+        rk = self.comm.all_to_all_v(loc.uniq[:U].contiguous(), send, recv)
+        slot, w = self.shard.resolve(rk)
+        rec = self._pack(self.shard.gather_rows(slot), w)
+        back = self.comm.all_to_all_v(rec, recv, send)
+        rows_u, w_u = self._unpack(back, D)
+        return rows_u, w_u, ("dist", slot, send, recv, U)
+
+    @staticmethod
+    def _pack(rows16: torch.Tensor, w32: torch.Tensor) -> torch.Tensor:
+        """[n, D] bf16 + [n] f32 -> [n, D/2 + 1] int32 records (one all-to-all)."""
+        n, D = rows16.shape
+        rec = torch.empty(n, D // 2 + 1, dtype=torch.int32, device=rows16.device)
+        rec[:, :D // 2] = rows16.contiguous().view(torch.int32).view(n, D // 2)
+        rec[:, D // 2] = w32.contiguous().view(torch.int32)
+        return rec
+
+    @staticmethod
+    def _unpack(rec: torch.Tensor, D: int):
+        n = rec.shape[0]
+        rows16 = rec[:, :D // 2].contiguous().view(torch.bfloat16).view(n, D)
+        w32 = rec[:, D // 2].contiguous().view(torch.float32)
+        return rows16, w32
+
+    def _push(self, loc, push, dE, g_wide):
+        cfg = self.cfg
+        if push[0] == "local":
+            slot = push[1]
+            n_dev = loc.n_uniq if self.gpu else None
+            if self.gpu:
+                self.shard.update_rows(slot, grad=dE, lr=cfg.emb_lr, n_dev=n_dev)
+                hipops().kv_update(self.shard.table.slots, slot, g_wide, n_dev,
+                                   *cfg.wide.args(), self.stats)
+            else:
+                U = loc.num_unique()
+                self.shard.update_rows(slot[:U], grad=dE[:U], lr=cfg.emb_lr)
+                self.shard.update_wide(slot[:U], g_wide[:U], cfg.wide, self.stats)
+            return
+        _, slot, send, recv, U = push
+        D = cfg.embedding_dim
+        rec = self._pack(dE[:U].to(torch.bfloat16), g_wide[:U])
+        got = self.comm.all_to_all_v(rec, send, recv)
+        g16, gw = self._unpack(got, D)
+        a = 0
+        for s in range(self.G):  # one update per source (slots unique within a source)
+            n = recv[s]
+            if n:
+                self.shard.update_rows(slot[a:a + n], grad16=g16[a:a + n], lr=cfg.emb_lr)
+                self.shard.update_wide(slot[a:a + n], gw[a:a + n].contiguous(), cfg.wide,
+                                       self.stats)
+            a += n
+
+    # ------------------------------------------------------------ progress
+    def progress(self, reset: bool = True) -> dict:
+        m = self.metrics.clone()
+        if self.G > 1:
+            m = self.comm.all_reduce_(m.to(self.comm.device) if self.comm.backend == "nccl"
+                                      else m.cpu())
+        m = m.cpu()
+        n = max(float(m[2]), 1.0)
+        out = {"examples": float(m[2]), "loss": float(m[0]) / n,
+               "accuracy": max(float(m[1]) / n, 1 - float(m[1]) / n) if m[2] > 0 else 0.0,
+               "auc": float(m[3]) / max(float(m[4]), 1.0)}
+        if reset:
+            self.metrics.zero_()
+        return out

@@ -24,9 +24,19 @@ def _view(t: torch.Tensor, kmajor: bool, rows: int, K: int) -> torch.Tensor:
     return t.reshape(rows, K) if kmajor else t.reshape(K, rows).t()
 
 
+def auto_splitk(M: int, N: int, K: int, target_blocks: int = 1024) -> int:
+    """K splits so that a small-output / long-K product (the weight gradient) still
+    puts >= ~4 blocks on each of the 256 CUs; each split keeps >= 8 K-tiles."""
+    tiles = -(-M // 128) * -(-N // 128)
+    return max(1, min(-(-target_blocks // tiles), K // 512))
+
+
 def gemm(A, a_kmajor: bool, B, b_kmajor: bool, M: int, N: int, K: int, *, bias=None,
-         relu: bool = False, mask=None, out_bf16: bool = True, out_f32=None, beta: float = 0.0):
-    """Returns the bf16 output (or None when ``out_bf16`` is False and ``out_f32`` given)."""
+         relu: bool = False, mask=None, out_bf16: bool = True, out_f32=None, beta: float = 0.0,
+         splitk: int = 1):
+    """Returns the bf16 output (or None when ``out_bf16`` is False and ``out_f32`` given).
+    ``splitk > 1`` (fp32 output only, beta 0 or 1) splits K over blocks and adds the
+    partial products atomically."""
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0) | \
         (EPI_MASK if mask is not None else 0)
     if is_gpu(A):
@@ -34,7 +44,7 @@ def gemm(A, a_kmajor: bool, B, b_kmajor: bool, M: int, N: int, K: int, *, bias=N
         lda = K if a_kmajor else M
         ldb = K if b_kmajor else N
         hipops().gemm_bf16(A, a_kmajor, lda, B, b_kmajor, ldb, M, N, K, epi, bias, mask, N, C, N,
-                           out_f32, N, beta)
+                           out_f32, N, beta, splitk)
         return C
     a = _view(A, a_kmajor, M, K).float()
     b = _view(B, b_kmajor, N, K).float()
@@ -70,5 +80,6 @@ def linear_weight_grad(dZ, X, out=None, beta: float = 0.0):
     Bn, N = dZ.shape
     K = X.shape[1]
     out = torch.empty(N, K, dtype=torch.float32, device=dZ.device) if out is None else out
-    gemm(dZ, False, X, False, N, K, Bn, out_bf16=False, out_f32=out, beta=beta)
+    sk = auto_splitk(N, K, Bn) if beta in (0.0, 1.0) else 1
+    gemm(dZ, False, X, False, N, K, Bn, out_bf16=False, out_f32=out, beta=beta, splitk=sk)
     return out

@@ -28,6 +28,18 @@ def test_gemm_layouts_match_fp32(ak, bk, M, N, K):
     torch.testing.assert_close(Cf, ref + 1.5, rtol=1e-4, atol=1e-3 * K ** 0.5)
 
 
+@pytest.mark.parametrize("beta", [0.0, 1.0])
+def test_gemm_split_k(beta):
+    torch.manual_seed(1)
+    M, N, K = 256, 384, 8192
+    A = torch.randn(K, M, device="cuda").to(torch.bfloat16)
+    B = torch.randn(K, N, device="cuda").to(torch.bfloat16)
+    Cf = torch.full((M, N), 2.0, device="cuda")
+    G.gemm(A, False, B, False, M, N, K, out_bf16=False, out_f32=Cf, beta=beta, splitk=7)
+    ref = _ref(A, False, B, False, M, N, K) + 2.0 * beta
+    torch.testing.assert_close(Cf, ref, rtol=1e-4, atol=1e-2)
+
+
 def test_gemm_asymmetric_identity():
     """A = I with an asymmetric B catches a transposed C-write (guide §3)."""
     M = N = K = 128

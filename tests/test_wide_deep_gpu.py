@@ -1,0 +1,119 @@
+"""Embedding / wide & deep HIP kernels (csrc/hip/embedding.hip) vs the PyTorch
+reference, and the GPU trainer vs the CPU trainer."""
+import numpy as np
+import pytest
+import torch
+
+from parameter_server_amd.models.wide_deep import WideDeepConfig, WideDeepTrainer
+from parameter_server_amd.ops import embedding as E
+from parameter_server_amd.ops.localize import Localizer, localize_torch
+from parameter_server_amd.ops.synthetic import criteo_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_shard_init_gather_update_match_cpu():
+    D, cap = 128, 1 << 12
+    keys = torch.randint(0, 1 << 40, (3000,), dtype=torch.int64).unique()
+    sc, sg = E.EmbeddingShard(cap, D, "cpu", seed=3), E.EmbeddingShard(cap, D, "cuda", seed=3)
+    slc, _ = sc.resolve(keys)
+    slg, _ = sg.resolve(keys.cuda())
+    assert torch.equal(slc, slg.cpu())  # same probing -> same slots
+    rc, rg = sc.gather_rows(slc), sg.gather_rows(slg)
+    # identical counter-based init stream (fp32 transcendental ulps may move a bf16 rounding)
+    torch.testing.assert_close(rg.cpu().float(), rc.float(), rtol=1e-2, atol=1e-4)
+    assert rc.float().std().item() == pytest.approx(0.01, rel=0.1)
+    sg.rows.copy_(sc.rows.cuda())
+    g = torch.randn(keys.numel(), D)
+    sc.update_rows(slc, grad=g, lr=0.1)
+    sg.update_rows(slg, grad=g.cuda(), lr=0.1)
+    torch.testing.assert_close(sg.rows.cpu().float(), sc.rows.float(), rtol=1e-2, atol=1e-3)
+    torch.testing.assert_close(sg.acc.cpu(), sc.acc, rtol=1e-5, atol=1e-7)
+    sg.update_rows(slg, grad16=g.cuda().to(torch.bfloat16), lr=0.1)  # bf16 push path runs
+
+
+def test_expand_and_grad_reduce():
+    B, S, D = 777, 39, 128
+    keys, _ = criteo_batch(B, seed=1, row0=0, num_features=1 << 20, cards=[50] * 26)
+    kg = keys.cuda()
+    loc = Localizer(B * S, 20, "cuda")(kg)
+    U = loc.num_unique()
+    src = torch.randn(U, D, device="cuda").to(torch.bfloat16)
+    X0 = E.expand(loc.local_col, B * S, src)
+    assert torch.equal(X0, src[loc.local_col.long()])
+    dX0 = torch.randn(B * S, D, device="cuda").to(torch.bfloat16)
+    dE = E.grad_reduce(loc, dX0, D, B * S)
+    ref = torch.zeros(U, D, device="cuda").index_add_(0, loc.local_col.long(), dX0.float())
+    torch.testing.assert_close(dE[:U], ref, rtol=1e-5, atol=1e-4)
+    lc = localize_torch(keys, 20)
+    torch.testing.assert_close(E.grad_reduce(lc, dX0.cpu(), D, U).sum(), ref.sum().cpu(),
+                               rtol=1e-4, atol=1e-2)
+
+
+def test_head_colsum_adam_match_cpu():
+    B, H, S = 1000, 256, 39
+    torch.manual_seed(0)
+    h = torch.relu(torch.randn(B, H)).to(torch.bfloat16)
+    w, b = torch.randn(H) * 0.1, torch.tensor([0.2])
+    U = 500
+    wide = torch.randn(U) * 0.1
+    lc = torch.randint(0, U, (B * S,), dtype=torch.int32)
+    y = torch.where(torch.rand(B) < 0.4, 1.0, -1.0)
+    outs = {}
+    for dev in ("cpu", "cuda"):
+        coef = torch.zeros(B, device=dev)
+        dh = torch.empty(B, H, dtype=torch.bfloat16, device=dev)
+        dw, db = torch.zeros(H, device=dev), torch.zeros(1, device=dev)
+        met = torch.zeros(8, dtype=torch.float64, device=dev)
+        hist = torch.zeros(2 * 2048, dtype=torch.int32, device=dev)
+        E.head(h.to(dev), w.to(dev), b.to(dev), wide.to(dev), lc.to(dev), S, y.to(dev), coef, dh,
+               dw, db, met, hist, 2048)
+        outs[dev] = [t.cpu() for t in (coef, dh, dw, db, met, hist)]
+    c, g = outs["cpu"], outs["cuda"]
+    torch.testing.assert_close(g[0], c[0], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(g[1].float(), c[1].float(), rtol=1e-2, atol=1e-3)
+    torch.testing.assert_close(g[2], c[2], rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(g[3], c[3], rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(g[4][:3], c[4][:3], rtol=1e-5, atol=1e-6)
+    assert abs(int((g[5] - c[5]).abs().sum())) <= 4  # bin edges may differ by an ulp
+    x = torch.randn(300, 200).to(torch.bfloat16)
+    torch.testing.assert_close(E.colsum(x.cuda(), torch.empty(200, device="cuda")).cpu(),
+                               x.float().sum(0), rtol=1e-4, atol=1e-3)
+    p, gr = torch.randn(1000), torch.randn(1000)
+    st = [torch.zeros(1000) for _ in range(2)]
+    pg, stg = p.cuda(), [t.cuda() for t in st]
+    p16 = torch.empty(1000, dtype=torch.bfloat16, device="cuda")
+    for step in (1, 2, 3):
+        E.adam(p, gr, st[0], st[1], lr=1e-2, step=step, gscale=0.5)
+        E.adam(pg, gr.cuda(), stg[0], stg[1], lr=1e-2, step=step, gscale=0.5, p16=p16)
+    torch.testing.assert_close(pg.cpu(), p, rtol=1e-5, atol=1e-6)
+    assert torch.equal(p16.cpu(), p.to(torch.bfloat16))
+
+
+def test_wide_deep_gpu_matches_cpu_trainer():
+    cfg = dict(num_features=1 << 20, embedding_dim=32, hidden=(128, 64), minibatch=512,
+               table_capacity=1 << 15, emb_lr=0.05, mlp_lr=3e-3)
+    tc = WideDeepTrainer(WideDeepConfig(**cfg), device="cpu")
+    tg = WideDeepTrainer(WideDeepConfig(**cfg), device="cuda")
+    lc, lg = [], []
+    for s in range(8):
+        k, l = criteo_batch(512, seed=9, row0=s * 512, num_features=1 << 20, cards=[200] * 26)
+        tc.step(k, l)
+        tg.step(k.cuda(), l.cuda())
+        lc.append(tc.progress()["loss"])
+        lg.append(tg.progress()["loss"])
+    np.testing.assert_allclose(lg, lc, rtol=2e-2)
+    assert lg[-1] < lg[0]
+
+
+def test_wide_deep_gpu_full_width_learns():
+    cfg = WideDeepConfig(num_features=10 ** 8, minibatch=4096, table_capacity=1 << 22)
+    tr = WideDeepTrainer(cfg, device="cuda")
+    for s in range(30):
+        k, l = criteo_batch(4096, seed=2, row0=s * 4096, num_features=cfg.num_features,
+                            device="cuda")
+        tr.step(k, l)
+        if s == 4:
+            first = tr.progress()
+    last = tr.progress()
+    assert last["loss"] < first["loss"] and np.isfinite(last["loss"])
