@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Localisation + backward of one 65,536 x 39 Criteo-shaped minibatch: radix-sort +
+RLE (sort32.hip) vs the sort-free hash dedup (hashloc.hip), per-call microseconds."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from parameter_server_amd.ops.linear import linear_backward  # noqa: E402
+from parameter_server_amd.ops.localize import Localizer  # noqa: E402
+from parameter_server_amd.ops.synthetic import criteo_batch  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+keys, _ = criteo_batch(B, seed=3, row0=0, num_features=10 ** 9, device="cuda")
+coef = torch.randn(B, device="cuda")
+
+
+def t(fn, it=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it * 1e3
+
+
+for mode in ("sort", "hash"):
+    L = Localizer(B * 39, 30, "cuda", mode=mode)
+    loc = L(keys)
+    us_loc = t(lambda: L(keys))
+    us_bwd = t(lambda: linear_backward(loc, coef, B=B, width=39))
+    print(json.dumps({"mode": mode, "B": B, "unique": loc.num_unique(), "localize_us": us_loc,
+                      "backward_us": us_bwd}), flush=True)

@@ -96,6 +96,13 @@ void wd_head(const void*, int64_t, int, const float*, const float*, const float*
 void colsum_bf16(const void*, int64_t, int, float*, hipStream_t);
 void adam_update(float*, const float*, float*, float*, int64_t, float, float, float, float, float,
                  float, float, void*, hipStream_t);
+// hashloc.hip
+size_t hashloc_temp_bytes(int64_t);
+void localize_hash(const uint64_t*, int64_t, KeyMix, unsigned long long*, int32_t*, int64_t,
+                   int64_t*, void*, size_t, uint64_t*, int32_t*, int32_t*, float*, int32_t*,
+                   hipStream_t);
+void hash_backward(const int32_t*, int64_t, int, const int32_t*, const float*, const float*,
+                   int64_t, float*, const int32_t*, int64_t, hipStream_t);
 // gemm.hip
 void gemm_bf16(bool, bool, const void*, int, const void*, int, int, int, int, int, const float*,
                const void*, int, void*, int, float*, int, float, int, hipStream_t);
@@ -672,6 +679,52 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::gemm_bf16(a_kmajor, b_kmajor, A.data_ptr(), (int)lda, B.data_ptr(), (int)ldb, (int)M,
                      (int)N, (int)K, epi, bp, xp, (int)ldaux, cp, (int)ldc, cfp, (int)ldcf,
                      (float)beta, splitk, cur_stream());
+  });
+
+  // ----------------------------------------------------- sort-free localisation
+  m.def("hashloc_temp_bytes", [](int64_t n) { return (int64_t)psamd::hashloc_temp_bytes(n); });
+  m.def("localize_hash", [](Tensor raw, int bits, Tensor slots, Tensor ids, Tensor epoch,
+                            Tensor temp, Tensor uniq, Tensor local_col, Tensor n_uniq,
+                            optional<Tensor> zero_a, Tensor err) {
+    chk(raw, at::kLong, "raw");
+    chk(slots, at::kLong, "slots");
+    chk(ids, at::kInt, "ids");
+    chk(epoch, at::kLong, "epoch");
+    chk(temp, at::kByte, "temp");
+    chk(uniq, at::kLong, "uniq");
+    chk(local_col, at::kInt, "local_col");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(err, at::kInt, "err");
+    const int64_t n = raw.numel();
+    const int64_t cap = slots.numel();
+    check(bits <= 32, "localize_hash: key bits <= 32");
+    check(ids.numel() == cap && cap >= 2 * n && (cap & (cap - 1)) == 0,
+          "hash table: power-of-two capacity >= 2n, ids[cap]");
+    check(uniq.numel() >= n && local_col.numel() >= n, "outputs too small");
+    check((size_t)temp.numel() >= psamd::hashloc_temp_bytes(n), "temp too small");
+    float* za = optr<float>(zero_a, at::kFloat, "zero_a");
+    if (za) check(zero_a->numel() >= n, "zero_a too small");
+    psamd::localize_hash(ptr<uint64_t>(raw), n, make_keymix(bits),
+                         ptr<unsigned long long>(slots), ptr<int32_t>(ids), cap,
+                         ptr<int64_t>(epoch), temp.data_ptr(), (size_t)temp.numel(),
+                         ptr<uint64_t>(uniq), ptr<int32_t>(local_col), ptr<int32_t>(n_uniq), za,
+                         ptr<int32_t>(err), cur_stream());
+  });
+  m.def("hash_backward", [](Tensor local_col, int64_t n, int width, optional<Tensor> rows,
+                            optional<Tensor> vals, Tensor coef, Tensor grad,
+                            optional<Tensor> n_uniq) {
+    chk(local_col, at::kInt, "local_col");
+    chk(coef, at::kFloat, "coef");
+    chk(grad, at::kFloat, "grad");
+    check(local_col.numel() >= n, "local_col too small");
+    const int32_t* rp = optr<int32_t>(rows, at::kInt, "rows");
+    if (rp) check(rows->numel() >= n, "rows too small");
+    else check(width > 0 && n % width == 0, "fixed width must divide n");
+    const float* vp = optr<float>(vals, at::kFloat, "vals");
+    if (vp) check(vals->numel() >= n, "vals too small");
+    psamd::hash_backward(ptr<int32_t>(local_col), n, width, rp, vp, ptr<float>(coef),
+                         coef.numel(), ptr<float>(grad), optr<int32_t>(n_uniq, at::kInt, "n_uniq"),
+                         grad.numel(), cur_stream());
   });
 
   // ------------------------------------------------------------- embeddings

@@ -64,6 +64,7 @@ class SparseLRConfig:
     countmin_k: int = 2
     consistency: str = "bsp"             # bsp | ssp:<tau> | asp
     push_mode: str = "sequential"        # sequential | aggregate
+    localize: str = "auto"               # auto | sort | hash (sort-free, 1 GPU, <= 32-bit keys)
     fixing_float_bytes: int = 0          # 0 = off, else 1..7 bytes per pushed gradient
     seed: int = 0
 
@@ -87,7 +88,11 @@ class SparseLRTrainer:
         cap = cfg.table_capacity or self.auto_capacity(cfg, self.G, self.bits)
         self.table = KVTable(cap, self.device, cfg.init)
         self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
-        self.localizer = Localizer(self.max_nnz, self.bits, self.device)
+        mode = cfg.localize
+        if mode == "auto":  # hash ids need no owner order: single-GPU, unfiltered steps
+            mode = "hash" if (self.G == 1 and cfg.tail_feature_freq <= 0) else "sort"
+        self.localize_mode = mode
+        self.localizer = Localizer(self.max_nnz, self.bits, self.device, mode=mode)
         self._localizers = [self.localizer]  # + a second buffer set for prefetching (G > 1)
         self.filter = (CountMinSketch(int(cfg.countmin_n), cfg.countmin_k, self.device)
                        if cfg.tail_feature_freq > 0 else None)
@@ -123,7 +128,8 @@ class SparseLRTrainer:
         next minibatch on a side stream while the current step waits for its
         exchange (``step(..., loc=..., prefetch=...)``)."""
         while len(self._localizers) <= buf:
-            self._localizers.append(Localizer(self.max_nnz, self.bits, self.device))
+            self._localizers.append(Localizer(self.max_nnz, self.bits, self.device,
+                                              mode=self.localize_mode))
         return self._localizers[buf](keys)
 
     def step(self, keys: torch.Tensor, labels: torch.Tensor, *, width: int | None = None,

@@ -89,6 +89,10 @@ def linear_forward(local_col, w_local, labels, *, B: int, width: int = 0, row_pt
 
 def linear_backward(loc, coef, *, B: int, width: int = 0, rows=None, vals=None, coef2=None):
     """grad[u] (and hess[u] if coef2 given) into loc.grad / loc.hess."""
+    if getattr(loc, "hashed", False):  # sort-free localisation: wave-aggregated atomics
+        hipops().hash_backward(loc.local_col, loc.nnz, width, rows, vals, coef, loc.grad,
+                               loc.n_uniq)
+        return loc.grad, None
     if is_gpu(coef):
         hipops().linear_bwd(loc.pos_s, loc.segid, loc.nnz, rows, width, vals, coef,
                             coef2 if loc.hess is not None else None, loc.grad,

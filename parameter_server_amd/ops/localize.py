@@ -36,15 +36,22 @@ class Localized:
     grad: torch.Tensor
     hess: torch.Tensor | None
     nnz: int
+    hashed: bool = False  # sort-free ids (no CSC order: pos_s / segid / seg_start are None)
 
     def num_unique(self) -> int:  # host sync
         return int(self.n_uniq.item())
 
 
 class Localizer:
-    """Reusable localisation workspace for up to ``max_nnz`` keys per call."""
+    """Reusable localisation workspace for up to ``max_nnz`` keys per call.
 
-    def __init__(self, max_nnz: int, bits: int, device="cpu", with_hess: bool = False):
+    ``mode="sort"``: radix sort + RLE (unique keys in sorted mixed order, CSC order
+    for the segmented backward). ``mode="hash"`` (GPU, key bits <= 32): sort-free
+    dedup in a per-step scratch hash table (csrc/hip/hashloc.hip); unique keys in
+    claim order, backward by wave-aggregated atomics."""
+
+    def __init__(self, max_nnz: int, bits: int, device="cpu", with_hess: bool = False,
+                 mode: str = "sort"):
         self.max_nnz = int(max_nnz)
         self.bits = int(bits)
         self.device = torch.device(device)
@@ -52,6 +59,21 @@ class Localizer:
         n = self.max_nnz
         dev = self.device
         self.gpu = dev.type == "cuda"
+        self.mode = mode if (self.gpu and self.bits <= 32 and not with_hess) else "sort"
+        if self.gpu and self.mode == "hash":
+            H = hipops()
+            cap = 1 << max(10, (2 * n - 1).bit_length())
+            self.hslots = torch.zeros(cap, dtype=torch.int64, device=dev)  # epoch 0 = empty
+            self.hids = torch.empty(cap, dtype=torch.int32, device=dev)
+            self.epoch = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.htemp = torch.empty(H.hashloc_temp_bytes(n), dtype=torch.uint8, device=dev)
+            self.uniq = torch.empty(n, dtype=torch.int64, device=dev)
+            self.local_col = torch.empty(n, dtype=torch.int32, device=dev)
+            self.n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.grad = torch.empty(n, dtype=torch.float32, device=dev)
+            self.hess = None
+            self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+            return
         if self.gpu:
             H = hipops()
             self.h = torch.empty(n, dtype=torch.int64, device=dev)
@@ -89,6 +111,11 @@ class Localizer:
 
     def _gpu(self, keys, n) -> Localized:
         H = hipops()
+        if self.mode == "hash":
+            H.localize_hash(keys, self.bits, self.hslots, self.hids, self.epoch, self.htemp,
+                            self.uniq, self.local_col, self.n_uniq, self.grad, self.err)
+            return Localized(self.uniq, None, None, None, self.local_col[:n], self.n_uniq,
+                             self.grad, None, n, hashed=True)
         if self.fast32:
             H.localize32(keys, self.bits, self.sort_temp, self.hs32, self.pos_s, self.segid,
                          self.uniq, self.seg_start, self.local_col, self.n_uniq, self.grad,
