@@ -53,10 +53,15 @@ class ISGDScheduler(App):
         self.monitor.flush()
 
     def merge_progress(self, src: dict, dst: dict) -> dict:
-        """Latest report replaces the old one, examples accumulate (sgd.h:82-87)."""
-        n = dst.get("num_examples_processed", 0)
+        """Latest report replaces the old one, examples accumulate (sgd.h:82-87); the
+        per-minibatch objective / auc / accuracy lists are appended (the reference's
+        "TODO also append objv"), so the printed loss is over every example counted."""
         out = dict(src)
-        out["num_examples_processed"] = src.get("num_examples_processed", 0) + n
+        out["num_examples_processed"] = src.get("num_examples_processed", 0) + \
+            dst.get("num_examples_processed", 0)
+        for k in ("objective", "auc", "accuracy"):
+            if k in src or k in dst:
+                out[k] = list(dst.get(k, [])) + list(src.get(k, []))
         return out
 
     def show_progress(self, t: float, progress: dict):
