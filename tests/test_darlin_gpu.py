@@ -90,3 +90,55 @@ def test_darlin_gpu_criteo_shaped_with_delay():
     prog = tr.train()
     assert prog[-1].objective < prog[0].objective
     assert prog[-1].objective < sd.rows * np.log(2)  # better than the zero model
+
+
+def _rehearsal_worker(rank, world, port, q):
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), PSAMD_DIST_BACKEND="gloo")
+    import torch.distributed as dist
+
+    from parameter_server_amd.data.slot_reader import SlotData
+    from parameter_server_amd.parallel.comm import init_from_env
+
+    comm, dev = init_from_env("cuda")
+    sd = sparse_classification(4000, groups=(1, 2, 3), keys_per_group=800, nnz_per_row=(1, 3, 4),
+                               seed=21)
+    n = sd.rows // world
+    a, b = rank * n, (rank + 1) * n
+    part = SlotData(labels=sd.labels[a:b], groups={
+        g: (off[a:b + 1] - off[a], k[off[a]:off[b]], None) for g, (off, k, v) in sd.groups.items()})
+    tr = DarlinTrainer(part, DarlinConfig(l1=1.0, max_pass=5, tail_freq=1, tau=1, seed=2),
+                       comm=comm, device=dev)
+    prog = tr.train()
+    q.put((rank, [p.objective for p in prog], tr.w.cpu().numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_darlin_two_rank_gpu_rehearsal_matches_single():
+    """2 ranks on one GPU (gloo-staged all-reduce): same objectives as 1 rank."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rehearsal_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in ps], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    sd = sparse_classification(4000, groups=(1, 2, 3), keys_per_group=800, nnz_per_row=(1, 3, 4),
+                               seed=21)
+    ref = DarlinTrainer(sd, DarlinConfig(l1=1.0, max_pass=5, tail_freq=1, tau=1, seed=2),
+                        device="cuda").train()
+    for _, objs, w in res:
+        np.testing.assert_allclose(objs, [p.objective for p in ref], rtol=1e-8)
+    np.testing.assert_array_equal(res[0][2], res[1][2])

@@ -79,3 +79,15 @@ def test_gloo_multi_rank_push_pull(world):
         np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-5)
     assert sum(r[2] for r in res) == 500  # every key lives on exactly one shard
     assert all(r[2] > 0 for r in res)     # and the shards are balanced-ish
+
+
+@pytest.mark.gpu
+def test_kvworker_gpu_single_rank():
+    kv = KVWorker(device="cuda", capacity=1 << 14)
+    keys = torch.randint(0, 1 << 40, (5000,), device="cuda")
+    vals = torch.randn(5000, device="cuda")
+    kv.wait(kv.push(keys, vals))
+    got = kv.wait(kv.pull(keys))
+    uk, inv = torch.unique(keys, return_inverse=True)
+    exp = torch.zeros(uk.numel(), device="cuda").index_add_(0, inv, vals)[inv]
+    torch.testing.assert_close(got, exp, rtol=1e-5, atol=1e-5)

@@ -117,3 +117,49 @@ def test_wide_deep_gpu_full_width_learns():
             first = tr.progress()
     last = tr.progress()
     assert last["loss"] < first["loss"] and np.isfinite(last["loss"])
+
+
+def _wd_rehearsal(rank, world, port, q):
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), PSAMD_DIST_BACKEND="gloo")
+    import torch.distributed as dist
+
+    from parameter_server_amd.parallel.comm import init_from_env
+
+    comm, dev = init_from_env("cuda")
+    cfg = WideDeepConfig(num_features=1 << 22, embedding_dim=64, hidden=(256, 128),
+                         minibatch=1024, table_capacity=1 << 16)
+    tr = WideDeepTrainer(cfg, comm, dev)
+    for s in range(6):
+        k, l = criteo_batch(1024, seed=50 + rank, row0=s * 1024, num_features=1 << 22,
+                            cards=[1000] * 26, device=dev)
+        tr.step(k, l)
+    p = tr.progress()
+    occ, _ = tr.shard.table.census()
+    q.put((rank, p, tr.param.cpu(), occ))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_wide_deep_two_rank_gpu_rehearsal():
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_wd_rehearsal, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in ps], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    assert torch.equal(res[0][2], res[1][2])
+    assert res[0][1]["examples"] == 2 * 6 * 1024 and np.isfinite(res[0][1]["loss"])
+    assert res[0][3] > 0 and res[1][3] > 0
