@@ -103,6 +103,8 @@ void localize_hash(const uint64_t*, int64_t, KeyMix, unsigned long long*, int32_
                    hipStream_t);
 void hash_backward(const int32_t*, int64_t, int, const int32_t*, const float*, const float*,
                    int64_t, float*, const int32_t*, int64_t, hipStream_t);
+void owner_bucket(const uint64_t*, const int32_t*, int64_t, const uint64_t*, int, void*, int64_t*,
+                  uint64_t*, int32_t*, hipStream_t);
 // gemm.hip
 void gemm_bf16(bool, bool, const void*, int, const void*, int, int, int, int, int, const float*,
                const void*, int, void*, int, float*, int, float, int, hipStream_t);
@@ -709,6 +711,23 @@ PYBIND11_MODULE(_hipops, m) {
                          ptr<int64_t>(epoch), temp.data_ptr(), (size_t)temp.numel(),
                          ptr<uint64_t>(uniq), ptr<int32_t>(local_col), ptr<int32_t>(n_uniq), za,
                          ptr<int32_t>(err), cur_stream());
+  });
+  m.def("owner_bucket", [](Tensor uniq, optional<Tensor> n_uniq, Tensor bounds, Tensor temp,
+                           Tensor offsets, Tensor keys_out, Tensor perm) {
+    chk(uniq, at::kLong, "uniq");
+    chk(bounds, at::kLong, "bounds");
+    chk(temp, at::kLong, "temp");
+    chk(offsets, at::kLong, "offsets");
+    chk(keys_out, at::kLong, "keys_out");
+    chk(perm, at::kInt, "perm");
+    const int G = (int)bounds.numel() - 1;
+    check(G >= 1 && G <= 64, "owner_bucket: 1..64 shards (bounds has G+1 entries)");
+    check(temp.numel() >= 128 && offsets.numel() >= G + 1, "temp[128] / offsets[G+1]");
+    check(keys_out.numel() >= uniq.numel() && perm.numel() >= uniq.numel(), "outputs too small");
+    psamd::owner_bucket(ptr<uint64_t>(uniq), optr<int32_t>(n_uniq, at::kInt, "n_uniq"),
+                        uniq.numel(), ptr<uint64_t>(bounds), G, temp.data_ptr(),
+                        ptr<int64_t>(offsets), ptr<uint64_t>(keys_out), ptr<int32_t>(perm),
+                        cur_stream());
   });
   m.def("hash_backward", [](Tensor local_col, int64_t n, int width, optional<Tensor> rows,
                             optional<Tensor> vals, Tensor coef, Tensor grad,

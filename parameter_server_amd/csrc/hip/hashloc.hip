@@ -253,4 +253,112 @@ void hash_backward(const int32_t* local_col, int64_t n, int width, const int32_t
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
+// ----------------------------------------------------------- owner bucketing
+// Multi-GPU exchanges need the unique keys grouped by owner shard. With
+// sort-free ids they are in claim order, so they are bucketed (G <= 64):
+//   count:   per-block LDS counts per owner -> one global atomic per (block, owner)
+//   scatter: every block reserves its per-owner runs with one atomic per owner
+//            on cursors that start at the owner offsets; keys_out[dst] = uniq[u],
+//            perm[dst] = u. Order inside an owner's run is not fixed.
+constexpr int kMaxOwners = 64;
+
+__device__ __forceinline__ int owner_of_key(uint64_t x, const uint64_t* __restrict__ bounds,
+                                            int G) {
+  int lo = 0, hi = G;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (bounds[mid] <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(kBlk)
+ob_count_kernel(const uint64_t* __restrict__ uniq, const int32_t* __restrict__ n_uniq,
+                int64_t n_host, const uint64_t* __restrict__ bounds, int G,
+                unsigned long long* __restrict__ totals) {
+  __shared__ uint32_t cnt[kMaxOwners];
+  if (threadIdx.x < kMaxOwners) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t U = dev_len(n_uniq, n_host);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < U;
+       i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[owner_of_key(uniq[i], bounds, G)], 1u);
+  __syncthreads();
+  if (threadIdx.x < G && cnt[threadIdx.x])
+    atomicAdd(&totals[threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+}
+
+// totals[0:G] -> offsets[0:G+1] (exclusive) and cursors[0:G] = offsets[0:G]
+__global__ void ob_offsets_kernel(const unsigned long long* __restrict__ totals, int G,
+                                  int64_t* __restrict__ offsets,
+                                  unsigned long long* __restrict__ cursors) {
+  if (threadIdx.x != 0) return;
+  unsigned long long run = 0;
+  for (int g = 0; g < G; ++g) {
+    offsets[g] = (int64_t)run;
+    cursors[g] = run;
+    run += totals[g];
+  }
+  offsets[G] = (int64_t)run;
+}
+
+__global__ void __launch_bounds__(kBlk)
+ob_scatter_kernel(const uint64_t* __restrict__ uniq, const int32_t* __restrict__ n_uniq,
+                  int64_t n_host, const uint64_t* __restrict__ bounds, int G,
+                  unsigned long long* __restrict__ cursors, uint64_t* __restrict__ keys_out,
+                  int32_t* __restrict__ perm) {
+  __shared__ uint32_t cnt[kMaxOwners];
+  __shared__ unsigned long long base[kMaxOwners];
+  const int64_t U = dev_len(n_uniq, n_host);
+  const int64_t per_block = (int64_t)blockDim.x * 16;
+  for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < U;
+       b0 += (int64_t)gridDim.x * per_block) {
+    if (threadIdx.x < kMaxOwners) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    int own[16];
+    uint32_t rk[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t i = b0 + j * blockDim.x + threadIdx.x;
+      own[j] = -1;
+      if (i < U) {
+        own[j] = owner_of_key(uniq[i], bounds, G);
+        rk[j] = atomicAdd(&cnt[own[j]], 1u);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < G && cnt[threadIdx.x])
+      base[threadIdx.x] = atomicAdd(&cursors[threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (own[j] < 0) continue;
+      const int64_t i = b0 + j * blockDim.x + threadIdx.x;
+      const int64_t dst = (int64_t)(base[own[j]] + rk[j]);
+      if (in_range(dst, U)) {
+        keys_out[dst] = uniq[i];
+        perm[dst] = (int32_t)i;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+void owner_bucket(const uint64_t* uniq, const int32_t* n_uniq, int64_t n_host,
+                  const uint64_t* bounds, int G, void* temp, int64_t* offsets,
+                  uint64_t* keys_out, int32_t* perm, hipStream_t st) {
+  if (G > kMaxOwners) throw std::runtime_error("owner_bucket: at most 64 shards");
+  unsigned long long* totals = (unsigned long long*)temp;
+  unsigned long long* cursors = totals + kMaxOwners;
+  PSAMD_HIP_CHECK(hipMemsetAsync(totals, 0, kMaxOwners * sizeof(unsigned long long), st));
+  ob_count_kernel<<<grid_for(n_host, kBlk, 1024), kBlk, 0, st>>>(uniq, n_uniq, n_host, bounds, G,
+                                                                  totals);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  ob_offsets_kernel<<<1, 64, 0, st>>>(totals, G, offsets, cursors);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  ob_scatter_kernel<<<grid_for(n_host, kBlk * 16, 1024), kBlk, 0, st>>>(
+      uniq, n_uniq, n_host, bounds, G, cursors, keys_out, perm);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace psamd

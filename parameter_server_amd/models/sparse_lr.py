@@ -89,8 +89,9 @@ class SparseLRTrainer:
         self.table = KVTable(cap, self.device, cfg.init)
         self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
         mode = cfg.localize
-        if mode == "auto":  # hash ids need no owner order: single-GPU, unfiltered steps
-            mode = "hash" if (self.G == 1 and cfg.tail_feature_freq <= 0) else "sort"
+        fused = self.G > 1 and cfg.tail_feature_freq <= 0 and cfg.fixing_float_bytes == 0
+        if mode == "auto":  # sort-free ids: 1 GPU, or the fused exchange (owner bucketing)
+            mode = "hash" if (cfg.tail_feature_freq <= 0 and (self.G == 1 or fused)) else "sort"
         self.localize_mode = mode
         self.localizer = Localizer(self.max_nnz, self.bits, self.device, mode=mode)
         self._localizers = [self.localizer]  # + a second buffer set for prefetching (G > 1)
@@ -158,7 +159,7 @@ class SparseLRTrainer:
                                 iv, isd, seed, self.table._err, self.table._inserted)
             push = ("local", slot, loc.n_uniq)
         elif self.fused:
-            w_local, push = self._exchange_fused(loc.uniq, loc.n_uniq)
+            w_local, push = self._exchange_fused(loc)
         else:
             w_local, push = self._pull(loc.uniq, loc.n_uniq)
         if self._prefetch is not None:  # single-GPU / non-fused paths: no blocking point
@@ -170,8 +171,9 @@ class SparseLRTrainer:
         grad, _ = linear_backward(loc, coef, B=B, width=width or 0, rows=rows, vals=vals)
         if push[0] == "fused":
             # deferred: travels with the next step's pull exchange (see _exchange_fused)
-            _, slot, send_c, recv_c, U = push
-            self.pending = (slot, send_c, recv_c, grad[:U].clone())
+            _, slot, send_c, recv_c, U, perm = push
+            g_send = grad[:U].clone() if perm is None else grad[perm[:U].long()]
+            self.pending = (slot, send_c, recv_c, g_send)
         else:
             self._push(grad, push)
         auc_from_hist(self.hist, self.metrics, self.step_dev)
@@ -180,7 +182,22 @@ class SparseLRTrainer:
         self.examples += B
 
     # ------------------------------------------------------- fused exchange (G > 1)
-    def _exchange_fused(self, uniq: torch.Tensor, n_uniq: torch.Tensor):
+    def _bucket(self, loc):
+        """Owner-group the claim-ordered unique keys of a sort-free localisation:
+        (keys in owner order, perm: owner-order position -> unique id, offsets[G+1])."""
+        n = loc.uniq.numel()
+        if getattr(self, "_bk", None) is None or self._bk[0].numel() < n:
+            dev = loc.uniq.device
+            self._bk = (torch.empty(n, dtype=torch.int64, device=dev),
+                        torch.empty(n, dtype=torch.int32, device=dev),
+                        torch.empty(128, dtype=torch.int64, device=dev),
+                        torch.empty(self.G + 1, dtype=torch.int64, device=dev))
+        keys_out, perm, temp, off = self._bk
+        hipops().owner_bucket(loc.uniq, loc.n_uniq, self.part.bounds_on(loc.uniq.device), temp,
+                              off, keys_out, perm)
+        return keys_out, perm, off
+
+    def _exchange_fused(self, loc):
         """One step of the multi-GPU data plane with 2 all-to-alls instead of 3:
 
         A: per peer [keys(t) | grads(t-1)] packed as int32 words (keys are u32 when
@@ -191,9 +208,14 @@ class SparseLRTrainer:
         B: weights back.
         The per-peer counts of both directions come from ONE all-gather of the
         G x G count matrix (the only host synchronisation of the step)."""
+        uniq, n_uniq = loc.uniq, loc.n_uniq
         G, dev = self.G, uniq.device
         kw = 1 if self.bits <= 32 else 2
-        off = self.part.split_sorted(uniq, n_uniq)
+        perm = None
+        if getattr(loc, "hashed", False):
+            uniq, perm, off = self._bucket(loc)
+        else:
+            off = self.part.split_sorted(uniq, n_uniq)
         send_t = (off[1:] - off[:-1]).to(torch.int64)
         M_dev = self.comm.all_gather_counts(send_t, to_host=False)
         if self._prefetch is not None:  # overlap the next minibatch with this sync
@@ -241,7 +263,11 @@ class SparseLRTrainer:
             slots_by_src.append(slot[a:a + recv_t[s]])
             a += recv_t[s]
         w_back = self.comm.all_to_all_v(w, recv_t, send_t)
-        return w_back, ("fused", slots_by_src, send_t, recv_t, U)
+        if perm is not None:  # back to unique-id order
+            w_local = torch.empty_like(w_back)
+            w_local[perm[:U].long()] = w_back
+            w_back = w_local
+        return w_back, ("fused", slots_by_src, send_t, recv_t, U, perm)
 
     def _apply_pushes(self, parts):
         """parts: [(slots, grads)] per source in rank order."""
