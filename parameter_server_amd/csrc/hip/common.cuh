@@ -95,6 +95,14 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// Sum over the wave, result in EVERY lane (xor butterfly; wave_sum is lane 0 only).
+template <typename T>
+__device__ __forceinline__ T wave_allsum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
 #pragma unroll

@@ -201,7 +201,7 @@ wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __
       const int32_t c = local_col[r * S + lane];
       if (in_range(c, wide_cap)) m += wide_w[c];
     }
-    m = wave_sum(m) + b[0];
+    m = wave_allsum(m) + b[0];  // every lane needs coef below
     const float y = labels[r] > 0.f ? 1.f : -1.f;
     const float ym = y * m;
     const float loss = ym > 0 ? log1pf(expf(-ym)) : -ym + log1pf(expf(ym));

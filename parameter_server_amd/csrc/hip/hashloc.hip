@@ -18,11 +18,9 @@
 // graph-capturable. Ids are dense in [0, U) and ordered by the position of the
 // occurrence that claimed each key (which occurrence wins a race is not fixed).
 //
-// Backward without a CSC order: grad[local_col[i]] += coef[row(i)] with hardware
-// fp32 atomics. For fixed-width rows a wave takes ONE slot (column) of 64
-// consecutive examples, so a small-cardinality slot's hot keys meet inside the
-// wave; a 64-lane match-any on the id (one ballot per id bit) lets singleton
-// lanes add directly and each duplicate group issue one pre-summed atomic.
+// Backward without a CSC order: grad[local_col[i]] += coef[row(i)] through a
+// per-block LDS accumulation cache (hot keys reach global memory once per
+// block), fp32 atomics for the rest.
 #include "common.cuh"
 
 #include <stdexcept>
@@ -155,55 +153,45 @@ hl_gather_kernel(const int32_t* __restrict__ slot_of, int64_t n, const int32_t* 
   if (blockIdx.x == 0 && threadIdx.x == 0) *epoch_dev += 1;  // epoch is read only by A
 }
 
-// grad[local_col[i]] += coef[row(i)] * (vals ? vals[i] : 1), wave-aggregated.
+// grad[local_col[i]] += coef[row(i)] * (vals ? vals[i] : 1).
+// Each block accumulates a contiguous chunk of nnz into a direct-mapped LDS cache
+// of (id, partial) pairs; hot ids (small-cardinality slots) are absorbed in LDS
+// and reach global memory once per block, colliding cold ids go straight to a
+// global fp32 atomic. Coalesced reads, no order required.
+constexpr int kCache = 4096;  // LDS entries (32 KB)
+constexpr int kBwdChunk = 16384;  // nnz per block iteration
+
 __global__ void __launch_bounds__(kBlk)
 hl_backward_kernel(const int32_t* __restrict__ local_col, int64_t n, int width,
                    const int32_t* __restrict__ rows, const float* __restrict__ vals,
                    const float* __restrict__ coef, int64_t B, float* __restrict__ grad,
-                   const int32_t* __restrict__ n_uniq, int64_t grad_cap, int id_bits) {
+                   const int32_t* __restrict__ n_uniq, int64_t grad_cap) {
+  __shared__ int32_t tag[kCache];
+  __shared__ float part[kCache];
   const int64_t U = dev_len(n_uniq, grad_cap);
-  const int lane = threadIdx.x & 63;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  const int64_t nwaves_total = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  // fixed width: wave job j -> slot j % width of examples [64 (j / width), +64)
-  const int64_t jobs = rows ? (n + 63) / 64 : ((B + 63) / 64) * width;
-  for (int64_t j = (((int64_t)blockIdx.x * blockDim.x) >> 6) + (threadIdx.x >> 6); j < jobs;
-       j += nwaves_total) {
-    int64_t i, r;
-    if (rows) {
-      i = j * 64 + lane;
-      r = i < n ? rows[i] : -1;
-    } else {
-      r = (j / width) * 64 + lane;
-      i = r * width + (j % width);
-      if (r >= B) i = n;
+  for (int64_t c0 = (int64_t)blockIdx.x * kBwdChunk; c0 < n;
+       c0 += (int64_t)gridDim.x * kBwdChunk) {
+    for (int e = threadIdx.x; e < kCache; e += kBlk) { tag[e] = -1; part[e] = 0.f; }
+    __syncthreads();
+    const int64_t c1 = min(n, c0 + kBwdChunk);
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlk) {
+      const int32_t u = local_col[i];
+      const int64_t r = rows ? rows[i] : i / width;
+      if (!in_range(u, U) || !in_range(r, B)) continue;
+      const float g = coef[r] * (vals ? vals[i] : 1.f);
+      const int e = (int)(((uint32_t)u * 0x9E3779B1u) >> 20);  // 12-bit index
+      int t = tag[e];
+      if (t == -1) {
+        const int o = atomicCAS(&tag[e], -1, u);
+        t = (o == -1) ? u : o;
+      }
+      if (t == u) atomicAdd(&part[e], g);
+      else atomicAdd(&grad[u], g);  // collision: bypass the cache
     }
-    int32_t u = -1;
-    float g = 0.f;
-    if (i < n) {
-      u = local_col[i];
-      if (in_range(u, U) && in_range(r, B)) g = coef[r] * (vals ? vals[i] : 1.f);
-      else u = -1;
-    }
-    const bool valid = u >= 0;
-    uint64_t peers = __ballot(valid);
-    for (int b = 0; b < id_bits; ++b) {
-      const bool bit = (u >> b) & 1;
-      const uint64_t bal = __ballot(bit);
-      peers &= bit ? bal : ~bal;
-    }
-    const bool single = valid && __popcll(peers) == 1;
-    if (single) atomicAdd(&grad[u], g);
-    // one wave reduction per duplicate group, led by its lowest lane
-    uint64_t leaders = __ballot(valid && !single && (peers & lt) == 0ull);
-    while (leaders) {
-      const int leader = __ffsll((long long)leaders) - 1;
-      const int32_t lu = __shfl(u, leader, 64);
-      float sg = (valid && u == lu) ? g : 0.f;
-      sg = wave_sum(sg);
-      if (lane == leader) atomicAdd(&grad[lu], sg);
-      leaders &= leaders - 1;
-    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kCache; e += kBlk)
+      if (tag[e] >= 0) atomicAdd(&grad[tag[e]], part[e]);
+    __syncthreads();
   }
 }
 
@@ -246,10 +234,9 @@ void hash_backward(const int32_t* local_col, int64_t n, int width, const int32_t
                    const float* vals, const float* coef, int64_t B, float* grad,
                    const int32_t* n_uniq, int64_t grad_cap, hipStream_t st) {
   if (n <= 0) return;
-  int id_bits = 1;
-  while ((1ll << id_bits) < grad_cap) ++id_bits;
-  hl_backward_kernel<<<grid_for(n, kBlk, 8192), kBlk, 0, st>>>(
-      local_col, n, width, rows, vals, coef, B, grad, n_uniq, grad_cap, id_bits);
+  const int64_t blocks = (n + kBwdChunk - 1) / kBwdChunk;
+  hl_backward_kernel<<<(unsigned)(blocks < 2048 ? blocks : 2048), kBlk, 0, st>>>(
+      local_col, n, width, rows, vals, coef, B, grad, n_uniq, grad_cap);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -48,7 +48,10 @@ class Localizer:
     ``mode="sort"``: radix sort + RLE (unique keys in sorted mixed order, CSC order
     for the segmented backward). ``mode="hash"`` (GPU, key bits <= 32): sort-free
     dedup in a per-step scratch hash table (csrc/hip/hashloc.hip); unique keys in
-    claim order, backward by wave-aggregated atomics."""
+    claim order, backward through an LDS accumulation cache + atomics. Measured on
+    MI355X for 65,536 x 39 Criteo-shaped keys (benchmarks/bench_localize.py):
+    sort 218 us + 26 us backward, hash 170 us + 144 us backward, so "sort" is the
+    default; "hash" avoids the O(bits) sort passes for very wide key batches."""
 
     def __init__(self, max_nnz: int, bits: int, device="cpu", with_hess: bool = False,
                  mode: str = "sort"):

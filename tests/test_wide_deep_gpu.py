@@ -17,18 +17,19 @@ def test_shard_init_gather_update_match_cpu():
     keys = torch.randint(0, 1 << 40, (3000,), dtype=torch.int64).unique()
     sc, sg = E.EmbeddingShard(cap, D, "cpu", seed=3), E.EmbeddingShard(cap, D, "cuda", seed=3)
     slc, _ = sc.resolve(keys)
-    slg, _ = sg.resolve(keys.cuda())
-    assert torch.equal(slc, slg.cpu())  # same probing -> same slots
-    rc, rg = sc.gather_rows(slc), sg.gather_rows(slg)
+    slg, _ = sg.resolve(keys.cuda())  # concurrent inserts may place keys differently
+    assert slg.unique().numel() == keys.numel()
+    rc, rg = sc.gather_rows(slc), sg.gather_rows(slg)  # rows in request-key order
     # identical counter-based init stream (fp32 transcendental ulps may move a bf16 rounding)
     torch.testing.assert_close(rg.cpu().float(), rc.float(), rtol=1e-2, atol=1e-4)
     assert rc.float().std().item() == pytest.approx(0.01, rel=0.1)
-    sg.rows.copy_(sc.rows.cuda())
+    sg.rows[slg] = rc.cuda()  # identical starting rows per key
     g = torch.randn(keys.numel(), D)
     sc.update_rows(slc, grad=g, lr=0.1)
     sg.update_rows(slg, grad=g.cuda(), lr=0.1)
-    torch.testing.assert_close(sg.rows.cpu().float(), sc.rows.float(), rtol=1e-2, atol=1e-3)
-    torch.testing.assert_close(sg.acc.cpu(), sc.acc, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(sg.gather_rows(slg).cpu().float(), sc.gather_rows(slc).float(),
+                               rtol=1e-2, atol=1e-3)
+    torch.testing.assert_close(sg.acc[slg].cpu(), sc.acc[slc], rtol=1e-5, atol=1e-7)
     sg.update_rows(slg, grad16=g.cuda().to(torch.bfloat16), lr=0.1)  # bf16 push path runs
 
 
