@@ -105,6 +105,12 @@ emb_expand_kernel(const int32_t* __restrict__ local_col, int64_t nnz,
 }
 
 // dE[u, :] = sum_{k in [seg_start[u], seg_start[u+1])} dX0[pos_s[k], :]
+// Short segments (<= kShortSeg occurrences): one 16-lane group per unique key.
+// Long segments (hot keys of small-cardinality slots, up to B occurrences): a whole
+// 256-thread block per key, 16 groups striding the occurrences, LDS reduction —
+// a hot key no longer serialises the kernel on one group.
+constexpr int kShortSeg = 64;
+
 __global__ void __launch_bounds__(256)
 emb_grad_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ seg_start,
                        const int32_t* __restrict__ n_uniq, int64_t u_cap, int64_t nnz,
@@ -114,6 +120,7 @@ emb_grad_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restr
   for (int64_t u = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; u < U;
        u += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
     const int64_t a = seg_start[u], b = seg_start[u + 1];
+    if (b - a > kShortSeg) continue;  // long segment: emb_grad_reduce_long_kernel
     for (int d0 = l * 8; d0 < D; d0 += kGroup * 8) {
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int64_t k = a; k < b; ++k) {
@@ -127,6 +134,47 @@ emb_grad_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restr
       float4* o = reinterpret_cast<float4*>(dE + u * D + d0);
       o[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
       o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+emb_grad_reduce_long_kernel(const int32_t* __restrict__ pos_s,
+                            const int32_t* __restrict__ seg_start,
+                            const int32_t* __restrict__ n_uniq, int64_t u_cap, int64_t nnz,
+                            const uint16_t* __restrict__ dX0, int D, float* __restrict__ dE) {
+  __shared__ float red[256 / kGroup][128];
+  const int64_t U = dev_len(n_uniq, u_cap);
+  const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  constexpr int kGroups = 256 / kGroup;
+  for (int64_t u = blockIdx.x; u < U; u += gridDim.x) {
+    const int64_t a = seg_start[u], b = seg_start[u + 1];
+    if (b - a <= kShortSeg) continue;  // block-uniform
+    for (int d0 = l * 8; d0 < D; d0 += kGroup * 8) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int64_t k = a + g; k < b; k += kGroups) {
+        const int32_t p = pos_s[k];
+        if (!in_range(p, nnz)) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(dX0 + (int64_t)p * D + d0);
+        const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += bf2f(h[j]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[g][(d0 & 127) + j] = acc[j];
+      __syncthreads();
+      if (g == 0) {
+        float s[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] = 0.f;
+        for (int q = 0; q < kGroups; ++q)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s[j] += red[q][(d0 & 127) + j];
+        float4* o = reinterpret_cast<float4*>(dE + u * D + d0);
+        o[0] = make_float4(s[0], s[1], s[2], s[3]);
+        o[1] = make_float4(s[4], s[5], s[6], s[7]);
+      }
     }
   }
 }
@@ -238,18 +286,24 @@ wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __
     if (lhist[i]) atomicAdd(&hist[i], lhist[i]);
 }
 
-// out[n] = sum_b x[b, n] (bf16 in, fp32 out); a 256-thread block owns 64 columns x all rows
+// out[n] += sum_b x[b, n] (bf16 in, fp32 out; out zeroed by the caller). Block =
+// 64 columns x 512 rows (4 threads per column, 128 rows each), fp32 atomics per
+// column: (N / 64) x (B / 512) blocks fill the chip.
+constexpr int kColRows = 512;
+
 __global__ void __launch_bounds__(256)
 colsum_bf16_kernel(const uint16_t* __restrict__ x, int64_t B, int N, float* __restrict__ out) {
   __shared__ float part[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.y * kColRows, r1 = min(B, r0 + kColRows);
   float s = 0.f;
   if (c < N)
-    for (int64_t r = q; r < B; r += 4) s += bf2f(x[r * N + c]);
+    for (int64_t r = r0 + q; r < r1; r += 4) s += bf2f(x[r * N + c]);
   part[q][threadIdx.x & 63] = s;
   __syncthreads();
-  if (q == 0 && c < N) out[c] = part[0][threadIdx.x] + part[1][threadIdx.x] +
-                                part[2][threadIdx.x] + part[3][threadIdx.x];
+  if (q == 0 && c < N)
+    atomicAdd(&out[c], part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] +
+                           part[3][threadIdx.x]);
 }
 
 // Adam with fp32 master weights; writes the bf16 copy used by the GEMMs.
@@ -305,6 +359,9 @@ void emb_grad_reduce(const int32_t* pos_s, const int32_t* seg_start, const int32
   emb_grad_reduce_kernel<<<grid_for(u_cap, 16, 8192), 256, 0, st>>>(
       pos_s, seg_start, n_uniq, u_cap, nnz, reinterpret_cast<const uint16_t*>(dX0), D, dE);
   PSAMD_HIP_CHECK(hipGetLastError());
+  emb_grad_reduce_long_kernel<<<(unsigned)std::min<int64_t>(u_cap, 2048), 256, 0, st>>>(
+      pos_s, seg_start, n_uniq, u_cap, nnz, reinterpret_cast<const uint16_t*>(dX0), D, dE);
+  PSAMD_HIP_CHECK(hipGetLastError());
 }
 
 void emb_update(const int64_t* slot, int64_t n, const int32_t* n_dev, int64_t cap,
@@ -331,8 +388,8 @@ void wd_head(const void* h, int64_t B, int H, const float* w, const float* b, co
 
 void colsum_bf16(const void* x, int64_t B, int N, float* out, hipStream_t st) {
   if (N <= 0) return;
-  colsum_bf16_kernel<<<(N + 63) / 64, 256, 0, st>>>(reinterpret_cast<const uint16_t*>(x), B, N,
-                                                     out);
+  const dim3 grid((N + 63) / 64, (unsigned)std::max<int64_t>(1, (B + kColRows - 1) / kColRows));
+  colsum_bf16_kernel<<<grid, 256, 0, st>>>(reinterpret_cast<const uint16_t*>(x), B, N, out);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -162,7 +162,7 @@ class WideDeepTrainer:
         # ---------------- MLP backward (ReLU masks fused into the dX GEMMs)
         for i in reversed(range(len(cfg.hidden))):
             GM.linear_weight_grad(dH, acts[i], out=self.dW[i])
-            E.colsum(dH, self.db[i])
+            E.colsum(dH, self.db[i], accumulate=True)  # grads zeroed at the step start
             mask = acts[i] if i > 0 else None
             dH = GM.linear_input_grad(dH, self.W16[i], mask=mask)
         dX0 = dH  # [B, S*D]

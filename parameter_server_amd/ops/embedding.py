@@ -166,11 +166,17 @@ def head(h, w, b, wide_w, local_col, S: int, labels, coef, dh, dw, db, metrics, 
     hist += torch.bincount(pb + torch.where(y > 0, nbins, 0), minlength=2 * nbins).to(hist.dtype)
 
 
-def colsum(x: torch.Tensor, out: torch.Tensor):
+def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = False):
+    """out (+)= column sums of x [B, N] (bf16) in fp32."""
     if is_gpu(x):
+        if not accumulate:
+            out.zero_()
         hipops().colsum_bf16(x, out)
         return out
-    out.copy_(x.float().sum(0))
+    if accumulate:
+        out += x.float().sum(0)
+    else:
+        out.copy_(x.float().sum(0))
     return out
 
 
