@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--num-features", type=float, default=1e9)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--table-slots", type=int, default=1 << 27, help="slots per GPU")
+    ap.add_argument("--gemm", default="mfma", choices=("mfma", "hipblaslt"))
     args = ap.parse_args()
     from parameter_server_amd.models.wide_deep import WideDeepConfig, WideDeepTrainer
     from parameter_server_amd.ops.synthetic import criteo_batch
@@ -33,7 +34,7 @@ def main():
     G, rank = comm.world, comm.rank
     B, N = args.minibatch, int(args.num_features)
     cfg = WideDeepConfig(num_features=N, embedding_dim=args.dim, minibatch=B,
-                         table_capacity=args.table_slots, seed=0)
+                         table_capacity=args.table_slots, gemm=args.gemm, seed=0)
     tr = WideDeepTrainer(cfg, comm, dev)
     keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
     labels = torch.empty(B, dtype=torch.float32, device=dev)
@@ -68,7 +69,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "dtype": "bf16 (fp32 accumulate)",
             "config": {"num_features": N, "embedding_dim": args.dim, "slots": 39,
-                       "hidden": list(cfg.hidden), "global_batch": G * B,
+                       "hidden": list(cfg.hidden), "global_batch": G * B, "gemm": args.gemm,
                        "table_slots_per_gpu": tr.shard.capacity,
                        "shard_gb": tr.shard.nbytes() / 2 ** 30, "mlp_params": tr.num_params},
             "train": {**p, "rows_rank0": occ},

@@ -56,6 +56,7 @@ class WideDeepConfig:
     table_capacity: int = 0              # slots per rank (0 = auto)
     table_load: float = 0.5
     max_table_bytes: int = 160 << 30     # HBM budget of one shard (slots + rows)
+    gemm: str = "mfma"                   # mfma (own fused-epilogue kernel) | hipblaslt
     seed: int = 0
 
 
@@ -152,7 +153,8 @@ class WideDeepTrainer:
         # ---------------- MLP forward
         acts = [X0]
         for i in range(len(cfg.hidden)):
-            acts.append(GM.linear_forward(acts[-1], self.W16[i], self.b[i], relu=True))
+            acts.append(GM.linear_forward(acts[-1], self.W16[i], self.b[i], relu=True,
+                                          backend=cfg.gemm))
         # ---------------- head (wide + deep), loss, metrics, head grads
         self.grad.zero_()
         H = acts[-1]
@@ -161,10 +163,10 @@ class WideDeepTrainer:
                self.dw_head, self.db_head, self.metrics, self.hist, AUC_BINS)
         # ---------------- MLP backward (ReLU masks fused into the dX GEMMs)
         for i in reversed(range(len(cfg.hidden))):
-            GM.linear_weight_grad(dH, acts[i], out=self.dW[i])
+            GM.linear_weight_grad(dH, acts[i], out=self.dW[i], backend=cfg.gemm)
             E.colsum(dH, self.db[i], accumulate=True)  # grads zeroed at the step start
             mask = acts[i] if i > 0 else None
-            dH = GM.linear_input_grad(dH, self.W16[i], mask=mask)
+            dH = GM.linear_input_grad(dH, self.W16[i], mask=mask, backend=cfg.gemm)
         dX0 = dH  # [B, S*D]
         # ---------------- sparse gradients
         u_cap = nnz

@@ -61,25 +61,44 @@ def gemm(A, a_kmajor: bool, B, b_kmajor: bool, M: int, N: int, K: int, *, bias=N
     return x.to(torch.bfloat16) if out_bf16 else None
 
 
-def linear_forward(X, W, bias=None, relu=False):
+# Layer products on the GPU: "mfma" = the hand-written kernel above with fused
+# epilogues; "hipblaslt" = the vendor library GEMM (torch.mm) + separate elementwise
+# epilogue kernels, kept as the measured reference point (benchmarks/bench_gemm.py).
+BACKENDS = ("mfma", "hipblaslt")
+
+
+def linear_forward(X, W, bias=None, relu=False, backend: str = "mfma"):
     """X [B, K] bf16, W [N, K] bf16 -> act(X W^T + b) [B, N] bf16."""
     Bn, K = X.shape
     N = W.shape[0]
+    if backend == "hipblaslt" and is_gpu(X):
+        Z = torch.mm(X, W.t()) if bias is None else torch.addmm(bias.to(X.dtype), X, W.t())
+        return Z.relu_() if relu else Z
     return gemm(X, True, W, True, Bn, N, K, bias=bias, relu=relu)
 
 
-def linear_input_grad(dZ, W, mask=None):
+def linear_input_grad(dZ, W, mask=None, backend: str = "mfma"):
     """dZ [B, N], W [N, K] -> dZ W [B, K] (times the ReLU mask of ``mask`` [B, K])."""
     Bn, N = dZ.shape
     K = W.shape[1]
+    if backend == "hipblaslt" and is_gpu(dZ):
+        dX = torch.mm(dZ, W)
+        return dX.mul_(mask > 0) if mask is not None else dX
     return gemm(dZ, True, W, False, Bn, K, N, mask=mask)
 
 
-def linear_weight_grad(dZ, X, out=None, beta: float = 0.0):
+def linear_weight_grad(dZ, X, out=None, beta: float = 0.0, backend: str = "mfma"):
     """dZ [B, N], X [B, K] -> dW = dZ^T X [N, K] fp32 (``out`` accumulates with ``beta``)."""
     Bn, N = dZ.shape
     K = X.shape[1]
     out = torch.empty(N, K, dtype=torch.float32, device=dZ.device) if out is None else out
+    if backend == "hipblaslt" and is_gpu(dZ):
+        r = torch.mm(dZ.t(), X, out_dtype=torch.float32)
+        if beta == 0.0:
+            out.copy_(r)
+        else:
+            out.mul_(beta).add_(r)
+        return out
     sk = auto_splitk(N, K, Bn) if beta in (0.0, 1.0) else 1
     gemm(dZ, False, X, False, N, K, Bn, out_bf16=False, out_f32=out, beta=beta, splitk=sk)
     return out
