@@ -86,8 +86,8 @@ void emb_init_rows(const int64_t*, const uint64_t*, int64_t, const int32_t*, int
 void emb_gather_rows(const int64_t*, int64_t, int64_t, const void*, int, void*, hipStream_t);
 void emb_expand(const int32_t*, int64_t, const int64_t*, int64_t, const void*, int64_t, int, void*,
                 hipStream_t);
-void emb_grad_reduce(const int32_t*, const int32_t*, const int32_t*, int64_t, int64_t, const void*,
-                     int, float*, hipStream_t);
+void emb_grad_reduce(const int32_t*, const int32_t*, const int32_t*, const int32_t*, int64_t,
+                     int64_t, const void*, int, float*, hipStream_t);
 void emb_update(const int64_t*, int64_t, const int32_t*, int64_t, const float*, const void*, void*,
                 float*, int, float, float, hipStream_t);
 void wd_head(const void*, int64_t, int, const float*, const float*, const float*, int64_t,
@@ -785,9 +785,11 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::emb_expand(ptr<int32_t>(local_col), nnz, ip, ip ? idx->numel() : 0, src.data_ptr(),
                       src.size(0), D, X0.data_ptr(), cur_stream());
   });
-  m.def("emb_grad_reduce", [](Tensor pos_s, Tensor seg_start, Tensor n_uniq, int64_t u_cap,
-                              int64_t nnz, Tensor dX0, int D, Tensor dE) {
+  m.def("emb_grad_reduce", [](Tensor pos_s, Tensor segid, Tensor seg_start, Tensor n_uniq,
+                              int64_t u_cap, int64_t nnz, Tensor dX0, int D, Tensor dE) {
     chk(pos_s, at::kInt, "pos_s");
+    chk(segid, at::kInt, "segid");
+    check(segid.numel() >= nnz, "segid too small");
     chk(seg_start, at::kInt, "seg_start");
     chk(n_uniq, at::kInt, "n_uniq");
     chk(dX0, at::kBFloat16, "dX0");
@@ -795,8 +797,9 @@ PYBIND11_MODULE(_hipops, m) {
     check(D > 0 && D % 8 == 0, "D % 8 == 0");
     check(seg_start.numel() >= u_cap + 1 && pos_s.numel() >= nnz, "segment arrays too small");
     check(dX0.numel() >= nnz * D && dE.numel() >= u_cap * D, "gradient buffers too small");
-    psamd::emb_grad_reduce(ptr<int32_t>(pos_s), ptr<int32_t>(seg_start), ptr<int32_t>(n_uniq),
-                           u_cap, nnz, dX0.data_ptr(), D, ptr<float>(dE), cur_stream());
+    psamd::emb_grad_reduce(ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<int32_t>(seg_start),
+                           ptr<int32_t>(n_uniq), u_cap, nnz, dX0.data_ptr(), D, ptr<float>(dE),
+                           cur_stream());
   });
   m.def("emb_update", [rows_check](Tensor slot, optional<Tensor> n_dev, optional<Tensor> grad,
                                    optional<Tensor> grad16, Tensor rows, Tensor acc, double lr,

@@ -105,11 +105,14 @@ emb_expand_kernel(const int32_t* __restrict__ local_col, int64_t nnz,
 }
 
 // dE[u, :] = sum_{k in [seg_start[u], seg_start[u+1])} dX0[pos_s[k], :]
-// Short segments (<= kShortSeg occurrences): one 16-lane group per unique key.
-// Long segments (hot keys of small-cardinality slots, up to B occurrences): a whole
-// 256-thread block per key, 16 groups striding the occurrences, LDS reduction —
-// a hot key no longer serialises the kernel on one group.
+// Short segments (<= kShortSeg occurrences): one 16-lane group per unique key,
+// plain stores. Long segments (hot keys of small-cardinality slots, up to B
+// occurrences) are zeroed by the first kernel and reduced by the second, which
+// walks the CSC positions in runs of kRun per 16-lane group and adds each run's
+// per-segment partial sum with fp32 atomics — a hot key is spread over
+// B / kRun groups instead of serialising one.
 constexpr int kShortSeg = 64;
+constexpr int kRun = 64;
 
 __global__ void __launch_bounds__(256)
 emb_grad_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ seg_start,
@@ -120,10 +123,10 @@ emb_grad_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restr
   for (int64_t u = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; u < U;
        u += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
     const int64_t a = seg_start[u], b = seg_start[u + 1];
-    if (b - a > kShortSeg) continue;  // long segment: emb_grad_reduce_long_kernel
+    const bool lng = b - a > kShortSeg;  // long: zero here, summed by the run kernel
     for (int d0 = l * 8; d0 < D; d0 += kGroup * 8) {
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int64_t k = a; k < b; ++k) {
+      for (int64_t k = lng ? b : a; k < b; ++k) {
         const int32_t p = pos_s[k];
         if (!in_range(p, nnz)) continue;
         const uint4 v = *reinterpret_cast<const uint4*>(dX0 + (int64_t)p * D + d0);
@@ -139,20 +142,31 @@ emb_grad_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restr
 }
 
 __global__ void __launch_bounds__(256)
-emb_grad_reduce_long_kernel(const int32_t* __restrict__ pos_s,
-                            const int32_t* __restrict__ seg_start,
-                            const int32_t* __restrict__ n_uniq, int64_t u_cap, int64_t nnz,
+emb_grad_reduce_long_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ segid,
+                            const int32_t* __restrict__ seg_start, int64_t u_cap, int64_t nnz,
                             const uint16_t* __restrict__ dX0, int D, float* __restrict__ dE) {
-  __shared__ float red[256 / kGroup][128];
-  const int64_t U = dev_len(n_uniq, u_cap);
   const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
-  constexpr int kGroups = 256 / kGroup;
-  for (int64_t u = blockIdx.x; u < U; u += gridDim.x) {
-    const int64_t a = seg_start[u], b = seg_start[u + 1];
-    if (b - a <= kShortSeg) continue;  // block-uniform
+  const int64_t runs = (nnz + kRun - 1) / kRun;
+  for (int64_t run = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; run < runs;
+       run += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
+    const int64_t k0 = run * kRun, k1 = min(nnz, k0 + kRun);
     for (int d0 = l * 8; d0 < D; d0 += kGroup * 8) {
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      for (int64_t k = a + g; k < b; k += kGroups) {
+      int64_t cur = -1;
+      bool cur_long = false;
+      for (int64_t k = k0; k < k1; ++k) {
+        const int64_t u = (int64_t)segid[k] - 1;
+        if (u != cur) {
+          if (cur_long) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) atomicAdd(dE + cur * D + d0 + j, acc[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+          cur = u;
+          cur_long = in_range(u, u_cap) && seg_start[u + 1] - seg_start[u] > kShortSeg;
+        }
+        if (!cur_long) continue;
         const int32_t p = pos_s[k];
         if (!in_range(p, nnz)) continue;
         const uint4 v = *reinterpret_cast<const uint4*>(dX0 + (int64_t)p * D + d0);
@@ -160,20 +174,9 @@ emb_grad_reduce_long_kernel(const int32_t* __restrict__ pos_s,
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += bf2f(h[j]);
       }
-      __syncthreads();
+      if (cur_long) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[g][(d0 & 127) + j] = acc[j];
-      __syncthreads();
-      if (g == 0) {
-        float s[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] = 0.f;
-        for (int q = 0; q < kGroups; ++q)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) s[j] += red[q][(d0 & 127) + j];
-        float4* o = reinterpret_cast<float4*>(dE + u * D + d0);
-        o[0] = make_float4(s[0], s[1], s[2], s[3]);
-        o[1] = make_float4(s[4], s[5], s[6], s[7]);
+        for (int j = 0; j < 8; ++j) atomicAdd(dE + cur * D + d0 + j, acc[j]);
       }
     }
   }
@@ -352,15 +355,15 @@ void emb_expand(const int32_t* local_col, int64_t nnz, const int64_t* idx, int64
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void emb_grad_reduce(const int32_t* pos_s, const int32_t* seg_start, const int32_t* n_uniq,
-                     int64_t u_cap, int64_t nnz, const void* dX0, int D, float* dE,
-                     hipStream_t st) {
+void emb_grad_reduce(const int32_t* pos_s, const int32_t* segid, const int32_t* seg_start,
+                     const int32_t* n_uniq, int64_t u_cap, int64_t nnz, const void* dX0, int D,
+                     float* dE, hipStream_t st) {
   if (u_cap <= 0) return;
   emb_grad_reduce_kernel<<<grid_for(u_cap, 16, 8192), 256, 0, st>>>(
       pos_s, seg_start, n_uniq, u_cap, nnz, reinterpret_cast<const uint16_t*>(dX0), D, dE);
   PSAMD_HIP_CHECK(hipGetLastError());
-  emb_grad_reduce_long_kernel<<<(unsigned)std::min<int64_t>(u_cap, 2048), 256, 0, st>>>(
-      pos_s, seg_start, n_uniq, u_cap, nnz, reinterpret_cast<const uint16_t*>(dX0), D, dE);
+  emb_grad_reduce_long_kernel<<<grid_for((nnz + kRun - 1) / kRun, 16, 8192), 256, 0, st>>>(
+      pos_s, segid, seg_start, u_cap, nnz, reinterpret_cast<const uint16_t*>(dX0), D, dE);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -14,9 +14,10 @@
 // A[row l&15][k 8(l>>4)..+7], B[k 8(l>>4)..+7][col l&15]; C col = l&15,
 // row = 4(l>>4)+j). Operands are staged global -> registers -> LDS as
 // [rows][BK+8] K-contiguous images (144-B row stride: the 16 lanes of a
-// ds_read_b128 group hit 16 distinct 16-B bank slots); an MN-major operand is
-// transposed during the LDS write (4 k-rows x 8 elements per thread ->
-// 8 x ds_write_b64). Double-buffered LDS with the next tile's global loads in
+// ds_read_b128 group hit 16 distinct 16-B bank slots); an MN-major operand keeps
+// its global layout in LDS ([BK][BM+16], coalesced 16-B loads and stores) and its
+// fragments are read with the gfx950 hardware transpose ds_read_b64_tr_b16.
+// Double-buffered LDS with the next tile's global loads in
 // flight during the current tile's MFMAs (one barrier per K-step). The block
 // index is remapped so consecutive tiles of one A panel share an XCD's L2.
 //
@@ -35,7 +36,16 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128, BK = 64, LDS_K = BK + 8;  // padded row (elements)
+constexpr int LDS_M = BM + 16;  // MN-major image row: [BK][BM + 16] (288-B stride)
 constexpr int THREADS = 256;
+constexpr int LDS_ELEMS = BM * LDS_K > BK * LDS_M ? BM * LDS_K : BK * LDS_M;
+static_assert(BM == BN, "square block tile");
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+
+// MN-major image: element (k, m) at [k][m ^ 64 * ((k >> 3) & 1)]; rows 8 apart then
+// land on disjoint 32-B bank windows for the transposed reads below.
+__device__ __forceinline__ int mn_off(int k, int m) { return k * LDS_M + (m ^ (((k >> 3) & 1) << 6)); }
 
 enum Epi : int {
   EPI_NONE = 0,      // C = acc
@@ -70,14 +80,12 @@ struct Stage {
           v[i] = make_uint4(0, 0, 0, 0);
       }
     } else {
-      // 16 k-quads x 16 row-octets: thread owns k 4kq..4kq+3, rows 8rc..8rc+7.
-      // kq varies fastest across lanes so the transposed LDS writes of a 16-lane
-      // group land on one row, 16 consecutive 8-B slots (conflict-free).
-      const int kq = tid & 15, rc = tid >> 4;
-      const int gr = r0 + rc * 8;
+      // 64 k-rows x 16 chunks of 8 m -> 4 chunks per thread (16 lanes = 256 B per row)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int gk = k0 + kq * 4 + i;
+        const int c = tid + i * THREADS;
+        const int kk = c >> 4, mc = (c & 15) * 8;
+        const int gr = r0 + mc, gk = k0 + kk;
         if (gr < rows && gk < K)
           v[i] = *reinterpret_cast<const uint4*>(p + (int64_t)gk * ld + gr);
         else
@@ -94,21 +102,36 @@ struct Stage {
         *reinterpret_cast<uint4*>(lds + row * LDS_K + kc) = v[i];
       }
     } else {
-      const int kq = tid & 15, rc = tid >> 4;
-      const unsigned short* e0 = reinterpret_cast<const unsigned short*>(&v[0]);
-      const unsigned short* e1 = reinterpret_cast<const unsigned short*>(&v[1]);
-      const unsigned short* e2 = reinterpret_cast<const unsigned short*>(&v[2]);
-      const unsigned short* e3 = reinterpret_cast<const unsigned short*>(&v[3]);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        uint2 w;
-        w.x = (uint32_t)e0[r] | ((uint32_t)e1[r] << 16);
-        w.y = (uint32_t)e2[r] | ((uint32_t)e3[r] << 16);
-        *reinterpret_cast<uint2*>(lds + (rc * 8 + r) * LDS_K + kq * 4) = w;
+      for (int i = 0; i < 4; ++i) {
+        const int c = tid + i * THREADS;
+        const int kk = c >> 4, mc = (c & 15) * 8;
+        *reinterpret_cast<uint4*>(lds + mn_off(kk, mc)) = v[i];
       }
     }
   }
 };
+
+// 16x16x32 operand fragment of rows [rb, rb+16), k [ks, ks+32): lane l gets
+// X[rb + (l & 15)][ks + 8 (l >> 4) + j], j = 0..7.
+template <bool KMAJOR>
+__device__ __forceinline__ bf16x8 load_frag(const __bf16* __restrict__ img, int rb, int ks,
+                                            int lane) {
+  if (KMAJOR)
+    return *reinterpret_cast<const bf16x8*>(img + (rb + (lane & 15)) * LDS_K + ks +
+                                            8 * (lane >> 4));
+  // [k][m] image: two hardware transposed reads (ds_read_b64_tr_b16) of 4 k-rows x 16
+  // m-columns; lane 4r+p of each 16-lane group addresses row r, columns 4p..4p+3.
+  const int q = lane >> 4, li = lane & 15, r = li >> 2, pc = li & 3;
+  const int k1 = ks + 8 * q + r;
+  typedef __attribute__((address_space(3))) v4i16 lds_v4;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + mn_off(k1, rb + 4 * pc)));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + mn_off(k1 + 4, rb + 4 * pc)));
+  const v4i16 both[2] = {lo, hi};
+  return *reinterpret_cast<const bf16x8*>(both);
+}
 
 template <bool A_KMAJOR, bool B_KMAJOR>
 __global__ void __launch_bounds__(THREADS)
@@ -116,7 +139,7 @@ gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict
                  int M, int N, int K, int epi, const float* __restrict__ bias,
                  const __bf16* __restrict__ aux, int ldaux, __bf16* __restrict__ C, int ldc,
                  float* __restrict__ Cf, int ldcf, float beta, int kchunk) {
-  __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][BM * LDS_K];  // [buf][A|B]
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][LDS_ELEMS];  // [buf][A|B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
@@ -148,15 +171,13 @@ gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict
       sa.load(A, lda, M, kend, m0, kbeg + (kt + 1) * BK, tid);
       sb.load(B, ldb, N, kend, n0, kbeg + (kt + 1) * BK, tid);
     }
-    const __bf16* As = lds[cur][0] + (wm * 64 + (lane & 15)) * LDS_K + 8 * (lane >> 4);
-    const __bf16* Bs = lds[cur][1] + (wn * 64 + (lane & 15)) * LDS_K + 8 * (lane >> 4);
 #pragma unroll
     for (int ks = 0; ks < BK; ks += 32) {
       bf16x8 a[4], b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        a[i] = *reinterpret_cast<const bf16x8*>(As + i * 16 * LDS_K + ks);
-        b[i] = *reinterpret_cast<const bf16x8*>(Bs + i * 16 * LDS_K + ks);
+        a[i] = load_frag<A_KMAJOR>(lds[cur][0], wm * 64 + i * 16, ks, lane);
+        b[i] = load_frag<B_KMAJOR>(lds[cur][1], wn * 64 + i * 16, ks, lane);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)

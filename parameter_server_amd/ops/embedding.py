@@ -130,7 +130,8 @@ def grad_reduce(loc, dX0: torch.Tensor, D: int, u_cap: int, out=None):
     if out is None:
         out = torch.empty(u_cap, D, dtype=torch.float32, device=dX0.device)
     if is_gpu(dX0):
-        hipops().emb_grad_reduce(loc.pos_s, loc.seg_start, loc.n_uniq, u_cap, nnz, dX0, D, out)
+        hipops().emb_grad_reduce(loc.pos_s, loc.segid, loc.seg_start, loc.n_uniq, u_cap, nnz, dX0,
+                                 D, out)
         return out
     out.zero_()
     seg = loc.segid[:nnz].long() - 1  # segid is 1-based in the localiser
