@@ -30,10 +30,11 @@ def t(fn, it=50):
     return s.elapsed_time(e) / it * 1e3
 
 
+import os
 for mode in ("sort", "hash"):
     L = Localizer(B * 39, 30, "cuda", mode=mode)
     loc = L(keys)
     us_loc = t(lambda: L(keys))
     us_bwd = t(lambda: linear_backward(loc, coef, B=B, width=39))
-    print(json.dumps({"mode": mode, "B": B, "unique": loc.num_unique(), "localize_us": us_loc,
+    print(json.dumps({"mode": mode, "digit_bits": getattr(L, "digit_bits", None), "B": B, "unique": loc.num_unique(), "localize_us": us_loc,
                       "backward_us": us_bwd}), flush=True)

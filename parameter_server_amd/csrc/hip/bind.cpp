@@ -47,7 +47,7 @@ void owner_of(const uint64_t*, int64_t, const uint64_t*, int, int32_t*, hipStrea
 // sort32.hip
 size_t localize32_temp_bytes(int64_t);
 void localize32(const uint64_t*, int64_t, KeyMix, void*, size_t, uint32_t*, int32_t*, int32_t*,
-                uint64_t*, int32_t*, int32_t*, int32_t*, float*, float*, hipStream_t);
+                uint64_t*, int32_t*, int32_t*, int32_t*, float*, float*, int, hipStream_t);
 // linear.hip
 void linear_fwd(const int64_t*, int64_t, int, const int32_t*, const float*, const float*, int64_t,
                 const float*, int, float*, float*, float*, double*, uint32_t*, int, hipStream_t);
@@ -350,7 +350,8 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("localize32_temp_bytes", [](int64_t n) { return (int64_t)psamd::localize32_temp_bytes(n); });
   m.def("localize32", [](Tensor keys, int bits, Tensor temp, Tensor hs, Tensor pos_s, Tensor segid,
                          Tensor uniq, Tensor seg_start, Tensor local_col, Tensor n_uniq,
-                         optional<Tensor> zero_a, optional<Tensor> zero_b) {
+                         optional<Tensor> zero_a, optional<Tensor> zero_b, int digit_bits) {
+    check(digit_bits == 8 || digit_bits == 10, "localize32 digit_bits: 8 or 10");
     chk(keys, at::kLong, "keys");
     chk(temp, at::kByte, "temp");
     chk(hs, at::kInt, "hs");
@@ -373,8 +374,11 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::localize32(ptr<uint64_t>(keys), n, make_keymix(bits), temp.data_ptr(),
                       (size_t)temp.numel(), ptr<uint32_t>(hs), ptr<int32_t>(pos_s),
                       ptr<int32_t>(segid), ptr<uint64_t>(uniq), ptr<int32_t>(seg_start),
-                      ptr<int32_t>(local_col), ptr<int32_t>(n_uniq), za, zb, cur_stream());
-  });
+                      ptr<int32_t>(local_col), ptr<int32_t>(n_uniq), za, zb, digit_bits,
+                      cur_stream());
+  }, py::arg("keys"), py::arg("bits"), py::arg("temp"), py::arg("hs"), py::arg("pos_s"),
+     py::arg("segid"), py::arg("uniq"), py::arg("seg_start"), py::arg("local_col"),
+     py::arg("n_uniq"), py::arg("zero_a"), py::arg("zero_b"), py::arg("digit_bits") = 8);
   m.def("seg_counts", [](Tensor seg_start, Tensor n_uniq, Tensor counts, int sat) {
     chk(seg_start, at::kInt, "seg_start");
     chk(n_uniq, at::kInt, "n_uniq");

@@ -25,8 +25,8 @@ constexpr int kBlk = 256;
 constexpr int kWaves = kBlk / 64;
 constexpr int kItems = 16;
 constexpr int kTile = kBlk * kItems;  // 4096
-constexpr int kBits = 8;
-constexpr int kDigits = 1 << kBits;
+constexpr int kMaxBits = 10;            // digit width: 8 (4 passes for 30-bit keys)
+constexpr int kMaxDigits = 1 << kMaxBits;  // or 10 (3 passes), a template parameter
 }  // namespace s32
 using namespace s32;
 
@@ -58,13 +58,14 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* ld
 }
 
 // ---------------------------------------------------------------- histogram
-template <bool kMix>
+template <bool kMix, int kBits>
 __global__ void __launch_bounds__(kBlk)
 hist32_kernel(const uint64_t* __restrict__ raw, const uint32_t* __restrict__ keys, int64_t n,
               KeyMix m, uint32_t* __restrict__ mixed_out, int shift, uint32_t* __restrict__ hist,
               int64_t T) {
+  constexpr int kDigits = 1 << kBits;
   __shared__ uint32_t cnt[kDigits];
-  cnt[threadIdx.x] = 0;  // kBlk == kDigits
+  for (int d = threadIdx.x; d < kDigits; d += kBlk) cnt[d] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kTile;
   if (!kMix && base + kTile <= n) {
@@ -95,7 +96,7 @@ hist32_kernel(const uint64_t* __restrict__ raw, const uint32_t* __restrict__ key
     }
   }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * T + blockIdx.x] = cnt[threadIdx.x];
+  for (int d = threadIdx.x; d < kDigits; d += kBlk) hist[(int64_t)d * T + blockIdx.x] = cnt[d];
 }
 
 // ------------------------------------------------------------ 2-launch scan
@@ -160,10 +161,13 @@ void scan2_u32(uint32_t* a, int64_t n, uint32_t* part, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------ scatter
+template <int kBits>
 __global__ void __launch_bounds__(kBlk)
 scatter32_kernel(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in,
                  uint32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t n,
                  int shift, const uint32_t* __restrict__ offs, int64_t T) {
+  constexpr int kDigits = 1 << kBits;
+  constexpr int kDPT = kDigits / kBlk;  // digits per thread in the offset scan
   __shared__ uint32_t skeys[kTile];
   __shared__ int32_t svals[kTile];
   __shared__ uint32_t wcnt[kWaves * kDigits];  // [wave][digit]
@@ -205,17 +209,33 @@ scatter32_kernel(const uint32_t* __restrict__ keys_in, const int32_t* __restrict
     rank[r] = base_cnt + (uint32_t)__popcll(peers & lt_mask);
   }
   __syncthreads();
-  // digit-major offsets: thread t handles digit t
+  // digit-major offsets: thread t handles digits [t*kDPT, (t+1)*kDPT)
   {
-    uint32_t c[kWaves], tot_d = 0;
+    uint32_t tot_d[kDPT], s_t = 0;
 #pragma unroll
-    for (int q = 0; q < kWaves; ++q) { c[q] = wcnt[q * kDigits + t]; tot_d += c[q]; }
+    for (int e = 0; e < kDPT; ++e) {
+      const int d = t * kDPT + e;
+      uint32_t c = 0;
+#pragma unroll
+      for (int q = 0; q < kWaves; ++q) c += wcnt[q * kDigits + d];
+      tot_d[e] = c;
+      s_t += c;
+    }
     uint32_t total;
-    const uint32_t ds = block_excl_scan_u32(tot_d, lds, &total, kWaves);
-    dstart[t] = ds;
-    uint32_t run = ds;
+    uint32_t run = block_excl_scan_u32(s_t, lds, &total, kWaves);
 #pragma unroll
-    for (int q = 0; q < kWaves; ++q) { wcnt[q * kDigits + t] = run; run += c[q]; }
+    for (int e = 0; e < kDPT; ++e) {
+      const int d = t * kDPT + e;
+      dstart[d] = run;
+      uint32_t r2 = run;
+#pragma unroll
+      for (int q = 0; q < kWaves; ++q) {
+        const uint32_t c = wcnt[q * kDigits + d];
+        wcnt[q * kDigits + d] = r2;
+        r2 += c;
+      }
+      run += tot_d[e];
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -319,17 +339,46 @@ rle32_write_kernel(const uint32_t* __restrict__ hs, const int32_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// Workspace: [mixed keys n*4][keys tmp n*4][vals tmp n*4][hist 256*T*4][part T*4]
+// Workspace: [mixed keys n*4][keys tmp n*4][vals tmp n*4][hist D*T*4][part T*4][scan parts]
+// (sized for the widest digit, D = 1024)
 size_t localize32_temp_bytes(int64_t n) {
   const int64_t T = (n + kTile - 1) / kTile;
-  const int64_t chunks = ((int64_t)kDigits * T + kScanChunk - 1) / kScanChunk + T;
-  return (size_t)n * 12 + (size_t)kDigits * T * 4 + (size_t)T * 4 + (size_t)chunks * 4 + 512;
+  const int64_t chunks = ((int64_t)kMaxDigits * T + kScanChunk - 1) / kScanChunk + T;
+  return (size_t)n * 12 + (size_t)kMaxDigits * T * 4 + (size_t)T * 4 + (size_t)chunks * 4 + 512;
 }
 
 // keys (raw u64) -> hs (mixed u32 sorted), pos_s; then RLE outputs.
+template <int kBits>
+static void radix32(const uint64_t* raw, int64_t n, KeyMix m, int64_t T, uint32_t* mixed,
+                    uint32_t* kt, int32_t* vt, uint32_t* hist, uint32_t* spart, uint32_t* hs,
+                    int32_t* pos_s, hipStream_t st) {
+  constexpr int kDigits = 1 << kBits;
+  const int passes = (m.bits + kBits - 1) / kBits;
+  const uint32_t* src_k = mixed;
+  const int32_t* src_v = nullptr;  // iota
+  for (int pass = 0; pass < passes; ++pass) {
+    const bool to_out = ((passes - 1 - pass) % 2) == 0;
+    uint32_t* dk = to_out ? hs : kt;
+    int32_t* dv = to_out ? pos_s : vt;
+    const int shift = pass * kBits;
+    if (pass == 0)
+      hist32_kernel<true, kBits><<<(unsigned)T, kBlk, 0, st>>>(raw, nullptr, n, m, mixed, shift,
+                                                               hist, T);
+    else
+      hist32_kernel<false, kBits><<<(unsigned)T, kBlk, 0, st>>>(nullptr, src_k, n, m, nullptr,
+                                                                shift, hist, T);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    scan2_u32(hist, (int64_t)kDigits * T, spart, st);
+    scatter32_kernel<kBits><<<(unsigned)T, kBlk, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    src_k = dk;
+    src_v = dv;
+  }
+}
+
 void localize32(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
                 uint32_t* hs, int32_t* pos_s, int32_t* segid, uint64_t* uniq, int32_t* seg_start,
-                int32_t* local_col, int32_t* n_uniq, float* zero_a, float* zero_b,
+                int32_t* local_col, int32_t* n_uniq, float* zero_a, float* zero_b, int digit_bits,
                 hipStream_t st) {
   if (n <= 0) return;
   if (m.bits > 32) throw std::runtime_error("localize32 needs key bits <= 32");
@@ -343,30 +392,14 @@ void localize32(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t tem
   int32_t* vt = (int32_t*)p;
   p += (size_t)n * 4;
   uint32_t* hist = (uint32_t*)p;
-  p += (size_t)kDigits * T * 4;
+  p += (size_t)kMaxDigits * T * 4;
   uint32_t* part = (uint32_t*)p;
   p += (size_t)T * 4;
   uint32_t* spart = (uint32_t*)p;  // chunk partials for scan2
-  const int passes = (m.bits + kBits - 1) / kBits;
-  const uint32_t* src_k = mixed;
-  const int32_t* src_v = nullptr;  // iota
-  for (int pass = 0; pass < passes; ++pass) {
-    const bool to_out = ((passes - 1 - pass) % 2) == 0;
-    uint32_t* dk = to_out ? hs : kt;
-    int32_t* dv = to_out ? pos_s : vt;
-    const int shift = pass * kBits;
-    if (pass == 0)
-      hist32_kernel<true><<<(unsigned)T, kBlk, 0, st>>>(raw, nullptr, n, m, mixed, shift, hist, T);
-    else
-      hist32_kernel<false><<<(unsigned)T, kBlk, 0, st>>>(nullptr, src_k, n, m, nullptr, shift,
-                                                         hist, T);
-    PSAMD_HIP_CHECK(hipGetLastError());
-    scan2_u32(hist, (int64_t)kDigits * T, spart, st);
-    scatter32_kernel<<<(unsigned)T, kBlk, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T);
-    PSAMD_HIP_CHECK(hipGetLastError());
-    src_k = dk;
-    src_v = dv;
-  }
+  if (digit_bits == 10)
+    radix32<10>(raw, n, m, T, mixed, kt, vt, hist, spart, hs, pos_s, st);
+  else
+    radix32<8>(raw, n, m, T, mixed, kt, vt, hist, spart, hs, pos_s, st);
   rle32_count_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, n, part);
   PSAMD_HIP_CHECK(hipGetLastError());
   scan2_u32(part, T, spart, st);

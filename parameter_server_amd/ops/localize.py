@@ -92,7 +92,13 @@ class Localizer:
             self.grad = torch.empty(n, dtype=torch.float32, device=dev)
             self.hess = torch.empty(n, dtype=torch.float32, device=dev) if with_hess else None
             self.fast32 = self.bits <= 32
-            if self.fast32:  # fused mix + u32 8-bit-digit sort + fused RLE (csrc/hip/sort32.hip)
+            # digit width of the u32 radix sort: 10-bit digits sort 21..30-bit keys in 3
+            # passes (vs 4 with 8 bits); PSAMD_SORT_DIGIT_BITS overrides for A/B runs
+            import os
+
+            db = int(os.environ.get("PSAMD_SORT_DIGIT_BITS", "0"))
+            self.digit_bits = db if db in (8, 10) else (10 if 24 < self.bits <= 30 else 8)
+            if self.fast32:  # fused mix + u32 radix sort + fused RLE (csrc/hip/sort32.hip)
                 self.hs32 = torch.empty(n, dtype=torch.int32, device=dev)
                 self.sort_temp = torch.empty(H.localize32_temp_bytes(n), dtype=torch.uint8,
                                              device=dev)
@@ -122,7 +128,7 @@ class Localizer:
         if self.fast32:
             H.localize32(keys, self.bits, self.sort_temp, self.hs32, self.pos_s, self.segid,
                          self.uniq, self.seg_start, self.local_col, self.n_uniq, self.grad,
-                         self.hess)
+                         self.hess, self.digit_bits)
             return Localized(self.uniq, self.seg_start, self.pos_s[:n], self.segid[:n],
                              self.local_col[:n], self.n_uniq, self.grad, self.hess, n)
         H.mix_iota(keys, self.bits, self.h, self.pos)
