@@ -240,8 +240,18 @@ __device__ __forceinline__ float planted_w(uint64_t key, uint64_t seed) {
   return 0.6f * sqrtf(-2.f * logf(u1)) * cosf(6.283185307f * u2);
 }
 
+// h % N without a 64-bit division: Barrett reduction with m = floor((2^64 - 1) / N);
+// q = umulhi(h, m) undershoots floor(h / N) by at most 2 -> <= 2 corrections. Exact.
+__device__ __forceinline__ uint64_t mod_barrett(uint64_t h, uint64_t N, uint64_t m) {
+  uint64_t r = h - __umul64hi(h, m) * N;
+  if (r >= N) r -= N;
+  if (r >= N) r -= N;
+  return r;
+}
+
 __device__ __forceinline__ uint64_t criteo_key(uint64_t seed, uint64_t gr, int j,
-                                               uint64_t num_features, float alpha) {
+                                               uint64_t num_features, uint64_t nf_m,
+                                               float alpha) {
   const float u = u01(rng64(seed + (uint64_t)j * 0x632be59bd9b4e019ull, gr));
   uint64_t id;
   if (j < 13) {
@@ -255,7 +265,7 @@ __device__ __forceinline__ uint64_t criteo_key(uint64_t seed, uint64_t gr, int j
     uint64_t v = (uint64_t)x;
     id = v >= 1 ? v - 1 : 0;
   }
-  return fmix64(((uint64_t)(j + 1) << 48) ^ id) % num_features;
+  return mod_barrett(fmix64(((uint64_t)(j + 1) << 48) ^ id), num_features, nf_m);
 }
 
 // One thread per (row, slot): a 256-thread block generates 6 rows (234 features);
@@ -263,8 +273,8 @@ __device__ __forceinline__ uint64_t criteo_key(uint64_t seed, uint64_t gr, int j
 constexpr int kGenRows = 6;
 __global__ void __launch_bounds__(256)
 criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_dev,
-                  int64_t row_scale, int64_t B, uint64_t num_features, float alpha,
-                  uint64_t* __restrict__ keys, float* __restrict__ labels) {
+                  int64_t row_scale, int64_t B, uint64_t num_features, uint64_t nf_m,
+                  float alpha, uint64_t* __restrict__ keys, float* __restrict__ labels) {
   __shared__ float logit[kGenRows];
   if (row0_dev) row0 += (*row0_dev) * row_scale;
   const int t = threadIdx.x;
@@ -274,7 +284,7 @@ criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_
     const int lr = t / 39, j = t % 39;
     const int64_t r = rb + lr;
     if (lr < kGenRows && r < B) {
-      const uint64_t key = criteo_key(seed, (uint64_t)(row0 + r), j, num_features, alpha);
+      const uint64_t key = criteo_key(seed, (uint64_t)(row0 + r), j, num_features, nf_m, alpha);
       keys[r * 39 + j] = key;
       const float pw = planted_w(key, seed);
       if (pw != 0.f) atomicAdd(&logit[lr], pw);
@@ -339,8 +349,9 @@ void criteo_gen(uint64_t seed, int64_t row0, const int64_t* row0_dev, int64_t ro
                 int64_t B, uint64_t num_features, float alpha, uint64_t* keys, float* labels,
                 hipStream_t st) {
   const int64_t blocks = (B + kGenRows - 1) / kGenRows;
+  const uint64_t nf_m = ~0ull / num_features;
   criteo_gen_kernel<<<(unsigned)(blocks < 65535 ? blocks : 65535), 256, 0, st>>>(
-      seed, row0, row0_dev, row_scale, B, num_features, alpha, keys, labels);
+      seed, row0, row0_dev, row_scale, B, num_features, nf_m, alpha, keys, labels);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
