@@ -38,7 +38,8 @@ PYBIND11_MODULE(_pscore, m) {
   });
   m.def("kv_resolve", [](uintptr_t slots, int64_t cap, uintptr_t keys, int64_t n,
                          uintptr_t out_slot, uintptr_t out_w, bool insert, int init_type,
-                         double init_v, double init_s, uint64_t seed) {
+                         double init_v, double init_s, uint64_t seed, uint64_t home_base,
+                         uint64_t home_m) {
     if (cap <= 0 || (cap & (cap - 1))) throw std::invalid_argument("capacity must be 2^k");
     bool full = false;
     int64_t ins;
@@ -46,10 +47,12 @@ PYBIND11_MODULE(_pscore, m) {
       py::gil_scoped_release rel;
       ins = kv_resolve(P<Slot>(slots), cap, P<const uint64_t>(keys), n, P<int64_t>(out_slot),
                        out_w ? P<float>(out_w) : nullptr, insert, init_type, (float)init_v,
-                       (float)init_s, seed, &full);
+                       (float)init_s, seed, &full, home_base, home_m);
     }
     return py::make_tuple(ins, full);
-  });
+  }, py::arg("slots"), py::arg("cap"), py::arg("keys"), py::arg("n"), py::arg("out_slot"),
+     py::arg("out_w"), py::arg("insert"), py::arg("init_type"), py::arg("init_v"),
+     py::arg("init_s"), py::arg("seed"), py::arg("home_base") = 0, py::arg("home_m") = 0);
   m.def("kv_gather", [](uintptr_t slots, uintptr_t idx, int64_t n, uintptr_t out, int field) {
     py::gil_scoped_release rel;
     kv_gather(P<const Slot>(slots), P<const int64_t>(idx), n, P<float>(out), field);

@@ -79,12 +79,15 @@ void kv_init(Slot* slots, int64_t cap) {
 
 int64_t kv_resolve(Slot* slots, int64_t cap, const uint64_t* keys, int64_t n, int64_t* out_slot,
                    float* out_w, bool insert, int init_type, float init_v, float init_s,
-                   uint64_t seed, bool* full) {
+                   uint64_t seed, bool* full, uint64_t home_base, uint64_t home_m) {
   const uint64_t mask = (uint64_t)cap - 1;
+  int lg = 0;
+  while ((1ll << lg) < cap) ++lg;
   int64_t inserted = 0;
   for (int64_t i = 0; i < n; ++i) {
     const uint64_t h = keys[i];
-    uint64_t idx = fmix64(h) & mask;
+    // home slot: hashed, or ordered for a shard's key range (kv_table.hip home_slot)
+    uint64_t idx = (home_m ? ((h - home_base) * home_m) >> (64 - lg) : fmix64(h)) & mask;
     int64_t found = -1;
     for (uint64_t p = 0; p <= mask; ++p) {
       Slot& s = slots[idx];

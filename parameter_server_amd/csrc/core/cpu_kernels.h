@@ -37,7 +37,7 @@ void kv_init(Slot* slots, int64_t cap);
 // returns number of inserted keys; -1 in out_slot for missing / full
 int64_t kv_resolve(Slot* slots, int64_t cap, const uint64_t* keys, int64_t n, int64_t* out_slot,
                    float* out_w, bool insert, int init_type, float init_v, float init_s,
-                   uint64_t seed, bool* full);
+                   uint64_t seed, bool* full, uint64_t home_base = 0, uint64_t home_m = 0);
 void kv_gather(const Slot* slots, const int64_t* idx, int64_t n, float* out, int field);
 void kv_set(Slot* slots, const int64_t* idx, int64_t n, const float* w, const float* z,
             const float* nn);

@@ -15,7 +15,7 @@ namespace psamd {
 // kv_table.hip
 void kv_init(void*, int64_t, hipStream_t);
 void kv_resolve(void*, int64_t, const uint64_t*, int64_t, const int32_t*, int64_t*, float*, bool,
-                int, float, float, uint64_t, int32_t*, int32_t*, hipStream_t);
+                int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t, hipStream_t);
 void kv_gather(const void*, int64_t, const int64_t*, int64_t, const int32_t*, float*, int,
                hipStream_t);
 void kv_set(void*, int64_t, const int64_t*, int64_t, const float*, const float*, const float*,
@@ -185,7 +185,7 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("kv_resolve", [](Tensor slots, Tensor keys, optional<Tensor> n_dev, Tensor out_slot,
                          optional<Tensor> out_w, bool insert, int init_type, double init_v,
                          double init_s, uint64_t seed, optional<Tensor> err,
-                         optional<Tensor> inserted) {
+                         optional<Tensor> inserted, uint64_t home_base, uint64_t home_m) {
     const int64_t cap = slot_capacity(slots);
     chk(keys, at::kLong, "keys");
     chk(out_slot, at::kLong, "out_slot");
@@ -197,8 +197,11 @@ PYBIND11_MODULE(_hipops, m) {
                       optr<int32_t>(n_dev, at::kInt, "n_dev"), ptr<int64_t>(out_slot), w, insert,
                       init_type, (float)init_v, (float)init_s, seed,
                       optr<int32_t>(err, at::kInt, "err"),
-                      optr<int32_t>(inserted, at::kInt, "inserted"), cur_stream());
-  });
+                      optr<int32_t>(inserted, at::kInt, "inserted"), home_base, home_m, cur_stream());
+  }, py::arg("slots"), py::arg("keys"), py::arg("n_dev"), py::arg("out_slot"),
+     py::arg("out_w"), py::arg("insert"), py::arg("init_type"), py::arg("init_v"),
+     py::arg("init_s"), py::arg("seed"), py::arg("err"), py::arg("inserted"),
+     py::arg("home_base") = 0, py::arg("home_m") = 0);
   m.def("kv_gather", [](Tensor slots, Tensor slot_idx, optional<Tensor> n_dev, Tensor out,
                         int field) {
     const int64_t cap = slot_capacity(slots);

@@ -71,7 +71,18 @@ __global__ void kv_init_kernel(Slot* __restrict__ slots, int64_t cap) {
 // table full) and optionally its weight. Fused gather is exact for zero init;
 // for non-zero init the caller uses a separate gather launch (the inserting
 // lane writes w after its CAS, a same-launch reader could see the old 0).
-__global__ void kv_resolve_kernel(Slot* __restrict__ slots, uint64_t mask,
+// Home slot: hashed (fmix64) for arbitrary keys, or ORDERED for a shard that owns
+// the mixed-key range [base, base + span): home = ((key - base) * m) >> (64 - log2 cap)
+// with m = floor((2^64 - 1) / span). Mixed keys are uniform, so the ordered map is as
+// balanced as hashing, and a localiser's sorted unique keys then visit the table in
+// increasing address order (TLB- and DRAM-page-friendly on a 64 GB table).
+__device__ __forceinline__ uint64_t home_slot(uint64_t h, uint64_t mask, uint64_t base,
+                                              uint64_t m, int shr) {
+  return m ? ((h - base) * m) >> shr : (fmix64(h) & mask);
+}
+
+__global__ void kv_resolve_kernel(Slot* __restrict__ slots, uint64_t mask, uint64_t home_base,
+                                  uint64_t home_m, int home_shr,
                                   const uint64_t* __restrict__ keys, int64_t n_host,
                                   const int32_t* __restrict__ n_dev,
                                   int64_t* __restrict__ out_slot, float* __restrict__ out_w,
@@ -83,7 +94,7 @@ __global__ void kv_resolve_kernel(Slot* __restrict__ slots, uint64_t mask,
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t h = keys[i];
-    uint64_t idx = fmix64(h) & mask;
+    uint64_t idx = home_slot(h, mask, home_base, home_m, home_shr) & mask;
     int64_t found = -1;
     float w = 0.f;
     for (uint64_t probe = 0; probe <= mask; ++probe) {
@@ -318,10 +329,14 @@ void kv_init(void* slots, int64_t cap, hipStream_t st) {
 
 void kv_resolve(void* slots, int64_t cap, const uint64_t* keys, int64_t n, const int32_t* n_dev,
                 int64_t* out_slot, float* out_w, bool insert, int init_type, float init_v,
-                float init_s, uint64_t seed, int32_t* err, int32_t* inserted, hipStream_t st) {
+                float init_s, uint64_t seed, int32_t* err, int32_t* inserted, uint64_t home_base,
+                uint64_t home_m, hipStream_t st) {
   const bool fused_w = out_w && init_type == kInitZero;
+  int lg = 0;
+  while ((1ll << lg) < cap) ++lg;
   kv_resolve_kernel<<<grid_for(n, 256), 256, 0, st>>>(
-      (Slot*)slots, (uint64_t)(cap - 1), keys, n, n_dev, out_slot, fused_w ? out_w : nullptr,
+      (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg, keys, n, n_dev, out_slot,
+      fused_w ? out_w : nullptr,
       insert ? 1 : 0, init_type, init_v, init_s, seed, err, inserted);
   PSAMD_HIP_CHECK(hipGetLastError());
   if (out_w && !fused_w) {

@@ -86,7 +86,9 @@ class SparseLRTrainer:
         self.tau = parse_consistency(cfg.consistency)
         self.clock = VectorClock(self.G, self.tau)
         cap = cfg.table_capacity or self.auto_capacity(cfg, self.G, self.bits)
-        self.table = KVTable(cap, self.device, cfg.init)
+        # ordered home slots over this shard's mixed-key range: sorted unique keys then
+        # walk the (up to 64 GB) table in increasing address order
+        self.table = KVTable(cap, self.device, cfg.init, key_range=self.part.range_of(self.rank))
         self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
         mode = cfg.localize
         fused = self.G > 1 and cfg.tail_feature_freq <= 0 and cfg.fixing_float_bytes == 0
@@ -156,7 +158,8 @@ class SparseLRTrainer:
             slot, w_local = self.slot_buf, self.w_buf
             it, iv, isd, seed = self.table.init.args()
             hipops().kv_resolve(self.table.slots, loc.uniq, loc.n_uniq, slot, w_local, True, it,
-                                iv, isd, seed, self.table._err, self.table._inserted)
+                                iv, isd, seed, self.table._err, self.table._inserted,
+                                self.table.home_base, self.table.home_m)
             push = ("local", slot, loc.n_uniq)
         elif self.fused:
             w_local, push = self._exchange_fused(loc)

@@ -44,7 +44,8 @@ class EmbeddingShard:
             w = torch.empty(n, dtype=torch.float32, device=self.device) if w is None else w
             H = hipops()
             H.kv_resolve(self.table.slots, mkeys, n_dev, slot, w, True, it, iv, isd, seed,
-                         self.table._err, self.table._inserted)
+                         self.table._err, self.table._inserted, self.table.home_base,
+                         self.table.home_m)
             H.emb_init_rows(slot, mkeys, n_dev, self.rows, self.inited, self.seed,
                             self.init_scale)
             return slot, w

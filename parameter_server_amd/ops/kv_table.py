@@ -65,8 +65,17 @@ def next_pow2(x: int) -> int:
 
 
 class KVTable:
-    def __init__(self, capacity: int, device="cpu", init: InitRule | None = None):
+    def __init__(self, capacity: int, device="cpu", init: InitRule | None = None,
+                 key_range: tuple[int, int] | None = None):
+        """``key_range = (lo, hi)``: the (mixed) key range this shard owns; keys then get
+        ORDERED home slots (see kv_table.hip home_slot) instead of hashed ones."""
         cap = next_pow2(max(64, int(capacity)))
+        self.home_base, self.home_m = 0, 0
+        if key_range is not None:
+            lo, hi = int(key_range[0]), int(key_range[1])
+            if hi > lo:
+                self.home_base = lo
+                self.home_m = ((1 << 64) - 1) // (hi - lo)
         self.capacity = cap
         self.device = torch.device(device)
         self.init = init or InitRule()
@@ -91,10 +100,11 @@ class KVTable:
         it, iv, isd, seed = self.init.args()
         if self.gpu:
             hipops().kv_resolve(self.slots, keys, n_dev, slot, w, insert, it, iv, isd, seed,
-                                self._err, self._inserted)
+                                self._err, self._inserted, self.home_base, self.home_m)
         else:
             ins, full = core().kv_resolve(ptr(self.slots), self.capacity, ptr(keys), n, ptr(slot),
-                                          ptr(w), insert, it, iv, isd, seed)
+                                          ptr(w), insert, it, iv, isd, seed, self.home_base,
+                                          self.home_m)
             self.num_inserted += ins
             if full:
                 raise RuntimeError("KVTable full: increase capacity")
