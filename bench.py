@@ -25,6 +25,7 @@ import time
 import torch
 
 METRIC = "examples/sec (whole node) sparse LR 10^9 feats at 1/2/4/8 MI355X"
+ALGO_NAMES = {"ftrl": "FTRL-proximal", "adagrad": "proximal AdaGrad", "sgd": "proximal SGD"}
 
 
 def main():
@@ -160,10 +161,10 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (Criteo-1TB-shaped: 13 int + 26 categorical slots, power-law ids "
-                    "hashed into 1e9 features; zero-init FTRL state)",
+                    f"hashed into {N:.0e} features; zero-init optimizer state)",
             "config": {
-                "model": "sparse logistic regression, FTRL-proximal L1=10 L2=1 (server-side), "
-                         f"{N:.0e} hashed features",
+                "model": f"sparse logistic regression, {ALGO_NAMES.get(args.algo, args.algo)} "
+                         f"L1=10 L2=1 (server-side), {N:.0e} hashed features",
                 "global_batch": G * B,
                 "seq_len": 39,
                 "nnz_per_example": 39,
