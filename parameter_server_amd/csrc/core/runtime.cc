@@ -15,8 +15,10 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#ifndef PSAMD_CORE_STANDALONE  // sanitizer test builds (tests/native) include this file
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#endif
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -35,9 +37,11 @@
 #include <unordered_map>
 #include <vector>
 
+#ifndef PSAMD_CORE_STANDALONE
 #include "module_parts.h"
 
 namespace py = pybind11;
+#endif
 
 namespace pscore {
 
@@ -410,6 +414,7 @@ int free_port() {
   return p;
 }
 
+#ifndef PSAMD_CORE_STANDALONE
 void register_runtime(py::module_& m) {
   py::class_<Van>(m, "Van")
       .def(py::init<std::string>())
@@ -473,5 +478,7 @@ void register_runtime(py::module_& m) {
   m.def("interface_ip", &interface_ip, py::arg("interface") = "");
   m.def("free_port", &free_port);
 }
+
+#endif  // PSAMD_CORE_STANDALONE
 
 }  // namespace pscore
