@@ -96,4 +96,5 @@ PYBIND11_MODULE(_pscore, m) {
   register_util(m);
   register_data(m);
   register_runtime(m);
+  register_setops(m);
 }

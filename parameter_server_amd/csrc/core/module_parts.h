@@ -7,4 +7,5 @@ namespace pscore {
 void register_util(pybind11::module_& m);
 void register_data(pybind11::module_& m);
 void register_runtime(pybind11::module_& m);
+void register_setops(pybind11::module_& m);
 }  // namespace pscore

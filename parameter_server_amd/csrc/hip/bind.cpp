@@ -105,6 +105,9 @@ void hash_backward(const int32_t*, int64_t, int, const int32_t*, const float*, c
                    int64_t, float*, const int32_t*, int64_t, hipStream_t);
 void owner_bucket(const uint64_t*, const int32_t*, int64_t, const uint64_t*, int, void*, int64_t*,
                   uint64_t*, int32_t*, hipStream_t);
+// spmv.hip
+void spmv(bool, const int64_t*, const void*, int, const void*, int, int64_t, int64_t, const void*,
+          int64_t, double, double, void*, int64_t, hipStream_t);
 // gemm.hip
 void gemm_bf16(bool, bool, const void*, int, const void*, int, int, int, int, int, const float*,
                const void*, int, void*, int, float*, int, float, int, hipStream_t);
@@ -884,5 +887,31 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::adam_update(ptr<float>(p), ptr<float>(g), ptr<float>(m_), ptr<float>(v), n, (float)lr,
                        (float)b1, (float)b2, (float)eps, (float)bc1, (float)bc2, (float)gscale,
                        p16p, cur_stream());
+  });
+  // SparseMatrix::times (utils/matrix.py): gather (row-reduce) or scatter (atomic) over the
+  // compressed major dimension; y = alpha * A x + beta * y.
+  m.def("spmv", [](bool scatter, Tensor off, Tensor idx, optional<Tensor> val, Tensor x, Tensor y,
+                   double alpha, double beta) {
+    chk(off, at::kLong, "offset");
+    check(idx.is_cuda() && idx.is_contiguous() &&
+              (idx.scalar_type() == at::kInt || idx.scalar_type() == at::kLong),
+          "spmv: index must be contiguous int32/int64 on the GPU");
+    check(x.is_cuda() && x.is_contiguous() &&
+              (x.scalar_type() == at::kFloat || x.scalar_type() == at::kDouble),
+          "spmv: x must be contiguous float32/float64 on the GPU");
+    chk(y, x.scalar_type(), "y");
+    const int64_t n_major = off.numel() - 1, nnz = idx.numel();
+    check(n_major >= 0, "spmv: offset must have n_major + 1 entries");
+    const void* vp = nullptr;
+    if (val.has_value() && val->defined()) {
+      chk(*val, x.scalar_type(), "value");
+      check(val->numel() == nnz, "spmv: value / index length mismatch");
+      vp = val->data_ptr();
+    }
+    if (scatter) check(x.numel() >= n_major, "spmv(scatter): x shorter than the major dimension");
+    else check(y.numel() >= n_major, "spmv(gather): y shorter than the major dimension");
+    psamd::spmv(scatter, ptr<int64_t>(off), idx.data_ptr(), (int)idx.element_size(), vp,
+                (int)x.element_size(), n_major, nnz, x.data_ptr(), x.numel(), alpha, beta,
+                y.data_ptr(), y.numel(), cur_stream());
   });
 }

@@ -22,46 +22,20 @@ import torch
 
 from ..ops.kv_table import KVTable, UpdateRule
 from ..system.message import KEY_MAX
+from ..utils import sarray
 from .shared_parameter import SharedParameter, comp_ass_op
 
 
 def ordered_match(src_key, src_val, dst_key, k: int = 1, op: str = "ASSIGN", dst_val=None):
     """Merge-join of sorted key arrays (reference parallelOrderedMatch,
-    src/util/parallel_ordered_match.h:5-86): for keys present in both, apply
-    ``dst_val[dst] (op)= src_val[src]``; returns (dst_val, number matched)."""
-    src_key = np.asarray(src_key)
-    dst_key = np.asarray(dst_key)
-    n = dst_key.size
-    if dst_val is None:
-        dst_val = np.zeros(n * k, dtype=np.asarray(src_val).dtype)
-    if src_key.size == 0 or n == 0:
-        return dst_val, 0
-    pos = np.searchsorted(dst_key, src_key)
-    pos_c = np.minimum(pos, n - 1)
-    hit = dst_key[pos_c] == src_key
-    sv = np.asarray(src_val).reshape(-1, k)[hit]
-    dv = dst_val.reshape(-1, k)
-    idx = pos_c[hit]
-    if op == "ASSIGN":
-        dv[idx] = sv
-    elif op == "PLUS":
-        np.add.at(dv, idx, sv)
-    elif op == "OR":
-        dv[idx] |= sv
-    else:
-        raise ValueError(op)
-    return dst_val, int(hit.sum())
+    src/util/parallel_ordered_match.h:5-86); native threaded join on CPU
+    (utils/sarray.py -> csrc/core/setops.cc). Returns (dst_val, number matched)."""
+    return sarray.ordered_match(src_key, src_val, dst_key, k, op, dst_val)
 
 
 def ordered_union(k1, v1, k2, v2, k: int = 1):
     """Sorted union with values summed on common keys (parallelUnion)."""
-    keys = np.union1d(k1, k2)
-    vals = np.zeros(keys.size * k, dtype=(v1 if v1 is not None and len(v1) else v2).dtype)
-    if len(k1):
-        ordered_match(k1, v1, keys, k, "PLUS", vals)
-    if len(k2):
-        ordered_match(k2, v2, keys, k, "PLUS", vals)
-    return keys, vals
+    return sarray.parallel_union(np.asarray(k1), np.asarray(v1), np.asarray(k2), np.asarray(v2), k)
 
 
 class KVVector(SharedParameter):
