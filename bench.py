@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--fixing-float", type=int, default=0)
     ap.add_argument("--progress", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check)")
+    ap.add_argument("--trace", default="",
+                    help="write per-rank traffic/phase JSON here ({rank} substituted); "
+                         "PSAMD_TRACE=1 adds roctx ranges + phase timers")
     args = ap.parse_args()
 
     from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
@@ -177,6 +180,10 @@ def main():
                       "table_occupied_rank0": occ, "nnz_w_rank0": nnz},
         }
         print(json.dumps(out), flush=True)
+    if args.trace:
+        from parameter_server_amd.utils import trace
+
+        trace.dump(args.trace, rank)
     if G > 1:
         import torch.distributed as dist
 

@@ -8,7 +8,6 @@ Parsing runs in the C++ runtime (``_pscore.parse_text``, csrc/core/data.cc).
 from __future__ import annotations
 
 import os
-import queue
 import random
 import re
 import threading
@@ -17,6 +16,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from ..ops.native import core
+from ..utils.threads import ThreadsafeLimitedQueue
 
 TEXT_FORMATS = {"DENSE": 1, "SPARSE": 2, "SPARSE_BINARY": 3, "ADFEA": 4, "LIBSVM": 5,
                 "TERAFEA": 6, "VW": 7, "CRITEO": 8}
@@ -151,9 +151,8 @@ class StreamReader:
         self.hadoop = hadoop_home
         self.max_lines = max_lines_per_file
         self.recordio = recordio
-        self._q: queue.Queue = queue.Queue()
-        self._bytes = 0
-        self._cv = threading.Condition()
+        self._q = ThreadsafeLimitedQueue(self.cap_bytes)
+        self._error: BaseException | None = None
         self._thread = None
         self.num_examples = 0
 
@@ -186,16 +185,13 @@ class StreamReader:
                     pending, have = ([rest], rest.rows) if rest.rows else ([], 0)
             if have:
                 self._put(ExampleBatch.concat(pending))
+        except BaseException as e:  # noqa: BLE001  (re-raised by the consumer)
+            self._error = e
         finally:
-            self._put(None)
+            self._q.push(None, 0, finished=True)
 
     def _put(self, b):
-        sz = 0 if b is None else b.keys.nbytes + b.labels.nbytes + b.row_ptr.nbytes
-        with self._cv:
-            while b is not None and self._bytes + sz > self.cap_bytes and self._bytes > 0:
-                self._cv.wait(0.1)
-            self._bytes += sz
-        self._q.put((b, sz))
+        self._q.push(b, max(1, b.keys.nbytes + b.labels.nbytes + b.row_ptr.nbytes))
 
     def start(self):
         self._thread = threading.Thread(target=self._produce, daemon=True, name="stream-reader")
@@ -206,11 +202,10 @@ class StreamReader:
         if self._thread is None:
             self.start()
         while True:
-            b, sz = self._q.get()
-            with self._cv:
-                self._bytes -= sz
-                self._cv.notify_all()
-            if b is None:
+            ok, b = self._q.pop()
+            if not ok:
+                if self._error is not None:
+                    raise self._error
                 return
             self.num_examples += b.rows
             yield b

@@ -40,6 +40,7 @@ from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.consistency import VectorClock, parse_consistency
 from ..parallel.partition import KeyPartition
+from ..utils.trace import trace_range
 
 
 @dataclass
@@ -150,8 +151,11 @@ class SparseLRTrainer:
             rows = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
             hipops().csr_rows(row_ptr, rows)
         if loc is None:
-            loc = self.localizer(keys)
+            with trace_range("localize"):
+                loc = self.localizer(keys)
         self._prefetch = prefetch
+        _pull = trace_range("pull")
+        _pull.__enter__()
         if self.filter is not None:
             w_local, push = self._pull_filtered(loc)
         elif self.G == 1 and self.gpu:
@@ -165,13 +169,19 @@ class SparseLRTrainer:
             w_local, push = self._exchange_fused(loc)
         else:
             w_local, push = self._pull(loc.uniq, loc.n_uniq)
+        _pull.__exit__(None, None, None)
         if self._prefetch is not None:  # single-GPU / non-fused paths: no blocking point
             self._prefetch()
             self._prefetch = None
+        _cmp = trace_range("compute")
+        _cmp.__enter__()
         _, coef, _ = linear_forward(loc.local_col, w_local, labels, B=B, width=width or 0,
                                     row_ptr=row_ptr, vals=vals, loss=self.cfg.loss,
                                     coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
         grad, _ = linear_backward(loc, coef, B=B, width=width or 0, rows=rows, vals=vals)
+        _cmp.__exit__(None, None, None)
+        _push = trace_range("push")
+        _push.__enter__()
         if push[0] == "fused":
             # deferred: travels with the next step's pull exchange (see _exchange_fused)
             _, slot, send_c, recv_c, U, perm = push
@@ -179,6 +189,7 @@ class SparseLRTrainer:
             self.pending = (slot, send_c, recv_c, g_send)
         else:
             self._push(grad, push)
+        _push.__exit__(None, None, None)
         auc_from_hist(self.hist, self.metrics, self.step_dev)
         self.clock.tick(self.rank, self.step_count)
         self.step_count += 1

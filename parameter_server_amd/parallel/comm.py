@@ -14,6 +14,8 @@ import os
 import torch
 import torch.distributed as dist
 
+from ..utils.trace import count_traffic
+
 
 class _Done:
     def wait(self):
@@ -81,6 +83,7 @@ class DistComm(Comm):
             sc = sc.cpu()
         rc = torch.empty_like(sc)
         dist.all_to_all_single(rc, sc.contiguous(), group=self.group)
+        count_traffic("all_to_all_counts", 8 * (sc.numel() - 1), 8 * (sc.numel() - 1))
         return rc
 
     def all_to_all_v(self, send: torch.Tensor, send_counts, recv_counts) -> torch.Tensor:
@@ -94,7 +97,10 @@ class DistComm(Comm):
                                input_split_sizes=sc, group=self.group)
         if staged:
             out = out.to(send.device)
-        self._sent += send.element_size() * (sum(sc) - sc[self.rank]) * max(1, send[0:1].numel())
+        row = send.element_size() * max(1, send[0:1].numel())
+        sent, got = row * (sum(sc) - sc[self.rank]), row * (sum(rc) - rc[self.rank])
+        self._sent += sent
+        count_traffic("all_to_all", sent, got)
         return out
 
     def all_gather_counts(self, counts: torch.Tensor, to_host: bool = True) -> torch.Tensor:
@@ -105,10 +111,17 @@ class DistComm(Comm):
             c = c.cpu()
         out = torch.empty(self.world * c.numel(), dtype=torch.int64, device=c.device)
         dist.all_gather_into_tensor(out, c, group=self.group)
+        count_traffic("all_gather", 8 * c.numel(), 8 * c.numel() * (self.world - 1))
         out = out.reshape(self.world, -1)
         return out.cpu() if to_host else out
 
+    def _count_reduce(self, t: torch.Tensor) -> None:
+        # ring all-reduce: each rank sends/receives 2 (G-1)/G of the buffer
+        b = t.numel() * t.element_size() * 2 * (self.world - 1) // max(1, self.world)
+        count_traffic("all_reduce", b, b)
+
     def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
+        self._count_reduce(t)
         ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
         if self.backend == "gloo" and t.is_cuda:
             h = t.cpu()
@@ -122,6 +135,7 @@ class DistComm(Comm):
         if self.backend == "gloo" and t.is_cuda:  # rehearsal mode: synchronous, staged
             self.all_reduce_(t, op)
             return _Done()
+        self._count_reduce(t)
         ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
         return dist.all_reduce(t, op=ops[op], group=self.group, async_op=True)
 
