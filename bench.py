@@ -28,6 +28,85 @@ METRIC = "examples/sec (whole node) sparse LR 10^9 feats at 1/2/4/8 MI355X"
 ALGO_NAMES = {"ftrl": "FTRL-proximal", "adagrad": "proximal AdaGrad", "sgd": "proximal SGD"}
 
 
+def single_gpu_pipeline(tr, B, N, seed, keys, labels, device, args):
+    """Two-stream software pipeline for one GPU: while the main stream runs step t
+    (pull / forward / backward / push of minibatch t), a high-priority side stream
+    generates minibatch t+1 and localises it into the other workspace. Each stream
+    replays its own LINEAR HIP graph (a single multi-stream graph replays much
+    slower on ROCm); the two are ordered with events: prep(t+1) waits for step(t-1)
+    (it overwrites that step's buffers), step(t) waits for prep(t). Each iteration
+    = one full training step + one full data preparation; the first timed step's
+    data is prepared in warm-up and the last iteration's preparation is unused, so
+    the timed region does exactly K generations, K localisations and K steps.
+    Returns (run, graph_used)."""
+    from parameter_server_amd.ops.synthetic import criteo_batch
+
+    main = torch.cuda.current_stream(device)
+    side = torch.cuda.Stream(device, priority=-1)
+    bufs = [(keys, labels), (torch.empty_like(keys), torch.empty_like(labels))]
+    gen_step = torch.zeros(1, dtype=torch.int64, device=device)  # minibatches generated
+    locs = [None, None]
+
+    def prep(buf):  # generate minibatch #gen_step into bufs[buf], localise it
+        k, lab = bufs[buf]
+        criteo_batch(B, seed=seed, row0=0, num_features=N, device=device, keys=k, labels=lab,
+                     row0_dev=gen_step, row_scale=B)
+        gen_step.add_(1)
+        locs[buf] = tr.localize(k, buf=buf)
+
+    def step(buf):
+        k, lab = bufs[buf]
+        tr.step(k, lab, width=39, loc=locs[buf])
+
+    preps = [lambda: prep(0), lambda: prep(1)]
+    steps_fn = [lambda: step(0), lambda: step(1)]
+    ev_step = torch.cuda.Event()
+    ev_prep = [torch.cuda.Event(), torch.cuda.Event()]
+    state = {"t": 0}
+
+    def iterate():
+        t = state["t"]
+        cur, nxt = t % 2, (t + 1) % 2
+        side.wait_event(ev_step)              # step(t-1) done with bufs[nxt]
+        with torch.cuda.stream(side):
+            preps[nxt]()
+            ev_prep[nxt].record(side)
+        main.wait_event(ev_prep[cur])         # minibatch t is localised
+        steps_fn[cur]()
+        ev_step.record(main)
+        state["t"] = t + 1
+
+    ev_step.record(main)
+    with torch.cuda.stream(side):
+        prep(0)
+        ev_prep[0].record(side)
+    for _ in range(max(2, args.warmup + args.warmup % 2)):
+        iterate()
+    if not args.graph:
+        return iterate, False
+    torch.cuda.synchronize()
+    gp, gs = [], []
+    for i in range(2):  # t is even here: parity i <-> bufs[i]
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            prep(i)
+        gp.append(g)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step(i)
+        gs.append(g)
+    # capture recorded prep(0), prep(1), step(0), step(1) without running them; the
+    # workspace of minibatch t (even) still holds its eager localisation, so the
+    # replays continue from there
+    preps[:] = [gp[0].replay, gp[1].replay]
+    steps_fn[:] = [gs[0].replay, gs[1].replay]
+    torch.cuda.synchronize()
+    for _ in range(2):
+        iterate()
+    torch.cuda.synchronize()
+    return iterate, True
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -38,6 +117,9 @@ def main():
     ap.add_argument("--algo", default="ftrl")
     ap.add_argument("--consistency", default="ssp:4")
     ap.add_argument("--graph", type=int, default=1, help="capture the 1-GPU step in a HIP graph")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="1 GPU: generate + localise minibatch t+1 on a high-priority side "
+                         "stream while step t trains (two alternating HIP graphs)")
     ap.add_argument("--fixing-float", type=int, default=0)
     ap.add_argument("--progress", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check)")
@@ -106,9 +188,12 @@ def main():
             state["t"] = t + 1
 
         run = pipelined_step
-    for _ in range(max(1, args.warmup)):
-        run()
-    if gpu and G == 1 and args.graph:
+    if gpu and G == 1 and args.pipeline:
+        run, graph_used = single_gpu_pipeline(tr, B, N, seed, keys, labels, device, args)
+    else:
+        for _ in range(max(1, args.warmup)):
+            run()
+    if gpu and G == 1 and args.graph and not args.pipeline:
         try:
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()

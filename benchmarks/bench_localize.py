@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Localisation + backward of one 65,536 x 39 Criteo-shaped minibatch: radix-sort +
-RLE (sort32.hip) vs the sort-free hash dedup (hashloc.hip), per-call microseconds."""
+RLE (sort32.hip) vs partition + LDS bitmaps (bucketloc.hip) vs the sort-free hash
+dedup (hashloc.hip), per-call microseconds."""
 import json
 import os
 import sys
@@ -30,8 +31,7 @@ def t(fn, it=50):
     return s.elapsed_time(e) / it * 1e3
 
 
-import os
-for mode in ("sort", "hash"):
+for mode in os.environ.get("PSAMD_LOC_MODES", "sort,bucket,hash").split(","):
     L = Localizer(B * 39, 30, "cuda", mode=mode)
     loc = L(keys)
     us_loc = t(lambda: L(keys))

@@ -105,6 +105,11 @@ void hash_backward(const int32_t*, int64_t, int, const int32_t*, const float*, c
                    int64_t, float*, const int32_t*, int64_t, hipStream_t);
 void owner_bucket(const uint64_t*, const int32_t*, int64_t, const uint64_t*, int, void*, int64_t*,
                   uint64_t*, int32_t*, hipStream_t);
+// bucketloc.hip
+size_t bucketloc_temp_bytes(int64_t);
+void localize_bucket(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, int32_t*,
+                     uint64_t*, int32_t*, int32_t*, int32_t*, float*, float*,
+                     unsigned long long*, hipStream_t);
 // spmv.hip
 void spmv(bool, const int64_t*, const void*, int, const void*, int, int64_t, int64_t, const void*,
           int64_t, double, double, void*, int64_t, hipStream_t);
@@ -385,6 +390,38 @@ PYBIND11_MODULE(_hipops, m) {
   }, py::arg("keys"), py::arg("bits"), py::arg("temp"), py::arg("hs"), py::arg("pos_s"),
      py::arg("segid"), py::arg("uniq"), py::arg("seg_start"), py::arg("local_col"),
      py::arg("n_uniq"), py::arg("zero_a"), py::arg("zero_b"), py::arg("digit_bits") = 8);
+  m.def("bucketloc_temp_bytes", [](int64_t n) { return (int64_t)psamd::bucketloc_temp_bytes(n); });
+  m.def("localize_bucket", [](Tensor keys, int bits, Tensor temp, Tensor pos_s, Tensor segid,
+                              Tensor uniq, Tensor seg_start, Tensor local_col, Tensor n_uniq,
+                              optional<Tensor> zero_a, optional<Tensor> zero_b,
+                              optional<Tensor> dbg) {
+    chk(keys, at::kLong, "keys");
+    chk(temp, at::kByte, "temp");
+    chk(pos_s, at::kInt, "pos_s");
+    chk(segid, at::kInt, "segid");
+    chk(uniq, at::kLong, "uniq");
+    chk(seg_start, at::kInt, "seg_start");
+    chk(local_col, at::kInt, "local_col");
+    chk(n_uniq, at::kInt, "n_uniq");
+    const int64_t n = keys.numel();
+    check(n >= 1 && n < (int64_t)INT32_MAX, "localize_bucket: 1 <= n < 2^31");
+    check(bits >= 2 && bits <= 32, "localize_bucket needs key bits <= 32");
+    check(pos_s.numel() >= n && segid.numel() >= n && uniq.numel() >= n &&
+              seg_start.numel() >= n + 1 && local_col.numel() >= n,
+          "localize_bucket buffers too small");
+    check((size_t)temp.numel() >= psamd::bucketloc_temp_bytes(n), "localize_bucket temp too small");
+    float* za = optr<float>(zero_a, at::kFloat, "zero_a");
+    float* zb = optr<float>(zero_b, at::kFloat, "zero_b");
+    if (za) check(zero_a->numel() >= n, "zero_a too small");
+    if (zb) check(zero_b->numel() >= n, "zero_b too small");
+    psamd::localize_bucket(ptr<uint64_t>(keys), n, make_keymix(bits), temp.data_ptr(),
+                           (size_t)temp.numel(), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
+                           ptr<uint64_t>(uniq), ptr<int32_t>(seg_start), ptr<int32_t>(local_col),
+                           ptr<int32_t>(n_uniq), za, zb,
+                           optr<unsigned long long>(dbg, at::kLong, "dbg"), cur_stream());
+  }, py::arg("keys"), py::arg("bits"), py::arg("temp"), py::arg("pos_s"), py::arg("segid"),
+     py::arg("uniq"), py::arg("seg_start"), py::arg("local_col"), py::arg("n_uniq"),
+     py::arg("zero_a"), py::arg("zero_b"), py::arg("dbg") = py::none());
   m.def("seg_counts", [](Tensor seg_start, Tensor n_uniq, Tensor counts, int sat) {
     chk(seg_start, at::kInt, "seg_start");
     chk(n_uniq, at::kInt, "n_uniq");

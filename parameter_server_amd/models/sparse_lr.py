@@ -65,7 +65,7 @@ class SparseLRConfig:
     countmin_k: int = 2
     consistency: str = "bsp"             # bsp | ssp:<tau> | asp
     push_mode: str = "sequential"        # sequential | aggregate
-    localize: str = "sort"               # sort | hash | auto (hash: sort-free, <= 32-bit keys)
+    localize: str = "sort"               # sort | bucket | hash | auto (bucket/hash: <= 32-bit keys)
     fixing_float_bytes: int = 0          # 0 = off, else 1..7 bytes per pushed gradient
     seed: int = 0
 
