@@ -28,17 +28,23 @@ METRIC = "examples/sec (whole node) sparse LR 10^9 feats at 1/2/4/8 MI355X"
 ALGO_NAMES = {"ftrl": "FTRL-proximal", "adagrad": "proximal AdaGrad", "sgd": "proximal SGD"}
 
 
-def single_gpu_pipeline(tr, B, N, seed, keys, labels, device, args):
-    """Two-stream software pipeline for one GPU: while the main stream runs step t
-    (pull / forward / backward / push of minibatch t), a high-priority side stream
-    generates minibatch t+1 and localises it into the other workspace. Each stream
-    replays its own LINEAR HIP graph (a single multi-stream graph replays much
-    slower on ROCm); the two are ordered with events: prep(t+1) waits for step(t-1)
-    (it overwrites that step's buffers), step(t) waits for prep(t). Each iteration
-    = one full training step + one full data preparation; the first timed step's
-    data is prepared in warm-up and the last iteration's preparation is unused, so
-    the timed region does exactly K generations, K localisations and K steps.
-    Returns (run, graph_used)."""
+def pipeline(tr, B, N, seed, keys, labels, device, args):
+    """Two-stream software pipeline: while the main stream runs step t (exchange /
+    pull, forward, backward, push of minibatch t), a high-priority side stream
+    generates minibatch t+1 and localises it into the other workspace. prep(t+1)
+    waits for step(t-1) (it overwrites that step's buffers), step(t) waits for
+    prep(t).
+
+    With --graph 1 every pure-device piece replays from a HIP graph: the side
+    stream's prep, and the step's compute segments (``SparseLRTrainer.step_segments``:
+    one linear graph per segment and buffer parity; a single multi-stream graph
+    replays much slower on ROCm). On N > 1 GPUs the step's two equal-split RCCL
+    all-to-alls of the padded exchange run between the graph replays; nothing in
+    the step reads back to the host, so the CPU stays ahead of the GPU.
+    Each iteration = one full training step + one full data preparation; the
+    first timed step's data is prepared in warm-up and the last iteration's
+    preparation is unused, so the timed region does exactly K generations,
+    K localisations and K steps. Returns (run, graph_used)."""
     from parameter_server_amd.ops.synthetic import criteo_batch
 
     main = torch.cuda.current_stream(device)
@@ -54,12 +60,16 @@ def single_gpu_pipeline(tr, B, N, seed, keys, labels, device, args):
         gen_step.add_(1)
         locs[buf] = tr.localize(k, buf=buf)
 
-    def step(buf):
+    def segments(buf):
         k, lab = bufs[buf]
-        tr.step(k, lab, width=39, loc=locs[buf])
+        return tr.step_segments(k, lab, width=39, loc=locs[buf])
+
+    def run_segments(buf):
+        for _, fn in segments(buf):
+            fn()
 
     preps = [lambda: prep(0), lambda: prep(1)]
-    steps_fn = [lambda: step(0), lambda: step(1)]
+    steps_fn = [lambda: run_segments(0), lambda: run_segments(1)]
     ev_step = torch.cuda.Event()
     ev_prep = [torch.cuda.Event(), torch.cuda.Event()]
     state = {"t": 0}
@@ -85,21 +95,32 @@ def single_gpu_pipeline(tr, B, N, seed, keys, labels, device, args):
     if not args.graph:
         return iterate, False
     torch.cuda.synchronize()
-    gp, gs = [], []
+    gp, plans = [], []
     for i in range(2):  # t is even here: parity i <-> bufs[i]
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             prep(i)
         gp.append(g)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            step(i)
-        gs.append(g)
+        plan = []
+        for kind, fn in segments(i):  # capture in order: a segment may bake in buffers
+            if kind == "compute":     # the previous one of the same parity selected
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    fn()
+                plan.append(g.replay)
+            else:
+                plan.append(fn)
+        plans.append(plan)
     # capture recorded prep(0), prep(1), step(0), step(1) without running them; the
     # workspace of minibatch t (even) still holds its eager localisation, so the
     # replays continue from there
+
+    def replay(plan):
+        for fn in plan:
+            fn()
+
     preps[:] = [gp[0].replay, gp[1].replay]
-    steps_fn[:] = [gs[0].replay, gs[1].replay]
+    steps_fn[:] = [lambda: replay(plans[0]), lambda: replay(plans[1])]
     torch.cuda.synchronize()
     for _ in range(2):
         iterate()
@@ -118,8 +139,10 @@ def main():
     ap.add_argument("--consistency", default="ssp:4")
     ap.add_argument("--graph", type=int, default=1, help="capture the 1-GPU step in a HIP graph")
     ap.add_argument("--pipeline", type=int, default=1,
-                    help="1 GPU: generate + localise minibatch t+1 on a high-priority side "
-                         "stream while step t trains (two alternating HIP graphs)")
+                    help="generate + localise minibatch t+1 on a high-priority side stream "
+                         "while step t trains (HIP graphs per stream / step segment)")
+    ap.add_argument("--exchange", default="padded", choices=["padded", "exact"],
+                    help="N > 1: fixed-capacity sync-free exchange, or count-sized all-to-all-v")
     ap.add_argument("--fixing-float", type=int, default=0)
     ap.add_argument("--progress", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check)")
@@ -142,7 +165,8 @@ def main():
     # DECAY alpha .01 beta 10.
     cfg = SparseLRConfig(num_features=N, minibatch=B, algo=args.algo, lr_type="decay",
                          alpha=0.01, beta=10.0, l1=10.0, l2=1.0, consistency=args.consistency,
-                         fixing_float_bytes=args.fixing_float, seed=rank)
+                         fixing_float_bytes=args.fixing_float, exchange=args.exchange,
+                         seed=rank)
     tr = SparseLRTrainer(cfg, comm, device)
     keys = torch.empty(B * 39, dtype=torch.int64, device=device)
     labels = torch.empty(B, dtype=torch.float32, device=device)
@@ -162,7 +186,7 @@ def main():
 
     run = one_step
     graph_used = False
-    if gpu and G > 1:
+    if gpu and G > 1 and not tr.padded:
         # multi-GPU: double-buffered minibatches; minibatch t+1 is generated and
         # localised on a side stream while step t waits for its exchange counts
         side = torch.cuda.Stream(device)
@@ -188,8 +212,8 @@ def main():
             state["t"] = t + 1
 
         run = pipelined_step
-    if gpu and G == 1 and args.pipeline:
-        run, graph_used = single_gpu_pipeline(tr, B, N, seed, keys, labels, device, args)
+    if gpu and args.pipeline and (G == 1 or tr.padded):
+        run, graph_used = pipeline(tr, B, N, seed, keys, labels, device, args)
     else:
         for _ in range(max(1, args.warmup)):
             run()
@@ -260,6 +284,8 @@ def main():
                 "consistency": args.consistency,
                 "table_slots_per_gpu": tr.table.capacity,
                 "hip_graph": graph_used,
+                "exchange": (f"{args.exchange} (capacity {tr.xc.C} keys/peer/step)"
+                             if tr.xc is not None else (args.exchange if G > 1 else None)),
             },
             "train": {"loss": prog["loss"], "auc": prog["auc"], "accuracy": prog["accuracy"],
                       "table_occupied_rank0": occ, "nnz_w_rank0": nnz},

@@ -16,6 +16,17 @@ namespace psamd {
 void kv_init(void*, int64_t, hipStream_t);
 void kv_resolve(void*, int64_t, const uint64_t*, int64_t, const int32_t*, int64_t*, float*, bool,
                 int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t, hipStream_t);
+void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int, int64_t*, float*,
+                     bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t,
+                     hipStream_t);
+// exchange.hip
+void xchg_pack_keys(const uint64_t*, const int32_t*, int64_t, const int64_t*, int, int64_t, int,
+                    int64_t, int32_t*, int32_t*, hipStream_t);
+void xchg_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
+                     int64_t, int, int64_t, int32_t*, hipStream_t);
+void xchg_clear_counts(int32_t*, int, int64_t, bool, bool, hipStream_t);
+void xchg_unpack_w(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
+                   int64_t, float*, hipStream_t);
 void kv_gather(const void*, int64_t, const int64_t*, int64_t, const int32_t*, float*, int,
                hipStream_t);
 void kv_set(void*, int64_t, const int64_t*, int64_t, const float*, const float*, const float*,
@@ -23,7 +34,7 @@ void kv_set(void*, int64_t, const int64_t*, int64_t, const float*, const float*,
 void kv_update(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int, int,
                float, float, float, float, float, float, double*, hipStream_t);
 void kv_accumulate(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int64_t*,
-                   int32_t*, hipStream_t);
+                   int32_t*, int64_t, hipStream_t);
 void kv_apply_accumulated(void*, int64_t, const int64_t*, const int32_t*, int64_t, int, int, float,
                           float, float, float, float, float, double*, hipStream_t);
 void kv_census(const void*, int64_t, unsigned long long*, hipStream_t);
@@ -210,6 +221,79 @@ PYBIND11_MODULE(_hipops, m) {
      py::arg("out_w"), py::arg("insert"), py::arg("init_type"), py::arg("init_v"),
      py::arg("init_s"), py::arg("seed"), py::arg("err"), py::arg("inserted"),
      py::arg("home_base") = 0, py::arg("home_m") = 0);
+  // ---------------- fixed-capacity exchange (exchange.hip) ----------------
+  // buffers: send/recv int32 [G * H]; row layout documented in exchange.hip
+  m.def("kv_resolve_rows", [](Tensor slots, Tensor recv, int64_t H, int64_t C, int kw,
+                              Tensor out_slot, Tensor out_w, bool insert, int init_type,
+                              double init_v, double init_s, uint64_t seed, optional<Tensor> err,
+                              optional<Tensor> inserted, uint64_t home_base, uint64_t home_m) {
+    const int64_t cap = slot_capacity(slots);
+    chk(recv, at::kInt, "recv");
+    chk(out_slot, at::kLong, "out_slot");
+    chk(out_w, at::kFloat, "out_w");
+    check(kw == 1 || kw == 2, "kw must be 1 (u32 keys) or 2 (u64 keys)");
+    check(C > 0 && H >= 4 + C * (kw + 1) && H % 4 == 0, "bad exchange row geometry");
+    check(recv.numel() % H == 0, "recv is not a whole number of rows");
+    const int G = (int)(recv.numel() / H);
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(out_slot.numel() >= G * C && out_w.numel() >= G * C, "out_slot/out_w < G*C");
+    psamd::kv_resolve_rows(slots.data_ptr(), cap, ptr<int32_t>(recv), G, H, C, kw,
+                           ptr<int64_t>(out_slot), ptr<float>(out_w), insert, init_type,
+                           (float)init_v, (float)init_s, seed, optr<int32_t>(err, at::kInt, "err"),
+                           optr<int32_t>(inserted, at::kInt, "inserted"), home_base, home_m,
+                           cur_stream());
+  });
+  m.def("xchg_pack_keys", [](Tensor ukeys, Tensor n_uniq, Tensor off, int64_t C, int kw,
+                             int64_t H, Tensor send, optional<Tensor> ovf) {
+    chk(ukeys, at::kLong, "ukeys");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(off, at::kLong, "off");
+    chk(send, at::kInt, "send");
+    const int G = (int)off.numel() - 1;
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(kw == 1 || kw == 2, "kw must be 1 or 2");
+    check(C > 0 && H >= 4 + C * (kw + 1) && H % 4 == 0, "bad exchange row geometry");
+    check(send.numel() == G * H, "send must be [G * H]");
+    psamd::xchg_pack_keys(ptr<uint64_t>(ukeys), ptr<int32_t>(n_uniq), ukeys.numel(),
+                          ptr<int64_t>(off), G, C, kw, H, ptr<int32_t>(send),
+                          optr<int32_t>(ovf, at::kInt, "ovf"), cur_stream());
+  });
+  m.def("xchg_pack_grads", [](Tensor grad, optional<Tensor> perm, Tensor n_uniq, Tensor off,
+                              int64_t C, int kw, int64_t H, Tensor send) {
+    chk(grad, at::kFloat, "grad");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(off, at::kLong, "off");
+    chk(send, at::kInt, "send");
+    const int G = (int)off.numel() - 1;
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(C > 0 && H >= 4 + C * (kw + 1) && H % 4 == 0, "bad exchange row geometry");
+    check(send.numel() == G * H, "send must be [G * H]");
+    const int32_t* pp = optr<int32_t>(perm, at::kInt, "perm");
+    if (pp) check(perm->numel() >= grad.numel(), "perm shorter than grad");
+    psamd::xchg_pack_grads(ptr<float>(grad), pp, ptr<int32_t>(n_uniq), grad.numel(),
+                           ptr<int64_t>(off), G, C, kw, H, ptr<int32_t>(send), cur_stream());
+  });
+  m.def("xchg_clear_counts", [](Tensor send, int64_t H, bool keys, bool grads) {
+    chk(send, at::kInt, "send");
+    check(H > 4 && send.numel() % H == 0, "send is not a whole number of rows");
+    const int G = (int)(send.numel() / H);
+    check(G >= 1 && G <= 64, "1..64 peers");
+    psamd::xchg_clear_counts(ptr<int32_t>(send), G, H, keys, grads, cur_stream());
+  });
+  m.def("xchg_unpack_w", [](Tensor recv_w, optional<Tensor> perm, Tensor n_uniq, Tensor off,
+                            int64_t C, Tensor w_local) {
+    chk(recv_w, at::kFloat, "recv_w");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(off, at::kLong, "off");
+    chk(w_local, at::kFloat, "w_local");
+    const int G = (int)off.numel() - 1;
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(recv_w.numel() >= G * C, "recv_w < G*C");
+    const int32_t* pp = optr<int32_t>(perm, at::kInt, "perm");
+    if (pp) check(perm->numel() >= w_local.numel(), "perm shorter than w_local");
+    psamd::xchg_unpack_w(ptr<float>(recv_w), pp, ptr<int32_t>(n_uniq), w_local.numel(),
+                         ptr<int64_t>(off), G, C, ptr<float>(w_local), cur_stream());
+  });
   m.def("kv_gather", [](Tensor slots, Tensor slot_idx, optional<Tensor> n_dev, Tensor out,
                         int field) {
     const int64_t cap = slot_capacity(slots);
@@ -255,7 +339,8 @@ PYBIND11_MODULE(_hipops, m) {
     check(touched.numel() >= slot_idx.numel(), "touched buffer too small");
     psamd::kv_accumulate(slots.data_ptr(), cap, ptr<int64_t>(slot_idx), ptr<float>(grad),
                          slot_idx.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"),
-                         ptr<int64_t>(touched), ptr<int32_t>(n_touched), cur_stream());
+                         ptr<int64_t>(touched), ptr<int32_t>(n_touched), touched.numel(),
+                         cur_stream());
   });
   m.def("kv_apply_accumulated", [](Tensor slots, Tensor touched, Tensor n_touched, int algo,
                                    int lr_type, double alpha, double beta, double l1, double l2,

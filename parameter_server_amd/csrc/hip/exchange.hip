@@ -1,0 +1,154 @@
+// Fixed-capacity multi-GPU exchange: pack / unpack kernels.
+//
+// The reference moves a pull or push as one ZeroMQ message per server, sized
+// by its sliced key list (src/system/message.h:120-159 sliceKeyOrderedMsg,
+// src/system/van.cc:117-170). Over RCCL a variable-size all-to-all needs the
+// per-peer sizes on the HOST, i.e. one device->host sync per step. Here every
+// peer gets a fixed row of H int32 words instead, with the live counts in the
+// row header, so the whole step (pack -> all-to-all -> owner update/resolve ->
+// all-to-all -> unpack) runs without a host round trip and replays from HIP
+// graphs between the collectives.
+//
+// Row p of the send buffer (H words, H >= 4 + C * (kw + 1)):
+//   [0] nkeys   keys of this step owned by rank p (<= C)
+//   [1] ngrads  gradients of the previous step's keys for rank p (<= C)
+//   [2..3]      padding (keeps the key region 16-B aligned)
+//   [4, 4 + C*kw)          keys: u32 (kw = 1, mixed key space <= 32 bits) or u64
+//   [4 + C*kw, 4 + C*kw + C) gradients (f32 bit patterns)
+// The unique keys of a step are owner-ordered (sorted mixed keys, or the owner
+// bucketing of a hash localisation with `perm` = owner-order -> unique id), and
+// off[G+1] (device) are the owner run offsets. Keys past C in a run are dropped
+// and counted in *ovf (the trainer raises on it; the capacity carries a large
+// statistical margin over the per-peer count of hashed keys).
+#include "common.cuh"
+
+namespace psamd {
+
+constexpr int kMaxPeers = 64;
+
+// Largest p with off[p] <= j (off non-decreasing, off[0] = 0).
+__device__ __forceinline__ int owner_of_pos(const int64_t* soff, int G, int64_t j) {
+  int lo = 0, hi = G - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (soff[mid] <= j) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void load_offsets(const int64_t* __restrict__ off, int G,
+                                             int64_t* soff) {
+  for (int t = threadIdx.x; t <= G; t += blockDim.x) soff[t] = off[t];
+  __syncthreads();
+}
+
+__global__ void xchg_pack_keys_kernel(const uint64_t* __restrict__ ukeys,
+                                      const int32_t* __restrict__ n_uniq, int64_t n_host,
+                                      const int64_t* __restrict__ off, int G, int64_t C, int kw,
+                                      int64_t H, int32_t* __restrict__ send,
+                                      int32_t* __restrict__ ovf) {
+  __shared__ int64_t soff[kMaxPeers + 1];
+  load_offsets(off, G, soff);
+  if (blockIdx.x == 0 && threadIdx.x < G) {
+    const int p = threadIdx.x;
+    const int64_t cnt = soff[p + 1] - soff[p];
+    send[(int64_t)p * H] = (int32_t)(cnt < C ? cnt : C);
+    if (cnt > C && ovf) atomicAdd(ovf, (int32_t)(cnt - C));
+  }
+  const int64_t n = dev_len(n_uniq, n_host);
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int p = owner_of_pos(soff, G, j);
+    const int64_t i = j - soff[p];
+    if (i >= C) continue;
+    int32_t* row = send + (int64_t)p * H + 4;
+    const uint64_t k = ukeys[j];
+    if (kw == 1) row[i] = (int32_t)(uint32_t)k;
+    else reinterpret_cast<uint64_t*>(row)[i] = k;
+  }
+}
+
+__global__ void xchg_pack_grads_kernel(const float* __restrict__ grad,
+                                       const int32_t* __restrict__ perm,
+                                       const int32_t* __restrict__ n_uniq, int64_t n_host,
+                                       const int64_t* __restrict__ off, int G, int64_t C, int kw,
+                                       int64_t H, int32_t* __restrict__ send) {
+  __shared__ int64_t soff[kMaxPeers + 1];
+  load_offsets(off, G, soff);
+  if (blockIdx.x == 0 && threadIdx.x < G) {
+    const int p = threadIdx.x;
+    const int64_t cnt = soff[p + 1] - soff[p];
+    send[(int64_t)p * H + 1] = (int32_t)(cnt < C ? cnt : C);
+  }
+  const int64_t n = dev_len(n_uniq, n_host);
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int p = owner_of_pos(soff, G, j);
+    const int64_t i = j - soff[p];
+    if (i >= C) continue;
+    const int64_t u = perm ? (int64_t)perm[j] : j;
+    const float g = in_range(u, n_host) ? grad[u] : 0.f;
+    reinterpret_cast<float*>(send + (int64_t)p * H + 4 + C * kw)[i] = g;
+  }
+}
+
+// Clears the gradient counts of every row (a flush / first step sends no grads).
+__global__ void xchg_clear_grads_kernel(int32_t* __restrict__ send, int G, int64_t H) {
+  if (threadIdx.x < G) send[(int64_t)threadIdx.x * H + 1] = 0;
+}
+
+__global__ void xchg_clear_keys_kernel(int32_t* __restrict__ send, int G, int64_t H) {
+  if (threadIdx.x < G) send[(int64_t)threadIdx.x * H] = 0;
+}
+
+// w_local[unique id] <- the owner's reply (recv_w row p = weights of the keys this
+// rank sent to p, in send order); dropped (overflow) keys read 0.
+__global__ void xchg_unpack_w_kernel(const float* __restrict__ recv_w,
+                                     const int32_t* __restrict__ perm,
+                                     const int32_t* __restrict__ n_uniq, int64_t n_host,
+                                     const int64_t* __restrict__ off, int G, int64_t C,
+                                     float* __restrict__ w_local) {
+  __shared__ int64_t soff[kMaxPeers + 1];
+  load_offsets(off, G, soff);
+  const int64_t n = dev_len(n_uniq, n_host);
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const int p = owner_of_pos(soff, G, j);
+    const int64_t i = j - soff[p];
+    const float v = i < C ? recv_w[(int64_t)p * C + i] : 0.f;
+    const int64_t u = perm ? (int64_t)perm[j] : j;
+    if (in_range(u, n_host)) w_local[u] = v;
+  }
+}
+
+void xchg_pack_keys(const uint64_t* ukeys, const int32_t* n_uniq, int64_t n_host,
+                    const int64_t* off, int G, int64_t C, int kw, int64_t H, int32_t* send,
+                    int32_t* ovf, hipStream_t st) {
+  xchg_pack_keys_kernel<<<grid_for(n_host, 256), 256, 0, st>>>(ukeys, n_uniq, n_host, off, G, C,
+                                                                kw, H, send, ovf);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void xchg_pack_grads(const float* grad, const int32_t* perm, const int32_t* n_uniq,
+                     int64_t n_host, const int64_t* off, int G, int64_t C, int kw, int64_t H,
+                     int32_t* send, hipStream_t st) {
+  xchg_pack_grads_kernel<<<grid_for(n_host, 256), 256, 0, st>>>(grad, perm, n_uniq, n_host, off,
+                                                                 G, C, kw, H, send);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void xchg_clear_counts(int32_t* send, int G, int64_t H, bool keys, bool grads, hipStream_t st) {
+  if (grads) xchg_clear_grads_kernel<<<1, 64, 0, st>>>(send, G, H);
+  if (keys) xchg_clear_keys_kernel<<<1, 64, 0, st>>>(send, G, H);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void xchg_unpack_w(const float* recv_w, const int32_t* perm, const int32_t* n_uniq,
+                   int64_t n_host, const int64_t* off, int G, int64_t C, float* w_local,
+                   hipStream_t st) {
+  xchg_unpack_w_kernel<<<grid_for(n_host, 256), 256, 0, st>>>(recv_w, perm, n_uniq, n_host, off,
+                                                               G, C, w_local);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace psamd

@@ -81,6 +81,43 @@ __device__ __forceinline__ uint64_t home_slot(uint64_t h, uint64_t mask, uint64_
   return m ? ((h - base) * m) >> shr : (fmix64(h) & mask);
 }
 
+// Probe for one key; insert it if asked. Returns the slot index (-1: absent or
+// table full) and the weight through *w.
+__device__ __forceinline__ int64_t resolve_key(Slot* __restrict__ slots, uint64_t mask,
+                                               uint64_t home_base, uint64_t home_m, int home_shr,
+                                               uint64_t h, int insert, int init_type,
+                                               float init_v, float init_s, uint64_t seed,
+                                               float* w, int* ins) {
+  uint64_t idx = home_slot(h, mask, home_base, home_m, home_shr) & mask;
+  *w = 0.f;
+  for (uint64_t probe = 0; probe <= mask; ++probe) {
+    uint64_t k = slots[idx].key;
+    if (k == h) {
+      *w = slots[idx].w;
+      return (int64_t)idx;
+    }
+    if (k == kEmptyKey) {
+      if (!insert) return -1;
+      unsigned long long prev = atomicCAS((unsigned long long*)&slots[idx].key,
+                                          (unsigned long long)kEmptyKey, (unsigned long long)h);
+      if (prev == kEmptyKey) {
+        if (init_type != kInitZero) {
+          *w = init_value(h, init_type, init_v, init_s, seed);
+          slots[idx].w = *w;
+        }
+        ++*ins;
+        return (int64_t)idx;
+      }
+      if (prev == h) {
+        *w = slots[idx].w;
+        return (int64_t)idx;
+      }
+    }
+    idx = (idx + 1) & mask;
+  }
+  return -1;
+}
+
 __global__ void kv_resolve_kernel(Slot* __restrict__ slots, uint64_t mask, uint64_t home_base,
                                   uint64_t home_m, int home_shr,
                                   const uint64_t* __restrict__ keys, int64_t n_host,
@@ -93,39 +130,9 @@ __global__ void kv_resolve_kernel(Slot* __restrict__ slots, uint64_t mask, uint6
   int local_ins = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const uint64_t h = keys[i];
-    uint64_t idx = home_slot(h, mask, home_base, home_m, home_shr) & mask;
-    int64_t found = -1;
-    float w = 0.f;
-    for (uint64_t probe = 0; probe <= mask; ++probe) {
-      uint64_t k = slots[idx].key;
-      if (k == h) {
-        found = (int64_t)idx;
-        w = slots[idx].w;
-        break;
-      }
-      if (k == kEmptyKey) {
-        if (!insert) break;
-        unsigned long long prev = atomicCAS((unsigned long long*)&slots[idx].key,
-                                            (unsigned long long)kEmptyKey,
-                                            (unsigned long long)h);
-        if (prev == kEmptyKey) {
-          found = (int64_t)idx;
-          if (init_type != kInitZero) {
-            w = init_value(h, init_type, init_v, init_s, seed);
-            slots[idx].w = w;
-          }
-          ++local_ins;
-          break;
-        }
-        if (prev == h) {
-          found = (int64_t)idx;
-          w = slots[idx].w;
-          break;
-        }
-      }
-      idx = (idx + 1) & mask;
-    }
+    float w;
+    const int64_t found = resolve_key(slots, mask, home_base, home_m, home_shr, keys[i], insert,
+                                      init_type, init_v, init_s, seed, &w, &local_ins);
     if (found < 0 && insert && err) atomicOr(err, 1);  // table full
     out_slot[i] = found;
     if (out_w) out_w[i] = w;
@@ -133,6 +140,54 @@ __global__ void kv_resolve_kernel(Slot* __restrict__ slots, uint64_t mask, uint6
   if (inserted) {
     int tot = wave_sum(local_ins);
     if ((threadIdx.x & 63) == 0 && tot) atomicAdd(inserted, tot);
+  }
+}
+
+// Owner side of the fixed-capacity exchange (exchange.hip): the received buffer
+// holds one row of H int32 words per source rank, [nkeys, ngrads, -, -, keys (C x kw
+// words), grads (C)]. blockIdx.y = source; resolves that row's nkeys keys into
+// out_slot[s*C + i] and out_w[s*C + i] (the weights that travel back).
+__global__ void kv_resolve_rows_kernel(Slot* __restrict__ slots, uint64_t mask,
+                                       uint64_t home_base, uint64_t home_m, int home_shr,
+                                       const int32_t* __restrict__ recv, int64_t H, int64_t C,
+                                       int kw, int64_t* __restrict__ out_slot,
+                                       float* __restrict__ out_w, int insert, int init_type,
+                                       float init_v, float init_s, uint64_t seed,
+                                       int32_t* __restrict__ err, int32_t* __restrict__ inserted) {
+  const int s = blockIdx.y;
+  const int32_t* row = recv + (int64_t)s * H;
+  const int64_t n = dev_len(row, C);
+  int local_ins = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = kw == 1 ? (uint64_t)(uint32_t)row[4 + i]
+                               : reinterpret_cast<const uint64_t*>(row + 4)[i];
+    float w;
+    const int64_t found = resolve_key(slots, mask, home_base, home_m, home_shr, h, insert,
+                                      init_type, init_v, init_s, seed, &w, &local_ins);
+    if (found < 0 && insert && err) atomicOr(err, 1);
+    out_slot[(int64_t)s * C + i] = found;
+    out_w[(int64_t)s * C + i] = w;
+  }
+  if (inserted) {
+    int tot = wave_sum(local_ins);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(inserted, tot);
+  }
+}
+
+// Re-read w of the rows' resolved slots after the resolve launch has completed
+// (non-zero init: a lane that lost the insert race to another row may have read w
+// before the inserting lane wrote it).
+__global__ void kv_gather_rows_kernel(const Slot* __restrict__ slots, int64_t cap,
+                                      const int32_t* __restrict__ recv, int64_t H, int64_t C,
+                                      const int64_t* __restrict__ slot_idx,
+                                      float* __restrict__ out_w) {
+  const int s = blockIdx.y;
+  const int64_t n = dev_len(recv + (int64_t)s * H, C);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t si = slot_idx[(int64_t)s * C + i];
+    out_w[(int64_t)s * C + i] = in_range(si, cap) ? slots[si].w : 0.f;
   }
 }
 
@@ -250,7 +305,8 @@ __global__ void kv_accumulate_kernel(Slot* __restrict__ slots, int64_t cap,
                                      const int64_t* __restrict__ slot_idx,
                                      const float* __restrict__ grad, int64_t n_host,
                                      const int32_t* __restrict__ n_dev,
-                                     int64_t* __restrict__ touched, int32_t* __restrict__ n_touched) {
+                                     int64_t* __restrict__ touched, int32_t* __restrict__ n_touched,
+                                     int64_t touched_cap) {
   const int64_t n = dev_len(n_dev, n_host);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -261,7 +317,7 @@ __global__ void kv_accumulate_kernel(Slot* __restrict__ slots, int64_t cap,
     atomicAdd(&slots[si].acc, g);
     if (atomicOr(&slots[si].flags, 1u) == 0u) {
       int pos = atomicAdd(n_touched, 1);
-      if (pos < n_host) touched[pos] = si;
+      if (pos < touched_cap) touched[pos] = si;
     }
   }
 }
@@ -346,6 +402,24 @@ void kv_resolve(void* slots, int64_t cap, const uint64_t* keys, int64_t n, const
   }
 }
 
+void kv_resolve_rows(void* slots, int64_t cap, const int32_t* recv, int G, int64_t H, int64_t C,
+                     int kw, int64_t* out_slot, float* out_w, bool insert, int init_type,
+                     float init_v, float init_s, uint64_t seed, int32_t* err, int32_t* inserted,
+                     uint64_t home_base, uint64_t home_m, hipStream_t st) {
+  int lg = 0;
+  while ((1ll << lg) < cap) ++lg;
+  dim3 grid(grid_for(C, 256, 1024), G);
+  kv_resolve_rows_kernel<<<grid, 256, 0, st>>>(
+      (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg, recv, H, C, kw, out_slot,
+      out_w, insert ? 1 : 0, init_type, init_v, init_s, seed, err, inserted);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  if (init_type != kInitZero) {
+    kv_gather_rows_kernel<<<grid, 256, 0, st>>>((const Slot*)slots, cap, recv, H, C, out_slot,
+                                                out_w);
+    PSAMD_HIP_CHECK(hipGetLastError());
+  }
+}
+
 void kv_gather(const void* slots, int64_t cap, const int64_t* slot_idx, int64_t n,
                const int32_t* n_dev, float* out, int field, hipStream_t st) {
   kv_gather_kernel<<<grid_for(n, 256), 256, 0, st>>>((const Slot*)slots, cap, slot_idx, n, n_dev,
@@ -370,9 +444,9 @@ void kv_update(void* slots, int64_t cap, const int64_t* slot_idx, const float* g
 
 void kv_accumulate(void* slots, int64_t cap, const int64_t* slot_idx, const float* grad,
                    int64_t n, const int32_t* n_dev, int64_t* touched, int32_t* n_touched,
-                   hipStream_t st) {
+                   int64_t touched_cap, hipStream_t st) {
   kv_accumulate_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, cap, slot_idx, grad, n,
-                                                         n_dev, touched, n_touched);
+                                                         n_dev, touched, n_touched, touched_cap);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -67,6 +67,12 @@ class SparseLRConfig:
     push_mode: str = "sequential"        # sequential | aggregate
     localize: str = "sort"               # sort | bucket | hash | auto (bucket/hash: <= 32-bit keys)
     fixing_float_bytes: int = 0          # 0 = off, else 1..7 bytes per pushed gradient
+    # multi-GPU data plane: "padded" = fixed-capacity rows per peer with device-side
+    # counts (no host sync, graph-replayable); "exact" = count exchange + sized
+    # all-to-all-v (one host sync per step)
+    exchange: str = "padded"
+    exchange_capacity: int = 0           # keys per peer per step; 0 = auto (first step)
+    exchange_slack: float = 1.5          # auto capacity = slack * max per-peer count + 1024
     seed: int = 0
 
     def update_rule(self) -> UpdateRule:
@@ -111,7 +117,12 @@ class SparseLRTrainer:
             self.w_buf = torch.empty(self.max_nnz, dtype=torch.float32, device=dev)
             self.touched = None
         # multi-GPU: fuse push(t-1) into the pull exchange of step t (2 all-to-alls/step)
+        if cfg.exchange not in ("padded", "exact"):
+            raise ValueError(f"exchange must be 'padded' or 'exact', not {cfg.exchange!r}")
         self.fused = self.G > 1 and self.filter is None and cfg.fixing_float_bytes == 0
+        self.padded = self.fused and cfg.exchange == "padded"
+        self.fused = self.fused and not self.padded
+        self.xc = None  # padded-exchange state (allocated on the first step)
         self.pending = None
         self._prefetch = None
         self.step_count = 0
@@ -144,6 +155,18 @@ class SparseLRTrainer:
         localised minibatch (``localize``); ``prefetch``: called once the step's
         exchange counts are in flight and before the step blocks on them (multi-GPU),
         so the caller can enqueue the next minibatch's work on another stream."""
+        if self.padded:
+            if loc is None:
+                with trace_range("localize"):
+                    loc = self.localizer(keys)
+            segs = self.step_segments(keys, labels, width=width, row_ptr=row_ptr, vals=vals,
+                                      rows=rows, loc=loc)
+            for kind, fn in segs:
+                if kind == "comm" and prefetch is not None:
+                    prefetch()  # overlap the next minibatch with this step's exchange
+                    prefetch = None
+                fn()
+            return
         B = labels.numel()
         if width is None and row_ptr is None:
             width = self.cfg.max_nnz_per_example
@@ -194,6 +217,208 @@ class SparseLRTrainer:
         self.clock.tick(self.rank, self.step_count)
         self.step_count += 1
         self.examples += B
+
+    # --------------------------------------------- padded exchange (G > 1, default)
+    def step_segments(self, keys: torch.Tensor, labels: torch.Tensor, *, width=None,
+                      row_ptr=None, vals=None, rows=None, loc=None):
+        """The step as an ordered list of ``(kind, fn)``: ``"compute"`` segments are
+        pure device work on fixed buffers (capturable in a HIP graph per localisation
+        buffer), ``"comm"`` segments are the two equal-split RCCL all-to-alls, and
+        ``"host"`` is the host bookkeeping. No segment reads anything back to the host,
+        so a step is enqueued without waiting for the GPU.
+
+          compute  owner-split the unique keys, pack [keys(t)] next to [grads(t-1)]
+          comm     all-to-all A
+          compute  owner: pushes of t-1 (one optimizer step per source, rank order),
+                   then lookup-or-insert of the pulled keys of t -> weights
+          comm     all-to-all B (weights back)
+          compute  unpack weights, forward, backward, pack grads(t) for step t+1, AUC
+          host     counters, vector clock
+        """
+        if not self.padded:
+            return [("compute", lambda: self.step(keys, labels, width=width, row_ptr=row_ptr,
+                                                  vals=vals, rows=rows, loc=loc))]
+        if loc is None:
+            loc = self.localizer(keys)
+        B = labels.numel()
+        if width is None and row_ptr is None:
+            width = self.cfg.max_nnz_per_example
+        if row_ptr is not None and rows is None and self.gpu:
+            rows = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
+        if self.xc is None:
+            self._xc_setup(loc)
+        xc = self.comm
+
+        def finish():
+            if row_ptr is not None and self.gpu:
+                hipops().csr_rows(row_ptr, rows)
+            self._x_finish(loc, labels, B, width, row_ptr, vals, rows)
+
+        def host():
+            self.clock.tick(self.rank, self.step_count)
+            self.step_count += 1
+            self.examples += B
+
+        return [("compute", lambda: self._x_pack_keys(loc)),
+                ("comm", lambda: xc.all_to_all_fixed(self.xc.send, self.xc.recv)),
+                ("compute", lambda: self._x_serve(resolve=True)),
+                ("comm", lambda: xc.all_to_all_fixed(self.xc.wsend, self.xc.wrecv)),
+                ("compute", finish),
+                ("host", host)]
+
+    def _xc_setup(self, loc):
+        """Allocate the fixed exchange rows. Capacity C (keys per peer per step) is the
+        same on every rank: configured, or slack x the max per-peer count of the first
+        minibatch over all ranks (collective; hashed keys split ~Binomial(U, 1/G),
+        so the margin is many standard deviations)."""
+        from types import SimpleNamespace
+
+        cfg, G, dev = self.cfg, self.G, self.device
+        C = int(cfg.exchange_capacity)
+        if C <= 0:
+            _, _, off = self._owner_order(loc)
+            cnt = (off[1:] - off[:-1]).max().to(torch.float64).reshape(1)
+            cnt = self.comm.all_reduce_(cnt.to(self.comm.device) if self.comm.backend == "nccl"
+                                        else cnt.cpu(), op="max")
+            C = int(math.ceil(float(cnt.item()) * cfg.exchange_slack)) + 1024
+        C = min(max(64, (C + 63) // 64 * 64), max(64, self.max_nnz))
+        kw = 1 if self.bits <= 32 else 2
+        H = (4 + C * (kw + 1) + 3) // 4 * 4
+        z32 = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
+        self.xc = SimpleNamespace(
+            C=C, kw=kw, H=H,
+            send=z32(G * H, torch.int32), recv=z32(G * H, torch.int32),
+            slot=torch.full((G * C,), -1, dtype=torch.int64, device=dev),
+            wsend=z32(G * C, torch.float32), wrecv=z32(G * C, torch.float32),
+            w_local=z32(self.max_nnz, torch.float32), ovf=z32(1, torch.int32),
+            off=z32(G + 1, torch.int64), cur=None,
+            touched=torch.empty(G * C, dtype=torch.int64, device=dev) if self.gpu else None,
+            n_touched=z32(1, torch.int32))
+
+    def _owner_order(self, loc):
+        """(keys in owner order, perm owner-order -> unique id | None, off[G+1])."""
+        if getattr(loc, "hashed", False):
+            return self._bucket(loc)
+        if self.gpu:
+            off = self.xc.off if self.xc is not None else torch.empty(
+                self.G + 1, dtype=torch.int64, device=self.device)
+            hipops().owner_split(loc.uniq, loc.n_uniq, self.part.bounds_on(self.device), off)
+            return loc.uniq, None, off
+        return loc.uniq, None, self.part.split_sorted(loc.uniq, loc.n_uniq)
+
+    def _x_pack_keys(self, loc):
+        xc = self.xc
+        ukeys, perm, off = self._owner_order(loc)
+        xc.cur = (perm, off, loc.n_uniq)
+        if self.gpu:
+            hipops().xchg_pack_keys(ukeys, loc.n_uniq, off, xc.C, xc.kw, xc.H, xc.send, xc.ovf)
+            return
+        H, C, kw = xc.H, xc.C, xc.kw
+        for p in range(self.G):
+            a, cnt = int(off[p]), int(off[p + 1] - off[p])
+            c = min(cnt, C)
+            xc.send[p * H] = c
+            xc.ovf += cnt - c
+            k = ukeys[a:a + c]
+            k32 = k.to(torch.int32) if kw == 1 else k.contiguous().view(torch.int32)
+            xc.send[p * H + 4:p * H + 4 + c * kw] = k32
+
+    def _x_serve(self, resolve: bool = True):
+        """Owner side: the pushes of the previous step, in source-rank order, then the
+        pulls of this step."""
+        xc, G, H, C, kw = self.xc, self.G, self.xc.H, self.xc.C, self.xc.kw
+        g0 = 4 + C * kw
+        rows = [xc.recv[s * H:(s + 1) * H] for s in range(G)]
+        if self.gpu:
+            hh = hipops()
+            if self.cfg.push_mode == "aggregate":
+                xc.n_touched.zero_()
+                for s in range(G):
+                    hh.kv_accumulate(self.table.slots, xc.slot[s * C:(s + 1) * C],
+                                     rows[s][g0:g0 + C].view(torch.float32), rows[s][1:2],
+                                     xc.touched, xc.n_touched)
+                hh.kv_apply_accumulated(self.table.slots, xc.touched, xc.n_touched,
+                                        *self.rule.args(), self.stats)
+            else:
+                for s in range(G):
+                    hh.kv_update(self.table.slots, xc.slot[s * C:(s + 1) * C],
+                                 rows[s][g0:g0 + C].view(torch.float32), rows[s][1:2],
+                                 *self.rule.args(), self.stats)
+            if resolve:
+                it, iv, isd, seed = self.table.init.args()
+                hh.kv_resolve_rows(self.table.slots, xc.recv, H, C, kw, xc.slot, xc.wsend, True,
+                                   it, iv, isd, seed, self.table._err, self.table._inserted,
+                                   self.table.home_base, self.table.home_m)
+            return
+        parts = []
+        for s in range(G):
+            ng = int(rows[s][1])
+            if ng:
+                parts.append((xc.slot[s * C:s * C + ng], rows[s][g0:g0 + ng].view(torch.float32)))
+        self._apply_pushes(parts)
+        if not resolve:
+            return
+        for s in range(G):
+            nk = int(rows[s][0])
+            if not nk:
+                continue
+            if kw == 1:
+                req = rows[s][4:4 + nk].to(torch.int64) & 0xFFFFFFFF
+            else:
+                req = rows[s][4:4 + 2 * nk].contiguous().view(torch.int64)
+            slot, w = self.table.resolve(req, insert=True)
+            xc.slot[s * C:s * C + nk] = slot
+            xc.wsend[s * C:s * C + nk] = w
+
+    def _x_finish(self, loc, labels, B, width, row_ptr, vals, rows):
+        xc = self.xc
+        perm, off, n_uniq = xc.cur
+        if self.gpu:
+            w_local = xc.w_local[:loc.uniq.numel()]
+            hipops().xchg_unpack_w(xc.wrecv, perm, n_uniq, off, xc.C, w_local)
+        else:
+            U = int(n_uniq)
+            w_local = torch.zeros(max(U, 1), dtype=torch.float32)
+            for p in range(self.G):
+                a, c = int(off[p]), min(int(off[p + 1] - off[p]), xc.C)
+                w_local[a:a + c] = xc.wrecv[p * xc.C:p * xc.C + c]
+        _, coef, _ = linear_forward(loc.local_col, w_local, labels, B=B, width=width or 0,
+                                    row_ptr=row_ptr, vals=vals, loss=self.cfg.loss,
+                                    coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
+        grad, _ = linear_backward(loc, coef, B=B, width=width or 0, rows=rows, vals=vals)
+        H, C, kw = xc.H, xc.C, xc.kw
+        if self.gpu:
+            hipops().xchg_pack_grads(grad[:loc.uniq.numel()], perm, n_uniq, off, C, kw, H,
+                                     xc.send)
+        else:
+            for p in range(self.G):
+                a, c = int(off[p]), min(int(off[p + 1] - off[p]), C)
+                xc.send[p * H + 1] = c
+                g0 = p * H + 4 + C * kw
+                xc.send[g0:g0 + c] = grad[a:a + c].contiguous().view(torch.int32)
+        auc_from_hist(self.hist, self.metrics, self.step_dev)
+
+    def _x_flush(self):
+        """Apply the gradients packed by the last step (a keys-free exchange)."""
+        xc = self.xc
+        if self.gpu:
+            hipops().xchg_clear_counts(xc.send, xc.H, True, False)
+        else:
+            for p in range(self.G):
+                xc.send[p * xc.H] = 0
+        self.comm.all_to_all_fixed(xc.send, xc.recv)
+        self._x_serve(resolve=False)
+        if self.gpu:
+            hipops().xchg_clear_counts(xc.send, xc.H, False, True)
+        else:
+            for p in range(self.G):
+                xc.send[p * xc.H + 1] = 0
+        ovf = int(xc.ovf.item())
+        if ovf:
+            raise RuntimeError(
+                f"padded exchange overflow: {ovf} keys exceeded the per-peer capacity "
+                f"{xc.C} (they were pulled as 0 and not pushed); set exchange_capacity "
+                f"or exchange_slack higher, or exchange='exact'")
 
     # ------------------------------------------------------- fused exchange (G > 1)
     def _bucket(self, loc):
@@ -295,7 +520,12 @@ class SparseLRTrainer:
             self.table.update(slot, g.contiguous(), self.rule, self.stats)
 
     def flush(self):
-        """Apply the deferred pushes of the last step (fused multi-GPU mode). Collective."""
+        """Apply the deferred pushes of the last step (fused / padded multi-GPU modes).
+        Collective."""
+        if self.padded:
+            if self.xc is not None:
+                self._x_flush()
+            return
         if not self.fused or self.pending is None:
             return
         slot_p, send_p, recv_p, g_p = self.pending

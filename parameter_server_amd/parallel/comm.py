@@ -32,6 +32,13 @@ class Comm:
     def all_to_all_v(self, send: torch.Tensor, send_counts, recv_counts) -> torch.Tensor:
         return send
 
+    def all_to_all_fixed(self, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
+        """Equal-split all-to-all into a preallocated ``recv`` (chunk p of ``send`` goes
+        to rank p). No host-side sizes, so it can sit between graph replays with no
+        device->host sync."""
+        recv.copy_(send)
+        return recv
+
     def all_gather_counts(self, counts: torch.Tensor, to_host: bool = True) -> torch.Tensor:
         """[world, world] int64 matrix (row r = counts sent by rank r); on the host
         unless ``to_host=False`` (then the caller syncs when it needs the values)."""
@@ -102,6 +109,19 @@ class DistComm(Comm):
         self._sent += sent
         count_traffic("all_to_all", sent, got)
         return out
+
+    def all_to_all_fixed(self, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
+        assert send.numel() == recv.numel() and send.numel() % self.world == 0
+        if self.backend == "gloo" and send.is_cuda:  # rehearsal mode: staged through host
+            out = torch.empty(recv.shape, dtype=recv.dtype)
+            dist.all_to_all_single(out, send.cpu(), group=self.group)
+            recv.copy_(out)
+        else:
+            dist.all_to_all_single(recv, send, group=self.group)
+        b = send.numel() * send.element_size() * (self.world - 1) // self.world
+        self._sent += b
+        count_traffic("all_to_all_fixed", b, b)
+        return recv
 
     def all_gather_counts(self, counts: torch.Tensor, to_host: bool = True) -> torch.Tensor:
         c = counts.to(torch.int64).reshape(-1).contiguous()

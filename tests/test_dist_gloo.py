@@ -74,19 +74,20 @@ def _reference(cfg_kw, steps, world):
     return dict(zip(unmix(k, bits).tolist(), w.tolist()))
 
 
-@pytest.mark.parametrize("ff_bytes", [0, 3])
-def test_two_rank_training_matches_protocol_reference(tmp_path, ff_bytes):
+@pytest.mark.parametrize("ff_bytes,exchange,world", [(0, "padded", 2), (0, "exact", 2),
+                                                    (3, "padded", 2), (0, "padded", 3)])
+def test_two_rank_training_matches_protocol_reference(tmp_path, ff_bytes, exchange, world):
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
-                  fixing_float_bytes=ff_bytes)
-    res = _run(tmp_path, cfg_kw)
+                  fixing_float_bytes=ff_bytes, exchange=exchange)
+    res = _run(tmp_path, cfg_kw, world=world)
     merged = {}
     for r in res:
         st = r["state"]
         for k, w in zip(st["keys"].tolist(), st["w"].tolist()):
             assert k not in merged, "a key lives on exactly one shard"
             merged[k] = w
-    assert res[0]["progress"]["examples"] == res[1]["progress"]["examples"] == 2 * 4 * 128
-    ref = _reference(cfg_kw, 4, 2)
+    assert all(r["progress"]["examples"] == world * 4 * 128 for r in res)
+    ref = _reference(cfg_kw, 4, world)
     assert merged.keys() == ref.keys()
     tol = 1e-5 if ff_bytes == 0 else 2e-3
     worst = max(abs(merged[k] - ref[k]) for k in ref)
@@ -99,3 +100,11 @@ def test_two_rank_aggregate_mode(tmp_path):
                   l2=0.0)
     res = _run(tmp_path, cfg_kw, steps=2)
     assert all(r["progress"]["loss"] > 0 for r in res)
+
+
+def test_padded_exchange_overflow_is_loud(tmp_path):
+    """A per-peer capacity below the live key count must fail, not silently drop."""
+    cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15,
+                  exchange="padded", exchange_capacity=64)
+    with pytest.raises(Exception, match="overflow"):
+        _run(tmp_path, cfg_kw, steps=2)

@@ -57,10 +57,14 @@ def _gpu_worker(rank, world, port, out_dir, cfg_kw, steps, pipelined=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ff_bytes,pipelined", [(0, False), (3, False), (0, True)])
-def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes, pipelined):
+@pytest.mark.parametrize("ff_bytes,pipelined,exchange,localize",
+                         [(0, False, "padded", "sort"), (0, False, "exact", "sort"),
+                          (3, False, "padded", "sort"), (0, True, "padded", "sort"),
+                          (0, True, "exact", "sort"), (0, False, "padded", "hash")])
+def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes, pipelined, exchange,
+                                                 localize):
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
-                  fixing_float_bytes=ff_bytes)
+                  fixing_float_bytes=ff_bytes, exchange=exchange, localize=localize)
     port = _free_port()
     mp.spawn(_gpu_worker, args=(2, port, str(tmp_path), cfg_kw, 4, pipelined), nprocs=2,
              join=True)
@@ -76,9 +80,11 @@ def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes, pipelined):
     assert max(abs(merged[k] - ref[k]) for k in ref) < tol
 
 
-def test_bench_two_rank_rehearsal_json(tmp_path):
-    """bench.py's multi-GPU path (pipelined fused exchange) under torchrun, 2 ranks on
-    one GPU over gloo; checks the one-line JSON contract."""
+@pytest.mark.parametrize("exchange", ["padded", "exact"])
+def test_bench_two_rank_rehearsal_json(tmp_path, exchange):
+    """bench.py's multi-GPU path (padded: graph-replayed compute segments around the
+    exchanges; exact: pipelined count-sized exchange) under torchrun, 2 ranks on one
+    GPU over gloo; checks the one-line JSON contract."""
     import json
     import subprocess
 
@@ -86,7 +92,8 @@ def test_bench_two_rank_rehearsal_json(tmp_path):
     env = dict(os.environ, PSAMD_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus",
-           "2", "--steps", "4", "--warmup", "2", "--minibatch", "4096", "--num-features", "1e8"]
+           "2", "--steps", "4", "--warmup", "2", "--minibatch", "4096", "--num-features", "1e8",
+           "--exchange", exchange]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -94,3 +101,4 @@ def test_bench_two_rank_rehearsal_json(tmp_path):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 4 and out["config"]["global_batch"] == 8192
     assert out["value"] > 0 and 0.3 < out["train"]["loss"] < 1.0
+    assert out["config"]["hip_graph"] == (exchange == "padded")
