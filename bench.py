@@ -24,6 +24,10 @@ import time
 
 import torch
 
+# thread-local capture: the RCCL watchdog thread of ProcessGroupNCCL keeps querying its
+# events while a rank captures its compute segments; global mode would invalidate
+# the capture on such a call from another thread
+CAPTURE_MODE = "thread_local"
 METRIC = "examples/sec (whole node) sparse LR 10^9 feats at 1/2/4/8 MI355X"
 ALGO_NAMES = {"ftrl": "FTRL-proximal", "adagrad": "proximal AdaGrad", "sgd": "proximal SGD"}
 
@@ -98,14 +102,14 @@ def pipeline(tr, B, N, seed, keys, labels, device, args):
     gp, plans = [], []
     for i in range(2):  # t is even here: parity i <-> bufs[i]
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
             prep(i)
         gp.append(g)
         plan = []
         for kind, fn in segments(i):  # capture in order: a segment may bake in buffers
             if kind == "compute":     # the previous one of the same parity selected
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                     fn()
                 plan.append(g.replay)
             else:
@@ -144,6 +148,10 @@ def main():
     ap.add_argument("--exchange", default="padded", choices=["padded", "exact"],
                     help="N > 1: fixed-capacity sync-free exchange, or count-sized all-to-all-v")
     ap.add_argument("--fixing-float", type=int, default=0)
+    ap.add_argument("--emulate-peers", type=int, default=0,
+                    help="1 process: run the N-GPU padded step with N emulated peers over a "
+                         "loopback exchange (per-GPU device cost of the N-GPU step, no "
+                         "collectives); reported as n_gpus 1 with 'emulated_peers'")
     ap.add_argument("--progress", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check)")
     ap.add_argument("--trace", default="",
@@ -156,8 +164,12 @@ def main():
     from parameter_server_amd.parallel.comm import init_from_env
 
     comm, device = init_from_env("cpu" if args.cpu else "cuda")
+    if args.emulate_peers > 1 and comm.world == 1:
+        from parameter_server_amd.parallel.comm import LoopbackComm
+
+        comm = LoopbackComm(args.emulate_peers, device)
     G, rank = comm.world, comm.rank
-    if G != args.gpus and rank == 0:
+    if G != args.gpus and rank == 0 and not args.emulate_peers:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {G}", file=sys.stderr)
     B = args.minibatch
     N = int(args.num_features)
@@ -227,7 +239,7 @@ def main():
                 one_step()  # warm the side stream
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 one_step()
             run = g.replay
             run()
@@ -257,14 +269,16 @@ def main():
     prog = tr.progress(reset=True)
     tr.table.check_ok()
     occ, nnz = tr.table.census()
-    total_examples = G * B * args.steps
+    emulated = comm.backend == "loopback" if hasattr(comm, "backend") else False
+    n_ranks = 1 if emulated else G
+    total_examples = n_ranks * B * args.steps
     value = total_examples / dt
     if rank == 0:
         out = {
             "metric": METRIC,
             "value": value,
             "unit": "examples/sec",
-            "n_gpus": G,
+            "n_gpus": n_ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
@@ -277,13 +291,14 @@ def main():
             "config": {
                 "model": f"sparse logistic regression, {ALGO_NAMES.get(args.algo, args.algo)} "
                          f"L1=10 L2=1 (server-side), {N:.0e} hashed features",
-                "global_batch": G * B,
+                "global_batch": n_ranks * B,
                 "seq_len": 39,
                 "nnz_per_example": 39,
-                "parallelism": f"dp{G}+kvshard{G}",
+                "parallelism": f"dp{n_ranks}+kvshard{n_ranks}",
                 "consistency": args.consistency,
                 "table_slots_per_gpu": tr.table.capacity,
                 "hip_graph": graph_used,
+                "emulated_peers": G if emulated else None,
                 "exchange": (f"{args.exchange} (capacity {tr.xc.C} keys/peer/step)"
                              if tr.xc is not None else (args.exchange if G > 1 else None)),
             },
@@ -295,9 +310,9 @@ def main():
         from parameter_server_amd.utils import trace
 
         trace.dump(args.trace, rank)
-    if G > 1:
-        import torch.distributed as dist
+    import torch.distributed as dist
 
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

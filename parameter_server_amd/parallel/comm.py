@@ -70,6 +70,25 @@ class LocalComm(Comm):
         self.device = torch.device(device)
 
 
+class LoopbackComm(Comm):
+    """Emulated ``world``-rank group inside ONE process (rank 0): every exchange
+    returns the local buffer, so the rank also plays the owner of every peer's key
+    range. Used to measure on one GPU the per-rank device work of an N-GPU step
+    (G exchange rows, G per-source owner updates, the row-wise resolve) without
+    the collectives; a benchmarking aid, not a training mode."""
+
+    backend = "loopback"
+
+    def __init__(self, world: int, device="cpu"):
+        self.world = int(world)
+        self.rank = 0
+        self.device = torch.device(device)
+
+    def all_gather_counts(self, counts: torch.Tensor, to_host: bool = True) -> torch.Tensor:
+        m = counts.reshape(1, -1).expand(self.world, -1)
+        return m.cpu() if to_host else m
+
+
 class DistComm(Comm):
     """torch.distributed process group (nccl = RCCL on ROCm, or gloo on CPU)."""
 
