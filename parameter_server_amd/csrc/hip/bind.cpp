@@ -27,6 +27,10 @@ void xchg_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, cons
 void xchg_clear_counts(int32_t*, int, int64_t, bool, bool, hipStream_t);
 void xchg_unpack_w(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
                    int64_t, float*, hipStream_t);
+void xchg_ff_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
+                        int64_t, int, int64_t, int, uint64_t, const int64_t*, int32_t*, float*,
+                        hipStream_t);
+void xchg_ff_decode(const int32_t*, int, int64_t, int, int64_t, int, float*, hipStream_t);
 void kv_gather(const void*, int64_t, const int64_t*, int64_t, const int32_t*, float*, int,
                hipStream_t);
 void kv_set(void*, int64_t, const int64_t*, int64_t, const float*, const float*, const float*,
@@ -232,7 +236,7 @@ PYBIND11_MODULE(_hipops, m) {
     chk(out_slot, at::kLong, "out_slot");
     chk(out_w, at::kFloat, "out_w");
     check(kw == 1 || kw == 2, "kw must be 1 (u32 keys) or 2 (u64 keys)");
-    check(C > 0 && H >= 4 + C * (kw + 1) && H % 4 == 0, "bad exchange row geometry");
+    check(C > 0 && H >= 4 + C * kw + 1 && H % 4 == 0, "bad exchange row geometry");
     check(recv.numel() % H == 0, "recv is not a whole number of rows");
     const int G = (int)(recv.numel() / H);
     check(G >= 1 && G <= 64, "1..64 peers");
@@ -252,7 +256,7 @@ PYBIND11_MODULE(_hipops, m) {
     const int G = (int)off.numel() - 1;
     check(G >= 1 && G <= 64, "1..64 peers");
     check(kw == 1 || kw == 2, "kw must be 1 or 2");
-    check(C > 0 && H >= 4 + C * (kw + 1) && H % 4 == 0, "bad exchange row geometry");
+    check(C > 0 && H >= 4 + C * kw + 1 && H % 4 == 0, "bad exchange row geometry");
     check(send.numel() == G * H, "send must be [G * H]");
     psamd::xchg_pack_keys(ptr<uint64_t>(ukeys), ptr<int32_t>(n_uniq), ukeys.numel(),
                           ptr<int64_t>(off), G, C, kw, H, ptr<int32_t>(send),
@@ -272,6 +276,40 @@ PYBIND11_MODULE(_hipops, m) {
     if (pp) check(perm->numel() >= grad.numel(), "perm shorter than grad");
     psamd::xchg_pack_grads(ptr<float>(grad), pp, ptr<int32_t>(n_uniq), grad.numel(),
                            ptr<int64_t>(off), G, C, kw, H, ptr<int32_t>(send), cur_stream());
+  });
+  m.def("xchg_ff_pack_grads", [](Tensor grad, optional<Tensor> perm, Tensor n_uniq, Tensor off,
+                                 int64_t C, int kw, int64_t H, int nb, uint64_t seed,
+                                 optional<Tensor> step, Tensor send, Tensor gstage) {
+    chk(grad, at::kFloat, "grad");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(off, at::kLong, "off");
+    chk(send, at::kInt, "send");
+    chk(gstage, at::kFloat, "gstage");
+    const int G = (int)off.numel() - 1;
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(kw == 1 || kw == 2, "kw must be 1 or 2");
+    check(nb >= 1 && nb <= 7, "FixingFloat bytes in [1, 7]");
+    check(C > 0 && H >= 4 + C * kw + (C * nb + 3) / 4 && H % 4 == 0, "bad exchange row geometry");
+    check(send.numel() == G * H, "send must be [G * H]");
+    check(gstage.numel() >= G * C, "gstage < G*C");
+    const int32_t* pp = optr<int32_t>(perm, at::kInt, "perm");
+    if (pp) check(perm->numel() >= grad.numel(), "perm shorter than grad");
+    psamd::xchg_ff_pack_grads(ptr<float>(grad), pp, ptr<int32_t>(n_uniq), grad.numel(),
+                              ptr<int64_t>(off), G, C, kw, H, nb, seed,
+                              optr<int64_t>(step, at::kLong, "step"), ptr<int32_t>(send),
+                              ptr<float>(gstage), cur_stream());
+  });
+  m.def("xchg_ff_decode", [](Tensor recv, int64_t C, int kw, int64_t H, int nb, Tensor gin) {
+    chk(recv, at::kInt, "recv");
+    chk(gin, at::kFloat, "gin");
+    check(kw == 1 || kw == 2, "kw must be 1 or 2");
+    check(nb >= 1 && nb <= 7, "FixingFloat bytes in [1, 7]");
+    check(C > 0 && H >= 4 + C * kw + (C * nb + 3) / 4 && H % 4 == 0, "bad exchange row geometry");
+    check(recv.numel() % H == 0, "recv is not a whole number of rows");
+    const int G = (int)(recv.numel() / H);
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(gin.numel() >= G * C, "gin < G*C");
+    psamd::xchg_ff_decode(ptr<int32_t>(recv), G, C, kw, H, nb, ptr<float>(gin), cur_stream());
   });
   m.def("xchg_clear_counts", [](Tensor send, int64_t H, bool keys, bool grads) {
     chk(send, at::kInt, "send");

@@ -9,12 +9,13 @@
 // all-to-all -> unpack) runs without a host round trip and replays from HIP
 // graphs between the collectives.
 //
-// Row p of the send buffer (H words, H >= 4 + C * (kw + 1)):
+// Row p of the send buffer (H words, H >= 4 + C * kw + gradient words):
 //   [0] nkeys   keys of this step owned by rank p (<= C)
 //   [1] ngrads  gradients of the previous step's keys for rank p (<= C)
-//   [2..3]      padding (keeps the key region 16-B aligned)
-//   [4, 4 + C*kw)          keys: u32 (kw = 1, mixed key space <= 32 bits) or u64
-//   [4 + C*kw, 4 + C*kw + C) gradients (f32 bit patterns)
+//   [2..3]      FixingFloat min / max of the row's gradients, else padding (keeps
+//               the key region 16-B aligned)
+//   [4, 4 + C*kw)  keys: u32 (kw = 1, mixed key space <= 32 bits) or u64
+//   [4 + C*kw, ..) gradients: C f32 bit patterns, or C nb-byte FixingFloat codes
 // The unique keys of a step are owner-ordered (sorted mixed keys, or the owner
 // bucketing of a hash localisation with `perm` = owner-order -> unique id), and
 // off[G+1] (device) are the owner run offsets. Keys past C in a run are dropped
@@ -148,6 +149,140 @@ void xchg_unpack_w(const float* recv_w, const int32_t* perm, const int32_t* n_un
                    hipStream_t st) {
   xchg_unpack_w_kernel<<<grid_for(n_host, 256), 256, 0, st>>>(recv_w, perm, n_uniq, n_host, off,
                                                                G, C, w_local);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// FixingFloat on the padded exchange (reference src/filter/fixing_float.h:44-95,
+// enabled per push by async_sgd.h:273-277): the gradient region of row p carries
+// ceil(C * nb / 4) words of nb-byte fixed-point codes; header words [2], [3] hold
+// the row's min / max as order-preserving ints (max gets +1e-6 when decoded, as
+// the reference does). Stochastic rounding draws from a counter RNG keyed by
+// (seed, device step clock, row, index), so graph replays draw fresh bits.
+__device__ __forceinline__ int ff_ord(float f) {
+  const int b = __float_as_int(f);
+  return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float ff_unord(int b) {
+  return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff);
+}
+
+__global__ void xchg_ff_init_kernel(int32_t* __restrict__ send, int G, int64_t H) {
+  if (threadIdx.x < G) {
+    send[(int64_t)threadIdx.x * H + 2] = ff_ord(3.4e38f);
+    send[(int64_t)threadIdx.x * H + 3] = ff_ord(-3.4e38f);
+  }
+}
+
+// Stage grad(t) in owner order into gstage[p*C + i] and reduce each row's min/max.
+__global__ void xchg_ff_stage_kernel(const float* __restrict__ grad,
+                                     const int32_t* __restrict__ perm,
+                                     const int32_t* __restrict__ n_uniq, int64_t n_host,
+                                     const int64_t* __restrict__ off, int G, int64_t C, int64_t H,
+                                     int32_t* __restrict__ send, float* __restrict__ gstage) {
+  __shared__ int64_t soff[kMaxPeers + 1];
+  load_offsets(off, G, soff);
+  if (blockIdx.x == 0 && threadIdx.x < G) {
+    const int p = threadIdx.x;
+    const int64_t cnt = soff[p + 1] - soff[p];
+    send[(int64_t)p * H + 1] = (int32_t)(cnt < C ? cnt : C);
+  }
+  const int64_t n = dev_len(n_uniq, n_host);
+  const int lane = threadIdx.x & 63;
+  for (int64_t j0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); j0 < n;
+       j0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = j0 + lane;
+    int p = -1;
+    float lo = 3.4e38f, hi = -3.4e38f;
+    if (j < n) {
+      p = owner_of_pos(soff, G, j);
+      const int64_t i = j - soff[p];
+      if (i < C) {
+        const int64_t u = perm ? (int64_t)perm[j] : j;
+        const float g = in_range(u, n_host) ? grad[u] : 0.f;
+        gstage[(int64_t)p * C + i] = g;
+        if (g == g) { lo = g; hi = g; }
+      } else {
+        p = -1;
+      }
+    }
+    const int p0 = __shfl(p, 0, 64);
+    const bool uniform = __ballot(p != p0) == 0ull;
+    if (uniform) {  // the common case: the whole wave is in one owner's run
+      lo = wave_min(lo);
+      hi = wave_max(hi);
+      if (lane == 0 && p0 >= 0) {
+        atomicMin(&send[(int64_t)p0 * H + 2], ff_ord(lo));
+        atomicMax(&send[(int64_t)p0 * H + 3], ff_ord(hi));
+      }
+    } else if (p >= 0) {
+      atomicMin(&send[(int64_t)p * H + 2], ff_ord(lo));
+      atomicMax(&send[(int64_t)p * H + 3], ff_ord(hi));
+    }
+  }
+}
+
+__global__ void xchg_ff_encode_kernel(const float* __restrict__ gstage, int64_t C, int kw,
+                                      int64_t H, int nb, uint64_t seed,
+                                      const int64_t* __restrict__ step,
+                                      int32_t* __restrict__ send) {
+  const int p = blockIdx.y;
+  int32_t* row = send + (int64_t)p * H;
+  const int64_t n = dev_len(row + 1, C);
+  const float lo = ff_unord(row[2]), hi = ff_unord(row[3]) + 1e-6f;
+  const double bin = (double)hi - (double)lo;
+  const double ratio = (double)((1ull << (8 * nb)) - 2ull);
+  const uint64_t sd = fmix64(seed ^ fmix64((step ? (uint64_t)*step : 0ull) * 0x9e3779b97f4a7c15ull +
+                                           (uint64_t)p));
+  uint8_t* code = reinterpret_cast<uint8_t*>(row + 4 + C * kw);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v = gstage[(int64_t)p * C + i];
+    v = v > hi ? hi : (v < lo ? lo : v);
+    const double t = bin > 0 ? ((double)v - lo) / bin * ratio : 0.0;
+    const double f = floor(t);
+    const double u = (double)u01(rng64(sd, (uint64_t)i)) - 1e-12;
+    uint64_t r = (uint64_t)f + ((t - f) > u ? 1ull : 0ull);
+    for (int b = 0; b < nb; ++b) { code[i * nb + b] = (uint8_t)(r & 0xff); r >>= 8; }
+  }
+}
+
+// Owner: codes of every source row -> gin[s*C + i] (f32), in front of the updates.
+__global__ void xchg_ff_decode_kernel(const int32_t* __restrict__ recv, int64_t C, int kw,
+                                      int64_t H, int nb, float* __restrict__ gin) {
+  const int s = blockIdx.y;
+  const int32_t* row = recv + (int64_t)s * H;
+  const int64_t n = dev_len(row + 1, C);
+  const float lo = ff_unord(row[2]), hi = ff_unord(row[3]) + 1e-6f;
+  const double bin = (double)hi - (double)lo;
+  const double ratio = (double)((1ull << (8 * nb)) - 2ull);
+  const uint8_t* code = reinterpret_cast<const uint8_t*>(row + 4 + C * kw);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t r = 0;
+    for (int b = 0; b < nb; ++b) r |= (uint64_t)code[i * nb + b] << (8 * b);
+    gin[(int64_t)s * C + i] = (float)((double)r / ratio * bin + lo);
+  }
+}
+
+void xchg_ff_pack_grads(const float* grad, const int32_t* perm, const int32_t* n_uniq,
+                        int64_t n_host, const int64_t* off, int G, int64_t C, int kw, int64_t H,
+                        int nb, uint64_t seed, const int64_t* step, int32_t* send, float* gstage,
+                        hipStream_t st) {
+  xchg_ff_init_kernel<<<1, 64, 0, st>>>(send, G, H);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  xchg_ff_stage_kernel<<<grid_for(n_host, 256), 256, 0, st>>>(grad, perm, n_uniq, n_host, off, G,
+                                                               C, H, send, gstage);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  dim3 grid(grid_for(C, 256, 512), G);
+  xchg_ff_encode_kernel<<<grid, 256, 0, st>>>(gstage, C, kw, H, nb, seed, step, send);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void xchg_ff_decode(const int32_t* recv, int G, int64_t C, int kw, int64_t H, int nb, float* gin,
+                    hipStream_t st) {
+  dim3 grid(grid_for(C, 256, 512), G);
+  xchg_ff_decode_kernel<<<grid, 256, 0, st>>>(recv, C, kw, H, nb, gin);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -11,14 +11,19 @@ One training step on a rank (all on the GPU, no host round trip when G == 1):
   localise      mix -> radix sort -> RLE  (unique keys, local cols, CSC order)
   [tail filter] CountMin insert/query of per-key counts, drop rare keys
   pull          G == 1: lookup-or-insert in the local HBM table;
-                G  > 1: keys are already sorted by owner -> count exchange ->
-                all-to-all-v of keys -> owner lookup -> all-to-all-v of weights
+                G  > 1 (exchange="padded", default): keys are sorted by owner ->
+                fixed-capacity row per peer [keys(t) | grads(t-1)] with the
+                counts in the row header -> equal-split all-to-all -> owner applies
+                the pushes of t-1, then resolves the pulls of t -> all-to-all of
+                weights. No host sync, so the step replays from HIP graphs between
+                the two collectives (exchange="exact": count all-gather + sized
+                all-to-all-v, one host sync per step)
   forward       Xw, loss, dL/dXw, accuracy, AUC histogram (one kernel)
   backward      segmented reduction over the CSC order -> grad per unique key
   push          G == 1: optimizer update at the cached slots (key caching: the
                 push never re-sends or re-hashes keys);
-                G  > 1: all-to-all-v of gradients [FixingFloat-compressed] ->
-                owner applies one optimizer step per source segment in rank
+                G  > 1: gradients ride the next step's exchange [FixingFloat nb-byte
+                codes] -> owner applies one optimizer step per source row in rank
                 order (reference semantics: one FTRL step per push message) or
                 sums them first (``push_mode='aggregate'``, synchronous SGD).
 """
@@ -119,9 +124,9 @@ class SparseLRTrainer:
         # multi-GPU: fuse push(t-1) into the pull exchange of step t (2 all-to-alls/step)
         if cfg.exchange not in ("padded", "exact"):
             raise ValueError(f"exchange must be 'padded' or 'exact', not {cfg.exchange!r}")
-        self.fused = self.G > 1 and self.filter is None and cfg.fixing_float_bytes == 0
-        self.padded = self.fused and cfg.exchange == "padded"
-        self.fused = self.fused and not self.padded
+        self.padded = self.G > 1 and self.filter is None and cfg.exchange == "padded"
+        self.fused = (self.G > 1 and self.filter is None and cfg.fixing_float_bytes == 0
+                      and not self.padded)
         self.xc = None  # padded-exchange state (allocated on the first step)
         self.pending = None
         self._prefetch = None
@@ -283,10 +288,14 @@ class SparseLRTrainer:
             C = int(math.ceil(float(cnt.item()) * cfg.exchange_slack)) + 1024
         C = min(max(64, (C + 63) // 64 * 64), max(64, self.max_nnz))
         kw = 1 if self.bits <= 32 else 2
-        H = (4 + C * (kw + 1) + 3) // 4 * 4
+        nb = int(cfg.fixing_float_bytes)  # FixingFloat: nb-byte codes instead of f32
+        gw = (C * nb + 3) // 4 if nb else C
+        H = (4 + C * kw + gw + 3) // 4 * 4
         z32 = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
         self.xc = SimpleNamespace(
-            C=C, kw=kw, H=H,
+            C=C, kw=kw, H=H, nb=nb,
+            gstage=z32(G * C, torch.float32) if nb else None,
+            gin=z32(G * C, torch.float32) if nb else None,
             send=z32(G * H, torch.int32), recv=z32(G * H, torch.int32),
             slot=torch.full((G * C,), -1, dtype=torch.int64, device=dev),
             wsend=z32(G * C, torch.float32), wrecv=z32(G * C, torch.float32),
@@ -329,21 +338,24 @@ class SparseLRTrainer:
         xc, G, H, C, kw = self.xc, self.G, self.xc.H, self.xc.C, self.xc.kw
         g0 = 4 + C * kw
         rows = [xc.recv[s * H:(s + 1) * H] for s in range(G)]
+        if xc.nb:  # FixingFloat codes -> f32, one launch for all source rows
+            self._x_ff_decode()
+            grads = [xc.gin[s * C:(s + 1) * C] for s in range(G)]
+        else:
+            grads = [rows[s][g0:g0 + C].view(torch.float32) for s in range(G)]
         if self.gpu:
             hh = hipops()
             if self.cfg.push_mode == "aggregate":
                 xc.n_touched.zero_()
                 for s in range(G):
-                    hh.kv_accumulate(self.table.slots, xc.slot[s * C:(s + 1) * C],
-                                     rows[s][g0:g0 + C].view(torch.float32), rows[s][1:2],
-                                     xc.touched, xc.n_touched)
+                    hh.kv_accumulate(self.table.slots, xc.slot[s * C:(s + 1) * C], grads[s],
+                                     rows[s][1:2], xc.touched, xc.n_touched)
                 hh.kv_apply_accumulated(self.table.slots, xc.touched, xc.n_touched,
                                         *self.rule.args(), self.stats)
             else:
                 for s in range(G):
-                    hh.kv_update(self.table.slots, xc.slot[s * C:(s + 1) * C],
-                                 rows[s][g0:g0 + C].view(torch.float32), rows[s][1:2],
-                                 *self.rule.args(), self.stats)
+                    hh.kv_update(self.table.slots, xc.slot[s * C:(s + 1) * C], grads[s],
+                                 rows[s][1:2], *self.rule.args(), self.stats)
             if resolve:
                 it, iv, isd, seed = self.table.init.args()
                 hh.kv_resolve_rows(self.table.slots, xc.recv, H, C, kw, xc.slot, xc.wsend, True,
@@ -354,7 +366,7 @@ class SparseLRTrainer:
         for s in range(G):
             ng = int(rows[s][1])
             if ng:
-                parts.append((xc.slot[s * C:s * C + ng], rows[s][g0:g0 + ng].view(torch.float32)))
+                parts.append((xc.slot[s * C:s * C + ng], grads[s][:ng]))
         self._apply_pushes(parts)
         if not resolve:
             return
@@ -387,7 +399,9 @@ class SparseLRTrainer:
                                     coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
         grad, _ = linear_backward(loc, coef, B=B, width=width or 0, rows=rows, vals=vals)
         H, C, kw = xc.H, xc.C, xc.kw
-        if self.gpu:
+        if xc.nb:
+            self._x_ff_pack(grad[:loc.uniq.numel()], perm, n_uniq, off)
+        elif self.gpu:
             hipops().xchg_pack_grads(grad[:loc.uniq.numel()], perm, n_uniq, off, C, kw, H,
                                      xc.send)
         else:
@@ -397,6 +411,39 @@ class SparseLRTrainer:
                 g0 = p * H + 4 + C * kw
                 xc.send[g0:g0 + c] = grad[a:a + c].contiguous().view(torch.int32)
         auc_from_hist(self.hist, self.metrics, self.step_dev)
+
+    def _x_ff_pack(self, grad, perm, n_uniq, off):
+        """FixingFloat push (reference fixing_float.h:44-95): per owner row min/max,
+        nb-byte stochastic-rounded codes; the device step clock varies the rounding
+        bits across graph replays."""
+        xc, H, C, kw, nb = self.xc, self.xc.H, self.xc.C, self.xc.kw, self.xc.nb
+        seed = (self.cfg.seed * 7919 + 17) & ((1 << 64) - 1)
+        if self.gpu:
+            hipops().xchg_ff_pack_grads(grad, perm, n_uniq, off, C, kw, H, nb, seed,
+                                        self.step_dev, xc.send, xc.gstage)
+            return
+        for p in range(self.G):
+            a, c = int(off[p]), min(int(off[p + 1] - off[p]), C)
+            xc.send[p * H + 1] = c
+            g = grad[a:a + c]
+            code, mm = ff.encode(g, nb, seed=seed + 1000003 * self.step_count + p)
+            xc.send[p * H + 2:p * H + 4] = mm.view(torch.int32)
+            g0 = p * H + 4 + C * kw
+            words = xc.send[g0:g0 + (C * nb + 3) // 4].view(torch.uint8)
+            words[:code.numel()] = code
+
+    def _x_ff_decode(self):
+        xc, H, C, kw, nb = self.xc, self.xc.H, self.xc.C, self.xc.kw, self.xc.nb
+        if self.gpu:
+            hipops().xchg_ff_decode(xc.recv, C, kw, H, nb, xc.gin)
+            return
+        for s in range(self.G):
+            row = xc.recv[s * H:(s + 1) * H]
+            n = int(row[1])
+            if n:
+                g0 = 4 + C * kw
+                code = row[g0:g0 + (C * nb + 3) // 4].view(torch.uint8)[:n * nb]
+                xc.gin[s * C:s * C + n] = ff.decode(code, nb, row[2:4].view(torch.float32), n)
 
     def _x_flush(self):
         """Apply the gradients packed by the last step (a keys-free exchange)."""

@@ -75,7 +75,8 @@ def _reference(cfg_kw, steps, world):
 
 
 @pytest.mark.parametrize("ff_bytes,exchange,world", [(0, "padded", 2), (0, "exact", 2),
-                                                    (3, "padded", 2), (0, "padded", 3)])
+                                                    (3, "padded", 2), (3, "exact", 2),
+                                                    (0, "padded", 3), (2, "padded", 3)])
 def test_two_rank_training_matches_protocol_reference(tmp_path, ff_bytes, exchange, world):
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
                   fixing_float_bytes=ff_bytes, exchange=exchange)

@@ -59,7 +59,8 @@ def _gpu_worker(rank, world, port, out_dir, cfg_kw, steps, pipelined=False):
 
 @pytest.mark.parametrize("ff_bytes,pipelined,exchange,localize",
                          [(0, False, "padded", "sort"), (0, False, "exact", "sort"),
-                          (3, False, "padded", "sort"), (0, True, "padded", "sort"),
+                          (3, False, "padded", "sort"), (3, False, "exact", "sort"),
+                          (0, True, "padded", "sort"),
                           (0, True, "exact", "sort"), (0, False, "padded", "hash")])
 def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes, pipelined, exchange,
                                                  localize):
