@@ -148,6 +148,7 @@ def main():
     ap.add_argument("--exchange", default="padded", choices=["padded", "exact"],
                     help="N > 1: fixed-capacity sync-free exchange, or count-sized all-to-all-v")
     ap.add_argument("--fixing-float", type=int, default=0)
+    ap.add_argument("--localize", default="sort", choices=["sort", "tile", "hash", "bucket", "auto"])
     ap.add_argument("--emulate-peers", type=int, default=0,
                     help="1 process: run the N-GPU padded step with N emulated peers over a "
                          "loopback exchange (per-GPU device cost of the N-GPU step, no "
@@ -178,6 +179,7 @@ def main():
     cfg = SparseLRConfig(num_features=N, minibatch=B, algo=args.algo, lr_type="decay",
                          alpha=0.01, beta=10.0, l1=10.0, l2=1.0, consistency=args.consistency,
                          fixing_float_bytes=args.fixing_float, exchange=args.exchange,
+                         localize=args.localize,
                          seed=rank)
     tr = SparseLRTrainer(cfg, comm, device)
     keys = torch.empty(B * 39, dtype=torch.int64, device=device)
@@ -298,6 +300,7 @@ def main():
                 "consistency": args.consistency,
                 "table_slots_per_gpu": tr.table.capacity,
                 "hip_graph": graph_used,
+                "localize": tr.localize_mode,
                 "emulated_peers": G if emulated else None,
                 "exchange": (f"{args.exchange} (capacity {tr.xc.C} keys/peer/step)"
                              if tr.xc is not None else (args.exchange if G > 1 else None)),

@@ -31,7 +31,7 @@ def t(fn, it=50):
     return s.elapsed_time(e) / it * 1e3
 
 
-for mode in os.environ.get("PSAMD_LOC_MODES", "sort,bucket,hash").split(","):
+for mode in os.environ.get("PSAMD_LOC_MODES", "sort,tile,hash").split(","):
     L = Localizer(B * 39, 30, "cuda", mode=mode)
     loc = L(keys)
     us_loc = t(lambda: L(keys))

@@ -19,6 +19,15 @@ void kv_resolve(void*, int64_t, const uint64_t*, int64_t, const int32_t*, int64_
 void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int, int64_t*, float*,
                      bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t,
                      hipStream_t);
+// tileloc.hip
+int64_t tileloc_stride(int64_t);
+size_t tileloc_sort_temp_bytes(int64_t);
+void localize_tile(const uint64_t*, int64_t, KeyMix, int, uint32_t*, int32_t*, uint16_t*, int32_t*,
+                   void*, size_t, uint32_t*, int32_t*, int32_t*, uint64_t*, int32_t*, int32_t*,
+                   int32_t*, int32_t*, float*, hipStream_t);
+void tile_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
+                   const float*, int64_t, float*, const int32_t*, const int32_t*, const int32_t*,
+                   float*, int64_t, hipStream_t);
 // exchange.hip
 void xchg_pack_keys(const uint64_t*, const int32_t*, int64_t, const int64_t*, int, int64_t, int,
                     int64_t, int32_t*, int32_t*, hipStream_t);
@@ -225,6 +234,62 @@ PYBIND11_MODULE(_hipops, m) {
      py::arg("out_w"), py::arg("insert"), py::arg("init_type"), py::arg("init_v"),
      py::arg("init_s"), py::arg("seed"), py::arg("err"), py::arg("inserted"),
      py::arg("home_base") = 0, py::arg("home_m") = 0);
+  // ---------------- tile-deduplicating localisation (tileloc.hip) ----------------
+  m.def("tileloc_stride", [](int64_t n) { return psamd::tileloc_stride(n); });
+  m.def("tileloc_sort_temp_bytes", [](int64_t n) { return (int64_t)psamd::tileloc_sort_temp_bytes(n); });
+  m.def("localize_tile", [](Tensor keys, int bits, int digit_bits, Tensor dkeys, Tensor dcnt,
+                            Tensor rep, Tensor n_ent, Tensor sort_temp, Tensor hs, Tensor pos_s,
+                            Tensor segid, Tensor uniq, Tensor seg_start, Tensor ent_uid,
+                            Tensor local_col, Tensor n_uniq, Tensor grad) {
+    chk(keys, at::kLong, "keys");
+    const int64_t n = keys.numel();
+    check(n > 0, "empty minibatch");
+    check(bits >= 2 && bits <= 31, "tile localisation needs 2..31 key bits");
+    const int64_t N = psamd::tileloc_stride(n);
+    const int64_t T = N / 4096;
+    for (auto* t : {&dkeys, &dcnt, &n_ent, &hs, &pos_s, &segid, &seg_start, &ent_uid, &local_col,
+                    &n_uniq})
+      chk(*t, at::kInt, "int32 buffer");
+    chk(rep, at::kShort, "rep");
+    chk(uniq, at::kLong, "uniq");
+    chk(grad, at::kFloat, "grad");
+    chk(sort_temp, at::kByte, "sort_temp");
+    check(dkeys.numel() >= N && hs.numel() >= N && pos_s.numel() >= N && segid.numel() >= N &&
+          uniq.numel() >= N && seg_start.numel() >= N + 1 && ent_uid.numel() >= N &&
+          grad.numel() >= N, "tile localisation buffers < stride");
+    check(dcnt.numel() >= T && rep.numel() >= n && local_col.numel() >= n, "tile buffers too small");
+    check((size_t)sort_temp.numel() >= psamd::tileloc_sort_temp_bytes(n), "sort_temp too small");
+    psamd::localize_tile(ptr<uint64_t>(keys), n, make_keymix(bits), digit_bits, ptr<uint32_t>(dkeys),
+                         ptr<int32_t>(dcnt), ptr<uint16_t>(rep), ptr<int32_t>(n_ent),
+                         sort_temp.data_ptr(), sort_temp.numel(), ptr<uint32_t>(hs),
+                         ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<uint64_t>(uniq),
+                         ptr<int32_t>(seg_start), ptr<int32_t>(ent_uid), ptr<int32_t>(local_col),
+                         ptr<int32_t>(n_uniq), ptr<float>(grad), cur_stream());
+  });
+  m.def("tile_backward", [](Tensor rep, Tensor dcnt, int64_t n, optional<Tensor> rows, int width,
+                            optional<Tensor> vals, Tensor coef, Tensor psum, Tensor pos_s,
+                            Tensor segid, Tensor n_ent, Tensor grad) {
+    chk(rep, at::kShort, "rep");
+    chk(dcnt, at::kInt, "dcnt");
+    chk(coef, at::kFloat, "coef");
+    chk(psum, at::kFloat, "psum");
+    chk(pos_s, at::kInt, "pos_s");
+    chk(segid, at::kInt, "segid");
+    chk(n_ent, at::kInt, "n_ent");
+    chk(grad, at::kFloat, "grad");
+    const int64_t N = psamd::tileloc_stride(n);
+    check(n > 0 && rep.numel() >= n, "rep too small");
+    check(dcnt.numel() >= N / 4096 && psum.numel() >= N && pos_s.numel() >= N &&
+          segid.numel() >= N, "tile backward buffers < stride");
+    const int32_t* r = optr<int32_t>(rows, at::kInt, "rows");
+    if (r) check(rows->numel() >= n, "rows too small");
+    else check(width > 0, "need rows or a fixed width");
+    const float* v = optr<float>(vals, at::kFloat, "vals");
+    if (v) check(vals->numel() >= n, "vals too small");
+    psamd::tile_backward(ptr<uint16_t>(rep), ptr<int32_t>(dcnt), n, r, width, v, ptr<float>(coef),
+                         coef.numel(), ptr<float>(psum), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
+                         ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), cur_stream());
+  });
   // ---------------- fixed-capacity exchange (exchange.hip) ----------------
   // buffers: send/recv int32 [G * H]; row layout documented in exchange.hip
   m.def("kv_resolve_rows", [](Tensor slots, Tensor recv, int64_t H, int64_t C, int kw,

@@ -176,7 +176,7 @@ hl_backward_kernel(const int32_t* __restrict__ local_col, int64_t n, int width,
     const int64_t c1 = min(n, c0 + kBwdChunk);
     for (int64_t i = c0 + threadIdx.x; i < c1; i += kBlk) {
       const int32_t u = local_col[i];
-      const int64_t r = rows ? rows[i] : i / width;
+      const int64_t r = rows ? (int64_t)rows[i] : (int64_t)((uint32_t)i / (uint32_t)width);
       if (!in_range(u, U) || !in_range(r, B)) continue;
       const float g = coef[r] * (vals ? vals[i] : 1.f);
       const int e = (int)(((uint32_t)u * 0x9E3779B1u) >> 20);  // 12-bit index

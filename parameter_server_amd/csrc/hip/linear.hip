@@ -134,7 +134,7 @@ linear_bwd_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__
       s = segid[i];
       const int32_t p = pos_s[i];
       if (in_range(p, n)) {
-        const int32_t r = rows ? rows[p] : p / width;
+        const int32_t r = rows ? rows[p] : (int32_t)((uint32_t)p / (uint32_t)width);
         if (in_range(r, B)) {
           const float x = vals ? vals[p] : 1.f;
           v = coef[r] * x;

@@ -57,18 +57,34 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* ld
   return r;
 }
 
+// Device-side element counts (n_dev): a launch sized for n_host keys only works
+// on the first ceil(n/kTile) tiles; per-tile arrays (histogram columns, tile
+// partials) use that live tile count as their stride, so later kernels and the
+// scans never touch the unused tail. n_dev == nullptr: host n, as before.
+__device__ __forceinline__ int64_t live_tiles(const int32_t* n_dev, int64_t n_host,
+                                              int64_t T_host) {
+  if (!n_dev) return T_host;
+  return (dev_len(n_dev, n_host) + kTile - 1) / kTile;
+}
+
 // ---------------------------------------------------------------- histogram
 template <bool kMix, int kBits>
 __global__ void __launch_bounds__(kBlk)
-hist32_kernel(const uint64_t* __restrict__ raw, const uint32_t* __restrict__ keys, int64_t n,
+hist32_kernel(const uint64_t* __restrict__ raw, const uint32_t* __restrict__ keys, int64_t n_host,
               KeyMix m, uint32_t* __restrict__ mixed_out, int shift, uint32_t* __restrict__ hist,
-              int64_t T) {
+              int64_t T_host, const int32_t* __restrict__ n_dev,
+              const int32_t* __restrict__ tile_cnt) {
   constexpr int kDigits = 1 << kBits;
+  const int64_t n = dev_len(n_dev, n_host);
+  const int64_t T = live_tiles(n_dev, n_host, T_host);
+  if ((int64_t)blockIdx.x >= T) return;
   __shared__ uint32_t cnt[kDigits];
   for (int d = threadIdx.x; d < kDigits; d += kBlk) cnt[d] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kTile;
-  if (!kMix && base + kTile <= n) {
+  // ragged input (tile_cnt): tile b holds tile_cnt[b] keys at [b*kTile, ...)
+  const int64_t lim = tile_cnt ? base + min(kTile, max(0, tile_cnt[blockIdx.x])) : n;
+  if (!kMix && base + kTile <= lim) {
     // full tile: 16-byte loads, 4 keys per load, 4 loads per thread
     const uint4* kv = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
@@ -80,10 +96,10 @@ hist32_kernel(const uint64_t* __restrict__ raw, const uint32_t* __restrict__ key
       atomicAdd(&cnt[(q.w >> shift) & (kDigits - 1)], 1u);
     }
   } else {
-#pragma unroll 4
+#pragma unroll
     for (int j = 0; j < kItems; ++j) {
       const int64_t i = base + j * kBlk + threadIdx.x;
-      if (i < n) {
+      if (i < lim) {
         uint32_t k;
         if (kMix) {
           k = (uint32_t)mix_key(raw[i], m);
@@ -105,8 +121,20 @@ hist32_kernel(const uint64_t* __restrict__ raw, const uint32_t* __restrict__ key
 // values), then scans its chunk. No single-block serial phase, no spinning.
 constexpr int kScanChunk = 2048;
 
+// n_dev: the scanned array holds live_tiles(n_dev) * per_tile entries.
+__device__ __forceinline__ int64_t scan_len(int64_t n_host, const int32_t* n_dev, int64_t n_items,
+                                            int64_t per_tile) {
+  if (!n_dev) return n_host;
+  const int64_t v = live_tiles(n_dev, n_items, 0) * per_tile;
+  return v < n_host ? v : n_host;
+}
+
 __global__ void __launch_bounds__(kBlk) chunk_sum_kernel(const uint32_t* __restrict__ a,
-                                                         int64_t n, uint32_t* __restrict__ part) {
+                                                         int64_t n_host, uint32_t* __restrict__ part,
+                                                         const int32_t* __restrict__ n_dev,
+                                                         int64_t n_items, int64_t per_tile) {
+  const int64_t n = scan_len(n_host, n_dev, n_items, per_tile);
+  if ((int64_t)blockIdx.x * kScanChunk >= n) return;
   __shared__ uint32_t lds[kWaves + 1];
   const int64_t base = (int64_t)blockIdx.x * kScanChunk;
   uint32_t s = 0;
@@ -120,8 +148,12 @@ __global__ void __launch_bounds__(kBlk) chunk_sum_kernel(const uint32_t* __restr
   if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
-__global__ void __launch_bounds__(kBlk) chunk_scan_kernel(uint32_t* __restrict__ a, int64_t n,
-                                                          const uint32_t* __restrict__ part) {
+__global__ void __launch_bounds__(kBlk) chunk_scan_kernel(uint32_t* __restrict__ a, int64_t n_host,
+                                                          const uint32_t* __restrict__ part,
+                                                          const int32_t* __restrict__ n_dev,
+                                                          int64_t n_items, int64_t per_tile) {
+  const int64_t n = scan_len(n_host, n_dev, n_items, per_tile);
+  if ((int64_t)blockIdx.x * kScanChunk >= n) return;
   __shared__ uint32_t tile[kScanChunk];
   __shared__ uint32_t lds[kWaves + 1];
   // prefix of earlier chunks
@@ -152,11 +184,12 @@ __global__ void __launch_bounds__(kBlk) chunk_scan_kernel(uint32_t* __restrict__
   }
 }
 
-void scan2_u32(uint32_t* a, int64_t n, uint32_t* part, hipStream_t st) {
+void scan2_u32(uint32_t* a, int64_t n, uint32_t* part, hipStream_t st,
+               const int32_t* n_dev = nullptr, int64_t n_items = 0, int64_t per_tile = 1) {
   const int64_t chunks = (n + kScanChunk - 1) / kScanChunk;
-  chunk_sum_kernel<<<(unsigned)chunks, kBlk, 0, st>>>(a, n, part);
+  chunk_sum_kernel<<<(unsigned)chunks, kBlk, 0, st>>>(a, n, part, n_dev, n_items, per_tile);
   PSAMD_HIP_CHECK(hipGetLastError());
-  chunk_scan_kernel<<<(unsigned)chunks, kBlk, 0, st>>>(a, n, part);
+  chunk_scan_kernel<<<(unsigned)chunks, kBlk, 0, st>>>(a, n, part, n_dev, n_items, per_tile);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
@@ -164,9 +197,13 @@ void scan2_u32(uint32_t* a, int64_t n, uint32_t* part, hipStream_t st) {
 template <int kBits>
 __global__ void __launch_bounds__(kBlk)
 scatter32_kernel(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in,
-                 uint32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t n,
-                 int shift, const uint32_t* __restrict__ offs, int64_t T) {
+                 uint32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t n_host,
+                 int shift, const uint32_t* __restrict__ offs, int64_t T_host,
+                 const int32_t* __restrict__ n_dev, const int32_t* __restrict__ tile_cnt) {
   constexpr int kDigits = 1 << kBits;
+  const int64_t n = dev_len(n_dev, n_host);
+  const int64_t T = live_tiles(n_dev, n_host, T_host);
+  if ((int64_t)blockIdx.x >= T) return;
   constexpr int kDPT = kDigits / kBlk;  // digits per thread in the offset scan
   __shared__ uint32_t skeys[kTile];
   __shared__ int32_t svals[kTile];
@@ -175,23 +212,30 @@ scatter32_kernel(const uint32_t* __restrict__ keys_in, const int32_t* __restrict
   __shared__ uint32_t lds[kWaves + 1];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t base = (int64_t)blockIdx.x * kTile;
-  const int tile_n = (int)min((int64_t)kTile, n - base);
+  const int tile_n = tile_cnt ? min(kTile, max(0, tile_cnt[blockIdx.x]))
+                              : (int)min((int64_t)kTile, n - base);
   for (int f = t; f < kWaves * kDigits; f += kBlk) wcnt[f] = 0;
   __syncthreads();
   uint32_t k[kItems];
   int32_t v[kItems];
   uint32_t rank[kItems];
   const uint64_t lt_mask = (1ull << lane) - 1ull;
+  // issue all 16 loads before the ranking chain (each round depends on the last
+  // through the LDS counters; loads inside it would serialise 16 memory latencies)
 #pragma unroll
   for (int r = 0; r < kItems; ++r) {
     const int li = w * (kTile / kWaves) + r * 64 + lane;  // wave-owned 1024-element segment
-    const bool valid = li < tile_n;
-    uint32_t d = kDigits;  // sentinel for invalid lanes
-    if (valid) {
+    if (li < tile_n) {
       k[r] = keys_in[base + li];
       v[r] = vals_in ? vals_in[base + li] : (int32_t)(base + li);
-      d = (k[r] >> shift) & (kDigits - 1);
     }
+  }
+#pragma unroll
+  for (int r = 0; r < kItems; ++r) {
+    const int li = w * (kTile / kWaves) + r * 64 + lane;
+    const bool valid = li < tile_n;
+    uint32_t d = kDigits;  // sentinel for invalid lanes
+    if (valid) d = (k[r] >> shift) & (kDigits - 1);
     // 64-lane match-any on the 8-bit digit
     uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -268,7 +312,10 @@ scatter32_kernel(const uint32_t* __restrict__ keys_in, const int32_t* __restrict
 
 // -------------------------------------------------------------- fused RLE
 __global__ void __launch_bounds__(kBlk) rle32_count_kernel(const uint32_t* __restrict__ hs,
-                                                           int64_t n, uint32_t* __restrict__ part) {
+                                                           int64_t n_host, uint32_t* __restrict__ part,
+                                                           const int32_t* __restrict__ n_dev) {
+  const int64_t n = dev_len(n_dev, n_host);
+  if ((int64_t)blockIdx.x >= live_tiles(n_dev, n_host, (n_host + kTile - 1) / kTile)) return;
   __shared__ uint32_t lds[kWaves + 1];
   const int64_t base = (int64_t)blockIdx.x * kTile;
   uint32_t c = 0;
@@ -284,33 +331,42 @@ __global__ void __launch_bounds__(kBlk) rle32_count_kernel(const uint32_t* __res
 
 // part[] holds the exclusive prefix of head counts per tile (scan_single_kernel).
 __global__ void __launch_bounds__(kBlk)
-rle32_write_kernel(const uint32_t* __restrict__ hs, const int32_t* __restrict__ pos_s, int64_t n,
+rle32_write_kernel(const uint32_t* __restrict__ hs, const int32_t* __restrict__ pos_s, int64_t n_host,
                    const uint32_t* __restrict__ part, int32_t* __restrict__ segid,
                    uint64_t* __restrict__ uniq, int32_t* __restrict__ seg_start,
                    int32_t* __restrict__ local_col, int32_t* __restrict__ n_uniq,
-                   float* __restrict__ zero_a, float* __restrict__ zero_b) {
-  __shared__ uint32_t flag[kTile + 1];
+                   float* __restrict__ zero_a, float* __restrict__ zero_b,
+                   const int32_t* __restrict__ n_dev, int64_t p_cap) {
+  const int64_t n = dev_len(n_dev, n_host);
+  if (n == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    *n_uniq = 0;
+    seg_start[0] = 0;
+  }
+  if ((int64_t)blockIdx.x >= live_tiles(n_dev, n_host, (n_host + kTile - 1) / kTile)) return;
+  // flag[] is read both coalesced (li = j*256 + t) and blocked (t*16 + q): pad one
+  // word per 16 so the blocked pass does not put all 64 lanes on 2 LDS banks
+  __shared__ uint32_t flag[kTile + kTile / 16 + 1];
   __shared__ uint32_t lds[kWaves + 1];
   const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * kTile;
   const int tile_n = (int)min((int64_t)kTile, n - base);
-#pragma unroll 4
+#pragma unroll
   for (int j = 0; j < kItems; ++j) {  // coalesced flag computation into LDS
     const int li = j * kBlk + t;
     const int64_t i = base + li;
-    flag[li] = (li < tile_n) ? ((i == 0 || hs[i] != hs[i - 1]) ? 1u : 0u) : 0u;
+    flag[li + (li >> 4)] = (li < tile_n) ? ((i == 0 || hs[i] != hs[i - 1]) ? 1u : 0u) : 0u;
   }
   __syncthreads();
   // blocked: thread t owns tile elements [t*16, t*16+16)
   uint32_t s = 0;
 #pragma unroll
-  for (int q = 0; q < kItems; ++q) s += flag[t * kItems + q];
+  for (int q = 0; q < kItems; ++q) s += flag[t * (kItems + 1) + q];
   uint32_t tot;
   uint32_t run = block_excl_scan_u32(s, lds, &tot, kWaves) + part[blockIdx.x];
 #pragma unroll
   for (int q = 0; q < kItems; ++q) {
-    run += flag[t * kItems + q];
-    flag[t * kItems + q] = run;  // inclusive 1-based segment id
+    run += flag[t * (kItems + 1) + q];
+    flag[t * (kItems + 1) + q] = run;  // inclusive 1-based segment id
   }
   __syncthreads();
 #pragma unroll 4
@@ -318,12 +374,12 @@ rle32_write_kernel(const uint32_t* __restrict__ hs, const int32_t* __restrict__ 
     const int li = j * kBlk + t;
     if (li >= tile_n) continue;
     const int64_t i = base + li;
-    const uint32_t sid = flag[li];
+    const uint32_t sid = flag[li + (li >> 4)];
     const int32_t s0 = (int32_t)sid - 1;
     segid[i] = (int32_t)sid;
     if (!in_range(s0, n)) continue;
     const int32_t p = pos_s[i];
-    if (in_range(p, n)) local_col[p] = s0;
+    if (in_range(p, p_cap)) local_col[p] = s0;
     const bool head = (i == 0) || hs[i] != hs[i - 1];
     if (head) {
       uniq[s0] = hs[i];
@@ -363,13 +419,14 @@ static void radix32(const uint64_t* raw, int64_t n, KeyMix m, int64_t T, uint32_
     const int shift = pass * kBits;
     if (pass == 0)
       hist32_kernel<true, kBits><<<(unsigned)T, kBlk, 0, st>>>(raw, nullptr, n, m, mixed, shift,
-                                                               hist, T);
+                                                               hist, T, nullptr, nullptr);
     else
       hist32_kernel<false, kBits><<<(unsigned)T, kBlk, 0, st>>>(nullptr, src_k, n, m, nullptr,
-                                                                shift, hist, T);
+                                                                shift, hist, T, nullptr, nullptr);
     PSAMD_HIP_CHECK(hipGetLastError());
     scan2_u32(hist, (int64_t)kDigits * T, spart, st);
-    scatter32_kernel<kBits><<<(unsigned)T, kBlk, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T);
+    scatter32_kernel<kBits><<<(unsigned)T, kBlk, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T,
+                                                          nullptr, nullptr);
     PSAMD_HIP_CHECK(hipGetLastError());
     src_k = dk;
     src_v = dv;
@@ -400,11 +457,85 @@ void localize32(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t tem
     radix32<10>(raw, n, m, T, mixed, kt, vt, hist, spart, hs, pos_s, st);
   else
     radix32<8>(raw, n, m, T, mixed, kt, vt, hist, spart, hs, pos_s, st);
-  rle32_count_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, n, part);
+  rle32_count_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, n, part, nullptr);
   PSAMD_HIP_CHECK(hipGetLastError());
   scan2_u32(part, T, spart, st);
   rle32_write_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, pos_s, n, part, segid, uniq, seg_start,
-                                                   local_col, n_uniq, zero_a, zero_b);
+                                                   local_col, n_uniq, zero_a, zero_b, nullptr, n);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// Sort + RLE of already-mixed u32 keys held in ragged tiles (the output of the
+// tile-deduplicating localiser, tileloc.hip): n_dev = total live keys, n_max the
+// workspace. After the first pass every kernel, scan and tile stride follows the
+// live count, so the cost scales with n_dev, not with n_max.
+size_t sort32_dev_temp_bytes(int64_t n_max) {
+  const int64_t T = (n_max + kTile - 1) / kTile;
+  const int64_t chunks = ((int64_t)kMaxDigits * T + kScanChunk - 1) / kScanChunk + T;
+  return (size_t)n_max * 8 + (size_t)kMaxDigits * T * 4 + (size_t)T * 4 + (size_t)chunks * 4 + 512;
+}
+
+// Pass 0 reads RAGGED tiles (tile b = tile_cnt[b] keys at [b*kTile, ...), values =
+// the implicit fixed-stride ids b*kTile + i) and writes them compacted; later passes
+// work on the n_dev compacted elements.
+template <int kBits>
+static void radix32_dev(const uint32_t* keys_in, const int32_t* tile_cnt, int64_t n, int64_t T,
+                        const int32_t* n_dev, int bits, uint32_t* kt, int32_t* vt, uint32_t* hist,
+                        uint32_t* spart, uint32_t* hs, int32_t* pos_s, hipStream_t st) {
+  constexpr int kDigits = 1 << kBits;
+  const int passes = (bits + kBits - 1) / kBits;
+  const uint32_t* src_k = keys_in;
+  const int32_t* src_v = nullptr;  // pass 0: fixed-stride ids (iota)
+  KeyMix none{};
+  for (int pass = 0; pass < passes; ++pass) {
+    const bool to_out = ((passes - 1 - pass) % 2) == 0;
+    uint32_t* dk = to_out ? hs : kt;
+    int32_t* dv = to_out ? pos_s : vt;
+    const int shift = pass * kBits;
+    const int32_t* nd = pass == 0 ? nullptr : n_dev;
+    const int32_t* tc = pass == 0 ? tile_cnt : nullptr;
+    hist32_kernel<false, kBits><<<(unsigned)T, kBlk, 0, st>>>(nullptr, src_k, n, none, nullptr,
+                                                              shift, hist, T, nd, tc);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    scan2_u32(hist, (int64_t)kDigits * T, spart, st, nd, n, kDigits);
+    scatter32_kernel<kBits><<<(unsigned)T, kBlk, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T,
+                                                          nd, tc);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    src_k = dk;
+    src_v = dv;
+  }
+}
+
+void sort_rle32_dev(const uint32_t* keys_in, const int32_t* tile_cnt, int64_t n_max,
+                    const int32_t* n_dev, int bits, int digit_bits, void* temp, size_t temp_bytes,
+                    uint32_t* hs, int32_t* pos_s, int32_t* segid, uint64_t* uniq,
+                    int32_t* seg_start, int32_t* ent_uid, int64_t p_cap, int32_t* n_uniq,
+                    float* zero_a, hipStream_t st) {
+  if (n_max <= 0) return;
+  if (bits > 32) throw std::runtime_error("sort_rle32_dev needs key bits <= 32");
+  if (temp_bytes < sort32_dev_temp_bytes(n_max))
+    throw std::runtime_error("sort_rle32_dev temp too small");
+  const int64_t T = (n_max + kTile - 1) / kTile;
+  char* p = (char*)temp;
+  uint32_t* kt = (uint32_t*)p;
+  p += (size_t)n_max * 4;
+  int32_t* vt = (int32_t*)p;
+  p += (size_t)n_max * 4;
+  uint32_t* hist = (uint32_t*)p;
+  p += (size_t)kMaxDigits * T * 4;
+  uint32_t* part = (uint32_t*)p;
+  p += (size_t)T * 4;
+  uint32_t* spart = (uint32_t*)p;
+  if (digit_bits == 10)
+    radix32_dev<10>(keys_in, tile_cnt, n_max, T, n_dev, bits, kt, vt, hist, spart, hs, pos_s, st);
+  else
+    radix32_dev<8>(keys_in, tile_cnt, n_max, T, n_dev, bits, kt, vt, hist, spart, hs, pos_s, st);
+  rle32_count_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, n_max, part, n_dev);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  scan2_u32(part, T, spart, st, n_dev, n_max, 1);
+  rle32_write_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, pos_s, n_max, part, segid, uniq, seg_start,
+                                                   ent_uid, n_uniq, zero_a, nullptr, n_dev, p_cap);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

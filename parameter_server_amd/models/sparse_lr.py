@@ -70,7 +70,8 @@ class SparseLRConfig:
     countmin_k: int = 2
     consistency: str = "bsp"             # bsp | ssp:<tau> | asp
     push_mode: str = "sequential"        # sequential | aggregate
-    localize: str = "sort"               # sort | bucket | hash | auto (bucket/hash: <= 32-bit keys)
+    localize: str = "sort"               # sort | tile | bucket | hash | auto (tile: <= 31-bit
+                                         # keys, bucket/hash: <= 32-bit keys)
     fixing_float_bytes: int = 0          # 0 = off, else 1..7 bytes per pushed gradient
     # multi-GPU data plane: "padded" = fixed-capacity rows per peer with device-side
     # counts (no host sync, graph-replayable); "exact" = count exchange + sized
@@ -103,9 +104,10 @@ class SparseLRTrainer:
         self.table = KVTable(cap, self.device, cfg.init, key_range=self.part.range_of(self.rank))
         self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
         mode = cfg.localize
-        fused = self.G > 1 and cfg.tail_feature_freq <= 0 and cfg.fixing_float_bytes == 0
-        if mode == "auto":  # sort-free ids: 1 GPU, or the fused exchange (owner bucketing)
-            mode = "hash" if (cfg.tail_feature_freq <= 0 and (self.G == 1 or fused)) else "sort"
+        if mode == "auto":  # tile dedup + sort of the tile-distinct keys (<= 31-bit keys)
+            mode = "tile"
+        if cfg.tail_feature_freq > 0 and mode in ("tile", "hash"):
+            mode = "sort"  # the tail filter needs per-key nnz counts (seg_start over nnz)
         self.localize_mode = mode
         self.localizer = Localizer(self.max_nnz, self.bits, self.device, mode=mode)
         self._localizers = [self.localizer]  # + a second buffer set for prefetching (G > 1)

@@ -37,9 +37,20 @@ class Localized:
     hess: torch.Tensor | None
     nnz: int
     hashed: bool = False  # sort-free ids (no CSC order: pos_s / segid / seg_start are None)
+    # tile-deduplicated ("tile" mode): pos_s / segid / seg_start run over the
+    # tile-distinct ENTRIES, not the nnz; the backward goes through tile_backward
+    tile: object = None
 
     def num_unique(self) -> int:  # host sync
         return int(self.n_uniq.item())
+
+
+@dataclass
+class TileInfo:
+    rep: torch.Tensor    # int16 [nnz] tile-local entry id of every position
+    dcnt: torch.Tensor   # int32 [tiles] distinct keys per 4096-key tile
+    n_ent: torch.Tensor  # int32[1] total entries (device)
+    psum: torch.Tensor   # float [tiles*4096] per-entry partial gradients (backward scratch)
 
 
 class Localizer:
@@ -68,11 +79,30 @@ class Localizer:
         n = self.max_nnz
         dev = self.device
         self.gpu = dev.type == "cuda"
-        if mode not in ("sort", "hash", "bucket"):
+        if mode not in ("sort", "hash", "bucket", "tile"):
             raise ValueError(f"unknown localisation mode {mode!r}")
-        if mode == "hash" and (with_hess or self.bits > 32):
+        if mode in ("hash", "tile") and (with_hess or self.bits > 32):
+            mode = "sort"
+        if mode == "tile" and self.bits > 31:
             mode = "sort"
         self.mode = mode if (self.gpu and self.bits <= 32) else "sort"
+        if self.gpu and self.mode == "tile":
+            H = hipops()
+            N = H.tileloc_stride(n)
+            i32 = lambda k: torch.empty(k, dtype=torch.int32, device=dev)  # noqa: E731
+            self.t_dkeys, self.t_dcnt, self.t_nent = i32(N), i32(N // 4096), i32(1)
+            self.t_rep = torch.empty(n, dtype=torch.int16, device=dev)
+            self.t_temp = torch.empty(H.tileloc_sort_temp_bytes(n), dtype=torch.uint8, device=dev)
+            self.t_hs, self.pos_s, self.segid, self.t_ent_uid = i32(N), i32(N), i32(N), i32(N)
+            self.seg_start = i32(N + 1)
+            self.uniq = torch.empty(N, dtype=torch.int64, device=dev)
+            self.local_col = i32(n)
+            self.n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.grad = torch.empty(N, dtype=torch.float32, device=dev)
+            self.t_psum = torch.empty(N, dtype=torch.float32, device=dev)
+            self.hess = None
+            self.digit_bits = 10 if 24 < self.bits <= 30 else 8
+            return
         if self.gpu and self.mode == "bucket":
             H = hipops()
             self.btemp = torch.empty(H.bucketloc_temp_bytes(n), dtype=torch.uint8, device=dev)
@@ -142,6 +172,14 @@ class Localizer:
 
     def _gpu(self, keys, n) -> Localized:
         H = hipops()
+        if self.mode == "tile":
+            H.localize_tile(keys, self.bits, self.digit_bits, self.t_dkeys, self.t_dcnt, self.t_rep,
+                            self.t_nent, self.t_temp, self.t_hs, self.pos_s, self.segid, self.uniq,
+                            self.seg_start, self.t_ent_uid, self.local_col, self.n_uniq,
+                            self.grad)
+            tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum)
+            return Localized(self.uniq, self.seg_start, self.pos_s, self.segid,
+                             self.local_col[:n], self.n_uniq, self.grad, None, n, tile=tile)
         if self.mode == "bucket":
             H.localize_bucket(keys, self.bits, self.btemp, self.pos_s, self.segid, self.uniq,
                               self.seg_start, self.local_col, self.n_uniq, self.grad, self.hess)
