@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Factorization machine (reference src/app/factor_machine, fm.m): k-dim bf16 factor rows +
+linear weights sharded over the ranks, packed [v | w] push/pull over RCCL.
+Metric: examples/sec (whole node), weak scaling (fixed minibatch per GPU).
+
+    python benchmarks/bench_fm.py --steps 20
+    torchrun --nproc-per-node N benchmarks/bench_fm.py ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--minibatch", type=int, default=16384)
+    ap.add_argument("--num-features", type=float, default=1e9)
+    ap.add_argument("--dim", type=int, default=16)
+    ap.add_argument("--table-slots", type=int, default=1 << 28, help="slots per GPU")
+    args = ap.parse_args()
+    from parameter_server_amd.models.fm import FMConfig, FMTrainer
+    from parameter_server_amd.ops.synthetic import criteo_batch
+    from parameter_server_amd.parallel.comm import init_from_env
+
+    comm, dev = init_from_env("cuda")
+    G, rank = comm.world, comm.rank
+    B, N = args.minibatch, int(args.num_features)
+    cfg = FMConfig(num_features=N, embedding_dim=args.dim, minibatch=B,
+                   table_capacity=args.table_slots, seed=0)
+    tr = FMTrainer(cfg, comm, dev)
+    keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
+    labels = torch.empty(B, dtype=torch.float32, device=dev)
+    t = [0]
+
+    def step():
+        criteo_batch(B, seed=77 + rank, row0=t[0] * B, num_features=N, device=dev, keys=keys,
+                     labels=labels)
+        tr.step(keys, labels)
+        t[0] += 1
+
+    for _ in range(args.warmup):
+        step()
+    tr.progress()
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    dt = time.perf_counter() - t0
+    x = torch.tensor([dt], dtype=torch.float64, device=dev if G > 1 else "cpu")
+    comm.all_reduce_(x, op="max")
+    dt = float(x.item())
+    p = tr.progress()
+    occ, _ = tr.shard.table.census()
+    if rank == 0:
+        print(json.dumps({
+            "metric": "examples/sec (whole node) factorization machine, 1e9 hashed features",
+            "value": G * B * args.steps / dt, "unit": "examples/sec", "n_gpus": G,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "weak", "dtype": "bf16 rows (fp32 math)",
+            "config": {"num_features": N, "embedding_dim": args.dim, "slots": 39,
+                       "global_batch": G * B, "table_slots_per_gpu": tr.shard.capacity,
+                       "shard_gb": tr.shard.nbytes() / 2 ** 30},
+            "train": {**p, "rows_rank0": occ},
+        }), flush=True)
+    if G > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

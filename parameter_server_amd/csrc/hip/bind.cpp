@@ -19,6 +19,11 @@ void kv_resolve(void*, int64_t, const uint64_t*, int64_t, const int32_t*, int64_
 void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int, int64_t*, float*,
                      bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t,
                      hipStream_t);
+// fm.hip
+void fm_fwd_bwd(const void*, const float*, int64_t, int, int, const int32_t*, const float*, int64_t,
+                const float*, float*, void*, double*, uint32_t*, int, hipStream_t);
+void fm_l2(float*, const void*, const int64_t*, int64_t, const int32_t*, int64_t, int, float,
+           hipStream_t);
 // tileloc.hip
 int64_t tileloc_stride(int64_t);
 size_t tileloc_sort_temp_bytes(int64_t);
@@ -234,6 +239,44 @@ PYBIND11_MODULE(_hipops, m) {
      py::arg("out_w"), py::arg("insert"), py::arg("init_type"), py::arg("init_v"),
      py::arg("init_s"), py::arg("seed"), py::arg("err"), py::arg("inserted"),
      py::arg("home_base") = 0, py::arg("home_m") = 0);
+  // ---------------- factorization machine (fm.hip) ----------------
+  m.def("fm_fwd_bwd", [](Tensor X0, optional<Tensor> vals, int64_t B, int S, Tensor local_col,
+                         Tensor w_local, Tensor labels, Tensor coef, Tensor dX0, Tensor metrics,
+                         optional<Tensor> hist, int nbins) {
+    chk(X0, at::kBFloat16, "X0");
+    chk(dX0, at::kBFloat16, "dX0");
+    chk(local_col, at::kInt, "local_col");
+    chk(w_local, at::kFloat, "w_local");
+    chk(labels, at::kFloat, "labels");
+    chk(coef, at::kFloat, "coef");
+    chk(metrics, at::kDouble, "metrics");
+    check(X0.dim() == 2 && X0.size(1) <= 128 && X0.size(1) > 0, "X0 must be [B*S, D<=128]");
+    check(S > 0 && S <= 64, "1..64 keys per example");
+    const int D = (int)X0.size(1);
+    check(X0.size(0) >= B * S && dX0.numel() >= B * S * D, "X0/dX0 too small");
+    check(local_col.numel() >= B * S && labels.numel() >= B && coef.numel() >= B, "too small");
+    check(metrics.numel() >= 3, "metrics[3]");
+    const float* v = optr<float>(vals, at::kFloat, "vals");
+    if (v) check(vals->numel() >= B * S, "vals too small");
+    uint32_t* h = optr<uint32_t>(hist, at::kInt, "hist");
+    if (h) check(hist->numel() >= 2 * nbins, "hist too small");
+    psamd::fm_fwd_bwd(X0.data_ptr(), v, B, S, D, ptr<int32_t>(local_col), ptr<float>(w_local),
+                      w_local.numel(), ptr<float>(labels), ptr<float>(coef), dX0.data_ptr(),
+                      ptr<double>(metrics), h, nbins, cur_stream());
+  });
+  m.def("fm_l2", [](Tensor dE, Tensor rows, optional<Tensor> idx, optional<Tensor> n_dev,
+                    int64_t u_cap, double lambda) {
+    chk(dE, at::kFloat, "dE");
+    chk(rows, at::kBFloat16, "rows");
+    check(rows.dim() == 2, "rows [n, D]");
+    const int D = (int)rows.size(1);
+    check(dE.numel() >= u_cap * D, "dE too small");
+    const int64_t* ip = optr<int64_t>(idx, at::kLong, "idx");
+    if (ip) check(idx->numel() >= u_cap, "idx too small");
+    else check(rows.size(0) >= u_cap, "rows too small");
+    psamd::fm_l2(ptr<float>(dE), rows.data_ptr(), ip, rows.size(0),
+                 optr<int32_t>(n_dev, at::kInt, "n_dev"), u_cap, D, (float)lambda, cur_stream());
+  });
   // ---------------- tile-deduplicating localisation (tileloc.hip) ----------------
   m.def("tileloc_stride", [](int64_t n) { return psamd::tileloc_stride(n); });
   m.def("tileloc_sort_temp_bytes", [](int64_t n) { return (int64_t)psamd::tileloc_sort_temp_bytes(n); });

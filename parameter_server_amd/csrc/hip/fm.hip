@@ -1,0 +1,145 @@
+// Factorization machine forward + backward (one wavefront per example).
+//
+// Reference: src/app/factor_machine/ (fm_worker.h, fm.m). The reference FM is an
+// unfinished sketch (not in the Makefile); fm.m gives the model it aims at:
+//   py = x.w + 1/2 sum_f [ (sum_i x_i v_if)^2 - sum_i x_i^2 v_if^2 ]
+//   p  = -y / (1 + exp(y py))              (logistic loss)
+//   gv_i = p * (x_i s_f - x_i^2 v_if),  s_f = sum_j x_j v_jf
+// (fm.m adds the x^2 v^2 term in the prediction; its gradient uses the standard
+// minus sign, which is what is implemented here.)
+//
+// Inputs are the expanded embedding rows X0 [B*S, D] (bf16, rows of the pulled
+// unique keys) and the pulled wide weights; x_i = vals ? vals[i] : 1. Per example:
+// lanes own features f = lane, lane + 64 (D <= 128), loop over the S positions to
+// build s_f and q_f = sum x^2 v^2; the wide margin is a 64-lane reduction. Outputs:
+// coef[b] = p (for the wide-weight gradient), dX0[b*S+i, f] = p (x_i s_f - x_i^2 v_if)
+// (bf16, reduced per unique key by emb_grad_reduce), loss / accuracy / AUC histogram.
+#include "common.cuh"
+
+namespace psamd {
+
+namespace {
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {  // round to nearest even
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256)
+fm_fwd_bwd_kernel(const uint16_t* __restrict__ X0, const float* __restrict__ vals, int64_t B,
+                  int S, int D, const int32_t* __restrict__ local_col,
+                  const float* __restrict__ w_local, int64_t w_cap,
+                  const float* __restrict__ labels, float* __restrict__ coef_out,
+                  uint16_t* __restrict__ dX0, double* __restrict__ metrics,
+                  uint32_t* __restrict__ hist, int nbins) {
+  extern __shared__ uint32_t lhist[];  // [2*nbins]
+  __shared__ double lds[16];
+  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) lhist[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (blockDim.x / 64);
+  double loss_acc = 0, corr_acc = 0, cnt = 0;
+  for (int64_t b = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6); b < B;
+       b += waves) {
+    const int64_t p0 = b * S;
+    float s0 = 0.f, s1 = 0.f, q0 = 0.f, q1 = 0.f;
+    const int f0 = lane, f1 = lane + 64;
+    for (int i = 0; i < S; ++i) {
+      const float x = vals ? vals[p0 + i] : 1.f;
+      const uint16_t* row = X0 + (p0 + i) * D;
+      if (f0 < D) {
+        const float v = bf16_to_f32(row[f0]) * x;
+        s0 += v;
+        q0 += v * v;
+      }
+      if (f1 < D) {
+        const float v = bf16_to_f32(row[f1]) * x;
+        s1 += v;
+        q1 += v * v;
+      }
+    }
+    float part = 0.5f * (s0 * s0 - q0 + s1 * s1 - q1);
+    if (lane < S) {
+      const int32_t c = local_col[p0 + lane];
+      const float x = vals ? vals[p0 + lane] : 1.f;
+      if (in_range(c, w_cap)) part += w_local[c] * x;
+    }
+    const float m = wave_allsum(part);
+    const float y = labels[b] > 0.f ? 1.f : -1.f;
+    const float ym = y * m;
+    const float tau = 1.f / (1.f + expf(ym));
+    const float coef = -y * tau;
+    if (lane == 0) {
+      coef_out[b] = coef;
+      loss_acc += ym > 20.f ? expf(-ym) : (ym < -20.f ? -ym : log1pf(expf(-ym)));
+      corr_acc += ((y > 0.f) == (m > 0.f)) ? 1.0 : 0.0;
+      cnt += 1.0;
+      if (hist) {
+        const float pr = 1.f / (1.f + expf(-m));
+        const float pb = pr == pr ? fminf(fmaxf(pr * nbins, 0.f), (float)(nbins - 1)) : 0.f;
+        atomicAdd(&lhist[(y > 0.f ? nbins : 0) + (int)pb], 1u);
+      }
+    }
+    for (int i = 0; i < S; ++i) {
+      const float x = vals ? vals[p0 + i] : 1.f;
+      const uint16_t* row = X0 + (p0 + i) * D;
+      uint16_t* drow = dX0 + (p0 + i) * D;
+      if (f0 < D) drow[f0] = f32_to_bf16(coef * (x * s0 - x * x * bf16_to_f32(row[f0])));
+      if (f1 < D) drow[f1] = f32_to_bf16(coef * (x * s1 - x * x * bf16_to_f32(row[f1])));
+    }
+  }
+  if (metrics) {
+    const double a = block_sum_f64(loss_acc, lds);
+    const double c = block_sum_f64(corr_acc, lds);
+    const double n = block_sum_f64(cnt, lds);
+    if (threadIdx.x == 0 && n > 0) {
+      atomicAdd(&metrics[0], a);
+      atomicAdd(&metrics[1], c);
+      atomicAdd(&metrics[2], n);
+    }
+  }
+  if (hist) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x)
+      if (lhist[i]) atomicAdd(&hist[i], lhist[i]);
+  }
+}
+
+// dE[u, :] += lambda * v_u (L2 on the factors, once per unique key and step, as fm.m);
+// v_u = rows[idx ? idx[u] : u] (bf16).
+__global__ void fm_l2_kernel(float* __restrict__ dE, const uint16_t* __restrict__ rows,
+                             const int64_t* __restrict__ idx, int64_t rows_cap,
+                             const int32_t* __restrict__ n_dev, int64_t u_cap, int D,
+                             float lambda) {
+  const int64_t n = dev_len(n_dev, u_cap) * D;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t u = e / D;
+    const int f = (int)(e - u * D);
+    const int64_t r = idx ? idx[u] : u;
+    if (in_range(r, rows_cap)) dE[e] += lambda * bf16_to_f32(rows[r * D + f]);
+  }
+}
+
+void fm_fwd_bwd(const void* X0, const float* vals, int64_t B, int S, int D,
+                const int32_t* local_col, const float* w_local, int64_t w_cap, const float* labels,
+                float* coef, void* dX0, double* metrics, uint32_t* hist, int nbins,
+                hipStream_t st) {
+  const int g = grid_for(B * 64, 256, 4096);
+  fm_fwd_bwd_kernel<<<g, 256, hist ? 2 * nbins * sizeof(uint32_t) : 0, st>>>(
+      (const uint16_t*)X0, vals, B, S, D, local_col, w_local, w_cap, labels, coef,
+      (uint16_t*)dX0, metrics, hist, hist ? nbins : 0);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void fm_l2(float* dE, const void* rows, const int64_t* idx, int64_t rows_cap, const int32_t* n_dev,
+           int64_t u_cap, int D, float lambda, hipStream_t st) {
+  fm_l2_kernel<<<grid_for(u_cap * D, 256, 4096), 256, 0, st>>>(dE, (const uint16_t*)rows, idx,
+                                                               rows_cap, n_dev, u_cap, D, lambda);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace psamd

@@ -60,7 +60,74 @@ class WideDeepConfig:
     seed: int = 0
 
 
-class WideDeepTrainer:
+class EmbeddingPS:
+    """Sparse side shared by the embedding models (wide & deep, factorization
+    machine): pull [bf16 row | wide weight] records of a minibatch's unique keys
+    from their owners and push [row gradient | wide gradient] back, one packed
+    all-to-all each way. Needs ``shard``, ``part``, ``comm``, ``G``, ``gpu``,
+    ``stats`` and ``cfg.{embedding_dim, emb_lr, wide}`` on the host class."""
+
+    # ------------------------------------------------------------ exchange (G > 1)
+    def _pull(self, loc):
+        """Owner split -> keys all-to-all -> resolve + gather [row | w] -> records back."""
+        D = self.cfg.embedding_dim
+        U = loc.num_unique()
+        off = self.part.split_sorted(loc.uniq, loc.n_uniq).cpu()
+        send = (off[1:] - off[:-1]).tolist()
+        recv = self.comm.exchange_counts(torch.tensor(send, dtype=torch.int64)).cpu().tolist()
+        rk = self.comm.all_to_all_v(loc.uniq[:U].contiguous(), send, recv)
+        slot, w = self.shard.resolve(rk)
+        rec = self._pack(self.shard.gather_rows(slot), w)
+        back = self.comm.all_to_all_v(rec, recv, send)
+        rows_u, w_u = self._unpack(back, D)
+        return rows_u, w_u, ("dist", slot, send, recv, U)
+
+    @staticmethod
+    def _pack(rows16: torch.Tensor, w32: torch.Tensor) -> torch.Tensor:
+        """[n, D] bf16 + [n] f32 -> [n, D/2 + 1] int32 records (one all-to-all)."""
+        n, D = rows16.shape
+        rec = torch.empty(n, D // 2 + 1, dtype=torch.int32, device=rows16.device)
+        rec[:, :D // 2] = rows16.contiguous().view(torch.int32).view(n, D // 2)
+        rec[:, D // 2] = w32.contiguous().view(torch.int32)
+        return rec
+
+    @staticmethod
+    def _unpack(rec: torch.Tensor, D: int):
+        n = rec.shape[0]
+        rows16 = rec[:, :D // 2].contiguous().view(torch.bfloat16).view(n, D)
+        w32 = rec[:, D // 2].contiguous().view(torch.float32)
+        return rows16, w32
+
+    def _push(self, loc, push, dE, g_wide):
+        cfg = self.cfg
+        if push[0] == "local":
+            slot = push[1]
+            n_dev = loc.n_uniq if self.gpu else None
+            if self.gpu:
+                self.shard.update_rows(slot, grad=dE, lr=cfg.emb_lr, n_dev=n_dev)
+                hipops().kv_update(self.shard.table.slots, slot, g_wide, n_dev,
+                                   *cfg.wide.args(), self.stats)
+            else:
+                U = loc.num_unique()
+                self.shard.update_rows(slot[:U], grad=dE[:U], lr=cfg.emb_lr)
+                self.shard.update_wide(slot[:U], g_wide[:U], cfg.wide, self.stats)
+            return
+        _, slot, send, recv, U = push
+        D = cfg.embedding_dim
+        rec = self._pack(dE[:U].to(torch.bfloat16), g_wide[:U])
+        got = self.comm.all_to_all_v(rec, send, recv)
+        g16, gw = self._unpack(got, D)
+        a = 0
+        for s in range(self.G):  # one update per source (slots unique within a source)
+            n = recv[s]
+            if n:
+                self.shard.update_rows(slot[a:a + n], grad16=g16[a:a + n], lr=cfg.emb_lr)
+                self.shard.update_wide(slot[a:a + n], gw[a:a + n].contiguous(), cfg.wide,
+                                       self.stats)
+            a += n
+
+
+class WideDeepTrainer(EmbeddingPS):
     def __init__(self, cfg: WideDeepConfig, comm: Comm | None = None, device="cpu"):
         self.cfg = cfg
         self.comm = comm or LocalComm(device)
@@ -184,65 +251,6 @@ class WideDeepTrainer:
                gscale=1.0 / (B * self.G), p16=self.param16)
         auc_from_hist(self.hist, self.metrics, self.step_dev)
         self.examples += B
-
-    # ------------------------------------------------------------ exchange (G > 1)
-    def _pull(self, loc):
-        """Owner split -> keys all-to-all -> resolve + gather [row | w] -> records back."""
-        D = self.cfg.embedding_dim
-        U = loc.num_unique()
-        off = self.part.split_sorted(loc.uniq, loc.n_uniq).cpu()
-        send = (off[1:] - off[:-1]).tolist()
-        recv = self.comm.exchange_counts(torch.tensor(send, dtype=torch.int64)).cpu().tolist()
-        rk = self.comm.all_to_all_v(loc.uniq[:U].contiguous(), send, recv)
-        slot, w = self.shard.resolve(rk)
-        rec = self._pack(self.shard.gather_rows(slot), w)
-        back = self.comm.all_to_all_v(rec, recv, send)
-        rows_u, w_u = self._unpack(back, D)
-        return rows_u, w_u, ("dist", slot, send, recv, U)
-
-    @staticmethod
-    def _pack(rows16: torch.Tensor, w32: torch.Tensor) -> torch.Tensor:
-        """[n, D] bf16 + [n] f32 -> [n, D/2 + 1] int32 records (one all-to-all)."""
-        n, D = rows16.shape
-        rec = torch.empty(n, D // 2 + 1, dtype=torch.int32, device=rows16.device)
-        rec[:, :D // 2] = rows16.contiguous().view(torch.int32).view(n, D // 2)
-        rec[:, D // 2] = w32.contiguous().view(torch.int32)
-        return rec
-
-    @staticmethod
-    def _unpack(rec: torch.Tensor, D: int):
-        n = rec.shape[0]
-        rows16 = rec[:, :D // 2].contiguous().view(torch.bfloat16).view(n, D)
-        w32 = rec[:, D // 2].contiguous().view(torch.float32)
-        return rows16, w32
-
-    def _push(self, loc, push, dE, g_wide):
-        cfg = self.cfg
-        if push[0] == "local":
-            slot = push[1]
-            n_dev = loc.n_uniq if self.gpu else None
-            if self.gpu:
-                self.shard.update_rows(slot, grad=dE, lr=cfg.emb_lr, n_dev=n_dev)
-                hipops().kv_update(self.shard.table.slots, slot, g_wide, n_dev,
-                                   *cfg.wide.args(), self.stats)
-            else:
-                U = loc.num_unique()
-                self.shard.update_rows(slot[:U], grad=dE[:U], lr=cfg.emb_lr)
-                self.shard.update_wide(slot[:U], g_wide[:U], cfg.wide, self.stats)
-            return
-        _, slot, send, recv, U = push
-        D = cfg.embedding_dim
-        rec = self._pack(dE[:U].to(torch.bfloat16), g_wide[:U])
-        got = self.comm.all_to_all_v(rec, send, recv)
-        g16, gw = self._unpack(got, D)
-        a = 0
-        for s in range(self.G):  # one update per source (slots unique within a source)
-            n = recv[s]
-            if n:
-                self.shard.update_rows(slot[a:a + n], grad16=g16[a:a + n], lr=cfg.emb_lr)
-                self.shard.update_wide(slot[a:a + n], gw[a:a + n].contiguous(), cfg.wide,
-                                       self.stats)
-            a += n
 
     # ------------------------------------------------------------ progress
     def progress(self, reset: bool = True) -> dict:

@@ -1,0 +1,88 @@
+"""Factorization machine (models/fm.py): the PyTorch step matches a direct
+autograd evaluation of the fm.m objective, a single CPU rank learns, and 2 gloo
+ranks shard the factor table."""
+import socket
+
+import torch
+import torch.multiprocessing as mp
+
+from parameter_server_amd.models.fm import FMConfig, FMTrainer
+from parameter_server_amd.ops.synthetic import criteo_batch
+
+CFG = dict(num_features=1 << 20, embedding_dim=8, minibatch=256, table_capacity=1 << 15,
+           emb_lr=0.05, lambda_v=0.0)
+
+
+def test_fm_gradient_matches_autograd():
+    tr = FMTrainer(FMConfig(**CFG))
+    B, S, D = 4, 39, 8
+    g = torch.Generator().manual_seed(0)
+    X0 = (torch.randn(B * S, D, generator=g) * 0.3).to(torch.bfloat16)
+    w = torch.randn(B * S, generator=g) * 0.1
+    lc = torch.arange(B * S, dtype=torch.int32)
+    y = torch.tensor([1.0, -1.0, 1.0, -1.0])
+    dX = tr._fwd_bwd_torch(X0, None, B, S, lc, w, y)
+    V = X0.float().reshape(B, S, D).clone().requires_grad_(True)
+    s = V.sum(1)
+    m = w.reshape(B, S).sum(1) + 0.5 * (s * s - (V * V).sum(1)).sum(1)
+    loss = torch.nn.functional.softplus(-y * m).sum()
+    loss.backward()
+    assert torch.allclose(dX.float(), V.grad.reshape(B * S, D), atol=1e-2, rtol=1e-2)
+    assert torch.allclose(tr.coef[:B], -y * torch.sigmoid(-y * m.detach()), atol=1e-6)
+
+
+def test_fm_cpu_learns():
+    tr = FMTrainer(FMConfig(**CFG))
+    first = last = None
+    for s in range(40):
+        k, l = criteo_batch(256, seed=5, row0=s * 256, num_features=CFG["num_features"],
+                            cards=[300] * 26)
+        tr.step(k, l)
+        if s == 9:
+            first = tr.progress()
+        if s == 39:
+            last = tr.progress()
+    assert last["loss"] < first["loss"] - 0.02, (first, last)
+    assert last["auc"] > 0.65
+    k, _ = criteo_batch(16, seed=5, row0=0, num_features=CFG["num_features"], cards=[300] * 26)
+    assert tr.predict(k, 16).shape == (16,)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from parameter_server_amd.parallel.comm import DistComm
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    tr = FMTrainer(FMConfig(**CFG), DistComm("cpu"), "cpu")
+    for s in range(10):
+        k, l = criteo_batch(256, seed=11 + rank, row0=s * 256, num_features=CFG["num_features"],
+                            cards=[300] * 26)
+        tr.step(k, l)
+    p = tr.progress()
+    occ, _ = tr.shard.table.census()
+    q.put((rank, p["examples"], occ))
+    dist.destroy_process_group()
+
+
+def test_fm_two_rank_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert all(r[1] == 2 * 10 * 256 for r in res)
+    assert all(r[2] > 0 for r in res)
