@@ -194,50 +194,55 @@ void scan2_u32(uint32_t* a, int64_t n, uint32_t* part, hipStream_t st,
 }
 
 // ------------------------------------------------------------------ scatter
+// kScatThreads threads per 4096-key tile: 16 waves x 256 keys (4 ranking rounds
+// per wave instead of 16), per-wave digit counters as u16 and the tile's global
+// digit offsets cached in LDS (68 KB -> 2 tiles per CU, 8 waves per SIMD).
+constexpr int kScatThreads = 1024;
+
 template <int kBits>
-__global__ void __launch_bounds__(kBlk)
+__global__ void __launch_bounds__(kScatThreads)
 scatter32_kernel(const uint32_t* __restrict__ keys_in, const int32_t* __restrict__ vals_in,
                  uint32_t* __restrict__ keys_out, int32_t* __restrict__ vals_out, int64_t n_host,
                  int shift, const uint32_t* __restrict__ offs, int64_t T_host,
                  const int32_t* __restrict__ n_dev, const int32_t* __restrict__ tile_cnt) {
   constexpr int kDigits = 1 << kBits;
+  constexpr int kT = kScatThreads;
+  constexpr int kW = kT / 64;
+  constexpr int kIt = kTile / kT;                       // keys per lane
+  constexpr int kDPT = kDigits >= kT ? kDigits / kT : 1;  // digits per thread in the scan
   const int64_t n = dev_len(n_dev, n_host);
   const int64_t T = live_tiles(n_dev, n_host, T_host);
   if ((int64_t)blockIdx.x >= T) return;
-  constexpr int kDPT = kDigits / kBlk;  // digits per thread in the offset scan
   __shared__ uint32_t skeys[kTile];
   __shared__ int32_t svals[kTile];
-  __shared__ uint32_t wcnt[kWaves * kDigits];  // [wave][digit]
-  __shared__ uint32_t dstart[kDigits];
-  __shared__ uint32_t lds[kWaves + 1];
+  __shared__ uint16_t wcnt[kW * kDigits];  // [wave][digit]: counts, then tile offsets
+  __shared__ int32_t goff[kDigits];        // global position of the tile's digit run - start
+  __shared__ uint32_t lds[kW + 1];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t base = (int64_t)blockIdx.x * kTile;
   const int tile_n = tile_cnt ? min(kTile, max(0, tile_cnt[blockIdx.x]))
                               : (int)min((int64_t)kTile, n - base);
-  for (int f = t; f < kWaves * kDigits; f += kBlk) wcnt[f] = 0;
+  for (int f = t; f < kW * kDigits; f += kT) wcnt[f] = 0;
   __syncthreads();
-  uint32_t k[kItems];
-  int32_t v[kItems];
-  uint32_t rank[kItems];
+  uint32_t k[kIt];
+  int32_t v[kIt];
+  uint32_t rank[kIt];
   const uint64_t lt_mask = (1ull << lane) - 1ull;
-  // issue all 16 loads before the ranking chain (each round depends on the last
-  // through the LDS counters; loads inside it would serialise 16 memory latencies)
 #pragma unroll
-  for (int r = 0; r < kItems; ++r) {
-    const int li = w * (kTile / kWaves) + r * 64 + lane;  // wave-owned 1024-element segment
+  for (int r = 0; r < kIt; ++r) {  // all loads in flight before the ranking chain
+    const int li = w * (kTile / kW) + r * 64 + lane;  // wave-owned 256-key segment
     if (li < tile_n) {
       k[r] = keys_in[base + li];
       v[r] = vals_in ? vals_in[base + li] : (int32_t)(base + li);
     }
   }
 #pragma unroll
-  for (int r = 0; r < kItems; ++r) {
-    const int li = w * (kTile / kWaves) + r * 64 + lane;
+  for (int r = 0; r < kIt; ++r) {
+    const int li = w * (kTile / kW) + r * 64 + lane;
     const bool valid = li < tile_n;
     uint32_t d = kDigits;  // sentinel for invalid lanes
     if (valid) d = (k[r] >> shift) & (kDigits - 1);
-    // 64-lane match-any on the 8-bit digit
-    uint64_t peers = __ballot(valid);
+    uint64_t peers = __ballot(valid);  // 64-lane match-any on the digit
 #pragma unroll
     for (int b = 0; b < kBits; ++b) {
       const bool bit = (d >> b) & 1u;
@@ -248,43 +253,46 @@ scatter32_kernel(const uint32_t* __restrict__ keys_in, const int32_t* __restrict
     if (valid) base_cnt = wcnt[w * kDigits + d];
     __builtin_amdgcn_wave_barrier();
     if (valid && (peers & lt_mask) == 0ull)
-      wcnt[w * kDigits + d] = base_cnt + (uint32_t)__popcll(peers);
+      wcnt[w * kDigits + d] = (uint16_t)(base_cnt + (uint32_t)__popcll(peers));
     __builtin_amdgcn_wave_barrier();
     rank[r] = base_cnt + (uint32_t)__popcll(peers & lt_mask);
   }
   __syncthreads();
-  // digit-major offsets: thread t handles digits [t*kDPT, (t+1)*kDPT)
-  {
+  {  // digit-major tile offsets; thread t owns digits [t*kDPT, (t+1)*kDPT)
     uint32_t tot_d[kDPT], s_t = 0;
 #pragma unroll
     for (int e = 0; e < kDPT; ++e) {
       const int d = t * kDPT + e;
       uint32_t c = 0;
+      if (d < kDigits) {
 #pragma unroll
-      for (int q = 0; q < kWaves; ++q) c += wcnt[q * kDigits + d];
+        for (int q = 0; q < kW; ++q) c += wcnt[q * kDigits + d];
+      }
       tot_d[e] = c;
       s_t += c;
     }
     uint32_t total;
-    uint32_t run = block_excl_scan_u32(s_t, lds, &total, kWaves);
+    uint32_t run = block_excl_scan_u32(s_t, lds, &total, kW);
 #pragma unroll
     for (int e = 0; e < kDPT; ++e) {
       const int d = t * kDPT + e;
-      dstart[d] = run;
-      uint32_t r2 = run;
+      if (d < kDigits) {
+        goff[d] = (int32_t)offs[(int64_t)d * T + blockIdx.x] - (int32_t)run;
+        uint32_t r2 = run;
 #pragma unroll
-      for (int q = 0; q < kWaves; ++q) {
-        const uint32_t c = wcnt[q * kDigits + d];
-        wcnt[q * kDigits + d] = r2;
-        r2 += c;
+        for (int q = 0; q < kW; ++q) {
+          const uint32_t c = wcnt[q * kDigits + d];
+          wcnt[q * kDigits + d] = (uint16_t)r2;
+          r2 += c;
+        }
       }
       run += tot_d[e];
     }
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kItems; ++r) {
-    const int li = w * (kTile / kWaves) + r * 64 + lane;
+  for (int r = 0; r < kIt; ++r) {
+    const int li = w * (kTile / kW) + r * 64 + lane;
     if (li < tile_n) {
       const uint32_t d = (k[r] >> shift) & (kDigits - 1);
       const uint32_t pos = wcnt[w * kDigits + d] + rank[r];
@@ -295,14 +303,14 @@ scatter32_kernel(const uint32_t* __restrict__ keys_in, const int32_t* __restrict
     }
   }
   __syncthreads();
-#pragma unroll 4
-  for (int j = 0; j < kItems; ++j) {
-    const int li = j * kBlk + t;
+#pragma unroll
+  for (int j = 0; j < kIt; ++j) {
+    const int li = j * kT + t;
     if (li < tile_n) {
       const uint32_t key = skeys[li];
       const uint32_t d = (key >> shift) & (kDigits - 1);
-      const int64_t g = (int64_t)offs[(int64_t)d * T + blockIdx.x] + (li - (int)dstart[d]);
-      if (in_range(g, n)) {
+      const int64_t g = (int64_t)goff[d] + li;
+      if (in_range(g, n_host)) {
         keys_out[g] = key;
         vals_out[g] = svals[li];
       }
@@ -425,7 +433,7 @@ static void radix32(const uint64_t* raw, int64_t n, KeyMix m, int64_t T, uint32_
                                                                 shift, hist, T, nullptr, nullptr);
     PSAMD_HIP_CHECK(hipGetLastError());
     scan2_u32(hist, (int64_t)kDigits * T, spart, st);
-    scatter32_kernel<kBits><<<(unsigned)T, kBlk, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T,
+    scatter32_kernel<kBits><<<(unsigned)T, kScatThreads, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T,
                                                           nullptr, nullptr);
     PSAMD_HIP_CHECK(hipGetLastError());
     src_k = dk;
@@ -499,7 +507,7 @@ static void radix32_dev(const uint32_t* keys_in, const int32_t* tile_cnt, int64_
                                                               shift, hist, T, nd, tc);
     PSAMD_HIP_CHECK(hipGetLastError());
     scan2_u32(hist, (int64_t)kDigits * T, spart, st, nd, n, kDigits);
-    scatter32_kernel<kBits><<<(unsigned)T, kBlk, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T,
+    scatter32_kernel<kBits><<<(unsigned)T, kScatThreads, 0, st>>>(src_k, src_v, dk, dv, n, shift, hist, T,
                                                           nd, tc);
     PSAMD_HIP_CHECK(hipGetLastError());
     src_k = dk;
