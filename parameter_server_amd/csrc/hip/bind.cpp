@@ -16,6 +16,8 @@ namespace psamd {
 void kv_init(void*, int64_t, hipStream_t);
 void kv_resolve(void*, int64_t, const uint64_t*, int64_t, const int32_t*, int64_t*, float*, bool,
                 int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t, hipStream_t);
+void kv_accumulate_rows(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int,
+                        int64_t, int64_t, int64_t*, int32_t*, int64_t, hipStream_t);
 void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int, int64_t*, float*,
                      bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t,
                      hipStream_t);
@@ -354,6 +356,25 @@ PYBIND11_MODULE(_hipops, m) {
                            (float)init_v, (float)init_s, seed, optr<int32_t>(err, at::kInt, "err"),
                            optr<int32_t>(inserted, at::kInt, "inserted"), home_base, home_m,
                            cur_stream());
+  });
+  // aggregated pushes of every source row in one launch; grad row s at grad[s*gstride]
+  m.def("kv_accumulate_rows", [](Tensor slots, Tensor slot_idx, Tensor grad, int64_t gstride,
+                                 Tensor recv, int64_t H, int64_t C, Tensor touched,
+                                 Tensor n_touched) {
+    const int64_t cap = slot_capacity(slots);
+    chk(slot_idx, at::kLong, "slot_idx");
+    chk(grad, at::kFloat, "grad");
+    chk(recv, at::kInt, "recv");
+    chk(touched, at::kLong, "touched");
+    chk(n_touched, at::kInt, "n_touched");
+    check(C > 0 && H > 4 && recv.numel() % H == 0, "bad exchange row geometry");
+    const int G = (int)(recv.numel() / H);
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(gstride >= C && grad.numel() >= (G - 1) * gstride + C, "grad rows out of bounds");
+    check(slot_idx.numel() >= G * C, "slot_idx < G*C");
+    psamd::kv_accumulate_rows(slots.data_ptr(), cap, ptr<int64_t>(slot_idx), ptr<float>(grad),
+                              gstride, ptr<int32_t>(recv), G, H, C, ptr<int64_t>(touched),
+                              ptr<int32_t>(n_touched), touched.numel(), cur_stream());
   });
   m.def("xchg_pack_keys", [](Tensor ukeys, Tensor n_uniq, Tensor off, int64_t C, int kw,
                              int64_t H, Tensor send, optional<Tensor> ovf) {

@@ -300,7 +300,30 @@ __global__ void kv_update_kernel(Slot* __restrict__ slots, int64_t cap,
   }
 }
 
-// Synchronous aggregation: acc += g; first toucher appends the slot to a list.
+// Synchronous aggregation: acc += g; the first toucher of a slot appends it to the
+// touched list (one list atomic per wavefront, not per lane).
+__device__ __forceinline__ void accumulate_one(Slot* __restrict__ slots, int64_t cap, int64_t si,
+                                               float g, bool valid, int64_t* __restrict__ touched,
+                                               int32_t* __restrict__ n_touched,
+                                               int64_t touched_cap) {
+  bool first = false;
+  if (valid && in_range(si, cap) && g == g) {  // NaN mark = filtered entry
+    atomicAdd(&slots[si].acc, g);
+    first = atomicOr(&slots[si].flags, 1u) == 0u;
+  }
+  const uint64_t m = __ballot(first);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(n_touched, (int)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (first) {
+    const int pos = base + (int)__popcll(m & ((1ull << lane) - 1ull));
+    if (pos < touched_cap) touched[pos] = si;
+  }
+}
+
 __global__ void kv_accumulate_kernel(Slot* __restrict__ slots, int64_t cap,
                                      const int64_t* __restrict__ slot_idx,
                                      const float* __restrict__ grad, int64_t n_host,
@@ -308,17 +331,34 @@ __global__ void kv_accumulate_kernel(Slot* __restrict__ slots, int64_t cap,
                                      int64_t* __restrict__ touched, int32_t* __restrict__ n_touched,
                                      int64_t touched_cap) {
   const int64_t n = dev_len(n_dev, n_host);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t si = slot_idx[i];
-    if (!in_range(si, cap)) continue;
-    const float g = grad[i];
-    if (g != g) continue;
-    atomicAdd(&slots[si].acc, g);
-    if (atomicOr(&slots[si].flags, 1u) == 0u) {
-      int pos = atomicAdd(n_touched, 1);
-      if (pos < touched_cap) touched[pos] = si;
-    }
+  // whole wavefronts iterate together (the list append uses a ballot)
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); i0 < n;
+       i0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = i0 + (threadIdx.x & 63);
+    const bool valid = i < n;
+    accumulate_one(slots, cap, valid ? slot_idx[i] : -1, valid ? grad[i] : 0.f, valid, touched,
+                   n_touched, touched_cap);
+  }
+}
+
+// The owner's pushes of one step, all source rows in ONE launch (blockIdx.y = source):
+// row s has ngrads = recv[s*H + 1] gradients at grad[s*gstride + i] for the slots
+// slot_idx[s*C + i] resolved by that source's pull.
+__global__ void kv_accumulate_rows_kernel(Slot* __restrict__ slots, int64_t cap,
+                                          const int64_t* __restrict__ slot_idx,
+                                          const float* __restrict__ grad, int64_t gstride,
+                                          const int32_t* __restrict__ recv, int64_t H, int64_t C,
+                                          int64_t* __restrict__ touched,
+                                          int32_t* __restrict__ n_touched, int64_t touched_cap) {
+  const int s = blockIdx.y;
+  const int64_t n = dev_len(recv + (int64_t)s * H + 1, C);
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); i0 < n;
+       i0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = i0 + (threadIdx.x & 63);
+    const bool valid = i < n;
+    accumulate_one(slots, cap, valid ? slot_idx[(int64_t)s * C + i] : -1,
+                   valid ? grad[(int64_t)s * gstride + i] : 0.f, valid, touched, n_touched,
+                   touched_cap);
   }
 }
 
@@ -447,6 +487,16 @@ void kv_accumulate(void* slots, int64_t cap, const int64_t* slot_idx, const floa
                    int64_t touched_cap, hipStream_t st) {
   kv_accumulate_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, cap, slot_idx, grad, n,
                                                          n_dev, touched, n_touched, touched_cap);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void kv_accumulate_rows(void* slots, int64_t cap, const int64_t* slot_idx, const float* grad,
+                        int64_t gstride, const int32_t* recv, int G, int64_t H, int64_t C,
+                        int64_t* touched, int32_t* n_touched, int64_t touched_cap,
+                        hipStream_t st) {
+  dim3 grid(grid_for(C, 256, 1024), G);
+  kv_accumulate_rows_kernel<<<grid, 256, 0, st>>>((Slot*)slots, cap, slot_idx, grad, gstride, recv,
+                                                  H, C, touched, n_touched, touched_cap);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -347,11 +347,14 @@ class SparseLRTrainer:
             grads = [rows[s][g0:g0 + C].view(torch.float32) for s in range(G)]
         if self.gpu:
             hh = hipops()
-            if self.cfg.push_mode == "aggregate":
+            if self.cfg.push_mode == "aggregate":  # all source rows: 2 launches, any G
                 xc.n_touched.zero_()
-                for s in range(G):
-                    hh.kv_accumulate(self.table.slots, xc.slot[s * C:(s + 1) * C], grads[s],
-                                     rows[s][1:2], xc.touched, xc.n_touched)
+                if xc.nb:
+                    gsrc, gstride = xc.gin, C
+                else:
+                    gsrc, gstride = xc.recv.view(torch.float32)[g0:], H
+                hh.kv_accumulate_rows(self.table.slots, xc.slot, gsrc, gstride, xc.recv, H, C,
+                                      xc.touched, xc.n_touched)
                 hh.kv_apply_accumulated(self.table.slots, xc.touched, xc.n_touched,
                                         *self.rule.args(), self.stats)
             else:

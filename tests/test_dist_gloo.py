@@ -95,12 +95,49 @@ def test_two_rank_training_matches_protocol_reference(tmp_path, ff_bytes, exchan
     assert worst < tol, worst
 
 
-def test_two_rank_aggregate_mode(tmp_path):
-    cfg_kw = dict(num_features=1 << 20, minibatch=64, table_capacity=1 << 15,
-                  push_mode="aggregate", algo="sgd", lr_type="constant", alpha=0.1, l1=0.0,
-                  l2=0.0)
-    res = _run(tmp_path, cfg_kw, steps=2)
-    assert all(r["progress"]["loss"] > 0 for r in res)
+def _reference_aggregate(cfg_kw, steps, world):
+    """Protocol simulation of push_mode="aggregate": every worker pulls the same model,
+    the owner sums the workers' gradients per key and applies one update."""
+    from parameter_server_amd.models import SparseLRConfig
+    from parameter_server_amd.ops import KVTable, linear_backward, linear_forward, localize_torch
+    from parameter_server_amd.ops.keymix import unmix
+    from parameter_server_amd.ops.synthetic import criteo_batch
+
+    cfg = SparseLRConfig(**cfg_kw)
+    t = KVTable(1 << 16)
+    rule = cfg.update_rule()
+    for s in range(steps):
+        slots, grads = [], []
+        for r in range(world):
+            k, l = criteo_batch(cfg.minibatch, seed=100 + r, row0=s * cfg.minibatch,
+                                num_features=cfg.num_features, cards=[200] * 26)
+            loc = localize_torch(k, 20)
+            slot, w = t.resolve(loc.uniq)
+            _, coef, _ = linear_forward(loc.local_col, w, l, B=cfg.minibatch, width=39)
+            g, _ = linear_backward(loc, coef, B=cfg.minibatch, width=39)
+            slots.append(slot)
+            grads.append(g.clone())
+        su, inv = torch.unique(torch.cat(slots), return_inverse=True)
+        g = torch.zeros(su.numel()).index_add_(0, inv, torch.cat(grads))
+        t.update(su, g, rule)
+    k, w, _, _ = t.occupied()
+    return dict(zip(unmix(k, 20).tolist(), w.tolist()))
+
+
+@pytest.mark.parametrize("exchange,world,ff", [("padded", 2, 0), ("exact", 2, 0), ("padded", 3, 0),
+                                               ("padded", 2, 3)])
+def test_aggregate_mode_matches_protocol_reference(tmp_path, exchange, world, ff):
+    cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
+                  push_mode="aggregate", exchange=exchange, fixing_float_bytes=ff)
+    res = _run(tmp_path, cfg_kw, world=world)
+    merged = {}
+    for r in res:
+        for k, w in zip(r["state"]["keys"].tolist(), r["state"]["w"].tolist()):
+            merged[k] = w
+    ref = _reference_aggregate(cfg_kw, 4, world)
+    assert merged.keys() == ref.keys()
+    tol = 1e-5 if ff == 0 else 2e-3
+    assert max(abs(merged[k] - ref[k]) for k in ref) < tol
 
 
 def test_padded_exchange_overflow_is_loud(tmp_path):

@@ -103,3 +103,24 @@ def test_bench_two_rank_rehearsal_json(tmp_path, exchange):
     assert out["n_gpus"] == 2 and out["steps"] == 4 and out["config"]["global_batch"] == 8192
     assert out["value"] > 0 and 0.3 < out["train"]["loss"] < 1.0
     assert out["config"]["hip_graph"] == (exchange == "padded")
+
+
+@pytest.mark.parametrize("exchange,ff", [("padded", 0), ("padded", 3), ("exact", 0)])
+def test_two_rank_gpu_aggregate_push_matches_reference(tmp_path, exchange, ff):
+    """push_mode="aggregate": one launch accumulates every source row into the slots,
+    one launch applies the summed gradient (KVBufferedVector semantics)."""
+    from test_dist_gloo import _reference_aggregate
+
+    cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
+                  push_mode="aggregate", exchange=exchange, fixing_float_bytes=ff)
+    port = _free_port()
+    mp.spawn(_gpu_worker, args=(2, port, str(tmp_path), cfg_kw, 4, False), nprocs=2, join=True)
+    res = [torch.load(tmp_path / f"g{r}.pt", weights_only=False) for r in range(2)]
+    merged = {}
+    for r in res:
+        for k, w in zip(r["state"]["keys"].tolist(), r["state"]["w"].tolist()):
+            merged[k] = w
+    ref = _reference_aggregate(cfg_kw, 4, 2)
+    assert merged.keys() == ref.keys()
+    tol = 1e-5 if ff == 0 else 2e-3
+    assert max(abs(merged[k] - ref[k]) for k in ref) < tol
