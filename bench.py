@@ -66,16 +66,29 @@ def pipeline(tr, B, N, seed, keys, labels, device, args):
 
     def segments(buf):
         k, lab = bufs[buf]
-        return tr.step_segments(k, lab, width=39, loc=locs[buf])
+        return tr.step_segments(k, lab, width=39, loc=locs[buf], parity=buf)
 
-    def run_segments(buf):
-        for _, fn in segments(buf):
+    # SSP pipelining (N > 1, exchange_lag 1): the exchange half of step t+1 (pack,
+    # RCCL all-to-all, owner update + resolve, all-to-all) runs on its own stream
+    # while the worker half of step t (forward, backward) runs on the main stream
+    split = tr.padded and tr.lag == 1
+    ncut = tr.EXCHANGE_SEGMENTS if split else 0
+    comm_s = torch.cuda.Stream(device) if split else main
+
+    def run(fns):
+        for fn in fns:
             fn()
 
+    def halves(buf):
+        segs = [fn for _, fn in segments(buf)]
+        return segs[:ncut], segs[ncut:]
+
     preps = [lambda: prep(0), lambda: prep(1)]
-    steps_fn = [lambda: run_segments(0), lambda: run_segments(1)]
+    xfns = [lambda: run(halves(0)[0]), lambda: run(halves(1)[0])]
+    wfns = [lambda: run(halves(0)[1]), lambda: run(halves(1)[1])]
     ev_step = torch.cuda.Event()
     ev_prep = [torch.cuda.Event(), torch.cuda.Event()]
+    ev_x = [torch.cuda.Event(), torch.cuda.Event()]
     state = {"t": 0}
 
     def iterate():
@@ -85,8 +98,15 @@ def pipeline(tr, B, N, seed, keys, labels, device, args):
         with torch.cuda.stream(side):
             preps[nxt]()
             ev_prep[nxt].record(side)
-        main.wait_event(ev_prep[cur])         # minibatch t is localised
-        steps_fn[cur]()
+        if split:  # exchange of step t+1 (needs minibatch t+1 and grads(t-1))
+            comm_s.wait_event(ev_prep[nxt])
+            with torch.cuda.stream(comm_s):
+                xfns[nxt]()
+                ev_x[nxt].record(comm_s)
+            main.wait_event(ev_x[cur])        # exchange of step t done
+        else:
+            main.wait_event(ev_prep[cur])     # minibatch t is localised
+        wfns[cur]()
         ev_step.record(main)
         state["t"] = t + 1
 
@@ -94,12 +114,17 @@ def pipeline(tr, B, N, seed, keys, labels, device, args):
     with torch.cuda.stream(side):
         prep(0)
         ev_prep[0].record(side)
+    if split:
+        comm_s.wait_event(ev_prep[0])
+        with torch.cuda.stream(comm_s):
+            xfns[0]()
+            ev_x[0].record(comm_s)
     for _ in range(max(2, args.warmup + args.warmup % 2)):
         iterate()
     if not args.graph:
         return iterate, False
     torch.cuda.synchronize()
-    gp, plans = [], []
+    gp, xplans, wplans = [], [], []
     for i in range(2):  # t is even here: parity i <-> bufs[i]
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
@@ -114,17 +139,14 @@ def pipeline(tr, B, N, seed, keys, labels, device, args):
                 plan.append(g.replay)
             else:
                 plan.append(fn)
-        plans.append(plan)
+        xplans.append(plan[:ncut])
+        wplans.append(plan[ncut:])
     # capture recorded prep(0), prep(1), step(0), step(1) without running them; the
-    # workspace of minibatch t (even) still holds its eager localisation, so the
-    # replays continue from there
-
-    def replay(plan):
-        for fn in plan:
-            fn()
-
+    # workspace of minibatch t (even) still holds its eager localisation (and with
+    # the split, the eager exchange of step t), so the replays continue from there
     preps[:] = [gp[0].replay, gp[1].replay]
-    steps_fn[:] = [lambda: replay(plans[0]), lambda: replay(plans[1])]
+    xfns[:] = [lambda: run(xplans[0]), lambda: run(xplans[1])]
+    wfns[:] = [lambda: run(wplans[0]), lambda: run(wplans[1])]
     torch.cuda.synchronize()
     for _ in range(2):
         iterate()

@@ -79,6 +79,11 @@ class SparseLRConfig:
     exchange: str = "padded"
     exchange_capacity: int = 0           # keys per peer per step; 0 = auto (first step)
     exchange_slack: float = 1.5          # auto capacity = slack * max per-peer count + 1024
+    # padded exchange pipelining depth: pushes of step t ride the exchange of step
+    # t + 1 + lag, so the exchange of step t+1 can run while step t computes; the
+    # pull of step t then misses at most `lag` steps of pushes (SSP staleness).
+    # -1 = from `consistency` (bsp -> 0, ssp:tau / asp -> 1)
+    exchange_lag: int = -1
     seed: int = 0
 
     def update_rule(self) -> UpdateRule:
@@ -130,6 +135,12 @@ class SparseLRTrainer:
         self.fused = (self.G > 1 and self.filter is None and cfg.fixing_float_bytes == 0
                       and not self.padded)
         self.xc = None  # padded-exchange state (allocated on the first step)
+        lag = cfg.exchange_lag if cfg.exchange_lag >= 0 else (0 if self.tau == 0 else 1)
+        if lag > self.tau:
+            raise ValueError(f"exchange_lag {lag} exceeds the staleness bound {self.tau}")
+        self.lag = int(min(lag, 1))  # parity-double-buffered exchange state: depth <= 1
+        self._xt = 0  # padded steps computed (worker halves run)
+        self._xx = 0  # padded exchanges issued (exchange halves run)
         self.pending = None
         self._prefetch = None
         self.step_count = 0
@@ -227,20 +238,26 @@ class SparseLRTrainer:
 
     # --------------------------------------------- padded exchange (G > 1, default)
     def step_segments(self, keys: torch.Tensor, labels: torch.Tensor, *, width=None,
-                      row_ptr=None, vals=None, rows=None, loc=None):
+                      row_ptr=None, vals=None, rows=None, loc=None, parity=None):
         """The step as an ordered list of ``(kind, fn)``: ``"compute"`` segments are
         pure device work on fixed buffers (capturable in a HIP graph per localisation
         buffer), ``"comm"`` segments are the two equal-split RCCL all-to-alls, and
         ``"host"`` is the host bookkeeping. No segment reads anything back to the host,
         so a step is enqueued without waiting for the GPU.
 
-          compute  owner-split the unique keys, pack [keys(t)] next to [grads(t-1)]
+          compute  owner-split the unique keys, pack [keys(t)] next to [grads(t-1-lag)]
           comm     all-to-all A
-          compute  owner: pushes of t-1 (one optimizer step per source, rank order),
-                   then lookup-or-insert of the pulled keys of t -> weights
+          compute  owner: pushes of t-1-lag (one optimizer step per source, rank
+                   order), then lookup-or-insert of the pulled keys of t -> weights
           comm     all-to-all B (weights back)
-          compute  unpack weights, forward, backward, pack grads(t) for step t+1, AUC
+          compute  unpack weights, forward, backward, pack grads(t), AUC
           host     counters, vector clock
+
+        The first four are the exchange half (``"comm"`` and the compute segments
+        before the last one), the last compute segment is the worker half; with
+        ``lag == 1`` the exchange half of step t+1 may run concurrently with the
+        worker half of step t (bench.py issues them on different streams). Buffers
+        alternate with the step parity (``parity``, default: steps issued % 2).
         """
         if not self.padded:
             return [("compute", lambda: self.step(keys, labels, width=width, row_ptr=row_ptr,
@@ -254,24 +271,33 @@ class SparseLRTrainer:
             rows = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
         if self.xc is None:
             self._xc_setup(loc)
-        xc = self.comm
+        comm, xc = self.comm, self.xc
+        par = self._xt % 2 if parity is None else int(parity) % 2
+        sb = (par - 1 - self.lag) % 2  # send buffer: holds grads(t-1-lag), gets keys(t)
 
         def finish():
             if row_ptr is not None and self.gpu:
                 hipops().csr_rows(row_ptr, rows)
-            self._x_finish(loc, labels, B, width, row_ptr, vals, rows)
+            self._x_finish(loc, labels, B, width, row_ptr, vals, rows, par)
 
         def host():
             self.clock.tick(self.rank, self.step_count)
             self.step_count += 1
+            self._xt += 1
             self.examples += B
 
-        return [("compute", lambda: self._x_pack_keys(loc)),
-                ("comm", lambda: xc.all_to_all_fixed(self.xc.send, self.xc.recv)),
-                ("compute", lambda: self._x_serve(resolve=True)),
-                ("comm", lambda: xc.all_to_all_fixed(self.xc.wsend, self.xc.wrecv)),
+        def exchanged():
+            self._xx += 1
+
+        return [("compute", lambda: self._x_pack_keys(loc, sb, par)),
+                ("comm", lambda: comm.all_to_all_fixed(xc.sends[sb], xc.recv)),
+                ("compute", lambda: self._x_serve(push_par=sb, resolve_par=par)),
+                ("comm", lambda: comm.all_to_all_fixed(xc.wsend, xc.wrecvs[par])),
+                ("host", exchanged),
                 ("compute", finish),
                 ("host", host)]
+
+    EXCHANGE_SEGMENTS = 5  # step_segments()[:5] = exchange half, [5:] = worker half
 
     def _xc_setup(self, loc):
         """Allocate the fixed exchange rows. Capacity C (keys per peer per step) is the
@@ -298,46 +324,52 @@ class SparseLRTrainer:
             C=C, kw=kw, H=H, nb=nb,
             gstage=z32(G * C, torch.float32) if nb else None,
             gin=z32(G * C, torch.float32) if nb else None,
-            send=z32(G * H, torch.int32), recv=z32(G * H, torch.int32),
-            slot=torch.full((G * C,), -1, dtype=torch.int64, device=dev),
-            wsend=z32(G * C, torch.float32), wrecv=z32(G * C, torch.float32),
+            # parity-double-buffered: sends[b] holds grads(t) then keys(t+1+lag);
+            # slots[p] the owner's resolved slots of pull step p (for its push)
+            sends=[z32(G * H, torch.int32) for _ in range(2)], recv=z32(G * H, torch.int32),
+            slots=[torch.full((G * C,), -1, dtype=torch.int64, device=dev) for _ in range(2)],
+            wsend=z32(G * C, torch.float32), wrecvs=[z32(G * C, torch.float32) for _ in range(2)],
             w_local=z32(self.max_nnz, torch.float32), ovf=z32(1, torch.int32),
-            off=z32(G + 1, torch.int64), cur=None,
+            offs=[z32(G + 1, torch.int64) for _ in range(2)], curs=[None, None],
             touched=torch.empty(G * C, dtype=torch.int64, device=dev) if self.gpu else None,
             n_touched=z32(1, torch.int32))
 
-    def _owner_order(self, loc):
+    def _owner_order(self, loc, par: int = 0):
         """(keys in owner order, perm owner-order -> unique id | None, off[G+1])."""
         if getattr(loc, "hashed", False):
-            return self._bucket(loc)
+            return self._bucket(loc, par)
         if self.gpu:
-            off = self.xc.off if self.xc is not None else torch.empty(
+            off = self.xc.offs[par] if self.xc is not None else torch.empty(
                 self.G + 1, dtype=torch.int64, device=self.device)
             hipops().owner_split(loc.uniq, loc.n_uniq, self.part.bounds_on(self.device), off)
             return loc.uniq, None, off
         return loc.uniq, None, self.part.split_sorted(loc.uniq, loc.n_uniq)
 
-    def _x_pack_keys(self, loc):
+    def _x_pack_keys(self, loc, sb: int, par: int):
         xc = self.xc
-        ukeys, perm, off = self._owner_order(loc)
-        xc.cur = (perm, off, loc.n_uniq)
+        ukeys, perm, off = self._owner_order(loc, par)
+        xc.curs[par] = (perm, off, loc.n_uniq)
+        send = xc.sends[sb]
         if self.gpu:
-            hipops().xchg_pack_keys(ukeys, loc.n_uniq, off, xc.C, xc.kw, xc.H, xc.send, xc.ovf)
+            hipops().xchg_pack_keys(ukeys, loc.n_uniq, off, xc.C, xc.kw, xc.H, send, xc.ovf)
             return
         H, C, kw = xc.H, xc.C, xc.kw
         for p in range(self.G):
             a, cnt = int(off[p]), int(off[p + 1] - off[p])
             c = min(cnt, C)
-            xc.send[p * H] = c
+            send[p * H] = c
             xc.ovf += cnt - c
             k = ukeys[a:a + c]
             k32 = k.to(torch.int32) if kw == 1 else k.contiguous().view(torch.int32)
-            xc.send[p * H + 4:p * H + 4 + c * kw] = k32
+            send[p * H + 4:p * H + 4 + c * kw] = k32
 
-    def _x_serve(self, resolve: bool = True):
-        """Owner side: the pushes of the previous step, in source-rank order, then the
-        pulls of this step."""
+    def _x_serve(self, push_par: int, resolve_par: int | None):
+        """Owner side: the pushes carried by this exchange (gradients of the pull step
+        with parity ``push_par``, whose resolved slots are ``slots[push_par]``) in
+        source-rank order, then (``resolve_par`` not None) the pulls of this step."""
         xc, G, H, C, kw = self.xc, self.G, self.xc.H, self.xc.C, self.xc.kw
+        pslot = xc.slots[push_par]
+        resolve = resolve_par is not None
         g0 = 4 + C * kw
         rows = [xc.recv[s * H:(s + 1) * H] for s in range(G)]
         if xc.nb:  # FixingFloat codes -> f32, one launch for all source rows
@@ -353,25 +385,25 @@ class SparseLRTrainer:
                     gsrc, gstride = xc.gin, C
                 else:
                     gsrc, gstride = xc.recv.view(torch.float32)[g0:], H
-                hh.kv_accumulate_rows(self.table.slots, xc.slot, gsrc, gstride, xc.recv, H, C,
+                hh.kv_accumulate_rows(self.table.slots, pslot, gsrc, gstride, xc.recv, H, C,
                                       xc.touched, xc.n_touched)
                 hh.kv_apply_accumulated(self.table.slots, xc.touched, xc.n_touched,
                                         *self.rule.args(), self.stats)
             else:
                 for s in range(G):
-                    hh.kv_update(self.table.slots, xc.slot[s * C:(s + 1) * C], grads[s],
+                    hh.kv_update(self.table.slots, pslot[s * C:(s + 1) * C], grads[s],
                                  rows[s][1:2], *self.rule.args(), self.stats)
             if resolve:
                 it, iv, isd, seed = self.table.init.args()
-                hh.kv_resolve_rows(self.table.slots, xc.recv, H, C, kw, xc.slot, xc.wsend, True,
-                                   it, iv, isd, seed, self.table._err, self.table._inserted,
-                                   self.table.home_base, self.table.home_m)
+                hh.kv_resolve_rows(self.table.slots, xc.recv, H, C, kw, xc.slots[resolve_par],
+                                   xc.wsend, True, it, iv, isd, seed, self.table._err,
+                                   self.table._inserted, self.table.home_base, self.table.home_m)
             return
         parts = []
         for s in range(G):
             ng = int(rows[s][1])
             if ng:
-                parts.append((xc.slot[s * C:s * C + ng], grads[s][:ng]))
+                parts.append((pslot[s * C:s * C + ng], grads[s][:ng]))
         self._apply_pushes(parts)
         if not resolve:
             return
@@ -384,40 +416,40 @@ class SparseLRTrainer:
             else:
                 req = rows[s][4:4 + 2 * nk].contiguous().view(torch.int64)
             slot, w = self.table.resolve(req, insert=True)
-            xc.slot[s * C:s * C + nk] = slot
+            xc.slots[resolve_par][s * C:s * C + nk] = slot
             xc.wsend[s * C:s * C + nk] = w
 
-    def _x_finish(self, loc, labels, B, width, row_ptr, vals, rows):
+    def _x_finish(self, loc, labels, B, width, row_ptr, vals, rows, par: int):
         xc = self.xc
-        perm, off, n_uniq = xc.cur
+        perm, off, n_uniq = xc.curs[par]
+        wrecv, send = xc.wrecvs[par], xc.sends[par]  # grads(t) -> sends[t % 2]
         if self.gpu:
             w_local = xc.w_local[:loc.uniq.numel()]
-            hipops().xchg_unpack_w(xc.wrecv, perm, n_uniq, off, xc.C, w_local)
+            hipops().xchg_unpack_w(wrecv, perm, n_uniq, off, xc.C, w_local)
         else:
             U = int(n_uniq)
             w_local = torch.zeros(max(U, 1), dtype=torch.float32)
             for p in range(self.G):
                 a, c = int(off[p]), min(int(off[p + 1] - off[p]), xc.C)
-                w_local[a:a + c] = xc.wrecv[p * xc.C:p * xc.C + c]
+                w_local[a:a + c] = wrecv[p * xc.C:p * xc.C + c]
         _, coef, _ = linear_forward(loc.local_col, w_local, labels, B=B, width=width or 0,
                                     row_ptr=row_ptr, vals=vals, loss=self.cfg.loss,
                                     coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
         grad, _ = linear_backward(loc, coef, B=B, width=width or 0, rows=rows, vals=vals)
         H, C, kw = xc.H, xc.C, xc.kw
         if xc.nb:
-            self._x_ff_pack(grad[:loc.uniq.numel()], perm, n_uniq, off)
+            self._x_ff_pack(grad[:loc.uniq.numel()], perm, n_uniq, off, send)
         elif self.gpu:
-            hipops().xchg_pack_grads(grad[:loc.uniq.numel()], perm, n_uniq, off, C, kw, H,
-                                     xc.send)
+            hipops().xchg_pack_grads(grad[:loc.uniq.numel()], perm, n_uniq, off, C, kw, H, send)
         else:
             for p in range(self.G):
                 a, c = int(off[p]), min(int(off[p + 1] - off[p]), C)
-                xc.send[p * H + 1] = c
+                send[p * H + 1] = c
                 g0 = p * H + 4 + C * kw
-                xc.send[g0:g0 + c] = grad[a:a + c].contiguous().view(torch.int32)
+                send[g0:g0 + c] = grad[a:a + c].contiguous().view(torch.int32)
         auc_from_hist(self.hist, self.metrics, self.step_dev)
 
-    def _x_ff_pack(self, grad, perm, n_uniq, off):
+    def _x_ff_pack(self, grad, perm, n_uniq, off, send):
         """FixingFloat push (reference fixing_float.h:44-95): per owner row min/max,
         nb-byte stochastic-rounded codes; the device step clock varies the rounding
         bits across graph replays."""
@@ -425,16 +457,16 @@ class SparseLRTrainer:
         seed = (self.cfg.seed * 7919 + 17) & ((1 << 64) - 1)
         if self.gpu:
             hipops().xchg_ff_pack_grads(grad, perm, n_uniq, off, C, kw, H, nb, seed,
-                                        self.step_dev, xc.send, xc.gstage)
+                                        self.step_dev, send, xc.gstage)
             return
         for p in range(self.G):
             a, c = int(off[p]), min(int(off[p + 1] - off[p]), C)
-            xc.send[p * H + 1] = c
+            send[p * H + 1] = c
             g = grad[a:a + c]
             code, mm = ff.encode(g, nb, seed=seed + 1000003 * self.step_count + p)
-            xc.send[p * H + 2:p * H + 4] = mm.view(torch.int32)
+            send[p * H + 2:p * H + 4] = mm.view(torch.int32)
             g0 = p * H + 4 + C * kw
-            words = xc.send[g0:g0 + (C * nb + 3) // 4].view(torch.uint8)
+            words = send[g0:g0 + (C * nb + 3) // 4].view(torch.uint8)
             words[:code.numel()] = code
 
     def _x_ff_decode(self):
@@ -451,20 +483,29 @@ class SparseLRTrainer:
                 xc.gin[s * C:s * C + n] = ff.decode(code, nb, row[2:4].view(torch.float32), n)
 
     def _x_flush(self):
-        """Apply the gradients packed by the last step (a keys-free exchange)."""
+        """Apply the gradients of the last 1 + lag steps (keys-free exchanges, oldest
+        first), so the shards hold every push issued so far."""
         xc = self.xc
-        if self.gpu:
-            hipops().xchg_clear_counts(xc.send, xc.H, True, False)
-        else:
-            for p in range(self.G):
-                xc.send[p * xc.H] = 0
-        self.comm.all_to_all_fixed(xc.send, xc.recv)
-        self._x_serve(resolve=False)
-        if self.gpu:
-            hipops().xchg_clear_counts(xc.send, xc.H, False, True)
-        else:
-            for p in range(self.G):
-                xc.send[p * xc.H + 1] = 0
+        if self.gpu:  # exchange halves may still run on another stream
+            torch.cuda.synchronize(self.device)
+        # exchange s carried grads(s - 1 - lag): pending = steps computed whose grads
+        # no issued exchange has carried yet, oldest first
+        T = self._xt
+        for s in range(max(0, self._xx - 1 - self.lag), T):
+            b = s % 2
+            send = xc.sends[b]
+            if self.gpu:
+                hipops().xchg_clear_counts(send, xc.H, True, False)
+            else:
+                for p in range(self.G):
+                    send[p * xc.H] = 0
+            self.comm.all_to_all_fixed(send, xc.recv)
+            self._x_serve(push_par=b, resolve_par=None)
+            if self.gpu:
+                hipops().xchg_clear_counts(send, xc.H, False, True)
+            else:
+                for p in range(self.G):
+                    send[p * xc.H + 1] = 0
         ovf = int(xc.ovf.item())
         if ovf:
             raise RuntimeError(
@@ -473,17 +514,21 @@ class SparseLRTrainer:
                 f"or exchange_slack higher, or exchange='exact'")
 
     # ------------------------------------------------------- fused exchange (G > 1)
-    def _bucket(self, loc):
+    def _bucket(self, loc, par: int = 0):
         """Owner-group the claim-ordered unique keys of a sort-free localisation:
-        (keys in owner order, perm: owner-order position -> unique id, offsets[G+1])."""
+        (keys in owner order, perm: owner-order position -> unique id, offsets[G+1]).
+        One buffer set per step parity (the padded exchange reads perm / off again in
+        the worker half of the step)."""
         n = loc.uniq.numel()
-        if getattr(self, "_bk", None) is None or self._bk[0].numel() < n:
+        bks = getattr(self, "_bks", None) or [None, None]
+        self._bks = bks
+        if bks[par] is None or bks[par][0].numel() < n:
             dev = loc.uniq.device
-            self._bk = (torch.empty(n, dtype=torch.int64, device=dev),
+            bks[par] = (torch.empty(n, dtype=torch.int64, device=dev),
                         torch.empty(n, dtype=torch.int32, device=dev),
                         torch.empty(128, dtype=torch.int64, device=dev),
                         torch.empty(self.G + 1, dtype=torch.int64, device=dev))
-        keys_out, perm, temp, off = self._bk
+        keys_out, perm, temp, off = bks[par]
         hipops().owner_bucket(loc.uniq, loc.n_uniq, self.part.bounds_on(loc.uniq.device), temp,
                               off, keys_out, perm)
         return keys_out, perm, off

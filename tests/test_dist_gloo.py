@@ -45,9 +45,11 @@ def _run(tmp_path, cfg_kw, steps=4, world=2):
     return [torch.load(tmp_path / f"r{r}.pt", weights_only=False) for r in range(world)]
 
 
-def _reference(cfg_kw, steps, world):
+def _reference(cfg_kw, steps, world, lag=0):
     """Single-process simulation of the protocol: every worker pulls from the same
-    model state, then pushes are applied per worker in rank order."""
+    model state, then pushes are applied per worker in rank order. ``lag`` = 1: the
+    pushes of step s are applied only after the pulls of step s + 1 (SSP, one step
+    of staleness: the padded exchange's pipelined mode)."""
     from parameter_server_amd.models import SparseLRConfig
     from parameter_server_amd.ops import KVTable, linear_backward, linear_forward, localize_torch
     from parameter_server_amd.ops.synthetic import criteo_batch
@@ -56,6 +58,7 @@ def _reference(cfg_kw, steps, world):
     t = KVTable(1 << 16)
     bits = 20
     rule = cfg.update_rule()
+    pending = []
     for s in range(steps):
         pushes = []
         for r in range(world):
@@ -66,6 +69,11 @@ def _reference(cfg_kw, steps, world):
             _, coef, _ = linear_forward(loc.local_col, w, l, B=cfg.minibatch, width=39)
             g, _ = linear_backward(loc, coef, B=cfg.minibatch, width=39)
             pushes.append((slot, g.clone()))
+        pending.append(pushes)
+        while len(pending) > lag:
+            for slot, g in pending.pop(0):
+                t.update(slot, g, rule)
+    for pushes in pending:
         for slot, g in pushes:
             t.update(slot, g, rule)
     k, w, _, _ = t.occupied()
@@ -146,3 +154,22 @@ def test_padded_exchange_overflow_is_loud(tmp_path):
                   exchange="padded", exchange_capacity=64)
     with pytest.raises(Exception, match="overflow"):
         _run(tmp_path, cfg_kw, steps=2)
+
+
+@pytest.mark.parametrize("world,ff", [(2, 0), (3, 0), (2, 3)])
+def test_ssp_pipelined_exchange_matches_stale_reference(tmp_path, world, ff):
+    """consistency ssp:tau -> exchange_lag 1: pulls of step s see pushes through s-2."""
+    cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
+                  consistency="ssp:4", fixing_float_bytes=ff)
+    res = _run(tmp_path, cfg_kw, steps=5, world=world)
+    merged = {}
+    for r in res:
+        for k, w in zip(r["state"]["keys"].tolist(), r["state"]["w"].tolist()):
+            merged[k] = w
+    ref = _reference(cfg_kw, 5, world, lag=1)
+    assert merged.keys() == ref.keys()
+    tol = 1e-5 if ff == 0 else 2e-3
+    assert max(abs(merged[k] - ref[k]) for k in ref) < tol
+    if ff == 0:  # and it differs from the BSP result (the lag is real)
+        bsp = _reference(cfg_kw, 5, world, lag=0)
+        assert max(abs(merged[k] - bsp[k]) for k in ref) > 1e-4
