@@ -179,39 +179,48 @@ linear_bwd_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__
 __global__ void auc_from_hist_kernel(uint32_t* __restrict__ hist, int nbins,
                                      double* __restrict__ metrics,
                                      int64_t* __restrict__ step_counter) {
-  __shared__ double s_neg[256], s_pos[256], s_area[256];
-  const int t = threadIdx.x;  // blockDim.x == 256
+  // Exact integer AUC: 2 * area = sum_b pos_b * (2 * neg_below_b + neg_b) fits u64
+  // (counts <= 2^32). Thread t owns the contiguous bins [t*per, t*per + per); the
+  // cross-thread prefix of negatives is a wave-shuffle scan + 4-wave combine (no
+  // serial loop), and the bins are zeroed for the next (graph-replayed) step.
+  __shared__ unsigned long long s_w[3][4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // blockDim.x == 256
   const int per = (nbins + 255) / 256;
   const int lo = min(nbins, t * per), hi = min(nbins, lo + per);
-  double neg = 0, pos = 0;
+  unsigned long long neg = 0, pos = 0;
   for (int b = lo; b < hi; ++b) { neg += hist[b]; pos += hist[nbins + b]; }
-  s_neg[t] = neg;
-  s_pos[t] = pos;
-  __syncthreads();
-  if (t == 0) {  // exclusive prefix over 256 partials; totals in slot 255 of s_area/s_pos
-    double run = 0, ptot = 0;
-    for (int k = 0; k < 256; ++k) { const double x = s_neg[k]; s_neg[k] = run; run += x; ptot += s_pos[k]; }
-    s_area[0] = run;
-    s_pos[0] = ptot;
+  unsigned long long x = neg;  // inclusive wave scan of negatives
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned long long y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
   }
+  const unsigned long long wpos = wave_sum(pos);
+  if (lane == 63) s_w[0][w] = x;
+  if (lane == 0) s_w[1][w] = wpos;
   __syncthreads();
-  const double Ntot = s_area[0], Ptot = s_pos[0];
-  __syncthreads();
-  double below = s_neg[t], area = 0;
+  unsigned long long before = 0, Ntot = 0, Ptot = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q < w) before += s_w[0][q];
+    Ntot += s_w[0][q];
+    Ptot += s_w[1][q];
+  }
+  unsigned long long below = before + x - neg, area2 = 0;
   for (int b = lo; b < hi; ++b) {
-    const double nb = hist[b], pb = hist[nbins + b];
-    area += pb * (below + 0.5 * nb);
+    const unsigned long long nb = hist[b], pb = hist[nbins + b];
+    area2 += pb * (2 * below + nb);
     below += nb;
     hist[b] = 0;
     hist[nbins + b] = 0;
   }
-  s_area[t] = area;
+  area2 = wave_sum(area2);
+  if (lane == 0) s_w[2][w] = area2;
   __syncthreads();
   if (t == 0) {
-    double A = 0;
-    for (int k = 0; k < 256; ++k) A += s_area[k];
+    const unsigned long long A2 = s_w[2][0] + s_w[2][1] + s_w[2][2] + s_w[2][3];
     if (Ptot > 0 && Ntot > 0) {
-      metrics[3] += A / (Ptot * Ntot);
+      metrics[3] += 0.5 * (double)A2 / ((double)Ptot * (double)Ntot);
       metrics[4] += 1.0;
     }
     if (step_counter) *step_counter += 1;  // device step clock (graph-replay safe)
@@ -309,7 +318,8 @@ void linear_fwd(const int64_t* row_ptr, int64_t B, int width, const int32_t* loc
                 hipStream_t st) {
   const size_t lds = hist ? (size_t)2 * nbins * sizeof(uint32_t) : 0;
   constexpr int kLPR = 8;
-  // cap the grid: each block zeroes and flushes a 2*nbins LDS histogram
+  // cap the grid: each block zeroes and scans a 2*nbins LDS histogram (measured: a
+  // 2048-block grid makes that the bottleneck, 90 us vs 37 us at 512 blocks)
   const int g = grid_for(B * kLPR, 256, 512);
   if (row_ptr)
     linear_fwd_kernel<true, kLPR><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
