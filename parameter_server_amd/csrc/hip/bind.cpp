@@ -23,7 +23,7 @@ void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int,
                      hipStream_t);
 // fm.hip
 void fm_fwd_bwd(const void*, const float*, int64_t, int, int, const int32_t*, const float*, int64_t,
-                const float*, float*, void*, double*, uint32_t*, int, hipStream_t);
+                const float*, float*, void*, double*, uint32_t*, int, int, hipStream_t);
 void fm_l2(float*, const void*, const int64_t*, int64_t, const int32_t*, int64_t, int, float,
            hipStream_t);
 // tileloc.hip
@@ -52,11 +52,11 @@ void kv_gather(const void*, int64_t, const int64_t*, int64_t, const int32_t*, fl
 void kv_set(void*, int64_t, const int64_t*, int64_t, const float*, const float*, const float*,
             hipStream_t);
 void kv_update(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int, int,
-               float, float, float, float, float, float, double*, hipStream_t);
+               float, float, float, float, float, float, double*, int, hipStream_t);
 void kv_accumulate(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int64_t*,
                    int32_t*, int64_t, hipStream_t);
 void kv_apply_accumulated(void*, int64_t, const int64_t*, const int32_t*, int64_t, int, int, float,
-                          float, float, float, float, float, double*, hipStream_t);
+                          float, float, float, float, float, double*, int, hipStream_t);
 void kv_census(const void*, int64_t, unsigned long long*, hipStream_t);
 // localize.hip
 void mix_iota(const uint64_t*, int64_t, KeyMix, uint64_t*, int32_t*, hipStream_t);
@@ -81,7 +81,8 @@ void localize32(const uint64_t*, int64_t, KeyMix, void*, size_t, uint32_t*, int3
                 uint64_t*, int32_t*, int32_t*, int32_t*, float*, float*, int, hipStream_t);
 // linear.hip
 void linear_fwd(const int64_t*, int64_t, int, const int32_t*, const float*, const float*, int64_t,
-                const float*, int, float*, float*, float*, double*, uint32_t*, int, hipStream_t);
+                const float*, int, float*, float*, float*, double*, uint32_t*, int, int,
+                hipStream_t);
 void linear_bwd(const int32_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
                 const float*, int64_t, const float*, float*, float*, int64_t, hipStream_t);
 void auc_from_hist(uint32_t*, int, double*, int64_t*, hipStream_t);
@@ -123,7 +124,7 @@ void emb_update(const int64_t*, int64_t, const int32_t*, int64_t, const float*, 
                 float*, int, float, float, hipStream_t);
 void wd_head(const void*, int64_t, int, const float*, const float*, const float*, int64_t,
              const int32_t*, int, const float*, float*, void*, float*, float*, double*, uint32_t*,
-             int, hipStream_t);
+             int, int, hipStream_t);
 void colsum_bf16(const void*, int64_t, int, float*, hipStream_t);
 void adam_update(float*, const float*, float*, float*, int64_t, float, float, float, float, float,
                  float, float, void*, hipStream_t);
@@ -199,6 +200,14 @@ psamd::KeyMix make_keymix(int bits) {
   return m;
 }
 
+// Stripe count of a contended-accumulator buffer (common.cuh acc_stripe).
+int acc_stripes_of(const Tensor& t) {
+  return t.numel() >= psamd::kAccStripes * psamd::kAccStride ? psamd::kAccStripes : 1;
+}
+int acc_stripes_of(const optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? acc_stripes_of(*t) : 1;
+}
+
 int64_t slot_capacity(const Tensor& slots) {
   chk(slots, at::kLong, "slots");
   check(slots.dim() == 2 && slots.size(1) == 4, "slots must be [capacity, 4] int64 (32-B slots)");
@@ -264,7 +273,7 @@ PYBIND11_MODULE(_hipops, m) {
     if (h) check(hist->numel() >= 2 * nbins, "hist too small");
     psamd::fm_fwd_bwd(X0.data_ptr(), v, B, S, D, ptr<int32_t>(local_col), ptr<float>(w_local),
                       w_local.numel(), ptr<float>(labels), ptr<float>(coef), dX0.data_ptr(),
-                      ptr<double>(metrics), h, nbins, cur_stream());
+                      ptr<double>(metrics), h, nbins, acc_stripes_of(metrics), cur_stream());
   });
   m.def("fm_l2", [](Tensor dE, Tensor rows, optional<Tensor> idx, optional<Tensor> n_dev,
                     int64_t u_cap, double lambda) {
@@ -494,7 +503,8 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::kv_update(slots.data_ptr(), cap, ptr<int64_t>(slot_idx), ptr<float>(grad),
                      slot_idx.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"), algo, lr_type,
                      (float)alpha, (float)beta, (float)l1, (float)l2, (float)grad_scale,
-                     (float)max_delta, optr<double>(stats, at::kDouble, "stats"), cur_stream());
+                     (float)max_delta, optr<double>(stats, at::kDouble, "stats"),
+                     acc_stripes_of(stats), cur_stream());
   });
   m.def("kv_accumulate", [](Tensor slots, Tensor slot_idx, Tensor grad, optional<Tensor> n_dev,
                             Tensor touched, Tensor n_touched) {
@@ -518,7 +528,8 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::kv_apply_accumulated(slots.data_ptr(), cap, ptr<int64_t>(touched), ptr<int32_t>(n_touched),
                                 touched.numel(), algo, lr_type, (float)alpha, (float)beta,
                                 (float)l1, (float)l2, (float)grad_scale, (float)max_delta,
-                                optr<double>(stats, at::kDouble, "stats"), cur_stream());
+                                optr<double>(stats, at::kDouble, "stats"), acc_stripes_of(stats),
+                                cur_stream());
   });
   m.def("kv_census", [](Tensor slots) {
     const int64_t cap = slot_capacity(slots);
@@ -727,7 +738,7 @@ PYBIND11_MODULE(_hipops, m) {
     if (mp) check(metrics->numel() >= 5, "metrics needs >= 5 slots");
     psamd::linear_fwd(rp, B, width, ptr<int32_t>(local_col), v, ptr<float>(w_local),
                       w_local.numel(), ptr<float>(labels), loss_type, xp, ptr<float>(coef), c2, mp, hp, nbins,
-                      cur_stream());
+                      acc_stripes_of(metrics), cur_stream());
   });
   m.def("linear_bwd", [](Tensor pos_s, Tensor segid, int64_t n, optional<Tensor> rows, int width,
                          optional<Tensor> vals, Tensor coef, optional<Tensor> coef2, Tensor grad,
@@ -1148,7 +1159,7 @@ PYBIND11_MODULE(_hipops, m) {
                    wide_w.numel(), ptr<int32_t>(local_col), S, ptr<float>(labels),
                    ptr<float>(coef), dh.data_ptr(), ptr<float>(dw), ptr<float>(db),
                    ptr<double>(metrics), reinterpret_cast<uint32_t*>(hist.data_ptr()), nbins,
-                   cur_stream());
+                   acc_stripes_of(metrics), cur_stream());
   });
   m.def("colsum_bf16", [](Tensor x, Tensor out) {
     chk(x, at::kBFloat16, "x");

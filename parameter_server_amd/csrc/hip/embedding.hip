@@ -236,7 +236,7 @@ wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __
                const int32_t* __restrict__ local_col, int S, const float* __restrict__ labels,
                float* __restrict__ coef_out, uint16_t* __restrict__ dh, float* __restrict__ dw,
                float* __restrict__ db, double* __restrict__ metrics, uint32_t* __restrict__ hist,
-               int nbins) {
+               int nbins, int acc_stripes) {
   extern __shared__ uint32_t lhist[];  // [2 * nbins]
   __shared__ float s_dw[512];
   __shared__ double red[16];
@@ -278,9 +278,10 @@ wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __
   const double n = block_sum_f64(cnt, red);
   const double d = block_sum_f64(dbsum, red);
   if (threadIdx.x == 0 && n > 0) {
-    atomicAdd(&metrics[0], a);
-    atomicAdd(&metrics[1], c);
-    atomicAdd(&metrics[2], n);
+    double* mt = acc_stripe(metrics, acc_stripes);
+    atomicAdd(&mt[0], a);
+    atomicAdd(&mt[1], c);
+    atomicAdd(&mt[2], n);
     atomicAdd(db, (float)d);
   }
   __syncthreads();
@@ -380,12 +381,12 @@ void emb_update(const int64_t* slot, int64_t n, const int32_t* n_dev, int64_t ca
 void wd_head(const void* h, int64_t B, int H, const float* w, const float* b, const float* wide_w,
              int64_t wide_cap, const int32_t* local_col, int S, const float* labels,
              float* coef, void* dh, float* dw, float* db, double* metrics, uint32_t* hist,
-             int nbins, hipStream_t st) {
+             int nbins, int acc_stripes, hipStream_t st) {
   if (B <= 0) return;
   const int blocks = (int)std::min<int64_t>((B + 3) / 4, 1024);
   wd_head_kernel<<<blocks, 256, 2 * nbins * sizeof(uint32_t), st>>>(
       reinterpret_cast<const uint16_t*>(h), B, H, w, b, wide_w, wide_cap, local_col, S, labels,
-      coef, reinterpret_cast<uint16_t*>(dh), dw, db, metrics, hist, nbins);
+      coef, reinterpret_cast<uint16_t*>(dh), dw, db, metrics, hist, nbins, acc_stripes);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -34,7 +34,7 @@ fm_fwd_bwd_kernel(const uint16_t* __restrict__ X0, const float* __restrict__ val
                   const float* __restrict__ w_local, int64_t w_cap,
                   const float* __restrict__ labels, float* __restrict__ coef_out,
                   uint16_t* __restrict__ dX0, double* __restrict__ metrics,
-                  uint32_t* __restrict__ hist, int nbins) {
+                  uint32_t* __restrict__ hist, int nbins, int acc_stripes) {
   extern __shared__ uint32_t lhist[];  // [2*nbins]
   __shared__ double lds[16];
   for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) lhist[i] = 0;
@@ -96,9 +96,10 @@ fm_fwd_bwd_kernel(const uint16_t* __restrict__ X0, const float* __restrict__ val
     const double c = block_sum_f64(corr_acc, lds);
     const double n = block_sum_f64(cnt, lds);
     if (threadIdx.x == 0 && n > 0) {
-      atomicAdd(&metrics[0], a);
-      atomicAdd(&metrics[1], c);
-      atomicAdd(&metrics[2], n);
+      double* mt = acc_stripe(metrics, acc_stripes);
+      atomicAdd(&mt[0], a);
+      atomicAdd(&mt[1], c);
+      atomicAdd(&mt[2], n);
     }
   }
   if (hist) {
@@ -127,11 +128,11 @@ __global__ void fm_l2_kernel(float* __restrict__ dE, const uint16_t* __restrict_
 void fm_fwd_bwd(const void* X0, const float* vals, int64_t B, int S, int D,
                 const int32_t* local_col, const float* w_local, int64_t w_cap, const float* labels,
                 float* coef, void* dX0, double* metrics, uint32_t* hist, int nbins,
-                hipStream_t st) {
+                int acc_stripes, hipStream_t st) {
   const int g = grid_for(B * 64, 256, 4096);
   fm_fwd_bwd_kernel<<<g, 256, hist ? 2 * nbins * sizeof(uint32_t) : 0, st>>>(
       (const uint16_t*)X0, vals, B, S, D, local_col, w_local, w_cap, labels, coef,
-      (uint16_t*)dX0, metrics, hist, hist ? nbins : 0);
+      (uint16_t*)dX0, metrics, hist, hist ? nbins : 0, acc_stripes);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -270,7 +270,7 @@ __global__ void kv_update_kernel(Slot* __restrict__ slots, int64_t cap,
                                  const int64_t* __restrict__ slot_idx,
                                  const float* __restrict__ grad, int64_t n_host,
                                  const int32_t* __restrict__ n_dev, UpdateParams p,
-                                 double* __restrict__ stats) {
+                                 double* __restrict__ stats, int acc_stripes) {
   __shared__ double lds[16];
   const int64_t n = dev_len(n_dev, n_host);
   double dnnz = 0, wsum = 0, dsum = 0;
@@ -293,9 +293,10 @@ __global__ void kv_update_kernel(Slot* __restrict__ slots, int64_t cap,
     double b = block_sum_f64(wsum, lds);
     double c = block_sum_f64(dsum, lds);
     if (threadIdx.x == 0) {
-      if (a != 0) atomicAdd(&stats[0], a);
-      if (b != 0) atomicAdd(&stats[1], b);
-      if (c != 0) atomicAdd(&stats[2], c);
+      double* st = acc_stripe(stats, acc_stripes);
+      if (a != 0) atomicAdd(&st[0], a);
+      if (b != 0) atomicAdd(&st[1], b);
+      if (c != 0) atomicAdd(&st[2], c);
     }
   }
 }
@@ -365,7 +366,8 @@ __global__ void kv_accumulate_rows_kernel(Slot* __restrict__ slots, int64_t cap,
 __global__ void kv_apply_accumulated_kernel(Slot* __restrict__ slots, int64_t cap,
                                             const int64_t* __restrict__ touched,
                                             const int32_t* __restrict__ n_touched, int64_t max_n,
-                                            UpdateParams p, double* __restrict__ stats) {
+                                            UpdateParams p, double* __restrict__ stats,
+                                            int acc_stripes) {
   __shared__ double lds[16];
   const int64_t n = dev_len(n_touched, max_n);
   double dnnz = 0, wsum = 0, dsum = 0;
@@ -389,9 +391,10 @@ __global__ void kv_apply_accumulated_kernel(Slot* __restrict__ slots, int64_t ca
     double b = block_sum_f64(wsum, lds);
     double c = block_sum_f64(dsum, lds);
     if (threadIdx.x == 0) {
-      if (a != 0) atomicAdd(&stats[0], a);
-      if (b != 0) atomicAdd(&stats[1], b);
-      if (c != 0) atomicAdd(&stats[2], c);
+      double* st = acc_stripe(stats, acc_stripes);
+      if (a != 0) atomicAdd(&st[0], a);
+      if (b != 0) atomicAdd(&st[1], b);
+      if (c != 0) atomicAdd(&st[2], c);
     }
   }
 }
@@ -475,10 +478,11 @@ void kv_set(void* slots, int64_t cap, const int64_t* slot_idx, int64_t n, const 
 
 void kv_update(void* slots, int64_t cap, const int64_t* slot_idx, const float* grad, int64_t n,
                const int32_t* n_dev, int algo, int lr_type, float alpha, float beta, float l1,
-               float l2, float grad_scale, float max_delta, double* stats, hipStream_t st) {
+               float l2, float grad_scale, float max_delta, double* stats, int acc_stripes,
+               hipStream_t st) {
   UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
   kv_update_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, cap, slot_idx, grad, n, n_dev,
-                                                     p, stats);
+                                                     p, stats, acc_stripes);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
@@ -502,11 +506,12 @@ void kv_accumulate_rows(void* slots, int64_t cap, const int64_t* slot_idx, const
 
 void kv_apply_accumulated(void* slots, int64_t cap, const int64_t* touched, const int32_t* n_touched,
                           int64_t max_n, int algo, int lr_type, float alpha, float beta, float l1,
-                          float l2, float grad_scale, float max_delta, double* stats,
+                          float l2, float grad_scale, float max_delta, double* stats, int acc_stripes,
                           hipStream_t st) {
   UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
   kv_apply_accumulated_kernel<<<grid_for(max_n, 256), 256, 0, st>>>((Slot*)slots, cap, touched,
-                                                                    n_touched, max_n, p, stats);
+                                                                    n_touched, max_n, p, stats,
+                                                                    acc_stripes);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -25,6 +25,50 @@ __device__ __forceinline__ float softplus(float x) {
   return x > 20.f ? x : (x < -20.f ? expf(x) : log1pf(expf(x)));
 }
 
+// Loss, dL/dm, accuracy and AUC bin of one example with margin m (lane-group leader).
+__device__ __forceinline__ void fwd_row_epilogue(int64_t r, float m, const float* __restrict__ labels,
+                                                 int loss_type, float* __restrict__ xw_out,
+                                                 float* __restrict__ coef_out,
+                                                 float* __restrict__ coef2_out, uint32_t* lhist,
+                                                 int nbins, double& loss_acc, double& corr_acc,
+                                                 double& cnt) {
+  const float y = labels[r] > 0.f ? 1.f : -1.f;
+  const float ym = y * m;
+  float loss, coef, coef2;
+  switch (loss_type) {
+    case kSquare: {
+      const float d = m - labels[r];
+      loss = 0.5f * d * d; coef = d; coef2 = 1.f;
+      break;
+    }
+    case kHinge:
+      loss = fmaxf(0.f, 1.f - ym); coef = ym < 1.f ? -y : 0.f; coef2 = 0.f;
+      break;
+    case kSquareHinge: {
+      const float h = fmaxf(0.f, 1.f - ym);
+      loss = h * h; coef = -2.f * y * h; coef2 = ym < 1.f ? 2.f : 0.f;
+      break;
+    }
+    default: {  // logit: tau = 1/(1+exp(y m))
+      loss = softplus(-ym);
+      const float tau = 1.f / (1.f + expf(ym));
+      coef = -y * tau; coef2 = tau * (1.f - tau);
+      break;
+    }
+  }
+  if (xw_out) xw_out[r] = m;
+  coef_out[r] = coef;
+  if (coef2_out) coef2_out[r] = coef2;
+  loss_acc += loss;
+  corr_acc += ((y > 0.f) == (m > 0.f)) ? 1.0 : 0.0;  // evaluation.h:55-57
+  cnt += 1.0;
+  if (lhist) {
+    const float p = 1.f / (1.f + expf(-m));
+    const float pb = p == p ? fminf(fmaxf(p * nbins, 0.f), (float)(nbins - 1)) : 0.f;
+    atomicAdd(&lhist[(y > 0.f ? nbins : 0) + (int)pb], 1u);
+  }
+}
+
 template <bool kHasRowPtr, int kLPR>
 __global__ void __launch_bounds__(256)
 linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
@@ -33,7 +77,7 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
                   const float* __restrict__ labels,
                   int loss_type, float* __restrict__ xw_out, float* __restrict__ coef_out,
                   float* __restrict__ coef2_out, double* __restrict__ metrics,
-                  uint32_t* __restrict__ hist, int nbins) {
+                  uint32_t* __restrict__ hist, int nbins, int acc_stripes) {
   // kLPR lanes cooperate on one example (strided over its nnz, then a shuffle
   // reduction), so B = 65536 rows launch 8x more waves than lane-per-row.
   extern __shared__ uint32_t lhist[];  // [2*nbins] when hist != nullptr
@@ -42,59 +86,70 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
     for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) lhist[i] = 0;
     __syncthreads();
   }
+  uint32_t* lh = hist ? lhist : nullptr;
   const int sub = threadIdx.x % kLPR;
   double loss_acc = 0, corr_acc = 0, cnt = 0;
   const int64_t groups_per_grid = ((int64_t)gridDim.x * blockDim.x) / kLPR;
-  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kLPR;
-       r < ((B + groups_per_grid - 1) / groups_per_grid) * groups_per_grid; r += groups_per_grid) {
-    const bool row_ok = r < B;
-    int64_t b = 0, e = 0;
-    if (row_ok) {
-      if (kHasRowPtr) { b = row_ptr[r]; e = row_ptr[r + 1]; }
-      else { b = r * width; e = b + width; }
-    }
-    float m = 0.f;
-    for (int64_t k = b + sub; k < e; k += kLPR) {
-      const int32_t c = local_col[k];
-      if (in_range(c, w_cap)) m += vals ? w_local[c] * vals[k] : w_local[c];
-    }
+  const int64_t g0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kLPR;
+  constexpr int kRows = 4, kPer = 8;  // fixed-width fast path: 4 rows x <= 8 nnz per lane
+  if (!kHasRowPtr && width <= kLPR * kPer) {
+    // every load of kRows rows is issued before any gather and every gather before
+    // the reductions: 2 dependent memory latencies per kRows rows, not 2 per row
+    for (int64_t r0 = g0; r0 < ((B + groups_per_grid * kRows - 1) / (groups_per_grid * kRows)) *
+                                   groups_per_grid * kRows;
+         r0 += groups_per_grid * kRows) {
+      int32_t c[kRows][kPer];
+      float xv[kRows][kPer];
 #pragma unroll
-    for (int off = kLPR / 2; off > 0; off >>= 1) m += __shfl_xor(m, off, 64);
-    if (!row_ok || sub != 0) continue;
-    const float y = labels[r] > 0.f ? 1.f : -1.f;
-    const float ym = y * m;
-    float loss, coef, coef2;
-    switch (loss_type) {
-      case kSquare: {
-        const float d = m - labels[r];
-        loss = 0.5f * d * d; coef = d; coef2 = 1.f;
-        break;
+      for (int q = 0; q < kRows; ++q) {
+        const int64_t r = r0 + q * groups_per_grid;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          const int k = j * kLPR + sub;
+          const bool ok = r < B && k < width;
+          c[q][j] = ok ? local_col[r * width + k] : -1;
+          xv[q][j] = (ok && vals) ? vals[r * width + k] : 1.f;
+        }
       }
-      case kHinge:
-        loss = fmaxf(0.f, 1.f - ym); coef = ym < 1.f ? -y : 0.f; coef2 = 0.f;
-        break;
-      case kSquareHinge: {
-        const float h = fmaxf(0.f, 1.f - ym);
-        loss = h * h; coef = -2.f * y * h; coef2 = ym < 1.f ? 2.f : 0.f;
-        break;
+      float m[kRows];
+#pragma unroll
+      for (int q = 0; q < kRows; ++q) {
+        m[q] = 0.f;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+          if (in_range(c[q][j], w_cap)) m[q] += w_local[c[q][j]] * xv[q][j];
+#pragma unroll
+        for (int off = kLPR / 2; off > 0; off >>= 1) m[q] += __shfl_xor(m[q], off, 64);
       }
-      default: {  // logit: tau = 1/(1+exp(y m))
-        loss = softplus(-ym);
-        const float tau = 1.f / (1.f + expf(ym));
-        coef = -y * tau; coef2 = tau * (1.f - tau);
-        break;
+      if (sub == 0) {
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) {
+          const int64_t r = r0 + q * groups_per_grid;
+          if (r < B)
+            fwd_row_epilogue(r, m[q], labels, loss_type, xw_out, coef_out, coef2_out, lh, nbins,
+                             loss_acc, corr_acc, cnt);
+        }
       }
     }
-    if (xw_out) xw_out[r] = m;
-    coef_out[r] = coef;
-    if (coef2_out) coef2_out[r] = coef2;
-    loss_acc += loss;
-    corr_acc += ((y > 0.f) == (m > 0.f)) ? 1.0 : 0.0;  // evaluation.h:55-57
-    cnt += 1.0;
-    if (hist) {
-      const float p = 1.f / (1.f + expf(-m));
-      const float pb = p == p ? fminf(fmaxf(p * nbins, 0.f), (float)(nbins - 1)) : 0.f;
-      atomicAdd(&lhist[(y > 0.f ? nbins : 0) + (int)pb], 1u);
+  } else {
+    for (int64_t r = g0; r < ((B + groups_per_grid - 1) / groups_per_grid) * groups_per_grid;
+         r += groups_per_grid) {
+      const bool row_ok = r < B;
+      int64_t b = 0, e = 0;
+      if (row_ok) {
+        if (kHasRowPtr) { b = row_ptr[r]; e = row_ptr[r + 1]; }
+        else { b = r * width; e = b + width; }
+      }
+      float m = 0.f;
+      for (int64_t k = b + sub; k < e; k += kLPR) {
+        const int32_t c = local_col[k];
+        if (in_range(c, w_cap)) m += vals ? w_local[c] * vals[k] : w_local[c];
+      }
+#pragma unroll
+      for (int off = kLPR / 2; off > 0; off >>= 1) m += __shfl_xor(m, off, 64);
+      if (!row_ok || sub != 0) continue;
+      fwd_row_epilogue(r, m, labels, loss_type, xw_out, coef_out, coef2_out, lh, nbins, loss_acc,
+                       corr_acc, cnt);
     }
   }
   if (metrics) {
@@ -102,9 +157,10 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
     double c = block_sum_f64(corr_acc, lds);
     double n = block_sum_f64(cnt, lds);
     if (threadIdx.x == 0 && n > 0) {
-      atomicAdd(&metrics[0], a);
-      atomicAdd(&metrics[1], c);
-      atomicAdd(&metrics[2], n);
+      double* mt = acc_stripe(metrics, acc_stripes);
+      atomicAdd(&mt[0], a);
+      atomicAdd(&mt[1], c);
+      atomicAdd(&mt[2], n);
     }
   }
   if (hist) {
@@ -315,7 +371,7 @@ void linear_fwd(const int64_t* row_ptr, int64_t B, int width, const int32_t* loc
                 const float* vals, const float* w_local, int64_t w_cap, const float* labels,
                 int loss_type,
                 float* xw, float* coef, float* coef2, double* metrics, uint32_t* hist, int nbins,
-                hipStream_t st) {
+                int acc_stripes, hipStream_t st) {
   const size_t lds = hist ? (size_t)2 * nbins * sizeof(uint32_t) : 0;
   constexpr int kLPR = 8;
   // cap the grid: each block zeroes and scans a 2*nbins LDS histogram (measured: a
@@ -324,11 +380,11 @@ void linear_fwd(const int64_t* row_ptr, int64_t B, int width, const int32_t* loc
   if (row_ptr)
     linear_fwd_kernel<true, kLPR><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
                                                  w_cap, labels, loss_type, xw, coef, coef2, metrics,
-                                                 hist, nbins);
+                                                 hist, nbins, acc_stripes);
   else
     linear_fwd_kernel<false, kLPR><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
                                                   w_cap, labels, loss_type, xw, coef, coef2, metrics,
-                                                  hist, nbins);
+                                                  hist, nbins, acc_stripes);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

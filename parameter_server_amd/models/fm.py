@@ -30,7 +30,7 @@ import torch
 from ..ops import embedding as E
 from ..ops.keymix import key_bits_for
 from ..ops.kv_table import UpdateRule, next_pow2
-from ..ops.linear import AUC_BINS, auc_from_hist, linear_backward
+from ..ops.linear import AUC_BINS, accum_total, auc_from_hist, linear_backward, new_accum
 from ..ops.localize import Localizer
 from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
@@ -77,8 +77,8 @@ class FMTrainer(EmbeddingPS):
         self.max_nnz = B * S
         self.localizer = Localizer(self.max_nnz, self.bits, dev)
         self.coef = torch.empty(B, dtype=torch.float32, device=dev)
-        self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
-        self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.metrics = new_accum(dev)
+        self.stats = new_accum(dev)
         self.hist = torch.zeros(2 * AUC_BINS, dtype=torch.int32, device=dev)
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
         if self.gpu:
@@ -175,7 +175,7 @@ class FMTrainer(EmbeddingPS):
         return w.reshape(B, S).sum(1) + 0.5 * (s * s - (V * V).sum(1)).sum(1)
 
     def progress(self, reset: bool = True) -> dict:
-        m = self.metrics.clone()
+        m = accum_total(self.metrics)[:8].clone()
         if self.G > 1:
             m = self.comm.all_reduce_(m.to(self.comm.device) if self.comm.backend == "nccl"
                                       else m.cpu())

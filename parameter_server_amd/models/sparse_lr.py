@@ -39,7 +39,8 @@ from ..ops import fixing_float as ff
 from ..ops.countmin import CountMinSketch
 from ..ops.keymix import key_bits_for, unmix
 from ..ops.kv_table import InitRule, KVTable, UpdateRule, next_pow2
-from ..ops.linear import AUC_BINS, auc_from_hist, linear_backward, linear_forward
+from ..ops.linear import (AUC_BINS, accum_total, auc_from_hist, linear_backward, linear_forward,
+                          new_accum)
 from ..ops.localize import Localizer
 from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
@@ -119,8 +120,8 @@ class SparseLRTrainer:
         self.filter = (CountMinSketch(int(cfg.countmin_n), cfg.countmin_k, self.device)
                        if cfg.tail_feature_freq > 0 else None)
         dev = self.device
-        self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
-        self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.metrics = new_accum(dev)  # [loss, correct, n, auc_sum, auc_n, ...] (striped)
+        self.stats = new_accum(dev)    # [nnz delta, sum w^2, sum dw^2] (striped)
         self.hist = torch.zeros(2 * AUC_BINS, dtype=torch.int32, device=dev)
         self.coef = torch.empty(cfg.minibatch, dtype=torch.float32, device=dev)
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)  # device step clock
@@ -732,7 +733,7 @@ class SparseLRTrainer:
         """Merged progress across ranks (reference ISGDScheduler::showProgress, sgd.h:45-80).
         Collective when G > 1 (also applies deferred pushes)."""
         self.flush()
-        m = torch.cat([self.metrics, self.stats]).clone()
+        m = torch.cat([accum_total(self.metrics)[:8], accum_total(self.stats)[:3]])
         if self.G > 1:
             m = self.comm.all_reduce_(m.to(self.comm.device) if self.comm.backend == "nccl"
                                       else m.cpu())
@@ -749,7 +750,7 @@ class SparseLRTrainer:
         }
         if reset:
             self.metrics.zero_()
-            self.stats[1:].zero_()
+            self.stats.view(-1, 16)[:, 1:].zero_()  # keep the cumulative nnz column
         return out
 
     # ------------------------------------------------------------ checkpoint

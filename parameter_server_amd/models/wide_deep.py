@@ -34,7 +34,7 @@ from ..ops import embedding as E
 from ..ops import gemm as GM
 from ..ops.keymix import key_bits_for
 from ..ops.kv_table import UpdateRule, next_pow2
-from ..ops.linear import AUC_BINS, auc_from_hist, linear_backward
+from ..ops.linear import AUC_BINS, accum_total, auc_from_hist, linear_backward, new_accum
 from ..ops.localize import Localizer
 from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
@@ -183,8 +183,8 @@ class WideDeepTrainer(EmbeddingPS):
         self.num_params = P
         # ---- buffers / metrics
         self.coef = torch.empty(B, dtype=torch.float32, device=dev)
-        self.metrics = torch.zeros(8, dtype=torch.float64, device=dev)
-        self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.metrics = new_accum(dev)
+        self.stats = new_accum(dev)
         self.hist = torch.zeros(2 * AUC_BINS, dtype=torch.int32, device=dev)
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
         if self.gpu:
@@ -254,7 +254,7 @@ class WideDeepTrainer(EmbeddingPS):
 
     # ------------------------------------------------------------ progress
     def progress(self, reset: bool = True) -> dict:
-        m = self.metrics.clone()
+        m = accum_total(self.metrics)[:8].clone()
         if self.G > 1:
             m = self.comm.all_reduce_(m.to(self.comm.device) if self.comm.backend == "nccl"
                                       else m.cpu())

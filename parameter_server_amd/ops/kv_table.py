@@ -83,7 +83,10 @@ class KVTable:
         self.gpu = self.device.type == "cuda"
         if self.gpu:
             self._err = torch.zeros(1, dtype=torch.int32, device=self.device)
-            self._inserted = torch.zeros(1, dtype=torch.int32, device=self.device)
+            # no per-wave insert counter on the hot path: one device atomic per wave on a
+            # single address serialises (measured ~50 us of a 55 us resolve at 234k
+            # keys); the occupancy comes from census() when it is needed
+            self._inserted = None
             hipops().kv_init(self.slots)
         else:
             core().kv_init(ptr(self.slots), cap)

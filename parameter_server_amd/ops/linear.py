@@ -18,6 +18,23 @@ from .native import hipops, is_gpu
 LOSS_TYPES = {"square": 1, "logit": 2, "hinge": 3, "square_hinge": 4}
 AUC_BINS = 2048
 
+# Striped float64 accumulators for the per-step loss / accuracy / optimizer stats
+# (csrc/hip/common.cuh acc_stripe): kernels add into stripe blockIdx % 64 (one
+# 128-B line each) instead of one contended address; logical slot k = the sum of
+# element k over the stripes. CPU code adds into stripe 0.
+ACC_STRIPES, ACC_STRIDE = 64, 16
+
+
+def new_accum(device) -> torch.Tensor:
+    return torch.zeros(ACC_STRIPES * ACC_STRIDE, dtype=torch.float64, device=device)
+
+
+def accum_total(t: torch.Tensor) -> torch.Tensor:
+    """Logical [16] view of a striped accumulator (a small tensor is returned as is)."""
+    if t.numel() >= ACC_STRIPES * ACC_STRIDE:
+        return t.view(-1, ACC_STRIDE).sum(0)
+    return t
+
 
 def loss_id(loss) -> int:
     return loss if isinstance(loss, int) else LOSS_TYPES[str(loss).lower()]
