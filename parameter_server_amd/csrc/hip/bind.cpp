@@ -81,11 +81,11 @@ void localize32(const uint64_t*, int64_t, KeyMix, void*, size_t, uint32_t*, int3
                 uint64_t*, int32_t*, int32_t*, int32_t*, float*, float*, int, hipStream_t);
 // linear.hip
 void linear_fwd(const int64_t*, int64_t, int, const int32_t*, const float*, const float*, int64_t,
-                const float*, int, float*, float*, float*, double*, uint32_t*, int, int,
+                const float*, int, float*, float*, float*, double*, uint32_t*, int, int, int,
                 hipStream_t);
 void linear_bwd(const int32_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
                 const float*, int64_t, const float*, float*, float*, int64_t, hipStream_t);
-void auc_from_hist(uint32_t*, int, double*, int64_t*, hipStream_t);
+void auc_from_hist(uint32_t*, int, int, double*, int64_t*, hipStream_t);
 void csr_rows(const int64_t*, int64_t, int32_t*, hipStream_t);
 void criteo_set_cards(const uint32_t*);
 void criteo_gen(uint64_t, int64_t, const int64_t*, int64_t, int64_t, uint64_t, float, uint64_t*,
@@ -738,7 +738,9 @@ PYBIND11_MODULE(_hipops, m) {
     if (mp) check(metrics->numel() >= 5, "metrics needs >= 5 slots");
     psamd::linear_fwd(rp, B, width, ptr<int32_t>(local_col), v, ptr<float>(w_local),
                       w_local.numel(), ptr<float>(labels), loss_type, xp, ptr<float>(coef), c2, mp, hp, nbins,
-                      acc_stripes_of(metrics), cur_stream());
+                      acc_stripes_of(metrics),
+                      hp ? (int)std::max<int64_t>(1, hist->numel() / (2 * nbins)) : 1,
+                      cur_stream());
   });
   m.def("linear_bwd", [](Tensor pos_s, Tensor segid, int64_t n, optional<Tensor> rows, int width,
                          optional<Tensor> vals, Tensor coef, optional<Tensor> coef2, Tensor grad,
@@ -764,7 +766,8 @@ PYBIND11_MODULE(_hipops, m) {
     chk(hist, at::kInt, "hist");
     chk(metrics, at::kDouble, "metrics");
     check(hist.numel() >= 2 * nbins && metrics.numel() >= 5, "auc sizes");
-    psamd::auc_from_hist(ptr<uint32_t>(hist), nbins, ptr<double>(metrics),
+    const int stripes = (int)std::max<int64_t>(1, hist.numel() / (2 * nbins));
+    psamd::auc_from_hist(ptr<uint32_t>(hist), nbins, stripes, ptr<double>(metrics),
                          optr<int64_t>(step_counter, at::kLong, "step_counter"), cur_stream());
   }, py::arg("hist"), py::arg("nbins"), py::arg("metrics"),
      py::arg("step_counter") = py::none());

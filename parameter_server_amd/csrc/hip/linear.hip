@@ -77,7 +77,7 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
                   const float* __restrict__ labels,
                   int loss_type, float* __restrict__ xw_out, float* __restrict__ coef_out,
                   float* __restrict__ coef2_out, double* __restrict__ metrics,
-                  uint32_t* __restrict__ hist, int nbins, int acc_stripes) {
+                  uint32_t* __restrict__ hist, int nbins, int acc_stripes, int hist_stripes) {
   // kLPR lanes cooperate on one example (strided over its nnz, then a shuffle
   // reduction), so B = 65536 rows launch 8x more waves than lane-per-row.
   extern __shared__ uint32_t lhist[];  // [2*nbins] when hist != nullptr
@@ -163,10 +163,11 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
       atomicAdd(&mt[2], n);
     }
   }
-  if (hist) {
+  if (hist) {  // flush into stripe blockIdx % hist_stripes (popular bins are contended)
     __syncthreads();
+    uint32_t* hs = hist + (int64_t)(blockIdx.x % hist_stripes) * 2 * nbins;
     for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x)
-      if (lhist[i]) atomicAdd(&hist[i], lhist[i]);
+      if (lhist[i]) atomicAdd(&hs[i], lhist[i]);
   }
 }
 
@@ -232,7 +233,7 @@ linear_bwd_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__
 
 // Bucketed AUC of one minibatch from its histogram; metrics[3] += auc, metrics[4] += 1.
 // Resets the histogram (so the next step starts clean inside a captured graph).
-__global__ void auc_from_hist_kernel(uint32_t* __restrict__ hist, int nbins,
+__global__ void auc_from_hist_kernel(uint32_t* __restrict__ hist, int nbins, int hist_stripes,
                                      double* __restrict__ metrics,
                                      int64_t* __restrict__ step_counter) {
   // Exact integer AUC: 2 * area = sum_b pos_b * (2 * neg_below_b + neg_b) fits u64
@@ -243,6 +244,16 @@ __global__ void auc_from_hist_kernel(uint32_t* __restrict__ hist, int nbins,
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // blockDim.x == 256
   const int per = (nbins + 255) / 256;
   const int lo = min(nbins, t * per), hi = min(nbins, lo + per);
+  // fold the stripes into stripe 0 (each thread owns its bins in every stripe)
+  for (int sp = 1; sp < hist_stripes; ++sp) {
+    uint32_t* hs = hist + (int64_t)sp * 2 * nbins;
+    for (int b = lo; b < hi; ++b) {
+      hist[b] += hs[b];
+      hist[nbins + b] += hs[nbins + b];
+      hs[b] = 0;
+      hs[nbins + b] = 0;
+    }
+  }
   unsigned long long neg = 0, pos = 0;
   for (int b = lo; b < hi; ++b) { neg += hist[b]; pos += hist[nbins + b]; }
   unsigned long long x = neg;  // inclusive wave scan of negatives
@@ -371,7 +382,7 @@ void linear_fwd(const int64_t* row_ptr, int64_t B, int width, const int32_t* loc
                 const float* vals, const float* w_local, int64_t w_cap, const float* labels,
                 int loss_type,
                 float* xw, float* coef, float* coef2, double* metrics, uint32_t* hist, int nbins,
-                int acc_stripes, hipStream_t st) {
+                int acc_stripes, int hist_stripes, hipStream_t st) {
   const size_t lds = hist ? (size_t)2 * nbins * sizeof(uint32_t) : 0;
   constexpr int kLPR = 8;
   // cap the grid: each block zeroes and scans a 2*nbins LDS histogram (measured: a
@@ -380,11 +391,11 @@ void linear_fwd(const int64_t* row_ptr, int64_t B, int width, const int32_t* loc
   if (row_ptr)
     linear_fwd_kernel<true, kLPR><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
                                                  w_cap, labels, loss_type, xw, coef, coef2, metrics,
-                                                 hist, nbins, acc_stripes);
+                                                 hist, nbins, acc_stripes, hist_stripes);
   else
     linear_fwd_kernel<false, kLPR><<<g, 256, lds, st>>>(row_ptr, B, width, local_col, vals, w_local,
                                                   w_cap, labels, loss_type, xw, coef, coef2, metrics,
-                                                  hist, nbins, acc_stripes);
+                                                  hist, nbins, acc_stripes, hist_stripes);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
@@ -396,9 +407,9 @@ void linear_bwd(const int32_t* pos_s, const int32_t* segid, int64_t n, const int
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void auc_from_hist(uint32_t* hist, int nbins, double* metrics, int64_t* step_counter,
-                   hipStream_t st) {
-  auc_from_hist_kernel<<<1, 256, 0, st>>>(hist, nbins, metrics, step_counter);
+void auc_from_hist(uint32_t* hist, int nbins, int hist_stripes, double* metrics,
+                   int64_t* step_counter, hipStream_t st) {
+  auc_from_hist_kernel<<<1, 256, 0, st>>>(hist, nbins, hist_stripes, metrics, step_counter);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

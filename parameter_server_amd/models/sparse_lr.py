@@ -39,8 +39,8 @@ from ..ops import fixing_float as ff
 from ..ops.countmin import CountMinSketch
 from ..ops.keymix import key_bits_for, unmix
 from ..ops.kv_table import InitRule, KVTable, UpdateRule, next_pow2
-from ..ops.linear import (AUC_BINS, accum_total, auc_from_hist, linear_backward, linear_forward,
-                          new_accum)
+from ..ops.linear import (AUC_BINS, HIST_STRIPES, accum_total, auc_from_hist, linear_backward,
+                          linear_forward, new_accum)
 from ..ops.localize import Localizer
 from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
@@ -122,7 +122,7 @@ class SparseLRTrainer:
         dev = self.device
         self.metrics = new_accum(dev)  # [loss, correct, n, auc_sum, auc_n, ...] (striped)
         self.stats = new_accum(dev)    # [nnz delta, sum w^2, sum dw^2] (striped)
-        self.hist = torch.zeros(2 * AUC_BINS, dtype=torch.int32, device=dev)
+        self.hist = torch.zeros(HIST_STRIPES * 2 * AUC_BINS, dtype=torch.int32, device=dev)
         self.coef = torch.empty(cfg.minibatch, dtype=torch.float32, device=dev)
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)  # device step clock
         if self.gpu:

@@ -23,6 +23,7 @@ AUC_BINS = 2048
 # 128-B line each) instead of one contended address; logical slot k = the sum of
 # element k over the stripes. CPU code adds into stripe 0.
 ACC_STRIPES, ACC_STRIDE = 64, 16
+HIST_STRIPES = 8  # AUC histogram copies (linear_fwd flushes block b into stripe b % 8)
 
 
 def new_accum(device) -> torch.Tensor:
@@ -100,7 +101,7 @@ def linear_forward(local_col, w_local, labels, *, B: int, width: int = 0, row_pt
         p = torch.sigmoid(m)
         b = torch.clamp((p * AUC_BINS).long(), 0, AUC_BINS - 1)
         off = torch.where(labels[:B] > 0, AUC_BINS, 0)
-        hist += torch.bincount(b + off, minlength=2 * AUC_BINS).to(hist.dtype)
+        hist[:2 * AUC_BINS] += torch.bincount(b + off, minlength=2 * AUC_BINS).to(hist.dtype)
     return (xw if xw is not None else m), coef, (coef2 if coef2 is not None else c2)
 
 
@@ -141,8 +142,9 @@ def auc_from_hist(hist: torch.Tensor, metrics: torch.Tensor, step_counter=None):
     if is_gpu(hist):
         hipops().auc_from_hist(hist, AUC_BINS, metrics, step_counter)
         return
-    neg = hist[:AUC_BINS].double()
-    pos = hist[AUC_BINS:].double()
+    h = hist.view(-1, 2 * AUC_BINS).sum(0)  # stripes (CPU code only writes stripe 0)
+    neg = h[:AUC_BINS].double()
+    pos = h[AUC_BINS:].double()
     P, N = float(pos.sum()), float(neg.sum())
     if P > 0 and N > 0:
         below = torch.cumsum(neg, 0) - neg
