@@ -766,7 +766,9 @@ PYBIND11_MODULE(_hipops, m) {
     chk(hist, at::kInt, "hist");
     chk(metrics, at::kDouble, "metrics");
     check(hist.numel() >= 2 * nbins && metrics.numel() >= 5, "auc sizes");
+    check(nbins == 2048, "auc_from_hist: 2048 bins (256 threads x 8)");
     const int stripes = (int)std::max<int64_t>(1, hist.numel() / (2 * nbins));
+    check(stripes <= 8, "auc_from_hist: at most 8 histogram stripes");
     psamd::auc_from_hist(ptr<uint32_t>(hist), nbins, stripes, ptr<double>(metrics),
                          optr<int64_t>(step_counter, at::kLong, "step_counter"), cur_stream());
   }, py::arg("hist"), py::arg("nbins"), py::arg("metrics"),

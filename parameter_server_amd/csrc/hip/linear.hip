@@ -237,25 +237,47 @@ __global__ void auc_from_hist_kernel(uint32_t* __restrict__ hist, int nbins, int
                                      double* __restrict__ metrics,
                                      int64_t* __restrict__ step_counter) {
   // Exact integer AUC: 2 * area = sum_b pos_b * (2 * neg_below_b + neg_b) fits u64
-  // (counts <= 2^32). Thread t owns the contiguous bins [t*per, t*per + per); the
-  // cross-thread prefix of negatives is a wave-shuffle scan + 4-wave combine (no
-  // serial loop), and the bins are zeroed for the next (graph-replayed) step.
+  // (counts <= 2^32). Thread t owns the contiguous bins [t*kPer, t*kPer + kPer) of
+  // every stripe; all stripe loads are issued before any use (one memory latency,
+  // not one per stripe and bin), the stripes are zeroed for the next graph-replayed
+  // step, and the cross-thread prefix is a wave-shuffle scan + 4-wave combine.
+  constexpr int kPer = 8;  // nbins == 256 * kPer (AUC_BINS = 2048), checked on the host
+  constexpr int kMaxStripes = 8;
   __shared__ unsigned long long s_w[3][4];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // blockDim.x == 256
-  const int per = (nbins + 255) / 256;
-  const int lo = min(nbins, t * per), hi = min(nbins, lo + per);
-  // fold the stripes into stripe 0 (each thread owns its bins in every stripe)
-  for (int sp = 1; sp < hist_stripes; ++sp) {
-    uint32_t* hs = hist + (int64_t)sp * 2 * nbins;
-    for (int b = lo; b < hi; ++b) {
-      hist[b] += hs[b];
-      hist[nbins + b] += hs[nbins + b];
-      hs[b] = 0;
-      hs[nbins + b] = 0;
+  const int lo = t * kPer;
+  uint32_t nb[kPer], pb[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) nb[q] = pb[q] = 0;
+  uint4 ln[kMaxStripes][2], lp[kMaxStripes][2];
+#pragma unroll
+  for (int sp = 0; sp < kMaxStripes; ++sp) {
+    if (sp < hist_stripes) {
+      const uint4* hn = reinterpret_cast<const uint4*>(hist + (int64_t)sp * 2 * nbins + lo);
+      const uint4* hp = reinterpret_cast<const uint4*>(hist + (int64_t)sp * 2 * nbins + nbins + lo);
+      ln[sp][0] = hn[0]; ln[sp][1] = hn[1];
+      lp[sp][0] = hp[0]; lp[sp][1] = hp[1];
+    }
+  }
+#pragma unroll
+  for (int sp = 0; sp < kMaxStripes; ++sp) {
+    if (sp < hist_stripes) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        nb[4 * h + 0] += ln[sp][h].x; nb[4 * h + 1] += ln[sp][h].y;
+        nb[4 * h + 2] += ln[sp][h].z; nb[4 * h + 3] += ln[sp][h].w;
+        pb[4 * h + 0] += lp[sp][h].x; pb[4 * h + 1] += lp[sp][h].y;
+        pb[4 * h + 2] += lp[sp][h].z; pb[4 * h + 3] += lp[sp][h].w;
+      }
+      uint4* zn = reinterpret_cast<uint4*>(hist + (int64_t)sp * 2 * nbins + lo);
+      uint4* zp = reinterpret_cast<uint4*>(hist + (int64_t)sp * 2 * nbins + nbins + lo);
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      zn[0] = z; zn[1] = z; zp[0] = z; zp[1] = z;
     }
   }
   unsigned long long neg = 0, pos = 0;
-  for (int b = lo; b < hi; ++b) { neg += hist[b]; pos += hist[nbins + b]; }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) { neg += nb[q]; pos += pb[q]; }
   unsigned long long x = neg;  // inclusive wave scan of negatives
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -274,12 +296,10 @@ __global__ void auc_from_hist_kernel(uint32_t* __restrict__ hist, int nbins, int
     Ptot += s_w[1][q];
   }
   unsigned long long below = before + x - neg, area2 = 0;
-  for (int b = lo; b < hi; ++b) {
-    const unsigned long long nb = hist[b], pb = hist[nbins + b];
-    area2 += pb * (2 * below + nb);
-    below += nb;
-    hist[b] = 0;
-    hist[nbins + b] = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    area2 += (unsigned long long)pb[q] * (2 * below + nb[q]);
+    below += nb[q];
   }
   area2 = wave_sum(area2);
   if (lane == 0) s_w[2][w] = area2;

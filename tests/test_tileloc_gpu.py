@@ -97,3 +97,25 @@ def test_trainer_tile_mode_matches_sort_mode():
     assert torch.equal(res["sort"][0], res["tile"][0])
     assert torch.allclose(res["sort"][1], res["tile"][1], rtol=1e-4, atol=1e-6)
     assert abs(res["sort"][2]["loss"] - res["tile"][2]["loss"]) < 1e-5
+
+
+@pytest.mark.parametrize("hot", [0, 1500, 50000])
+def test_sort_backward_hot_keys_matches_reference(hot):
+    """CSC segmented backward with hot keys: segments spanning hundreds of
+    wavefronts combine their per-wave pieces atomically."""
+    g = torch.Generator().manual_seed(hot + 7)
+    n = 200000
+    k = torch.randint(0, 1 << 30, (n,), generator=g, dtype=torch.int64)
+    if hot:
+        idx = torch.randperm(n, generator=g)[:hot]
+        k[idx] = 12345
+        k[idx[: hot // 3]] = 777  # a second hot key
+    ref = localize_torch(k, 30)
+    loc = Localizer(n, 30, DEV, mode="sort")(k.to(DEV))
+    width = 39
+    B = (n + width - 1) // width
+    coef = torch.randn(B, generator=g)
+    grad, _ = linear_backward(loc, coef.to(DEV), B=B, width=width)
+    U = loc.num_unique()
+    want = _ref_grad(ref, coef, width)
+    assert torch.allclose(grad[:U].double().cpu(), want, rtol=1e-4, atol=1e-3)
