@@ -383,7 +383,9 @@ void wd_head(const void* h, int64_t B, int H, const float* w, const float* b, co
              float* coef, void* dh, float* dw, float* db, double* metrics, uint32_t* hist,
              int nbins, int acc_stripes, hipStream_t st) {
   if (B <= 0) return;
-  const int blocks = (int)std::min<int64_t>((B + 3) / 4, 1024);
+  // 256 blocks (16 examples per wave): every block ends with H + 4 same-address
+  // atomics (dw, db, metrics) that serialise across blocks, so fewer, fuller blocks
+  const int blocks = (int)std::min<int64_t>((B + 3) / 4, 256);
   wd_head_kernel<<<blocks, 256, 2 * nbins * sizeof(uint32_t), st>>>(
       reinterpret_cast<const uint16_t*>(h), B, H, w, b, wide_w, wide_cap, local_col, S, labels,
       coef, reinterpret_cast<uint16_t*>(dh), dw, db, metrics, hist, nbins, acc_stripes);
