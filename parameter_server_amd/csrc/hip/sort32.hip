@@ -14,6 +14,10 @@
 // and stored digit-run contiguous.
 // RLE (unique keys, segment ids, local columns) is fused into 2 kernels + scan.
 // All global indices are bounds-checked.
+// Tried and measured (65,536 x 39 Criteo keys): one-sweep passes with per-digit
+// decoupled look-back (1 global-histogram kernel + 3 scatter passes) were correct
+// but 7.9 ms vs 0.2 ms: with ~600 tiles resident at once every tile walks the
+// predecessors' published counts serially; the reduce-then-scan passes stay.
 #include "common.cuh"
 #include <stdexcept>
 #include <string>
