@@ -345,9 +345,11 @@ __device__ __forceinline__ uint64_t mod_barrett(uint64_t h, uint64_t N, uint64_t
   return r;
 }
 
+// u -> feature id of slot j; for categorical slots cm1 = powf(C_j, 1 - alpha) - 1
+// comes precomputed per block (same device powf, so the same ids as inline).
 __device__ __forceinline__ uint64_t criteo_key(uint64_t seed, uint64_t gr, int j,
                                                uint64_t num_features, uint64_t nf_m,
-                                               float alpha) {
+                                               float alpha, float cm1) {
   const float u = u01(rng64(seed + (uint64_t)j * 0x632be59bd9b4e019ull, gr));
   uint64_t id;
   if (j < 13) {
@@ -355,43 +357,50 @@ __device__ __forceinline__ uint64_t criteo_key(uint64_t seed, uint64_t gr, int j
     const float x = expf(u * 12.f) - 1.f;
     id = (uint64_t)(2.f * log2f(1.f + x));
   } else {
-    const float C = (float)c_cards[j - 13];
     const float oma = 1.f - alpha;
-    const float x = powf((powf(C, oma) - 1.f) * u + 1.f, 1.f / oma);
+    const float x = powf(cm1 * u + 1.f, 1.f / oma);
     uint64_t v = (uint64_t)x;
     id = v >= 1 ? v - 1 : 0;
   }
   return mod_barrett(fmix64(((uint64_t)(j + 1) << 48) ^ id), num_features, nf_m);
 }
 
-// One thread per (row, slot): a 256-thread block generates 6 rows (234 features);
-// per-row planted logits are summed in LDS, then 6 lanes draw the labels.
-constexpr int kGenRows = 6;
-__global__ void __launch_bounds__(256)
+// One thread per (row, slot): a 512-thread block generates 13 rows (507 features,
+// 99% of the lanes); the planted weights of a row are summed in slot order by one
+// lane (no LDS atomics), which then draws the row's label.
+constexpr int kGenRows = 13;
+constexpr int kGenThreads = 512;
+__global__ void __launch_bounds__(kGenThreads)
 criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_dev,
                   int64_t row_scale, int64_t B, uint64_t num_features, uint64_t nf_m,
                   float alpha, uint64_t* __restrict__ keys, float* __restrict__ labels) {
-  __shared__ float logit[kGenRows];
+  __shared__ float spw[kGenRows * 39];
+  __shared__ float s_cm1[26];
   if (row0_dev) row0 += (*row0_dev) * row_scale;
   const int t = threadIdx.x;
-  if (t < kGenRows) logit[t] = -1.2f;
+  if (t < 26) s_cm1[t] = powf((float)c_cards[t], 1.f - alpha) - 1.f;
   __syncthreads();
+  const int lr = t / 39, j = t % 39;
   for (int64_t rb = (int64_t)blockIdx.x * kGenRows; rb < B; rb += (int64_t)gridDim.x * kGenRows) {
-    const int lr = t / 39, j = t % 39;
     const int64_t r = rb + lr;
-    if (lr < kGenRows && r < B) {
-      const uint64_t key = criteo_key(seed, (uint64_t)(row0 + r), j, num_features, nf_m, alpha);
-      keys[r * 39 + j] = key;
-      const float pw = planted_w(key, seed);
-      if (pw != 0.f) atomicAdd(&logit[lr], pw);
+    if (lr < kGenRows) {
+      float pw = 0.f;
+      if (r < B) {
+        const uint64_t key = criteo_key(seed, (uint64_t)(row0 + r), j, num_features, nf_m,
+                                        alpha, j >= 13 ? s_cm1[j - 13] : 0.f);
+        keys[r * 39 + j] = key;
+        pw = planted_w(key, seed);
+      }
+      spw[t] = pw;
     }
     __syncthreads();
     if (t < kGenRows && rb + t < B) {
+      float logit = -1.2f;
+      for (int q = 0; q < 39; ++q) logit += spw[t * 39 + q];
       const int64_t r2 = rb + t;
-      const float p = 1.f / (1.f + expf(-logit[t]));
+      const float p = 1.f / (1.f + expf(-logit));
       const float u = u01(rng64(seed ^ 0xabcdefull, (uint64_t)(row0 + r2)));
       labels[r2] = u < p ? 1.f : -1.f;
-      logit[t] = -1.2f;
     }
     __syncthreads();
   }
@@ -447,7 +456,7 @@ void criteo_gen(uint64_t seed, int64_t row0, const int64_t* row0_dev, int64_t ro
                 hipStream_t st) {
   const int64_t blocks = (B + kGenRows - 1) / kGenRows;
   const uint64_t nf_m = ~0ull / num_features;
-  criteo_gen_kernel<<<(unsigned)(blocks < 65535 ? blocks : 65535), 256, 0, st>>>(
+  criteo_gen_kernel<<<(unsigned)(blocks < 65535 ? blocks : 65535), kGenThreads, 0, st>>>(
       seed, row0, row0_dev, row_scale, B, num_features, nf_m, alpha, keys, labels);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
