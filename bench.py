@@ -32,27 +32,41 @@ METRIC = "examples/sec (whole node) sparse LR 10^9 feats at 1/2/4/8 MI355X"
 ALGO_NAMES = {"ftrl": "FTRL-proximal", "adagrad": "proximal AdaGrad", "sgd": "proximal SGD"}
 
 
-def pipeline_deep(tr, B, N, seed, keys, labels, device, args, nprep=2):
-    """1 GPU: ``nprep`` preparation streams, each generating + localising every
-    nprep-th minibatch into its own workspaces (2 * nprep buffers), so up to nprep
-    latency-bound localisations run concurrently with the training step on the main
-    stream. Minibatch t uses buffer t % (2 * nprep) and prep stream t % nprep; its
-    preparation is issued nprep steps ahead and waits for the step that last used
-    the buffer (step t - nprep). Stream s generates rows (nprep * k + s) * B from its
-    own device counter, so graph replays on different streams never share state.
-    Same accounting as ``pipeline``: the timed region does exactly K generations,
-    K localisations and K steps. Returns (run, graph_used)."""
+def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
+    """Software pipeline over HIP streams (every piece replays from HIP graphs):
+
+    * ``nprep`` high-priority preparation streams: stream s generates and localises
+      every nprep-th minibatch (t % nprep == s) into its own workspaces, issued nprep
+      steps ahead; with 2 * nprep buffers a preparation waits only for the step that
+      last used its buffer. The kernels of a localisation are latency bound, so
+      several run concurrently with the step at little cost (1 GPU, 65,536 x 39 keys:
+      1 stream 0.309 ms/step, 2 -> 0.241, 3 -> 0.230).
+    * main stream: the training step (``SparseLRTrainer.step_segments``, one linear
+      graph per compute segment and buffer; a single multi-stream graph replays
+      much slower on ROCm). N > 1: the padded exchange's two equal-split RCCL
+      all-to-alls run between the graph replays, nothing reads back to the host.
+    * N > 1 with exchange lag 1 (SSP): the exchange half of step t+1 (pack,
+      all-to-all, owner update + resolve, all-to-all) runs on its own stream while
+      the worker half of step t (forward, backward) runs on the main stream.
+
+    Each iteration = one full training step + one full data preparation; the first
+    steps' data is prepared in warm-up and the last iterations' preparations are
+    unused, so the timed region does exactly K generations, K localisations and K
+    steps. Returns (run, graph_used)."""
     from parameter_server_amd.ops.synthetic import criteo_batch
 
-    NB = 2 * nprep
+    NB = 2 * nprep  # even: buffer parity == step parity (the exchange's double buffers)
     main = torch.cuda.current_stream(device)
-    sides = [torch.cuda.Stream(device, priority=-1) for _ in range(nprep)]
+    # preparation stream priority: high on 1 GPU (the preparation is the long pole);
+    # normal next to the SSP exchange stream, which then runs at high priority
+    prio = int(os.environ.get("PSAMD_PREP_PRIORITY", "0" if tr.G > 1 else "-1"))
+    sides = [torch.cuda.Stream(device, priority=prio) for _ in range(nprep)]
     bufs = [(keys, labels)] + [(torch.empty_like(keys), torch.empty_like(labels))
                                for _ in range(NB - 1)]
     ctr = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(nprep)]
     locs = [None] * NB
 
-    def prep(b):  # buffer b belongs to stream b % nprep
+    def prep(b):  # buffer b belongs to prep stream b % nprep (rows (nprep*k + s) * B)
         sidx = b % nprep
         k, lab = bufs[b]
         criteo_batch(B, seed=seed, row0=sidx * B, num_features=N, device=device, keys=k,
@@ -60,28 +74,53 @@ def pipeline_deep(tr, B, N, seed, keys, labels, device, args, nprep=2):
         ctr[sidx].add_(1)
         locs[b] = tr.localize(k, buf=b)
 
-    def step(b):
+    def segments(b):
         k, lab = bufs[b]
-        for _, fn in tr.step_segments(k, lab, width=39, loc=locs[b]):
+        return tr.step_segments(k, lab, width=39, loc=locs[b], parity=b % 2)
+
+    split = tr.padded and tr.lag == 1
+    ncut = tr.EXCHANGE_SEGMENTS if split else 0
+    comm_s = torch.cuda.Stream(device, priority=-1) if split else main
+
+    def run(fns):
+        for fn in fns:
             fn()
 
+    def halves(b):
+        segs = [fn for _, fn in segments(b)]
+        return segs[:ncut], segs[ncut:]
+
     preps = [(lambda b=b: prep(b)) for b in range(NB)]
-    steps_fn = [(lambda b=b: step(b)) for b in range(NB)]
+    xfns = [(lambda b=b: run(halves(b)[0])) for b in range(NB)]
+    wfns = [(lambda b=b: run(halves(b)[1])) for b in range(NB)]
     ev_step = [torch.cuda.Event() for _ in range(NB)]
     ev_prep = [torch.cuda.Event() for _ in range(NB)]
+    ev_x = [torch.cuda.Event() for _ in range(NB)]
     state = {"t": 0}
+
+    def issue_exchange(t):  # exchange half of step t: minibatch t ready, grads(t-2) packed
+        b = t % NB
+        comm_s.wait_event(ev_prep[b])
+        comm_s.wait_event(ev_step[(t - 2) % NB])
+        with torch.cuda.stream(comm_s):
+            xfns[b]()
+            ev_x[b].record(comm_s)
 
     def iterate():
         t = state["t"]
         nb = (t + nprep) % NB                 # minibatch t + nprep
-        s = sides[(t + nprep) % nprep]
-        s.wait_event(ev_step[nb])             # step(t - nprep) done with bufs[nb]
+        s = sides[nb % nprep]
+        s.wait_event(ev_step[nb])             # step(t + nprep - NB) done with bufs[nb]
         with torch.cuda.stream(s):
             preps[nb]()
             ev_prep[nb].record(s)
         cur = t % NB
-        main.wait_event(ev_prep[cur])
-        steps_fn[cur]()
+        if split:
+            issue_exchange(t + 1)
+            main.wait_event(ev_x[cur])        # exchange of step t done
+        else:
+            main.wait_event(ev_prep[cur])     # minibatch t is localised
+        wfns[cur]()
         ev_step[cur].record(main)
         state["t"] = t + 1
 
@@ -91,133 +130,22 @@ def pipeline_deep(tr, B, N, seed, keys, labels, device, args, nprep=2):
         with torch.cuda.stream(sides[b]):
             prep(b)
             ev_prep[b].record(sides[b])
+    if split:
+        issue_exchange(0)
     warm = max(NB, args.warmup + (-args.warmup) % NB)
     for _ in range(warm):
         iterate()
     if not args.graph:
         return iterate, False
     torch.cuda.synchronize()
-    gp, gs = [], []
+    gp, xplans, wplans = [], [], []
     for b in range(NB):  # t % NB == 0 here: buffer b <-> minibatch t + b
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
             prep(b)
         gp.append(g)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
-            step(b)
-        gs.append(g)
-    # capture did not run anything: the workspaces of minibatches t .. t+nprep-1
-    # still hold their eager preparations, so the replays continue from there
-    preps[:] = [g.replay for g in gp]
-    steps_fn[:] = [g.replay for g in gs]
-    torch.cuda.synchronize()
-    for _ in range(NB):
-        iterate()
-    torch.cuda.synchronize()
-    return iterate, True
-
-
-def pipeline(tr, B, N, seed, keys, labels, device, args):
-    """Two-stream software pipeline: while the main stream runs step t (exchange /
-    pull, forward, backward, push of minibatch t), a high-priority side stream
-    generates minibatch t+1 and localises it into the other workspace. prep(t+1)
-    waits for step(t-1) (it overwrites that step's buffers), step(t) waits for
-    prep(t).
-
-    With --graph 1 every pure-device piece replays from a HIP graph: the side
-    stream's prep, and the step's compute segments (``SparseLRTrainer.step_segments``:
-    one linear graph per segment and buffer parity; a single multi-stream graph
-    replays much slower on ROCm). On N > 1 GPUs the step's two equal-split RCCL
-    all-to-alls of the padded exchange run between the graph replays; nothing in
-    the step reads back to the host, so the CPU stays ahead of the GPU.
-    Each iteration = one full training step + one full data preparation; the
-    first timed step's data is prepared in warm-up and the last iteration's
-    preparation is unused, so the timed region does exactly K generations,
-    K localisations and K steps. Returns (run, graph_used)."""
-    from parameter_server_amd.ops.synthetic import criteo_batch
-
-    main = torch.cuda.current_stream(device)
-    side = torch.cuda.Stream(device, priority=-1)
-    bufs = [(keys, labels), (torch.empty_like(keys), torch.empty_like(labels))]
-    gen_step = torch.zeros(1, dtype=torch.int64, device=device)  # minibatches generated
-    locs = [None, None]
-
-    def prep(buf):  # generate minibatch #gen_step into bufs[buf], localise it
-        k, lab = bufs[buf]
-        criteo_batch(B, seed=seed, row0=0, num_features=N, device=device, keys=k, labels=lab,
-                     row0_dev=gen_step, row_scale=B)
-        gen_step.add_(1)
-        locs[buf] = tr.localize(k, buf=buf)
-
-    def segments(buf):
-        k, lab = bufs[buf]
-        return tr.step_segments(k, lab, width=39, loc=locs[buf], parity=buf)
-
-    # SSP pipelining (N > 1, exchange_lag 1): the exchange half of step t+1 (pack,
-    # RCCL all-to-all, owner update + resolve, all-to-all) runs on its own stream
-    # while the worker half of step t (forward, backward) runs on the main stream
-    split = tr.padded and tr.lag == 1
-    ncut = tr.EXCHANGE_SEGMENTS if split else 0
-    comm_s = torch.cuda.Stream(device) if split else main
-
-    def run(fns):
-        for fn in fns:
-            fn()
-
-    def halves(buf):
-        segs = [fn for _, fn in segments(buf)]
-        return segs[:ncut], segs[ncut:]
-
-    preps = [lambda: prep(0), lambda: prep(1)]
-    xfns = [lambda: run(halves(0)[0]), lambda: run(halves(1)[0])]
-    wfns = [lambda: run(halves(0)[1]), lambda: run(halves(1)[1])]
-    ev_step = torch.cuda.Event()
-    ev_prep = [torch.cuda.Event(), torch.cuda.Event()]
-    ev_x = [torch.cuda.Event(), torch.cuda.Event()]
-    state = {"t": 0}
-
-    def iterate():
-        t = state["t"]
-        cur, nxt = t % 2, (t + 1) % 2
-        side.wait_event(ev_step)              # step(t-1) done with bufs[nxt]
-        with torch.cuda.stream(side):
-            preps[nxt]()
-            ev_prep[nxt].record(side)
-        if split:  # exchange of step t+1 (needs minibatch t+1 and grads(t-1))
-            comm_s.wait_event(ev_prep[nxt])
-            with torch.cuda.stream(comm_s):
-                xfns[nxt]()
-                ev_x[nxt].record(comm_s)
-            main.wait_event(ev_x[cur])        # exchange of step t done
-        else:
-            main.wait_event(ev_prep[cur])     # minibatch t is localised
-        wfns[cur]()
-        ev_step.record(main)
-        state["t"] = t + 1
-
-    ev_step.record(main)
-    with torch.cuda.stream(side):
-        prep(0)
-        ev_prep[0].record(side)
-    if split:
-        comm_s.wait_event(ev_prep[0])
-        with torch.cuda.stream(comm_s):
-            xfns[0]()
-            ev_x[0].record(comm_s)
-    for _ in range(max(2, args.warmup + args.warmup % 2)):
-        iterate()
-    if not args.graph:
-        return iterate, False
-    torch.cuda.synchronize()
-    gp, xplans, wplans = [], [], []
-    for i in range(2):  # t is even here: parity i <-> bufs[i]
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
-            prep(i)
-        gp.append(g)
         plan = []
-        for kind, fn in segments(i):  # capture in order: a segment may bake in buffers
+        for kind, fn in segments(b):  # capture in order: a segment may bake in buffers
             if kind == "compute":     # the previous one of the same parity selected
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
@@ -227,14 +155,14 @@ def pipeline(tr, B, N, seed, keys, labels, device, args):
                 plan.append(fn)
         xplans.append(plan[:ncut])
         wplans.append(plan[ncut:])
-    # capture recorded prep(0), prep(1), step(0), step(1) without running them; the
-    # workspace of minibatch t (even) still holds its eager localisation (and with
-    # the split, the eager exchange of step t), so the replays continue from there
-    preps[:] = [gp[0].replay, gp[1].replay]
-    xfns[:] = [lambda: run(xplans[0]), lambda: run(xplans[1])]
-    wfns[:] = [lambda: run(wplans[0]), lambda: run(wplans[1])]
+    # capture ran nothing: the workspaces of the minibatches in flight still hold
+    # their eager preparations (and the eager exchange of step t), so the replays
+    # continue from there
+    preps[:] = [g.replay for g in gp]
+    xfns[:] = [(lambda b=b: run(xplans[b])) for b in range(NB)]
+    wfns[:] = [(lambda b=b: run(wplans[b])) for b in range(NB)]
     torch.cuda.synchronize()
-    for _ in range(2):
+    for _ in range(NB):
         iterate()
     torch.cuda.synchronize()
     return iterate, True
@@ -253,10 +181,12 @@ def main():
     ap.add_argument("--pipeline", type=int, default=1,
                     help="generate + localise minibatch t+1 on a high-priority side stream "
                          "while step t trains (HIP graphs per stream / step segment)")
-    ap.add_argument("--prep-streams", type=int, default=3,
-                    help="1 GPU: concurrent data-preparation streams (each generates + "
-                         "localises every n-th minibatch ahead of the training step). "
-                         "Measured ms/step: 1 -> 0.309, 2 -> 0.241, 3 -> 0.230, 4 -> 0.43")
+    ap.add_argument("--prep-streams", type=int, default=0,
+                    help="concurrent data-preparation streams (each generates + localises "
+                         "every n-th minibatch ahead of the training step). Measured 1 GPU "
+                         "ms/step: 1 -> 0.309, 2 -> 0.241, 3 -> 0.230, 4 -> 0.43; 8 emulated "
+                         "peers (SSP split, 2 more streams): 1 -> 0.333, 2 -> 0.260, 3 -> "
+                         "0.66). 0 = auto: 3 on 1 GPU, 2 with N > 1")
     ap.add_argument("--exchange", default="padded", choices=["padded", "exact"],
                     help="N > 1: fixed-capacity sync-free exchange, or count-sized all-to-all-v")
     ap.add_argument("--fixing-float", type=int, default=0)
@@ -344,11 +274,10 @@ def main():
             state["t"] = t + 1
 
         run = pipelined_step
-    if gpu and args.pipeline and G == 1 and args.prep_streams > 1:
-        run, graph_used = pipeline_deep(tr, B, N, seed, keys, labels, device, args,
-                                        nprep=args.prep_streams)
-    elif gpu and args.pipeline and (G == 1 or tr.padded):
-        run, graph_used = pipeline(tr, B, N, seed, keys, labels, device, args)
+    if gpu and args.pipeline and (G == 1 or tr.padded):
+        nprep = args.prep_streams or (3 if G == 1 else 2)
+        args.prep_streams = nprep
+        run, graph_used = pipeline(tr, B, N, seed, keys, labels, device, args, nprep=nprep)
     else:
         for _ in range(max(1, args.warmup)):
             run()
@@ -422,7 +351,7 @@ def main():
                 "push": args.push_mode if G > 1 else None,
                 "table_slots_per_gpu": tr.table.capacity,
                 "hip_graph": graph_used,
-                "prep_streams": args.prep_streams if (gpu and G == 1 and args.pipeline) else 1,
+                "prep_streams": args.prep_streams if (gpu and args.pipeline) else 1,
                 "localize": tr.localize_mode,
                 "emulated_peers": G if emulated else None,
                 "exchange": (f"{args.exchange} (capacity {tr.xc.C} keys/peer/step)"
