@@ -45,9 +45,15 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
       graph per compute segment and buffer; a single multi-stream graph replays
       much slower on ROCm). N > 1: the padded exchange's two equal-split RCCL
       all-to-alls run between the graph replays, nothing reads back to the host.
-    * N > 1 with exchange lag 1 (SSP): the exchange half of step t+1 (pack,
-      all-to-all, owner update + resolve, all-to-all) runs on its own stream while
-      the worker half of step t (forward, backward) runs on the main stream.
+    * N > 1 with exchange lag 1 (SSP): the exchange half of step t+2 (pack,
+      all-to-all, owner update + resolve, all-to-all) is issued right after the
+      worker half of step t, on the preparation stream of minibatch t+2 (behind its
+      localisation), so it runs while the main stream trains step t+1. Counting
+      RCCL's own stream this keeps 4 busy streams; one more (a dedicated exchange
+      stream, PSAMD_XCHG_STREAM=own) oversubscribes the hardware queues (8
+      emulated peers: 0.333 vs 0.308 ms/step). Consecutive exchanges are chained
+      (owner updates in step order). tests/test_bench_pipeline_gpu.py checks the
+      pipeline trains exactly what the sequential trainer trains.
 
     Each iteration = one full training step + one full data preparation; the first
     steps' data is prepared in warm-up and the last iterations' preparations are
@@ -80,7 +86,13 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
 
     split = tr.padded and tr.lag == 1
     ncut = tr.EXCHANGE_SEGMENTS if split else 0
-    comm_s = torch.cuda.Stream(device, priority=-1) if split else main
+    # where the exchange half runs: "prep" = on the preparation stream of its own
+    # minibatch, right after the localisation (no extra stream: RCCL's own stream
+    # is already one more, and past 4 busy streams the queues oversubscribe);
+    # "own" = a dedicated high-priority exchange stream
+    xmode = os.environ.get("PSAMD_XCHG_STREAM", "prep") if split else "none"
+    comm_s = torch.cuda.Stream(device, priority=-1) if xmode == "own" else main
+    xd = min(nprep, 2)  # "prep": exchange of step t + xd issued after step t
 
     def run(fns):
         for fn in fns:
@@ -100,11 +112,14 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
 
     def issue_exchange(t):  # exchange half of step t: minibatch t ready, grads(t-2) packed
         b = t % NB
-        comm_s.wait_event(ev_prep[b])
-        comm_s.wait_event(ev_step[(t - 2) % NB])
-        with torch.cuda.stream(comm_s):
+        xs = sides[b % nprep] if xmode == "prep" else comm_s
+        if xmode != "prep":
+            xs.wait_event(ev_prep[b])     # (on its prep stream it follows the prep)
+        xs.wait_event(ev_step[(t - 2) % NB])
+        xs.wait_event(ev_x[(t - 1) % NB])  # owner updates of consecutive steps in order
+        with torch.cuda.stream(xs):
             xfns[b]()
-            ev_x[b].record(comm_s)
+            ev_x[b].record(xs)
 
     def iterate():
         t = state["t"]
@@ -115,13 +130,17 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
             preps[nb]()
             ev_prep[nb].record(s)
         cur = t % NB
-        if split:
+        if xmode == "own":
             issue_exchange(t + 1)
             main.wait_event(ev_x[cur])        # exchange of step t done
+        elif split:
+            main.wait_event(ev_x[cur])
         else:
             main.wait_event(ev_prep[cur])     # minibatch t is localised
         wfns[cur]()
         ev_step[cur].record(main)
+        if xmode == "prep":                   # needs step t + xd - 2 <= t issued and
+            issue_exchange(t + xd)            # the prep of t + xd (issued at t + xd - nprep)
         state["t"] = t + 1
 
     for b in range(NB):
@@ -130,8 +149,13 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
         with torch.cuda.stream(sides[b]):
             prep(b)
             ev_prep[b].record(sides[b])
-    if split:
+    for b in range(NB):
+        ev_x[b].record(main)
+    if xmode == "own":
         issue_exchange(0)
+    elif split:
+        for t in range(xd):  # exchanges of minibatches 0 .. xd-1
+            issue_exchange(t)
     warm = max(NB, args.warmup + (-args.warmup) % NB)
     for _ in range(warm):
         iterate()
@@ -185,8 +209,9 @@ def main():
                     help="concurrent data-preparation streams (each generates + localises "
                          "every n-th minibatch ahead of the training step). Measured 1 GPU "
                          "ms/step: 1 -> 0.309, 2 -> 0.241, 3 -> 0.230, 4 -> 0.43; 8 emulated "
-                         "peers (SSP split, 2 more streams): 1 -> 0.333, 2 -> 0.260, 3 -> "
-                         "0.66). 0 = auto: 3 on 1 GPU, 2 with N > 1")
+                         "peers with a communicator stream, exchange on the prep streams: "
+                         "1 -> 0.46, 2 -> 0.308, 3 -> 0.334). 0 = auto: 3 on 1 GPU, 2 with "
+                         "N > 1")
     ap.add_argument("--exchange", default="padded", choices=["padded", "exact"],
                     help="N > 1: fixed-capacity sync-free exchange, or count-sized all-to-all-v")
     ap.add_argument("--fixing-float", type=int, default=0)

@@ -79,10 +79,26 @@ class LoopbackComm(Comm):
 
     backend = "loopback"
 
-    def __init__(self, world: int, device="cpu"):
+    def __init__(self, world: int, device="cpu", comm_stream: bool = True):
         self.world = int(world)
         self.rank = 0
         self.device = torch.device(device)
+        # model ProcessGroupNCCL's stream structure: the collective runs on the
+        # communicator's own stream, ordered after the caller's stream and before
+        # the caller's next work (so the emulation sees the same number of streams)
+        self._cs = (torch.cuda.Stream(self.device) if comm_stream and self.device.type == "cuda"
+                    else None)
+
+    def all_to_all_fixed(self, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
+        if self._cs is None:
+            recv.copy_(send)
+            return recv
+        cur = torch.cuda.current_stream(self.device)
+        self._cs.wait_stream(cur)
+        with torch.cuda.stream(self._cs):
+            recv.copy_(send)
+        cur.wait_stream(self._cs)
+        return recv
 
     def all_gather_counts(self, counts: torch.Tensor, to_host: bool = True) -> torch.Tensor:
         m = counts.reshape(1, -1).expand(self.world, -1)

@@ -1,0 +1,83 @@
+"""bench.py's multi-stream software pipeline must train exactly what the plain
+sequential trainer trains: the same minibatches (per-stream row counters), the
+exchange half of step t on the preparation stream of minibatch t (or on its own
+stream) overlapping the worker half of step t-1, SSP lag 1. Any missing stream
+dependency shows up here as different weights (an exchange reading a buffer
+before its localisation, two owner updates racing, a push applied early/late).
+
+Runs on one GPU over the loopback exchange (2 emulated ranks: the padded
+exchange, owner updates and SSP split are the N-GPU code paths)."""
+import argparse
+import importlib.util
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("psamd_bench", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _trainer(B, N):
+    from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+    from parameter_server_amd.parallel.comm import LoopbackComm
+
+    cfg = SparseLRConfig(num_features=N, minibatch=B, algo="ftrl", lr_type="decay", alpha=0.01,
+                         beta=10.0, l1=10.0, l2=1.0, consistency="ssp:4")
+    tr = SparseLRTrainer(cfg, LoopbackComm(2, "cuda"), "cuda")
+    assert tr.padded and tr.lag == 1
+    return tr
+
+
+def _weights(tr):
+    keys, w, _, _ = tr.table.occupied()
+    o = torch.argsort(keys)
+    return keys[o].cpu(), w[o].float().cpu()
+
+
+@pytest.mark.parametrize("xmode,nprep,graph", [("prep", 2, 1), ("prep", 1, 1), ("own", 2, 1),
+                                               ("prep", 3, 0)])
+def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph):
+    from parameter_server_amd.ops.synthetic import criteo_batch
+
+    monkeypatch.setenv("PSAMD_XCHG_STREAM", xmode)
+    bench = _bench()
+    B, N, seed, extra = 4096, 10 ** 6, 77, 5
+    dev = torch.device("cuda")
+    tr = _trainer(B, N)
+    keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
+    labels = torch.empty(B, dtype=torch.float32, device=dev)
+    args = argparse.Namespace(warmup=0, graph=graph)
+    it, _ = bench.pipeline(tr, B, N, seed, keys, labels, dev, args, nprep=nprep)
+    NB = 2 * nprep
+    T = NB + (NB if graph else 0) + extra
+    for _ in range(extra):
+        it()
+    torch.cuda.synchronize()
+    tr._x_flush()  # pushes no issued exchange carried yet (none in prep mode, nprep >= 2)
+    pk, pw = _weights(tr)
+    loss_p = tr.progress()["loss"]
+
+    ref = _trainer(B, N)
+    for m in range(T):
+        k, lab = criteo_batch(B, seed=seed, row0=m * B, num_features=N, device=dev)
+        ref.step(k, lab, width=39)
+    ref._x_flush()
+    torch.cuda.synchronize()
+    rk, rw = _weights(ref)
+    # the pipeline also resolved (inserted) the keys of the minibatches prepared
+    # ahead: those carry no update (w = 0); every trained key must agree
+    pos = torch.searchsorted(pk, rk)
+    assert torch.equal(pk[pos], rk)
+    assert torch.allclose(pw[pos], rw, rtol=1e-4, atol=1e-6), (pw[pos] - rw).abs().max()
+    extra_mask = torch.ones(pk.numel(), dtype=torch.bool)
+    extra_mask[pos] = False
+    assert torch.all(pw[extra_mask] == 0)
+    assert abs(loss_p - ref.progress()["loss"]) < 1e-4
