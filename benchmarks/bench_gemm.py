@@ -42,3 +42,17 @@ for name, (M, N, K, ak, bk) in {
     fl = 2.0 * M * N * K
     rows.append({"shape": name, "ours_tflops": fl / ours / 1e12, "torch_tflops": fl / ref / 1e12})
     print(json.dumps(rows[-1]), flush=True)
+
+if "--wd-sweep" in sys.argv:
+    # weight-gradient split-K sweep on the wide & deep shapes (fp32 output, beta 0)
+    for N, K in ((1024, 4992), (512, 1024), (256, 512)):
+        Bn = 16384
+        dZ = (torch.rand(Bn, N, device="cuda") - 0.5).to(torch.bfloat16)
+        X = (torch.rand(Bn, K, device="cuda") - 0.5).to(torch.bfloat16)
+        out = torch.empty(N, K, device="cuda")
+        for sk in (1, 2, 4, 8, 16, 32):
+            dt = t(lambda: G.gemm(dZ, False, X, False, N, K, Bn, out_bf16=False, out_f32=out,
+                                  splitk=sk))
+            print(json.dumps({"dW": f"{N}x{K}x{Bn}", "splitk": sk, "us": dt * 1e6,
+                              "tflops": 2.0 * N * K * Bn / dt / 1e12,
+                              "auto": G.auto_splitk(N, K, Bn)}), flush=True)

@@ -124,9 +124,10 @@ void emb_grad_reduce(const int32_t*, const int32_t*, const int32_t*, const int32
 void emb_update(const int64_t*, int64_t, const int32_t*, int64_t, const float*, const void*, void*,
                 float*, int, float, float, hipStream_t);
 void wd_head(const void*, int64_t, int, const float*, const float*, const float*, int64_t,
-             const int32_t*, int, const float*, float*, void*, float*, float*, double*, uint32_t*,
-             int, int, hipStream_t);
-void colsum_bf16(const void*, int64_t, int, float*, hipStream_t);
+             const int32_t*, int, const float*, float*, void*, float*, float*, float*, double*,
+             uint32_t*, int, int, hipStream_t);
+void colred_bf16(const void*, int64_t, int, const float*, float*, const float*, float*,
+                 hipStream_t);
 void adam_update(float*, const float*, float*, float*, int64_t, float, float, float, float, float,
                  float, float, void*, hipStream_t);
 // hashloc.hip
@@ -148,7 +149,7 @@ void spmv(bool, const int64_t*, const void*, int, const void*, int, int64_t, int
           int64_t, double, double, void*, int64_t, hipStream_t);
 // gemm.hip
 void gemm_bf16(bool, bool, const void*, int, const void*, int, int, int, int, int, const float*,
-               const void*, int, void*, int, float*, int, float, int, hipStream_t);
+               const void*, int, void*, int, float*, int, float, int, float*, hipStream_t);
 }  // namespace psamd
 
 using at::Tensor;
@@ -954,7 +955,7 @@ PYBIND11_MODULE(_hipops, m) {
                         int64_t ldb, int64_t M, int64_t N, int64_t K, int epi,
                         optional<Tensor> bias, optional<Tensor> aux, int64_t ldaux,
                         optional<Tensor> C, int64_t ldc, optional<Tensor> Cf, int64_t ldcf,
-                        double beta, int splitk) {
+                        double beta, int splitk, optional<Tensor> colsum) {
     chk(A, at::kBFloat16, "A");
     chk(B, at::kBFloat16, "B");
     check(M > 0 && N > 0 && K > 0 && M < INT32_MAX && N < INT32_MAX && K < INT32_MAX,
@@ -992,11 +993,13 @@ PYBIND11_MODULE(_hipops, m) {
     if (cfp) check(ldcf >= N && Cf->numel() >= (M - 1) * ldcf + N, "Cf too small");
     check(cp || cfp, "GEMM needs an output");
     if (splitk > 1)
-      check(!cp && cfp && epi == 0 && (beta == 0.0 || beta == 1.0),
+      check(!cp && cfp && (epi & ~8) == 0 && (beta == 0.0 || beta == 1.0),
             "split-K: fp32 output only, no epilogue, beta 0 or 1");
+    float* csp = optr<float>(colsum, at::kFloat, "colsum");
+    check(!(epi & 8) || (csp && colsum->numel() >= N), "EPI_COLSUM needs colsum[N]");
     psamd::gemm_bf16(a_kmajor, b_kmajor, A.data_ptr(), (int)lda, B.data_ptr(), (int)ldb, (int)M,
                      (int)N, (int)K, epi, bp, xp, (int)ldaux, cp, (int)ldc, cfp, (int)ldcf,
-                     (float)beta, splitk, cur_stream());
+                     (float)beta, splitk, csp, cur_stream());
   });
 
   // ----------------------------------------------------- sort-free localisation
@@ -1145,7 +1148,7 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("wd_head", [](Tensor h, Tensor w, Tensor b, Tensor wide_w, Tensor local_col, int S,
                       Tensor labels, Tensor coef, Tensor dh, Tensor dw, Tensor db, Tensor metrics,
-                      Tensor hist, int nbins) {
+                      Tensor hist, int nbins, optional<Tensor> db_h) {
     chk(h, at::kBFloat16, "h");
     chk(w, at::kFloat, "w");
     chk(b, at::kFloat, "b");
@@ -1165,9 +1168,12 @@ PYBIND11_MODULE(_hipops, m) {
     check(S > 0 && S <= 64 && local_col.numel() >= B * S, "S in (0, 64], local_col [B*S]");
     check(labels.numel() >= B && coef.numel() >= B && dh.numel() >= B * H, "head buffers small");
     check(metrics.numel() >= 3 && hist.numel() >= 2 * nbins && nbins > 0, "metrics / hist");
+    float* dbh = optr<float>(db_h, at::kFloat, "db_h");
+    check(!dbh || db_h->numel() >= H, "db_h [H]");
+    check(H % 8 == 0, "head width H % 8 == 0");
     psamd::wd_head(h.data_ptr(), B, H, ptr<float>(w), ptr<float>(b), ptr<float>(wide_w),
                    wide_w.numel(), ptr<int32_t>(local_col), S, ptr<float>(labels),
-                   ptr<float>(coef), dh.data_ptr(), ptr<float>(dw), ptr<float>(db),
+                   ptr<float>(coef), dh.data_ptr(), ptr<float>(dw), ptr<float>(db), dbh,
                    ptr<double>(metrics), reinterpret_cast<uint32_t*>(hist.data_ptr()), nbins,
                    acc_stripes_of(metrics), cur_stream());
   });
@@ -1175,7 +1181,9 @@ PYBIND11_MODULE(_hipops, m) {
     chk(x, at::kBFloat16, "x");
     chk(out, at::kFloat, "out");
     check(x.dim() == 2 && out.numel() >= x.size(1), "colsum: x [B, N], out [N]");
-    psamd::colsum_bf16(x.data_ptr(), x.size(0), (int)x.size(1), ptr<float>(out), cur_stream());
+    check(x.size(1) % 8 == 0, "colsum: N % 8 == 0");
+    psamd::colred_bf16(x.data_ptr(), x.size(0), (int)x.size(1), nullptr, ptr<float>(out), nullptr,
+                       nullptr, cur_stream());
   });
   m.def("adam_update", [](Tensor p, Tensor g, Tensor m_, Tensor v, double lr, double b1,
                           double b2, double eps, int64_t step, double gscale,

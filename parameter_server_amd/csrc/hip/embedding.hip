@@ -349,48 +349,59 @@ emb_update_kernel(const int64_t* __restrict__ slot, int64_t n, const int32_t* __
 }
 
 // ---------------------------------------------------------------- head
-// One wave per example. h [B, H] bf16 (H <= 512), w [H] fp32.
+// A wave per example (h [B, H] bf16, H <= 512, w [H] fp32): logit, loss,
+// metrics, AUC bin, coef, dh. Per-row work only: every load of a row is issued
+// at once (H / 64 h values + the S wide weights per lane), 4 examples per wave
+// and B / 16 blocks (the previous 256-block version walked 16 examples per wave
+// and did the dw reduction in LDS atomics: 71 us at B = 16384).
+// The column reductions (dw = h^T coef, db of the last hidden layer) run after it
+// in colred_bf16_kernel.
 __global__ void __launch_bounds__(256)
 wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __restrict__ w,
                const float* __restrict__ b, const float* __restrict__ wide_w, int64_t wide_cap,
                const int32_t* __restrict__ local_col, int S, const float* __restrict__ labels,
-               float* __restrict__ coef_out, uint16_t* __restrict__ dh, float* __restrict__ dw,
-               float* __restrict__ db, double* __restrict__ metrics, uint32_t* __restrict__ hist,
-               int nbins, int acc_stripes) {
-  extern __shared__ uint32_t lhist[];  // [2 * nbins]
-  __shared__ float s_dw[512];
+               float* __restrict__ coef_out, uint16_t* __restrict__ dh, float* __restrict__ db,
+               double* __restrict__ metrics, uint32_t* __restrict__ hist, int nbins,
+               int acc_stripes) {
   __shared__ double red[16];
-  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) lhist[i] = 0;
-  for (int i = threadIdx.x; i < H; i += blockDim.x) s_dw[i] = 0.f;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63;
   double loss_acc = 0, corr = 0, cnt = 0, dbsum = 0;
-  for (int64_t r = (int64_t)blockIdx.x * nw + wid; r < B; r += (int64_t)gridDim.x * nw) {
+  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < B;
+       r += (int64_t)gridDim.x * (blockDim.x >> 6)) {
+    float hv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = lane + 64 * q;
+      hv[q] = k < H ? bf2f(h[r * H + k]) : 0.f;
+    }
     float m = 0.f;
-    for (int k = lane; k < H; k += 64) m += bf2f(h[r * H + k]) * w[k];
     if (lane < S) {
       const int32_t c = local_col[r * S + lane];
-      if (in_range(c, wide_cap)) m += wide_w[c];
+      if (in_range(c, wide_cap)) m = wide_w[c];
     }
-    m = wave_allsum(m) + b[0];  // every lane needs coef below
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = lane + 64 * q;
+      if (k < H) m += hv[q] * w[k];
+    }
+    m = wave_allsum(m) + b[0];
     const float y = labels[r] > 0.f ? 1.f : -1.f;
     const float ym = y * m;
-    const float loss = ym > 0 ? log1pf(expf(-ym)) : -ym + log1pf(expf(ym));
     const float coef = -y / (1.f + expf(ym));
-    for (int k = lane; k < H; k += 64) {
-      const float hv = bf2f(h[r * H + k]);
-      dh[r * H + k] = f2bf(hv > 0.f ? coef * w[k] : 0.f);
-      atomicAdd(&s_dw[k], coef * hv);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = lane + 64 * q;
+      if (k < H) dh[r * H + k] = f2bf(hv[q] > 0.f ? coef * w[k] : 0.f);
     }
     if (lane == 0) {
       coef_out[r] = coef;
-      loss_acc += loss;
+      loss_acc += ym > 0 ? log1pf(expf(-ym)) : -ym + log1pf(expf(ym));
       corr += ((y > 0.f) == (m > 0.f)) ? 1.0 : 0.0;
       cnt += 1.0;
       dbsum += coef;
       const float p = 1.f / (1.f + expf(-m));
       const float pb = p == p ? fminf(fmaxf(p * nbins, 0.f), (float)(nbins - 1)) : 0.f;
-      atomicAdd(&lhist[(y > 0.f ? nbins : 0) + (int)pb], 1u);
+      atomicAdd(&hist[(y > 0.f ? nbins : 0) + (int)pb], 1u);
     }
   }
   const double a = block_sum_f64(loss_acc, red);
@@ -402,32 +413,72 @@ wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __
     atomicAdd(&mt[0], a);
     atomicAdd(&mt[1], c);
     atomicAdd(&mt[2], n);
-    atomicAdd(db, (float)d);
+    atomicAdd(&mt[5], d);  // db of the head, folded into db by wd_head_db_kernel
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < H; i += blockDim.x) atomicAdd(&dw[i], s_dw[i]);
-  for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x)
-    if (lhist[i]) atomicAdd(&hist[i], lhist[i]);
 }
 
-// out[n] += sum_b x[b, n] (bf16 in, fp32 out; out zeroed by the caller). Block =
-// 64 columns x 512 rows (4 threads per column, 128 rows each), fp32 atomics per
-// column: (N / 64) x (B / 512) blocks fill the chip.
-constexpr int kColRows = 512;
+// out[n] += sum_r s_r x[r, n]  and  out_pos[n] += g[n] sum_r s_r [x[r, n] > 0]
+// (bf16 x [B, N], N % 8 == 0; s = 1 when null). A block covers 8 * tpr columns
+// (tpr threads per row, 16-B loads) and kColredRows rows, 256 / tpr rows per
+// pass; per-block partials meet in LDS, one fp32 atomic per column and block.
+// Used for the head's dw = h^T coef and last-layer db = w * sum coef [h > 0], and
+// as the stand-alone column sum (bias gradient of the library-GEMM backend).
+constexpr int kColredRows = 128;
 
 __global__ void __launch_bounds__(256)
-colsum_bf16_kernel(const uint16_t* __restrict__ x, int64_t B, int N, float* __restrict__ out) {
-  __shared__ float part[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
-  const int64_t r0 = (int64_t)blockIdx.y * kColRows, r1 = min(B, r0 + kColRows);
-  float s = 0.f;
-  if (c < N)
-    for (int64_t r = r0 + q; r < r1; r += 4) s += bf2f(x[r * N + c]);
-  part[q][threadIdx.x & 63] = s;
+colred_bf16_kernel(const uint16_t* __restrict__ x, int64_t B, int N, int tpr,
+                   const float* __restrict__ s, float* __restrict__ out,
+                   const float* __restrict__ g, float* __restrict__ out_pos) {
+  __shared__ float red[2][256 * 8];
+  const int t = threadIdx.x, cl = t % tpr, rg = t / tpr, nrg = 256 / tpr;
+  const int n0 = blockIdx.x * tpr * 8 + cl * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * kColredRows, r1 = min(B, r0 + kColredRows);
+  float a[8], c[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = c[j] = 0.f;
+  if (n0 < N) {
+#pragma unroll 4
+    for (int64_t r = r0 + rg; r < r1; r += nrg) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + r * N + n0);
+      const float sr = s ? s[r] : 1.f;
+      const uint16_t* hv = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xv = bf2f(hv[j]);
+        a[j] += sr * xv;
+        c[j] += xv > 0.f ? sr : 0.f;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][rg * tpr * 8 + cl * 8 + j] = a[j];
+    red[1][rg * tpr * 8 + cl * 8 + j] = c[j];
+  }
   __syncthreads();
-  if (q == 0 && c < N)
-    atomicAdd(&out[c], part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] +
-                           part[3][threadIdx.x]);
+  for (int i = t; i < tpr * 8; i += 256) {
+    const int n = blockIdx.x * tpr * 8 + i;
+    if (n >= N) continue;
+    float sa = 0.f, sc = 0.f;
+    for (int q = 0; q < nrg; ++q) {
+      sa += red[0][q * tpr * 8 + i];
+      sc += red[1][q * tpr * 8 + i];
+    }
+    unsafeAtomicAdd(out + n, sa);
+    if (out_pos) unsafeAtomicAdd(out_pos + n, g[n] * sc);
+  }
+}
+
+// db (head bias) += the striped coef sums the head kernel left in metrics[5]
+__global__ void __launch_bounds__(64)
+wd_head_db_kernel(double* __restrict__ metrics, int acc_stripes, float* __restrict__ db) {
+  double d = 0;  // one stripe per lane (acc_stripes <= 64)
+  if ((int)threadIdx.x < acc_stripes) {
+    d = metrics[threadIdx.x * kAccStride + 5];
+    metrics[threadIdx.x * kAccStride + 5] = 0;
+  }
+  for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+  if (threadIdx.x == 0) db[0] += (float)d;
 }
 
 // Adam with fp32 master weights; writes the bf16 copy used by the GEMMs.
@@ -518,24 +569,33 @@ void emb_update(const int64_t* slot, int64_t n, const int32_t* n_dev, int64_t ca
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
+void colred_bf16(const void* x, int64_t B, int N, const float* s, float* out, const float* g,
+                 float* out_pos, hipStream_t st);
+
 void wd_head(const void* h, int64_t B, int H, const float* w, const float* b, const float* wide_w,
              int64_t wide_cap, const int32_t* local_col, int S, const float* labels,
-             float* coef, void* dh, float* dw, float* db, double* metrics, uint32_t* hist,
-             int nbins, int acc_stripes, hipStream_t st) {
+             float* coef, void* dh, float* dw, float* db, float* db_h, double* metrics,
+             uint32_t* hist, int nbins, int acc_stripes, hipStream_t st) {
   if (B <= 0) return;
-  // 256 blocks (16 examples per wave): every block ends with H + 4 same-address
-  // atomics (dw, db, metrics) that serialise across blocks, so fewer, fuller blocks
-  const int blocks = (int)std::min<int64_t>((B + 3) / 4, 256);
-  wd_head_kernel<<<blocks, 256, 2 * nbins * sizeof(uint32_t), st>>>(
+  // 4 examples per wave: 4 x fewer blocks ending in the 4 striped metric atomics
+  wd_head_kernel<<<(unsigned)std::min<int64_t>((B + 15) / 16, 65535), 256, 0, st>>>(
       reinterpret_cast<const uint16_t*>(h), B, H, w, b, wide_w, wide_cap, local_col, S, labels,
-      coef, reinterpret_cast<uint16_t*>(dh), dw, db, metrics, hist, nbins, acc_stripes);
+      coef, reinterpret_cast<uint16_t*>(dh), db, metrics, hist, nbins, acc_stripes);
   PSAMD_HIP_CHECK(hipGetLastError());
+  wd_head_db_kernel<<<1, 64, 0, st>>>(metrics, acc_stripes, db);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  colred_bf16(h, B, H, coef, dw, db_h ? w : nullptr, db_h, st);
 }
 
-void colsum_bf16(const void* x, int64_t B, int N, float* out, hipStream_t st) {
-  if (N <= 0) return;
-  const dim3 grid((N + 63) / 64, (unsigned)std::max<int64_t>(1, (B + kColRows - 1) / kColRows));
-  colsum_bf16_kernel<<<grid, 256, 0, st>>>(reinterpret_cast<const uint16_t*>(x), B, N, out);
+void colred_bf16(const void* x, int64_t B, int N, const float* s, float* out, const float* g,
+                 float* out_pos, hipStream_t st) {
+  if (N <= 0 || B <= 0) return;
+  int tpr = 64;
+  while (tpr > 1 && tpr * 8 >= 2 * N) tpr >>= 1;  // 8 * tpr >= N > 4 * tpr (or 64)
+  const dim3 grid((unsigned)((N + 8 * tpr - 1) / (8 * tpr)),
+                  (unsigned)((B + kColredRows - 1) / kColredRows));
+  colred_bf16_kernel<<<grid, 256, 0, st>>>(reinterpret_cast<const uint16_t*>(x), B, N, tpr, s,
+                                           out, g, out_pos);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -22,7 +22,9 @@
 // index is remapped so consecutive tiles of one A panel share an XCD's L2.
 //
 // Fused epilogues: + bias[n], ReLU, multiply by the ReLU mask of an auxiliary
-// bf16 tensor (backward through an activation), bf16 and/or fp32 stores.
+// bf16 tensor (backward through an activation), bf16 and/or fp32 stores, and the
+// output's column sums (the input-gradient GEMM of layer i emits dZ of layer i-1,
+// whose column sums are that layer's bias gradient: no second pass over dZ).
 #include "common.cuh"
 
 #include <hip/hip_bf16.h>
@@ -52,7 +54,10 @@ enum Epi : int {
   EPI_BIAS = 1,      // + bias[n]
   EPI_RELU = 2,      // max(., 0)
   EPI_MASK = 4,      // * (aux[m, n] > 0)   (backward through ReLU)
+  EPI_COLSUM = 8,    // colsum[n] += sum_m C[m, n]  (bias gradient of the layer below)
+  EPI_VEC = 16,      // (set by the host) vectorised epilogue through LDS, see below
 };
+constexpr int EPI_LDS = 68;  // fp32 row stride of a wave's 64 x 64 staging tile
 
 __device__ __forceinline__ int xcd_swizzle(int bid, int nwg) {
   // bijective remap: the blocks that land on one XCD (bid % 8) get a contiguous range
@@ -138,7 +143,8 @@ __global__ void __launch_bounds__(THREADS)
 gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict__ B, int ldb,
                  int M, int N, int K, int epi, const float* __restrict__ bias,
                  const __bf16* __restrict__ aux, int ldaux, __bf16* __restrict__ C, int ldc,
-                 float* __restrict__ Cf, int ldcf, float beta, int kchunk) {
+                 float* __restrict__ Cf, int ldcf, float beta, int kchunk,
+                 float* __restrict__ colsum) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[2][2][LDS_ELEMS];  // [buf][A|B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -193,31 +199,125 @@ gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict
     cur ^= 1;
   }
 
+  if ((epi & EPI_VEC) && !split) {
+    // Vectorised epilogue: the MFMA layout gives a lane 4 rows of ONE column per
+    // 16x16 tile, so direct stores are 2-byte scatters (and the ReLU-mask reads
+    // 2-byte gathers). Stage the wave's 64 x 64 fp32 tile in LDS (free after the
+    // main loop's last barrier; 4 x 17 KB <= 72 KB), then each lane owns 8
+    // consecutive columns of 8 rows: 16-B mask loads, 16-B bf16 stores, 32-B fp32
+    // stores, and column sums reduced over the 8 row lanes with 3 shuffles.
+    float* W = reinterpret_cast<float*>(&lds[0][0][0]) + wid * (64 * EPI_LDS);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          W[(i * 16 + 4 * (lane >> 4) + r) * EPI_LDS + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    const int cg = lane & 7, rr = lane >> 3;
+    const int n = n0 + wn * 64 + cg * 8;
+    const bool nok = n < N;  // host guarantees N % 8 == 0
+    float bn[8], cs[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      bn[q] = ((epi & EPI_BIAS) && nok) ? bias[n + q] : 0.f;
+      cs[q] = 0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = it * 8 + rr;
+      const int m = m0 + wm * 64 + row;
+      if (m >= M || !nok) continue;
+      const float4 x0 = *reinterpret_cast<const float4*>(&W[row * EPI_LDS + cg * 8]);
+      const float4 x1 = *reinterpret_cast<const float4*>(&W[row * EPI_LDS + cg * 8 + 4]);
+      float x[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        x[q] += bn[q];
+        if (epi & EPI_RELU) x[q] = fmaxf(x[q], 0.f);
+      }
+      if (epi & EPI_MASK) {
+        const bf16x8 mv = *reinterpret_cast<const bf16x8*>(aux + (int64_t)m * ldaux + n);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = ((float)mv[q] > 0.f) ? x[q] : 0.f;
+      }
+      if (C) {
+        bf16x8 o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          o[q] = (__bf16)x[q];
+          cs[q] += (float)o[q];
+        }
+        *reinterpret_cast<bf16x8*>(C + (int64_t)m * ldc + n) = o;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cs[q] += x[q];
+      }
+      if (Cf) {
+        float4* p = reinterpret_cast<float4*>(Cf + (int64_t)m * ldcf + n);
+        float4 y0 = make_float4(x[0], x[1], x[2], x[3]), y1 = make_float4(x[4], x[5], x[6], x[7]);
+        if (beta != 0.f) {
+          const float4 o0 = p[0], o1 = p[1];
+          y0.x += beta * o0.x; y0.y += beta * o0.y; y0.z += beta * o0.z; y0.w += beta * o0.w;
+          y1.x += beta * o1.x; y1.y += beta * o1.y; y1.z += beta * o1.z; y1.w += beta * o1.w;
+        }
+        p[0] = y0;
+        p[1] = y1;
+      }
+    }
+    if (epi & EPI_COLSUM) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        cs[q] += __shfl_xor(cs[q], 8, 64);
+        cs[q] += __shfl_xor(cs[q], 16, 64);
+        cs[q] += __shfl_xor(cs[q], 32, 64);
+      }
+      // every lane of column group cg now holds its 8 sums: lane (rr, cg) adds
+      // column n + rr, so ONE atomic instruction covers the wave's 64 columns
+      float v = cs[0];
+#pragma unroll
+      for (int q = 1; q < 8; ++q) v = rr == q ? cs[q] : v;
+      if (nok) unsafeAtomicAdd(colsum + n + rr, v);
+    }
+    return;
+  }
+
   // epilogue: lane holds rows 4(l>>4)+r, col l&15 of every 16x16 tile
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-    if (n >= N) continue;
-    const float bn = (epi & EPI_BIAS) ? bias[n] : 0.f;
+    float cs = 0.f;  // this lane's part of the tile column sum (EPI_COLSUM)
+    if (n < N) {
+      const float bn = (epi & EPI_BIAS) ? bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
-        if (m >= M) continue;
-        float x = acc[i][j][r] + bn;
-        if (epi & EPI_RELU) x = fmaxf(x, 0.f);
-        if (epi & EPI_MASK) x = ((float)aux[(int64_t)m * ldaux + n] > 0.f) ? x : 0.f;
-        if (split) {  // fp32 output only (host pre-scales Cf by beta)
-          unsafeAtomicAdd(Cf + (int64_t)m * ldcf + n, x);
-          continue;
-        }
-        if (C) C[(int64_t)m * ldc + n] = (__bf16)x;
-        if (Cf) {
-          float* p = Cf + (int64_t)m * ldcf + n;
-          *p = beta != 0.f ? x + beta * *p : x;
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + r;
+          if (m >= M) continue;
+          float x = acc[i][j][r] + bn;
+          if (epi & EPI_RELU) x = fmaxf(x, 0.f);
+          if (epi & EPI_MASK) x = ((float)aux[(int64_t)m * ldaux + n] > 0.f) ? x : 0.f;
+          if (split) {  // fp32 output only (host pre-scales Cf by beta)
+            unsafeAtomicAdd(Cf + (int64_t)m * ldcf + n, x);
+            cs += x;
+            continue;
+          }
+          const __bf16 xb = (__bf16)x;
+          if (C) C[(int64_t)m * ldc + n] = xb;
+          cs += C ? (float)xb : x;  // the sum of what the next GEMM reads
+          if (Cf) {
+            float* p = Cf + (int64_t)m * ldcf + n;
+            *p = beta != 0.f ? x + beta * *p : x;
+          }
         }
       }
+    }
+    if (epi & EPI_COLSUM) {  // block-uniform: the 4 lanes of a column, one atomic
+      cs += __shfl_xor(cs, 16, 64);
+      cs += __shfl_xor(cs, 32, 64);
+      if (n < N && lane < 16) unsafeAtomicAdd(colsum + n, cs);
     }
   }
 }
@@ -226,7 +326,8 @@ gemm_bf16_kernel(const __bf16* __restrict__ A, int lda, const __bf16* __restrict
 
 void gemm_bf16(bool a_kmajor, bool b_kmajor, const void* A, int lda, const void* B, int ldb,
                int M, int N, int K, int epi, const float* bias, const void* aux, int ldaux,
-               void* C, int ldc, float* Cf, int ldcf, float beta, int splitk, hipStream_t st) {
+               void* C, int ldc, float* Cf, int ldcf, float beta, int splitk, float* colsum,
+               hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (splitk < 1) splitk = 1;
@@ -240,13 +341,18 @@ void gemm_bf16(bool a_kmajor, bool b_kmajor, const void* A, int lda, const void*
       throw std::runtime_error("split-K GEMM supports beta 0 or 1");
   }
   const dim3 grid(tiles, splitk);
+  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (splitk == 1 && N % 8 == 0 && (!C || (ldc % 8 == 0 && al16(C))) &&
+      (!Cf || (ldcf % 4 == 0 && al16(Cf))) && (!(epi & EPI_MASK) || (ldaux % 8 == 0 && al16(aux))))
+    epi |= EPI_VEC;
   auto a = reinterpret_cast<const __bf16*>(A);
   auto b = reinterpret_cast<const __bf16*>(B);
   auto x = reinterpret_cast<const __bf16*>(aux);
   auto c = reinterpret_cast<__bf16*>(C);
 #define PSAMD_GEMM(AK, BKM)                                                               \
   gemm_bf16_kernel<AK, BKM><<<grid, THREADS, 0, st>>>(a, lda, b, ldb, M, N, K, epi, bias, x, \
-                                                      ldaux, c, ldc, Cf, ldcf, beta, kchunk)
+                                                      ldaux, c, ldc, Cf, ldcf, beta, kchunk, \
+                                                      colsum)
   if (a_kmajor && b_kmajor) PSAMD_GEMM(true, true);
   else if (a_kmajor) PSAMD_GEMM(true, false);
   else if (b_kmajor) PSAMD_GEMM(false, true);

@@ -226,14 +226,17 @@ class WideDeepTrainer(EmbeddingPS):
         self.grad.zero_()
         H = acts[-1]
         dH = torch.empty_like(H)
+        L = len(cfg.hidden)
         E.head(H, self.w_head, self.b_head, w_wide, loc.local_col, S, labels, self.coef, dH,
-               self.dw_head, self.db_head, self.metrics, self.hist, AUC_BINS)
-        # ---------------- MLP backward (ReLU masks fused into the dX GEMMs)
-        for i in reversed(range(len(cfg.hidden))):
+               self.dw_head, self.db_head, self.metrics, self.hist, AUC_BINS,
+               db_h=self.db[L - 1])
+        # ---------------- MLP backward: ReLU masks and the bias gradient of the
+        # layer below fused into the dX GEMMs (grads zeroed at the step start)
+        for i in reversed(range(L)):
             GM.linear_weight_grad(dH, acts[i], out=self.dW[i], backend=cfg.gemm)
-            E.colsum(dH, self.db[i], accumulate=True)  # grads zeroed at the step start
             mask = acts[i] if i > 0 else None
-            dH = GM.linear_input_grad(dH, self.W16[i], mask=mask, backend=cfg.gemm)
+            dH = GM.linear_input_grad(dH, self.W16[i], mask=mask, backend=cfg.gemm,
+                                      colsum=self.db[i - 1] if i > 0 else None)
         dX0 = dH  # [B, S*D]
         # ---------------- sparse gradients
         u_cap = nnz

@@ -141,11 +141,13 @@ def grad_reduce(loc, dX0: torch.Tensor, D: int, u_cap: int, out=None):
 
 
 def head(h, w, b, wide_w, local_col, S: int, labels, coef, dh, dw, db, metrics, hist,
-         nbins: int):
-    """Deep logit + wide margin, logistic loss, metrics, AUC histogram, head grads."""
+         nbins: int, db_h=None):
+    """Deep logit + wide margin, logistic loss, metrics, AUC histogram, head grads;
+    ``db_h`` (optional) += column sums of ``dh`` (bias gradient of the last hidden
+    layer, computed as w * sum_r coef_r [h > 0] without re-reading dh)."""
     if is_gpu(h):
         hipops().wd_head(h, w, b, wide_w, local_col, S, labels, coef, dh, dw, db, metrics, hist,
-                         nbins)
+                         nbins, db_h)
         return
     B, H = h.shape
     hf = h.float()
@@ -160,6 +162,8 @@ def head(h, w, b, wide_w, local_col, S: int, labels, coef, dh, dw, db, metrics, 
     dh.copy_((c[:, None] * w[None, :] * (hf > 0)).to(torch.bfloat16))
     dw += (c[:, None] * hf).sum(0)
     db += c.sum()
+    if db_h is not None:
+        db_h += w * (c[:, None] * (hf > 0)).sum(0)
     metrics[0] += loss.double().sum()
     metrics[1] += ((y > 0) == (m > 0)).double().sum()
     metrics[2] += B

@@ -17,7 +17,7 @@ import torch
 
 from .native import hipops, is_gpu
 
-EPI_BIAS, EPI_RELU, EPI_MASK = 1, 2, 4
+EPI_BIAS, EPI_RELU, EPI_MASK, EPI_COLSUM = 1, 2, 4, 8
 
 
 def _view(t: torch.Tensor, kmajor: bool, rows: int, K: int) -> torch.Tensor:
@@ -26,25 +26,28 @@ def _view(t: torch.Tensor, kmajor: bool, rows: int, K: int) -> torch.Tensor:
 
 def auto_splitk(M: int, N: int, K: int, target_blocks: int = 1024) -> int:
     """K splits so that a small-output / long-K product (the weight gradient) still
-    puts >= ~4 blocks on each of the 256 CUs; each split keeps >= 8 K-tiles."""
+    puts >= ~4 blocks on each of the 256 CUs; each split keeps >= 16 K-tiles."""
     tiles = -(-M // 128) * -(-N // 128)
-    return max(1, min(-(-target_blocks // tiles), K // 512))
+    # measured (benchmarks/bench_gemm.py --wd-sweep, K = 16384): 1024x4992 best at 4
+    # splits, 512x1024 at 16 (32: +50 % from the fp32 atomics), 256x512 at 16-32
+    return max(1, min(-(-target_blocks // tiles), K // 1024))
 
 
 def gemm(A, a_kmajor: bool, B, b_kmajor: bool, M: int, N: int, K: int, *, bias=None,
          relu: bool = False, mask=None, out_bf16: bool = True, out_f32=None, beta: float = 0.0,
-         splitk: int = 1):
+         splitk: int = 1, colsum=None):
     """Returns the bf16 output (or None when ``out_bf16`` is False and ``out_f32`` given).
     ``splitk > 1`` (fp32 output only, beta 0 or 1) splits K over blocks and adds the
-    partial products atomically."""
+    partial products atomically. ``colsum`` [N] fp32 += the output's column sums
+    (of the bf16 values when there is a bf16 output)."""
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0) | \
-        (EPI_MASK if mask is not None else 0)
+        (EPI_MASK if mask is not None else 0) | (EPI_COLSUM if colsum is not None else 0)
     if is_gpu(A):
         C = torch.empty(M, N, dtype=torch.bfloat16, device=A.device) if out_bf16 else None
         lda = K if a_kmajor else M
         ldb = K if b_kmajor else N
         hipops().gemm_bf16(A, a_kmajor, lda, B, b_kmajor, ldb, M, N, K, epi, bias, mask, N, C, N,
-                           out_f32, N, beta, splitk)
+                           out_f32, N, beta, splitk, colsum)
         return C
     a = _view(A, a_kmajor, M, K).float()
     b = _view(B, b_kmajor, N, K).float()
@@ -55,6 +58,8 @@ def gemm(A, a_kmajor: bool, B, b_kmajor: bool, M: int, N: int, K: int, *, bias=N
         x = x.clamp_min(0)
     if mask is not None:
         x = x * (mask.reshape(M, N).float() > 0)
+    if colsum is not None:
+        colsum += (x.to(torch.bfloat16).float() if out_bf16 else x).sum(0)
     if out_f32 is not None:
         o = out_f32.view(M, N)
         o.copy_(x + beta * o if beta != 0.0 else x)
@@ -77,14 +82,19 @@ def linear_forward(X, W, bias=None, relu=False, backend: str = "mfma"):
     return gemm(X, True, W, True, Bn, N, K, bias=bias, relu=relu)
 
 
-def linear_input_grad(dZ, W, mask=None, backend: str = "mfma"):
-    """dZ [B, N], W [N, K] -> dZ W [B, K] (times the ReLU mask of ``mask`` [B, K])."""
+def linear_input_grad(dZ, W, mask=None, backend: str = "mfma", colsum=None):
+    """dZ [B, N], W [N, K] -> dZ W [B, K] (times the ReLU mask of ``mask`` [B, K]);
+    ``colsum`` [K] += its column sums (the bias gradient of the layer below)."""
     Bn, N = dZ.shape
     K = W.shape[1]
     if backend == "hipblaslt" and is_gpu(dZ):
         dX = torch.mm(dZ, W)
-        return dX.mul_(mask > 0) if mask is not None else dX
-    return gemm(dZ, True, W, False, Bn, K, N, mask=mask)
+        if mask is not None:
+            dX.mul_(mask > 0)
+        if colsum is not None:
+            hipops().colsum_bf16(dX, colsum)
+        return dX
+    return gemm(dZ, True, W, False, Bn, K, N, mask=mask, colsum=colsum)
 
 
 def linear_weight_grad(dZ, X, out=None, beta: float = 0.0, backend: str = "mfma"):

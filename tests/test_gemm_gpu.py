@@ -68,3 +68,18 @@ def test_linear_layer_products_and_epilogues():
     # CPU path = same math
     Hc = G.linear_forward(X.cpu(), W.cpu(), b.cpu(), relu=True)
     torch.testing.assert_close(Hc.float(), H.cpu().float(), rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(384, 1024, 512), (200, 136, 72), (16384, 256, 512)])
+def test_input_grad_colsum_epilogue(M, N, K):
+    """EPI_COLSUM: the masked input gradient's column sums (bias gradient of the
+    layer below) accumulate into colsum, equal to summing the bf16 output."""
+    torch.manual_seed(M + N)
+    dZ = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    W = (torch.randn(K, N, device="cuda") * 0.05).to(torch.bfloat16)
+    mask = torch.relu(torch.randn(M, N, device="cuda")).to(torch.bfloat16)
+    cs = torch.full((N,), 1.0, device="cuda")
+    dX = G.linear_input_grad(dZ, W, mask=mask, colsum=cs)
+    torch.testing.assert_close(cs - 1.0, dX.float().sum(0), rtol=1e-4, atol=1e-2)
+    ref = (dZ.float() @ W.float()) * (mask.float() > 0)
+    torch.testing.assert_close(dX.float(), ref, rtol=2e-2, atol=2e-2)

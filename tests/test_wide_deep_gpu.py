@@ -87,9 +87,10 @@ def test_head_colsum_adam_match_cpu():
         dw, db = torch.zeros(H, device=dev), torch.zeros(1, device=dev)
         met = torch.zeros(8, dtype=torch.float64, device=dev)
         hist = torch.zeros(2 * 2048, dtype=torch.int32, device=dev)
+        dbh = torch.full((H,), 0.5, device=dev)
         E.head(h.to(dev), w.to(dev), b.to(dev), wide.to(dev), lc.to(dev), S, y.to(dev), coef, dh,
-               dw, db, met, hist, 2048)
-        outs[dev] = [t.cpu() for t in (coef, dh, dw, db, met, hist)]
+               dw, db, met, hist, 2048, db_h=dbh)
+        outs[dev] = [t.cpu() for t in (coef, dh, dw, db, met, hist, dbh)]
     c, g = outs["cpu"], outs["cuda"]
     torch.testing.assert_close(g[0], c[0], rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(g[1].float(), c[1].float(), rtol=1e-2, atol=1e-3)
@@ -97,6 +98,9 @@ def test_head_colsum_adam_match_cpu():
     torch.testing.assert_close(g[3], c[3], rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(g[4][:3], c[4][:3], rtol=1e-5, atol=1e-6)
     assert abs(int((g[5] - c[5]).abs().sum())) <= 4  # bin edges may differ by an ulp
+    torch.testing.assert_close(g[6], c[6], rtol=1e-4, atol=1e-3)
+    # db_h is the column sum of dh (up to dh's bf16 rounding)
+    torch.testing.assert_close(g[6] - 0.5, g[1].float().sum(0), rtol=1e-2, atol=1e-2)
     x = torch.randn(300, 200).to(torch.bfloat16)
     torch.testing.assert_close(E.colsum(x.cuda(), torch.empty(200, device="cuda")).cpu(),
                                x.float().sum(0), rtol=1e-4, atol=1e-3)
