@@ -56,3 +56,29 @@ if "--wd-sweep" in sys.argv:
             print(json.dumps({"dW": f"{N}x{K}x{Bn}", "splitk": sk, "us": dt * 1e6,
                               "tflops": 2.0 * N * K * Bn / dt / 1e12,
                               "auto": G.auto_splitk(N, K, Bn)}), flush=True)
+
+if "--wd-backends" in sys.argv:
+    # each wide & deep layer product: own kernel (fused epilogue) vs hipBLASLt
+    Bn = 16384
+    for K, N in ((4992, 1024), (1024, 512), (512, 256)):
+        X = (torch.rand(Bn, K, device="cuda") - 0.5).to(torch.bfloat16)
+        W = ((torch.rand(N, K, device="cuda") - 0.5) * 0.05).to(torch.bfloat16)
+        b = torch.rand(N, device="cuda")
+        bb = b.to(torch.bfloat16)
+        dZ = (torch.rand(Bn, N, device="cuda") - 0.5).to(torch.bfloat16)
+        cs = torch.zeros(K, device="cuda")
+        dW = torch.empty(N, K, device="cuda")
+        fl = 2.0 * Bn * N * K
+        res = {
+            "fwd own (bias+relu)": t(lambda: G.linear_forward(X, W, b, relu=True)),
+            "fwd addmm+relu_": t(lambda: torch.addmm(bb, X, W.t()).relu_()),
+            "fwd _addmm_activation": t(lambda: torch._addmm_activation(bb, X, W.t())),
+            "dX own (mask+colsum)": t(lambda: G.linear_input_grad(dZ, W, mask=X, colsum=cs)),
+            "dX own plain": t(lambda: G.linear_input_grad(dZ, W)),
+            "dX mm": t(lambda: torch.mm(dZ, W)),
+            "dW own split": t(lambda: G.linear_weight_grad(dZ, X, out=dW)),
+            "dW mm fp32": t(lambda: torch.mm(dZ.t(), X, out_dtype=torch.float32)),
+        }
+        for k, v in res.items():
+            print(json.dumps({"layer": f"{K}->{N}", "op": k, "us": v * 1e6,
+                              "tflops": fl / v / 1e12}), flush=True)

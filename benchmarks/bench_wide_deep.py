@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--num-features", type=float, default=1e9)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--table-slots", type=int, default=1 << 27, help="slots per GPU")
-    ap.add_argument("--gemm", default="mfma", choices=("mfma", "hipblaslt"))
+    ap.add_argument("--gemm", default="auto", choices=("auto", "mfma", "hipblaslt"))
     args = ap.parse_args()
     from parameter_server_amd.models.wide_deep import WideDeepConfig, WideDeepTrainer
     from parameter_server_amd.ops.synthetic import criteo_batch

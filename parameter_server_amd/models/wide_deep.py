@@ -56,7 +56,7 @@ class WideDeepConfig:
     table_capacity: int = 0              # slots per rank (0 = auto)
     table_load: float = 0.5
     max_table_bytes: int = 160 << 30     # HBM budget of one shard (slots + rows)
-    gemm: str = "mfma"                   # mfma (own fused-epilogue kernel) | hipblaslt
+    gemm: str = "auto"                   # auto (measured per product) | mfma | hipblaslt
     seed: int = 0
 
 
@@ -175,6 +175,7 @@ class WideDeepTrainer(EmbeddingPS):
         self.W = [views[2 * i] for i in range(nl)]
         self.b = [views[2 * i + 1] for i in range(nl)]
         self.W16 = [v16[2 * i] for i in range(nl)]
+        self.b16 = [v16[2 * i + 1] for i in range(nl)]
         self.dW = [gviews[2 * i] for i in range(nl)]
         self.db = [gviews[2 * i + 1] for i in range(nl)]
         self.w_head, self.b_head = views[-2], views[-1]
@@ -221,7 +222,7 @@ class WideDeepTrainer(EmbeddingPS):
         acts = [X0]
         for i in range(len(cfg.hidden)):
             acts.append(GM.linear_forward(acts[-1], self.W16[i], self.b[i], relu=True,
-                                          backend=cfg.gemm))
+                                          backend=cfg.gemm, bias16=self.b16[i]))
         # ---------------- head (wide + deep), loss, metrics, head grads
         self.grad.zero_()
         H = acts[-1]

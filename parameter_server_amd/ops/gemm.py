@@ -67,17 +67,33 @@ def gemm(A, a_kmajor: bool, B, b_kmajor: bool, M: int, N: int, K: int, *, bias=N
 
 
 # Layer products on the GPU: "mfma" = the hand-written kernel above with fused
-# epilogues; "hipblaslt" = the vendor library GEMM (torch.mm) + separate elementwise
-# epilogue kernels, kept as the measured reference point (benchmarks/bench_gemm.py).
-BACKENDS = ("mfma", "hipblaslt")
+# epilogues; "hipblaslt" = the vendor library GEMM (torch.mm / addmm with its own
+# bias + ReLU epilogue) + separate elementwise kernels; "auto" = per product, the
+# faster of the two as measured on MI355X (benchmarks/bench_gemm.py --wd-backends,
+# B = 16384): the library for the plain long-K products (forward with K >= 1024:
+# 134 vs 250 us at 4992 -> 1024, 23 vs 31 us at 1024 -> 512; the unmasked input
+# gradient: 172 vs 270 us), the own kernel where its fused epilogue saves passes
+# (masked input gradient + bias-gradient column sums, short-K forward 14 vs 19 us)
+# and for every weight gradient (split-K: 285 vs 311, 53 vs 102, 42 vs 96 us).
+BACKENDS = ("mfma", "hipblaslt", "auto")
+_addmm_act = getattr(torch, "_addmm_activation", None)
 
 
-def linear_forward(X, W, bias=None, relu=False, backend: str = "mfma"):
-    """X [B, K] bf16, W [N, K] bf16 -> act(X W^T + b) [B, N] bf16."""
+def linear_forward(X, W, bias=None, relu=False, backend: str = "mfma", bias16=None):
+    """X [B, K] bf16, W [N, K] bf16 -> act(X W^T + b) [B, N] bf16 (``bias16``: a bf16
+    copy of ``bias`` for the library path)."""
     Bn, K = X.shape
     N = W.shape[0]
+    if backend == "auto":
+        backend = "hipblaslt" if K >= 1024 else "mfma"
     if backend == "hipblaslt" and is_gpu(X):
-        Z = torch.mm(X, W.t()) if bias is None else torch.addmm(bias.to(X.dtype), X, W.t())
+        if bias is None:
+            Z = torch.mm(X, W.t())
+            return Z.relu_() if relu else Z
+        b = bias16 if bias16 is not None else bias.to(X.dtype)
+        if relu and _addmm_act is not None:
+            return _addmm_act(b, X, W.t())
+        Z = torch.addmm(b, X, W.t())
         return Z.relu_() if relu else Z
     return gemm(X, True, W, True, Bn, N, K, bias=bias, relu=relu)
 
@@ -87,6 +103,8 @@ def linear_input_grad(dZ, W, mask=None, backend: str = "mfma", colsum=None):
     ``colsum`` [K] += its column sums (the bias gradient of the layer below)."""
     Bn, N = dZ.shape
     K = W.shape[1]
+    if backend == "auto":
+        backend = "hipblaslt" if mask is None and colsum is None and K >= 1024 else "mfma"
     if backend == "hipblaslt" and is_gpu(dZ):
         dX = torch.mm(dZ, W)
         if mask is not None:
