@@ -302,6 +302,79 @@ emb_grad_cross_kernel(const int32_t* __restrict__ segid, const int32_t* __restri
         make_float2(acc[2 * c], acc[2 * c + 1]);
 }
 
+// Narrow rows (D = 8 .. 64, the FM factors): the same 64-entry runs, but lane =
+// entry: each lane loads its own D-wide row (D / 8 16-B loads), a segmented
+// inclusive scan over the wave (6 shuffle steps per dim; segments are contiguous,
+// so "same segment id at distance off" is the segment test) leaves each
+// segment's run-local sum in its last lane, which stores it (kind 1) or parks it
+// in the run partials (kinds 2 / 3) exactly like emb_grad_seg_kernel.
+template <int D>
+__global__ void __launch_bounds__(256)
+emb_grad_lane_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ segid,
+                     const int32_t* __restrict__ seg_start, int64_t u_cap, int64_t nnz,
+                     const uint16_t* __restrict__ dX0, float* __restrict__ dE,
+                     float* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int64_t run = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t k0 = run * kSegRun;
+  if (k0 >= nnz) return;
+  const int64_t k = k0 + lane;
+  const bool live = k < nnz;
+  const int32_t p = live ? pos_s[k] : 0;
+  const bool take = live && in_range(p, nnz);
+  const int32_t u = live ? segid[k] - 1 : -1;
+  float x[D];
+  const uint4* row = reinterpret_cast<const uint4*>(dX0 + (int64_t)(take ? p : 0) * D);
+#pragma unroll
+  for (int v = 0; v < D / 8; ++v) {
+    const uint4 w = row[v];
+    const uint16_t* h = reinterpret_cast<const uint16_t*>(&w);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[v * 8 + j] = take ? bf2f(h[j]) : 0.f;
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t uo = __shfl_up(u, off, 64);
+    const bool add = lane >= off && uo == u;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const float y = __shfl_up(x[d], off, 64);
+      x[d] += add ? y : 0.f;
+    }
+  }
+  int32_t un = __shfl_down(u, 1, 64);
+  if (lane == 63) un = k + 1 < nnz ? segid[k + 1] - 1 : -1;
+  if (!live || (un == u && lane != 63) || !in_range(u, u_cap)) return;
+  const int64_t a = seg_start[u], b = seg_start[u + 1];
+  float* dst = a < k0 ? part + run * 2 * D
+             : (b > k0 + kSegRun ? part + run * 2 * D + D : dE + (int64_t)u * D);
+#pragma unroll
+  for (int v = 0; v < D / 4; ++v)
+    reinterpret_cast<float4*>(dst)[v] =
+        make_float4(x[4 * v], x[4 * v + 1], x[4 * v + 2], x[4 * v + 3]);
+}
+
+// emb_grad_cross_kernel for narrow rows: lane d < D sums dim d.
+template <int D>
+__global__ void __launch_bounds__(256)
+emb_grad_cross_narrow_kernel(const int32_t* __restrict__ segid,
+                             const int32_t* __restrict__ seg_start, int64_t u_cap, int64_t nnz,
+                             const float* __restrict__ part, float* __restrict__ dE) {
+  const int lane = threadIdx.x & 63;
+  const int64_t run = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t k0 = run * kSegRun;
+  if (k0 >= nnz || lane >= D) return;
+  const int32_t u = segid[min(nnz, k0 + kSegRun) - 1] - 1;
+  if (!in_range(u, u_cap)) return;
+  const int64_t a = seg_start[u], b = seg_start[u + 1];
+  if (a < k0 || b <= k0 + kSegRun) return;
+  const int64_t re = (b - 1) / kSegRun;
+  float acc = part[run * 2 * D + D + lane];
+#pragma unroll 8
+  for (int64_t r = run + 1; r <= re; ++r) acc += part[r * 2 * D + lane];
+  dE[(int64_t)u * D + lane] = acc;
+}
+
 // Row-wise AdaGrad (one accumulator per row, DLRM-style) on bf16 rows, fp32 math.
 __global__ void __launch_bounds__(256)
 emb_update_kernel(const int64_t* __restrict__ slot, int64_t n, const int32_t* __restrict__ n_dev,
@@ -527,19 +600,37 @@ void emb_expand(const int32_t* local_col, int64_t nnz, const int64_t* idx, int64
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
+static bool seg_path(int D) {
+  return D == 8 || D == 16 || D == 32 || D == 64 || D == 128 || D == 256;
+}
+
 int64_t emb_grad_part_floats(int64_t nnz, int D) {
-  return (D == 128 || D == 256) ? ((nnz + kSegRun - 1) / kSegRun) * 2 * D : 0;
+  return seg_path(D) ? ((nnz + kSegRun - 1) / kSegRun) * 2 * D : 0;
 }
 
 void emb_grad_reduce(const int32_t* pos_s, const int32_t* segid, const int32_t* seg_start,
                      const int32_t* n_uniq, int64_t u_cap, int64_t nnz, const void* dX0, int D,
                      float* dE, float* part, hipStream_t st) {
   if (u_cap <= 0 || nnz <= 0) return;
-  if (part && (D == 128 || D == 256)) {
+  if (part && seg_path(D)) {
     const int64_t runs = (nnz + kSegRun - 1) / kSegRun;
     const dim3 grid((unsigned)((runs + 3) / 4));
     const uint32_t* x = reinterpret_cast<const uint32_t*>(dX0);
-    if (D == 128) {
+    const uint16_t* x16 = reinterpret_cast<const uint16_t*>(dX0);
+#define PSAMD_NARROW(DD)                                                                    \
+  emb_grad_lane_kernel<DD><<<grid, 256, 0, st>>>(pos_s, segid, seg_start, u_cap, nnz, x16, dE, \
+                                                 part);                                      \
+  PSAMD_HIP_CHECK(hipGetLastError());                                                       \
+  emb_grad_cross_narrow_kernel<DD><<<grid, 256, 0, st>>>(segid, seg_start, u_cap, nnz, part, dE)
+    if (D == 8) {
+      PSAMD_NARROW(8);
+    } else if (D == 16) {
+      PSAMD_NARROW(16);
+    } else if (D == 32) {
+      PSAMD_NARROW(32);
+    } else if (D == 64) {
+      PSAMD_NARROW(64);
+    } else if (D == 128) {
       emb_grad_seg_kernel<1><<<grid, 256, 0, st>>>(pos_s, segid, seg_start, u_cap, nnz, x, dE, part);
       PSAMD_HIP_CHECK(hipGetLastError());
       emb_grad_cross_kernel<1><<<grid, 256, 0, st>>>(segid, seg_start, u_cap, nnz, part, dE);
@@ -548,6 +639,7 @@ void emb_grad_reduce(const int32_t* pos_s, const int32_t* segid, const int32_t* 
       PSAMD_HIP_CHECK(hipGetLastError());
       emb_grad_cross_kernel<2><<<grid, 256, 0, st>>>(segid, seg_start, u_cap, nnz, part, dE);
     }
+#undef PSAMD_NARROW
     PSAMD_HIP_CHECK(hipGetLastError());
     return;
   }

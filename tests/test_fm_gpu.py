@@ -39,3 +39,34 @@ def test_fm_gpu_vals_and_learning():
         if s % 10 == 9:
             losses.append(tr.progress()["loss"])
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("D,S,with_vals", [(16, 39, False), (8, 39, True), (32, 64, True),
+                                           (16, 5, True), (48, 39, True)])
+def test_fm_kernel_matches_torch(D, S, with_vals):
+    """fm_fwd_bwd (lane-per-position kernel for D <= 32, S <= 64; the feature-lane
+    kernel otherwise) against the PyTorch forward/backward of the same inputs."""
+    from parameter_server_amd.ops.linear import AUC_BINS, accum_total, new_accum
+    from parameter_server_amd.ops.native import hipops
+
+    B, U = 1000, 700
+    g = torch.Generator().manual_seed(D + S)
+    X0 = (torch.randn(B * S, D, generator=g) * 0.3).to(torch.bfloat16)
+    vals = torch.rand(B * S, generator=g) + 0.5 if with_vals else None
+    lc = torch.randint(0, U, (B * S,), generator=g, dtype=torch.int32)
+    w = torch.randn(U, generator=g) * 0.1
+    y = torch.where(torch.rand(B, generator=g) < 0.4, 1.0, -1.0)
+    ref = FMTrainer(FMConfig(**dict(CFG, embedding_dim=D, slots=S, minibatch=B)))
+    dref = ref._fwd_bwd_torch(X0, vals, B, S, lc, w, y)
+    coef = torch.empty(B, device="cuda")
+    dX0 = torch.empty(B * S, D, dtype=torch.bfloat16, device="cuda")
+    met = new_accum("cuda")
+    hist = torch.zeros(2 * AUC_BINS, dtype=torch.int32, device="cuda")
+    hipops().fm_fwd_bwd(X0.cuda(), None if vals is None else vals.cuda(), B, S, lc.cuda(),
+                        w.cuda(), y.cuda(), coef, dX0, met, hist, AUC_BINS)
+    torch.testing.assert_close(coef.cpu(), ref.coef[:B], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dX0.float().cpu(), dref.float(), rtol=2e-2, atol=1e-3)
+    m = accum_total(met).cpu()
+    assert abs(float(m[0]) - float(ref.metrics[0])) < 1e-3 * B
+    assert float(m[2]) == B
+    assert abs(int((hist.cpu() - ref.hist).abs().sum())) <= 4
