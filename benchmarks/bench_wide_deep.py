@@ -25,13 +25,22 @@ def main():
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--table-slots", type=int, default=1 << 27, help="slots per GPU")
     ap.add_argument("--gemm", default="auto", choices=("auto", "mfma", "hipblaslt"))
+    ap.add_argument("--emulate-peers", type=int, default=0,
+                    help="1 process: the N-GPU step (key exchange + owner updates + dense "
+                         "all-reduce) with N emulated peers over a loopback comm")
     args = ap.parse_args()
     from parameter_server_amd.models.wide_deep import WideDeepConfig, WideDeepTrainer
     from parameter_server_amd.ops.synthetic import criteo_batch
     from parameter_server_amd.parallel.comm import init_from_env
 
     comm, dev = init_from_env("cuda")
+    if args.emulate_peers > 1 and comm.world == 1:
+        from parameter_server_amd.parallel.comm import LoopbackComm
+
+        comm = LoopbackComm(args.emulate_peers, dev)
     G, rank = comm.world, comm.rank
+    emu = comm.backend == "loopback" if hasattr(comm, "backend") else False
+    NG = 1 if emu else G  # GPUs actually running
     B, N = args.minibatch, int(args.num_features)
     cfg = WideDeepConfig(num_features=N, embedding_dim=args.dim, minibatch=B,
                          table_capacity=args.table_slots, gemm=args.gemm, seed=0)
@@ -57,7 +66,7 @@ def main():
     torch.cuda.synchronize()
     comm.barrier()
     dt = time.perf_counter() - t0
-    x = torch.tensor([dt], dtype=torch.float64, device=dev if G > 1 else "cpu")
+    x = torch.tensor([dt], dtype=torch.float64, device=dev if NG > 1 else "cpu")
     comm.all_reduce_(x, op="max")
     dt = float(x.item())
     p = tr.progress()
@@ -65,16 +74,17 @@ def main():
     if rank == 0:
         print(json.dumps({
             "metric": "examples/sec (whole node) wide&deep 1e9x128 bf16 embeddings + MLP",
-            "value": G * B * args.steps / dt, "unit": "examples/sec", "n_gpus": G,
+            "value": NG * B * args.steps / dt, "unit": "examples/sec", "n_gpus": NG,
+            "emulated_peers": G if emu else None,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True, "scaling": "weak", "dtype": "bf16 (fp32 accumulate)",
             "config": {"num_features": N, "embedding_dim": args.dim, "slots": 39,
-                       "hidden": list(cfg.hidden), "global_batch": G * B, "gemm": args.gemm,
+                       "hidden": list(cfg.hidden), "global_batch": NG * B, "gemm": args.gemm,
                        "table_slots_per_gpu": tr.shard.capacity,
                        "shard_gb": tr.shard.nbytes() / 2 ** 30, "mlp_params": tr.num_params},
             "train": {**p, "rows_rank0": occ},
         }), flush=True)
-    if G > 1:
+    if NG > 1:
         import torch.distributed as dist
 
         dist.destroy_process_group()

@@ -10,11 +10,13 @@
 //   emb_gather_rows  rows[slot[i]] -> out[i]          (pull replies, G > 1)
 //   emb_expand       X0[p] = src[idx[p]], p = b*S + s (the [B, S*D] MLP input)
 //   emb_grad_reduce  dE[u] = sum of dX0 rows of u's occurrences (CSC order of the
-//                    localiser: no atomics, fp32 accumulation)
+//                    localiser, 64-entry runs per wavefront: no atomics, fp32
+//                    accumulation, deterministic cross-run partials)
 //   emb_update       row-wise AdaGrad: acc += mean(g^2); row -= lr g / sqrt(acc + eps)
 //   wd_head          deep logit (h.w + b) + wide margin, logistic loss, metrics,
-//                    AUC histogram, dL/dlogit, dh = coef w * relu'(h), dw, db
-//   colsum_bf16      bias gradients
+//                    AUC histogram, dL/dlogit, dh = coef w * relu'(h), db
+//   colred_bf16      column reductions: dw = h^T coef, the last hidden layer's bias
+//                    gradient, plain column sums (library-GEMM backend)
 //   adam_update      fp32 master weights + bf16 copy for the GEMMs
 #include "common.cuh"
 
