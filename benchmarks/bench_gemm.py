@@ -78,6 +78,12 @@ if "--wd-backends" in sys.argv:
             "dX mm": t(lambda: torch.mm(dZ, W)),
             "dW own split": t(lambda: G.linear_weight_grad(dZ, X, out=dW)),
             "dW mm fp32": t(lambda: torch.mm(dZ.t(), X, out_dtype=torch.float32)),
+            "dW transpose+mm NT": t(lambda: torch.mm(dZ.t().contiguous(), X.t().contiguous().t(),
+                                                     out_dtype=torch.float32)),
+            "dW transpose only": t(lambda: (dZ.t().contiguous(), X.t().contiguous())),
+            "dW transpose+own NT": t(lambda: G.gemm(dZ.t().contiguous(), True,
+                                                    X.t().contiguous(), True, N, K, Bn,
+                                                    out_bf16=False, out_f32=dW)),
         }
         for k, v in res.items():
             print(json.dumps({"layer": f"{K}->{N}", "op": k, "us": v * 1e6,
