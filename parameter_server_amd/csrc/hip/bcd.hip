@@ -174,6 +174,91 @@ bcd_dual_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row
   }
 }
 
+// K11, load-balanced: the block's CSC range is cut ONCE on the host (the matrix
+// does not change between passes) into chunks of two kinds, one wavefront each:
+//  * small: whole columns of <= 64 entries packed into <= 64 entries: the in-wave
+//    segmented scan above, every column stored with a plain store;
+//  * hot: <= kHotChunk entries of ONE column (> 64 entries): lanes accumulate
+//    their strided entries (independent iterations, loads in flight), one wave
+//    sum, one fp64 atomic per chunk.
+// The flat kernel above sends one atomic per 64 entries of a wave-spanning
+// column: a column present in every example (4 M entries) serialises ~62 k
+// same-address fp64 atomics (~1.5 ms for the block); here it is 4 M / 4096.
+constexpr int64_t kHotBit = int64_t(1) << 62;
+
+__device__ __forceinline__ void bcd_gu(int64_t i, int64_t c, int64_t c0,
+                                       const int32_t* __restrict__ row,
+                                       const float* __restrict__ val,
+                                       const double* __restrict__ ym, const float* __restrict__ y,
+                                       int64_t nrows, double dl, double& g, double& u) {
+  const int32_t r = row[i];
+  if (!in_range(r, nrows)) return;
+  const double tau = 1.0 / (1.0 + exp(ym[r]));
+  const double yr = (double)y[r];
+  const double t2 = tau * (1.0 - tau);
+  if (val) {
+    const double v = (double)val[i];
+    g += -yr * tau * v;
+    u += fmin(t2 * exp(fabs(v) * dl), 0.25) * v * v;
+  } else {
+    g += -yr * tau;
+    u += fmin(t2 * exp(dl), 0.25);
+  }
+}
+
+__global__ void __launch_bounds__(256)
+bcd_grad_chunk_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row,
+                      const float* __restrict__ val, const int64_t* __restrict__ chunks,
+                      int64_t nchunks, int64_t c0, int64_t ncols,
+                      const double* __restrict__ ym, const float* __restrict__ y, int64_t nrows,
+                      const double* __restrict__ delta, const uint8_t* __restrict__ active,
+                      double* __restrict__ G, double* __restrict__ U) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t k = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); k < nchunks;
+       k += nw) {
+    const int64_t e0 = chunks[k], e1 = chunks[k + 1];
+    const bool hot = (e0 & kHotBit) != 0;
+    const int64_t a = e0 & ~kHotBit, b = e1 & ~kHotBit;
+    if (hot) {
+      const int64_t c = (int64_t)col[a] - c0;  // wave-uniform
+      if (c < 0 || c >= ncols || !active[c0 + c]) continue;
+      const double dl = delta[c0 + c];
+      double g = 0, u = 0;
+#pragma unroll 4
+      for (int64_t i = a + lane; i < b; i += 64) bcd_gu(i, c, c0, row, val, ym, y, nrows, dl, g, u);
+      g = wave_allsum(g);
+      u = wave_allsum(u);
+      if (lane == 0) {
+        unsafeAtomicAdd(&G[c], g);
+        unsafeAtomicAdd(&U[c], u);
+      }
+      continue;
+    }
+    const int64_t i = a + lane;
+    const bool valid = i < b;
+    int64_t c = -1;
+    double g = 0, u = 0;
+    if (valid) {
+      c = (int64_t)col[i] - c0;
+      if (c < 0 || c >= ncols) c = -1;
+      else if (active[c0 + c]) bcd_gu(i, c, c0, row, val, ym, y, nrows, delta[c0 + c], g, u);
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double go = shfl_up_d(g, off);
+      const double uo = shfl_up_d(u, off);
+      const int64_t co = __shfl_up(c, off, 64);
+      if (lane >= off && co == c) { g += go; u += uo; }
+    }
+    const int64_t c_next = __shfl_down(c, 1, 64);
+    if (valid && c >= 0 && (lane == 63 || i + 1 >= b || c_next != c)) {
+      G[c] = g;  // whole column inside the chunk
+      U[c] = u;
+    }
+  }
+}
+
 // objective: out[0] += sum_i log(1 + exp(-ym_i))
 __global__ void __launch_bounds__(256)
 bcd_objective_kernel(const double* __restrict__ ym, int64_t n, double* __restrict__ out) {
@@ -221,6 +306,18 @@ void bcd_grad(const int32_t* col, const int32_t* row, const float* val, int64_t 
   if (p1 <= p0) return;
   bcd_grad_kernel<<<grid_for(p1 - p0, 256, 4096), 256, 0, st>>>(
       col, row, val, p0, p1, c0, ncols, ym, y, nrows, delta, active, G, U);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void bcd_grad_chunked(const int32_t* col, const int32_t* row, const float* val,
+                      const int64_t* chunks, int64_t nchunks, int64_t c0, int64_t ncols,
+                      const double* ym, const float* y, int64_t nrows, const double* delta,
+                      const uint8_t* active, double* G, double* U, hipStream_t st) {
+  PSAMD_HIP_CHECK(hipMemsetAsync(G, 0, ncols * sizeof(double), st));
+  PSAMD_HIP_CHECK(hipMemsetAsync(U, 0, ncols * sizeof(double), st));
+  if (nchunks <= 0) return;
+  bcd_grad_chunk_kernel<<<grid_for(nchunks, 4, 16384), 256, 0, st>>>(
+      col, row, val, chunks, nchunks, c0, ncols, ym, y, nrows, delta, active, G, U);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -106,6 +106,9 @@ void key_signature(const uint64_t*, int64_t, unsigned long long*, hipStream_t);
 void bcd_grad(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
               const double*, const float*, int64_t, const double*, const uint8_t*, double*,
               double*, hipStream_t);
+void bcd_grad_chunked(const int32_t*, const int32_t*, const float*, const int64_t*, int64_t,
+                      int64_t, int64_t, const double*, const float*, int64_t, const double*,
+                      const uint8_t*, double*, double*, hipStream_t);
 void bcd_update(int64_t, int64_t, const double*, const double*, double*, double*, uint8_t*,
                 double*, double, double, double, double, unsigned long long*, hipStream_t);
 void bcd_dual(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
@@ -883,6 +886,33 @@ PYBIND11_MODULE(_hipops, m) {
       check(val->numel() == col.numel(), "val size mismatch");
     }
   };
+  m.def("bcd_grad_chunked", [](Tensor col, Tensor row, optional<Tensor> val, Tensor chunks,
+                                int64_t c0, int64_t ncols, Tensor ym, Tensor y, Tensor delta,
+                                Tensor active, Tensor G, Tensor U) {
+    // chunks: [n + 1] int64 entry offsets (bit 62 = hot chunk), built and range-checked
+    // on the host once per block (models/darlin.py build_chunks)
+    chk(col, at::kInt, "col");
+    chk(row, at::kInt, "row");
+    chk(chunks, at::kLong, "chunks");
+    check(chunks.numel() >= 1, "chunks needs the end sentinel");
+    chk(ym, at::kDouble, "ym");
+    chk(y, at::kFloat, "y");
+    chk(delta, at::kDouble, "delta");
+    chk(active, at::kByte, "active");
+    chk(G, at::kDouble, "G");
+    chk(U, at::kDouble, "U");
+    check(row.numel() == col.numel(), "col/row size mismatch");
+    const float* vp = optr<float>(val, at::kFloat, "val");
+    if (vp) check(val->numel() == col.numel(), "val size mismatch");
+    check(y.numel() == ym.numel(), "y/ym size mismatch");
+    check(delta.numel() == active.numel(), "delta/active size mismatch");
+    check(c0 >= 0 && ncols >= 0 && c0 + ncols <= delta.numel(), "column block outside model");
+    check(G.numel() >= ncols && U.numel() >= ncols, "G/U too small");
+    psamd::bcd_grad_chunked(ptr<int32_t>(col), ptr<int32_t>(row), vp, ptr<int64_t>(chunks),
+                            chunks.numel() - 1, c0, ncols, ptr<double>(ym), ptr<float>(y),
+                            ym.numel(), ptr<double>(delta), ptr<uint8_t>(active), ptr<double>(G),
+                            ptr<double>(U), cur_stream());
+  });
   m.def("bcd_grad", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                 int64_t p1, int64_t c0, int64_t ncols, Tensor ym, Tensor y,
                                 Tensor delta, Tensor active, Tensor G, Tensor U) {

@@ -139,6 +139,7 @@ class Block:
     c1: int
     p0: int
     p1: int
+    chunks: object = None  # device work list of the chunked gradient kernel (GPU)
 
     @property
     def ncols(self):
@@ -273,8 +274,27 @@ class DarlinTrainer:
             fb = int(_flip(np.array([b - 1], np.uint64))[0])
             c0 = self.group_base[g] + int(np.searchsorted(gk, fa, side="left"))
             c1 = self.group_base[g] + int(np.searchsorted(gk, fb, side="right"))
-            self.blocks.append(Block(g, a, b, c0, c1, int(colptr[c0]), int(colptr[c1])))
+            blk = Block(g, a, b, c0, c1, int(colptr[c0]), int(colptr[c1]))
+            if dev.type == "cuda":
+                blk.chunks = torch.from_numpy(bcd.build_chunks(colptr, c0, c1)).to(dev)
+            self.blocks.append(blk)
         self.blk_order, self.prior_order = block_orders(self.blocks, cfg, self.rng)
+        # row-sorted copy of every block's entries for the dual update: each example
+        # has ~1 entry per block, so its margin update walks ym sequentially
+        # (coalesced, uncontended atomics) instead of gathering it in column order
+        self.col_r, self.row_r, self.val_r = self.col, self.row, self.val
+        if dev.type == "cuda" and self.nnz:
+            self.col_r, self.row_r = torch.empty_like(self.col), torch.empty_like(self.row)
+            self.val_r = None if self.val is None else torch.empty_like(self.val)
+            for blk in self.blocks:
+                p0, p1 = blk.p0, blk.p1
+                if p1 <= p0:
+                    continue
+                rs, perm = torch.sort(self.row[p0:p1], stable=True)
+                self.row_r[p0:p1] = rs
+                self.col_r[p0:p1] = self.col[p0:p1][perm]
+                if self.val is not None:
+                    self.val_r[p0:p1] = self.val[p0:p1][perm]
         # model state (replicated per rank) and margins
         f64 = torch.float64
         self.w = torch.full((base,), float(cfg.init_w), dtype=f64, device=dev)
@@ -295,7 +315,7 @@ class DarlinTrainer:
         GU = torch.empty(2 * b.ncols, dtype=torch.float64, device=self.device)
         G, U = GU[:b.ncols], GU[b.ncols:]
         bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
-                 self.delta, self.active, G, U)
+                 self.delta, self.active, G, U, chunks=b.chunks)
         work = self.comm.all_reduce_async(GU) if self.G > 1 else None
         return (b, GU, work)
 
@@ -307,7 +327,8 @@ class DarlinTrainer:
         c = self.cfg
         dw, _ = bcd.update(b.c0, b.ncols, G, U, self.w, self.delta, self.active, c.eta, c.l1,
                            c.delta_max, self.kkt_thr, vio=self.vio)
-        bcd.dual(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, dw, self.y, self.ym)
+        bcd.dual(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, dw, self.y,
+                 self.ym)
 
     def run_pass(self, it: int, reset_kkt: bool = False) -> BCDProgress:
         cfg = self.cfg

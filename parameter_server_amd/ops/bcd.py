@@ -20,21 +20,61 @@ darlin.h:472-502, objective darlin.h:504-511, server evaluate darlin.h:248-265.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from .native import hipops, is_gpu
 
 
+HOT_BIT = 1 << 62
+
+
+def build_chunks(colptr, c0: int, c1: int, small: int = 64, hot: int = 4096) -> np.ndarray:
+    """Load-balanced work list of the CSC columns [c0, c1) for ``grad``'s chunked
+    kernel: int64 entry offsets (+ end sentinel); columns of <= ``small`` entries
+    are packed whole into chunks of <= ``small`` entries, longer ("hot") columns
+    are cut into pieces of <= ``hot`` entries flagged with HOT_BIT."""
+    cp = np.asarray(colptr, dtype=np.int64)
+    n = np.diff(cp[c0:c1 + 1])
+    out = []
+    cur, cur_len = -1, 0
+    for j in np.flatnonzero(n):
+        a, m = int(cp[c0 + j]), int(n[j])
+        if m > small:
+            if cur >= 0:
+                out.append(cur)
+                cur = -1
+            out.extend(p | HOT_BIT for p in range(a, a + m, hot))
+            continue
+        if cur < 0 or cur_len + m > small:
+            if cur >= 0:
+                out.append(cur)
+            cur, cur_len = a, 0
+        cur_len += m
+    if cur >= 0:
+        out.append(cur)
+    out.append(int(cp[c1]))
+    ch = np.asarray(out, dtype=np.int64)
+    pos = ch & ~HOT_BIT
+    assert np.all(np.diff(pos) > 0) and pos[0] >= cp[c0] and pos[-1] == cp[c1]
+    return ch
+
+
 def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, active,
-         G=None, U=None):
-    """Block gradient: returns (G, U) fp64[ncols] (inactive columns contribute 0)."""
+         G=None, U=None, chunks=None):
+    """Block gradient: returns (G, U) fp64[ncols] (inactive columns contribute 0).
+    ``chunks`` (device int64 from ``build_chunks``) selects the load-balanced kernel."""
     dev = ym.device
     if G is None:
         G = torch.empty(ncols, dtype=torch.float64, device=dev)
     if U is None:
         U = torch.empty(ncols, dtype=torch.float64, device=dev)
     if is_gpu(ym):
-        hipops().bcd_grad(col, row, val, p0, p1, c0, ncols, ym, y, delta, active, G, U)
+        if chunks is not None:
+            hipops().bcd_grad_chunked(col, row, val, chunks, c0, ncols, ym, y, delta, active,
+                                      G, U)
+        else:
+            hipops().bcd_grad(col, row, val, p0, p1, c0, ncols, ym, y, delta, active, G, U)
         return G, U
     G.zero_()
     U.zero_()

@@ -49,6 +49,12 @@ def test_bcd_kernels_match_torch(valued):
                           D(active))
         torch.testing.assert_close(Gg.cpu(), Gc, rtol=1e-10, atol=1e-10)
         torch.testing.assert_close(Ug.cpu(), Uc, rtol=1e-10, atol=1e-10)
+        for small, hot in ((64, 4096), (64, 1000), (16, 64)):  # load-balanced chunk kernel
+            ch = D(bcd.build_chunks(colptr, c0, c1, small=small, hot=hot))
+            Gk, Uk = bcd.grad(D(col), D(row), D(val), p0, p1, c0, c1 - c0, D(ym), D(y),
+                              D(delta), D(active), chunks=ch)
+            torch.testing.assert_close(Gk.cpu(), Gc, rtol=1e-10, atol=1e-10)
+            torch.testing.assert_close(Uk.cpu(), Uc, rtol=1e-10, atol=1e-10)
         for thr in (1e20, 0.05):
             wc, dc, ac = T(w.copy()), T(delta.copy()), T(active.copy())
             wg, dg, ag = D(w.copy()), D(delta.copy()), D(active.copy())
