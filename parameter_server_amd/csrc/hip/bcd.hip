@@ -111,17 +111,23 @@ bcd_grad_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row
 // (darlin.h:206-246). dw receives the applied change (0 if inactive / filtered).
 // Violation is max-reduced as the bit pattern of a non-negative double.
 __global__ void __launch_bounds__(256)
-bcd_update_kernel(int64_t c0, int64_t ncols, const double* __restrict__ G,
-                  const double* __restrict__ U, double* __restrict__ w, double* __restrict__ delta,
+bcd_update_kernel(int64_t c0, int64_t ncols, double* __restrict__ G, double* __restrict__ U,
+                  double* __restrict__ w, double* __restrict__ delta,
                   uint8_t* __restrict__ active, double* __restrict__ dw, double eta, double lambda,
-                  double delta_max, double kkt_thr, unsigned long long* __restrict__ vio_bits) {
+                  double delta_max, double kkt_thr, unsigned long long* __restrict__ vio_bits,
+                  int consume) {
   double vmax = 0;
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < ncols;
        j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t k = c0 + j;
     double d = 0;
+    const double gj = G[j], uj = U[j];
+    if (consume) {  // leave G / U zeroed for the block's next gradient (no memsets)
+      G[j] = 0;
+      U[j] = 0;
+    }
     if (active[k]) {
-      const double g = G[j], u = U[j] / eta + 1e-10;
+      const double g = gj, u = uj / eta + 1e-10;
       const double gp = g + lambda, gn = g - lambda;
       const double wk = w[k];
       double vio = 0;
@@ -312,21 +318,25 @@ void bcd_grad(const int32_t* col, const int32_t* row, const float* val, int64_t 
 void bcd_grad_chunked(const int32_t* col, const int32_t* row, const float* val,
                       const int64_t* chunks, int64_t nchunks, int64_t c0, int64_t ncols,
                       const double* ym, const float* y, int64_t nrows, const double* delta,
-                      const uint8_t* active, double* G, double* U, hipStream_t st) {
-  PSAMD_HIP_CHECK(hipMemsetAsync(G, 0, ncols * sizeof(double), st));
-  PSAMD_HIP_CHECK(hipMemsetAsync(U, 0, ncols * sizeof(double), st));
+                      const uint8_t* active, double* G, double* U, bool zeroed,
+                      hipStream_t st) {
+  if (!zeroed) {
+    PSAMD_HIP_CHECK(hipMemsetAsync(G, 0, ncols * sizeof(double), st));
+    PSAMD_HIP_CHECK(hipMemsetAsync(U, 0, ncols * sizeof(double), st));
+  }
   if (nchunks <= 0) return;
   bcd_grad_chunk_kernel<<<grid_for(nchunks, 4, 16384), 256, 0, st>>>(
       col, row, val, chunks, nchunks, c0, ncols, ym, y, nrows, delta, active, G, U);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void bcd_update(int64_t c0, int64_t ncols, const double* G, const double* U, double* w,
-                double* delta, uint8_t* active, double* dw, double eta, double lambda,
-                double delta_max, double kkt_thr, unsigned long long* vio_bits, hipStream_t st) {
+void bcd_update(int64_t c0, int64_t ncols, double* G, double* U, double* w, double* delta,
+                uint8_t* active, double* dw, double eta, double lambda, double delta_max,
+                double kkt_thr, unsigned long long* vio_bits, bool consume, hipStream_t st) {
   if (ncols <= 0) return;
   bcd_update_kernel<<<grid_for(ncols, 256, 4096), 256, 0, st>>>(
-      c0, ncols, G, U, w, delta, active, dw, eta, lambda, delta_max, kkt_thr, vio_bits);
+      c0, ncols, G, U, w, delta, active, dw, eta, lambda, delta_max, kkt_thr, vio_bits,
+      consume ? 1 : 0);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -108,9 +108,9 @@ void bcd_grad(const int32_t*, const int32_t*, const float*, int64_t, int64_t, in
               double*, hipStream_t);
 void bcd_grad_chunked(const int32_t*, const int32_t*, const float*, const int64_t*, int64_t,
                       int64_t, int64_t, const double*, const float*, int64_t, const double*,
-                      const uint8_t*, double*, double*, hipStream_t);
-void bcd_update(int64_t, int64_t, const double*, const double*, double*, double*, uint8_t*,
-                double*, double, double, double, double, unsigned long long*, hipStream_t);
+                      const uint8_t*, double*, double*, bool, hipStream_t);
+void bcd_update(int64_t, int64_t, double*, double*, double*, double*, uint8_t*, double*, double,
+                double, double, double, unsigned long long*, bool, hipStream_t);
 void bcd_dual(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
               const double*, const float*, double*, int64_t, hipStream_t);
 void bcd_objective(const double*, int64_t, double*, hipStream_t);
@@ -888,7 +888,7 @@ PYBIND11_MODULE(_hipops, m) {
   };
   m.def("bcd_grad_chunked", [](Tensor col, Tensor row, optional<Tensor> val, Tensor chunks,
                                 int64_t c0, int64_t ncols, Tensor ym, Tensor y, Tensor delta,
-                                Tensor active, Tensor G, Tensor U) {
+                                Tensor active, Tensor G, Tensor U, bool zeroed) {
     // chunks: [n + 1] int64 entry offsets (bit 62 = hot chunk), built and range-checked
     // on the host once per block (models/darlin.py build_chunks)
     chk(col, at::kInt, "col");
@@ -911,7 +911,7 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::bcd_grad_chunked(ptr<int32_t>(col), ptr<int32_t>(row), vp, ptr<int64_t>(chunks),
                             chunks.numel() - 1, c0, ncols, ptr<double>(ym), ptr<float>(y),
                             ym.numel(), ptr<double>(delta), ptr<uint8_t>(active), ptr<double>(G),
-                            ptr<double>(U), cur_stream());
+                            ptr<double>(U), zeroed, cur_stream());
   });
   m.def("bcd_grad", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                 int64_t p1, int64_t c0, int64_t ncols, Tensor ym, Tensor y,
@@ -933,7 +933,7 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("bcd_update", [](int64_t c0, int64_t ncols, Tensor G, Tensor U, Tensor w, Tensor delta,
                          Tensor active, Tensor dw, double eta, double lambda, double delta_max,
-                         double kkt_thr, Tensor vio_bits) {
+                         double kkt_thr, Tensor vio_bits, bool consume) {
     chk(G, at::kDouble, "G");
     chk(U, at::kDouble, "U");
     chk(w, at::kDouble, "w");
@@ -947,7 +947,8 @@ PYBIND11_MODULE(_hipops, m) {
     check(eta > 0, "eta must be > 0");
     psamd::bcd_update(c0, ncols, ptr<double>(G), ptr<double>(U), ptr<double>(w),
                       ptr<double>(delta), ptr<uint8_t>(active), ptr<double>(dw), eta, lambda,
-                      delta_max, kkt_thr, ptr<unsigned long long>(vio_bits), cur_stream());
+                      delta_max, kkt_thr, ptr<unsigned long long>(vio_bits), consume,
+                      cur_stream());
   });
   m.def("bcd_dual", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                 int64_t p1, int64_t c0, int64_t ncols, Tensor dw, Tensor y,

@@ -140,6 +140,8 @@ class Block:
     p0: int
     p1: int
     chunks: object = None  # device work list of the chunked gradient kernel (GPU)
+    gu: object = None      # device [G | U] buffer of the block (GPU)
+    busy: bool = False     # gu holds a launched, not yet consumed gradient
 
     @property
     def ncols(self):
@@ -277,6 +279,8 @@ class DarlinTrainer:
             blk = Block(g, a, b, c0, c1, int(colptr[c0]), int(colptr[c1]))
             if dev.type == "cuda":
                 blk.chunks = torch.from_numpy(bcd.build_chunks(colptr, c0, c1)).to(dev)
+                # persistent [G | U], zeroed by the update that consumes it
+                blk.gu = torch.zeros(2 * (c1 - c0), dtype=torch.float64, device=dev)
             self.blocks.append(blk)
         self.blk_order, self.prior_order = block_orders(self.blocks, cfg, self.rng)
         # row-sorted copy of every block's entries for the dual update: each example
@@ -312,21 +316,28 @@ class DarlinTrainer:
 
     # -------------------------------------------------------------- one pass
     def _launch(self, b: Block):
-        GU = torch.empty(2 * b.ncols, dtype=torch.float64, device=self.device)
+        # the block's persistent [G | U] unless a previous launch of the same block is
+        # still in flight (a prior block re-launched within the delay window)
+        zeroed = b.gu is not None and not b.busy
+        GU = b.gu if zeroed else torch.empty(2 * b.ncols, dtype=torch.float64, device=self.device)
+        if zeroed:
+            b.busy = True
         G, U = GU[:b.ncols], GU[b.ncols:]
         bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
-                 self.delta, self.active, G, U, chunks=b.chunks)
+                 self.delta, self.active, G, U, chunks=b.chunks, zeroed=zeroed)
         work = self.comm.all_reduce_async(GU) if self.G > 1 else None
-        return (b, GU, work)
+        return (b, GU, work, zeroed)
 
     def _finish(self, item):
-        b, GU, work = item
+        b, GU, work, persistent = item
         if work is not None:
             work.wait()
         G, U = GU[:b.ncols], GU[b.ncols:]
         c = self.cfg
         dw, _ = bcd.update(b.c0, b.ncols, G, U, self.w, self.delta, self.active, c.eta, c.l1,
-                           c.delta_max, self.kkt_thr, vio=self.vio)
+                           c.delta_max, self.kkt_thr, vio=self.vio, consume=persistent)
+        if persistent:
+            b.busy = False
         bcd.dual(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, dw, self.y,
                  self.ym)
 

@@ -61,9 +61,10 @@ def build_chunks(colptr, c0: int, c1: int, small: int = 64, hot: int = 4096) -> 
 
 
 def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, active,
-         G=None, U=None, chunks=None):
+         G=None, U=None, chunks=None, zeroed: bool = False):
     """Block gradient: returns (G, U) fp64[ncols] (inactive columns contribute 0).
-    ``chunks`` (device int64 from ``build_chunks``) selects the load-balanced kernel."""
+    ``chunks`` (device int64 from ``build_chunks``) selects the load-balanced kernel;
+    ``zeroed``: G / U already hold zeros (left by ``update(consume=True)``)."""
     dev = ym.device
     if G is None:
         G = torch.empty(ncols, dtype=torch.float64, device=dev)
@@ -72,7 +73,7 @@ def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, act
     if is_gpu(ym):
         if chunks is not None:
             hipops().bcd_grad_chunked(col, row, val, chunks, c0, ncols, ym, y, delta, active,
-                                      G, U)
+                                      G, U, zeroed)
         else:
             hipops().bcd_grad(col, row, val, p0, p1, c0, ncols, ym, y, delta, active, G, U)
         return G, U
@@ -99,10 +100,11 @@ def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, act
 
 
 def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
-           delta_max: float, kkt_thr: float, dw=None, vio=None):
+           delta_max: float, kkt_thr: float, dw=None, vio=None, consume: bool = False):
     """Coordinate update of block [c0, c0+ncols). Returns (dw fp64[ncols], vio) where
     ``vio`` is an int64[1] tensor holding the max KKT violation as fp64 bits
-    (max-accumulated across calls; see ``violation``)."""
+    (max-accumulated across calls; see ``violation``). ``consume`` zeroes G / U
+    after reading them."""
     dev = w.device
     if dw is None:
         dw = torch.empty(ncols, dtype=torch.float64, device=dev)
@@ -110,7 +112,7 @@ def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
         vio = torch.zeros(1, dtype=torch.int64, device=dev)
     if is_gpu(w):
         hipops().bcd_update(c0, ncols, G, U, w, delta, active, dw, eta, lam, delta_max, kkt_thr,
-                            vio)
+                            vio, consume)
         return dw, vio
     sl = slice(c0, c0 + ncols)
     act = active[sl].bool()
@@ -136,6 +138,9 @@ def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
     cur = violation(vio)
     if vm > cur:
         vio.copy_(torch.tensor([vm], dtype=torch.float64).view(torch.int64))
+    if consume:
+        G[:ncols] = 0
+        U[:ncols] = 0
     return dw, vio
 
 
