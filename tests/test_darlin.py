@@ -317,3 +317,30 @@ darlin {{ max_pass_of_data: 6 epsilon: 1e-9 feature_block_ratio: 2
     assert set(saved) == set(ref)
     for k in ref:
         assert abs(saved[k] - ref[k]) < 1e-4 * max(1.0, abs(ref[k]))
+
+
+def test_build_chunks_partitions_columns():
+    """Chunked-gradient work list: chunks tile [colptr[c0], colptr[c1]) exactly, small
+    chunks hold whole columns (<= small entries), hot chunks one column's piece."""
+    import numpy as np
+
+    from parameter_server_amd.ops.bcd import HOT_BIT, build_chunks
+
+    rng = np.random.default_rng(3)
+    n = rng.integers(0, 20, 500)
+    n[::37] = rng.integers(65, 9000, n[::37].size)
+    cp = np.zeros(n.size + 1, np.int64)
+    np.cumsum(n, out=cp[1:])
+    for c0, c1, small, hot in [(0, 500, 64, 4096), (37, 38, 64, 4096), (5, 300, 16, 100),
+                               (200, 200, 64, 4096)]:
+        ch = build_chunks(cp, c0, c1, small=small, hot=hot)
+        pos, isHot = ch & ~HOT_BIT, (ch & HOT_BIT) != 0
+        assert pos[0] == cp[c0] or c0 == c1 and pos[0] == cp[c1]
+        assert pos[-1] == cp[c1]
+        col_of = np.repeat(np.arange(n.size), n)
+        for a, b, h in zip(pos[:-1], pos[1:], isHot[:-1]):
+            cols = np.unique(col_of[a:b])
+            if h:
+                assert cols.size == 1 and n[cols[0]] > small and b - a <= hot
+            else:
+                assert b - a <= small and cp[cols[0]] == a and cp[cols[-1] + 1] == b
