@@ -190,6 +190,9 @@ bcd_dual_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row
 // The flat kernel above sends one atomic per 64 entries of a wave-spanning
 // column: a column present in every example (4 M entries) serialises ~62 k
 // same-address fp64 atomics (~1.5 ms for the block); here it is 4 M / 4096.
+// Measured and not kept (5.55 ms/pass, 4 M rows): interleaving {ym, y} per row
+// for the random row gather (5.55, no change: the rows live in L2 / MALL) and
+// forcing 8 waves/SIMD with __launch_bounds__(256, 8) (6.33: 12 VGPRs spill).
 constexpr int64_t kHotBit = int64_t(1) << 62;
 
 __device__ __forceinline__ void bcd_gu(int64_t i, int64_t c, int64_t c0,
