@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--table-slots", type=int, default=1 << 27, help="slots per GPU")
     ap.add_argument("--gemm", default="auto", choices=("auto", "mfma", "hipblaslt"))
+    ap.add_argument("--overlap-wgrad", type=int, default=1,
+                    help="weight-gradient GEMMs on a side stream next to the dX chain")
     ap.add_argument("--emulate-peers", type=int, default=0,
                     help="1 process: the N-GPU step (key exchange + owner updates + dense "
                          "all-reduce) with N emulated peers over a loopback comm")
@@ -43,7 +45,8 @@ def main():
     NG = 1 if emu else G  # GPUs actually running
     B, N = args.minibatch, int(args.num_features)
     cfg = WideDeepConfig(num_features=N, embedding_dim=args.dim, minibatch=B,
-                         table_capacity=args.table_slots, gemm=args.gemm, seed=0)
+                         table_capacity=args.table_slots, gemm=args.gemm, seed=0,
+                         overlap_wgrad=bool(args.overlap_wgrad))
     tr = WideDeepTrainer(cfg, comm, dev)
     keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
     labels = torch.empty(B, dtype=torch.float32, device=dev)

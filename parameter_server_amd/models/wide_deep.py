@@ -57,6 +57,7 @@ class WideDeepConfig:
     table_load: float = 0.5
     max_table_bytes: int = 160 << 30     # HBM budget of one shard (slots + rows)
     gemm: str = "auto"                   # auto (measured per product) | mfma | hipblaslt
+    overlap_wgrad: bool = True           # GPU: weight-gradient GEMMs on a side stream
     seed: int = 0
 
 
@@ -192,6 +193,7 @@ class WideDeepTrainer(EmbeddingPS):
             self.slot_buf = torch.empty(self.max_nnz, dtype=torch.int64, device=dev)
             self.w_buf = torch.empty(self.max_nnz, dtype=torch.float32, device=dev)
             self.dE = torch.empty(self.max_nnz, D, dtype=torch.float32, device=dev)
+        self._side = torch.cuda.Stream(dev) if self.gpu else None
         self.step_count = 0
         self.examples = 0
         self.t0 = time.time()
@@ -233,8 +235,21 @@ class WideDeepTrainer(EmbeddingPS):
                db_h=self.db[L - 1])
         # ---------------- MLP backward: ReLU masks and the bias gradient of the
         # layer below fused into the dX GEMMs (grads zeroed at the step start)
+        # The weight gradient of layer i and the input gradient of layer i both read
+        # dH only, so on the GPU the weight gradients run on a side stream next to the
+        # input-gradient chain and the sparse push (GEMMs that each use part of the
+        # chip overlap); the side stream joins before the dense all-reduce / Adam.
+        side = self._side if self.gpu and cfg.overlap_wgrad else None
+        main = torch.cuda.current_stream(dev) if side is not None else None
         for i in reversed(range(L)):
-            GM.linear_weight_grad(dH, acts[i], out=self.dW[i], backend=cfg.gemm)
+            if side is not None:
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    GM.linear_weight_grad(dH, acts[i], out=self.dW[i], backend=cfg.gemm)
+                dH.record_stream(side)
+                acts[i].record_stream(side)
+            else:
+                GM.linear_weight_grad(dH, acts[i], out=self.dW[i], backend=cfg.gemm)
             mask = acts[i] if i > 0 else None
             dH = GM.linear_input_grad(dH, self.W16[i], mask=mask, backend=cfg.gemm,
                                       colsum=self.db[i - 1] if i > 0 else None)
@@ -247,6 +262,8 @@ class WideDeepTrainer(EmbeddingPS):
             dE = E.grad_reduce(loc, dX0, D, loc.num_unique())
         g_wide, _ = linear_backward(loc, self.coef[:B], B=B, width=S)
         self._push(loc, push, dE, g_wide)
+        if side is not None:
+            main.wait_stream(side)
         # ---------------- dense update: one all-reduce, fused Adam
         if self.G > 1:
             self.comm.all_reduce_(self.grad)
