@@ -7,7 +7,7 @@ power-law ids hashed into 10^9 features), random-init (zero) FTRL state.
 
 Every rank is a colocated worker + server shard (weak scaling: the per-GPU
 minibatch is fixed). A timed step is the full training step: on-device data
-generation, key localisation, pull (RCCL all-to-all-v when N > 1), forward,
+generation, key localisation, pull (RCCL all-to-all when N > 1), forward,
 backward, push + server-side FTRL update, progress metrics (loss, accuracy,
 bucketed AUC). Nothing is skipped or cached across steps.
 
@@ -35,7 +35,7 @@ ALGO_NAMES = {"ftrl": "FTRL-proximal", "adagrad": "proximal AdaGrad", "sgd": "pr
 def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     """Software pipeline over HIP streams (every piece replays from HIP graphs):
 
-    * ``nprep`` high-priority preparation streams: stream s generates and localises
+    * ``nprep`` preparation streams (high priority on 1 GPU): stream s generates and localises
       every nprep-th minibatch (t % nprep == s) into its own workspaces, issued nprep
       steps ahead; with 2 * nprep buffers a preparation waits only for the step that
       last used its buffer. The kernels of a localisation are latency bound, so
