@@ -14,7 +14,9 @@ from parameter_server_amd.ops.localize import Localizer  # noqa: E402
 from parameter_server_amd.ops.synthetic import criteo_batch  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-keys, _ = criteo_batch(B, seed=3, row0=0, num_features=10 ** 9, device="cuda")
+BITS = int(os.environ.get("PSAMD_LOC_BITS", "30"))  # 34: 10^10 features
+keys, _ = criteo_batch(B, seed=3, row0=0, num_features=10 ** 10 if BITS > 32 else 10 ** 9,
+                       device="cuda")
 coef = torch.randn(B, device="cuda")
 
 
@@ -32,9 +34,9 @@ def t(fn, it=50):
 
 
 for mode in os.environ.get("PSAMD_LOC_MODES", "sort,tile,hash").split(","):
-    L = Localizer(B * 39, 30, "cuda", mode=mode)
+    L = Localizer(B * 39, BITS, "cuda", mode=mode)
     loc = L(keys)
     us_loc = t(lambda: L(keys))
     us_bwd = t(lambda: linear_backward(loc, coef, B=B, width=39))
-    print(json.dumps({"mode": mode, "digit_bits": getattr(L, "digit_bits", None), "B": B, "unique": loc.num_unique(), "localize_us": us_loc,
+    print(json.dumps({"mode": mode, "bits": BITS, "digit_bits": getattr(L, "digit_bits", None), "B": B, "unique": loc.num_unique(), "localize_us": us_loc,
                       "backward_us": us_bwd}), flush=True)

@@ -77,6 +77,8 @@ void owner_split(const uint64_t*, const int32_t*, int64_t, const uint64_t*, int,
 void owner_of(const uint64_t*, int64_t, const uint64_t*, int, int32_t*, hipStream_t);
 // sort32.hip
 size_t localize32_temp_bytes(int64_t);
+size_t sort40_temp_bytes(int64_t);
+void sort40(const uint64_t*, int64_t, KeyMix, void*, size_t, uint64_t*, int32_t*, hipStream_t);
 void localize32(const uint64_t*, int64_t, KeyMix, void*, size_t, uint32_t*, int32_t*, int32_t*,
                 uint64_t*, int32_t*, int32_t*, int32_t*, float*, float*, int, hipStream_t);
 // linear.hip
@@ -627,6 +629,20 @@ PYBIND11_MODULE(_hipops, m) {
                cur_stream());
   });
   m.def("localize32_temp_bytes", [](int64_t n) { return (int64_t)psamd::localize32_temp_bytes(n); });
+  m.def("sort40_temp_bytes", [](int64_t n) { return (int64_t)psamd::sort40_temp_bytes(n); });
+  m.def("sort40", [](Tensor keys, int bits, Tensor temp, Tensor hs, Tensor pos_s) {
+    chk(keys, at::kLong, "keys");
+    chk(temp, at::kByte, "temp");
+    chk(hs, at::kLong, "hs");
+    chk(pos_s, at::kInt, "pos_s");
+    const int64_t n = keys.numel();
+    check(n >= 1 && n < (int64_t(1) << 22), "sort40: 1 <= n < 2^22");
+    check(bits > 30 && bits <= 40, "sort40 needs 30 < key bits <= 40");
+    check(hs.numel() >= n && pos_s.numel() >= n, "sort40 buffers too small");
+    check((size_t)temp.numel() >= psamd::sort40_temp_bytes(n), "sort40 temp too small");
+    psamd::sort40(ptr<uint64_t>(keys), n, make_keymix(bits), temp.data_ptr(),
+                  (size_t)temp.numel(), ptr<uint64_t>(hs), ptr<int32_t>(pos_s), cur_stream());
+  });
   m.def("localize32", [](Tensor keys, int bits, Tensor temp, Tensor hs, Tensor pos_s, Tensor segid,
                          Tensor uniq, Tensor seg_start, Tensor local_col, Tensor n_uniq,
                          optional<Tensor> zero_a, optional<Tensor> zero_b, int digit_bits) {

@@ -19,6 +19,8 @@
 // but 7.9 ms vs 0.2 ms: with ~600 tiles resident at once every tile walks the
 // predecessors' published counts serially; the reduce-then-scan passes stay.
 #include "common.cuh"
+
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -474,6 +476,86 @@ void localize32(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t tem
   scan2_u32(part, T, spart, st);
   rle32_write_kernel<<<(unsigned)T, kBlk, 0, st>>>(hs, pos_s, n, part, segid, uniq, seg_start,
                                                    local_col, n_uniq, zero_a, zero_b, nullptr, n);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// 33..40-bit key spaces (10^10 features: 34 bits) with n < 2^22 keys: the same
+// 10-bit u32 passes, 4 of them instead of the generic u64 sort's 5 x 8-bit ones.
+// The mixed key h splits into lo = h mod 2^30 (the u32 sort key) and hi = h >> 30
+// (<= 10 bits), carried in the value next to the position: v = pos | hi << 22.
+// Passes 0-2 sort (lo, v) by lo's three digits; pass 3 swaps the roles, key = v,
+// value = lo, digit = v >> 22 = hi, so the stable result is ordered by (hi, lo) = h.
+// The combine kernel writes the sorted u64 keys and positions for the u64 RLE.
+constexpr int kPos40 = 22;
+
+__global__ void __launch_bounds__(kBlk)
+mix40_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, uint32_t* __restrict__ lo,
+             int32_t* __restrict__ v) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlk) {
+    const uint64_t h = mix_key(raw[i], m);
+    lo[i] = (uint32_t)(h & ((1u << 30) - 1));
+    v[i] = (int32_t)((uint32_t)i | ((uint32_t)(h >> 30) << kPos40));
+  }
+}
+
+__global__ void __launch_bounds__(kBlk)
+combine40_kernel(const uint32_t* __restrict__ v, const int32_t* __restrict__ lo, int64_t n,
+                 uint64_t* __restrict__ hs, int32_t* __restrict__ pos_s) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlk + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlk) {
+    const uint32_t vi = v[i];
+    hs[i] = ((uint64_t)(vi >> kPos40) << 30) | (uint64_t)(uint32_t)lo[i];
+    pos_s[i] = (int32_t)(vi & ((1u << kPos40) - 1));
+  }
+}
+
+size_t sort40_temp_bytes(int64_t n) {
+  const int64_t T = (n + kTile - 1) / kTile;
+  const int64_t chunks = ((int64_t)kMaxDigits * T + kScanChunk - 1) / kScanChunk + T;
+  const int64_t na = (n + 3) & ~int64_t(3);  // 16-B aligned arrays (vector loads)
+  return (size_t)na * 16 + (size_t)kMaxDigits * T * 4 + (size_t)chunks * 4 + 512;
+}
+
+void sort40(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
+            uint64_t* hs, int32_t* pos_s, hipStream_t st) {
+  if (n <= 0) return;
+  if (m.bits <= 30 || m.bits > 40) throw std::runtime_error("sort40 needs 30 < key bits <= 40");
+  if (n >= (int64_t(1) << kPos40)) throw std::runtime_error("sort40 needs n < 2^22 keys");
+  if (temp_bytes < sort40_temp_bytes(n)) throw std::runtime_error("sort40 temp too small");
+  const int64_t T = (n + kTile - 1) / kTile;
+  const int64_t na = (n + 3) & ~int64_t(3);
+  char* p = (char*)temp;
+  uint32_t* ak = (uint32_t*)p;
+  p += (size_t)na * 4;
+  int32_t* av = (int32_t*)p;
+  p += (size_t)na * 4;
+  uint32_t* bk = (uint32_t*)p;
+  p += (size_t)na * 4;
+  int32_t* bv = (int32_t*)p;
+  p += (size_t)na * 4;
+  uint32_t* hist = (uint32_t*)p;
+  p += (size_t)kMaxDigits * T * 4;
+  uint32_t* spart = (uint32_t*)p;
+  const unsigned g = (unsigned)std::min<int64_t>((n + kBlk - 1) / kBlk, 4096);
+  mix40_kernel<<<g, kBlk, 0, st>>>(raw, n, m, ak, av);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  KeyMix none{};
+  auto pass = [&](const uint32_t* sk, const int32_t* sv, uint32_t* dk, int32_t* dv, int shift) {
+    hist32_kernel<false, 10><<<(unsigned)T, kBlk, 0, st>>>(nullptr, sk, n, none, nullptr, shift,
+                                                           hist, T, nullptr, nullptr);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    scan2_u32(hist, (int64_t)1024 * T, spart, st);
+    scatter32_kernel<10><<<(unsigned)T, kScatThreads, 0, st>>>(sk, sv, dk, dv, n, shift, hist, T,
+                                                              nullptr, nullptr);
+    PSAMD_HIP_CHECK(hipGetLastError());
+  };
+  pass(ak, av, bk, bv, 0);
+  pass(bk, bv, ak, av, 10);
+  pass(ak, av, bk, bv, 20);
+  // pass 3: key = v (digit hi = v >> 22), value = lo
+  pass(reinterpret_cast<const uint32_t*>(bv), reinterpret_cast<const int32_t*>(bk), ak, av,
+       kPos40);
+  combine40_kernel<<<g, kBlk, 0, st>>>(ak, av, n, hs, pos_s);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -33,7 +33,11 @@ def test_mix_roundtrip_gpu_vs_cpu(bits):
 
 
 @pytest.mark.parametrize("bits,n", [(30, 200000), (64, 50000), (12, 30000), (30, 2600000),
-                                    (64, 1500000), (7, 5000)])
+                                    (64, 1500000), (7, 5000),
+                                    # 33..40 bits: 4 x 10-bit passes (sort40), then >= 2^22
+                                    # keys on the generic u64 sort
+                                    (34, 200000), (33, 5001), (40, 1000003), (34, 1),
+                                    (36, 2555904), (34, 4200000)])
 def test_localize_matches_torch(bits, n):
     g = torch.Generator().manual_seed(n)
     hi = min(1 << bits, 1 << 62)
