@@ -25,12 +25,14 @@ def _bench():
     return mod
 
 
-def _trainer(B, N):
+def _trainer(B, N, **kw):
     from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
     from parameter_server_amd.parallel.comm import LoopbackComm
 
-    cfg = SparseLRConfig(num_features=N, minibatch=B, algo="ftrl", lr_type="decay", alpha=0.01,
-                         beta=10.0, l1=10.0, l2=1.0, consistency="ssp:4")
+    args = dict(num_features=N, minibatch=B, algo="ftrl", lr_type="decay", alpha=0.01,
+                beta=10.0, l1=10.0, l2=1.0, consistency="ssp:4")
+    args.update(kw)
+    cfg = SparseLRConfig(**args)
     tr = SparseLRTrainer(cfg, LoopbackComm(2, "cuda"), "cuda")
     assert tr.padded and tr.lag == 1
     return tr
@@ -42,16 +44,18 @@ def _weights(tr):
     return keys[o].cpu(), w[o].float().cpu()
 
 
-@pytest.mark.parametrize("xmode,nprep,graph", [("prep", 2, 1), ("prep", 1, 1), ("own", 2, 1),
-                                               ("prep", 3, 0)])
-def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph):
+@pytest.mark.parametrize("xmode,nprep,graph,kw", [
+    ("prep", 2, 1, {}), ("prep", 1, 1, {}), ("own", 2, 1, {}), ("prep", 3, 0, {}),
+    ("prep", 2, 1, {"fixing_float_bytes": 2}), ("prep", 2, 1, {"push_mode": "aggregate"}),
+    ("prep", 2, 1, {"algo": "adagrad"})])
+def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     from parameter_server_amd.ops.synthetic import criteo_batch
 
     monkeypatch.setenv("PSAMD_XCHG_STREAM", xmode)
     bench = _bench()
     B, N, seed, extra = 4096, 10 ** 6, 77, 5
     dev = torch.device("cuda")
-    tr = _trainer(B, N)
+    tr = _trainer(B, N, **kw)
     keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
     labels = torch.empty(B, dtype=torch.float32, device=dev)
     args = argparse.Namespace(warmup=0, graph=graph)
@@ -65,7 +69,7 @@ def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph):
     pk, pw = _weights(tr)
     loss_p = tr.progress()["loss"]
 
-    ref = _trainer(B, N)
+    ref = _trainer(B, N, **kw)
     for m in range(T):
         k, lab = criteo_batch(B, seed=seed, row0=m * B, num_features=N, device=dev)
         ref.step(k, lab, width=39)
@@ -76,7 +80,10 @@ def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph):
     # ahead: those carry no update (w = 0); every trained key must agree
     pos = torch.searchsorted(pk, rk)
     assert torch.equal(pk[pos], rk)
-    assert torch.allclose(pw[pos], rw, rtol=1e-4, atol=1e-6), (pw[pos] - rw).abs().max()
+    # FixingFloat: a 1-ulp difference of a gradient (hot-key sums combine per-wave
+    # pieces atomically, in any order) can flip one stochastic-rounding step
+    atol = 2e-5 if kw.get("fixing_float_bytes") else 1e-6
+    assert torch.allclose(pw[pos], rw, rtol=1e-4, atol=atol), (pw[pos] - rw).abs().max()
     extra_mask = torch.ones(pk.numel(), dtype=torch.bool)
     extra_mask[pos] = False
     assert torch.all(pw[extra_mask] == 0)
