@@ -124,6 +124,12 @@ void emb_gather_rows(const int64_t*, int64_t, int64_t, const void*, int, void*, 
 void emb_expand(const int32_t*, int64_t, const int64_t*, int64_t, const void*, int64_t, int, void*,
                 hipStream_t);
 int64_t emb_grad_part_floats(int64_t, int);
+void emb_padded_serve(const int32_t*, int64_t, int64_t, int, int, const int64_t*, const float*,
+                      int64_t, void*, uint8_t*, int, uint64_t, float, int32_t*, hipStream_t);
+void emb_unpack_records(const int32_t*, int64_t, int, const int64_t*, const int32_t*, int64_t,
+                        int, void*, float*, hipStream_t);
+void emb_pack_grads(const float*, const float*, const int64_t*, const int32_t*, int64_t, int64_t,
+                    int, int, int32_t*, hipStream_t);
 void emb_grad_reduce(const int32_t*, const int32_t*, const int32_t*, const int32_t*, int64_t,
                      int64_t, const void*, int, float*, float*, hipStream_t);
 void emb_update(const int64_t*, int64_t, const int32_t*, int64_t, const float*, const void*, void*,
@@ -1150,6 +1156,64 @@ PYBIND11_MODULE(_hipops, m) {
     const int64_t* ip = optr<int64_t>(idx, at::kLong, "idx");
     psamd::emb_expand(ptr<int32_t>(local_col), nnz, ip, ip ? idx->numel() : 0, src.data_ptr(),
                       src.size(0), D, X0.data_ptr(), cur_stream());
+  });
+  // padded (sync-free) exchange of the embedding models; records [C x D bf16 | C f32]
+  // per peer chunk (Q = C*D/2 + C int32 words)
+  m.def("emb_padded_serve", [](Tensor recv, int64_t H, int64_t C, int kw, Tensor slot, Tensor w,
+                               Tensor rows, Tensor inited, int64_t seed, double scale,
+                               Tensor out) {
+    chk(recv, at::kInt, "recv");
+    chk(slot, at::kLong, "slot");
+    chk(w, at::kFloat, "w");
+    chk(rows, at::kBFloat16, "rows");
+    chk(inited, at::kByte, "inited");
+    chk(out, at::kInt, "out");
+    check(kw == 1 || kw == 2, "kw 1 or 2");
+    check(rows.dim() == 2 && rows.size(1) % 8 == 0, "rows [cap, D], D % 8 == 0");
+    const int D = (int)rows.size(1);
+    check(C > 0 && C % 4 == 0 && H >= 4 + C * kw, "C % 4 == 0, H >= 4 + C kw");
+    const int64_t G = recv.numel() / H;
+    check(G >= 1 && recv.numel() == G * H, "recv = G rows of H");
+    check(slot.numel() >= G * C && w.numel() >= G * C, "slot / w [G*C]");
+    check(inited.numel() >= rows.size(0), "inited [cap]");
+    check(out.numel() >= G * (C * (D / 2) + C), "out [G * Q]");
+    psamd::emb_padded_serve(ptr<int32_t>(recv), H, C, kw, (int)G, ptr<int64_t>(slot),
+                            ptr<float>(w), rows.size(0), rows.data_ptr(), ptr<uint8_t>(inited), D,
+                            (uint64_t)seed, (float)scale, ptr<int32_t>(out), cur_stream());
+  });
+  m.def("emb_unpack_records", [](Tensor in, int64_t C, Tensor off, Tensor n_uniq, Tensor rows_u,
+                                 Tensor w_u) {
+    chk(in, at::kInt, "in");
+    chk(off, at::kLong, "off");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(rows_u, at::kBFloat16, "rows_u");
+    chk(w_u, at::kFloat, "w_u");
+    check(rows_u.dim() == 2 && rows_u.size(1) % 8 == 0, "rows_u [u_cap, D]");
+    const int D = (int)rows_u.size(1);
+    const int G = (int)off.numel() - 1;
+    check(G >= 1 && C > 0 && C % 4 == 0, "off [G+1], C % 4 == 0");
+    check(in.numel() >= (int64_t)G * (C * (D / 2) + C), "in [G * Q]");
+    check(w_u.numel() >= rows_u.size(0), "w_u [u_cap]");
+    psamd::emb_unpack_records(ptr<int32_t>(in), C, G, ptr<int64_t>(off), ptr<int32_t>(n_uniq),
+                              rows_u.size(0), D, rows_u.data_ptr(), ptr<float>(w_u),
+                              cur_stream());
+  });
+  m.def("emb_pack_grads", [](Tensor dE, Tensor g_wide, Tensor off, Tensor n_uniq, int64_t C,
+                             Tensor out) {
+    chk(dE, at::kFloat, "dE");
+    chk(g_wide, at::kFloat, "g_wide");
+    chk(off, at::kLong, "off");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(out, at::kInt, "out");
+    check(dE.dim() == 2 && dE.size(1) % 8 == 0, "dE [u_cap, D]");
+    const int D = (int)dE.size(1);
+    const int G = (int)off.numel() - 1;
+    check(G >= 1 && C > 0 && C % 4 == 0, "off [G+1], C % 4 == 0");
+    check(g_wide.numel() >= dE.size(0), "g_wide [u_cap]");
+    check(out.numel() >= (int64_t)G * (C * (D / 2) + C), "out [G * Q]");
+    psamd::emb_pack_grads(ptr<float>(dE), ptr<float>(g_wide), ptr<int64_t>(off),
+                          ptr<int32_t>(n_uniq), dE.size(0), C, G, D, ptr<int32_t>(out),
+                          cur_stream());
   });
   m.def("emb_grad_reduce", [](Tensor pos_s, Tensor segid, Tensor seg_start, Tensor n_uniq,
                               int64_t u_cap, int64_t nnz, Tensor dX0, int D, Tensor dE) {

@@ -20,6 +20,8 @@
 //   adam_update      fp32 master weights + bf16 copy for the GEMMs
 #include "common.cuh"
 
+#include <algorithm>
+
 #include <hip/hip_bf16.h>
 
 namespace psamd {
@@ -43,6 +45,21 @@ __device__ __forceinline__ float group_sum(float v) {
 }
 
 // ---------------------------------------------------------------- init / gather
+// deterministic N(0, scale) row of a key (16-lane group, lane l), then the init flag
+__device__ __forceinline__ void init_row(uint16_t* __restrict__ rows, int64_t s, uint64_t key,
+                                         int D, uint64_t seed, float scale, int l,
+                                         uint8_t* __restrict__ inited) {
+  for (int d = l; d < D; d += kGroup) {  // Box-Muller on a counter-based stream
+    const uint64_t r = rng64(seed ^ key, (uint64_t)d);
+    const float u1 = ((r >> 40) + 1) * (1.f / 16777217.f);
+    const float u2 = ((r >> 16) & 0xffffff) * (1.f / 16777216.f);
+    const float z = sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
+    rows[s * D + d] = f2bf(z * scale);
+  }
+  __threadfence_block();
+  if (l == 0) inited[s] = 1;  // racing duplicates write identical rows
+}
+
 __global__ void __launch_bounds__(256)
 emb_init_rows_kernel(const int64_t* __restrict__ slot, const uint64_t* __restrict__ keys, int64_t n,
                      const int32_t* __restrict__ n_dev, int64_t cap, uint16_t* __restrict__ rows,
@@ -53,16 +70,7 @@ emb_init_rows_kernel(const int64_t* __restrict__ slot, const uint64_t* __restric
        i += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
     const int64_t s = slot[i];
     if (!in_range(s, cap) || inited[s]) continue;
-    const uint64_t key = keys[i];
-    for (int d = l; d < D; d += kGroup) {  // Box-Muller on a counter-based stream
-      const uint64_t r = rng64(seed ^ key, (uint64_t)d);
-      const float u1 = ((r >> 40) + 1) * (1.f / 16777217.f);
-      const float u2 = ((r >> 16) & 0xffffff) * (1.f / 16777216.f);
-      const float z = sqrtf(-2.f * logf(u1)) * cospif(2.f * u2);
-      rows[s * D + d] = f2bf(z * scale);
-    }
-    __threadfence_block();
-    if (l == 0) inited[s] = 1;  // racing duplicates write identical rows
+    init_row(rows, s, keys[i], D, seed, scale, l, inited);
   }
 }
 
@@ -375,6 +383,124 @@ emb_grad_cross_narrow_kernel(const int32_t* __restrict__ segid,
 #pragma unroll 8
   for (int64_t r = run + 1; r <= re; ++r) acc += part[r * 2 * D + lane];
   dE[(int64_t)u * D + lane] = acc;
+}
+
+// ------------------------------------------- padded exchange (G > 1, sync-free)
+// The embedding models' pull / push over the sparse-LR padded exchange layout
+// (exchange.hip): every peer gets a fixed row of C keys with the live count in
+// the row header, so sizes never travel to the host. Records of a peer chunk:
+// [C x D bf16 rows | C fp32 wide values] (Q = C*D/2 + C words), one equal-split
+// all-to-all each way; the owner serves all G rows in one launch per kernel.
+
+// owner: first touch of the pulled keys' rows (the KV resolve inserted them)
+__global__ void __launch_bounds__(256)
+emb_init_rows_padded_kernel(const int32_t* __restrict__ recv, int64_t H, int64_t C, int kw,
+                            const int64_t* __restrict__ slot, int64_t cap,
+                            uint16_t* __restrict__ rows, uint8_t* __restrict__ inited, int D,
+                            uint64_t seed, float scale) {
+  const int sidx = blockIdx.y;
+  const int32_t* row = recv + (int64_t)sidx * H;
+  const int64_t n = dev_len(row, C);
+  const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; i < n;
+       i += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
+    const int64_t s = slot[(int64_t)sidx * C + i];
+    if (!in_range(s, cap) || inited[s]) continue;
+    const uint64_t key = kw == 1 ? (uint64_t)(uint32_t)row[4 + i]
+                                 : reinterpret_cast<const uint64_t*>(row + 4)[i];
+    init_row(rows, s, key, D, seed, scale, l, inited);
+  }
+}
+
+// owner: [row | w] records of every pulled key, chunk per source row
+__global__ void __launch_bounds__(256)
+emb_gather_records_kernel(const int32_t* __restrict__ recv, int64_t H, int64_t C,
+                          const int64_t* __restrict__ slot, const float* __restrict__ w,
+                          int64_t cap, const uint16_t* __restrict__ rows, int D,
+                          int32_t* __restrict__ out) {
+  const int sidx = blockIdx.y;
+  const int64_t n = dev_len(recv + (int64_t)sidx * H, C);
+  const int64_t Q = C * (D / 2) + C;
+  uint16_t* orows = reinterpret_cast<uint16_t*>(out + (int64_t)sidx * Q);
+  float* ow = reinterpret_cast<float*>(out + (int64_t)sidx * Q + C * (D / 2));
+  const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  const int vec = D / 8;
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; i < n;
+       i += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
+    const int64_t s = slot[(int64_t)sidx * C + i];
+    uint4* o = reinterpret_cast<uint4*>(orows + i * D);
+    if (in_range(s, cap)) {
+      const uint4* src = reinterpret_cast<const uint4*>(rows + s * D);
+      for (int v = l; v < vec; v += kGroup) o[v] = src[v];
+    } else {
+      for (int v = l; v < vec; v += kGroup) o[v] = make_uint4(0, 0, 0, 0);
+    }
+    if (l == 0) ow[i] = w[(int64_t)sidx * C + i];
+  }
+}
+
+__device__ __forceinline__ int owner_of(const int64_t* __restrict__ off, int G, int64_t u) {
+  int lo = 0, hi = G - 1;  // largest p with off[p] <= u
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= u) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// worker: records back -> rows_u [U, D] bf16 and w_u [U] in unique-key order
+// (keys past a full row C came back as nothing: zero rows, counted in ovf on pack)
+__global__ void __launch_bounds__(256)
+emb_unpack_records_kernel(const int32_t* __restrict__ in, int64_t C, int G,
+                          const int64_t* __restrict__ off, const int32_t* __restrict__ n_uniq,
+                          int64_t u_cap, int D, uint16_t* __restrict__ rows_u,
+                          float* __restrict__ w_u) {
+  const int64_t U = dev_len(n_uniq, u_cap);
+  const int64_t Q = C * (D / 2) + C;
+  const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  const int vec = D / 8;
+  for (int64_t u = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; u < U;
+       u += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
+    const int p = owner_of(off, G, u);
+    const int64_t j = u - off[p];
+    uint4* o = reinterpret_cast<uint4*>(rows_u + u * D);
+    if (j < C) {
+      const uint4* src = reinterpret_cast<const uint4*>(in + (int64_t)p * Q) + j * vec;
+      for (int v = l; v < vec; v += kGroup) o[v] = src[v];
+      if (l == 0) w_u[u] = reinterpret_cast<const float*>(in + (int64_t)p * Q + C * (D / 2))[j];
+    } else {
+      for (int v = l; v < vec; v += kGroup) o[v] = make_uint4(0, 0, 0, 0);
+      if (l == 0) w_u[u] = 0.f;
+    }
+  }
+}
+
+// worker: [dE bf16 | wide gradient] of every unique key into its owner's chunk
+__global__ void __launch_bounds__(256)
+emb_pack_grads_kernel(const float* __restrict__ dE, const float* __restrict__ g_wide,
+                      const int64_t* __restrict__ off, const int32_t* __restrict__ n_uniq,
+                      int64_t u_cap, int64_t C, int G, int D, int32_t* __restrict__ out) {
+  const int64_t U = dev_len(n_uniq, u_cap);
+  const int64_t Q = C * (D / 2) + C;
+  const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  for (int64_t u = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; u < U;
+       u += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
+    const int p = owner_of(off, G, u);
+    const int64_t j = u - off[p];
+    if (j >= C) continue;
+    uint16_t* orow = reinterpret_cast<uint16_t*>(out + (int64_t)p * Q) + j * D;
+    for (int d0 = l * 8; d0 < D; d0 += kGroup * 8) {
+      const float4 a = *reinterpret_cast<const float4*>(dE + u * D + d0);
+      const float4 b = *reinterpret_cast<const float4*>(dE + u * D + d0 + 4);
+      uint4 o;
+      uint16_t* h = reinterpret_cast<uint16_t*>(&o);
+      h[0] = f2bf(a.x); h[1] = f2bf(a.y); h[2] = f2bf(a.z); h[3] = f2bf(a.w);
+      h[4] = f2bf(b.x); h[5] = f2bf(b.y); h[6] = f2bf(b.z); h[7] = f2bf(b.w);
+      *reinterpret_cast<uint4*>(orow + d0) = o;
+    }
+    if (l == 0) reinterpret_cast<float*>(out + (int64_t)p * Q + C * (D / 2))[j] = g_wide[u];
+  }
 }
 
 // Row-wise AdaGrad (one accumulator per row, DLRM-style) on bf16 rows, fp32 math.
@@ -699,6 +825,38 @@ void adam_update(float* p, const float* g, float* m, float* v, int64_t n, float 
   if (n <= 0) return;
   adam_update_kernel<<<grid_for(n, 256, 4096), 256, 0, st>>>(
       p, g, m, v, n, lr, b1, b2, eps, bc1, bc2, gscale, reinterpret_cast<uint16_t*>(p16));
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void emb_padded_serve(const int32_t* recv, int64_t H, int64_t C, int kw, int G,
+                      const int64_t* slot, const float* w, int64_t cap, void* rows,
+                      uint8_t* inited, int D, uint64_t seed, float scale, int32_t* out,
+                      hipStream_t st) {
+  if (C <= 0 || G <= 0) return;
+  const dim3 grid((unsigned)std::min<int64_t>((C + 15) / 16, 2048), (unsigned)G);
+  auto r = reinterpret_cast<uint16_t*>(rows);
+  emb_init_rows_padded_kernel<<<grid, 256, 0, st>>>(recv, H, C, kw, slot, cap, r, inited, D,
+                                                    seed, scale);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  emb_gather_records_kernel<<<grid, 256, 0, st>>>(recv, H, C, slot, w, cap, r, D, out);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void emb_unpack_records(const int32_t* in, int64_t C, int G, const int64_t* off,
+                        const int32_t* n_uniq, int64_t u_cap, int D, void* rows_u, float* w_u,
+                        hipStream_t st) {
+  if (u_cap <= 0) return;
+  emb_unpack_records_kernel<<<grid_for(u_cap, 16, 8192), 256, 0, st>>>(
+      in, C, G, off, n_uniq, u_cap, D, reinterpret_cast<uint16_t*>(rows_u), w_u);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void emb_pack_grads(const float* dE, const float* g_wide, const int64_t* off,
+                    const int32_t* n_uniq, int64_t u_cap, int64_t C, int G, int D, int32_t* out,
+                    hipStream_t st) {
+  if (u_cap <= 0) return;
+  emb_pack_grads_kernel<<<grid_for(u_cap, 16, 8192), 256, 0, st>>>(dE, g_wide, off, n_uniq,
+                                                                   u_cap, C, G, D, out);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

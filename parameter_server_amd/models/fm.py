@@ -53,6 +53,9 @@ class FMConfig:
     table_capacity: int = 0
     table_load: float = 0.5
     max_table_bytes: int = 96 << 30
+    exchange: str = "padded"             # G > 1 on GPU: sync-free fixed rows | "exact"
+    exchange_slack: float = 1.5
+    exchange_capacity: int = 0
     seed: int = 0
 
 
@@ -119,7 +122,9 @@ class FMTrainer(EmbeddingPS):
             hipops().fm_fwd_bwd(X0, vals, B, S, loc.local_col, w_wide, labels, self.coef, dX0,
                                 self.metrics, self.hist, AUC_BINS)
             dE = E.grad_reduce(loc, dX0, D, u_cap, out=self.dE)
-            hipops().fm_l2(dE, rows_src, rows_idx, loc.n_uniq, u_cap, cfg.lambda_v)
+            # pulled rows (G > 1) hold the U unique keys' rows only: no more than that
+            l2_cap = u_cap if rows_idx is not None else min(u_cap, rows_src.shape[0])
+            hipops().fm_l2(dE, rows_src, rows_idx, loc.n_uniq, l2_cap, cfg.lambda_v)
         else:
             dX0 = self._fwd_bwd_torch(X0, vals, B, S, loc.local_col, w_wide, labels)
             U = loc.num_unique()
@@ -175,6 +180,7 @@ class FMTrainer(EmbeddingPS):
         return w.reshape(B, S).sum(1) + 0.5 * (s * s - (V * V).sum(1)).sum(1)
 
     def progress(self, reset: bool = True) -> dict:
+        self._xe_check()
         m = accum_total(self.metrics)[:8].clone()
         if self.G > 1:
             m = self.comm.all_reduce_(m.to(self.comm.device) if self.comm.backend == "nccl"

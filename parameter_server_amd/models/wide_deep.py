@@ -58,6 +58,9 @@ class WideDeepConfig:
     max_table_bytes: int = 160 << 30     # HBM budget of one shard (slots + rows)
     gemm: str = "auto"                   # auto (measured per product) | mfma | hipblaslt
     overlap_wgrad: bool = True           # GPU: weight-gradient GEMMs on a side stream
+    exchange: str = "padded"             # G > 1 on GPU: sync-free fixed rows | "exact"
+    exchange_slack: float = 1.5          # padded row capacity = slack x first max + 1024
+    exchange_capacity: int = 0           # explicit per-peer capacity (0 = from slack)
     seed: int = 0
 
 
@@ -69,8 +72,86 @@ class EmbeddingPS:
     ``stats`` and ``cfg.{embedding_dim, emb_lr, wide}`` on the host class."""
 
     # ------------------------------------------------------------ exchange (G > 1)
+    _xe = None  # padded-exchange state (GPU, G > 1)
+
+    def _padded(self) -> bool:
+        return self.gpu and self.G > 1 and getattr(self.cfg, "exchange", "padded") == "padded"
+
+    def _xe_setup(self, off):
+        """Per-peer capacity C agreed by all ranks (slack x the largest per-peer count of
+        the first minibatch + 1024, a multiple of 8) and the fixed exchange buffers."""
+        from types import SimpleNamespace
+
+        cfg, G, dev = self.cfg, self.G, self.device
+        cnt = (off[1:] - off[:-1]).max().reshape(1).to(torch.int64)
+        cnt = cnt if self.comm.backend == "nccl" else cnt.cpu()
+        m = int(self.comm.all_reduce_(cnt, op="max").item())
+        C = getattr(cfg, "exchange_capacity", 0) or \
+            int(math.ceil(m * getattr(cfg, "exchange_slack", 1.5))) + 1024
+        C = (C + 7) // 8 * 8
+        kw = 1 if self.bits <= 32 else 2
+        D = cfg.embedding_dim
+        H, Q = (4 + C * kw + 1 + 3) // 4 * 4, C * (D // 2) + C  # row geometry of exchange.hip
+        i32 = dict(dtype=torch.int32, device=dev)
+        self._xe = SimpleNamespace(
+            C=C, kw=kw, H=H, Q=Q, D=D,
+            send_k=torch.zeros(G * H, **i32), recv_k=torch.zeros(G * H, **i32),
+            slot=torch.full((G * C,), -1, dtype=torch.int64, device=dev),
+            w=torch.zeros(G * C, dtype=torch.float32, device=dev),
+            rec_s=torch.zeros(G * Q, **i32), rec_r=torch.zeros(G * Q, **i32),
+            grad_s=torch.zeros(G * Q, **i32), grad_r=torch.zeros(G * Q, **i32),
+            ovf=torch.zeros(1, **i32),
+            rows_u=torch.zeros(self.max_nnz, D, dtype=torch.bfloat16, device=dev),
+            w_u=torch.zeros(self.max_nnz, dtype=torch.float32, device=dev))
+
+    def _xe_check(self):
+        if self._xe is not None:
+            ovf = int(self._xe.ovf.item())
+            if ovf:
+                raise RuntimeError(
+                    f"padded exchange overflow: {ovf} keys exceeded the per-peer capacity "
+                    f"{self._xe.C} (pulled as zero rows, not pushed); set exchange_capacity "
+                    f"or exchange_slack higher, or exchange='exact'")
+
+    def _pull_padded(self, loc):
+        """Sync-free pull (no sizes on the host): pack keys into fixed rows of C ->
+        equal-split all-to-all -> owner: one resolve / row-init / record-gather launch
+        for all G rows -> all-to-all of [row | w] records -> unpack in key order."""
+        off = self.part.split_sorted(loc.uniq, loc.n_uniq)
+        if self._xe is None:
+            self._xe_setup(off)
+        xe, hh, tb = self._xe, hipops(), self.shard.table
+        hh.xchg_pack_keys(loc.uniq, loc.n_uniq, off, xe.C, xe.kw, xe.H, xe.send_k, xe.ovf)
+        self.comm.all_to_all_fixed(xe.send_k, xe.recv_k)
+        it, iv, isd, seed = tb.init.args()
+        hh.kv_resolve_rows(tb.slots, xe.recv_k, xe.H, xe.C, xe.kw, xe.slot, xe.w, True, it, iv,
+                           isd, seed, tb._err, tb._inserted, tb.home_base, tb.home_m)
+        hh.emb_padded_serve(xe.recv_k, xe.H, xe.C, xe.kw, xe.slot, xe.w, self.shard.rows,
+                            self.shard.inited, self.shard.seed, self.shard.init_scale, xe.rec_s)
+        self.comm.all_to_all_fixed(xe.rec_s, xe.rec_r)
+        hh.emb_unpack_records(xe.rec_r, xe.C, off, loc.n_uniq, xe.rows_u, xe.w_u)
+        return xe.rows_u, xe.w_u, ("padded", off)
+
+    def _push_padded(self, loc, off, dE, g_wide):
+        """[dE | wide grad] into the owners' rows -> all-to-all -> one row-wise AdaGrad and
+        one wide update per source row (rank order), counts read on the device."""
+        cfg, xe = self.cfg, self._xe
+        C, D, Q, H = xe.C, xe.D, xe.Q, xe.H
+        hipops().emb_pack_grads(dE, g_wide, off, loc.n_uniq, C, xe.grad_s)
+        self.comm.all_to_all_fixed(xe.grad_s, xe.grad_r)
+        for s in range(self.G):
+            chunk = xe.grad_r[s * Q:(s + 1) * Q]
+            g16 = chunk[:C * (D // 2)].view(torch.bfloat16).view(C, D)
+            gw = chunk[C * (D // 2):].view(torch.float32)
+            n_dev = xe.recv_k[s * H:s * H + 1]  # keys this source pulled (its row header)
+            slot_s = xe.slot[s * C:(s + 1) * C]
+            self.shard.update_rows(slot_s, grad16=g16, lr=cfg.emb_lr, n_dev=n_dev)
+            self.shard.update_wide(slot_s, gw, cfg.wide, self.stats, n_dev=n_dev)
+
     def _pull(self, loc):
         """Owner split -> keys all-to-all -> resolve + gather [row | w] -> records back."""
+        if self._padded():
+            return self._pull_padded(loc)
         D = self.cfg.embedding_dim
         U = loc.num_unique()
         off = self.part.split_sorted(loc.uniq, loc.n_uniq).cpu()
@@ -112,6 +193,9 @@ class EmbeddingPS:
                 U = loc.num_unique()
                 self.shard.update_rows(slot[:U], grad=dE[:U], lr=cfg.emb_lr)
                 self.shard.update_wide(slot[:U], g_wide[:U], cfg.wide, self.stats)
+            return
+        if push[0] == "padded":
+            self._push_padded(loc, push[1], dE, g_wide)
             return
         _, slot, send, recv, U = push
         D = cfg.embedding_dim
@@ -275,6 +359,7 @@ class WideDeepTrainer(EmbeddingPS):
 
     # ------------------------------------------------------------ progress
     def progress(self, reset: bool = True) -> dict:
+        self._xe_check()
         m = accum_total(self.metrics)[:8].clone()
         if self.G > 1:
             m = self.comm.all_reduce_(m.to(self.comm.device) if self.comm.backend == "nccl"

@@ -146,7 +146,7 @@ def test_wide_deep_gpu_full_width_learns():
     assert last["loss"] < first["loss"] and np.isfinite(last["loss"])
 
 
-def _wd_rehearsal(rank, world, port, q):
+def _wd_rehearsal(rank, world, port, q, exchange="padded", model="wd"):
     import os
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -156,21 +156,35 @@ def _wd_rehearsal(rank, world, port, q):
     from parameter_server_amd.parallel.comm import init_from_env
 
     comm, dev = init_from_env("cuda")
-    cfg = WideDeepConfig(num_features=1 << 22, embedding_dim=64, hidden=(256, 128),
-                         minibatch=1024, table_capacity=1 << 16)
-    tr = WideDeepTrainer(cfg, comm, dev)
+    if model == "wd":
+        cfg = WideDeepConfig(num_features=1 << 22, embedding_dim=64, hidden=(256, 128),
+                             minibatch=1024, table_capacity=1 << 16, exchange=exchange)
+        tr = WideDeepTrainer(cfg, comm, dev)
+    else:
+        from parameter_server_amd.models.fm import FMConfig, FMTrainer
+
+        tr = FMTrainer(FMConfig(num_features=1 << 22, embedding_dim=16, minibatch=1024,
+                                table_capacity=1 << 16, emb_lr=0.05, lambda_v=0.5,
+                                exchange=exchange), comm, dev)
     for s in range(6):
         k, l = criteo_batch(1024, seed=50 + rank, row0=s * 1024, num_features=1 << 22,
                             cards=[1000] * 26, device=dev)
         tr.step(k, l)
     p = tr.progress()
     occ, _ = tr.shard.table.census()
-    q.put((rank, p, tr.param.cpu(), occ))
+    from parameter_server_amd.ops.kv_table import EMPTY_KEY
+
+    idx = torch.nonzero(tr.shard.table.slots[:, 0] != EMPTY_KEY).flatten()
+    keys, w, _, _ = tr.shard.table.occupied()
+    o = torch.argsort(keys)
+    rows = tr.shard.rows[idx[o]].float().cpu()
+    q.put((rank, p, tr.param.cpu() if model == "wd" else None, occ, keys[o].cpu(), w[o].cpu(),
+           rows))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_wide_deep_two_rank_gpu_rehearsal():
+def _run_rehearsal(exchange, model="wd"):
     import socket
 
     import torch.multiprocessing as mp
@@ -181,12 +195,35 @@ def test_wide_deep_two_rank_gpu_rehearsal():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_wd_rehearsal, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_wd_rehearsal, args=(r, 2, port, q, exchange, model))
+          for r in range(2)]
     for p in ps:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in ps], key=lambda r: r[0])
+    res = sorted([q.get(timeout=120) for _ in ps], key=lambda r: r[0])
     for p in ps:
         p.join(timeout=60)
+    return res
+
+
+@pytest.mark.parametrize("exchange", ["padded", "exact"])
+def test_wide_deep_two_rank_gpu_rehearsal(exchange):
+    res = _run_rehearsal(exchange)
     assert torch.equal(res[0][2], res[1][2])
     assert res[0][1]["examples"] == 2 * 6 * 1024 and np.isfinite(res[0][1]["loss"])
     assert res[0][3] > 0 and res[1][3] > 0
+
+
+@pytest.mark.parametrize("model", ["wd", "fm"])
+def test_padded_exchange_matches_exact(model):
+    """Sync-free padded pull/push (fixed rows, device-side counts) trains what the
+    count-sized all-to-all-v exchange trains: same shard keys, wide weights, loss."""
+    pad, ex = _run_rehearsal("padded", model), _run_rehearsal("exact", model)
+    for rp, re_ in zip(pad, ex):
+        assert rp[3] == re_[3]
+        assert torch.equal(rp[4], re_[4])
+        # wide gradients of hot keys combine per-wave pieces atomically (any order)
+        torch.testing.assert_close(rp[5], re_[5], rtol=1e-3, atol=2e-5)
+        torch.testing.assert_close(rp[6], re_[6], rtol=1e-2, atol=1e-3)
+        assert abs(rp[1]["loss"] - re_[1]["loss"]) < 1e-4
+        if model == "wd":
+            torch.testing.assert_close(rp[2], re_[2], rtol=1e-3, atol=1e-5)
