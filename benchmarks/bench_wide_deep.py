@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--table-slots", type=int, default=1 << 27, help="slots per GPU")
     ap.add_argument("--gemm", default="auto", choices=("auto", "mfma", "hipblaslt"))
+    ap.add_argument("--prefetch", type=int, default=1,
+                    help="generate + localise minibatch t+1 on a side stream during step t")
     ap.add_argument("--overlap-wgrad", type=int, default=1,
                     help="weight-gradient GEMMs on a side stream next to the dX chain")
     ap.add_argument("--emulate-peers", type=int, default=0,
@@ -48,14 +50,41 @@ def main():
                          table_capacity=args.table_slots, gemm=args.gemm, seed=0,
                          overlap_wgrad=bool(args.overlap_wgrad))
     tr = WideDeepTrainer(cfg, comm, dev)
-    keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
-    labels = torch.empty(B, dtype=torch.float32, device=dev)
+    bufs = [(torch.empty(B * 39, dtype=torch.int64, device=dev),
+             torch.empty(B, dtype=torch.float32, device=dev)) for _ in range(2)]
     t = [0]
+    locs = [None, None]
+    side = torch.cuda.Stream(dev)
+    main = torch.cuda.current_stream(dev)
+    ev_prep = [torch.cuda.Event() for _ in range(2)]
+    ev_step = [torch.cuda.Event() for _ in range(2)]
+
+    def prep(i):  # minibatch i into buffer i % 2, on the side stream
+        b = i % 2
+        side.wait_event(ev_step[b])  # the step that last read this buffer is done
+        with torch.cuda.stream(side):
+            k, lab = bufs[b]
+            criteo_batch(B, seed=77 + rank, row0=i * B, num_features=N, device=dev, keys=k,
+                         labels=lab)
+            locs[b] = tr.localize(k, buf=b)
+            ev_prep[b].record(side)
 
     def step():
-        criteo_batch(B, seed=77 + rank, row0=t[0] * B, num_features=N, device=dev, keys=keys,
-                     labels=labels)
-        tr.step(keys, labels)
+        # generation + localisation of minibatch t+1 overlaps the training step of t
+        i = t[0]
+        b = i % 2
+        if args.prefetch:
+            if i == 0:
+                prep(0)
+            prep(i + 1)
+            main.wait_event(ev_prep[b])
+            tr.step(bufs[b][0], bufs[b][1], loc=locs[b])
+            ev_step[b].record(main)
+        else:
+            k, lab = bufs[0]
+            criteo_batch(B, seed=77 + rank, row0=i * B, num_features=N, device=dev, keys=k,
+                         labels=lab)
+            tr.step(k, lab)
         t[0] += 1
 
     for _ in range(args.warmup):

@@ -94,7 +94,8 @@ class FMTrainer(EmbeddingPS):
         self.t0 = time.time()
 
     # ------------------------------------------------------------------ step
-    def step(self, keys: torch.Tensor, labels: torch.Tensor, vals: torch.Tensor | None = None):
+    def step(self, keys: torch.Tensor, labels: torch.Tensor, vals: torch.Tensor | None = None,
+             loc=None):
         """One minibatch: ``keys`` [B*S] raw feature ids (row-major, S per example),
         ``labels`` [B] in {-1, +1} (or {0, 1}), optional feature values ``vals``."""
         cfg = self.cfg
@@ -103,7 +104,7 @@ class FMTrainer(EmbeddingPS):
         nnz = B * S
         if keys.numel() != nnz:
             raise ValueError(f"expected {nnz} keys, got {keys.numel()}")
-        loc = self.localizer(keys)
+        loc = self.localizer(keys) if loc is None else loc
         if self.G == 1:
             if self.gpu:
                 slot, w_wide = self.shard.resolve(loc.uniq, loc.n_uniq, self.slot_buf, self.w_buf)

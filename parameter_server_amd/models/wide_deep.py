@@ -71,6 +71,15 @@ class EmbeddingPS:
     all-to-all each way. Needs ``shard``, ``part``, ``comm``, ``G``, ``gpu``,
     ``stats`` and ``cfg.{embedding_dim, emb_lr, wide}`` on the host class."""
 
+    def localize(self, keys: torch.Tensor, buf: int = 0):
+        """Localise a minibatch into workspace ``buf`` (buffer 0 = the step's own), so
+        the next minibatch can be prepared on a side stream while a step trains
+        (``step(..., loc=...)``)."""
+        locs = self.__dict__.setdefault("_localizers", [self.localizer])
+        while len(locs) <= buf:
+            locs.append(Localizer(self.max_nnz, self.bits, self.device))
+        return locs[buf](keys)
+
     # ------------------------------------------------------------ exchange (G > 1)
     _xe = None  # padded-exchange state (GPU, G > 1)
 
@@ -283,15 +292,16 @@ class WideDeepTrainer(EmbeddingPS):
         self.t0 = time.time()
 
     # ------------------------------------------------------------------ step
-    def step(self, keys: torch.Tensor, labels: torch.Tensor):
-        """One minibatch (``keys`` [B*S] raw feature ids, row-major; ``labels`` [B])."""
+    def step(self, keys: torch.Tensor, labels: torch.Tensor, loc=None):
+        """One minibatch (``keys`` [B*S] raw feature ids, row-major; ``labels`` [B];
+        ``loc``: its localisation from ``localize`` if already prepared)."""
         cfg, dev = self.cfg, self.device
         S, D = cfg.slots, cfg.embedding_dim
         B = labels.numel()
         nnz = B * S
         if keys.numel() != nnz:
             raise ValueError(f"expected {nnz} keys, got {keys.numel()}")
-        loc = self.localizer(keys)
+        loc = self.localizer(keys) if loc is None else loc
         # ---------------- pull rows + wide weights of the unique keys
         if self.G == 1:
             if self.gpu:
