@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--num-features", type=float, default=1e9)
     ap.add_argument("--dim", type=int, default=16)
     ap.add_argument("--table-slots", type=int, default=1 << 28, help="slots per GPU")
+    ap.add_argument("--prefetch", type=int, default=1,
+                    help="generate + localise minibatch t+1 on a side stream during step t")
     args = ap.parse_args()
     from parameter_server_amd.models.fm import FMConfig, FMTrainer
     from parameter_server_amd.ops.synthetic import criteo_batch
@@ -35,14 +37,40 @@ def main():
     cfg = FMConfig(num_features=N, embedding_dim=args.dim, minibatch=B,
                    table_capacity=args.table_slots, seed=0)
     tr = FMTrainer(cfg, comm, dev)
-    keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
-    labels = torch.empty(B, dtype=torch.float32, device=dev)
+    bufs = [(torch.empty(B * 39, dtype=torch.int64, device=dev),
+             torch.empty(B, dtype=torch.float32, device=dev)) for _ in range(2)]
     t = [0]
+    locs = [None, None]
+    side = torch.cuda.Stream(dev)
+    main_s = torch.cuda.current_stream(dev)
+    ev_prep = [torch.cuda.Event() for _ in range(2)]
+    ev_step = [torch.cuda.Event() for _ in range(2)]
+
+    def prep(i):  # minibatch i into buffer i % 2, on the side stream
+        b = i % 2
+        side.wait_event(ev_step[b])  # the step that last read this buffer is done
+        with torch.cuda.stream(side):
+            k, lab = bufs[b]
+            criteo_batch(B, seed=77 + rank, row0=i * B, num_features=N, device=dev, keys=k,
+                         labels=lab)
+            locs[b] = tr.localize(k, buf=b)
+            ev_prep[b].record(side)
 
     def step():
-        criteo_batch(B, seed=77 + rank, row0=t[0] * B, num_features=N, device=dev, keys=keys,
-                     labels=labels)
-        tr.step(keys, labels)
+        i = t[0]
+        b = i % 2
+        if args.prefetch:
+            if i == 0:
+                prep(0)
+            prep(i + 1)
+            main_s.wait_event(ev_prep[b])
+            tr.step(bufs[b][0], bufs[b][1], loc=locs[b])
+            ev_step[b].record(main_s)
+        else:
+            k, lab = bufs[0]
+            criteo_batch(B, seed=77 + rank, row0=i * B, num_features=N, device=dev, keys=k,
+                         labels=lab)
+            tr.step(k, lab)
         t[0] += 1
 
     for _ in range(args.warmup):
