@@ -22,8 +22,9 @@ void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int,
                      bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t,
                      hipStream_t);
 // fm.hip
-void fm_fwd_bwd(const void*, const float*, int64_t, int, int, const int32_t*, const float*, int64_t,
-                const float*, float*, void*, double*, uint32_t*, int, int, hipStream_t);
+void fm_fwd_bwd(const void*, const void*, const int64_t*, int64_t, int64_t, const float*, int64_t,
+                int, int, const int32_t*, const float*, int64_t, const float*, float*, void*,
+                double*, uint32_t*, int, int, hipStream_t);
 void fm_l2(float*, const void*, const int64_t*, int64_t, const int32_t*, int64_t, int, float,
            hipStream_t);
 // tileloc.hip
@@ -284,9 +285,38 @@ PYBIND11_MODULE(_hipops, m) {
     if (v) check(vals->numel() >= B * S, "vals too small");
     uint32_t* h = optr<uint32_t>(hist, at::kInt, "hist");
     if (h) check(hist->numel() >= 2 * nbins, "hist too small");
-    psamd::fm_fwd_bwd(X0.data_ptr(), v, B, S, D, ptr<int32_t>(local_col), ptr<float>(w_local),
+    psamd::fm_fwd_bwd(X0.data_ptr(), nullptr, nullptr, 0, 0, v, B, S, D, ptr<int32_t>(local_col),
+                      ptr<float>(w_local),
                       w_local.numel(), ptr<float>(labels), ptr<float>(coef), dX0.data_ptr(),
                       ptr<double>(metrics), h, nbins, acc_stripes_of(metrics), cur_stream());
+  });
+  m.def("fm_fwd_bwd_gather", [](Tensor rows, optional<Tensor> idx, optional<Tensor> vals, int64_t B,
+                                int S, Tensor local_col, Tensor w_local, Tensor labels, Tensor coef,
+                                Tensor dX0, Tensor metrics, optional<Tensor> hist, int nbins) {
+    // rows [R, D] bf16 read through local_col (and idx) -- no expanded X0
+    chk(rows, at::kBFloat16, "rows");
+    chk(dX0, at::kBFloat16, "dX0");
+    chk(local_col, at::kInt, "local_col");
+    chk(w_local, at::kFloat, "w_local");
+    chk(labels, at::kFloat, "labels");
+    chk(coef, at::kFloat, "coef");
+    chk(metrics, at::kDouble, "metrics");
+    check(rows.dim() == 2, "rows [R, D]");
+    const int D = (int)rows.size(1);
+    check(D == 8 || D == 16 || D == 32, "row gather: D in {8, 16, 32}");
+    check(S > 0 && S <= 64, "1..64 keys per example");
+    check(dX0.numel() >= B * S * D, "dX0 too small");
+    check(local_col.numel() >= B * S && labels.numel() >= B && coef.numel() >= B, "too small");
+    check(metrics.numel() >= 3, "metrics[3]");
+    const int64_t* ip = optr<int64_t>(idx, at::kLong, "idx");
+    const float* v = optr<float>(vals, at::kFloat, "vals");
+    if (v) check(vals->numel() >= B * S, "vals too small");
+    uint32_t* h = optr<uint32_t>(hist, at::kInt, "hist");
+    if (h) check(hist->numel() >= 2 * nbins, "hist too small");
+    psamd::fm_fwd_bwd(nullptr, rows.data_ptr(), ip, ip ? idx->numel() : 0, rows.size(0), v, B, S,
+                      D, ptr<int32_t>(local_col), ptr<float>(w_local), w_local.numel(),
+                      ptr<float>(labels), ptr<float>(coef), dX0.data_ptr(), ptr<double>(metrics),
+                      h, nbins, acc_stripes_of(metrics), cur_stream());
   });
   m.def("fm_l2", [](Tensor dE, Tensor rows, optional<Tensor> idx, optional<Tensor> n_dev,
                     int64_t u_cap, double lambda) {

@@ -17,6 +17,7 @@
 #include "common.cuh"
 
 #include <algorithm>
+#include <stdexcept>
 
 namespace psamd {
 
@@ -118,9 +119,55 @@ fm_fwd_bwd_kernel(const uint16_t* __restrict__ X0, const float* __restrict__ val
 // writes its own dX0 row with 16-B stores. 4 examples per wave; the AUC
 // histogram goes straight to global (one atomic per example, no per-block
 // LDS histogram to clear and flush).
+//
+// Gather mode (X0 == nullptr): the rows are read straight from the embedding store,
+// row = rows[idx ? idx[local_col[p]] : local_col[p]], so the [B*S, D] expansion is
+// never written and re-read (emb_expand 121 us + its re-read, B = 65536, D = 16).
+//
+// s_f = sum over the wave of x v_f for all D features: a transpose-reduce butterfly
+// (each xor stage hands half of the remaining features to the partner lane, so
+// D/2 + D/4 + ... + 1 shuffles, then plain xor sums for the last stages) leaves the
+// total of feature f in lane bfly_lane(f); readlane broadcasts it as a wave-uniform
+// value. D = 16: 17 shuffles instead of 16 full 6-stage all-sums (96).
+template <int D>
+__device__ __forceinline__ int bfly_lane(int f) {
+  // stage k (offset 32 >> k) decides feature bit (log2(D) - 1 - k)
+  int l = 0;
+#pragma unroll
+  for (int k = 0, n = D; n > 1; ++k, n >>= 1)
+    if (f & (n >> 1)) l |= 32 >> k;
+  return l;
+}
+
+template <int D>
+__device__ __forceinline__ void wave_sum_vec(float (&v)[D], float (&s)[D]) {
+  const int lane = threadIdx.x & 63;
+  float w[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) w[j] = v[j];
+  int off = 32;
+#pragma unroll
+  for (int n = D; n > 1; n >>= 1, off >>= 1) {
+    const bool hi = lane & off;
+#pragma unroll
+    for (int j = 0; j < n / 2; ++j) {
+      const float keep = hi ? w[j + n / 2] : w[j];
+      const float send = hi ? w[j] : w[j + n / 2];
+      w[j] = keep + __shfl_xor(send, off, 64);
+    }
+  }
+  float t = w[0];
+  for (; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+  const int ti = __float_as_int(t);
+#pragma unroll
+  for (int f = 0; f < D; ++f) s[f] = __int_as_float(__builtin_amdgcn_readlane(ti, bfly_lane<D>(f)));
+}
+
 template <int D>
 __global__ void __launch_bounds__(256)
-fm_rows_kernel(const uint16_t* __restrict__ X0, const float* __restrict__ vals, int64_t B, int S,
+fm_rows_kernel(const uint16_t* __restrict__ X0, const uint16_t* __restrict__ rows,
+               const int64_t* __restrict__ idx, int64_t idx_cap, int64_t rows_cap,
+               const float* __restrict__ vals, int64_t B, int S,
                const int32_t* __restrict__ local_col, const float* __restrict__ w_local,
                int64_t w_cap, const float* __restrict__ labels, float* __restrict__ coef_out,
                uint16_t* __restrict__ dX0, double* __restrict__ metrics,
@@ -134,28 +181,35 @@ fm_rows_kernel(const uint16_t* __restrict__ X0, const float* __restrict__ vals, 
     const int64_t p = b * S + lane;
     const bool on = lane < S;
     const float x = on ? (vals ? vals[p] : 1.f) : 0.f;
+    const int32_t col = on ? local_col[p] : -1;
+    const uint16_t* src = nullptr;
+    if (X0) {
+      if (on) src = X0 + p * D;
+    } else if (on) {
+      int64_t r = col;
+      if (idx) r = in_range(r, idx_cap) ? idx[r] : -1;
+      if (in_range(r, rows_cap)) src = rows + r * D;  // unresolved key: zero row
+    }
     float v[D];
 #pragma unroll
     for (int c = 0; c < D / 8; ++c) {
       uint4 w = make_uint4(0, 0, 0, 0);
-      if (on) w = reinterpret_cast<const uint4*>(X0 + p * D)[c];
+      if (src) w = reinterpret_cast<const uint4*>(src)[c];
       const uint16_t* h = reinterpret_cast<const uint16_t*>(&w);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[c * 8 + j] = bf16_to_f32(h[j]);
     }
     float part = 0.f;
-    if (on) {
-      const int32_t c = local_col[p];
-      if (in_range(c, w_cap)) part = w_local[c] * x;
-    }
-    float s[D], s2 = 0.f;
+    if (on && in_range(col, w_cap)) part = w_local[col] * x;
+    float xv[D], s[D], s2 = 0.f;
 #pragma unroll
     for (int f = 0; f < D; ++f) {
-      const float xv = x * v[f];
-      part -= 0.5f * xv * xv;
-      s[f] = wave_allsum(xv);
-      s2 += s[f] * s[f];
+      xv[f] = x * v[f];
+      part -= 0.5f * xv[f] * xv[f];
     }
+    wave_sum_vec<D>(xv, s);
+#pragma unroll
+    for (int f = 0; f < D; ++f) s2 += s[f] * s[f];
     const float m = wave_allsum(part) + 0.5f * s2;
     const float y = labels[b] > 0.f ? 1.f : -1.f;
     const float ym = y * m;
@@ -214,16 +268,20 @@ __global__ void fm_l2_kernel(float* __restrict__ dE, const uint16_t* __restrict_
   }
 }
 
-void fm_fwd_bwd(const void* X0, const float* vals, int64_t B, int S, int D,
+// X0 [B*S, D] expanded rows, or X0 == nullptr and rows [rows_cap, D] gathered through
+// local_col (and idx [idx_cap] if given); the gather form needs S <= 64, D in {8, 16, 32}.
+void fm_fwd_bwd(const void* X0, const void* rows, const int64_t* idx, int64_t idx_cap,
+                int64_t rows_cap, const float* vals, int64_t B, int S, int D,
                 const int32_t* local_col, const float* w_local, int64_t w_cap, const float* labels,
                 float* coef, void* dX0, double* metrics, uint32_t* hist, int nbins,
                 int acc_stripes, hipStream_t st) {
   if (S <= 64 && (D == 8 || D == 16 || D == 32)) {
     const unsigned g = (unsigned)std::min<int64_t>((B + 15) / 16, 1 << 20);
-#define PSAMD_FM(DD)                                                                       \
-  fm_rows_kernel<DD><<<g, 256, 0, st>>>((const uint16_t*)X0, vals, B, S, local_col, w_local, \
-                                        w_cap, labels, coef, (uint16_t*)dX0, metrics, hist, \
-                                        hist ? nbins : 0, acc_stripes)
+#define PSAMD_FM(DD)                                                                          \
+  fm_rows_kernel<DD><<<g, 256, 0, st>>>((const uint16_t*)X0, (const uint16_t*)rows, idx, idx_cap, \
+                                        rows_cap, vals, B, S, local_col, w_local, w_cap, labels, \
+                                        coef, (uint16_t*)dX0, metrics, hist, hist ? nbins : 0,  \
+                                        acc_stripes)
     if (D == 8) PSAMD_FM(8);
     else if (D == 16) PSAMD_FM(16);
     else PSAMD_FM(32);
@@ -231,6 +289,7 @@ void fm_fwd_bwd(const void* X0, const float* vals, int64_t B, int S, int D,
     PSAMD_HIP_CHECK(hipGetLastError());
     return;
   }
+  if (!X0) throw std::runtime_error("fm_fwd_bwd: row gather needs S <= 64, D in {8, 16, 32}");
   const int g = grid_for(B * 64, 256, 4096);
   fm_fwd_bwd_kernel<<<g, 256, hist ? 2 * nbins * sizeof(uint32_t) : 0, st>>>(
       (const uint16_t*)X0, vals, B, S, D, local_col, w_local, w_cap, labels, coef,

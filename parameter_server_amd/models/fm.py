@@ -110,18 +110,25 @@ class FMTrainer(EmbeddingPS):
                 slot, w_wide = self.shard.resolve(loc.uniq, loc.n_uniq, self.slot_buf, self.w_buf)
             else:
                 slot, w_wide = self.shard.resolve(loc.uniq[:loc.num_unique()])
-            X0 = E.expand(loc.local_col, nnz, self.shard.rows, idx=slot)
             rows_src, rows_idx = self.shard.rows, slot
             push = ("local", slot)
         else:
             rows_u, w_wide, push = self._pull(loc)
-            X0 = E.expand(loc.local_col, nnz, rows_u)
             rows_src, rows_idx = rows_u, None
         u_cap = nnz
+        # narrow factors on the GPU: the forward gathers the rows itself (no [B*S, D] X0)
+        gather = self.gpu and S <= 64 and D in (8, 16, 32)
+        if not gather:
+            X0 = E.expand(loc.local_col, nnz, rows_src, idx=rows_idx)
         if self.gpu:
             dX0 = self.dX0[:nnz]
-            hipops().fm_fwd_bwd(X0, vals, B, S, loc.local_col, w_wide, labels, self.coef, dX0,
-                                self.metrics, self.hist, AUC_BINS)
+            if gather:
+                hipops().fm_fwd_bwd_gather(rows_src, rows_idx, vals, B, S, loc.local_col, w_wide,
+                                           labels, self.coef, dX0, self.metrics, self.hist,
+                                           AUC_BINS)
+            else:
+                hipops().fm_fwd_bwd(X0, vals, B, S, loc.local_col, w_wide, labels, self.coef,
+                                    dX0, self.metrics, self.hist, AUC_BINS)
             dE = E.grad_reduce(loc, dX0, D, u_cap, out=self.dE)
             # pulled rows (G > 1) hold the U unique keys' rows only: no more than that
             l2_cap = u_cap if rows_idx is not None else min(u_cap, rows_src.shape[0])
