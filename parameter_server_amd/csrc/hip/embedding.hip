@@ -312,9 +312,25 @@ emb_grad_cross_kernel(const int32_t* __restrict__ segid, const int32_t* __restri
         make_float2(acc[2 * c], acc[2 * c + 1]);
 }
 
+// One step of a wave-wide segmented inclusive scan over DPP lane moves (GFX9 DPP
+// controls: 0x110 + n = row_shr:n, 0x142 = row_bcast:15, 0x143 = row_bcast:31). Lanes
+// the move does not write (no source lane, or a row outside ROW_MASK) keep the "old"
+// operand: segment id -2 (never equal) and value 0.
+template <int CTRL, int ROW_MASK, int D>
+__device__ __forceinline__ void seg_scan_step(int32_t u, float (&x)[D]) {
+  const int32_t uo = __builtin_amdgcn_update_dpp(-2, u, CTRL, ROW_MASK, 0xf, false);
+  const bool add = uo == u;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const float y = __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(x[d]), CTRL, ROW_MASK, 0xf, false));
+    x[d] += add ? y : 0.f;
+  }
+}
+
 // Narrow rows (D = 8 .. 64, the FM factors): the same 64-entry runs, but lane =
 // entry: each lane loads its own D-wide row (D / 8 16-B loads), a segmented
-// inclusive scan over the wave (6 shuffle steps per dim; segments are contiguous,
+// inclusive scan over the wave (6 DPP steps per dim; segments are contiguous,
 // so "same segment id at distance off" is the segment test) leaves each
 // segment's run-local sum in its last lane, which stores it (kind 1) or parks it
 // in the run partials (kinds 2 / 3) exactly like emb_grad_seg_kernel.
@@ -342,16 +358,14 @@ emb_grad_lane_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restric
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[v * 8 + j] = take ? bf2f(h[j]) : 0.f;
   }
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int32_t uo = __shfl_up(u, off, 64);
-    const bool add = lane >= off && uo == u;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const float y = __shfl_up(x[d], off, 64);
-      x[d] += add ? y : 0.f;
-    }
-  }
+  // segmented inclusive scan on DPP (VALU lane moves, no LDS bpermute): row_shr 1/2/4/8
+  // inside each 16-lane row, then row_bcast:15 / :31 carry row ends into later rows
+  seg_scan_step<0x111, 0xf>(u, x);
+  seg_scan_step<0x112, 0xf>(u, x);
+  seg_scan_step<0x114, 0xf>(u, x);
+  seg_scan_step<0x118, 0xf>(u, x);
+  seg_scan_step<0x142, 0xa>(u, x);
+  seg_scan_step<0x143, 0xc>(u, x);
   int32_t un = __shfl_down(u, 1, 64);
   if (lane == 63) un = k + 1 < nnz ? segid[k + 1] - 1 : -1;
   if (!live || (un == u && lane != 63) || !in_range(u, u_cap)) return;
