@@ -32,7 +32,7 @@ import torch
 
 from ..ops import embedding as E
 from ..ops import gemm as GM
-from ..ops.keymix import key_bits_for
+from ..ops.keymix import key_bits_for, mix, unmix
 from ..ops.kv_table import UpdateRule, next_pow2
 from ..ops.linear import AUC_BINS, accum_total, auc_from_hist, linear_backward, new_accum
 from ..ops.localize import Localizer
@@ -79,6 +79,52 @@ class EmbeddingPS:
         while len(locs) <= buf:
             locs.append(Localizer(self.max_nnz, self.bits, self.device))
         return locs[buf](keys)
+
+    # ------------------------------------------------------------ checkpoint
+    _dense_state: tuple = ()  # replicated dense tensors saved with the shard
+
+    def state_dict(self) -> dict:
+        """Resume snapshot of this rank: the shard's keys (raw ids, so a snapshot reloads
+        under any world size), wide FTRL state, embedding rows + AdaGrad accumulators,
+        the replicated dense state and the step counter. Write with
+        ``utils.checkpoint.save_snapshot``; merge ranks with ``merge_state_dicts``.
+        (The reference has no resume path: src/parameter/kv_store.h:63-73 only writes
+        the text model; src/app/factor_machine has no checkpoint at all.)"""
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+        st = self.shard.state()
+        sd = {"keys": unmix(st.pop("mkeys"), self.bits).cpu()}
+        sd.update({k: v.cpu() for k, v in st.items()})
+        for name in self._dense_state:
+            sd[name] = getattr(self, name).detach().cpu()
+        sd.update(step=self.step_count, examples=int(self.examples), bits=self.bits,
+                  rank=self.rank, world=self.G, dim=self.cfg.embedding_dim)
+        return sd
+
+    @staticmethod
+    def merge_state_dicts(sds: list) -> dict:
+        """Concatenate per-rank snapshots (key-disjoint shards; dense state and counters
+        are replicated, taken from the first)."""
+        out = dict(sds[0])
+        for k in ("keys", "w", "z", "n", "rows", "acc"):
+            out[k] = torch.cat([sd[k] for sd in sds])
+        return out
+
+    def load_state_dict(self, sd: dict) -> None:
+        """Load the keys this rank owns (any world size wrote ``sd``) and the dense state."""
+        if int(sd["bits"]) != self.bits or int(sd["dim"]) != self.cfg.embedding_dim:
+            raise ValueError(f"snapshot bits/dim {sd['bits']}/{sd['dim']} != "
+                             f"{self.bits}/{self.cfg.embedding_dim}")
+        mk = mix(sd["keys"].to(self.device), self.bits)
+        own = self.part.owner_of(mk) == self.rank
+        self.shard.load_state(mk[own], *(sd[k].to(self.device)[own]
+                                         for k in ("w", "z", "n", "rows", "acc")))
+        for name in self._dense_state:
+            getattr(self, name).copy_(sd[name].to(self.device))
+        if "param" in self._dense_state:
+            self.param16.copy_(self.param.to(torch.bfloat16))
+        self.step_count = int(sd.get("step", 0))
+        self.examples = int(sd.get("examples", 0))
 
     # ------------------------------------------------------------ exchange (G > 1)
     _xe = None  # padded-exchange state (GPU, G > 1)
@@ -222,6 +268,8 @@ class EmbeddingPS:
 
 
 class WideDeepTrainer(EmbeddingPS):
+    _dense_state = ("param", "m", "v")  # MLP params + Adam moments
+
     def __init__(self, cfg: WideDeepConfig, comm: Comm | None = None, device="cpu"):
         self.cfg = cfg
         self.comm = comm or LocalComm(device)

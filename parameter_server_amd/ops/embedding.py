@@ -13,7 +13,7 @@ import math
 
 import torch
 
-from .kv_table import KVTable, UpdateRule
+from .kv_table import EMPTY_KEY, KVTable, UpdateRule
 from .native import hipops, is_gpu
 
 
@@ -32,6 +32,23 @@ class EmbeddingShard:
 
     def nbytes(self) -> int:
         return self.table.nbytes() + self.capacity * (self.dim * 2 + 4 + 1)
+
+    # -------------------------------------------------------------- checkpoint
+    def state(self) -> dict:
+        """Every occupied slot: mixed key, wide state (w, z, n), bf16 row, row AdaGrad
+        accumulator (device tensors, one entry per key)."""
+        mk, w, z, n = self.table.occupied()
+        mask = self.table.slots[:, 0] != EMPTY_KEY
+        return {"mkeys": mk, "w": w, "z": z, "n": n, "rows": self.rows[mask],
+                "acc": self.acc[mask]}
+
+    def load_state(self, mkeys, w, z, n, rows, acc) -> torch.Tensor:
+        """Insert keys with their saved state (rows are marked initialised)."""
+        slot = self.table.load(mkeys, w, z, n)
+        self.rows[slot] = rows.to(self.device, torch.bfloat16)
+        self.acc[slot] = acc.to(self.device, torch.float32)
+        self.inited[slot] = 1
+        return slot
 
     # -------------------------------------------------------------- pull side
     def resolve(self, mkeys: torch.Tensor, n_dev=None, slot=None, w=None):
