@@ -192,6 +192,25 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     return iterate, True
 
 
+def spawn_ranks(n: int, argv: list[str] | None = None, script: str | None = None) -> int:
+    """Re-launch this script as ``n`` ranks through torch.distributed.run (rendezvous on
+    127.0.0.1, a free port) as a CHILD process, and return its exit code. Called
+    before any GPU call, so the parent never initialises the device."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           script or os.path.abspath(__file__)] + list(sys.argv[1:] if argv is None else argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -232,6 +251,11 @@ def main():
                     help="write per-rank traffic/phase JSON here ({rank} substituted); "
                          "PSAMD_TRACE=1 adds roctx ranges + phase timers")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.emulate_peers:
+        # `python bench.py --gpus N`: fan out N ranks (one per GPU) before anything
+        # touches the GPU, like the reference's launcher owns process fan-out
+        # (script/local.sh:1-43); this process only waits and forwards the exit code.
+        return spawn_ranks(args.gpus)
 
     from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
     from parameter_server_amd.ops.synthetic import criteo_batch
@@ -397,4 +421,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)
