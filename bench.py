@@ -41,27 +41,37 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
       last used its buffer. The kernels of a localisation are latency bound, so
       several run concurrently with the step at little cost (1 GPU, 65,536 x 39 keys:
       1 stream 0.309 ms/step, 2 -> 0.241, 3 -> 0.230).
-    * main stream: the training step (``SparseLRTrainer.step_segments``, one linear
-      graph per compute segment and buffer; a single multi-stream graph replays
-      much slower on ROCm). N > 1: the padded exchange's two equal-split RCCL
-      all-to-alls run between the graph replays, nothing reads back to the host.
-    * N > 1 with exchange lag 1 (SSP): the exchange half of step t+2 (pack,
-      all-to-all, owner update + resolve, all-to-all) is issued right after the
-      worker half of step t, on the preparation stream of minibatch t+2 (behind its
-      localisation), so it runs while the main stream trains step t+1. Counting
+    * main stream: the worker half of the training step (``SparseLRTrainer.step_segments``,
+      one linear graph per compute segment and ring position; a single multi-stream
+      graph replays much slower on ROCm). N > 1: the padded exchange's two
+      equal-split RCCL all-to-alls run between the graph replays, nothing reads back
+      to the host.
+    * N > 1 with exchange lag >= 1 (SSP / ASP): the exchange half of step t+xd (pack,
+      all-to-all, owner push apply + pull resolve, all-to-all) is issued right after the
+      worker half of step t, on the preparation stream of minibatch t+xd (behind its
+      localisation), so it runs while the main stream trains; it waits only for the
+      localisation of its minibatch, the worker step whose gradients it carries
+      (t+xd-1-lag) and the previous exchange (owner updates in step order). Counting
       RCCL's own stream this keeps 4 busy streams; one more (a dedicated exchange
-      stream, PSAMD_XCHG_STREAM=own) oversubscribes the hardware queues (8
-      emulated peers: 0.333 vs 0.308 ms/step). Consecutive exchanges are chained
-      (owner updates in step order). tests/test_bench_pipeline_gpu.py checks the
-      pipeline trains exactly what the sequential trainer trains.
+      stream, PSAMD_XCHG_STREAM=own) oversubscribes the hardware queues (8 emulated
+      peers: 0.333 vs 0.308 ms/step).
+    * ASP: the owner's push apply of each exchange replays on its own stream; later
+      exchanges wait for it only when they reuse its ring entry (the apply of exchange
+      t - depth), never to see its pushes.
 
-    Each iteration = one full training step + one full data preparation; the first
-    steps' data is prepared in warm-up and the last iterations' preparations are
-    unused, so the timed region does exactly K generations, K localisations and K
-    steps. Returns (run, graph_used)."""
+    Graphs are captured per phase t % P, P = lcm(2 * nprep buffers, exchange ring).
+    tests/test_bench_pipeline_gpu.py checks the pipeline trains exactly what the
+    sequential trainer trains. Each iteration = one full training step + one full
+    data preparation; the first steps' data is prepared in warm-up and the last
+    iterations' preparations are unused, so the timed region does exactly K
+    generations, K localisations and K steps. Returns (run, graph_used)."""
+    import math
+
     from parameter_server_amd.ops.synthetic import criteo_batch
 
-    NB = 2 * nprep  # even: buffer parity == step parity (the exchange's double buffers)
+    NB = 2 * nprep
+    R = tr.R if tr.padded else 1
+    P = NB * R // math.gcd(NB, R)  # graph phases: (buffer, ring position) pairs
     main = torch.cuda.current_stream(device)
     # preparation stream priority: high on 1 GPU (the preparation is the long pole);
     # normal next to the SSP exchange stream, which then runs at high priority
@@ -80,11 +90,13 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
         ctr[sidx].add_(1)
         locs[b] = tr.localize(k, buf=b)
 
-    def segments(b):
+    def segments(t):
+        b = t % NB
         k, lab = bufs[b]
-        return tr.step_segments(k, lab, width=39, loc=locs[b], parity=b % 2)
+        return tr.step_segments(k, lab, width=39, loc=locs[b], step=t)
 
-    split = tr.padded and tr.lag == 1
+    split = tr.padded and tr.lag >= 1
+    asp = tr.padded and tr.asp
     ncut = tr.EXCHANGE_SEGMENTS if split else 0
     # where the exchange half runs: "prep" = on the preparation stream of its own
     # minibatch, right after the localisation (no extra stream: RCCL's own stream
@@ -92,101 +104,145 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     # "own" = a dedicated high-priority exchange stream
     xmode = os.environ.get("PSAMD_XCHG_STREAM", "prep") if split else "none"
     comm_s = torch.cuda.Stream(device, priority=-1) if xmode == "own" else main
-    xd = min(nprep, 2)  # "prep": exchange of step t + xd issued after step t
+    apply_s = torch.cuda.Stream(device) if asp else None
+    # exchange of step t + xd issued after worker t: needs worker t + xd - 1 - lag
+    # issued (xd <= lag + 1) and the preparation of t + xd (xd <= nprep)
+    xd = min(nprep, 2, tr.lag + 1) if split else 0
+    E = 64  # event rings, indexed by step (every look-back here is < 64 steps)
+    ev_buf = [torch.cuda.Event() for _ in range(NB)]   # worker done with buffer b
+    ev_w = [torch.cuda.Event() for _ in range(E)]      # worker half of step t done
+    ev_prep = [torch.cuda.Event() for _ in range(NB)]
+    ev_x = [torch.cuda.Event() for _ in range(E)]      # exchange half of step t done
+    ev_a = [torch.cuda.Event() for _ in range(E)]      # asp: push apply of exchange t done
+    recorded_a = set()
 
-    def run(fns):
-        for fn in fns:
-            fn()
+    def run_plan(plan, t, xs):
+        """Run one half's segments; an "async" segment (ASP push apply) goes to its
+        own stream behind what ``xs`` has issued so far."""
+        for kind, fn in plan:
+            if kind == "async":
+                e = torch.cuda.Event()
+                e.record(xs)
+                apply_s.wait_event(e)
+                with torch.cuda.stream(apply_s):
+                    fn()
+                ev_a[t % E].record(apply_s)
+                recorded_a.add(t % E)
+            else:
+                fn()
 
-    def halves(b):
-        segs = [fn for _, fn in segments(b)]
+    def halves(t):
+        segs = list(segments(t))
         return segs[:ncut], segs[ncut:]
 
+    # eager plans until capture: phase j -> (exchange half, worker half)
+    xplans = [None] * P
+    wplans = [None] * P
+
+    def xplan(t):
+        j = t % P
+        if xplans[j] is None or not graphs["on"]:
+            return halves(t)[0]
+        return xplans[j]
+
+    def wplan(t):
+        j = t % P
+        if wplans[j] is None or not graphs["on"]:
+            return halves(t)[1]
+        return wplans[j]
+
     preps = [(lambda b=b: prep(b)) for b in range(NB)]
-    xfns = [(lambda b=b: run(halves(b)[0])) for b in range(NB)]
-    wfns = [(lambda b=b: run(halves(b)[1])) for b in range(NB)]
-    ev_step = [torch.cuda.Event() for _ in range(NB)]
-    ev_prep = [torch.cuda.Event() for _ in range(NB)]
-    ev_x = [torch.cuda.Event() for _ in range(NB)]
+    graphs = {"on": False}
     state = {"t": 0}
 
-    def issue_exchange(t):  # exchange half of step t: minibatch t ready, grads(t-2) packed
-        b = t % NB
-        xs = sides[b % nprep] if xmode == "prep" else comm_s
+    def issue_exchange(t):
+        xs = sides[(t % NB) % nprep] if xmode == "prep" else comm_s
         if xmode != "prep":
-            xs.wait_event(ev_prep[b])     # (on its prep stream it follows the prep)
-        xs.wait_event(ev_step[(t - 2) % NB])
-        xs.wait_event(ev_x[(t - 1) % NB])  # owner updates of consecutive steps in order
+            xs.wait_event(ev_prep[t % NB])  # (on its prep stream it follows the prep)
+        c = t - 1 - tr.lag
+        if c >= 0:
+            xs.wait_event(ev_w[c % E])      # the gradients it carries are packed
+        if t >= 1:
+            xs.wait_event(ev_x[(t - 1) % E])  # owner updates of consecutive steps in order
+        g = tr.sched.apply_gate(t) if asp else None
+        if g is not None and g % E in recorded_a:
+            xs.wait_event(ev_a[g % E])      # asp: ring entry of exchange t is free again
         with torch.cuda.stream(xs):
-            xfns[b]()
-            ev_x[b].record(xs)
+            run_plan(xplan(t), t, xs)
+            ev_x[t % E].record(xs)
 
     def iterate():
         t = state["t"]
         nb = (t + nprep) % NB                 # minibatch t + nprep
         s = sides[nb % nprep]
-        s.wait_event(ev_step[nb])             # step(t + nprep - NB) done with bufs[nb]
+        s.wait_event(ev_buf[nb])              # step(t + nprep - NB) done with bufs[nb]
         with torch.cuda.stream(s):
             preps[nb]()
             ev_prep[nb].record(s)
         cur = t % NB
         if xmode == "own":
             issue_exchange(t + 1)
-            main.wait_event(ev_x[cur])        # exchange of step t done
+            main.wait_event(ev_x[t % E])      # exchange of step t done
         elif split:
-            main.wait_event(ev_x[cur])
+            main.wait_event(ev_x[t % E])
         else:
             main.wait_event(ev_prep[cur])     # minibatch t is localised
-        wfns[cur]()
-        ev_step[cur].record(main)
-        if xmode == "prep":                   # needs step t + xd - 2 <= t issued and
-            issue_exchange(t + xd)            # the prep of t + xd (issued at t + xd - nprep)
+        run_plan(wplan(t), t, main)
+        ev_buf[cur].record(main)
+        ev_w[t % E].record(main)
+        if xmode == "prep":
+            issue_exchange(t + xd)
         state["t"] = t + 1
 
-    for b in range(NB):
-        ev_step[b].record(main)
+    for e in ev_buf:
+        e.record(main)
     for b in range(nprep):  # minibatches 0 .. nprep-1
         with torch.cuda.stream(sides[b]):
             prep(b)
             ev_prep[b].record(sides[b])
-    for b in range(NB):
-        ev_x[b].record(main)
     if xmode == "own":
         issue_exchange(0)
     elif split:
         for t in range(xd):  # exchanges of minibatches 0 .. xd-1
             issue_exchange(t)
-    warm = max(NB, args.warmup + (-args.warmup) % NB)
+    warm = max(NB, args.warmup)
+    warm += (-warm) % P  # capture at a multiple of P: phase j <-> buffer j % NB, ring j % R
     for _ in range(warm):
         iterate()
     if not args.graph:
         return iterate, False
     torch.cuda.synchronize()
-    gp, xplans, wplans = [], [], []
-    for b in range(NB):  # t % NB == 0 here: buffer b <-> minibatch t + b
+    t0 = state["t"]
+    gp = []
+    for b in range(NB):  # t0 % NB == 0: buffer b <-> minibatch t0 + b
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
             prep(b)
         gp.append(g)
-        plan = []
-        for kind, fn in segments(b):  # capture in order: a segment may bake in buffers
-            if kind == "compute":     # the previous one of the same parity selected
+
+    def capture(plan):
+        out = []
+        for kind, fn in plan:  # in order: a segment may bake in buffers the previous
+            if kind in ("compute", "async"):  # one of the same ring entry selected
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                     fn()
-                plan.append(g.replay)
+                out.append((kind, g.replay))
             else:
-                plan.append(fn)
-        xplans.append(plan[:ncut])
-        wplans.append(plan[ncut:])
+                out.append((kind, fn))
+        return out
+
+    for j in range(P):
+        xh, wh = halves(t0 + j)
+        xplans[j] = capture(xh)
+        wplans[j] = capture(wh)
     # capture ran nothing: the workspaces of the minibatches in flight still hold
-    # their eager preparations (and the eager exchange of step t), so the replays
+    # their eager preparations (and the eager exchanges issued ahead), so the replays
     # continue from there
     preps[:] = [g.replay for g in gp]
-    xfns[:] = [(lambda b=b: run(xplans[b])) for b in range(NB)]
-    wfns[:] = [(lambda b=b: run(wplans[b])) for b in range(NB)]
+    graphs["on"] = True
     torch.cuda.synchronize()
-    for _ in range(NB):
+    for _ in range(P):
         iterate()
     torch.cuda.synchronize()
     return iterate, True
@@ -245,6 +301,9 @@ def main():
                     help="1 process: run the N-GPU padded step with N emulated peers over a "
                          "loopback exchange (per-GPU device cost of the N-GPU step, no "
                          "collectives); reported as n_gpus 1 with 'emulated_peers'")
+    ap.add_argument("--emulate-backend", default="copy", choices=["copy", "nccl"],
+                    help="emulated peers: exchanges as stream copies, or through a real "
+                         "1-rank RCCL communicator (RCCL kernels + ProcessGroupNCCL waits)")
     ap.add_argument("--progress", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check)")
     ap.add_argument("--trace", default="",
@@ -263,9 +322,10 @@ def main():
 
     comm, device = init_from_env("cpu" if args.cpu else "cuda")
     if args.emulate_peers > 1 and comm.world == 1:
-        from parameter_server_amd.parallel.comm import LoopbackComm
+        from parameter_server_amd.parallel.comm import LoopbackComm, nccl_loopback
 
-        comm = LoopbackComm(args.emulate_peers, device)
+        comm = (nccl_loopback(args.emulate_peers, device) if args.emulate_backend == "nccl"
+                else LoopbackComm(args.emulate_peers, device))
     G, rank = comm.world, comm.rank
     if G != args.gpus and rank == 0 and not args.emulate_peers:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {G}", file=sys.stderr)
@@ -396,7 +456,7 @@ def main():
                 "seq_len": 39,
                 "nnz_per_example": 39,
                 "parallelism": f"dp{n_ranks}+kvshard{n_ranks}",
-                "consistency": args.consistency,
+                "consistency": tr.consistency_desc(),
                 "push": args.push_mode if G > 1 else None,
                 "table_slots_per_gpu": tr.table.capacity,
                 "hip_graph": graph_used,

@@ -310,8 +310,8 @@ bcd_server_stats_kernel(const double* __restrict__ w, const uint8_t* __restrict_
 void bcd_grad(const int32_t* col, const int32_t* row, const float* val, int64_t p0, int64_t p1,
               int64_t c0, int64_t ncols, const double* ym, const float* y, int64_t nrows,
               const double* delta, const uint8_t* active, double* G, double* U, hipStream_t st) {
-  PSAMD_HIP_CHECK(hipMemsetAsync(G, 0, ncols * sizeof(double), st));
-  PSAMD_HIP_CHECK(hipMemsetAsync(U, 0, ncols * sizeof(double), st));
+  fill_async<double>(G, ncols, 0.0, st);
+  fill_async<double>(U, ncols, 0.0, st);
   if (p1 <= p0) return;
   bcd_grad_kernel<<<grid_for(p1 - p0, 256, 4096), 256, 0, st>>>(
       col, row, val, p0, p1, c0, ncols, ym, y, nrows, delta, active, G, U);
@@ -324,8 +324,8 @@ void bcd_grad_chunked(const int32_t* col, const int32_t* row, const float* val,
                       const uint8_t* active, double* G, double* U, bool zeroed,
                       hipStream_t st) {
   if (!zeroed) {
-    PSAMD_HIP_CHECK(hipMemsetAsync(G, 0, ncols * sizeof(double), st));
-    PSAMD_HIP_CHECK(hipMemsetAsync(U, 0, ncols * sizeof(double), st));
+    fill_async<double>(G, ncols, 0.0, st);
+    fill_async<double>(U, ncols, 0.0, st);
   }
   if (nchunks <= 0) return;
   bcd_grad_chunk_kernel<<<grid_for(nchunks, 4, 16384), 256, 0, st>>>(

@@ -18,6 +18,9 @@ void kv_resolve(void*, int64_t, const uint64_t*, int64_t, const int32_t*, int64_
                 int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t, hipStream_t);
 void kv_accumulate_rows(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int,
                         int64_t, int64_t, int64_t*, int32_t*, int64_t, hipStream_t);
+void kv_update_rows(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int,
+                    int64_t, int64_t, unsigned long long*, int64_t, int32_t*, int, int, float, float,
+                    float, float, float, float, double*, int, hipStream_t);
 void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int, int64_t*, float*,
                      bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t,
                      hipStream_t);
@@ -42,6 +45,7 @@ void xchg_pack_keys(const uint64_t*, const int32_t*, int64_t, const int64_t*, in
 void xchg_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
                      int64_t, int, int64_t, int32_t*, hipStream_t);
 void xchg_clear_counts(int32_t*, int, int64_t, bool, bool, hipStream_t);
+void xchg_publish(const int32_t*, int32_t*, hipStream_t);
 void xchg_unpack_w(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
                    int64_t, float*, hipStream_t);
 void xchg_ff_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
@@ -78,6 +82,10 @@ void owner_split(const uint64_t*, const int32_t*, int64_t, const uint64_t*, int,
 void owner_of(const uint64_t*, int64_t, const uint64_t*, int, int32_t*, hipStream_t);
 // sort32.hip
 size_t localize32_temp_bytes(int64_t);
+size_t partloc_temp_bytes(int64_t, int);
+bool partloc_supported(int64_t, int);
+void localize_part(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, int32_t*, uint64_t*,
+                   int32_t*, int32_t*, int32_t*, float*, float*, int32_t*, int64_t, hipStream_t);
 size_t sort40_temp_bytes(int64_t);
 void sort40(const uint64_t*, int64_t, KeyMix, void*, size_t, uint64_t*, int32_t*, hipStream_t);
 void localize32(const uint64_t*, int64_t, KeyMix, void*, size_t, uint32_t*, int32_t*, int32_t*,
@@ -100,7 +108,9 @@ void cm_insert(uint32_t*, uint64_t, int, uint32_t, const uint64_t*, const uint8_
 void cm_query(const uint32_t*, uint64_t, int, uint32_t, const uint64_t*, int64_t, const int32_t*,
               int, int32_t*, uint8_t*, hipStream_t);
 void compact_kept(const int32_t*, const int32_t*, int64_t, const int32_t*, int32_t*, int32_t*,
-                  int32_t*, hipStream_t);
+                  int32_t*, const uint64_t*, uint64_t*, hipStream_t);
+void cm_insert_seg(uint32_t*, uint64_t, int, uint32_t, const uint64_t*, const int32_t*, int64_t,
+                   const int32_t*, hipStream_t);
 void ff_minmax(const float*, int64_t, float*, hipStream_t);
 void ff_encode(const float*, int64_t, const float*, int, uint64_t, uint8_t*, hipStream_t);
 void ff_decode(const uint8_t*, int64_t, const float*, int, float*, hipStream_t);
@@ -428,6 +438,42 @@ PYBIND11_MODULE(_hipops, m) {
                               gstride, ptr<int32_t>(recv), G, H, C, ptr<int64_t>(touched),
                               ptr<int32_t>(n_touched), touched.numel(), cur_stream());
   });
+  m.def("kv_update_rows", [](Tensor slots, Tensor slot_idx, Tensor grad, int64_t gstride,
+                             Tensor recv, int64_t H, int64_t C, Tensor link, Tensor nxt, int algo,
+                             int lr_type, double alpha, double beta, double l1, double l2,
+                             double grad_scale, double max_delta, optional<Tensor> stats) {
+    const int64_t cap = slot_capacity(slots);
+    chk(slot_idx, at::kLong, "slot_idx");
+    chk(grad, at::kFloat, "grad");
+    chk(recv, at::kInt, "recv");
+    chk(link, at::kLong, "link");
+    chk(nxt, at::kInt, "nxt");
+    check(C > 0 && H > 4 && recv.numel() % H == 0, "bad exchange row geometry");
+    const int G = (int)(recv.numel() / H);
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(gstride >= C && grad.numel() >= (G - 1) * gstride + C, "grad rows out of bounds");
+    check(slot_idx.numel() >= G * C, "slot_idx < G*C");
+    check(nxt.numel() >= G * C, "nxt < G*C");
+    const int64_t L = link.numel();
+    check(L >= 2 * G * C && (L & (L - 1)) == 0, "link: power of two >= 2*G*C");
+    double* st = optr<double>(stats, at::kDouble, "stats");
+    const int stripes = acc_stripes_of(stats);
+    psamd::kv_update_rows(slots.data_ptr(), cap, ptr<int64_t>(slot_idx), ptr<float>(grad), gstride,
+                          ptr<int32_t>(recv), G, H, C,
+                          reinterpret_cast<unsigned long long*>(link.data_ptr<int64_t>()), L,
+                          ptr<int32_t>(nxt), algo, lr_type, (float)alpha, (float)beta, (float)l1,
+                          (float)l2, (float)grad_scale, (float)max_delta, st, stripes,
+                          cur_stream());
+  });
+  m.def("xchg_publish", [](Tensor src, Tensor host_dst) {
+    chk(src, at::kInt, "src");
+    check(host_dst.device().is_cpu() && host_dst.is_pinned() && host_dst.scalar_type() == at::kInt &&
+              host_dst.numel() >= 1,
+          "host_dst must be a pinned int32 host tensor");
+    void* dptr = nullptr;
+    PSAMD_HIP_CHECK(hipHostGetDevicePointer(&dptr, host_dst.data_ptr(), 0));
+    psamd::xchg_publish(ptr<int32_t>(src), reinterpret_cast<int32_t*>(dptr), cur_stream());
+  });
   m.def("xchg_pack_keys", [](Tensor ukeys, Tensor n_uniq, Tensor off, int64_t C, int kw,
                              int64_t H, Tensor send, optional<Tensor> ovf) {
     chk(ukeys, at::kLong, "ukeys");
@@ -710,6 +756,38 @@ PYBIND11_MODULE(_hipops, m) {
   }, py::arg("keys"), py::arg("bits"), py::arg("temp"), py::arg("hs"), py::arg("pos_s"),
      py::arg("segid"), py::arg("uniq"), py::arg("seg_start"), py::arg("local_col"),
      py::arg("n_uniq"), py::arg("zero_a"), py::arg("zero_b"), py::arg("digit_bits") = 8);
+  m.def("partloc_temp_bytes", [](int64_t n, int bits) {
+    return (int64_t)psamd::partloc_temp_bytes(n, bits);
+  });
+  m.def("partloc_supported", [](int64_t n, int bits) { return psamd::partloc_supported(n, bits); });
+  m.def("localize_part", [](Tensor keys, int bits, Tensor temp, Tensor pos_s, Tensor segid,
+                            Tensor uniq, Tensor seg_start, Tensor local_col, Tensor n_uniq,
+                            optional<Tensor> zero_a, optional<Tensor> zero_b, Tensor err) {
+    chk(keys, at::kLong, "keys");
+    chk(temp, at::kByte, "temp");
+    chk(pos_s, at::kInt, "pos_s");
+    chk(segid, at::kInt, "segid");
+    chk(uniq, at::kLong, "uniq");
+    chk(seg_start, at::kInt, "seg_start");
+    chk(local_col, at::kInt, "local_col");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(err, at::kInt, "err");
+    const int64_t n = keys.numel();
+    check(psamd::partloc_supported(n, bits), "localize_part: needs bits <= 32 and n <= 10M");
+    check(pos_s.numel() >= n && segid.numel() >= n && uniq.numel() >= n &&
+              seg_start.numel() >= n + 1 && local_col.numel() >= n,
+          "localize_part buffers too small");
+    check((size_t)temp.numel() >= psamd::partloc_temp_bytes(n, bits), "localize_part temp too small");
+    float* za = optr<float>(zero_a, at::kFloat, "zero_a");
+    float* zb = optr<float>(zero_b, at::kFloat, "zero_b");
+    if (za) check(zero_a->numel() >= n, "zero_a too small");
+    if (zb) check(zero_b->numel() >= n, "zero_b too small");
+    psamd::localize_part(ptr<uint64_t>(keys), n, make_keymix(bits), temp.data_ptr(),
+                         (size_t)temp.numel(), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
+                         ptr<uint64_t>(uniq), ptr<int32_t>(seg_start), ptr<int32_t>(local_col),
+                         ptr<int32_t>(n_uniq), za, zb, ptr<int32_t>(err), uniq.numel(),
+                         cur_stream());
+  });
   m.def("bucketloc_temp_bytes", [](int64_t n) { return (int64_t)psamd::bucketloc_temp_bytes(n); });
   m.def("localize_bucket", [](Tensor keys, int bits, Tensor temp, Tensor pos_s, Tensor segid,
                               Tensor uniq, Tensor seg_start, Tensor local_col, Tensor n_uniq,
@@ -882,16 +960,34 @@ PYBIND11_MODULE(_hipops, m) {
                     freq, kp, cp, cur_stream());
   });
   m.def("compact_kept", [](Tensor keep, Tensor incl, optional<Tensor> n_dev, Tensor kept_idx,
-                           Tensor n_kept, optional<Tensor> remap) {
+                           Tensor n_kept, optional<Tensor> remap, optional<Tensor> keys_in,
+                           optional<Tensor> keys_out) {
     chk(keep, at::kInt, "keep");
     chk(incl, at::kInt, "incl");
     chk(kept_idx, at::kInt, "kept_idx");
     chk(n_kept, at::kInt, "n_kept");
     check(kept_idx.numel() >= keep.numel() && incl.numel() >= keep.numel(), "compact sizes");
+    const uint64_t* ki = optr<uint64_t>(keys_in, at::kLong, "keys_in");
+    uint64_t* ko = optr<uint64_t>(keys_out, at::kLong, "keys_out");
+    check((ki == nullptr) == (ko == nullptr), "keys_in and keys_out go together");
+    if (ki) check(keys_in->numel() >= keep.numel() && keys_out->numel() >= keep.numel(),
+                  "compact key buffers too small");
     psamd::compact_kept(ptr<int32_t>(keep), ptr<int32_t>(incl), keep.numel(),
                         optr<int32_t>(n_dev, at::kInt, "n_dev"), ptr<int32_t>(kept_idx),
-                        ptr<int32_t>(n_kept), optr<int32_t>(remap, at::kInt, "remap"),
+                        ptr<int32_t>(n_kept), optr<int32_t>(remap, at::kInt, "remap"), ki, ko,
                         cur_stream());
+  });
+  m.def("cm_insert_seg", [](Tensor table, int k, int vmax, Tensor keys, Tensor seg_start,
+                            optional<Tensor> n_dev) {
+    chk(table, at::kInt, "table");
+    chk(keys, at::kLong, "keys");
+    chk(seg_start, at::kInt, "seg_start");
+    check(k >= 1 && k <= 30 && vmax >= 1 && vmax <= 255, "countmin k/vmax");
+    check(seg_start.numel() >= keys.numel() + 1 || n_dev.has_value(), "seg_start too small");
+    const int64_t n = std::min<int64_t>(keys.numel(), seg_start.numel() - 1);
+    psamd::cm_insert_seg(ptr<uint32_t>(table), (uint64_t)table.numel() * 4, k, (uint32_t)vmax,
+                         ptr<uint64_t>(keys), ptr<int32_t>(seg_start), n,
+                         optr<int32_t>(n_dev, at::kInt, "n_dev"), cur_stream());
   });
   m.def("ff_minmax", [](Tensor x, Tensor mm) {
     chk(x, at::kFloat, "x");

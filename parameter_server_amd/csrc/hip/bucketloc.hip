@@ -429,7 +429,7 @@ void localize_bucket(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_
   p += (size_t)n * 4;
   int32_t* pp = (int32_t*)p;
 
-  PSAMD_HIP_CHECK(hipMemsetAsync(count, 0, (size_t)nbk * 4, st));
+  fill_async<uint32_t>(count, nbk, 0u, st);
   const int gh = grid_for(n, kHistBlk, 512);
   bl_hist_kernel<<<gh, kHistBlk, 0, st>>>(raw, n, m, R, nbk, count);
   PSAMD_HIP_CHECK(hipGetLastError());

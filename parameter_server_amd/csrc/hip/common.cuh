@@ -160,4 +160,21 @@ __host__ __device__ __forceinline__ float u01(uint64_t r) {  // (0,1]
   return ((float)(r >> 40) + 1.0f) * (1.0f / 16777216.0f);
 }
 
+// Device fill by a kernel, never hipMemsetAsync: inside a captured HIP graph a memset
+// node can run on a blit/SDMA engine outside the stream order the kernels around it
+// see (measured: a scratch table reset by a memset node was not reset on replay).
+template <typename T>
+__global__ void fill_kernel(T* __restrict__ p, int64_t n, T v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+template <typename T>
+inline void fill_async(T* p, int64_t n, T v, hipStream_t st) {
+  if (n <= 0) return;
+  fill_kernel<T><<<grid_for(n, 256, 4096), 256, 0, st>>>(p, n, v);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace psamd

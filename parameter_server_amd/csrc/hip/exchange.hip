@@ -122,6 +122,18 @@ __global__ void xchg_unpack_w_kernel(const float* __restrict__ recv_w,
   }
 }
 
+// Copies the device overflow counter into host-mapped (pinned) memory so the
+// host can poll it every step without a stream synchronisation: the trainer
+// raises at the first step whose published count is non-zero.
+__global__ void xchg_publish_kernel(const int32_t* __restrict__ src, int32_t* __restrict__ dst) {
+  if (threadIdx.x == 0) dst[0] = src[0];
+}
+
+void xchg_publish(const int32_t* src, int32_t* host_mapped_dst, hipStream_t st) {
+  xchg_publish_kernel<<<1, 64, 0, st>>>(src, host_mapped_dst);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
 void xchg_pack_keys(const uint64_t* ukeys, const int32_t* n_uniq, int64_t n_host,
                     const int64_t* off, int G, int64_t C, int kw, int64_t H, int32_t* send,
                     int32_t* ovf, hipStream_t st) {

@@ -62,6 +62,27 @@ __global__ void cm_insert_kernel(uint32_t* __restrict__ table, uint64_t n_cells,
   }
 }
 
+// Tail-filter insert of a localised minibatch (reference MinibatchReader::read,
+// src/learner/sgd.h:140-146): count of unique key i = its occurrences
+// seg_start[i+1] - seg_start[i], saturated to a byte; device unique count.
+__global__ void cm_insert_seg_kernel(uint32_t* __restrict__ table, uint64_t n_cells, int k,
+                                     uint32_t vmax, const uint64_t* __restrict__ keys,
+                                     const int32_t* __restrict__ seg_start, int64_t n_host,
+                                     const int32_t* __restrict__ n_dev) {
+  const int64_t n = dev_len(n_dev, n_host);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = sketch_hash(keys[i]);
+    const uint32_t delta = (h >> 17) | (h << 15);
+    const int32_t occ = seg_start[i + 1] - seg_start[i];
+    const uint32_t c = occ <= 0 ? 0u : (occ > 255 ? 255u : (uint32_t)occ);
+    for (int j = 0; j < k; ++j) {
+      sat_add_byte(table, h % n_cells, c, vmax);
+      h += delta;
+    }
+  }
+}
+
 // keep[i] = (min count > freq) ; also returns the min count.
 __global__ void cm_query_kernel(const uint32_t* __restrict__ table, uint64_t n_cells, int k,
                                 uint32_t vmax, const uint64_t* __restrict__ keys, int64_t n_host,
@@ -89,12 +110,17 @@ __global__ void compact_kept_kernel(const int32_t* __restrict__ keep,
                                     const int32_t* __restrict__ incl, int64_t n_host,
                                     const int32_t* __restrict__ n_dev,
                                     int32_t* __restrict__ kept_idx, int32_t* __restrict__ n_kept,
-                                    int32_t* __restrict__ remap) {
+                                    int32_t* __restrict__ remap,
+                                    const uint64_t* __restrict__ keys_in,
+                                    uint64_t* __restrict__ keys_out) {
   const int64_t n = dev_len(n_dev, n_host);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t dst = incl[i] - 1;
-    if (keep[i]) kept_idx[dst] = (int32_t)i;
+    if (keep[i] && in_range(dst, n_host)) {
+      kept_idx[dst] = (int32_t)i;
+      if (keys_out) keys_out[dst] = keys_in[i];
+    }
     if (remap) remap[i] = keep[i] ? dst : -1;
     if (i == n - 1) *n_kept = incl[i];
   }
@@ -198,10 +224,18 @@ void cm_query(const uint32_t* table, uint64_t n_cells, int k, uint32_t vmax, con
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
+void cm_insert_seg(uint32_t* table, uint64_t n_cells, int k, uint32_t vmax, const uint64_t* keys,
+                   const int32_t* seg_start, int64_t n, const int32_t* n_dev, hipStream_t st) {
+  cm_insert_seg_kernel<<<grid_for(n, 256), 256, 0, st>>>(table, n_cells, k, vmax, keys, seg_start,
+                                                         n, n_dev);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
 void compact_kept(const int32_t* keep, const int32_t* incl, int64_t n, const int32_t* n_dev,
-                  int32_t* kept_idx, int32_t* n_kept, int32_t* remap, hipStream_t st) {
+                  int32_t* kept_idx, int32_t* n_kept, int32_t* remap, const uint64_t* keys_in,
+                  uint64_t* keys_out, hipStream_t st) {
   compact_kept_kernel<<<grid_for(n, 256), 256, 0, st>>>(keep, incl, n, n_dev, kept_idx, n_kept,
-                                                        remap);
+                                                        remap, keys_in, keys_out);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
@@ -227,7 +261,7 @@ void ff_decode(const uint8_t* code, int64_t n, const float* mm, int nbytes, floa
 }
 
 void key_signature(const uint64_t* keys, int64_t n, unsigned long long* sig, hipStream_t st) {
-  PSAMD_HIP_CHECK(hipMemsetAsync(sig, 0, sizeof(unsigned long long), st));
+  fill_async<unsigned long long>(sig, 1, 0ull, st);
   key_signature_kernel<<<grid_for(n, 256, 1024), 256, 0, st>>>(keys, n, sig);
   PSAMD_HIP_CHECK(hipGetLastError());
 }

@@ -337,7 +337,7 @@ void owner_bucket(const uint64_t* uniq, const int32_t* n_uniq, int64_t n_host,
   if (G > kMaxOwners) throw std::runtime_error("owner_bucket: at most 64 shards");
   unsigned long long* totals = (unsigned long long*)temp;
   unsigned long long* cursors = totals + kMaxOwners;
-  PSAMD_HIP_CHECK(hipMemsetAsync(totals, 0, kMaxOwners * sizeof(unsigned long long), st));
+  fill_async<unsigned long long>(totals, kMaxOwners, 0ull, st);
   ob_count_kernel<<<grid_for(n_host, kBlk, 1024), kBlk, 0, st>>>(uniq, n_uniq, n_host, bounds, G,
                                                                   totals);
   PSAMD_HIP_CHECK(hipGetLastError());

@@ -399,6 +399,126 @@ __global__ void kv_apply_accumulated_kernel(Slot* __restrict__ slots, int64_t ca
   }
 }
 
+// ---------------------------------------------------------------------------
+// The owner's pushes of one exchange, ALL G source rows, with per-push semantics
+// (reference KVStore::setValue applies every push message as its own optimizer
+// step, src/parameter/kv_store.h:47-57): a slot pushed by several sources gets
+// their gradients one after the other in source-rank order. Instead of G
+// launches (one per source row, the rows run in order), two launches for any G:
+//   link:  each entry e = s*C + i (slot k) swaps itself into a per-exchange scratch
+//          hash keyed by k (64-bit word = k << 32 | head entry) and keeps the
+//          entry it replaced in nxt[e] -> one chain per slot, <= G entries long
+//          (a source row holds distinct keys, so distinct slots);
+//   apply: the entry that is the final head of its chain walks it, applies the
+//          gradients in increasing entry order (= source order) to a register copy
+//          of the slot and stores it once.
+// Bitwise the same weights as the per-row launch sequence. Scratch: link[HS] u64
+// (HS = power of two >= 2 * G * C), reset to ~0 by the launcher, nxt[G * C] i32.
+constexpr int kMaxChain = 64;  // source rows per exchange (exchange.hip kMaxPeers)
+__device__ __forceinline__ uint64_t link_probe_start(int64_t k, uint64_t hmask) {
+  return fmix64((uint64_t)k) & hmask;
+}
+
+__global__ void kv_link_rows_kernel(const int64_t* __restrict__ slot_idx, int64_t cap,
+                                    const float* __restrict__ grad, int64_t gstride,
+                                    const int32_t* __restrict__ recv, int64_t H, int64_t C,
+                                    unsigned long long* __restrict__ link, uint64_t hmask,
+                                    int32_t* __restrict__ nxt) {
+  const int s = blockIdx.y;
+  const int64_t n = dev_len(recv + (int64_t)s * H + 1, C);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = (int64_t)s * C + i;
+    const int64_t k = slot_idx[e];
+    const float g = grad[(int64_t)s * gstride + i];
+    if (!in_range(k, cap) || g != g) continue;  // NaN mark = filtered entry
+    uint64_t h = link_probe_start(k, hmask);
+    for (uint64_t probe = 0; probe <= hmask; ++probe) {
+      unsigned long long cur = link[h];
+      bool done = false;
+      while (true) {
+        if (cur == ~0ull) {  // empty: claim it for k
+          const unsigned long long mine = ((unsigned long long)k << 32) | (uint32_t)e;
+          const unsigned long long prev = atomicCAS(&link[h], cur, mine);
+          if (prev == cur) { nxt[e] = -1; done = true; break; }
+          cur = prev;
+          continue;
+        }
+        if ((int64_t)(cur >> 32) != k) break;  // another slot: next probe
+        const unsigned long long mine = (cur & 0xffffffff00000000ull) | (uint32_t)e;
+        const unsigned long long prev = atomicCAS(&link[h], cur, mine);
+        if (prev == cur) { nxt[e] = (int32_t)(uint32_t)(cur & 0xffffffffull); done = true; break; }
+        cur = prev;
+      }
+      if (done) break;
+      h = (h + 1) & hmask;
+    }
+  }
+}
+
+__global__ void kv_apply_rows_kernel(Slot* __restrict__ slots, int64_t cap,
+                                     const int64_t* __restrict__ slot_idx,
+                                     const float* __restrict__ grad, int64_t gstride,
+                                     const int32_t* __restrict__ recv, int64_t H, int64_t C,
+                                     const unsigned long long* __restrict__ link, uint64_t hmask,
+                                     const int32_t* __restrict__ nxt, int64_t n_ent,
+                                     UpdateParams p, double* __restrict__ stats, int acc_stripes) {
+  __shared__ double lds[16];
+  const int s = blockIdx.y;
+  const int64_t n = dev_len(recv + (int64_t)s * H + 1, C);
+  double dnnz = 0, wsum = 0, dsum = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = (int64_t)s * C + i;
+    const int64_t k = slot_idx[e];
+    const float g0 = grad[(int64_t)s * gstride + i];
+    if (!in_range(k, cap) || g0 != g0) continue;
+    uint64_t h = link_probe_start(k, hmask);
+    unsigned long long cur = ~0ull;
+    for (uint64_t probe = 0; probe <= hmask; ++probe) {
+      cur = link[h];
+      if (cur == ~0ull || (int64_t)(cur >> 32) == k) break;
+      h = (h + 1) & hmask;
+    }
+    if (cur == ~0ull || (int64_t)(uint32_t)(cur & 0xffffffffull) != e) continue;  // not the head
+    // chain length (<= number of source rows) and apply in increasing entry order
+    int len = 0;
+    for (int32_t c = (int32_t)e; c >= 0 && len < kMaxChain; c = nxt[c]) {
+      if (!in_range((int64_t)c, n_ent)) break;
+      ++len;
+    }
+    Slot sl = slots[k];
+    int64_t last = -1;
+    for (int it = 0; it < len; ++it) {
+      int64_t best = INT64_MAX;
+      int walked = 0;
+      for (int32_t c = (int32_t)e; c >= 0 && walked < len; c = nxt[c], ++walked)
+        if ((int64_t)c > last && (int64_t)c < best) best = c;
+      if (best == INT64_MAX) break;
+      const int64_t bs = best / C, bi = best - bs * C;
+      const float g = grad[bs * gstride + bi] * p.grad_scale;
+      const float w_old = apply_update(sl, g, p);
+      dnnz += (double)((sl.w != 0.f) - (w_old != 0.f));
+      wsum += (double)sl.w * sl.w;
+      const double d = (double)sl.w - w_old;
+      dsum += d * d;
+      last = best;
+    }
+    slots[k] = sl;
+  }
+  if (stats) {
+    double a = block_sum_f64(dnnz, lds);
+    double b = block_sum_f64(wsum, lds);
+    double c = block_sum_f64(dsum, lds);
+    if (threadIdx.x == 0) {
+      double* st = acc_stripe(stats, acc_stripes);
+      if (a != 0) atomicAdd(&st[0], a);
+      if (b != 0) atomicAdd(&st[1], b);
+      if (c != 0) atomicAdd(&st[2], c);
+    }
+  }
+}
+
 // Occupancy / sparsity census: out[0] = occupied slots, out[1] = nonzero w.
 __global__ void kv_census_kernel(const Slot* __restrict__ slots, int64_t cap,
                                  unsigned long long* __restrict__ out) {
@@ -512,6 +632,27 @@ void kv_apply_accumulated(void* slots, int64_t cap, const int64_t* touched, cons
   kv_apply_accumulated_kernel<<<grid_for(max_n, 256), 256, 0, st>>>((Slot*)slots, cap, touched,
                                                                     n_touched, max_n, p, stats,
                                                                     acc_stripes);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void kv_update_rows(void* slots, int64_t cap, const int64_t* slot_idx, const float* grad,
+                    int64_t gstride, const int32_t* recv, int G, int64_t H, int64_t C,
+                    unsigned long long* link, int64_t link_size, int32_t* nxt, int algo,
+                    int lr_type, float alpha, float beta, float l1, float l2, float grad_scale,
+                    float max_delta, double* stats, int acc_stripes, hipStream_t st) {
+  if (cap > (int64_t(1) << 32)) throw std::runtime_error("kv_update_rows: capacity > 2^32");
+  if (link_size < 2 * (int64_t)G * C || (link_size & (link_size - 1)))
+    throw std::runtime_error("kv_update_rows: link scratch must be a power of two >= 2*G*C");
+  if (G < 1 || G > kMaxChain) throw std::runtime_error("kv_update_rows: 1..64 source rows");
+  UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
+  fill_async<unsigned long long>(link, link_size, ~0ull, st);
+  dim3 grid(grid_for(C, 256, 1024), G);
+  kv_link_rows_kernel<<<grid, 256, 0, st>>>(slot_idx, cap, grad, gstride, recv, H, C, link,
+                                            (uint64_t)(link_size - 1), nxt);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  kv_apply_rows_kernel<<<grid, 256, 0, st>>>((Slot*)slots, cap, slot_idx, grad, gstride, recv, H,
+                                             C, link, (uint64_t)(link_size - 1), nxt,
+                                             (int64_t)G * C, p, stats, acc_stripes);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

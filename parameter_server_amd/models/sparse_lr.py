@@ -44,7 +44,7 @@ from ..ops.linear import (AUC_BINS, HIST_STRIPES, accum_total, auc_from_hist, li
 from ..ops.localize import Localizer
 from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
-from ..parallel.consistency import VectorClock, parse_consistency
+from ..parallel.consistency import ExchangeSchedule, parse_consistency
 from ..parallel.partition import KeyPartition
 from ..utils.trace import trace_range
 
@@ -81,10 +81,11 @@ class SparseLRConfig:
     exchange_capacity: int = 0           # keys per peer per step; 0 = auto (first step)
     exchange_slack: float = 1.5          # auto capacity = slack * max per-peer count + 1024
     # padded exchange pipelining depth: pushes of step t ride the exchange of step
-    # t + 1 + lag, so the exchange of step t+1 can run while step t computes; the
-    # pull of step t then misses at most `lag` steps of pushes (SSP staleness).
-    # -1 = from `consistency` (bsp -> 0, ssp:tau / asp -> 1)
+    # t + 1 + lag, so the exchanges of steps t+1 .. t+lag can run while step t
+    # computes; the pull of step t then misses exactly the `lag` most recent steps of
+    # pushes. -1 = from `consistency` (bsp -> 0, ssp:tau -> tau, asp -> 1)
     exchange_lag: int = -1
+    asp_depth: int = 4                   # asp: exchanges whose push applies may be in flight
     seed: int = 0
 
     def update_rule(self) -> UpdateRule:
@@ -103,7 +104,6 @@ class SparseLRTrainer:
         self.part = KeyPartition(self.bits, self.G)
         self.rule = cfg.update_rule()
         self.tau = parse_consistency(cfg.consistency)
-        self.clock = VectorClock(self.G, self.tau)
         cap = cfg.table_capacity or self.auto_capacity(cfg, self.G, self.bits)
         # ordered home slots over this shard's mixed-key range: sorted unique keys then
         # walk the (up to 64 GB) table in increasing address order
@@ -132,14 +132,20 @@ class SparseLRTrainer:
         # multi-GPU: fuse push(t-1) into the pull exchange of step t (2 all-to-alls/step)
         if cfg.exchange not in ("padded", "exact"):
             raise ValueError(f"exchange must be 'padded' or 'exact', not {cfg.exchange!r}")
-        self.padded = self.G > 1 and self.filter is None and cfg.exchange == "padded"
+        self.padded = self.G > 1 and cfg.exchange == "padded"
         self.fused = (self.G > 1 and self.filter is None and cfg.fixing_float_bytes == 0
                       and not self.padded)
         self.xc = None  # padded-exchange state (allocated on the first step)
-        lag = cfg.exchange_lag if cfg.exchange_lag >= 0 else (0 if self.tau == 0 else 1)
-        if lag > self.tau:
-            raise ValueError(f"exchange_lag {lag} exceeds the staleness bound {self.tau}")
-        self.lag = int(min(lag, 1))  # parity-double-buffered exchange state: depth <= 1
+        # consistency on the padded exchange: the pushes of step t ride exchange t+1+lag
+        # and are applied before its pulls, so the pull of step t sees exactly the
+        # pushes of steps <= t-1-lag (bsp: lag 0; ssp:tau: lag tau). asp: lag 1 and the
+        # owner applies pushes on their own stream, which later pulls do not wait for
+        # (only buffer reuse bounds it: async_depth exchanges in flight).
+        self.sched = ExchangeSchedule(self.tau, cfg.exchange_lag, cfg.asp_depth)
+        self.lag, self.asp, self.async_depth = self.sched.lag, self.sched.asp, self.sched.depth
+        # rings of R exchange buffers indexed by step (>= 2: the exchange of step t+1
+        # runs while the worker half of step t still reads its weights)
+        self.R = self.sched.R
         self._xt = 0  # padded steps computed (worker halves run)
         self._xx = 0  # padded exchanges issued (exchange halves run)
         self.pending = None
@@ -233,32 +239,36 @@ class SparseLRTrainer:
             self._push(grad, push)
         _push.__exit__(None, None, None)
         auc_from_hist(self.hist, self.metrics, self.step_dev)
-        self.clock.tick(self.rank, self.step_count)
         self.step_count += 1
         self.examples += B
 
     # --------------------------------------------- padded exchange (G > 1, default)
     def step_segments(self, keys: torch.Tensor, labels: torch.Tensor, *, width=None,
-                      row_ptr=None, vals=None, rows=None, loc=None, parity=None):
+                      row_ptr=None, vals=None, rows=None, loc=None, step=None):
         """The step as an ordered list of ``(kind, fn)``: ``"compute"`` segments are
         pure device work on fixed buffers (capturable in a HIP graph per localisation
-        buffer), ``"comm"`` segments are the two equal-split RCCL all-to-alls, and
-        ``"host"`` is the host bookkeeping. No segment reads anything back to the host,
-        so a step is enqueued without waiting for the GPU.
+        buffer and ring position), ``"comm"`` segments are the two equal-split RCCL
+        all-to-alls, ``"async"`` (ASP only) is the owner's push apply that pulls do
+        not wait for, and ``"host"`` is the host bookkeeping. No segment reads anything
+        back to the host, so a step is enqueued without waiting for the GPU.
 
           compute  owner-split the unique keys, pack [keys(t)] next to [grads(t-1-lag)]
           comm     all-to-all A
-          compute  owner: pushes of t-1-lag (one optimizer step per source, rank
-                   order), then lookup-or-insert of the pulled keys of t -> weights
+          compute  owner: apply the pushes of t-1-lag (one optimizer step per source,
+                   rank order, all sources in one launch), then lookup-or-insert of
+                   the pulled keys of t -> weights       [ASP: resolve only]
+          async    [ASP: apply the pushes of t-1-lag; the next pulls do not wait]
           comm     all-to-all B (weights back)
           compute  unpack weights, forward, backward, pack grads(t), AUC
-          host     counters, vector clock
+          host     counters, overflow check
 
-        The first four are the exchange half (``"comm"`` and the compute segments
-        before the last one), the last compute segment is the worker half; with
-        ``lag == 1`` the exchange half of step t+1 may run concurrently with the
-        worker half of step t (bench.py issues them on different streams). Buffers
-        alternate with the step parity (``parity``, default: steps issued % 2).
+        Everything before the last compute segment is the exchange half, the rest the
+        worker half (``EXCHANGE_SEGMENTS``); with lag >= 1 the exchange half of step
+        t+1 may run while the worker half of step t computes (bench.py issues them on
+        different streams). Buffers live in rings of ``self.R`` entries indexed by the
+        absolute step ``step`` (default: the next step to compute); only ``step %
+        self.R`` matters, so a graph captured for ring position j replays for every
+        step t with t % R == j.
         """
         if not self.padded:
             return [("compute", lambda: self.step(keys, labels, width=width, row_ptr=row_ptr,
@@ -273,32 +283,53 @@ class SparseLRTrainer:
         if self.xc is None:
             self._xc_setup(loc)
         comm, xc = self.comm, self.xc
-        par = self._xt % 2 if parity is None else int(parity) % 2
-        sb = (par - 1 - self.lag) % 2  # send buffer: holds grads(t-1-lag), gets keys(t)
+        t = self._xt if step is None else int(step)
+        r = self.sched.ring(t)        # ring position of step t
+        gb = self.sched.grad_ring(t)  # grads(t-1-lag) live here; keys(t) join them
 
         def finish():
             if row_ptr is not None and self.gpu:
                 hipops().csr_rows(row_ptr, rows)
-            self._x_finish(loc, labels, B, width, row_ptr, vals, rows, par)
+            self._x_finish(loc, labels, B, width, row_ptr, vals, rows, r)
 
         def host():
-            self.clock.tick(self.rank, self.step_count)
             self.step_count += 1
             self._xt += 1
             self.examples += B
+            self._x_poll_overflow()
 
         def exchanged():
             self._xx += 1
 
-        return [("compute", lambda: self._x_pack_keys(loc, sb, par)),
-                ("comm", lambda: comm.all_to_all_fixed(xc.sends[sb], xc.recv)),
-                ("compute", lambda: self._x_serve(push_par=sb, resolve_par=par)),
-                ("comm", lambda: comm.all_to_all_fixed(xc.wsend, xc.wrecvs[par])),
-                ("host", exchanged),
-                ("compute", finish),
-                ("host", host)]
+        segs = [("compute", lambda: self._x_pack_keys(loc, gb, r)),
+                ("comm", lambda: comm.all_to_all_fixed(xc.sends[gb], xc.recvs[r]))]
+        if self.asp:
+            segs += [("compute", lambda: self._x_resolve(r)),
+                     ("async", lambda: self._x_apply(r, gb))]
+        else:
+            segs += [("compute", lambda: (self._x_apply(r, gb), self._x_resolve(r)))]
+        segs += [("comm", lambda: comm.all_to_all_fixed(xc.wsend, xc.wrecvs[r])),
+                 ("host", exchanged),
+                 ("compute", finish),
+                 ("host", host)]
+        return segs
 
-    EXCHANGE_SEGMENTS = 5  # step_segments()[:5] = exchange half, [5:] = worker half
+    @property
+    def EXCHANGE_SEGMENTS(self) -> int:  # step_segments()[:n] = exchange half
+        return 6 if self.asp else 5
+
+    def consistency_desc(self) -> str:
+        """The consistency the data plane actually enforces (reported by bench.py)."""
+        if self.G == 1:
+            return "bsp (1 shard: every pull sees every earlier push)"
+        if not self.padded or self.lag == 0 and not self.asp:
+            return "bsp (pull of step t sees every push of steps <= t-1)"
+        if self.asp:
+            return (f"asp (pushes applied asynchronously to pulls; pull of step t misses "
+                    f">= {self.lag} and, bounded only by the {self.R}-entry ring, "
+                    f"<= {self.lag + self.async_depth} steps of pushes)")
+        return (f"ssp:{int(self.tau)} (pull of step t sees exactly the pushes of steps "
+                f"<= t-1-{self.lag})")
 
     def _xc_setup(self, loc):
         """Allocate the fixed exchange rows. Capacity C (keys per peer per step) is the
@@ -307,10 +338,10 @@ class SparseLRTrainer:
         so the margin is many standard deviations)."""
         from types import SimpleNamespace
 
-        cfg, G, dev = self.cfg, self.G, self.device
+        cfg, G, dev, R = self.cfg, self.G, self.device, self.R
         C = int(cfg.exchange_capacity)
         if C <= 0:
-            _, _, off = self._owner_order(loc)
+            _, _, off, _ = self._owner_order(loc)
             cnt = (off[1:] - off[:-1]).max().to(torch.float64).reshape(1)
             cnt = self.comm.all_reduce_(cnt.to(self.comm.device) if self.comm.backend == "nccl"
                                         else cnt.cpu(), op="max")
@@ -324,35 +355,88 @@ class SparseLRTrainer:
         self.xc = SimpleNamespace(
             C=C, kw=kw, H=H, nb=nb,
             gstage=z32(G * C, torch.float32) if nb else None,
-            gin=z32(G * C, torch.float32) if nb else None,
-            # parity-double-buffered: sends[b] holds grads(t) then keys(t+1+lag);
-            # slots[p] the owner's resolved slots of pull step p (for its push)
-            sends=[z32(G * H, torch.int32) for _ in range(2)], recv=z32(G * H, torch.int32),
-            slots=[torch.full((G * C,), -1, dtype=torch.int64, device=dev) for _ in range(2)],
-            wsend=z32(G * C, torch.float32), wrecvs=[z32(G * C, torch.float32) for _ in range(2)],
+            gins=[z32(G * C, torch.float32) for _ in range(R)] if nb else None,
+            # rings of R entries indexed by step: sends[j] holds grads(j) then keys(j+1+lag);
+            # recvs[j] what exchange j received; slots[j] the owner's resolved slots of
+            # pull step j (its push arrives lag+1 exchanges later)
+            sends=[z32(G * H, torch.int32) for _ in range(R)],
+            recvs=[z32(G * H, torch.int32) for _ in range(R)],
+            slots=[torch.full((G * C,), -1, dtype=torch.int64, device=dev) for _ in range(R)],
+            wsend=z32(G * C, torch.float32), wrecvs=[z32(G * C, torch.float32) for _ in range(R)],
             w_local=z32(self.max_nnz, torch.float32), ovf=z32(1, torch.int32),
-            offs=[z32(G + 1, torch.int64) for _ in range(2)], curs=[None, None],
+            offs=[z32(G + 1, torch.int64) for _ in range(R)], curs=[None] * R,
             touched=torch.empty(G * C, dtype=torch.int64, device=dev) if self.gpu else None,
-            n_touched=z32(1, torch.int32))
+            n_touched=z32(1, torch.int32),
+            # per-exchange chain scratch of the one-launch sequential push apply
+            link=(torch.empty(next_pow2(2 * G * C), dtype=torch.int64, device=dev)
+                  if self.gpu else None),
+            nxt=torch.empty(G * C, dtype=torch.int32, device=dev) if self.gpu else None,
+            ovf_host=(torch.zeros(1, dtype=torch.int32, pin_memory=True) if self.gpu else None))
 
-    def _owner_order(self, loc, par: int = 0):
-        """(keys in owner order, perm owner-order -> unique id | None, off[G+1])."""
+    def _tail_filter(self, loc, ring: int):
+        """Tail-feature filter on the padded exchange (reference MinibatchReader::read,
+        src/learner/sgd.h:131-150): insert this minibatch's per-key occurrence counts
+        into the worker's CountMin, keep the keys whose estimate > tail_feature_freq.
+        Returns (kept keys in sorted order, kept -> unique id, device kept count);
+        device-side compaction, no host sync, so the step stays graph-capturable.
+        Filtered keys are neither pulled (w = 0) nor pushed."""
+        U = loc.uniq.numel()
+        freq = self.cfg.tail_feature_freq
+        if not self.gpu:
+            n = int(loc.n_uniq.reshape(-1)[0])
+            self.filter.insert_segments(loc.uniq, loc.seg_start, loc.n_uniq)
+            keep, _ = self.filter.query(loc.uniq[:n], freq)
+            idx = torch.nonzero(keep, as_tuple=False).flatten().to(torch.int32)
+            return (loc.uniq[:n][idx.long()].contiguous(), idx,
+                    torch.tensor([idx.numel()], dtype=torch.int32))
+        tf = getattr(self, "_tf", None)
+        if tf is None or tf["keep"].numel() < U:
+            i32 = lambda k: torch.empty(k, dtype=torch.int32, device=self.device)  # noqa: E731
+            tf = self._tf = {"keep": i32(U), "incl": i32(U),
+                             "keys": [torch.empty(U, dtype=torch.int64, device=self.device)
+                                      for _ in range(self.R)],
+                             "idx": [i32(U) for _ in range(self.R)],
+                             "n": [torch.zeros(1, dtype=torch.int32, device=self.device)
+                                   for _ in range(self.R)]}
+        keep, incl = tf["keep"][:U], tf["incl"][:U]
+        self.filter.insert_segments(loc.uniq, loc.seg_start, loc.n_uniq)
+        hh = hipops()
+        keep.zero_()
+        hh.cm_query(self.filter.cells.view(torch.int32), self.filter.k, self.filter.vmax,
+                    loc.uniq, loc.n_uniq, freq, keep, None)
+        torch.cumsum(keep, 0, dtype=torch.int32, out=incl)
+        kk, ki, nk = tf["keys"][ring], tf["idx"][ring], tf["n"][ring]
+        hh.compact_kept(keep, incl, loc.n_uniq, ki, nk, None, loc.uniq, kk)
+        return kk, ki, nk
+
+    def _owner_order(self, loc, ring: int = 0):
+        """(keys in owner order, perm owner-order -> unique id | None, off[G+1], count)."""
+        if self.filter is not None and self.xc is not None:
+            kk, ki, nk = self._tail_filter(loc, ring)
+            off = self.xc.offs[ring]
+            if self.gpu:
+                hipops().owner_split(kk, nk, self.part.bounds_on(self.device), off)
+            else:
+                off = self.part.split_sorted(kk, nk)
+            return kk, ki, off, nk
         if getattr(loc, "hashed", False):
-            return self._bucket(loc, par)
+            return self._bucket(loc, ring) + (loc.n_uniq,)
         if self.gpu:
-            off = self.xc.offs[par] if self.xc is not None else torch.empty(
+            off = self.xc.offs[ring] if self.xc is not None else torch.empty(
                 self.G + 1, dtype=torch.int64, device=self.device)
             hipops().owner_split(loc.uniq, loc.n_uniq, self.part.bounds_on(self.device), off)
-            return loc.uniq, None, off
-        return loc.uniq, None, self.part.split_sorted(loc.uniq, loc.n_uniq)
+            return loc.uniq, None, off, loc.n_uniq
+        return loc.uniq, None, self.part.split_sorted(loc.uniq, loc.n_uniq), loc.n_uniq
 
-    def _x_pack_keys(self, loc, sb: int, par: int):
+    def _x_pack_keys(self, loc, gb: int, r: int):
         xc = self.xc
-        ukeys, perm, off = self._owner_order(loc, par)
-        xc.curs[par] = (perm, off, loc.n_uniq)
-        send = xc.sends[sb]
+        ukeys, perm, off, nkeys = self._owner_order(loc, r)
+        xc.curs[r] = (perm, off, nkeys)
+        send = xc.sends[gb]
         if self.gpu:
-            hipops().xchg_pack_keys(ukeys, loc.n_uniq, off, xc.C, xc.kw, xc.H, send, xc.ovf)
+            hh = hipops()
+            hh.xchg_pack_keys(ukeys, nkeys, off, xc.C, xc.kw, xc.H, send, xc.ovf)
+            hh.xchg_publish(xc.ovf, xc.ovf_host)
             return
         H, C, kw = xc.H, xc.C, xc.kw
         for p in range(self.G):
@@ -364,75 +448,101 @@ class SparseLRTrainer:
             k32 = k.to(torch.int32) if kw == 1 else k.contiguous().view(torch.int32)
             send[p * H + 4:p * H + 4 + c * kw] = k32
 
-    def _x_serve(self, push_par: int, resolve_par: int | None):
-        """Owner side: the pushes carried by this exchange (gradients of the pull step
-        with parity ``push_par``, whose resolved slots are ``slots[push_par]``) in
-        source-rank order, then (``resolve_par`` not None) the pulls of this step."""
-        xc, G, H, C, kw = self.xc, self.G, self.xc.H, self.xc.C, self.xc.kw
-        pslot = xc.slots[push_par]
-        resolve = resolve_par is not None
-        g0 = 4 + C * kw
-        rows = [xc.recv[s * H:(s + 1) * H] for s in range(G)]
+    def _x_poll_overflow(self):
+        """Raise at the first step whose exchange dropped keys (the device counter is
+        published into pinned host memory by the pack kernel: no stream sync; on the
+        GPU the check sees a pack that has completed, at most the pipeline depth
+        behind). Dropped keys would have been pulled as 0 and their pushes lost."""
+        xc = self.xc
+        ovf = int(xc.ovf_host[0]) if xc.ovf_host is not None else int(xc.ovf.item())
+        if ovf:
+            raise RuntimeError(
+                f"padded exchange overflow at step {self.step_count}: {ovf} keys exceeded the "
+                f"per-peer capacity {xc.C} (pulled as 0, pushes dropped); set exchange_capacity "
+                f"or exchange_slack higher, or exchange='exact'")
+
+    def _x_grads(self, r: int):
+        """Gradient source of the pushes received by exchange ``r``: (tensor, row stride)."""
+        xc = self.xc
         if xc.nb:  # FixingFloat codes -> f32, one launch for all source rows
-            self._x_ff_decode()
-            grads = [xc.gin[s * C:(s + 1) * C] for s in range(G)]
-        else:
-            grads = [rows[s][g0:g0 + C].view(torch.float32) for s in range(G)]
+            self._x_ff_decode(r)
+            return xc.gins[r], xc.C
+        g0 = 4 + xc.C * xc.kw
+        return xc.recvs[r].view(torch.float32)[g0:], xc.H
+
+    def _x_apply(self, r: int, gb: int):
+        """Owner: the pushes carried by exchange ``r`` (gradients of the pull step
+        whose resolved slots are ``slots[gb]``), every source row in ONE launch pair
+        with per-push semantics (source-rank order per key) or summed per key
+        (``push_mode='aggregate'``)."""
+        xc, G, H, C = self.xc, self.G, self.xc.H, self.xc.C
+        pslot, recv = xc.slots[gb], xc.recvs[r]
         if self.gpu:
+            gsrc, gstride = self._x_grads(r)
             hh = hipops()
-            if self.cfg.push_mode == "aggregate":  # all source rows: 2 launches, any G
+            if self.cfg.push_mode == "aggregate":
                 xc.n_touched.zero_()
-                if xc.nb:
-                    gsrc, gstride = xc.gin, C
-                else:
-                    gsrc, gstride = xc.recv.view(torch.float32)[g0:], H
-                hh.kv_accumulate_rows(self.table.slots, pslot, gsrc, gstride, xc.recv, H, C,
+                hh.kv_accumulate_rows(self.table.slots, pslot, gsrc, gstride, recv, H, C,
                                       xc.touched, xc.n_touched)
                 hh.kv_apply_accumulated(self.table.slots, xc.touched, xc.n_touched,
                                         *self.rule.args(), self.stats)
             else:
-                for s in range(G):
-                    hh.kv_update(self.table.slots, pslot[s * C:(s + 1) * C], grads[s],
-                                 rows[s][1:2], *self.rule.args(), self.stats)
-            if resolve:
-                it, iv, isd, seed = self.table.init.args()
-                hh.kv_resolve_rows(self.table.slots, xc.recv, H, C, kw, xc.slots[resolve_par],
-                                   xc.wsend, True, it, iv, isd, seed, self.table._err,
-                                   self.table._inserted, self.table.home_base, self.table.home_m)
+                hh.kv_update_rows(self.table.slots, pslot, gsrc, gstride, recv, H, C, xc.link,
+                                  xc.nxt, *self.rule.args(), self.stats)
             return
+        rows = [recv[s * H:(s + 1) * H] for s in range(G)]
+        if xc.nb:
+            self._x_ff_decode(r)
+            grads = [xc.gins[r][s * C:(s + 1) * C] for s in range(G)]
+        else:
+            g0 = 4 + C * xc.kw
+            grads = [rows[s][g0:g0 + C].view(torch.float32) for s in range(G)]
         parts = []
         for s in range(G):
             ng = int(rows[s][1])
             if ng:
                 parts.append((pslot[s * C:s * C + ng], grads[s][:ng]))
         self._apply_pushes(parts)
-        if not resolve:
+
+    def _x_resolve(self, r: int):
+        """Owner: lookup-or-insert the keys pulled by exchange ``r`` -> slots[r], wsend."""
+        xc, G, H, C, kw = self.xc, self.G, self.xc.H, self.xc.C, self.xc.kw
+        recv = xc.recvs[r]
+        if self.gpu:
+            it, iv, isd, seed = self.table.init.args()
+            hipops().kv_resolve_rows(self.table.slots, recv, H, C, kw, xc.slots[r], xc.wsend,
+                                     True, it, iv, isd, seed, self.table._err,
+                                     self.table._inserted, self.table.home_base,
+                                     self.table.home_m)
             return
         for s in range(G):
-            nk = int(rows[s][0])
+            row = recv[s * H:(s + 1) * H]
+            nk = int(row[0])
             if not nk:
                 continue
             if kw == 1:
-                req = rows[s][4:4 + nk].to(torch.int64) & 0xFFFFFFFF
+                req = row[4:4 + nk].to(torch.int64) & 0xFFFFFFFF
             else:
-                req = rows[s][4:4 + 2 * nk].contiguous().view(torch.int64)
+                req = row[4:4 + 2 * nk].contiguous().view(torch.int64)
             slot, w = self.table.resolve(req, insert=True)
-            xc.slots[resolve_par][s * C:s * C + nk] = slot
+            xc.slots[r][s * C:s * C + nk] = slot
             xc.wsend[s * C:s * C + nk] = w
 
-    def _x_finish(self, loc, labels, B, width, row_ptr, vals, rows, par: int):
+    def _x_finish(self, loc, labels, B, width, row_ptr, vals, rows, r: int):
         xc = self.xc
-        perm, off, n_uniq = xc.curs[par]
-        wrecv, send = xc.wrecvs[par], xc.sends[par]  # grads(t) -> sends[t % 2]
+        perm, off, n_uniq = xc.curs[r]
+        wrecv, send = xc.wrecvs[r], xc.sends[r]  # grads(t) -> sends[t % R]
         if self.gpu:
             w_local = xc.w_local[:loc.uniq.numel()]
+            if self.filter is not None:
+                w_local.zero_()  # filtered keys: w = 0
             hipops().xchg_unpack_w(wrecv, perm, n_uniq, off, xc.C, w_local)
         else:
-            U = int(n_uniq)
-            w_local = torch.zeros(max(U, 1), dtype=torch.float32)
+            w_local = torch.zeros(max(int(loc.n_uniq.reshape(-1)[0]), 1), dtype=torch.float32)
             for p in range(self.G):
                 a, c = int(off[p]), min(int(off[p + 1] - off[p]), xc.C)
-                w_local[a:a + c] = wrecv[p * xc.C:p * xc.C + c]
+                dst = perm[a:a + c].long() if perm is not None else slice(a, a + c)
+                w_local[dst] = wrecv[p * xc.C:p * xc.C + c]
         _, coef, _ = linear_forward(loc.local_col, w_local, labels, B=B, width=width or 0,
                                     row_ptr=row_ptr, vals=vals, loss=self.cfg.loss,
                                     coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
@@ -447,7 +557,8 @@ class SparseLRTrainer:
                 a, c = int(off[p]), min(int(off[p + 1] - off[p]), C)
                 send[p * H + 1] = c
                 g0 = p * H + 4 + C * kw
-                send[g0:g0 + c] = grad[a:a + c].contiguous().view(torch.int32)
+                g = grad[perm[a:a + c].long()] if perm is not None else grad[a:a + c]
+                send[g0:g0 + c] = g.contiguous().view(torch.int32)
         auc_from_hist(self.hist, self.metrics, self.step_dev)
 
     def _x_ff_pack(self, grad, perm, n_uniq, off, send):
@@ -463,56 +574,60 @@ class SparseLRTrainer:
         for p in range(self.G):
             a, c = int(off[p]), min(int(off[p + 1] - off[p]), C)
             send[p * H + 1] = c
-            g = grad[a:a + c]
+            g = grad[perm[a:a + c].long()] if perm is not None else grad[a:a + c]
             code, mm = ff.encode(g, nb, seed=seed + 1000003 * self.step_count + p)
             send[p * H + 2:p * H + 4] = mm.view(torch.int32)
             g0 = p * H + 4 + C * kw
             words = send[g0:g0 + (C * nb + 3) // 4].view(torch.uint8)
             words[:code.numel()] = code
 
-    def _x_ff_decode(self):
+    def _x_ff_decode(self, r: int):
         xc, H, C, kw, nb = self.xc, self.xc.H, self.xc.C, self.xc.kw, self.xc.nb
+        recv, gin = xc.recvs[r], xc.gins[r]
         if self.gpu:
-            hipops().xchg_ff_decode(xc.recv, C, kw, H, nb, xc.gin)
+            hipops().xchg_ff_decode(recv, C, kw, H, nb, gin)
             return
         for s in range(self.G):
-            row = xc.recv[s * H:(s + 1) * H]
+            row = recv[s * H:(s + 1) * H]
             n = int(row[1])
             if n:
                 g0 = 4 + C * kw
                 code = row[g0:g0 + (C * nb + 3) // 4].view(torch.uint8)[:n * nb]
-                xc.gin[s * C:s * C + n] = ff.decode(code, nb, row[2:4].view(torch.float32), n)
+                gin[s * C:s * C + n] = ff.decode(code, nb, row[2:4].view(torch.float32), n)
 
     def _x_flush(self):
-        """Apply the gradients of the last 1 + lag steps (keys-free exchanges, oldest
-        first), so the shards hold every push issued so far."""
+        """Apply the gradients that no issued exchange has carried yet (keys-free
+        exchanges, oldest first), so the shards hold every push issued so far.
+        Collective."""
         xc = self.xc
-        if self.gpu:  # exchange halves may still run on another stream
+        if self.gpu:  # exchange halves / async applies may still run on other streams
             torch.cuda.synchronize(self.device)
-        # exchange s carried grads(s - 1 - lag): pending = steps computed whose grads
-        # no issued exchange has carried yet, oldest first
-        T = self._xt
-        for s in range(max(0, self._xx - 1 - self.lag), T):
-            b = s % 2
-            send = xc.sends[b]
+        # exchange s carried grads(s - 1 - lag); steps computed whose grads no issued
+        # exchange has carried yet, oldest first
+        for s in self.sched.pending(self._xx, self._xt):
+            b = self.sched.ring(s)
+            send, recv = xc.sends[b], xc.recvs[b]
             if self.gpu:
                 hipops().xchg_clear_counts(send, xc.H, True, False)
             else:
                 for p in range(self.G):
                     send[p * xc.H] = 0
-            self.comm.all_to_all_fixed(send, xc.recv)
-            self._x_serve(push_par=b, resolve_par=None)
+            self.comm.all_to_all_fixed(send, recv)
+            self._x_apply(b, b)
             if self.gpu:
                 hipops().xchg_clear_counts(send, xc.H, False, True)
             else:
                 for p in range(self.G):
                     send[p * xc.H + 1] = 0
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
         ovf = int(xc.ovf.item())
         if ovf:
             raise RuntimeError(
                 f"padded exchange overflow: {ovf} keys exceeded the per-peer capacity "
                 f"{xc.C} (they were pulled as 0 and not pushed); set exchange_capacity "
                 f"or exchange_slack higher, or exchange='exact'")
+
 
     # ------------------------------------------------------- fused exchange (G > 1)
     def _bucket(self, loc, par: int = 0):
@@ -521,7 +636,7 @@ class SparseLRTrainer:
         One buffer set per step parity (the padded exchange reads perm / off again in
         the worker half of the step)."""
         n = loc.uniq.numel()
-        bks = getattr(self, "_bks", None) or [None, None]
+        bks = getattr(self, "_bks", None) or [None] * self.R
         self._bks = bks
         if bks[par] is None or bks[par][0].numel() < n:
             dev = loc.uniq.device

@@ -36,6 +36,18 @@ class CountMinSketch:
             core().cm_insert(ptr(self.cells), self.n, self.k, self.vmax, ptr(keys), ptr(counts),
                              keys.numel())
 
+    def insert_segments(self, keys: torch.Tensor, seg_start: torch.Tensor, n_dev=None):
+        """Insert unique keys with counts = their occurrence run lengths
+        ``seg_start[i+1] - seg_start[i]`` (saturated to a byte); ``n_dev``: device count
+        (no host sync: graph-capturable)."""
+        if is_gpu(keys):
+            hipops().cm_insert_seg(self.cells.view(torch.int32), self.k, self.vmax,
+                                   keys.contiguous(), seg_start.contiguous(), n_dev)
+            return
+        n = keys.numel() if n_dev is None else int(n_dev.reshape(-1)[0])
+        cnt = (seg_start[1:n + 1] - seg_start[:n]).clamp(max=255).to(torch.uint8)
+        self.insert(keys[:n], cnt)
+
     def query(self, keys: torch.Tensor, freq: int = 0, n_dev=None):
         """(keep int32 [n] = count > freq, count uint8 [n])."""
         keys = keys.contiguous()

@@ -68,7 +68,13 @@ class Localizer:
     outputs except the order of positions inside a key's segment. Measured 1045 us
     on the same batch (device-scope atomics and the cross-bucket look-back are
     latency bound, and power-law hot keys make a few buckets 40K elements long),
-    so it is an alternative, not the default."""
+    so it is an alternative, not the default.
+    ``mode="part"`` (csrc/hip/partloc.hip, GPU, key bits <= 32): one partition pass on
+    the top key bits, then one workgroup per bucket deduplicates its keys in an LDS
+    hash and sorts only the DISTINCT keys; same outputs as "sort" except the order of
+    positions inside a key's segment (5 launches instead of 16).
+    ``check()`` raises if a bucket overflowed its LDS hash (never for mixed keys of
+    realistic batches; the bucket count bounds the distinct keys per bucket)."""
 
     def __init__(self, max_nnz: int, bits: int, device="cpu", with_hess: bool = False,
                  mode: str = "sort"):
@@ -79,8 +85,10 @@ class Localizer:
         n = self.max_nnz
         dev = self.device
         self.gpu = dev.type == "cuda"
-        if mode not in ("sort", "hash", "bucket", "tile"):
+        if mode not in ("sort", "hash", "bucket", "tile", "part"):
             raise ValueError(f"unknown localisation mode {mode!r}")
+        if mode == "part" and not (self.gpu and hipops().partloc_supported(n, self.bits)):
+            mode = "sort"
         if mode in ("hash", "tile") and (with_hess or self.bits > 32):
             mode = "sort"
         if mode == "tile" and self.bits > 31:
@@ -102,6 +110,19 @@ class Localizer:
             self.t_psum = torch.empty(N, dtype=torch.float32, device=dev)
             self.hess = None
             self.digit_bits = 10 if 24 < self.bits <= 30 else 8
+            return
+        if self.gpu and self.mode == "part":
+            H = hipops()
+            i32 = lambda k: torch.empty(k, dtype=torch.int32, device=dev)  # noqa: E731
+            self.ptemp = torch.empty(H.partloc_temp_bytes(n, self.bits), dtype=torch.uint8,
+                                     device=dev)
+            self.pos_s, self.segid, self.local_col = i32(n), i32(n), i32(n)
+            self.seg_start = i32(n + 1)
+            self.uniq = torch.empty(n, dtype=torch.int64, device=dev)
+            self.n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.grad = torch.empty(n, dtype=torch.float32, device=dev)
+            self.hess = torch.empty(n, dtype=torch.float32, device=dev) if with_hess else None
+            self.err = torch.zeros(1, dtype=torch.int32, device=dev)
             return
         if self.gpu and self.mode == "bucket":
             H = hipops()
@@ -168,6 +189,11 @@ class Localizer:
             self.scan_temp = torch.empty(max(1, H.scan_temp_bytes(n)), dtype=torch.uint8,
                                          device=dev)
 
+    def check(self):
+        """Host sync: raise if a "part" localisation overflowed a bucket's LDS hash."""
+        if getattr(self, "err", None) is not None and self.mode == "part" and int(self.err.item()):
+            raise RuntimeError("localize_part: a bucket's distinct keys overflowed its LDS hash")
+
     def __call__(self, keys: torch.Tensor) -> Localized:
         n = keys.numel()
         if n > self.max_nnz:
@@ -188,6 +214,12 @@ class Localizer:
             tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum)
             return Localized(self.uniq, self.seg_start, self.pos_s, self.segid,
                              self.local_col[:n], self.n_uniq, self.grad, None, n, tile=tile)
+        if self.mode == "part":
+            H.localize_part(keys, self.bits, self.ptemp, self.pos_s, self.segid, self.uniq,
+                            self.seg_start, self.local_col, self.n_uniq, self.grad, self.hess,
+                            self.err)
+            return Localized(self.uniq, self.seg_start, self.pos_s[:n], self.segid[:n],
+                             self.local_col[:n], self.n_uniq, self.grad, self.hess, n)
         if self.mode == "bucket":
             H.localize_bucket(keys, self.bits, self.btemp, self.pos_s, self.segid, self.uniq,
                               self.seg_start, self.local_col, self.n_uniq, self.grad, self.hess)

@@ -79,10 +79,13 @@ class LoopbackComm(Comm):
 
     backend = "loopback"
 
-    def __init__(self, world: int, device="cpu", comm_stream: bool = True):
+    def __init__(self, world: int, device="cpu", comm_stream: bool = True, group=None):
         self.world = int(world)
         self.rank = 0
         self.device = torch.device(device)
+        # group: a real 1-rank process group (nccl = RCCL) that carries every exchange,
+        # so the emulation runs RCCL's kernels, streams and work-completion waits
+        self.group = group
         # model ProcessGroupNCCL's stream structure: the collective runs on the
         # communicator's own stream, ordered after the caller's stream and before
         # the caller's next work (so the emulation sees the same number of streams)
@@ -90,6 +93,9 @@ class LoopbackComm(Comm):
                     else None)
 
     def all_to_all_fixed(self, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
+        if self.group is not None:
+            dist.all_to_all_single(recv, send, group=self.group)
+            return recv
         if self._cs is None:
             recv.copy_(send)
             return recv
@@ -103,6 +109,32 @@ class LoopbackComm(Comm):
     def all_gather_counts(self, counts: torch.Tensor, to_host: bool = True) -> torch.Tensor:
         m = counts.reshape(1, -1).expand(self.world, -1)
         return m.cpu() if to_host else m
+
+    def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
+        if self.group is not None and t.is_cuda:
+            ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+            dist.all_reduce(t, op=ops[op], group=self.group)
+        return t
+
+    def barrier(self):
+        if self.group is not None:
+            dist.barrier(group=self.group, device_ids=[self.device.index or 0])
+
+
+def nccl_loopback(world: int, device) -> LoopbackComm:
+    """Emulated ``world``-rank exchange whose collectives run through a real 1-rank
+    RCCL communicator (rehearses the NCCL code path on a 1-GPU box: RCCL refuses two
+    ranks on one device)."""
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(device))
+    return LoopbackComm(world, device, comm_stream=False, group=dist.group.WORLD)
 
 
 class DistComm(Comm):

@@ -4,44 +4,29 @@ Reference: Darlin submits block t+1 with ``wait_time = t - tau`` and the
 per-customer Executor only admits a task whose dependencies are finished
 (src/app/linear_method/darlin.h:81-93, src/system/executor.cc:172-177); the
 async-SGD ``max_delay`` flag is declared but never read (linear.proto:47).
-Here one vector clock per shard records, for every worker, the last step whose
-push has been applied; a pull for step c may be served only when
-min_w clock[w] >= c - 1 - tau. GPU pipelines record a HIP event per applied
-push so a stream can wait on exactly the step it depends on.
+
+On the GPU data plane there are no per-message dependencies to check: every
+step is one collective exchange, so the schedule itself is the vector clock.
+``ExchangeSchedule`` fixes which step's pushes ride which exchange and which
+ring buffers a step uses: the pushes of step t ride exchange t+1+lag and the
+owner applies them before it resolves that exchange's pulls, so a pull of step
+t has seen exactly the pushes of steps <= t-1-lag of EVERY worker (the
+collective cannot start before all ranks have packed those gradients: the
+vector clock min_w clock[w] >= t-1-lag holds by construction). ASP decouples the
+owner's push apply from the pulls (its own stream, no event the pulls wait on);
+``EventClock`` holds the per-exchange HIP events of those applies, which gate
+only buffer reuse (``apply_gate``).
+
+``VectorClock`` is the host-side admissibility clock of the KVWorker/KVServer
+API (parameter/sharded_kv.py): a pull with timestamp t may be served once every
+worker's pushes through t-1-tau are applied.
 """
 from __future__ import annotations
 
+import math
 import threading
 
 INF = float("inf")
-
-
-class VectorClock:
-    def __init__(self, num_workers: int, tau: float = 0):
-        self.clock = [-1] * num_workers
-        self.tau = tau
-        self._cv = threading.Condition()
-
-    def tick(self, worker: int, step: int):
-        with self._cv:
-            if step > self.clock[worker]:
-                self.clock[worker] = step
-            self._cv.notify_all()
-
-    def min_clock(self) -> int:
-        return min(self.clock)
-
-    def admissible(self, step: int) -> bool:
-        """Can a pull for minibatch ``step`` be served now?"""
-        return self.tau == INF or self.min_clock() >= step - 1 - self.tau
-
-    def wait(self, step: int, timeout: float | None = None) -> bool:
-        with self._cv:
-            return self._cv.wait_for(lambda: self.admissible(step), timeout=timeout)
-
-    def staleness(self, step: int) -> int:
-        """How many of this worker's predecessors' pushes the pull may miss."""
-        return max(0, step - 1 - self.min_clock())
 
 
 def parse_consistency(mode: str | int | float) -> float:
@@ -58,24 +43,119 @@ def parse_consistency(mode: str | int | float) -> float:
     return float(m)
 
 
-class EventClock:
-    """Per-step HIP events of applied pushes (device-side vector clock)."""
+class ExchangeSchedule:
+    """Step -> exchange / buffer bookkeeping of the padded multi-GPU exchange.
 
-    def __init__(self):
+    ``lag``: pushes of step t ride exchange t+1+lag (bsp 0, ssp:tau tau unless a
+    smaller ``lag`` is asked for, asp 1). ``depth`` (asp only): exchanges whose push
+    applies may still be running when a later exchange resolves its pulls.
+    Buffers live in rings of ``R = max(2, lag + 1 + depth)`` entries indexed by step.
+    """
+
+    def __init__(self, tau: float, lag: int = -1, asp_depth: int = 4):
+        self.tau = float(tau)
+        self.asp = math.isinf(self.tau)
+        if self.asp:
+            self.lag = int(lag) if lag >= 0 else 1
+            self.depth = max(1, int(asp_depth))
+        else:
+            self.lag = int(lag) if lag >= 0 else int(self.tau)
+            self.depth = 0
+            if self.lag > self.tau:
+                raise ValueError(f"exchange_lag {self.lag} exceeds the staleness bound {self.tau}")
+        if self.lag < 0:
+            raise ValueError("exchange lag must be >= 0")
+        self.R = max(2, self.lag + 1 + self.depth)
+
+    def ring(self, t: int) -> int:
+        """Ring entry of step t's pull (resolved slots, weights, offsets) and of the
+        gradients step t computes."""
+        return t % self.R
+
+    def carried(self, t: int) -> int:
+        """Step whose pushes ride exchange t (negative: none yet)."""
+        return t - 1 - self.lag
+
+    def grad_ring(self, t: int) -> int:
+        """Ring entry holding the gradients exchange t carries (its send buffer)."""
+        return self.carried(t) % self.R
+
+    def visible_through(self, t: int) -> int:
+        """Every push of steps <= this is applied before the pull of step t (bsp/ssp);
+        asp: a lower bound only."""
+        return t - 1 - self.lag - self.depth
+
+    def apply_gate(self, t: int) -> int | None:
+        """asp: exchange whose (asynchronous) push apply must have finished before
+        exchange t starts (it frees the slot ring entry exchange t overwrites)."""
+        if not self.asp:
+            return None
+        g = t - self.depth
+        return g if g >= 0 else None
+
+    def pending(self, exchanged: int, computed: int) -> range:
+        """Steps computed whose gradients no issued exchange has carried yet."""
+        return range(max(0, exchanged - 1 - self.lag), computed)
+
+    def staleness_bounds(self) -> tuple[int, float]:
+        """(min, max) steps of pushes a pull may miss."""
+        return self.lag, (self.lag + self.depth if self.asp else self.lag)
+
+
+class EventClock:
+    """Per-exchange HIP events of applied pushes (device-side vector clock)."""
+
+    def __init__(self, size: int = 64):
+        self.size = int(size)
         self.events = {}
 
     def record(self, step: int, stream=None):
         import torch
 
-        ev = torch.cuda.Event()
+        ev = self.events.get(step % self.size)
+        if ev is None:
+            ev = torch.cuda.Event()
+            self.events[step % self.size] = ev
         ev.record(stream)
-        self.events[step] = ev
-        for s in [s for s in self.events if s < step - 64]:
-            del self.events[s]
+        return ev
 
-    def wait_for(self, step: int, stream=None):
-        ev = self.events.get(step)
+    def wait_for(self, step: int | None, stream=None):
+        """Make ``stream`` wait for the apply of exchange ``step`` (no-op if None or
+        never recorded)."""
+        if step is None:
+            return
+        ev = self.events.get(step % self.size)
         if ev is not None:
             import torch
 
             (stream or torch.cuda.current_stream()).wait_event(ev)
+
+
+class VectorClock:
+    """Host-side vector clock: clock[w] = last step whose push from worker w is applied."""
+
+    def __init__(self, num_workers: int, tau: float = 0):
+        self.clock = [-1] * num_workers
+        self.tau = tau
+        self._cv = threading.Condition()
+
+    def tick(self, worker: int, step: int):
+        with self._cv:
+            if step > self.clock[worker]:
+                self.clock[worker] = step
+            self._cv.notify_all()
+
+    def min_clock(self) -> int:
+        return min(self.clock)
+
+    def admissible(self, step: int) -> bool:
+        """Can a pull for timestamp ``step`` be served now?"""
+        return self.tau == INF or self.min_clock() >= step - 1 - self.tau
+
+    def wait(self, step: int, timeout: float | None = None) -> bool:
+        with self._cv:
+            return self._cv.wait_for(lambda: self.admissible(step), timeout=timeout)
+
+    def staleness(self, step: int) -> int:
+        """How many steps of pushes a pull at ``step`` may miss right now."""
+        return max(0, step - 1 - self.min_clock())

@@ -34,7 +34,7 @@ def _trainer(B, N, **kw):
     args.update(kw)
     cfg = SparseLRConfig(**args)
     tr = SparseLRTrainer(cfg, LoopbackComm(2, "cuda"), "cuda")
-    assert tr.padded and tr.lag == 1
+    assert tr.padded
     return tr
 
 
@@ -46,6 +46,8 @@ def _weights(tr):
 
 @pytest.mark.parametrize("xmode,nprep,graph,kw", [
     ("prep", 2, 1, {}), ("prep", 1, 1, {}), ("own", 2, 1, {}), ("prep", 3, 0, {}),
+    ("prep", 2, 1, {"consistency": "ssp:1"}), ("prep", 2, 1, {"consistency": "ssp:2"}),
+    ("prep", 3, 1, {"consistency": "bsp"}),
     ("prep", 2, 1, {"fixing_float_bytes": 2}), ("prep", 2, 1, {"push_mode": "aggregate"}),
     ("prep", 2, 1, {"algo": "adagrad"})])
 def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
@@ -60,11 +62,10 @@ def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     labels = torch.empty(B, dtype=torch.float32, device=dev)
     args = argparse.Namespace(warmup=0, graph=graph)
     it, _ = bench.pipeline(tr, B, N, seed, keys, labels, dev, args, nprep=nprep)
-    NB = 2 * nprep
-    T = NB + (NB if graph else 0) + extra
     for _ in range(extra):
         it()
     torch.cuda.synchronize()
+    T = tr._xt  # worker steps the pipeline ran
     tr._x_flush()  # pushes no issued exchange carried yet (none in prep mode, nprep >= 2)
     pk, pw = _weights(tr)
     loss_p = tr.progress()["loss"]
@@ -88,3 +89,26 @@ def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     extra_mask[pos] = False
     assert torch.all(pw[extra_mask] == 0)
     assert abs(loss_p - ref.progress()["loss"]) < 1e-4
+
+
+def test_asp_pipeline_trains(monkeypatch):
+    """asp: the owner's push applies replay on their own stream and pulls never wait
+    for them, so the result is timing dependent; it must still train every key and
+    stay within the ring (flush applies everything)."""
+    monkeypatch.setenv("PSAMD_XCHG_STREAM", "prep")
+    bench = _bench()
+    B, N, seed = 4096, 10 ** 6, 78
+    dev = torch.device("cuda")
+    tr = _trainer(B, N, consistency="asp")
+    assert tr.asp and tr.R == tr.lag + 1 + tr.async_depth
+    keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
+    labels = torch.empty(B, dtype=torch.float32, device=dev)
+    args = argparse.Namespace(warmup=0, graph=1)
+    it, used = bench.pipeline(tr, B, N, seed, keys, labels, dev, args, nprep=2)
+    assert used
+    for _ in range(12):
+        it()
+    torch.cuda.synchronize()
+    p = tr.progress()
+    assert 0.0 < p["loss"] < 0.7 and p["nnz_w"] > 0
+    tr.table.check_ok()

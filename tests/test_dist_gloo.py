@@ -40,6 +40,7 @@ def _worker(rank, world, port, out_dir, cfg_kw, steps):
 
 
 def _run(tmp_path, cfg_kw, steps=4, world=2):
+    tmp_path.mkdir(parents=True, exist_ok=True)
     port = _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path), cfg_kw, steps), nprocs=world, join=True)
     return [torch.load(tmp_path / f"r{r}.pt", weights_only=False) for r in range(world)]
@@ -156,20 +157,84 @@ def test_padded_exchange_overflow_is_loud(tmp_path):
         _run(tmp_path, cfg_kw, steps=2)
 
 
-@pytest.mark.parametrize("world,ff", [(2, 0), (3, 0), (2, 3)])
-def test_ssp_pipelined_exchange_matches_stale_reference(tmp_path, world, ff):
-    """consistency ssp:tau -> exchange_lag 1: pulls of step s see pushes through s-2."""
+@pytest.mark.parametrize("tau,world,ff", [(1, 2, 0), (2, 2, 0), (4, 2, 0), (1, 3, 0), (2, 3, 0),
+                                           (4, 3, 0), (4, 2, 3)])
+def test_ssp_exchange_matches_stale_reference(tmp_path, tau, world, ff):
+    """consistency ssp:tau -> the pull of step s sees exactly the pushes of steps
+    <= s-1-tau (ring of tau+1 exchange buffers)."""
+    steps = 7
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
-                  consistency="ssp:4", fixing_float_bytes=ff)
-    res = _run(tmp_path, cfg_kw, steps=5, world=world)
+                  consistency=f"ssp:{tau}", fixing_float_bytes=ff)
+    res = _run(tmp_path, cfg_kw, steps=steps, world=world)
     merged = {}
     for r in res:
         for k, w in zip(r["state"]["keys"].tolist(), r["state"]["w"].tolist()):
             merged[k] = w
-    ref = _reference(cfg_kw, 5, world, lag=1)
+    ref = _reference(cfg_kw, steps, world, lag=tau)
     assert merged.keys() == ref.keys()
     tol = 1e-5 if ff == 0 else 2e-3
     assert max(abs(merged[k] - ref[k]) for k in ref) < tol
-    if ff == 0:  # and it differs from the BSP result (the lag is real)
-        bsp = _reference(cfg_kw, 5, world, lag=0)
-        assert max(abs(merged[k] - bsp[k]) for k in ref) > 1e-4
+    if ff == 0:  # and it differs from the neighbouring staleness (the lag is real)
+        other = _reference(cfg_kw, steps, world, lag=tau - 1)
+        assert max(abs(merged[k] - other[k]) for k in ref) > 1e-4
+
+
+def test_explicit_smaller_lag_within_bound(tmp_path):
+    """exchange_lag < tau is a legal SSP(tau) schedule with staleness exactly lag."""
+    cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
+                  consistency="ssp:4", exchange_lag=1)
+    res = _run(tmp_path, cfg_kw, steps=5, world=2)
+    merged = {k: w for r in res for k, w in zip(r["state"]["keys"].tolist(),
+                                                 r["state"]["w"].tolist())}
+    ref = _reference(cfg_kw, 5, 2, lag=1)
+    assert max(abs(merged[k] - ref[k]) for k in ref) < 1e-5
+
+
+def test_asp_differs_from_ssp1(tmp_path):
+    """asp: the owner applies the pushes an exchange carries AFTER resolving its pulls
+    (on the GPU on its own stream, which pulls never wait for). Run in program order
+    (CPU) that is one more step of staleness than ssp:1."""
+    cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
+                  consistency="asp")
+    res = _run(tmp_path, cfg_kw, steps=6, world=2)
+    merged = {k: w for r in res for k, w in zip(r["state"]["keys"].tolist(),
+                                                 r["state"]["w"].tolist())}
+    ref = _reference(cfg_kw, 6, 2, lag=2)
+    assert max(abs(merged[k] - ref[k]) for k in ref) < 1e-5
+    ssp1 = _reference(cfg_kw, 6, 2, lag=1)
+    assert max(abs(merged[k] - ssp1[k]) for k in ref) > 1e-4
+
+
+def test_exchange_schedule_rings():
+    from parameter_server_amd.parallel.consistency import ExchangeSchedule
+
+    s = ExchangeSchedule(4)
+    assert (s.lag, s.R, s.asp) == (4, 5, False)
+    for t in range(20):  # the send buffer of exchange t holds grads(t-5), written by step t-5
+        assert s.grad_ring(t) == (t - 5) % 5 and s.visible_through(t) == t - 5
+    b = ExchangeSchedule(0)
+    assert (b.lag, b.R) == (0, 2) and b.visible_through(3) == 2
+    a = ExchangeSchedule(float("inf"), asp_depth=3)
+    assert a.asp and a.lag == 1 and a.R == 5 and a.apply_gate(7) == 4 and a.apply_gate(1) is None
+    assert list(a.pending(exchanged=10, computed=10)) == [8, 9]
+    with pytest.raises(ValueError):
+        ExchangeSchedule(2, lag=3)
+
+
+@pytest.mark.parametrize("world,ff", [(2, 0), (3, 0), (2, 2)])
+def test_tail_filter_padded_matches_exact(tmp_path, world, ff):
+    """tail_feature_freq on the sync-free padded exchange (device CountMin insert /
+    query + keep-mask compaction) trains the same weights as the host-synchronous
+    exact path (reference MinibatchReader::read, sgd.h:131-150)."""
+    base = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
+                tail_feature_freq=1, countmin_n=1 << 16, fixing_float_bytes=ff)
+    res_p = _run(tmp_path / "p", dict(base, exchange="padded"), steps=5, world=world)
+    res_e = _run(tmp_path / "e", dict(base, exchange="exact"), steps=5, world=world)
+    wp = {k: w for r in res_p for k, w in zip(r["state"]["keys"].tolist(), r["state"]["w"].tolist())}
+    we = {k: w for r in res_e for k, w in zip(r["state"]["keys"].tolist(), r["state"]["w"].tolist())}
+    assert wp.keys() == we.keys()
+    tol = 1e-5 if ff == 0 else 2e-3
+    assert max(abs(wp[k] - we[k]) for k in we) < tol
+    # the filter is live: fewer keys than without it
+    res_n = _run(tmp_path / "n", dict(base, tail_feature_freq=0), steps=5, world=world)
+    assert sum(r["state"]["keys"].numel() for r in res_n) > len(wp)
