@@ -92,33 +92,62 @@ class EmbeddingPS:
         the text model; src/app/factor_machine has no checkpoint at all.)"""
         if self.gpu:
             torch.cuda.synchronize(self.device)
+        self._xe_check()  # a dropped pull / push must not be written as a valid state
         st = self.shard.state()
         sd = {"keys": unmix(st.pop("mkeys"), self.bits).cpu()}
         sd.update({k: v.cpu() for k, v in st.items()})
         for name in self._dense_state:
             sd[name] = getattr(self, name).detach().cpu()
         sd.update(step=self.step_count, examples=int(self.examples), bits=self.bits,
-                  rank=self.rank, world=self.G, dim=self.cfg.embedding_dim)
+                  rank=self.rank, world=self.G, dim=self.cfg.embedding_dim,
+                  model=type(self).__name__, wide_rule=self._wide_rule_tag())
         return sd
+
+    _SHARD_KEYS = ("keys", "w", "z", "n", "rows", "acc", "cnt")
+
+    def _wide_rule_tag(self) -> str:
+        r = self.cfg.wide
+        return f"{r.algo}/{r.lr_type}"
 
     @staticmethod
     def merge_state_dicts(sds: list) -> dict:
         """Concatenate per-rank snapshots (key-disjoint shards; dense state and counters
         are replicated, taken from the first)."""
         out = dict(sds[0])
-        for k in ("keys", "w", "z", "n", "rows", "acc"):
-            out[k] = torch.cat([sd[k] for sd in sds])
+        for k in EmbeddingPS._SHARD_KEYS:
+            if k in out:
+                out[k] = torch.cat([sd[k] for sd in sds])
         return out
 
-    def load_state_dict(self, sd: dict) -> None:
-        """Load the keys this rank owns (any world size wrote ``sd``) and the dense state."""
+    def load_state_dict(self, sd: dict, chunk: int = 1 << 24) -> None:
+        """Load the keys this rank owns (any world size wrote ``sd``) and the dense state.
+
+        Ownership is decided on the host (mix + owner_of have CPU paths) and only the
+        owned slice travels to the device, ``chunk`` keys at a time: a merged snapshot of
+        a 1e9 x 128 table (~256 GB of rows) never has to fit on one GPU."""
         if int(sd["bits"]) != self.bits or int(sd["dim"]) != self.cfg.embedding_dim:
             raise ValueError(f"snapshot bits/dim {sd['bits']}/{sd['dim']} != "
                              f"{self.bits}/{self.cfg.embedding_dim}")
-        mk = mix(sd["keys"].to(self.device), self.bits)
-        own = self.part.owner_of(mk) == self.rank
-        self.shard.load_state(mk[own], *(sd[k].to(self.device)[own]
-                                         for k in ("w", "z", "n", "rows", "acc")))
+        model = sd.get("model")
+        if model is not None and str(model) != type(self).__name__:
+            raise ValueError(f"snapshot of a {model}, not a {type(self).__name__}")
+        rule = sd.get("wide_rule")
+        if rule is not None and str(rule) != self._wide_rule_tag():
+            raise ValueError(f"snapshot wide rule {rule} != {self._wide_rule_tag()}")
+        if rule is None or "cnt" not in sd:
+            if self.cfg.wide.algo.lower() in ("sgd", "standard") and \
+                    self.cfg.wide.lr_type.lower() == "decay":
+                raise ValueError("snapshot has no update counts; a decaying SGD wide rule "
+                                 "cannot resume from it")
+        keys = sd["keys"].cpu()
+        for a in range(0, keys.numel(), chunk):
+            mk = mix(keys[a:a + chunk].contiguous(), self.bits)
+            own = torch.nonzero(self.part.owner_of(mk) == self.rank).flatten()
+            if own.numel() == 0:
+                continue
+            vals = [sd[k][a:a + chunk][own].to(self.device) for k in ("w", "z", "n", "rows", "acc")]
+            cnt = sd["cnt"][a:a + chunk][own].to(self.device) if "cnt" in sd else None
+            self.shard.load_state(mk[own].to(self.device), *vals, cnt=cnt)
         for name in self._dense_state:
             getattr(self, name).copy_(sd[name].to(self.device))
         if "param" in self._dense_state:

@@ -39,14 +39,17 @@ class EmbeddingShard:
         accumulator (device tensors, one entry per key)."""
         mk, w, z, n = self.table.occupied()
         mask = self.table.slots[:, 0] != EMPTY_KEY
+        # cnt | flags word: the update count a decaying SGD wide rule reads
         return {"mkeys": mk, "w": w, "z": z, "n": n, "rows": self.rows[mask],
-                "acc": self.acc[mask]}
+                "acc": self.acc[mask], "cnt": self.table.slots[mask, 3]}
 
-    def load_state(self, mkeys, w, z, n, rows, acc) -> torch.Tensor:
+    def load_state(self, mkeys, w, z, n, rows, acc, cnt=None) -> torch.Tensor:
         """Insert keys with their saved state (rows are marked initialised)."""
         slot = self.table.load(mkeys, w, z, n)
         self.rows[slot] = rows.to(self.device, torch.bfloat16)
         self.acc[slot] = acc.to(self.device, torch.float32)
+        if cnt is not None:
+            self.table.slots[slot, 3] = cnt.to(self.device, torch.int64)
         self.inited[slot] = 1
         return slot
 

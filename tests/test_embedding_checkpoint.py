@@ -73,3 +73,57 @@ def test_two_rank_snapshot_reloads_into_one():
     assert torch.equal(ta["rows"], tb["rows"]) and torch.equal(ta["w"], tb["w"])
     with pytest.raises(ValueError):
         WideDeepTrainer(WideDeepConfig(**dict(WD_CFG, embedding_dim=16))).load_state_dict(sd)
+
+
+def _reload_worker(rank, world, port, snap, out_dir):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from parameter_server_amd.parallel.comm import init_from_env
+
+    comm, dev = init_from_env("cpu")
+    tr = FMTrainer(FMConfig(**FM_CFG), comm, dev)
+    tr.load_state_dict(load_snapshot(snap), chunk=97)  # several host chunks
+    torch.save(tr.state_dict(), os.path.join(out_dir, f"s{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_one_rank_snapshot_reloads_into_two_ranks(tmp_path):
+    """A 1-rank snapshot loaded by 2 gloo ranks: the shards are key-disjoint, together
+    hold every key, and carry the saved values (ownership decided on the host)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    a = FMTrainer(FMConfig(**FM_CFG))
+    for s in range(2):
+        a.step(*_batch(128, s))
+    snap = str(tmp_path / "one.safetensors")
+    save_snapshot(snap, a.state_dict())
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_reload_worker, args=(2, port, snap, str(tmp_path)), nprocs=2, join=True)
+    shards = [torch.load(tmp_path / f"s{r}.pt", weights_only=True) for r in range(2)]
+    k0, k1 = set(shards[0]["keys"].tolist()), set(shards[1]["keys"].tolist())
+    assert k0 and k1 and not (k0 & k1)
+    ta, _ = _table(a)
+    assert k0 | k1 == set(ta["keys"].tolist())
+    merged = FMTrainer.merge_state_dicts(shards)
+    o = torch.argsort(merged["keys"])
+    for k in ("w", "z", "n", "rows", "acc", "cnt"):
+        assert torch.equal(merged[k][o], a.state_dict()[k][torch.argsort(a.state_dict()["keys"])]), k
+
+
+def test_snapshot_refuses_other_model():
+    a = FMTrainer(FMConfig(**FM_CFG))
+    a.step(*_batch(128, 0))
+    sd = a.state_dict()
+    wd = WideDeepTrainer(WideDeepConfig(**dict(WD_CFG, embedding_dim=FM_CFG["embedding_dim"])))
+    with pytest.raises(ValueError, match="FMTrainer"):
+        wd.load_state_dict(sd)
