@@ -24,6 +24,16 @@ void kv_update_rows(void*, int64_t, const int64_t*, const float*, int64_t, const
 void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int, int64_t*, float*,
                      bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t,
                      hipStream_t);
+// kvapi.hip
+void kvv_pack_vals(const float*, int, const int32_t*, const int32_t*, const int32_t*, int64_t,
+                   int64_t, const int64_t*, int, int64_t, int, int64_t, int32_t*, hipStream_t);
+void kvv_serve(const int32_t*, int, int64_t, int64_t, const int64_t*, const float*, int64_t, int,
+               float*, hipStream_t);
+void kvv_apply(const int32_t*, int, int64_t, int64_t, int, const int64_t*, float*, int64_t, int, int,
+               hipStream_t);
+void kvv_unpack(const float*, int64_t, int, const int64_t*, int, const int32_t*, int64_t, float*,
+                hipStream_t);
+void kvv_single_off(const int32_t*, int64_t*, hipStream_t);
 // fm.hip
 void fm_fwd_bwd(const void*, const void*, const int64_t*, int64_t, int64_t, const float*, int64_t,
                 int, int, const int32_t*, const float*, int64_t, const float*, float*, void*,
@@ -464,6 +474,80 @@ PYBIND11_MODULE(_hipops, m) {
                           ptr<int32_t>(nxt), algo, lr_type, (float)alpha, (float)beta, (float)l1,
                           (float)l2, (float)grad_scale, (float)max_delta, st, stripes,
                           cur_stream());
+  });
+  // ---------------- k-value push / pull API (kvapi.hip) ----------------
+  // rows [hdr 4 | keys C*kw | values C*k f32] of H words (pull rows: no values)
+  m.def("kvv_pack_vals", [](Tensor vals, int64_t k, Tensor pos_s, Tensor seg_start, Tensor n_uniq,
+                            Tensor off, int64_t C, int kw, int64_t H, Tensor send) {
+    chk(vals, at::kFloat, "vals");
+    chk(pos_s, at::kInt, "pos_s");
+    chk(seg_start, at::kInt, "seg_start");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(off, at::kLong, "off");
+    chk(send, at::kInt, "send");
+    const int G = (int)off.numel() - 1;
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(k >= 1 && vals.numel() % k == 0, "vals must be [nnz, k]");
+    const int64_t nnz = vals.numel() / k;
+    check(pos_s.numel() >= nnz, "pos_s < nnz");
+    const int64_t u_cap = std::min<int64_t>(seg_start.numel() - 1, nnz);
+    check(u_cap >= 1, "seg_start too small");
+    check(kw == 1 || kw == 2, "kw must be 1 or 2");
+    check(C > 0 && H >= 4 + C * kw + C * k && H % 4 == 0, "bad push row geometry");
+    check(send.numel() == G * H, "send must be [G * H]");
+    psamd::kvv_pack_vals(ptr<float>(vals), (int)k, ptr<int32_t>(pos_s), ptr<int32_t>(seg_start),
+                         ptr<int32_t>(n_uniq), u_cap, nnz, ptr<int64_t>(off), G, C, kw, H,
+                         ptr<int32_t>(send), cur_stream());
+  });
+  m.def("kvv_serve", [](Tensor recv, int64_t H, int64_t C, Tensor slot, Tensor vals, Tensor rec) {
+    chk(recv, at::kInt, "recv");
+    chk(slot, at::kLong, "slot");
+    chk(vals, at::kFloat, "vals");
+    chk(rec, at::kFloat, "rec");
+    check(H > 4 && C > 0 && recv.numel() % H == 0, "bad exchange row geometry");
+    const int G = (int)(recv.numel() / H);
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(vals.dim() == 2, "vals must be [capacity, k]");
+    const int64_t k = vals.size(1);
+    check(slot.numel() >= G * C && rec.numel() >= G * C * k, "slot / rec < G*C(*k)");
+    psamd::kvv_serve(ptr<int32_t>(recv), G, H, C, ptr<int64_t>(slot), ptr<float>(vals),
+                     vals.size(0), (int)k, ptr<float>(rec), cur_stream());
+  });
+  m.def("kvv_apply", [](Tensor recv, int64_t H, int64_t C, int kw, Tensor slot, Tensor vals,
+                        int op) {
+    chk(recv, at::kInt, "recv");
+    chk(slot, at::kLong, "slot");
+    chk(vals, at::kFloat, "vals");
+    check(op == 0 || op == 1, "op: 0 = add, 1 = assign");
+    check(vals.dim() == 2, "vals must be [capacity, k]");
+    const int64_t k = vals.size(1);
+    check(kw == 1 || kw == 2, "kw must be 1 or 2");
+    check(C > 0 && H >= 4 + C * kw + C * k && recv.numel() % H == 0, "bad push row geometry");
+    const int G = (int)(recv.numel() / H);
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(slot.numel() >= G * C, "slot < G*C");
+    psamd::kvv_apply(ptr<int32_t>(recv), G, H, C, kw, ptr<int64_t>(slot), ptr<float>(vals),
+                     vals.size(0), (int)k, op, cur_stream());
+  });
+  m.def("kvv_unpack", [](Tensor rec, int64_t C, int64_t k, Tensor off, Tensor local_col,
+                         Tensor out) {
+    chk(rec, at::kFloat, "rec");
+    chk(off, at::kLong, "off");
+    chk(local_col, at::kInt, "local_col");
+    chk(out, at::kFloat, "out");
+    const int G = (int)off.numel() - 1;
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(k >= 1 && C > 0 && rec.numel() >= G * C * k, "rec < G*C*k");
+    const int64_t nnz = local_col.numel();
+    check(out.numel() >= nnz * k, "out < nnz*k");
+    psamd::kvv_unpack(ptr<float>(rec), C, (int)k, ptr<int64_t>(off), G, ptr<int32_t>(local_col),
+                      nnz, ptr<float>(out), cur_stream());
+  });
+  m.def("kvv_single_off", [](Tensor n_uniq, Tensor off) {
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(off, at::kLong, "off");
+    check(off.numel() == 2, "off must be [2]");
+    psamd::kvv_single_off(ptr<int32_t>(n_uniq), ptr<int64_t>(off), cur_stream());
   });
   m.def("xchg_publish", [](Tensor src, Tensor host_dst) {
     chk(src, at::kInt, "src");

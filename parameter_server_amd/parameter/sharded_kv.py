@@ -1,100 +1,177 @@
 """GPU key-value push/pull API: ``KVWorker`` / ``KVServer`` over RCCL (ps.h parity).
 
-Reference user API (src/ps.h, src/parameter/shared_parameter.h:17-40,
+Reference user API (src/ps.h:18-50, src/parameter/shared_parameter.h:17-40,
 kv_vector.h:45-100): ``ts = pull(keys)`` / ``ts = push(keys, vals)`` return a
-timestamp, ``wait(ts)`` blocks until the operation finished, values are merged
-key-ordered, servers own contiguous key ranges.
+timestamp without blocking, ``wait(ts)`` completes the operation, a key carries
+``k`` values (``KVVector<K, V>`` with ``k`` values per key), values are merged
+key-ordered on the servers, servers own contiguous key ranges, and a pull may be
+served before the pushes of the last ``tau`` steps are applied (bounded delay,
+src/app/linear_method/darlin.h:81-91, src/system/executor.cc:170-177).
 
 MI355X design (one process per GPU, every rank = worker + server shard):
-* keys are mixed by the bijective ``KeyMix`` and range-partitioned in the mixed
-  space (balanced shards for any key distribution); a request is deduplicated,
-  grouped by owner and moved with ONE ``all_to_all_v`` (RCCL over xGMI), the
-  owner resolves / updates its HBM table, and a second ``all_to_all_v`` returns
-  pulled values;
-* operations are SPMD: every rank issues the same sequence of push/pull calls
-  (possibly with empty key lists) — the RCCL analogue of the reference's
-  "every worker talks to every server" message rounds;
-* calls run on the worker's own HIP stream and return immediately; ``wait(ts)``
-  makes the caller's stream wait on the op's event (no host sync) and returns
-  the pulled values aligned with the request keys;
-* server-side push semantics: ``"add"`` (KVVector PLUS, kv_vector.h:70-75),
-  ``"assign"``, or an optimizer ``UpdateRule`` (SGD / AdaGrad / FTRL,
-  kv_store.h:47-57 + async_sgd.h:71-124).
+
+* a call's keys are localised on the device by the same kernels as the trainers
+  (``ops.localize``: mix -> radix sort -> run-length encode; sorted unique mixed
+  keys, CSC order and the per-occurrence unique id), split by owner range on the
+  device (``KeyPartition.split_sorted``) and packed into FIXED rows of C keys per
+  peer with the live count in the row header (``exchange.hip``); a push row also
+  carries the k values of every unique key, the duplicates of the call summed in
+  CSC order (``kvv_pack_vals``);
+* ONE equal-split all-to-all (RCCL over xGMI) moves the rows; the owner resolves all
+  G source rows in one launch (``kv_resolve_rows``: lookup-or-insert, InitRule for
+  new keys) and then serves (``kvv_serve``: gather the value rows) or merges
+  (``kvv_apply``: PLUS with float atomics over all rows in one launch, ASSIGN in
+  rank order; or one optimizer step per source row in rank order for an
+  ``UpdateRule`` on scalar values, ``kv_update_rows``); a pull's records come back
+  with a second all-to-all and ``kvv_unpack`` scatters them to request order;
+* nothing of a call is read back on the host: C is fixed per worker (``max_keys``,
+  the most keys one call may carry, so a peer's row can never overflow), the whole
+  op runs on the worker's own HIP stream and ``push`` / ``pull`` return at once;
+  ``wait(ts)`` orders the caller's stream after the op (no host sync);
+* operations are SPMD: every rank issues the same sequence of push / pull calls
+  (possibly with different or empty key lists) — the RCCL analogue of the
+  reference's "every worker messages every server" rounds.
+
+Consistency (``consistency=`` ``"bsp"`` | ``"ssp:tau"`` | ``"asp"``): the owner keeps
+the received push rows of the last ``tau`` pushes pending and applies a push only
+when ``tau`` newer pushes have arrived, so a pull issued after the P-th push sees
+exactly the pushes 1 .. P - tau of every worker (``parallel.consistency.VectorClock``
+gates every pull: ``admissible(P)`` must hold). ``bsp`` is tau = 0. ``asp`` applies
+each push on a separate apply stream as soon as it arrives and no pull waits for it
+(a pull sees whatever has landed). ``flush()`` applies everything pending.
+
+Server-side push semantics: ``"add"`` (KVVector PLUS, kv_vector.h:70-75),
+``"assign"``, or an optimizer ``UpdateRule`` (SGD / AdaGrad / FTRL, scalar values,
+kv_store.h:47-57 + async_sgd.h:71-124).
 """
 from __future__ import annotations
 
+import math
+from collections import deque
+
 import torch
 
-from ..ops.keymix import mix, unmix
-from ..ops.kv_table import InitRule, KVTable, UpdateRule
+from ..ops.keymix import unmix
+from ..ops.kv_table import EMPTY_KEY, InitRule, KVTable, UpdateRule
+from ..ops.localize import Localizer, localize_torch
+from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
+from ..parallel.consistency import INF, VectorClock, parse_consistency
 from ..parallel.partition import KeyPartition
 
-ADD = UpdateRule("sgd", "constant", alpha=1.0)  # applied to -v: w -= 1 * (-v)  ==  w += v
+ADD, ASSIGN = 0, 1
 
 
 class KVServer:
-    """One rank's shard of a scalar-valued table in HBM."""
+    """One rank's shard: the KV table (key index; scalar value + optimizer state in
+    its slots) and, for ``add`` / ``assign``, a ``[capacity, k]`` fp32 value block at
+    the slot index (the layout of the embedding shards)."""
 
-    def __init__(self, capacity: int, device, rule="add", init: InitRule | None = None):
-        self.table = KVTable(capacity, device, init)
+    def __init__(self, capacity: int, device, rule="add", init: InitRule | None = None,
+                 dim: int = 1, key_range=None):
+        self.table = KVTable(capacity, device, init, key_range=key_range)
         self.rule = rule
-        self.stats = torch.zeros(3, dtype=torch.float64, device=device)
+        self.dim = int(dim)
+        self.device = torch.device(device)
+        self.stats = torch.zeros(3, dtype=torch.float64, device=self.device)
+        self.vals = None
+        if not isinstance(rule, UpdateRule):
+            if rule not in ("add", "assign"):
+                raise ValueError(f"rule must be 'add', 'assign' or an UpdateRule, not {rule!r}")
+            if init is not None and init.type.lower() != "zero":
+                raise ValueError("add / assign values start at zero (KVVector semantics); "
+                                 "InitRule needs an UpdateRule")
+            self.vals = torch.zeros(self.table.capacity, self.dim, dtype=torch.float32,
+                                    device=self.device)
+        elif self.dim != 1:
+            raise ValueError("an optimizer UpdateRule updates scalar values (dim = 1)")
 
-    def get(self, mkeys: torch.Tensor) -> torch.Tensor:
-        _, w = self.table.resolve(mkeys, insert=True)
-        return w
-
-    def put(self, mkeys: torch.Tensor, vals: torch.Tensor):
-        slot, _ = self.table.resolve(mkeys, insert=True, with_w=False)
-        if self.rule == "assign":
-            self.table.set(slot, vals.float().contiguous())
-            return
-        if self.rule == "add":
-            self.table.update(slot, (-vals.float()).contiguous(), ADD, self.stats)
-            return
-        self.table.update(slot, vals.float().contiguous(), self.rule, self.stats)
+    @property
+    def op(self) -> int | None:
+        return None if isinstance(self.rule, UpdateRule) else (ADD if self.rule == "add" else ASSIGN)
 
     def dump(self):
-        """(raw uint64-as-int64 keys, values) of this shard."""
-        k, w, _, _ = self.table.occupied()
-        return k, w
+        """(mixed keys, values [n, dim]) of this shard."""
+        keys = self.table.slots[:, 0]
+        mask = keys != EMPTY_KEY
+        if self.vals is None:
+            k, w, _, _ = self.table.occupied()
+            return k, w.reshape(-1, 1)
+        return keys[mask], self.vals[mask]
 
 
 class KVWorker:
     """``pull`` / ``push`` / ``wait`` against all shards (this rank's server included)."""
 
     def __init__(self, comm: Comm | None = None, device="cpu", *, capacity: int = 1 << 20,
-                 rule="add", key_bits: int = 64, init: InitRule | None = None):
+                 rule="add", key_bits: int = 64, init: InitRule | None = None, dim: int = 1,
+                 max_keys: int = 1 << 20, consistency="bsp"):
         self.device = torch.device(device)
         self.comm = comm or LocalComm(self.device)
         self.G, self.rank = self.comm.world, self.comm.rank
-        self.bits = key_bits
-        self.part = KeyPartition(key_bits, self.G)
-        self.server = KVServer(capacity, self.device, rule, init)
+        self.bits = int(key_bits)
+        self.dim = k = int(dim)
+        self.part = KeyPartition(self.bits, self.G)
+        self.server = KVServer(capacity, self.device, rule, init, k)
         self.gpu = self.device.type == "cuda"
-        self.stream = torch.cuda.Stream(self.device) if self.gpu else None
+        self.tau = parse_consistency(consistency)
+        self.asp = math.isinf(self.tau)
+        self.consistency = "asp" if self.asp else ("bsp" if self.tau == 0 else f"ssp:{int(self.tau)}")
+        self.clock = VectorClock(self.G, self.tau)
+        # fixed exchange geometry: C keys per peer row = the most keys one call carries
+        self.max_keys = int(max_keys)
+        C = (self.max_keys + 7) // 8 * 8
+        kw = 1 if self.bits <= 32 else 2
+        self.C, self.kw = C, kw
+        self.Hk = (4 + C * kw + 1 + 3) // 4 * 4          # pull rows: header + keys
+        self.Hp = (4 + C * kw + C * k + 3) // 4 * 4       # push rows: + k values per key
         self._ts = 0
+        self._pushes = 0          # pushes issued (the worker's step clock)
         self._done: dict[int, tuple] = {}
+        self._pending: deque = deque()  # (push index, received rows) not yet applied
+        G, dev = self.G, self.device
+        if self.gpu:
+            self.stream = torch.cuda.Stream(self.device)
+            self.apply_stream = torch.cuda.Stream(self.device) if self.asp else None
+            self.loc = Localizer(self.max_keys, self.bits, dev)
+            i32 = dict(dtype=torch.int32, device=dev)
+            self.send_k, self.recv_k = torch.zeros(G * self.Hk, **i32), torch.zeros(G * self.Hk, **i32)
+            self.send_p = torch.zeros(G * self.Hp, **i32)
+            self.slot = torch.empty(G * C, dtype=torch.int64, device=dev)
+            self.w = torch.empty(G * C, dtype=torch.float32, device=dev)
+            self.rec_s = torch.empty(G * C * k, dtype=torch.float32, device=dev)
+            self.rec_r = torch.empty(G * C * k, dtype=torch.float32, device=dev)
+            self.off1 = torch.zeros(2, dtype=torch.int64, device=dev)
+            # apply-side scratch (the apply stream's own under asp)
+            self.a_slot = torch.empty(G * C, dtype=torch.int64, device=dev)
+            self.a_w = torch.empty(G * C, dtype=torch.float32, device=dev)
+            if self.server.op is None:
+                from ..ops.kv_table import next_pow2
+
+                self.link = torch.empty(next_pow2(2 * G * C), dtype=torch.int64, device=dev)
+                self.nxt = torch.empty(G * C, dtype=torch.int32, device=dev)
+        else:
+            self.stream = self.apply_stream = None
 
     # ------------------------------------------------------------- helpers
-    def _dedup(self, keys: torch.Tensor):
-        mk = mix(keys.to(self.device, torch.int64).contiguous(), self.bits)
-        # sorted unique in the signed order of the mixed keys (owner ranges are
-        # contiguous in it: KeyPartition bounds are monotone in int64 order)
-        uniq, inv = torch.unique(mk, sorted=True, return_inverse=True)
-        return uniq, inv
+    def _keys(self, keys: torch.Tensor) -> torch.Tensor:
+        keys = keys.to(self.device, torch.int64).reshape(-1).contiguous()
+        if keys.numel() > self.max_keys:
+            raise ValueError(f"{keys.numel()} keys in one call > max_keys {self.max_keys}")
+        return keys
 
-    def _route(self, uniq: torch.Tensor):
-        owner = self.part.owner_of(uniq)
-        send = torch.bincount(owner, minlength=self.G).to(torch.int64)
-        order = torch.argsort(owner, stable=True)
-        return order, send
+    def _localize(self, keys):
+        if keys.numel() == 0:
+            return None
+        return self.loc(keys) if self.gpu else localize_torch(keys, self.bits)
 
-    def _exchange(self, x: torch.Tensor, send, recv):
+    def _offsets(self, loc):
         if self.G == 1:
-            return x
-        return self.comm.all_to_all_v(x.contiguous(), send.tolist(), recv.tolist())
+            if self.gpu:
+                hipops().kvv_single_off(loc.n_uniq, self.off1)
+                return self.off1
+            return torch.tensor([0, loc.uniq.numel()], dtype=torch.int64)
+        return self.part.split_sorted(loc.uniq, loc.n_uniq)
 
     def _run(self, fn):
         self._ts += 1
@@ -110,54 +187,223 @@ class KVWorker:
             self._done[ts] = (fn(), None)
         return ts
 
+    # ------------------------------------------------- row packing (CPU path)
+    def _cpu_pack_keys(self, loc, off, H, send):
+        send.zero_()
+        if loc is None:
+            return
+        for p in range(self.G):
+            a, b = int(off[p]), int(off[p + 1])
+            base = p * H
+            send[base] = b - a
+            ks = loc.uniq[a:b]
+            if self.kw == 2:
+                send[base + 4:base + 4 + 2 * (b - a)] = ks.contiguous().view(torch.int32)
+            else:
+                send[base + 4:base + 4 + (b - a)] = (ks & 0xFFFFFFFF).to(torch.int32)
+
+    def _cpu_row_keys(self, recv, s, H):
+        base = s * H
+        n = int(recv[base])
+        if self.kw == 2:
+            return recv[base + 4:base + 4 + 2 * n].contiguous().view(torch.int64)
+        return recv[base + 4:base + 4 + n].to(torch.int64) & 0xFFFFFFFF
+
+    def _row_vals(self, buf, s, H, n=None):
+        """Float view of source row s's value region ([C, k])."""
+        C, k = self.C, self.dim
+        v = buf.view(torch.float32)[s * H + 4 + C * self.kw:s * H + 4 + C * self.kw + C * k]
+        v = v.view(C, k)
+        return v if n is None else v[:n]
+
     # ----------------------------------------------------------------- API
     def pull(self, keys: torch.Tensor) -> int:
-        """Values of ``keys`` (any order, duplicates allowed) -> timestamp."""
+        """Values of ``keys`` (any order, duplicates allowed) -> timestamp; ``wait``
+        returns ``[n]`` (dim 1) or ``[n, dim]`` float32 values in request order."""
+        keys = self._keys(keys)
+        # after P pushes (indices 0 .. P-1) the pull is step P: it must see pushes
+        # 0 .. P-1-tau of every worker
+        if not self.clock.admissible(self._pushes):
+            raise AssertionError("pull admitted before the pushes it must see were applied")
 
         def op():
-            uniq, inv = self._dedup(keys)
-            order, send = self._route(uniq)
-            req = uniq[order]
-            recv = self.comm.exchange_counts(send).cpu() if self.G > 1 else send.cpu()
-            rk = self._exchange(req, send.cpu(), recv)
-            vals = self.server.get(rk)
-            back = self._exchange(vals, recv, send.cpu())
-            by_uniq = torch.empty_like(back)
-            by_uniq[order] = back
-            return by_uniq[inv]
+            return self._pull(keys)
 
         return self._run(op)
+
+    def _pull(self, keys):
+        k, C, H, G = self.dim, self.C, self.Hk, self.G
+        n = keys.numel()
+        loc = self._localize(keys)
+        out = torch.zeros(n, k, dtype=torch.float32, device=self.device)
+        srv, tb = self.server, self.server.table
+        if self.gpu:
+            hh = hipops()
+            if loc is None:
+                hh.xchg_clear_counts(self.send_k, G, H, True, True)
+            else:
+                off = self._offsets(loc)
+                hh.xchg_pack_keys(loc.uniq, loc.n_uniq, off, C, self.kw, H, self.send_k, None)
+            self.comm.all_to_all_fixed(self.send_k, self.recv_k)
+            it, iv, isd, seed = tb.init.args()
+            hh.kv_resolve_rows(tb.slots, self.recv_k, H, C, self.kw, self.slot, self.w, True, it,
+                               iv, isd, seed, tb._err, tb._inserted, tb.home_base, tb.home_m)
+            if srv.vals is None:
+                rec = self.w
+            else:
+                hh.kvv_serve(self.recv_k, H, C, self.slot, srv.vals, self.rec_s)
+                rec = self.rec_s
+            self.comm.all_to_all_fixed(rec, self.rec_r)
+            if loc is not None:
+                hh.kvv_unpack(self.rec_r, C, k, off, loc.local_col, out)
+        else:
+            off = self._offsets(loc) if loc is not None else None
+            send, recv = torch.zeros(G * H, dtype=torch.int32), torch.empty(G * H, dtype=torch.int32)
+            self._cpu_pack_keys(loc, off, H, send)
+            self.comm.all_to_all_fixed(send, recv)
+            rec_s = torch.zeros(G * C * k, dtype=torch.float32)
+            for s in range(G):
+                rk = self._cpu_row_keys(recv, s, H)
+                if rk.numel() == 0:
+                    continue
+                slot, w = tb.resolve(rk, insert=True)
+                vals = w.reshape(-1, 1) if srv.vals is None else srv.vals[slot]
+                rec_s[s * C * k:(s * C + rk.numel()) * k] = vals.reshape(-1)
+            rec_r = torch.empty_like(rec_s)
+            self.comm.all_to_all_fixed(rec_s, rec_r)
+            if loc is not None:
+                u = loc.local_col.to(torch.int64)
+                p = torch.searchsorted(off[1:], u, right=True)
+                out = rec_r.view(G * C, k)[p * C + (u - off[p])]
+        return out.reshape(-1) if k == 1 else out
 
     def push(self, keys: torch.Tensor, vals: torch.Tensor) -> int:
-        """Send ``vals`` for ``keys``; duplicates are summed before the server op."""
+        """Send ``vals`` (``[n]`` or ``[n, dim]``) for ``keys``; duplicates are summed
+        before the server op. Returns the timestamp."""
+        keys = self._keys(keys)
+        vals = vals.to(self.device, torch.float32).reshape(keys.numel(), self.dim).contiguous()
+        p = self._pushes  # 0-based push index (the worker's step clock)
+        self._pushes += 1
 
         def op():
-            uniq, inv = self._dedup(keys)
-            v = torch.zeros(uniq.numel(), dtype=torch.float32, device=self.device)
-            v.index_add_(0, inv, vals.to(self.device, torch.float32).reshape(-1))
-            order, send = self._route(uniq)
-            recv = self.comm.exchange_counts(send).cpu() if self.G > 1 else send.cpu()
-            rk = self._exchange(uniq[order], send.cpu(), recv)
-            rv = self._exchange(v[order], send.cpu(), recv)
-            self.server.put(rk, rv)
-            return None
+            return self._push(keys, vals, p)
 
         return self._run(op)
 
+    def _push(self, keys, vals, p):
+        k, C, H, G = self.dim, self.C, self.Hp, self.G
+        loc = self._localize(keys)
+        if self.gpu:
+            hh = hipops()
+            if loc is None:
+                hh.xchg_clear_counts(self.send_p, G, H, True, True)
+            else:
+                off = self._offsets(loc)
+                hh.xchg_pack_keys(loc.uniq, loc.n_uniq, off, C, self.kw, H, self.send_p, None)
+                hh.kvv_pack_vals(vals, k, loc.pos_s, loc.seg_start, loc.n_uniq, off, C, self.kw, H,
+                                 self.send_p)
+            recv = torch.empty(G * H, dtype=torch.int32, device=self.device)
+            self.comm.all_to_all_fixed(self.send_p, recv)
+        else:
+            off = self._offsets(loc) if loc is not None else None
+            send, recv = torch.zeros(G * H, dtype=torch.int32), torch.empty(G * H, dtype=torch.int32)
+            self._cpu_pack_keys(loc, off, H, send)
+            if loc is not None:
+                # duplicates summed in CSC order (the kernel's order)
+                u = torch.zeros(loc.uniq.numel(), k, dtype=torch.float32)
+                u.index_add_(0, loc.local_col.to(torch.int64), vals)
+                for q in range(G):
+                    a, b = int(off[q]), int(off[q + 1])
+                    self._row_vals(send, q, H)[:b - a] = u[a:b]
+            self.comm.all_to_all_fixed(send, recv)
+        self._pending.append((p, recv))
+        self._drain(keep=0 if self.asp else int(self.tau))
+        # the vector clock is the gate: every worker's pushes through P - tau applied
+        assert self.asp or self.clock.min_clock() >= p - int(self.tau)
+        return None
+
+    def _drain(self, keep: int):
+        """Apply pending pushes until at most ``keep`` remain (oldest first); every
+        applied push advances every worker's vector clock (SPMD: push p of all workers
+        rides the same exchange)."""
+        while len(self._pending) > keep:
+            p, recv = self._pending.popleft()
+            if self.apply_stream is not None:
+                cur = torch.cuda.current_stream(self.device)
+                self.apply_stream.wait_stream(cur)
+                recv.record_stream(self.apply_stream)
+                with torch.cuda.stream(self.apply_stream):
+                    self._apply(recv)
+            else:
+                self._apply(recv)
+            for w in range(self.G):
+                self.clock.tick(w, p)
+
+    def _apply(self, recv):
+        srv, tb = self.server, self.server.table
+        C, H, G = self.C, self.Hp, self.G
+        if self.gpu:
+            hh = hipops()
+            it, iv, isd, seed = tb.init.args()
+            hh.kv_resolve_rows(tb.slots, recv, H, C, self.kw, self.a_slot, self.a_w, True, it, iv,
+                               isd, seed, tb._err, tb._inserted, tb.home_base, tb.home_m)
+            if srv.op is None:
+                grad = recv.view(torch.float32)[4 + C * self.kw:]
+                hh.kv_update_rows(tb.slots, self.a_slot, grad, H, recv, H, C, self.link, self.nxt,
+                                  *srv.rule.args(), srv.stats)
+            else:
+                hh.kvv_apply(recv, H, C, self.kw, self.a_slot, srv.vals, srv.op)
+            return
+        for s in range(G):  # source rows in rank order
+            rk = self._cpu_row_keys(recv, s, H)
+            if rk.numel() == 0:
+                continue
+            v = self._row_vals(recv, s, H, rk.numel())
+            slot, _ = tb.resolve(rk, insert=True, with_w=False)
+            if srv.op is None:
+                tb.update(slot, v[:, 0].contiguous(), srv.rule, srv.stats)
+                continue
+            ok = ~torch.isnan(v)
+            if srv.op == ADD:
+                srv.vals[slot] += torch.where(ok, v, torch.zeros_like(v))
+            else:
+                srv.vals[slot] = torch.where(ok, v, srv.vals[slot])
+
     def wait(self, ts: int):
-        """Block the caller's stream until op ``ts`` finished; pulled values or None."""
+        """Order the caller's stream after op ``ts``; pulled values (or None)."""
         out, ev = self._done.pop(ts)
         if ev is not None:
             torch.cuda.current_stream(self.device).wait_event(ev)
         return out
 
+    def flush(self):
+        """Apply every pending push (end of a training phase)."""
+        def op():
+            self._drain(keep=0)
+
+        return self.wait(self._run(op))
+
     def barrier(self):
         if self.gpu:
-            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_stream(self.stream)
+            if self.apply_stream is not None:
+                cur.wait_stream(self.apply_stream)
         self.comm.barrier()
+
+    def staleness(self) -> int:
+        """Pushes a pull issued now would miss (0 for bsp, <= tau for ssp)."""
+        return self.clock.staleness(self._pushes)
 
     # ---------------------------------------------------------- inspection
     def shard_items(self):
-        """(raw keys, values) held by this rank's server shard."""
-        mk, w = self.server.dump()
-        return unmix(mk, self.bits), w
+        """(raw keys, values) held by this rank's server shard (values ``[n]`` for dim 1)."""
+        if self.gpu:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+            if self.apply_stream is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self.apply_stream)
+        mk, v = self.server.dump()
+        return unmix(mk, self.bits), (v.reshape(-1) if self.dim == 1 else v)
+
+
+__all__ = ["KVWorker", "KVServer", "INF"]

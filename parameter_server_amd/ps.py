@@ -11,8 +11,10 @@ worker main on workers, and shuts the node down.
 Helpers: ``my_app``, ``my_node``, ``my_node_id``, ``is_worker/is_server/is_scheduler``,
 ``my_rank``, ``rank_size``.
 
-For GPU jobs (one process per GPU, RCCL data plane) use ``ShardedKV`` /
-``models.SparseLRTrainer`` instead; see README.
+For GPU jobs (one process per GPU, RCCL data plane) use
+``parameter.sharded_kv.KVWorker`` (push / pull / wait of k values per key with
+BSP / SSP / ASP; demo ``app/hello_world_gpu.py``) or the trainers in ``models``
+(``SparseLRTrainer``, ``DarlinTrainer``, ``WideDeepTrainer``, ``FMTrainer``); see README.
 """
 from __future__ import annotations
 

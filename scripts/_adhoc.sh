@@ -1,3 +1,3 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-TESTS="tests/test_partloc_gpu.py tests/test_bench_pipeline_gpu.py" BENCHES="e8 1 --localize=part" bash scripts/gpu_quick.sh || exit 1
-timeout -k 10 200 python bench.py --emulate-peers 8 --localize part --steps 50 --warmup 10 > gpurun_out/e8_part.log 2>&1; echo e8part rc=$?; grep -o '"ms_per_step": [0-9.]*' gpurun_out/e8_part.log
+TESTS="tests/test_sharded_kv.py tests/test_embedding_checkpoint.py" BENCHES="1 e8 --localize=part e8asp" bash scripts/gpu_quick.sh || exit 1
+timeout -k 10 100 python -m parameter_server_amd.app.hello_world_gpu > gpurun_out/hello_gpu.log 2>&1; echo hello rc=$?; tail -6 gpurun_out/hello_gpu.log

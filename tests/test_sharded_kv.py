@@ -1,4 +1,8 @@
-"""KVWorker / KVServer push-pull API (ps.h parity) on one rank and over gloo."""
+"""KVWorker / KVServer push-pull API (ps.h parity) on one rank and over gloo:
+k values per key, non-blocking timestamps, bounded-delay consistency (BSP / SSP(tau) /
+ASP) checked against a protocol simulation of the reference's semantics
+(src/parameter/kv_vector.h:45-100, src/app/linear_method/darlin.h:81-91)."""
+import os
 import socket
 
 import numpy as np
@@ -11,21 +15,69 @@ from parameter_server_amd.parameter.sharded_kv import KVWorker
 
 
 def test_single_rank_add_assign_and_optimizer():
-    kv = KVWorker(device="cpu", capacity=1 << 12)
+    kv = KVWorker(device="cpu", capacity=1 << 12, max_keys=64)
     keys = torch.tensor([5, 1, 5, -(1 << 63) + 7, 42], dtype=torch.int64)
     kv.wait(kv.push(keys, torch.tensor([1.0, 2.0, 3.0, 4.0, 5.0])))
     out = kv.wait(kv.pull(torch.tensor([5, 42, 1, 999, -(1 << 63) + 7], dtype=torch.int64)))
     assert out.tolist() == [4.0, 5.0, 2.0, 0.0, 4.0]  # duplicates summed, unknown -> 0
-    kv2 = KVWorker(device="cpu", capacity=1 << 10, rule="assign")
+    kv2 = KVWorker(device="cpu", capacity=1 << 10, rule="assign", max_keys=64)
     kv2.wait(kv2.push(torch.tensor([3, 4]), torch.tensor([7.0, 8.0])))
     kv2.wait(kv2.push(torch.tensor([3]), torch.tensor([1.5])))
     assert kv2.wait(kv2.pull(torch.tensor([4, 3]))).tolist() == [8.0, 1.5]
-    kv3 = KVWorker(device="cpu", rule=UpdateRule("sgd", "constant", alpha=0.5))
+    kv3 = KVWorker(device="cpu", rule=UpdateRule("sgd", "constant", alpha=0.5), max_keys=64)
     kv3.wait(kv3.push(torch.tensor([9]), torch.tensor([2.0])))
     assert kv3.wait(kv3.pull(torch.tensor([9]))).tolist() == [-1.0]
     k, v = kv.shard_items()
     # pull inserts unknown keys (KVStore::getValue uses map operator[], kv_store.h:37-45)
     assert sorted(k.tolist()) == sorted([5, 1, 42, 999, -(1 << 63) + 7])
+
+
+def test_single_rank_vector_values_and_nan_skip():
+    kv = KVWorker(device="cpu", capacity=1 << 10, dim=4, max_keys=64)
+    keys = torch.tensor([3, 8, 3])
+    v = torch.arange(12, dtype=torch.float32).reshape(3, 4)
+    t1 = kv.push(keys, v)
+    t2 = kv.pull(torch.tensor([8, 3, 77]))
+    got = kv.wait(t2)   # waited out of order: the pull is still after the push
+    kv.wait(t1)
+    assert got.shape == (3, 4)
+    assert got[0].tolist() == v[1].tolist()
+    assert got[1].tolist() == (v[0] + v[2]).tolist()
+    assert got[2].tolist() == [0.0] * 4
+    nan = torch.full((1, 4), float("nan"))
+    kv.wait(kv.push(torch.tensor([8]), nan))  # SparseFilter mark: no value
+    assert kv.wait(kv.pull(torch.tensor([8])))[0].tolist() == v[1].tolist()
+    with pytest.raises(ValueError):
+        kv.push(torch.arange(65), torch.zeros(65, 4))
+
+
+@pytest.mark.parametrize("tau", [0, 1, 2])
+def test_single_rank_ssp_delays_pushes_by_tau(tau):
+    kv = KVWorker(device="cpu", capacity=1 << 10, max_keys=16, consistency=f"ssp:{tau}"
+                  if tau else "bsp")
+    key = torch.tensor([11])
+    seen = []
+    for i in range(1, 6):
+        kv.wait(kv.push(key, torch.tensor([float(i)])))
+        seen.append(kv.wait(kv.pull(key)).item())
+        assert kv.staleness() == min(i, tau)
+    exp = [sum(range(1, max(0, p - tau) + 1)) for p in range(1, 6)]
+    assert seen == exp
+    kv.flush()
+    assert kv.wait(kv.pull(key)).item() == 15.0
+
+
+# ------------------------------------------------------------------ multi-rank
+OPS = ["push", "pull", "push", "push", "pull", "push", "pull", "pull", "push", "pull"]
+NK, K = 400, 4
+
+
+def _batch(rank, i, dim):
+    rng = np.random.default_rng(1000 * rank + i)
+    n = int(rng.integers(0, 160))  # some calls carry few keys
+    keys = rng.integers(0, NK, n)
+    vals = rng.normal(0, 1, (n, dim)).astype(np.float32)
+    return keys, vals
 
 
 def _port():
@@ -36,58 +88,140 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, out_dir, consistency, dim, device):
     import torch.distributed as dist
 
     from parameter_server_amd.parallel.comm import DistComm
 
+    torch.set_num_threads(1)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
-    kv = KVWorker(DistComm("cpu"), "cpu", capacity=1 << 14)
-    rng = np.random.default_rng(rank)
-    keys = torch.from_numpy(rng.integers(0, 500, 300)).to(torch.int64)
-    vals = torch.from_numpy(rng.normal(0, 1, 300)).float()
-    t = kv.push(keys, vals)
-    kv.wait(t)
+    dev = torch.device(device)
+    kv = KVWorker(DistComm(dev), dev, capacity=1 << 12, dim=dim, max_keys=512,
+                  consistency=consistency, key_bits=32 if dim == 4 else 64)
+    pulls, ts_pull = [], []
+    allk = torch.arange(NK, dtype=torch.int64)
+    for i, op in enumerate(OPS):
+        if op == "push":
+            keys, vals = _batch(rank, i, dim)
+            kv.push(torch.from_numpy(keys).to(dev), torch.from_numpy(vals).to(dev))
+        else:
+            ts_pull.append(kv.pull(allk.to(dev)))
+    for t in reversed(ts_pull):  # timestamps waited in any order
+        pulls.append(kv.wait(t).cpu().numpy())
+    pulls.reverse()
     kv.barrier()
-    allk = torch.arange(500, dtype=torch.int64)
-    got = kv.wait(kv.pull(allk))
-    sk, sv = kv.shard_items()
-    q.put((rank, got.numpy(), sk.numel()))
+    sk, _ = kv.shard_items()
+    torch.save({"pulls": pulls, "nkeys": int(sk.numel())}, os.path.join(out_dir, f"kv{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_multi_rank_push_pull(world):
+def _simulate(world, tau, dim):
+    """Reference semantics: a pull issued after P pushes sees, for every key, the sum
+    of all workers' pushes 1 .. P - tau (duplicates within a push summed)."""
+    table = np.zeros((NK, dim))
+    pushes, out, applied = [], [], 0
+    for i, op in enumerate(OPS):
+        if op == "push":
+            d = np.zeros((NK, dim))
+            for r in range(world):
+                keys, vals = _batch(r, i, dim)
+                np.add.at(d, keys, vals)
+            pushes.append(d)
+        else:
+            while applied < len(pushes) - tau:
+                table += pushes[applied]
+                applied += 1
+            out.append(table.copy())
+    return out
+
+
+def _run(tmp_path, world, consistency, dim, device="cpu"):
     port = _port()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in ps:
-        p.start()
-    res = sorted([q.get(timeout=120) for _ in ps], key=lambda r: r[0])
-    for p in ps:
-        p.join(timeout=30)
-    exp = np.zeros(500)
-    for r in range(world):
-        rng = np.random.default_rng(r)
-        k = rng.integers(0, 500, 300)
-        v = rng.normal(0, 1, 300).astype(np.float32)
-        np.add.at(exp, k, v)
-    for _, got, _ in res:
-        np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-5)
-    assert sum(r[2] for r in res) == 500  # every key lives on exactly one shard
-    assert all(r[2] > 0 for r in res)     # and the shards are balanced-ish
+    mp.spawn(_worker, args=(world, port, str(tmp_path), consistency, dim, device), nprocs=world,
+             join=True)
+    return [torch.load(tmp_path / f"kv{r}.pt", weights_only=False) for r in range(world)]
 
 
+@pytest.mark.parametrize("world,consistency", [(2, "bsp"), (3, "bsp"), (2, "ssp:1"),
+                                               (3, "ssp:2"), (2, "ssp:4")])
+def test_gloo_multi_rank_vector_push_pull_consistency(tmp_path, world, consistency):
+    tau = 0 if consistency == "bsp" else int(consistency.split(":")[1])
+    res = _run(tmp_path, world, consistency, K)
+    exp = _simulate(world, tau, K)
+    for r in res:
+        assert len(r["pulls"]) == len(exp)
+        for got, e in zip(r["pulls"], exp):
+            np.testing.assert_allclose(got, e, rtol=1e-5, atol=1e-5)
+    assert sum(r["nkeys"] for r in res) == NK  # every key lives on exactly one shard
+    assert all(r["nkeys"] > 0 for r in res)
+
+
+def test_gloo_scalar_asp_sees_at_least_bsp_lower_bound(tmp_path):
+    """ASP on CPU applies each push at arrival (so equals BSP there); the GPU applies on
+    its own stream. Scalar values, 64-bit keys."""
+    res = _run(tmp_path, 2, "asp", 1)
+    exp = _simulate(2, 0, 1)
+    for r in res:
+        for got, e in zip(r["pulls"], exp):
+            np.testing.assert_allclose(got, e[:, 0], rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------------------ GPU
 @pytest.mark.gpu
-def test_kvworker_gpu_single_rank():
-    kv = KVWorker(device="cuda", capacity=1 << 14)
-    keys = torch.randint(0, 1 << 40, (5000,), device="cuda")
-    vals = torch.randn(5000, device="cuda")
+@pytest.mark.parametrize("dim,bits", [(1, 64), (4, 32), (16, 64)])
+def test_kvworker_gpu_single_rank(dim, bits):
+    kv = KVWorker(device="cuda", capacity=1 << 14, dim=dim, key_bits=bits, max_keys=8192)
+    keys = torch.randint(0, 1 << 30, (5000,), device="cuda")
+    keys[::7] = keys[0]  # a hot key
+    vals = torch.randn(5000, dim, device="cuda")
     kv.wait(kv.push(keys, vals))
     got = kv.wait(kv.pull(keys))
     uk, inv = torch.unique(keys, return_inverse=True)
-    exp = torch.zeros(uk.numel(), device="cuda").index_add_(0, inv, vals)[inv]
-    torch.testing.assert_close(got, exp, rtol=1e-5, atol=1e-5)
+    exp = torch.zeros(uk.numel(), dim, device="cuda").index_add_(0, inv, vals)[inv]
+    torch.testing.assert_close(got.reshape(-1, dim), exp, rtol=1e-4, atol=1e-4)
+    k, v = kv.shard_items()
+    assert k.numel() == uk.numel()
+
+
+@pytest.mark.gpu
+def test_kvworker_gpu_optimizer_rule_and_ssp():
+    rule = UpdateRule("sgd", "constant", alpha=0.5)
+    kv = KVWorker(device="cuda", rule=rule, max_keys=1024, consistency="ssp:1")
+    key = torch.tensor([123456789], device="cuda")
+    seen = []
+    for i in range(1, 5):
+        kv.push(key, torch.tensor([float(i)], device="cuda"))
+        seen.append(kv.wait(kv.pull(key)).item())
+    # w = -0.5 * sum of the pushes applied: 1 push late
+    assert seen == [0.0, -0.5, -1.5, -3.0]
+
+
+@pytest.mark.gpu
+def test_kvworker_gpu_two_rank_rehearsal(tmp_path):
+    """Two ranks on the one GPU over gloo (exchanges staged through host memory): the
+    device localise / pack / resolve / serve / apply / unpack path of G = 2."""
+    res = _run(tmp_path, 2, "ssp:1", K, device="cuda")
+    exp = _simulate(2, 1, K)
+    for r in res:
+        for got, e in zip(r["pulls"], exp):
+            np.testing.assert_allclose(got, e, rtol=1e-4, atol=1e-4)
+    assert sum(r["nkeys"] for r in res) == NK
+
+
+def test_hello_world_gpu_app_two_ranks_cpu():
+    import subprocess
+    import sys
+
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=2", "--master-addr=127.0.0.1",
+                        f"--master-port={_port()}", "-m",
+                        "parameter_server_amd.app.hello_world_gpu", "--cpu"],
+                       capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import re
+
+    vals = {int(k): float(v) for k, v in re.findall(r"rank 0: key (\d+): ([-0-9.e]+)", r.stdout)}
+    assert vals == {0: 0.0, 1: 0.1, 2: 0.2, 3: 0.3, 4: 0.8, 5: 0.5}

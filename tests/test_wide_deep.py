@@ -59,7 +59,7 @@ def _worker(rank, world, port, q):
         tr.step(k, l)
     p = tr.progress()
     occ, _ = tr.shard.table.census()
-    q.put((rank, p, tr.param.clone(), occ))
+    q.put((rank, p, tr.param.detach().numpy().copy(), occ))  # numpy: no fd sharing
     dist.barrier()
     dist.destroy_process_group()
 
@@ -74,7 +74,7 @@ def test_wide_deep_two_ranks_gloo():
     res = sorted([q.get(timeout=240) for _ in ps], key=lambda r: r[0])
     for p in ps:
         p.join(timeout=60)
-    assert torch.equal(res[0][2], res[1][2])  # dense replicas identical after all-reduce
+    assert (res[0][2] == res[1][2]).all()  # dense replicas identical after all-reduce
     assert res[0][1]["examples"] == 2 * 12 * 256
     assert 0.3 < res[0][1]["loss"] < 0.75
     assert res[0][3] > 0 and res[1][3] > 0  # both shards hold rows
