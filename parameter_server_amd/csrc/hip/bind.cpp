@@ -24,6 +24,16 @@ void kv_update_rows(void*, int64_t, const int64_t*, const float*, int64_t, const
 void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int, int64_t*, float*,
                      bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t,
                      hipStream_t);
+// tploc.hip
+int64_t tploc_stride(int64_t);
+bool tploc_supported(int64_t, int);
+size_t tploc_temp_bytes(int64_t, int);
+void localize_tp(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint16_t*, int32_t*,
+                 int32_t*, uint64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, float*,
+                 int32_t*, int64_t, hipStream_t);
+void tp_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
+                 const float*, int64_t, float*, const int32_t*, const int32_t*, const int32_t*,
+                 float*, int64_t, hipStream_t);
 // kvapi.hip
 void kvv_pack_vals(const float*, int, const int32_t*, const int32_t*, const int32_t*, int64_t,
                    int64_t, const int64_t*, int, int64_t, int, int64_t, int32_t*, hipStream_t);
@@ -350,6 +360,66 @@ PYBIND11_MODULE(_hipops, m) {
     else check(rows.size(0) >= u_cap, "rows too small");
     psamd::fm_l2(ptr<float>(dE), rows.data_ptr(), ip, rows.size(0),
                  optr<int32_t>(n_dev, at::kInt, "n_dev"), u_cap, D, (float)lambda, cur_stream());
+  });
+  // ---------------- tile dedup + bucket partition localisation (tploc.hip) ----------------
+  m.def("tploc_stride", [](int64_t n) { return psamd::tploc_stride(n); });
+  m.def("tploc_supported", [](int64_t n, int bits) { return psamd::tploc_supported(n, bits); });
+  m.def("tploc_temp_bytes", [](int64_t n, int bits) { return (int64_t)psamd::tploc_temp_bytes(n, bits); });
+  m.def("localize_tp", [](Tensor keys, int bits, Tensor temp, Tensor dcnt, Tensor rep, Tensor pos_s,
+                          Tensor segid, Tensor uniq, Tensor seg_start, Tensor ent_uid,
+                          Tensor local_col, Tensor n_uniq, Tensor n_ent, Tensor grad, Tensor err) {
+    chk(keys, at::kLong, "keys");
+    chk(temp, at::kByte, "temp");
+    chk(dcnt, at::kInt, "dcnt");
+    chk(rep, at::kShort, "rep");
+    chk(pos_s, at::kInt, "pos_s");
+    chk(segid, at::kInt, "segid");
+    chk(uniq, at::kLong, "uniq");
+    chk(seg_start, at::kInt, "seg_start");
+    chk(ent_uid, at::kInt, "ent_uid");
+    chk(local_col, at::kInt, "local_col");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(n_ent, at::kInt, "n_ent");
+    chk(grad, at::kFloat, "grad");
+    chk(err, at::kInt, "err");
+    const int64_t n = keys.numel();
+    check(psamd::tploc_supported(n, bits), "tp localisation: 2..31 key bits, n <= 10.4M");
+    const int64_t N = psamd::tploc_stride(n);
+    const int64_t T = N / 8192;
+    check(pos_s.numel() >= N && segid.numel() >= N && uniq.numel() >= N &&
+              seg_start.numel() >= N + 1 && ent_uid.numel() >= N && grad.numel() >= N,
+          "tp localisation buffers < stride");
+    check(dcnt.numel() >= T && rep.numel() >= n && local_col.numel() >= n, "tp buffers too small");
+    check((size_t)temp.numel() >= psamd::tploc_temp_bytes(n, bits), "tp temp too small");
+    psamd::localize_tp(ptr<uint64_t>(keys), n, make_keymix(bits), temp.data_ptr(),
+                       (size_t)temp.numel(), ptr<int32_t>(dcnt), ptr<uint16_t>(rep),
+                       ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<uint64_t>(uniq),
+                       ptr<int32_t>(seg_start), ptr<int32_t>(ent_uid), ptr<int32_t>(local_col),
+                       ptr<int32_t>(n_uniq), ptr<int32_t>(n_ent), ptr<float>(grad),
+                       ptr<int32_t>(err), uniq.numel(), cur_stream());
+  });
+  m.def("tp_backward", [](Tensor rep, Tensor dcnt, int64_t n, optional<Tensor> rows, int width,
+                          optional<Tensor> vals, Tensor coef, Tensor psum, Tensor pos_s,
+                          Tensor segid, Tensor n_ent, Tensor grad) {
+    chk(rep, at::kShort, "rep");
+    chk(dcnt, at::kInt, "dcnt");
+    chk(coef, at::kFloat, "coef");
+    chk(psum, at::kFloat, "psum");
+    chk(pos_s, at::kInt, "pos_s");
+    chk(segid, at::kInt, "segid");
+    chk(n_ent, at::kInt, "n_ent");
+    chk(grad, at::kFloat, "grad");
+    const int64_t N = psamd::tploc_stride(n);
+    check(n > 0 && rep.numel() >= n && dcnt.numel() >= N / 8192, "tp backward: rep / dcnt");
+    check(psum.numel() >= N && pos_s.numel() >= N && segid.numel() >= N, "tp backward buffers");
+    const int32_t* r = optr<int32_t>(rows, at::kInt, "rows");
+    if (r) check(rows->numel() >= n, "rows too small");
+    else check(width > 0, "width must be > 0 without rows");
+    const float* v = optr<float>(vals, at::kFloat, "vals");
+    if (v) check(vals->numel() >= n, "vals too small");
+    psamd::tp_backward(ptr<uint16_t>(rep), ptr<int32_t>(dcnt), n, r, width, v, ptr<float>(coef),
+                       coef.numel(), ptr<float>(psum), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
+                       ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), cur_stream());
   });
   // ---------------- tile-deduplicating localisation (tileloc.hip) ----------------
   m.def("tileloc_stride", [](int64_t n) { return psamd::tileloc_stride(n); });

@@ -1,0 +1,679 @@
+// Localisation by tile dedup + bucket partition ("tp", mixed key spaces <= 31 bits).
+//
+// Reference: Localizer::countUniqIndex / remapIndex (src/util/localizer.h:69-191) sort
+// every (key, position) pair of a minibatch and rebuild a CSR with local ids.
+//
+// Measured on MI355X for a 65,536 x 39 Criteo-shaped minibatch (2.56 M keys, 234 K
+// distinct): 1 944 hot keys hold 77 % of the occurrences, and a full LSD radix sort
+// (sort32.hip) is 16 small launches, ~200 us. Device-scope atomics run at ~20 per
+// ns (benchmarks/probe_atomics.py), so a global hash with per-key atomics cannot beat
+// it either. This path touches each occurrence once, in LDS, and works on the
+// tile-distinct "entries" (~1 M) afterwards, with no global atomics at all:
+//
+//   tile     one 512-thread workgroup per tile of 8192 occurrences: mix, LDS hash
+//            dedup, counting sort of the tile's distinct keys by bucket (top BB key
+//            bits) -> tkeys[tile][pos], per-tile bucket offsets toff[tile][b],
+//            rep[i] = tile entry of occurrence i (u16)
+//   dedup    one workgroup per bucket: gather the bucket's entries from every tile
+//            (a key occurs at most once per tile, so a hot key is <= #tiles entries
+//            and buckets stay balanced), LDS hash -> distinct keys + entry counts,
+//            bitonic sort of the distinct keys -> dscr[b], dcount[b], ecount[b]
+//   emit     one workgroup per bucket: unique / entry bases = prefix of dcount /
+//            ecount over the earlier buckets; uniq, seg_start (over entries), and the
+//            entry CSC (pos_s = entry id, segid), ranked in tile order by one wave
+//            (deterministic); ent_uid[entry] = unique id
+//   gather   local_col[i] = ent_uid[tile * 8192 + rep[i]]
+// Backward: per tile, LDS float accumulation of coef[row] * val into its entries
+// (psum), then a 64-lane segmented scan of psum over the entry CSC.
+//
+// Buckets are ranges of the mixed key space, so the unique keys come out sorted
+// (the multi-GPU owner split and the ordered home slots of the KV table rely on it).
+#include "common.cuh"
+
+#include <stdexcept>
+#include <string>
+
+namespace psamd {
+
+namespace tp {
+constexpr int kThr = 1024;              // tile workgroup
+constexpr int kIt = 8;
+constexpr int kTile = kThr * kIt;       // 8192 occurrences
+constexpr int kHash = 2 * kTile;        // LDS hash slots of a tile (load <= 0.5)
+constexpr int kMaxBk = 4096;            // buckets
+constexpr int kMaxT = 640;              // tiles (n <= 5.2 M)
+constexpr int kBThr = 256;              // bucket / emit workgroups
+constexpr int kECap = 4096;             // entries of one bucket held in LDS
+constexpr int kDH = 2048;               // distinct-key hash of one bucket
+constexpr uint32_t kEmpty = 0xffffffffu;
+}  // namespace tp
+
+__device__ __forceinline__ uint32_t tp_hash(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+template <int kN>
+__device__ __forceinline__ uint32_t tp_block_scan(uint32_t v, uint32_t* lds, uint32_t* total) {
+  constexpr int kW = kN / 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int w = 0; w < kW; ++w) {
+      const uint32_t t = lds[w];
+      lds[w] = run;
+      run += t;
+    }
+    lds[kW] = run;
+  }
+  __syncthreads();
+  const uint32_t r = x - v + lds[wid];
+  *total = lds[kW];
+  __syncthreads();
+  return r;
+}
+
+// sum of a[0:b) by one workgroup (a few thousand L2-resident words)
+template <int kN>
+__device__ __forceinline__ uint32_t tp_prefix(const uint32_t* __restrict__ a, int b, uint32_t* lds) {
+  uint32_t s = 0;
+  for (int i = threadIdx.x; i < b; i += kN) s += a[i];
+  uint32_t tot;
+  tp_block_scan<kN>(s, lds, &tot);
+  return tot;
+}
+
+__device__ __forceinline__ uint64_t tp_match_any(uint32_t v, int nbits, uint64_t active) {
+  uint64_t peers = active;
+  for (int b = 0; b < nbits; ++b) {
+    const bool bit = (v >> b) & 1u;
+    const uint64_t bal = __ballot(bit);
+    peers &= bit ? bal : ~bal;
+  }
+  return peers;
+}
+
+// ------------------------------------------------------------------------ tile
+__global__ void __launch_bounds__(tp::kThr)
+tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift, int nbk,
+               uint32_t* __restrict__ tkeys, uint16_t* __restrict__ toff,
+               int32_t* __restrict__ dcnt, uint16_t* __restrict__ rep) {
+  using namespace tp;
+  __shared__ uint32_t hk[kHash];    // keys; after the bucket sort: entry position
+  __shared__ uint32_t cnt[kMaxBk];  // per-bucket counts, then offsets
+  __shared__ uint32_t lds[kThr / 64 + 1];
+  const int t = threadIdx.x;
+  for (int i = t; i < kHash; i += kThr) hk[i] = kEmpty;
+  for (int d = t; d < nbk; d += kThr) cnt[d] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  uint64_t kr[kIt];
+  uint16_t sl[kIt];
+#pragma unroll
+  for (int j = 0; j < kIt; ++j) {  // all loads in flight before the LDS insert chain
+    const int64_t i = base + j * kThr + t;
+    kr[j] = i < n ? raw[i] : 0ull;
+  }
+#pragma unroll
+  for (int j = 0; j < kIt; ++j) {
+    const int64_t i = base + j * kThr + t;
+    sl[j] = 0;
+    if (i < n) {
+      const uint32_t k = (uint32_t)mix_key(kr[j], m);
+      uint32_t h = tp_hash(k) & (kHash - 1);
+      for (int probe = 0; probe < kHash; ++probe) {  // <= kTile keys: a free slot exists
+        const uint32_t cur = hk[h];
+        if (cur == k) break;
+        if (cur == kEmpty) {
+          const uint32_t prev = atomicCAS(&hk[h], kEmpty, k);
+          if (prev == kEmpty || prev == k) break;
+        }
+        h = (h + 1) & (kHash - 1);
+      }
+      sl[j] = (uint16_t)h;
+    }
+  }
+  __syncthreads();
+  // counting sort of the distinct keys by bucket; thread t owns slots q*kThr + t
+  constexpr int kPer = kHash / kThr;  // 32
+  uint32_t rr[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const uint32_t k = hk[q * kThr + t];
+    rr[q] = k != kEmpty ? atomicAdd(&cnt[k >> shift], 1u) : kEmpty;
+  }
+  __syncthreads();
+  // exclusive scan of the bucket counts (nbk <= kMaxBk: 8 per thread)
+  constexpr int kDP = kMaxBk / kThr;
+  uint32_t c[kDP], s = 0;
+#pragma unroll
+  for (int e = 0; e < kDP; ++e) {
+    const int d = t * kDP + e;
+    c[e] = d < nbk ? cnt[d] : 0u;
+    s += c[e];
+  }
+  uint32_t D;
+  uint32_t run = tp_block_scan<kThr>(s, lds, &D);
+  uint16_t* to = toff + (int64_t)blockIdx.x * (nbk + 1);
+#pragma unroll
+  for (int e = 0; e < kDP; ++e) {
+    const int d = t * kDP + e;
+    if (d < nbk) {
+      cnt[d] = run;
+      to[d] = (uint16_t)run;
+    }
+    run += c[e];
+  }
+  if (t == 0) {
+    to[nbk] = (uint16_t)D;
+    dcnt[blockIdx.x] = (int32_t)D;
+  }
+  __syncthreads();
+  uint32_t* tk = tkeys + base;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    if (rr[q] != kEmpty) {
+      const uint32_t k = hk[q * kThr + t];
+      const uint32_t pos = cnt[k >> shift] + rr[q];
+      tk[pos] = k;
+      rr[q] = pos;
+    }
+  }
+  __syncthreads();  // every hk read is done: reuse it as slot -> entry position
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (rr[q] != kEmpty) hk[q * kThr + t] = rr[q];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kIt; ++j) {
+    const int64_t i = base + j * kThr + t;
+    if (i < n) rep[i] = (uint16_t)hk[sl[j]];
+  }
+}
+
+// ---------------------------------------------------------------------- bucket
+// One workgroup per bucket b (a range of the mixed key space):
+//   gather   the bucket's entries from every tile, in tile order (flat: every
+//            thread loads independent entries, the tile of an entry found by binary
+//            search over the per-tile run prefix); entry ids go straight to beid
+//   dedup    LDS hash of the distinct keys with entry counts; rank sort of the
+//            distinct keys (rank = number of smaller keys: one pass, no bitonic
+//            network of barriers)
+//   rank     every wave walks its quarter of the entries in order twice: per-wave
+//            per-key counts, then ranks = bucket-local segment start + entries of the
+//            key in earlier quarters + earlier lanes (deterministic CSC)
+// Outputs per bucket (scratch): sorted distinct keys + local segment starts, and per
+// entry (gather order) its entry id and (distinct index | local CSC position << 16).
+__global__ void __launch_bounds__(tp::kBThr)
+tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbk,
+                 int T, uint32_t* __restrict__ dkey, uint16_t* __restrict__ dstart,
+                 int32_t* __restrict__ beid, uint32_t* __restrict__ bjp,
+                 uint32_t* __restrict__ dcount, uint32_t* __restrict__ ecount,
+                 int32_t* __restrict__ err) {
+  using namespace tp;
+  constexpr int kWv = kBThr / 64;
+  __shared__ uint32_t ek[kECap];
+  __shared__ uint64_t sbuf[kDH];   // hash (keys | counts), then the sorted (key | start)
+  __shared__ uint64_t ubuf[(kECap * 2 + kWv * kDH * 2) / 8];  // compacted list, then ej + cntw
+  __shared__ uint32_t tpre[kMaxT + 1];
+  __shared__ uint16_t tlo[kMaxT];
+  __shared__ uint32_t lds[kBThr / 64 + 1];
+  uint32_t* hkey = reinterpret_cast<uint32_t*>(sbuf);
+  uint32_t* hcnt = hkey + kDH;
+  uint64_t* dl = ubuf;                                           // [kDH]
+  uint16_t* ej = reinterpret_cast<uint16_t*>(ubuf);              // [kECap]
+  uint16_t* cntw = ej + kECap;                                   // [kWv][kDH]
+  const int t = threadIdx.x, b = blockIdx.x, lane = t & 63, wv = t >> 6;
+  for (int s = t; s < kDH; s += kBThr) {
+    hkey[s] = kEmpty;
+    hcnt[s] = 0;
+  }
+  // per-tile runs [toff[q][b], toff[q][b+1]): thread t owns tiles [t*per, t*per + per)
+  const int per = (T + kBThr - 1) / kBThr;
+  const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
+  uint32_t c = 0;
+  for (int q = q0; q < q1; ++q) {
+    const uint16_t* to = toff + (int64_t)q * (nbk + 1);
+    const uint32_t lo = to[b], hi = to[b + 1];
+    tlo[q] = (uint16_t)lo;
+    tpre[q] = hi - lo;
+    c += hi - lo;
+  }
+  uint32_t E;
+  uint32_t w = tp_block_scan<kBThr>(c, lds, &E);
+  for (int q = q0; q < q1; ++q) {
+    const uint32_t len = tpre[q];
+    tpre[q] = w;
+    w += len;
+  }
+  if (t == 0) tpre[T] = E;
+  __syncthreads();
+  const uint32_t En = E < (uint32_t)kECap ? E : (uint32_t)kECap;
+  bool bad = E > (uint32_t)kECap;
+  int32_t* be = beid + (int64_t)b * kECap;
+  for (uint32_t g = t; g < En; g += kBThr) {
+    int lo = 0, hi = T - 1;  // last tile with tpre[q] <= g
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tpre[mid] <= g) lo = mid; else hi = mid - 1;
+    }
+    const int64_t idx = (int64_t)lo * kTile + tlo[lo] + (g - tpre[lo]);
+    ek[g] = tkeys[idx];
+    be[g] = (int32_t)idx;
+  }
+  __syncthreads();
+  for (uint32_t g = t; g < En; g += kBThr) {
+    const uint32_t key = ek[g];
+    uint32_t h = tp_hash(key) & (kDH - 1);
+    bool ok = false;
+    for (int p = 0; p < kDH / 2; ++p) {
+      const uint32_t cur = hkey[h];
+      if (cur == kEmpty) {
+        const uint32_t prev = atomicCAS(&hkey[h], kEmpty, key);
+        if (prev == kEmpty || prev == key) { ok = true; break; }
+      } else if (cur == key) {
+        ok = true;
+        break;
+      }
+      h = (h + 1) & (kDH - 1);
+    }
+    if (ok) atomicAdd(&hcnt[h], 1u);
+    else bad = true;
+  }
+  if (bad) atomicOr(err, 1);
+  __syncthreads();
+  // compact the occupied slots (strided: conflict-free LDS reads)
+  constexpr int kPer = kDH / kBThr;  // 8
+  uint64_t ent[kPer];
+  uint32_t cc = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int s = q * kBThr + t;
+    ent[q] = hkey[s] != kEmpty ? (((uint64_t)hkey[s] << 32) | hcnt[s]) : ~0ull;
+    cc += ent[q] != ~0ull;
+  }
+  uint32_t D;
+  uint32_t wd = tp_block_scan<kBThr>(cc, lds, &D);
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (ent[q] != ~0ull) dl[wd++] = ent[q];
+  __syncthreads();
+  // rank sort: keys are distinct, rank = number of smaller keys (broadcast LDS reads)
+  for (uint32_t i = t; i < D; i += kBThr) {
+    const uint64_t x = dl[i];
+    uint32_t r = 0;
+    for (uint32_t q = 0; q < D; ++q) r += dl[q] < x;
+    sbuf[r] = x;
+  }
+  __syncthreads();
+  // local segment starts: exclusive prefix of the sorted counts (chunks of kBThr);
+  // sbuf[j] becomes (key << 32 | start)
+  uint32_t carry = 0;
+  for (uint32_t j0 = 0; j0 < D; j0 += kBThr) {
+    const uint32_t j = j0 + t;
+    const uint64_t v = j < D ? sbuf[j] : 0ull;
+    uint32_t tot;
+    const uint32_t ex = tp_block_scan<kBThr>((uint32_t)(v & 0xffffffffull), lds, &tot) + carry;
+    if (j < D) {
+      dkey[(int64_t)b * kDH + j] = (uint32_t)(v >> 32);
+      dstart[(int64_t)b * kDH + j] = (uint16_t)ex;
+      sbuf[j] = (v & 0xffffffff00000000ull) | ex;
+    }
+    carry += tot;
+  }
+  for (int s = t; s < kWv * kDH; s += kBThr) cntw[s] = 0;  // (dl is dead)
+  __syncthreads();
+  if (t == 0) {
+    dcount[b] = D;
+    ecount[b] = En;
+  }
+  // walk 1: wave wv owns entries [wv*Q, wv*Q + Q): distinct index + per-wave counts
+  constexpr int kHB = __builtin_ctz(kDH);
+  const uint32_t Q = (En + kWv - 1) / kWv;
+  const uint32_t g_lo = wv * Q, g_hi = g_lo + Q < En ? g_lo + Q : En;
+  for (uint32_t g0 = g_lo; g0 < g_hi; g0 += 64) {
+    const uint32_t g = g0 + lane;
+    uint32_t j = 0xffffu;
+    if (g < g_hi && D > 0) {
+      const uint32_t key = ek[g];
+      int lo = 0, hi = (int)D - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((uint32_t)(sbuf[mid] >> 32) < key) lo = mid + 1; else hi = mid;
+      }
+      if ((uint32_t)(sbuf[lo] >> 32) == key) j = (uint32_t)lo;
+    }
+    const bool ok = j != 0xffffu;
+    const uint64_t peers = tp_match_any(j, kHB, __ballot(ok));
+    if (ok && (peers & ((1ull << lane) - 1ull)) == 0ull)
+      cntw[wv * kDH + j] += (uint16_t)__popcll(peers);
+    if (g < g_hi) ej[g] = (uint16_t)j;
+  }
+  __syncthreads();
+  // per key: the bucket-local start of each wave's run of it
+  for (uint32_t j = t; j < D; j += kBThr) {
+    uint32_t run = (uint32_t)sbuf[j];
+#pragma unroll
+    for (int q = 0; q < kWv; ++q) {
+      const uint32_t cq = cntw[q * kDH + j];
+      cntw[q * kDH + j] = (uint16_t)run;
+      run += cq;
+    }
+  }
+  __syncthreads();
+  // walk 2: ranks in order
+  uint32_t* bj = bjp + (int64_t)b * kECap;
+  for (uint32_t g0 = g_lo; g0 < g_hi; g0 += 64) {
+    const uint32_t g = g0 + lane;
+    const uint32_t j = g < g_hi ? ej[g] : 0xffffu;
+    const bool ok = j != 0xffffu;
+    const uint64_t peers = tp_match_any(j, kHB, __ballot(ok));
+    const uint64_t below = peers & ((1ull << lane) - 1ull);
+    uint32_t rbase = 0;
+    if (ok && below == 0ull) {
+      rbase = cntw[wv * kDH + j];
+      cntw[wv * kDH + j] = (uint16_t)(rbase + (uint32_t)__popcll(peers));
+    }
+    const int leader = ok ? (int)(__ffsll((long long)peers) - 1) : lane;
+    rbase = __shfl(rbase, leader, 64);
+    if (g < g_hi) bj[g] = ok ? (j | ((rbase + (uint32_t)__popcll(below)) << 16)) : 0xffffffffu;
+  }
+}
+
+// ------------------------------------------------------------------------ emit
+// Flat writes of the global outputs (bases = prefix over the earlier buckets).
+__global__ void __launch_bounds__(tp::kBThr)
+tp_emit_kernel(int nbk, const uint32_t* __restrict__ dkey, const uint16_t* __restrict__ dstart,
+               const int32_t* __restrict__ beid, const uint32_t* __restrict__ bjp,
+               const uint32_t* __restrict__ dcount, const uint32_t* __restrict__ ecount,
+               int32_t* __restrict__ pos_s, int32_t* __restrict__ segid,
+               uint64_t* __restrict__ uniq, int32_t* __restrict__ seg_start,
+               int32_t* __restrict__ ent_uid, int32_t* __restrict__ n_uniq,
+               int32_t* __restrict__ n_ent, float* __restrict__ zero_a, int64_t u_cap,
+               int64_t e_cap) {
+  using namespace tp;
+  __shared__ uint32_t lds[2 * (kBThr / 64 + 1)];
+  const int t = threadIdx.x, b = blockIdx.x;
+  uint32_t su = 0, se = 0;
+  for (int i = t; i < b; i += kBThr) {
+    su += dcount[i];
+    se += ecount[i];
+  }
+  uint32_t ubase, ebase;
+  tp_block_scan<kBThr>(su, lds, &ubase);
+  tp_block_scan<kBThr>(se, lds + kBThr / 64 + 1, &ebase);
+  const uint32_t D = dcount[b], En = ecount[b];
+  for (uint32_t j = t; j < D; j += kBThr) {
+    const int64_t u = (int64_t)ubase + j;
+    if (in_range(u, u_cap)) {
+      uniq[u] = dkey[(int64_t)b * kDH + j];
+      seg_start[u] = (int32_t)(ebase + dstart[(int64_t)b * kDH + j]);
+      if (zero_a) zero_a[u] = 0.f;
+    }
+  }
+  for (uint32_t g = t; g < En; g += kBThr) {
+    const uint32_t v = bjp[(int64_t)b * kECap + g];
+    if (v == 0xffffffffu) continue;
+    const int32_t id = beid[(int64_t)b * kECap + g];
+    const uint32_t u = ubase + (v & 0xffffu);
+    const int64_t q = (int64_t)ebase + (v >> 16);
+    if (in_range(q, e_cap)) {
+      pos_s[q] = id;
+      segid[q] = (int32_t)(u + 1);
+    }
+    if (in_range((int64_t)id, e_cap)) ent_uid[id] = (int32_t)u;
+  }
+  if (b == nbk - 1 && t == 0) {
+    const uint32_t U = ubase + D, Et = ebase + En;
+    *n_uniq = (int32_t)U;
+    *n_ent = (int32_t)Et;
+    if (in_range((int64_t)U, u_cap + 1)) seg_start[U] = (int32_t)Et;
+  }
+}
+
+// ---------------------------------------------------------------------- gather
+__global__ void tp_gather_kernel(const uint16_t* __restrict__ rep,
+                                 const int32_t* __restrict__ ent_uid, int64_t n,
+                                 int32_t* __restrict__ local_col) {
+  constexpr int kPer = 4;
+  const int64_t i0 = (blockIdx.x * (int64_t)blockDim.x) * kPer + threadIdx.x;
+  int64_t e[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int64_t i = i0 + q * blockDim.x;
+    e[q] = i < n ? (int64_t)((uint32_t)i & ~(uint32_t)(tp::kTile - 1)) + rep[i] : -1;
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int64_t i = i0 + q * blockDim.x;
+    if (e[q] >= 0) local_col[i] = ent_uid[e[q]];
+  }
+}
+
+// -------------------------------------------------------------------- backward
+// psum[tile entry] = sum over the tile's occurrences of the entry of coef[row] * val.
+// Variable-width rows (rows != null): one LDS float atomic per occurrence.
+__global__ void __launch_bounds__(tp::kThr)
+tp_bwd_accum_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ dcnt, int64_t n,
+                    const int32_t* __restrict__ rows, int width, const float* __restrict__ vals,
+                    const float* __restrict__ coef, int64_t B, float* __restrict__ psum) {
+  using namespace tp;
+  __shared__ float acc[kTile];
+  const int t = threadIdx.x;
+  for (int i = t; i < kTile; i += kThr) acc[i] = 0.f;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  float v[kIt];
+  uint16_t e[kIt];
+#pragma unroll
+  for (int j = 0; j < kIt; ++j) {
+    const int64_t i = base + j * kThr + t;
+    v[j] = 0.f;
+    e[j] = 0;
+    if (i < n) {
+      const int64_t r = rows ? (int64_t)rows[i] : (int64_t)((uint32_t)i / (uint32_t)width);
+      e[j] = rep[i];
+      if (in_range(r, B)) v[j] = coef[r] * (vals ? vals[i] : 1.f);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kIt; ++j)
+    if (v[j] != 0.f) atomicAdd(&acc[e[j]], v[j]);
+  __syncthreads();
+  const int cnt = min(kTile, max(0, dcnt[blockIdx.x]));
+  for (int i = t; i < cnt; i += kThr) psum[base + i] = acc[i];
+}
+
+// Fixed-width rows: thread = (slot, run of L consecutive rows) walks down its column,
+// so a hot key of a slot repeats along the walk and is summed in a register until the
+// key changes (one LDS atomic per run instead of per occurrence); the lanes of a wave
+// hold adjacent slots of the same rows, so the rep / vals loads stay coalesced.
+// (Row-major lanes: LDS atomic waits on hot entries dominated, SQ_WAIT_INST_LDS.)
+__global__ void __launch_bounds__(tp::kThr)
+tp_bwd_accum_cols_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ dcnt,
+                         int64_t n, int width, const float* __restrict__ vals,
+                         const float* __restrict__ coef, int64_t B, float* __restrict__ psum) {
+  using namespace tp;
+  __shared__ float acc[kTile];
+  const int t = threadIdx.x;
+  for (int i = t; i < kTile; i += kThr) acc[i] = 0.f;
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int64_t lim = n - base < kTile ? n - base : kTile;
+  const int64_t r0 = base / width, r1 = (base + lim - 1) / width;
+  const int nr = (int)(r1 - r0 + 1);
+  const int L = (nr * width + kThr - 1) / kThr;  // rows per thread
+  const int nseg = (nr + L - 1) / L;
+  const int slot = t % width, seg = t / width;
+  __syncthreads();
+  if (seg < nseg) {
+    const int ra = seg * L, rb = ra + L < nr ? ra + L : nr;
+    uint32_t cur = 0xffffffffu;
+    float sum = 0.f;
+    for (int rl = ra; rl < rb; ++rl) {
+      const int64_t r = r0 + rl;
+      const int64_t i = r * width + slot;  // global position
+      if (i < base || i >= base + lim || !in_range(r, B)) continue;
+      const uint32_t e = rep[i];
+      const float v = coef[r] * (vals ? vals[i] : 1.f);
+      if (e != cur) {
+        if (cur != 0xffffffffu && sum != 0.f) atomicAdd(&acc[cur], sum);
+        cur = e;
+        sum = v;
+      } else {
+        sum += v;
+      }
+    }
+    if (cur != 0xffffffffu && sum != 0.f) atomicAdd(&acc[cur], sum);
+  }
+  __syncthreads();
+  const int cnt = min(kTile, max(0, dcnt[blockIdx.x]));
+  for (int i = t; i < cnt; i += kThr) psum[base + i] = acc[i];
+}
+
+__global__ void __launch_bounds__(256)
+tp_seg_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ segid,
+                     int64_t n_host, const int32_t* __restrict__ n_dev,
+                     const float* __restrict__ psum, int64_t p_cap, float* __restrict__ grad,
+                     int64_t grad_cap) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n = dev_len(n_dev, n_host);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); i0 < n;
+       i0 += stride) {
+    const int64_t i = i0 + lane;
+    const bool valid = i < n;
+    int32_t s = -1;
+    float v = 0.f;
+    if (valid) {
+      s = segid[i];
+      const int32_t p = pos_s[i];
+      if (in_range(p, p_cap)) v = psum[p];
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const float vo = __shfl_up(v, off, 64);
+      const int32_t so = __shfl_up(s, off, 64);
+      if (lane >= off && so == s) v += vo;
+    }
+    const int32_t s_next = __shfl_down(s, 1, 64);
+    const int32_t s_lane0 = __shfl(s, 0, 64);
+    int32_t prev_of_lane0 = -2;
+    if (lane == 0 && i0 > 0) prev_of_lane0 = segid[i0 - 1];
+    prev_of_lane0 = __shfl(prev_of_lane0, 0, 64);
+    const bool tail = valid && (lane == 63 || s_next != s || i + 1 >= n);
+    if (tail) {
+      const bool starts_inside = (s != s_lane0) || (prev_of_lane0 != s);
+      bool ends_inside = true;
+      if (lane == 63 && i + 1 < n) ends_inside = segid[i + 1] != s;
+      const int32_t u = s - 1;
+      if (in_range(u, grad_cap)) {
+        if (starts_inside && ends_inside) grad[u] = v;
+        else atomicAdd(&grad[u], v);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+struct TpGeom {
+  int nbk, shift;
+  int64_t T, N;
+};
+
+static TpGeom tp_geom(int64_t n, int bits) {
+  TpGeom g;
+  g.T = (n + tp::kTile - 1) / tp::kTile;
+  g.N = g.T * tp::kTile;
+  // <= 1280 occurrences per bucket on average: even if every key is distinct a
+  // bucket's distinct keys stay under kDH / 2 (measured on Criteo-shaped batches:
+  // <= 1615 entries and 157 distinct keys per bucket at 2048 buckets)
+  int bb = 0;
+  while (bb < 12 && (n >> bb) > 1280) ++bb;
+  if (bb > bits) bb = bits;
+  g.nbk = 1 << bb;
+  g.shift = bits - bb;
+  return g;
+}
+
+int64_t tploc_stride(int64_t n) { return tp_geom(n, 31).N; }
+
+bool tploc_supported(int64_t n, int bits) {
+  return bits >= 2 && bits <= 31 && n > 0 && (n >> 12) <= 1280 &&
+         (n + tp::kTile - 1) / tp::kTile <= tp::kMaxT;
+}
+
+static size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+size_t tploc_temp_bytes(int64_t n, int bits) {
+  const TpGeom g = tp_geom(n, bits);
+  return al16((size_t)g.N * 4)                                 // tkeys
+         + al16((size_t)g.T * (g.nbk + 1) * 2)                 // toff (u16)
+         + al16((size_t)g.nbk * tp::kDH * 4)                   // dkey
+         + al16((size_t)g.nbk * tp::kDH * 2)                   // dstart
+         + al16((size_t)g.nbk * tp::kECap * 4) * 2             // beid, bjp
+         + al16((size_t)g.nbk * 8) + 256;                      // dcount, ecount
+}
+
+void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
+                 int32_t* dcnt, uint16_t* rep, int32_t* pos_s, int32_t* segid, uint64_t* uniq,
+                 int32_t* seg_start, int32_t* ent_uid, int32_t* local_col, int32_t* n_uniq,
+                 int32_t* n_ent, float* grad, int32_t* err, int64_t u_cap, hipStream_t st) {
+  if (n <= 0) return;
+  if (!tploc_supported(n, m.bits)) throw std::runtime_error("localize_tp: unsupported size");
+  if (temp_bytes < tploc_temp_bytes(n, m.bits)) throw std::runtime_error("localize_tp: temp");
+  const TpGeom g = tp_geom(n, m.bits);
+  char* p = (char*)temp;
+  auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
+  uint32_t* tkeys = (uint32_t*)take((size_t)g.N * 4);
+  uint16_t* toff = (uint16_t*)take((size_t)g.T * (g.nbk + 1) * 2);
+  uint32_t* dkey = (uint32_t*)take((size_t)g.nbk * tp::kDH * 4);
+  uint16_t* dstart = (uint16_t*)take((size_t)g.nbk * tp::kDH * 2);
+  int32_t* beid = (int32_t*)take((size_t)g.nbk * tp::kECap * 4);
+  uint32_t* bjp = (uint32_t*)take((size_t)g.nbk * tp::kECap * 4);
+  uint32_t* dcount = (uint32_t*)take((size_t)g.nbk * 8);
+  uint32_t* ecount = dcount + g.nbk;
+  tp_tile_kernel<<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff, dcnt,
+                                                     rep);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  tp_bucket_kernel<<<(unsigned)g.nbk, tp::kBThr, 0, st>>>(tkeys, toff, g.nbk, (int)g.T, dkey,
+                                                          dstart, beid, bjp, dcount, ecount, err);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  tp_emit_kernel<<<(unsigned)g.nbk, tp::kBThr, 0, st>>>(g.nbk, dkey, dstart, beid, bjp, dcount,
+                                                        ecount, pos_s, segid, uniq, seg_start,
+                                                        ent_uid, n_uniq, n_ent, grad, u_cap, g.N);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  tp_gather_kernel<<<(unsigned)((n + 1023) / 1024), 256, 0, st>>>(rep, ent_uid, n, local_col);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void tp_backward(const uint16_t* rep, const int32_t* dcnt, int64_t n, const int32_t* rows,
+                 int width, const float* vals, const float* coef, int64_t B, float* psum,
+                 const int32_t* pos_s, const int32_t* segid, const int32_t* n_ent, float* grad,
+                 int64_t grad_cap, hipStream_t st) {
+  if (n <= 0) return;
+  const TpGeom g = tp_geom(n, 31);
+  if (rows == nullptr && width >= 2 && width <= tp::kThr)
+    tp_bwd_accum_cols_kernel<<<(unsigned)g.T, tp::kThr, 0, st>>>(rep, dcnt, n, width, vals, coef,
+                                                                 B, psum);
+  else
+    tp_bwd_accum_kernel<<<(unsigned)g.T, tp::kThr, 0, st>>>(rep, dcnt, n, rows, width, vals, coef,
+                                                            B, psum);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  tp_seg_reduce_kernel<<<grid_for(g.N, 256, 8192), 256, 0, st>>>(pos_s, segid, g.N, n_ent, psum,
+                                                                 g.N, grad, grad_cap);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace psamd

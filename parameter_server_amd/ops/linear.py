@@ -109,8 +109,9 @@ def linear_backward(loc, coef, *, B: int, width: int = 0, rows=None, vals=None, 
     """grad[u] (and hess[u] if coef2 given) into loc.grad / loc.hess."""
     if getattr(loc, "tile", None) is not None:  # tile-deduplicated localisation
         t = loc.tile
-        hipops().tile_backward(t.rep, t.dcnt, loc.nnz, rows, width, vals, coef, t.psum, loc.pos_s,
-                               loc.segid, t.n_ent, loc.grad)
+        bwd = hipops().tp_backward if t.size == 8192 else hipops().tile_backward
+        bwd(t.rep, t.dcnt, loc.nnz, rows, width, vals, coef, t.psum, loc.pos_s, loc.segid, t.n_ent,
+            loc.grad)
         return loc.grad, None
     if getattr(loc, "hashed", False):  # sort-free localisation: wave-aggregated atomics
         hipops().hash_backward(loc.local_col, loc.nnz, width, rows, vals, coef, loc.grad,

@@ -50,7 +50,8 @@ class TileInfo:
     rep: torch.Tensor    # int16 [nnz] tile-local entry id of every position
     dcnt: torch.Tensor   # int32 [tiles] distinct keys per 4096-key tile
     n_ent: torch.Tensor  # int32[1] total entries (device)
-    psum: torch.Tensor   # float [tiles*4096] per-entry partial gradients (backward scratch)
+    psum: torch.Tensor   # float [tiles*size] per-entry partial gradients (backward scratch)
+    size: int = 4096     # occurrences per tile (4096: "tile" mode, 8192: "tp" mode)
 
 
 class Localizer:
@@ -74,7 +75,12 @@ class Localizer:
     hash and sorts only the DISTINCT keys; same outputs as "sort" except the order of
     positions inside a key's segment (5 launches instead of 16).
     ``check()`` raises if a bucket overflowed its LDS hash (never for mixed keys of
-    realistic batches; the bucket count bounds the distinct keys per bucket)."""
+    realistic batches; the bucket count bounds the distinct keys per bucket).
+    ``mode="tp"`` (csrc/hip/tploc.hip, GPU, key bits <= 31, <= 10.4 M keys): LDS dedup of
+    8192-occurrence tiles, then one workgroup per key-range bucket deduplicates the
+    tile-distinct entries (a hot key is at most one entry per tile) and emits sorted
+    unique keys, an entry-level CSC and local columns: 4 launches, no global atomics;
+    the backward accumulates per tile in LDS and scans the entry CSC (``TileInfo``)."""
 
     def __init__(self, max_nnz: int, bits: int, device="cpu", with_hess: bool = False,
                  mode: str = "sort"):
@@ -85,9 +91,11 @@ class Localizer:
         n = self.max_nnz
         dev = self.device
         self.gpu = dev.type == "cuda"
-        if mode not in ("sort", "hash", "bucket", "tile", "part"):
+        if mode not in ("sort", "hash", "bucket", "tile", "part", "tp"):
             raise ValueError(f"unknown localisation mode {mode!r}")
         if mode == "part" and not (self.gpu and hipops().partloc_supported(n, self.bits)):
+            mode = "sort"
+        if mode == "tp" and (with_hess or not (self.gpu and hipops().tploc_supported(n, self.bits))):
             mode = "sort"
         if mode in ("hash", "tile") and (with_hess or self.bits > 32):
             mode = "sort"
@@ -110,6 +118,23 @@ class Localizer:
             self.t_psum = torch.empty(N, dtype=torch.float32, device=dev)
             self.hess = None
             self.digit_bits = 10 if 24 < self.bits <= 30 else 8
+            return
+        if self.gpu and self.mode == "tp":
+            H = hipops()
+            N = H.tploc_stride(n)
+            i32 = lambda k: torch.empty(k, dtype=torch.int32, device=dev)  # noqa: E731
+            self.ptemp = torch.empty(H.tploc_temp_bytes(n, self.bits), dtype=torch.uint8,
+                                     device=dev)
+            self.t_dcnt, self.t_rep = i32(N // 8192), torch.empty(n, dtype=torch.int16, device=dev)
+            self.pos_s, self.segid, self.t_ent_uid = i32(N), i32(N), i32(N)
+            self.seg_start, self.local_col = i32(N + 1), i32(n)
+            self.uniq = torch.empty(N, dtype=torch.int64, device=dev)
+            self.n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.t_nent = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.grad = torch.empty(N, dtype=torch.float32, device=dev)
+            self.t_psum = torch.empty(N, dtype=torch.float32, device=dev)
+            self.hess = None
+            self.err = torch.zeros(1, dtype=torch.int32, device=dev)
             return
         if self.gpu and self.mode == "part":
             H = hipops()
@@ -191,8 +216,9 @@ class Localizer:
 
     def check(self):
         """Host sync: raise if a "part" localisation overflowed a bucket's LDS hash."""
-        if getattr(self, "err", None) is not None and self.mode == "part" and int(self.err.item()):
-            raise RuntimeError("localize_part: a bucket's distinct keys overflowed its LDS hash")
+        if getattr(self, "err", None) is not None and self.mode in ("part", "tp") and \
+                int(self.err.item()):
+            raise RuntimeError(f"localize_{self.mode}: a bucket overflowed its LDS capacity")
 
     def __call__(self, keys: torch.Tensor) -> Localized:
         n = keys.numel()
@@ -212,6 +238,13 @@ class Localizer:
                             self.seg_start, self.t_ent_uid, self.local_col, self.n_uniq,
                             self.grad)
             tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum)
+            return Localized(self.uniq, self.seg_start, self.pos_s, self.segid,
+                             self.local_col[:n], self.n_uniq, self.grad, None, n, tile=tile)
+        if self.mode == "tp":
+            H.localize_tp(keys, self.bits, self.ptemp, self.t_dcnt, self.t_rep, self.pos_s,
+                          self.segid, self.uniq, self.seg_start, self.t_ent_uid, self.local_col,
+                          self.n_uniq, self.t_nent, self.grad, self.err)
+            tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum, 8192)
             return Localized(self.uniq, self.seg_start, self.pos_s, self.segid,
                              self.local_col[:n], self.n_uniq, self.grad, None, n, tile=tile)
         if self.mode == "part":
