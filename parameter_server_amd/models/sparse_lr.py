@@ -71,8 +71,9 @@ class SparseLRConfig:
     countmin_k: int = 2
     consistency: str = "bsp"             # bsp | ssp:<tau> | asp
     push_mode: str = "sequential"        # sequential | aggregate
-    localize: str = "sort"               # sort | tile | bucket | hash | auto (tile: <= 31-bit
-                                         # keys, bucket/hash: <= 32-bit keys)
+    localize: str = "auto"               # auto (= tp where supported, else sort) | tp | sort |
+                                         # tile | part | bucket | hash (tp / tile: <= 31-bit
+                                         # keys, bucket / hash / part: <= 32-bit keys)
     fixing_float_bytes: int = 0          # 0 = off, else 1..7 bytes per pushed gradient
     # multi-GPU data plane: "padded" = fixed-capacity rows per peer with device-side
     # counts (no host sync, graph-replayable); "exact" = count exchange + sized
@@ -110,12 +111,12 @@ class SparseLRTrainer:
         self.table = KVTable(cap, self.device, cfg.init, key_range=self.part.range_of(self.rank))
         self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
         mode = cfg.localize
-        if mode == "auto":  # tile dedup + sort of the tile-distinct keys (<= 31-bit keys)
-            mode = "tile"
-        if cfg.tail_feature_freq > 0 and mode in ("tile", "hash"):
+        if mode == "auto":  # tile dedup + key-range buckets (Localizer falls back to sort
+            mode = "tp"     # for > 31-bit keys or > 5.2 M keys per minibatch)
+        if cfg.tail_feature_freq > 0 and mode in ("tile", "hash", "tp"):
             mode = "sort"  # the tail filter needs per-key nnz counts (seg_start over nnz)
-        self.localize_mode = mode
         self.localizer = Localizer(self.max_nnz, self.bits, self.device, mode=mode)
+        self.localize_mode = self.localizer.mode  # after the Localizer's fallbacks
         self._localizers = [self.localizer]  # + a second buffer set for prefetching (G > 1)
         self.filter = (CountMinSketch(int(cfg.countmin_n), cfg.countmin_k, self.device)
                        if cfg.tail_feature_freq > 0 else None)

@@ -245,8 +245,9 @@ class Localizer:
                           self.segid, self.uniq, self.seg_start, self.t_ent_uid, self.local_col,
                           self.n_uniq, self.t_nent, self.grad, self.err)
             tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum, 8192)
-            return Localized(self.uniq, self.seg_start, self.pos_s, self.segid,
-                             self.local_col[:n], self.n_uniq, self.grad, None, n, tile=tile)
+            # unique keys <= n: expose n-sized views (the workspace is tile-rounded)
+            return Localized(self.uniq[:n], self.seg_start, self.pos_s, self.segid,
+                             self.local_col[:n], self.n_uniq, self.grad[:n], None, n, tile=tile)
         if self.mode == "part":
             H.localize_part(keys, self.bits, self.ptemp, self.pos_s, self.segid, self.uniq,
                             self.seg_start, self.local_col, self.n_uniq, self.grad, self.hess,
