@@ -30,7 +30,7 @@ bool tploc_supported(int64_t, int);
 size_t tploc_temp_bytes(int64_t, int);
 void localize_tp(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint16_t*, int32_t*,
                  int32_t*, uint64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, float*,
-                 int32_t*, int64_t, hipStream_t);
+                 int32_t*, int64_t, uint64_t*, hipStream_t);
 void tp_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
                  const float*, int64_t, float*, const int32_t*, const int32_t*, const int32_t*,
                  float*, int64_t, hipStream_t);
@@ -367,7 +367,8 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("tploc_temp_bytes", [](int64_t n, int bits) { return (int64_t)psamd::tploc_temp_bytes(n, bits); });
   m.def("localize_tp", [](Tensor keys, int bits, Tensor temp, Tensor dcnt, Tensor rep, Tensor pos_s,
                           Tensor segid, Tensor uniq, Tensor seg_start, Tensor ent_uid,
-                          Tensor local_col, Tensor n_uniq, Tensor n_ent, Tensor grad, Tensor err) {
+                          Tensor local_col, Tensor n_uniq, Tensor n_ent, Tensor grad, Tensor err,
+                          optional<Tensor> prof) {
     chk(keys, at::kLong, "keys");
     chk(temp, at::kByte, "temp");
     chk(dcnt, at::kInt, "dcnt");
@@ -396,7 +397,9 @@ PYBIND11_MODULE(_hipops, m) {
                        ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<uint64_t>(uniq),
                        ptr<int32_t>(seg_start), ptr<int32_t>(ent_uid), ptr<int32_t>(local_col),
                        ptr<int32_t>(n_uniq), ptr<int32_t>(n_ent), ptr<float>(grad),
-                       ptr<int32_t>(err), uniq.numel(), cur_stream());
+                       ptr<int32_t>(err), uniq.numel(),
+                       reinterpret_cast<uint64_t*>(optr<int64_t>(prof, at::kLong, "prof")),
+                       cur_stream());
   });
   m.def("tp_backward", [](Tensor rep, Tensor dcnt, int64_t n, optional<Tensor> rows, int width,
                           optional<Tensor> vals, Tensor coef, Tensor psum, Tensor pos_s,

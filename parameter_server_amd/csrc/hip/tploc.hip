@@ -40,9 +40,10 @@ constexpr int kThr = 1024;              // tile workgroup
 constexpr int kIt = 8;
 constexpr int kTile = kThr * kIt;       // 8192 occurrences
 constexpr int kHash = 2 * kTile;        // LDS hash slots of a tile (load <= 0.5)
-constexpr int kMaxBk = 4096;            // buckets
+constexpr int kMaxBk = 2048;            // buckets (tile LDS: 72 KB -> 2 workgroups per CU)
 constexpr int kMaxT = 640;              // tiles (n <= 5.2 M)
-constexpr int kBThr = 256;              // bucket / emit workgroups
+constexpr int kBThr = 256;              // emit workgroups
+constexpr int kBkThr = 512;             // bucket workgroups
 constexpr int kECap = 4096;             // entries of one bucket held in LDS
 constexpr int kDH = 2048;               // distinct-key hash of one bucket
 constexpr uint32_t kEmpty = 0xffffffffu;
@@ -155,7 +156,7 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
     rr[q] = k != kEmpty ? atomicAdd(&cnt[k >> shift], 1u) : kEmpty;
   }
   __syncthreads();
-  // exclusive scan of the bucket counts (nbk <= kMaxBk: 8 per thread)
+  // exclusive scan of the bucket counts (nbk <= kMaxBk: 2 per thread)
   constexpr int kDP = kMaxBk / kThr;
   uint32_t c[kDP], s = 0;
 #pragma unroll
@@ -205,43 +206,47 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
 
 // ---------------------------------------------------------------------- bucket
 // One workgroup per bucket b (a range of the mixed key space):
-//   gather   the bucket's entries from every tile, in tile order (flat: every
-//            thread loads independent entries, the tile of an entry found by binary
-//            search over the per-tile run prefix); entry ids go straight to beid
-//   dedup    LDS hash of the distinct keys with entry counts; rank sort of the
-//            distinct keys (rank = number of smaller keys: one pass, no bitonic
-//            network of barriers)
-//   rank     every wave walks its quarter of the entries in order twice: per-wave
-//            per-key counts, then ranks = bucket-local segment start + entries of the
-//            key in earlier quarters + earlier lanes (deterministic CSC)
-// Outputs per bucket (scratch): sorted distinct keys + local segment starts, and per
-// entry (gather order) its entry id and (distinct index | local CSC position << 16).
-__global__ void __launch_bounds__(tp::kBThr)
+//   gather+insert  the bucket's entries from every tile (flat: each thread locates its
+//                  entries by binary search over the per-tile run prefix and loads them
+//                  together), each key inserted into an LDS hash with an entry count;
+//                  the entry's hash slot is kept, its entry id goes straight to beid
+//   compact        occupied slots -> (key | count | slot) list
+//   rank sort      distinct keys are unique: rank = number of smaller keys (one pass
+//                  of broadcast LDS reads instead of a bitonic network of barriers)
+//   starts         exclusive prefix of the counts in key order -> dkey / dstart, and
+//                  per slot: sorted index + cursor
+//   assign         every entry takes the next position of its key's segment (LDS
+//                  atomic: the order inside a segment is not fixed)
+// Per-phase shader-clock marks (prof != null) are a tuning aid
+// (benchmarks/prof_tp_phases.py): each phase of the earlier walk-based version cost
+// 1.5-6 K cycles, so phases, not work, set the time of a workgroup.
+__global__ void __launch_bounds__(tp::kBkThr)
 tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbk,
                  int T, uint32_t* __restrict__ dkey, uint16_t* __restrict__ dstart,
                  int32_t* __restrict__ beid, uint32_t* __restrict__ bjp,
                  uint32_t* __restrict__ dcount, uint32_t* __restrict__ ecount,
-                 int32_t* __restrict__ err) {
+                 int32_t* __restrict__ err, uint64_t* __restrict__ prof) {
   using namespace tp;
-  constexpr int kWv = kBThr / 64;
-  __shared__ uint32_t ek[kECap];
-  __shared__ uint64_t sbuf[kDH];   // hash (keys | counts), then the sorted (key | start)
-  __shared__ uint64_t ubuf[(kECap * 2 + kWv * kDH * 2) / 8];  // compacted list, then ej + cntw
+#define TP_MARK(k) \
+  if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 12 + (k)] = clock64();
+  TP_MARK(0)
+  __shared__ uint16_t eh[kECap];    // hash slot of every gathered entry
+  __shared__ uint64_t hs[kDH];      // hash (key u32 | count u32), then the sorted list
+  __shared__ uint64_t dl[kDH];      // compacted (key | count << 16 | slot), then cur/jj
   __shared__ uint32_t tpre[kMaxT + 1];
   __shared__ uint16_t tlo[kMaxT];
-  __shared__ uint32_t lds[kBThr / 64 + 1];
-  uint32_t* hkey = reinterpret_cast<uint32_t*>(sbuf);
+  __shared__ uint32_t lds[kBkThr / 64 + 1];
+  uint32_t* hkey = reinterpret_cast<uint32_t*>(hs);
   uint32_t* hcnt = hkey + kDH;
-  uint64_t* dl = ubuf;                                           // [kDH]
-  uint16_t* ej = reinterpret_cast<uint16_t*>(ubuf);              // [kECap]
-  uint16_t* cntw = ej + kECap;                                   // [kWv][kDH]
-  const int t = threadIdx.x, b = blockIdx.x, lane = t & 63, wv = t >> 6;
-  for (int s = t; s < kDH; s += kBThr) {
+  uint32_t* cur = reinterpret_cast<uint32_t*>(dl);    // [kDH] per slot, after the sort
+  uint16_t* jj = reinterpret_cast<uint16_t*>(cur + kDH);  // [kDH] per slot
+  const int t = threadIdx.x, b = blockIdx.x;
+  for (int s = t; s < kDH; s += kBkThr) {
     hkey[s] = kEmpty;
     hcnt[s] = 0;
   }
   // per-tile runs [toff[q][b], toff[q][b+1]): thread t owns tiles [t*per, t*per + per)
-  const int per = (T + kBThr - 1) / kBThr;
+  const int per = (T + kBkThr - 1) / kBkThr;
   const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
   uint32_t c = 0;
   for (int q = q0; q < q1; ++q) {
@@ -252,7 +257,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     c += hi - lo;
   }
   uint32_t E;
-  uint32_t w = tp_block_scan<kBThr>(c, lds, &E);
+  uint32_t w = tp_block_scan<kBkThr>(c, lds, &E);
   for (int q = q0; q < q1; ++q) {
     const uint32_t len = tpre[q];
     tpre[q] = w;
@@ -260,30 +265,42 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
   }
   if (t == 0) tpre[T] = E;
   __syncthreads();
+  TP_MARK(1)
   const uint32_t En = E < (uint32_t)kECap ? E : (uint32_t)kECap;
   bool bad = E > (uint32_t)kECap;
   int32_t* be = beid + (int64_t)b * kECap;
-  for (uint32_t g = t; g < En; g += kBThr) {
-    int lo = 0, hi = T - 1;  // last tile with tpre[q] <= g
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (tpre[mid] <= g) lo = mid; else hi = mid - 1;
+  constexpr int kG = kECap / kBkThr;  // entries per thread: locate all, then load all
+  int64_t idx[kG];
+#pragma unroll
+  for (int q = 0; q < kG; ++q) {
+    const uint32_t g = q * kBkThr + t;
+    idx[q] = -1;
+    if (g < En) {
+      int lo = 0, hi = T - 1;  // last tile with tpre[q] <= g
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tpre[mid] <= g) lo = mid; else hi = mid - 1;
+      }
+      idx[q] = (int64_t)lo * kTile + tlo[lo] + (g - tpre[lo]);
     }
-    const int64_t idx = (int64_t)lo * kTile + tlo[lo] + (g - tpre[lo]);
-    ek[g] = tkeys[idx];
-    be[g] = (int32_t)idx;
   }
-  __syncthreads();
-  for (uint32_t g = t; g < En; g += kBThr) {
-    const uint32_t key = ek[g];
+  uint32_t kv[kG];
+#pragma unroll
+  for (int q = 0; q < kG; ++q) kv[q] = idx[q] >= 0 ? tkeys[idx[q]] : 0u;
+#pragma unroll
+  for (int q = 0; q < kG; ++q) {
+    if (idx[q] < 0) continue;
+    const uint32_t g = q * kBkThr + t;
+    be[g] = (int32_t)idx[q];
+    const uint32_t key = kv[q];
     uint32_t h = tp_hash(key) & (kDH - 1);
     bool ok = false;
     for (int p = 0; p < kDH / 2; ++p) {
-      const uint32_t cur = hkey[h];
-      if (cur == kEmpty) {
+      const uint32_t cu = hkey[h];
+      if (cu == kEmpty) {
         const uint32_t prev = atomicCAS(&hkey[h], kEmpty, key);
         if (prev == kEmpty || prev == key) { ok = true; break; }
-      } else if (cur == key) {
+      } else if (cu == key) {
         ok = true;
         break;
       }
@@ -291,105 +308,74 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     }
     if (ok) atomicAdd(&hcnt[h], 1u);
     else bad = true;
+    eh[g] = ok ? (uint16_t)h : (uint16_t)0xffffu;
   }
   if (bad) atomicOr(err, 1);
   __syncthreads();
+  TP_MARK(2)
   // compact the occupied slots (strided: conflict-free LDS reads)
-  constexpr int kPer = kDH / kBThr;  // 8
+  constexpr int kPer = kDH / kBkThr;  // 4
   uint64_t ent[kPer];
   uint32_t cc = 0;
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
-    const int s = q * kBThr + t;
-    ent[q] = hkey[s] != kEmpty ? (((uint64_t)hkey[s] << 32) | hcnt[s]) : ~0ull;
+    const int s = q * kBkThr + t;
+    ent[q] = hkey[s] != kEmpty
+                 ? (((uint64_t)hkey[s] << 32) | ((uint64_t)hcnt[s] << 16) | (uint64_t)s)
+                 : ~0ull;
     cc += ent[q] != ~0ull;
   }
   uint32_t D;
-  uint32_t wd = tp_block_scan<kBThr>(cc, lds, &D);
+  uint32_t wd = tp_block_scan<kBkThr>(cc, lds, &D);
 #pragma unroll
   for (int q = 0; q < kPer; ++q)
     if (ent[q] != ~0ull) dl[wd++] = ent[q];
   __syncthreads();
-  // rank sort: keys are distinct, rank = number of smaller keys (broadcast LDS reads)
-  for (uint32_t i = t; i < D; i += kBThr) {
+  TP_MARK(3)
+  // rank sort into hs (the hash is dead): keys are distinct, rank = # smaller keys
+  for (uint32_t i = t; i < D; i += kBkThr) {
     const uint64_t x = dl[i];
     uint32_t r = 0;
     for (uint32_t q = 0; q < D; ++q) r += dl[q] < x;
-    sbuf[r] = x;
+    hs[r] = x;
   }
   __syncthreads();
-  // local segment starts: exclusive prefix of the sorted counts (chunks of kBThr);
-  // sbuf[j] becomes (key << 32 | start)
+  TP_MARK(4)
+  // local segment starts in key order; per slot: sorted index + cursor (dl is dead)
   uint32_t carry = 0;
-  for (uint32_t j0 = 0; j0 < D; j0 += kBThr) {
+  for (uint32_t j0 = 0; j0 < D; j0 += kBkThr) {
     const uint32_t j = j0 + t;
-    const uint64_t v = j < D ? sbuf[j] : 0ull;
+    const uint64_t v = j < D ? hs[j] : 0ull;
+    const uint32_t cnt = (uint32_t)(v >> 16) & 0xffffu;
     uint32_t tot;
-    const uint32_t ex = tp_block_scan<kBThr>((uint32_t)(v & 0xffffffffull), lds, &tot) + carry;
+    const uint32_t ex = tp_block_scan<kBkThr>(cnt, lds, &tot) + carry;
     if (j < D) {
+      const uint32_t slot = (uint32_t)v & 0xffffu;
       dkey[(int64_t)b * kDH + j] = (uint32_t)(v >> 32);
       dstart[(int64_t)b * kDH + j] = (uint16_t)ex;
-      sbuf[j] = (v & 0xffffffff00000000ull) | ex;
+      cur[slot] = ex;
+      jj[slot] = (uint16_t)j;
     }
     carry += tot;
   }
-  for (int s = t; s < kWv * kDH; s += kBThr) cntw[s] = 0;  // (dl is dead)
   __syncthreads();
+  TP_MARK(5)
   if (t == 0) {
     dcount[b] = D;
     ecount[b] = En;
   }
-  // walk 1: wave wv owns entries [wv*Q, wv*Q + Q): distinct index + per-wave counts
-  constexpr int kHB = __builtin_ctz(kDH);
-  const uint32_t Q = (En + kWv - 1) / kWv;
-  const uint32_t g_lo = wv * Q, g_hi = g_lo + Q < En ? g_lo + Q : En;
-  for (uint32_t g0 = g_lo; g0 < g_hi; g0 += 64) {
-    const uint32_t g = g0 + lane;
-    uint32_t j = 0xffffu;
-    if (g < g_hi && D > 0) {
-      const uint32_t key = ek[g];
-      int lo = 0, hi = (int)D - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if ((uint32_t)(sbuf[mid] >> 32) < key) lo = mid + 1; else hi = mid;
-      }
-      if ((uint32_t)(sbuf[lo] >> 32) == key) j = (uint32_t)lo;
-    }
-    const bool ok = j != 0xffffu;
-    const uint64_t peers = tp_match_any(j, kHB, __ballot(ok));
-    if (ok && (peers & ((1ull << lane) - 1ull)) == 0ull)
-      cntw[wv * kDH + j] += (uint16_t)__popcll(peers);
-    if (g < g_hi) ej[g] = (uint16_t)j;
-  }
-  __syncthreads();
-  // per key: the bucket-local start of each wave's run of it
-  for (uint32_t j = t; j < D; j += kBThr) {
-    uint32_t run = (uint32_t)sbuf[j];
-#pragma unroll
-    for (int q = 0; q < kWv; ++q) {
-      const uint32_t cq = cntw[q * kDH + j];
-      cntw[q * kDH + j] = (uint16_t)run;
-      run += cq;
-    }
-  }
-  __syncthreads();
-  // walk 2: ranks in order
   uint32_t* bj = bjp + (int64_t)b * kECap;
-  for (uint32_t g0 = g_lo; g0 < g_hi; g0 += 64) {
-    const uint32_t g = g0 + lane;
-    const uint32_t j = g < g_hi ? ej[g] : 0xffffu;
-    const bool ok = j != 0xffffu;
-    const uint64_t peers = tp_match_any(j, kHB, __ballot(ok));
-    const uint64_t below = peers & ((1ull << lane) - 1ull);
-    uint32_t rbase = 0;
-    if (ok && below == 0ull) {
-      rbase = cntw[wv * kDH + j];
-      cntw[wv * kDH + j] = (uint16_t)(rbase + (uint32_t)__popcll(peers));
+  for (uint32_t g = t; g < En; g += kBkThr) {
+    const uint32_t h = eh[g];
+    if (h == 0xffffu) {
+      bj[g] = 0xffffffffu;
+      continue;
     }
-    const int leader = ok ? (int)(__ffsll((long long)peers) - 1) : lane;
-    rbase = __shfl(rbase, leader, 64);
-    if (g < g_hi) bj[g] = ok ? (j | ((rbase + (uint32_t)__popcll(below)) << 16)) : 0xffffffffu;
+    const uint32_t pos = atomicAdd(&cur[h], 1u);
+    bj[g] = (uint32_t)jj[h] | (pos << 16);
   }
+  TP_MARK(6)
+#undef TP_MARK
 }
 
 // ------------------------------------------------------------------------ emit
@@ -517,7 +503,35 @@ tp_bwd_accum_cols_kernel(const uint16_t* __restrict__ rep, const int32_t* __rest
   const int nseg = (nr + L - 1) / L;
   const int slot = t % width, seg = t / width;
   __syncthreads();
-  if (seg < nseg) {
+  constexpr int kL = 16;  // rows a thread prefetches into registers before its walk
+  if (seg < nseg && L <= kL) {
+    const int ra = seg * L;
+    uint32_t ee[kL];
+    float vv[kL];
+#pragma unroll
+    for (int q = 0; q < kL; ++q) {  // every load of the walk in flight at once
+      const int rl = ra + q;
+      const int64_t r = r0 + rl;
+      const int64_t i = r * width + slot;
+      const bool ok = q < L && rl < nr && i >= base && i < base + lim && in_range(r, B);
+      ee[q] = ok ? (uint32_t)rep[i] : 0xffffffffu;
+      vv[q] = ok ? coef[r] * (vals ? vals[i] : 1.f) : 0.f;
+    }
+    uint32_t cur = 0xffffffffu;
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < kL; ++q) {
+      if (ee[q] == 0xffffffffu) continue;
+      if (ee[q] != cur) {
+        if (cur != 0xffffffffu && sum != 0.f) atomicAdd(&acc[cur], sum);
+        cur = ee[q];
+        sum = vv[q];
+      } else {
+        sum += vv[q];
+      }
+    }
+    if (cur != 0xffffffffu && sum != 0.f) atomicAdd(&acc[cur], sum);
+  } else if (seg < nseg) {
     const int ra = seg * L, rb = ra + L < nr ? ra + L : nr;
     uint32_t cur = 0xffffffffu;
     float sum = 0.f;
@@ -600,7 +614,7 @@ static TpGeom tp_geom(int64_t n, int bits) {
   // bucket's distinct keys stay under kDH / 2 (measured on Criteo-shaped batches:
   // <= 1615 entries and 157 distinct keys per bucket at 2048 buckets)
   int bb = 0;
-  while (bb < 12 && (n >> bb) > 1280) ++bb;
+  while (bb < 11 && (n >> bb) > 1280) ++bb;
   if (bb > bits) bb = bits;
   g.nbk = 1 << bb;
   g.shift = bits - bb;
@@ -610,7 +624,7 @@ static TpGeom tp_geom(int64_t n, int bits) {
 int64_t tploc_stride(int64_t n) { return tp_geom(n, 31).N; }
 
 bool tploc_supported(int64_t n, int bits) {
-  return bits >= 2 && bits <= 31 && n > 0 && (n >> 12) <= 1280 &&
+  return bits >= 2 && bits <= 31 && n > 0 && (n >> 11) <= 1280 &&
          (n + tp::kTile - 1) / tp::kTile <= tp::kMaxT;
 }
 
@@ -629,7 +643,8 @@ size_t tploc_temp_bytes(int64_t n, int bits) {
 void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
                  int32_t* dcnt, uint16_t* rep, int32_t* pos_s, int32_t* segid, uint64_t* uniq,
                  int32_t* seg_start, int32_t* ent_uid, int32_t* local_col, int32_t* n_uniq,
-                 int32_t* n_ent, float* grad, int32_t* err, int64_t u_cap, hipStream_t st) {
+                 int32_t* n_ent, float* grad, int32_t* err, int64_t u_cap, uint64_t* prof,
+                 hipStream_t st) {
   if (n <= 0) return;
   if (!tploc_supported(n, m.bits)) throw std::runtime_error("localize_tp: unsupported size");
   if (temp_bytes < tploc_temp_bytes(n, m.bits)) throw std::runtime_error("localize_tp: temp");
@@ -647,8 +662,9 @@ void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t te
   tp_tile_kernel<<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff, dcnt,
                                                      rep);
   PSAMD_HIP_CHECK(hipGetLastError());
-  tp_bucket_kernel<<<(unsigned)g.nbk, tp::kBThr, 0, st>>>(tkeys, toff, g.nbk, (int)g.T, dkey,
-                                                          dstart, beid, bjp, dcount, ecount, err);
+  tp_bucket_kernel<<<(unsigned)g.nbk, tp::kBkThr, 0, st>>>(tkeys, toff, g.nbk, (int)g.T, dkey,
+                                                          dstart, beid, bjp, dcount, ecount, err,
+                                                          prof);
   PSAMD_HIP_CHECK(hipGetLastError());
   tp_emit_kernel<<<(unsigned)g.nbk, tp::kBThr, 0, st>>>(g.nbk, dkey, dstart, beid, bjp, dcount,
                                                         ecount, pos_s, segid, uniq, seg_start,
@@ -671,7 +687,7 @@ void tp_backward(const uint16_t* rep, const int32_t* dcnt, int64_t n, const int3
     tp_bwd_accum_kernel<<<(unsigned)g.T, tp::kThr, 0, st>>>(rep, dcnt, n, rows, width, vals, coef,
                                                             B, psum);
   PSAMD_HIP_CHECK(hipGetLastError());
-  tp_seg_reduce_kernel<<<grid_for(g.N, 256, 8192), 256, 0, st>>>(pos_s, segid, g.N, n_ent, psum,
+  tp_seg_reduce_kernel<<<grid_for(g.N, 256, 2048), 256, 0, st>>>(pos_s, segid, g.N, n_ent, psum,
                                                                  g.N, grad, grad_cap);
   PSAMD_HIP_CHECK(hipGetLastError());
 }

@@ -243,7 +243,8 @@ class Localizer:
         if self.mode == "tp":
             H.localize_tp(keys, self.bits, self.ptemp, self.t_dcnt, self.t_rep, self.pos_s,
                           self.segid, self.uniq, self.seg_start, self.t_ent_uid, self.local_col,
-                          self.n_uniq, self.t_nent, self.grad, self.err)
+                          self.n_uniq, self.t_nent, self.grad, self.err,
+                          getattr(self, "tp_prof", None))
             tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum, 8192)
             # unique keys <= n: expose n-sized views (the workspace is tile-rounded)
             return Localized(self.uniq[:n], self.seg_start, self.pos_s, self.segid,

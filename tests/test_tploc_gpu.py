@@ -46,9 +46,8 @@ def _check(k, bits, width=39):
     key_of_eid = torch.full(((int(tiles.max()) + 1) * TILE,), -1, dtype=torch.int64)
     key_of_eid[eid_of_occ] = mk
     assert torch.equal(key_of_eid[pos], ref.uniq[segid - 1])
-    # within a key's segment the entries are in tile order (deterministic)
-    same = segid[1:] == segid[:-1]
-    assert torch.all(pos[1:][same] > pos[:-1][same])
+    # every entry exactly once
+    assert torch.equal(torch.sort(pos).values, torch.unique(eid_of_occ))
     # backward
     B = (n + width - 1) // width
     coef = torch.randn(B, device=DEV)
