@@ -304,6 +304,9 @@ def main():
     ap.add_argument("--emulate-backend", default="copy", choices=["copy", "nccl"],
                     help="emulated peers: exchanges as stream copies, or through a real "
                          "1-rank RCCL communicator (RCCL kernels + ProcessGroupNCCL waits)")
+    ap.add_argument("--prefill", type=float, default=0,
+                    help="insert this many random keys into each shard before timing (the "
+                         "populated-table regime, e.g. 5e8 on 2^31 slots = 23%% load)")
     ap.add_argument("--progress", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check)")
     ap.add_argument("--trace", default="",
@@ -339,6 +342,14 @@ def main():
                          localize=args.localize, push_mode=args.push_mode,
                          seed=rank)
     tr = SparseLRTrainer(cfg, comm, device)
+    prefill_occ = None
+    if args.prefill > 0:
+        t0 = time.time()
+        prefill_occ = tr.prefill(int(args.prefill))
+        if rank == 0:
+            print(f"prefill: {prefill_occ} occupied slots of {tr.table.capacity} "
+                  f"({prefill_occ / tr.table.capacity:.1%}) in {time.time() - t0:.1f} s",
+                  file=sys.stderr, flush=True)
     keys = torch.empty(B * 39, dtype=torch.int64, device=device)
     labels = torch.empty(B, dtype=torch.float32, device=device)
     seed = 1000003 * (rank + 1)
@@ -465,6 +476,7 @@ def main():
                 "emulated_peers": G if emulated else None,
                 "exchange": (f"{args.exchange} (capacity {tr.xc.C} keys/peer/step)"
                              if tr.xc is not None else (args.exchange if G > 1 else None)),
+                "prefill_keys_per_gpu": int(args.prefill) if args.prefill > 0 else None,
             },
             "train": {"loss": prog["loss"], "auc": prog["auc"], "accuracy": prog["accuracy"],
                       "table_occupied_rank0": occ, "nnz_w_rank0": nnz},

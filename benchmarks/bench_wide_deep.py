@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--emulate-peers", type=int, default=0,
                     help="1 process: the N-GPU step (key exchange + owner updates + dense "
                          "all-reduce) with N emulated peers over a loopback comm")
+    ap.add_argument("--prefill", type=float, default=0,
+                    help="random keys (with rows) inserted per GPU before timing")
     args = ap.parse_args()
     from parameter_server_amd.models.wide_deep import WideDeepConfig, WideDeepTrainer
     from parameter_server_amd.ops.synthetic import criteo_batch
@@ -50,6 +52,13 @@ def main():
                          table_capacity=args.table_slots, gemm=args.gemm, seed=0,
                          overlap_wgrad=bool(args.overlap_wgrad))
     tr = WideDeepTrainer(cfg, comm, dev)
+    if args.prefill > 0:
+        import time as _t
+
+        t0 = _t.time()
+        occ = tr.prefill(int(args.prefill))
+        print(f"prefill: {occ} occupied of {tr.shard.capacity} slots "
+              f"({occ / tr.shard.capacity:.1%}) in {_t.time() - t0:.1f} s", flush=True)
     bufs = [(torch.empty(B * 39, dtype=torch.int64, device=dev),
              torch.empty(B, dtype=torch.float32, device=dev)) for _ in range(2)]
     t = [0]

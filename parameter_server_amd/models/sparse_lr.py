@@ -156,6 +156,24 @@ class SparseLRTrainer:
         self.comm_bytes = 0
         self.t0 = time.time()
 
+    def prefill(self, count: int, chunk: int = 1 << 24, seed: int = 12345) -> int:
+        """Insert ``count`` random keys of this shard's mixed-key range (zero state), so
+        a benchmark can measure the populated-table regime (probe lengths, TLB / DRAM
+        page behaviour of a large table) instead of an almost empty one. Returns the
+        occupied slots afterwards. (Reference: KVStore grows its hash map with every
+        new key, src/parameter/kv_store.h:37-57.)"""
+        lo, hi = self.part.range_of(self.rank)
+        g = torch.Generator(device=self.device).manual_seed(seed + self.rank)
+        done = 0
+        while done < count:
+            n = min(chunk, count - done)
+            mk = torch.randint(lo, min(hi, 1 << 63), (n,), generator=g, device=self.device,
+                               dtype=torch.int64)
+            self.table.resolve(mk, insert=True, with_w=False)
+            done += n
+        self.table.check_ok()
+        return self.table.census()[0]
+
     @staticmethod
     def auto_capacity(cfg: SparseLRConfig, G: int, bits: int) -> int:
         n = cfg.num_features if cfg.num_features else (1 << 27)

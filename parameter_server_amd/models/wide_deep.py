@@ -155,6 +155,21 @@ class EmbeddingPS:
         self.step_count = int(sd.get("step", 0))
         self.examples = int(sd.get("examples", 0))
 
+    def prefill(self, count: int, chunk: int = 1 << 23, seed: int = 12345) -> int:
+        """Insert ``count`` random keys of this shard's mixed-key range with initialised
+        rows (the populated-table regime of a long run); returns the occupied slots."""
+        lo, hi = self.part.range_of(self.rank)
+        g = torch.Generator(device=self.device).manual_seed(seed + self.rank)
+        done = 0
+        while done < count:
+            n = min(chunk, count - done)
+            mk = torch.randint(lo, min(hi, 1 << 63), (n,), generator=g, device=self.device,
+                               dtype=torch.int64)
+            self.shard.resolve(mk)
+            done += n
+        self.shard.table.check_ok()
+        return self.shard.table.census()[0]
+
     # ------------------------------------------------------------ exchange (G > 1)
     _xe = None  # padded-exchange state (GPU, G > 1)
 
