@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--l1", type=float, default=10.0)
     ap.add_argument("--tail-freq", type=int, default=4)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--host-preprocess", action="store_true",
+                    help="build the CSC with numpy (reference path) instead of on the GPU")
+    ap.add_argument("--device-data", action="store_true",
+                    help="keep the generated slots on the GPU (no host copy / upload)")
     args = ap.parse_args()
 
     from parameter_server_amd.data.synthetic import criteo_slots
@@ -41,9 +45,11 @@ def main():
     G, rank = comm.world, comm.rank
     t0 = time.time()
     sd = criteo_slots(args.rows, seed=17, row0=rank * args.rows,
-                      num_features=int(args.num_features), device=device)
+                      num_features=int(args.num_features), device=device,
+                      on_device=args.device_data and not args.cpu)
     cfg = DarlinConfig(l1=args.l1, tau=args.tau, tail_freq=args.tail_freq,
-                       max_pass=args.passes + args.warmup, epsilon=0.0, seed=0)
+                       max_pass=args.passes + args.warmup, epsilon=0.0, seed=0,
+                       host_preprocess=args.host_preprocess)
     tr = DarlinTrainer(sd, cfg, comm=comm, device=device)
     prep = time.time() - t0
     for it in range(args.warmup):
@@ -74,6 +80,9 @@ def main():
                        "blocks": len(tr.blocks), "tau": args.tau, "l1": args.l1,
                        "tail_freq": args.tail_freq},
             "preprocess_sec": prep,
+            "trainer_preprocess_sec": tr.preprocess_time,
+            "preprocess_breakdown_sec": tr.prep_times,
+            "preprocess_path": "host numpy" if args.host_preprocess else "gpu",
             "train": {"objective": p.objective, "relative_obj": p.relative_obj,
                       "nnz_w": p.nnz_w, "active_set": p.nnz_active_set},
         }), flush=True)

@@ -41,12 +41,23 @@ def sparse_classification(rows: int, groups=(1, 2, 3), keys_per_group: int = 100
 
 
 def criteo_slots(rows: int, *, seed: int = 0, row0: int = 0, num_features: int = 10 ** 9,
-                 alpha: float = 1.1, device="cpu") -> SlotData:
-    """Criteo-shaped slot data: group s+1 holds slot s (one key per example)."""
+                 alpha: float = 1.1, device="cpu", on_device: bool = False) -> SlotData:
+    """Criteo-shaped slot data: group s+1 holds slot s (one key per example).
+    ``on_device``: keep the groups as device tensors (keys int64 = raw uint64 bits) for
+    the GPU Darlin preprocessing, instead of host numpy arrays."""
     from ..ops.synthetic import NUM_SLOTS, criteo_batch
 
     keys, labels = criteo_batch(rows, seed=seed, row0=row0, num_features=num_features,
                                 alpha=alpha, device=device)
+    if on_device:
+        import torch
+
+        kd = keys.view(rows, NUM_SLOTS)
+        sd = SlotData(labels=labels.cpu().numpy().astype(np.float32))
+        off = torch.arange(rows + 1, dtype=torch.int64, device=keys.device)
+        for s in range(NUM_SLOTS):
+            sd.groups[s + 1] = (off, kd[:, s].contiguous(), None)
+        return sd
     k = keys.view(rows, NUM_SLOTS).cpu().numpy().view(np.uint64)
     sd = SlotData(labels=labels.cpu().numpy().astype(np.float32))
     off = np.arange(rows + 1, dtype=np.int64)

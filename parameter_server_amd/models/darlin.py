@@ -45,6 +45,7 @@ import torch
 
 from ..data.slot_reader import SlotData, merge_slot_info
 from ..ops import bcd
+from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.partition import even_divide
 
@@ -77,6 +78,7 @@ class DarlinConfig:
     tail_freq: int = 0              # tail_feature_freq
     init_w: float = 0.0             # init_w (ZERO / CONSTANT)
     seed: int = 0
+    host_preprocess: bool = False   # GPU trainer: build the CSC with numpy instead (reference)
 
     @classmethod
     def from_lm(cls, lm, seed: int = 0) -> "DarlinConfig":
@@ -216,6 +218,24 @@ class DarlinTrainer:
 
     def _preprocess(self, data: SlotData):
         cfg = self.cfg
+        sync = (lambda: torch.cuda.synchronize(self.device)) if self.device.type == "cuda" \
+            else (lambda: None)
+        t0 = time.time()
+        if self.device.type == "cuda" and not getattr(cfg, "host_preprocess", False):
+            col, row, val, colptr, base, nkeys = self._build_csc_gpu(data)
+        else:
+            col, row, val, colptr, base, nkeys = self._build_csc_host(data)
+        sync()
+        t1 = time.time()
+        self._finish_preprocess(data, col, row, val, colptr, base, nkeys)
+        sync()
+        self.prep_times = {"csc": t1 - t0, "blocks_and_row_copies": time.time() - t1}
+
+    def _build_csc_host(self, data: SlotData):
+        """Reference-shaped host preprocessing (numpy): per group np.unique, tail filter,
+        searchsorted column map, stable argsort CSR -> CSC (bcd.h:324-465,
+        sparse_matrix.h:186-241). The GPU path (``_build_csc_gpu``) produces the same
+        arrays bit for bit."""
         self.info = self._global_info(data)
         self.num_ex = int(self.info["num_ex"])
         rows = data.rows
@@ -251,7 +271,6 @@ class DarlinTrainer:
             if valued:
                 vals.append((np.ones(keys.size, np.float32) if v is None else v)[keep])
             base += gk.size
-        self.num_cols = base
         if base >= (1 << 31):
             raise ValueError("at most 2^31-1 global columns")
         col = np.concatenate(cols) if cols else np.zeros(0, np.int64)
@@ -261,13 +280,170 @@ class DarlinTrainer:
         val = np.concatenate(vals)[order] if valued else None
         colptr = np.zeros(base + 1, np.int64)
         np.cumsum(np.bincount(col, minlength=base), out=colptr[1:])
-        self.colptr = colptr
         dev = self.device
-        self.col = torch.from_numpy(col.astype(np.int32)).to(dev)
-        self.row = torch.from_numpy(row.astype(np.int32)).to(dev)
-        self.val = None if val is None else torch.from_numpy(val.astype(np.float32)).to(dev)
+        col = torch.from_numpy(col.astype(np.int32)).to(dev)
+        row = torch.from_numpy(row.astype(np.int32)).to(dev)
+        val = None if val is None else torch.from_numpy(val.astype(np.float32)).to(dev)
+        return col, row, val, colptr, base, len(gids)
+
+    # -------------------------------------------------------- GPU preprocess
+    def _group_tensors(self, data: SlotData, g: int):
+        """(offsets int64, keys int64 (raw uint64 bits), vals f32 | None) of group g on
+        the device; numpy groups are uploaded, device tensors used as they are."""
+        dev = self.device
+        off, keys, v = data.groups[g]
+        def up(x, dt):
+            if isinstance(x, torch.Tensor):
+                return x.to(dev, dt)
+            return torch.from_numpy(np.ascontiguousarray(x)).to(dev, dt, non_blocking=False)
+        k = keys if isinstance(keys, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(keys).view(np.int64))
+        return up(off, torch.int64), k.to(dev, torch.int64), \
+            (None if v is None else up(v, torch.float32))
+
+    def _sort_unique(self, keys: torch.Tensor, end_bit: int):
+        """Own radix sort (primitives.hip) + fused run-length encode (localize.hip) of
+        raw uint64 keys < 2^end_bit: (sorted unique keys, segment starts, positions in
+        key order (stable), 1-based segment id of every sorted position)."""
+        H = hipops()
+        n = keys.numel()
+        dev = keys.device
+        i32 = lambda m: torch.empty(m, dtype=torch.int32, device=dev)  # noqa: E731
+        temp = torch.empty(max(1, H.sort_pairs_temp_bytes(n, end_bit)), dtype=torch.uint8,
+                           device=dev)
+        hs = torch.empty_like(keys)
+        pos = torch.arange(n, dtype=torch.int32, device=dev)
+        pos_s = i32(n)
+        H.sort_pairs(temp, keys, hs, pos, pos_s, n, end_bit)
+        flags, segid, local_col = i32(n), i32(n), i32(n)
+        uniq = torch.empty(n, dtype=torch.int64, device=dev)
+        seg_start = i32(n + 1)
+        n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
+        scan_temp = torch.empty(max(1, H.scan_temp_bytes(n)), dtype=torch.uint8, device=dev)
+        H.rle(hs, pos_s, n, flags, segid, scan_temp, uniq, seg_start, local_col, n_uniq, None,
+              None)
+        U = int(n_uniq.item())
+        return uniq[:U], seg_start[:U + 1].to(torch.int64), pos_s, segid
+
+    def _group_keys_dev(self, uf: torch.Tensor, cnt: torch.Tensor, info_g) -> torch.Tensor:
+        """Device twin of ``_group_keys``: global sorted (flipped) kept keys of a group;
+        G > 1 sums the counts at owner ranks (all-to-all-v) and all-gathers the kept
+        lists (owner ranges are ordered, so the concatenation is sorted)."""
+        freq = self.cfg.tail_freq
+        if self.G == 1:
+            return uf[cnt > freq] if freq > 0 else uf
+        comm, dev = self.comm, self.device
+        lo = int(_flip(np.array([info_g["min_key"]], np.uint64))[0])
+        hi = int(_flip(np.array([info_g["max_key"] - 1], np.uint64))[0]) + 1
+        bounds = torch.tensor([even_divide(lo, hi, self.G, r)[0] for r in range(1, self.G)],
+                              dtype=torch.int64, device=dev)
+        owner = torch.searchsorted(bounds, uf, right=True)
+        sc = torch.bincount(owner, minlength=self.G).to(torch.int64)
+        rc = comm.exchange_counts(sc).cpu()
+        scl = sc.cpu()
+        rk = comm.all_to_all_v(uf.contiguous(), scl.tolist(), rc.tolist()).to(dev)
+        rn = comm.all_to_all_v(cnt.contiguous(), scl.tolist(), rc.tolist()).to(dev)
+        if rk.numel():
+            raw = rk ^ SIGN  # back to raw uint64 bits for the unsigned sort
+            end_bit = max(1, int(info_g["max_key"] - 1).bit_length())
+            u, seg, pos_s, segid = self._sort_unique(raw, end_bit)
+            tot = torch.zeros(u.numel(), dtype=torch.int64, device=dev)
+            tot.index_add_(0, segid[:rk.numel()].to(torch.int64) - 1, rn[pos_s[:rk.numel()].long()])
+            uf2 = u ^ SIGN
+            kept = uf2[tot > freq] if freq > 0 else uf2
+        else:
+            kept = torch.zeros(0, dtype=torch.int64, device=dev)
+        n = torch.full((self.G,), kept.numel(), dtype=torch.int64)
+        rcnt = comm.exchange_counts(n).cpu()
+        return comm.all_to_all_v(kept.repeat(self.G), n.tolist(), rcnt.tolist()).to(dev)
+
+    def _build_csc_gpu(self, data: SlotData):
+        """CSC of the rank's examples over the global column space, on the device:
+        per group one own radix sort + run-length encode of the keys (the sorted order
+        IS the group's CSC order: columns ascending, rows ascending inside a column,
+        so no separate transpose), tail filter on the device counts, global column
+        map by a device searchsorted; only the kept key lists and the column pointer
+        come back to the host (block division, model output). Same arrays as
+        ``_build_csc_host`` bit for bit (tests/test_darlin_gpu.py)."""
+        dev = self.device
+        H = hipops()
+        rows = data.rows
+        if rows >= (1 << 31):
+            raise ValueError("a rank holds at most 2^31-1 examples")
+        self.rows = rows
+        gt = {g: self._group_tensors(data, g) for g in sorted(data.groups)}
+        # ExampleInfo on the device: unsigned min / max via the flipped order
+        loc = {0: {"min_key": 0, "max_key": 1, "nnz_ele": rows, "nnz_ex": rows}}
+        for g, (off, k, _) in gt.items():
+            if k.numel() == 0:
+                continue
+            mn, mx = torch.aminmax(k ^ SIGN)
+            ne = int((off[1:] > off[:-1]).sum().item())
+            mn, mx = int(mn.item()) + (1 << 63), int(mx.item()) + (1 << 63)  # unflip
+            loc[g] = {"min_key": mn, "max_key": mx + 1,
+                      "nnz_ele": int(k.numel()), "nnz_ex": ne}
+        local_info = {"num_ex": rows, "slots": loc}
+        infos = self.comm.all_gather_obj(local_info) if self.G > 1 else [local_info]
+        self.info = merge_slot_info(infos)
+        self.num_ex = int(self.info["num_ex"])
+        gids = sorted(g for g in self.info["slots"] if g != 0)
+        valued = any(gt.get(g, (None, None, None))[2] is not None for g in gids)
+        self.group_keys, self.group_base = {}, {}
+        cols, rws, vals, counts = [], [], [], []
+        base = 0
+        for g in gids:
+            off, k, v = gt.get(g, (None, torch.zeros(0, dtype=torch.int64, device=dev), None))
+            n = k.numel()
+            info_g = self.info["slots"][g]
+            if n:
+                end_bit = max(1, int(info_g["max_key"] - 1).bit_length())
+                uniq, seg, pos_s, segid = self._sort_unique(k, end_bit)
+                uf = uniq ^ SIGN
+                cnt = seg[1:] - seg[:-1]
+            else:
+                uf = torch.zeros(0, dtype=torch.int64, device=dev)
+                cnt = torch.zeros(0, dtype=torch.int64, device=dev)
+            gk = self._group_keys_dev(uf, cnt, info_g)
+            self.group_keys[g] = gk.cpu().numpy()
+            self.group_base[g] = base
+            ccount = torch.zeros(gk.numel(), dtype=torch.int64, device=dev)
+            if n and gk.numel():
+                p = torch.searchsorted(gk, uf)
+                pc = p.clamp(max=gk.numel() - 1)
+                hit = (p < gk.numel()) & (gk[pc] == uf)
+                ucol = torch.where(hit, p + base, torch.full_like(p, -1))
+                ccount.index_add_(0, pc[hit], cnt[hit])
+                rows_of = torch.empty(n, dtype=torch.int32, device=dev)
+                H.csr_rows(off, rows_of)
+                ps = pos_s[:n].long()
+                ck = ucol[segid[:n].long() - 1]
+                keep = ck >= 0
+                cols.append(ck[keep].to(torch.int32))
+                rws.append(rows_of[ps][keep])
+                if valued:
+                    vv = torch.ones(n, dtype=torch.float32, device=dev) if v is None else v
+                    vals.append(vv[ps][keep])
+            counts.append(ccount)
+            base += gk.numel()
+        if base >= (1 << 31):
+            raise ValueError("at most 2^31-1 global columns")
+        col = torch.cat(cols) if cols else torch.zeros(0, dtype=torch.int32, device=dev)
+        row = torch.cat(rws) if rws else torch.zeros(0, dtype=torch.int32, device=dev)
+        val = (torch.cat(vals) if vals else torch.zeros(0, dtype=torch.float32, device=dev)) \
+            if valued else None
+        colptr = np.zeros(base + 1, np.int64)
+        if base:
+            colptr[1:] = torch.cumsum(torch.cat(counts), 0).cpu().numpy()
+        return col, row, val, colptr, base, len(gids)
+
+    def _finish_preprocess(self, data, col, row, val, colptr, base, ngroups):
+        cfg = self.cfg
+        dev = self.device
+        self.num_cols = base
+        self.colptr = colptr
+        self.col, self.row, self.val = col, row, val
         self.y = torch.from_numpy(np.where(data.labels > 0, 1.0, -1.0).astype(np.float32)).to(dev)
-        self.nnz = int(col.size)
+        self.nnz = int(col.numel())
         # blocks: key ranges -> global column ranges
         self.blocks: list[Block] = []
         for g, a, b in divide_feature_blocks(self.info, cfg.block_ratio):
@@ -304,14 +480,14 @@ class DarlinTrainer:
         self.w = torch.full((base,), float(cfg.init_w), dtype=f64, device=dev)
         self.delta = torch.full((base,), float(cfg.delta_init), dtype=f64, device=dev)
         self.active = torch.ones(base, dtype=torch.uint8, device=dev)
-        self.ym = torch.zeros(rows, dtype=f64, device=dev)
+        self.ym = torch.zeros(self.rows, dtype=f64, device=dev)
         if cfg.init_w != 0 and base:
             bcd.dual(self.col, self.row, self.val, 0, self.nnz, 0, base, self.w, self.y, self.ym)
         self.vio = torch.zeros(1, dtype=torch.int64, device=dev)
         # owned column share for the server-side statistics
         self.own = even_divide(0, base, self.G, self.rank)
         if self.verbose and self.rank == 0:
-            print(f"Darlin: {self.num_ex} examples, {base} features in {len(gids)} groups, "
+            print(f"Darlin: {self.num_ex} examples, {base} features in {ngroups} groups, "
                   f"{len(self.blocks)} blocks", file=sys.stderr)
 
     # -------------------------------------------------------------- one pass

@@ -148,3 +148,44 @@ def test_darlin_two_rank_gpu_rehearsal_matches_single():
     for _, objs, w in res:
         np.testing.assert_allclose(objs, [p.objective for p in ref], rtol=1e-8)
     np.testing.assert_array_equal(res[0][2], res[1][2])
+
+
+def _same_csc(a, b):
+    assert a.num_cols == b.num_cols and a.nnz == b.nnz and a.num_ex == b.num_ex
+    np.testing.assert_array_equal(a.colptr, b.colptr)
+    assert torch.equal(a.col.cpu(), b.col.cpu()) and torch.equal(a.row.cpu(), b.row.cpu())
+    assert (a.val is None) == (b.val is None)
+    if a.val is not None:
+        assert torch.equal(a.val.cpu(), b.val.cpu())
+    assert sorted(a.group_keys) == sorted(b.group_keys)
+    for g in a.group_keys:
+        np.testing.assert_array_equal(a.group_keys[g], b.group_keys[g])
+    assert [(k.c0, k.c1, k.p0, k.p1) for k in a.blocks] == [(k.c0, k.c1, k.p0, k.p1) for k in b.blocks]
+    assert a.info == b.info
+
+
+@pytest.mark.parametrize("valued,freq", [(False, 0), (True, 2)])
+def test_darlin_gpu_preprocess_bit_identical_to_host(valued, freq):
+    """Device CSC build (own radix sort + RLE, device tail filter / column map) ==
+    the numpy reference path, array for array."""
+    sd = sparse_classification(5000, groups=(1, 2, 3, 5), keys_per_group=3000,
+                               nnz_per_row=(1, 3, 5, 2), binary=not valued, seed=11)
+    cfg = DarlinConfig(l1=1.0, tail_freq=freq, seed=0)
+    g = DarlinTrainer(sd, cfg, device="cuda")
+    h = DarlinTrainer(sd, DarlinConfig(l1=1.0, tail_freq=freq, seed=0, host_preprocess=True),
+                      device="cuda")
+    _same_csc(g, h)
+
+
+def test_darlin_gpu_preprocess_criteo_and_device_data():
+    """Criteo-shaped slots: host numpy groups and device-resident groups give the same
+    CSC as the numpy path."""
+    sd = criteo_slots(50_000, seed=5, num_features=10 ** 7, device="cuda")
+    cfg = DarlinConfig(l1=1.0, tail_freq=3, seed=0)
+    h = DarlinTrainer(sd, DarlinConfig(l1=1.0, tail_freq=3, seed=0, host_preprocess=True),
+                      device="cuda")
+    g = DarlinTrainer(sd, cfg, device="cuda")
+    _same_csc(g, h)
+    dev_sd = criteo_slots(50_000, seed=5, num_features=10 ** 7, device="cuda", on_device=True)
+    d = DarlinTrainer(dev_sd, cfg, device="cuda")
+    _same_csc(d, h)
