@@ -431,6 +431,7 @@ def main():
         run()
         if args.progress and rank == 0 and (i + 1) % 10 == 0:
             print(f"step {i + 1}", file=sys.stderr)
+    t_issue = time.perf_counter() - t0  # host time to enqueue the K steps (CPU-bound check)
     if gpu:
         torch.cuda.synchronize()
     comm.barrier()
@@ -453,6 +454,7 @@ def main():
             "n_gpus": n_ranks,
             "steps": args.steps,
             "warmup": args.warmup,
+            "host_issue_ms_per_step": t_issue / args.steps * 1e3,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",

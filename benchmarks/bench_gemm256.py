@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""256x256 LDS-DMA GEMM (gemm256.hip) vs the 128x128 kernel (gemm.hip) vs hipBLASLt
+(torch.mm) on the wide & deep K-major products and a square reference; uniform
+[-1, 1) bf16 operands; TFLOP/s = 2 M N K / time."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from parameter_server_amd.ops import gemm as GM  # noqa: E402
+from parameter_server_amd.ops.native import hipops  # noqa: E402
+
+H = hipops()
+dev = "cuda"
+
+
+def t(fn, it=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it * 1e3
+
+
+SHAPES = [("wd fwd 4992->1024", 16384, 1024, 4992), ("wd fwd 1024->512", 16384, 512, 1024),
+          ("wd dX 1024->4992 (W^T copy)", 16384, 4992, 1024), ("wd fwd 512->256", 16384, 256, 512),
+          ("square 8192", 8192, 8192, 8192), ("square 4096", 4096, 4096, 4096)]
+for name, M, N, K in SHAPES:
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+    B = (torch.rand(N, K, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    H.gemm_nt256(A, B, M, N, K, bias, True, C, None)
+    ref = torch.relu(A[:512].float() @ B.float().t() + bias)
+    err = ((C[:512].float() - ref).abs() / (ref.abs() + 1)).max().item()
+    fl = 2.0 * M * N * K
+    us_new = t(lambda: H.gemm_nt256(A, B, M, N, K, bias, True, C, None))
+    us_old = t(lambda: GM.gemm(A, True, B, True, M, N, K, bias=bias, relu=True))
+    us_lib = t(lambda: torch.mm(A, B.t()))
+    print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "max_rel_err_vs_fp32": err,
+                      "gemm256_us": us_new, "gemm256_tflops": fl / us_new / 1e6,
+                      "gemm128_tflops": fl / us_old / 1e6, "hipblaslt_tflops": fl / us_lib / 1e6}),
+          flush=True)

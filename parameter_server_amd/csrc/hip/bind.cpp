@@ -34,6 +34,9 @@ void localize_tp(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint
 void tp_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
                  const float*, int64_t, float*, const int32_t*, const int32_t*, const int32_t*,
                  float*, int64_t, hipStream_t);
+// gemm256.hip
+void gemm_nt256(const __bf16*, int64_t, const __bf16*, int64_t, int, int, int, const float*, bool,
+                __bf16*, int64_t, float*, int64_t, hipStream_t);
 // kvapi.hip
 void kvv_pack_vals(const float*, int, const int32_t*, const int32_t*, const int32_t*, int64_t,
                    int64_t, const int64_t*, int, int64_t, int, int64_t, int32_t*, hipStream_t);
@@ -547,6 +550,26 @@ PYBIND11_MODULE(_hipops, m) {
                           ptr<int32_t>(nxt), algo, lr_type, (float)alpha, (float)beta, (float)l1,
                           (float)l2, (float)grad_scale, (float)max_delta, st, stripes,
                           cur_stream());
+  });
+  // ---------------- 256x256 LDS-DMA bf16 GEMM, K-major operands (gemm256.hip) ----------------
+  m.def("gemm_nt256", [](Tensor A, Tensor B, int64_t M, int64_t N, int64_t K,
+                         optional<Tensor> bias, bool relu, optional<Tensor> C,
+                         optional<Tensor> Cf) {
+    chk(A, at::kBFloat16, "A");
+    chk(B, at::kBFloat16, "B");
+    check(M > 0 && N > 0 && K > 0 && K % 64 == 0, "gemm_nt256: K must be a multiple of 64");
+    check(A.numel() >= M * K && B.numel() >= N * K, "gemm_nt256: A [M, K], B [N, K]");
+    check(((uintptr_t)A.data_ptr() % 16) == 0 && ((uintptr_t)B.data_ptr() % 16) == 0,
+          "gemm_nt256: 16-B aligned operands");
+    const float* bp = optr<float>(bias, at::kFloat, "bias");
+    if (bp) check(bias->numel() >= N, "bias too small");
+    __bf16* cp = C.has_value() && C->defined() ? (chk(*C, at::kBFloat16, "C"), ptr<__bf16>(*C)) : nullptr;
+    float* fp = optr<float>(Cf, at::kFloat, "Cf");
+    check(cp || fp, "gemm_nt256: need an output");
+    if (cp) check(C->numel() >= M * N, "C too small");
+    if (fp) check(Cf->numel() >= M * N, "Cf too small");
+    psamd::gemm_nt256(ptr<__bf16>(A), K, ptr<__bf16>(B), K, (int)M, (int)N, (int)K, bp, relu, cp, N,
+                      fp, N, cur_stream());
   });
   // ---------------- k-value push / pull API (kvapi.hip) ----------------
   // rows [hdr 4 | keys C*kw | values C*k f32] of H words (pull rows: no values)

@@ -1,0 +1,153 @@
+// 256 x 256-tile bf16 MFMA GEMM for K-major operands ("NT": C = A B^T):
+//
+//   C[m, n] = act(sum_k A[m * lda + k] * B[n * ldb + k] + bias[n])   (fp32 accumulate)
+//
+// The wide & deep forward products X W^T (X [B, K_in], W [N_out, K_in], the torch
+// layout) and, with the transposed weight copy, the input gradients dZ W take this
+// form. The 128 x 128 register-staged kernel of gemm.hip measured 684 TFLOP/s on the
+// 16384 x 1024 x 4992 forward; this one is built for the long-K products:
+//
+// * 512 threads = 8 wave64 as 2 (M) x 4 (N); a wave owns a 128 x 64 output = 8 x 4
+//   v_mfma_f32_16x16x32_bf16 tiles (lane l: A[row l&15][k 8(l>>4)..+7],
+//   B[k 8(l>>4)..+7][col l&15]; C col l&15, rows 4(l>>4)+j), 64 MFMAs per K-step.
+// * operands go global -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR round
+//   trip, 4 instructions per operand per thread per 256 x 64 tile); two 64 KiB
+//   buffers (A | B), the next K-step's DMA in flight while the MFMAs of this one run,
+//   one counted wait + one barrier per K-step; all LDS in one __shared__ array.
+// * LDS image [256 rows][64 k] of 128-B rows with the 16-B chunk c of row r stored at
+//   c ^ ((r >> 1) & 7): the 16 lanes of a ds_read_b128 lane group (rows r..r+15, one
+//   logical chunk) then cover all 64 banks. LDS-DMA writes lane-linear, so the
+//   swizzle is applied to the per-lane GLOBAL source address.
+// * bijective XCD remap of the block index: the tiles of one A panel run on one XCD
+//   (its 4 MiB L2 keeps the panel for all its N tiles).
+// * fused epilogue: + bias[n], ReLU, bf16 and / or fp32 stores.
+// Requirements (checked by the binding): K % 64 == 0, lda / ldb multiples of 8
+// (16-B rows), 16-B aligned operands. Rows past M / N are clamped on load and
+// masked on store.
+#include "common.cuh"
+
+#include <hip/hip_bf16.h>
+
+#include <stdexcept>
+
+namespace psamd {
+
+namespace g256 {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int BM = 256, BN = 256, BK = 64, TH = 512;
+constexpr int TILE_BYTES = BM * BK * 2;   // 32 KiB per operand tile
+constexpr int BUF_BYTES = 2 * TILE_BYTES; // A | B
+}  // namespace g256
+
+__device__ __forceinline__ int g256_swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+__device__ __forceinline__ int g256_xcd(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + bid / 8;
+}
+
+// LDS-DMA of one 256 x 64 operand tile (rows r0.., k k0..) into the image at dst:
+// wave-instruction wi fills bytes [wi*1024, +1024) = rows wi*8 .. wi*8+7.
+__device__ __forceinline__ void g256_stage(const __bf16* __restrict__ p, int64_t ld, int rows,
+                                           int r0, int k0, char* dst, int wave, int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int wi = q * 8 + wave;
+    const int row = wi * 8 + (lane >> 3);
+    const int c = g256_swz(row, lane & 7);
+    int gr = r0 + row;
+    gr = gr < rows ? gr : rows - 1;
+    const __bf16* src = p + (int64_t)gr * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(dst + wi * 1024),
+                                     16, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(g256::TH)
+gemm_nt256_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B,
+                  int64_t ldb, int M, int N, int K, const float* __restrict__ bias, int relu,
+                  __bf16* __restrict__ C, int64_t ldc, float* __restrict__ Cf, int64_t ldcf,
+                  int tiles_n) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];  // 128 KiB
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int id = g256_xcd(blockIdx.x, gridDim.x);
+  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = K / BK;
+  g256_stage(A, lda, M, m0, 0, smem, wave, lane);
+  g256_stage(B, ldb, N, n0, 0, smem + TILE_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * BUF_BYTES;
+    if (kt + 1 < nk) {  // next K-step's DMA in flight during this one's MFMAs
+      char* nxt = smem + ((kt + 1) & 1) * BUF_BYTES;
+      g256_stage(A, lda, M, m0, (kt + 1) * BK, nxt, wave, lane);
+      g256_stage(B, ldb, N, n0, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + (lane >> 4);
+      bf16x8 a[8], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = wc * 64 + j * 16 + (lane & 15);
+        b[j] = *reinterpret_cast<const bf16x8*>(cur + TILE_BYTES + r * 128 + g256_swz(r, c) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = wr * 128 + i * 16 + (lane & 15);
+        a[i] = *reinterpret_cast<const bf16x8*>(cur + r * 128 + g256_swz(r, c) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next K-step has landed
+    __syncthreads();                                   // ... and this one is read
+  }
+  // epilogue: C[m][n], m = m0 + wr*128 + i*16 + 4*(lane>>4) + r, n = n0 + wc*64 + j*16 + (lane&15)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
+    if (n >= N) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= M) continue;
+        float v = acc[i][j][r] + bv;
+        if (relu) v = v > 0.f ? v : 0.f;
+        if (C) C[(int64_t)m * ldc + n] = (__bf16)v;
+        if (Cf) Cf[(int64_t)m * ldcf + n] = v;
+      }
+    }
+  }
+}
+
+void gemm_nt256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
+                const float* bias, bool relu, __bf16* C, int64_t ldc, float* Cf, int64_t ldcf,
+                hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  if (K % g256::BK != 0 || lda % 8 || ldb % 8) throw std::runtime_error("gemm_nt256: K % 64, ld % 8");
+  const int tiles_m = (M + g256::BM - 1) / g256::BM, tiles_n = (N + g256::BN - 1) / g256::BN;
+  gemm_nt256_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
+                                                            relu ? 1 : 0, C, ldc, Cf, ldcf, tiles_n);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace psamd
