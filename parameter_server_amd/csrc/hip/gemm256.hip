@@ -109,16 +109,46 @@ gemm_nt256_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
         const int r = wr * 128 + i * 16 + (lane & 15);
         a[i] = *reinterpret_cast<const bf16x8*>(cur + r * 128 + g256_swz(r, c) * 16);
       }
+      __builtin_amdgcn_s_setprio(1);  // MFMA cluster at raised priority (guide T5)
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next K-step has landed
     __syncthreads();                                   // ... and this one is read
   }
   // epilogue: C[m][n], m = m0 + wr*128 + i*16 + 4*(lane>>4) + r, n = n0 + wc*64 + j*16 + (lane&15)
+  if (C && !Cf && (ldc & 7) == 0 && m0 + BM <= M && n0 + BN <= N) {
+    // full bf16 tile: stage the 256 x 256 tile in the (now free) LDS, then 16-B stores
+    // of whole 512-B rows (fragment-order stores would be 32-B row pieces)
+    __bf16* st = reinterpret_cast<__bf16*>(smem);  // [256][256] bf16 = 128 KiB
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nl = wc * 64 + j * 16 + (lane & 15);
+      const float bv = bias ? bias[n0 + nl] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ml = wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+          float v = acc[i][j][r] + bv;
+          if (relu) v = v > 0.f ? v : 0.f;
+          st[ml * BN + nl] = (__bf16)v;
+        }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int q = 0; q < BM * BN / 8 / TH; ++q) {  // 16 chunks of 8 bf16 per thread
+      const int ch = q * TH + t;
+      const int ml = ch >> 5, nc = (ch & 31) * 8;
+      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + ml) * ldc + n0 + nc) =
+          *reinterpret_cast<const uint4*>(st + ml * BN + nc);
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + wc * 64 + j * 16 + (lane & 15);

@@ -66,8 +66,9 @@ def gemm(A, a_kmajor: bool, B, b_kmajor: bool, M: int, N: int, K: int, *, bias=N
     return x.to(torch.bfloat16) if out_bf16 else None
 
 
-# Layer products on the GPU: "mfma" = the hand-written kernel above with fused
-# epilogues; "hipblaslt" = the vendor library GEMM (torch.mm / addmm with its own
+# Layer products on the GPU: "mfma" = the hand-written kernels (forward products with
+# K % 64 == 0 and N >= 256 on the 256x256 LDS-DMA kernel of gemm256.hip, the rest on
+# the 128x128 kernel above with fused epilogues); "hipblaslt" = the vendor library GEMM (torch.mm / addmm with its own
 # bias + ReLU epilogue) + separate elementwise kernels; "auto" = per product, the
 # faster of the two as measured on MI355X (benchmarks/bench_gemm.py --wd-backends,
 # B = 16384): the library for the plain long-K products (forward with K >= 1024:
@@ -95,6 +96,14 @@ def linear_forward(X, W, bias=None, relu=False, backend: str = "mfma", bias16=No
             return _addmm_act(b, X, W.t())
         Z = torch.addmm(b, X, W.t())
         return Z.relu_() if relu else Z
+    if is_gpu(X) and K % 64 == 0 and -(-Bn // 256) * -(-N // 256) >= 256 and \
+            X.is_contiguous() and W.is_contiguous():
+        # 256x256 LDS-DMA kernel (gemm256.hip) once its tiles fill the 256 CUs: 1085 vs
+        # 739 TFLOP/s for the 128x128 kernel on 16384 x 1024 x 4992; with fewer tiles
+        # (16384 x 512) the 128x128 kernel wins (profiles/r2_gemm256.log)
+        Z = torch.empty(Bn, N, dtype=torch.bfloat16, device=X.device)
+        hipops().gemm_nt256(X, W, Bn, N, K, bias, relu, Z, None)
+        return Z
     return gemm(X, True, W, True, Bn, N, K, bias=bias, relu=relu)
 
 
@@ -111,6 +120,15 @@ def linear_input_grad(dZ, W, mask=None, backend: str = "mfma", colsum=None):
             dX.mul_(mask > 0)
         if colsum is not None:
             hipops().colsum_bf16(dX, colsum)
+        return dX
+    if is_gpu(dZ) and mask is None and colsum is None and N % 64 == 0 and \
+            -(-Bn // 256) * -(-K // 256) >= 256 and dZ.is_contiguous():
+        # unmasked long-N input gradient (layer 0): the 256x256 LDS-DMA kernel on a
+        # transposed weight copy (10 MB for 1024 x 4992) beats the MN-major 128x128
+        # kernel: 750 vs 628 TFLOP/s on 16384 x 4992 x 1024 (profiles/r2_gemm256.log)
+        Wt = W.t().contiguous()
+        dX = torch.empty(Bn, K, dtype=torch.bfloat16, device=dZ.device)
+        hipops().gemm_nt256(dZ, Wt, Bn, K, N, None, False, dX, None)
         return dX
     return gemm(dZ, True, W, False, Bn, K, N, mask=mask, colsum=colsum)
 
