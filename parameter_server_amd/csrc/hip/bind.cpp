@@ -36,7 +36,7 @@ void tp_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int, 
                  float*, int64_t, hipStream_t);
 // gemm256.hip
 void gemm_nt256(const __bf16*, int64_t, const __bf16*, int64_t, int, int, int, const float*, bool,
-                __bf16*, int64_t, float*, int64_t, hipStream_t);
+                __bf16*, int64_t, float*, int64_t, int, hipStream_t);
 // kvapi.hip
 void kvv_pack_vals(const float*, int, const int32_t*, const int32_t*, const int32_t*, int64_t,
                    int64_t, const int64_t*, int, int64_t, int, int64_t, int32_t*, hipStream_t);
@@ -554,7 +554,7 @@ PYBIND11_MODULE(_hipops, m) {
   // ---------------- 256x256 LDS-DMA bf16 GEMM, K-major operands (gemm256.hip) ----------------
   m.def("gemm_nt256", [](Tensor A, Tensor B, int64_t M, int64_t N, int64_t K,
                          optional<Tensor> bias, bool relu, optional<Tensor> C,
-                         optional<Tensor> Cf) {
+                         optional<Tensor> Cf, int variant) {
     chk(A, at::kBFloat16, "A");
     chk(B, at::kBFloat16, "B");
     check(M > 0 && N > 0 && K > 0 && K % 64 == 0, "gemm_nt256: K must be a multiple of 64");
@@ -568,9 +568,11 @@ PYBIND11_MODULE(_hipops, m) {
     check(cp || fp, "gemm_nt256: need an output");
     if (cp) check(C->numel() >= M * N, "C too small");
     if (fp) check(Cf->numel() >= M * N, "Cf too small");
+    check(variant == 0 || variant == 1, "variant: 0 = one barrier per K-step, 1 = ping-pong");
     psamd::gemm_nt256(ptr<__bf16>(A), K, ptr<__bf16>(B), K, (int)M, (int)N, (int)K, bp, relu, cp, N,
-                      fp, N, cur_stream());
-  });
+                      fp, N, variant, cur_stream());
+  }, py::arg("A"), py::arg("B"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bias"),
+     py::arg("relu"), py::arg("C"), py::arg("Cf"), py::arg("variant") = 0);
   // ---------------- k-value push / pull API (kvapi.hip) ----------------
   // rows [hdr 4 | keys C*kw | values C*k f32] of H words (pull rows: no values)
   m.def("kvv_pack_vals", [](Tensor vals, int64_t k, Tensor pos_s, Tensor seg_start, Tensor n_uniq,

@@ -169,14 +169,215 @@ gemm_nt256_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
   }
 }
 
+// ---------------------------------------------------------------------------
+// Ping-pong variant: the K-step is cut into 4 phases (one 64 x 32 C-quadrant of every
+// wave each, 16 MFMAs), a phase into a LOAD interval (issue one half-tile of the next
+// K-step's LDS-DMA, ds_read the quadrant's fragments, retire them) and an MFMA
+// interval, each closed by a raw s_barrier. The second wave row (waves 4-7: one per
+// SIMD next to a first-row wave) runs one barrier behind, so on every SIMD one wave
+// issues MFMAs while the other loads. Half-tiles: A rows by quadrant row
+// (mq0 = rows {0-63, 128-191}, mq1 = {64-127, 192-255}), B rows by quadrant column
+// (nq0 = n % 64 < 32, nq1 = the rest); quadrant order (0,0) (0,1) (1,1) (1,0) keeps one
+// A and one B fragment set live. DMA order of K-step t+1 during t: A-mq0, B-nq0,
+// B-nq1, A-mq1; counted waits (vmcnt(4) at the end of phases 0, 1, 3: everything but
+// the last two half-tiles) retire every half-tile at least one barrier before any wave
+// reads it, and every LOAD interval retires its own ds_reads (lgkmcnt(0)) before its
+// barrier, so a region is re-staged >= 3 barriers after its last read.
+__device__ __forceinline__ void gpp_stage_a(const __bf16* __restrict__ p, int64_t ld, int rows,
+                                            int r0, int k0, char* img, int mq, int wave,
+                                            int lane) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int wi = q * 8 + wave;                                 // 0..15
+    const int rowb = mq * 64 + (wi >> 3) * 128 + (wi & 7) * 8;  // first of 8 image rows
+    const int row = rowb + (lane >> 3);
+    const int c = g256_swz(row, lane & 7);
+    int gr = r0 + row;
+    gr = gr < rows ? gr : rows - 1;
+    __builtin_amdgcn_global_load_lds((const void*)(p + (int64_t)gr * ld + k0 + c * 8),
+                                     (__attribute__((address_space(3))) void*)(img + rowb * 128),
+                                     16, 0, 0);
+  }
+}
+__device__ __forceinline__ void gpp_stage_b(const __bf16* __restrict__ p, int64_t ld, int rows,
+                                            int r0, int k0, char* img, int nq, int wave,
+                                            int lane) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int wi = q * 8 + wave;                                 // 0..15
+    const int rowb = (wi >> 2) * 64 + nq * 32 + (wi & 3) * 8;
+    const int row = rowb + (lane >> 3);
+    const int c = g256_swz(row, lane & 7);
+    int gr = r0 + row;
+    gr = gr < rows ? gr : rows - 1;
+    __builtin_amdgcn_global_load_lds((const void*)(p + (int64_t)gr * ld + k0 + c * 8),
+                                     (__attribute__((address_space(3))) void*)(img + rowb * 128),
+                                     16, 0, 0);
+  }
+}
+
+#define GPP_BAR() __builtin_amdgcn_s_barrier()
+
+__global__ void __launch_bounds__(g256::TH)
+gemm_nt256pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B,
+                    int64_t ldb, int M, int N, int K, const float* __restrict__ bias, int relu,
+                    __bf16* __restrict__ C, int64_t ldc, float* __restrict__ Cf, int64_t ldcf,
+                    int tiles_n) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];  // 128 KiB, one array
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int id = g256_xcd(blockIdx.x, gridDim.x);
+  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = K / BK;
+  // prologue: K-step 0, every half-tile, then one full barrier
+  gpp_stage_a(A, lda, M, m0, 0, smem, 0, wave, lane);
+  gpp_stage_b(B, ldb, N, n0, 0, smem + TILE_BYTES, 0, wave, lane);
+  gpp_stage_b(B, ldb, N, n0, 0, smem + TILE_BYTES, 1, wave, lane);
+  gpp_stage_a(A, lda, M, m0, 0, smem, 1, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wr == 1) GPP_BAR();  // the second wave row runs one barrier behind
+  bf16x8 af[4][2], bf[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * BUF_BYTES;
+    char* nxt = smem + ((kt + 1) & 1) * BUF_BYTES;
+    const bool more = kt + 1 < nk;
+    const int kn = (kt + 1) * BK;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int mq = (p == 0 || p == 1) ? 0 : 1;
+      const int nq = (p == 1 || p == 2) ? 1 : 0;
+      // ---- LOAD interval: one half-tile of K-step kt+1, this quadrant's fragments
+      if (more) {
+        if (p == 0) gpp_stage_a(A, lda, M, m0, kn, nxt, 0, wave, lane);
+        if (p == 1) gpp_stage_b(B, ldb, N, n0, kn, nxt + TILE_BYTES, 0, wave, lane);
+        if (p == 2) gpp_stage_b(B, ldb, N, n0, kn, nxt + TILE_BYTES, 1, wave, lane);
+        if (p == 3) gpp_stage_a(A, lda, M, m0, kn, nxt, 1, wave, lane);
+      }
+      if (p != 2) {  // B fragments of column quadrant nq (p2 reuses p1's)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int r = wc * 64 + nq * 32 + j * 16 + (lane & 15);
+            bf[ks][j] = *reinterpret_cast<const bf16x8*>(cur + TILE_BYTES + r * 128 +
+                                                          g256_swz(r, c) * 16);
+          }
+        }
+      }
+      if (p == 0 || p == 2) {  // A fragments of row quadrant mq (p1 / p3 reuse them)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = wr * 128 + mq * 64 + i * 16 + (lane & 15);
+            af[i][ks] = *reinterpret_cast<const bf16x8*>(cur + r * 128 + g256_swz(r, c) * 16);
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (p != 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      GPP_BAR();
+      // ---- MFMA interval
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[mq][nq][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf[ks][j],
+                                                                       acc[mq][nq][i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      GPP_BAR();
+    }
+  }
+  if (wr == 0) GPP_BAR();  // match the second row's extra barrier
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // epilogue: quadrant (mq, nq), tile (i, j): m = wr*128 + mq*64 + i*16 + 4(lane>>4) + r,
+  // n = wc*64 + nq*32 + j*16 + (lane&15)
+  if (C && !Cf && (ldc & 7) == 0 && m0 + BM <= M && n0 + BN <= N) {
+    __bf16* st = reinterpret_cast<__bf16*>(smem);  // [256][256] bf16
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int nl = wc * 64 + nq * 32 + j * 16 + (lane & 15);
+        const float bv = bias ? bias[n0 + nl] : 0.f;
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int ml = wr * 128 + mq * 64 + i * 16 + 4 * (lane >> 4) + r;
+              float v = acc[mq][nq][i][j][r] + bv;
+              if (relu) v = v > 0.f ? v : 0.f;
+              st[ml * BN + nl] = (__bf16)v;
+            }
+      }
+    __syncthreads();
+#pragma unroll 4
+    for (int q = 0; q < BM * BN / 8 / TH; ++q) {
+      const int ch = q * TH + t;
+      const int ml = ch >> 5, nc = (ch & 31) * 8;
+      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + ml) * ldc + n0 + nc) =
+          *reinterpret_cast<const uint4*>(st + ml * BN + nc);
+    }
+    return;
+  }
+#pragma unroll
+  for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wc * 64 + nq * 32 + j * 16 + (lane & 15);
+      if (n >= N) continue;
+      const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wr * 128 + mq * 64 + i * 16 + 4 * (lane >> 4) + r;
+            if (m >= M) continue;
+            float v = acc[mq][nq][i][j][r] + bv;
+            if (relu) v = v > 0.f ? v : 0.f;
+            if (C) C[(int64_t)m * ldc + n] = (__bf16)v;
+            if (Cf) Cf[(int64_t)m * ldcf + n] = v;
+          }
+    }
+}
+#undef GPP_BAR
+
 void gemm_nt256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
                 const float* bias, bool relu, __bf16* C, int64_t ldc, float* Cf, int64_t ldcf,
-                hipStream_t st) {
+                int variant, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   if (K % g256::BK != 0 || lda % 8 || ldb % 8) throw std::runtime_error("gemm_nt256: K % 64, ld % 8");
   const int tiles_m = (M + g256::BM - 1) / g256::BM, tiles_n = (N + g256::BN - 1) / g256::BN;
-  gemm_nt256_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
-                                                            relu ? 1 : 0, C, ldc, Cf, ldcf, tiles_n);
+  if (variant == 1)
+    gemm_nt256pp_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
+                                                                relu ? 1 : 0, C, ldc, Cf, ldcf,
+                                                                tiles_n);
+  else
+    gemm_nt256_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
+                                                              relu ? 1 : 0, C, ldc, Cf, ldcf,
+                                                              tiles_n);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -22,7 +22,8 @@ def _ref(A, B, bias, relu):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 128), (300, 1000, 192),
                                    (1024, 4992, 1024), (4097, 260, 640), (64, 64, 64)])
 @pytest.mark.parametrize("epi", ["none", "bias_relu"])
-def test_gemm256_matches_fp32(M, N, K, epi):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_gemm256_matches_fp32(M, N, K, epi, variant):
     g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
     A = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
     B = (torch.rand(N, K, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
@@ -30,11 +31,27 @@ def test_gemm256_matches_fp32(M, N, K, epi):
     relu = epi != "none"
     C = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
     Cf = torch.full((M, N), float("nan"), dtype=torch.float32, device=DEV)
-    hipops().gemm_nt256(A, B, M, N, K, bias, relu, C, None)
-    hipops().gemm_nt256(A, B, M, N, K, bias, relu, None, Cf)
+    hipops().gemm_nt256(A, B, M, N, K, bias, relu, C, None, variant)
+    hipops().gemm_nt256(A, B, M, N, K, bias, relu, None, Cf, variant)
     ref = _ref(A, B, bias, relu)
     torch.testing.assert_close(Cf, ref, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(C.float(), ref, rtol=1e-2, atol=2e-2)
+
+
+def test_gemm256_pingpong_repeatable_long_k():
+    """The ping-pong schedule's counted waits: a long-K product repeated many times is
+    bit-identical every time and equals the one-barrier kernel's fp32 output
+    (a stale LDS-DMA read would show up as a differing tile)."""
+    M, N, K = 2048, 2048, 4096
+    g = torch.Generator(device=DEV).manual_seed(5)
+    A = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
+    B = (torch.rand(N, K, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
+    ref = torch.empty(M, N, device=DEV)
+    hipops().gemm_nt256(A, B, M, N, K, None, False, None, ref, 0)
+    out = torch.empty(M, N, device=DEV)
+    for _ in range(10):
+        hipops().gemm_nt256(A, B, M, N, K, None, False, None, out, 1)
+        assert torch.equal(out, ref)
 
 
 def test_gemm256_rejects_bad_k():
