@@ -73,9 +73,13 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     R = tr.R if tr.padded else 1
     P = NB * R // math.gcd(NB, R)  # graph phases: (buffer, ring position) pairs
     main = torch.cuda.current_stream(device)
-    # preparation stream priority: high on 1 GPU (the preparation is the long pole);
-    # normal next to the SSP exchange stream, which then runs at high priority
-    prio = int(os.environ.get("PSAMD_PREP_PRIORITY", "0" if tr.G > 1 else "-1"))
+    # preparation streams at high priority, also with N > 1: ROCm maps streams of each
+    # priority onto its own set of hardware queues, and normal-priority pool streams
+    # share queues with the null stream and RCCL's streams, which serialises a
+    # preparation stream behind the training step (rocprofv3 Queue_Id: 8 emulated peers
+    # through a real RCCL communicator 0.304 -> 0.204 ms / step, loopback copy 0.227 ->
+    # 0.208; profiles/r2_emulated8_priority.log)
+    prio = int(os.environ.get("PSAMD_PREP_PRIORITY", "-1"))
     sides = [torch.cuda.Stream(device, priority=prio) for _ in range(nprep)]
     bufs = [(keys, labels)] + [(torch.empty_like(keys), torch.empty_like(labels))
                                for _ in range(NB - 1)]

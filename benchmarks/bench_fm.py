@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--minibatch", type=int, default=16384)
     ap.add_argument("--num-features", type=float, default=1e9)
     ap.add_argument("--dim", type=int, default=16)
+    ap.add_argument("--compact-rows", type=int, default=1,
+                    help="1 GPU: gather each unique key's row once per step (0: per occurrence "
+                         "through the slot index)")
     ap.add_argument("--table-slots", type=int, default=1 << 28, help="slots per GPU")
     ap.add_argument("--prefetch", type=int, default=1,
                     help="generate + localise minibatch t+1 on a side stream during step t")
@@ -34,7 +37,7 @@ def main():
     comm, dev = init_from_env("cuda")
     G, rank = comm.world, comm.rank
     B, N = args.minibatch, int(args.num_features)
-    cfg = FMConfig(num_features=N, embedding_dim=args.dim, minibatch=B,
+    cfg = FMConfig(num_features=N, embedding_dim=args.dim, minibatch=B, compact_rows=bool(args.compact_rows),
                    table_capacity=args.table_slots, seed=0)
     tr = FMTrainer(cfg, comm, dev)
     bufs = [(torch.empty(B * 39, dtype=torch.int64, device=dev),

@@ -154,7 +154,8 @@ void bcd_server_stats(const double*, const uint8_t*, int64_t, int64_t, double*, 
 // embedding.hip
 void emb_init_rows(const int64_t*, const uint64_t*, int64_t, const int32_t*, int64_t, void*,
                    uint8_t*, int, uint64_t, float, hipStream_t);
-void emb_gather_rows(const int64_t*, int64_t, int64_t, const void*, int, void*, hipStream_t);
+void emb_gather_rows(const int64_t*, int64_t, const int32_t*, int64_t, const void*, int, void*,
+                     hipStream_t);
 void emb_expand(const int32_t*, int64_t, const int64_t*, int64_t, const void*, int64_t, int, void*,
                 hipStream_t);
 int64_t emb_grad_part_floats(int64_t, int);
@@ -1445,14 +1446,17 @@ PYBIND11_MODULE(_hipops, m) {
                          ptr<uint8_t>(inited), (int)rows.size(1), seed, (float)scale,
                          cur_stream());
   });
-  m.def("emb_gather_rows", [rows_check](Tensor slot, Tensor rows, Tensor out) {
+  m.def("emb_gather_rows", [rows_check](Tensor slot, Tensor rows, Tensor out,
+                                         optional<Tensor> n_dev) {
+    // out[i, :] = rows[slot[i], :] for i < n_dev (device count, clamped) or slot.numel()
     chk(slot, at::kLong, "slot");
     rows_check(rows, rows.size(0), (int)rows.size(1));
     chk(out, at::kBFloat16, "out");
     check(out.numel() >= slot.numel() * rows.size(1), "out too small");
-    psamd::emb_gather_rows(ptr<int64_t>(slot), slot.numel(), rows.size(0), rows.data_ptr(),
-                           (int)rows.size(1), out.data_ptr(), cur_stream());
-  });
+    psamd::emb_gather_rows(ptr<int64_t>(slot), slot.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"),
+                           rows.size(0), rows.data_ptr(), (int)rows.size(1), out.data_ptr(),
+                           cur_stream());
+  }, py::arg("slot"), py::arg("rows"), py::arg("out"), py::arg("n_dev") = py::none());
   m.def("emb_expand", [](Tensor local_col, int64_t nnz, optional<Tensor> idx, Tensor src,
                          Tensor X0) {
     chk(local_col, at::kInt, "local_col");

@@ -75,10 +75,12 @@ emb_init_rows_kernel(const int64_t* __restrict__ slot, const uint64_t* __restric
 }
 
 __global__ void __launch_bounds__(256)
-emb_gather_rows_kernel(const int64_t* __restrict__ slot, int64_t n, int64_t cap,
+emb_gather_rows_kernel(const int64_t* __restrict__ slot, int64_t n_host,
+                       const int32_t* __restrict__ n_dev, int64_t cap,
                        const uint16_t* __restrict__ rows, int D, uint16_t* __restrict__ out) {
   const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
   const int vec = D / 8;  // 16-B vectors per row
+  const int64_t n = dev_len(n_dev, n_host);
   for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; i < n;
        i += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
     const int64_t s = slot[i];
@@ -725,11 +727,12 @@ void emb_init_rows(const int64_t* slot, const uint64_t* keys, int64_t n, const i
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void emb_gather_rows(const int64_t* slot, int64_t n, int64_t cap, const void* rows, int D,
-                     void* out, hipStream_t st) {
+void emb_gather_rows(const int64_t* slot, int64_t n, const int32_t* n_dev, int64_t cap,
+                     const void* rows, int D, void* out, hipStream_t st) {
   if (n <= 0) return;
   emb_gather_rows_kernel<<<grid_for(n, 16, 8192), 256, 0, st>>>(
-      slot, n, cap, reinterpret_cast<const uint16_t*>(rows), D, reinterpret_cast<uint16_t*>(out));
+      slot, n, n_dev, cap, reinterpret_cast<const uint16_t*>(rows), D,
+      reinterpret_cast<uint16_t*>(out));
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -30,6 +30,7 @@
 // (the multi-GPU owner split and the ordered home slots of the KV table rely on it).
 #include "common.cuh"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -680,7 +681,9 @@ void tp_backward(const uint16_t* rep, const int32_t* dcnt, int64_t n, const int3
                  int64_t grad_cap, hipStream_t st) {
   if (n <= 0) return;
   const TpGeom g = tp_geom(n, 31);
-  if (rows == nullptr && width >= 2 && width <= tp::kThr)
+  static const char* bwd_env = getenv("PSAMD_TP_BWD");  // "rows": A/B the row-major walk
+  const bool cols = !(bwd_env && bwd_env[0] == 'r');
+  if (cols && rows == nullptr && width >= 2 && width <= tp::kThr)
     tp_bwd_accum_cols_kernel<<<(unsigned)g.T, tp::kThr, 0, st>>>(rep, dcnt, n, width, vals, coef,
                                                                  B, psum);
   else

@@ -56,6 +56,7 @@ class FMConfig:
     exchange: str = "padded"             # G > 1 on GPU: sync-free fixed rows | "exact"
     exchange_slack: float = 1.5
     exchange_capacity: int = 0
+    compact_rows: bool = True            # 1 GPU: gather each unique key's row once per step
     seed: int = 0
 
 
@@ -89,6 +90,7 @@ class FMTrainer(EmbeddingPS):
             self.w_buf = torch.empty(self.max_nnz, dtype=torch.float32, device=dev)
             self.dX0 = torch.empty(self.max_nnz, D, dtype=torch.bfloat16, device=dev)
             self.dE = torch.empty(self.max_nnz, D, dtype=torch.float32, device=dev)
+            self.rows_u = torch.empty(self.max_nnz, D, dtype=torch.bfloat16, device=dev)
         self.step_count = 0
         self.examples = 0
         self.t0 = time.time()
@@ -111,6 +113,12 @@ class FMTrainer(EmbeddingPS):
             else:
                 slot, w_wide = self.shard.resolve(loc.uniq[:loc.num_unique()])
             rows_src, rows_idx = self.shard.rows, slot
+            if self.gpu and cfg.compact_rows:
+                # each unique key's factor row gathered ONCE from the (huge, randomly
+                # addressed) table into a compact L2-sized buffer; the per-occurrence
+                # gathers of the forward then read that buffer
+                hipops().emb_gather_rows(slot, self.shard.rows, self.rows_u, loc.n_uniq)
+                rows_src, rows_idx = self.rows_u, None
             push = ("local", slot)
         else:
             rows_u, w_wide, push = self._pull(loc)
