@@ -63,7 +63,7 @@ def main():
              torch.empty(B, dtype=torch.float32, device=dev)) for _ in range(2)]
     t = [0]
     locs = [None, None]
-    side = torch.cuda.Stream(dev)
+    side = torch.cuda.Stream(dev, priority=int(os.environ.get("PSAMD_PREP_PRIORITY", "-1")))  # own HW queues
     main = torch.cuda.current_stream(dev)
     ev_prep = [torch.cuda.Event() for _ in range(2)]
     ev_step = [torch.cuda.Event() for _ in range(2)]
