@@ -68,6 +68,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     import math
 
     from parameter_server_amd.ops.synthetic import criteo_batch
+    from parameter_server_amd.parallel.consistency import EventClock
 
     NB = 2 * nprep
     R = tr.R if tr.padded else 1
@@ -117,8 +118,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     ev_w = [torch.cuda.Event() for _ in range(E)]      # worker half of step t done
     ev_prep = [torch.cuda.Event() for _ in range(NB)]
     ev_x = [torch.cuda.Event() for _ in range(E)]      # exchange half of step t done
-    ev_a = [torch.cuda.Event() for _ in range(E)]      # asp: push apply of exchange t done
-    recorded_a = set()
+    aclock = EventClock(E)                             # asp: push apply of exchange t done
 
     def run_plan(plan, t, xs):
         """Run one half's segments; an "async" segment (ASP push apply) goes to its
@@ -130,8 +130,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
                 apply_s.wait_event(e)
                 with torch.cuda.stream(apply_s):
                     fn()
-                ev_a[t % E].record(apply_s)
-                recorded_a.add(t % E)
+                aclock.record(t, apply_s)
             else:
                 fn()
 
@@ -168,9 +167,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
             xs.wait_event(ev_w[c % E])      # the gradients it carries are packed
         if t >= 1:
             xs.wait_event(ev_x[(t - 1) % E])  # owner updates of consecutive steps in order
-        g = tr.sched.apply_gate(t) if asp else None
-        if g is not None and g % E in recorded_a:
-            xs.wait_event(ev_a[g % E])      # asp: ring entry of exchange t is free again
+        if asp:  # ring entry of exchange t is free again once that apply is done
+            aclock.wait_for(tr.sched.apply_gate(t), xs)
         with torch.cuda.stream(xs):
             run_plan(xplan(t), t, xs)
             ev_x[t % E].record(xs)

@@ -23,7 +23,10 @@ void kv_update_rows(void*, int64_t, const int64_t*, const float*, int64_t, const
                     float, float, float, float, double*, int, hipStream_t);
 void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int, int64_t*, float*,
                      bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t,
-                     hipStream_t);
+                     uint64_t*, int32_t*, int, hipStream_t);
+void kv_apply_part(void*, int64_t, const int64_t*, const uint64_t*, const float*, int64_t,
+                   const int32_t*, int, int64_t, int64_t, const int32_t*, int, int, int, float, float,
+                   float, float, float, float, double*, int, hipStream_t);
 // tploc.hip
 int64_t tploc_stride(int64_t);
 bool tploc_supported(int64_t, int);
@@ -489,7 +492,8 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("kv_resolve_rows", [](Tensor slots, Tensor recv, int64_t H, int64_t C, int kw,
                               Tensor out_slot, Tensor out_w, bool insert, int init_type,
                               double init_v, double init_s, uint64_t seed, optional<Tensor> err,
-                              optional<Tensor> inserted, uint64_t home_base, uint64_t home_m) {
+                              optional<Tensor> inserted, uint64_t home_base, uint64_t home_m,
+                              optional<Tensor> out_key, optional<Tensor> bnd, int lgP) {
     const int64_t cap = slot_capacity(slots);
     chk(recv, at::kInt, "recv");
     chk(out_slot, at::kLong, "out_slot");
@@ -500,11 +504,46 @@ PYBIND11_MODULE(_hipops, m) {
     const int G = (int)(recv.numel() / H);
     check(G >= 1 && G <= 64, "1..64 peers");
     check(out_slot.numel() >= G * C && out_w.numel() >= G * C, "out_slot/out_w < G*C");
+    int64_t* ok = optr<int64_t>(out_key, at::kLong, "out_key");
+    if (ok) check(out_key->numel() >= G * C, "out_key < G*C");
+    int32_t* bp = optr<int32_t>(bnd, at::kInt, "bnd");
+    check(lgP >= 0 && lgP <= 20, "lgP in 0..20");
+    if (bp) check(bnd->numel() >= G * ((1 << lgP) + 1), "bnd < G*(P+1)");
     psamd::kv_resolve_rows(slots.data_ptr(), cap, ptr<int32_t>(recv), G, H, C, kw,
                            ptr<int64_t>(out_slot), ptr<float>(out_w), insert, init_type,
                            (float)init_v, (float)init_s, seed, optr<int32_t>(err, at::kInt, "err"),
                            optr<int32_t>(inserted, at::kInt, "inserted"), home_base, home_m,
-                           cur_stream());
+                           reinterpret_cast<uint64_t*>(ok), bp, lgP, cur_stream());
+  }, py::arg("slots"), py::arg("recv"), py::arg("H"), py::arg("C"), py::arg("kw"),
+     py::arg("out_slot"), py::arg("out_w"), py::arg("insert"), py::arg("init_type"),
+     py::arg("init_v"), py::arg("init_s"), py::arg("seed"), py::arg("err"), py::arg("inserted"),
+     py::arg("home_base"), py::arg("home_m"), py::arg("out_key") = py::none(),
+     py::arg("bnd") = py::none(), py::arg("lgP") = 0);
+  // per-push apply of every source row, partitioned by key range (see kv_apply_part_kernel)
+  m.def("kv_apply_part", [](Tensor slots, Tensor slot_idx, Tensor keys, Tensor grad,
+                            int64_t gstride, Tensor recv, int64_t H, int64_t C, Tensor bnd, int lgP,
+                            int algo, int lr_type, double alpha, double beta, double l1, double l2,
+                            double grad_scale, double max_delta, optional<Tensor> stats) {
+    const int64_t cap = slot_capacity(slots);
+    chk(slot_idx, at::kLong, "slot_idx");
+    chk(keys, at::kLong, "keys");
+    chk(grad, at::kFloat, "grad");
+    chk(recv, at::kInt, "recv");
+    chk(bnd, at::kInt, "bnd");
+    check(C > 0 && H > 4 && recv.numel() % H == 0, "bad exchange row geometry");
+    const int G = (int)(recv.numel() / H);
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(gstride >= C && grad.numel() >= (G - 1) * gstride + C, "grad rows out of bounds");
+    check(slot_idx.numel() >= G * C && keys.numel() >= G * C, "slot_idx/keys < G*C");
+    check(lgP >= 0 && lgP <= 20, "lgP in 0..20");
+    check(bnd.numel() >= G * ((1 << lgP) + 1), "bnd < G*(P+1)");
+    double* st = optr<double>(stats, at::kDouble, "stats");
+    const int stripes = acc_stripes_of(stats);
+    psamd::kv_apply_part(slots.data_ptr(), cap, ptr<int64_t>(slot_idx),
+                         reinterpret_cast<const uint64_t*>(keys.data_ptr<int64_t>()),
+                         ptr<float>(grad), gstride, ptr<int32_t>(recv), G, H, C, ptr<int32_t>(bnd),
+                         lgP, algo, lr_type, (float)alpha, (float)beta, (float)l1, (float)l2,
+                         (float)grad_scale, (float)max_delta, st, stripes, cur_stream());
   });
   // aggregated pushes of every source row in one launch; grad row s at grad[s*gstride]
   m.def("kv_accumulate_rows", [](Tensor slots, Tensor slot_idx, Tensor grad, int64_t gstride,

@@ -81,6 +81,14 @@ __device__ __forceinline__ uint64_t home_slot(uint64_t h, uint64_t mask, uint64_
   return m ? ((h - base) * m) >> shr : (fmix64(h) & mask);
 }
 
+// Partition of a key in an ordered-home shard: the top lgP bits of its home
+// position, so partitions are contiguous, equally wide key ranges and a sorted
+// key list splits into P consecutive runs (owner push apply, kv_apply_part).
+__device__ __forceinline__ int key_part(uint64_t h, uint64_t base, uint64_t m, int lgP) {
+  if (lgP == 0) return 0;
+  return (int)(((h - base) * m) >> (64 - lgP));
+}
+
 // Probe for one key; insert it if asked. Returns the slot index (-1: absent or
 // table full) and the weight through *w.
 __device__ __forceinline__ int64_t resolve_key(Slot* __restrict__ slots, uint64_t mask,
@@ -153,10 +161,16 @@ __global__ void kv_resolve_rows_kernel(Slot* __restrict__ slots, uint64_t mask,
                                        int kw, int64_t* __restrict__ out_slot,
                                        float* __restrict__ out_w, int insert, int init_type,
                                        float init_v, float init_s, uint64_t seed,
-                                       int32_t* __restrict__ err, int32_t* __restrict__ inserted) {
+                                       int32_t* __restrict__ err, int32_t* __restrict__ inserted,
+                                       uint64_t* __restrict__ out_key, int32_t* __restrict__ bnd,
+                                       int lgP) {
   const int s = blockIdx.y;
   const int32_t* row = recv + (int64_t)s * H;
   const int64_t n = dev_len(row, C);
+  const int P = 1 << lgP;
+  int32_t* rb = bnd ? bnd + (int64_t)s * (P + 1) : nullptr;
+  if (rb && n == 0 && blockIdx.x == 0)
+    for (int q = threadIdx.x; q <= P; q += blockDim.x) rb[q] = 0;
   int local_ins = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -168,6 +182,19 @@ __global__ void kv_resolve_rows_kernel(Slot* __restrict__ slots, uint64_t mask,
     if (found < 0 && insert && err) atomicOr(err, 1);
     out_slot[(int64_t)s * C + i] = found;
     out_w[(int64_t)s * C + i] = w;
+    if (out_key) out_key[(int64_t)s * C + i] = h;
+    if (rb) {  // partition bounds of this (sorted) row: rb[q] = #keys of partition < q
+      const int q = key_part(h, home_base, home_m, lgP);
+      int q0 = 0;
+      if (i > 0) {
+        const uint64_t hp = kw == 1 ? (uint64_t)(uint32_t)row[4 + i - 1]
+                                    : reinterpret_cast<const uint64_t*>(row + 4)[i - 1];
+        q0 = key_part(hp, home_base, home_m, lgP) + 1;
+      }
+      for (int j = q0; j <= q; ++j) rb[j] = (int32_t)i;
+      if (i == n - 1)
+        for (int j = q + 1; j <= P; ++j) rb[j] = (int32_t)n;
+    }
   }
   if (inserted) {
     int tot = wave_sum(local_ins);
@@ -519,6 +546,139 @@ __global__ void kv_apply_rows_kernel(Slot* __restrict__ slots, int64_t cap,
   }
 }
 
+// The same per-push semantics in ONE launch without global atomics or scratch
+// resets, for shards with an ordered home whose source rows are sorted by key
+// (the localisers' unique lists are): the resolve of the pull recorded each row's
+// keys and the bounds of P = 2^lgP key-range partitions (kv_resolve_rows), so
+// every partition is a run of consecutive entries in each row and no key spans
+// two partitions. One workgroup per partition gathers its runs into LDS in
+// windows of <= kApWin entries (a window ends at the smallest "last loaded key"
+// of the rows that did not fit, so every key's entries share a window), chains
+// entries of equal slot through an LDS hash, and the head of each chain applies
+// its gradients in increasing entry order (= source-rank order) to a register
+// copy of the slot: bitwise the weights of kv_apply_rows.
+constexpr int kApWin = 1024;   // entries per window
+constexpr int kApHash = 2048;  // LDS hash slots (power of two, >= 2 * kApWin)
+
+__global__ __launch_bounds__(256) void kv_apply_part_kernel(
+    Slot* __restrict__ slots, int64_t cap, const int64_t* __restrict__ slot_idx,
+    const uint64_t* __restrict__ keys, const float* __restrict__ grad, int64_t gstride,
+    const int32_t* __restrict__ recv, int64_t H, int64_t C, int G,
+    const int32_t* __restrict__ bnd, int lgP, UpdateParams p, double* __restrict__ stats,
+    int acc_stripes) {
+  __shared__ uint32_t hk[kApHash];
+  __shared__ int32_t hh[kApHash];
+  __shared__ int32_t went[kApWin], wnx[kApWin], whs[kApWin];
+  __shared__ float wg[kApWin];
+  __shared__ int32_t ra[kMaxChain], re[kMaxChain], roff[kMaxChain + 1], rcnt[kMaxChain];
+  __shared__ uint64_t thr;
+  __shared__ double red[16];
+  const int tid = threadIdx.x, P = 1 << lgP, part = blockIdx.x;
+  const int CH = max(1, kApWin / G);
+  if (tid < G) {
+    const int32_t n = (int32_t)dev_len(recv + (int64_t)tid * H + 1, C);
+    const int32_t* rb = bnd + (int64_t)tid * (P + 1);
+    const int32_t a = min(rb[part], n), b = min(rb[part + 1], n);
+    ra[tid] = a;
+    re[tid] = max(a, b);
+  }
+  for (int h = tid; h < kApHash; h += blockDim.x) {
+    hk[h] = 0xffffffffu;
+    hh[h] = -1;
+  }
+  double dnnz = 0, wsum = 0, dsum = 0;
+  for (;;) {
+    __syncthreads();
+    if (tid == 0) {
+      int off = 0;
+      uint64_t t = ~0ull;
+      for (int s = 0; s < G; ++s) {
+        const int rem = re[s] - ra[s];
+        roff[s] = off;
+        off += min(rem, CH);
+        if (rem > CH) t = min(t, keys[(int64_t)s * C + ra[s] + CH - 1]);
+        rcnt[s] = 0;
+      }
+      roff[G] = off;
+      thr = t;
+    }
+    __syncthreads();
+    const int tot = roff[G];
+    if (tot == 0) break;
+    const uint64_t th = thr;
+    for (int w = tid; w < tot; w += blockDim.x) {
+      int lo = 0, hi = G - 1;  // row of window entry w: last s with roff[s] <= w
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (roff[mid] <= w) lo = mid; else hi = mid - 1;
+      }
+      const int s = lo;
+      const int64_t i = ra[s] + (w - roff[s]);
+      const int64_t e = (int64_t)s * C + i;
+      int32_t ent = -1;
+      const uint64_t key = keys[e];  // three independent loads in flight together
+      const int64_t k = slot_idx[e];
+      const float g = grad[(int64_t)s * gstride + i];
+      if (key <= th) {
+        atomicAdd(&rcnt[s], 1);
+        if (in_range(k, cap) && g == g) {  // NaN mark = filtered entry
+          const uint32_t ks = (uint32_t)k;
+          uint32_t hp = (ks * 0x9E3779B1u) >> (32 - 11);  // log2(kApHash) = 11
+          for (int probe = 0; probe < kApHash; ++probe) {
+            const uint32_t prev = atomicCAS(&hk[hp], 0xffffffffu, ks);
+            if (prev == 0xffffffffu || prev == ks) break;
+            hp = (hp + 1) & (kApHash - 1);
+          }
+          ent = (int32_t)e;
+          wg[w] = g;
+          whs[w] = (int32_t)hp;
+          wnx[w] = atomicExch(&hh[hp], w);
+        }
+      }
+      went[w] = ent;
+    }
+    __syncthreads();
+    for (int w = tid; w < tot; w += blockDim.x) {
+      if (went[w] < 0 || hh[whs[w]] != w) continue;  // not the head of its chain
+      int len = 0;
+      for (int c = w; c >= 0 && len < kMaxChain; c = wnx[c]) ++len;
+      const int64_t k = (int64_t)hk[whs[w]];
+      Slot sl = slots[k];
+      int32_t last = -1;
+      for (int it = 0; it < len; ++it) {  // next entry in increasing (source) order
+        int32_t best = INT32_MAX, bw = -1, walked = 0;
+        for (int c = w; c >= 0 && walked < len; c = wnx[c], ++walked)
+          if (went[c] > last && went[c] < best) { best = went[c]; bw = c; }
+        if (bw < 0) break;
+        const float w_old = apply_update(sl, wg[bw] * p.grad_scale, p);
+        dnnz += (double)((sl.w != 0.f) - (w_old != 0.f));
+        wsum += (double)sl.w * sl.w;
+        const double d = (double)sl.w - w_old;
+        dsum += d * d;
+        last = best;
+      }
+      slots[k] = sl;
+    }
+    __syncthreads();
+    if (tid < G) ra[tid] += rcnt[tid];
+    for (int h = tid; h < kApHash; h += blockDim.x) {
+      hk[h] = 0xffffffffu;
+      hh[h] = -1;
+    }
+  }
+  if (stats) {
+    double a = block_sum_f64(dnnz, red);
+    double b = block_sum_f64(wsum, red);
+    double c = block_sum_f64(dsum, red);
+    if (tid == 0) {
+      double* st = acc_stripe(stats, acc_stripes);
+      if (a != 0) atomicAdd(&st[0], a);
+      if (b != 0) atomicAdd(&st[1], b);
+      if (c != 0) atomicAdd(&st[2], c);
+    }
+  }
+}
+
 // Occupancy / sparsity census: out[0] = occupied slots, out[1] = nonzero w.
 __global__ void kv_census_kernel(const Slot* __restrict__ slots, int64_t cap,
                                  unsigned long long* __restrict__ out) {
@@ -568,13 +728,15 @@ void kv_resolve(void* slots, int64_t cap, const uint64_t* keys, int64_t n, const
 void kv_resolve_rows(void* slots, int64_t cap, const int32_t* recv, int G, int64_t H, int64_t C,
                      int kw, int64_t* out_slot, float* out_w, bool insert, int init_type,
                      float init_v, float init_s, uint64_t seed, int32_t* err, int32_t* inserted,
-                     uint64_t home_base, uint64_t home_m, hipStream_t st) {
+                     uint64_t home_base, uint64_t home_m, uint64_t* out_key, int32_t* bnd,
+                     int lgP, hipStream_t st) {
   int lg = 0;
   while ((1ll << lg) < cap) ++lg;
   dim3 grid(grid_for(C, 256, 1024), G);
+  if (bnd && !home_m) throw std::runtime_error("kv_resolve_rows: partition bounds need an ordered home");
   kv_resolve_rows_kernel<<<grid, 256, 0, st>>>(
       (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg, recv, H, C, kw, out_slot,
-      out_w, insert ? 1 : 0, init_type, init_v, init_s, seed, err, inserted);
+      out_w, insert ? 1 : 0, init_type, init_v, init_s, seed, err, inserted, out_key, bnd, lgP);
   PSAMD_HIP_CHECK(hipGetLastError());
   if (init_type != kInitZero) {
     kv_gather_rows_kernel<<<grid, 256, 0, st>>>((const Slot*)slots, cap, recv, H, C, out_slot,
@@ -653,6 +815,21 @@ void kv_update_rows(void* slots, int64_t cap, const int64_t* slot_idx, const flo
   kv_apply_rows_kernel<<<grid, 256, 0, st>>>((Slot*)slots, cap, slot_idx, grad, gstride, recv, H,
                                              C, link, (uint64_t)(link_size - 1), nxt,
                                              (int64_t)G * C, p, stats, acc_stripes);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void kv_apply_part(void* slots, int64_t cap, const int64_t* slot_idx, const uint64_t* keys,
+                   const float* grad, int64_t gstride, const int32_t* recv, int G, int64_t H,
+                   int64_t C, const int32_t* bnd, int lgP, int algo, int lr_type, float alpha,
+                   float beta, float l1, float l2, float grad_scale, float max_delta,
+                   double* stats, int acc_stripes, hipStream_t st) {
+  if (cap > (int64_t(1) << 32) - 1) throw std::runtime_error("kv_apply_part: capacity >= 2^32");
+  if ((int64_t)G * C >= (int64_t(1) << 31)) throw std::runtime_error("kv_apply_part: G*C >= 2^31");
+  if (G < 1 || G > kMaxChain) throw std::runtime_error("kv_apply_part: 1..64 source rows");
+  if (lgP < 0 || lgP > 20) throw std::runtime_error("kv_apply_part: lgP in 0..20");
+  UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
+  kv_apply_part_kernel<<<1 << lgP, 256, 0, st>>>((Slot*)slots, cap, slot_idx, keys, grad, gstride,
+                                                 recv, H, C, G, bnd, lgP, p, stats, acc_stripes);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -30,6 +30,7 @@ One training step on a rank (all on the GPU, no host round trip when G == 1):
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -108,7 +109,11 @@ class SparseLRTrainer:
         cap = cfg.table_capacity or self.auto_capacity(cfg, self.G, self.bits)
         # ordered home slots over this shard's mixed-key range: sorted unique keys then
         # walk the (up to 64 GB) table in increasing address order
-        self.table = KVTable(cap, self.device, cfg.init, key_range=self.part.range_of(self.rank))
+        # (the loopback emulation's one rank owns every peer's range: order over all)
+        self._loopback = getattr(self.comm, "backend", "") == "loopback"
+        rng = ((self.part.range_of(0)[0], self.part.range_of(self.G - 1)[1]) if self._loopback
+               else self.part.range_of(self.rank))
+        self.table = KVTable(cap, self.device, cfg.init, key_range=rng)
         self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
         mode = cfg.localize
         if mode == "auto":  # tile dedup + key-range buckets (Localizer falls back to sort
@@ -371,6 +376,18 @@ class SparseLRTrainer:
         gw = (C * nb + 3) // 4 if nb else C
         H = (4 + C * kw + gw + 3) // 4 * 4
         z32 = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
+        # the partitioned apply needs rows sorted by key (not the hashed localisers'
+        # bucket order) and an ordered home (key range -> partition)
+        part_apply = (self.gpu and cfg.push_mode != "aggregate" and self.table.home_m != 0
+                      and not getattr(loc, "hashed", False)
+                      and os.environ.get("PSAMD_OWNER_APPLY", "part") == "part")
+        # ~G*C/512 partitions (~1-2 entries per thread of a 256-thread workgroup, rows
+        # are ~2/3 full): a few workgroups per CU hide the chain of dependent loads each
+        # one runs; many more (tiny ones) pay per-workgroup setup and stats atomics
+        # (profiles/r2_owner_apply.log: 8 x 45120 entries, 2^9 -> 21 us, link pair 58 us)
+        lgP = max(0, min(16, math.floor(math.log2(max(1, G * C // 512))))) if part_apply else -1
+        if part_apply and os.environ.get("PSAMD_APPLY_LGP"):
+            lgP = int(os.environ["PSAMD_APPLY_LGP"])
         self.xc = SimpleNamespace(
             C=C, kw=kw, H=H, nb=nb,
             gstage=z32(G * C, torch.float32) if nb else None,
@@ -388,8 +405,14 @@ class SparseLRTrainer:
             n_touched=z32(1, torch.int32),
             # per-exchange chain scratch of the one-launch sequential push apply
             link=(torch.empty(next_pow2(2 * G * C), dtype=torch.int64, device=dev)
-                  if self.gpu else None),
-            nxt=torch.empty(G * C, dtype=torch.int32, device=dev) if self.gpu else None,
+                  if self.gpu and lgP < 0 else None),
+            nxt=torch.empty(G * C, dtype=torch.int32, device=dev) if self.gpu and lgP < 0 else None,
+            # partitioned one-launch apply (kv_apply_part): the pull's keys and the
+            # per-row bounds of 2^lgP key-range partitions, per ring entry
+            lgP=lgP, pkeys=([torch.empty(G * C, dtype=torch.int64, device=dev) for _ in range(R)]
+                            if lgP >= 0 else None),
+            bnd=([torch.zeros(G * ((1 << lgP) + 1), dtype=torch.int32, device=dev)
+                  for _ in range(R)] if lgP >= 0 else None),
             ovf_host=(torch.zeros(1, dtype=torch.int32, pin_memory=True) if self.gpu else None))
 
     def _tail_filter(self, loc, ring: int):
@@ -505,6 +528,9 @@ class SparseLRTrainer:
                                       xc.touched, xc.n_touched)
                 hh.kv_apply_accumulated(self.table.slots, xc.touched, xc.n_touched,
                                         *self.rule.args(), self.stats)
+            elif xc.bnd is not None:
+                hh.kv_apply_part(self.table.slots, pslot, xc.pkeys[gb], gsrc, gstride, recv, H, C,
+                                 xc.bnd[gb], xc.lgP, *self.rule.args(), self.stats)
             else:
                 hh.kv_update_rows(self.table.slots, pslot, gsrc, gstride, recv, H, C, xc.link,
                                   xc.nxt, *self.rule.args(), self.stats)
@@ -532,7 +558,9 @@ class SparseLRTrainer:
             hipops().kv_resolve_rows(self.table.slots, recv, H, C, kw, xc.slots[r], xc.wsend,
                                      True, it, iv, isd, seed, self.table._err,
                                      self.table._inserted, self.table.home_base,
-                                     self.table.home_m)
+                                     self.table.home_m,
+                                     xc.pkeys[r] if xc.bnd is not None else None,
+                                     xc.bnd[r] if xc.bnd is not None else None, max(xc.lgP, 0))
             return
         for s in range(G):
             row = recv[s * H:(s + 1) * H]
