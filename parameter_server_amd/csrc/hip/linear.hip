@@ -329,11 +329,15 @@ __global__ void csr_rows_kernel(const int64_t* __restrict__ row_ptr, int64_t B,
 // hashed into [0, num_features). Labels from a planted sparse logistic model.
 __constant__ uint32_t c_cards[26];
 
+// Planted weight of a feature: ~20 % of features carry N(0, 0.6^2) signal. The
+// transcendentals use the hardware approximations (v_log / v_sqrt / v_cos): the
+// weights only shape the labels, and a label flips only if its uniform draw lands
+// within ~1e-6 of the logistic probability.
 __device__ __forceinline__ float planted_w(uint64_t key, uint64_t seed) {
   const uint64_t r = rng64(seed ^ 0x5bd1e995ull, key);
-  if ((r & 0xff) >= 51) return 0.f;  // ~20% of features carry signal
+  if ((r & 0xff) >= 51) return 0.f;
   const float u1 = u01(rng64(seed, key * 2 + 7)), u2 = u01(r);
-  return 0.6f * sqrtf(-2.f * logf(u1)) * cosf(6.283185307f * u2);
+  return 0.6f * __fsqrt_rn(-2.f * __logf(u1)) * __cosf(6.283185307f * u2);
 }
 
 // h % N without a 64-bit division: Barrett reduction with m = floor((2^64 - 1) / N);
@@ -345,62 +349,66 @@ __device__ __forceinline__ uint64_t mod_barrett(uint64_t h, uint64_t N, uint64_t
   return r;
 }
 
-// u -> feature id of slot j; for categorical slots cm1 = powf(C_j, 1 - alpha) - 1
-// comes precomputed per block (same device powf, so the same ids as inline).
+// u -> feature id of slot j (j is wave-uniform at every call site, so the integer /
+// categorical branch never diverges). Integer slots: a heavy-tailed count x =
+// e^(12u) - 1 log2-bucketised, floor(2 log2(1 + x)) = floor(u * 24 log2 e) (the
+// CPU reference evaluates the same f32 product). Categorical slots: power-law id,
+// x = (cm1 * u + 1)^(1 / (1 - alpha)) with cm1 = C_j^(1 - alpha) - 1 per block.
 __device__ __forceinline__ uint64_t criteo_key(uint64_t seed, uint64_t gr, int j,
                                                uint64_t num_features, uint64_t nf_m,
-                                               float alpha, float cm1) {
+                                               float inv_oma, float cm1) {
   const float u = u01(rng64(seed + (uint64_t)j * 0x632be59bd9b4e019ull, gr));
   uint64_t id;
   if (j < 13) {
-    // integer feature: heavy tailed count, log2 bucketised (~<= 40 buckets)
-    const float x = expf(u * 12.f) - 1.f;
-    id = (uint64_t)(2.f * log2f(1.f + x));
+    id = (uint64_t)(u * 34.62468098f);  // 24 * log2(e)
   } else {
-    const float oma = 1.f - alpha;
-    const float x = powf(cm1 * u + 1.f, 1.f / oma);
+    const float x = powf(cm1 * u + 1.f, inv_oma);
     uint64_t v = (uint64_t)x;
     id = v >= 1 ? v - 1 : 0;
   }
   return mod_barrett(fmix64(((uint64_t)(j + 1) << 48) ^ id), num_features, nf_m);
 }
 
-// One thread per (row, slot): a 512-thread block generates 13 rows (507 features,
-// 99% of the lanes); the planted weights of a row are summed in slot order by one
-// lane (no LDS atomics), which then draws the row's label.
-constexpr int kGenRows = 13;
-constexpr int kGenThreads = 512;
+// 64 rows per block, one per lane; wave g of the 3 generates slots 13g .. 13g+12 of
+// every row (integer slots in wave 0, categorical in waves 1-2: no divergence), the
+// keys are staged in LDS and leave as one contiguous 64 x 39 x 8 B run, and wave 0
+// sums the three partial planted logits of its row and draws the label.
+constexpr int kGenRows = 64;
+constexpr int kGenThreads = 192;
 __global__ void __launch_bounds__(kGenThreads)
 criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_dev,
                   int64_t row_scale, int64_t B, uint64_t num_features, uint64_t nf_m,
                   float alpha, uint64_t* __restrict__ keys, float* __restrict__ labels) {
-  __shared__ float spw[kGenRows * 39];
+  __shared__ uint64_t sk[kGenRows * 39];
+  __shared__ float spw[3][kGenRows];
   __shared__ float s_cm1[26];
   if (row0_dev) row0 += (*row0_dev) * row_scale;
-  const int t = threadIdx.x;
-  if (t < 26) s_cm1[t] = powf((float)c_cards[t], 1.f - alpha) - 1.f;
+  const int t = threadIdx.x, lane = t & 63;
+  const int g = __builtin_amdgcn_readfirstlane(t >> 6);
+  const float oma = 1.f - alpha, inv_oma = 1.f / oma;
+  if (t < 26) s_cm1[t] = powf((float)c_cards[t], oma) - 1.f;
   __syncthreads();
-  const int lr = t / 39, j = t % 39;
   for (int64_t rb = (int64_t)blockIdx.x * kGenRows; rb < B; rb += (int64_t)gridDim.x * kGenRows) {
-    const int64_t r = rb + lr;
-    if (lr < kGenRows) {
-      float pw = 0.f;
-      if (r < B) {
+    const int64_t r = rb + lane;
+    float pw = 0.f;
+    if (r < B) {
+      for (int jj = 0; jj < 13; ++jj) {
+        const int j = g * 13 + jj;
         const uint64_t key = criteo_key(seed, (uint64_t)(row0 + r), j, num_features, nf_m,
-                                        alpha, j >= 13 ? s_cm1[j - 13] : 0.f);
-        keys[r * 39 + j] = key;
-        pw = planted_w(key, seed);
+                                        inv_oma, j >= 13 ? s_cm1[j - 13] : 0.f);
+        sk[lane * 39 + j] = key;
+        pw += planted_w(key, seed);
       }
-      spw[t] = pw;
     }
+    spw[g][lane] = pw;
     __syncthreads();
-    if (t < kGenRows && rb + t < B) {
-      float logit = -1.2f;
-      for (int q = 0; q < 39; ++q) logit += spw[t * 39 + q];
-      const int64_t r2 = rb + t;
+    const int nrow = (int)min<int64_t>(kGenRows, B - rb);
+    for (int i = t; i < nrow * 39; i += kGenThreads) keys[rb * 39 + i] = sk[i];
+    if (g == 0 && r < B) {
+      const float logit = -1.2f + spw[0][lane] + spw[1][lane] + spw[2][lane];
       const float p = 1.f / (1.f + expf(-logit));
-      const float u = u01(rng64(seed ^ 0xabcdefull, (uint64_t)(row0 + r2)));
-      labels[r2] = u < p ? 1.f : -1.f;
+      const float u = u01(rng64(seed ^ 0xabcdefull, (uint64_t)(row0 + r)));
+      labels[r] = u < p ? 1.f : -1.f;
     }
     __syncthreads();
   }

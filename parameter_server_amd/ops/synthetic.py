@@ -103,8 +103,8 @@ def _criteo_cpu(B, seed, row0, num_features, alpha, cards):
         for j in range(NUM_SLOTS):
             u = f32(_u01(_rng64((seed + j * 0x632BE59BD9B4E019) & M64, gr)))
             if j < 13:
-                x = f32(np.exp(f32(u * f32(12.0)), dtype=f32) - f32(1.0))
-                idv = int(f32(2.0) * np.log2(f32(1.0) + x, dtype=f32))
+                # floor(2 log2(1 + (e^(12u) - 1))) = floor(u * 24 log2 e), in f32 as the kernel
+                idv = int(f32(u) * f32(34.62468098))
             else:
                 C = f32(cards[j - 13])
                 oma = f32(1.0 - alpha)
