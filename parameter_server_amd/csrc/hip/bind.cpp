@@ -28,6 +28,12 @@ void kv_apply_part(void*, int64_t, const int64_t*, const uint64_t*, const float*
                    const int32_t*, int, int64_t, int64_t, const int32_t*, int, int, int, float, float,
                    float, float, float, float, double*, int, hipStream_t);
 // tploc.hip
+void tp_gather(const uint16_t*, const int32_t*, int64_t, int32_t*, hipStream_t);
+bool tp_fwd_bwd_supported(int);
+void tp_fwd_bwd(const uint16_t*, const int32_t*, const int32_t*, int64_t, int, const float*,
+                const float*, int64_t, const float*, int64_t, int, float*, double*, uint32_t*, int,
+                int, int, float*, const int32_t*, const int32_t*, const int32_t*, float*, int64_t,
+                hipStream_t);
 int64_t tploc_stride(int64_t);
 bool tploc_supported(int64_t, int);
 size_t tploc_temp_bytes(int64_t, int);
@@ -374,8 +380,8 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("tploc_temp_bytes", [](int64_t n, int bits) { return (int64_t)psamd::tploc_temp_bytes(n, bits); });
   m.def("localize_tp", [](Tensor keys, int bits, Tensor temp, Tensor dcnt, Tensor rep, Tensor pos_s,
                           Tensor segid, Tensor uniq, Tensor seg_start, Tensor ent_uid,
-                          Tensor local_col, Tensor n_uniq, Tensor n_ent, Tensor grad, Tensor err,
-                          optional<Tensor> prof) {
+                          optional<Tensor> local_col, Tensor n_uniq, Tensor n_ent, Tensor grad,
+                          Tensor err, optional<Tensor> prof) {
     chk(keys, at::kLong, "keys");
     chk(temp, at::kByte, "temp");
     chk(dcnt, at::kInt, "dcnt");
@@ -385,24 +391,25 @@ PYBIND11_MODULE(_hipops, m) {
     chk(uniq, at::kLong, "uniq");
     chk(seg_start, at::kInt, "seg_start");
     chk(ent_uid, at::kInt, "ent_uid");
-    chk(local_col, at::kInt, "local_col");
+    int32_t* lc = optr<int32_t>(local_col, at::kInt, "local_col");
     chk(n_uniq, at::kInt, "n_uniq");
     chk(n_ent, at::kInt, "n_ent");
     chk(grad, at::kFloat, "grad");
     chk(err, at::kInt, "err");
     const int64_t n = keys.numel();
     check(psamd::tploc_supported(n, bits), "tp localisation: 2..31 key bits, n <= 10.4M");
+    if (lc) check(local_col->numel() >= n, "local_col too small");
     const int64_t N = psamd::tploc_stride(n);
     const int64_t T = N / 8192;
     check(pos_s.numel() >= N && segid.numel() >= N && uniq.numel() >= N &&
               seg_start.numel() >= N + 1 && ent_uid.numel() >= N && grad.numel() >= N,
           "tp localisation buffers < stride");
-    check(dcnt.numel() >= T && rep.numel() >= n && local_col.numel() >= n, "tp buffers too small");
+    check(dcnt.numel() >= T && rep.numel() >= n, "tp buffers too small");
     check((size_t)temp.numel() >= psamd::tploc_temp_bytes(n, bits), "tp temp too small");
     psamd::localize_tp(ptr<uint64_t>(keys), n, make_keymix(bits), temp.data_ptr(),
                        (size_t)temp.numel(), ptr<int32_t>(dcnt), ptr<uint16_t>(rep),
                        ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<uint64_t>(uniq),
-                       ptr<int32_t>(seg_start), ptr<int32_t>(ent_uid), ptr<int32_t>(local_col),
+                       ptr<int32_t>(seg_start), ptr<int32_t>(ent_uid), lc,
                        ptr<int32_t>(n_uniq), ptr<int32_t>(n_ent), ptr<float>(grad),
                        ptr<int32_t>(err), uniq.numel(),
                        reinterpret_cast<uint64_t*>(optr<int64_t>(prof, at::kLong, "prof")),
@@ -430,6 +437,52 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::tp_backward(ptr<uint16_t>(rep), ptr<int32_t>(dcnt), n, r, width, v, ptr<float>(coef),
                        coef.numel(), ptr<float>(psum), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
                        ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), cur_stream());
+  });
+  m.def("tp_gather", [](Tensor rep, Tensor ent_uid, int64_t n, Tensor local_col) {
+    chk(rep, at::kShort, "rep");
+    chk(ent_uid, at::kInt, "ent_uid");
+    chk(local_col, at::kInt, "local_col");
+    check(n > 0 && rep.numel() >= n && local_col.numel() >= n &&
+              ent_uid.numel() >= psamd::tploc_stride(n), "tp gather buffers");
+    psamd::tp_gather(ptr<uint16_t>(rep), ptr<int32_t>(ent_uid), n, ptr<int32_t>(local_col),
+                     cur_stream());
+  });
+  m.def("tp_fwd_bwd_supported", [](int width) { return psamd::tp_fwd_bwd_supported(width); });
+  m.def("tp_fwd_bwd", [](Tensor rep, Tensor dcnt, Tensor ent_uid, int64_t n, int width,
+                         optional<Tensor> vals, Tensor w_local, Tensor labels, int64_t B,
+                         int loss_type, Tensor coef, optional<Tensor> metrics,
+                         optional<Tensor> hist, int nbins, Tensor psum, Tensor pos_s,
+                         Tensor segid, Tensor n_ent, Tensor grad) {
+    chk(rep, at::kShort, "rep");
+    chk(dcnt, at::kInt, "dcnt");
+    chk(ent_uid, at::kInt, "ent_uid");
+    chk(w_local, at::kFloat, "w_local");
+    chk(labels, at::kFloat, "labels");
+    chk(coef, at::kFloat, "coef");
+    chk(psum, at::kFloat, "psum");
+    chk(pos_s, at::kInt, "pos_s");
+    chk(segid, at::kInt, "segid");
+    chk(n_ent, at::kInt, "n_ent");
+    chk(grad, at::kFloat, "grad");
+    check(psamd::tp_fwd_bwd_supported(width) && n == B * (int64_t)width && n > 0,
+          "tp_fwd_bwd: fixed width 9..64 (tp_fwd_bwd_supported) and n == B * width");
+    const int64_t N = psamd::tploc_stride(n);
+    check(rep.numel() >= n && dcnt.numel() >= N / 8192 && ent_uid.numel() >= N,
+          "tp_fwd_bwd: rep / dcnt / ent_uid");
+    check(psum.numel() >= N && pos_s.numel() >= N && segid.numel() >= N, "tp_fwd_bwd buffers");
+    check(labels.numel() >= B && coef.numel() >= B, "labels/coef too small");
+    const float* v = optr<float>(vals, at::kFloat, "vals");
+    if (v) check(vals->numel() >= n, "vals too small");
+    uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
+    if (hp) check(nbins > 0 && nbins <= 8192 && hist->numel() >= 2 * nbins, "hist size");
+    double* mp = optr<double>(metrics, at::kDouble, "metrics");
+    if (mp) check(metrics->numel() >= 5, "metrics needs >= 5 slots");
+    psamd::tp_fwd_bwd(ptr<uint16_t>(rep), ptr<int32_t>(dcnt), ptr<int32_t>(ent_uid), n, width, v,
+                      ptr<float>(w_local), w_local.numel(), ptr<float>(labels), B, loss_type,
+                      ptr<float>(coef), mp, hp, nbins, acc_stripes_of(metrics),
+                      hp ? (int)std::max<int64_t>(1, hist->numel() / (2 * nbins)) : 1,
+                      ptr<float>(psum), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
+                      ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), cur_stream());
   });
   // ---------------- tile-deduplicating localisation (tileloc.hip) ----------------
   m.def("tileloc_stride", [](int64_t n) { return psamd::tileloc_stride(n); });

@@ -14,16 +14,11 @@
 // does a 64-lane segmented scan; only segments that cross a wave boundary
 // issue one float atomic per wave piece.
 #include "common.cuh"
+#include "loss.cuh"
 #include <stdexcept>
 #include <string>
 
 namespace psamd {
-
-enum LossType : int { kSquare = 1, kLogit = 2, kHinge = 3, kSquareHinge = 4 };
-
-__device__ __forceinline__ float softplus(float x) {
-  return x > 20.f ? x : (x < -20.f ? expf(x) : log1pf(expf(x)));
-}
 
 // Loss, dL/dm, accuracy and AUC bin of one example with margin m (lane-group leader).
 __device__ __forceinline__ void fwd_row_epilogue(int64_t r, float m, const float* __restrict__ labels,
@@ -32,41 +27,15 @@ __device__ __forceinline__ void fwd_row_epilogue(int64_t r, float m, const float
                                                  float* __restrict__ coef2_out, uint32_t* lhist,
                                                  int nbins, double& loss_acc, double& corr_acc,
                                                  double& cnt) {
-  const float y = labels[r] > 0.f ? 1.f : -1.f;
-  const float ym = y * m;
   float loss, coef, coef2;
-  switch (loss_type) {
-    case kSquare: {
-      const float d = m - labels[r];
-      loss = 0.5f * d * d; coef = d; coef2 = 1.f;
-      break;
-    }
-    case kHinge:
-      loss = fmaxf(0.f, 1.f - ym); coef = ym < 1.f ? -y : 0.f; coef2 = 0.f;
-      break;
-    case kSquareHinge: {
-      const float h = fmaxf(0.f, 1.f - ym);
-      loss = h * h; coef = -2.f * y * h; coef2 = ym < 1.f ? 2.f : 0.f;
-      break;
-    }
-    default: {  // logit: tau = 1/(1+exp(y m))
-      loss = softplus(-ym);
-      const float tau = 1.f / (1.f + expf(ym));
-      coef = -y * tau; coef2 = tau * (1.f - tau);
-      break;
-    }
-  }
+  loss_terms(m, labels[r], loss_type, loss, coef, coef2);
   if (xw_out) xw_out[r] = m;
   coef_out[r] = coef;
   if (coef2_out) coef2_out[r] = coef2;
   loss_acc += loss;
-  corr_acc += ((y > 0.f) == (m > 0.f)) ? 1.0 : 0.0;  // evaluation.h:55-57
+  corr_acc += ((labels[r] > 0.f) == (m > 0.f)) ? 1.0 : 0.0;  // evaluation.h:55-57
   cnt += 1.0;
-  if (lhist) {
-    const float p = 1.f / (1.f + expf(-m));
-    const float pb = p == p ? fminf(fmaxf(p * nbins, 0.f), (float)(nbins - 1)) : 0.f;
-    atomicAdd(&lhist[(y > 0.f ? nbins : 0) + (int)pb], 1u);
-  }
+  if (lhist) atomicAdd(&lhist[auc_bin(m, labels[r], nbins)], 1u);
 }
 
 template <bool kHasRowPtr, int kLPR>

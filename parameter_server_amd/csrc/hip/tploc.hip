@@ -29,6 +29,7 @@
 // Buckets are ranges of the mixed key space, so the unique keys come out sorted
 // (the multi-GPU owner split and the ordered home slots of the KV table rely on it).
 #include "common.cuh"
+#include "loss.cuh"
 
 #include <cstdlib>
 #include <stdexcept>
@@ -601,6 +602,147 @@ tp_seg_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restric
   }
 }
 
+// Fused forward + per-tile backward of a fixed-width linear model on a tp
+// localisation, one workgroup per 8192-occurrence tile (replaces the local-column
+// gather, linear_fwd and tp_bwd_accum: three launches and two global round trips).
+// Every row overlapping the tile gets kFbLanes lanes strided over its occurrences.
+//   prologue (all global loads in flight together): each lane's occurrences
+//     (rep, val) into registers, the rows' labels into LDS, the tile's entry
+//     weights wl[e] = w_local[ent_uid[tile + e]] into LDS; an occurrence of a row
+//     cut by the tile boundary resolves its weight through the global entry map
+//     and keeps w * val in its register slot;
+//   forward: margins from registers + LDS, a shuffle reduction per lane group, the
+//     leader computes the loss terms (the tile holding a row's first occurrence
+//     owns its coef output, metrics and AUC bin);
+//   backward: the same registers add coef * val into wl (re-zeroed) at rep, then
+//     the per-entry partials psum[tile + e] go to tp_seg_reduce_kernel.
+// PER = occurrences per lane per row (width <= 8 * PER), NP = row passes held in
+// registers (128 rows each): compile-time so the register slots stay registers.
+constexpr int kFbLanes = 8;
+constexpr int kFbMaxRows = tp::kTile / 8 + 2;  // width >= 8
+constexpr uint16_t kFbNone = 0xffff, kFbExt = 0xfffe;
+
+template <int PER, int NP>
+__global__ void __launch_bounds__(tp::kThr)  // (PER 5: 58 VGPRs -> 2 workgroups per CU)
+tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ dcnt,
+                  const int32_t* __restrict__ ent_uid, int64_t n, int width,
+                  const float* __restrict__ vals, const float* __restrict__ w_local, int64_t w_cap,
+                  const float* __restrict__ labels, int64_t B, int loss_type,
+                  float* __restrict__ coef_out, double* __restrict__ metrics,
+                  uint32_t* __restrict__ hist, int nbins, int acc_stripes, int hist_stripes,
+                  float* __restrict__ psum) {
+  using namespace tp;
+  __shared__ float wl[kTile];
+  __shared__ float crow[kFbMaxRows];  // labels, then coef of the tile's rows
+  __shared__ double red[16];
+  extern __shared__ uint32_t lhist[];  // [2 * nbins] when hist != nullptr
+  constexpr int kRowsPass = kThr / kFbLanes;
+  const int t = threadIdx.x, sub = t % kFbLanes, g = t / kFbLanes;
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int lim = (int)(n - base < kTile ? n - base : kTile);
+  const int64_t r0 = base / width;
+  const int nr = (int)((base + lim - 1) / width - r0 + 1);
+  const int cnt = min(kTile, max(0, dcnt[blockIdx.x]));
+  uint16_t ce[NP][PER];
+  float cv[NP][PER];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int ri = p * kRowsPass + g;
+    const int64_t r = r0 + ri;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int k = sub + q * kFbLanes;
+      ce[p][q] = kFbNone;
+      cv[p][q] = 0.f;
+      if (ri < nr && r < B && k < width) {
+        const int64_t i = r * width + k;
+        const int64_t o = i - base;
+        ce[p][q] = (o >= 0 && o < lim) ? rep[i] : kFbExt;
+        cv[p][q] = vals ? vals[i] : 1.f;
+      }
+    }
+  }
+  for (int i = t; i < nr; i += kThr) crow[i] = r0 + i < B ? labels[r0 + i] : 0.f;
+  for (int i = t; i < cnt; i += kThr) {
+    const int32_t u = ent_uid[base + i];
+    wl[i] = in_range(u, w_cap) ? w_local[u] : 0.f;
+  }
+  if (hist)
+    for (int i = t; i < 2 * nbins; i += kThr) lhist[i] = 0u;
+  // boundary rows: the outside part of row 0 / row nr-1 (only their lane groups)
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int ri = p * kRowsPass + g;
+    if (ri != 0 && ri != nr - 1) continue;
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+      if (ce[p][q] == kFbExt) {
+        const int64_t i = (r0 + ri) * width + sub + q * kFbLanes;
+        const int32_t u = ent_uid[(i & ~(int64_t)(kTile - 1)) + rep[i]];
+        cv[p][q] *= in_range(u, w_cap) ? w_local[u] : 0.f;
+      }
+  }
+  __syncthreads();
+  double loss_acc = 0, corr_acc = 0, rows_acc = 0;
+  float cf[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    float m = 0.f;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const uint16_t e = ce[p][q];
+      if (e == kFbExt) m += cv[p][q];
+      else if (e != kFbNone) m += wl[e] * cv[p][q];
+    }
+#pragma unroll
+    for (int off = kFbLanes / 2; off > 0; off >>= 1) m += __shfl_xor(m, off, 64);
+    const int ri = p * kRowsPass + g;
+    const int64_t r = r0 + ri;
+    float c = 0.f;
+    if (ri < nr && r < B) {
+      const float lab = crow[ri];
+      float loss, c2;
+      loss_terms(m, lab, loss_type, loss, c, c2);
+      if (sub == 0 && r * width >= base) {  // first occurrence in this tile: the row is ours
+        coef_out[r] = c;
+        loss_acc += loss;
+        corr_acc += ((lab > 0.f) == (m > 0.f)) ? 1.0 : 0.0;
+        rows_acc += 1.0;
+        if (hist) atomicAdd(&lhist[auc_bin(m, lab, nbins)], 1u);
+      }
+    }
+    cf[p] = c;  // every lane of the group holds its row's coef
+  }
+  __syncthreads();
+  for (int i = t; i < cnt; i += kThr) wl[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    if (cf[p] == 0.f) continue;
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+      if (ce[p][q] < kFbExt) atomicAdd(&wl[ce[p][q]], cf[p] * cv[p][q]);
+  }
+  if (metrics) {
+    const double a = block_sum_f64(loss_acc, red);
+    const double b = block_sum_f64(corr_acc, red);
+    const double c = block_sum_f64(rows_acc, red);
+    if (t == 0 && c > 0) {
+      double* mt = acc_stripe(metrics, acc_stripes);
+      atomicAdd(&mt[0], a);
+      atomicAdd(&mt[1], b);
+      atomicAdd(&mt[2], c);
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < cnt; i += kThr) psum[base + i] = wl[i];
+  if (hist) {
+    uint32_t* hs = hist + (int64_t)(blockIdx.x % hist_stripes) * 2 * nbins;
+    for (int i = t; i < 2 * nbins; i += kThr)
+      if (lhist[i]) atomicAdd(&hs[i], lhist[i]);
+  }
+}
+
 // ---------------------------------------------------------------------------
 struct TpGeom {
   int nbk, shift;
@@ -671,8 +813,10 @@ void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t te
                                                         ecount, pos_s, segid, uniq, seg_start,
                                                         ent_uid, n_uniq, n_ent, grad, u_cap, g.N);
   PSAMD_HIP_CHECK(hipGetLastError());
-  tp_gather_kernel<<<(unsigned)((n + 1023) / 1024), 256, 0, st>>>(rep, ent_uid, n, local_col);
-  PSAMD_HIP_CHECK(hipGetLastError());
+  if (local_col) {  // (skipped when the fused forward reads the entry map directly)
+    tp_gather_kernel<<<(unsigned)((n + 1023) / 1024), 256, 0, st>>>(rep, ent_uid, n, local_col);
+    PSAMD_HIP_CHECK(hipGetLastError());
+  }
 }
 
 void tp_backward(const uint16_t* rep, const int32_t* dcnt, int64_t n, const int32_t* rows,
@@ -689,6 +833,57 @@ void tp_backward(const uint16_t* rep, const int32_t* dcnt, int64_t n, const int3
   else
     tp_bwd_accum_kernel<<<(unsigned)g.T, tp::kThr, 0, st>>>(rep, dcnt, n, rows, width, vals, coef,
                                                             B, psum);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  tp_seg_reduce_kernel<<<grid_for(g.N, 256, 2048), 256, 0, st>>>(pos_s, segid, g.N, n_ent, psum,
+                                                                 g.N, grad, grad_cap);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void tp_gather(const uint16_t* rep, const int32_t* ent_uid, int64_t n, int32_t* local_col,
+               hipStream_t st) {
+  if (n <= 0) return;
+  tp_gather_kernel<<<(unsigned)((n + 1023) / 1024), 256, 0, st>>>(rep, ent_uid, n, local_col);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+// register-held occurrences: PER = ceil(width / 8) in 2..8, NP = the row passes of
+// the narrowest width with that PER (fewer register slots -> 2 workgroups per CU)
+static int tp_fb_passes(int width) {
+  return (int)((tp::kTile / width + 2 + tp::kThr / kFbLanes - 1) / (tp::kThr / kFbLanes));
+}
+static constexpr int kFbNP[9] = {0, 0, 8, 4, 3, 2, 2, 2, 2};
+
+bool tp_fwd_bwd_supported(int width) {
+  if (width < 9 || width > 64) return false;
+  return tp_fb_passes(width) <= kFbNP[(width + kFbLanes - 1) / kFbLanes];
+}
+
+void tp_fwd_bwd(const uint16_t* rep, const int32_t* dcnt, const int32_t* ent_uid, int64_t n,
+                int width, const float* vals, const float* w_local, int64_t w_cap,
+                const float* labels, int64_t B, int loss_type, float* coef_out, double* metrics,
+                uint32_t* hist, int nbins, int acc_stripes, int hist_stripes, float* psum,
+                const int32_t* pos_s, const int32_t* segid, const int32_t* n_ent, float* grad,
+                int64_t grad_cap, hipStream_t st) {
+  if (n <= 0) return;
+  if (!tp_fwd_bwd_supported(width) || n != B * (int64_t)width)
+    throw std::runtime_error("tp_fwd_bwd: unsupported width or n != B * width");
+  const TpGeom g = tp_geom(n, 31);
+  const size_t lds = hist ? (size_t)2 * nbins * sizeof(uint32_t) : 0;
+  const int per = (width + kFbLanes - 1) / kFbLanes;
+#define PSAMD_FB(PER, NP)                                                                     \
+  tp_fwd_bwd_kernel<PER, NP><<<(unsigned)g.T, tp::kThr, lds, st>>>(                          \
+      rep, dcnt, ent_uid, n, width, vals, w_local, w_cap, labels, B, loss_type, coef_out,     \
+      metrics, hist, nbins, acc_stripes, hist_stripes, psum)
+  switch (per) {  // NP = kFbNP[PER] row passes in registers (tp_fwd_bwd_supported)
+    case 2: PSAMD_FB(2, 8); break;
+    case 3: PSAMD_FB(3, 4); break;
+    case 4: PSAMD_FB(4, 3); break;
+    case 5: PSAMD_FB(5, 2); break;
+    case 6: PSAMD_FB(6, 2); break;
+    case 7: PSAMD_FB(7, 2); break;
+    default: PSAMD_FB(8, 2); break;
+  }
+#undef PSAMD_FB
   PSAMD_HIP_CHECK(hipGetLastError());
   tp_seg_reduce_kernel<<<grid_for(g.N, 256, 2048), 256, 0, st>>>(pos_s, segid, g.N, n_ent, psum,
                                                                  g.N, grad, grad_cap);

@@ -40,8 +40,8 @@ from ..ops import fixing_float as ff
 from ..ops.countmin import CountMinSketch
 from ..ops.keymix import key_bits_for, unmix
 from ..ops.kv_table import InitRule, KVTable, UpdateRule, next_pow2
-from ..ops.linear import (AUC_BINS, HIST_STRIPES, accum_total, auc_from_hist, linear_backward,
-                          linear_forward, new_accum)
+from ..ops.linear import (AUC_BINS, HIST_STRIPES, accum_total, auc_from_hist, linear_fwd_bwd,
+                          new_accum)
 from ..ops.localize import Localizer
 from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
@@ -120,7 +120,9 @@ class SparseLRTrainer:
             mode = "tp"     # for > 31-bit keys or > 5.2 M keys per minibatch)
         if cfg.tail_feature_freq > 0 and mode in ("tile", "hash", "tp"):
             mode = "sort"  # the tail filter needs per-key nnz counts (seg_start over nnz)
-        self.localizer = Localizer(self.max_nnz, self.bits, self.device, mode=mode)
+        # local columns on demand: the fused tp forward/backward reads the entry map
+        self.localizer = Localizer(self.max_nnz, self.bits, self.device, mode=mode,
+                                   lazy_cols=True)
         self.localize_mode = self.localizer.mode  # after the Localizer's fallbacks
         self._localizers = [self.localizer]  # + a second buffer set for prefetching (G > 1)
         self.filter = (CountMinSketch(int(cfg.countmin_n), cfg.countmin_k, self.device)
@@ -193,7 +195,7 @@ class SparseLRTrainer:
         exchange (``step(..., loc=..., prefetch=...)``)."""
         while len(self._localizers) <= buf:
             self._localizers.append(Localizer(self.max_nnz, self.bits, self.device,
-                                              mode=self.localize_mode))
+                                              mode=self.localize_mode, lazy_cols=True))
         return self._localizers[buf](keys)
 
     def step(self, keys: torch.Tensor, labels: torch.Tensor, *, width: int | None = None,
@@ -247,10 +249,9 @@ class SparseLRTrainer:
             self._prefetch = None
         _cmp = trace_range("compute")
         _cmp.__enter__()
-        _, coef, _ = linear_forward(loc.local_col, w_local, labels, B=B, width=width or 0,
-                                    row_ptr=row_ptr, vals=vals, loss=self.cfg.loss,
-                                    coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
-        grad, _ = linear_backward(loc, coef, B=B, width=width or 0, rows=rows, vals=vals)
+        coef, grad = linear_fwd_bwd(loc, w_local, labels, B=B, width=width or 0, row_ptr=row_ptr,
+                                    rows=rows, vals=vals, loss=self.cfg.loss, coef=self.coef[:B],
+                                    metrics=self.metrics, hist=self.hist)
         _cmp.__exit__(None, None, None)
         _push = trace_range("push")
         _push.__enter__()
@@ -590,10 +591,9 @@ class SparseLRTrainer:
                 a, c = int(off[p]), min(int(off[p + 1] - off[p]), xc.C)
                 dst = perm[a:a + c].long() if perm is not None else slice(a, a + c)
                 w_local[dst] = wrecv[p * xc.C:p * xc.C + c]
-        _, coef, _ = linear_forward(loc.local_col, w_local, labels, B=B, width=width or 0,
-                                    row_ptr=row_ptr, vals=vals, loss=self.cfg.loss,
-                                    coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
-        grad, _ = linear_backward(loc, coef, B=B, width=width or 0, rows=rows, vals=vals)
+        coef, grad = linear_fwd_bwd(loc, w_local, labels, B=B, width=width or 0, row_ptr=row_ptr,
+                                    rows=rows, vals=vals, loss=self.cfg.loss, coef=self.coef[:B],
+                                    metrics=self.metrics, hist=self.hist)
         H, C, kw = xc.H, xc.C, xc.kw
         if xc.nb:
             self._x_ff_pack(grad[:loc.uniq.numel()], perm, n_uniq, off, send)

@@ -137,6 +137,31 @@ def linear_backward(loc, coef, *, B: int, width: int = 0, rows=None, vals=None, 
     return loc.grad, loc.hess
 
 
+def linear_fwd_bwd(loc, w_local, labels, *, B: int, width: int = 0, row_ptr=None, rows=None,
+                   vals=None, loss="logit", coef=None, metrics=None, hist=None):
+    """Forward (loss, dL/dm, metrics, AUC histogram) and backward into loc.grad of one
+    minibatch; returns (coef, grad). A fixed-width "tp" localisation runs ONE fused
+    per-tile kernel plus the entry scan (tploc.hip tp_fwd_bwd: no per-occurrence
+    local-column gather, no coef round trip through memory); anything else runs
+    linear_forward + linear_backward."""
+    t = getattr(loc, "tile", None)
+    if (t is not None and t.size == 8192 and t.ent_uid is not None and row_ptr is None
+            and rows is None and width and loc.nnz == B * width and is_gpu(w_local)
+            and hipops().tp_fwd_bwd_supported(width)):
+        coef = torch.empty(B, dtype=torch.float32, device=w_local.device) if coef is None else coef
+        hipops().tp_fwd_bwd(t.rep, t.dcnt, t.ent_uid, loc.nnz, width, vals, w_local, labels, B,
+                            loss_id(loss), coef, metrics, hist, AUC_BINS, t.psum, loc.pos_s,
+                            loc.segid, t.n_ent, loc.grad)
+        return coef, loc.grad
+    from .localize import ensure_local_col
+
+    _, coef, _ = linear_forward(ensure_local_col(loc), w_local, labels, B=B, width=width,
+                                row_ptr=row_ptr, vals=vals, loss=loss, coef=coef,
+                                metrics=metrics, hist=hist)
+    grad, _ = linear_backward(loc, coef, B=B, width=width, rows=rows, vals=vals)
+    return coef, grad
+
+
 def auc_from_hist(hist: torch.Tensor, metrics: torch.Tensor, step_counter=None):
     """metrics[3] += AUC of the histogram, metrics[4] += 1; zeroes hist; optionally
     increments a device step counter (one epilogue kernel per step)."""

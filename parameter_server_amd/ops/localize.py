@@ -52,6 +52,19 @@ class TileInfo:
     n_ent: torch.Tensor  # int32[1] total entries (device)
     psum: torch.Tensor   # float [tiles*size] per-entry partial gradients (backward scratch)
     size: int = 4096     # occurrences per tile (4096: "tile" mode, 8192: "tp" mode)
+    ent_uid: torch.Tensor | None = None  # int32 [tiles*size] tile entry -> unique id ("tp")
+    cols_ready: bool = True  # False: local_col not materialised yet (ensure_local_col)
+
+
+def ensure_local_col(loc: "Localized") -> torch.Tensor:
+    """local_col of a lazily localised "tp" minibatch (``Localizer(lazy_cols=True)``
+    skips the per-occurrence gather: the fused forward/backward reads the tile entry
+    map instead); runs the gather on first use."""
+    t = getattr(loc, "tile", None)
+    if t is not None and not t.cols_ready:
+        hipops().tp_gather(t.rep, t.ent_uid, loc.nnz, loc.local_col)
+        t.cols_ready = True
+    return loc.local_col
 
 
 class Localizer:
@@ -83,8 +96,9 @@ class Localizer:
     the backward accumulates per tile in LDS and scans the entry CSC (``TileInfo``)."""
 
     def __init__(self, max_nnz: int, bits: int, device="cpu", with_hess: bool = False,
-                 mode: str = "sort"):
+                 mode: str = "sort", lazy_cols: bool = False):
         self.max_nnz = int(max_nnz)
+        self.lazy_cols = bool(lazy_cols)  # "tp": local_col on demand (ensure_local_col)
         self.bits = int(bits)
         self.device = torch.device(device)
         self.with_hess = with_hess
@@ -242,10 +256,12 @@ class Localizer:
                              self.local_col[:n], self.n_uniq, self.grad, None, n, tile=tile)
         if self.mode == "tp":
             H.localize_tp(keys, self.bits, self.ptemp, self.t_dcnt, self.t_rep, self.pos_s,
-                          self.segid, self.uniq, self.seg_start, self.t_ent_uid, self.local_col,
+                          self.segid, self.uniq, self.seg_start, self.t_ent_uid,
+                          None if self.lazy_cols else self.local_col,
                           self.n_uniq, self.t_nent, self.grad, self.err,
                           getattr(self, "tp_prof", None))
-            tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum, 8192)
+            tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum, 8192,
+                            self.t_ent_uid, not self.lazy_cols)
             # unique keys <= n: expose n-sized views (the workspace is tile-rounded)
             return Localized(self.uniq[:n], self.seg_start, self.pos_s, self.segid,
                              self.local_col[:n], self.n_uniq, self.grad[:n], None, n, tile=tile)
