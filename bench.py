@@ -396,6 +396,13 @@ def main():
             state["t"] = t + 1
 
         run = pipelined_step
+    import contextlib
+
+    scope = contextlib.ExitStack()
+    mprio = os.environ.get("PSAMD_MAIN_PRIORITY")
+    if gpu and mprio is not None:
+        # the training step on its own stream of this priority instead of the null stream
+        scope.enter_context(torch.cuda.stream(torch.cuda.Stream(device, priority=int(mprio))))
     if gpu and args.pipeline and (G == 1 or tr.padded):
         nprep = args.prep_streams or (3 if G == 1 else 2)
         args.prep_streams = nprep
@@ -486,6 +493,7 @@ def main():
                       "table_occupied_rank0": occ, "nnz_w_rank0": nnz},
         }
         print(json.dumps(out), flush=True)
+    scope.close()
     if args.trace:
         from parameter_server_amd.utils import trace
 

@@ -50,7 +50,7 @@ void gemm_nt256(const __bf16*, int64_t, const __bf16*, int64_t, int, int, int, c
 void kvv_pack_vals(const float*, int, const int32_t*, const int32_t*, const int32_t*, int64_t,
                    int64_t, const int64_t*, int, int64_t, int, int64_t, int32_t*, hipStream_t);
 void kvv_serve(const int32_t*, int, int64_t, int64_t, const int64_t*, const float*, int64_t, int,
-               float*, hipStream_t);
+               int64_t, float*, hipStream_t);
 void kvv_apply(const int32_t*, int, int64_t, int64_t, int, const int64_t*, float*, int64_t, int, int,
                hipStream_t);
 void kvv_unpack(const float*, int64_t, int, const int64_t*, int, const int32_t*, int64_t, float*,
@@ -683,7 +683,7 @@ PYBIND11_MODULE(_hipops, m) {
     check(pos_s.numel() >= nnz, "pos_s < nnz");
     const int64_t u_cap = std::min<int64_t>(seg_start.numel() - 1, nnz);
     check(u_cap >= 1, "seg_start too small");
-    check(kw == 1 || kw == 2, "kw must be 1 or 2");
+    check(kw >= 0 && kw <= 2, "kw must be 0 (key-less row of a registered key set), 1 or 2");
     check(C > 0 && H >= 4 + C * kw + C * k && H % 4 == 0, "bad push row geometry");
     check(send.numel() == G * H, "send must be [G * H]");
     psamd::kvv_pack_vals(ptr<float>(vals), (int)k, ptr<int32_t>(pos_s), ptr<int32_t>(seg_start),
@@ -695,14 +695,28 @@ PYBIND11_MODULE(_hipops, m) {
     chk(slot, at::kLong, "slot");
     chk(vals, at::kFloat, "vals");
     chk(rec, at::kFloat, "rec");
-    check(H > 4 && C > 0 && recv.numel() % H == 0, "bad exchange row geometry");
+    check(H >= 4 && C > 0 && recv.numel() % H == 0, "bad exchange row geometry");
     const int G = (int)(recv.numel() / H);
     check(G >= 1 && G <= 64, "1..64 peers");
     check(vals.dim() == 2, "vals must be [capacity, k]");
     const int64_t k = vals.size(1);
     check(slot.numel() >= G * C && rec.numel() >= G * C * k, "slot / rec < G*C(*k)");
     psamd::kvv_serve(ptr<int32_t>(recv), G, H, C, ptr<int64_t>(slot), ptr<float>(vals),
-                     vals.size(0), (int)k, ptr<float>(rec), cur_stream());
+                     vals.size(0), (int)k, k, ptr<float>(rec), cur_stream());
+  });
+  // scalar tables (optimizer rules): serve the w field of the 32-B KV slots
+  m.def("kv_serve_w", [](Tensor recv, int64_t H, int64_t C, Tensor slot, Tensor slots, Tensor rec) {
+    chk(recv, at::kInt, "recv");
+    chk(slot, at::kLong, "slot");
+    chk(rec, at::kFloat, "rec");
+    const int64_t cap = slot_capacity(slots);
+    check(H >= 4 && C > 0 && recv.numel() % H == 0, "bad exchange row geometry");
+    const int G = (int)(recv.numel() / H);
+    check(G >= 1 && G <= 64, "1..64 peers");
+    check(slot.numel() >= G * C && rec.numel() >= G * C, "slot / rec < G*C");
+    const float* w = reinterpret_cast<const float*>(static_cast<const char*>(slots.data_ptr()) + 8);
+    psamd::kvv_serve(ptr<int32_t>(recv), G, H, C, ptr<int64_t>(slot), w, cap, 1, 8,
+                     ptr<float>(rec), cur_stream());
   });
   m.def("kvv_apply", [](Tensor recv, int64_t H, int64_t C, int kw, Tensor slot, Tensor vals,
                         int op) {
@@ -712,7 +726,7 @@ PYBIND11_MODULE(_hipops, m) {
     check(op == 0 || op == 1, "op: 0 = add, 1 = assign");
     check(vals.dim() == 2, "vals must be [capacity, k]");
     const int64_t k = vals.size(1);
-    check(kw == 1 || kw == 2, "kw must be 1 or 2");
+    check(kw >= 0 && kw <= 2, "kw must be 0 (key-less row), 1 or 2");
     check(C > 0 && H >= 4 + C * kw + C * k && recv.numel() % H == 0, "bad push row geometry");
     const int G = (int)(recv.numel() / H);
     check(G >= 1 && G <= 64, "1..64 peers");

@@ -10,6 +10,10 @@
 // (header word 0 = live key count), rows go through ONE equal-split all-to-all, and
 // the owner resolves, serves or merges all G source rows in one launch each. No
 // per-call sizes reach the host, so push / pull never synchronise the stream.
+// Registered key sets (KVWorker.register_keys, the reference's KeyCachingFilter,
+// src/filter/key_caching.h:6-76) push key-less rows [hdr 4 | values C*k] (kw = 0)
+// against the owner's cached slots, and their pulls need no request rows at all: the
+// owner serves its cached slots straight into the one value all-to-all.
 #include "common.cuh"
 
 namespace psamd {
@@ -41,6 +45,7 @@ __global__ void kvv_pack_vals_kernel(const float* __restrict__ vals, int k,
   if (blockIdx.x == 0 && threadIdx.x < G) {  // header word 1: value count (= key count)
     const int64_t cnt = soff[threadIdx.x + 1] - soff[threadIdx.x];
     send[(int64_t)threadIdx.x * H + 1] = (int32_t)(cnt < C ? cnt : C);
+    if (kw == 0) send[(int64_t)threadIdx.x * H] = (int32_t)(cnt < C ? cnt : C);  // key-less row
   }
   const int64_t n = dev_len(n_uniq, u_cap);
   const int64_t total = n * k;
@@ -64,11 +69,12 @@ __global__ void kvv_pack_vals_kernel(const float* __restrict__ vals, int k,
 }
 
 // Owner: the value rows of every resolved entry of every source row -> rec[s*C*k ..].
-// grid.y = source row.
+// grid.y = source row; table row sl starts at table_vals + sl * stride (stride = k for a
+// [cap, k] value block, 8 floats for the w field of the 32-B KV slots).
 __global__ void kvv_serve_kernel(const int32_t* __restrict__ recv, int64_t H, int64_t C,
                                  const int64_t* __restrict__ slot,
                                  const float* __restrict__ table_vals, int64_t cap, int k,
-                                 float* __restrict__ rec) {
+                                 int64_t stride, float* __restrict__ rec) {
   const int s = blockIdx.y;
   const int64_t n = dev_len(recv + (int64_t)s * H, C);
   const int64_t total = n * k;
@@ -77,7 +83,7 @@ __global__ void kvv_serve_kernel(const int32_t* __restrict__ recv, int64_t H, in
     const int64_t i = e / k;
     const int j = (int)(e - i * k);
     const int64_t sl = slot[(int64_t)s * C + i];
-    rec[(int64_t)s * C * k + e] = in_range(sl, cap) ? table_vals[sl * k + j] : 0.f;
+    rec[(int64_t)s * C * k + e] = in_range(sl, cap) ? table_vals[sl * stride + j] : 0.f;
   }
 }
 
@@ -142,9 +148,10 @@ void kvv_pack_vals(const float* vals, int k, const int32_t* pos_s, const int32_t
 }
 
 void kvv_serve(const int32_t* recv, int G, int64_t H, int64_t C, const int64_t* slot,
-               const float* table_vals, int64_t cap, int k, float* rec, hipStream_t st) {
+               const float* table_vals, int64_t cap, int k, int64_t stride, float* rec,
+               hipStream_t st) {
   dim3 grid(grid_for(C * k, 256, 1024), G);
-  kvv_serve_kernel<<<grid, 256, 0, st>>>(recv, H, C, slot, table_vals, cap, k, rec);
+  kvv_serve_kernel<<<grid, 256, 0, st>>>(recv, H, C, slot, table_vals, cap, k, stride, rec);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

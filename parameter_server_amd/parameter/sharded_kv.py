@@ -40,6 +40,18 @@ gates every pull: ``admissible(P)`` must hold). ``bsp`` is tau = 0. ``asp`` appl
 each push on a separate apply stream as soon as it arrives and no pull waits for it
 (a pull sees whatever has landed). ``flush()`` applies everything pending.
 
+Key caching (reference KeyCachingFilter, src/filter/key_caching.h:6-76: the sender
+hashes a key list into a signature and, when the receiver already holds the list of
+that signature, sends the values only): ``h = register_keys(keys)`` is a collective
+call that localises the keys once, sends them to the owners once, and keeps the
+localisation on the worker and the resolved slots of every source row on the owners.
+``pull(h)`` then needs no request exchange at all (the owners serve their cached
+slots straight into the one value all-to-all) and ``push(h, vals)`` sends key-less
+rows ``[hdr | values]``. The device key signature (``ops.fixing_float.key_signature``)
+deduplicates registrations: registering a key list whose signature every rank already
+holds returns the existing handle. Handle calls are SPMD like every other call (every
+rank passes its handle of the same ``register_keys`` call).
+
 Server-side push semantics: ``"add"`` (KVVector PLUS, kv_vector.h:70-75),
 ``"assign"``, or an optimizer ``UpdateRule`` (SGD / AdaGrad / FTRL, scalar values,
 kv_store.h:47-57 + async_sgd.h:71-124).
@@ -60,6 +72,24 @@ from ..parallel.consistency import INF, VectorClock, parse_consistency
 from ..parallel.partition import KeyPartition
 
 ADD, ASSIGN = 0, 1
+
+
+class KeyHandle:
+    """A registered key list (``KVWorker.register_keys``): the worker's localisation
+    (unique-id per request position, duplicates' CSC order, per-owner offsets) and the
+    owner's resolved slots of every source row, cached for key-less push / pull."""
+
+    def __init__(self, hid: int, n: int, signature: int):
+        self.id, self.n, self.signature = hid, n, signature
+        self.loc = None    # worker: localisation of the key list
+        self.off = None    # worker: per-owner offsets of its unique keys [G + 1]
+        self.slot = None   # owner: resolved slots of every source row [G * C] (GPU)
+        self.hdr = None    # owner: received row headers [G * 4] (live counts, GPU)
+        self.rows = None   # owner (CPU path): [(slots, count)] per source row
+        self.live = True
+
+    def __repr__(self):
+        return f"KeyHandle(id={self.id}, n={self.n}, signature={self.signature:#018x})"
 
 
 class KVServer:
@@ -125,10 +155,12 @@ class KVWorker:
         self.C, self.kw = C, kw
         self.Hk = (4 + C * kw + 1 + 3) // 4 * 4          # pull rows: header + keys
         self.Hp = (4 + C * kw + C * k + 3) // 4 * 4       # push rows: + k values per key
+        self.Hv = (4 + C * k + 3) // 4 * 4                # key-less push rows (registered keys)
         self._ts = 0
         self._pushes = 0          # pushes issued (the worker's step clock)
         self._done: dict[int, tuple] = {}
-        self._pending: deque = deque()  # (push index, received rows) not yet applied
+        self._pending: deque = deque()  # (push index, received rows, handle) not yet applied
+        self._handles: list[KeyHandle] = []  # registered key lists, in registration order
         G, dev = self.G, self.device
         if self.gpu:
             self.stream = torch.cuda.Stream(self.device)
@@ -217,9 +249,89 @@ class KVWorker:
         return v if n is None else v[:n]
 
     # ----------------------------------------------------------------- API
-    def pull(self, keys: torch.Tensor) -> int:
-        """Values of ``keys`` (any order, duplicates allowed) -> timestamp; ``wait``
-        returns ``[n]`` (dim 1) or ``[n, dim]`` float32 values in request order."""
+    def register_keys(self, keys: torch.Tensor) -> KeyHandle:
+        """Collective: register a key list for key-less push / pull (key caching).
+        Localises the keys once and resolves them at their owners (inserting new keys
+        with the InitRule), keeping both sides' results. A list whose device signature
+        and length every rank has registered before returns that handle (one host read
+        of the signature: a setup call, not a per-step one)."""
+        from ..ops.fixing_float import key_signature
+
+        keys = self._keys(keys)
+        sig = key_signature(keys) if keys.numel() else 0
+        old = next((h for h in self._handles
+                    if h.live and h.signature == sig and h.n == keys.numel()), None)
+        hit = old is not None
+        if self.G > 1:  # reuse only when every rank holds the list (SPMD geometry)
+            t = torch.tensor([1.0 if hit else 0.0], dtype=torch.float64,
+                             device=self.device if getattr(self.comm, "backend", "") == "nccl"
+                             else "cpu")
+            hit = float(self.comm.all_reduce_(t, op="min").item()) > 0
+        if hit:
+            return old
+        h = KeyHandle(len(self._handles), keys.numel(), sig)
+        self._handles.append(h)
+
+        def op():
+            self._register(keys, h)
+
+        self.wait(self._run(op))
+        return h
+
+    def release(self, h: KeyHandle) -> None:
+        """Drop a registered key list's cached state (collective in effect: call it on
+        every rank with the same handle)."""
+        h.live = False
+        h.loc = h.off = h.slot = h.hdr = h.rows = None
+
+    def _register(self, keys, h: KeyHandle):
+        C, H, G = self.C, self.Hk, self.G
+        loc = self._localize(keys)
+        tb = self.server.table
+        n = keys.numel()
+        if self.gpu:
+            hh = hipops()
+            if loc is None:
+                hh.xchg_clear_counts(self.send_k, G, H, True, True)
+            else:
+                off = self._offsets(loc)
+                hh.xchg_pack_keys(loc.uniq, loc.n_uniq, off, C, self.kw, H, self.send_k, None)
+                h.off = off.clone()
+                h.loc = (loc.local_col[:n].clone(), loc.pos_s[:n].clone(),
+                         loc.seg_start[:n + 1].clone(), loc.n_uniq.clone())
+            self.comm.all_to_all_fixed(self.send_k, self.recv_k)
+            it, iv, isd, seed = tb.init.args()
+            slot = torch.empty(G * C, dtype=torch.int64, device=self.device)
+            hh.kv_resolve_rows(tb.slots, self.recv_k, H, C, self.kw, slot, self.w, True, it, iv,
+                               isd, seed, tb._err, tb._inserted, tb.home_base, tb.home_m)
+            h.slot = slot
+            h.hdr = self.recv_k.view(G, H)[:, :4].contiguous().reshape(-1)
+            return
+        off = self._offsets(loc) if loc is not None else None
+        send, recv = torch.zeros(G * H, dtype=torch.int32), torch.empty(G * H, dtype=torch.int32)
+        self._cpu_pack_keys(loc, off, H, send)
+        self.comm.all_to_all_fixed(send, recv)
+        h.loc, h.off = loc, off
+        h.rows = []
+        for s in range(G):
+            rk = self._cpu_row_keys(recv, s, H)
+            slot = tb.resolve(rk, insert=True, with_w=False)[0] if rk.numel() else None
+            h.rows.append((slot, rk.numel()))
+
+    def _check_handle(self, h: KeyHandle):
+        if not h.live or h.id >= len(self._handles) or self._handles[h.id] is not h:
+            raise ValueError(f"{h!r} is not a live handle of this worker")
+
+    def pull(self, keys) -> int:
+        """Values of ``keys`` (any order, duplicates allowed; or a ``KeyHandle`` from
+        ``register_keys``) -> timestamp; ``wait`` returns ``[n]`` (dim 1) or ``[n, dim]``
+        float32 values in request order."""
+        if isinstance(keys, KeyHandle):
+            self._check_handle(keys)
+            if not self.clock.admissible(self._pushes):
+                raise AssertionError("pull admitted before the pushes it must see were applied")
+            h = keys
+            return self._run(lambda: self._pull_cached(h))
         keys = self._keys(keys)
         # after P pushes (indices 0 .. P-1) the pull is step P: it must see pushes
         # 0 .. P-1-tau of every worker
@@ -277,9 +389,47 @@ class KVWorker:
                 out = rec_r.view(G * C, k)[p * C + (u - off[p])]
         return out.reshape(-1) if k == 1 else out
 
-    def push(self, keys: torch.Tensor, vals: torch.Tensor) -> int:
-        """Send ``vals`` (``[n]`` or ``[n, dim]``) for ``keys``; duplicates are summed
-        before the server op. Returns the timestamp."""
+    def _pull_cached(self, h: KeyHandle):
+        """Pull of a registered key list: no request rows; every owner serves the
+        cached slots of every source row into the value all-to-all."""
+        k, C, G = self.dim, self.C, self.G
+        srv, tb = self.server, self.server.table
+        out = torch.zeros(h.n, k, dtype=torch.float32, device=self.device)
+        if self.gpu:
+            hh = hipops()
+            if srv.vals is None:
+                hh.kv_serve_w(h.hdr, 4, C, h.slot, tb.slots, self.rec_s)
+            else:
+                hh.kvv_serve(h.hdr, 4, C, h.slot, srv.vals, self.rec_s)
+            self.comm.all_to_all_fixed(self.rec_s, self.rec_r)
+            if h.loc is not None:
+                hh.kvv_unpack(self.rec_r, C, k, h.off, h.loc[0], out)
+        else:
+            rec_s = torch.zeros(G * C * k, dtype=torch.float32)
+            for s, (slot, cnt) in enumerate(h.rows):
+                if not cnt:
+                    continue
+                vals = (tb.gather(slot, 0).reshape(-1, 1) if srv.vals is None else srv.vals[slot])
+                rec_s[s * C * k:(s * C + cnt) * k] = vals.reshape(-1)
+            rec_r = torch.empty_like(rec_s)
+            self.comm.all_to_all_fixed(rec_s, rec_r)
+            if h.loc is not None:
+                u = h.loc.local_col.to(torch.int64)
+                p = torch.searchsorted(h.off[1:], u, right=True)
+                out = rec_r.view(G * C, k)[p * C + (u - h.off[p])]
+        return out.reshape(-1) if k == 1 else out
+
+    def push(self, keys, vals: torch.Tensor) -> int:
+        """Send ``vals`` (``[n]`` or ``[n, dim]``) for ``keys`` (or a ``KeyHandle``:
+        key-less rows against the owners' cached slots); duplicates are summed before
+        the server op. Returns the timestamp."""
+        if isinstance(keys, KeyHandle):
+            self._check_handle(keys)
+            h = keys
+            vals = vals.to(self.device, torch.float32).reshape(h.n, self.dim).contiguous()
+            p = self._pushes
+            self._pushes += 1
+            return self._run(lambda: self._push_cached(h, vals, p))
         keys = self._keys(keys)
         vals = vals.to(self.device, torch.float32).reshape(keys.numel(), self.dim).contiguous()
         p = self._pushes  # 0-based push index (the worker's step clock)
@@ -316,9 +466,34 @@ class KVWorker:
                     a, b = int(off[q]), int(off[q + 1])
                     self._row_vals(send, q, H)[:b - a] = u[a:b]
             self.comm.all_to_all_fixed(send, recv)
-        self._pending.append((p, recv))
+        self._pending.append((p, recv, None))
         self._drain(keep=0 if self.asp else int(self.tau))
         # the vector clock is the gate: every worker's pushes through P - tau applied
+        assert self.asp or self.clock.min_clock() >= p - int(self.tau)
+        return None
+
+    def _push_cached(self, h: KeyHandle, vals, p):
+        k, C, H, G = self.dim, self.C, self.Hv, self.G
+        if self.gpu:
+            hh = hipops()
+            send = torch.zeros(G * H, dtype=torch.int32, device=self.device)
+            if h.loc is not None:
+                _, pos_s, seg_start, n_uniq = h.loc
+                hh.kvv_pack_vals(vals, k, pos_s, seg_start, n_uniq, h.off, C, 0, H, send)
+            recv = torch.empty(G * H, dtype=torch.int32, device=self.device)
+            self.comm.all_to_all_fixed(send, recv)
+        else:
+            send, recv = torch.zeros(G * H, dtype=torch.int32), torch.empty(G * H, dtype=torch.int32)
+            if h.loc is not None:
+                u = torch.zeros(h.loc.uniq.numel(), k, dtype=torch.float32)
+                u.index_add_(0, h.loc.local_col.to(torch.int64), vals)
+                for q in range(G):
+                    a, b = int(h.off[q]), int(h.off[q + 1])
+                    send[q * H] = b - a
+                    send.view(torch.float32)[q * H + 4:q * H + 4 + (b - a) * k] = u[a:b].reshape(-1)
+            self.comm.all_to_all_fixed(send, recv)
+        self._pending.append((p, recv, h))
+        self._drain(keep=0 if self.asp else int(self.tau))
         assert self.asp or self.clock.min_clock() >= p - int(self.tau)
         return None
 
@@ -327,15 +502,16 @@ class KVWorker:
         applied push advances every worker's vector clock (SPMD: push p of all workers
         rides the same exchange)."""
         while len(self._pending) > keep:
-            p, recv = self._pending.popleft()
+            p, recv, h = self._pending.popleft()
+            apply = self._apply if h is None else (lambda r, h=h: self._apply_cached(r, h))
             if self.apply_stream is not None:
                 cur = torch.cuda.current_stream(self.device)
                 self.apply_stream.wait_stream(cur)
                 recv.record_stream(self.apply_stream)
                 with torch.cuda.stream(self.apply_stream):
-                    self._apply(recv)
+                    apply(recv)
             else:
-                self._apply(recv)
+                apply(recv)
             for w in range(self.G):
                 self.clock.tick(w, p)
 
@@ -368,6 +544,32 @@ class KVWorker:
                 srv.vals[slot] += torch.where(ok, v, torch.zeros_like(v))
             else:
                 srv.vals[slot] = torch.where(ok, v, srv.vals[slot])
+
+    def _apply_cached(self, recv, h: KeyHandle):
+        """Owner merge of key-less rows against the cached slots of their source rows."""
+        srv, tb = self.server, self.server.table
+        C, H, G, k = self.C, self.Hv, self.G, self.dim
+        if self.gpu:
+            hh = hipops()
+            if srv.op is None:
+                hh.kv_update_rows(tb.slots, h.slot, recv.view(torch.float32)[4:], H, recv, H, C,
+                                  self.link, self.nxt, *srv.rule.args(), srv.stats)
+            else:
+                hh.kvv_apply(recv, H, C, 0, h.slot, srv.vals, srv.op)
+            return
+        for s, (slot, cnt) in enumerate(h.rows):  # source rows in rank order
+            n = int(recv[s * H])
+            if not cnt or not n:
+                continue
+            v = recv.view(torch.float32)[s * H + 4:s * H + 4 + n * k].view(n, k)
+            if srv.op is None:
+                tb.update(slot[:n], v[:, 0].contiguous(), srv.rule, srv.stats)
+                continue
+            ok = ~torch.isnan(v)
+            if srv.op == ADD:
+                srv.vals[slot[:n]] += torch.where(ok, v, torch.zeros_like(v))
+            else:
+                srv.vals[slot[:n]] = torch.where(ok, v, srv.vals[slot[:n]])
 
     def wait(self, ts: int):
         """Order the caller's stream after op ``ts``; pulled values (or None)."""
@@ -406,4 +608,4 @@ class KVWorker:
         return unmix(mk, self.bits), (v.reshape(-1) if self.dim == 1 else v)
 
 
-__all__ = ["KVWorker", "KVServer", "INF"]
+__all__ = ["KVWorker", "KVServer", "KeyHandle", "INF"]
