@@ -26,3 +26,51 @@ tot = (p[:, 6] - p[:, 0])
 print(f"buckets {nb}: cycles per workgroup mean {tot.mean():.0f} max {tot.max():.0f}")
 for i, n in enumerate(names):
     print(f"  {n:10s} mean {d[:, i].mean():8.0f}  max {d[:, i].max():8.0f}")
+
+# ---- fused forward + backward (tploc.hip tp_fwd_bwd FB_MARK) ----
+from parameter_server_amd.ops.linear import AUC_BINS, linear_fwd_bwd, new_accum  # noqa: E402
+from parameter_server_amd.ops.native import hipops  # noqa: E402
+
+labels = (torch.rand(B, device="cuda") < 0.3).float()
+L2 = Localizer(B * 39, 30, "cuda", mode="tp", lazy_cols=True)
+loc = L2(keys)
+w = torch.randn(int(loc.uniq.numel()), device="cuda") * 0.01
+met, hist = new_accum("cuda"), torch.zeros(8 * 2 * AUC_BINS, dtype=torch.int32, device="cuda")
+cf = torch.empty(B, device="cuda")
+T = (B * 39 + 8191) // 8192
+prof = torch.zeros(T * 16, dtype=torch.int64, device="cuda")
+
+
+def run():
+    hipops().tp_fb_set_prof(None)
+    for _ in range(5):
+        linear_fwd_bwd(loc, w, labels, B=B, width=39, coef=cf, metrics=met, hist=hist)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(50):
+        linear_fwd_bwd(loc, w, labels, B=B, width=39, coef=cf, metrics=met, hist=hist)
+    e.record()
+    torch.cuda.synchronize()
+    us = s.elapsed_time(e) / 50 * 1e3
+    hipops().tp_fb_set_prof(prof)
+    for _ in range(3):
+        linear_fwd_bwd(loc, w, labels, B=B, width=39, coef=cf, metrics=met, hist=hist)
+    torch.cuda.synchronize()
+    hipops().tp_fb_set_prof(None)
+    p = prof.view(T, 16).cpu()
+    ph = p[:, :7].double()
+    d = ph[:, 1:] - ph[:, :-1]
+    names = ["loads", "forward", "hist+zero", "atomics", "atomics-drain", "psum"]
+    tot = ph[:, 6] - ph[:, 0]
+    print(f"fused: {us:.1f} us per fwd+bwd (+ entry scan); "
+          f"tiles {T}: cycles per workgroup mean {tot.mean():.0f} max {tot.max():.0f}")
+    for i, n in enumerate(names):
+        print(f"  {n:13s} mean {d[:, i].mean():8.0f}  max {d[:, i].max():8.0f}")
+    rt0, rt1 = p[:, 8].double(), p[:, 9].double()  # 100 MHz realtime
+    t0 = rt0.min()
+    print(f"  wall (realtime, us): last start {(rt0.max() - t0) / 100:.1f}, "
+          f"last end {(rt1.max() - t0) / 100:.1f}, mean duration {((rt1 - rt0) / 100).mean():.1f}")
+
+
+run()

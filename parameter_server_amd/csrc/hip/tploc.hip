@@ -611,19 +611,42 @@ tp_seg_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restric
 //     weights wl[e] = w_local[ent_uid[tile + e]] into LDS; an occurrence of a row
 //     cut by the tile boundary resolves its weight through the global entry map
 //     and keeps w * val in its register slot;
-//   forward: margins from registers + LDS, a shuffle reduction per lane group, the
+//   forward: margins from registers + LDS, a DPP reduction per lane group, the
 //     leader computes the loss terms (the tile holding a row's first occurrence
 //     owns its coef output, metrics and AUC bin);
-//   backward: the same registers add coef * val into wl (re-zeroed) at rep, then
-//     the per-entry partials psum[tile + e] go to tp_seg_reduce_kernel.
+//   backward: the same registers add coef * val into per-entry accumulators at rep,
+//     then the per-entry partials psum[tile + e] go to tp_seg_reduce_kernel.
+// The backward accumulates in 64-bit FIXED POINT with integer LDS atomics: on gfx950 a
+// ds_add_f32 wave-instruction costs ~195 cycles whatever the addresses, ds_add_u64
+// ~13-18 (benchmarks/micro/lds_atomics.hip, profiles/r2_lds_atomics.log), and the
+// float atomics were 45 % of the kernel. The tile's scale 2^k (k = 48 - e, every
+// |coef * val| < 2^e) keeps any sum of 8192 addends below 2^61 and quantises each
+// addend at 2^-(k+1) relative to the tile's largest: the partials are the exactly
+// rounded sums, independent of atomic order (deterministic).
 // PER = occurrences per lane per row (width <= 8 * PER), NP = row passes held in
 // registers (128 rows each): compile-time so the register slots stay registers.
 constexpr int kFbLanes = 8;
 constexpr int kFbMaxRows = tp::kTile / 8 + 2;  // width >= 8
+constexpr int kFbMaxBins = 2048;                // AUC bins held in LDS (2 x 2048 u32)
 constexpr uint16_t kFbNone = 0xffff, kFbExt = 0xfffe;
 
+// Sum over the 8 lanes of an aligned lane group, result in all 8 (DPP: quad_perm
+// [1,0,3,2], [2,3,0,1], then row_half_mirror; no LDS crossbar, bitwise equal in all 8).
+__device__ __forceinline__ float group8_sum(float m) {
+  m += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m), 0xB1, 0xf, 0xf, false));
+  m += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m), 0x4E, 0xf, 0xf, false));
+  m += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(m), 0x141, 0xf, 0xf, false));
+  return m;
+}
+
+// Phase marks of the fused kernel (a tuning aid, benchmarks/prof_tp_phases.py): null
+// unless tp_fb_set_prof() installed a buffer of 16 u64 per workgroup.
+__device__ uint64_t* g_fb_prof = nullptr;
+#define FB_MARK(k)                                                             \
+  if (fbp && threadIdx.x == 0) fbp[(int64_t)blockIdx.x * 16 + (k)] = clock64()
+
 template <int PER, int NP>
-__global__ void __launch_bounds__(tp::kThr)  // (PER 5: 58 VGPRs -> 2 workgroups per CU)
+__global__ void __launch_bounds__(tp::kThr)  // 68 KB LDS -> 2 workgroups per CU
 tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ dcnt,
                   const int32_t* __restrict__ ent_uid, int64_t n, int width,
                   const float* __restrict__ vals, const float* __restrict__ w_local, int64_t w_cap,
@@ -632,10 +655,15 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
                   uint32_t* __restrict__ hist, int nbins, int acc_stripes, int hist_stripes,
                   float* __restrict__ psum) {
   using namespace tp;
-  __shared__ float wl[kTile];
-  __shared__ float crow[kFbMaxRows];  // labels, then coef of the tile's rows
-  __shared__ double red[16];
-  extern __shared__ uint32_t lhist[];  // [2 * nbins] when hist != nullptr
+  // one 64 KB region: forward = entry weights (f32, [0, 32 KB)) + AUC histogram
+  // ([32 KB, 48 KB)); backward = the entries' fixed-point accumulators (i64)
+  __shared__ unsigned long long region[kTile];
+  __shared__ float crow[kFbMaxRows];  // labels of the tile's rows
+  __shared__ float sacc[4];           // tile sums of loss, correct, rows
+  __shared__ uint32_t smax;           // bits of the tile's largest |coef * val|
+  float* const wl = reinterpret_cast<float*>(region);
+  uint32_t* const lhist = reinterpret_cast<uint32_t*>(region) + kTile;
+  long long* const acc = reinterpret_cast<long long*>(region);
   constexpr int kRowsPass = kThr / kFbLanes;
   const int t = threadIdx.x, sub = t % kFbLanes, g = t / kFbLanes;
   const int64_t base = (int64_t)blockIdx.x * kTile;
@@ -643,6 +671,9 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
   const int64_t r0 = base / width;
   const int nr = (int)((base + lim - 1) / width - r0 + 1);
   const int cnt = min(kTile, max(0, dcnt[blockIdx.x]));
+  uint64_t* const fbp = g_fb_prof;
+  if (fbp && threadIdx.x == 0) fbp[(int64_t)blockIdx.x * 16 + 8] = __builtin_amdgcn_s_memrealtime();
+  FB_MARK(0);
   uint16_t ce[NP][PER];
   float cv[NP][PER];
 #pragma unroll
@@ -657,19 +688,18 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
       if (ri < nr && r < B && k < width) {
         const int64_t i = r * width + k;
         const int64_t o = i - base;
-        ce[p][q] = (o >= 0 && o < lim) ? rep[i] : kFbExt;
-        cv[p][q] = vals ? vals[i] : 1.f;
+        const bool in = o >= 0 && o < lim;
+        const uint16_t e = rep[i];  // outside the tile: the entry in the neighbour tile
+        ce[p][q] = in ? e : kFbExt;
+        cv[p][q] = in ? (vals ? vals[i] : 1.f) : __int_as_float((int)e);
       }
     }
   }
-  for (int i = t; i < nr; i += kThr) crow[i] = r0 + i < B ? labels[r0 + i] : 0.f;
-  for (int i = t; i < cnt; i += kThr) {
-    const int32_t u = ent_uid[base + i];
-    wl[i] = in_range(u, w_cap) ? w_local[u] : 0.f;
-  }
-  if (hist)
-    for (int i = t; i < 2 * nbins; i += kThr) lhist[i] = 0u;
-  // boundary rows: the outside part of row 0 / row nr-1 (only their lane groups)
+  if (t < 4) sacc[t] = 0.f;
+  if (t == 0) smax = 0u;
+  // boundary rows: the outside part of row 0 / row nr-1 (only their lane groups) read
+  // their weights through the neighbour tile's entry map; issued first, so the chain
+  // rep -> ent_uid -> w_local overlaps the tile's own entry-weight loads
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     const int ri = p * kRowsPass + g;
@@ -678,13 +708,22 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
     for (int q = 0; q < PER; ++q)
       if (ce[p][q] == kFbExt) {
         const int64_t i = (r0 + ri) * width + sub + q * kFbLanes;
-        const int32_t u = ent_uid[(i & ~(int64_t)(kTile - 1)) + rep[i]];
-        cv[p][q] *= in_range(u, w_cap) ? w_local[u] : 0.f;
+        const int32_t u = ent_uid[(i & ~(int64_t)(kTile - 1)) + __float_as_int(cv[p][q])];
+        cv[p][q] = (in_range(u, w_cap) ? w_local[u] : 0.f) * (vals ? vals[i] : 1.f);
       }
   }
+  for (int i = t; i < nr; i += kThr) crow[i] = r0 + i < B ? labels[r0 + i] : 0.f;
+  for (int i = t; i < cnt; i += kThr) {
+    const int32_t u = ent_uid[base + i];
+    wl[i] = in_range(u, w_cap) ? w_local[u] : 0.f;
+  }
+  if (hist)
+    for (int i = t; i < 2 * nbins; i += kThr) lhist[i] = 0u;
   __syncthreads();
-  double loss_acc = 0, corr_acc = 0, rows_acc = 0;
+  FB_MARK(1);
+  float loss_acc = 0.f, corr_acc = 0.f, rows_acc = 0.f;
   float cf[NP];
+  float vmax = 0.f;
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     float m = 0.f;
@@ -694,8 +733,7 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
       if (e == kFbExt) m += cv[p][q];
       else if (e != kFbNone) m += wl[e] * cv[p][q];
     }
-#pragma unroll
-    for (int off = kFbLanes / 2; off > 0; off >>= 1) m += __shfl_xor(m, off, 64);
+    m = group8_sum(m);
     const int ri = p * kRowsPass + g;
     const int64_t r = r0 + ri;
     float c = 0.f;
@@ -706,41 +744,72 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
       if (sub == 0 && r * width >= base) {  // first occurrence in this tile: the row is ours
         coef_out[r] = c;
         loss_acc += loss;
-        corr_acc += ((lab > 0.f) == (m > 0.f)) ? 1.0 : 0.0;
-        rows_acc += 1.0;
+        corr_acc += ((lab > 0.f) == (m > 0.f)) ? 1.f : 0.f;
+        rows_acc += 1.f;
         if (hist) atomicAdd(&lhist[auc_bin(m, lab, nbins)], 1u);
       }
     }
     cf[p] = c;  // every lane of the group holds its row's coef
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+      if (ce[p][q] < kFbExt) vmax = fmaxf(vmax, fabsf(c * cv[p][q]));
+  }
+  vmax = wave_max(vmax);
+  if ((t & 63) == 0 && vmax > 0.f) atomicMax(&smax, __float_as_uint(vmax));  // ds_max_u32
+  if (metrics && rows_acc > 0.f) {  // leader lanes: tile sums (ds_add_f32, 3 per leader)
+    atomicAdd(&sacc[0], loss_acc);
+    atomicAdd(&sacc[1], corr_acc);
+    atomicAdd(&sacc[2], rows_acc);
   }
   __syncthreads();
-  for (int i = t; i < cnt; i += kThr) wl[i] = 0.f;
+  FB_MARK(2);
+  if (hist) {  // flush the AUC bins before the region turns into accumulators
+    uint32_t* hs = hist + (int64_t)(blockIdx.x % hist_stripes) * 2 * nbins;
+    for (int i = t; i < 2 * nbins; i += kThr)
+      if (lhist[i]) atomicAdd(&hs[i], lhist[i]);
+  }
+  if (metrics && t == 0 && sacc[2] > 0.f) {
+    double* mt = acc_stripe(metrics, acc_stripes);
+    atomicAdd(&mt[0], (double)sacc[0]);
+    atomicAdd(&mt[1], (double)sacc[1]);
+    atomicAdd(&mt[2], (double)sacc[2]);
+  }
+  const uint32_t mb = smax;
   __syncthreads();
+  for (int i = t; i < cnt; i += kThr) acc[i] = 0ll;
+  __syncthreads();
+  FB_MARK(3);
+  // scale 2^k with every |addend| < 2^e: k = 48 - e (sums of 8192 stay < 2^61)
+  int e2 = 0;
+  if (mb) (void)frexpf(__uint_as_float(mb), &e2);
+  const int k2 = min(100, 48 - e2);
+  const double sc = ldexp(1.0, k2);
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     if (cf[p] == 0.f) continue;
 #pragma unroll
     for (int q = 0; q < PER; ++q)
-      if (ce[p][q] < kFbExt) atomicAdd(&wl[ce[p][q]], cf[p] * cv[p][q]);
+      if (ce[p][q] < kFbExt) {
+        const long long fx = __double2ll_rn((double)(cf[p] * cv[p][q]) * sc);
+        if (fx) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[ce[p][q]]),
+                          (unsigned long long)fx);  // ds_add_u64
+      }
   }
-  if (metrics) {
-    const double a = block_sum_f64(loss_acc, red);
-    const double b = block_sum_f64(corr_acc, red);
-    const double c = block_sum_f64(rows_acc, red);
-    if (t == 0 && c > 0) {
-      double* mt = acc_stripe(metrics, acc_stripes);
-      atomicAdd(&mt[0], a);
-      atomicAdd(&mt[1], b);
-      atomicAdd(&mt[2], c);
-    }
-  }
+  FB_MARK(4);
   __syncthreads();
-  for (int i = t; i < cnt; i += kThr) psum[base + i] = wl[i];
-  if (hist) {
-    uint32_t* hs = hist + (int64_t)(blockIdx.x % hist_stripes) * 2 * nbins;
-    for (int i = t; i < 2 * nbins; i += kThr)
-      if (lhist[i]) atomicAdd(&hs[i], lhist[i]);
+  FB_MARK(5);
+  const double isc = ldexp(1.0, -k2);
+  for (int i = t; i < cnt; i += kThr) psum[base + i] = (float)((double)acc[i] * isc);
+  FB_MARK(6);
+  if (fbp && threadIdx.x == 0) {
+    fbp[(int64_t)blockIdx.x * 16 + 9] = __builtin_amdgcn_s_memrealtime();
+    fbp[(int64_t)blockIdx.x * 16 + 10] = __smid();
   }
+}
+#undef FB_MARK
+
+void tp_fb_set_prof(uint64_t* p) {
+  PSAMD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_fb_prof), &p, sizeof(p)));
 }
 
 // ---------------------------------------------------------------------------
@@ -868,7 +937,9 @@ void tp_fwd_bwd(const uint16_t* rep, const int32_t* dcnt, const int32_t* ent_uid
   if (!tp_fwd_bwd_supported(width) || n != B * (int64_t)width)
     throw std::runtime_error("tp_fwd_bwd: unsupported width or n != B * width");
   const TpGeom g = tp_geom(n, 31);
-  const size_t lds = hist ? (size_t)2 * nbins * sizeof(uint32_t) : 0;
+  if (hist && (nbins <= 0 || nbins > kFbMaxBins))
+    throw std::runtime_error("tp_fwd_bwd: 1..2048 AUC bins (LDS histogram)");
+  const size_t lds = 0;
   const int per = (width + kFbLanes - 1) / kFbLanes;
 #define PSAMD_FB(PER, NP)                                                                     \
   tp_fwd_bwd_kernel<PER, NP><<<(unsigned)g.T, tp::kThr, lds, st>>>(                          \

@@ -1,0 +1,12 @@
+#!/bin/bash
+# PMC passes over the standalone tp localisation + fused forward/backward microbenchmark.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out/pmc; export TMPDIR=/tmp PSAMD_LOC_MODES=tp
+R="$GRAFT_REPO_ROOT"
+timeout -s KILL 60 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || true
+cd /tmp
+i=0
+for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" \
+           "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SMEM" ; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $set -d "$R/gpurun_out/pmc/p$i" -o run --output-format csv -- python3 "$R/benchmarks/bench_localize.py" > "$R/gpurun_out/pmc/p$i.log" 2>&1 || exit 1
+done
