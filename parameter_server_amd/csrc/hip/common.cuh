@@ -98,6 +98,22 @@ __device__ __forceinline__ bool in_range(int64_t i, int64_t cap) {
   return (uint64_t)i < (uint64_t)cap;
 }
 
+// One step of a wave-wide segmented inclusive scan over DPP lane moves (GFX9 DPP
+// controls: 0x110 + n = row_shr:n, 0x142 = row_bcast:15, 0x143 = row_bcast:31). Lanes
+// the move does not write (no source lane, or a row outside ROW_MASK) keep the "old"
+// operand: segment id -2 (never equal) and value 0.
+template <int CTRL, int ROW_MASK, int D>
+__device__ __forceinline__ void seg_scan_step(int32_t u, float (&x)[D]) {
+  const int32_t uo = __builtin_amdgcn_update_dpp(-2, u, CTRL, ROW_MASK, 0xf, false);
+  const bool add = uo == u;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    const float y = __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(x[d]), CTRL, ROW_MASK, 0xf, false));
+    x[d] += add ? y : 0.f;
+  }
+}
+
 // Wave-level reductions (64 lanes) -------------------------------------------
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

@@ -314,22 +314,6 @@ emb_grad_cross_kernel(const int32_t* __restrict__ segid, const int32_t* __restri
         make_float2(acc[2 * c], acc[2 * c + 1]);
 }
 
-// One step of a wave-wide segmented inclusive scan over DPP lane moves (GFX9 DPP
-// controls: 0x110 + n = row_shr:n, 0x142 = row_bcast:15, 0x143 = row_bcast:31). Lanes
-// the move does not write (no source lane, or a row outside ROW_MASK) keep the "old"
-// operand: segment id -2 (never equal) and value 0.
-template <int CTRL, int ROW_MASK, int D>
-__device__ __forceinline__ void seg_scan_step(int32_t u, float (&x)[D]) {
-  const int32_t uo = __builtin_amdgcn_update_dpp(-2, u, CTRL, ROW_MASK, 0xf, false);
-  const bool add = uo == u;
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    const float y = __int_as_float(
-        __builtin_amdgcn_update_dpp(0, __float_as_int(x[d]), CTRL, ROW_MASK, 0xf, false));
-    x[d] += add ? y : 0.f;
-  }
-}
-
 // Narrow rows (D = 8 .. 64, the FM factors): the same 64-entry runs, but lane =
 // entry: each lane loads its own D-wide row (D / 8 16-B loads), a segmented
 // inclusive scan over the wave (6 DPP steps per dim; segments are contiguous,

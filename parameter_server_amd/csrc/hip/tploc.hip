@@ -563,6 +563,8 @@ tp_seg_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restric
                      int64_t n_host, const int32_t* __restrict__ n_dev,
                      const float* __restrict__ psum, int64_t p_cap, float* __restrict__ grad,
                      int64_t grad_cap) {
+  // segmented scan over the entry CSC on DPP lane moves (no ds_bpermute); run ends
+  // store grad[u], runs cut by a wave boundary add atomically (grad zeroed by emit)
   const int lane = threadIdx.x & 63;
   const int64_t n = dev_len(n_dev, n_host);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -570,33 +572,28 @@ tp_seg_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restric
        i0 += stride) {
     const int64_t i = i0 + lane;
     const bool valid = i < n;
-    int32_t s = -1;
-    float v = 0.f;
+    int32_t s = -3;
+    float x[1] = {0.f};
     if (valid) {
       s = segid[i];
       const int32_t p = pos_s[i];
-      if (in_range(p, p_cap)) v = psum[p];
+      if (in_range(p, p_cap)) x[0] = psum[p];
     }
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const float vo = __shfl_up(v, off, 64);
-      const int32_t so = __shfl_up(s, off, 64);
-      if (lane >= off && so == s) v += vo;
-    }
-    const int32_t s_next = __shfl_down(s, 1, 64);
-    const int32_t s_lane0 = __shfl(s, 0, 64);
-    int32_t prev_of_lane0 = -2;
-    if (lane == 0 && i0 > 0) prev_of_lane0 = segid[i0 - 1];
-    prev_of_lane0 = __shfl(prev_of_lane0, 0, 64);
-    const bool tail = valid && (lane == 63 || s_next != s || i + 1 >= n);
-    if (tail) {
-      const bool starts_inside = (s != s_lane0) || (prev_of_lane0 != s);
-      bool ends_inside = true;
-      if (lane == 63 && i + 1 < n) ends_inside = segid[i + 1] != s;
+    const int32_t s_next = i + 1 < n ? segid[i + 1] : -1;
+    const int32_t s_prev0 = i0 > 0 ? segid[i0 - 1] : -1;
+    seg_scan_step<0x111, 0xf>(s, x);
+    seg_scan_step<0x112, 0xf>(s, x);
+    seg_scan_step<0x114, 0xf>(s, x);
+    seg_scan_step<0x118, 0xf>(s, x);
+    seg_scan_step<0x142, 0xa>(s, x);
+    seg_scan_step<0x143, 0xc>(s, x);
+    const int32_t s_lane0 = __builtin_amdgcn_readfirstlane(s);
+    if (valid && (s_next != s || lane == 63)) {
+      const bool starts_inside = s != s_lane0 || s_prev0 != s;
       const int32_t u = s - 1;
       if (in_range(u, grad_cap)) {
-        if (starts_inside && ends_inside) grad[u] = v;
-        else atomicAdd(&grad[u], v);
+        if (starts_inside && s_next != s) grad[u] = x[0];
+        else atomicAdd(&grad[u], x[0]);
       }
     }
   }
