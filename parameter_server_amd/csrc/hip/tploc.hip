@@ -452,19 +452,40 @@ __global__ void tp_gather_kernel(const uint16_t* __restrict__ rep,
 
 // -------------------------------------------------------------------- backward
 // psum[tile entry] = sum over the tile's occurrences of the entry of coef[row] * val.
-// Variable-width rows (rows != null): one LDS float atomic per occurrence.
+// Tiles accumulate in 64-bit FIXED POINT with integer LDS atomics (gfx950: ds_add_f32
+// ~195 cycles per wave-instruction, ds_add_u64 ~13-18; profiles/r2_lds_atomics.log):
+// scale 2^(48 - e) with every |addend| < 2^e keeps any sum of a tile's 8192 addends
+// below 2^61, and the partials are exactly rounded, order-independent sums.
+__device__ __forceinline__ int fx_shift(uint32_t maxbits) {
+  int e = 0;
+  if (maxbits) (void)frexpf(__uint_as_float(maxbits), &e);
+  return min(100, 48 - e);
+}
+__device__ __forceinline__ void fx_add(long long* acc, int idx, float v, double sc) {
+  const long long fx = __double2ll_rn((double)v * sc);
+  if (fx) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[idx]), (unsigned long long)fx);
+}
+// every wave's max |v| -> the tile's (LDS ds_max_u32 on the float bits of |v|)
+__device__ __forceinline__ void fx_tile_max(float vmax, uint32_t* smax) {
+  vmax = wave_max(vmax);
+  if ((threadIdx.x & 63) == 0 && vmax > 0.f) atomicMax(smax, __float_as_uint(vmax));
+}
+
+// Variable-width rows (rows != null): one LDS atomic per occurrence.
 __global__ void __launch_bounds__(tp::kThr)
 tp_bwd_accum_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ dcnt, int64_t n,
                     const int32_t* __restrict__ rows, int width, const float* __restrict__ vals,
                     const float* __restrict__ coef, int64_t B, float* __restrict__ psum) {
   using namespace tp;
-  __shared__ float acc[kTile];
+  __shared__ long long acc[kTile];
+  __shared__ uint32_t smax;
   const int t = threadIdx.x;
-  for (int i = t; i < kTile; i += kThr) acc[i] = 0.f;
-  __syncthreads();
+  for (int i = t; i < kTile; i += kThr) acc[i] = 0ll;
+  if (t == 0) smax = 0u;
   const int64_t base = (int64_t)blockIdx.x * kTile;
   float v[kIt];
   uint16_t e[kIt];
+  float vmax = 0.f;
 #pragma unroll
   for (int j = 0; j < kIt; ++j) {
     const int64_t i = base + j * kThr + t;
@@ -475,13 +496,20 @@ tp_bwd_accum_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict_
       e[j] = rep[i];
       if (in_range(r, B)) v[j] = coef[r] * (vals ? vals[i] : 1.f);
     }
+    vmax = fmaxf(vmax, fabsf(v[j]));
   }
+  __syncthreads();  // acc / smax zeroed
+  fx_tile_max(vmax, &smax);
+  __syncthreads();
+  const int k2 = fx_shift(smax);
+  const double sc = ldexp(1.0, k2);
 #pragma unroll
   for (int j = 0; j < kIt; ++j)
-    if (v[j] != 0.f) atomicAdd(&acc[e[j]], v[j]);
+    if (v[j] != 0.f) fx_add(acc, e[j], v[j], sc);
   __syncthreads();
   const int cnt = min(kTile, max(0, dcnt[blockIdx.x]));
-  for (int i = t; i < cnt; i += kThr) psum[base + i] = acc[i];
+  const double isc = ldexp(1.0, -k2);
+  for (int i = t; i < cnt; i += kThr) psum[base + i] = (float)((double)acc[i] * isc);
 }
 
 // Fixed-width rows: thread = (slot, run of L consecutive rows) walks down its column,
@@ -494,9 +522,11 @@ tp_bwd_accum_cols_kernel(const uint16_t* __restrict__ rep, const int32_t* __rest
                          int64_t n, int width, const float* __restrict__ vals,
                          const float* __restrict__ coef, int64_t B, float* __restrict__ psum) {
   using namespace tp;
-  __shared__ float acc[kTile];
+  __shared__ long long acc[kTile];
+  __shared__ uint32_t smax;
   const int t = threadIdx.x;
-  for (int i = t; i < kTile; i += kThr) acc[i] = 0.f;
+  for (int i = t; i < kTile; i += kThr) acc[i] = 0ll;
+  if (t == 0) smax = 0u;
   const int64_t base = (int64_t)blockIdx.x * kTile;
   const int64_t lim = n - base < kTile ? n - base : kTile;
   const int64_t r0 = base / width, r1 = (base + lim - 1) / width;
@@ -504,12 +534,13 @@ tp_bwd_accum_cols_kernel(const uint16_t* __restrict__ rep, const int32_t* __rest
   const int L = (nr * width + kThr - 1) / kThr;  // rows per thread
   const int nseg = (nr + L - 1) / L;
   const int slot = t % width, seg = t / width;
-  __syncthreads();
+  const int ra = seg * L, rb = ra + L < nr ? ra + L : nr;
   constexpr int kL = 16;  // rows a thread prefetches into registers before its walk
-  if (seg < nseg && L <= kL) {
-    const int ra = seg * L;
-    uint32_t ee[kL];
-    float vv[kL];
+  const bool regs = seg < nseg && L <= kL;
+  uint32_t ee[kL];
+  float vv[kL];
+  float vmax = 0.f;
+  if (regs) {
 #pragma unroll
     for (int q = 0; q < kL; ++q) {  // every load of the walk in flight at once
       const int rl = ra + q;
@@ -518,25 +549,36 @@ tp_bwd_accum_cols_kernel(const uint16_t* __restrict__ rep, const int32_t* __rest
       const bool ok = q < L && rl < nr && i >= base && i < base + lim && in_range(r, B);
       ee[q] = ok ? (uint32_t)rep[i] : 0xffffffffu;
       vv[q] = ok ? coef[r] * (vals ? vals[i] : 1.f) : 0.f;
+      vmax = fmaxf(vmax, fabsf(vv[q]));
     }
-    uint32_t cur = 0xffffffffu;
-    float sum = 0.f;
+  } else if (seg < nseg) {  // long walks (width > 1024 / kL rows): a max pre-pass
+    for (int rl = ra; rl < rb; ++rl) {
+      const int64_t r = r0 + rl;
+      const int64_t i = r * width + slot;
+      if (i >= base && i < base + lim && in_range(r, B))
+        vmax = fmaxf(vmax, fabsf(coef[r] * (vals ? vals[i] : 1.f)));
+    }
+  }
+  __syncthreads();  // acc / smax zeroed
+  fx_tile_max(vmax, &smax);
+  __syncthreads();
+  const int k2 = fx_shift(smax);
+  const double sc = ldexp(1.0, k2);
+  uint32_t cur = 0xffffffffu;
+  float sum = 0.f;  // a run of equal keys down the column (<= L addends < 2^e each)
+  if (regs) {
 #pragma unroll
     for (int q = 0; q < kL; ++q) {
       if (ee[q] == 0xffffffffu) continue;
       if (ee[q] != cur) {
-        if (cur != 0xffffffffu && sum != 0.f) atomicAdd(&acc[cur], sum);
+        if (cur != 0xffffffffu && sum != 0.f) fx_add(acc, cur, sum, sc);
         cur = ee[q];
         sum = vv[q];
       } else {
         sum += vv[q];
       }
     }
-    if (cur != 0xffffffffu && sum != 0.f) atomicAdd(&acc[cur], sum);
   } else if (seg < nseg) {
-    const int ra = seg * L, rb = ra + L < nr ? ra + L : nr;
-    uint32_t cur = 0xffffffffu;
-    float sum = 0.f;
     for (int rl = ra; rl < rb; ++rl) {
       const int64_t r = r0 + rl;
       const int64_t i = r * width + slot;  // global position
@@ -544,18 +586,19 @@ tp_bwd_accum_cols_kernel(const uint16_t* __restrict__ rep, const int32_t* __rest
       const uint32_t e = rep[i];
       const float v = coef[r] * (vals ? vals[i] : 1.f);
       if (e != cur) {
-        if (cur != 0xffffffffu && sum != 0.f) atomicAdd(&acc[cur], sum);
+        if (cur != 0xffffffffu && sum != 0.f) fx_add(acc, cur, sum, sc);
         cur = e;
         sum = v;
       } else {
         sum += v;
       }
     }
-    if (cur != 0xffffffffu && sum != 0.f) atomicAdd(&acc[cur], sum);
   }
+  if (cur != 0xffffffffu && sum != 0.f) fx_add(acc, cur, sum, sc);
   __syncthreads();
   const int cnt = min(kTile, max(0, dcnt[blockIdx.x]));
-  for (int i = t; i < cnt; i += kThr) psum[base + i] = acc[i];
+  const double isc = ldexp(1.0, -k2);
+  for (int i = t; i < cnt; i += kThr) psum[base + i] = (float)((double)acc[i] * isc);
 }
 
 __global__ void __launch_bounds__(256)
@@ -751,8 +794,7 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
     for (int q = 0; q < PER; ++q)
       if (ce[p][q] < kFbExt) vmax = fmaxf(vmax, fabsf(c * cv[p][q]));
   }
-  vmax = wave_max(vmax);
-  if ((t & 63) == 0 && vmax > 0.f) atomicMax(&smax, __float_as_uint(vmax));  // ds_max_u32
+  fx_tile_max(vmax, &smax);
   if (metrics && rows_acc > 0.f) {  // leader lanes: tile sums (ds_add_f32, 3 per leader)
     atomicAdd(&sacc[0], loss_acc);
     atomicAdd(&sacc[1], corr_acc);
@@ -776,21 +818,14 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
   for (int i = t; i < cnt; i += kThr) acc[i] = 0ll;
   __syncthreads();
   FB_MARK(3);
-  // scale 2^k with every |addend| < 2^e: k = 48 - e (sums of 8192 stay < 2^61)
-  int e2 = 0;
-  if (mb) (void)frexpf(__uint_as_float(mb), &e2);
-  const int k2 = min(100, 48 - e2);
+  const int k2 = fx_shift(mb);  // every |addend| < 2^e -> scale 2^(48 - e)
   const double sc = ldexp(1.0, k2);
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     if (cf[p] == 0.f) continue;
 #pragma unroll
     for (int q = 0; q < PER; ++q)
-      if (ce[p][q] < kFbExt) {
-        const long long fx = __double2ll_rn((double)(cf[p] * cv[p][q]) * sc);
-        if (fx) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[ce[p][q]]),
-                          (unsigned long long)fx);  // ds_add_u64
-      }
+      if (ce[p][q] < kFbExt) fx_add(acc, ce[p][q], cf[p] * cv[p][q], sc);  // ds_add_u64
   }
   FB_MARK(4);
   __syncthreads();
