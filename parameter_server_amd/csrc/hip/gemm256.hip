@@ -364,13 +364,228 @@ gemm_nt256pp_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
 }
 #undef GPP_BAR
 
+// ---------------------------------------------------------------------------
+// Deep-prefetch variant (variant 2): the ping-pong structure above, but each half-tile
+// region is re-staged for K-step t+2 as soon as its last read of K-step t retired, so
+// every half-tile has ~7 phases (instead of 4) between its DMA and its first read. Reads
+// per K-step: p0 A-mq0 + B-nq0 (the B-nq0 fragments stay in registers for p3), p1
+// B-nq1, p2 A-mq1, p3 none; stages during K-step t (into the same buffer, K-step t+2):
+// p1 A-mq0 + B-nq0, p2 B-nq1, p3 A-mq1. Counted waits (per wave, glds in issue order:
+// A0B0 = 4, B1 = 2, A1 = 2 per K-step): p3(t) retires A0B0(t+1) (12 younger), p0(t)
+// retires B1(t) (10 younger), p1(t) retires A1(t) (12 younger); each read follows its
+// wait by at least one barrier of both wave rows (the second row runs one barrier
+// behind), and each region is re-staged a phase after its last read was retired
+// (lgkmcnt(0)) before a barrier both rows have passed.
+#define GP8_BAR() __builtin_amdgcn_s_barrier()
+#define GP8_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+__global__ void __launch_bounds__(g256::TH)
+gemm_nt256p8_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B,
+                    int64_t ldb, int M, int N, int K, const float* __restrict__ bias, int relu,
+                    __bf16* __restrict__ C, int64_t ldc, float* __restrict__ Cf, int64_t ldcf,
+                    int tiles_n) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];  // 128 KiB, one array
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int id = g256_xcd(blockIdx.x, gridDim.x);
+  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = K / BK;
+  // prologue: K-steps 0 and 1, each in the steady-state order A0 B0 | B1 | A1
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    if (kt < nk) {
+      char* buf = smem + kt * BUF_BYTES;
+      gpp_stage_a(A, lda, M, m0, kt * BK, buf, 0, wave, lane);
+      gpp_stage_b(B, ldb, N, n0, kt * BK, buf + TILE_BYTES, 0, wave, lane);
+      gpp_stage_b(B, ldb, N, n0, kt * BK, buf + TILE_BYTES, 1, wave, lane);
+      gpp_stage_a(A, lda, M, m0, kt * BK, buf, 1, wave, lane);
+    }
+  }
+  if (nk > 1) GP8_VM(12); else GP8_VM(4);  // A0B0(0) landed
+  GP8_BAR();
+  if (wr == 1) GP8_BAR();  // the second wave row runs one barrier behind
+  bf16x8 af[4][2], bf0[2][2], bf1[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * BUF_BYTES;
+    const bool s2 = kt + 2 < nk, s1 = kt + 1 < nk;
+    const int k2 = (kt + 2) * BK;
+    // ---- p0: read A-mq0, B-nq0; retire B1(kt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wc * 64 + j * 16 + (lane & 15);
+        bf0[ks][j] = *reinterpret_cast<const bf16x8*>(cur + TILE_BYTES + r * 128 + g256_swz(r, c) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wr * 128 + i * 16 + (lane & 15);
+        af[i][ks] = *reinterpret_cast<const bf16x8*>(cur + r * 128 + g256_swz(r, c) * 16);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (s1) GP8_VM(10); else GP8_VM(2);
+    GP8_BAR();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[0][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf0[ks][j],
+                                                                   acc[0][0][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    GP8_BAR();
+    // ---- p1: stage A0 B0 (kt+2); read B-nq1; retire A1(kt)
+    if (s2) {
+      gpp_stage_a(A, lda, M, m0, k2, cur, 0, wave, lane);
+      gpp_stage_b(B, ldb, N, n0, k2, cur + TILE_BYTES, 0, wave, lane);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wc * 64 + 32 + j * 16 + (lane & 15);
+        bf1[ks][j] = *reinterpret_cast<const bf16x8*>(cur + TILE_BYTES + r * 128 + g256_swz(r, c) * 16);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (s2) GP8_VM(12); else if (s1) GP8_VM(8); else GP8_VM(0);
+    GP8_BAR();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[0][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf1[ks][j],
+                                                                   acc[0][1][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    GP8_BAR();
+    // ---- p2: stage B1 (kt+2); read A-mq1
+    if (s2) gpp_stage_b(B, ldb, N, n0, k2, cur + TILE_BYTES, 1, wave, lane);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wr * 128 + 64 + i * 16 + (lane & 15);
+        af[i][ks] = *reinterpret_cast<const bf16x8*>(cur + r * 128 + g256_swz(r, c) * 16);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    GP8_BAR();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[1][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf1[ks][j],
+                                                                   acc[1][1][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    GP8_BAR();
+    // ---- p3: stage A1 (kt+2); no reads; retire A0B0(kt+1)
+    if (s2) gpp_stage_a(A, lda, M, m0, k2, cur, 1, wave, lane);
+    if (s2) GP8_VM(12); else if (s1) GP8_VM(4);
+    GP8_BAR();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[1][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][ks], bf0[ks][j],
+                                                                   acc[1][0][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    GP8_BAR();
+  }
+  if (wr == 0) GP8_BAR();  // match the second row's extra barrier
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (C && !Cf && (ldc & 7) == 0 && m0 + BM <= M && n0 + BN <= N) {
+    __bf16* st = reinterpret_cast<__bf16*>(smem);  // [256][256] bf16
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int nl = wc * 64 + nq * 32 + j * 16 + (lane & 15);
+        const float bv = bias ? bias[n0 + nl] : 0.f;
+#pragma unroll
+        for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int ml = wr * 128 + mq * 64 + i * 16 + 4 * (lane >> 4) + r;
+              float v = acc[mq][nq][i][j][r] + bv;
+              if (relu) v = v > 0.f ? v : 0.f;
+              st[ml * BN + nl] = (__bf16)v;
+            }
+      }
+    __syncthreads();
+#pragma unroll 4
+    for (int q = 0; q < BM * BN / 8 / TH; ++q) {
+      const int ch = q * TH + t;
+      const int ml = ch >> 5, nc = (ch & 31) * 8;
+      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + ml) * ldc + n0 + nc) =
+          *reinterpret_cast<const uint4*>(st + ml * BN + nc);
+    }
+    return;
+  }
+#pragma unroll
+  for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wc * 64 + nq * 32 + j * 16 + (lane & 15);
+      if (n >= N) continue;
+      const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+      for (int mq = 0; mq < 2; ++mq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wr * 128 + mq * 64 + i * 16 + 4 * (lane >> 4) + r;
+            if (m >= M) continue;
+            float v = acc[mq][nq][i][j][r] + bv;
+            if (relu) v = v > 0.f ? v : 0.f;
+            if (C) C[(int64_t)m * ldc + n] = (__bf16)v;
+            if (Cf) Cf[(int64_t)m * ldcf + n] = v;
+          }
+    }
+}
+#undef GP8_BAR
+#undef GP8_VM
+
 void gemm_nt256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
                 const float* bias, bool relu, __bf16* C, int64_t ldc, float* Cf, int64_t ldcf,
                 int variant, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   if (K % g256::BK != 0 || lda % 8 || ldb % 8) throw std::runtime_error("gemm_nt256: K % 64, ld % 8");
   const int tiles_m = (M + g256::BM - 1) / g256::BM, tiles_n = (N + g256::BN - 1) / g256::BN;
-  if (variant == 1)
+  if (variant == 2)
+    gemm_nt256p8_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
+                                                                relu ? 1 : 0, C, ldc, Cf, ldcf,
+                                                                tiles_n);
+  else if (variant == 1)
     gemm_nt256pp_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
                                                                 relu ? 1 : 0, C, ldc, Cf, ldcf,
                                                                 tiles_n);
