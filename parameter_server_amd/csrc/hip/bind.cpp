@@ -90,7 +90,7 @@ void kv_gather(const void*, int64_t, const int64_t*, int64_t, const int32_t*, fl
 void kv_set(void*, int64_t, const int64_t*, int64_t, const float*, const float*, const float*,
             hipStream_t);
 void kv_update(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int, int,
-               float, float, float, float, float, float, double*, int, hipStream_t);
+               float, float, float, float, float, float, double*, int, uint32_t*, int, int, double*, int64_t*, hipStream_t);
 void kv_accumulate(void*, int64_t, const int64_t*, const float*, int64_t, const int32_t*, int64_t*,
                    int32_t*, int64_t, hipStream_t);
 void kv_apply_accumulated(void*, int64_t, const int64_t*, const int32_t*, int64_t, int, int, float,
@@ -883,18 +883,31 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("kv_update", [](Tensor slots, Tensor slot_idx, Tensor grad, optional<Tensor> n_dev,
                         int algo, int lr_type, double alpha, double beta, double l1, double l2,
-                        double grad_scale, double max_delta, optional<Tensor> stats) {
+                        double grad_scale, double max_delta, optional<Tensor> stats,
+                        optional<Tensor> hist, optional<Tensor> metrics,
+                        optional<Tensor> step_counter) {
     const int64_t cap = slot_capacity(slots);
     chk(slot_idx, at::kLong, "slot_idx");
     chk(grad, at::kFloat, "grad");
     check(grad.numel() >= slot_idx.numel(), "grad too small");
     check(alpha > 0, "learning rate alpha must be > 0");
+    // optional: the step's AUC histogram -> metrics (auc_from_hist folded into block 0)
+    uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
+    double* mp = optr<double>(metrics, at::kDouble, "metrics");
+    constexpr int kBins = 2048;
+    if (hp) check(mp && hist->numel() % (2 * kBins) == 0 && hist->numel() / (2 * kBins) <= 8,
+                  "kv_update: hist = stripes x 2 x 2048 (<= 8 stripes) with metrics");
     psamd::kv_update(slots.data_ptr(), cap, ptr<int64_t>(slot_idx), ptr<float>(grad),
                      slot_idx.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"), algo, lr_type,
                      (float)alpha, (float)beta, (float)l1, (float)l2, (float)grad_scale,
                      (float)max_delta, optr<double>(stats, at::kDouble, "stats"),
-                     acc_stripes_of(stats), cur_stream());
-  });
+                     acc_stripes_of(stats), hp, kBins,
+                     hp ? (int)(hist->numel() / (2 * kBins)) : 1, mp,
+                     optr<int64_t>(step_counter, at::kLong, "step_counter"), cur_stream());
+  }, py::arg("slots"), py::arg("slot_idx"), py::arg("grad"), py::arg("n_dev"), py::arg("algo"),
+     py::arg("lr_type"), py::arg("alpha"), py::arg("beta"), py::arg("l1"), py::arg("l2"),
+     py::arg("grad_scale"), py::arg("max_delta"), py::arg("stats"), py::arg("hist") = py::none(),
+     py::arg("metrics") = py::none(), py::arg("step_counter") = py::none());
   m.def("kv_accumulate", [](Tensor slots, Tensor slot_idx, Tensor grad, optional<Tensor> n_dev,
                             Tensor touched, Tensor n_touched) {
     const int64_t cap = slot_capacity(slots);

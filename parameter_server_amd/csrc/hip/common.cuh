@@ -114,6 +114,25 @@ __device__ __forceinline__ void seg_scan_step(int32_t u, float (&x)[D]) {
   }
 }
 
+// Sum over the wave by DPP lane moves (inclusive scan: the total lands in lane 63), no
+// ds_bpermute / LDS: row_shr 1/2/4/8, then row_bcast:15 / :31 (rows outside the mask,
+// and lanes without a source, take the "old" operand 0).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_f64<0x111, 0xf>(v);
+  v += dpp_f64<0x112, 0xf>(v);
+  v += dpp_f64<0x114, 0xf>(v);
+  v += dpp_f64<0x118, 0xf>(v);
+  v += dpp_f64<0x142, 0xa>(v);
+  v += dpp_f64<0x143, 0xc>(v);
+  return v;  // lane 63
+}
+
 // Wave-level reductions (64 lanes) -------------------------------------------
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

@@ -17,6 +17,7 @@
 // launches (reference semantics: every push message is one optimizer step)
 // or by the accumulate/apply pair (synchronous / BSP aggregation).
 #include "common.cuh"
+#include "loss.cuh"
 #include <stdexcept>
 #include <string>
 
@@ -297,8 +298,12 @@ __global__ void kv_update_kernel(Slot* __restrict__ slots, int64_t cap,
                                  const int64_t* __restrict__ slot_idx,
                                  const float* __restrict__ grad, int64_t n_host,
                                  const int32_t* __restrict__ n_dev, UpdateParams p,
-                                 double* __restrict__ stats, int acc_stripes) {
-  __shared__ double lds[16];
+                                 double* __restrict__ stats, int acc_stripes,
+                                 uint32_t* __restrict__ hist, int nbins, int hist_stripes,
+                                 double* __restrict__ metrics, int64_t* __restrict__ step_counter) {
+  // block 0 also turns the step's AUC histogram into metrics (the forward finished
+  // before this launch): the separate single-block AUC launch leaves the critical path
+  if (hist && blockIdx.x == 0) auc_hist_block(hist, nbins, hist_stripes, metrics, step_counter);
   const int64_t n = dev_len(n_dev, n_host);
   double dnnz = 0, wsum = 0, dsum = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -315,11 +320,9 @@ __global__ void kv_update_kernel(Slot* __restrict__ slots, int64_t cap,
     const double d = (double)s.w - w_old;
     dsum += d * d;
   }
-  if (stats) {
-    double a = block_sum_f64(dnnz, lds);
-    double b = block_sum_f64(wsum, lds);
-    double c = block_sum_f64(dsum, lds);
-    if (threadIdx.x == 0) {
+  if (stats) {  // per-wave DPP sums, lane 63 adds to the striped accumulators (no barriers)
+    const double a = wave_sum_dpp(dnnz), b = wave_sum_dpp(wsum), c = wave_sum_dpp(dsum);
+    if ((threadIdx.x & 63) == 63) {
       double* st = acc_stripe(stats, acc_stripes);
       if (a != 0) atomicAdd(&st[0], a);
       if (b != 0) atomicAdd(&st[1], b);
@@ -761,10 +764,13 @@ void kv_set(void* slots, int64_t cap, const int64_t* slot_idx, int64_t n, const 
 void kv_update(void* slots, int64_t cap, const int64_t* slot_idx, const float* grad, int64_t n,
                const int32_t* n_dev, int algo, int lr_type, float alpha, float beta, float l1,
                float l2, float grad_scale, float max_delta, double* stats, int acc_stripes,
-               hipStream_t st) {
+               uint32_t* hist, int nbins, int hist_stripes, double* metrics,
+               int64_t* step_counter, hipStream_t st) {
   UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
+  if (hist && nbins != 2048) throw std::runtime_error("kv_update: the fused AUC needs 2048 bins");
   kv_update_kernel<<<grid_for(n, 256), 256, 0, st>>>((Slot*)slots, cap, slot_idx, grad, n, n_dev,
-                                                     p, stats, acc_stripes);
+                                                     p, stats, acc_stripes, hist, nbins,
+                                                     hist_stripes, metrics, step_counter);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

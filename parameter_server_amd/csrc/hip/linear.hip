@@ -200,87 +200,11 @@ linear_bwd_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__
   }
 }
 
-// Bucketed AUC of one minibatch from its histogram; metrics[3] += auc, metrics[4] += 1.
-// Resets the histogram (so the next step starts clean inside a captured graph).
+// Bucketed AUC of one minibatch from its histogram (auc_hist_block, loss.cuh).
 __global__ void auc_from_hist_kernel(uint32_t* __restrict__ hist, int nbins, int hist_stripes,
                                      double* __restrict__ metrics,
                                      int64_t* __restrict__ step_counter) {
-  // Exact integer AUC: 2 * area = sum_b pos_b * (2 * neg_below_b + neg_b) fits u64
-  // (counts <= 2^32). Thread t owns the contiguous bins [t*kPer, t*kPer + kPer) of
-  // every stripe; all stripe loads are issued before any use (one memory latency,
-  // not one per stripe and bin), the stripes are zeroed for the next graph-replayed
-  // step, and the cross-thread prefix is a wave-shuffle scan + 4-wave combine.
-  constexpr int kPer = 8;  // nbins == 256 * kPer (AUC_BINS = 2048), checked on the host
-  constexpr int kMaxStripes = 8;
-  __shared__ unsigned long long s_w[3][4];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // blockDim.x == 256
-  const int lo = t * kPer;
-  uint32_t nb[kPer], pb[kPer];
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) nb[q] = pb[q] = 0;
-  uint4 ln[kMaxStripes][2], lp[kMaxStripes][2];
-#pragma unroll
-  for (int sp = 0; sp < kMaxStripes; ++sp) {
-    if (sp < hist_stripes) {
-      const uint4* hn = reinterpret_cast<const uint4*>(hist + (int64_t)sp * 2 * nbins + lo);
-      const uint4* hp = reinterpret_cast<const uint4*>(hist + (int64_t)sp * 2 * nbins + nbins + lo);
-      ln[sp][0] = hn[0]; ln[sp][1] = hn[1];
-      lp[sp][0] = hp[0]; lp[sp][1] = hp[1];
-    }
-  }
-#pragma unroll
-  for (int sp = 0; sp < kMaxStripes; ++sp) {
-    if (sp < hist_stripes) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        nb[4 * h + 0] += ln[sp][h].x; nb[4 * h + 1] += ln[sp][h].y;
-        nb[4 * h + 2] += ln[sp][h].z; nb[4 * h + 3] += ln[sp][h].w;
-        pb[4 * h + 0] += lp[sp][h].x; pb[4 * h + 1] += lp[sp][h].y;
-        pb[4 * h + 2] += lp[sp][h].z; pb[4 * h + 3] += lp[sp][h].w;
-      }
-      uint4* zn = reinterpret_cast<uint4*>(hist + (int64_t)sp * 2 * nbins + lo);
-      uint4* zp = reinterpret_cast<uint4*>(hist + (int64_t)sp * 2 * nbins + nbins + lo);
-      const uint4 z = make_uint4(0, 0, 0, 0);
-      zn[0] = z; zn[1] = z; zp[0] = z; zp[1] = z;
-    }
-  }
-  unsigned long long neg = 0, pos = 0;
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) { neg += nb[q]; pos += pb[q]; }
-  unsigned long long x = neg;  // inclusive wave scan of negatives
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const unsigned long long y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  const unsigned long long wpos = wave_sum(pos);
-  if (lane == 63) s_w[0][w] = x;
-  if (lane == 0) s_w[1][w] = wpos;
-  __syncthreads();
-  unsigned long long before = 0, Ntot = 0, Ptot = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (q < w) before += s_w[0][q];
-    Ntot += s_w[0][q];
-    Ptot += s_w[1][q];
-  }
-  unsigned long long below = before + x - neg, area2 = 0;
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    area2 += (unsigned long long)pb[q] * (2 * below + nb[q]);
-    below += nb[q];
-  }
-  area2 = wave_sum(area2);
-  if (lane == 0) s_w[2][w] = area2;
-  __syncthreads();
-  if (t == 0) {
-    const unsigned long long A2 = s_w[2][0] + s_w[2][1] + s_w[2][2] + s_w[2][3];
-    if (Ptot > 0 && Ntot > 0) {
-      metrics[3] += 0.5 * (double)A2 / ((double)Ptot * (double)Ntot);
-      metrics[4] += 1.0;
-    }
-    if (step_counter) *step_counter += 1;  // device step clock (graph-replay safe)
-  }
+  auc_hist_block(hist, nbins, hist_stripes, metrics, step_counter);
 }
 
 // Expand a CSR row pointer into a per-nnz row index (COO rows).

@@ -261,9 +261,10 @@ class SparseLRTrainer:
             g_send = grad[:U].clone() if perm is None else grad[perm[:U].long()]
             self.pending = (slot, send_c, recv_c, g_send)
         else:
-            self._push(grad, push)
+            folded = self._push(grad, push, fold_auc=True)
         _push.__exit__(None, None, None)
-        auc_from_hist(self.hist, self.metrics, self.step_dev)
+        if push[0] == "fused" or not folded:
+            auc_from_hist(self.hist, self.metrics, self.step_dev)
         self.step_count += 1
         self.examples += B
 
@@ -833,7 +834,9 @@ class SparseLRTrainer:
         w_local[kept_idx] = w_kept
         return w_local, ("filtered", kept_idx, push)
 
-    def _push(self, grad: torch.Tensor, push):
+    def _push(self, grad: torch.Tensor, push, fold_auc: bool = False) -> bool:
+        """Apply a push; True when the step's AUC epilogue rode along (``fold_auc``: the
+        1-GPU KV update's block 0 turns the histogram into metrics, one launch less)."""
         kind = push[0]
         if kind == "filtered":
             kept_idx, inner = push[1], push[2]
@@ -843,10 +846,15 @@ class SparseLRTrainer:
             slot, n_dev = push[1], push[2]
             if n_dev is None:
                 self.table.update(slot, grad[:slot.numel()], self.rule, self.stats)
-            else:
+                return False
+            if fold_auc:
                 hipops().kv_update(self.table.slots, slot, grad, n_dev, *self.rule.args(),
-                                   self.stats)
-            return
+                                   self.stats, hist=self.hist, metrics=self.metrics,
+                                   step_counter=self.step_dev)
+                return True
+            hipops().kv_update(self.table.slots, slot, grad, n_dev, *self.rule.args(),
+                               self.stats)
+            return False
         _, slot, send_counts, recv_counts, U = push
         g = grad[:U].contiguous()
         nb = self.cfg.fixing_float_bytes
