@@ -564,7 +564,6 @@ wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __
                float* __restrict__ coef_out, uint16_t* __restrict__ dh, float* __restrict__ db,
                double* __restrict__ metrics, uint32_t* __restrict__ hist, int nbins,
                int acc_stripes) {
-  __shared__ double red[16];
   const int lane = threadIdx.x & 63;
   double loss_acc = 0, corr = 0, cnt = 0, dbsum = 0;
   for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < B;
@@ -605,11 +604,10 @@ wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __
       atomicAdd(&hist[(y > 0.f ? nbins : 0) + (int)pb], 1u);
     }
   }
-  const double a = block_sum_f64(loss_acc, red);
-  const double c = block_sum_f64(corr, red);
-  const double n = block_sum_f64(cnt, red);
-  const double d = block_sum_f64(dbsum, red);
-  if (threadIdx.x == 0 && n > 0) {
+  // per-wave DPP sums, lane 63 adds (no barriers)
+  const double a = wave_sum_dpp(loss_acc), c = wave_sum_dpp(corr), n = wave_sum_dpp(cnt);
+  const double d = wave_sum_dpp(dbsum);
+  if ((threadIdx.x & 63) == 63 && n > 0) {
     double* mt = acc_stripe(metrics, acc_stripes);
     atomicAdd(&mt[0], a);
     atomicAdd(&mt[1], c);

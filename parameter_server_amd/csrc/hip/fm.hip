@@ -39,7 +39,6 @@ fm_fwd_bwd_kernel(const uint16_t* __restrict__ X0, const float* __restrict__ val
                   uint16_t* __restrict__ dX0, double* __restrict__ metrics,
                   uint32_t* __restrict__ hist, int nbins, int acc_stripes) {
   extern __shared__ uint32_t lhist[];  // [2*nbins]
-  __shared__ double lds[16];
   for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) lhist[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -94,11 +93,9 @@ fm_fwd_bwd_kernel(const uint16_t* __restrict__ X0, const float* __restrict__ val
       if (f1 < D) drow[f1] = f32_to_bf16(coef * (x * s1 - x * x * bf16_to_f32(row[f1])));
     }
   }
-  if (metrics) {
-    const double a = block_sum_f64(loss_acc, lds);
-    const double c = block_sum_f64(corr_acc, lds);
-    const double n = block_sum_f64(cnt, lds);
-    if (threadIdx.x == 0 && n > 0) {
+  if (metrics) {  // per-wave DPP sums, lane 63 adds (no barriers)
+    const double a = wave_sum_dpp(loss_acc), c = wave_sum_dpp(corr_acc), n = wave_sum_dpp(cnt);
+    if ((threadIdx.x & 63) == 63 && n > 0) {
       double* mt = acc_stripe(metrics, acc_stripes);
       atomicAdd(&mt[0], a);
       atomicAdd(&mt[1], c);
@@ -172,7 +169,6 @@ fm_rows_kernel(const uint16_t* __restrict__ X0, const uint16_t* __restrict__ row
                int64_t w_cap, const float* __restrict__ labels, float* __restrict__ coef_out,
                uint16_t* __restrict__ dX0, double* __restrict__ metrics,
                uint32_t* __restrict__ hist, int nbins, int acc_stripes) {
-  __shared__ double lds[16];
   const int lane = threadIdx.x & 63;
   const int64_t waves = (int64_t)gridDim.x * (blockDim.x / 64);
   double loss_acc = 0, corr_acc = 0, cnt = 0;
@@ -239,11 +235,9 @@ fm_rows_kernel(const uint16_t* __restrict__ X0, const uint16_t* __restrict__ row
       }
     }
   }
-  if (metrics) {
-    const double a = block_sum_f64(loss_acc, lds);
-    const double c = block_sum_f64(corr_acc, lds);
-    const double n = block_sum_f64(cnt, lds);
-    if (threadIdx.x == 0 && n > 0) {
+  if (metrics) {  // per-wave DPP sums, lane 63 adds (no barriers)
+    const double a = wave_sum_dpp(loss_acc), c = wave_sum_dpp(corr_acc), n = wave_sum_dpp(cnt);
+    if ((threadIdx.x & 63) == 63 && n > 0) {
       double* mt = acc_stripe(metrics, acc_stripes);
       atomicAdd(&mt[0], a);
       atomicAdd(&mt[1], c);

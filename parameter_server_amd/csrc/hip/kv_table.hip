@@ -398,7 +398,6 @@ __global__ void kv_apply_accumulated_kernel(Slot* __restrict__ slots, int64_t ca
                                             const int32_t* __restrict__ n_touched, int64_t max_n,
                                             UpdateParams p, double* __restrict__ stats,
                                             int acc_stripes) {
-  __shared__ double lds[16];
   const int64_t n = dev_len(n_touched, max_n);
   double dnnz = 0, wsum = 0, dsum = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -416,11 +415,9 @@ __global__ void kv_apply_accumulated_kernel(Slot* __restrict__ slots, int64_t ca
     const double d = (double)s.w - w_old;
     dsum += d * d;
   }
-  if (stats) {
-    double a = block_sum_f64(dnnz, lds);
-    double b = block_sum_f64(wsum, lds);
-    double c = block_sum_f64(dsum, lds);
-    if (threadIdx.x == 0) {
+  if (stats) {  // per-wave DPP sums, lane 63 adds to the striped accumulators (no barriers)
+    const double a = wave_sum_dpp(dnnz), b = wave_sum_dpp(wsum), c = wave_sum_dpp(dsum);
+    if ((threadIdx.x & 63) == 63) {
       double* st = acc_stripe(stats, acc_stripes);
       if (a != 0) atomicAdd(&st[0], a);
       if (b != 0) atomicAdd(&st[1], b);
@@ -493,7 +490,6 @@ __global__ void kv_apply_rows_kernel(Slot* __restrict__ slots, int64_t cap,
                                      const unsigned long long* __restrict__ link, uint64_t hmask,
                                      const int32_t* __restrict__ nxt, int64_t n_ent,
                                      UpdateParams p, double* __restrict__ stats, int acc_stripes) {
-  __shared__ double lds[16];
   const int s = blockIdx.y;
   const int64_t n = dev_len(recv + (int64_t)s * H + 1, C);
   double dnnz = 0, wsum = 0, dsum = 0;
@@ -536,11 +532,9 @@ __global__ void kv_apply_rows_kernel(Slot* __restrict__ slots, int64_t cap,
     }
     slots[k] = sl;
   }
-  if (stats) {
-    double a = block_sum_f64(dnnz, lds);
-    double b = block_sum_f64(wsum, lds);
-    double c = block_sum_f64(dsum, lds);
-    if (threadIdx.x == 0) {
+  if (stats) {  // per-wave DPP sums, lane 63 adds to the striped accumulators (no barriers)
+    const double a = wave_sum_dpp(dnnz), b = wave_sum_dpp(wsum), c = wave_sum_dpp(dsum);
+    if ((threadIdx.x & 63) == 63) {
       double* st = acc_stripe(stats, acc_stripes);
       if (a != 0) atomicAdd(&st[0], a);
       if (b != 0) atomicAdd(&st[1], b);
@@ -575,7 +569,6 @@ __global__ __launch_bounds__(256) void kv_apply_part_kernel(
   __shared__ float wg[kApWin];
   __shared__ int32_t ra[kMaxChain], re[kMaxChain], roff[kMaxChain + 1], rcnt[kMaxChain];
   __shared__ uint64_t thr;
-  __shared__ double red[16];
   const int tid = threadIdx.x, P = 1 << lgP, part = blockIdx.x;
   const int CH = max(1, kApWin / G);
   if (tid < G) {
@@ -669,11 +662,9 @@ __global__ __launch_bounds__(256) void kv_apply_part_kernel(
       hh[h] = -1;
     }
   }
-  if (stats) {
-    double a = block_sum_f64(dnnz, red);
-    double b = block_sum_f64(wsum, red);
-    double c = block_sum_f64(dsum, red);
-    if (tid == 0) {
+  if (stats) {  // per-wave DPP sums, lane 63 adds to the striped accumulators (no barriers)
+    const double a = wave_sum_dpp(dnnz), b = wave_sum_dpp(wsum), c = wave_sum_dpp(dsum);
+    if ((threadIdx.x & 63) == 63) {
       double* st = acc_stripe(stats, acc_stripes);
       if (a != 0) atomicAdd(&st[0], a);
       if (b != 0) atomicAdd(&st[1], b);

@@ -50,7 +50,6 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
   // kLPR lanes cooperate on one example (strided over its nnz, then a shuffle
   // reduction), so B = 65536 rows launch 8x more waves than lane-per-row.
   extern __shared__ uint32_t lhist[];  // [2*nbins] when hist != nullptr
-  __shared__ double lds[16];
   if (hist) {
     for (int i = threadIdx.x; i < 2 * nbins; i += blockDim.x) lhist[i] = 0;
     __syncthreads();
@@ -121,11 +120,9 @@ linear_fwd_kernel(const int64_t* __restrict__ row_ptr, int64_t B, int width,
                        corr_acc, cnt);
     }
   }
-  if (metrics) {
-    double a = block_sum_f64(loss_acc, lds);
-    double c = block_sum_f64(corr_acc, lds);
-    double n = block_sum_f64(cnt, lds);
-    if (threadIdx.x == 0 && n > 0) {
+  if (metrics) {  // per-wave DPP sums, lane 63 adds (no barriers)
+    const double a = wave_sum_dpp(loss_acc), c = wave_sum_dpp(corr_acc), n = wave_sum_dpp(cnt);
+    if ((threadIdx.x & 63) == 63 && n > 0) {
       double* mt = acc_stripe(metrics, acc_stripes);
       atomicAdd(&mt[0], a);
       atomicAdd(&mt[1], c);

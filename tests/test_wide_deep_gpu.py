@@ -178,8 +178,10 @@ def _wd_rehearsal(rank, world, port, q, exchange="padded", model="wd"):
     keys, w, _, _ = tr.shard.table.occupied()
     o = torch.argsort(keys)
     rows = tr.shard.rows[idx[o]].float().cpu()
-    q.put((rank, p, tr.param.cpu() if model == "wd" else None, occ, keys[o].cpu(), w[o].cpu(),
-           rows))
+    # numpy by value: a torch tensor goes through a shared-memory fd that the parent
+    # may fetch only after this process exited (FileNotFoundError in resource_sharer)
+    q.put((rank, p, tr.param.cpu().numpy() if model == "wd" else None, occ,
+           keys[o].cpu().numpy(), w[o].cpu().numpy(), rows.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -202,7 +204,8 @@ def _run_rehearsal(exchange, model="wd"):
     res = sorted([q.get(timeout=120) for _ in ps], key=lambda r: r[0])
     for p in ps:
         p.join(timeout=60)
-    return res
+    t = lambda a: None if a is None else torch.from_numpy(a)  # noqa: E731
+    return [(r, p, t(a), occ, t(k), t(w), t(rows)) for r, p, a, occ, k, w, rows in res]
 
 
 @pytest.mark.parametrize("exchange", ["padded", "exact"])
