@@ -76,7 +76,7 @@ void tile_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int
 void xchg_pack_keys(const uint64_t*, const int32_t*, int64_t, const int64_t*, int, int64_t, int,
                     int64_t, int32_t*, int32_t*, hipStream_t);
 void xchg_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
-                     int64_t, int, int64_t, int32_t*, hipStream_t);
+                     int64_t, int, int64_t, int32_t*, uint32_t*, int, double*, int64_t*, hipStream_t);
 void xchg_clear_counts(int32_t*, int, int64_t, bool, bool, hipStream_t);
 void xchg_publish(const int32_t*, int32_t*, hipStream_t);
 void xchg_unpack_w(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
@@ -790,7 +790,8 @@ PYBIND11_MODULE(_hipops, m) {
                           optr<int32_t>(ovf, at::kInt, "ovf"), cur_stream());
   });
   m.def("xchg_pack_grads", [](Tensor grad, optional<Tensor> perm, Tensor n_uniq, Tensor off,
-                              int64_t C, int kw, int64_t H, Tensor send) {
+                              int64_t C, int kw, int64_t H, Tensor send, optional<Tensor> hist,
+                              optional<Tensor> metrics, optional<Tensor> step_counter) {
     chk(grad, at::kFloat, "grad");
     chk(n_uniq, at::kInt, "n_uniq");
     chk(off, at::kLong, "off");
@@ -801,9 +802,18 @@ PYBIND11_MODULE(_hipops, m) {
     check(send.numel() == G * H, "send must be [G * H]");
     const int32_t* pp = optr<int32_t>(perm, at::kInt, "perm");
     if (pp) check(perm->numel() >= grad.numel(), "perm shorter than grad");
+    // optional: the step's AUC histogram (stripes x 2 x 2048) -> metrics in block 0
+    uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
+    double* mp = optr<double>(metrics, at::kDouble, "metrics");
+    if (hp) check(mp && hist->numel() % 4096 == 0 && hist->numel() / 4096 <= 8,
+                  "xchg_pack_grads: hist = stripes x 2 x 2048 (<= 8 stripes) with metrics");
     psamd::xchg_pack_grads(ptr<float>(grad), pp, ptr<int32_t>(n_uniq), grad.numel(),
-                           ptr<int64_t>(off), G, C, kw, H, ptr<int32_t>(send), cur_stream());
-  });
+                           ptr<int64_t>(off), G, C, kw, H, ptr<int32_t>(send), hp,
+                           hp ? (int)(hist->numel() / 4096) : 1, mp,
+                           optr<int64_t>(step_counter, at::kLong, "step_counter"), cur_stream());
+  }, py::arg("grad"), py::arg("perm"), py::arg("n_uniq"), py::arg("off"), py::arg("C"),
+     py::arg("kw"), py::arg("H"), py::arg("send"), py::arg("hist") = py::none(),
+     py::arg("metrics") = py::none(), py::arg("step_counter") = py::none());
   m.def("xchg_ff_pack_grads", [](Tensor grad, optional<Tensor> perm, Tensor n_uniq, Tensor off,
                                  int64_t C, int kw, int64_t H, int nb, uint64_t seed,
                                  optional<Tensor> step, Tensor send, Tensor gstage) {

@@ -22,6 +22,7 @@
 // and counted in *ovf (the trainer raises on it; the capacity carries a large
 // statistical margin over the per-peer count of hashed keys).
 #include "common.cuh"
+#include "loss.cuh"
 
 namespace psamd {
 
@@ -73,8 +74,14 @@ __global__ void xchg_pack_grads_kernel(const float* __restrict__ grad,
                                        const int32_t* __restrict__ perm,
                                        const int32_t* __restrict__ n_uniq, int64_t n_host,
                                        const int64_t* __restrict__ off, int G, int64_t C, int kw,
-                                       int64_t H, int32_t* __restrict__ send) {
+                                       int64_t H, int32_t* __restrict__ send,
+                                       uint32_t* __restrict__ hist, int hist_stripes,
+                                       double* __restrict__ metrics,
+                                       int64_t* __restrict__ step_counter) {
   __shared__ int64_t soff[kMaxPeers + 1];
+  // block 0 also turns the step's AUC histogram into metrics (the forward is done):
+  // the single-block AUC launch leaves the worker half of the step
+  if (hist && blockIdx.x == 0) auc_hist_block(hist, 2048, hist_stripes, metrics, step_counter);
   load_offsets(off, G, soff);
   if (blockIdx.x == 0 && threadIdx.x < G) {
     const int p = threadIdx.x;
@@ -144,9 +151,11 @@ void xchg_pack_keys(const uint64_t* ukeys, const int32_t* n_uniq, int64_t n_host
 
 void xchg_pack_grads(const float* grad, const int32_t* perm, const int32_t* n_uniq,
                      int64_t n_host, const int64_t* off, int G, int64_t C, int kw, int64_t H,
-                     int32_t* send, hipStream_t st) {
+                     int32_t* send, uint32_t* hist, int hist_stripes, double* metrics,
+                     int64_t* step_counter, hipStream_t st) {
   xchg_pack_grads_kernel<<<grid_for(n_host, 256), 256, 0, st>>>(grad, perm, n_uniq, n_host, off,
-                                                                 G, C, kw, H, send);
+                                                                 G, C, kw, H, send, hist, hist_stripes,
+                                                                 metrics, step_counter);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

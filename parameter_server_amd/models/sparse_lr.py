@@ -598,8 +598,11 @@ class SparseLRTrainer:
         H, C, kw = xc.H, xc.C, xc.kw
         if xc.nb:
             self._x_ff_pack(grad[:loc.uniq.numel()], perm, n_uniq, off, send)
-        elif self.gpu:
-            hipops().xchg_pack_grads(grad[:loc.uniq.numel()], perm, n_uniq, off, C, kw, H, send)
+        elif self.gpu:  # (+ the step's AUC epilogue in block 0: one launch less)
+            hipops().xchg_pack_grads(grad[:loc.uniq.numel()], perm, n_uniq, off, C, kw, H, send,
+                                     hist=self.hist, metrics=self.metrics,
+                                     step_counter=self.step_dev)
+            return
         else:
             for p in range(self.G):
                 a, c = int(off[p]), min(int(off[p + 1] - off[p]), C)
