@@ -109,7 +109,10 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     # "own" = a dedicated high-priority exchange stream
     xmode = os.environ.get("PSAMD_XCHG_STREAM", "prep") if split else "none"
     comm_s = torch.cuda.Stream(device, priority=-1) if xmode == "own" else main
-    apply_s = torch.cuda.Stream(device) if asp else None
+    # (normal priority: at high priority, like the preparation streams, 8 emulated peers
+    # measured 0.369 vs 0.340 ms / step; PSAMD_APPLY_PRIORITY overrides)
+    apply_s = (torch.cuda.Stream(device, priority=int(os.environ.get("PSAMD_APPLY_PRIORITY", "0")))
+               if asp else None)
     # exchange of step t + xd issued after worker t: needs worker t + xd - 1 - lag
     # issued (xd <= lag + 1) and the preparation of t + xd (xd <= nprep)
     xd = min(nprep, 2, tr.lag + 1) if split else 0
