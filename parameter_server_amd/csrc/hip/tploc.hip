@@ -46,7 +46,9 @@ constexpr int kMaxBk = 2048;            // buckets (tile LDS: 72 KB -> 2 workgro
 constexpr int kMaxT = 640;              // tiles (n <= 5.2 M)
 constexpr int kBThr = 256;              // emit workgroups
 constexpr int kBkThr = 512;             // bucket workgroups
-constexpr int kECap = 4096;             // entries of one bucket held in LDS
+constexpr int kECap = 4096;             // entries of one bucket (global stride)
+constexpr int kECapL = 4064;            // ... held in LDS (bucket kernel LDS <= 40 KB:
+                                        // 4 workgroups per CU instead of 3)
 constexpr int kDH = 2048;               // distinct-key hash of one bucket
 constexpr uint32_t kEmpty = 0xffffffffu;
 }  // namespace tp
@@ -232,12 +234,15 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
 #define TP_MARK(k) \
   if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 12 + (k)] = clock64();
   TP_MARK(0)
-  __shared__ uint16_t eh[kECap];    // hash slot of every gathered entry
+  // 40,932 B of LDS (<= 40 KB: 4 workgroups of 512 threads per CU)
+  __shared__ uint16_t eh[kECapL];   // hash slot of every gathered entry
   __shared__ uint64_t hs[kDH];      // hash (key u32 | count u32), then the sorted list
-  __shared__ uint64_t dl[kDH];      // compacted (key | count << 16 | slot), then cur/jj
-  __shared__ uint32_t tpre[kMaxT + 1];
-  __shared__ uint16_t tlo[kMaxT];
+  __shared__ uint64_t dl[kDH];      // per-tile runs (tpre / tlo, until the inserts), then
+                                    // compacted (key | count << 16 | slot), then cur/jj
   __shared__ uint32_t lds[kBkThr / 64 + 1];
+  static_assert((kMaxT + 1) * 4 + kMaxT * 2 <= kDH * 8, "tile runs must fit in dl");
+  uint32_t* tpre = reinterpret_cast<uint32_t*>(dl);                // [kMaxT + 1]
+  uint16_t* tlo = reinterpret_cast<uint16_t*>(tpre + kMaxT + 1);  // [kMaxT]
   uint32_t* hkey = reinterpret_cast<uint32_t*>(hs);
   uint32_t* hcnt = hkey + kDH;
   uint32_t* cur = reinterpret_cast<uint32_t*>(dl);    // [kDH] per slot, after the sort
@@ -268,10 +273,10 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
   if (t == 0) tpre[T] = E;
   __syncthreads();
   TP_MARK(1)
-  const uint32_t En = E < (uint32_t)kECap ? E : (uint32_t)kECap;
-  bool bad = E > (uint32_t)kECap;
+  const uint32_t En = E < (uint32_t)kECapL ? E : (uint32_t)kECapL;
+  bool bad = E > (uint32_t)kECapL;
   int32_t* be = beid + (int64_t)b * kECap;
-  constexpr int kG = kECap / kBkThr;  // entries per thread: locate all, then load all
+  constexpr int kG = (kECapL + kBkThr - 1) / kBkThr;  // entries per thread: locate all, then load all
   int64_t idx[kG];
 #pragma unroll
   for (int q = 0; q < kG; ++q) {
