@@ -75,3 +75,67 @@ def test_tp_fused_falls_back_for_variable_rows():
     m, c, lo, g = _reference(L.local_col[:B * width], w, labels, B, width, None)
     torch.testing.assert_close(c_f[:B], c, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(g_f[:U], g, rtol=1e-3, atol=1e-4)
+
+
+def test_tp_fused_fixed_point_partials_are_deterministic_and_exact():
+    """The per-tile entry partials accumulate in 64-bit fixed point with integer LDS
+    atomics: repeated runs give bitwise identical partials whatever the atomic order,
+    and the gradient matches an fp64 scatter-add to ~1 ulp. (The entry scan combines
+    runs cut by a wave boundary with float atomics into the gradient the localiser
+    zeroed, so the gradient is compared from the first run only.)"""
+    B, width = 65536, 39
+    keys, labels = criteo_batch(B, seed=9, row0=0, num_features=10 ** 9, device=DEV)
+    n = keys.numel()
+    L = Localizer(n, 30, DEV, mode="tp", lazy_cols=True)(keys)
+    U = int(L.n_uniq.item())
+    w = torch.randn(U, device=DEV) * 0.05
+    outs, parts = [], []
+    for _ in range(3):
+        c_f, g_f = linear_fwd_bwd(L, w, labels, B=B, width=width, coef=torch.empty(B, device=DEV))
+        outs.append(g_f[:U].clone())
+        parts.append(L.tile.psum.clone())
+    assert all(torch.equal(parts[0], p) for p in parts[1:])
+    cols = ensure_local_col(L)[:n].long()
+    m = w[cols].reshape(B, width).double().sum(1).float()
+    _, c, _ = loss_terms_torch(m, labels, 2)
+    g64 = torch.zeros(U, dtype=torch.float64, device=DEV).index_add_(
+        0, cols, c.double().repeat_interleave(width))
+    # exactly rounded tile partials, then an fp32 scan over <= 312 tiles per key
+    torch.testing.assert_close(outs[0].double(), g64, rtol=1e-5, atol=1e-6)
+
+
+def test_kv_update_folds_the_auc_epilogue():
+    """kv_update(..., hist=, metrics=, step_counter=) computes the step's bucketed AUC in
+    its block 0 exactly like auc_from_hist, zeroes the histogram and ticks the clock."""
+    from parameter_server_amd.ops.kv_table import KVTable, UpdateRule
+    from parameter_server_amd.ops.linear import HIST_STRIPES, auc_from_hist
+    from parameter_server_amd.ops.native import hipops
+
+    g = torch.Generator(device="cpu").manual_seed(4)
+    hist = torch.randint(0, 50, (HIST_STRIPES * 2 * AUC_BINS,), generator=g,
+                         dtype=torch.int32).to(DEV)
+    h2 = hist.clone()
+    m_ref, m_new = new_accum(DEV), new_accum(DEV)
+    s_ref = torch.zeros(1, dtype=torch.int64, device=DEV)
+    s_new = torch.zeros(1, dtype=torch.int64, device=DEV)
+    auc_from_hist(h2, m_ref, s_ref)
+    t = KVTable(1 << 12, DEV)
+    keys = torch.arange(1, 1001, dtype=torch.int64, device=DEV)
+    slot, _ = t.resolve(keys)
+    grad = torch.randn(1000, device=DEV)
+    stats = new_accum(DEV)
+    rule = UpdateRule("ftrl", "decay", 0.01, 10.0, 1.0, 1.0)
+    hipops().kv_update(t.slots, slot, grad, None, *rule.args(), stats, hist=hist,
+                       metrics=m_new, step_counter=s_new)
+    torch.cuda.synchronize()
+    assert int(hist.abs().sum()) == 0 and int(s_new.item()) == 1
+    torch.testing.assert_close(accum_total(m_new)[3:5], accum_total(m_ref)[3:5], rtol=0, atol=0)
+    # the update itself is unchanged
+    t2 = KVTable(1 << 12, DEV)
+    slot2, _ = t2.resolve(keys)
+    hipops().kv_update(t2.slots, slot2, grad, None, *rule.args(), new_accum(DEV))
+    # (concurrent inserts may place colliding keys differently: compare by key)
+    a, b = t.occupied(), t2.occupied()
+    oa, ob = torch.argsort(a[0]), torch.argsort(b[0])
+    for x, y in zip(a, b):
+        assert torch.equal(x[oa], y[ob])
