@@ -108,14 +108,16 @@ bcd_grad_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row
 
 // K13 -------------------------------------------------------------------------
 // Per-coordinate proximal Newton step with trust region and KKT filter
-// (darlin.h:206-246). dw receives the applied change (0 if inactive / filtered).
+// (darlin.h:206-246). dw receives the applied change (0 if inactive; filtered: 0, or
+// NaN with nan_filtered = the reference server's NaN mark, darlin.h:228-231, which
+// tells the replicas of a sharded server to drop the column from their active set).
 // Violation is max-reduced as the bit pattern of a non-negative double.
 __global__ void __launch_bounds__(256)
 bcd_update_kernel(int64_t c0, int64_t ncols, double* __restrict__ G, double* __restrict__ U,
                   double* __restrict__ w, double* __restrict__ delta,
                   uint8_t* __restrict__ active, double* __restrict__ dw, double eta, double lambda,
                   double delta_max, double kkt_thr, unsigned long long* __restrict__ vio_bits,
-                  int consume) {
+                  int consume, int nan_filtered) {
   double vmax = 0;
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < ncols;
        j += (int64_t)gridDim.x * blockDim.x) {
@@ -139,6 +141,7 @@ bcd_update_kernel(int64_t c0, int64_t ncols, double* __restrict__ G, double* __r
       }
       if (filtered) {
         active[k] = 0;
+        if (nan_filtered) d = __builtin_nan("");
       } else {
         vmax = fmax(vmax, vio);
         d = -wk;
@@ -157,6 +160,30 @@ bcd_update_kernel(int64_t c0, int64_t ncols, double* __restrict__ G, double* __r
   for (int off = 32; off > 0; off >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, off, 64));
   if ((threadIdx.x & 63) == 0 && vmax > 0)
     atomicMax(vio_bits, (unsigned long long)__double_as_longlong(vmax));
+}
+
+// Sharded server, replica side: the owners' updates of a block arrive as one
+// all-gathered dw (NaN = KKT-filtered). Every rank replays them on its replica of
+// w / delta / active outside its own slice [own0, own1) with the owner's exact
+// arithmetic (the replicas stay bitwise equal), and turns NaN marks into 0 for the
+// dual update.
+__global__ void __launch_bounds__(256)
+bcd_replica_kernel(int64_t c0, int64_t ncols, int64_t own0, int64_t own1, double* __restrict__ dw,
+                   double* __restrict__ w, double* __restrict__ delta,
+                   uint8_t* __restrict__ active, double delta_max) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < ncols;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    const double d = dw[j];
+    const bool mine = j >= own0 && j < own1;
+    if (d != d) {
+      dw[j] = 0;
+      if (!mine) active[c0 + j] = 0;
+    } else if (!mine && active[c0 + j]) {
+      const int64_t k = c0 + j;
+      delta[k] = fmin(delta_max, 2 * fabs(d) + .1);
+      w[k] = w[k] + d;
+    }
+  }
 }
 
 // K12 -------------------------------------------------------------------------
@@ -335,11 +362,20 @@ void bcd_grad_chunked(const int32_t* col, const int32_t* row, const float* val,
 
 void bcd_update(int64_t c0, int64_t ncols, double* G, double* U, double* w, double* delta,
                 uint8_t* active, double* dw, double eta, double lambda, double delta_max,
-                double kkt_thr, unsigned long long* vio_bits, bool consume, hipStream_t st) {
+                double kkt_thr, unsigned long long* vio_bits, bool consume, bool nan_filtered,
+                hipStream_t st) {
   if (ncols <= 0) return;
   bcd_update_kernel<<<grid_for(ncols, 256, 4096), 256, 0, st>>>(
       c0, ncols, G, U, w, delta, active, dw, eta, lambda, delta_max, kkt_thr, vio_bits,
-      consume ? 1 : 0);
+      consume ? 1 : 0, nan_filtered ? 1 : 0);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void bcd_replica(int64_t c0, int64_t ncols, int64_t own0, int64_t own1, double* dw, double* w,
+                 double* delta, uint8_t* active, double delta_max, hipStream_t st) {
+  if (ncols <= 0) return;
+  bcd_replica_kernel<<<grid_for(ncols, 256, 4096), 256, 0, st>>>(c0, ncols, own0, own1, dw, w,
+                                                                  delta, active, delta_max);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -156,7 +156,9 @@ void bcd_grad_chunked(const int32_t*, const int32_t*, const float*, const int64_
                       int64_t, int64_t, const double*, const float*, int64_t, const double*,
                       const uint8_t*, double*, double*, bool, hipStream_t);
 void bcd_update(int64_t, int64_t, double*, double*, double*, double*, uint8_t*, double*, double,
-                double, double, double, unsigned long long*, bool, hipStream_t);
+                double, double, double, unsigned long long*, bool, bool, hipStream_t);
+void bcd_replica(int64_t, int64_t, int64_t, int64_t, double*, double*, double*, uint8_t*, double,
+                 hipStream_t);
 void bcd_dual(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
               const double*, const float*, double*, int64_t, hipStream_t);
 void bcd_objective(const double*, int64_t, double*, hipStream_t);
@@ -1404,7 +1406,7 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("bcd_update", [](int64_t c0, int64_t ncols, Tensor G, Tensor U, Tensor w, Tensor delta,
                          Tensor active, Tensor dw, double eta, double lambda, double delta_max,
-                         double kkt_thr, Tensor vio_bits, bool consume) {
+                         double kkt_thr, Tensor vio_bits, bool consume, bool nan_filtered) {
     chk(G, at::kDouble, "G");
     chk(U, at::kDouble, "U");
     chk(w, at::kDouble, "w");
@@ -1419,7 +1421,19 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::bcd_update(c0, ncols, ptr<double>(G), ptr<double>(U), ptr<double>(w),
                       ptr<double>(delta), ptr<uint8_t>(active), ptr<double>(dw), eta, lambda,
                       delta_max, kkt_thr, ptr<unsigned long long>(vio_bits), consume,
-                      cur_stream());
+                      nan_filtered, cur_stream());
+  });
+  m.def("bcd_replica", [](int64_t c0, int64_t ncols, int64_t own0, int64_t own1, Tensor dw,
+                          Tensor w, Tensor delta, Tensor active, double delta_max) {
+    chk(dw, at::kDouble, "dw");
+    chk(w, at::kDouble, "w");
+    chk(delta, at::kDouble, "delta");
+    chk(active, at::kByte, "active");
+    check(w.numel() == delta.numel() && w.numel() == active.numel(), "model arrays mismatch");
+    check(c0 >= 0 && ncols >= 0 && c0 + ncols <= w.numel(), "column block outside model");
+    check(dw.numel() >= ncols, "dw too small");
+    psamd::bcd_replica(c0, ncols, own0, own1, ptr<double>(dw), ptr<double>(w), ptr<double>(delta),
+                       ptr<uint8_t>(active), delta_max, cur_stream());
   });
   m.def("bcd_dual", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                 int64_t p1, int64_t c0, int64_t ncols, Tensor dw, Tensor y,

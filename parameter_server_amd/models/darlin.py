@@ -79,6 +79,7 @@ class DarlinConfig:
     init_w: float = 0.0             # init_w (ZERO / CONSTANT)
     seed: int = 0
     host_preprocess: bool = False   # GPU trainer: build the CSC with numpy instead (reference)
+    shard_server: bool = True       # G > 1: owners update their slice of each block
 
     @classmethod
     def from_lm(cls, lm, seed: int = 0) -> "DarlinConfig":
@@ -173,6 +174,10 @@ class DarlinTrainer:
         self.device = torch.device(device)
         self.verbose = verbose
         self.rng = random.Random(cfg.seed)
+        # sharded server: reduce-scatter [G | U] to the owners + all-gather dw, instead of
+        # an all-reduce of [G | U] and the identical update on every rank
+        self.shard = self.G > 1 and cfg.shard_server and hasattr(self.comm, "backend") \
+            and self.comm.backend in ("nccl", "gloo")
         t0 = time.time()
         self._preprocess(data)
         self.preprocess_time = time.time() - t0
@@ -492,6 +497,8 @@ class DarlinTrainer:
 
     # -------------------------------------------------------------- one pass
     def _launch(self, b: Block):
+        if self.shard:
+            return self._launch_sharded(b)
         # the block's persistent [G | U] unless a previous launch of the same block is
         # still in flight (a prior block re-launched within the delay window)
         zeroed = b.gu is not None and not b.busy
@@ -505,6 +512,8 @@ class DarlinTrainer:
         return (b, GU, work, zeroed)
 
     def _finish(self, item):
+        if self.shard:
+            return self._finish_sharded(item)
         b, GU, work, persistent = item
         if work is not None:
             work.wait()
@@ -514,6 +523,51 @@ class DarlinTrainer:
                            c.delta_max, self.kkt_thr, vio=self.vio, consume=persistent)
         if persistent:
             b.busy = False
+        bcd.dual(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, dw, self.y,
+                 self.ym)
+
+    # ---- sharded server (G > 1): rank r owns the r-th even slice of every block
+    def _own_slice(self, b: Block) -> tuple[int, int, int]:
+        """(m, own0, own1): the block's slice width m = ceil(ncols / G) and this rank's
+        columns [own0, own1) relative to c0 (empty past ncols)."""
+        m = -(-b.ncols // self.G)
+        j0 = min(self.rank * m, b.ncols)
+        return m, j0, min(j0 + m, b.ncols)
+
+    def _launch_sharded(self, b: Block):
+        """Worker half of a block: gradient into a [G | U] padded to G equal slices,
+        then two reduce-scatters over RCCL: every owner receives the sums of its slice
+        only (the reference's push of G, U to the servers of the block's key range,
+        darlin.h:318-354, each server summing what its workers pushed)."""
+        m, _, _ = self._own_slice(b)
+        P = m * self.G
+        dev = self.device
+        GU = torch.zeros(2 * P, dtype=torch.float64, device=dev)
+        bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
+                 self.delta, self.active, GU[:b.ncols], GU[P:P + b.ncols], chunks=b.chunks,
+                 zeroed=True)
+        mine = torch.empty(2 * m, dtype=torch.float64, device=dev)
+        w1 = self.comm.reduce_scatter_async(mine[:m], GU[:P])
+        w2 = self.comm.reduce_scatter_async(mine[m:], GU[P:])
+        return (b, mine, (w1, w2))
+
+    def _finish_sharded(self, item):
+        """Server half on the owner's slice (the coordinate update of darlin.h:206-246
+        with NaN marks for KKT-filtered columns), one all-gather of the block's dw (the
+        workers' pull of the new weights), then every rank replays the other owners'
+        updates on its replica and applies the dual update."""
+        b, mine, works = item
+        for wk in works:
+            wk.wait()
+        m, j0, j1 = self._own_slice(b)
+        c = self.cfg
+        dwo = torch.zeros(m, dtype=torch.float64, device=self.device)
+        bcd.update(b.c0 + j0, j1 - j0, mine[:m], mine[m:], self.w, self.delta, self.active,
+                   c.eta, c.l1, c.delta_max, self.kkt_thr, dw=dwo, vio=self.vio,
+                   nan_filtered=True)
+        dw = torch.empty(m * self.G, dtype=torch.float64, device=self.device)
+        self.comm.all_gather_into_async(dw, dwo).wait()
+        bcd.replica(b.c0, b.ncols, j0, j1, dw, self.w, self.delta, self.active, c.delta_max)
         bcd.dual(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, dw, self.y,
                  self.ym)
 

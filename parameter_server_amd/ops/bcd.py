@@ -100,11 +100,14 @@ def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, act
 
 
 def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
-           delta_max: float, kkt_thr: float, dw=None, vio=None, consume: bool = False):
+           delta_max: float, kkt_thr: float, dw=None, vio=None, consume: bool = False,
+           nan_filtered: bool = False):
     """Coordinate update of block [c0, c0+ncols). Returns (dw fp64[ncols], vio) where
     ``vio`` is an int64[1] tensor holding the max KKT violation as fp64 bits
     (max-accumulated across calls; see ``violation``). ``consume`` zeroes G / U
-    after reading them."""
+    after reading them. ``nan_filtered``: a KKT-filtered column's dw is NaN instead of
+    0 (the reference server's mark, src/app/linear_method/darlin.h:228-231), for
+    ``replica``."""
     dev = w.device
     if dw is None:
         dw = torch.empty(ncols, dtype=torch.float64, device=dev)
@@ -112,7 +115,7 @@ def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
         vio = torch.zeros(1, dtype=torch.int64, device=dev)
     if is_gpu(w):
         hipops().bcd_update(c0, ncols, G, U, w, delta, active, dw, eta, lam, delta_max, kkt_thr,
-                            vio, consume)
+                            vio, consume, nan_filtered)
         return dw, vio
     sl = slice(c0, c0 + ncols)
     act = active[sl].bool()
@@ -133,7 +136,7 @@ def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
     delta[sl] = torch.where(upd, torch.clamp(2 * d.abs() + .1, max=delta_max), dk)
     w[sl] = wk + d
     active[sl] = torch.where(filt, torch.zeros_like(active[sl]), active[sl])
-    dw[:ncols] = d
+    dw[:ncols] = torch.where(filt, torch.full_like(d, float("nan")), d) if nan_filtered else d
     vm = float(torch.where(upd, v, torch.zeros_like(v)).max()) if ncols else 0.0
     cur = violation(vio)
     if vm > cur:
@@ -142,6 +145,29 @@ def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
         G[:ncols] = 0
         U[:ncols] = 0
     return dw, vio
+
+
+def replica(c0: int, ncols: int, own0: int, own1: int, dw, w, delta, active, delta_max: float):
+    """Replay the owners' coordinate updates of block [c0, c0+ncols) (all-gathered
+    ``dw`` with NaN marks) on this rank's replica outside its own slice [own0, own1):
+    NaN -> column leaves the active set, else (if active) w += d and the trust region
+    becomes min(delta_max, 2|d| + .1), the owner's arithmetic exactly. NaN marks are
+    then zeroed in ``dw`` (in place) for the dual update."""
+    if is_gpu(w):
+        hipops().bcd_replica(c0, ncols, own0, own1, dw, w, delta, active, delta_max)
+        return dw
+    d = dw[:ncols]
+    nan = torch.isnan(d)
+    j = torch.arange(ncols, device=d.device)
+    other = (j < own0) | (j >= own1)
+    sl = slice(c0, c0 + ncols)
+    act = active[sl].bool()
+    upd = other & ~nan & act
+    delta[sl] = torch.where(upd, torch.clamp(2 * d.abs() + .1, max=delta_max), delta[sl])
+    w[sl] = torch.where(upd, w[sl] + d, w[sl])
+    active[sl] = torch.where(other & nan, torch.zeros_like(active[sl]), active[sl])
+    d[nan] = 0
+    return dw
 
 
 def violation(vio) -> float:

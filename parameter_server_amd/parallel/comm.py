@@ -65,6 +65,17 @@ class Comm:
         current stream after it (RCCL runs it on its own stream meanwhile)."""
         return _Done()
 
+    def reduce_scatter_async(self, out: torch.Tensor, inp: torch.Tensor):
+        """Start ``out = sum over ranks of chunk[rank] of inp`` (``inp`` holds ``world``
+        equal chunks of ``out.numel()``); ``wait()`` orders the current stream after it."""
+        out.copy_(inp[:out.numel()])
+        return _Done()
+
+    def all_gather_into_async(self, out: torch.Tensor, inp: torch.Tensor):
+        """Start ``out = cat over ranks of inp``; ``wait()`` as above."""
+        out[:inp.numel()].copy_(inp)
+        return _Done()
+
     def all_gather_obj(self, obj):
         return [obj]
 
@@ -237,6 +248,29 @@ class DistComm(Comm):
         self._count_reduce(t)
         ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
         return dist.all_reduce(t, op=ops[op], group=self.group, async_op=True)
+
+    def reduce_scatter_async(self, out: torch.Tensor, inp: torch.Tensor):
+        n = out.numel()
+        assert inp.numel() == n * self.world
+        b = n * out.element_size() * (self.world - 1)
+        count_traffic("reduce_scatter", b, b)
+        if self.backend == "gloo":  # gloo has no reduce-scatter: all-reduce, keep own chunk
+            h = inp.detach().to("cpu", copy=True)
+            dist.all_reduce(h, group=self.group)
+            out.copy_(h[self.rank * n:(self.rank + 1) * n])
+            return _Done()
+        return dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=True)
+
+    def all_gather_into_async(self, out: torch.Tensor, inp: torch.Tensor):
+        assert out.numel() == inp.numel() * self.world
+        b = inp.numel() * inp.element_size() * (self.world - 1)
+        count_traffic("all_gather", b, b)
+        if self.backend == "gloo" and inp.is_cuda:  # rehearsal mode: staged through host
+            h = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_gather_into_tensor(h, inp.cpu(), group=self.group)
+            out.copy_(h)
+            return _Done()
+        return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
 
     def all_gather_obj(self, obj):
         out = [None] * self.world

@@ -246,11 +246,16 @@ def _dist_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_trainer_two_ranks_gloo_equals_single_rank():
+@pytest.mark.parametrize("world", [2, 3])
+def test_trainer_two_ranks_gloo_equals_single_rank(world):
+    """Sharded server (reduce-scatter of [G | U] to the owners, owner update with NaN
+    marks, all-gather of dw, replica replay): every rank's replica equals the
+    single-rank trainer and the replicas stay bitwise identical (world 3: blocks whose
+    width is not a multiple of 3, padded slices)."""
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_dist_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=240) for _ in ps])
@@ -264,7 +269,8 @@ def test_trainer_two_ranks_gloo_equals_single_rank():
         np.testing.assert_allclose(objs, [p.objective for p in prog], rtol=1e-9)
         assert nnz == [p.nnz_w for p in prog]
         np.testing.assert_allclose(w, tr.w.numpy(), atol=1e-9)
-    np.testing.assert_array_equal(res[0][3], res[1][3])  # replicas stay bitwise identical
+    for r in range(1, world):  # replicas stay bitwise identical
+        np.testing.assert_array_equal(res[0][3], res[r][3])
 
 
 def test_darlin_plumbing_1_2_2_matches_trainer(tmp_path):
