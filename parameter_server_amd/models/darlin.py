@@ -79,7 +79,13 @@ class DarlinConfig:
     init_w: float = 0.0             # init_w (ZERO / CONSTANT)
     seed: int = 0
     host_preprocess: bool = False   # GPU trainer: build the CSC with numpy instead (reference)
-    shard_server: bool = True       # G > 1: owners update their slice of each block
+    # G > 1, per block: "on" = reduce-scatter [G | U] to the owners of the block's
+    # slices + all-gather dw (3 x ncols x 8 B over the links, 2 collectives), "off" = one
+    # all-reduce of [G | U] and the identical update on every rank (4 x ncols x 8 B, 1
+    # collective), "auto" = sharded for blocks of >= shard_min_cols columns (bandwidth-
+    # bound), all-reduce below (latency-bound)
+    shard_server: str = "auto"
+    shard_min_cols: int = 1 << 16
 
     @classmethod
     def from_lm(cls, lm, seed: int = 0) -> "DarlinConfig":
@@ -174,10 +180,12 @@ class DarlinTrainer:
         self.device = torch.device(device)
         self.verbose = verbose
         self.rng = random.Random(cfg.seed)
-        # sharded server: reduce-scatter [G | U] to the owners + all-gather dw, instead of
-        # an all-reduce of [G | U] and the identical update on every rank
-        self.shard = self.G > 1 and cfg.shard_server and hasattr(self.comm, "backend") \
-            and self.comm.backend in ("nccl", "gloo")
+        # sharded server (see DarlinConfig.shard_server); both block paths keep the
+        # replicas of w / delta / active bitwise equal, so they mix freely
+        if cfg.shard_server not in ("auto", "on", "off"):
+            raise ValueError(f"shard_server must be auto / on / off, got {cfg.shard_server!r}")
+        self.shard = self.G > 1 and cfg.shard_server != "off" and \
+            getattr(self.comm, "backend", None) in ("nccl", "gloo")
         t0 = time.time()
         self._preprocess(data)
         self.preprocess_time = time.time() - t0
@@ -496,8 +504,12 @@ class DarlinTrainer:
                   f"{len(self.blocks)} blocks", file=sys.stderr)
 
     # -------------------------------------------------------------- one pass
+    def _sharded(self, b: Block) -> bool:
+        return self.shard and (self.cfg.shard_server == "on"
+                               or b.ncols >= self.cfg.shard_min_cols)
+
     def _launch(self, b: Block):
-        if self.shard:
+        if self._sharded(b):
             return self._launch_sharded(b)
         # the block's persistent [G | U] unless a previous launch of the same block is
         # still in flight (a prior block re-launched within the delay window)
@@ -512,7 +524,7 @@ class DarlinTrainer:
         return (b, GU, work, zeroed)
 
     def _finish(self, item):
-        if self.shard:
+        if self._sharded(item[0]):
             return self._finish_sharded(item)
         b, GU, work, persistent = item
         if work is not None:

@@ -225,7 +225,7 @@ def _free_port():
     return p
 
 
-def _dist_worker(rank, world, port, q):
+def _dist_worker(rank, world, port, q, shard="auto"):
     import torch.distributed as dist
 
     from parameter_server_amd.parallel.comm import DistComm
@@ -238,24 +238,25 @@ def _dist_worker(rank, world, port, q):
     a, b = rank * n, (rank + 1) * n
     part = SlotData(labels=sd.labels[a:b], groups={
         g: (off[a:b + 1] - off[a], k[off[a]:off[b]], None) for g, (off, k, v) in sd.groups.items()})
-    tr = DarlinTrainer(part, DarlinConfig(l1=1.0, max_pass=6, tail_freq=1, seed=3),
-                       comm=DistComm("cpu"))
+    tr = DarlinTrainer(part, DarlinConfig(l1=1.0, max_pass=6, tail_freq=1, seed=3,
+                                          shard_server=shard), comm=DistComm("cpu"))
     prog = tr.train()
     q.put((rank, [p.objective for p in prog], [p.nnz_w for p in prog], tr.w.numpy().copy()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_trainer_two_ranks_gloo_equals_single_rank(world):
-    """Sharded server (reduce-scatter of [G | U] to the owners, owner update with NaN
+@pytest.mark.parametrize("world,shard", [(2, "auto"), (2, "on"), (3, "on")])
+def test_trainer_two_ranks_gloo_equals_single_rank(world, shard):
+    """All-reduce path (auto: these blocks are small) and sharded server (reduce-scatter of [G | U] to the owners, owner update with NaN
     marks, all-gather of dw, replica replay): every rank's replica equals the
     single-rank trainer and the replicas stay bitwise identical (world 3: blocks whose
     width is not a multiple of 3, padded slices)."""
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_dist_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_dist_worker, args=(r, world, port, q, shard))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=240) for _ in ps])
