@@ -111,8 +111,13 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     comm_s = torch.cuda.Stream(device, priority=-1) if xmode == "own" else main
     # (normal priority: at high priority, like the preparation streams, 8 emulated peers
     # measured 0.369 vs 0.340 ms / step; PSAMD_APPLY_PRIORITY overrides)
+    # ASP owner applies: "stream" = on their own stream; "tail" = at the end of the
+    # exchange half on its own (preparation) stream, after the weights went back and
+    # after the event the next exchange and the worker wait for (so neither waits for
+    # the apply: still asynchronous, one stream less)
+    asp_apply = os.environ.get("PSAMD_ASP_APPLY", "stream") if asp else "none"
     apply_s = (torch.cuda.Stream(device, priority=int(os.environ.get("PSAMD_APPLY_PRIORITY", "0")))
-               if asp else None)
+               if asp_apply == "stream" else None)
     # exchange of step t + xd issued after worker t: needs worker t + xd - 1 - lag
     # issued (xd <= lag + 1) and the preparation of t + xd (xd <= nprep)
     xd = min(nprep, 2, tr.lag + 1) if split else 0
@@ -173,8 +178,19 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
         if asp:  # ring entry of exchange t is free again once that apply is done
             aclock.wait_for(tr.sched.apply_gate(t), xs)
         with torch.cuda.stream(xs):
-            run_plan(xplan(t), t, xs)
-            ev_x[t % E].record(xs)
+            if asp_apply == "tail":
+                plan = xplan(t)
+                for kind, fn in plan:
+                    if kind != "async":
+                        fn()
+                ev_x[t % E].record(xs)
+                for kind, fn in plan:
+                    if kind == "async":
+                        fn()
+                aclock.record(t, xs)
+            else:
+                run_plan(xplan(t), t, xs)
+                ev_x[t % E].record(xs)
 
     def iterate():
         t = state["t"]

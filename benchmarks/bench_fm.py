@@ -19,6 +19,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--localize", default="sort", choices=("sort", "part"))
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--minibatch", type=int, default=16384)
     ap.add_argument("--num-features", type=float, default=1e9)
@@ -37,7 +38,7 @@ def main():
     comm, dev = init_from_env("cuda")
     G, rank = comm.world, comm.rank
     B, N = args.minibatch, int(args.num_features)
-    cfg = FMConfig(num_features=N, embedding_dim=args.dim, minibatch=B, compact_rows=bool(args.compact_rows),
+    cfg = FMConfig(localize=args.localize, num_features=N, embedding_dim=args.dim, minibatch=B, compact_rows=bool(args.compact_rows),
                    table_capacity=args.table_slots, seed=0)
     tr = FMTrainer(cfg, comm, dev)
     bufs = [(torch.empty(B * 39, dtype=torch.int64, device=dev),

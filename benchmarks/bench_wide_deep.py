@@ -19,6 +19,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--localize", default="sort", choices=("sort", "part"))
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--minibatch", type=int, default=16384)
     ap.add_argument("--num-features", type=float, default=1e9)
@@ -48,7 +49,7 @@ def main():
     emu = comm.backend == "loopback" if hasattr(comm, "backend") else False
     NG = 1 if emu else G  # GPUs actually running
     B, N = args.minibatch, int(args.num_features)
-    cfg = WideDeepConfig(num_features=N, embedding_dim=args.dim, minibatch=B,
+    cfg = WideDeepConfig(localize=args.localize, num_features=N, embedding_dim=args.dim, minibatch=B,
                          table_capacity=args.table_slots, gemm=args.gemm, seed=0,
                          overlap_wgrad=bool(args.overlap_wgrad))
     tr = WideDeepTrainer(cfg, comm, dev)

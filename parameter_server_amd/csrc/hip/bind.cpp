@@ -76,7 +76,7 @@ void tile_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int
 void xchg_pack_keys(const uint64_t*, const int32_t*, int64_t, const int64_t*, int, int64_t, int,
                     int64_t, int32_t*, int32_t*, hipStream_t);
 void xchg_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
-                     int64_t, int, int64_t, int32_t*, uint32_t*, int, double*, int64_t*, hipStream_t);
+                     int64_t, int, int64_t, int32_t*, uint32_t*, int, double*, int64_t*, const int32_t*, int32_t*, hipStream_t);
 void xchg_clear_counts(int32_t*, int, int64_t, bool, bool, hipStream_t);
 void xchg_publish(const int32_t*, int32_t*, hipStream_t);
 void xchg_unpack_w(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
@@ -767,6 +767,17 @@ PYBIND11_MODULE(_hipops, m) {
     check(off.numel() == 2, "off must be [2]");
     psamd::kvv_single_off(ptr<int32_t>(n_uniq), ptr<int64_t>(off), cur_stream());
   });
+  // device-visible pointer of a pinned int32 host flag (nullptr when absent)
+  auto host_flag = [](const optional<Tensor>& src, const optional<Tensor>& host_dst) -> int32_t* {
+    if (!host_dst.has_value() || !host_dst->defined()) return nullptr;
+    check(src.has_value() && src->defined(), "ovf_host needs ovf");
+    check(host_dst->device().is_cpu() && host_dst->is_pinned() &&
+              host_dst->scalar_type() == at::kInt && host_dst->numel() >= 1,
+          "ovf_host must be a pinned int32 host tensor");
+    void* dptr = nullptr;
+    PSAMD_HIP_CHECK(hipHostGetDevicePointer(&dptr, host_dst->data_ptr(), 0));
+    return reinterpret_cast<int32_t*>(dptr);
+  };
   m.def("xchg_publish", [](Tensor src, Tensor host_dst) {
     chk(src, at::kInt, "src");
     check(host_dst.device().is_cpu() && host_dst.is_pinned() && host_dst.scalar_type() == at::kInt &&
@@ -791,9 +802,10 @@ PYBIND11_MODULE(_hipops, m) {
                           ptr<int64_t>(off), G, C, kw, H, ptr<int32_t>(send),
                           optr<int32_t>(ovf, at::kInt, "ovf"), cur_stream());
   });
-  m.def("xchg_pack_grads", [](Tensor grad, optional<Tensor> perm, Tensor n_uniq, Tensor off,
+  m.def("xchg_pack_grads", [host_flag](Tensor grad, optional<Tensor> perm, Tensor n_uniq, Tensor off,
                               int64_t C, int kw, int64_t H, Tensor send, optional<Tensor> hist,
-                              optional<Tensor> metrics, optional<Tensor> step_counter) {
+                              optional<Tensor> metrics, optional<Tensor> step_counter,
+                              optional<Tensor> ovf, optional<Tensor> ovf_host) {
     chk(grad, at::kFloat, "grad");
     chk(n_uniq, at::kInt, "n_uniq");
     chk(off, at::kLong, "off");
@@ -812,10 +824,13 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::xchg_pack_grads(ptr<float>(grad), pp, ptr<int32_t>(n_uniq), grad.numel(),
                            ptr<int64_t>(off), G, C, kw, H, ptr<int32_t>(send), hp,
                            hp ? (int)(hist->numel() / 4096) : 1, mp,
-                           optr<int64_t>(step_counter, at::kLong, "step_counter"), cur_stream());
+                           optr<int64_t>(step_counter, at::kLong, "step_counter"),
+                           optr<int32_t>(ovf, at::kInt, "ovf"), host_flag(ovf, ovf_host),
+                           cur_stream());
   }, py::arg("grad"), py::arg("perm"), py::arg("n_uniq"), py::arg("off"), py::arg("C"),
      py::arg("kw"), py::arg("H"), py::arg("send"), py::arg("hist") = py::none(),
-     py::arg("metrics") = py::none(), py::arg("step_counter") = py::none());
+     py::arg("metrics") = py::none(), py::arg("step_counter") = py::none(),
+     py::arg("ovf") = py::none(), py::arg("ovf_host") = py::none());
   m.def("xchg_ff_pack_grads", [](Tensor grad, optional<Tensor> perm, Tensor n_uniq, Tensor off,
                                  int64_t C, int kw, int64_t H, int nb, uint64_t seed,
                                  optional<Tensor> step, Tensor send, Tensor gstage) {

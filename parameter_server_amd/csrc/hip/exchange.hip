@@ -77,8 +77,14 @@ __global__ void xchg_pack_grads_kernel(const float* __restrict__ grad,
                                        int64_t H, int32_t* __restrict__ send,
                                        uint32_t* __restrict__ hist, int hist_stripes,
                                        double* __restrict__ metrics,
-                                       int64_t* __restrict__ step_counter) {
+                                       int64_t* __restrict__ step_counter,
+                                       const int32_t* __restrict__ ovf,
+                                       int32_t* __restrict__ ovf_host) {
   __shared__ int64_t soff[kMaxPeers + 1];
+  // the overflow counter (final for this step: its key pack ran earlier in stream
+  // order) goes to the host-mapped flag here instead of in a 1-thread launch of its
+  // own (4 us of launch + system-scope release per step at 8 peers)
+  if (ovf_host && blockIdx.x == 0 && threadIdx.x == 0) ovf_host[0] = ovf[0];
   // block 0 also turns the step's AUC histogram into metrics (the forward is done):
   // the single-block AUC launch leaves the worker half of the step
   if (hist && blockIdx.x == 0) auc_hist_block(hist, 2048, hist_stripes, metrics, step_counter);
@@ -152,10 +158,12 @@ void xchg_pack_keys(const uint64_t* ukeys, const int32_t* n_uniq, int64_t n_host
 void xchg_pack_grads(const float* grad, const int32_t* perm, const int32_t* n_uniq,
                      int64_t n_host, const int64_t* off, int G, int64_t C, int kw, int64_t H,
                      int32_t* send, uint32_t* hist, int hist_stripes, double* metrics,
-                     int64_t* step_counter, hipStream_t st) {
+                     int64_t* step_counter, const int32_t* ovf, int32_t* ovf_host,
+                     hipStream_t st) {
   xchg_pack_grads_kernel<<<grid_for(n_host, 256), 256, 0, st>>>(grad, perm, n_uniq, n_host, off,
                                                                  G, C, kw, H, send, hist, hist_stripes,
-                                                                 metrics, step_counter);
+                                                                 metrics, step_counter, ovf,
+                                                                 ovf_host);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

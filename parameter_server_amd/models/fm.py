@@ -57,6 +57,7 @@ class FMConfig:
     exchange_slack: float = 1.5
     exchange_capacity: int = 0
     compact_rows: bool = True            # 1 GPU: gather each unique key's row once per step
+    localize: str = "sort"               # GPU key localisation: "sort" | "part" (ops/localize.py)
     seed: int = 0
 
 
@@ -79,7 +80,7 @@ class FMTrainer(EmbeddingPS):
         self.shard = E.EmbeddingShard(cap, D, dev, init_scale=cfg.emb_init_scale,
                                       seed=cfg.seed * 7919 + 17)
         self.max_nnz = B * S
-        self.localizer = Localizer(self.max_nnz, self.bits, dev)
+        self.localizer = Localizer(self.max_nnz, self.bits, dev, mode=cfg.localize)
         self.coef = torch.empty(B, dtype=torch.float32, device=dev)
         self.metrics = new_accum(dev)
         self.stats = new_accum(dev)

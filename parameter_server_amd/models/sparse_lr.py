@@ -480,7 +480,8 @@ class SparseLRTrainer:
         if self.gpu:
             hh = hipops()
             hh.xchg_pack_keys(ukeys, nkeys, off, xc.C, xc.kw, xc.H, send, xc.ovf)
-            hh.xchg_publish(xc.ovf, xc.ovf_host)
+            if xc.nb:  # (FixingFloat push: no pack_grads launch to carry the flag)
+                hh.xchg_publish(xc.ovf, xc.ovf_host)
             return
         H, C, kw = xc.H, xc.C, xc.kw
         for p in range(self.G):
@@ -601,7 +602,8 @@ class SparseLRTrainer:
         elif self.gpu:  # (+ the step's AUC epilogue in block 0: one launch less)
             hipops().xchg_pack_grads(grad[:loc.uniq.numel()], perm, n_uniq, off, C, kw, H, send,
                                      hist=self.hist, metrics=self.metrics,
-                                     step_counter=self.step_dev)
+                                     step_counter=self.step_dev, ovf=xc.ovf,
+                                     ovf_host=xc.ovf_host)
             return
         else:
             for p in range(self.G):

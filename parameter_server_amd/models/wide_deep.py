@@ -61,6 +61,7 @@ class WideDeepConfig:
     exchange: str = "padded"             # G > 1 on GPU: sync-free fixed rows | "exact"
     exchange_slack: float = 1.5          # padded row capacity = slack x first max + 1024
     exchange_capacity: int = 0           # explicit per-peer capacity (0 = from slack)
+    localize: str = "sort"               # GPU key localisation: "sort" | "part" (ops/localize.py)
     seed: int = 0
 
 
@@ -77,7 +78,8 @@ class EmbeddingPS:
         (``step(..., loc=...)``)."""
         locs = self.__dict__.setdefault("_localizers", [self.localizer])
         while len(locs) <= buf:
-            locs.append(Localizer(self.max_nnz, self.bits, self.device))
+            locs.append(Localizer(self.max_nnz, self.bits, self.device,
+                                  mode=getattr(self.cfg, "localize", "sort")))
         return locs[buf](keys)
 
     # ------------------------------------------------------------ checkpoint
@@ -332,7 +334,7 @@ class WideDeepTrainer(EmbeddingPS):
         self.shard = E.EmbeddingShard(cap, D, dev, init_scale=cfg.emb_init_scale,
                                       seed=cfg.seed * 7919 + 17)
         self.max_nnz = B * S
-        self.localizer = Localizer(self.max_nnz, self.bits, dev)
+        self.localizer = Localizer(self.max_nnz, self.bits, dev, mode=cfg.localize)
         # ---- dense MLP: flat fp32 params / grads / Adam state, bf16 copy for the GEMMs
         dims = [S * D] + list(cfg.hidden)
         shapes = []

@@ -91,11 +91,13 @@ def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     assert abs(loss_p - ref.progress()["loss"]) < 1e-4
 
 
-def test_asp_pipeline_trains(monkeypatch):
-    """asp: the owner's push applies replay on their own stream and pulls never wait
-    for them, so the result is timing dependent; it must still train every key and
-    stay within the ring (flush applies everything)."""
+@pytest.mark.parametrize("apply", ["stream", "tail"])
+def test_asp_pipeline_trains(monkeypatch, apply):
+    """asp: the owner's push applies replay on their own stream (or at the tail of the
+    exchange half) and pulls never wait for them, so the result is timing dependent;
+    it must still train every key and stay within the ring (flush applies everything)."""
     monkeypatch.setenv("PSAMD_XCHG_STREAM", "prep")
+    monkeypatch.setenv("PSAMD_ASP_APPLY", apply)
     bench = _bench()
     B, N, seed = 4096, 10 ** 6, 78
     dev = torch.device("cuda")

@@ -230,3 +230,30 @@ def test_padded_exchange_matches_exact(model):
         assert abs(rp[1]["loss"] - re_[1]["loss"]) < 1e-4
         if model == "wd":
             torch.testing.assert_close(rp[2], re_[2], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("model", ["wd", "fm"])
+def test_part_localisation_matches_sort(model):
+    """localize='part' (partition + per-bucket LDS dedup) trains what the radix sort
+    trains: same unique keys, the order inside a key's segment only changes the
+    order of the fp32 gradient sums."""
+    from parameter_server_amd.models import FMConfig, FMTrainer
+
+    losses = {}
+    for mode in ("sort", "part"):
+        if model == "wd":
+            tr = WideDeepTrainer(WideDeepConfig(num_features=10 ** 8, minibatch=4096,
+                                                table_capacity=1 << 20, localize=mode),
+                                 device="cuda")
+        else:
+            tr = FMTrainer(FMConfig(num_features=10 ** 8, minibatch=4096,
+                                    table_capacity=1 << 20, localize=mode), device="cuda")
+        assert tr.localizer.mode == mode
+        ls = []
+        for s in range(6):
+            k, l = criteo_batch(4096, seed=4, row0=s * 4096, num_features=10 ** 8,
+                                device="cuda")
+            tr.step(k, l)
+            ls.append(tr.progress()["loss"])
+        losses[mode] = ls
+    np.testing.assert_allclose(losses["part"], losses["sort"], rtol=2e-3)
