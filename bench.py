@@ -55,9 +55,10 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
       RCCL's own stream this keeps 4 busy streams; one more (a dedicated exchange
       stream, PSAMD_XCHG_STREAM=own) oversubscribes the hardware queues (8 emulated
       peers: 0.333 vs 0.308 ms/step).
-    * ASP: the owner's push apply of each exchange replays on its own stream; later
-      exchanges wait for it only when they reuse its ring entry (the apply of exchange
-      t - depth), never to see its pushes.
+    * ASP: the owner's push apply of each exchange replays at the tail of its exchange
+      half, after the event the worker and the next exchange wait for; later exchanges
+      wait for it only when they reuse its ring entry (the apply of exchange t - depth),
+      never to see its pushes.
 
     Graphs are captured per phase t % P, P = lcm(2 * nprep buffers, exchange ring).
     tests/test_bench_pipeline_gpu.py checks the pipeline trains exactly what the
@@ -111,11 +112,13 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     comm_s = torch.cuda.Stream(device, priority=-1) if xmode == "own" else main
     # (normal priority: at high priority, like the preparation streams, 8 emulated peers
     # measured 0.369 vs 0.340 ms / step; PSAMD_APPLY_PRIORITY overrides)
-    # ASP owner applies: "stream" = on their own stream; "tail" = at the end of the
-    # exchange half on its own (preparation) stream, after the weights went back and
-    # after the event the next exchange and the worker wait for (so neither waits for
-    # the apply: still asynchronous, one stream less)
-    asp_apply = os.environ.get("PSAMD_ASP_APPLY", "stream") if asp else "none"
+    # ASP owner applies: "tail" (default) = at the end of the exchange half on its
+    # (preparation) stream, after the weights went back and after the event that the
+    # next exchange and the worker wait for, so neither waits for the apply (still
+    # asynchronous) and no fifth busy stream oversubscribes the 4 hardware queues;
+    # "stream" = on a stream of their own. 8 emulated peers: 0.355 -> 0.164 ms / step,
+    # with fixing-float 1 B 0.392 -> 0.175 (profiles/r2_asp_tail.log)
+    asp_apply = os.environ.get("PSAMD_ASP_APPLY", "tail") if asp else "none"
     apply_s = (torch.cuda.Stream(device, priority=int(os.environ.get("PSAMD_APPLY_PRIORITY", "0")))
                if asp_apply == "stream" else None)
     # exchange of step t + xd issued after worker t: needs worker t + xd - 1 - lag

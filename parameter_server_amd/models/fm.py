@@ -57,7 +57,9 @@ class FMConfig:
     exchange_slack: float = 1.5
     exchange_capacity: int = 0
     compact_rows: bool = True            # 1 GPU: gather each unique key's row once per step
-    localize: str = "sort"               # GPU key localisation: "sort" | "part" (ops/localize.py)
+    # GPU key localisation (ops/localize.py): "part" = partition + per-bucket LDS dedup
+    # (B = 65536: 0.563 vs 0.587 ms / step with the radix sort, profiles/r2_asp_tail.log)
+    localize: str = "part"
     seed: int = 0
 
 
