@@ -121,14 +121,17 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     asp_apply = os.environ.get("PSAMD_ASP_APPLY", "tail") if asp else "none"
     apply_s = (torch.cuda.Stream(device, priority=int(os.environ.get("PSAMD_APPLY_PRIORITY", "0")))
                if asp_apply == "stream" else None)
-    # exchange of step t + xd issued after worker t: needs worker t + xd - 1 - lag
-    # issued (xd <= lag + 1) and the preparation of t + xd (xd <= nprep)
-    xd = min(nprep, 2, tr.lag + 1) if split else 0
+    # exchange of step t + xd issued after worker t: needs the worker of the step it
+    # carries (t + xd - 1 - lag, or t + xd - lag with post applies) issued and the
+    # preparation of t + xd (xd <= nprep)
+    post = tr.padded and tr.sched.post
+    xd = min(nprep, 2, tr.lag if post else tr.lag + 1) if split else 0
     E = 64  # event rings, indexed by step (every look-back here is < 64 steps)
     ev_buf = [torch.cuda.Event() for _ in range(NB)]   # worker done with buffer b
     ev_w = [torch.cuda.Event() for _ in range(E)]      # worker half of step t done
     ev_prep = [torch.cuda.Event() for _ in range(NB)]
     ev_x = [torch.cuda.Event() for _ in range(E)]      # exchange half of step t done
+    ev_post = [torch.cuda.Event() for _ in range(E)]   # ... and its post apply (ssp)
     aclock = EventClock(E)                             # asp: push apply of exchange t done
 
     def run_plan(plan, t, xs):
@@ -173,24 +176,30 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
         xs = sides[(t % NB) % nprep] if xmode == "prep" else comm_s
         if xmode != "prep":
             xs.wait_event(ev_prep[t % NB])  # (on its prep stream it follows the prep)
-        c = t - 1 - tr.lag
+        c = tr.sched.carried(t)
         if c >= 0:
             xs.wait_event(ev_w[c % E])      # the gradients it carries are packed
-        if t >= 1:
-            xs.wait_event(ev_x[(t - 1) % E])  # owner updates of consecutive steps in order
+        if t >= 1:  # owner updates of consecutive steps in order
+            xs.wait_event((ev_post if post else ev_x)[(t - 1) % E])
         if asp:  # ring entry of exchange t is free again once that apply is done
             aclock.wait_for(tr.sched.apply_gate(t), xs)
         with torch.cuda.stream(xs):
-            if asp_apply == "tail":
+            if asp_apply == "tail" or post:
+                # the apply after the event the worker waits for (ssp post apply: the
+                # next exchange waits for it; asp: nothing waits for it)
+                late = ("async", "post")
                 plan = xplan(t)
                 for kind, fn in plan:
-                    if kind != "async":
+                    if kind not in late:
                         fn()
                 ev_x[t % E].record(xs)
                 for kind, fn in plan:
-                    if kind == "async":
+                    if kind in late:
                         fn()
-                aclock.record(t, xs)
+                if post:
+                    ev_post[t % E].record(xs)
+                else:
+                    aclock.record(t, xs)
             else:
                 run_plan(xplan(t), t, xs)
                 ev_x[t % E].record(xs)
@@ -247,7 +256,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     def capture(plan):
         out = []
         for kind, fn in plan:  # in order: a segment may bake in buffers the previous
-            if kind in ("compute", "async"):  # one of the same ring entry selected
+            if kind in ("compute", "async", "post"):  # one of the same ring entry selected
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                     fn()

@@ -67,6 +67,10 @@ class SparseLRConfig:
     table_load: float = 0.5              # auto capacity = num_features / G / load
     max_table_bytes: int = 96 << 30      # cap for the auto size (per GPU)
     init: InitRule = field(default_factory=InitRule)
+    # ssp (lag >= 1) owner apply of the carried pushes: "post" = after the exchange's
+    # pulls are resolved and the weights sent back (off the worker's critical path),
+    # "pre" = before resolving them; same visibility (parallel/consistency.py)
+    ssp_apply: str = "post"
     tail_feature_freq: int = 0           # keep keys seen > freq times (0 = off)
     countmin_n: float = 1e8
     countmin_k: int = 2
@@ -149,7 +153,8 @@ class SparseLRTrainer:
         # pushes of steps <= t-1-lag (bsp: lag 0; ssp:tau: lag tau). asp: lag 1 and the
         # owner applies pushes on their own stream, which later pulls do not wait for
         # (only buffer reuse bounds it: async_depth exchanges in flight).
-        self.sched = ExchangeSchedule(self.tau, cfg.exchange_lag, cfg.asp_depth)
+        self.sched = ExchangeSchedule(self.tau, cfg.exchange_lag, cfg.asp_depth,
+                                      post=cfg.ssp_apply == "post")
         self.lag, self.asp, self.async_depth = self.sched.lag, self.sched.asp, self.sched.depth
         # rings of R exchange buffers indexed by step (>= 2: the exchange of step t+1
         # runs while the worker half of step t still reads its weights)
@@ -282,9 +287,11 @@ class SparseLRTrainer:
           comm     all-to-all A
           compute  owner: apply the pushes of t-1-lag (one optimizer step per source,
                    rank order, all sources in one launch), then lookup-or-insert of
-                   the pulled keys of t -> weights       [ASP: resolve only]
+                   the pulled keys of t -> weights       [ASP / SSP post: resolve only]
           async    [ASP: apply the pushes of t-1-lag; the next pulls do not wait]
           comm     all-to-all B (weights back)
+          post     [SSP post (lag >= 1): apply the pushes of t-lag carried by this
+                   exchange; the worker does not wait for it, the next exchange does]
           compute  unpack weights, forward, backward, pack grads(t), AUC
           host     counters, overflow check
 
@@ -329,20 +336,26 @@ class SparseLRTrainer:
 
         segs = [("compute", lambda: self._x_pack_keys(loc, gb, r)),
                 ("comm", lambda: comm.all_to_all_fixed(xc.sends[gb], xc.recvs[r]))]
+        if self.cfg.ssp_apply not in ("post", "pre"):
+            raise ValueError(f"ssp_apply must be 'post' or 'pre', not {self.cfg.ssp_apply!r}")
         if self.asp:
             segs += [("compute", lambda: self._x_resolve(r)),
                      ("async", lambda: self._x_apply(r, gb))]
+        elif self.sched.post:
+            segs += [("compute", lambda: self._x_resolve(r))]
         else:
             segs += [("compute", lambda: (self._x_apply(r, gb), self._x_resolve(r)))]
         segs += [("comm", lambda: comm.all_to_all_fixed(xc.wsend, xc.wrecvs[r])),
-                 ("host", exchanged),
-                 ("compute", finish),
+                 ("host", exchanged)]
+        if self.sched.post:  # the carried pushes, after the weights went back
+            segs += [("post", lambda: self._x_apply(r, gb))]
+        segs += [("compute", finish),
                  ("host", host)]
         return segs
 
     @property
     def EXCHANGE_SEGMENTS(self) -> int:  # step_segments()[:n] = exchange half
-        return 6 if self.asp else 5
+        return 6 if self.asp or self.sched.post else 5
 
     def consistency_desc(self) -> str:
         """The consistency the data plane actually enforces (reported by bench.py)."""

@@ -9,7 +9,8 @@ On the GPU data plane there are no per-message dependencies to check: every
 step is one collective exchange, so the schedule itself is the vector clock.
 ``ExchangeSchedule`` fixes which step's pushes ride which exchange and which
 ring buffers a step uses: the pushes of step t ride exchange t+1+lag and the
-owner applies them before it resolves that exchange's pulls, so a pull of step
+owner applies them before it resolves that exchange's pulls (or, ssp, they ride
+exchange t+lag and are applied right after its pulls), so a pull of step
 t has seen exactly the pushes of steps <= t-1-lag of EVERY worker (the
 collective cannot start before all ranks have packed those gradients: the
 vector clock min_w clock[w] >= t-1-lag holds by construction). ASP decouples the
@@ -46,13 +47,23 @@ def parse_consistency(mode: str | int | float) -> float:
 class ExchangeSchedule:
     """Step -> exchange / buffer bookkeeping of the padded multi-GPU exchange.
 
-    ``lag``: pushes of step t ride exchange t+1+lag (bsp 0, ssp:tau tau unless a
-    smaller ``lag`` is asked for, asp 1). ``depth`` (asp only): exchanges whose push
-    applies may still be running when a later exchange resolves its pulls.
-    Buffers live in rings of ``R = max(2, lag + 1 + depth)`` entries indexed by step.
+    ``lag``: the pull of step t sees exactly the pushes of steps <= t-1-lag (bsp 0,
+    ssp:tau tau unless a smaller ``lag`` is asked for, asp 1: at least). ``depth``
+    (asp only): exchanges whose push applies may still be running when a later
+    exchange resolves its pulls. Buffers live in rings of ``R = max(2, lag + 1 +
+    depth)`` entries indexed by step.
+
+    Where the owner applies the pushes an exchange carries:
+    * pre (bsp, asp): exchange t carries the pushes of step t-1-lag and applies them
+      BEFORE resolving its pulls (asp: asynchronously beside them);
+    * post (ssp with lag >= 1, the default there): exchange t carries the pushes of
+      step t-lag and applies them AFTER its pulls are resolved and the weights have
+      gone back, so the worker never waits for an apply; the next exchange resolves
+      after it. The pull of step t still sees exactly the pushes of steps <= t-1-lag
+      (applied by exchanges <= t-1), one step of staleness fewer to carry.
     """
 
-    def __init__(self, tau: float, lag: int = -1, asp_depth: int = 4):
+    def __init__(self, tau: float, lag: int = -1, asp_depth: int = 4, post: bool = True):
         self.tau = float(tau)
         self.asp = math.isinf(self.tau)
         if self.asp:
@@ -66,6 +77,7 @@ class ExchangeSchedule:
         if self.lag < 0:
             raise ValueError("exchange lag must be >= 0")
         self.R = max(2, self.lag + 1 + self.depth)
+        self.post = bool(post) and not self.asp and self.lag >= 1
 
     def ring(self, t: int) -> int:
         """Ring entry of step t's pull (resolved slots, weights, offsets) and of the
@@ -74,7 +86,7 @@ class ExchangeSchedule:
 
     def carried(self, t: int) -> int:
         """Step whose pushes ride exchange t (negative: none yet)."""
-        return t - 1 - self.lag
+        return t - self.lag if self.post else t - 1 - self.lag
 
     def grad_ring(self, t: int) -> int:
         """Ring entry holding the gradients exchange t carries (its send buffer)."""
@@ -95,7 +107,7 @@ class ExchangeSchedule:
 
     def pending(self, exchanged: int, computed: int) -> range:
         """Steps computed whose gradients no issued exchange has carried yet."""
-        return range(max(0, exchanged - 1 - self.lag), computed)
+        return range(max(0, self.carried(exchanged)), computed)
 
     def staleness_bounds(self) -> tuple[int, float]:
         """(min, max) steps of pushes a pull may miss."""

@@ -208,10 +208,18 @@ def test_asp_differs_from_ssp1(tmp_path):
 def test_exchange_schedule_rings():
     from parameter_server_amd.parallel.consistency import ExchangeSchedule
 
-    s = ExchangeSchedule(4)
-    assert (s.lag, s.R, s.asp) == (4, 5, False)
+    s = ExchangeSchedule(4, post=False)
+    assert (s.lag, s.R, s.asp, s.post) == (4, 5, False, False)
     for t in range(20):  # the send buffer of exchange t holds grads(t-5), written by step t-5
         assert s.grad_ring(t) == (t - 5) % 5 and s.visible_through(t) == t - 5
+    assert list(s.pending(exchanged=10, computed=10)) == [5, 6, 7, 8, 9]
+    # post apply (ssp default): exchange t carries grads(t-4), applied after its pulls
+    p = ExchangeSchedule(4)
+    assert (p.lag, p.R, p.post) == (4, 5, True)
+    for t in range(20):
+        assert p.grad_ring(t) == (t - 4) % 5 and p.visible_through(t) == t - 5
+    assert list(p.pending(exchanged=10, computed=10)) == [6, 7, 8, 9]
+    assert not ExchangeSchedule(0).post and not ExchangeSchedule(float("inf")).post
     b = ExchangeSchedule(0)
     assert (b.lag, b.R) == (0, 2) and b.visible_through(3) == 2
     a = ExchangeSchedule(float("inf"), asp_depth=3)
