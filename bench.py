@@ -179,8 +179,16 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
         c = tr.sched.carried(t)
         if c >= 0:
             xs.wait_event(ev_w[c % E])      # the gradients it carries are packed
-        if t >= 1:  # owner updates of consecutive steps in order
-            xs.wait_event((ev_post if post else ev_x)[(t - 1) % E])
+        # owner updates of consecutive steps in order: exchange t resolves after exchange
+        # t-1 is done (ssp post: including its apply). With the apply at the tail only
+        # the resolve needs that (it rewrites wsend and must see the apply), so the key
+        # pack and all-to-all A of exchange t overlap the tail of exchange t-1
+        chain = ev_post if post else ev_x
+        # (not with the tail filter: its CountMin and keep-mask scratch are shared by
+        # the key packs of consecutive exchanges)
+        early = (post or asp_apply == "tail") and tr.filter is None
+        if t >= 1 and not early:
+            xs.wait_event(chain[(t - 1) % E])
         if asp:  # ring entry of exchange t is free again once that apply is done
             aclock.wait_for(tr.sched.apply_gate(t), xs)
         with torch.cuda.stream(xs):
@@ -189,9 +197,15 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
                 # next exchange waits for it; asp: nothing waits for it)
                 late = ("async", "post")
                 plan = xplan(t)
+                ncomm, waited = 0, t < 1 or not early
                 for kind, fn in plan:
-                    if kind not in late:
-                        fn()
+                    if kind in late:
+                        continue
+                    if kind == "compute" and ncomm == 1 and not waited:  # the resolve
+                        xs.wait_event(chain[(t - 1) % E])
+                        waited = True
+                    fn()
+                    ncomm += kind == "comm"
                 ev_x[t % E].record(xs)
                 for kind, fn in plan:
                     if kind in late:
