@@ -332,8 +332,9 @@ def main():
                          "every n-th minibatch ahead of the training step). Measured 1 GPU "
                          "ms/step: 1 -> 0.309, 2 -> 0.241, 3 -> 0.230, 4 -> 0.43; 8 emulated "
                          "peers with a communicator stream, exchange on the prep streams: "
-                         "1 -> 0.46, 2 -> 0.308, 3 -> 0.334). 0 = auto: 3 on 1 GPU, 2 with "
-                         "N > 1")
+                         "1 -> 0.46, 2 -> 0.308, 3 -> 0.334 in round 1; with the applies at the "
+                         "tail of the exchange half (round 2): 2 -> 0.162, 3 -> 0.139). 0 = "
+                         "auto: 3")
     ap.add_argument("--exchange", default="padded", choices=["padded", "exact"],
                     help="N > 1: fixed-capacity sync-free exchange, or count-sized all-to-all-v")
     ap.add_argument("--fixing-float", type=int, default=0)
@@ -449,7 +450,7 @@ def main():
         # the training step on its own stream of this priority instead of the null stream
         scope.enter_context(torch.cuda.stream(torch.cuda.Stream(device, priority=int(mprio))))
     if gpu and args.pipeline and (G == 1 or tr.padded):
-        nprep = args.prep_streams or (3 if G == 1 else 2)
+        nprep = args.prep_streams or 3
         args.prep_streams = nprep
         run, graph_used = pipeline(tr, B, N, seed, keys, labels, device, args, nprep=nprep)
     else:

@@ -46,6 +46,7 @@ def _weights(tr):
 
 @pytest.mark.parametrize("xmode,nprep,graph,kw", [
     ("prep", 2, 1, {}), ("prep", 1, 1, {}), ("own", 2, 1, {}), ("prep", 3, 0, {}),
+    ("prep", 3, 1, {}), ("prep", 3, 1, {"consistency": "ssp:2"}),
     ("prep", 2, 1, {"consistency": "ssp:1"}), ("prep", 2, 1, {"consistency": "ssp:2"}),
     ("prep", 3, 1, {"consistency": "bsp"}),
     ("prep", 2, 1, {"fixing_float_bytes": 2}), ("prep", 2, 1, {"push_mode": "aggregate"}),
