@@ -13,9 +13,9 @@ run() {
 }
 run "config 2: AdaGrad, BSP, 1e8 features, 1 GPU" --algo adagrad --consistency bsp --num-features 1e8 &&
 run "config 3: FTRL-L1, SSP 4, 1e9 features (1 GPU)" &&
-run "config 3: FTRL-L1, SSP 4, 1e9 features, 8 emulated peers" --emulate-peers 8 &&
-run "config 4: async (asp) FTRL, fixing-float 1 B + key caching, 1e9, 8 emulated peers" --consistency asp --fixing-float 1 --emulate-peers 8 &&
-run "config 4: async (asp) SGD, fixing-float 2 B + key caching, 1e9, 8 emulated peers" --algo sgd --consistency asp --fixing-float 2 --emulate-peers 8 &&
+run "config 3: FTRL-L1, SSP 4, 1e9 features, 8 emulated peers" --emulate-peers 8 --emulate-backend nccl &&
+run "config 4: async (asp) FTRL, fixing-float 1 B + key caching, 1e9, 8 emulated peers" --consistency asp --fixing-float 1 --emulate-peers 8 --emulate-backend nccl &&
+run "config 4: async (asp) SGD, fixing-float 2 B + key caching, 1e9, 8 emulated peers" --algo sgd --consistency asp --fixing-float 2 --emulate-peers 8 --emulate-backend nccl &&
 run "1e10 features (KeyMix 34 bits, u64 keys), FTRL SSP 4, 1 GPU" --num-features 1e10 &&
-run "1e10 features, 8 emulated peers" --num-features 1e10 --emulate-peers 8
+run "1e10 features, 8 emulated peers" --num-features 1e10 --emulate-peers 8 --emulate-backend nccl
 cat $out
