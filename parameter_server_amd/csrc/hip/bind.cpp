@@ -400,7 +400,7 @@ PYBIND11_MODULE(_hipops, m) {
     chk(grad, at::kFloat, "grad");
     chk(err, at::kInt, "err");
     const int64_t n = keys.numel();
-    check(psamd::tploc_supported(n, bits), "tp localisation: 2..31 key bits, n <= 10.4M");
+    check(psamd::tploc_supported(n, bits), "tp localisation: 2..34 key bits, n <= 5.2M");
     if (lc) check(local_col->numel() >= n, "local_col too small");
     const int64_t N = psamd::tploc_stride(n);
     const int64_t T = N / 8192;

@@ -1,4 +1,4 @@
-// Localisation by tile dedup + bucket partition ("tp", mixed key spaces <= 31 bits).
+// Localisation by tile dedup + bucket partition ("tp", mixed key spaces <= 34 bits).
 //
 // Reference: Localizer::countUniqIndex / remapIndex (src/util/localizer.h:69-191) sort
 // every (key, position) pair of a minibatch and rebuild a CSR with local ids.
@@ -42,6 +42,12 @@ constexpr int kThr = 1024;              // tile workgroup
 constexpr int kIt = 8;
 constexpr int kTile = kThr * kIt;       // 8192 occurrences
 constexpr int kHash = 2 * kTile;        // LDS hash slots of a tile (load <= 0.5)
+constexpr int kHB = 14;                 // log2 kHash
+// Quotient encoding of the tile hash: a key k (<= 34 bits, uniformly mixed) probes from
+// home slot k mod kHash, and the slot keeps (k >> kHB) << kDispB | displacement, which
+// with the slot index gives k back: 34-bit keys in 32-bit LDS words.
+constexpr int kDispB = 12;
+constexpr uint32_t kMaxDisp = (1u << kDispB) - 1;  // never reached at load <= 0.5
 constexpr int kMaxBk = 2048;            // buckets (tile LDS: 72 KB -> 2 workgroups per CU)
 constexpr int kMaxT = 640;              // tiles (n <= 5.2 M)
 constexpr int kBThr = 256;              // emit workgroups
@@ -111,12 +117,16 @@ __device__ __forceinline__ uint64_t tp_match_any(uint32_t v, int nbits, uint64_t
 }
 
 // ------------------------------------------------------------------------ tile
+// kQuot = false (<= 31-bit keys): the slot keeps the key itself, home tp_hash(key);
+// kQuot = true (32..34 bits): quotient encoding, home = low kHB key bits.
+template <bool kQuot>
 __global__ void __launch_bounds__(tp::kThr)
 tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift, int nbk,
                uint32_t* __restrict__ tkeys, uint16_t* __restrict__ toff,
-               int32_t* __restrict__ dcnt, uint16_t* __restrict__ rep) {
+               int32_t* __restrict__ dcnt, uint16_t* __restrict__ rep,
+               int32_t* __restrict__ err) {
   using namespace tp;
-  __shared__ uint32_t hk[kHash];    // keys; after the bucket sort: entry position
+  __shared__ uint32_t hk[kHash];    // quotient-encoded keys; after the bucket sort: entry position
   __shared__ uint32_t cnt[kMaxBk];  // per-bucket counts, then offsets
   __shared__ uint32_t lds[kThr / 64 + 1];
   const int t = threadIdx.x;
@@ -126,6 +136,7 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
   const int64_t base = (int64_t)blockIdx.x * kTile;
   uint64_t kr[kIt];
   uint16_t sl[kIt];
+  bool bad = false;
 #pragma unroll
   for (int j = 0; j < kIt; ++j) {  // all loads in flight before the LDS insert chain
     const int64_t i = base + j * kThr + t;
@@ -136,28 +147,38 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
     const int64_t i = base + j * kThr + t;
     sl[j] = 0;
     if (i < n) {
-      const uint32_t k = (uint32_t)mix_key(kr[j], m);
-      uint32_t h = tp_hash(k) & (kHash - 1);
-      for (int probe = 0; probe < kHash; ++probe) {  // <= kTile keys: a free slot exists
+      const uint64_t k = mix_key(kr[j], m);
+      const uint32_t q = kQuot ? (uint32_t)(k >> kHB) << kDispB : (uint32_t)k;
+      uint32_t h = (kQuot ? (uint32_t)k : tp_hash((uint32_t)k)) & (kHash - 1);
+      uint32_t d = 0;
+      for (; d < kMaxDisp; ++d) {  // slot h holds key k iff it holds q | d (q: kQuot = false)
+        const uint32_t want = kQuot ? q | d : q;
         const uint32_t cur = hk[h];
-        if (cur == k) break;
+        if (cur == want) break;
         if (cur == kEmpty) {
-          const uint32_t prev = atomicCAS(&hk[h], kEmpty, k);
-          if (prev == kEmpty || prev == k) break;
+          const uint32_t prev = atomicCAS(&hk[h], kEmpty, want);
+          if (prev == kEmpty || prev == want) break;
         }
         h = (h + 1) & (kHash - 1);
       }
+      bad |= d == kMaxDisp;
       sl[j] = (uint16_t)h;
     }
   }
+  if (bad && err) atomicOr(err, 2);
   __syncthreads();
-  // counting sort of the distinct keys by bucket; thread t owns slots q*kThr + t
-  constexpr int kPer = kHash / kThr;  // 32
+  // counting sort of the distinct keys by bucket (top key bits); thread t owns slots
+  // q*kThr + t. The tile keys leave as their low `shift` bits (the bucket holds the rest).
+  constexpr int kPer = kHash / kThr;  // 16
+  auto decode = [](uint32_t v, int s) -> uint64_t {
+    if (!kQuot) return v;
+    return ((uint64_t)(v >> kDispB) << kHB) | ((uint32_t)(s - (int)(v & kMaxDisp)) & (kHash - 1));
+  };
   uint32_t rr[kPer];
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
-    const uint32_t k = hk[q * kThr + t];
-    rr[q] = k != kEmpty ? atomicAdd(&cnt[k >> shift], 1u) : kEmpty;
+    const uint32_t v = hk[q * kThr + t];
+    rr[q] = v != kEmpty ? atomicAdd(&cnt[decode(v, q * kThr + t) >> shift], 1u) : kEmpty;
   }
   __syncthreads();
   // exclusive scan of the bucket counts (nbk <= kMaxBk: 2 per thread)
@@ -187,12 +208,13 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
   }
   __syncthreads();
   uint32_t* tk = tkeys + base;
+  const uint64_t smask = (1ull << shift) - 1;
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     if (rr[q] != kEmpty) {
-      const uint32_t k = hk[q * kThr + t];
+      const uint64_t k = decode(hk[q * kThr + t], q * kThr + t);
       const uint32_t pos = cnt[k >> shift] + rr[q];
-      tk[pos] = k;
+      tk[pos] = (uint32_t)(k & smask);
       rr[q] = pos;
     }
   }
@@ -388,7 +410,8 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
 // ------------------------------------------------------------------------ emit
 // Flat writes of the global outputs (bases = prefix over the earlier buckets).
 __global__ void __launch_bounds__(tp::kBThr)
-tp_emit_kernel(int nbk, const uint32_t* __restrict__ dkey, const uint16_t* __restrict__ dstart,
+tp_emit_kernel(int nbk, int shift, const uint32_t* __restrict__ dkey,
+               const uint16_t* __restrict__ dstart,
                const int32_t* __restrict__ beid, const uint32_t* __restrict__ bjp,
                const uint32_t* __restrict__ dcount, const uint32_t* __restrict__ ecount,
                int32_t* __restrict__ pos_s, int32_t* __restrict__ segid,
@@ -411,7 +434,7 @@ tp_emit_kernel(int nbk, const uint32_t* __restrict__ dkey, const uint16_t* __res
   for (uint32_t j = t; j < D; j += kBThr) {
     const int64_t u = (int64_t)ubase + j;
     if (in_range(u, u_cap)) {
-      uniq[u] = dkey[(int64_t)b * kDH + j];
+      uniq[u] = ((uint64_t)b << shift) | dkey[(int64_t)b * kDH + j];
       seg_start[u] = (int32_t)(ebase + dstart[(int64_t)b * kDH + j]);
       if (zero_a) zero_a[u] = 0.f;
     }
@@ -873,8 +896,9 @@ static TpGeom tp_geom(int64_t n, int bits) {
 int64_t tploc_stride(int64_t n) { return tp_geom(n, 31).N; }
 
 bool tploc_supported(int64_t n, int bits) {
-  return bits >= 2 && bits <= 31 && n > 0 && (n >> 11) <= 1280 &&
-         (n + tp::kTile - 1) / tp::kTile <= tp::kMaxT;
+  // <= 34 bits: quotient-encoded tile hash; bucket suffixes (bits - log2 nbk) < 32 bits
+  return bits >= 2 && bits <= 34 && n > 0 && (n >> 11) <= 1280 &&
+         (n + tp::kTile - 1) / tp::kTile <= tp::kMaxT && tp_geom(n, bits).shift <= 31;
 }
 
 static size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -908,14 +932,20 @@ void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t te
   uint32_t* bjp = (uint32_t*)take((size_t)g.nbk * tp::kECap * 4);
   uint32_t* dcount = (uint32_t*)take((size_t)g.nbk * 8);
   uint32_t* ecount = dcount + g.nbk;
-  tp_tile_kernel<<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff, dcnt,
-                                                     rep);
+  static const char* quot_env = getenv("PSAMD_TP_QUOT");  // "1": A/B the encoding at <= 31 bits
+  if (m.bits > 31 || (quot_env && quot_env[0] == '1'))
+    tp_tile_kernel<true><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
+                                                             dcnt, rep, err);
+  else
+    tp_tile_kernel<false><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
+                                                              dcnt, rep, err);
   PSAMD_HIP_CHECK(hipGetLastError());
   tp_bucket_kernel<<<(unsigned)g.nbk, tp::kBkThr, 0, st>>>(tkeys, toff, g.nbk, (int)g.T, dkey,
                                                           dstart, beid, bjp, dcount, ecount, err,
                                                           prof);
   PSAMD_HIP_CHECK(hipGetLastError());
-  tp_emit_kernel<<<(unsigned)g.nbk, tp::kBThr, 0, st>>>(g.nbk, dkey, dstart, beid, bjp, dcount,
+  tp_emit_kernel<<<(unsigned)g.nbk, tp::kBThr, 0, st>>>(g.nbk, g.shift, dkey, dstart, beid, bjp,
+                                                        dcount,
                                                         ecount, pos_s, segid, uniq, seg_start,
                                                         ent_uid, n_uniq, n_ent, grad, u_cap, g.N);
   PSAMD_HIP_CHECK(hipGetLastError());

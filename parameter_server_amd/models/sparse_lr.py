@@ -121,7 +121,7 @@ class SparseLRTrainer:
         self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
         mode = cfg.localize
         if mode == "auto":  # tile dedup + key-range buckets (Localizer falls back to sort
-            mode = "tp"     # for > 31-bit keys or > 5.2 M keys per minibatch)
+            mode = "tp"     # for > 34-bit keys or > 5.2 M keys per minibatch)
         if cfg.tail_feature_freq > 0 and mode in ("tile", "hash", "tp"):
             mode = "sort"  # the tail filter needs per-key nnz counts (seg_start over nnz)
         # local columns on demand: the fused tp forward/backward reads the entry map

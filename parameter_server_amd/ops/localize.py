@@ -89,7 +89,7 @@ class Localizer:
     positions inside a key's segment (5 launches instead of 16).
     ``check()`` raises if a bucket overflowed its LDS hash (never for mixed keys of
     realistic batches; the bucket count bounds the distinct keys per bucket).
-    ``mode="tp"`` (csrc/hip/tploc.hip, GPU, key bits <= 31, <= 10.4 M keys): LDS dedup of
+    ``mode="tp"`` (csrc/hip/tploc.hip, GPU, key bits <= 34, <= 5.2 M keys): LDS dedup of
     8192-occurrence tiles, then one workgroup per key-range bucket deduplicates the
     tile-distinct entries (a hot key is at most one entry per tile) and emits sorted
     unique keys, an entry-level CSC and local columns: 4 launches, no global atomics;
@@ -115,7 +115,8 @@ class Localizer:
             mode = "sort"
         if mode == "tile" and self.bits > 31:
             mode = "sort"
-        self.mode = mode if (self.gpu and self.bits <= 32) else "sort"
+        # (tp: up to 34-bit keys through its quotient-encoded tile hash)
+        self.mode = mode if (self.gpu and (self.bits <= 32 or mode == "tp")) else "sort"
         if self.gpu and self.mode == "tile":
             H = hipops()
             N = H.tileloc_stride(n)
@@ -232,7 +233,7 @@ class Localizer:
         """Host sync: raise if a "part" localisation overflowed a bucket's LDS hash."""
         if getattr(self, "err", None) is not None and self.mode in ("part", "tp") and \
                 int(self.err.item()):
-            raise RuntimeError(f"localize_{self.mode}: a bucket overflowed its LDS capacity")
+            raise RuntimeError(f"localize_{self.mode}: a bucket or tile overflowed its LDS capacity")
 
     def __call__(self, keys: torch.Tensor) -> Localized:
         n = keys.numel()

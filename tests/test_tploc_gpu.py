@@ -60,7 +60,8 @@ def _check(k, bits, width=39):
 
 
 @pytest.mark.parametrize("bits,n", [(30, 1), (30, 1000), (30, 100003), (20, 300000), (8, 5000),
-                                    (31, 2000000), (27, 65536 * 39), (30, 65536 * 39)])
+                                    (31, 2000000), (27, 65536 * 39), (30, 65536 * 39),
+                                    (32, 300000), (33, 100003), (34, 65536 * 39)])
 def test_tploc_matches_torch(bits, n):
     g = torch.Generator().manual_seed(n + bits)
     k = torch.randint(0, 1 << min(bits + 4, 62), (n,), generator=g, dtype=torch.int64)
@@ -88,3 +89,12 @@ def test_tploc_all_distinct():
     n = 65536 * 39
     k = torch.randperm(1 << 22)[:n].to(torch.int64) * 97 + 11
     _check(k, 30)
+
+
+def test_tploc_34bit_criteo_1e10():
+    """10^10 hashed features = 34-bit mixed keys: the quotient-encoded tile hash keeps
+    them in 32-bit LDS words; the buckets hold the top bits."""
+    from parameter_server_amd.ops.synthetic import criteo_batch
+
+    keys, _ = criteo_batch(65536, seed=5, row0=0, num_features=10 ** 10, device=DEV)
+    _check(keys.cpu(), 34)
