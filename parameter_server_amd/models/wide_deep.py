@@ -422,7 +422,9 @@ class WideDeepTrainer(EmbeddingPS):
                self.dw_head, self.db_head, self.metrics, self.hist, AUC_BINS,
                db_h=self.db[L - 1])
         # ---------------- MLP backward: ReLU masks and the bias gradient of the
-        # layer below fused into the dX GEMMs (grads zeroed at the step start)
+        # layer below fused into the dX GEMMs (grads zeroed at the step start, so the
+        # weight-gradient GEMMs accumulate with beta 1: no zeroing pass of their own,
+        # which on the side stream waited ~128 us for CUs behind the dX GEMM)
         # The weight gradient of layer i and the input gradient of layer i both read
         # dH only, so on the GPU the weight gradients run on a side stream next to the
         # input-gradient chain and the sparse push (GEMMs that each use part of the
@@ -433,11 +435,12 @@ class WideDeepTrainer(EmbeddingPS):
             if side is not None:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
-                    GM.linear_weight_grad(dH, acts[i], out=self.dW[i], backend=cfg.gemm)
+                    GM.linear_weight_grad(dH, acts[i], out=self.dW[i], beta=1.0,
+                                          backend=cfg.gemm)
                 dH.record_stream(side)
                 acts[i].record_stream(side)
             else:
-                GM.linear_weight_grad(dH, acts[i], out=self.dW[i], backend=cfg.gemm)
+                GM.linear_weight_grad(dH, acts[i], out=self.dW[i], beta=1.0, backend=cfg.gemm)
             mask = acts[i] if i > 0 else None
             dH = GM.linear_input_grad(dH, self.W16[i], mask=mask, backend=cfg.gemm,
                                       colsum=self.db[i - 1] if i > 0 else None)

@@ -142,6 +142,8 @@ def linear_weight_grad(dZ, X, out=None, beta: float = 0.0, backend: str = "mfma"
         r = torch.mm(dZ.t(), X, out_dtype=torch.float32)
         if beta == 0.0:
             out.copy_(r)
+        elif beta == 1.0:
+            out.add_(r)
         else:
             out.mul_(beta).add_(r)
         return out
