@@ -19,7 +19,7 @@ import torch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--localize", default="part", choices=("sort", "part"))
+    ap.add_argument("--localize", default="sort", choices=("sort", "part"))
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--minibatch", type=int, default=16384)
     ap.add_argument("--num-features", type=float, default=1e9)

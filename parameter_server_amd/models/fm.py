@@ -57,9 +57,11 @@ class FMConfig:
     exchange_slack: float = 1.5
     exchange_capacity: int = 0
     compact_rows: bool = True            # 1 GPU: gather each unique key's row once per step
-    # GPU key localisation (ops/localize.py): "part" = partition + per-bucket LDS dedup
-    # (B = 65536: 0.563 vs 0.587 ms / step with the radix sort, profiles/r2_asp_tail.log)
-    localize: str = "part"
+    # GPU key localisation (ops/localize.py): "sort" (deterministic order inside a key's
+    # occurrence segment, so bitwise-reproducible gradient sums) or "part" (partition +
+    # per-bucket LDS dedup, run order inside a segment set by atomics; B = 65536: 0.563
+    # vs 0.587 ms / step, profiles/r2_asp_tail.log)
+    localize: str = "sort"
     seed: int = 0
 
 

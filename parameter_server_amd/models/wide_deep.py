@@ -61,7 +61,7 @@ class WideDeepConfig:
     exchange: str = "padded"             # G > 1 on GPU: sync-free fixed rows | "exact"
     exchange_slack: float = 1.5          # padded row capacity = slack x first max + 1024
     exchange_capacity: int = 0           # explicit per-peer capacity (0 = from slack)
-    localize: str = "sort"               # GPU key localisation: "sort" | "part" (ops/localize.py)
+    localize: str = "sort"               # GPU key localisation: "sort" (deterministic) | "part"
     seed: int = 0
 
 
