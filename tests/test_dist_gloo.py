@@ -157,14 +157,19 @@ def test_padded_exchange_overflow_is_loud(tmp_path):
         _run(tmp_path, cfg_kw, steps=2)
 
 
-@pytest.mark.parametrize("tau,world,ff", [(1, 2, 0), (2, 2, 0), (4, 2, 0), (1, 3, 0), (2, 3, 0),
-                                           (4, 3, 0), (4, 2, 3)])
-def test_ssp_exchange_matches_stale_reference(tmp_path, tau, world, ff):
+@pytest.mark.parametrize("tau,world,ff,apply", [(1, 2, 0, "post"), (2, 2, 0, "post"),
+                                                 (4, 2, 0, "post"), (1, 3, 0, "post"),
+                                                 (2, 3, 0, "post"), (4, 3, 0, "post"),
+                                                 (4, 2, 3, "post"), (2, 2, 0, "pre"),
+                                                 (4, 3, 0, "pre")])
+def test_ssp_exchange_matches_stale_reference(tmp_path, tau, world, ff, apply):
     """consistency ssp:tau -> the pull of step s sees exactly the pushes of steps
-    <= s-1-tau (ring of tau+1 exchange buffers)."""
+    <= s-1-tau (ring of tau+1 exchange buffers), with the owner applying the carried
+    pushes after (post: exchange t carries step t-tau) or before (pre: step t-1-tau)
+    resolving the pulls."""
     steps = 7
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
-                  consistency=f"ssp:{tau}", fixing_float_bytes=ff)
+                  consistency=f"ssp:{tau}", fixing_float_bytes=ff, ssp_apply=apply)
     res = _run(tmp_path, cfg_kw, steps=steps, world=world)
     merged = {}
     for r in res:
