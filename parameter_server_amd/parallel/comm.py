@@ -17,6 +17,19 @@ import torch.distributed as dist
 from ..utils.trace import count_traffic
 
 
+def nccl_options():
+    """ProcessGroupNCCL options: collectives on a HIGH-priority stream
+    (PSAMD_NCCL_HIGH_PRIO=0 turns it off). Every rank's all-to-all kernel then gets
+    its CUs ahead of the preparation kernels on the other streams, so a rank that is
+    busy preparing minibatches does not hold its peers' spinning RCCL kernels back."""
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+    except (AttributeError, RuntimeError):
+        return None
+    opts.is_high_priority_stream = os.environ.get("PSAMD_NCCL_HIGH_PRIO", "1") != "0"
+    return opts
+
+
 class _Done:
     def wait(self):
         return True
@@ -156,7 +169,8 @@ def nccl_loopback(world: int, device) -> LoopbackComm:
             with socket.socket() as s:
                 s.bind(("127.0.0.1", 0))
                 os.environ["MASTER_PORT"] = str(s.getsockname()[1])
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(device))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(device),
+                                pg_options=nccl_options())
     return LoopbackComm(world, device, comm_stream=False, group=dist.group.WORLD)
 
 
@@ -307,5 +321,6 @@ def init_from_env(device_type: str = "cuda", backend: str | None = None):
         kw = {}
         if backend == "nccl":
             kw["device_id"] = device
+            kw["pg_options"] = nccl_options()
         dist.init_process_group(backend=backend, **kw)
     return DistComm(device), device
