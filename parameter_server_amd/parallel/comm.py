@@ -21,7 +21,10 @@ def nccl_options():
     """ProcessGroupNCCL options: collectives on a HIGH-priority stream
     (PSAMD_NCCL_HIGH_PRIO=0 turns it off). Every rank's all-to-all kernel then gets
     its CUs ahead of the preparation kernels on the other streams, so a rank that is
-    busy preparing minibatches does not hold its peers' spinning RCCL kernels back."""
+    busy preparing minibatches does not hold its peers' spinning RCCL kernels back.
+    The 1-rank loopback cannot show that (no peer waits): 8 emulated peers measured
+    0.140-0.147 ms/step with it, 0.139-0.140 without; the real multi-GPU effect is
+    unmeasured on a 1-GPU box."""
     try:
         opts = dist.ProcessGroupNCCL.Options()
     except (AttributeError, RuntimeError):
