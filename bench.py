@@ -125,7 +125,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
     # carries (t + xd - 1 - lag, or t + xd - lag with post applies) issued and the
     # preparation of t + xd (xd <= nprep)
     post = tr.padded and tr.sched.post
-    xd = min(nprep, 2, tr.lag if post else tr.lag + 1) if split else 0
+    xd_cap = int(os.environ.get("PSAMD_XD", "2"))  # exchanges issued ahead (A/B knob)
+    xd = min(nprep, xd_cap, tr.lag if post else tr.lag + 1) if split else 0
     E = 64  # event rings, indexed by step (every look-back here is < 64 steps)
     ev_buf = [torch.cuda.Event() for _ in range(NB)]   # worker done with buffer b
     ev_w = [torch.cuda.Event() for _ in range(E)]      # worker half of step t done
