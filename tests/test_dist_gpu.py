@@ -81,11 +81,13 @@ def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes, pipelined, 
     assert max(abs(merged[k] - ref[k]) for k in ref) < tol
 
 
-@pytest.mark.parametrize("exchange", ["padded", "exact"])
-def test_bench_two_rank_rehearsal_json(tmp_path, exchange):
+@pytest.mark.parametrize("exchange,consistency", [("padded", "ssp:4"), ("exact", "ssp:4"),
+                                                  ("padded", "ssp:1"), ("padded", "asp")])
+def test_bench_two_rank_rehearsal_json(tmp_path, exchange, consistency):
     """bench.py's multi-GPU path (padded: graph-replayed compute segments around the
-    exchanges; exact: pipelined count-sized exchange) under torchrun, 2 ranks on one
-    GPU over gloo; checks the one-line JSON contract."""
+    exchanges, post / tail owner applies; exact: pipelined count-sized exchange) under
+    torchrun, 2 ranks on one GPU over gloo (every rank must issue its collectives in
+    the same order, or the run hangs); checks the one-line JSON contract."""
     import json
     import subprocess
 
@@ -94,7 +96,7 @@ def test_bench_two_rank_rehearsal_json(tmp_path, exchange):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus",
            "2", "--steps", "4", "--warmup", "2", "--minibatch", "4096", "--num-features", "1e8",
-           "--exchange", exchange]
+           "--exchange", exchange, "--consistency", consistency]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
