@@ -98,7 +98,7 @@ def test_darlin_gpu_criteo_shaped_with_delay():
     assert prog[-1].objective < sd.rows * np.log(2)  # better than the zero model
 
 
-def _rehearsal_worker(rank, world, port, q):
+def _rehearsal_worker(rank, world, port, q, shard="auto"):
     import os
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -115,16 +115,19 @@ def _rehearsal_worker(rank, world, port, q):
     a, b = rank * n, (rank + 1) * n
     part = SlotData(labels=sd.labels[a:b], groups={
         g: (off[a:b + 1] - off[a], k[off[a]:off[b]], None) for g, (off, k, v) in sd.groups.items()})
-    tr = DarlinTrainer(part, DarlinConfig(l1=1.0, max_pass=5, tail_freq=1, tau=1, seed=2),
-                       comm=comm, device=dev)
+    tr = DarlinTrainer(part, DarlinConfig(l1=1.0, max_pass=5, tail_freq=1, tau=1, seed=2,
+                                          shard_server=shard), comm=comm, device=dev)
     prog = tr.train()
     q.put((rank, [p.objective for p in prog], tr.w.cpu().numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_darlin_two_rank_gpu_rehearsal_matches_single():
-    """2 ranks on one GPU (gloo-staged all-reduce): same objectives as 1 rank."""
+@pytest.mark.parametrize("shard", ["auto", "on"])
+def test_darlin_two_rank_gpu_rehearsal_matches_single(shard):
+    """2 ranks on one GPU (gloo-staged all-reduce, or the sharded server: reduce-scatter,
+    owner update with NaN marks, all-gather of dw, bcd_replica): same objectives as 1
+    rank, bitwise-equal replicas."""
     import socket
 
     import torch.multiprocessing as mp
@@ -135,7 +138,7 @@ def test_darlin_two_rank_gpu_rehearsal_matches_single():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_rehearsal_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_rehearsal_worker, args=(r, 2, port, q, shard)) for r in range(2)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=300) for _ in ps], key=lambda r: r[0])
