@@ -268,6 +268,10 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
             prep(b)
         gp.append(g)
 
+    # (the all-to-alls stay eager between the graph replays. Measured and not kept:
+    # capturing them into the graphs too, 8 emulated peers over the 1-rank RCCL
+    # loopback: host issue 0.147 -> 0.089 ms/step but the step stays GPU-bound at
+    # 0.141 ms, and the process hung at exit; profiles/r2_capture_comm.log)
     def capture(plan):
         out = []
         for kind, fn in plan:  # in order: a segment may bake in buffers the previous
