@@ -119,8 +119,10 @@ __device__ __forceinline__ uint64_t tp_match_any(uint32_t v, int nbits, uint64_t
 // ------------------------------------------------------------------------ tile
 // kQuot = false (<= 31-bit keys): the slot keeps the key itself, home tp_hash(key);
 // kQuot = true (32..34 bits): quotient encoding, home = low kHB key bits.
+// (8 waves per SIMD = 2 workgroups per CU: <= 64 VGPRs. The quotient variant compiled to
+// 66 without the bound, i.e. 1 workgroup per CU: localise 90 vs 80 us.)
 template <bool kQuot>
-__global__ void __launch_bounds__(tp::kThr)
+__global__ void __launch_bounds__(tp::kThr, 8)
 tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift, int nbk,
                uint32_t* __restrict__ tkeys, uint16_t* __restrict__ toff,
                int32_t* __restrict__ dcnt, uint16_t* __restrict__ rep,
