@@ -55,41 +55,53 @@ __device__ __forceinline__ void auc_hist_block(uint32_t* __restrict__ hist, int 
                                                int64_t* __restrict__ step_counter) {
   // Exact integer AUC: 2 * area = sum_b pos_b * (2 * neg_below_b + neg_b) fits u64
   // (counts <= 2^32). Thread t owns the contiguous bins [t*kPer, t*kPer + kPer) of
-  // every stripe; all stripe loads are issued before any use (one memory latency,
-  // not one per stripe and bin), the stripes are zeroed for the next graph-replayed
-  // step, and the cross-thread prefix is a wave-shuffle scan + 4-wave combine.
+  // every stripe; the stripe loads go in batches of kBatch (one memory latency per
+  // batch), the stripes are zeroed for the next graph-replayed step, and the
+  // cross-thread prefix is a wave-shuffle scan + 4-wave combine. kBatch = 1 keeps this
+  // epilogue at 16 VGPRs of loads: with all 8 stripes in flight (128 VGPRs) it set the
+  // register count of the whole kernel it is folded into (kv_update 126 VGPRs + 16
+  // spilled, 4 waves per SIMD for every block, not just block 0; now 58, 8 waves). The
+  // 1-GPU step did not change measurably (A/B on one box, 3 runs each: 0.1301 vs 0.1288
+  // ms, within run-to-run noise): the update is bound by its random slot lines.
   constexpr int kPer = 8;  // nbins == 256 * kPer (AUC_BINS = 2048), checked on the host
   constexpr int kMaxStripes = 8;
+  constexpr int kBatch = 1;
   __shared__ unsigned long long s_w[3][4];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // blockDim.x == 256
   const int lo = t * kPer;
   uint32_t nb[kPer], pb[kPer];
 #pragma unroll
   for (int q = 0; q < kPer; ++q) nb[q] = pb[q] = 0;
-  uint4 ln[kMaxStripes][2], lp[kMaxStripes][2];
+#pragma unroll 1
+  for (int s0 = 0; s0 < kMaxStripes && s0 < hist_stripes; s0 += kBatch) {
+    uint4 ln[kBatch][2], lp[kBatch][2];
 #pragma unroll
-  for (int sp = 0; sp < kMaxStripes; ++sp) {
-    if (sp < hist_stripes) {
-      const uint4* hn = reinterpret_cast<const uint4*>(hist + (int64_t)sp * 2 * nbins + lo);
-      const uint4* hp = reinterpret_cast<const uint4*>(hist + (int64_t)sp * 2 * nbins + nbins + lo);
-      ln[sp][0] = hn[0]; ln[sp][1] = hn[1];
-      lp[sp][0] = hp[0]; lp[sp][1] = hp[1];
-    }
-  }
-#pragma unroll
-  for (int sp = 0; sp < kMaxStripes; ++sp) {
-    if (sp < hist_stripes) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        nb[4 * h + 0] += ln[sp][h].x; nb[4 * h + 1] += ln[sp][h].y;
-        nb[4 * h + 2] += ln[sp][h].z; nb[4 * h + 3] += ln[sp][h].w;
-        pb[4 * h + 0] += lp[sp][h].x; pb[4 * h + 1] += lp[sp][h].y;
-        pb[4 * h + 2] += lp[sp][h].z; pb[4 * h + 3] += lp[sp][h].w;
+    for (int b = 0; b < kBatch; ++b) {
+      const int sp = s0 + b;
+      if (sp < hist_stripes) {
+        const uint4* hn = reinterpret_cast<const uint4*>(hist + (int64_t)sp * 2 * nbins + lo);
+        const uint4* hp =
+            reinterpret_cast<const uint4*>(hist + (int64_t)sp * 2 * nbins + nbins + lo);
+        ln[b][0] = hn[0]; ln[b][1] = hn[1];
+        lp[b][0] = hp[0]; lp[b][1] = hp[1];
       }
-      uint4* zn = reinterpret_cast<uint4*>(hist + (int64_t)sp * 2 * nbins + lo);
-      uint4* zp = reinterpret_cast<uint4*>(hist + (int64_t)sp * 2 * nbins + nbins + lo);
-      const uint4 z = make_uint4(0, 0, 0, 0);
-      zn[0] = z; zn[1] = z; zp[0] = z; zp[1] = z;
+    }
+#pragma unroll
+    for (int b = 0; b < kBatch; ++b) {
+      const int sp = s0 + b;
+      if (sp < hist_stripes) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          nb[4 * h + 0] += ln[b][h].x; nb[4 * h + 1] += ln[b][h].y;
+          nb[4 * h + 2] += ln[b][h].z; nb[4 * h + 3] += ln[b][h].w;
+          pb[4 * h + 0] += lp[b][h].x; pb[4 * h + 1] += lp[b][h].y;
+          pb[4 * h + 2] += lp[b][h].z; pb[4 * h + 3] += lp[b][h].w;
+        }
+        uint4* zn = reinterpret_cast<uint4*>(hist + (int64_t)sp * 2 * nbins + lo);
+        uint4* zp = reinterpret_cast<uint4*>(hist + (int64_t)sp * 2 * nbins + nbins + lo);
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        zn[0] = z; zn[1] = z; zp[0] = z; zp[1] = z;
+      }
     }
   }
   unsigned long long neg = 0, pos = 0;
