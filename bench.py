@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -32,7 +33,7 @@ METRIC = "examples/sec (whole node) sparse LR 10^9 feats at 1/2/4/8 MI355X"
 ALGO_NAMES = {"ftrl": "FTRL-proximal", "adagrad": "proximal AdaGrad", "sgd": "proximal SGD"}
 
 
-def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
+def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     """Software pipeline over HIP streams (every piece replays from HIP graphs):
 
     * ``nprep`` preparation streams (high priority on 1 GPU): stream s generates and localises
@@ -208,6 +209,11 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
                     fn()
                     ncomm += kind == "comm"
                 ev_x[t % E].record(xs)
+                if asp and t >= 1:
+                    # push applies in exchange order: apply t-1 ran at the tail of its
+                    # own (other) preparation stream; two applies at once would race on
+                    # the hot keys' optimizer state (and on shared apply scratch)
+                    aclock.wait_for(t - 1, xs)
                 for kind, fn in plan:
                     if kind in late:
                         fn()
@@ -221,6 +227,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
 
     def iterate():
         t = state["t"]
+        if watch is not None and not graphs["on"]:
+            watch.beat("pipeline-warmup", t)
         nb = (t + nprep) % NB                 # minibatch t + nprep
         s = sides[nb % nprep]
         s.wait_event(ev_buf[nb])              # step(t + nprep - NB) done with bufs[nb]
@@ -285,6 +293,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1):
         return out
 
     for j in range(P):
+        if watch is not None:
+            watch.beat("capture", j)
         xh, wh = halves(t0 + j)
         xplans[j] = capture(xh)
         wplans[j] = capture(wh)
@@ -379,7 +389,12 @@ def main():
     from parameter_server_amd.ops.synthetic import criteo_batch
     from parameter_server_amd.parallel.comm import init_from_env
 
+    from parameter_server_amd.utils.watchdog import StallWatch, default_timeout, maybe_inject
+
+    watch = StallWatch(int(os.environ.get("RANK", "0")), default_timeout())
     comm, device = init_from_env("cpu" if args.cpu else "cuda")
+    watch.comm = comm
+    watch.beat("setup")
     if args.emulate_peers > 1 and comm.world == 1:
         from parameter_server_amd.parallel.comm import LoopbackComm, nccl_loopback
 
@@ -460,12 +475,15 @@ def main():
     if gpu and mprio is not None:
         # the training step on its own stream of this priority instead of the null stream
         scope.enter_context(torch.cuda.stream(torch.cuda.Stream(device, priority=int(mprio))))
+    watch.beat("warmup")
     if gpu and args.pipeline and (G == 1 or tr.padded):
         nprep = args.prep_streams or 3
         args.prep_streams = nprep
-        run, graph_used = pipeline(tr, B, N, seed, keys, labels, device, args, nprep=nprep)
+        run, graph_used = pipeline(tr, B, N, seed, keys, labels, device, args, nprep=nprep,
+                                   watch=watch)
     else:
-        for _ in range(max(1, args.warmup)):
+        for i in range(max(1, args.warmup)):
+            watch.beat("warmup", i)
             run()
     if gpu and G == 1 and args.graph and not args.pipeline:
         try:
@@ -487,6 +505,7 @@ def main():
             if rank == 0:
                 print(f"graph capture unavailable ({e!r}); eager", file=sys.stderr)
             run = one_step
+    watch.beat("pre-timing")
     tr.progress(reset=True)
 
     comm.barrier()
@@ -494,17 +513,22 @@ def main():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        watch.beat("timed", i)
+        maybe_inject(rank, i)
         run()
         if args.progress and rank == 0 and (i + 1) % 10 == 0:
             print(f"step {i + 1}", file=sys.stderr)
     t_issue = time.perf_counter() - t0  # host time to enqueue the K steps (CPU-bound check)
+    watch.beat("timed-drain")
     if gpu:
         torch.cuda.synchronize()
     comm.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=device if comm.world > 1 and gpu else "cpu")
+    watch.beat("report")
+    t = torch.tensor([dt, -dt], dtype=torch.float64,
+                     device=device if comm.world > 1 and gpu else "cpu")
     comm.all_reduce_(t, op="max")
-    dt = float(t.item())
+    dt, dt_min = float(t[0].item()), -float(t[1].item())
     prog = tr.progress(reset=True)
     tr.table.check_ok()
     occ, nnz = tr.table.census()
@@ -546,7 +570,16 @@ def main():
                              if tr.xc is not None else (args.exchange if G > 1 else None)),
                 "prefill_keys_per_gpu": int(args.prefill) if args.prefill > 0 else None,
             },
+            "comm": {"backend": getattr(comm, "backend", "local"),
+                     "world": comm.world,
+                     "rccl_world": (torch.distributed.get_world_size()
+                                    if torch.distributed.is_initialized()
+                                    and torch.distributed.get_backend() == "nccl" else 0),
+                     "per_rank_ms": [dt_min * 1e3, dt * 1e3],
+                     "collectives_rank0": comm.chain.n if comm.chain is not None else 0,
+                     "timeout_s": float(os.environ.get("PSAMD_COMM_TIMEOUT", "180"))},
             "train": {"loss": prog["loss"], "auc": prog["auc"], "accuracy": prog["accuracy"],
+                      "trains": bool(prog["loss"] < math.log(2)),
                       "table_occupied_rank0": occ, "nnz_w_rank0": nnz},
         }
         print(json.dumps(out), flush=True)
@@ -557,9 +590,20 @@ def main():
         trace.dump(args.trace, rank)
     import torch.distributed as dist
 
+    watch.beat("teardown")
     if dist.is_initialized():
         dist.destroy_process_group()
+    watch.stop()
 
 
 if __name__ == "__main__":
-    sys.exit(main() or 0)
+    try:
+        rc = main() or 0
+    except BaseException as e:  # name the rank / phase / step / collective that failed
+        from parameter_server_amd.utils import watchdog
+
+        w = watchdog.CURRENT
+        print(f"[psamd] FAILED {w.describe() if w is not None else ''}: {type(e).__name__}: "
+              f"{str(e)[:300]}", file=sys.stderr, flush=True)
+        raise
+    sys.exit(rc)

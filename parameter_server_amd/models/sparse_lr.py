@@ -63,6 +63,7 @@ class SparseLRConfig:
     l1: float = 10.0
     l2: float = 1.0
     grad_scale: float = 1.0
+    max_delta: float = 0.0               # per-update |dw| clip (trust region), 0 = off
     table_capacity: int = 0              # slots per shard (power of 2); 0 = auto
     table_load: float = 0.5              # auto capacity = num_features / G / load
     max_table_bytes: int = 96 << 30      # cap for the auto size (per GPU)
@@ -96,7 +97,24 @@ class SparseLRConfig:
 
     def update_rule(self) -> UpdateRule:
         return UpdateRule(self.algo, self.lr_type, self.alpha, self.beta, self.l1, self.l2,
-                          self.grad_scale)
+                          self.grad_scale, self.max_delta)
+
+
+# Per-algorithm server defaults for the pushed minibatch-SUM gradients (the reference's
+# push format, async_sgd.h:263-289). FTRL-proximal is the reference CTR online config
+# (example/linear/ctr/online_l1lr.conf: L1 10 / L2 1, DECAY alpha .01 beta 10).
+ALGO_DEFAULTS = {
+    "ftrl": dict(lr_type="decay", alpha=0.01, beta=10.0, l1=10.0, l2=1.0, grad_scale=1.0,
+                 max_delta=0.0),
+    "adagrad": dict(lr_type="decay", alpha=0.01, beta=10.0, l1=10.0, l2=1.0, grad_scale=1.0,
+                    max_delta=0.0),
+    "sgd": dict(lr_type="decay", alpha=0.01, beta=10.0, l1=10.0, l2=1.0, grad_scale=1.0,
+                max_delta=0.0),
+}
+
+
+def algo_defaults(algo: str) -> dict:
+    return dict(ALGO_DEFAULTS[algo.lower()])
 
 
 class SparseLRTrainer:

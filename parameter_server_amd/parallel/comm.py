@@ -6,9 +6,30 @@ every rank is a colocated worker + server shard and a push or pull step is ONE
 grouped all-to-all-v (``torch.distributed.all_to_all_single`` -> RCCL
 ``ncclSend/ncclRecv`` in a group, one direct xGMI link per peer pair), preceded by
 a tiny all-to-all of the per-peer element counts.
+
+Device ordering. The training pipeline issues collectives from several HIP
+streams (the exchange half of step t runs on preparation stream t % 3). A
+synchronous ProcessGroupNCCL collective launches its RCCL kernel on the CALLER's
+stream, so two collectives of the one communicator issued from two streams could
+be in flight at once, and the ranks could then pair up different operations.
+Every collective here is therefore chained on the device: it waits for the
+completion event of the previous collective of this communicator (whatever stream
+that ran on) and records its own, so the device order of the collectives is their
+host issue order on every rank. The key packs, applies and resolves around them
+still overlap freely. Asynchronous collectives (reduce-scatter / all-gather of the
+Darlin and wide-and-deep servers) run on one communicator stream inside the same
+chain.
+
+Failing fast. ``init_from_env`` sets a collective timeout (PSAMD_COMM_TIMEOUT
+seconds, default 180); a collective that a stalled or dead peer never joins
+raises (gloo) or is aborted by the ProcessGroupNCCL watchdog (RCCL), so the job
+exits non-zero instead of hanging. The reference has no such bound: a dead peer
+stalls its Executor forever (src/system/executor.cc:160-166). ``Comm.last_op``
+names the last collective issued (for bench.py's stall report).
 """
 from __future__ import annotations
 
+import datetime
 import os
 
 import torch
@@ -17,24 +38,45 @@ import torch.distributed as dist
 from ..utils.trace import count_traffic
 
 
+def comm_timeout() -> datetime.timedelta:
+    return datetime.timedelta(seconds=float(os.environ.get("PSAMD_COMM_TIMEOUT", "180")))
+
+
 def nccl_options():
-    """ProcessGroupNCCL options: collectives on a HIGH-priority stream
-    (PSAMD_NCCL_HIGH_PRIO=0 turns it off). Every rank's all-to-all kernel then gets
-    its CUs ahead of the preparation kernels on the other streams, so a rank that is
-    busy preparing minibatches does not hold its peers' spinning RCCL kernels back.
-    The 1-rank loopback cannot show that (no peer waits): 8 emulated peers measured
-    0.140-0.147 ms/step with it, 0.139-0.140 without; the real multi-GPU effect is
-    unmeasured on a 1-GPU box."""
+    """ProcessGroupNCCL options. PSAMD_NCCL_HIGH_PRIO=1 puts the communicator's
+    internal stream at high priority. Off by default: the 8-peer loopback measured
+    0.140-0.147 ms/step with it vs 0.139-0.140 without, and the collectives of the
+    data plane are synchronous (they run on the caller's stream, where the option
+    does nothing); the real multi-GPU effect is unmeasured."""
     try:
         opts = dist.ProcessGroupNCCL.Options()
     except (AttributeError, RuntimeError):
         return None
-    opts.is_high_priority_stream = os.environ.get("PSAMD_NCCL_HIGH_PRIO", "1") != "0"
+    opts.is_high_priority_stream = os.environ.get("PSAMD_NCCL_HIGH_PRIO", "0") == "1"
+    try:
+        opts._timeout = comm_timeout()
+    except (AttributeError, TypeError):
+        pass
     return opts
+
+
+_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
 
 
 class _Done:
     def wait(self):
+        return True
+
+
+class _ChainedWork:
+    """Handle of an asynchronous chained collective: ``wait()`` orders the current
+    stream after it (no host block)."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
         return True
 
 
@@ -50,9 +92,70 @@ def _a2a_equal(recv: torch.Tensor, send: torch.Tensor, group=None) -> None:
         work.wait()
 
 
+class _DeviceChain:
+    """Total device order of one communicator's collectives (see the module doc).
+    ``run(name, fn)`` runs ``fn`` (a synchronous collective on the current stream)
+    after the previous chained collective and records its completion;
+    ``run_async`` runs it on the communicator stream and returns a handle."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.on = self.device.type == "cuda"
+        self.ev = None           # completion of the last chained collective
+        self._cs = None          # communicator stream of the asynchronous collectives
+        self.n = 0
+        self.last = None
+
+    def _note(self, name):
+        self.n += 1
+        self.last = name
+
+    def run(self, name, fn):
+        self._note(name)
+        if not self.on:
+            return fn()
+        cur = torch.cuda.current_stream(self.device)
+        if self.ev is not None:
+            cur.wait_event(self.ev)
+        out = fn()
+        if self.ev is None:
+            self.ev = torch.cuda.Event()
+        # (re-recording one event is safe: a wait enqueued earlier is bound to the
+        # record that preceded it)
+        self.ev.record(cur)
+        return out
+
+    def run_async(self, name, fn, tensors=()):
+        self._note(name)
+        if not self.on:
+            fn()
+            return _Done()
+        if self._cs is None:
+            self._cs = torch.cuda.Stream(self.device)
+        cur = torch.cuda.current_stream(self.device)
+        self._cs.wait_stream(cur)
+        if self.ev is not None:
+            self._cs.wait_event(self.ev)
+        with torch.cuda.stream(self._cs):
+            fn()
+        for t in tensors:  # the caller's buffers are in use on the communicator stream
+            t.record_stream(self._cs)
+        done = torch.cuda.Event()
+        done.record(self._cs)
+        self.ev = done
+        return _ChainedWork(done)
+
+
 class Comm:
     rank = 0
     world = 1
+    chain = None
+
+    @property
+    def last_op(self) -> str:
+        """'<name> #<n>' of the last collective issued (stall diagnostics)."""
+        c = self.chain
+        return f"{c.last} #{c.n}" if c is not None and c.n else "none"
 
     def exchange_counts(self, send_counts: torch.Tensor) -> torch.Tensor:
         return send_counts.clone()
@@ -130,10 +233,12 @@ class LoopbackComm(Comm):
         # the caller's next work (so the emulation sees the same number of streams)
         self._cs = (torch.cuda.Stream(self.device) if comm_stream and self.device.type == "cuda"
                     else None)
+        # the real communicator's device chain (rehearsed on the 1-rank RCCL loopback)
+        self.chain = _DeviceChain(self.device if group is not None else "cpu")
 
     def all_to_all_fixed(self, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
         if self.group is not None:
-            _a2a_equal(recv, send, self.group)
+            self.chain.run("all_to_all_fixed", lambda: _a2a_equal(recv, send, self.group))
             return recv
         if self._cs is None:
             recv.copy_(send)
@@ -151,13 +256,13 @@ class LoopbackComm(Comm):
 
     def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
         if self.group is not None and t.is_cuda:
-            ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
-            dist.all_reduce(t, op=ops[op], group=self.group)
+            self.chain.run("all_reduce", lambda: dist.all_reduce(t, op=_OPS[op], group=self.group))
         return t
 
     def barrier(self):
         if self.group is not None:
-            dist.barrier(group=self.group, device_ids=[self.device.index or 0])
+            self.chain.run("barrier", lambda: dist.barrier(group=self.group,
+                                                           device_ids=[self.device.index or 0]))
 
 
 def nccl_loopback(world: int, device) -> LoopbackComm:
@@ -173,7 +278,7 @@ def nccl_loopback(world: int, device) -> LoopbackComm:
                 s.bind(("127.0.0.1", 0))
                 os.environ["MASTER_PORT"] = str(s.getsockname()[1])
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(device),
-                                pg_options=nccl_options())
+                                pg_options=nccl_options(), timeout=comm_timeout())
     return LoopbackComm(world, device, comm_stream=False, group=dist.group.WORLD)
 
 
@@ -188,6 +293,8 @@ class DistComm(Comm):
         self.backend = dist.get_backend(group)
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self._sent = 0
+        # device order of the collectives (RCCL on GPU tensors); gloo only counts
+        self.chain = _DeviceChain(self.device if self.backend == "nccl" else "cpu")
 
     def exchange_counts(self, send_counts: torch.Tensor) -> torch.Tensor:
         sc = send_counts.to(torch.int64)
@@ -196,7 +303,8 @@ class DistComm(Comm):
         elif self.backend == "gloo" and sc.is_cuda:
             sc = sc.cpu()
         rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc.contiguous(), group=self.group)
+        self.chain.run("exchange_counts",
+                       lambda: dist.all_to_all_single(rc, sc.contiguous(), group=self.group))
         count_traffic("all_to_all_counts", 8 * (sc.numel() - 1), 8 * (sc.numel() - 1))
         return rc
 
@@ -207,8 +315,8 @@ class DistComm(Comm):
         src = send.cpu() if staged else send
         out = torch.empty((sum(rc),) + tuple(send.shape[1:]), dtype=send.dtype,
                           device=src.device)
-        dist.all_to_all_single(out, src.contiguous(), output_split_sizes=rc,
-                               input_split_sizes=sc, group=self.group)
+        self.chain.run("all_to_all_v", lambda: dist.all_to_all_single(
+            out, src.contiguous(), output_split_sizes=rc, input_split_sizes=sc, group=self.group))
         if staged:
             out = out.to(send.device)
         row = send.element_size() * max(1, send[0:1].numel())
@@ -221,10 +329,11 @@ class DistComm(Comm):
         assert send.numel() == recv.numel() and send.numel() % self.world == 0
         if self.backend == "gloo" and send.is_cuda:  # rehearsal mode: staged through host
             out = torch.empty(recv.shape, dtype=recv.dtype)
-            dist.all_to_all_single(out, send.cpu(), group=self.group)
+            self.chain.run("all_to_all_fixed",
+                           lambda: dist.all_to_all_single(out, send.cpu(), group=self.group))
             recv.copy_(out)
         else:
-            _a2a_equal(recv, send, self.group)
+            self.chain.run("all_to_all_fixed", lambda: _a2a_equal(recv, send, self.group))
         b = send.numel() * send.element_size() * (self.world - 1) // self.world
         self._sent += b
         count_traffic("all_to_all_fixed", b, b)
@@ -237,7 +346,8 @@ class DistComm(Comm):
         elif c.is_cuda:
             c = c.cpu()
         out = torch.empty(self.world * c.numel(), dtype=torch.int64, device=c.device)
-        dist.all_gather_into_tensor(out, c, group=self.group)
+        self.chain.run("all_gather_counts",
+                       lambda: dist.all_gather_into_tensor(out, c, group=self.group))
         count_traffic("all_gather", 8 * c.numel(), 8 * c.numel() * (self.world - 1))
         out = out.reshape(self.world, -1)
         return out.cpu() if to_host else out
@@ -249,13 +359,12 @@ class DistComm(Comm):
 
     def all_reduce_(self, t: torch.Tensor, op="sum") -> torch.Tensor:
         self._count_reduce(t)
-        ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
         if self.backend == "gloo" and t.is_cuda:
             h = t.cpu()
-            dist.all_reduce(h, op=ops[op], group=self.group)
+            self.chain.run("all_reduce", lambda: dist.all_reduce(h, op=_OPS[op], group=self.group))
             t.copy_(h)
             return t
-        dist.all_reduce(t, op=ops[op], group=self.group)
+        self.chain.run("all_reduce", lambda: dist.all_reduce(t, op=_OPS[op], group=self.group))
         return t
 
     def all_reduce_async(self, t: torch.Tensor, op="sum"):
@@ -263,8 +372,10 @@ class DistComm(Comm):
             self.all_reduce_(t, op)
             return _Done()
         self._count_reduce(t)
-        ops = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
-        return dist.all_reduce(t, op=ops[op], group=self.group, async_op=True)
+        if self.backend == "gloo":
+            return dist.all_reduce(t, op=_OPS[op], group=self.group, async_op=True)
+        return self.chain.run_async(
+            "all_reduce", lambda: dist.all_reduce(t, op=_OPS[op], group=self.group), (t,))
 
     def reduce_scatter_async(self, out: torch.Tensor, inp: torch.Tensor):
         n = out.numel()
@@ -273,10 +384,12 @@ class DistComm(Comm):
         count_traffic("reduce_scatter", b, b)
         if self.backend == "gloo":  # gloo has no reduce-scatter: all-reduce, keep own chunk
             h = inp.detach().to("cpu", copy=True)
-            dist.all_reduce(h, group=self.group)
+            self.chain.run("reduce_scatter", lambda: dist.all_reduce(h, group=self.group))
             out.copy_(h[self.rank * n:(self.rank + 1) * n])
             return _Done()
-        return dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=True)
+        return self.chain.run_async(
+            "reduce_scatter", lambda: dist.reduce_scatter_tensor(out, inp, group=self.group),
+            (out, inp))
 
     def all_gather_into_async(self, out: torch.Tensor, inp: torch.Tensor):
         assert out.numel() == inp.numel() * self.world
@@ -284,21 +397,27 @@ class DistComm(Comm):
         count_traffic("all_gather", b, b)
         if self.backend == "gloo" and inp.is_cuda:  # rehearsal mode: staged through host
             h = torch.empty(out.shape, dtype=out.dtype)
-            dist.all_gather_into_tensor(h, inp.cpu(), group=self.group)
+            self.chain.run("all_gather",
+                           lambda: dist.all_gather_into_tensor(h, inp.cpu(), group=self.group))
             out.copy_(h)
             return _Done()
-        return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
+        if self.backend == "gloo":
+            return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
+        return self.chain.run_async(
+            "all_gather", lambda: dist.all_gather_into_tensor(out, inp, group=self.group),
+            (out, inp))
 
     def all_gather_obj(self, obj):
         out = [None] * self.world
-        dist.all_gather_object(out, obj, group=self.group)
+        self.chain.run("all_gather_obj", lambda: dist.all_gather_object(out, obj, group=self.group))
         return out
 
     def barrier(self):
         if self.backend == "nccl":
-            dist.barrier(group=self.group, device_ids=[self.device.index or 0])
+            self.chain.run("barrier", lambda: dist.barrier(group=self.group,
+                                                           device_ids=[self.device.index or 0]))
         else:
-            dist.barrier(group=self.group)
+            self.chain.run("barrier", lambda: dist.barrier(group=self.group))
 
     def bytes_moved(self) -> int:
         return self._sent
@@ -325,5 +444,5 @@ def init_from_env(device_type: str = "cuda", backend: str | None = None):
         if backend == "nccl":
             kw["device_id"] = device
             kw["pg_options"] = nccl_options()
-        dist.init_process_group(backend=backend, **kw)
+        dist.init_process_group(backend=backend, timeout=comm_timeout(), **kw)
     return DistComm(device), device

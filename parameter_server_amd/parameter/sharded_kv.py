@@ -24,10 +24,18 @@ MI355X design (one process per GPU, every rank = worker + server shard):
   rank order; or one optimizer step per source row in rank order for an
   ``UpdateRule`` on scalar values, ``kv_update_rows``); a pull's records come back
   with a second all-to-all and ``kvv_unpack`` scatters them to request order;
-* nothing of a call is read back on the host: C is fixed per worker (``max_keys``,
-  the most keys one call may carry, so a peer's row can never overflow), the whole
-  op runs on the worker's own HIP stream and ``push`` / ``pull`` return at once;
-  ``wait(ts)`` orders the caller's stream after the op (no host sync);
+* nothing of a call is read back on the host: a peer row holds C keys, sized to a
+  peer's SHARE of the most keys one call may carry (``max_keys``): keys are mixed
+  (KeyMix) before the range split, so a call's unique keys spread ~Binomial(U, 1/G)
+  over the owners and C = ``peer_slack`` x max_keys / G + 6 standard deviations
+  (the reference slices a message to each server's key range,
+  src/system/message.h:120-159; a fixed row of max_keys per peer would move G x the
+  live payload over xGMI). A row that would overflow keeps its first C keys and the
+  excess is counted on the device; the count is published to pinned host memory
+  (no stream sync) and the next call, ``wait``, ``flush`` or ``check`` raises on it
+  (``peer_capacity=max_keys`` makes overflow impossible). The whole op runs on the
+  worker's own HIP stream and ``push`` / ``pull`` return at once; ``wait(ts)``
+  orders the caller's stream after the op (no host sync);
 * operations are SPMD: every rank issues the same sequence of push / pull calls
   (possibly with different or empty key lists) — the RCCL analogue of the
   reference's "every worker messages every server" rounds.
@@ -35,10 +43,14 @@ MI355X design (one process per GPU, every rank = worker + server shard):
 Consistency (``consistency=`` ``"bsp"`` | ``"ssp:tau"`` | ``"asp"``): the owner keeps
 the received push rows of the last ``tau`` pushes pending and applies a push only
 when ``tau`` newer pushes have arrived, so a pull issued after the P-th push sees
-exactly the pushes 1 .. P - tau of every worker (``parallel.consistency.VectorClock``
-gates every pull: ``admissible(P)`` must hold). ``bsp`` is tau = 0. ``asp`` applies
-each push on a separate apply stream as soon as it arrives and no pull waits for it
-(a pull sees whatever has landed). ``flush()`` applies everything pending.
+exactly the pushes 1 .. P - tau of every worker. What enforces this is the SPMD
+order of the collectives: push P of every worker rides the same all-to-all, so when
+the owner applies it, it holds every worker's push P. The ``VectorClock`` records
+the applied pushes per worker for ``staleness()`` and asserts the bound; it is
+bookkeeping that the collective order makes true, not a gate that could block.
+``bsp`` is tau = 0. ``asp`` applies each push on a separate apply stream as soon as
+it arrives and no pull waits for it (a pull sees whatever has landed).
+``flush()`` applies everything pending.
 
 Key caching (reference KeyCachingFilter, src/filter/key_caching.h:6-76: the sender
 hashes a key list into a signature and, when the receiver already holds the list of
@@ -49,7 +61,7 @@ localisation on the worker and the resolved slots of every source row on the own
 slots straight into the one value all-to-all) and ``push(h, vals)`` sends key-less
 rows ``[hdr | values]``. The device key signature (``ops.fixing_float.key_signature``)
 deduplicates registrations: registering a key list whose signature every rank already
-holds returns the existing handle. Handle calls are SPMD like every other call (every
+holds, under the SAME handle on every rank, returns the existing handle. Handle calls are SPMD like every other call (every
 rank passes its handle of the same ``register_keys`` call).
 
 Server-side push semantics: ``"add"`` (KVVector PLUS, kv_vector.h:70-75),
@@ -135,7 +147,8 @@ class KVWorker:
 
     def __init__(self, comm: Comm | None = None, device="cpu", *, capacity: int = 1 << 20,
                  rule="add", key_bits: int = 64, init: InitRule | None = None, dim: int = 1,
-                 max_keys: int = 1 << 20, consistency="bsp"):
+                 max_keys: int = 1 << 20, consistency="bsp", peer_capacity: int = 0,
+                 peer_slack: float = 1.2):
         self.device = torch.device(device)
         self.comm = comm or LocalComm(self.device)
         self.G, self.rank = self.comm.world, self.comm.rank
@@ -148,9 +161,15 @@ class KVWorker:
         self.asp = math.isinf(self.tau)
         self.consistency = "asp" if self.asp else ("bsp" if self.tau == 0 else f"ssp:{int(self.tau)}")
         self.clock = VectorClock(self.G, self.tau)
-        # fixed exchange geometry: C keys per peer row = the most keys one call carries
+        # fixed exchange geometry: C keys per peer row, a peer's share of the most keys
+        # one call carries (slack x mean + 6 sigma of the binomial split), <= max_keys
         self.max_keys = int(max_keys)
-        C = (self.max_keys + 7) // 8 * 8
+        C = int(peer_capacity)
+        if C <= 0:
+            mean = self.max_keys / self.G
+            C = int(math.ceil(peer_slack * mean + 6 * math.sqrt(mean) + 64))
+        C = max(8, min(C, self.max_keys))
+        C = (C + 7) // 8 * 8
         kw = 1 if self.bits <= 32 else 2
         self.C, self.kw = C, kw
         self.Hk = (4 + C * kw + 1 + 3) // 4 * 4          # pull rows: header + keys
@@ -174,6 +193,9 @@ class KVWorker:
             self.rec_s = torch.empty(G * C * k, dtype=torch.float32, device=dev)
             self.rec_r = torch.empty(G * C * k, dtype=torch.float32, device=dev)
             self.off1 = torch.zeros(2, dtype=torch.int64, device=dev)
+            # keys dropped by a full peer row (device counter + pinned host mirror)
+            self.ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.ovf_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             # apply-side scratch (the apply stream's own under asp)
             self.a_slot = torch.empty(G * C, dtype=torch.int64, device=dev)
             self.a_w = torch.empty(G * C, dtype=torch.float32, device=dev)
@@ -184,8 +206,29 @@ class KVWorker:
                 self.nxt = torch.empty(G * C, dtype=torch.int32, device=dev)
         else:
             self.stream = self.apply_stream = None
+            self.ovf = torch.zeros(1, dtype=torch.int32)
+            self.ovf_host = self.ovf
 
     # ------------------------------------------------------------- helpers
+    def check(self, sync: bool = False) -> None:
+        """Raise if a call dropped keys because a peer row was full. The pack kernels
+        publish the device count to pinned host memory (seen once they completed);
+        ``sync=True`` waits for the worker's stream first."""
+        if sync and self.gpu:
+            self.stream.synchronize()
+        n = int(self.ovf_host[0])
+        if n:
+            raise RuntimeError(
+                f"KVWorker exchange overflow: {n} keys exceeded the per-peer row capacity "
+                f"{self.C} (max_keys {self.max_keys}, {self.G} shards); those keys were not "
+                f"pulled / pushed. Pass a larger peer_capacity (max_keys makes overflow "
+                f"impossible) or peer_slack")
+
+    def _pack_keys(self, loc, off, H, send):
+        hh = hipops()
+        hh.xchg_pack_keys(loc.uniq, loc.n_uniq, off, self.C, self.kw, H, send, self.ovf)
+        hh.xchg_publish(self.ovf, self.ovf_host)
+
     def _keys(self, keys: torch.Tensor) -> torch.Tensor:
         keys = keys.to(self.device, torch.int64).reshape(-1).contiguous()
         if keys.numel() > self.max_keys:
@@ -226,6 +269,9 @@ class KVWorker:
             return
         for p in range(self.G):
             a, b = int(off[p]), int(off[p + 1])
+            if b - a > self.C:  # full row: keep the first C keys, count the rest
+                self.ovf += b - a - self.C
+                b = a + self.C
             base = p * H
             send[base] = b - a
             ks = loc.uniq[a:b]
@@ -257,16 +303,23 @@ class KVWorker:
         of the signature: a setup call, not a per-step one)."""
         from ..ops.fixing_float import key_signature
 
+        self.check()
         keys = self._keys(keys)
         sig = key_signature(keys) if keys.numel() else 0
         old = next((h for h in self._handles
                     if h.live and h.signature == sig and h.n == keys.numel()), None)
         hit = old is not None
-        if self.G > 1:  # reuse only when every rank holds the list (SPMD geometry)
-            t = torch.tensor([1.0 if hit else 0.0], dtype=torch.float64,
+        if self.G > 1:
+            # reuse only when every rank holds the list under the SAME handle: owners
+            # apply key-less rows against the cached slots of their own handle, so a
+            # crossed match (rank A's list X is handle 0, rank B's is handle 1) would
+            # land values on the wrong keys. min(id) == max(id) >= 0 over all ranks.
+            hid = float(old.id) if hit else -1.0
+            t = torch.tensor([hid, -hid], dtype=torch.float64,
                              device=self.device if getattr(self.comm, "backend", "") == "nccl"
                              else "cpu")
-            hit = float(self.comm.all_reduce_(t, op="min").item()) > 0
+            t = self.comm.all_reduce_(t, op="max").cpu()
+            hit = float(t[0]) == -float(t[1]) and float(t[0]) >= 0
         if hit:
             return old
         h = KeyHandle(len(self._handles), keys.numel(), sig)
@@ -276,13 +329,17 @@ class KVWorker:
             self._register(keys, h)
 
         self.wait(self._run(op))
+        self.check(sync=True)  # (a setup call: a full row would break the handle for good)
         return h
 
     def release(self, h: KeyHandle) -> None:
         """Drop a registered key list's cached state (collective in effect: call it on
-        every rank with the same handle)."""
+        every rank with the same handle). Pushes of ``h`` still pending under SSP keep
+        the owner-side slots until they are applied (``_drain`` frees them then)."""
         h.live = False
-        h.loc = h.off = h.slot = h.hdr = h.rows = None
+        h.loc = h.off = None
+        if not any(e[2] is h for e in self._pending):
+            h.slot = h.hdr = h.rows = None
 
     def _register(self, keys, h: KeyHandle):
         C, H, G = self.C, self.Hk, self.G
@@ -295,7 +352,7 @@ class KVWorker:
                 hh.xchg_clear_counts(self.send_k, G, H, True, True)
             else:
                 off = self._offsets(loc)
-                hh.xchg_pack_keys(loc.uniq, loc.n_uniq, off, C, self.kw, H, self.send_k, None)
+                self._pack_keys(loc, off, H, self.send_k)
                 h.off = off.clone()
                 h.loc = (loc.local_col[:n].clone(), loc.pos_s[:n].clone(),
                          loc.seg_start[:n + 1].clone(), loc.n_uniq.clone())
@@ -326,6 +383,7 @@ class KVWorker:
         """Values of ``keys`` (any order, duplicates allowed; or a ``KeyHandle`` from
         ``register_keys``) -> timestamp; ``wait`` returns ``[n]`` (dim 1) or ``[n, dim]``
         float32 values in request order."""
+        self.check()
         if isinstance(keys, KeyHandle):
             self._check_handle(keys)
             if not self.clock.admissible(self._pushes):
@@ -355,7 +413,7 @@ class KVWorker:
                 hh.xchg_clear_counts(self.send_k, G, H, True, True)
             else:
                 off = self._offsets(loc)
-                hh.xchg_pack_keys(loc.uniq, loc.n_uniq, off, C, self.kw, H, self.send_k, None)
+                self._pack_keys(loc, off, H, self.send_k)
             self.comm.all_to_all_fixed(self.send_k, self.recv_k)
             it, iv, isd, seed = tb.init.args()
             hh.kv_resolve_rows(tb.slots, self.recv_k, H, C, self.kw, self.slot, self.w, True, it,
@@ -386,7 +444,9 @@ class KVWorker:
             if loc is not None:
                 u = loc.local_col.to(torch.int64)
                 p = torch.searchsorted(off[1:], u, right=True)
-                out = rec_r.view(G * C, k)[p * C + (u - off[p])]
+                i = u - off[p]
+                out = rec_r.view(G * C, k)[p * C + i.clamp(max=C - 1)]
+                out[i >= C] = 0.0  # dropped by a full row (counted in ovf)
         return out.reshape(-1) if k == 1 else out
 
     def _pull_cached(self, h: KeyHandle):
@@ -416,13 +476,16 @@ class KVWorker:
             if h.loc is not None:
                 u = h.loc.local_col.to(torch.int64)
                 p = torch.searchsorted(h.off[1:], u, right=True)
-                out = rec_r.view(G * C, k)[p * C + (u - h.off[p])]
+                i = u - h.off[p]
+                out = rec_r.view(G * C, k)[p * C + i.clamp(max=C - 1)]
+                out[i >= C] = 0.0
         return out.reshape(-1) if k == 1 else out
 
     def push(self, keys, vals: torch.Tensor) -> int:
         """Send ``vals`` (``[n]`` or ``[n, dim]``) for ``keys`` (or a ``KeyHandle``:
         key-less rows against the owners' cached slots); duplicates are summed before
         the server op. Returns the timestamp."""
+        self.check()
         if isinstance(keys, KeyHandle):
             self._check_handle(keys)
             h = keys
@@ -449,7 +512,7 @@ class KVWorker:
                 hh.xchg_clear_counts(self.send_p, G, H, True, True)
             else:
                 off = self._offsets(loc)
-                hh.xchg_pack_keys(loc.uniq, loc.n_uniq, off, C, self.kw, H, self.send_p, None)
+                self._pack_keys(loc, off, H, self.send_p)
                 hh.kvv_pack_vals(vals, k, loc.pos_s, loc.seg_start, loc.n_uniq, off, C, self.kw, H,
                                  self.send_p)
             recv = torch.empty(G * H, dtype=torch.int32, device=self.device)
@@ -464,6 +527,7 @@ class KVWorker:
                 u.index_add_(0, loc.local_col.to(torch.int64), vals)
                 for q in range(G):
                     a, b = int(off[q]), int(off[q + 1])
+                    b = min(b, a + C)
                     self._row_vals(send, q, H)[:b - a] = u[a:b]
             self.comm.all_to_all_fixed(send, recv)
         self._pending.append((p, recv, None))
@@ -489,6 +553,7 @@ class KVWorker:
                 u.index_add_(0, h.loc.local_col.to(torch.int64), vals)
                 for q in range(G):
                     a, b = int(h.off[q]), int(h.off[q + 1])
+                    b = min(b, a + C)
                     send[q * H] = b - a
                     send.view(torch.float32)[q * H + 4:q * H + 4 + (b - a) * k] = u[a:b].reshape(-1)
             self.comm.all_to_all_fixed(send, recv)
@@ -514,6 +579,8 @@ class KVWorker:
                 apply(recv)
             for w in range(self.G):
                 self.clock.tick(w, p)
+            if h is not None and not h.live and not any(e[2] is h for e in self._pending):
+                h.slot = h.hdr = h.rows = None  # released with pushes still pending
 
     def _apply(self, recv):
         srv, tb = self.server, self.server.table
@@ -583,7 +650,9 @@ class KVWorker:
         def op():
             self._drain(keep=0)
 
-        return self.wait(self._run(op))
+        out = self.wait(self._run(op))
+        self.check(sync=True)
+        return out
 
     def barrier(self):
         if self.gpu:

@@ -38,3 +38,26 @@ def test_bench_single_rank_unchanged():
     for k in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data"):
         assert k in r
+
+
+def test_bench_stalled_rank_fails_fast():
+    """A rank that stops joining collectives (injected sleep at timed step 1) makes the
+    job exit non-zero within the collective timeout, and the surviving ranks name
+    their rank, phase, step and last collective (no silent hang)."""
+    import time
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(PSAMD_COMM_TIMEOUT="8", PSAMD_INJECT_STALL="1:1:600")
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "3",
+                          "--steps", "4", "--warmup", "1", "--minibatch", "1024",
+                          "--num-features", "1e6"],
+                         capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    dt = time.time() - t0
+    assert out.returncode != 0
+    assert dt < 120, dt
+    assert "[psamd] FAILED rank 0: phase timed" in out.stderr or \
+        "[psamd] FAILED rank 2: phase timed" in out.stderr, out.stderr[-3000:]
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]

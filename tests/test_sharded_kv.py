@@ -225,3 +225,86 @@ def test_hello_world_gpu_app_two_ranks_cpu():
 
     vals = {int(k): float(v) for k, v in re.findall(r"rank 0: key (\d+): ([-0-9.e]+)", r.stdout)}
     assert vals == {0: 0.0, 1: 0.1, 2: 0.2, 3: 0.3, 4: 0.8, 5: 0.5}
+
+
+# ----------------------------------------------- row sizing / overflow / registration
+def test_rows_sized_to_peer_share():
+    """8 shards, 2^20 keys x 16 values per call: a peer row carries ~1/8 of the keys,
+    so the bytes on the wire of a push + pull stay within 1.5 x the live payload."""
+    from parameter_server_amd.parallel.comm import LoopbackComm
+
+    G, n, k = 8, 1 << 20, 16
+    kv = KVWorker(LoopbackComm(G), "cpu", dim=k, max_keys=n, key_bits=64, capacity=1 << 10)
+    assert kv.C < 1.25 * n / G
+    push_wire = G * kv.Hp * 4          # push rows: header + keys + values
+    pull_wire = G * kv.Hk * 4 + G * kv.C * k * 4  # request rows + value records
+    live = n * (kv.kw * 4 + k * 4) + n * (kv.kw * 4) + n * k * 4
+    assert push_wire + pull_wire <= 1.5 * live, (push_wire + pull_wire) / live
+
+
+def test_skewed_keys_overflow_raises():
+    """Keys that all mix into owner 0's range overflow its row: the excess is counted
+    and the next call fails loudly instead of silently dropping keys."""
+    from parameter_server_amd.ops.keymix import unmix
+    from parameter_server_amd.parallel.comm import LoopbackComm
+
+    G, n = 4, 4096
+    kv = KVWorker(LoopbackComm(G), "cpu", dim=1, max_keys=n, key_bits=64, capacity=1 << 14)
+    ok = unmix(torch.arange(100, dtype=torch.int64), 64)  # fits in a row
+    kv.wait(kv.push(ok, torch.ones(100)))
+    np.testing.assert_allclose(kv.wait(kv.pull(ok)).numpy(), 1.0)
+    bad = unmix(torch.arange(n, dtype=torch.int64), 64)   # all owned by shard 0
+    assert int(kv.part.owner_of(torch.arange(n, dtype=torch.int64)).max()) == 0
+    kv.wait(kv.push(bad, torch.ones(n)))
+    with pytest.raises(RuntimeError, match="overflow"):
+        kv.pull(ok)
+
+
+def _cross_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from parameter_server_amd.parallel.comm import DistComm
+
+    kv = KVWorker(DistComm("cpu"), "cpu", capacity=1 << 12, max_keys=256)
+    X = torch.arange(0, 50, dtype=torch.int64)
+    Y = torch.arange(1000, 1040, dtype=torch.int64)
+    first, second = (X, Y) if rank == 0 else (Y, X)
+    h0 = kv.register_keys(first)
+    h1 = kv.register_keys(second)
+    hx = kv.register_keys(X)  # rank 0: X is handle 0, rank 1: handle 1 -> must not reuse
+    kv.wait(kv.push(hx, torch.full((50,), float(rank + 1))))
+    got = kv.wait(kv.pull(X)).numpy()
+    torch.save({"ids": (h0.id, h1.id, hx.id), "got": got}, os.path.join(out_dir, f"x{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_crossed_registration_gets_new_handle(tmp_path):
+    port = _port()
+    mp.spawn(_cross_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    res = [torch.load(tmp_path / f"x{r}.pt", weights_only=False) for r in range(2)]
+    assert res[0]["ids"] == res[1]["ids"] == (0, 1, 2)
+    for r in res:  # every key got both ranks' pushes: 1 + 2
+        np.testing.assert_allclose(r["got"], 3.0)
+
+
+@pytest.mark.gpu
+def test_skewed_keys_overflow_raises_gpu():
+    """Device path: the pack kernel counts the dropped keys and publishes the count to
+    pinned host memory; flush() (sync) raises."""
+    from parameter_server_amd.ops.keymix import unmix
+    from parameter_server_amd.parallel.comm import LoopbackComm
+
+    G, n = 4, 4096
+    kv = KVWorker(LoopbackComm(G, "cuda"), "cuda", dim=1, max_keys=n, key_bits=64,
+                  capacity=1 << 14)
+    ok = unmix(torch.arange(100, dtype=torch.int64), 64).cuda()
+    kv.wait(kv.push(ok, torch.ones(100, device="cuda")))
+    np.testing.assert_allclose(kv.wait(kv.pull(ok)).cpu().numpy(), 1.0)
+    kv.flush()
+    bad = unmix(torch.arange(n, dtype=torch.int64), 64).cuda()
+    kv.wait(kv.push(bad, torch.ones(n, device="cuda")))
+    with pytest.raises(RuntimeError, match="overflow"):
+        kv.flush()
