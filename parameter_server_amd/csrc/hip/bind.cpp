@@ -131,7 +131,7 @@ void linear_bwd(const int32_t*, const int32_t*, int64_t, const int32_t*, int, co
                 const float*, int64_t, const float*, float*, float*, int64_t, hipStream_t);
 void auc_from_hist(uint32_t*, int, int, double*, int64_t*, hipStream_t);
 void csr_rows(const int64_t*, int64_t, int32_t*, hipStream_t);
-void criteo_set_cards(const uint32_t*);
+void criteo_set_tables(const uint32_t*, const float*);
 void criteo_gen(uint64_t, int64_t, const int64_t*, int64_t, int64_t, uint64_t, float, uint64_t*,
                 float*, hipStream_t);
 void add_i64(int64_t*, int64_t, hipStream_t);
@@ -1254,9 +1254,10 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::csr_rows(ptr<int64_t>(row_ptr), row_ptr.numel() - 1, ptr<int32_t>(rows),
                     cur_stream());
   });
-  m.def("criteo_set_cards", [](std::vector<uint32_t> cards) {
+  m.def("criteo_set_tables", [](std::vector<uint32_t> cards, std::vector<float> gauss) {
     check(cards.size() == 26, "need 26 cardinalities");
-    psamd::criteo_set_cards(cards.data());
+    check(gauss.size() == 256, "need 256 Gaussian quantiles");
+    psamd::criteo_set_tables(cards.data(), gauss.data());
   });
   m.def("add_i64", [](Tensor p, int64_t v) {
     chk(p, at::kLong, "p");

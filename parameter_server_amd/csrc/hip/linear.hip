@@ -214,20 +214,39 @@ __global__ void csr_rows_kernel(const int64_t* __restrict__ row_ptr, int64_t B,
 }
 
 // ---------------------------------------------------------------------------
-// Criteo-shaped synthetic minibatch: 13 integer slots (log-bucketised) + 26
-// categorical slots with the Criteo-Kaggle cardinalities and power-law ids,
-// hashed into [0, num_features). Labels from a planted sparse logistic model.
+// Criteo-shaped synthetic minibatch: 13 integer slots (log-bucketised counts) + 26
+// categorical slots with per-slot cardinalities and power-law ids, hashed into
+// [0, num_features). Labels from a planted sparse logistic model shared by every
+// seed (the ranks of a data-parallel job sample rows of ONE ground truth).
+//
+// Cost model (the generator runs inside every timed step): 32-bit hashes only (a
+// 64-bit multiply is 4 VALU ops on CDNA), the power-law inverse CDF on the native
+// v_log_f32 / v_exp_f32, the planted weights from a 256-entry Gaussian quantile table
+// instead of Box-Muller (no log / sqrt / cos, no divergent branch), and the key hash
+// a 32-bit bijection + multiply-shift range reduction when num_features <= 2^32.
+// ops/synthetic.py holds the bit-for-bit CPU reference (numpy f32 log2 / exp2 may
+// differ from the hardware approximations in the last ulp for a few keys).
 __constant__ uint32_t c_cards[26];
+__constant__ float c_gauss[256];  // 0.6 * Phi^-1((i + 0.5) / 256)
 
-// Planted weight of a feature: ~20 % of features carry N(0, 0.6^2) signal. The
-// transcendentals use the hardware approximations (v_log / v_sqrt / v_cos): the
-// weights only shape the labels, and a label flips only if its uniform draw lands
-// within ~1e-6 of the logistic probability.
-__device__ __forceinline__ float planted_w(uint64_t key, uint64_t seed) {
-  const uint64_t r = rng64(seed ^ 0x5bd1e995ull, key);
-  if ((r & 0xff) >= 51) return 0.f;
-  const float u1 = u01(rng64(seed, key * 2 + 7)), u2 = u01(r);
-  return 0.6f * __fsqrt_rn(-2.f * __logf(u1)) * __cosf(6.283185307f * u2);
+__host__ __device__ __forceinline__ uint32_t gen_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// uniform bits of (global row, stream s)
+__device__ __forceinline__ uint32_t gen_row_bits(uint64_t gr, uint32_t s) {
+  return gen_mix32((uint32_t)gr ^ gen_mix32((uint32_t)(gr >> 32) ^ s));
+}
+__device__ __forceinline__ float gen_u01(uint32_t x) {  // (0, 1]
+  return (float)((x >> 8) + 1u) * (1.0f / 16777216.0f);
+}
+__device__ __forceinline__ float gen_planted(uint64_t key) {  // ~20 % of keys carry signal
+  const uint32_t h = gen_mix32((uint32_t)key ^ gen_mix32((uint32_t)(key >> 32) ^ 0x5bd1e995u));
+  return (h & 0xffu) < 51u ? c_gauss[h >> 24] : 0.f;
 }
 
 // h % N without a 64-bit division: Barrett reduction with m = floor((2^64 - 1) / N);
@@ -239,23 +258,23 @@ __device__ __forceinline__ uint64_t mod_barrett(uint64_t h, uint64_t N, uint64_t
   return r;
 }
 
-// u -> feature id of slot j (j is wave-uniform at every call site, so the integer /
-// categorical branch never diverges). Integer slots: a heavy-tailed count x =
-// e^(12u) - 1 log2-bucketised, floor(2 log2(1 + x)) = floor(u * 24 log2 e) (the
-// CPU reference evaluates the same f32 product). Categorical slots: power-law id,
-// x = (cm1 * u + 1)^(1 / (1 - alpha)) with cm1 = C_j^(1 - alpha) - 1 per block.
-__device__ __forceinline__ uint64_t criteo_key(uint64_t seed, uint64_t gr, int j,
-                                               uint64_t num_features, uint64_t nf_m,
-                                               float inv_oma, float cm1) {
-  const float u = u01(rng64(seed + (uint64_t)j * 0x632be59bd9b4e019ull, gr));
-  uint64_t id;
+// uniform u -> feature id of slot j -> key. Integer slots: a heavy-tailed count
+// x = e^(12u) - 1 log2-bucketised, floor(2 log2(1 + x)) = floor(u * 24 log2 e).
+// Categorical slots: power-law id x = (cm1 u + 1)^(1 / (1 - alpha)) - 1, cm1 =
+// C_j^(1 - alpha) - 1. (j is wave-uniform at every call site: no divergence.)
+template <bool kWide>
+__device__ __forceinline__ uint64_t gen_key(float u, int j, uint64_t num_features, uint64_t nf_m,
+                                            float inv_oma, float cm1) {
+  uint32_t id;
   if (j < 13) {
-    id = (uint64_t)(u * 34.62468098f);  // 24 * log2(e)
+    id = (uint32_t)(u * 34.62468098f);
   } else {
-    const float x = powf(cm1 * u + 1.f, inv_oma);
-    uint64_t v = (uint64_t)x;
-    id = v >= 1 ? v - 1 : 0;
+    const float x = __builtin_amdgcn_exp2f(inv_oma * __builtin_amdgcn_logf(cm1 * u + 1.f));
+    const uint32_t v = (uint32_t)x;
+    id = v >= 1u ? v - 1u : 0u;
   }
+  if (!kWide)  // bijective 32-bit hash per slot, multiply-shift into [0, N), N <= 2^32
+    return ((uint64_t)gen_mix32(id + 0x9e3779b9u * (uint32_t)(j + 1)) * num_features) >> 32;
   return mod_barrett(fmix64(((uint64_t)(j + 1) << 48) ^ id), num_features, nf_m);
 }
 
@@ -265,6 +284,7 @@ __device__ __forceinline__ uint64_t criteo_key(uint64_t seed, uint64_t gr, int j
 // sums the three partial planted logits of its row and draws the label.
 constexpr int kGenRows = 64;
 constexpr int kGenThreads = 192;
+template <bool kWide>
 __global__ void __launch_bounds__(kGenThreads)
 criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_dev,
                   int64_t row_scale, int64_t B, uint64_t num_features, uint64_t nf_m,
@@ -272,22 +292,29 @@ criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_
   __shared__ uint64_t sk[kGenRows * 39];
   __shared__ float spw[3][kGenRows];
   __shared__ float s_cm1[26];
+  __shared__ uint32_t s_seed[40];  // per-slot streams + the label stream
   if (row0_dev) row0 += (*row0_dev) * row_scale;
   const int t = threadIdx.x, lane = t & 63;
   const int g = __builtin_amdgcn_readfirstlane(t >> 6);
   const float oma = 1.f - alpha, inv_oma = 1.f / oma;
   if (t < 26) s_cm1[t] = powf((float)c_cards[t], oma) - 1.f;
+  if (t < 40)
+    s_seed[t] = gen_mix32((uint32_t)seed ^
+                          gen_mix32((uint32_t)(seed >> 32) + 0x9e3779b9u * (uint32_t)(t + 1)));
   __syncthreads();
   for (int64_t rb = (int64_t)blockIdx.x * kGenRows; rb < B; rb += (int64_t)gridDim.x * kGenRows) {
     const int64_t r = rb + lane;
+    const uint64_t gr = (uint64_t)(row0 + r);
     float pw = 0.f;
     if (r < B) {
+#pragma unroll
       for (int jj = 0; jj < 13; ++jj) {
         const int j = g * 13 + jj;
-        const uint64_t key = criteo_key(seed, (uint64_t)(row0 + r), j, num_features, nf_m,
-                                        inv_oma, j >= 13 ? s_cm1[j - 13] : 0.f);
+        const float u = gen_u01(gen_row_bits(gr, s_seed[j]));
+        const uint64_t key = gen_key<kWide>(u, j, num_features, nf_m, inv_oma,
+                                            j >= 13 ? s_cm1[j - 13] : 0.f);
         sk[lane * 39 + j] = key;
-        pw += planted_w(key, seed);
+        pw += gen_planted(key);
       }
     }
     spw[g][lane] = pw;
@@ -296,9 +323,8 @@ criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_
     for (int i = t; i < nrow * 39; i += kGenThreads) keys[rb * 39 + i] = sk[i];
     if (g == 0 && r < B) {
       const float logit = -1.2f + spw[0][lane] + spw[1][lane] + spw[2][lane];
-      const float p = 1.f / (1.f + expf(-logit));
-      const float u = u01(rng64(seed ^ 0xabcdefull, (uint64_t)(row0 + r)));
-      labels[r] = u < p ? 1.f : -1.f;
+      const float p = 1.f / (1.f + __expf(-logit));
+      labels[r] = gen_u01(gen_row_bits(gr, s_seed[39])) < p ? 1.f : -1.f;
     }
     __syncthreads();
   }
@@ -345,8 +371,9 @@ void csr_rows(const int64_t* row_ptr, int64_t B, int32_t* rows, hipStream_t st) 
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void criteo_set_cards(const uint32_t* cards26) {
+void criteo_set_tables(const uint32_t* cards26, const float* gauss256) {
   PSAMD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_cards), cards26, 26 * sizeof(uint32_t)));
+  PSAMD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_gauss), gauss256, 256 * sizeof(float)));
 }
 
 void criteo_gen(uint64_t seed, int64_t row0, const int64_t* row0_dev, int64_t row_scale,
@@ -354,8 +381,13 @@ void criteo_gen(uint64_t seed, int64_t row0, const int64_t* row0_dev, int64_t ro
                 hipStream_t st) {
   const int64_t blocks = (B + kGenRows - 1) / kGenRows;
   const uint64_t nf_m = ~0ull / num_features;
-  criteo_gen_kernel<<<(unsigned)(blocks < 65535 ? blocks : 65535), kGenThreads, 0, st>>>(
-      seed, row0, row0_dev, row_scale, B, num_features, nf_m, alpha, keys, labels);
+  const unsigned grid = (unsigned)(blocks < 65535 ? blocks : 65535);
+  if (num_features <= (1ull << 32))
+    criteo_gen_kernel<false><<<grid, kGenThreads, 0, st>>>(seed, row0, row0_dev, row_scale, B,
+                                                           num_features, nf_m, alpha, keys, labels);
+  else
+    criteo_gen_kernel<true><<<grid, kGenThreads, 0, st>>>(seed, row0, row0_dev, row_scale, B,
+                                                          num_features, nf_m, alpha, keys, labels);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -14,14 +14,13 @@
 //            dedup, counting sort of the tile's distinct keys by bucket (top BB key
 //            bits) -> tkeys[tile][pos], per-tile bucket offsets toff[tile][b],
 //            rep[i] = tile entry of occurrence i (u16)
-//   dedup    one workgroup per bucket: gather the bucket's entries from every tile
+//   bucket   one workgroup per bucket: gather the bucket's entries from every tile
 //            (a key occurs at most once per tile, so a hot key is <= #tiles entries
 //            and buckets stay balanced), LDS hash -> distinct keys + entry counts,
-//            bitonic sort of the distinct keys -> dscr[b], dcount[b], ecount[b]
-//   emit     one workgroup per bucket: unique / entry bases = prefix of dcount /
-//            ecount over the earlier buckets; uniq, seg_start (over entries), and the
-//            entry CSC (pos_s = entry id, segid), ranked in tile order by one wave
-//            (deterministic); ent_uid[entry] = unique id
+//            rank sort of the distinct keys; the bucket's global unique / entry bases
+//            by a decoupled look-back over the earlier buckets' published counts;
+//            then uniq, seg_start (over entries), the entry CSC (pos_s = entry id,
+//            segid) and ent_uid[entry] = unique id, straight from LDS
 //   gather   local_col[i] = ent_uid[tile * 8192 + rep[i]]
 // Backward: per tile, LDS float accumulation of coef[row] * val into its entries
 // (psum), then a 64-lane segmented scan of psum over the entry CSC.
@@ -233,37 +232,57 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
 }
 
 // ---------------------------------------------------------------------- bucket
-// One workgroup per bucket b (a range of the mixed key space):
+// One workgroup per bucket b (a range of the mixed key space) dedups the bucket AND
+// writes its slice of the global outputs (the separate emit pass and its global round
+// trip of per-bucket key / start / entry lists are gone):
 //   gather+insert  the bucket's entries from every tile (flat: each thread locates its
 //                  entries by binary search over the per-tile run prefix and loads them
-//                  together), each key inserted into an LDS hash with an entry count;
-//                  the entry's hash slot is kept, its entry id goes straight to beid
-//   compact        occupied slots -> (key | count | slot) list
-//   rank sort      distinct keys are unique: rank = number of smaller keys (one pass
-//                  of broadcast LDS reads instead of a bitonic network of barriers)
-//   starts         exclusive prefix of the counts in key order -> dkey / dstart, and
-//                  per slot: sorted index + cursor
+//                  together; the entry ids stay in registers), each key inserted into an
+//                  LDS hash with an entry count
+//   compact        occupied slots -> (key | count | slot) list; the bucket's distinct
+//                  and entry counts are PUBLISHED for the look-back
+//   rank sort      distinct keys are unique: rank = number of smaller keys
+//   look-back      one wave derives the bucket's global bases (unique ids, entries) from
+//                  the earlier buckets' published counts (decoupled look-back: 64 status
+//                  words per step, nearest inclusive prefix ends it) and publishes its
+//                  own inclusive prefix
+//   starts         prefix of the counts in key order -> uniq, seg_start (global)
 //   assign         every entry takes the next position of its key's segment (LDS
-//                  atomic: the order inside a segment is not fixed)
+//                  atomic: the order inside a segment is not fixed) -> entry CSC
+//                  (pos_s, segid), ent_uid
+// Workgroups are dispatched in blockIdx order, so a bucket only ever waits for buckets
+// that are running or done; the spin is bounded anyway (err bit 4, no hang). The status
+// words carry an 8-bit launch epoch (device counter, advanced by the last bucket), so
+// they need no reset between launches or graph replays.
 // Per-phase shader-clock marks (prof != null) are a tuning aid
-// (benchmarks/prof_tp_phases.py): each phase of the earlier walk-based version cost
-// 1.5-6 K cycles, so phases, not work, set the time of a workgroup.
+// (benchmarks/prof_tp_phases.py).
+namespace tp {
+constexpr uint64_t kStA = 1, kStP = 2;  // status flags: aggregate / inclusive prefix
+constexpr uint32_t kStM = (1u << 27) - 1;
+}  // namespace tp
+__device__ __forceinline__ uint64_t tp_status(uint32_t ep, uint64_t flag, uint32_t d, uint32_t e) {
+  return ((uint64_t)ep << 56) | (flag << 54) | ((uint64_t)(d & tp::kStM) << 27) | (e & tp::kStM);
+}
+
 __global__ void __launch_bounds__(tp::kBkThr)
 tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbk,
-                 int T, uint32_t* __restrict__ dkey, uint16_t* __restrict__ dstart,
-                 int32_t* __restrict__ beid, uint32_t* __restrict__ bjp,
-                 uint32_t* __restrict__ dcount, uint32_t* __restrict__ ecount,
-                 int32_t* __restrict__ err, uint64_t* __restrict__ prof) {
+                 int T, int shift, uint64_t* __restrict__ status, uint32_t* __restrict__ epoch,
+                 int32_t* __restrict__ pos_s, int32_t* __restrict__ segid,
+                 uint64_t* __restrict__ uniq, int32_t* __restrict__ seg_start,
+                 int32_t* __restrict__ ent_uid, int32_t* __restrict__ n_uniq,
+                 int32_t* __restrict__ n_ent, float* __restrict__ zero_a, int64_t u_cap,
+                 int64_t e_cap, int32_t* __restrict__ err, uint64_t* __restrict__ prof) {
   using namespace tp;
 #define TP_MARK(k) \
   if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 12 + (k)] = clock64();
   TP_MARK(0)
-  // 40,932 B of LDS (<= 40 KB: 4 workgroups of 512 threads per CU)
+  // 40,944 B of LDS (<= 40 KB: 4 workgroups of 512 threads per CU)
   __shared__ uint16_t eh[kECapL];   // hash slot of every gathered entry
   __shared__ uint64_t hs[kDH];      // hash (key u32 | count u32), then the sorted list
   __shared__ uint64_t dl[kDH];      // per-tile runs (tpre / tlo, until the inserts), then
                                     // compacted (key | count << 16 | slot), then cur/jj
   __shared__ uint32_t lds[kBkThr / 64 + 1];
+  __shared__ uint32_t sb[3];        // epoch, unique base, entry base
   static_assert((kMaxT + 1) * 4 + kMaxT * 2 <= kDH * 8, "tile runs must fit in dl");
   uint32_t* tpre = reinterpret_cast<uint32_t*>(dl);                // [kMaxT + 1]
   uint16_t* tlo = reinterpret_cast<uint16_t*>(tpre + kMaxT + 1);  // [kMaxT]
@@ -272,6 +291,10 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
   uint32_t* cur = reinterpret_cast<uint32_t*>(dl);    // [kDH] per slot, after the sort
   uint16_t* jj = reinterpret_cast<uint16_t*>(cur + kDH);  // [kDH] per slot
   const int t = threadIdx.x, b = blockIdx.x;
+  if (t == 0) {
+    uint32_t ep = (__hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u) & 0xffu;
+    sb[0] = ep ? ep : 1u;
+  }
   for (int s = t; s < kDH; s += kBkThr) {
     hkey[s] = kEmpty;
     hcnt[s] = 0;
@@ -297,11 +320,11 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
   if (t == 0) tpre[T] = E;
   __syncthreads();
   TP_MARK(1)
+  const uint32_t ep = sb[0];
   const uint32_t En = E < (uint32_t)kECapL ? E : (uint32_t)kECapL;
   bool bad = E > (uint32_t)kECapL;
-  int32_t* be = beid + (int64_t)b * kECap;
   constexpr int kG = (kECapL + kBkThr - 1) / kBkThr;  // entries per thread: locate all, then load all
-  int64_t idx[kG];
+  int32_t idx[kG];
 #pragma unroll
   for (int q = 0; q < kG; ++q) {
     const uint32_t g = q * kBkThr + t;
@@ -312,7 +335,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
         const int mid = (lo + hi + 1) >> 1;
         if (tpre[mid] <= g) lo = mid; else hi = mid - 1;
       }
-      idx[q] = (int64_t)lo * kTile + tlo[lo] + (g - tpre[lo]);
+      idx[q] = lo * kTile + tlo[lo] + (int32_t)(g - tpre[lo]);
     }
   }
   uint32_t kv[kG];
@@ -322,7 +345,6 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
   for (int q = 0; q < kG; ++q) {
     if (idx[q] < 0) continue;
     const uint32_t g = q * kBkThr + t;
-    be[g] = (int32_t)idx[q];
     const uint32_t key = kv[q];
     uint32_t h = tp_hash(key) & (kDH - 1);
     bool ok = false;
@@ -358,6 +380,9 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
   }
   uint32_t D;
   uint32_t wd = tp_block_scan<kBkThr>(cc, lds, &D);
+  if (t == 0)  // publish this bucket's counts (bucket 0: they are its inclusive prefix)
+    __hip_atomic_store(&status[b], tp_status(ep, b == 0 ? kStP : kStA, D, En), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
   for (int q = 0; q < kPer; ++q)
     if (ent[q] != ~0ull) dl[wd++] = ent[q];
@@ -370,9 +395,56 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     for (uint32_t q = 0; q < D; ++q) r += dl[q] < x;
     hs[r] = x;
   }
+  // look-back (wave 0): bases = sums of the earlier buckets' counts
+  if (t < 64) {
+    const int lane = t;
+    uint32_t su = 0, se = 0;
+    if (b > 0) {
+      int j = b - 1;
+      uint32_t spins = 0;
+      while (true) {
+        const int jl = j - lane;  // lane 0 = nearest earlier bucket
+        const uint64_t st =
+            jl >= 0 ? __hip_atomic_load(&status[jl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : tp_status(ep, kStP, 0, 0);
+        const uint32_t f = (uint32_t)(st >> 56) == ep ? (uint32_t)(st >> 54) & 3u : 0u;
+        const uint64_t pm = __ballot(f == kStP), nr = __ballot(f == 0);
+        const int fp = pm ? __builtin_ctzll(pm) : 64;  // nearest inclusive prefix
+        const uint64_t need = fp >= 63 ? ~0ull : ((2ull << fp) - 1);
+        if (nr & need) {  // an earlier bucket has not published yet
+          if (++spins > (1u << 22)) {
+            if (lane == 0) atomicOr(err, 4);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        const bool inc = lane <= fp;
+        su += wave_allsum(inc ? (uint32_t)(st >> 27) & kStM : 0u);
+        se += wave_allsum(inc ? (uint32_t)st & kStM : 0u);
+        if (fp < 64) break;
+        j -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&status[b], tp_status(ep, kStP, su + D, se + En), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      sb[1] = su;
+      sb[2] = se;
+      if (b == nbk - 1) {  // every bucket has published: the launch is done with the epoch
+        const uint32_t U = su + D, Et = se + En;
+        *n_uniq = (int32_t)U;
+        *n_ent = (int32_t)Et;
+        if (in_range((int64_t)U, u_cap + 1)) seg_start[U] = (int32_t)Et;
+        __hip_atomic_store(epoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
   __syncthreads();
   TP_MARK(4)
-  // local segment starts in key order; per slot: sorted index + cursor (dl is dead)
+  const uint32_t ubase = sb[1], ebase = sb[2];
+  // segment starts in key order -> uniq / seg_start; per slot: sorted index + cursor
   uint32_t carry = 0;
   for (uint32_t j0 = 0; j0 < D; j0 += kBkThr) {
     const uint32_t j = j0 + t;
@@ -382,8 +454,12 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     const uint32_t ex = tp_block_scan<kBkThr>(cnt, lds, &tot) + carry;
     if (j < D) {
       const uint32_t slot = (uint32_t)v & 0xffffu;
-      dkey[(int64_t)b * kDH + j] = (uint32_t)(v >> 32);
-      dstart[(int64_t)b * kDH + j] = (uint16_t)ex;
+      const int64_t u = (int64_t)ubase + j;
+      if (in_range(u, u_cap)) {
+        uniq[u] = ((uint64_t)b << shift) | (uint32_t)(v >> 32);
+        seg_start[u] = (int32_t)(ebase + ex);
+        if (zero_a) zero_a[u] = 0.f;
+      }
       cur[slot] = ex;
       jj[slot] = (uint16_t)j;
     }
@@ -391,74 +467,22 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
   }
   __syncthreads();
   TP_MARK(5)
-  if (t == 0) {
-    dcount[b] = D;
-    ecount[b] = En;
-  }
-  uint32_t* bj = bjp + (int64_t)b * kECap;
-  for (uint32_t g = t; g < En; g += kBkThr) {
-    const uint32_t h = eh[g];
-    if (h == 0xffffu) {
-      bj[g] = 0xffffffffu;
-      continue;
-    }
+#pragma unroll
+  for (int q = 0; q < kG; ++q) {
+    if (idx[q] < 0) continue;
+    const uint32_t h = eh[q * kBkThr + t];
+    if (h == 0xffffu) continue;
     const uint32_t pos = atomicAdd(&cur[h], 1u);
-    bj[g] = (uint32_t)jj[h] | (pos << 16);
+    const uint32_t u = ubase + jj[h];
+    const int64_t e = (int64_t)ebase + pos;
+    if (in_range(e, e_cap)) {
+      pos_s[e] = idx[q];
+      segid[e] = (int32_t)(u + 1);
+    }
+    if (in_range((int64_t)idx[q], e_cap)) ent_uid[idx[q]] = (int32_t)u;
   }
   TP_MARK(6)
 #undef TP_MARK
-}
-
-// ------------------------------------------------------------------------ emit
-// Flat writes of the global outputs (bases = prefix over the earlier buckets).
-__global__ void __launch_bounds__(tp::kBThr)
-tp_emit_kernel(int nbk, int shift, const uint32_t* __restrict__ dkey,
-               const uint16_t* __restrict__ dstart,
-               const int32_t* __restrict__ beid, const uint32_t* __restrict__ bjp,
-               const uint32_t* __restrict__ dcount, const uint32_t* __restrict__ ecount,
-               int32_t* __restrict__ pos_s, int32_t* __restrict__ segid,
-               uint64_t* __restrict__ uniq, int32_t* __restrict__ seg_start,
-               int32_t* __restrict__ ent_uid, int32_t* __restrict__ n_uniq,
-               int32_t* __restrict__ n_ent, float* __restrict__ zero_a, int64_t u_cap,
-               int64_t e_cap) {
-  using namespace tp;
-  __shared__ uint32_t lds[2 * (kBThr / 64 + 1)];
-  const int t = threadIdx.x, b = blockIdx.x;
-  uint32_t su = 0, se = 0;
-  for (int i = t; i < b; i += kBThr) {
-    su += dcount[i];
-    se += ecount[i];
-  }
-  uint32_t ubase, ebase;
-  tp_block_scan<kBThr>(su, lds, &ubase);
-  tp_block_scan<kBThr>(se, lds + kBThr / 64 + 1, &ebase);
-  const uint32_t D = dcount[b], En = ecount[b];
-  for (uint32_t j = t; j < D; j += kBThr) {
-    const int64_t u = (int64_t)ubase + j;
-    if (in_range(u, u_cap)) {
-      uniq[u] = ((uint64_t)b << shift) | dkey[(int64_t)b * kDH + j];
-      seg_start[u] = (int32_t)(ebase + dstart[(int64_t)b * kDH + j]);
-      if (zero_a) zero_a[u] = 0.f;
-    }
-  }
-  for (uint32_t g = t; g < En; g += kBThr) {
-    const uint32_t v = bjp[(int64_t)b * kECap + g];
-    if (v == 0xffffffffu) continue;
-    const int32_t id = beid[(int64_t)b * kECap + g];
-    const uint32_t u = ubase + (v & 0xffffu);
-    const int64_t q = (int64_t)ebase + (v >> 16);
-    if (in_range(q, e_cap)) {
-      pos_s[q] = id;
-      segid[q] = (int32_t)(u + 1);
-    }
-    if (in_range((int64_t)id, e_cap)) ent_uid[id] = (int32_t)u;
-  }
-  if (b == nbk - 1 && t == 0) {
-    const uint32_t U = ubase + D, Et = ebase + En;
-    *n_uniq = (int32_t)U;
-    *n_ent = (int32_t)Et;
-    if (in_range((int64_t)U, u_cap + 1)) seg_start[U] = (int32_t)Et;
-  }
 }
 
 // ---------------------------------------------------------------------- gather
@@ -907,14 +931,13 @@ static size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 size_t tploc_temp_bytes(int64_t n, int bits) {
   const TpGeom g = tp_geom(n, bits);
-  return al16((size_t)g.N * 4)                                 // tkeys
-         + al16((size_t)g.T * (g.nbk + 1) * 2)                 // toff (u16)
-         + al16((size_t)g.nbk * tp::kDH * 4)                   // dkey
-         + al16((size_t)g.nbk * tp::kDH * 2)                   // dstart
-         + al16((size_t)g.nbk * tp::kECap * 4) * 2             // beid, bjp
-         + al16((size_t)g.nbk * 8) + 256;                      // dcount, ecount
+  return al16((size_t)g.nbk * 8 + 16)                          // look-back status + epoch
+         + al16((size_t)g.N * 4)                               // tkeys
+         + al16((size_t)g.T * (g.nbk + 1) * 2);                // toff (u16)
 }
 
+// temp's first (nbk * 8 + 16) bytes (status words + epoch) must be zero before the
+// first launch (the Python side allocates it zeroed); they need no reset afterwards
 void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
                  int32_t* dcnt, uint16_t* rep, int32_t* pos_s, int32_t* segid, uint64_t* uniq,
                  int32_t* seg_start, int32_t* ent_uid, int32_t* local_col, int32_t* n_uniq,
@@ -926,14 +949,10 @@ void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t te
   const TpGeom g = tp_geom(n, m.bits);
   char* p = (char*)temp;
   auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
+  uint64_t* status = (uint64_t*)take((size_t)g.nbk * 8 + 16);
+  uint32_t* epoch = (uint32_t*)(status + g.nbk);
   uint32_t* tkeys = (uint32_t*)take((size_t)g.N * 4);
   uint16_t* toff = (uint16_t*)take((size_t)g.T * (g.nbk + 1) * 2);
-  uint32_t* dkey = (uint32_t*)take((size_t)g.nbk * tp::kDH * 4);
-  uint16_t* dstart = (uint16_t*)take((size_t)g.nbk * tp::kDH * 2);
-  int32_t* beid = (int32_t*)take((size_t)g.nbk * tp::kECap * 4);
-  uint32_t* bjp = (uint32_t*)take((size_t)g.nbk * tp::kECap * 4);
-  uint32_t* dcount = (uint32_t*)take((size_t)g.nbk * 8);
-  uint32_t* ecount = dcount + g.nbk;
   static const char* quot_env = getenv("PSAMD_TP_QUOT");  // "1": A/B the encoding at <= 31 bits
   if (m.bits > 31 || (quot_env && quot_env[0] == '1'))
     tp_tile_kernel<true><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
@@ -942,14 +961,9 @@ void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t te
     tp_tile_kernel<false><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
                                                               dcnt, rep, err);
   PSAMD_HIP_CHECK(hipGetLastError());
-  tp_bucket_kernel<<<(unsigned)g.nbk, tp::kBkThr, 0, st>>>(tkeys, toff, g.nbk, (int)g.T, dkey,
-                                                          dstart, beid, bjp, dcount, ecount, err,
-                                                          prof);
-  PSAMD_HIP_CHECK(hipGetLastError());
-  tp_emit_kernel<<<(unsigned)g.nbk, tp::kBThr, 0, st>>>(g.nbk, g.shift, dkey, dstart, beid, bjp,
-                                                        dcount,
-                                                        ecount, pos_s, segid, uniq, seg_start,
-                                                        ent_uid, n_uniq, n_ent, grad, u_cap, g.N);
+  tp_bucket_kernel<<<(unsigned)g.nbk, tp::kBkThr, 0, st>>>(
+      tkeys, toff, g.nbk, (int)g.T, g.shift, status, epoch, pos_s, segid, uniq, seg_start, ent_uid,
+      n_uniq, n_ent, grad, u_cap, g.N, err, prof);
   PSAMD_HIP_CHECK(hipGetLastError());
   if (local_col) {  // (skipped when the fused forward reads the entry map directly)
     tp_gather_kernel<<<(unsigned)((n + 1023) / 1024), 256, 0, st>>>(rep, ent_uid, n, local_col);

@@ -192,13 +192,15 @@ class SparseLRTrainer:
         page behaviour of a large table) instead of an almost empty one. Returns the
         occupied slots afterwards. (Reference: KVStore grows its hash map with every
         new key, src/parameter/kv_store.h:37-57.)"""
-        lo, hi = self.part.range_of(self.rank)
+        from ..ops.keymix import random_keys_in_range
+
+        # the table's own key range (the loopback emulation's one rank owns all G ranges)
+        lo, hi = self.table.key_range or self.part.range_of(self.rank)
         g = torch.Generator(device=self.device).manual_seed(seed + self.rank)
         done = 0
         while done < count:
             n = min(chunk, count - done)
-            mk = torch.randint(lo, min(hi, 1 << 63), (n,), generator=g, device=self.device,
-                               dtype=torch.int64)
+            mk = random_keys_in_range(lo, hi, n, g, self.device)
             self.table.resolve(mk, insert=True, with_w=False)
             done += n
         self.table.check_ok()

@@ -160,13 +160,15 @@ class EmbeddingPS:
     def prefill(self, count: int, chunk: int = 1 << 23, seed: int = 12345) -> int:
         """Insert ``count`` random keys of this shard's mixed-key range with initialised
         rows (the populated-table regime of a long run); returns the occupied slots."""
-        lo, hi = self.part.range_of(self.rank)
+        from ..ops.keymix import random_keys_in_range
+
+        # the table's own key range (the loopback emulation's one rank owns all G ranges)
+        lo, hi = self.shard.table.key_range or self.part.range_of(self.rank)
         g = torch.Generator(device=self.device).manual_seed(seed + self.rank)
         done = 0
         while done < count:
             n = min(chunk, count - done)
-            mk = torch.randint(lo, min(hi, 1 << 63), (n,), generator=g, device=self.device,
-                               dtype=torch.int64)
+            mk = random_keys_in_range(lo, hi, n, g, self.device)
             self.shard.resolve(mk)
             done += n
         self.shard.table.check_ok()

@@ -39,3 +39,21 @@ def unmix(h: torch.Tensor, bits: int) -> torch.Tensor:
 def to_unsigned_order(x: torch.Tensor) -> torch.Tensor:
     """Map uint64-in-int64 to int64 whose signed order equals the unsigned order."""
     return x ^ torch.tensor(-(1 << 63), dtype=torch.int64, device=x.device)
+
+
+def random_keys_in_range(lo: int, hi: int, n: int, generator=None, device="cpu") -> torch.Tensor:
+    """``n`` uniform random (mixed) keys of the unsigned range [lo, hi) as int64 bit
+    patterns (the table's key format). Ranges past 2^63 (64-bit key spaces, e.g. the
+    upper shards of raw-u64 keys) are drawn as high and low 32-bit halves with
+    wrap-around int64 arithmetic instead of ``torch.randint``, which stops at 2^63."""
+    lo, hi = int(lo), int(hi)
+    span = hi - lo
+    if span <= 0:
+        raise ValueError(f"empty key range [{lo}, {hi})")
+    if hi <= (1 << 63):
+        return torch.randint(lo, hi, (n,), generator=generator, device=device, dtype=torch.int64)
+    # span > 2^32 here: offset = (h << 32) + l with h < span >> 32, l < 2^32 -> offset < span
+    h = torch.randint(0, span >> 32, (n,), generator=generator, device=device, dtype=torch.int64)
+    low = torch.randint(0, 1 << 32, (n,), generator=generator, device=device, dtype=torch.int64)
+    base = lo - (1 << 64) if lo >= (1 << 63) else lo
+    return (h << 32) + low + base

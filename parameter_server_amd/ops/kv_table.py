@@ -71,6 +71,7 @@ class KVTable:
         ORDERED home slots (see kv_table.hip home_slot) instead of hashed ones."""
         cap = next_pow2(max(64, int(capacity)))
         self.home_base, self.home_m = 0, 0
+        self.key_range = (int(key_range[0]), int(key_range[1])) if key_range is not None else None
         if key_range is not None:
             lo, hi = int(key_range[0]), int(key_range[1])
             if hi > lo:

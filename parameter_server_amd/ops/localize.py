@@ -138,7 +138,8 @@ class Localizer:
             H = hipops()
             N = H.tploc_stride(n)
             i32 = lambda k: torch.empty(k, dtype=torch.int32, device=dev)  # noqa: E731
-            self.ptemp = torch.empty(H.tploc_temp_bytes(n, self.bits), dtype=torch.uint8,
+            # zeroed once: the bucket look-back's status words + launch epoch (tploc.hip)
+            self.ptemp = torch.zeros(H.tploc_temp_bytes(n, self.bits), dtype=torch.uint8,
                                      device=dev)
             self.t_dcnt, self.t_rep = i32(N // 8192), torch.empty(n, dtype=torch.int16, device=dev)
             self.pos_s, self.segid, self.t_ent_uid = i32(N), i32(N), i32(N)

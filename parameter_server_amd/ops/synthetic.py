@@ -29,10 +29,21 @@ NUM_SLOTS = 39
 _cards_set = {}
 
 
+def gauss_table() -> list[float]:
+    """Planted-weight quantiles 0.6 * Phi^-1((i + 0.5) / 256), f32 (shared by the GPU
+    kernel, which holds them in constant memory, and the CPU reference)."""
+    import statistics
+
+    nd = statistics.NormalDist(0.0, 0.6)
+    import numpy as np
+
+    return [float(np.float32(nd.inv_cdf((i + 0.5) / 256))) for i in range(256)]
+
+
 def _set_cards(device, cards):
     key = (str(device), tuple(cards))
     if _cards_set.get(str(device)) != key:
-        hipops().criteo_set_cards([int(c) for c in cards])
+        hipops().criteo_set_tables([int(c) for c in cards], gauss_table())
         _cards_set[str(device)] = key
 
 
@@ -57,65 +68,78 @@ def criteo_batch(B: int, *, seed: int, row0: int, num_features: int, alpha: floa
 
 
 # ----------------------------------------------------------------------------- CPU path
-M64 = (1 << 64) - 1
+def _mix32(x):
+    """gen_mix32 of linear.hip on numpy uint32 arrays (wrapping arithmetic)."""
+    import numpy as np
 
-
-def _rng64(seed, idx):
-    z = (seed + 0x9E3779B97F4A7C15 * (idx + 1)) & M64
-    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
-    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
-    return z ^ (z >> 31)
-
-
-def _u01(r):
-    return ((r >> 40) + 1.0) * (1.0 / 16777216.0)
+    x = x.astype(np.uint32)
+    x ^= x >> np.uint32(16)
+    x *= np.uint32(0x7FEB352D)
+    x ^= x >> np.uint32(15)
+    x *= np.uint32(0x846CA68B)
+    x ^= x >> np.uint32(16)
+    return x
 
 
 def _fmix64(k):
-    k ^= k >> 33
-    k = (k * 0xFF51AFD7ED558CCD) & M64
-    k ^= k >> 33
-    k = (k * 0xC4CEB9FE1A85EC53) & M64
-    k ^= k >> 33
+    import numpy as np
+
+    k = k.astype(np.uint64)
+    k ^= k >> np.uint64(33)
+    k *= np.uint64(0xFF51AFD7ED558CCD)
+    k ^= k >> np.uint64(33)
+    k *= np.uint64(0xC4CEB9FE1A85EC53)
+    k ^= k >> np.uint64(33)
     return k
 
 
-def _planted_w(key, seed):
-    r = _rng64(seed ^ 0x5BD1E995, key)
-    if (r & 0xFF) >= 51:
-        return 0.0
-    u1 = _u01(_rng64(seed, key * 2 + 7))
-    u2 = _u01(r)
-    return 0.6 * math.sqrt(-2 * math.log(u1)) * math.cos(6.283185307 * u2)
-
-
 def _criteo_cpu(B, seed, row0, num_features, alpha, cards):
-    """Scalar reference generator (small B only: tests). float32 rounding of the
-    power-law inverse CDF can differ from the GPU in the last ulp for a few rows."""
+    """Vectorised reference of criteo_gen_kernel (linear.hip): same streams, hashes and
+    tables. numpy's f32 log2 / exp2 may differ from the hardware v_log / v_exp in the
+    last ulp, which moves a large power-law id (and so its key) for a few rows."""
     import numpy as np
 
-    keys = np.empty(B * NUM_SLOTS, dtype=np.uint64)
-    labels = np.empty(B, dtype=np.float32)
-    f32 = np.float32
-    for r in range(B):
-        gr = row0 + r
-        logit = -1.2
+    with np.errstate(over="ignore"):
+        u32 = np.uint32
+        gr = np.uint64(row0) + np.arange(B, dtype=np.uint64)
+        lo, hi = gr.astype(np.uint32), (gr >> np.uint64(32)).astype(np.uint32)
+        s_lo, s_hi = u32(seed & 0xFFFFFFFF), u32((seed >> 32) & 0xFFFFFFFF)
+        sj = [_mix32(np.array([s_lo], dtype=np.uint32)
+                     ^ _mix32(np.array([s_hi + u32(0x9E3779B9) * u32(j + 1)], dtype=np.uint32)))[0]
+              for j in range(40)]
+
+        def u01(j):
+            x = _mix32(lo ^ _mix32(hi ^ sj[j]))
+            return ((x >> u32(8)) + u32(1)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+
+        gauss = np.array(gauss_table(), dtype=np.float32)
+        oma = np.float32(1.0 - np.float32(alpha))
+        inv_oma = np.float32(np.float32(1.0) / oma)
+        keys = np.empty((B, NUM_SLOTS), dtype=np.uint64)
+        logit = np.full(B, np.float32(-1.2), dtype=np.float32)
+        wide = num_features > (1 << 32)
         for j in range(NUM_SLOTS):
-            u = f32(_u01(_rng64((seed + j * 0x632BE59BD9B4E019) & M64, gr)))
+            u = u01(j)
             if j < 13:
-                # floor(2 log2(1 + (e^(12u) - 1))) = floor(u * 24 log2 e), in f32 as the kernel
-                idv = int(f32(u) * f32(34.62468098))
+                idv = (u * np.float32(34.62468098)).astype(np.uint32)
             else:
-                C = f32(cards[j - 13])
-                oma = f32(1.0 - alpha)
-                x = np.power(f32((np.power(C, oma, dtype=f32) - f32(1.0)) * u + f32(1.0)),
-                             f32(1.0) / oma, dtype=f32)
-                v = int(x)
-                idv = v - 1 if v >= 1 else 0
-            key = _fmix64(((j + 1) << 48) ^ idv) % num_features
-            keys[r * NUM_SLOTS + j] = key
-            logit += _planted_w(key, seed & M64)
-        p = 1.0 / (1.0 + math.exp(-logit))
-        u = _u01(_rng64((seed ^ 0xABCDEF) & M64, gr))
-        labels[r] = 1.0 if u < p else -1.0
-    return torch.from_numpy(keys.view(np.int64).copy()), torch.from_numpy(labels)
+                cm1 = np.float32(np.power(np.float32(cards[j - 13]), oma, dtype=np.float32)
+                                 - np.float32(1.0))
+                x = np.exp2(inv_oma * np.log2(cm1 * u + np.float32(1.0), dtype=np.float32),
+                            dtype=np.float32)
+                v = x.astype(np.uint32)
+                idv = np.where(v >= 1, v - u32(1), u32(0)).astype(np.uint32)
+            if not wide:
+                h = _mix32(idv + u32(0x9E3779B9) * u32(j + 1)).astype(np.uint64)
+                key = (h * np.uint64(num_features)) >> np.uint64(32)
+            else:
+                key = _fmix64((np.uint64(j + 1) << np.uint64(48)) ^ idv.astype(np.uint64))
+                key = key % np.uint64(num_features)
+            keys[:, j] = key
+            hp = _mix32(key.astype(np.uint32) ^ _mix32((key >> np.uint64(32)).astype(np.uint32)
+                                                      ^ u32(0x5BD1E995)))
+            logit += np.where((hp & u32(0xFF)) < 51, gauss[hp >> u32(24)], np.float32(0.0))
+        p = np.float32(1.0) / (np.float32(1.0) + np.exp(-logit, dtype=np.float32))
+        labels = np.where(u01(39) < p, np.float32(1.0), np.float32(-1.0)).astype(np.float32)
+    return (torch.from_numpy(keys.reshape(-1).view(np.int64).copy()),
+            torch.from_numpy(labels))
