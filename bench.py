@@ -359,7 +359,7 @@ def main():
                          "key and applies one step (KVBufferedVector semantics; measured slower "
                          "on MI355X: device-scope atomics per entry, 0.437 vs 0.367 ms at 8 "
                          "emulated peers)")
-    ap.add_argument("--localize", default="auto", choices=["sort", "tp", "part", "tile", "hash", "bucket", "auto"])
+    ap.add_argument("--localize", default="auto", choices=["sort", "tp", "part", "auto"])
     ap.add_argument("--emulate-peers", type=int, default=0,
                     help="1 process: run the N-GPU padded step with N emulated peers over a "
                          "loopback exchange (per-GPU device cost of the N-GPU step, no "

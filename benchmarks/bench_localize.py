@@ -34,7 +34,7 @@ def t(fn, it=50):
     return s.elapsed_time(e) / it * 1e3
 
 
-for mode in os.environ.get("PSAMD_LOC_MODES", "sort,tile,hash").split(","):
+for mode in os.environ.get("PSAMD_LOC_MODES", "sort,part,tp").split(","):
     L = Localizer(B * 39, BITS, "cuda", mode=mode)
     loc = L(keys)
     us_loc = t(lambda: L(keys))

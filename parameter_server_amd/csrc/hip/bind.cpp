@@ -63,15 +63,6 @@ void fm_fwd_bwd(const void*, const void*, const int64_t*, int64_t, int64_t, cons
                 double*, uint32_t*, int, int, hipStream_t);
 void fm_l2(float*, const void*, const int64_t*, int64_t, const int32_t*, int64_t, int, float,
            hipStream_t);
-// tileloc.hip
-int64_t tileloc_stride(int64_t);
-size_t tileloc_sort_temp_bytes(int64_t);
-void localize_tile(const uint64_t*, int64_t, KeyMix, int, uint32_t*, int32_t*, uint16_t*, int32_t*,
-                   void*, size_t, uint32_t*, int32_t*, int32_t*, uint64_t*, int32_t*, int32_t*,
-                   int32_t*, int32_t*, float*, hipStream_t);
-void tile_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
-                   const float*, int64_t, float*, const int32_t*, const int32_t*, const int32_t*,
-                   float*, int64_t, hipStream_t);
 // exchange.hip
 void xchg_pack_keys(const uint64_t*, const int32_t*, int64_t, const int64_t*, int, int64_t, int,
                     int64_t, int32_t*, int32_t*, hipStream_t);
@@ -188,20 +179,6 @@ void colred_bf16(const void*, int64_t, int, const float*, float*, const float*, 
                  hipStream_t);
 void adam_update(float*, const float*, float*, float*, int64_t, float, float, float, float, float,
                  float, float, void*, hipStream_t);
-// hashloc.hip
-size_t hashloc_temp_bytes(int64_t);
-void localize_hash(const uint64_t*, int64_t, KeyMix, unsigned long long*, int32_t*, int64_t,
-                   int64_t*, void*, size_t, uint64_t*, int32_t*, int32_t*, float*, int32_t*,
-                   hipStream_t);
-void hash_backward(const int32_t*, int64_t, int, const int32_t*, const float*, const float*,
-                   int64_t, float*, const int32_t*, int64_t, hipStream_t);
-void owner_bucket(const uint64_t*, const int32_t*, int64_t, const uint64_t*, int, void*, int64_t*,
-                  uint64_t*, int32_t*, hipStream_t);
-// bucketloc.hip
-size_t bucketloc_temp_bytes(int64_t);
-void localize_bucket(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, int32_t*,
-                     uint64_t*, int32_t*, int32_t*, int32_t*, float*, float*,
-                     unsigned long long*, hipStream_t);
 // spmv.hip
 void spmv(bool, const int64_t*, const void*, int, const void*, int, int64_t, int64_t, const void*,
           int64_t, double, double, void*, int64_t, hipStream_t);
@@ -495,62 +472,6 @@ PYBIND11_MODULE(_hipops, m) {
                       hp ? (int)std::max<int64_t>(1, hist->numel() / (2 * nbins)) : 1,
                       ptr<float>(psum), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
                       ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), cur_stream());
-  });
-  // ---------------- tile-deduplicating localisation (tileloc.hip) ----------------
-  m.def("tileloc_stride", [](int64_t n) { return psamd::tileloc_stride(n); });
-  m.def("tileloc_sort_temp_bytes", [](int64_t n) { return (int64_t)psamd::tileloc_sort_temp_bytes(n); });
-  m.def("localize_tile", [](Tensor keys, int bits, int digit_bits, Tensor dkeys, Tensor dcnt,
-                            Tensor rep, Tensor n_ent, Tensor sort_temp, Tensor hs, Tensor pos_s,
-                            Tensor segid, Tensor uniq, Tensor seg_start, Tensor ent_uid,
-                            Tensor local_col, Tensor n_uniq, Tensor grad) {
-    chk(keys, at::kLong, "keys");
-    const int64_t n = keys.numel();
-    check(n > 0, "empty minibatch");
-    check(bits >= 2 && bits <= 31, "tile localisation needs 2..31 key bits");
-    const int64_t N = psamd::tileloc_stride(n);
-    const int64_t T = N / 4096;
-    for (auto* t : {&dkeys, &dcnt, &n_ent, &hs, &pos_s, &segid, &seg_start, &ent_uid, &local_col,
-                    &n_uniq})
-      chk(*t, at::kInt, "int32 buffer");
-    chk(rep, at::kShort, "rep");
-    chk(uniq, at::kLong, "uniq");
-    chk(grad, at::kFloat, "grad");
-    chk(sort_temp, at::kByte, "sort_temp");
-    check(dkeys.numel() >= N && hs.numel() >= N && pos_s.numel() >= N && segid.numel() >= N &&
-          uniq.numel() >= N && seg_start.numel() >= N + 1 && ent_uid.numel() >= N &&
-          grad.numel() >= N, "tile localisation buffers < stride");
-    check(dcnt.numel() >= T && rep.numel() >= n && local_col.numel() >= n, "tile buffers too small");
-    check((size_t)sort_temp.numel() >= psamd::tileloc_sort_temp_bytes(n), "sort_temp too small");
-    psamd::localize_tile(ptr<uint64_t>(keys), n, make_keymix(bits), digit_bits, ptr<uint32_t>(dkeys),
-                         ptr<int32_t>(dcnt), ptr<uint16_t>(rep), ptr<int32_t>(n_ent),
-                         sort_temp.data_ptr(), sort_temp.numel(), ptr<uint32_t>(hs),
-                         ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<uint64_t>(uniq),
-                         ptr<int32_t>(seg_start), ptr<int32_t>(ent_uid), ptr<int32_t>(local_col),
-                         ptr<int32_t>(n_uniq), ptr<float>(grad), cur_stream());
-  });
-  m.def("tile_backward", [](Tensor rep, Tensor dcnt, int64_t n, optional<Tensor> rows, int width,
-                            optional<Tensor> vals, Tensor coef, Tensor psum, Tensor pos_s,
-                            Tensor segid, Tensor n_ent, Tensor grad) {
-    chk(rep, at::kShort, "rep");
-    chk(dcnt, at::kInt, "dcnt");
-    chk(coef, at::kFloat, "coef");
-    chk(psum, at::kFloat, "psum");
-    chk(pos_s, at::kInt, "pos_s");
-    chk(segid, at::kInt, "segid");
-    chk(n_ent, at::kInt, "n_ent");
-    chk(grad, at::kFloat, "grad");
-    const int64_t N = psamd::tileloc_stride(n);
-    check(n > 0 && rep.numel() >= n, "rep too small");
-    check(dcnt.numel() >= N / 4096 && psum.numel() >= N && pos_s.numel() >= N &&
-          segid.numel() >= N, "tile backward buffers < stride");
-    const int32_t* r = optr<int32_t>(rows, at::kInt, "rows");
-    if (r) check(rows->numel() >= n, "rows too small");
-    else check(width > 0, "need rows or a fixed width");
-    const float* v = optr<float>(vals, at::kFloat, "vals");
-    if (v) check(vals->numel() >= n, "vals too small");
-    psamd::tile_backward(ptr<uint16_t>(rep), ptr<int32_t>(dcnt), n, r, width, v, ptr<float>(coef),
-                         coef.numel(), ptr<float>(psum), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
-                         ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), cur_stream());
   });
   // ---------------- fixed-capacity exchange (exchange.hip) ----------------
   // buffers: send/recv int32 [G * H]; row layout documented in exchange.hip
@@ -1128,46 +1049,6 @@ PYBIND11_MODULE(_hipops, m) {
                          ptr<int32_t>(n_uniq), za, zb, ptr<int32_t>(err), uniq.numel(),
                          cur_stream());
   });
-  m.def("bucketloc_temp_bytes", [](int64_t n) { return (int64_t)psamd::bucketloc_temp_bytes(n); });
-  m.def("localize_bucket", [](Tensor keys, int bits, Tensor temp, Tensor pos_s, Tensor segid,
-                              Tensor uniq, Tensor seg_start, Tensor local_col, Tensor n_uniq,
-                              optional<Tensor> zero_a, optional<Tensor> zero_b,
-                              optional<Tensor> dbg) {
-    chk(keys, at::kLong, "keys");
-    chk(temp, at::kByte, "temp");
-    chk(pos_s, at::kInt, "pos_s");
-    chk(segid, at::kInt, "segid");
-    chk(uniq, at::kLong, "uniq");
-    chk(seg_start, at::kInt, "seg_start");
-    chk(local_col, at::kInt, "local_col");
-    chk(n_uniq, at::kInt, "n_uniq");
-    const int64_t n = keys.numel();
-    check(n >= 1 && n < (int64_t)INT32_MAX, "localize_bucket: 1 <= n < 2^31");
-    check(bits >= 2 && bits <= 32, "localize_bucket needs key bits <= 32");
-    check(pos_s.numel() >= n && segid.numel() >= n && uniq.numel() >= n &&
-              seg_start.numel() >= n + 1 && local_col.numel() >= n,
-          "localize_bucket buffers too small");
-    check((size_t)temp.numel() >= psamd::bucketloc_temp_bytes(n), "localize_bucket temp too small");
-    float* za = optr<float>(zero_a, at::kFloat, "zero_a");
-    float* zb = optr<float>(zero_b, at::kFloat, "zero_b");
-    if (za) check(zero_a->numel() >= n, "zero_a too small");
-    if (zb) check(zero_b->numel() >= n, "zero_b too small");
-    psamd::localize_bucket(ptr<uint64_t>(keys), n, make_keymix(bits), temp.data_ptr(),
-                           (size_t)temp.numel(), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
-                           ptr<uint64_t>(uniq), ptr<int32_t>(seg_start), ptr<int32_t>(local_col),
-                           ptr<int32_t>(n_uniq), za, zb,
-                           optr<unsigned long long>(dbg, at::kLong, "dbg"), cur_stream());
-  }, py::arg("keys"), py::arg("bits"), py::arg("temp"), py::arg("pos_s"), py::arg("segid"),
-     py::arg("uniq"), py::arg("seg_start"), py::arg("local_col"), py::arg("n_uniq"),
-     py::arg("zero_a"), py::arg("zero_b"), py::arg("dbg") = py::none());
-  m.def("seg_counts", [](Tensor seg_start, Tensor n_uniq, Tensor counts, int sat) {
-    chk(seg_start, at::kInt, "seg_start");
-    chk(n_uniq, at::kInt, "n_uniq");
-    chk(counts, at::kByte, "counts");
-    check(seg_start.numel() >= counts.numel() + 1, "seg_start too small");
-    psamd::seg_counts(ptr<int32_t>(seg_start), ptr<int32_t>(n_uniq), counts.numel(),
-                      ptr<uint8_t>(counts), sat, cur_stream());
-  });
   m.def("owner_split", [](Tensor uniq, optional<Tensor> n_uniq, Tensor bounds, Tensor offsets) {
     chk(uniq, at::kLong, "uniq");
     chk(bounds, at::kLong, "bounds");
@@ -1534,68 +1415,6 @@ PYBIND11_MODULE(_hipops, m) {
                      (float)beta, splitk, csp, cur_stream());
   });
 
-  // ----------------------------------------------------- sort-free localisation
-  m.def("hashloc_temp_bytes", [](int64_t n) { return (int64_t)psamd::hashloc_temp_bytes(n); });
-  m.def("localize_hash", [](Tensor raw, int bits, Tensor slots, Tensor ids, Tensor epoch,
-                            Tensor temp, Tensor uniq, Tensor local_col, Tensor n_uniq,
-                            optional<Tensor> zero_a, Tensor err) {
-    chk(raw, at::kLong, "raw");
-    chk(slots, at::kLong, "slots");
-    chk(ids, at::kInt, "ids");
-    chk(epoch, at::kLong, "epoch");
-    chk(temp, at::kByte, "temp");
-    chk(uniq, at::kLong, "uniq");
-    chk(local_col, at::kInt, "local_col");
-    chk(n_uniq, at::kInt, "n_uniq");
-    chk(err, at::kInt, "err");
-    const int64_t n = raw.numel();
-    const int64_t cap = slots.numel();
-    check(bits <= 32, "localize_hash: key bits <= 32");
-    check(ids.numel() == cap && cap >= 2 * n && (cap & (cap - 1)) == 0,
-          "hash table: power-of-two capacity >= 2n, ids[cap]");
-    check(uniq.numel() >= n && local_col.numel() >= n, "outputs too small");
-    check((size_t)temp.numel() >= psamd::hashloc_temp_bytes(n), "temp too small");
-    float* za = optr<float>(zero_a, at::kFloat, "zero_a");
-    if (za) check(zero_a->numel() >= n, "zero_a too small");
-    psamd::localize_hash(ptr<uint64_t>(raw), n, make_keymix(bits),
-                         ptr<unsigned long long>(slots), ptr<int32_t>(ids), cap,
-                         ptr<int64_t>(epoch), temp.data_ptr(), (size_t)temp.numel(),
-                         ptr<uint64_t>(uniq), ptr<int32_t>(local_col), ptr<int32_t>(n_uniq), za,
-                         ptr<int32_t>(err), cur_stream());
-  });
-  m.def("owner_bucket", [](Tensor uniq, optional<Tensor> n_uniq, Tensor bounds, Tensor temp,
-                           Tensor offsets, Tensor keys_out, Tensor perm) {
-    chk(uniq, at::kLong, "uniq");
-    chk(bounds, at::kLong, "bounds");
-    chk(temp, at::kLong, "temp");
-    chk(offsets, at::kLong, "offsets");
-    chk(keys_out, at::kLong, "keys_out");
-    chk(perm, at::kInt, "perm");
-    const int G = (int)bounds.numel() - 1;
-    check(G >= 1 && G <= 64, "owner_bucket: 1..64 shards (bounds has G+1 entries)");
-    check(temp.numel() >= 128 && offsets.numel() >= G + 1, "temp[128] / offsets[G+1]");
-    check(keys_out.numel() >= uniq.numel() && perm.numel() >= uniq.numel(), "outputs too small");
-    psamd::owner_bucket(ptr<uint64_t>(uniq), optr<int32_t>(n_uniq, at::kInt, "n_uniq"),
-                        uniq.numel(), ptr<uint64_t>(bounds), G, temp.data_ptr(),
-                        ptr<int64_t>(offsets), ptr<uint64_t>(keys_out), ptr<int32_t>(perm),
-                        cur_stream());
-  });
-  m.def("hash_backward", [](Tensor local_col, int64_t n, int width, optional<Tensor> rows,
-                            optional<Tensor> vals, Tensor coef, Tensor grad,
-                            optional<Tensor> n_uniq) {
-    chk(local_col, at::kInt, "local_col");
-    chk(coef, at::kFloat, "coef");
-    chk(grad, at::kFloat, "grad");
-    check(local_col.numel() >= n, "local_col too small");
-    const int32_t* rp = optr<int32_t>(rows, at::kInt, "rows");
-    if (rp) check(rows->numel() >= n, "rows too small");
-    else check(width > 0 && n % width == 0, "fixed width must divide n");
-    const float* vp = optr<float>(vals, at::kFloat, "vals");
-    if (vp) check(vals->numel() >= n, "vals too small");
-    psamd::hash_backward(ptr<int32_t>(local_col), n, width, rp, vp, ptr<float>(coef),
-                         coef.numel(), ptr<float>(grad), optr<int32_t>(n_uniq, at::kInt, "n_uniq"),
-                         grad.numel(), cur_stream());
-  });
 
   // ------------------------------------------------------------- embeddings
   auto rows_check = [](const Tensor& rows, int64_t cap, int D) {

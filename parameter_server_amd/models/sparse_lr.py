@@ -78,8 +78,7 @@ class SparseLRConfig:
     consistency: str = "bsp"             # bsp | ssp:<tau> | asp
     push_mode: str = "sequential"        # sequential | aggregate
     localize: str = "auto"               # auto (= tp where supported, else sort) | tp | sort |
-                                         # tile | part | bucket | hash (tp / tile: <= 31-bit
-                                         # keys, bucket / hash / part: <= 32-bit keys)
+                                         # part (tp: <= 34-bit keys, part: <= 32-bit keys)
     fixing_float_bytes: int = 0          # 0 = off, else 1..7 bytes per pushed gradient
     # multi-GPU data plane: "padded" = fixed-capacity rows per peer with device-side
     # counts (no host sync, graph-replayable); "exact" = count exchange + sized
@@ -140,7 +139,7 @@ class SparseLRTrainer:
         mode = cfg.localize
         if mode == "auto":  # tile dedup + key-range buckets (Localizer falls back to sort
             mode = "tp"     # for > 34-bit keys or > 5.2 M keys per minibatch)
-        if cfg.tail_feature_freq > 0 and mode in ("tile", "hash", "tp"):
+        if cfg.tail_feature_freq > 0 and mode == "tp":
             mode = "sort"  # the tail filter needs per-key nnz counts (seg_start over nnz)
         # local columns on demand: the fused tp forward/backward reads the entry map
         self.localizer = Localizer(self.max_nnz, self.bits, self.device, mode=mode,
@@ -411,10 +410,9 @@ class SparseLRTrainer:
         gw = (C * nb + 3) // 4 if nb else C
         H = (4 + C * kw + gw + 3) // 4 * 4
         z32 = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
-        # the partitioned apply needs rows sorted by key (not the hashed localisers'
-        # bucket order) and an ordered home (key range -> partition)
+        # the partitioned apply needs rows sorted by key and an ordered home (key range
+        # -> partition)
         part_apply = (self.gpu and cfg.push_mode != "aggregate" and self.table.home_m != 0
-                      and not getattr(loc, "hashed", False)
                       and os.environ.get("PSAMD_OWNER_APPLY", "part") == "part")
         # ~G*C/512 partitions (~1-2 entries per thread of a 256-thread workgroup, rows
         # are ~2/3 full): a few workgroups per CU hide the chain of dependent loads each
@@ -496,8 +494,6 @@ class SparseLRTrainer:
             else:
                 off = self.part.split_sorted(kk, nk)
             return kk, ki, off, nk
-        if getattr(loc, "hashed", False):
-            return self._bucket(loc, ring) + (loc.n_uniq,)
         if self.gpu:
             off = self.xc.offs[ring] if self.xc is not None else torch.empty(
                 self.G + 1, dtype=torch.int64, device=self.device)
@@ -716,25 +712,6 @@ class SparseLRTrainer:
 
 
     # ------------------------------------------------------- fused exchange (G > 1)
-    def _bucket(self, loc, par: int = 0):
-        """Owner-group the claim-ordered unique keys of a sort-free localisation:
-        (keys in owner order, perm: owner-order position -> unique id, offsets[G+1]).
-        One buffer set per step parity (the padded exchange reads perm / off again in
-        the worker half of the step)."""
-        n = loc.uniq.numel()
-        bks = getattr(self, "_bks", None) or [None] * self.R
-        self._bks = bks
-        if bks[par] is None or bks[par][0].numel() < n:
-            dev = loc.uniq.device
-            bks[par] = (torch.empty(n, dtype=torch.int64, device=dev),
-                        torch.empty(n, dtype=torch.int32, device=dev),
-                        torch.empty(128, dtype=torch.int64, device=dev),
-                        torch.empty(self.G + 1, dtype=torch.int64, device=dev))
-        keys_out, perm, temp, off = bks[par]
-        hipops().owner_bucket(loc.uniq, loc.n_uniq, self.part.bounds_on(loc.uniq.device), temp,
-                              off, keys_out, perm)
-        return keys_out, perm, off
-
     def _exchange_fused(self, loc):
         """One step of the multi-GPU data plane with 2 all-to-alls instead of 3:
 
@@ -750,10 +727,7 @@ class SparseLRTrainer:
         G, dev = self.G, uniq.device
         kw = 1 if self.bits <= 32 else 2
         perm = None
-        if getattr(loc, "hashed", False):
-            uniq, perm, off = self._bucket(loc)
-        else:
-            off = self.part.split_sorted(uniq, n_uniq)
+        off = self.part.split_sorted(uniq, n_uniq)
         send_t = (off[1:] - off[:-1]).to(torch.int64)
         M_dev = self.comm.all_gather_counts(send_t, to_host=False)
         if self._prefetch is not None:  # overlap the next minibatch with this sync

@@ -107,15 +107,10 @@ def linear_forward(local_col, w_local, labels, *, B: int, width: int = 0, row_pt
 
 def linear_backward(loc, coef, *, B: int, width: int = 0, rows=None, vals=None, coef2=None):
     """grad[u] (and hess[u] if coef2 given) into loc.grad / loc.hess."""
-    if getattr(loc, "tile", None) is not None:  # tile-deduplicated localisation
+    if getattr(loc, "tile", None) is not None:  # tile-deduplicated ("tp") localisation
         t = loc.tile
-        bwd = hipops().tp_backward if t.size == 8192 else hipops().tile_backward
-        bwd(t.rep, t.dcnt, loc.nnz, rows, width, vals, coef, t.psum, loc.pos_s, loc.segid, t.n_ent,
-            loc.grad)
-        return loc.grad, None
-    if getattr(loc, "hashed", False):  # sort-free localisation: wave-aggregated atomics
-        hipops().hash_backward(loc.local_col, loc.nnz, width, rows, vals, coef, loc.grad,
-                               loc.n_uniq)
+        hipops().tp_backward(t.rep, t.dcnt, loc.nnz, rows, width, vals, coef, t.psum, loc.pos_s,
+                             loc.segid, t.n_ent, loc.grad)
         return loc.grad, None
     if is_gpu(coef):
         hipops().linear_bwd(loc.pos_s, loc.segid, loc.nnz, rows, width, vals, coef,
@@ -145,7 +140,7 @@ def linear_fwd_bwd(loc, w_local, labels, *, B: int, width: int = 0, row_ptr=None
     local-column gather, no coef round trip through memory); anything else runs
     linear_forward + linear_backward."""
     t = getattr(loc, "tile", None)
-    if (t is not None and t.size == 8192 and t.ent_uid is not None and row_ptr is None
+    if (t is not None and t.ent_uid is not None and row_ptr is None
             and rows is None and width and loc.nnz == B * width and is_gpu(w_local)
             and hipops().tp_fwd_bwd_supported(width)):
         coef = torch.empty(B, dtype=torch.float32, device=w_local.device) if coef is None else coef

@@ -36,9 +36,8 @@ class Localized:
     grad: torch.Tensor
     hess: torch.Tensor | None
     nnz: int
-    hashed: bool = False  # sort-free ids (no CSC order: pos_s / segid / seg_start are None)
-    # tile-deduplicated ("tile" mode): pos_s / segid / seg_start run over the
-    # tile-distinct ENTRIES, not the nnz; the backward goes through tile_backward
+    # tile-deduplicated ("tp" mode): pos_s / segid / seg_start run over the
+    # tile-distinct ENTRIES, not the nnz; the backward goes through tp_backward
     tile: object = None
 
     def num_unique(self) -> int:  # host sync
@@ -48,11 +47,10 @@ class Localized:
 @dataclass
 class TileInfo:
     rep: torch.Tensor    # int16 [nnz] tile-local entry id of every position
-    dcnt: torch.Tensor   # int32 [tiles] distinct keys per 4096-key tile
+    dcnt: torch.Tensor   # int32 [tiles] distinct keys per 8192-key tile
     n_ent: torch.Tensor  # int32[1] total entries (device)
-    psum: torch.Tensor   # float [tiles*size] per-entry partial gradients (backward scratch)
-    size: int = 4096     # occurrences per tile (4096: "tile" mode, 8192: "tp" mode)
-    ent_uid: torch.Tensor | None = None  # int32 [tiles*size] tile entry -> unique id ("tp")
+    psum: torch.Tensor   # float [tiles*8192] per-entry partial gradients (backward scratch)
+    ent_uid: torch.Tensor | None = None  # int32 [tiles*8192] tile entry -> unique id
     cols_ready: bool = True  # False: local_col not materialised yet (ensure_local_col)
 
 
@@ -71,19 +69,8 @@ class Localizer:
     """Reusable localisation workspace for up to ``max_nnz`` keys per call.
 
     ``mode="sort"``: radix sort + RLE (unique keys in sorted mixed order, CSC order
-    for the segmented backward). ``mode="hash"`` (GPU, key bits <= 32): sort-free
-    dedup in a per-step scratch hash table (csrc/hip/hashloc.hip); unique keys in
-    claim order, backward through an LDS accumulation cache + atomics. Measured on
-    MI355X for 65,536 x 39 Criteo-shaped keys (benchmarks/bench_localize.py):
-    sort 205 us + 26 us backward, hash 169 us + 153 us backward, so "sort" is the
-    default; "hash" avoids the O(bits) sort passes for very wide key batches.
-    ``mode="bucket"`` (csrc/hip/bucketloc.hip): one partition pass on the top 12
-    key bits + per-bucket LDS presence bitmaps (no comparison sort); exact same
-    outputs except the order of positions inside a key's segment. Measured 1045 us
-    on the same batch (device-scope atomics and the cross-bucket look-back are
-    latency bound, and power-law hot keys make a few buckets 40K elements long),
-    so it is an alternative, not the default.
-    ``mode="part"`` (csrc/hip/partloc.hip, GPU, key bits <= 32): one partition pass on
+    for the segmented backward).
+    ``mode="part"``    ``mode="part"`` (csrc/hip/partloc.hip, GPU, key bits <= 32): one partition pass on
     the top key bits, then one workgroup per bucket deduplicates its keys in an LDS
     hash and sorts only the DISTINCT keys; same outputs as "sort" except the order of
     positions inside a key's segment (5 launches instead of 16).
@@ -93,7 +80,10 @@ class Localizer:
     8192-occurrence tiles, then one workgroup per key-range bucket deduplicates the
     tile-distinct entries (a hot key is at most one entry per tile) and emits sorted
     unique keys, an entry-level CSC and local columns: 4 launches, no global atomics;
-    the backward accumulates per tile in LDS and scans the entry CSC (``TileInfo``)."""
+    the backward accumulates per tile in LDS and scans the entry CSC (``TileInfo``).
+    (Measured and removed in round 3: a sort-free global scratch hash, a partition
+    with per-bucket presence bitmaps and a 4096-key tile dedup + radix sort; none beat
+    "tp" on the Criteo-shaped batch, profiles/r2_localize_tp_vs_sort.log.)"""
 
     def __init__(self, max_nnz: int, bits: int, device="cpu", with_hess: bool = False,
                  mode: str = "sort", lazy_cols: bool = False):
@@ -105,35 +95,14 @@ class Localizer:
         n = self.max_nnz
         dev = self.device
         self.gpu = dev.type == "cuda"
-        if mode not in ("sort", "hash", "bucket", "tile", "part", "tp"):
+        if mode not in ("sort", "part", "tp"):
             raise ValueError(f"unknown localisation mode {mode!r}")
         if mode == "part" and not (self.gpu and hipops().partloc_supported(n, self.bits)):
             mode = "sort"
         if mode == "tp" and (with_hess or not (self.gpu and hipops().tploc_supported(n, self.bits))):
             mode = "sort"
-        if mode in ("hash", "tile") and (with_hess or self.bits > 32):
-            mode = "sort"
-        if mode == "tile" and self.bits > 31:
-            mode = "sort"
         # (tp: up to 34-bit keys through its quotient-encoded tile hash)
         self.mode = mode if (self.gpu and (self.bits <= 32 or mode == "tp")) else "sort"
-        if self.gpu and self.mode == "tile":
-            H = hipops()
-            N = H.tileloc_stride(n)
-            i32 = lambda k: torch.empty(k, dtype=torch.int32, device=dev)  # noqa: E731
-            self.t_dkeys, self.t_dcnt, self.t_nent = i32(N), i32(N // 4096), i32(1)
-            self.t_rep = torch.empty(n, dtype=torch.int16, device=dev)
-            self.t_temp = torch.empty(H.tileloc_sort_temp_bytes(n), dtype=torch.uint8, device=dev)
-            self.t_hs, self.pos_s, self.segid, self.t_ent_uid = i32(N), i32(N), i32(N), i32(N)
-            self.seg_start = i32(N + 1)
-            self.uniq = torch.empty(N, dtype=torch.int64, device=dev)
-            self.local_col = i32(n)
-            self.n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
-            self.grad = torch.empty(N, dtype=torch.float32, device=dev)
-            self.t_psum = torch.empty(N, dtype=torch.float32, device=dev)
-            self.hess = None
-            self.digit_bits = 10 if 24 < self.bits <= 30 else 8
-            return
         if self.gpu and self.mode == "tp":
             H = hipops()
             N = H.tploc_stride(n)
@@ -163,32 +132,6 @@ class Localizer:
             self.n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
             self.grad = torch.empty(n, dtype=torch.float32, device=dev)
             self.hess = torch.empty(n, dtype=torch.float32, device=dev) if with_hess else None
-            self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-            return
-        if self.gpu and self.mode == "bucket":
-            H = hipops()
-            self.btemp = torch.empty(H.bucketloc_temp_bytes(n), dtype=torch.uint8, device=dev)
-            self.pos_s = torch.empty(n, dtype=torch.int32, device=dev)
-            self.segid = torch.empty(n, dtype=torch.int32, device=dev)
-            self.uniq = torch.empty(n, dtype=torch.int64, device=dev)
-            self.seg_start = torch.empty(n + 1, dtype=torch.int32, device=dev)
-            self.local_col = torch.empty(n, dtype=torch.int32, device=dev)
-            self.n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
-            self.grad = torch.empty(n, dtype=torch.float32, device=dev)
-            self.hess = torch.empty(n, dtype=torch.float32, device=dev) if with_hess else None
-            return
-        if self.gpu and self.mode == "hash":
-            H = hipops()
-            cap = 1 << max(10, (2 * n - 1).bit_length())
-            self.hslots = torch.zeros(cap, dtype=torch.int64, device=dev)  # epoch 0 = empty
-            self.hids = torch.empty(cap, dtype=torch.int32, device=dev)
-            self.epoch = torch.zeros(1, dtype=torch.int64, device=dev)
-            self.htemp = torch.empty(H.hashloc_temp_bytes(n), dtype=torch.uint8, device=dev)
-            self.uniq = torch.empty(n, dtype=torch.int64, device=dev)
-            self.local_col = torch.empty(n, dtype=torch.int32, device=dev)
-            self.n_uniq = torch.zeros(1, dtype=torch.int32, device=dev)
-            self.grad = torch.empty(n, dtype=torch.float32, device=dev)
-            self.hess = None
             self.err = torch.zeros(1, dtype=torch.int32, device=dev)
             return
         if self.gpu:
@@ -248,22 +191,14 @@ class Localizer:
 
     def _gpu(self, keys, n) -> Localized:
         H = hipops()
-        if self.mode == "tile":
-            H.localize_tile(keys, self.bits, self.digit_bits, self.t_dkeys, self.t_dcnt, self.t_rep,
-                            self.t_nent, self.t_temp, self.t_hs, self.pos_s, self.segid, self.uniq,
-                            self.seg_start, self.t_ent_uid, self.local_col, self.n_uniq,
-                            self.grad)
-            tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum)
-            return Localized(self.uniq, self.seg_start, self.pos_s, self.segid,
-                             self.local_col[:n], self.n_uniq, self.grad, None, n, tile=tile)
         if self.mode == "tp":
             H.localize_tp(keys, self.bits, self.ptemp, self.t_dcnt, self.t_rep, self.pos_s,
                           self.segid, self.uniq, self.seg_start, self.t_ent_uid,
                           None if self.lazy_cols else self.local_col,
                           self.n_uniq, self.t_nent, self.grad, self.err,
                           getattr(self, "tp_prof", None))
-            tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum, 8192,
-                            self.t_ent_uid, not self.lazy_cols)
+            tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum, self.t_ent_uid,
+                            not self.lazy_cols)
             # unique keys <= n: expose n-sized views (the workspace is tile-rounded)
             return Localized(self.uniq[:n], self.seg_start, self.pos_s, self.segid,
                              self.local_col[:n], self.n_uniq, self.grad[:n], None, n, tile=tile)
@@ -273,16 +208,6 @@ class Localizer:
                             self.err)
             return Localized(self.uniq, self.seg_start, self.pos_s[:n], self.segid[:n],
                              self.local_col[:n], self.n_uniq, self.grad, self.hess, n)
-        if self.mode == "bucket":
-            H.localize_bucket(keys, self.bits, self.btemp, self.pos_s, self.segid, self.uniq,
-                              self.seg_start, self.local_col, self.n_uniq, self.grad, self.hess)
-            return Localized(self.uniq, self.seg_start, self.pos_s[:n], self.segid[:n],
-                             self.local_col[:n], self.n_uniq, self.grad, self.hess, n)
-        if self.mode == "hash":
-            H.localize_hash(keys, self.bits, self.hslots, self.hids, self.epoch, self.htemp,
-                            self.uniq, self.local_col, self.n_uniq, self.grad, self.err)
-            return Localized(self.uniq, None, None, None, self.local_col[:n], self.n_uniq,
-                             self.grad, None, n, hashed=True)
         if self.fast32:
             H.localize32(keys, self.bits, self.sort_temp, self.hs32, self.pos_s, self.segid,
                          self.uniq, self.seg_start, self.local_col, self.n_uniq, self.grad,

@@ -61,7 +61,7 @@ def _gpu_worker(rank, world, port, out_dir, cfg_kw, steps, pipelined=False):
                          [(0, False, "padded", "sort"), (0, False, "exact", "sort"),
                           (3, False, "padded", "sort"), (3, False, "exact", "sort"),
                           (0, True, "padded", "sort"),
-                          (0, True, "exact", "sort"), (0, False, "padded", "hash")])
+                          (0, True, "exact", "sort"), (0, False, "padded", "tp")])
 def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes, pipelined, exchange,
                                                  localize):
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
