@@ -409,9 +409,12 @@ def main():
     B = args.minibatch
     N = int(args.num_features)
     # reference CTR online config (example/linear/ctr/online_l1lr.conf): FTRL, L1 10 / L2 1,
-    # DECAY alpha .01 beta 10.
-    cfg = SparseLRConfig(num_features=N, minibatch=B, algo=args.algo, lr_type="decay",
-                         alpha=0.01, beta=10.0, l1=10.0, l2=1.0, consistency=args.consistency,
+    # DECAY alpha .01 beta 10; AdaGrad / SGD with their own step sizes (sparse_lr.ALGO_DEFAULTS)
+    from parameter_server_amd.models.sparse_lr import algo_defaults
+
+    hyper = algo_defaults(args.algo)
+    cfg = SparseLRConfig(num_features=N, minibatch=B, algo=args.algo, **hyper,
+                         consistency=args.consistency,
                          fixing_float_bytes=args.fixing_float, exchange=args.exchange,
                          localize=args.localize, push_mode=args.push_mode,
                          seed=rank)
@@ -554,7 +557,9 @@ def main():
                     f"hashed into {N:.0e} features; zero-init optimizer state)",
             "config": {
                 "model": f"sparse logistic regression, {ALGO_NAMES.get(args.algo, args.algo)} "
-                         f"L1=10 L2=1 (server-side), {N:.0e} hashed features",
+                         f"L1={hyper['l1']:g} L2={hyper['l2']:g} {hyper['lr_type'].upper()} "
+                         f"alpha={hyper['alpha']:g} beta={hyper['beta']:g} (server-side), "
+                         f"{N:.0e} hashed features",
                 "global_batch": n_ranks * B,
                 "seq_len": 39,
                 "nnz_per_example": 39,

@@ -188,7 +188,11 @@ bcd_replica_kernel(int64_t c0, int64_t ncols, int64_t own0, int64_t own1, double
 
 // K12 -------------------------------------------------------------------------
 // ym_i += y_i * dw_c * x_ic for every nnz of the block with dw_c != 0.
-// scale_by_y = false is the plain SpMV  ym_i += w_c x_ic  used at init.
+// kUnique: every row occurs at most once in the block's range (one key per example
+// and feature group, the Criteo / TERAFEA slot layout; checked at preprocessing), so
+// the update is a plain read-modify-write of ym (no fp64 atomics); otherwise one
+// atomic per entry (rows sorted within the block: coalesced, uncontended).
+template <bool kUnique>
 __global__ void __launch_bounds__(256)
 bcd_dual_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row,
                 const float* __restrict__ val, int64_t p0, int64_t p1, int64_t c0, int64_t ncols,
@@ -203,7 +207,8 @@ bcd_dual_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row
     const int32_t r = row[i];
     if (!in_range(r, nrows)) continue;
     const double x = val ? (double)val[i] : 1.0;
-    unsafeAtomicAdd(&ym[r], (double)y[r] * d * x);
+    if (kUnique) ym[r] += (double)y[r] * d * x;
+    else unsafeAtomicAdd(&ym[r], (double)y[r] * d * x);
   }
 }
 
@@ -381,10 +386,14 @@ void bcd_replica(int64_t c0, int64_t ncols, int64_t own0, int64_t own1, double* 
 
 void bcd_dual(const int32_t* col, const int32_t* row, const float* val, int64_t p0, int64_t p1,
               int64_t c0, int64_t ncols, const double* dw, const float* y, double* ym,
-              int64_t nrows, hipStream_t st) {
+              int64_t nrows, bool unique_rows, hipStream_t st) {
   if (p1 <= p0) return;
-  bcd_dual_kernel<<<grid_for(p1 - p0, 256, 4096), 256, 0, st>>>(col, row, val, p0, p1, c0, ncols,
-                                                                 dw, y, ym, nrows);
+  if (unique_rows)
+    bcd_dual_kernel<true><<<grid_for(p1 - p0, 256, 4096), 256, 0, st>>>(
+        col, row, val, p0, p1, c0, ncols, dw, y, ym, nrows);
+  else
+    bcd_dual_kernel<false><<<grid_for(p1 - p0, 256, 4096), 256, 0, st>>>(
+        col, row, val, p0, p1, c0, ncols, dw, y, ym, nrows);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

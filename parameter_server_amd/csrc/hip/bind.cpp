@@ -151,7 +151,7 @@ void bcd_update(int64_t, int64_t, double*, double*, double*, double*, uint8_t*, 
 void bcd_replica(int64_t, int64_t, int64_t, int64_t, double*, double*, double*, uint8_t*, double,
                  hipStream_t);
 void bcd_dual(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
-              const double*, const float*, double*, int64_t, hipStream_t);
+              const double*, const float*, double*, int64_t, bool, hipStream_t);
 void bcd_objective(const double*, int64_t, double*, hipStream_t);
 void bcd_server_stats(const double*, const uint8_t*, int64_t, int64_t, double*, hipStream_t);
 // embedding.hip
@@ -1334,7 +1334,7 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("bcd_dual", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                 int64_t p1, int64_t c0, int64_t ncols, Tensor dw, Tensor y,
-                                Tensor ym) {
+                                Tensor ym, bool unique_rows) {
     csc_check(col, row, val, p0, p1);
     chk(dw, at::kDouble, "dw");
     chk(y, at::kFloat, "y");
@@ -1343,7 +1343,7 @@ PYBIND11_MODULE(_hipops, m) {
     check(ncols >= 0 && dw.numel() >= ncols, "dw too small");
     psamd::bcd_dual(ptr<int32_t>(col), ptr<int32_t>(row), optr<float>(val, at::kFloat, "val"), p0,
                     p1, c0, ncols, ptr<double>(dw), ptr<float>(y), ptr<double>(ym), ym.numel(),
-                    cur_stream());
+                    unique_rows, cur_stream());
   });
   m.def("bcd_objective", [](Tensor ym, Tensor out) {
     chk(ym, at::kDouble, "ym");

@@ -151,6 +151,7 @@ class Block:
     chunks: object = None  # device work list of the chunked gradient kernel (GPU)
     gu: object = None      # device [G | U] buffer of the block (GPU)
     busy: bool = False     # gu holds a launched, not yet consumed gradient
+    unique_rows: bool = False  # no example has two entries in the block (dual w/o atomics)
 
     @property
     def ncols(self):
@@ -484,6 +485,9 @@ class DarlinTrainer:
                 if p1 <= p0:
                     continue
                 rs, perm = torch.sort(self.row[p0:p1], stable=True)
+                # one entry per example and feature group (slot data): the dual
+                # update needs no atomics
+                blk.unique_rows = bool((rs[1:] != rs[:-1]).all()) if p1 - p0 > 1 else True
                 self.row_r[p0:p1] = rs
                 self.col_r[p0:p1] = self.col[p0:p1][perm]
                 if self.val is not None:
@@ -536,7 +540,7 @@ class DarlinTrainer:
         if persistent:
             b.busy = False
         bcd.dual(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, dw, self.y,
-                 self.ym)
+                 self.ym, b.unique_rows)
 
     # ---- sharded server (G > 1): rank r owns the r-th even slice of every block
     def _own_slice(self, b: Block) -> tuple[int, int, int]:
@@ -581,7 +585,7 @@ class DarlinTrainer:
         self.comm.all_gather_into_async(dw, dwo).wait()
         bcd.replica(b.c0, b.ncols, j0, j1, dw, self.w, self.delta, self.active, c.delta_max)
         bcd.dual(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, dw, self.y,
-                 self.ym)
+                 self.ym, b.unique_rows)
 
     def run_pass(self, it: int, reset_kkt: bool = False) -> BCDProgress:
         cfg = self.cfg

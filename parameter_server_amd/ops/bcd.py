@@ -175,10 +175,12 @@ def violation(vio) -> float:
     return float(vio.detach().cpu().view(torch.float64)[0])
 
 
-def dual(col, row, val, p0: int, p1: int, c0: int, ncols: int, dw, y, ym):
-    """ym_i += y_i * dw_c * x_ic over the block (in place)."""
+def dual(col, row, val, p0: int, p1: int, c0: int, ncols: int, dw, y, ym,
+         unique_rows: bool = False):
+    """ym_i += y_i * dw_c * x_ic over the block (in place). ``unique_rows``: no row
+    occurs twice in [p0, p1) (GPU: plain read-modify-write instead of atomics)."""
     if is_gpu(ym):
-        hipops().bcd_dual(col, row, val, p0, p1, c0, ncols, dw, y, ym)
+        hipops().bcd_dual(col, row, val, p0, p1, c0, ncols, dw, y, ym, bool(unique_rows))
         return ym
     c = col[p0:p1].long() - c0
     r = row[p0:p1].long()

@@ -100,7 +100,9 @@ class _DeviceChain:
 
     def __init__(self, device):
         self.device = torch.device(device)
-        self.on = self.device.type == "cuda"
+        # PSAMD_COMM_CHAIN=0: no device ordering (A/B of its host cost only; unsafe
+        # with collectives issued from several streams)
+        self.on = self.device.type == "cuda" and os.environ.get("PSAMD_COMM_CHAIN", "1") != "0"
         self.ev = None           # completion of the last chained collective
         self._cs = None          # communicator stream of the asynchronous collectives
         self.n = 0

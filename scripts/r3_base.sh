@@ -5,6 +5,8 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_tploc_gpu.py tests/test_gpu_ops.py tests/test_tp_fused_gpu.py > gpurun_out/r3_pytest_tp.log 2>&1 || { tail -30 gpurun_out/r3_pytest_tp.log; exit 1; }
 tail -2 gpurun_out/r3_pytest_tp.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3_smoke.log 2>&1 || { tail -20 gpurun_out/r3_smoke.log; exit 1; }
+tail -1 gpurun_out/r3_smoke.log
 timeout -k 10 240 python bench.py --steps 200 --warmup 20 > gpurun_out/r3_b1.log 2>&1 || exit $?
 tail -1 gpurun_out/r3_b1.log | cut -c1-400
 timeout -k 10 240 python bench.py --steps 200 --warmup 20 --minibatch 10000 > gpurun_out/r3_b1_10k.log 2>&1 || exit $?
