@@ -350,8 +350,10 @@ def main():
                          "1 -> 0.46, 2 -> 0.308, 3 -> 0.334 in round 1; with the applies at the "
                          "tail of the exchange half (round 2): 2 -> 0.162, 3 -> 0.139). 0 = "
                          "auto: 3")
-    ap.add_argument("--exchange", default="padded", choices=["padded", "exact"],
-                    help="N > 1: fixed-capacity sync-free exchange, or count-sized all-to-all-v")
+    ap.add_argument("--exchange", default="padded", choices=["padded", "exact", "p2p"],
+                    help="N > 1: fixed-capacity sync-free exchange, count-sized all-to-all-v, "
+                         "or one-sided peer-HBM pulls + inbox pushes (asp only, no collective "
+                         "per step: parallel/p2p.py)")
     ap.add_argument("--fixing-float", type=int, default=0)
     ap.add_argument("--push-mode", default="sequential", choices=["sequential", "aggregate"],
                     help="N > 1: one optimizer step per source row in rank order (per-push, "

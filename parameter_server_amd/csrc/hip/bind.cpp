@@ -27,6 +27,17 @@ void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int,
 void kv_apply_part(void*, int64_t, const int64_t*, const uint64_t*, const float*, int64_t,
                    const int32_t*, int, int64_t, int64_t, const int32_t*, int, int, int, float, float,
                    float, float, float, float, double*, int, hipStream_t);
+// p2p.hip
+void p2p_lookup_rows(const void*, int, int, const int32_t*, int64_t, int64_t, int, float*, int64_t*,
+                     int, float, float, uint64_t, int32_t*, int32_t*, hipStream_t);
+void p2p_post(const int32_t*, int64_t, int64_t, int, int, int, int32_t, int, void* const*,
+              void* const*, int32_t*, int32_t*, int64_t, hipStream_t);
+void p2p_gather(const int32_t*, const int32_t*, int, int, int, int64_t, int64_t, int, int32_t*,
+                int32_t*, hipStream_t);
+void p2p_commit(int32_t*, const int32_t*, int, int64_t*, hipStream_t);
+void ipc_export(const void*, uint8_t*);
+void* ipc_import(const uint8_t*);
+void ipc_close(void*, int64_t);
 // tploc.hip
 void tp_gather(const uint16_t*, const int32_t*, int64_t, int32_t*, hipStream_t);
 bool tp_fwd_bwd_supported(int);
@@ -353,6 +364,75 @@ PYBIND11_MODULE(_hipops, m) {
     else check(rows.size(0) >= u_cap, "rows too small");
     psamd::fm_l2(ptr<float>(dE), rows.data_ptr(), ip, rows.size(0),
                  optr<int32_t>(n_dev, at::kInt, "n_dev"), u_cap, D, (float)lambda, cur_stream());
+  });
+  // ---------------- one-sided peer-HBM exchange (p2p.hip) ----------------
+  m.def("ipc_export", [](Tensor t) {
+    check(t.is_cuda(), "ipc_export: device tensor");
+    std::string out(72, '\0');
+    psamd::ipc_export(t.data_ptr(), reinterpret_cast<uint8_t*>(&out[0]));
+    return py::bytes(out);
+  });
+  m.def("ipc_import", [](py::bytes b) {
+    std::string s = b;
+    check(s.size() == 72, "ipc_import: 72-byte handle");
+    return (int64_t) reinterpret_cast<intptr_t>(psamd::ipc_import(reinterpret_cast<const uint8_t*>(s.data())));
+  });
+  m.def("ipc_close", [](int64_t ptr, int64_t off) {
+    psamd::ipc_close(reinterpret_cast<void*>(static_cast<intptr_t>(ptr)), off);
+  });
+  m.def("p2p_lookup_rows", [](Tensor tabs, int G, int self, Tensor send, int64_t H, int64_t C, int kw,
+                              Tensor wout, Tensor slot_out, int init_type, double init_v,
+                              double init_s, uint64_t seed, Tensor err, Tensor inserted) {
+    chk(tabs, at::kLong, "tabs");
+    chk(send, at::kInt, "send");
+    chk(wout, at::kFloat, "wout");
+    chk(slot_out, at::kLong, "slot_out");
+    chk(err, at::kInt, "err");
+    chk(inserted, at::kInt, "inserted");
+    check(G >= 1 && G <= 64 && self >= 0 && self < G, "p2p: 1..64 ranks");
+    check(tabs.numel() == 5 * G, "tabs: 5 int64 per rank");
+    check(kw == 1 || kw == 2, "kw 1 or 2");
+    check(H >= 4 + C * kw + C, "row too short");
+    check(send.numel() >= G * H && wout.numel() >= G * C && slot_out.numel() >= G * C,
+          "p2p_lookup_rows buffers too small");
+    psamd::p2p_lookup_rows(tabs.data_ptr(), G, self, ptr<int32_t>(send), H, C, kw, ptr<float>(wout),
+                           ptr<int64_t>(slot_out), init_type, (float)init_v, (float)init_s, seed,
+                           ptr<int32_t>(err), ptr<int32_t>(inserted), cur_stream());
+  });
+  m.def("p2p_post", [](Tensor send, int64_t H, int64_t C, int kw, int G, int self, int64_t seq,
+                       int Q, Tensor rings, Tensor applied, Tensor ok, Tensor err, int64_t spin) {
+    chk(send, at::kInt, "send");
+    chk(rings, at::kLong, "rings");
+    chk(applied, at::kLong, "applied");
+    chk(ok, at::kInt, "ok");
+    chk(err, at::kInt, "err");
+    check(G >= 1 && G <= 64 && self >= 0 && self < G, "p2p: 1..64 ranks");
+    check(rings.numel() == G && applied.numel() == G && ok.numel() >= G, "p2p_post: G pointers");
+    check(send.numel() >= G * H && H >= 4 + C * kw + C, "p2p_post: send rows");
+    check(seq >= 1 && seq < (int64_t(1) << 31) && Q >= 1, "p2p_post: 1 <= seq < 2^31, Q >= 1");
+    psamd::p2p_post(ptr<int32_t>(send), H, C, kw, G, self, (int32_t)seq, Q,
+                    reinterpret_cast<void* const*>(rings.data_ptr()),
+                    reinterpret_cast<void* const*>(applied.data_ptr()), ptr<int32_t>(ok),
+                    ptr<int32_t>(err), spin, cur_stream());
+  });
+  m.def("p2p_gather", [](Tensor inbox, Tensor applied, int G, int self, int Q, int64_t H, int64_t C,
+                         int kw, Tensor stage, Tensor ready) {
+    chk(inbox, at::kInt, "inbox");
+    chk(applied, at::kInt, "applied");
+    chk(stage, at::kInt, "stage");
+    chk(ready, at::kInt, "ready");
+    check(G >= 1 && G <= 64 && self >= 0 && self < G, "p2p: 1..64 ranks");
+    check(inbox.numel() >= (int64_t)G * Q * H && stage.numel() >= G * H, "p2p_gather: buffers");
+    check(applied.numel() >= G && ready.numel() >= G, "p2p_gather: counters");
+    psamd::p2p_gather(ptr<int32_t>(inbox), ptr<int32_t>(applied), G, self, Q, H, C, kw,
+                      ptr<int32_t>(stage), ptr<int32_t>(ready), cur_stream());
+  });
+  m.def("p2p_commit", [](Tensor applied, Tensor ready, int G, optional<Tensor> total) {
+    chk(applied, at::kInt, "applied");
+    chk(ready, at::kInt, "ready");
+    check(G >= 1 && G <= 64 && applied.numel() >= G && ready.numel() >= G, "p2p_commit");
+    psamd::p2p_commit(ptr<int32_t>(applied), ptr<int32_t>(ready), G,
+                      optr<int64_t>(total, at::kLong, "total"), cur_stream());
   });
   // ---------------- tile dedup + bucket partition localisation (tploc.hip) ----------------
   m.def("tploc_stride", [](int64_t n) { return psamd::tploc_stride(n); });

@@ -82,8 +82,11 @@ class SparseLRConfig:
     fixing_float_bytes: int = 0          # 0 = off, else 1..7 bytes per pushed gradient
     # multi-GPU data plane: "padded" = fixed-capacity rows per peer with device-side
     # counts (no host sync, graph-replayable); "exact" = count exchange + sized
-    # all-to-all-v (one host sync per step)
+    # all-to-all-v (one host sync per step); "p2p" = one-sided peer-HBM pulls and
+    # inbox pushes, no collective per step (asynchronous only, parallel/p2p.py)
     exchange: str = "padded"
+    p2p_queue: int = 16                  # p2p: inbox entries per source (staleness bound)
+    p2p_rounds: int = 2                  # p2p: inbox entries applied per source per step
     exchange_capacity: int = 0           # keys per peer per step; 0 = auto (first step)
     exchange_slack: float = 1.5          # auto capacity = slack * max per-peer count + 1024
     # padded exchange pipelining depth: pushes of step t ride the exchange of step
@@ -159,11 +162,17 @@ class SparseLRTrainer:
             self.w_buf = torch.empty(self.max_nnz, dtype=torch.float32, device=dev)
             self.touched = None
         # multi-GPU: fuse push(t-1) into the pull exchange of step t (2 all-to-alls/step)
-        if cfg.exchange not in ("padded", "exact"):
-            raise ValueError(f"exchange must be 'padded' or 'exact', not {cfg.exchange!r}")
+        if cfg.exchange not in ("padded", "exact", "p2p"):
+            raise ValueError(f"exchange must be 'padded', 'exact' or 'p2p', not {cfg.exchange!r}")
+        self.p2p = self.G > 1 and cfg.exchange == "p2p"
+        if self.p2p and (not self.gpu or self.filter is not None or cfg.fixing_float_bytes
+                         or cfg.push_mode == "aggregate" or not math.isinf(self.tau)):
+            raise ValueError("exchange='p2p' is the asynchronous GPU data plane: consistency "
+                             "'asp', no tail filter / fixing-float, sequential pushes")
+        self.px = None  # PeerExchange (p2p, set up on the first step)
         self.padded = self.G > 1 and cfg.exchange == "padded"
         self.fused = (self.G > 1 and self.filter is None and cfg.fixing_float_bytes == 0
-                      and not self.padded)
+                      and not self.padded and not self.p2p)
         self.xc = None  # padded-exchange state (allocated on the first step)
         # consistency on the padded exchange: the pushes of step t ride exchange t+1+lag
         # and are applied before its pulls, so the pull of step t sees exactly the
@@ -230,6 +239,10 @@ class SparseLRTrainer:
         localised minibatch (``localize``); ``prefetch``: called once the step's
         exchange counts are in flight and before the step blocks on them (multi-GPU),
         so the caller can enqueue the next minibatch's work on another stream."""
+        if self.p2p:
+            if loc is None:
+                loc = self.localizer(keys)
+            return self._p2p_step(loc, labels, width, prefetch)
         if self.padded:
             if loc is None:
                 with trace_range("localize"):
@@ -380,6 +393,10 @@ class SparseLRTrainer:
         """The consistency the data plane actually enforces (reported by bench.py)."""
         if self.G == 1:
             return "bsp (1 shard: every pull sees every earlier push)"
+        if self.p2p:
+            return (f"asp-p2p (one-sided pulls from the owners' HBM and inbox pushes, no "
+                    f"collective per step; owners apply at their own pace, a pusher waits "
+                    f"only {self.cfg.p2p_queue} steps ahead of an owner)")
         if not self.padded or self.lag == 0 and not self.asp:
             return "bsp (pull of step t sees every push of steps <= t-1)"
         if self.asp:
@@ -711,6 +728,75 @@ class SparseLRTrainer:
                 f"or exchange_slack higher, or exchange='exact'")
 
 
+    # ------------------------------------------ one-sided peer exchange (G > 1, p2p)
+    def _p2p_setup(self, loc):
+        """Row geometry (C keys per owner row: slack x the largest per-owner count of the
+        first minibatch over all ranks, like the padded exchange) and the IPC mappings."""
+        from types import SimpleNamespace
+
+        from ..parallel.p2p import PeerExchange
+
+        cfg, G, dev = self.cfg, self.G, self.device
+        off = torch.empty(G + 1, dtype=torch.int64, device=dev)
+        hipops().owner_split(loc.uniq, loc.n_uniq, self.part.bounds_on(dev), off)
+        C = int(cfg.exchange_capacity)
+        if C <= 0:
+            cnt = (off[1:] - off[:-1]).max().to(torch.float64).reshape(1)
+            cnt = self.comm.all_reduce_(cnt if self.comm.backend == "nccl" else cnt.cpu(),
+                                        op="max")
+            C = int(math.ceil(float(cnt.item()) * cfg.exchange_slack)) + 1024
+        C = min(max(64, (C + 63) // 64 * 64), max(64, self.max_nnz))
+        kw = 1 if self.bits <= 32 else 2
+        H = (4 + C * kw + C + 3) // 4 * 4
+        i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)  # noqa: E731
+        self.xc = SimpleNamespace(
+            C=C, kw=kw, H=H, off=off, send=i32(G * H),
+            wout=torch.zeros(G * C, dtype=torch.float32, device=dev),
+            slot=torch.full((G * C,), -1, dtype=torch.int64, device=dev),
+            w_local=torch.zeros(self.max_nnz, dtype=torch.float32, device=dev),
+            a_slot=torch.full((G * C,), -1, dtype=torch.int64, device=dev),
+            a_w=torch.zeros(G * C, dtype=torch.float32, device=dev),
+            link=torch.empty(next_pow2(2 * G * C), dtype=torch.int64, device=dev),
+            nxt=torch.empty(G * C, dtype=torch.int32, device=dev), ovf=i32(1),
+            ovf_host=torch.zeros(1, dtype=torch.int32, pin_memory=True))
+        self.px = PeerExchange(self.comm, self.table, C, kw, H, dev, Q=cfg.p2p_queue)
+
+    def _p2p_step(self, loc, labels, width, prefetch=None):
+        """One asynchronous step: pack this minibatch's keys per owner, pull them
+        one-sided (own row: lookup-or-insert), forward + backward, pack the gradients
+        next to the keys, apply the own row locally, post the peer rows into the
+        owners' inboxes, and apply whatever the peers have posted here so far."""
+        if self.xc is None:
+            self._p2p_setup(loc)
+        xc, hh, G, r = self.xc, hipops(), self.G, self.rank
+        C, kw, H = xc.C, xc.kw, xc.H
+        B = labels.numel()
+        width = width or self.cfg.max_nnz_per_example
+        hh.owner_split(loc.uniq, loc.n_uniq, self.part.bounds_on(self.device), xc.off)
+        hh.xchg_pack_keys(loc.uniq, loc.n_uniq, xc.off, C, kw, H, xc.send, xc.ovf)
+        self.px.lookup(xc.send, xc.wout, xc.slot)
+        if prefetch is not None:  # the next minibatch's preparation overlaps this step
+            prefetch()
+        U = loc.uniq.numel()
+        w_local = xc.w_local[:U]
+        hh.xchg_unpack_w(xc.wout, None, loc.n_uniq, xc.off, C, w_local)
+        _, grad = linear_fwd_bwd(loc, w_local, labels, B=B, width=width, loss=self.cfg.loss,
+                                 coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
+        hh.xchg_pack_grads(grad[:U], None, loc.n_uniq, xc.off, C, kw, H, xc.send, hist=self.hist,
+                           metrics=self.metrics, step_counter=self.step_dev, ovf=xc.ovf,
+                           ovf_host=xc.ovf_host)
+        g_own = xc.send.view(torch.float32)[r * H + 4 + C * kw:r * H + 4 + C * kw + C]
+        hh.kv_update(self.table.slots, xc.slot[r * C:(r + 1) * C], g_own,
+                     xc.send[r * H + 1:r * H + 2], *self.rule.args(), self.stats)
+        self.px.post(xc.send)
+        self.px.apply(self.rule, self.stats, xc.a_slot, xc.a_w, xc.link, xc.nxt,
+                      rounds=self.cfg.p2p_rounds)
+        self.step_count += 1
+        self.examples += B
+        if int(xc.ovf_host[0]):
+            raise RuntimeError(f"p2p exchange overflow: keys exceeded the per-owner row "
+                               f"capacity {C}; set exchange_capacity or exchange_slack higher")
+
     # ------------------------------------------------------- fused exchange (G > 1)
     def _exchange_fused(self, loc):
         """One step of the multi-GPU data plane with 2 all-to-alls instead of 3:
@@ -795,6 +881,11 @@ class SparseLRTrainer:
     def flush(self):
         """Apply the deferred pushes of the last step (fused / padded multi-GPU modes).
         Collective."""
+        if self.p2p:
+            if self.px is not None:
+                xc = self.xc
+                self.px.drain(self.rule, self.stats, xc.a_slot, xc.a_w, xc.link, xc.nxt)
+            return
         if self.padded:
             if self.xc is not None:
                 self._x_flush()

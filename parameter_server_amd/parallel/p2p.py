@@ -1,0 +1,149 @@
+"""One-sided peer-HBM exchange: asynchronous SGD without per-step collectives.
+
+The reference's async-SGD worker pulls and pushes without ever waiting for another
+worker (src/app/linear_method/async_sgd.h:219-238) and a server applies each push as
+it arrives (src/parameter/kv_store.h:47-57). The default multi-GPU data plane here is
+SPMD: every push / pull rides an RCCL all-to-all, so one slow rank stalls all of
+them. ``PeerExchange`` is the straggler-tolerant alternative (SURVEY §7.4 option b):
+at setup every rank exports its KV shard, its push inbox and its applied counters
+as IPC handles (``hipIpcGetMemHandle``; one host all-gather), and maps its peers'.
+Then, per step and without any collective (kernels in csrc/hip/p2p.hip):
+
+* pull: the keys owned by peer p are probed straight in p's table over xGMI
+  (read only; a key not inserted yet reads as its init value);
+* push: the rows of this step (keys + gradients per owner) are written into each
+  owner's inbox ring, entry ``[self][seq % Q]``, and published by a sequence word;
+* apply: each owner, at its own pace, applies the ready inbox entries of every
+  source (one entry per source per round, per-push semantics in rank order) with
+  the table kernels of the padded exchange, and publishes its applied counters.
+
+A pusher waits (bounded device spin) only when it is ``Q`` steps ahead of what an
+owner has applied from it: the staleness bound of this mode. Between ranks there is
+no lock step, so a slow rank delays only the application of its own pushes.
+
+Validated on one MI355X with several processes sharing the GPU (real IPC mappings,
+the same kernels); the xGMI path itself needs a multi-GPU node.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+from ..ops.native import hipops
+
+
+def _u64_to_i64(x: int) -> int:
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+class PeerExchange:
+    def __init__(self, comm, table, C: int, kw: int, H: int, device, Q: int = 16,
+                 spin_us: int = 5_000_000):
+        self.comm, self.table = comm, table
+        self.G, self.rank = comm.world, comm.rank
+        self.C, self.kw, self.H, self.Q = int(C), int(kw), int(H), int(Q)
+        self.spin = int(spin_us)  # give-up time of a push waiting for inbox space
+        self.device = dev = torch.device(device)
+        G, H, Q = self.G, self.H, self.Q
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.inbox = torch.zeros(G * Q * H, **i32)   # [source][Q][H]; seq word 0 = empty
+        self.applied = torch.zeros(G, **i32)          # last sequence applied per source
+        self.stage = torch.zeros(G * H, **i32)
+        self.ready = torch.zeros(G, **i32)
+        self.ok = torch.zeros(G, **i32)
+        self.err = torch.zeros(1, **i32)
+        self.total = torch.zeros(1, dtype=torch.int64, device=dev)  # entries applied
+        self.seq = 0                                  # pushes posted by this rank
+        hh = hipops()
+        cap = table.capacity
+        lg = (cap - 1).bit_length()
+        geom = [int(cap - 1), int(table.home_base), int(table.home_m), 64 - lg]
+        mine = {"slots": hh.ipc_export(table.slots), "inbox": hh.ipc_export(self.inbox),
+                "applied": hh.ipc_export(self.applied), "geom": geom}
+        allh = comm.all_gather_obj(mine)
+        self._opened = []
+        tabs, rings, applieds = [], [], []
+        for p, h in enumerate(allh):
+            if p == self.rank:
+                sp, ip, ap = table.slots.data_ptr(), self.inbox.data_ptr(), self.applied.data_ptr()
+            else:
+                sp, ip, ap = (self._open(h["slots"]), self._open(h["inbox"]),
+                              self._open(h["applied"]))
+            tabs += [sp] + [_u64_to_i64(v) for v in h["geom"]]
+            rings.append(ip)
+            applieds.append(ap)
+        self.tabs = torch.tensor(tabs, dtype=torch.int64).to(dev)
+        self.rings = torch.tensor(rings, dtype=torch.int64).to(dev)
+        self.applieds = torch.tensor(applieds, dtype=torch.int64).to(dev)
+
+    def _open(self, handle: bytes) -> int:
+        ptr = hipops().ipc_import(handle)
+        off = int.from_bytes(handle[64:72], "little", signed=True)
+        self._opened.append((ptr, off))
+        return ptr
+
+    # ------------------------------------------------------------------ step
+    def lookup(self, send, wout, slot_out):
+        """Weights of every row's keys: own row resolved with insert (slots ->
+        ``slot_out[self*C:]``), peer rows probed in the peers' tables."""
+        it, iv, isd, seed = self.table.init.args()
+        hipops().p2p_lookup_rows(self.tabs, self.G, self.rank, send, self.H, self.C, self.kw,
+                                 wout, slot_out, it, iv, isd, seed, self.table._err,
+                                 self.table._inserted)
+
+    def post(self, send):
+        """Write the peer rows of ``send`` (keys + gradients) into the owners' inboxes."""
+        self.seq += 1
+        hipops().p2p_post(send, self.H, self.C, self.kw, self.G, self.rank, self.seq, self.Q,
+                          self.rings, self.applieds, self.ok, self.err, self.spin)
+
+    def apply(self, rule, stats, slots_scratch, wscratch, link, nxt, rounds: int = 1):
+        """Owner: apply up to ``rounds`` ready inbox entries per source."""
+        hh, tb = hipops(), self.table
+        G, H, C = self.G, self.H, self.C
+        it, iv, isd, seed = tb.init.args()
+        for _ in range(rounds):
+            hh.p2p_gather(self.inbox, self.applied, G, self.rank, self.Q, H, C, self.kw,
+                          self.stage, self.ready)
+            hh.kv_resolve_rows(tb.slots, self.stage, H, C, self.kw, slots_scratch, wscratch, True,
+                               it, iv, isd, seed, tb._err, tb._inserted, tb.home_base, tb.home_m,
+                               None, None, 0)
+            g = self.stage.view(torch.float32)[4 + C * self.kw:]
+            hh.kv_update_rows(tb.slots, slots_scratch, g, H, self.stage, H, C, link, nxt,
+                              *rule.args(), stats)
+            hh.p2p_commit(self.applied, self.ready, G, self.total)
+
+    def check(self):
+        """Host sync: raise if a push gave up waiting for ring space (a peer stopped
+        applying for ``spin_us``)."""
+        if int(self.err.item()):
+            raise RuntimeError("p2p exchange: a push timed out waiting for an owner's inbox "
+                               "space (that owner stopped applying)")
+
+    def drain(self, rule, stats, slots_scratch, wscratch, link, nxt, timeout: float = 120.0):
+        """Collective at the end of training: apply every push every rank posted. (No
+        device sync before the host all-gather: a post of this rank may be waiting for
+        ring space on a peer that only frees it while draining.)"""
+        posted = self.comm.all_gather_obj(self.seq)
+        want = torch.tensor(posted, dtype=torch.int32)
+        want[self.rank] = 0
+        t0 = time.time()
+        while True:
+            got = self.applied.cpu()
+            got[self.rank] = 0
+            if bool((got >= want).all()):
+                break
+            if time.time() - t0 > timeout:
+                raise RuntimeError(f"p2p drain: applied {got.tolist()} of {want.tolist()}")
+            self.apply(rule, stats, slots_scratch, wscratch, link, nxt)
+            torch.cuda.synchronize(self.device)
+        self.check()
+        self.comm.barrier()
+
+    def close(self):
+        torch.cuda.synchronize(self.device)
+        for ptr, off in self._opened:
+            hipops().ipc_close(ptr, off)
+        self._opened = []

@@ -75,3 +75,18 @@ def test_aggregate_push_mode_cpu():
                          push_mode="aggregate")
     tr = _train(cfg, steps=3, B=128)
     assert tr.table.census()[0] > 0
+
+
+def test_p2p_exchange_is_asp_gpu_only():
+    """exchange='p2p' (one-sided peer-HBM data plane) is the asynchronous GPU mode: a
+    CPU run or a synchronous consistency is refused up front."""
+    import pytest
+
+    from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+    from parameter_server_amd.parallel.comm import LoopbackComm
+
+    for cons in ("asp", "bsp"):
+        cfg = SparseLRConfig(num_features=1 << 20, minibatch=64, table_capacity=1 << 12,
+                             consistency=cons, exchange="p2p")
+        with pytest.raises(ValueError, match="p2p"):
+            SparseLRTrainer(cfg, LoopbackComm(2), "cpu")
