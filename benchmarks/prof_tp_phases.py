@@ -17,15 +17,21 @@ L.tp_prof = torch.zeros(4096 * 12, dtype=torch.int64, device="cuda")
 for _ in range(3):
     L(keys)
 torch.cuda.synchronize()
-p = L.tp_prof.view(-1, 12)[:, :7].cpu()
+full = L.tp_prof.view(-1, 12).cpu()
+p = full[:, :8]
 nb = int((p[:, 0] != 0).sum())
 p = p[:nb].double()
 d = p[:, 1:] - p[:, :-1]
-names = ["toff+scan", "gather+insert", "compact", "ranksort", "starts", "assign"]
-tot = (p[:, 6] - p[:, 0])
+names = ["toff+scan", "gather+insert", "compact+publish", "ranksort", "look-back",
+         "uniq/starts", "entries"]
+tot = (p[:, 7] - p[:, 0])
 print(f"buckets {nb}: cycles per workgroup mean {tot.mean():.0f} max {tot.max():.0f}")
 for i, n in enumerate(names):
-    print(f"  {n:10s} mean {d[:, i].mean():8.0f}  max {d[:, i].max():8.0f}")
+    print(f"  {n:15s} mean {d[:, i].mean():8.0f}  max {d[:, i].max():8.0f}")
+rt0, rt1 = full[:nb, 8].double(), full[:nb, 9].double()  # 100 MHz realtime
+t0 = rt0.min()
+print(f"  wall (realtime, us): last start {(rt0.max() - t0) / 100:.1f}, "
+      f"last end {(rt1.max() - t0) / 100:.1f}, mean duration {((rt1 - rt0) / 100).mean():.1f}")
 
 # ---- fused forward + backward (tploc.hip tp_fwd_bwd FB_MARK) ----
 from parameter_server_amd.ops.linear import AUC_BINS, linear_fwd_bwd, new_accum  # noqa: E402

@@ -24,7 +24,9 @@
 //    of the block after an all-reduce of (G, U); there is no pull phase.
 #include "common.cuh"
 
+#include <algorithm>
 #include <cmath>
+#include <stdexcept>
 
 namespace psamd {
 
@@ -300,6 +302,100 @@ bcd_grad_chunk_kernel(const int32_t* __restrict__ col, const int32_t* __restrict
   }
 }
 
+// K11, row order, for NARROW blocks (ncols <= kRowCols: the integer slots and the
+// low-cardinality categorical slots of CTR data). The block's entries come from the
+// row-sorted copy the dual update uses, so the per-row reads of ym / y stream
+// sequentially instead of gathering one random 64-B line per entry (the column-order
+// kernel's cost: ~106 us per 4 M-entry block, profiles/r3_darlin_prof.log). G / U
+// accumulate per column in LDS as 64-bit FIXED POINT with integer LDS atomics
+// (ds_add_u64 ~15 cycles vs ~195 for a float LDS atomic on gfx950), in `copies`
+// replicas (copies x ncols <= 2048; 50 KB of LDS: 3 workgroups of 512 per CU) so that
+// lanes of different waves on a hot column serialise less; each
+// workgroup writes its exact partial sums, and bcd_rows_reduce adds the W partials of
+// every column in a fixed order: the result is deterministic. Scale 2^k (host: the
+// block's entry count x the largest |addend| < 2^(61-k), so the partials AND their
+// sum are exact int64 sums).
+constexpr int kRowCols = 2048;
+
+template <bool kVal>
+__global__ void __launch_bounds__(512)
+bcd_grad_rows_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row,
+                     const float* __restrict__ val, int64_t p0, int64_t p1, int64_t c0,
+                     int ncols, int copies, const double* __restrict__ ym,
+                     const float* __restrict__ y, int64_t nrows, const double* __restrict__ delta,
+                     const uint8_t* __restrict__ active, int k2,
+                     long long* __restrict__ part) {
+  __shared__ long long acc[2 * kRowCols];  // [copies][2][ncols] (G, U), copies*ncols <= 2048
+  __shared__ double cdl[kRowCols];            // per column: exp(delta) (binary) or delta
+  __shared__ uint8_t cact[kRowCols];
+  const int t = threadIdx.x;
+  const int stride = 2 * ncols;
+  for (int i = t; i < copies * stride; i += blockDim.x) acc[i] = 0;
+  for (int c = t; c < ncols; c += blockDim.x) {
+    const double dl = delta[c0 + c];
+    cdl[c] = kVal ? dl : exp(dl);
+    cact[c] = active[c0 + c];
+  }
+  __syncthreads();
+  const int64_t n = p1 - p0;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t a = p0 + per * blockIdx.x, b = min(p1, a + per);
+  long long* my = acc + (int64_t)((t >> 6) % copies) * stride;
+  const double sc = ldexp(1.0, k2);
+#pragma unroll 4
+  for (int64_t i = a + t; i < b; i += blockDim.x) {
+    const int c = col[i] - (int)c0;
+    if (c < 0 || c >= ncols || !cact[c]) continue;
+    const int32_t r = row[i];
+    if (!in_range(r, nrows)) continue;
+    const double tau = 1.0 / (1.0 + exp(ym[r]));
+    const double yr = (double)y[r];
+    const double t2 = tau * (1.0 - tau);
+    double g, u;
+    if (kVal) {
+      const double v = (double)val[i];
+      g = -yr * tau * v;
+      u = fmin(t2 * exp(fabs(v) * cdl[c]), 0.25) * v * v;
+    } else {
+      g = -yr * tau;
+      u = fmin(t2 * cdl[c], 0.25);
+    }
+    atomicAdd(reinterpret_cast<unsigned long long*>(&my[c]),
+              (unsigned long long)__double2ll_rn(g * sc));
+    atomicAdd(reinterpret_cast<unsigned long long*>(&my[ncols + c]),
+              (unsigned long long)__double2ll_rn(u * sc));
+  }
+  __syncthreads();
+  long long* out = part + (int64_t)blockIdx.x * stride;
+  for (int i = t; i < stride; i += blockDim.x) {
+    long long s = 0;
+    for (int q = 0; q < copies; ++q) s += acc[q * stride + i];
+    out[i] = s;
+  }
+}
+
+// G[c] / U[c] = sum over the W workgroup partials x 2^-k: one workgroup per output, its
+// threads strided over the partials, then a wave / block sum (int64: exact, so the
+// order does not matter and the result is deterministic).
+__global__ void __launch_bounds__(256)
+bcd_rows_reduce_kernel(const long long* __restrict__ part, int W, int ncols, int k2,
+                       double* __restrict__ G, double* __restrict__ U) {
+  __shared__ long long ws[4];
+  const int i = blockIdx.x;  // output 0 .. 2*ncols-1
+  long long s = 0;
+  for (int w = threadIdx.x; w < W; w += blockDim.x) s += part[(int64_t)w * 2 * ncols + i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const long long tot = ws[0] + ws[1] + ws[2] + ws[3];
+    const double v = (double)tot * ldexp(1.0, -k2);
+    if (i < ncols) G[i] = v;
+    else U[i - ncols] = v;
+  }
+}
+
 // objective: out[0] += sum_i log(1 + exp(-ym_i))
 __global__ void __launch_bounds__(256)
 bcd_objective_kernel(const double* __restrict__ ym, int64_t n, double* __restrict__ out) {
@@ -362,6 +458,30 @@ void bcd_grad_chunked(const int32_t* col, const int32_t* row, const float* val,
   if (nchunks <= 0) return;
   bcd_grad_chunk_kernel<<<grid_for(nchunks, 4, 16384), 256, 0, st>>>(
       col, row, val, chunks, nchunks, c0, ncols, ym, y, nrows, delta, active, G, U);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+int bcd_rows_max_cols() { return kRowCols; }
+
+void bcd_grad_rows(const int32_t* col, const int32_t* row, const float* val, int64_t p0,
+                   int64_t p1, int64_t c0, int64_t ncols, const double* ym, const float* y,
+                   int64_t nrows, const double* delta, const uint8_t* active, int k2, int W,
+                   long long* part, double* G, double* U, hipStream_t st) {
+  if (ncols <= 0) return;
+  if (ncols > kRowCols) throw std::runtime_error("bcd_grad_rows: ncols > 2048");
+  const int copies = std::max(1, std::min(8, kRowCols / (int)ncols));
+  if (p1 > p0) {
+    if (val)
+      bcd_grad_rows_kernel<true><<<W, 512, 0, st>>>(col, row, val, p0, p1, c0, (int)ncols, copies,
+                                                    ym, y, nrows, delta, active, k2, part);
+    else
+      bcd_grad_rows_kernel<false><<<W, 512, 0, st>>>(col, row, val, p0, p1, c0, (int)ncols, copies,
+                                                     ym, y, nrows, delta, active, k2, part);
+    PSAMD_HIP_CHECK(hipGetLastError());
+  } else {
+    fill_async<long long>(part, (int64_t)W * 2 * ncols, 0, st);
+  }
+  bcd_rows_reduce_kernel<<<(unsigned)(2 * ncols), 256, 0, st>>>(part, W, (int)ncols, k2, G, U);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -4,6 +4,7 @@
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <stdexcept>
@@ -45,13 +46,17 @@ void tp_fb_set_prof(uint64_t*);
 void tp_fwd_bwd(const uint16_t*, const int32_t*, const int32_t*, int64_t, int, const float*,
                 const float*, int64_t, const float*, int64_t, int, float*, double*, uint32_t*, int,
                 int, int, float*, const int32_t*, const int32_t*, const int32_t*, float*, int64_t,
-                hipStream_t);
+                bool, hipStream_t);
+void tp_seg_update(const int32_t*, const int32_t*, int64_t, const int32_t*, const float*,
+                   const int32_t*, const int32_t*, float*, int32_t*, int64_t, const int64_t*, void*,
+                   int64_t, int, int, float, float, float, float, float, float, double*, int,
+                   uint32_t*, int, int, double*, int64_t*, hipStream_t);
 int64_t tploc_stride(int64_t);
 bool tploc_supported(int64_t, int);
 size_t tploc_temp_bytes(int64_t, int);
 void localize_tp(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint16_t*, int32_t*,
                  int32_t*, uint64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, float*,
-                 int32_t*, int64_t, uint64_t*, hipStream_t);
+                 int32_t*, int32_t*, int64_t, uint64_t*, hipStream_t);
 void tp_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
                  const float*, int64_t, float*, const int32_t*, const int32_t*, const int32_t*,
                  float*, int64_t, hipStream_t);
@@ -164,6 +169,10 @@ void bcd_replica(int64_t, int64_t, int64_t, int64_t, double*, double*, double*, 
 void bcd_dual(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
               const double*, const float*, double*, int64_t, bool, hipStream_t);
 void bcd_objective(const double*, int64_t, double*, hipStream_t);
+int bcd_rows_max_cols();
+void bcd_grad_rows(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
+                   const double*, const float*, int64_t, const double*, const uint8_t*, int, int,
+                   long long*, double*, double*, hipStream_t);
 void bcd_server_stats(const double*, const uint8_t*, int64_t, int64_t, double*, hipStream_t);
 // embedding.hip
 void emb_init_rows(const int64_t*, const uint64_t*, int64_t, const int32_t*, int64_t, void*,
@@ -382,13 +391,13 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("p2p_lookup_rows", [](Tensor tabs, int G, int self, Tensor send, int64_t H, int64_t C, int kw,
                               Tensor wout, Tensor slot_out, int init_type, double init_v,
-                              double init_s, uint64_t seed, Tensor err, Tensor inserted) {
+                              double init_s, uint64_t seed, Tensor err,
+                              optional<Tensor> inserted) {
     chk(tabs, at::kLong, "tabs");
     chk(send, at::kInt, "send");
     chk(wout, at::kFloat, "wout");
     chk(slot_out, at::kLong, "slot_out");
     chk(err, at::kInt, "err");
-    chk(inserted, at::kInt, "inserted");
     check(G >= 1 && G <= 64 && self >= 0 && self < G, "p2p: 1..64 ranks");
     check(tabs.numel() == 5 * G, "tabs: 5 int64 per rank");
     check(kw == 1 || kw == 2, "kw 1 or 2");
@@ -397,7 +406,8 @@ PYBIND11_MODULE(_hipops, m) {
           "p2p_lookup_rows buffers too small");
     psamd::p2p_lookup_rows(tabs.data_ptr(), G, self, ptr<int32_t>(send), H, C, kw, ptr<float>(wout),
                            ptr<int64_t>(slot_out), init_type, (float)init_v, (float)init_s, seed,
-                           ptr<int32_t>(err), ptr<int32_t>(inserted), cur_stream());
+                           ptr<int32_t>(err), optr<int32_t>(inserted, at::kInt, "inserted"),
+                           cur_stream());
   });
   m.def("p2p_post", [](Tensor send, int64_t H, int64_t C, int kw, int G, int self, int64_t seq,
                        int Q, Tensor rings, Tensor applied, Tensor ok, Tensor err, int64_t spin) {
@@ -441,7 +451,7 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("localize_tp", [](Tensor keys, int bits, Tensor temp, Tensor dcnt, Tensor rep, Tensor pos_s,
                           Tensor segid, Tensor uniq, Tensor seg_start, Tensor ent_uid,
                           optional<Tensor> local_col, Tensor n_uniq, Tensor n_ent, Tensor grad,
-                          Tensor err, optional<Tensor> prof) {
+                          optional<Tensor> pieces, Tensor err, optional<Tensor> prof) {
     chk(keys, at::kLong, "keys");
     chk(temp, at::kByte, "temp");
     chk(dcnt, at::kInt, "dcnt");
@@ -471,7 +481,7 @@ PYBIND11_MODULE(_hipops, m) {
                        ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<uint64_t>(uniq),
                        ptr<int32_t>(seg_start), ptr<int32_t>(ent_uid), lc,
                        ptr<int32_t>(n_uniq), ptr<int32_t>(n_ent), ptr<float>(grad),
-                       ptr<int32_t>(err), uniq.numel(),
+                       optr<int32_t>(pieces, at::kInt, "pieces"), ptr<int32_t>(err), uniq.numel(),
                        reinterpret_cast<uint64_t*>(optr<int64_t>(prof, at::kLong, "prof")),
                        cur_stream());
   });
@@ -498,6 +508,42 @@ PYBIND11_MODULE(_hipops, m) {
                        coef.numel(), ptr<float>(psum), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
                        ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), cur_stream());
   });
+  m.def("tp_seg_update", [](Tensor pos_s, Tensor segid, int64_t n, Tensor n_ent, Tensor psum,
+                            Tensor seg_start, Tensor n_uniq, Tensor grad, Tensor pieces,
+                            Tensor slot_idx, Tensor slots, int algo, int lr_type, double alpha,
+                            double beta, double l1, double l2, double grad_scale,
+                            double max_delta, optional<Tensor> stats, optional<Tensor> hist,
+                            optional<Tensor> metrics, optional<Tensor> step_counter) {
+    chk(pos_s, at::kInt, "pos_s");
+    chk(segid, at::kInt, "segid");
+    chk(n_ent, at::kInt, "n_ent");
+    chk(psum, at::kFloat, "psum");
+    chk(seg_start, at::kInt, "seg_start");
+    chk(n_uniq, at::kInt, "n_uniq");
+    chk(grad, at::kFloat, "grad");
+    chk(pieces, at::kInt, "pieces");
+    chk(slot_idx, at::kLong, "slot_idx");
+    const int64_t cap = slot_capacity(slots);
+    check(n > 0, "tp_seg_update: n > 0");
+    check(alpha > 0, "learning rate alpha must be > 0");
+    const int64_t N = psamd::tploc_stride(n);
+    check(pos_s.numel() >= N && segid.numel() >= N && psum.numel() >= N &&
+              seg_start.numel() >= N + 1, "tp_seg_update: entry buffers < stride");
+    const int64_t ucap = std::min({grad.numel(), pieces.numel(), slot_idx.numel()});
+    uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
+    double* mp = optr<double>(metrics, at::kDouble, "metrics");
+    constexpr int kBins = 2048;
+    if (hp) check(mp && hist->numel() % (2 * kBins) == 0 && hist->numel() / (2 * kBins) <= 8,
+                  "tp_seg_update: hist = stripes x 2 x 2048 (<= 8 stripes) with metrics");
+    psamd::tp_seg_update(ptr<int32_t>(pos_s), ptr<int32_t>(segid), n, ptr<int32_t>(n_ent),
+                         ptr<float>(psum), ptr<int32_t>(seg_start), ptr<int32_t>(n_uniq),
+                         ptr<float>(grad), ptr<int32_t>(pieces), ucap, ptr<int64_t>(slot_idx),
+                         slots.data_ptr(), cap, algo, lr_type, (float)alpha, (float)beta,
+                         (float)l1, (float)l2, (float)grad_scale, (float)max_delta,
+                         optr<double>(stats, at::kDouble, "stats"), acc_stripes_of(stats), hp,
+                         kBins, hp ? (int)(hist->numel() / (2 * kBins)) : 1, mp,
+                         optr<int64_t>(step_counter, at::kLong, "step_counter"), cur_stream());
+  });
   m.def("tp_gather", [](Tensor rep, Tensor ent_uid, int64_t n, Tensor local_col) {
     chk(rep, at::kShort, "rep");
     chk(ent_uid, at::kInt, "ent_uid");
@@ -521,7 +567,7 @@ PYBIND11_MODULE(_hipops, m) {
                          optional<Tensor> vals, Tensor w_local, Tensor labels, int64_t B,
                          int loss_type, Tensor coef, optional<Tensor> metrics,
                          optional<Tensor> hist, int nbins, Tensor psum, Tensor pos_s,
-                         Tensor segid, Tensor n_ent, Tensor grad) {
+                         Tensor segid, Tensor n_ent, Tensor grad, bool reduce) {
     chk(rep, at::kShort, "rep");
     chk(dcnt, at::kInt, "dcnt");
     chk(ent_uid, at::kInt, "ent_uid");
@@ -551,7 +597,7 @@ PYBIND11_MODULE(_hipops, m) {
                       ptr<float>(coef), mp, hp, nbins, acc_stripes_of(metrics),
                       hp ? (int)std::max<int64_t>(1, hist->numel() / (2 * nbins)) : 1,
                       ptr<float>(psum), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
-                      ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), cur_stream());
+                      ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), reduce, cur_stream());
   });
   // ---------------- fixed-capacity exchange (exchange.hip) ----------------
   // buffers: send/recv int32 [G * H]; row layout documented in exchange.hip
@@ -1424,6 +1470,32 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::bcd_dual(ptr<int32_t>(col), ptr<int32_t>(row), optr<float>(val, at::kFloat, "val"), p0,
                     p1, c0, ncols, ptr<double>(dw), ptr<float>(y), ptr<double>(ym), ym.numel(),
                     unique_rows, cur_stream());
+  });
+  m.def("bcd_rows_max_cols", []() { return psamd::bcd_rows_max_cols(); });
+  m.def("bcd_grad_rows", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
+                                     int64_t p1, int64_t c0, int64_t ncols, Tensor ym, Tensor y,
+                                     Tensor delta, Tensor active, int k2, int W, Tensor part,
+                                     Tensor G, Tensor U) {
+    csc_check(col, row, val, p0, p1);
+    chk(ym, at::kDouble, "ym");
+    chk(y, at::kFloat, "y");
+    chk(delta, at::kDouble, "delta");
+    chk(active, at::kByte, "active");
+    chk(part, at::kLong, "part");
+    chk(G, at::kDouble, "G");
+    chk(U, at::kDouble, "U");
+    check(y.numel() == ym.numel(), "y/ym size mismatch");
+    check(ncols >= 0 && ncols <= psamd::bcd_rows_max_cols(), "bcd_grad_rows: ncols <= 2048");
+    check(c0 >= 0 && c0 + ncols <= delta.numel() && delta.numel() == active.numel(),
+          "block columns out of range");
+    check(G.numel() >= ncols && U.numel() >= ncols, "G/U too small");
+    check(W >= 1 && W <= 65535 && part.numel() >= (int64_t)W * 2 * ncols, "partials buffer");
+    check(k2 >= 0 && k2 <= 62, "fixed-point scale 2^0..2^62");
+    psamd::bcd_grad_rows(ptr<int32_t>(col), ptr<int32_t>(row), optr<float>(val, at::kFloat, "val"),
+                         p0, p1, c0, ncols, ptr<double>(ym), ptr<float>(y), ym.numel(),
+                         ptr<double>(delta), ptr<uint8_t>(active), k2, W,
+                         reinterpret_cast<long long*>(part.data_ptr()), ptr<double>(G),
+                         ptr<double>(U), cur_stream());
   });
   m.def("bcd_objective", [](Tensor ym, Tensor out) {
     chk(ym, at::kDouble, "ym");

@@ -27,7 +27,7 @@
 //
 // Buckets are ranges of the mixed key space, so the unique keys come out sorted
 // (the multi-GPU owner split and the ordered home slots of the KV table rely on it).
-#include "common.cuh"
+#include "kv_slot.cuh"
 #include "loss.cuh"
 
 #include <cstdlib>
@@ -270,12 +270,14 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
                  int32_t* __restrict__ pos_s, int32_t* __restrict__ segid,
                  uint64_t* __restrict__ uniq, int32_t* __restrict__ seg_start,
                  int32_t* __restrict__ ent_uid, int32_t* __restrict__ n_uniq,
-                 int32_t* __restrict__ n_ent, float* __restrict__ zero_a, int64_t u_cap,
-                 int64_t e_cap, int32_t* __restrict__ err, uint64_t* __restrict__ prof) {
+                 int32_t* __restrict__ n_ent, float* __restrict__ zero_a,
+                 int32_t* __restrict__ zero_b, int64_t u_cap, int64_t e_cap,
+                 int32_t* __restrict__ err, uint64_t* __restrict__ prof) {
   using namespace tp;
 #define TP_MARK(k) \
   if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 12 + (k)] = clock64();
   TP_MARK(0)
+  if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 12 + 8] = __builtin_amdgcn_s_memrealtime();
   // 40,944 B of LDS (<= 40 KB: 4 workgroups of 512 threads per CU)
   __shared__ uint16_t eh[kECapL];   // hash slot of every gathered entry
   __shared__ uint64_t hs[kDH];      // hash (key u32 | count u32), then the sorted list
@@ -395,6 +397,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     for (uint32_t q = 0; q < D; ++q) r += dl[q] < x;
     hs[r] = x;
   }
+  TP_MARK(4)
   // look-back (wave 0): bases = sums of the earlier buckets' counts
   if (t < 64) {
     const int lane = t;
@@ -442,7 +445,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     }
   }
   __syncthreads();
-  TP_MARK(4)
+  TP_MARK(5)
   const uint32_t ubase = sb[1], ebase = sb[2];
   // segment starts in key order -> uniq / seg_start; per slot: sorted index + cursor
   uint32_t carry = 0;
@@ -459,6 +462,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
         uniq[u] = ((uint64_t)b << shift) | (uint32_t)(v >> 32);
         seg_start[u] = (int32_t)(ebase + ex);
         if (zero_a) zero_a[u] = 0.f;
+        if (zero_b) zero_b[u] = 0;
       }
       cur[slot] = ex;
       jj[slot] = (uint16_t)j;
@@ -466,7 +470,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     carry += tot;
   }
   __syncthreads();
-  TP_MARK(5)
+  TP_MARK(6)
 #pragma unroll
   for (int q = 0; q < kG; ++q) {
     if (idx[q] < 0) continue;
@@ -481,7 +485,8 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     }
     if (in_range((int64_t)idx[q], e_cap)) ent_uid[idx[q]] = (int32_t)u;
   }
-  TP_MARK(6)
+  TP_MARK(7)
+  if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 12 + 9] = __builtin_amdgcn_s_memrealtime();
 #undef TP_MARK
 }
 
@@ -692,6 +697,91 @@ tp_seg_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restric
         if (starts_inside && s_next != s) grad[u] = x[0];
         else atomicAdd(&grad[u], x[0]);
       }
+    }
+  }
+}
+
+// Entry scan fused with the 1-GPU optimizer update (replaces tp_seg_reduce + kv_update:
+// one launch and the grad[] round trip less). The segmented scan of tp_seg_reduce;
+// a key whose entries all lie in one wave's 64-entry chunk has its full gradient in
+// the lane that ends the run, which applies the update to the key's slot at once.
+// A key spanning several chunks (hot keys) adds its pieces to grad[u] and counts them
+// in pieces[u] (both zeroed by the bucket kernel); the piece that completes the count
+// (known from seg_start: chunks spanned) reads the sum back and applies the update.
+// Block 0 also turns the step's AUC histogram into metrics (as kv_update did).
+__global__ void __launch_bounds__(256)
+tp_seg_update_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ segid,
+                     int64_t n_host, const int32_t* __restrict__ n_dev,
+                     const float* __restrict__ psum, int64_t p_cap,
+                     const int32_t* __restrict__ seg_start, const int32_t* __restrict__ n_uniq,
+                     float* __restrict__ grad, int32_t* __restrict__ pieces, int64_t u_cap,
+                     const int64_t* __restrict__ slot_idx, Slot* __restrict__ slots, int64_t cap,
+                     UpdateParams p, double* __restrict__ stats, int acc_stripes,
+                     uint32_t* __restrict__ hist, int nbins, int hist_stripes,
+                     double* __restrict__ metrics, int64_t* __restrict__ step_counter) {
+  if (hist && blockIdx.x == 0) auc_hist_block(hist, nbins, hist_stripes, metrics, step_counter);
+  const int lane = threadIdx.x & 63;
+  const int64_t n = dev_len(n_dev, n_host);
+  const int64_t U = dev_len(n_uniq, u_cap);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  double dnnz = 0, wsum = 0, dsum = 0;
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~63); i0 < n;
+       i0 += stride) {
+    const int64_t i = i0 + lane;
+    const bool valid = i < n;
+    int32_t s = -3;
+    float x[1] = {0.f};
+    if (valid) {
+      s = segid[i];
+      const int32_t q = pos_s[i];
+      if (in_range(q, p_cap)) x[0] = psum[q];
+    }
+    const int32_t s_next = i + 1 < n ? segid[i + 1] : -1;
+    const int32_t s_prev0 = i0 > 0 ? segid[i0 - 1] : -1;
+    seg_scan_step<0x111, 0xf>(s, x);
+    seg_scan_step<0x112, 0xf>(s, x);
+    seg_scan_step<0x114, 0xf>(s, x);
+    seg_scan_step<0x118, 0xf>(s, x);
+    seg_scan_step<0x142, 0xa>(s, x);
+    seg_scan_step<0x143, 0xc>(s, x);
+    const int32_t s_lane0 = __builtin_amdgcn_readfirstlane(s);
+    if (!(valid && (s_next != s || lane == 63))) continue;
+    const int64_t u = (int64_t)s - 1;
+    if (u < 0 || u >= U) continue;
+    const bool starts_inside = s != s_lane0 || s_prev0 != s;
+    float g = x[0];
+    bool apply = starts_inside && s_next != s;
+    if (!apply) {  // a piece of a key spanning several 64-entry chunks
+      atomicAdd(&grad[u], g);
+      const int64_t e0 = seg_start[u], e1 = seg_start[u + 1];
+      const int32_t np = (int32_t)((e1 - 1) / 64 - e0 / 64 + 1);
+      __threadfence();
+      if (atomicAdd(&pieces[u], 1) == np - 1) {
+        __threadfence();
+        g = __hip_atomic_load(&grad[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        apply = true;
+      }
+    }
+    if (!apply) continue;
+    const int64_t si = slot_idx[u];
+    if (!in_range(si, cap)) continue;
+    const float gs = g * p.grad_scale;
+    if (gs != gs) continue;  // NaN mark = filtered entry
+    Slot sl = slots[si];
+    const float w_old = apply_update(sl, gs, p);
+    slots[si] = sl;
+    dnnz += (double)((sl.w != 0.f) - (w_old != 0.f));
+    wsum += (double)sl.w * sl.w;
+    const double d = (double)sl.w - w_old;
+    dsum += d * d;
+  }
+  if (stats) {
+    const double a = wave_sum_dpp(dnnz), b = wave_sum_dpp(wsum), c = wave_sum_dpp(dsum);
+    if (lane == 63) {
+      double* st = acc_stripe(stats, acc_stripes);
+      if (a != 0) atomicAdd(&st[0], a);
+      if (b != 0) atomicAdd(&st[1], b);
+      if (c != 0) atomicAdd(&st[2], c);
     }
   }
 }
@@ -941,8 +1031,8 @@ size_t tploc_temp_bytes(int64_t n, int bits) {
 void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
                  int32_t* dcnt, uint16_t* rep, int32_t* pos_s, int32_t* segid, uint64_t* uniq,
                  int32_t* seg_start, int32_t* ent_uid, int32_t* local_col, int32_t* n_uniq,
-                 int32_t* n_ent, float* grad, int32_t* err, int64_t u_cap, uint64_t* prof,
-                 hipStream_t st) {
+                 int32_t* n_ent, float* grad, int32_t* pieces, int32_t* err, int64_t u_cap,
+                 uint64_t* prof, hipStream_t st) {
   if (n <= 0) return;
   if (!tploc_supported(n, m.bits)) throw std::runtime_error("localize_tp: unsupported size");
   if (temp_bytes < tploc_temp_bytes(n, m.bits)) throw std::runtime_error("localize_tp: temp");
@@ -963,7 +1053,7 @@ void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t te
   PSAMD_HIP_CHECK(hipGetLastError());
   tp_bucket_kernel<<<(unsigned)g.nbk, tp::kBkThr, 0, st>>>(
       tkeys, toff, g.nbk, (int)g.T, g.shift, status, epoch, pos_s, segid, uniq, seg_start, ent_uid,
-      n_uniq, n_ent, grad, u_cap, g.N, err, prof);
+      n_uniq, n_ent, grad, pieces, u_cap, g.N, err, prof);
   PSAMD_HIP_CHECK(hipGetLastError());
   if (local_col) {  // (skipped when the fused forward reads the entry map directly)
     tp_gather_kernel<<<(unsigned)((n + 1023) / 1024), 256, 0, st>>>(rep, ent_uid, n, local_col);
@@ -1015,7 +1105,7 @@ void tp_fwd_bwd(const uint16_t* rep, const int32_t* dcnt, const int32_t* ent_uid
                 const float* labels, int64_t B, int loss_type, float* coef_out, double* metrics,
                 uint32_t* hist, int nbins, int acc_stripes, int hist_stripes, float* psum,
                 const int32_t* pos_s, const int32_t* segid, const int32_t* n_ent, float* grad,
-                int64_t grad_cap, hipStream_t st) {
+                int64_t grad_cap, bool reduce, hipStream_t st) {
   if (n <= 0) return;
   if (!tp_fwd_bwd_supported(width) || n != B * (int64_t)width)
     throw std::runtime_error("tp_fwd_bwd: unsupported width or n != B * width");
@@ -1039,8 +1129,26 @@ void tp_fwd_bwd(const uint16_t* rep, const int32_t* dcnt, const int32_t* ent_uid
   }
 #undef PSAMD_FB
   PSAMD_HIP_CHECK(hipGetLastError());
+  if (!reduce) return;  // (the caller runs tp_seg_update instead)
   tp_seg_reduce_kernel<<<grid_for(g.N, 256, 2048), 256, 0, st>>>(pos_s, segid, g.N, n_ent, psum,
                                                                  g.N, grad, grad_cap);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void tp_seg_update(const int32_t* pos_s, const int32_t* segid, int64_t n, const int32_t* n_ent,
+                   const float* psum, const int32_t* seg_start, const int32_t* n_uniq, float* grad,
+                   int32_t* pieces, int64_t u_cap, const int64_t* slot_idx, void* slots,
+                   int64_t cap, int algo, int lr_type, float alpha, float beta, float l1, float l2,
+                   float grad_scale, float max_delta, double* stats, int acc_stripes,
+                   uint32_t* hist, int nbins, int hist_stripes, double* metrics,
+                   int64_t* step_counter, hipStream_t st) {
+  if (n <= 0) return;
+  if (hist && nbins != 2048) throw std::runtime_error("tp_seg_update: the fused AUC needs 2048 bins");
+  const TpGeom g = tp_geom(n, 31);
+  UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
+  tp_seg_update_kernel<<<grid_for(g.N, 256, 2048), 256, 0, st>>>(
+      pos_s, segid, g.N, n_ent, psum, g.N, seg_start, n_uniq, grad, pieces, u_cap, slot_idx,
+      (Slot*)slots, cap, p, stats, acc_stripes, hist, nbins, hist_stripes, metrics, step_counter);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

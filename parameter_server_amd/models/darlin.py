@@ -152,6 +152,8 @@ class Block:
     gu: object = None      # device [G | U] buffer of the block (GPU)
     busy: bool = False     # gu holds a launched, not yet consumed gradient
     unique_rows: bool = False  # no example has two entries in the block (dual w/o atomics)
+    row_mode: bool = False     # narrow block: row-order gradient (bcd.grad_rows)
+    fx_k: int = 0              # its fixed-point scale 2^k
 
     @property
     def ncols(self):
@@ -477,6 +479,11 @@ class DarlinTrainer:
         # has ~1 entry per block, so its margin update walks ym sequentially
         # (coalesced, uncontended atomics) instead of gathering it in column order
         self.col_r, self.row_r, self.val_r = self.col, self.row, self.val
+        # workgroups of the row-order gradient (3 per CU) and its partial-sum buffer
+        self.rows_W = 768
+        rows_max = hipops().bcd_rows_max_cols() if dev.type == "cuda" else 0
+        self.rows_part = (torch.empty(self.rows_W * 2 * max(rows_max, 1), dtype=torch.int64,
+                                      device=dev) if dev.type == "cuda" else None)
         if dev.type == "cuda" and self.nnz:
             self.col_r, self.row_r = torch.empty_like(self.col), torch.empty_like(self.row)
             self.val_r = None if self.val is None else torch.empty_like(self.val)
@@ -492,6 +499,11 @@ class DarlinTrainer:
                 self.col_r[p0:p1] = self.col[p0:p1][perm]
                 if self.val is not None:
                     self.val_r[p0:p1] = self.val[p0:p1][perm]
+                # narrow blocks: gradient in row order too (sequential ym / y reads)
+                if 0 < blk.ncols <= rows_max:
+                    vmax = 1.0 if self.val is None else float(self.val[p0:p1].abs().max())
+                    blk.row_mode = True
+                    blk.fx_k = bcd.fixed_point_shift(p1 - p0, vmax)
         # model state (replicated per rank) and margins
         f64 = torch.float64
         self.w = torch.full((base,), float(cfg.init_w), dtype=f64, device=dev)
@@ -512,6 +524,17 @@ class DarlinTrainer:
         return self.shard and (self.cfg.shard_server == "on"
                                or b.ncols >= self.cfg.shard_min_cols)
 
+    def _grad(self, b: Block, G, U, zeroed: bool):
+        """Block gradient into G / U: row order for narrow blocks, the load-balanced
+        column-order kernel otherwise."""
+        if b.row_mode:
+            bcd.grad_rows(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, self.ym,
+                          self.y, self.delta, self.active, G, U, self.rows_part, self.rows_W,
+                          b.fx_k)
+            return
+        bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
+                 self.delta, self.active, G, U, chunks=b.chunks, zeroed=zeroed)
+
     def _launch(self, b: Block):
         if self._sharded(b):
             return self._launch_sharded(b)
@@ -522,8 +545,7 @@ class DarlinTrainer:
         if zeroed:
             b.busy = True
         G, U = GU[:b.ncols], GU[b.ncols:]
-        bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
-                 self.delta, self.active, G, U, chunks=b.chunks, zeroed=zeroed)
+        self._grad(b, G, U, zeroed)
         work = self.comm.all_reduce_async(GU) if self.G > 1 else None
         return (b, GU, work, zeroed)
 
@@ -559,9 +581,7 @@ class DarlinTrainer:
         P = m * self.G
         dev = self.device
         GU = torch.zeros(2 * P, dtype=torch.float64, device=dev)
-        bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
-                 self.delta, self.active, GU[:b.ncols], GU[P:P + b.ncols], chunks=b.chunks,
-                 zeroed=True)
+        self._grad(b, GU[:b.ncols], GU[P:P + b.ncols], True)
         mine = torch.empty(2 * m, dtype=torch.float64, device=dev)
         w1 = self.comm.reduce_scatter_async(mine[:m], GU[:P])
         w2 = self.comm.reduce_scatter_async(mine[m:], GU[P:])

@@ -44,12 +44,15 @@ class FMConfig:
     embedding_dim: int = 16              # k (fm.m: 5; multiple of 8 for the row kernels)
     slots: int = 39                      # keys per example
     minibatch: int = 10000               # fm.m: m = 10000
-    emb_lr: float = 0.2                  # eta_v (row-wise AdaGrad)
+    # eta_v (row-wise AdaGrad: the first step moves every coordinate by ~eta_v, and 741
+    # slot pairs add up: .2 over-shoots; Criteo-shaped B = 16384, 50 steps: .2 -> loss
+    # .613 AUC .741, .02 with eta_w = .05 -> .523 / .797, profiles/r3_train_sweep.log)
+    emb_lr: float = 0.02
     emb_init_scale: float = 0.01         # sigma
     lambda_v: float = 10.0               # L2 on V (once per unique key and step, as fm.m)
-    # linear weights: AdaGrad eta_w = .1 with L2 lambda_w = 1 (proximal form)
-    wide: UpdateRule = field(default_factory=lambda: UpdateRule("adagrad", "constant", 0.1, 1e-6,
-                                                                 0.0, 1.0))
+    # linear weights: AdaGrad eta_w = .05 with L2 lambda_w = 1 (proximal form)
+    wide: UpdateRule = field(default_factory=lambda: UpdateRule("adagrad", "constant", 0.05,
+                                                                 1e-6, 0.0, 1.0))
     table_capacity: int = 0
     table_load: float = 0.5
     max_table_bytes: int = 96 << 30

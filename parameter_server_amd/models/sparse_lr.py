@@ -40,8 +40,8 @@ from ..ops import fixing_float as ff
 from ..ops.countmin import CountMinSketch
 from ..ops.keymix import key_bits_for, unmix
 from ..ops.kv_table import InitRule, KVTable, UpdateRule, next_pow2
-from ..ops.linear import (AUC_BINS, HIST_STRIPES, accum_total, auc_from_hist, linear_fwd_bwd,
-                          new_accum)
+from ..ops.linear import (AUC_BINS, HIST_STRIPES, accum_total, auc_from_hist, fused_update_ok,
+                          linear_fwd_bwd, new_accum)
 from ..ops.localize import Localizer
 from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
@@ -104,13 +104,20 @@ class SparseLRConfig:
 
 # Per-algorithm server defaults for the pushed minibatch-SUM gradients (the reference's
 # push format, async_sgd.h:263-289). FTRL-proximal is the reference CTR online config
-# (example/linear/ctr/online_l1lr.conf: L1 10 / L2 1, DECAY alpha .01 beta 10).
+# (example/linear/ctr/online_l1lr.conf: L1 10 / L2 1, DECAY alpha .01 beta 10). AdaGrad
+# normalises by the accumulated gradient norm like FTRL, so the same step trains. Plain
+# SGD takes the raw minibatch sum: a hot key's gradient is ~B x larger than a rare
+# key's, and with G workers an owner applies up to G pushes of a key per step, so its
+# step is 30x smaller (benchmarks/train_check.py, 65,536 x 39 Criteo-shaped, 50 steps:
+# alpha .01 diverges at 1 GPU (loss 4.7); .001 trains at 1 GPU (0.556) but diverges with
+# 8 asynchronous peers + 2-byte fixing-float (2.56); .0003 trains there (0.621, AUC .734);
+# profiles/r3_train_sweep.log).
 ALGO_DEFAULTS = {
     "ftrl": dict(lr_type="decay", alpha=0.01, beta=10.0, l1=10.0, l2=1.0, grad_scale=1.0,
                  max_delta=0.0),
     "adagrad": dict(lr_type="decay", alpha=0.01, beta=10.0, l1=10.0, l2=1.0, grad_scale=1.0,
                     max_delta=0.0),
-    "sgd": dict(lr_type="decay", alpha=0.01, beta=10.0, l1=10.0, l2=1.0, grad_scale=1.0,
+    "sgd": dict(lr_type="decay", alpha=0.0003, beta=10.0, l1=10.0, l2=1.0, grad_scale=1.0,
                 max_delta=0.0),
 }
 
@@ -286,6 +293,19 @@ class SparseLRTrainer:
             self._prefetch = None
         _cmp = trace_range("compute")
         _cmp.__enter__()
+        if push[0] == "local" and push[2] is not None and fused_update_ok(
+                loc, w_local, B=B, width=width or 0, row_ptr=row_ptr, rows=rows) and \
+                os.environ.get("PSAMD_FUSED_UPDATE", "1") != "0":
+            # 1 GPU: the entry scan applies the FTRL / AdaGrad / SGD update and the AUC
+            # epilogue itself (tp_seg_update)
+            linear_fwd_bwd(loc, w_local, labels, B=B, width=width, vals=vals, loss=self.cfg.loss,
+                           coef=self.coef[:B], metrics=self.metrics, hist=self.hist,
+                           update=(self.table.slots, push[1], self.rule, self.stats,
+                                   self.step_dev))
+            _cmp.__exit__(None, None, None)
+            self.step_count += 1
+            self.examples += B
+            return
         coef, grad = linear_fwd_bwd(loc, w_local, labels, B=B, width=width or 0, row_ptr=row_ptr,
                                     rows=rows, vals=vals, loss=self.cfg.loss, coef=self.coef[:B],
                                     metrics=self.metrics, hist=self.hist)

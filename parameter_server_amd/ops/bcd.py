@@ -99,6 +99,30 @@ def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, act
     return G, U
 
 
+def grad_rows(col_r, row_r, val_r, p0: int, p1: int, c0: int, ncols: int, ym, y, delta,
+              active, G, U, part, W: int, k2: int):
+    """Block gradient of a NARROW block (ncols <= ``hipops().bcd_rows_max_cols()``) from
+    the row-sorted entries: sequential per-row reads, LDS fixed-point column sums at
+    scale 2^k2 (``fixed_point_shift`` of the block's entry count), W workgroup partials
+    in ``part`` reduced in a
+    fixed order (deterministic). Same result as ``grad`` up to the 2^-k2 quantisation."""
+    if is_gpu(ym):
+        hipops().bcd_grad_rows(col_r, row_r, val_r, p0, p1, c0, ncols, ym, y, delta, active,
+                               int(k2), int(W), part, G, U)
+        return G, U
+    return grad(col_r, row_r, val_r, p0, p1, c0, ncols, ym, y, delta, active, G, U)
+
+
+def fixed_point_shift(entries: int, max_abs_val: float) -> int:
+    """k such that the sum of ALL of a block's ``entries`` addends (|g| <= |v|,
+    |u| <= v^2 / 4) stays below 2^61 at scale 2^k (grad_rows: the per-workgroup
+    partials and their reduction are exact int64 sums)."""
+    import math
+
+    bound = max(1.0, max_abs_val, 0.25 * max_abs_val * max_abs_val) * max(1, entries)
+    return max(0, min(60, 61 - math.ceil(math.log2(bound))))
+
+
 def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
            delta_max: float, kkt_thr: float, dw=None, vio=None, consume: bool = False,
            nan_filtered: bool = False):

@@ -132,22 +132,40 @@ def linear_backward(loc, coef, *, B: int, width: int = 0, rows=None, vals=None, 
     return loc.grad, loc.hess
 
 
+def _tp_fused(loc, w_local, B, width, row_ptr, rows) -> bool:
+    t = getattr(loc, "tile", None)
+    return (t is not None and t.ent_uid is not None and row_ptr is None and rows is None
+            and bool(width) and loc.nnz == B * width and is_gpu(w_local)
+            and hipops().tp_fwd_bwd_supported(width))
+
+
 def linear_fwd_bwd(loc, w_local, labels, *, B: int, width: int = 0, row_ptr=None, rows=None,
-                   vals=None, loss="logit", coef=None, metrics=None, hist=None):
+                   vals=None, loss="logit", coef=None, metrics=None, hist=None, update=None):
     """Forward (loss, dL/dm, metrics, AUC histogram) and backward into loc.grad of one
     minibatch; returns (coef, grad). A fixed-width "tp" localisation runs ONE fused
     per-tile kernel plus the entry scan (tploc.hip tp_fwd_bwd: no per-occurrence
     local-column gather, no coef round trip through memory); anything else runs
-    linear_forward + linear_backward."""
-    t = getattr(loc, "tile", None)
-    if (t is not None and t.ent_uid is not None and row_ptr is None
-            and rows is None and width and loc.nnz == B * width and is_gpu(w_local)
-            and hipops().tp_fwd_bwd_supported(width)):
+    linear_forward + linear_backward.
+
+    ``update = (slots, slot_idx, rule, stats, step_counter)`` (tp path only): the entry
+    scan also applies the optimizer update to every key's slot and folds the step's
+    AUC epilogue (tp_seg_update: no grad round trip, one launch less); returns
+    (coef, None). Check ``fused_update_ok`` first."""
+    if _tp_fused(loc, w_local, B, width, row_ptr, rows):
+        t = loc.tile
         coef = torch.empty(B, dtype=torch.float32, device=w_local.device) if coef is None else coef
         hipops().tp_fwd_bwd(t.rep, t.dcnt, t.ent_uid, loc.nnz, width, vals, w_local, labels, B,
                             loss_id(loss), coef, metrics, hist, AUC_BINS, t.psum, loc.pos_s,
-                            loc.segid, t.n_ent, loc.grad)
+                            loc.segid, t.n_ent, loc.grad, update is None)
+        if update is not None:
+            slots, slot_idx, rule, stats, step_counter = update
+            hipops().tp_seg_update(loc.pos_s, loc.segid, loc.nnz, t.n_ent, t.psum, loc.seg_start,
+                                   loc.n_uniq, loc.grad, t.pieces, slot_idx, slots, *rule.args(),
+                                   stats, hist, metrics, step_counter)
+            return coef, None
         return coef, loc.grad
+    if update is not None:
+        raise ValueError("a fused update needs the tp forward/backward (fused_update_ok)")
     from .localize import ensure_local_col
 
     _, coef, _ = linear_forward(ensure_local_col(loc), w_local, labels, B=B, width=width,
@@ -155,6 +173,13 @@ def linear_fwd_bwd(loc, w_local, labels, *, B: int, width: int = 0, row_ptr=None
                                 metrics=metrics, hist=hist)
     grad, _ = linear_backward(loc, coef, B=B, width=width, rows=rows, vals=vals)
     return coef, grad
+
+
+def fused_update_ok(loc, w_local, *, B: int, width: int = 0, row_ptr=None, rows=None) -> bool:
+    """Can ``linear_fwd_bwd(..., update=...)`` run (tp localisation with its pieces
+    counters, fixed width, GPU)?"""
+    return (_tp_fused(loc, w_local, B, width, row_ptr, rows)
+            and getattr(loc.tile, "pieces", None) is not None)
 
 
 def auc_from_hist(hist: torch.Tensor, metrics: torch.Tensor, step_counter=None):

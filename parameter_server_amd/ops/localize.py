@@ -52,6 +52,7 @@ class TileInfo:
     psum: torch.Tensor   # float [tiles*8192] per-entry partial gradients (backward scratch)
     ent_uid: torch.Tensor | None = None  # int32 [tiles*8192] tile entry -> unique id
     cols_ready: bool = True  # False: local_col not materialised yet (ensure_local_col)
+    pieces: torch.Tensor | None = None  # int32 [U] zeroed per localisation (tp_seg_update)
 
 
 def ensure_local_col(loc: "Localized") -> torch.Tensor:
@@ -118,6 +119,7 @@ class Localizer:
             self.t_nent = torch.zeros(1, dtype=torch.int32, device=dev)
             self.grad = torch.empty(N, dtype=torch.float32, device=dev)
             self.t_psum = torch.empty(N, dtype=torch.float32, device=dev)
+            self.t_pieces = i32(N)
             self.hess = None
             self.err = torch.zeros(1, dtype=torch.int32, device=dev)
             return
@@ -195,10 +197,10 @@ class Localizer:
             H.localize_tp(keys, self.bits, self.ptemp, self.t_dcnt, self.t_rep, self.pos_s,
                           self.segid, self.uniq, self.seg_start, self.t_ent_uid,
                           None if self.lazy_cols else self.local_col,
-                          self.n_uniq, self.t_nent, self.grad, self.err,
+                          self.n_uniq, self.t_nent, self.grad, self.t_pieces, self.err,
                           getattr(self, "tp_prof", None))
             tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum, self.t_ent_uid,
-                            not self.lazy_cols)
+                            not self.lazy_cols, self.t_pieces[:n])
             # unique keys <= n: expose n-sized views (the workspace is tile-rounded)
             return Localized(self.uniq[:n], self.seg_start, self.pos_s, self.segid,
                              self.local_col[:n], self.n_uniq, self.grad[:n], None, n, tile=tile)

@@ -139,3 +139,38 @@ def test_kv_update_folds_the_auc_epilogue():
     oa, ob = torch.argsort(a[0]), torch.argsort(b[0])
     for x, y in zip(a, b):
         assert torch.equal(x[oa], y[ob])
+
+
+@pytest.mark.parametrize("algo", ["ftrl", "adagrad", "sgd"])
+def test_fused_seg_update_matches_scan_then_update(algo, monkeypatch):
+    """1 GPU: the entry scan that applies the optimizer update itself (tp_seg_update,
+    hot keys combined by piece counting) trains the same table as tp_seg_reduce +
+    kv_update: same keys, weights and state to float rounding, same metrics."""
+    from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+    from parameter_server_amd.models.sparse_lr import algo_defaults
+
+    B = 16384
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("PSAMD_FUSED_UPDATE", fused)
+        cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B, table_capacity=1 << 22, algo=algo,
+                             **algo_defaults(algo))
+        tr = SparseLRTrainer(cfg, device=DEV)
+        assert tr.localize_mode == "tp"
+        for t in range(6):
+            k, lab = criteo_batch(B, seed=21, row0=t * B, num_features=cfg.num_features,
+                                  device=DEV)
+            tr.step(k, lab, width=39)
+        p = tr.progress()
+        keys, w, z, n = tr.table.occupied()
+        o = torch.argsort(keys)
+        outs.append((p, keys[o].cpu(), w[o].cpu(), z[o].cpu(), n[o].cpu()))
+    (pa, ka, wa, za, na), (pb, kb, wb, zb, nb) = outs
+    assert torch.equal(ka, kb)
+    torch.testing.assert_close(wa, wb, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(za, zb, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(na, nb, rtol=1e-4, atol=1e-4)
+    assert pa["examples"] == pb["examples"] == 6 * B
+    assert pa["loss"] == pytest.approx(pb["loss"], rel=1e-4)
+    assert pa["auc"] == pytest.approx(pb["auc"], abs=1e-3)
+    assert pa["nnz_w"] == pytest.approx(pb["nnz_w"], abs=3)
