@@ -249,12 +249,45 @@ __device__ __forceinline__ void bcd_gu(int64_t i, int64_t c, int64_t c0,
   }
 }
 
+// rowq[i] = {-y_i tau_i, tau_i (1 - tau_i)}: the per-example factors of G / U packed in
+// one 16-B record, recomputed per wide block (bcd_rowq_kernel, a 4 M-row stream), so the
+// random per-entry gather fetches ONE line instead of two (ym and y) and skips the
+// exp: the wide blocks' gradient is bound by these gathers.
+__global__ void __launch_bounds__(256)
+bcd_rowq_kernel(const double* __restrict__ ym, const float* __restrict__ y, int64_t n,
+                double2* __restrict__ rowq) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const double tau = 1.0 / (1.0 + exp(ym[i]));
+    rowq[i] = make_double2(-(double)y[i] * tau, tau * (1.0 - tau));
+  }
+}
+
+__device__ __forceinline__ void bcd_gu_q(int64_t i, const int32_t* __restrict__ row,
+                                         const float* __restrict__ val,
+                                         const double2* __restrict__ rowq, int64_t nrows,
+                                         double dl, double& g, double& u) {
+  const int32_t r = row[i];
+  if (!in_range(r, nrows)) return;
+  const double2 q = rowq[r];
+  if (val) {
+    const double v = (double)val[i];
+    g += q.x * v;
+    u += fmin(q.y * exp(fabs(v) * dl), 0.25) * v * v;
+  } else {
+    g += q.x;
+    u += fmin(q.y * dl, 0.25);  // binary: dl is exp(delta) here
+  }
+}
+
+template <bool kQ>
 __global__ void __launch_bounds__(256)
 bcd_grad_chunk_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row,
                       const float* __restrict__ val, const int64_t* __restrict__ chunks,
                       int64_t nchunks, int64_t c0, int64_t ncols,
                       const double* __restrict__ ym, const float* __restrict__ y, int64_t nrows,
                       const double* __restrict__ delta, const uint8_t* __restrict__ active,
+                      const double2* __restrict__ rowq,
                       double* __restrict__ G, double* __restrict__ U) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -268,8 +301,14 @@ bcd_grad_chunk_kernel(const int32_t* __restrict__ col, const int32_t* __restrict
       if (c < 0 || c >= ncols || !active[c0 + c]) continue;
       const double dl = delta[c0 + c];
       double g = 0, u = 0;
+      if (kQ) {
+        const double dq = val ? dl : exp(dl);
 #pragma unroll 4
-      for (int64_t i = a + lane; i < b; i += 64) bcd_gu(i, c, c0, row, val, ym, y, nrows, dl, g, u);
+        for (int64_t i = a + lane; i < b; i += 64) bcd_gu_q(i, row, val, rowq, nrows, dq, g, u);
+      } else {
+#pragma unroll 4
+        for (int64_t i = a + lane; i < b; i += 64) bcd_gu(i, c, c0, row, val, ym, y, nrows, dl, g, u);
+      }
       g = wave_allsum(g);
       u = wave_allsum(u);
       if (lane == 0) {
@@ -285,7 +324,14 @@ bcd_grad_chunk_kernel(const int32_t* __restrict__ col, const int32_t* __restrict
     if (valid) {
       c = (int64_t)col[i] - c0;
       if (c < 0 || c >= ncols) c = -1;
-      else if (active[c0 + c]) bcd_gu(i, c, c0, row, val, ym, y, nrows, delta[c0 + c], g, u);
+      else if (active[c0 + c]) {
+        if (kQ) {
+          const double dl = delta[c0 + c];
+          bcd_gu_q(i, row, val, rowq, nrows, val ? dl : exp(dl), g, u);
+        } else {
+          bcd_gu(i, c, c0, row, val, ym, y, nrows, delta[c0 + c], g, u);
+        }
+      }
     }
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -449,15 +495,23 @@ void bcd_grad(const int32_t* col, const int32_t* row, const float* val, int64_t 
 void bcd_grad_chunked(const int32_t* col, const int32_t* row, const float* val,
                       const int64_t* chunks, int64_t nchunks, int64_t c0, int64_t ncols,
                       const double* ym, const float* y, int64_t nrows, const double* delta,
-                      const uint8_t* active, double* G, double* U, bool zeroed,
+                      const uint8_t* active, double* rowq, double* G, double* U, bool zeroed,
                       hipStream_t st) {
   if (!zeroed) {
     fill_async<double>(G, ncols, 0.0, st);
     fill_async<double>(U, ncols, 0.0, st);
   }
   if (nchunks <= 0) return;
-  bcd_grad_chunk_kernel<<<grid_for(nchunks, 4, 16384), 256, 0, st>>>(
-      col, row, val, chunks, nchunks, c0, ncols, ym, y, nrows, delta, active, G, U);
+  if (rowq) {
+    bcd_rowq_kernel<<<grid_for(nrows, 256, 4096), 256, 0, st>>>(ym, y, nrows, (double2*)rowq);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    bcd_grad_chunk_kernel<true><<<grid_for(nchunks, 4, 16384), 256, 0, st>>>(
+        col, row, val, chunks, nchunks, c0, ncols, ym, y, nrows, delta, active,
+        (const double2*)rowq, G, U);
+  } else {
+    bcd_grad_chunk_kernel<false><<<grid_for(nchunks, 4, 16384), 256, 0, st>>>(
+        col, row, val, chunks, nchunks, c0, ncols, ym, y, nrows, delta, active, nullptr, G, U);
+  }
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -48,7 +48,7 @@ void tp_fwd_bwd(const uint16_t*, const int32_t*, const int32_t*, int64_t, int, c
                 int, int, float*, const int32_t*, const int32_t*, const int32_t*, float*, int64_t,
                 bool, hipStream_t);
 void tp_seg_update(const int32_t*, const int32_t*, int64_t, const int32_t*, const float*,
-                   const int32_t*, const int32_t*, float*, int32_t*, int64_t, const int64_t*, void*,
+                   const int32_t*, const int32_t*, unsigned long long*, int64_t, const int64_t*, void*,
                    int64_t, int, int, float, float, float, float, float, float, double*, int,
                    uint32_t*, int, int, double*, int64_t*, hipStream_t);
 int64_t tploc_stride(int64_t);
@@ -56,7 +56,7 @@ bool tploc_supported(int64_t, int);
 size_t tploc_temp_bytes(int64_t, int);
 void localize_tp(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint16_t*, int32_t*,
                  int32_t*, uint64_t*, int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, float*,
-                 int32_t*, int32_t*, int64_t, uint64_t*, hipStream_t);
+                 unsigned long long*, int32_t*, int64_t, uint64_t*, hipStream_t);
 void tp_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int, const float*,
                  const float*, int64_t, float*, const int32_t*, const int32_t*, const int32_t*,
                  float*, int64_t, hipStream_t);
@@ -161,7 +161,7 @@ void bcd_grad(const int32_t*, const int32_t*, const float*, int64_t, int64_t, in
               double*, hipStream_t);
 void bcd_grad_chunked(const int32_t*, const int32_t*, const float*, const int64_t*, int64_t,
                       int64_t, int64_t, const double*, const float*, int64_t, const double*,
-                      const uint8_t*, double*, double*, bool, hipStream_t);
+                      const uint8_t*, double*, double*, double*, bool, hipStream_t);
 void bcd_update(int64_t, int64_t, double*, double*, double*, double*, uint8_t*, double*, double,
                 double, double, double, unsigned long long*, bool, bool, hipStream_t);
 void bcd_replica(int64_t, int64_t, int64_t, int64_t, double*, double*, double*, uint8_t*, double,
@@ -481,7 +481,8 @@ PYBIND11_MODULE(_hipops, m) {
                        ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<uint64_t>(uniq),
                        ptr<int32_t>(seg_start), ptr<int32_t>(ent_uid), lc,
                        ptr<int32_t>(n_uniq), ptr<int32_t>(n_ent), ptr<float>(grad),
-                       optr<int32_t>(pieces, at::kInt, "pieces"), ptr<int32_t>(err), uniq.numel(),
+                       reinterpret_cast<unsigned long long*>(optr<int64_t>(pieces, at::kLong, "pieces")),
+                       ptr<int32_t>(err), uniq.numel(),
                        reinterpret_cast<uint64_t*>(optr<int64_t>(prof, at::kLong, "prof")),
                        cur_stream());
   });
@@ -509,7 +510,7 @@ PYBIND11_MODULE(_hipops, m) {
                        ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), cur_stream());
   });
   m.def("tp_seg_update", [](Tensor pos_s, Tensor segid, int64_t n, Tensor n_ent, Tensor psum,
-                            Tensor seg_start, Tensor n_uniq, Tensor grad, Tensor pieces,
+                            Tensor seg_start, Tensor n_uniq, Tensor pieces,
                             Tensor slot_idx, Tensor slots, int algo, int lr_type, double alpha,
                             double beta, double l1, double l2, double grad_scale,
                             double max_delta, optional<Tensor> stats, optional<Tensor> hist,
@@ -520,8 +521,7 @@ PYBIND11_MODULE(_hipops, m) {
     chk(psum, at::kFloat, "psum");
     chk(seg_start, at::kInt, "seg_start");
     chk(n_uniq, at::kInt, "n_uniq");
-    chk(grad, at::kFloat, "grad");
-    chk(pieces, at::kInt, "pieces");
+    chk(pieces, at::kLong, "pieces");
     chk(slot_idx, at::kLong, "slot_idx");
     const int64_t cap = slot_capacity(slots);
     check(n > 0, "tp_seg_update: n > 0");
@@ -529,7 +529,7 @@ PYBIND11_MODULE(_hipops, m) {
     const int64_t N = psamd::tploc_stride(n);
     check(pos_s.numel() >= N && segid.numel() >= N && psum.numel() >= N &&
               seg_start.numel() >= N + 1, "tp_seg_update: entry buffers < stride");
-    const int64_t ucap = std::min({grad.numel(), pieces.numel(), slot_idx.numel()});
+    const int64_t ucap = std::min(pieces.numel(), slot_idx.numel());
     uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
     double* mp = optr<double>(metrics, at::kDouble, "metrics");
     constexpr int kBins = 2048;
@@ -537,7 +537,8 @@ PYBIND11_MODULE(_hipops, m) {
                   "tp_seg_update: hist = stripes x 2 x 2048 (<= 8 stripes) with metrics");
     psamd::tp_seg_update(ptr<int32_t>(pos_s), ptr<int32_t>(segid), n, ptr<int32_t>(n_ent),
                          ptr<float>(psum), ptr<int32_t>(seg_start), ptr<int32_t>(n_uniq),
-                         ptr<float>(grad), ptr<int32_t>(pieces), ucap, ptr<int64_t>(slot_idx),
+                         reinterpret_cast<unsigned long long*>(pieces.data_ptr()), ucap,
+                         ptr<int64_t>(slot_idx),
                          slots.data_ptr(), cap, algo, lr_type, (float)alpha, (float)beta,
                          (float)l1, (float)l2, (float)grad_scale, (float)max_delta,
                          optr<double>(stats, at::kDouble, "stats"), acc_stripes_of(stats), hp,
@@ -1384,7 +1385,8 @@ PYBIND11_MODULE(_hipops, m) {
   };
   m.def("bcd_grad_chunked", [](Tensor col, Tensor row, optional<Tensor> val, Tensor chunks,
                                 int64_t c0, int64_t ncols, Tensor ym, Tensor y, Tensor delta,
-                                Tensor active, Tensor G, Tensor U, bool zeroed) {
+                                Tensor active, Tensor G, Tensor U, bool zeroed,
+                                optional<Tensor> rowq) {
     // chunks: [n + 1] int64 entry offsets (bit 62 = hot chunk), built and range-checked
     // on the host once per block (models/darlin.py build_chunks)
     chk(col, at::kInt, "col");
@@ -1404,10 +1406,12 @@ PYBIND11_MODULE(_hipops, m) {
     check(delta.numel() == active.numel(), "delta/active size mismatch");
     check(c0 >= 0 && ncols >= 0 && c0 + ncols <= delta.numel(), "column block outside model");
     check(G.numel() >= ncols && U.numel() >= ncols, "G/U too small");
+    double* rq = optr<double>(rowq, at::kDouble, "rowq");
+    if (rq) check(rowq->numel() >= 2 * ym.numel(), "rowq: 2 doubles per example");
     psamd::bcd_grad_chunked(ptr<int32_t>(col), ptr<int32_t>(row), vp, ptr<int64_t>(chunks),
                             chunks.numel() - 1, c0, ncols, ptr<double>(ym), ptr<float>(y),
-                            ym.numel(), ptr<double>(delta), ptr<uint8_t>(active), ptr<double>(G),
-                            ptr<double>(U), zeroed, cur_stream());
+                            ym.numel(), ptr<double>(delta), ptr<uint8_t>(active), rq,
+                            ptr<double>(G), ptr<double>(U), zeroed, cur_stream());
   });
   m.def("bcd_grad", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                 int64_t p1, int64_t c0, int64_t ncols, Tensor ym, Tensor y,

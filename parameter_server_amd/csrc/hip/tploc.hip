@@ -271,7 +271,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
                  uint64_t* __restrict__ uniq, int32_t* __restrict__ seg_start,
                  int32_t* __restrict__ ent_uid, int32_t* __restrict__ n_uniq,
                  int32_t* __restrict__ n_ent, float* __restrict__ zero_a,
-                 int32_t* __restrict__ zero_b, int64_t u_cap, int64_t e_cap,
+                 unsigned long long* __restrict__ zero_b, int64_t u_cap, int64_t e_cap,
                  int32_t* __restrict__ err, uint64_t* __restrict__ prof) {
   using namespace tp;
 #define TP_MARK(k) \
@@ -390,11 +390,26 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     if (ent[q] != ~0ull) dl[wd++] = ent[q];
   __syncthreads();
   TP_MARK(3)
-  // rank sort into hs (the hash is dead): keys are distinct, rank = # smaller keys
+  // rank sort into hs (the hash is dead): keys are distinct, rank = # smaller keys.
+  // Broadcast LDS reads, two keys per 16-B read and four reads in flight (a one-at-a-
+  // time loop waited out the LDS latency on every key). dl[D .. D+7] padded with ~0
+  // (larger than any entry: key < 2^32 in the high word) so the tail needs no test.
+  if (t < 8) dl[D + t] = ~0ull;
+  __syncthreads();
   for (uint32_t i = t; i < D; i += kBkThr) {
     const uint64_t x = dl[i];
     uint32_t r = 0;
-    for (uint32_t q = 0; q < D; ++q) r += dl[q] < x;
+    const uint4* d4 = reinterpret_cast<const uint4*>(dl);
+    for (uint32_t q = 0; q < (D + 7) / 8; ++q) {
+      uint4 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = d4[q * 4 + k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        r += (((uint64_t)v[k].y << 32) | v[k].x) < x;
+        r += (((uint64_t)v[k].w << 32) | v[k].z) < x;
+      }
+    }
     hs[r] = x;
   }
   TP_MARK(4)
@@ -462,7 +477,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
         uniq[u] = ((uint64_t)b << shift) | (uint32_t)(v >> 32);
         seg_start[u] = (int32_t)(ebase + ex);
         if (zero_a) zero_a[u] = 0.f;
-        if (zero_b) zero_b[u] = 0;
+        if (zero_b) zero_b[u] = 0ull;
       }
       cur[slot] = ex;
       jj[slot] = (uint16_t)j;
@@ -705,16 +720,21 @@ tp_seg_reduce_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restric
 // one launch and the grad[] round trip less). The segmented scan of tp_seg_reduce;
 // a key whose entries all lie in one wave's 64-entry chunk has its full gradient in
 // the lane that ends the run, which applies the update to the key's slot at once.
-// A key spanning several chunks (hot keys) adds its pieces to grad[u] and counts them
-// in pieces[u] (both zeroed by the bucket kernel); the piece that completes the count
-// (known from seg_start: chunks spanned) reads the sum back and applies the update.
+// A key spanning several chunks (hot keys: <= #tiles entries, so <= 6 chunks) adds
+// each piece as ONE 64-bit integer atomic to acc[u] (zeroed by the bucket kernel):
+// the piece in fixed point (scale 2^30) shifted left by 8, plus 1 in the low byte. The
+// atomic returns the running (sum, count) together, so the piece that completes the
+// count (chunks spanned, from seg_start) holds the whole sum and applies the update -
+// no fence, no re-read (a device-scope __threadfence writes back the XCD's L2 and made
+// a fence-based version 6x slower than the unfused pair). Binary features only (the
+// host checks): |gradient| <= rows < 2^25 fits the 56-bit fixed-point field.
 // Block 0 also turns the step's AUC histogram into metrics (as kv_update did).
 __global__ void __launch_bounds__(256)
 tp_seg_update_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ segid,
                      int64_t n_host, const int32_t* __restrict__ n_dev,
                      const float* __restrict__ psum, int64_t p_cap,
                      const int32_t* __restrict__ seg_start, const int32_t* __restrict__ n_uniq,
-                     float* __restrict__ grad, int32_t* __restrict__ pieces, int64_t u_cap,
+                     unsigned long long* __restrict__ acc, int64_t u_cap,
                      const int64_t* __restrict__ slot_idx, Slot* __restrict__ slots, int64_t cap,
                      UpdateParams p, double* __restrict__ stats, int acc_stripes,
                      uint32_t* __restrict__ hist, int nbins, int hist_stripes,
@@ -752,13 +772,13 @@ tp_seg_update_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restric
     float g = x[0];
     bool apply = starts_inside && s_next != s;
     if (!apply) {  // a piece of a key spanning several 64-entry chunks
-      atomicAdd(&grad[u], g);
+      const long long fx = __double2ll_rn((double)g * 1073741824.0);  // 2^30
+      const unsigned long long add = ((unsigned long long)fx << 8) + 1ull;
+      const unsigned long long tot = atomicAdd(&acc[u], add) + add;
       const int64_t e0 = seg_start[u], e1 = seg_start[u + 1];
-      const int32_t np = (int32_t)((e1 - 1) / 64 - e0 / 64 + 1);
-      __threadfence();
-      if (atomicAdd(&pieces[u], 1) == np - 1) {
-        __threadfence();
-        g = __hip_atomic_load(&grad[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t np = (uint32_t)((e1 - 1) / 64 - e0 / 64 + 1);
+      if ((uint32_t)(tot & 0xffull) == np) {
+        g = (float)((double)((long long)tot >> 8) * (1.0 / 1073741824.0));
         apply = true;
       }
     }
@@ -1031,8 +1051,8 @@ size_t tploc_temp_bytes(int64_t n, int bits) {
 void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
                  int32_t* dcnt, uint16_t* rep, int32_t* pos_s, int32_t* segid, uint64_t* uniq,
                  int32_t* seg_start, int32_t* ent_uid, int32_t* local_col, int32_t* n_uniq,
-                 int32_t* n_ent, float* grad, int32_t* pieces, int32_t* err, int64_t u_cap,
-                 uint64_t* prof, hipStream_t st) {
+                 int32_t* n_ent, float* grad, unsigned long long* pieces, int32_t* err,
+                 int64_t u_cap, uint64_t* prof, hipStream_t st) {
   if (n <= 0) return;
   if (!tploc_supported(n, m.bits)) throw std::runtime_error("localize_tp: unsupported size");
   if (temp_bytes < tploc_temp_bytes(n, m.bits)) throw std::runtime_error("localize_tp: temp");
@@ -1136,8 +1156,8 @@ void tp_fwd_bwd(const uint16_t* rep, const int32_t* dcnt, const int32_t* ent_uid
 }
 
 void tp_seg_update(const int32_t* pos_s, const int32_t* segid, int64_t n, const int32_t* n_ent,
-                   const float* psum, const int32_t* seg_start, const int32_t* n_uniq, float* grad,
-                   int32_t* pieces, int64_t u_cap, const int64_t* slot_idx, void* slots,
+                   const float* psum, const int32_t* seg_start, const int32_t* n_uniq,
+                   unsigned long long* acc, int64_t u_cap, const int64_t* slot_idx, void* slots,
                    int64_t cap, int algo, int lr_type, float alpha, float beta, float l1, float l2,
                    float grad_scale, float max_delta, double* stats, int acc_stripes,
                    uint32_t* hist, int nbins, int hist_stripes, double* metrics,
@@ -1147,7 +1167,7 @@ void tp_seg_update(const int32_t* pos_s, const int32_t* segid, int64_t n, const 
   const TpGeom g = tp_geom(n, 31);
   UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
   tp_seg_update_kernel<<<grid_for(g.N, 256, 2048), 256, 0, st>>>(
-      pos_s, segid, g.N, n_ent, psum, g.N, seg_start, n_uniq, grad, pieces, u_cap, slot_idx,
+      pos_s, segid, g.N, n_ent, psum, g.N, seg_start, n_uniq, acc, u_cap, slot_idx,
       (Slot*)slots, cap, p, stats, acc_stripes, hist, nbins, hist_stripes, metrics, step_counter);
   PSAMD_HIP_CHECK(hipGetLastError());
 }

@@ -484,6 +484,9 @@ class DarlinTrainer:
         rows_max = hipops().bcd_rows_max_cols() if dev.type == "cuda" else 0
         self.rows_part = (torch.empty(self.rows_W * 2 * max(rows_max, 1), dtype=torch.int64,
                                       device=dev) if dev.type == "cuda" else None)
+        # wide blocks: packed per-example gradient factors (bcd.grad rowq)
+        self.rowq = (torch.empty(2 * self.rows, dtype=torch.float64, device=dev)
+                     if dev.type == "cuda" else None)
         if dev.type == "cuda" and self.nnz:
             self.col_r, self.row_r = torch.empty_like(self.col), torch.empty_like(self.row)
             self.val_r = None if self.val is None else torch.empty_like(self.val)
@@ -533,7 +536,8 @@ class DarlinTrainer:
                           b.fx_k)
             return
         bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
-                 self.delta, self.active, G, U, chunks=b.chunks, zeroed=zeroed)
+                 self.delta, self.active, G, U, chunks=b.chunks, zeroed=zeroed,
+                 rowq=self.rowq if b.chunks is not None else None)
 
     def _launch(self, b: Block):
         if self._sharded(b):

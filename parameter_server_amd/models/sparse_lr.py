@@ -294,7 +294,7 @@ class SparseLRTrainer:
         _cmp = trace_range("compute")
         _cmp.__enter__()
         if push[0] == "local" and push[2] is not None and fused_update_ok(
-                loc, w_local, B=B, width=width or 0, row_ptr=row_ptr, rows=rows) and \
+                loc, w_local, B=B, width=width or 0, row_ptr=row_ptr, rows=rows, vals=vals) and \
                 os.environ.get("PSAMD_FUSED_UPDATE", "1") != "0":
             # 1 GPU: the entry scan applies the FTRL / AdaGrad / SGD update and the AUC
             # epilogue itself (tp_seg_update)

@@ -61,9 +61,11 @@ def build_chunks(colptr, c0: int, c1: int, small: int = 64, hot: int = 4096) -> 
 
 
 def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, active,
-         G=None, U=None, chunks=None, zeroed: bool = False):
+         G=None, U=None, chunks=None, zeroed: bool = False, rowq=None):
     """Block gradient: returns (G, U) fp64[ncols] (inactive columns contribute 0).
     ``chunks`` (device int64 from ``build_chunks``) selects the load-balanced kernel;
+    ``rowq`` (fp64 [2 * rows] scratch, with ``chunks``): the per-example factors are
+    packed first so each entry gathers one 16-B record (wide blocks);
     ``zeroed``: G / U already hold zeros (left by ``update(consume=True)``)."""
     dev = ym.device
     if G is None:
@@ -73,7 +75,7 @@ def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, act
     if is_gpu(ym):
         if chunks is not None:
             hipops().bcd_grad_chunked(col, row, val, chunks, c0, ncols, ym, y, delta, active,
-                                      G, U, zeroed)
+                                      G, U, zeroed, rowq)
         else:
             hipops().bcd_grad(col, row, val, p0, p1, c0, ncols, ym, y, delta, active, G, U)
         return G, U

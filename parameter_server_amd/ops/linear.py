@@ -160,8 +160,8 @@ def linear_fwd_bwd(loc, w_local, labels, *, B: int, width: int = 0, row_ptr=None
         if update is not None:
             slots, slot_idx, rule, stats, step_counter = update
             hipops().tp_seg_update(loc.pos_s, loc.segid, loc.nnz, t.n_ent, t.psum, loc.seg_start,
-                                   loc.n_uniq, loc.grad, t.pieces, slot_idx, slots, *rule.args(),
-                                   stats, hist, metrics, step_counter)
+                                   loc.n_uniq, t.pieces, slot_idx, slots, *rule.args(), stats,
+                                   hist, metrics, step_counter)
             return coef, None
         return coef, loc.grad
     if update is not None:
@@ -175,10 +175,11 @@ def linear_fwd_bwd(loc, w_local, labels, *, B: int, width: int = 0, row_ptr=None
     return coef, grad
 
 
-def fused_update_ok(loc, w_local, *, B: int, width: int = 0, row_ptr=None, rows=None) -> bool:
-    """Can ``linear_fwd_bwd(..., update=...)`` run (tp localisation with its pieces
-    counters, fixed width, GPU)?"""
-    return (_tp_fused(loc, w_local, B, width, row_ptr, rows)
+def fused_update_ok(loc, w_local, *, B: int, width: int = 0, row_ptr=None, rows=None,
+                    vals=None) -> bool:
+    """Can ``linear_fwd_bwd(..., update=...)`` run (tp localisation with its (sum, count)
+    accumulators, fixed width, binary features: |gradient| <= B < 2^25, GPU)?"""
+    return (vals is None and B < (1 << 25) and _tp_fused(loc, w_local, B, width, row_ptr, rows)
             and getattr(loc.tile, "pieces", None) is not None)
 
 

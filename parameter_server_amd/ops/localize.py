@@ -52,7 +52,7 @@ class TileInfo:
     psum: torch.Tensor   # float [tiles*8192] per-entry partial gradients (backward scratch)
     ent_uid: torch.Tensor | None = None  # int32 [tiles*8192] tile entry -> unique id
     cols_ready: bool = True  # False: local_col not materialised yet (ensure_local_col)
-    pieces: torch.Tensor | None = None  # int32 [U] zeroed per localisation (tp_seg_update)
+    pieces: torch.Tensor | None = None  # int64 [U] zeroed per localisation (tp_seg_update)
 
 
 def ensure_local_col(loc: "Localized") -> torch.Tensor:
@@ -119,7 +119,7 @@ class Localizer:
             self.t_nent = torch.zeros(1, dtype=torch.int32, device=dev)
             self.grad = torch.empty(N, dtype=torch.float32, device=dev)
             self.t_psum = torch.empty(N, dtype=torch.float32, device=dev)
-            self.t_pieces = i32(N)
+            self.t_pieces = torch.empty(N, dtype=torch.int64, device=dev)
             self.hess = None
             self.err = torch.zeros(1, dtype=torch.int32, device=dev)
             return
