@@ -200,17 +200,38 @@ bcd_dual_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row
                 const float* __restrict__ val, int64_t p0, int64_t p1, int64_t c0, int64_t ncols,
                 const double* __restrict__ dw, const float* __restrict__ y, double* __restrict__ ym,
                 int64_t nrows) {
-  for (int64_t i = p0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < p1;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t c = (int64_t)col[i] - c0;
-    if (c < 0 || c >= ncols) continue;
-    const double d = dw[c];
-    if (d == 0) continue;
-    const int32_t r = row[i];
-    if (!in_range(r, nrows)) continue;
-    const double x = val ? (double)val[i] : 1.0;
-    if (kUnique) ym[r] += (double)y[r] * d * x;
-    else unsafeAtomicAdd(&ym[r], (double)y[r] * d * x);
+  // kR entries per thread per round with their loads in flight together (entry ->
+  // dw[col] and entry -> row -> y / ym are dependent chains)
+  constexpr int kR = 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = p0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < p1;
+       i0 += (int64_t)kR * stride) {
+    int64_t cc[kR];
+    int32_t rr[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const int64_t i = i0 + q * stride;
+      cc[q] = -1;
+      rr[q] = -1;
+      if (i < p1) {
+        const int64_t c = (int64_t)col[i] - c0;
+        cc[q] = (c >= 0 && c < ncols) ? c : -1;
+        rr[q] = row[i];
+      }
+    }
+    double d[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      d[q] = (cc[q] >= 0 && in_range(rr[q], nrows)) ? dw[cc[q]] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      if (d[q] == 0) continue;
+      const int32_t r = rr[q];
+      const double x = val ? (double)val[i0 + q * stride] : 1.0;
+      if (kUnique) ym[r] += (double)y[r] * d[q] * x;
+      else unsafeAtomicAdd(&ym[r], (double)y[r] * d[q] * x);
+    }
   }
 }
 
@@ -388,28 +409,53 @@ bcd_grad_rows_kernel(const int32_t* __restrict__ col, const int32_t* __restrict_
   const int64_t a = p0 + per * blockIdx.x, b = min(p1, a + per);
   long long* my = acc + (int64_t)((t >> 6) % copies) * stride;
   const double sc = ldexp(1.0, k2);
-#pragma unroll 4
-  for (int64_t i = a + t; i < b; i += blockDim.x) {
-    const int c = col[i] - (int)c0;
-    if (c < 0 || c >= ncols || !cact[c]) continue;
-    const int32_t r = row[i];
-    if (!in_range(r, nrows)) continue;
-    const double tau = 1.0 / (1.0 + exp(ym[r]));
-    const double yr = (double)y[r];
-    const double t2 = tau * (1.0 - tau);
-    double g, u;
-    if (kVal) {
-      const double v = (double)val[i];
-      g = -yr * tau * v;
-      u = fmin(t2 * exp(fabs(v) * cdl[c]), 0.25) * v * v;
-    } else {
-      g = -yr * tau;
-      u = fmin(t2 * cdl[c], 0.25);
+  // kR entries per thread per round, every load of a round in flight before the math
+  // (entries -> rows -> ym / y is a two-deep dependent chain)
+  constexpr int kR = 8;
+  for (int64_t i0 = a + t; i0 < b; i0 += (int64_t)kR * blockDim.x) {
+    int cc[kR];
+    int32_t rr[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const int64_t i = i0 + (int64_t)q * blockDim.x;
+      cc[q] = -1;
+      rr[q] = -1;
+      if (i < b) {
+        const int c = col[i] - (int)c0;
+        cc[q] = (c >= 0 && c < ncols) ? c : -1;
+        rr[q] = row[i];
+      }
     }
-    atomicAdd(reinterpret_cast<unsigned long long*>(&my[c]),
-              (unsigned long long)__double2ll_rn(g * sc));
-    atomicAdd(reinterpret_cast<unsigned long long*>(&my[ncols + c]),
-              (unsigned long long)__double2ll_rn(u * sc));
+    double ymv[kR];
+    float yv[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const bool ok = cc[q] >= 0 && in_range(rr[q], nrows);
+      ymv[q] = ok ? ym[rr[q]] : 0.0;
+      yv[q] = ok ? y[rr[q]] : 0.f;
+      if (!ok) cc[q] = -1;
+    }
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const int c = cc[q];
+      if (c < 0 || !cact[c]) continue;
+      const double tau = 1.0 / (1.0 + exp(ymv[q]));
+      const double yr = (double)yv[q];
+      const double t2 = tau * (1.0 - tau);
+      double g, u;
+      if (kVal) {
+        const double v = (double)val[i0 + (int64_t)q * blockDim.x];
+        g = -yr * tau * v;
+        u = fmin(t2 * exp(fabs(v) * cdl[c]), 0.25) * v * v;
+      } else {
+        g = -yr * tau;
+        u = fmin(t2 * cdl[c], 0.25);
+      }
+      atomicAdd(reinterpret_cast<unsigned long long*>(&my[c]),
+                (unsigned long long)__double2ll_rn(g * sc));
+      atomicAdd(reinterpret_cast<unsigned long long*>(&my[ncols + c]),
+                (unsigned long long)__double2ll_rn(u * sc));
+    }
   }
   __syncthreads();
   long long* out = part + (int64_t)blockIdx.x * stride;
