@@ -203,7 +203,9 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
                 for kind, fn in plan:
                     if kind in late:
                         continue
-                    if kind == "compute" and ncomm == 1 and not waited:  # the resolve
+                    # the resolve (eager collectives: the compute after all-to-all A;
+                    # captured: the graph of all-to-all A + resolve + all-to-all B)
+                    if (kind == "cgraph" or (kind == "compute" and ncomm == 1)) and not waited:
                         xs.wait_event(chain[(t - 1) % E])
                         waited = True
                     fn()
@@ -269,27 +271,83 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
         return iterate, False
     torch.cuda.synchronize()
     t0 = state["t"]
+    held = []  # every captured graph
+
+    def release():
+        torch.cuda.synchronize()
+        for g in held:
+            g.reset()
+        held.clear()
+
+    iterate.release = release
     gp = []
     for b in range(NB):  # t0 % NB == 0: buffer b <-> minibatch t0 + b
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
             prep(b)
         gp.append(g)
+        held.append(g)
 
-    # (the all-to-alls stay eager between the graph replays. Measured and not kept:
-    # capturing them into the graphs too, 8 emulated peers over the 1-rank RCCL
-    # loopback: host issue 0.147 -> 0.089 ms/step but the step stays GPU-bound at
-    # 0.141 ms, and the process hung at exit; profiles/r2_capture_comm.log)
+    # The all-to-alls are captured too (PSAMD_CAPTURE_COMM=0: eager between the graph
+    # replays, as in round 2), so a step issues graph replays and event waits only.
+    # Segments group into as few graphs as their waits allow: the compute before an
+    # exchange's first collective (it need not wait for the previous exchange), then
+    # everything up to the next late segment, whose collectives are ordered as a whole
+    # on the communicator's device chain (wait before the replay, mark after it).
+    # Every graph is released before the process group is destroyed: a live graph
+    # holding RCCL work keeps the communicator's teardown waiting (the round-2 capture
+    # experiment hung at exit that way, profiles/r2_capture_comm.log).
+    cchain = getattr(tr.comm, "chain", None)
+    ccomm = (os.environ.get("PSAMD_CAPTURE_COMM", "1") != "0" and tr.padded
+             and cchain is not None and getattr(tr.comm, "backend", "") != "gloo")
+
+    def graph_of(fns):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
+            for fn in fns:
+                fn()
+        held.append(g)
+        return g.replay
+
+    def chained(rep, n):
+        def f():
+            s = torch.cuda.current_stream(device)
+            cchain.wait(s)
+            rep()
+            cchain.mark(s, n)
+        return f
+
     def capture(plan):
         out = []
-        for kind, fn in plan:  # in order: a segment may bake in buffers the previous
-            if kind in ("compute", "async", "post"):  # one of the same ring entry selected
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
-                    fn()
-                out.append((kind, g.replay))
+        if not ccomm:
+            for kind, fn in plan:  # in order: a segment may bake in buffers the previous
+                if kind in ("compute", "async", "post"):  # one of the same ring entry selected
+                    out.append((kind, graph_of([fn])))
+                else:
+                    out.append((kind, fn))
+            return out
+        grp, hosts = [], []
+
+        def flush():
+            if grp:
+                nc = sum(k == "comm" for k, _ in grp)
+                rep = graph_of([fn for _, fn in grp])
+                out.append(("cgraph", chained(rep, nc)) if nc else ("compute", rep))
+            out.extend(hosts)  # host bookkeeping right after the group it sat in
+            grp.clear()
+            hosts.clear()
+
+        for kind, fn in plan:
+            if kind == "host":
+                hosts.append((kind, fn))
+            elif kind in ("async", "post"):
+                flush()
+                out.append((kind, graph_of([fn])))
             else:
-                out.append((kind, fn))
+                if kind == "comm" and not any(k == "comm" for k, _ in grp):
+                    flush()
+                grp.append((kind, fn))
+        flush()
         return out
 
     for j in range(P):
@@ -447,6 +505,7 @@ def main():
 
     run = one_step
     graph_used = False
+    one_graph = None
     if gpu and G > 1 and not tr.padded:
         # multi-GPU: double-buffered minibatches; minibatch t+1 is generated and
         # localised on a side stream while step t waits for its exchange counts
@@ -506,6 +565,7 @@ def main():
             run()
             torch.cuda.synchronize()
             graph_used = True
+            one_graph = g
         except Exception as e:  # fall back to eager launches
             if rank == 0:
                 print(f"graph capture unavailable ({e!r}); eager", file=sys.stderr)
@@ -598,6 +658,12 @@ def main():
     import torch.distributed as dist
 
     watch.beat("teardown")
+    # graphs first (one holding RCCL work keeps the communicator's teardown waiting)
+    if getattr(run, "release", None) is not None:
+        run.release()
+    if one_graph is not None:
+        one_graph.reset()
+    del run, one_graph
     if dist.is_initialized():
         dist.destroy_process_group()
     watch.stop()

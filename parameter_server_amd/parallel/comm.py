@@ -114,7 +114,9 @@ class _DeviceChain:
 
     def run(self, name, fn):
         self._note(name)
-        if not self.on:
+        if not self.on or torch.cuda.is_current_stream_capturing():
+            # (a collective captured into a HIP graph: the replay of that graph is what
+            # gets ordered, by wait() before it and mark() after it)
             return fn()
         cur = torch.cuda.current_stream(self.device)
         if self.ev is not None:
@@ -126,6 +128,23 @@ class _DeviceChain:
         # record that preceded it)
         self.ev.record(cur)
         return out
+
+    def wait(self, stream):
+        """``stream`` waits for the last chained collective (before replaying a graph
+        that contains collectives)."""
+        if self.on and self.ev is not None:
+            stream.wait_event(self.ev)
+
+    def mark(self, stream, n: int = 1):
+        """The work just issued on ``stream`` (a graph replay holding ``n``
+        collectives) is now the last chained collective."""
+        self.n += n
+        self.last = "graph"
+        if not self.on:
+            return
+        if self.ev is None:
+            self.ev = torch.cuda.Event()
+        self.ev.record(stream)
 
     def run_async(self, name, fn, tensors=()):
         self._note(name)

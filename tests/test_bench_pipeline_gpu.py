@@ -50,11 +50,16 @@ def _weights(tr):
     ("prep", 2, 1, {"consistency": "ssp:1"}), ("prep", 2, 1, {"consistency": "ssp:2"}),
     ("prep", 3, 1, {"consistency": "bsp"}),
     ("prep", 2, 1, {"fixing_float_bytes": 2}), ("prep", 2, 1, {"push_mode": "aggregate"}),
-    ("prep", 2, 1, {"algo": "adagrad"})])
+    ("prep", 2, 1, {"algo": "adagrad"}),
+    ("prep", 2, 1, {"_env": {"PSAMD_CAPTURE_COMM": "0"}}),
+    ("prep", 3, 1, {"consistency": "bsp", "_env": {"PSAMD_CAPTURE_COMM": "0"}})])
 def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     from parameter_server_amd.ops.synthetic import criteo_batch
 
     monkeypatch.setenv("PSAMD_XCHG_STREAM", xmode)
+    kw = dict(kw)
+    for k, v in kw.pop("_env", {}).items():  # (default: collectives captured in the graphs)
+        monkeypatch.setenv(k, v)
     bench = _bench()
     B, N, seed, extra = 4096, 10 ** 6, 77, 5
     dev = torch.device("cuda")
@@ -115,3 +120,23 @@ def test_asp_pipeline_trains(monkeypatch, apply):
     p = tr.progress()
     assert 0.0 < p["loss"] < 0.7 and p["nnz_w"] > 0
     tr.table.check_ok()
+
+
+@pytest.mark.parametrize("consistency", ["asp", "bsp", "ssp:4"])
+def test_bench_captured_collectives_exit_cleanly(consistency):
+    """bench.py with emulated peers over the real 1-rank RCCL communicator: the
+    all-to-alls replay inside the step graphs, and the process exits (graphs released
+    before the process group is destroyed; round 2's capture attempt hung at exit)."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, PSAMD_CAPTURE_COMM="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "20",
+                        "--warmup", "6", "--emulate-peers", "4", "--minibatch", "16384",
+                        "--consistency", consistency],
+                       capture_output=True, text=True, timeout=100, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["config"]["hip_graph"] and out["config"]["emulated_peers"] == 4
+    assert out["comm"]["rccl_world"] == 1
