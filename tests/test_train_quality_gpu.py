@@ -1,0 +1,69 @@
+"""Every benchmarked configuration must train: 50 minibatches of
+synthetic Criteo-shaped data (B = 65,536, 10^9 hashed features) from zero init,
+the progressive loss / AUC of the last 10 minibatches must beat a constant
+predictor by a margin (loss < 0.65, AUC > 0.7), for each server algorithm with its
+default hyper-parameters (``sparse_lr.algo_defaults``), at 1 GPU (bsp) and at 8
+emulated peers (asp + fixing-float 2 B: bench.py's config 4'), and for the FM model.
+The reference's defaults these mirror: src/app/linear_method/async_sgd.h:101-124,
+learning_rate.h:15-22."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+STEPS, WINDOW, B = 50, 10, 65536
+
+
+def _lr(algo, mode):
+    from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+    from parameter_server_amd.models.sparse_lr import algo_defaults
+    from parameter_server_amd.ops.synthetic import criteo_batch
+    from parameter_server_amd.parallel.comm import LoopbackComm
+
+    dev = torch.device("cuda", 0)
+    emu = mode == "e8asp2"
+    cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, algo=algo,
+                         consistency="asp" if emu else "bsp",
+                         fixing_float_bytes=2 if emu else 0, table_capacity=1 << 26,
+                         **algo_defaults(algo))
+    tr = SparseLRTrainer(cfg, LoopbackComm(8, dev) if emu else None, dev)
+    keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
+    labels = torch.empty(B, dtype=torch.float32, device=dev)
+    for t in range(STEPS):
+        criteo_batch(B, seed=1000003, row0=t * B, num_features=10 ** 9, device=dev, keys=keys,
+                     labels=labels)
+        tr.step(keys, labels, width=39)
+        if t + 1 == STEPS - WINDOW:
+            tr.progress(reset=True)
+    if emu:
+        tr.flush()
+    return tr.progress(reset=True)
+
+
+@pytest.mark.parametrize("mode", ["1", "e8asp2"])
+@pytest.mark.parametrize("algo", ["ftrl", "adagrad", "sgd"])
+def test_sparse_lr_trains(algo, mode):
+    p = _lr(algo, mode)
+    assert p["loss"] < 0.65 and p["auc"] > 0.7, p
+    assert p["loss"] < math.log(2)
+
+
+def test_fm_trains():
+    from parameter_server_amd.models.fm import FMConfig, FMTrainer
+    from parameter_server_amd.ops.synthetic import criteo_batch
+
+    dev = torch.device("cuda", 0)
+    Bf = 16384
+    tr = FMTrainer(FMConfig(num_features=10 ** 9, minibatch=Bf, table_capacity=1 << 24), None, dev)
+    keys = torch.empty(Bf * 39, dtype=torch.int64, device=dev)
+    labels = torch.empty(Bf, dtype=torch.float32, device=dev)
+    for t in range(STEPS):
+        criteo_batch(Bf, seed=77, row0=t * Bf, num_features=10 ** 9, device=dev, keys=keys,
+                     labels=labels)
+        tr.step(keys, labels)
+        if t + 1 == STEPS - WINDOW:
+            tr.progress(reset=True)
+    p = tr.progress(reset=True)
+    assert p["loss"] < 0.65 and p["auc"] > 0.7, p
