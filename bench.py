@@ -297,9 +297,17 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     # Every graph is released before the process group is destroyed: a live graph
     # holding RCCL work keeps the communicator's teardown waiting (the round-2 capture
     # experiment hung at exit that way, profiles/r2_capture_comm.log).
+    # PSAMD_CAPTURE_COMM: 1 = capture, 0 = eager, auto (default) = capture when the
+    # communicator is the 1-rank RCCL loopback of emulated peers (validated there,
+    # tests/test_bench_pipeline_gpu.py) and eager for a real multi-rank RCCL group,
+    # where graph-captured all-to-alls have not run on this project's hardware yet (a
+    # hang there would cost the whole scaling run; PSAMD_CAPTURE_COMM=1 opts in)
     cchain = getattr(tr.comm, "chain", None)
-    ccomm = (os.environ.get("PSAMD_CAPTURE_COMM", "1") != "0" and tr.padded
-             and cchain is not None and getattr(tr.comm, "backend", "") != "gloo")
+    cmode = os.environ.get("PSAMD_CAPTURE_COMM", "auto")
+    multi = torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1
+    ccomm = (tr.padded and cchain is not None and getattr(tr.comm, "backend", "") != "gloo"
+             and (cmode == "1" or (cmode == "auto" and not multi)))
+    pipeline.captured_comm = ccomm
 
     def graph_of(fns):
         g = torch.cuda.CUDAGraph()
@@ -630,6 +638,8 @@ def main():
                 "push": args.push_mode if G > 1 else None,
                 "table_slots_per_gpu": tr.table.capacity,
                 "hip_graph": graph_used,
+                "collectives_in_graphs": bool(getattr(pipeline, "captured_comm", False)
+                                              and graph_used),
                 "prep_streams": args.prep_streams if (gpu and args.pipeline) else 1,
                 "localize": tr.localize_mode,
                 "emulated_peers": G if emulated else None,

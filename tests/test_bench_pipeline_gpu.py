@@ -139,4 +139,5 @@ def test_bench_captured_collectives_exit_cleanly(consistency):
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert out["config"]["hip_graph"] and out["config"]["emulated_peers"] == 4
+    assert out["config"]["collectives_in_graphs"]
     assert out["comm"]["rccl_world"] == 1
