@@ -232,16 +232,18 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
 }
 
 // ---------------------------------------------------------------------- bucket
-// One workgroup per bucket b (a range of the mixed key space) dedups the bucket AND
-// writes its slice of the global outputs (the separate emit pass and its global round
-// trip of per-bucket key / start / entry lists are gone):
-//   gather+insert  the bucket's entries from every tile (flat: each thread locates its
-//                  entries by binary search over the per-tile run prefix and loads them
-//                  together; the entry ids stay in registers), each key inserted into an
-//                  LDS hash with an entry count
-//   compact        occupied slots -> (key | count | slot) list; the bucket's distinct
-//                  and entry counts are PUBLISHED for the look-back
-//   rank sort      distinct keys are unique: rank = number of smaller keys
+// One workgroup per COARSE bucket c: the fine buckets 2c and 2c+1 of the tile kernel's
+// counting sort (a range of the mixed key space; the two runs of a tile are adjacent,
+// so the pair is one run per tile). It dedups the pair AND writes its slice of the
+// global outputs:
+//   build          the entries from every tile (flat: each thread locates its entries
+//                  by binary search over the per-tile run prefix and loads them
+//                  together; the entry ids stay in registers), each key (suffix plus the
+//                  fine bucket's low bit above it) inserted into an LDS hash with an entry
+//                  count, then the occupied slots compacted -> (key | count | slot) list;
+//                  the pair's distinct and entry counts are PUBLISHED for the look-back
+//   rank sort      distinct keys are unique: rank = number of smaller keys (2 or 4
+//                  threads per key when they are few)
 //   look-back      one wave derives the bucket's global bases (unique ids, entries) from
 //                  the earlier buckets' published counts (decoupled look-back: 64 status
 //                  words per step, nearest inclusive prefix ends it) and publishes its
@@ -250,6 +252,12 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
 //   assign         every entry takes the next position of its key's segment (LDS
 //                  atomic: the order inside a segment is not fixed) -> entry CSC
 //                  (pos_s, segid), ent_uid
+// Pairs: 1024 workgroups of 512 threads at 40 KB of LDS are ONE round on the 256 CUs
+// (2048 single buckets were two rounds, 43 us; profiles/r3_tp_phases.log). A pair whose
+// entries overflow the LDS capacity (or its hash) falls back to its two fine buckets one
+// after the other: count both, publish, look back, then build / sort / write each again.
+// The fine geometry (<= 1280 occurrences per fine bucket) keeps that fallback exact even
+// when every key is distinct.
 // Workgroups are dispatched in blockIdx order, so a bucket only ever waits for buckets
 // that are running or done; the spin is bounded anyway (err bit 4, no hang). The status
 // words carry an 8-bit launch epoch (device counter, advanced by the last bucket), so
@@ -259,56 +267,43 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
 namespace tp {
 constexpr uint64_t kStA = 1, kStP = 2;  // status flags: aggregate / inclusive prefix
 constexpr uint32_t kStM = (1u << 27) - 1;
+constexpr int kG = (kECapL + kBkThr - 1) / kBkThr;  // entries per thread
 }  // namespace tp
 __device__ __forceinline__ uint64_t tp_status(uint32_t ep, uint64_t flag, uint32_t d, uint32_t e) {
   return ((uint64_t)ep << 56) | (flag << 54) | ((uint64_t)(d & tp::kStM) << 27) | (e & tp::kStM);
 }
 
-__global__ void __launch_bounds__(tp::kBkThr)
-tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbk,
-                 int T, int shift, uint64_t* __restrict__ status, uint32_t* __restrict__ epoch,
-                 int32_t* __restrict__ pos_s, int32_t* __restrict__ segid,
-                 uint64_t* __restrict__ uniq, int32_t* __restrict__ seg_start,
-                 int32_t* __restrict__ ent_uid, int32_t* __restrict__ n_uniq,
-                 int32_t* __restrict__ n_ent, float* __restrict__ zero_a,
-                 unsigned long long* __restrict__ zero_b, int64_t u_cap, int64_t e_cap,
-                 int32_t* __restrict__ err, uint64_t* __restrict__ prof) {
+// Build the dedup state of fine buckets [f0, f0 + nf) (nf = 2: a pair; the key inserted
+// is (hb + fine bucket - f0) << shift | suffix). Leaves: eh[g] = hash slot of entry g,
+// idx[] = tile entry ids (registers), hkey / hcnt = the hash, dl[0..D) = the compacted
+// occupied slots. Returns (block-uniform) whether every entry found a slot within the
+// LDS capacity; *E / *D = entries / distinct keys.
+__device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
+                                            const uint16_t* __restrict__ toff, int nbf, int T,
+                                            int shift, int f0, int nf, uint32_t hb,
+                                            uint32_t* hkey, uint32_t* hcnt, uint64_t* dl,
+                                            uint16_t* eh, uint32_t* lds, uint32_t* flag,
+                                            int32_t (&idx)[tp::kG], uint32_t* E_out,
+                                            uint32_t* D_out, uint64_t* prof) {
   using namespace tp;
-#define TP_MARK(k) \
-  if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 12 + (k)] = clock64();
-  TP_MARK(0)
-  if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 12 + 8] = __builtin_amdgcn_s_memrealtime();
-  // 40,944 B of LDS (<= 40 KB: 4 workgroups of 512 threads per CU)
-  __shared__ uint16_t eh[kECapL];   // hash slot of every gathered entry
-  __shared__ uint64_t hs[kDH];      // hash (key u32 | count u32), then the sorted list
-  __shared__ uint64_t dl[kDH];      // per-tile runs (tpre / tlo, until the inserts), then
-                                    // compacted (key | count << 16 | slot), then cur/jj
-  __shared__ uint32_t lds[kBkThr / 64 + 1];
-  __shared__ uint32_t sb[3];        // epoch, unique base, entry base
-  static_assert((kMaxT + 1) * 4 + kMaxT * 2 <= kDH * 8, "tile runs must fit in dl");
+  const int t = threadIdx.x;
   uint32_t* tpre = reinterpret_cast<uint32_t*>(dl);                // [kMaxT + 1]
   uint16_t* tlo = reinterpret_cast<uint16_t*>(tpre + kMaxT + 1);  // [kMaxT]
-  uint32_t* hkey = reinterpret_cast<uint32_t*>(hs);
-  uint32_t* hcnt = hkey + kDH;
-  uint32_t* cur = reinterpret_cast<uint32_t*>(dl);    // [kDH] per slot, after the sort
-  uint16_t* jj = reinterpret_cast<uint16_t*>(cur + kDH);  // [kDH] per slot
-  const int t = threadIdx.x, b = blockIdx.x;
-  if (t == 0) {
-    uint32_t ep = (__hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u) & 0xffu;
-    sb[0] = ep ? ep : 1u;
-  }
+  uint16_t* tmid = tlo + kMaxT;                                   // [kMaxT]
   for (int s = t; s < kDH; s += kBkThr) {
     hkey[s] = kEmpty;
     hcnt[s] = 0;
   }
-  // per-tile runs [toff[q][b], toff[q][b+1]): thread t owns tiles [t*per, t*per + per)
+  if (t == 0) *flag = 0;
+  // per-tile runs [toff[q][f0], toff[q][f0 + nf]): thread t owns tiles [t*per, t*per + per)
   const int per = (T + kBkThr - 1) / kBkThr;
   const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
   uint32_t c = 0;
   for (int q = q0; q < q1; ++q) {
-    const uint16_t* to = toff + (int64_t)q * (nbk + 1);
-    const uint32_t lo = to[b], hi = to[b + 1];
+    const uint16_t* to = toff + (int64_t)q * (nbf + 1);
+    const uint32_t lo = to[f0], hi = to[f0 + nf];
     tlo[q] = (uint16_t)lo;
+    tmid[q] = (uint16_t)((nf == 2 ? to[f0 + 1] : hi) - lo);
     tpre[q] = hi - lo;
     c += hi - lo;
   }
@@ -321,23 +316,23 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
   }
   if (t == 0) tpre[T] = E;
   __syncthreads();
-  TP_MARK(1)
-  const uint32_t ep = sb[0];
+  if (prof && t == 0) prof[(int64_t)blockIdx.x * 12 + 1] = clock64();
   const uint32_t En = E < (uint32_t)kECapL ? E : (uint32_t)kECapL;
   bool bad = E > (uint32_t)kECapL;
-  constexpr int kG = (kECapL + kBkThr - 1) / kBkThr;  // entries per thread: locate all, then load all
-  int32_t idx[kG];
+  uint32_t hib = 0;  // bit q: entry q lies in the pair's second fine bucket
 #pragma unroll
   for (int q = 0; q < kG; ++q) {
     const uint32_t g = q * kBkThr + t;
     idx[q] = -1;
     if (g < En) {
-      int lo = 0, hi = T - 1;  // last tile with tpre[q] <= g
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (tpre[mid] <= g) lo = mid; else hi = mid - 1;
+      int lo = 0, up = T - 1;  // last tile with tpre[q] <= g
+      while (lo < up) {
+        const int mid = (lo + up + 1) >> 1;
+        if (tpre[mid] <= g) lo = mid; else up = mid - 1;
       }
-      idx[q] = lo * kTile + tlo[lo] + (int32_t)(g - tpre[lo]);
+      const uint32_t off = g - tpre[lo];
+      idx[q] = lo * kTile + tlo[lo] + (int32_t)off;
+      hib |= (off >= tmid[lo] ? 1u : 0u) << q;
     }
   }
   uint32_t kv[kG];
@@ -347,7 +342,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
   for (int q = 0; q < kG; ++q) {
     if (idx[q] < 0) continue;
     const uint32_t g = q * kBkThr + t;
-    const uint32_t key = kv[q];
+    const uint32_t key = kv[q] | ((hb + ((hib >> q) & 1u)) << shift);
     uint32_t h = tp_hash(key) & (kDH - 1);
     bool ok = false;
     for (int p = 0; p < kDH / 2; ++p) {
@@ -365,9 +360,9 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     else bad = true;
     eh[g] = ok ? (uint16_t)h : (uint16_t)0xffffu;
   }
-  if (bad) atomicOr(err, 1);
+  if (bad) atomicOr(flag, 1u);
   __syncthreads();
-  TP_MARK(2)
+  if (prof && t == 0) prof[(int64_t)blockIdx.x * 12 + 2] = clock64();
   // compact the occupied slots (strided: conflict-free LDS reads)
   constexpr int kPer = kDH / kBkThr;  // 4
   uint64_t ent[kPer];
@@ -381,88 +376,89 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     cc += ent[q] != ~0ull;
   }
   uint32_t D;
-  uint32_t wd = tp_block_scan<kBkThr>(cc, lds, &D);
-  if (t == 0)  // publish this bucket's counts (bucket 0: they are its inclusive prefix)
-    __hip_atomic_store(&status[b], tp_status(ep, b == 0 ? kStP : kStA, D, En), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t wd = tp_block_scan<kBkThr>(cc, lds, &D);  // (its barriers: every locate is done)
 #pragma unroll
   for (int q = 0; q < kPer; ++q)
     if (ent[q] != ~0ull) dl[wd++] = ent[q];
+  *E_out = En;
+  *D_out = D;
+  const bool good = *flag == 0u;
   __syncthreads();
-  TP_MARK(3)
-  // rank sort into hs (the hash is dead): keys are distinct, rank = # smaller keys.
-  // Broadcast LDS reads, two keys per 16-B read and four reads in flight (a one-at-a-
-  // time loop waited out the LDS latency on every key). dl[D .. D+7] padded with ~0
-  // (larger than any entry: key < 2^32 in the high word) so the tail needs no test.
-  if (t < 8) dl[D + t] = ~0ull;
+  return good;
+}
+
+// rank sort of dl[0..D) into hs (distinct keys: rank = # smaller keys). Broadcast LDS
+// reads, two keys per 16-B read and four reads in flight; dl[D .. D+7] padded with ~0
+// (larger than any entry: key < 2^32 in the high word) so the tail needs no test. With
+// <= 256 keys, 2 or 4 threads split each key's scan and add their counts in LDS.
+__device__ __forceinline__ void tp_bk_ranksort(uint64_t* dl, uint64_t* hs, uint32_t D) {
+  using namespace tp;
+  const int t = threadIdx.x;
+  if (t < 8 && D + t < (uint32_t)kDH) dl[D + t] = ~0ull;
+  uint32_t* rk = reinterpret_cast<uint32_t*>(hs + 1024);  // beyond any output rank < 256
+  const int tpk = D <= 128 ? 4 : D <= 256 ? 2 : 1;
+  if (tpk > 1 && t < 256) rk[t] = 0;
   __syncthreads();
-  for (uint32_t i = t; i < D; i += kBkThr) {
-    const uint64_t x = dl[i];
-    uint32_t r = 0;
-    const uint4* d4 = reinterpret_cast<const uint4*>(dl);
-    for (uint32_t q = 0; q < (D + 7) / 8; ++q) {
-      uint4 v[4];
+  const uint4* d4 = reinterpret_cast<const uint4*>(dl);
+  const uint32_t nq = (D + 7) / 8;
+  if (tpk > 1) {
+    const int nk = kBkThr / tpk, i = t % nk, h = t / nk;
+    const uint32_t pq = (nq + tpk - 1) / tpk;
+    const uint32_t qa = h * pq, qb = qa + pq < nq ? qa + pq : nq;
+    if ((uint32_t)i < D) {
+      const uint64_t x = dl[i];
+      uint32_t r = 0;
+      for (uint32_t q = qa; q < qb; ++q) {
+        uint4 v[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = d4[q * 4 + k];
+        for (int k = 0; k < 4; ++k) v[k] = d4[q * 4 + k];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        r += (((uint64_t)v[k].y << 32) | v[k].x) < x;
-        r += (((uint64_t)v[k].w << 32) | v[k].z) < x;
-      }
-    }
-    hs[r] = x;
-  }
-  TP_MARK(4)
-  // look-back (wave 0): bases = sums of the earlier buckets' counts
-  if (t < 64) {
-    const int lane = t;
-    uint32_t su = 0, se = 0;
-    if (b > 0) {
-      int j = b - 1;
-      uint32_t spins = 0;
-      while (true) {
-        const int jl = j - lane;  // lane 0 = nearest earlier bucket
-        const uint64_t st =
-            jl >= 0 ? __hip_atomic_load(&status[jl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                    : tp_status(ep, kStP, 0, 0);
-        const uint32_t f = (uint32_t)(st >> 56) == ep ? (uint32_t)(st >> 54) & 3u : 0u;
-        const uint64_t pm = __ballot(f == kStP), nr = __ballot(f == 0);
-        const int fp = pm ? __builtin_ctzll(pm) : 64;  // nearest inclusive prefix
-        const uint64_t need = fp >= 63 ? ~0ull : ((2ull << fp) - 1);
-        if (nr & need) {  // an earlier bucket has not published yet
-          if (++spins > (1u << 22)) {
-            if (lane == 0) atomicOr(err, 4);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
+        for (int k = 0; k < 4; ++k) {
+          r += (((uint64_t)v[k].y << 32) | v[k].x) < x;
+          r += (((uint64_t)v[k].w << 32) | v[k].z) < x;
         }
-        const bool inc = lane <= fp;
-        su += wave_allsum(inc ? (uint32_t)(st >> 27) & kStM : 0u);
-        se += wave_allsum(inc ? (uint32_t)st & kStM : 0u);
-        if (fp < 64) break;
-        j -= 64;
       }
-      if (lane == 0)
-        __hip_atomic_store(&status[b], tp_status(ep, kStP, su + D, se + En), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      atomicAdd(&rk[i], r);
     }
-    if (lane == 0) {
-      sb[1] = su;
-      sb[2] = se;
-      if (b == nbk - 1) {  // every bucket has published: the launch is done with the epoch
-        const uint32_t U = su + D, Et = se + En;
-        *n_uniq = (int32_t)U;
-        *n_ent = (int32_t)Et;
-        if (in_range((int64_t)U, u_cap + 1)) seg_start[U] = (int32_t)Et;
-        __hip_atomic_store(epoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (h == 0 && (uint32_t)i < D) hs[rk[i]] = dl[i];
+  } else {
+    for (uint32_t i = t; i < D; i += kBkThr) {
+      const uint64_t x = dl[i];
+      uint32_t r = 0;
+      for (uint32_t q = 0; q < nq; ++q) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = d4[q * 4 + k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          r += (((uint64_t)v[k].y << 32) | v[k].x) < x;
+          r += (((uint64_t)v[k].w << 32) | v[k].z) < x;
+        }
       }
+      hs[r] = x;
     }
   }
-  __syncthreads();
-  TP_MARK(5)
-  const uint32_t ubase = sb[1], ebase = sb[2];
-  // segment starts in key order -> uniq / seg_start; per slot: sorted index + cursor
+}
+
+// starts + assign: the sorted keys hs[0..D) -> uniq / seg_start from (ubase, ebase);
+// every entry of idx[] takes the next position of its key's segment.
+__device__ __forceinline__ void tp_bk_emit(const uint64_t* hs, uint64_t* dl, const uint16_t* eh,
+                                           const int32_t (&idx)[tp::kG], uint32_t D,
+                                           uint32_t ubase, uint32_t ebase, uint64_t key0,
+                                           uint32_t* lds, int32_t* __restrict__ pos_s,
+                                           int32_t* __restrict__ segid,
+                                           uint64_t* __restrict__ uniq,
+                                           int32_t* __restrict__ seg_start,
+                                           int32_t* __restrict__ ent_uid,
+                                           float* __restrict__ zero_a,
+                                           unsigned long long* __restrict__ zero_b,
+                                           int64_t u_cap, int64_t e_cap, uint64_t* prof) {
+  using namespace tp;
+  const int t = threadIdx.x;
+  uint32_t* cur = reinterpret_cast<uint32_t*>(dl);        // [kDH] per slot
+  uint16_t* jj = reinterpret_cast<uint16_t*>(cur + kDH);  // [kDH] per slot
+  __syncthreads();  // (dl: the rank sort's source is dead)
   uint32_t carry = 0;
   for (uint32_t j0 = 0; j0 < D; j0 += kBkThr) {
     const uint32_t j = j0 + t;
@@ -474,7 +470,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
       const uint32_t slot = (uint32_t)v & 0xffffu;
       const int64_t u = (int64_t)ubase + j;
       if (in_range(u, u_cap)) {
-        uniq[u] = ((uint64_t)b << shift) | (uint32_t)(v >> 32);
+        uniq[u] = key0 | (uint32_t)(v >> 32);
         seg_start[u] = (int32_t)(ebase + ex);
         if (zero_a) zero_a[u] = 0.f;
         if (zero_b) zero_b[u] = 0ull;
@@ -485,7 +481,7 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     carry += tot;
   }
   __syncthreads();
-  TP_MARK(6)
+  if (prof && t == 0) prof[(int64_t)blockIdx.x * 12 + 6] = clock64();
 #pragma unroll
   for (int q = 0; q < kG; ++q) {
     if (idx[q] < 0) continue;
@@ -500,9 +496,270 @@ tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict_
     }
     if (in_range((int64_t)idx[q], e_cap)) ent_uid[idx[q]] = (int32_t)u;
   }
-  TP_MARK(7)
-  if (prof && threadIdx.x == 0) prof[(int64_t)blockIdx.x * 12 + 9] = __builtin_amdgcn_s_memrealtime();
-#undef TP_MARK
+  __syncthreads();
+}
+
+// Decoupled look-back of fine bucket fs (wave 0; the caller syncs after): the bases
+// (sums of every earlier fine bucket's counts) go to sb[1] / sb[2]; the inclusive prefix
+// is published at fs and at twin (a pair's second fine bucket, published empty); the
+// workgroup holding the last fine bucket writes the totals and advances the epoch.
+__device__ __forceinline__ void tp_bk_lookback(uint64_t* __restrict__ status, int fs, int twin,
+                                               int nbf, uint32_t ep, uint32_t D, uint32_t E,
+                                               uint32_t* sb, uint32_t* __restrict__ epoch,
+                                               int32_t* __restrict__ n_uniq,
+                                               int32_t* __restrict__ n_ent,
+                                               int32_t* __restrict__ seg_start, int64_t u_cap,
+                                               int32_t* __restrict__ err) {
+  using namespace tp;
+  const int lane = threadIdx.x;
+  if (lane >= 64) return;
+  uint32_t su = 0, se = 0;
+  if (fs > 0) {
+    int j = fs - 1;
+    uint32_t spins = 0;
+    while (true) {
+      const int jl = j - lane;  // lane 0 = nearest earlier bucket
+      const uint64_t st =
+          jl >= 0 ? __hip_atomic_load(&status[jl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                  : tp_status(ep, kStP, 0, 0);
+      const uint32_t f = (uint32_t)(st >> 56) == ep ? (uint32_t)(st >> 54) & 3u : 0u;
+      const uint64_t pm = __ballot(f == kStP), nr = __ballot(f == 0);
+      const int fp = pm ? __builtin_ctzll(pm) : 64;  // nearest inclusive prefix
+      const uint64_t need = fp >= 63 ? ~0ull : ((2ull << fp) - 1);
+      if (nr & need) {  // an earlier bucket has not published yet
+        if (++spins > (1u << 22)) {
+          if (lane == 0) atomicOr(err, 4);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      const bool inc = lane <= fp;
+      su += wave_allsum(inc ? (uint32_t)(st >> 27) & kStM : 0u);
+      se += wave_allsum(inc ? (uint32_t)st & kStM : 0u);
+      if (fp < 64) break;
+      j -= 64;
+    }
+  }
+  if (lane == 0) {
+    const uint64_t inc = tp_status(ep, kStP, su + D, se + E);
+    if (fs > 0) __hip_atomic_store(&status[fs], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (twin != fs) __hip_atomic_store(&status[twin], inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sb[1] = su;
+    sb[2] = se;
+    if (twin == nbf - 1) {  // every bucket has published: the launch is done with the epoch
+      const uint32_t U = su + D, Et = se + E;
+      *n_uniq = (int32_t)U;
+      *n_ent = (int32_t)Et;
+      if (in_range((int64_t)U, u_cap + 1)) seg_start[U] = (int32_t)Et;
+      __hip_atomic_store(epoch, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Fallback for one fine bucket f of an overflowing pair, register-light (plain loops,
+// no per-thread entry arrays, so it does not raise the common path's register count):
+// the per-tile runs live in the eh region, entries are located again for the assign
+// and find their key's rank by binary search in the sorted list.
+__device__ __forceinline__ void tp_bk_fine_light(
+    const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbf, int T,
+    int shift, int f, uint32_t hb, uint64_t key0, uint32_t* hkey, uint32_t* hcnt, uint64_t* hs,
+    uint64_t* dl, uint16_t* ehraw, uint32_t* lds, uint32_t* sb, uint64_t* __restrict__ status,
+    uint32_t ep, uint32_t* __restrict__ epoch, int32_t* __restrict__ pos_s,
+    int32_t* __restrict__ segid, uint64_t* __restrict__ uniq, int32_t* __restrict__ seg_start,
+    int32_t* __restrict__ ent_uid, int32_t* __restrict__ n_uniq, int32_t* __restrict__ n_ent,
+    float* __restrict__ zero_a, unsigned long long* __restrict__ zero_b, int64_t u_cap,
+    int64_t e_cap, int32_t* __restrict__ err) {
+  using namespace tp;
+  static_assert((kMaxT + 1) * 4 + kMaxT * 2 <= kECapL * 2, "tile runs must fit in eh");
+  const int t = threadIdx.x;
+  uint32_t* tpre = reinterpret_cast<uint32_t*>(ehraw);             // [kMaxT + 1]
+  uint16_t* tlo = reinterpret_cast<uint16_t*>(tpre + kMaxT + 1);  // [kMaxT]
+  for (int s = t; s < kDH; s += kBkThr) {
+    hkey[s] = kEmpty;
+    hcnt[s] = 0;
+  }
+  const int per = (T + kBkThr - 1) / kBkThr;
+  const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
+  uint32_t c = 0;
+  for (int q = q0; q < q1; ++q) {
+    const uint16_t* to = toff + (int64_t)q * (nbf + 1);
+    const uint32_t lo = to[f], hi = to[f + 1];
+    tlo[q] = (uint16_t)lo;
+    tpre[q] = hi - lo;
+    c += hi - lo;
+  }
+  uint32_t E;
+  uint32_t w = tp_block_scan<kBkThr>(c, lds, &E);
+  for (int q = q0; q < q1; ++q) {
+    const uint32_t len = tpre[q];
+    tpre[q] = w;
+    w += len;
+  }
+  if (t == 0) tpre[T] = E;
+  __syncthreads();
+  auto locate = [&](uint32_t g) -> int32_t {
+    int lo = 0, up = T - 1;  // last tile with tpre[q] <= g
+    while (lo < up) {
+      const int mid = (lo + up + 1) >> 1;
+      if (tpre[mid] <= g) lo = mid; else up = mid - 1;
+    }
+    return lo * kTile + tlo[lo] + (int32_t)(g - tpre[lo]);
+  };
+  bool bad = false;
+  for (uint32_t g = t; g < E; g += kBkThr) {
+    const uint32_t key = tkeys[locate(g)] | (hb << shift);
+    uint32_t h = tp_hash(key) & (kDH - 1);
+    bool ok = false;
+    for (int p = 0; p < kDH / 2; ++p) {
+      const uint32_t cu = hkey[h];
+      if (cu == kEmpty) {
+        const uint32_t prev = atomicCAS(&hkey[h], kEmpty, key);
+        if (prev == kEmpty || prev == key) { ok = true; break; }
+      } else if (cu == key) {
+        ok = true;
+        break;
+      }
+      h = (h + 1) & (kDH - 1);
+    }
+    if (ok) atomicAdd(&hcnt[h], 1u);
+    else bad = true;
+  }
+  if (bad) atomicOr(err, 1);
+  __syncthreads();
+  constexpr int kPer = kDH / kBkThr;
+  uint32_t cc = 0;
+  for (int q = 0; q < kPer; ++q) cc += hkey[q * kBkThr + t] != kEmpty;
+  uint32_t D;
+  uint32_t wd = tp_block_scan<kBkThr>(cc, lds, &D);
+  for (int q = 0; q < kPer; ++q) {
+    const int s = q * kBkThr + t;
+    if (hkey[s] != kEmpty) dl[wd++] = ((uint64_t)hkey[s] << 32) | ((uint64_t)hcnt[s] << 16) | (uint64_t)s;
+  }
+  if (t == 0)
+    __hip_atomic_store(&status[f], tp_status(ep, f == 0 ? kStP : kStA, D, E), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  tp_bk_ranksort(dl, hs, D);
+  tp_bk_lookback(status, f, f, nbf, ep, D, E, sb, epoch, n_uniq, n_ent, seg_start, u_cap, err);
+  __syncthreads();
+  const uint32_t ubase = sb[1], ebase = sb[2];
+  uint32_t* cur = reinterpret_cast<uint32_t*>(dl);  // [D] per sorted key
+  uint32_t carry = 0;
+  for (uint32_t j0 = 0; j0 < D; j0 += kBkThr) {
+    const uint32_t j = j0 + t;
+    const uint64_t v = j < D ? hs[j] : 0ull;
+    const uint32_t cnt = (uint32_t)(v >> 16) & 0xffffu;
+    uint32_t tot;
+    const uint32_t ex = tp_block_scan<kBkThr>(cnt, lds, &tot) + carry;
+    if (j < D) {
+      const int64_t u = (int64_t)ubase + j;
+      if (in_range(u, u_cap)) {
+        uniq[u] = key0 | (uint32_t)(v >> 32);
+        seg_start[u] = (int32_t)(ebase + ex);
+        if (zero_a) zero_a[u] = 0.f;
+        if (zero_b) zero_b[u] = 0ull;
+      }
+      cur[j] = ex;
+    }
+    carry += tot;
+  }
+  __syncthreads();
+  for (uint32_t g = t; g < E; g += kBkThr) {
+    const int32_t id = locate(g);
+    const uint32_t key = tkeys[id] | (hb << shift);
+    uint32_t lo = 0, up = D - 1;  // the sorted key's index
+    while (lo < up) {
+      const uint32_t mid = (lo + up) >> 1;
+      if ((uint32_t)(hs[mid] >> 32) < key) lo = mid + 1; else up = mid;
+    }
+    if (D == 0 || (uint32_t)(hs[lo] >> 32) != key) continue;  // (only after an overflow)
+    const uint32_t pos = atomicAdd(&cur[lo], 1u);
+    const uint32_t u = ubase + lo;
+    const int64_t e = (int64_t)ebase + pos;
+    if (in_range(e, e_cap)) {
+      pos_s[e] = id;
+      segid[e] = (int32_t)(u + 1);
+    }
+    if (in_range((int64_t)id, e_cap)) ent_uid[id] = (int32_t)u;
+  }
+  __syncthreads();
+}
+
+// One workgroup per pair of fine buckets (pair = false: per fine bucket). The status
+// words are per FINE bucket: a pair publishes its counts at 2b and an empty aggregate at
+// 2b+1, so the look-back sums the same either way. A pair that overflows the LDS
+// capacity or its hash (nearly distinct keys) processes its two fine buckets one after
+// the other instead (tp_bk_fine_light), each with its own publish and look-back; the
+// fine geometry keeps that exact even when every key is distinct. (Tried and dropped:
+// redoing the whole launch in a gated fine-bucket kernel, +4.8 us per step for the
+// empty launch; the fallback as a second copy of the register-staged path, 95 VGPRs.)
+// (8 waves per SIMD = 4 workgroups per CU: <= 64 VGPRs)
+__global__ void __launch_bounds__(tp::kBkThr, 8)
+tp_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbf,
+                 int pair, int T, int shift, uint64_t* __restrict__ status,
+                 uint32_t* __restrict__ epoch, int32_t* __restrict__ pos_s,
+                 int32_t* __restrict__ segid, uint64_t* __restrict__ uniq,
+                 int32_t* __restrict__ seg_start, int32_t* __restrict__ ent_uid,
+                 int32_t* __restrict__ n_uniq, int32_t* __restrict__ n_ent,
+                 float* __restrict__ zero_a, unsigned long long* __restrict__ zero_b,
+                 int64_t u_cap, int64_t e_cap, int32_t* __restrict__ err,
+                 uint64_t* __restrict__ prof) {
+  using namespace tp;
+  // 40,960 B of LDS (<= 40 KB: 4 workgroups of 512 threads per CU)
+  __shared__ uint16_t eh[kECapL];   // hash slot of every gathered entry
+  __shared__ uint64_t hs[kDH];      // hash (key u32 | count u32), then the sorted list
+  __shared__ uint64_t dl[kDH];      // per-tile runs (until the inserts), then compacted
+                                    // (key | count << 16 | slot), then cur/jj
+  __shared__ uint32_t lds[kBkThr / 64 + 1];
+  __shared__ uint32_t sb[4];        // epoch, unique base, entry base, build flag
+  static_assert((kMaxT + 1) * 4 + kMaxT * 4 <= kDH * 8, "tile runs must fit in dl");
+  uint32_t* hkey = reinterpret_cast<uint32_t*>(hs);
+  uint32_t* hcnt = hkey + kDH;
+  const int t = threadIdx.x, b = blockIdx.x;
+  if (prof && t == 0) {
+    prof[(int64_t)b * 12 + 0] = clock64();
+    prof[(int64_t)b * 12 + 8] = __builtin_amdgcn_s_memrealtime();
+  }
+  if (t == 0) {
+    uint32_t ep = (__hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u) & 0xffu;
+    sb[0] = ep ? ep : 1u;
+  }
+  const int f0 = pair ? 2 * b : b, twin = pair ? f0 + 1 : f0;
+  const uint64_t key0 = (uint64_t)f0 << shift;
+  int32_t idx[kG];
+  uint32_t E, D;
+  const bool good = tp_bk_build(tkeys, toff, nbf, T, shift, f0, pair ? 2 : 1, 0u, hkey, hcnt, dl,
+                                eh, lds, &sb[3], idx, &E, &D, prof);
+  const uint32_t ep = sb[0];
+  if (!good && pair) {
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s)
+      tp_bk_fine_light(tkeys, toff, nbf, T, shift, f0 + s, (uint32_t)s, key0, hkey, hcnt, hs, dl,
+                       eh, lds, sb, status, ep, epoch, pos_s, segid, uniq, seg_start, ent_uid,
+                       n_uniq, n_ent, zero_a, zero_b, u_cap, e_cap, err);
+    return;
+  }
+  if (!good && t == 0) atomicOr(err, 1);
+  if (t == 0) {  // publish (fine bucket 0: its inclusive prefix); a pair's twin is empty
+    if (twin != f0)
+      __hip_atomic_store(&status[twin], tp_status(ep, kStA, 0, 0), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&status[f0], tp_status(ep, f0 == 0 ? kStP : kStA, D, E), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (prof && t == 0) prof[(int64_t)b * 12 + 3] = clock64();
+  tp_bk_ranksort(dl, hs, D);
+  if (prof && t == 0) prof[(int64_t)b * 12 + 4] = clock64();
+  tp_bk_lookback(status, f0, twin, nbf, ep, D, E, sb, epoch, n_uniq, n_ent, seg_start, u_cap, err);
+  __syncthreads();
+  if (prof && t == 0) prof[(int64_t)b * 12 + 5] = clock64();
+  tp_bk_emit(hs, dl, eh, idx, D, sb[1], sb[2], key0, lds, pos_s, segid, uniq, seg_start, ent_uid,
+             zero_a, zero_b, u_cap, e_cap, prof);
+  if (prof && t == 0) {
+    prof[(int64_t)b * 12 + 7] = clock64();
+    prof[(int64_t)b * 12 + 9] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // ---------------------------------------------------------------------- gather
@@ -1071,9 +1328,12 @@ void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t te
     tp_tile_kernel<false><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
                                                               dcnt, rep, err);
   PSAMD_HIP_CHECK(hipGetLastError());
-  tp_bucket_kernel<<<(unsigned)g.nbk, tp::kBkThr, 0, st>>>(
-      tkeys, toff, g.nbk, (int)g.T, g.shift, status, epoch, pos_s, segid, uniq, seg_start, ent_uid,
-      n_uniq, n_ent, grad, pieces, u_cap, g.N, err, prof);
+  // buckets in pairs of fine buckets: one round of workgroups (the pair's key bit above
+  // a <= 30-bit suffix keeps the LDS hash's empty word unreachable)
+  const bool pair = g.nbk >= 2 && g.shift <= 30;
+  tp_bucket_kernel<<<(unsigned)(pair ? g.nbk / 2 : g.nbk), tp::kBkThr, 0, st>>>(
+      tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, status, epoch, pos_s, segid, uniq,
+      seg_start, ent_uid, n_uniq, n_ent, grad, pieces, u_cap, g.N, err, prof);
   PSAMD_HIP_CHECK(hipGetLastError());
   if (local_col) {  // (skipped when the fused forward reads the entry map directly)
     tp_gather_kernel<<<(unsigned)((n + 1023) / 1024), 256, 0, st>>>(rep, ent_uid, n, local_col);

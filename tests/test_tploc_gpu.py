@@ -98,3 +98,23 @@ def test_tploc_34bit_criteo_1e10():
 
     keys, _ = criteo_batch(65536, seed=5, row0=0, num_features=10 ** 10, device=DEV)
     _check(keys.cpu(), 34)
+
+
+def test_tploc_pair_overflow_redo_sequence():
+    """Buckets run in pairs of fine buckets; a pair that overflows (nearly distinct
+    keys) flags the launch and the gated fine-bucket kernel redoes it. The flag carries
+    the launch epoch, so calls before and after in the same workspace are unaffected."""
+    from parameter_server_amd.ops.synthetic import criteo_batch
+
+    n = 65536 * 39
+    crit, _ = criteo_batch(65536, seed=9, row0=0, num_features=10 ** 9, device=DEV)
+    dist = (torch.randperm(1 << 22)[:n].to(torch.int64) * 97 + 11).to(DEV)
+    lz = Localizer(n, 30, DEV, mode="tp")
+    for k in (crit, dist, crit, crit, dist, dist, crit):
+        ref = localize_torch(k.cpu(), 30)
+        loc = lz(k)
+        lz.check()
+        U = loc.num_unique()
+        assert U == ref.uniq.numel()
+        assert torch.equal(loc.uniq[:U].cpu(), ref.uniq)
+        assert torch.equal(loc.local_col.cpu(), ref.local_col)
