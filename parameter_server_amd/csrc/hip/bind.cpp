@@ -52,6 +52,7 @@ void tp_seg_update(const int32_t*, const int32_t*, int64_t, const int32_t*, cons
                    int64_t, int, int, float, float, float, float, float, float, double*, int,
                    uint32_t*, int, int, double*, int64_t*, hipStream_t);
 int64_t tploc_stride(int64_t);
+int tploc_tile();
 bool tploc_supported(int64_t, int);
 size_t tploc_temp_bytes(int64_t, int);
 void localize_tp(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint16_t*, int32_t*,
@@ -470,7 +471,7 @@ PYBIND11_MODULE(_hipops, m) {
     check(psamd::tploc_supported(n, bits), "tp localisation: 2..34 key bits, n <= 5.2M");
     if (lc) check(local_col->numel() >= n, "local_col too small");
     const int64_t N = psamd::tploc_stride(n);
-    const int64_t T = N / 8192;
+    const int64_t T = N / psamd::tploc_tile();
     check(pos_s.numel() >= N && segid.numel() >= N && uniq.numel() >= N &&
               seg_start.numel() >= N + 1 && ent_uid.numel() >= N && grad.numel() >= N,
           "tp localisation buffers < stride");
@@ -498,7 +499,7 @@ PYBIND11_MODULE(_hipops, m) {
     chk(n_ent, at::kInt, "n_ent");
     chk(grad, at::kFloat, "grad");
     const int64_t N = psamd::tploc_stride(n);
-    check(n > 0 && rep.numel() >= n && dcnt.numel() >= N / 8192, "tp backward: rep / dcnt");
+    check(n > 0 && rep.numel() >= n && dcnt.numel() >= N / psamd::tploc_tile(), "tp backward: rep / dcnt");
     check(psum.numel() >= N && pos_s.numel() >= N && segid.numel() >= N, "tp backward buffers");
     const int32_t* r = optr<int32_t>(rows, at::kInt, "rows");
     if (r) check(rows->numel() >= n, "rows too small");
@@ -583,7 +584,7 @@ PYBIND11_MODULE(_hipops, m) {
     check(psamd::tp_fwd_bwd_supported(width) && n == B * (int64_t)width && n > 0,
           "tp_fwd_bwd: fixed width 9..64 (tp_fwd_bwd_supported) and n == B * width");
     const int64_t N = psamd::tploc_stride(n);
-    check(rep.numel() >= n && dcnt.numel() >= N / 8192 && ent_uid.numel() >= N,
+    check(rep.numel() >= n && dcnt.numel() >= N / psamd::tploc_tile() && ent_uid.numel() >= N,
           "tp_fwd_bwd: rep / dcnt / ent_uid");
     check(psum.numel() >= N && pos_s.numel() >= N && segid.numel() >= N, "tp_fwd_bwd buffers");
     check(labels.numel() >= B && coef.numel() >= B, "labels/coef too small");

@@ -38,6 +38,11 @@ namespace psamd {
 
 namespace tp {
 constexpr int kThr = 1024;              // tile workgroup
+// 8192 occurrences per tile (a 65,536 x 39 minibatch is 313 tiles). Measured and not
+// kept: 10,240 (250 tiles, at most one per CU): tile 24.7 -> 24.2 us and fused
+// forward+backward 24.3 -> 23.7, but 136 / 87 KB of LDS per workgroup left no room for
+// the other streams' kernels and the pipelined step went 0.118 -> 0.126 ms
+// (profiles/r3_tile_count.log).
 constexpr int kIt = 8;
 constexpr int kTile = kThr * kIt;       // 8192 occurrences
 constexpr int kHash = 2 * kTile;        // LDS hash slots of a tile (load <= 0.5)
@@ -772,7 +777,7 @@ __global__ void tp_gather_kernel(const uint16_t* __restrict__ rep,
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     const int64_t i = i0 + q * blockDim.x;
-    e[q] = i < n ? (int64_t)((uint32_t)i & ~(uint32_t)(tp::kTile - 1)) + rep[i] : -1;
+    e[q] = i < n ? (i / tp::kTile) * tp::kTile + rep[i] : -1;
   }
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
@@ -1169,7 +1174,7 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
     for (int q = 0; q < PER; ++q)
       if (ce[p][q] == kFbExt) {
         const int64_t i = (r0 + ri) * width + sub + q * kFbLanes;
-        const int32_t u = ent_uid[(i & ~(int64_t)(kTile - 1)) + __float_as_int(cv[p][q])];
+        const int32_t u = ent_uid[(i / kTile) * kTile + __float_as_int(cv[p][q])];
         cv[p][q] = (in_range(u, w_cap) ? w_local[u] : 0.f) * (vals ? vals[i] : 1.f);
       }
   }
@@ -1287,6 +1292,7 @@ static TpGeom tp_geom(int64_t n, int bits) {
 }
 
 int64_t tploc_stride(int64_t n) { return tp_geom(n, 31).N; }
+int tploc_tile() { return tp::kTile; }
 
 bool tploc_supported(int64_t n, int bits) {
   // <= 34 bits: quotient-encoded tile hash; bucket suffixes (bits - log2 nbk) < 32 bits

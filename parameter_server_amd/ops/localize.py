@@ -24,6 +24,8 @@ import torch
 from .keymix import mix, to_unsigned_order
 from .native import hipops, is_gpu
 
+TP_TILE = 8192  # occurrences per tp tile (csrc/hip/tploc.hip tp::kTile)
+
 
 @dataclass
 class Localized:
@@ -47,10 +49,10 @@ class Localized:
 @dataclass
 class TileInfo:
     rep: torch.Tensor    # int16 [nnz] tile-local entry id of every position
-    dcnt: torch.Tensor   # int32 [tiles] distinct keys per 8192-key tile
+    dcnt: torch.Tensor   # int32 [tiles] distinct keys per TP_TILE-key tile
     n_ent: torch.Tensor  # int32[1] total entries (device)
-    psum: torch.Tensor   # float [tiles*8192] per-entry partial gradients (backward scratch)
-    ent_uid: torch.Tensor | None = None  # int32 [tiles*8192] tile entry -> unique id
+    psum: torch.Tensor   # float [tiles*TP_TILE] per-entry partial gradients (backward scratch)
+    ent_uid: torch.Tensor | None = None  # int32 [tiles*TP_TILE] tile entry -> unique id
     cols_ready: bool = True  # False: local_col not materialised yet (ensure_local_col)
     pieces: torch.Tensor | None = None  # int64 [U] zeroed per localisation (tp_seg_update)
 
@@ -78,7 +80,7 @@ class Localizer:
     ``check()`` raises if a bucket overflowed its LDS hash (never for mixed keys of
     realistic batches; the bucket count bounds the distinct keys per bucket).
     ``mode="tp"`` (csrc/hip/tploc.hip, GPU, key bits <= 34, <= 5.2 M keys): LDS dedup of
-    8192-occurrence tiles, then one workgroup per key-range bucket deduplicates the
+    TP_TILE (8192)-occurrence tiles, then one workgroup per key-range bucket deduplicates the
     tile-distinct entries (a hot key is at most one entry per tile) and emits sorted
     unique keys, an entry-level CSC and local columns: 4 launches, no global atomics;
     the backward accumulates per tile in LDS and scans the entry CSC (``TileInfo``).
@@ -111,7 +113,7 @@ class Localizer:
             # zeroed once: the bucket look-back's status words + launch epoch (tploc.hip)
             self.ptemp = torch.zeros(H.tploc_temp_bytes(n, self.bits), dtype=torch.uint8,
                                      device=dev)
-            self.t_dcnt, self.t_rep = i32(N // 8192), torch.empty(n, dtype=torch.int16, device=dev)
+            self.t_dcnt, self.t_rep = i32(N // TP_TILE), torch.empty(n, dtype=torch.int16, device=dev)
             self.pos_s, self.segid, self.t_ent_uid = i32(N), i32(N), i32(N)
             self.seg_start, self.local_col = i32(N + 1), i32(n)
             self.uniq = torch.empty(N, dtype=torch.int64, device=dev)
