@@ -56,3 +56,27 @@ for name, M, N, K in SHAPES:
                       "gemm256p8_us": us_p8, "gemm256p8_tflops": fl / us_p8 / 1e6,
                       "gemm128_tflops": fl / us_old / 1e6, "hipblaslt_tflops": fl / us_lib / 1e6}),
           flush=True)
+
+# weight gradient dW [N_out, K_in] = dZ^T X over B = 16384 rows (MN-major operands):
+# TN 256x256 (transposed LDS reads, split-K) vs the 128x128 split-K kernel vs hipBLASLt
+for name, Bn, No, Ki in [("wd dW0 4992->1024", 16384, 1024, 4992), ("wd dW1 1024->512", 16384, 512, 1024),
+                         ("wd dW2 512->256", 16384, 256, 512)]:
+    g = torch.Generator(device=dev).manual_seed(Bn + No + Ki)
+    dZ = (torch.rand(Bn, No, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+    X = (torch.rand(Bn, Ki, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+    out = torch.zeros(No, Ki, device=dev)
+    S = GM.tn256_splits(No, Ki, Bn)
+    part = torch.empty(S * No * Ki, device=dev)
+    ref = dZ.float().t() @ X.float()
+    H.gemm_tn256(dZ, X, No, Ki, Bn, S, part, out, 0.0)
+    err = ((out - ref).abs() / (ref.abs() + 1)).max().item()
+    fl = 2.0 * Bn * No * Ki
+    us_tn = t(lambda: H.gemm_tn256(dZ, X, No, Ki, Bn, S, part, out, 1.0))
+    sk = GM.auto_splitk(No, Ki, Bn)
+    us_128 = t(lambda: GM.gemm(dZ, False, X, False, No, Ki, Bn, out_bf16=False, out_f32=out,
+                               beta=1.0, splitk=sk))
+    us_lib = t(lambda: torch.mm(dZ.t(), X, out_dtype=torch.float32))
+    print(json.dumps({"shape": name, "M": No, "N": Ki, "K": Bn, "splits": S, "max_rel_err_vs_fp32": err,
+                      "tn256_us": us_tn, "tn256_tflops": fl / us_tn / 1e6,
+                      "gemm128_splitk_us": us_128, "gemm128_tflops": fl / us_128 / 1e6,
+                      "hipblaslt_us": us_lib, "hipblaslt_tflops": fl / us_lib / 1e6}), flush=True)

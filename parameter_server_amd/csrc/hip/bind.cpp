@@ -62,6 +62,9 @@ void tp_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int, 
                  const float*, int64_t, float*, const int32_t*, const int32_t*, const int32_t*,
                  float*, int64_t, hipStream_t);
 // gemm256.hip
+void gemm_tn256(const __bf16*, int64_t, const __bf16*, int64_t, int, int, int, int, float*, float*,
+                float, hipStream_t);
+void transpose_bf16(const void*, int, int, void*, hipStream_t);
 void gemm_nt256(const __bf16*, int64_t, const __bf16*, int64_t, int, int, int, const float*, bool,
                 __bf16*, int64_t, float*, int64_t, int, hipStream_t);
 // kvapi.hip
@@ -728,6 +731,33 @@ PYBIND11_MODULE(_hipops, m) {
                       fp, N, variant, cur_stream());
   }, py::arg("A"), py::arg("B"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bias"),
      py::arg("relu"), py::arg("C"), py::arg("Cf"), py::arg("variant") = 0);
+  // C [M, N] f32 = beta C + A^T B for MN-major A [K, M], B [K, N] (the weight gradient):
+  // split-K partials into part [splits, M, N], then a fixed-order sum (gemm256.hip)
+  m.def("gemm_tn256", [](Tensor A, Tensor B, int64_t M, int64_t N, int64_t K, int64_t splits,
+                         Tensor part, Tensor C, double beta) {
+    chk(A, at::kBFloat16, "A");
+    chk(B, at::kBFloat16, "B");
+    chk(part, at::kFloat, "part");
+    chk(C, at::kFloat, "C");
+    check(M > 0 && N > 0 && K > 0 && K % 64 == 0 && M % 8 == 0 && N % 8 == 0,
+          "gemm_tn256: K % 64, M % 8, N % 8");
+    check(splits >= 1 && splits <= K / 64, "gemm_tn256: 1 <= splits <= K / 64");
+    check(A.numel() >= K * M && B.numel() >= K * N, "gemm_tn256: A [K, M], B [K, N]");
+    check(part.numel() >= splits * M * N && C.numel() >= M * N, "gemm_tn256: part / C size");
+    check(((uintptr_t)A.data_ptr() % 16) == 0 && ((uintptr_t)B.data_ptr() % 16) == 0 &&
+              ((uintptr_t)C.data_ptr() % 16) == 0 && ((uintptr_t)part.data_ptr() % 16) == 0,
+          "gemm_tn256: 16-B aligned operands");
+    psamd::gemm_tn256(ptr<__bf16>(A), M, ptr<__bf16>(B), N, (int)M, (int)N, (int)K, (int)splits,
+                      ptr<float>(part), ptr<float>(C), (float)beta, cur_stream());
+  });
+  m.def("transpose_bf16", [](Tensor in, Tensor out) {
+    chk(in, at::kBFloat16, "in");
+    chk(out, at::kBFloat16, "out");
+    check(in.dim() == 2 && out.numel() >= in.numel(), "transpose_bf16: in [R, C], out [C, R]");
+    const int64_t R = in.size(0), C = in.size(1);
+    check(R % 64 == 0 && C % 64 == 0, "transpose_bf16: R, C multiples of 64");
+    psamd::transpose_bf16(in.data_ptr(), (int)R, (int)C, out.data_ptr(), cur_stream());
+  });
   // ---------------- k-value push / pull API (kvapi.hip) ----------------
   // rows [hdr 4 | keys C*kw | values C*k f32] of H words (pull rows: no values)
   m.def("kvv_pack_vals", [](Tensor vals, int64_t k, Tensor pos_s, Tensor seg_start, Tensor n_uniq,

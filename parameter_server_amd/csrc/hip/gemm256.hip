@@ -575,6 +575,213 @@ gemm_nt256p8_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __r
 #undef GP8_BAR
 #undef GP8_VM
 
+// ---------------------------------------------------------------------------
+// "TN" 256 x 256 kernel for MN-major operands (the weight gradient dW = dZ^T X of a
+// linear layer: both operands are [batch][features] with the reduction over the batch
+// rows):
+//
+//   P[split][m][n] = sum_{k in the split} A[k * lda + m] * B[k * ldb + n]   (fp32)
+//
+// Same geometry as gemm_nt256_kernel (8 waves as 2 x 4, a wave owns 128 x 64, 64
+// v_mfma_f32_16x16x32_bf16 per K-step, LDS-DMA double buffer, one counted wait + one
+// barrier per K-step), but a tile is staged as it lies in memory, [64 k][256 m] with
+// 512-B k-rows, and the MFMA fragments (8 consecutive k of one m per lane) come out of
+// it with ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q, columns
+// 4p..4p+3 of a 4-row x 16-column block, and lane i receives column i of the 4 rows
+// (guide T10); two reads give the 8 k of a fragment. The 16-B chunk c of k-row r sits
+// at chunk c ^ f(r), f(r) = 2 (r & 3) + 8 ((r >> 3) & 1): the 8 rows a 32-lane half reads
+// (two groups 8 rows apart) then cover all 64 banks (conflict-free). LDS-DMA writes
+// lane-linear, so the swizzle is applied to the per-lane global source address.
+// K is split over gridDim.y (K-steps shared out evenly, so any split count): every split
+// writes its own fp32 partial tile (no atomics), gemm_splitk_reduce sums them in a fixed
+// order. Requirements (binding): M, N multiples of 8, K a multiple of 64 with >= 1 K-step
+// per split, 16-B aligned operands, lda / ldb multiples of 8.
+__device__ __forceinline__ int gtn_swz(int r) { return ((r & 3) << 1) | (((r >> 3) & 1) << 3); }
+
+// LDS-DMA of a [64 k][256 cols] tile (k rows k0.., columns c0..) into dst: wave
+// instruction wi fills k-rows 2wi, 2wi+1 (lane l: row 2wi + l/32, chunk position l%32).
+__device__ __forceinline__ void gtn_stage(const __bf16* __restrict__ p, int64_t ld, int cols,
+                                          int c0, int k0, char* dst, int wave, int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int wi = q * 8 + wave;
+    const int r = 2 * wi + (lane >> 5);
+    const int c = (lane & 31) ^ gtn_swz(r);
+    int col = c0 + c * 8;
+    col = col + 8 <= cols ? col : cols - 8;  // (clamped; the stores mask it)
+    const __bf16* src = p + (int64_t)(k0 + r) * ld + col;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(dst + wi * 1024),
+                                     16, 0, 0);
+  }
+}
+
+typedef short gtn_s4 __attribute__((ext_vector_type(4)));
+
+// one transposed read: 4 bf16 (k rows kr..kr+3) of column (cb + lane's i) of the image
+__device__ __forceinline__ gtn_s4 gtn_tr(const char* img, int kr, int cb, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const int r = kr + q;
+  const int col = cb + 4 * p;  // first of the 4 columns this lane addresses
+  const int c = (col >> 3) ^ gtn_swz(r);
+  const char* a = img + r * 512 + c * 16 + (col & 7) * 2;
+  // (the builtin, not inline asm: the compiler then counts the read's lgkmcnt itself)
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) gtn_s4*)(const __attribute__((address_space(3))) char*)a);
+}
+
+__global__ void __launch_bounds__(g256::TH)
+gemm_tn256_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B,
+                  int64_t ldb, int M, int N, int K, float* __restrict__ P, int tiles_n) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];  // 128 KiB
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int id = g256_xcd(blockIdx.x, gridDim.x);
+  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  // split y of S takes K-steps [y * NK / S, (y+1) * NK / S) (any S: uneven by one step)
+  const int NK = K / BK, S = gridDim.y;
+  const int ks0 = (int)((int64_t)blockIdx.y * NK / S), ks1 = (int)((int64_t)(blockIdx.y + 1) * NK / S);
+  const int kb = ks0 * BK;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = ks1 - ks0;
+  gtn_stage(A, lda, M, m0, kb, smem, wave, lane);
+  gtn_stage(B, ldb, N, n0, kb, smem + TILE_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int g = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * BUF_BYTES;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * BUF_BYTES;
+      gtn_stage(A, lda, M, m0, kb + (kt + 1) * BK, nxt, wave, lane);
+      gtn_stage(B, ldb, N, n0, kb + (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kr = ks * 32 + 8 * g;
+      bf16x8 a[8], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cb = wc * 64 + j * 16;
+        const gtn_s4 lo = gtn_tr(cur + TILE_BYTES, kr, cb, lane);
+        const gtn_s4 hi = gtn_tr(cur + TILE_BYTES, kr + 4, cb, lane);
+        b[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int cb = wr * 128 + i * 16;
+        const gtn_s4 lo = gtn_tr(cur, kr, cb, lane);
+        const gtn_s4 hi = gtn_tr(cur, kr + 4, cb, lane);
+        a[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next K-step has landed
+    __syncthreads();                                   // ... and this one is read
+  }
+  // C[m][n]: m = m0 + wr*128 + i*16 + 4*(lane>>4) + r, n = n0 + wc*64 + j*16 + (lane&15)
+  float* out = P + (int64_t)blockIdx.y * M * N;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
+    if (n >= N) continue;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+        if (m < M) out[(int64_t)m * N + n] = acc[i][j][r];
+      }
+  }
+}
+
+// out[i] = beta * out[i] + sum over the S partials (fixed order: deterministic)
+__global__ void __launch_bounds__(256)
+gemm_splitk_reduce_kernel(const float4* __restrict__ P, int S, int64_t n4, float4* __restrict__ out,
+                          float beta) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 a = beta != 0.f ? out[i] : float4{0.f, 0.f, 0.f, 0.f};
+    if (beta != 0.f && beta != 1.f) a = float4{a.x * beta, a.y * beta, a.z * beta, a.w * beta};
+    for (int s = 0; s < S; ++s) {
+      const float4 v = P[(int64_t)s * n4 + i];
+      a.x += v.x;
+      a.y += v.y;
+      a.z += v.z;
+      a.w += v.w;
+    }
+    out[i] = a;
+  }
+}
+
+void gemm_tn256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
+                int splits, float* part, float* out, float beta, hipStream_t st) {
+  if (M <= 0 || N <= 0) return;
+  if (splits < 1 || K % g256::BK != 0 || K / g256::BK < splits || M % 8 || N % 8 || lda % 8 ||
+      ldb % 8)
+    throw std::runtime_error("gemm_tn256: K % 64, K / 64 >= splits, M / N / ld % 8");
+  const int tiles_m = (M + g256::BM - 1) / g256::BM, tiles_n = (N + g256::BN - 1) / g256::BN;
+  dim3 grid(tiles_m * tiles_n, splits);
+  gemm_tn256_kernel<<<grid, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, part, tiles_n);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  const int64_t n4 = (int64_t)M * N / 4;
+  gemm_splitk_reduce_kernel<<<grid_for(n4, 256, 4096), 256, 0, st>>>(
+      reinterpret_cast<const float4*>(part), splits, n4, reinterpret_cast<float4*>(out), beta);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+// out [C, R] = in [R, C]^T, bf16, R and C multiples of 64: a 64 x 64 tile through LDS
+// (rows padded by 8 elements), 16-B loads and stores. The weight copy W^T that lets the
+// input gradient dZ W run on the K-major 256 x 256 kernel (torch's strided copy took
+// ~50 us for 1024 x 4992).
+__global__ void __launch_bounds__(256)
+transpose_bf16_kernel(const uint16_t* __restrict__ in, int R, int C, uint16_t* __restrict__ out) {
+  __shared__ uint16_t tile[64][72];
+  const int t = threadIdx.x;
+  const int tc = blockIdx.x % (C / 64), tr = blockIdx.x / (C / 64);
+  const int r0 = tr * 64, c0 = tc * 64;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int idx = q * 256 + t, r = idx >> 3, ch = idx & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(in + (int64_t)(r0 + r) * C + c0 + ch * 8);
+    *reinterpret_cast<uint4*>(&tile[r][ch * 8]) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int idx = q * 256 + t, j = idx >> 3, ch = idx & 7;  // output row j = input col
+    uint16_t h[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h[e] = tile[ch * 8 + e][j];
+    uint4 v;
+    v.x = h[0] | ((uint32_t)h[1] << 16);
+    v.y = h[2] | ((uint32_t)h[3] << 16);
+    v.z = h[4] | ((uint32_t)h[5] << 16);
+    v.w = h[6] | ((uint32_t)h[7] << 16);
+    *reinterpret_cast<uint4*>(out + (int64_t)(c0 + j) * R + r0 + ch * 8) = v;
+  }
+}
+
+void transpose_bf16(const void* in, int R, int C, void* out, hipStream_t st) {
+  if (R <= 0 || C <= 0) return;
+  if (R % 64 || C % 64) throw std::runtime_error("transpose_bf16: R, C multiples of 64");
+  transpose_bf16_kernel<<<(unsigned)((R / 64) * (C / 64)), 256, 0, st>>>(
+      (const uint16_t*)in, R, C, (uint16_t*)out);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
 void gemm_nt256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
                 const float* bias, bool relu, __bf16* C, int64_t ldc, float* Cf, int64_t ldcf,
                 int variant, hipStream_t st) {

@@ -126,7 +126,11 @@ def linear_input_grad(dZ, W, mask=None, backend: str = "mfma", colsum=None):
         # unmasked long-N input gradient (layer 0): the 256x256 LDS-DMA kernel on a
         # transposed weight copy (10 MB for 1024 x 4992) beats the MN-major 128x128
         # kernel: 750 vs 628 TFLOP/s on 16384 x 4992 x 1024 (profiles/r2_gemm256.log)
-        Wt = W.t().contiguous()
+        if N % 64 == 0 and K % 64 == 0 and W.is_contiguous():
+            Wt = torch.empty(K, N, dtype=torch.bfloat16, device=W.device)
+            hipops().transpose_bf16(W, Wt)  # (~5 us; torch's strided copy ~50 us)
+        else:
+            Wt = W.t().contiguous()
         dX = torch.empty(Bn, K, dtype=torch.bfloat16, device=dZ.device)
         hipops().gemm_nt256(dZ, Wt, Bn, K, N, None, False, dX, None)
         return dX
@@ -147,6 +151,31 @@ def linear_weight_grad(dZ, X, out=None, beta: float = 0.0, backend: str = "mfma"
         else:
             out.mul_(beta).add_(r)
         return out
+    if is_gpu(dZ) and tn256_ok(N, K, Bn) and dZ.is_contiguous() and X.is_contiguous() and \
+            out.is_contiguous():
+        # 256x256 kernel reading both MN-major operands through transposed LDS reads
+        # (gemm256.hip gemm_tn256), split-K partials summed in a fixed order
+        S = tn256_splits(N, K, Bn)
+        part = torch.empty(S * N * K, dtype=torch.float32, device=dZ.device)
+        hipops().gemm_tn256(dZ, X, N, K, Bn, S, part, out, float(beta))
+        return out
     sk = auto_splitk(N, K, Bn) if beta in (0.0, 1.0) else 1
     gemm(dZ, False, X, False, N, K, Bn, out_bf16=False, out_f32=out, beta=beta, splitk=sk)
     return out
+
+
+def tn256_ok(M: int, N: int, K: int) -> bool:
+    """gemm_tn256 takes the weight gradient [M, N] over K batch rows when both output
+    sides fill 256-wide tiles and the batch is a multiple of 64 (>= 8 K-steps)."""
+    import os
+
+    if os.environ.get("PSAMD_TN256", "1") == "0":
+        return False
+    return M >= 256 and N >= 256 and M % 8 == 0 and N % 8 == 0 and K % 64 == 0 and K >= 512
+
+
+def tn256_splits(M: int, N: int, K: int) -> int:
+    """K splits: enough workgroups for the 256 CUs (one 128 KB workgroup each, so at most
+    256 in one round), each split >= 8 K-steps (512 rows)."""
+    tiles = -(-M // 256) * -(-N // 256)
+    return max(1, min(256 // tiles if tiles <= 256 else 1, K // 512))

@@ -3,6 +3,7 @@ import pytest
 import torch
 
 from parameter_server_amd.ops import gemm as G
+from parameter_server_amd.ops.native import hipops
 
 pytestmark = pytest.mark.gpu
 
@@ -83,3 +84,44 @@ def test_input_grad_colsum_epilogue(M, N, K):
     torch.testing.assert_close(cs - 1.0, dX.float().sum(0), rtol=1e-4, atol=1e-2)
     ref = (dZ.float() @ W.float()) * (mask.float() > 0)
     torch.testing.assert_close(dX.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K,S,beta", [(256, 256, 512, 1, 0.0), (512, 1024, 4096, 7, 1.0),
+                                          (1024, 4992, 2048, 3, 1.0), (264, 520, 1024, 2, 0.5),
+                                          (256, 512, 16384, 32, 0.0)])
+def test_gemm_tn256_weight_grad(M, N, K, S, beta):
+    """TN 256x256 kernel (transposed LDS reads of MN-major operands, split-K partials with
+    uneven splits, fixed-order reduce) against fp32: C = beta C + A^T B."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + S)
+    A = (torch.rand(K, M, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+    B = (torch.rand(K, N, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
+    C = torch.randn(M, N, device="cuda", generator=g)
+    ref = A.float().t() @ B.float() + beta * C
+    part = torch.full((S * M * N,), float("nan"), device="cuda")
+    hipops().gemm_tn256(A, B, M, N, K, S, part, C, beta)
+    torch.testing.assert_close(C, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
+
+
+def test_linear_weight_grad_routes_to_tn256():
+    from parameter_server_amd.ops import gemm as GM
+
+    torch.manual_seed(3)
+    Bn, N, K = 4096, 512, 1024
+    dZ = torch.randn(Bn, N, device="cuda").to(torch.bfloat16)
+    X = torch.randn(Bn, K, device="cuda").to(torch.bfloat16)
+    assert GM.tn256_ok(N, K, Bn)
+    out = torch.ones(N, K, device="cuda")
+    GM.linear_weight_grad(dZ, X, out=out, beta=1.0, backend="mfma")
+    ref = dZ.float().t() @ X.float() + 1.0
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3 * Bn ** 0.5)
+    out2 = torch.ones(N, K, device="cuda")
+    GM.linear_weight_grad(dZ, X, out=out2, beta=1.0, backend="mfma")
+    assert torch.equal(out, out2)  # fixed-order split-K sum
+
+
+@pytest.mark.parametrize("R,C", [(64, 64), (1024, 4992), (192, 640)])
+def test_transpose_bf16(R, C):
+    x = torch.randn(R, C, device="cuda").to(torch.bfloat16)
+    y = torch.empty(C, R, dtype=torch.bfloat16, device="cuda")
+    hipops().transpose_bf16(x, y)
+    assert torch.equal(y, x.t().contiguous())

@@ -146,7 +146,7 @@ def test_wide_deep_gpu_full_width_learns():
     assert last["loss"] < first["loss"] and np.isfinite(last["loss"])
 
 
-def _wd_rehearsal(rank, world, port, q, exchange="padded", model="wd"):
+def _wd_rehearsal(rank, world, port, q, exchange="padded", model="wd", steps=6):
     import os
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -166,7 +166,7 @@ def _wd_rehearsal(rank, world, port, q, exchange="padded", model="wd"):
         tr = FMTrainer(FMConfig(num_features=1 << 22, embedding_dim=16, minibatch=1024,
                                 table_capacity=1 << 16, emb_lr=0.05, lambda_v=0.5,
                                 exchange=exchange), comm, dev)
-    for s in range(6):
+    for s in range(steps):
         k, l = criteo_batch(1024, seed=50 + rank, row0=s * 1024, num_features=1 << 22,
                             cards=[1000] * 26, device=dev)
         tr.step(k, l)
@@ -186,7 +186,7 @@ def _wd_rehearsal(rank, world, port, q, exchange="padded", model="wd"):
     dist.destroy_process_group()
 
 
-def _run_rehearsal(exchange, model="wd"):
+def _run_rehearsal(exchange, model="wd", steps=6):
     import socket
 
     import torch.multiprocessing as mp
@@ -197,7 +197,7 @@ def _run_rehearsal(exchange, model="wd"):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_wd_rehearsal, args=(r, 2, port, q, exchange, model))
+    ps = [ctx.Process(target=_wd_rehearsal, args=(r, 2, port, q, exchange, model, steps))
           for r in range(2)]
     for p in ps:
         p.start()
@@ -220,7 +220,11 @@ def test_wide_deep_two_rank_gpu_rehearsal(exchange):
 def test_padded_exchange_matches_exact(model):
     """Sync-free padded pull/push (fixed rows, device-side counts) trains what the
     count-sized all-to-all-v exchange trains: same shard keys, wide weights, loss."""
-    pad, ex = _run_rehearsal("padded", model), _run_rehearsal("exact", model)
+    # 2 steps: the second pulls rows the first pushed. (Over 6 steps the two runs drift
+    # apart chaotically from the order of fp32 atomics in the wide / bias gradients: at
+    # steps 1-2 the embedding rows are bitwise equal, at step 6 ~8 % of them differ by up
+    # to one AdaGrad step, benchmarks/wd_exchange_debug.py.)
+    pad, ex = _run_rehearsal("padded", model, 2), _run_rehearsal("exact", model, 2)
     for rp, re_ in zip(pad, ex):
         assert rp[3] == re_[3]
         assert torch.equal(rp[4], re_[4])
