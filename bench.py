@@ -231,12 +231,6 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
         t = state["t"]
         if watch is not None and not graphs["on"]:
             watch.beat("pipeline-warmup", t)
-        nb = (t + nprep) % NB                 # minibatch t + nprep
-        s = sides[nb % nprep]
-        s.wait_event(ev_buf[nb])              # step(t + nprep - NB) done with bufs[nb]
-        with torch.cuda.stream(s):
-            preps[nb]()
-            ev_prep[nb].record(s)
         cur = t % NB
         if xmode == "own":
             issue_exchange(t + 1)
@@ -245,9 +239,18 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             main.wait_event(ev_x[t % E])
         else:
             main.wait_event(ev_prep[cur])     # minibatch t is localised
+        # the training step is issued first: after an idle GPU (the first timed step)
+        # its kernels start one graph launch earlier (short runs: step 0 took ~0.1 ms
+        # longer than the steady state behind the preparation's launch)
         run_plan(wplan(t), t, main)
         ev_buf[cur].record(main)
         ev_w[t % E].record(main)
+        nb = (t + nprep) % NB                 # minibatch t + nprep
+        s = sides[nb % nprep]
+        s.wait_event(ev_buf[nb])              # step(t + nprep - NB) done with bufs[nb]
+        with torch.cuda.stream(s):
+            preps[nb]()
+            ev_prep[nb].record(s)
         if xmode == "prep":
             issue_exchange(t + xd)
         state["t"] = t + 1
@@ -584,17 +587,30 @@ def main():
     comm.barrier()
     if gpu:
         torch.cuda.synchronize()
+    # PSAMD_STEP_EVENTS=1: a main-stream event after every timed step (diagnostic of the
+    # pipeline's fill / drain in short runs; prints per-step GPU ms to stderr)
+    sev = ([torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+           if gpu and os.environ.get("PSAMD_STEP_EVENTS") == "1" else None)
     t0 = time.perf_counter()
+    if sev:
+        sev[0].record()
     for i in range(args.steps):
         watch.beat("timed", i)
         maybe_inject(rank, i)
         run()
+        if sev:
+            sev[i + 1].record()
         if args.progress and rank == 0 and (i + 1) % 10 == 0:
             print(f"step {i + 1}", file=sys.stderr)
     t_issue = time.perf_counter() - t0  # host time to enqueue the K steps (CPU-bound check)
     watch.beat("timed-drain")
     if gpu:
         torch.cuda.synchronize()
+    t_main = time.perf_counter() - t0
+    if sev and rank == 0:
+        print("step_events_ms", [round(sev[i].elapsed_time(sev[i + 1]), 4)
+                                 for i in range(args.steps)],
+              "wall_to_sync_ms", round(t_main * 1e3, 4), file=sys.stderr)
     comm.barrier()
     dt = time.perf_counter() - t0
     watch.beat("report")

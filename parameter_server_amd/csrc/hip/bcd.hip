@@ -488,6 +488,176 @@ bcd_rows_reduce_kernel(const long long* __restrict__ part, int W, int ncols, int
   }
 }
 
+// Row pass over DENSE per-row block layouts (blocks with at most one entry per example,
+// the slot layout of CTR data): dcol[i] = column of example i's entry relative to the
+// block's c0 (-1: none), dval[i] its value (null: binary). 4 B per example instead of a
+// (col, row) pair per entry, read in example order. One pass applies the PENDING dual
+// update of block j (ym_i += y_i dw_c x_ic, the update that ran last on the stream) and
+// then, on the updated margin, the gradient of the NEXT block k: the dual update of a
+// block is always followed by the next block's gradient in the BCD loop, so the pair
+// fuses without changing the order of anything (bitwise equal to bcd_dual + grad).
+//   bcd_rowpass_grad_kernel: k narrow (ncols <= kRowCols): fixed-point LDS column sums
+//     as bcd_grad_rows_kernel (W partials, then bcd_rows_reduce);
+//   bcd_rowpass_q_kernel: k wide: writes rowq[i] for the examples of block k (what
+//     bcd_rowq_kernel wrote for all of them) for the chunked column-order gradient;
+//     without a grad block it is the dense dual update alone.
+struct RowDual {
+  const int32_t* dcol;  // null: no pending dual update
+  const float* dval;
+  const double* dw;
+  int ncols;
+};
+
+__device__ __forceinline__ double rp_dual_delta(const RowDual& d, int c, int64_t i, double dwc,
+                                                double yr) {
+  const double x = d.dval ? (double)d.dval[i] : 1.0;
+  return yr * dwc * x;  // the bcd_dual_kernel expression: (y * dw) * x
+}
+
+template <bool kDual>
+__global__ void __launch_bounds__(512)
+bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restrict__ y,
+                        RowDual dj, const int32_t* __restrict__ dcol, const float* __restrict__ dval,
+                        int64_t c0, int ncols, int copies, const double* __restrict__ delta,
+                        const uint8_t* __restrict__ active, int k2, long long* __restrict__ part) {
+  __shared__ long long acc[2 * kRowCols];  // [copies][2][ncols] (G, U)
+  __shared__ double cdl[kRowCols];
+  __shared__ uint8_t cact[kRowCols];
+  const int t = threadIdx.x;
+  const int stride = 2 * ncols;
+  for (int i = t; i < copies * stride; i += blockDim.x) acc[i] = 0;
+  for (int c = t; c < ncols; c += blockDim.x) {
+    const double dl = delta[c0 + c];
+    cdl[c] = dval ? dl : exp(dl);
+    cact[c] = active[c0 + c];
+  }
+  __syncthreads();
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t a = per * blockIdx.x, b = min(n, a + per);
+  long long* my = acc + (int64_t)((t >> 6) % copies) * stride;
+  const double sc = ldexp(1.0, k2);
+  constexpr int kR = 8;  // examples per thread per round, loads in flight together
+  for (int64_t i0 = a + t; i0 < b; i0 += (int64_t)kR * blockDim.x) {
+    int ck[kR], cj[kR];
+    double m[kR];
+    float yv[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const int64_t i = i0 + (int64_t)q * blockDim.x;
+      ck[q] = -1;
+      cj[q] = -1;
+      m[q] = 0;
+      yv[q] = 0.f;
+      if (i < b) {
+        const int c = dcol[i];
+        ck[q] = (c >= 0 && c < ncols) ? c : -1;
+        if (kDual) {
+          const int d = dj.dcol[i];
+          cj[q] = (d >= 0 && d < dj.ncols) ? d : -1;
+        }
+        if (ck[q] >= 0 || cj[q] >= 0) {
+          m[q] = ym[i];
+          yv[q] = y[i];
+        }
+      }
+    }
+    if (kDual) {
+      double dwv[kR];
+#pragma unroll
+      for (int q = 0; q < kR; ++q) dwv[q] = cj[q] >= 0 ? dj.dw[cj[q]] : 0.0;
+#pragma unroll
+      for (int q = 0; q < kR; ++q) {
+        if (dwv[q] == 0) continue;
+        const int64_t i = i0 + (int64_t)q * blockDim.x;
+        m[q] += rp_dual_delta(dj, cj[q], i, dwv[q], (double)yv[q]);
+        ym[i] = m[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const int c = ck[q];
+      if (c < 0 || !cact[c]) continue;
+      const double tau = 1.0 / (1.0 + exp(m[q]));
+      const double yr = (double)yv[q];
+      const double t2 = tau * (1.0 - tau);
+      double g, u;
+      if (dval) {
+        const double v = (double)dval[i0 + (int64_t)q * blockDim.x];
+        g = -yr * tau * v;
+        u = fmin(t2 * exp(fabs(v) * cdl[c]), 0.25) * v * v;
+      } else {
+        g = -yr * tau;
+        u = fmin(t2 * cdl[c], 0.25);
+      }
+      atomicAdd(reinterpret_cast<unsigned long long*>(&my[c]),
+                (unsigned long long)__double2ll_rn(g * sc));
+      atomicAdd(reinterpret_cast<unsigned long long*>(&my[ncols + c]),
+                (unsigned long long)__double2ll_rn(u * sc));
+    }
+  }
+  __syncthreads();
+  long long* out = part + (int64_t)blockIdx.x * stride;
+  for (int i = t; i < stride; i += blockDim.x) {
+    long long s = 0;
+    for (int q = 0; q < copies; ++q) s += acc[q * stride + i];
+    out[i] = s;
+  }
+}
+
+template <bool kDual, bool kQ>
+__global__ void __launch_bounds__(256)
+bcd_rowpass_q_kernel(int64_t n, double* __restrict__ ym, const float* __restrict__ y, RowDual dj,
+                     const int32_t* __restrict__ dcol, int ncols, double2* __restrict__ rowq) {
+  constexpr int kR = 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n;
+       i0 += (int64_t)kR * stride) {
+    int ck[kR], cj[kR];
+    double m[kR];
+    float yv[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const int64_t i = i0 + q * stride;
+      ck[q] = -1;
+      cj[q] = -1;
+      m[q] = 0;
+      yv[q] = 0.f;
+      if (i < n) {
+        if (kQ) {
+          const int c = dcol[i];
+          ck[q] = (c >= 0 && c < ncols) ? c : -1;
+        }
+        if (kDual) {
+          const int d = dj.dcol[i];
+          cj[q] = (d >= 0 && d < dj.ncols) ? d : -1;
+        }
+      }
+    }
+    double dwv[kR];
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      dwv[q] = kDual && cj[q] >= 0 ? dj.dw[cj[q]] : 0.0;
+      const int64_t i = i0 + q * stride;
+      if (ck[q] >= 0 || dwv[q] != 0) {
+        m[q] = ym[i];
+        yv[q] = y[i];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const int64_t i = i0 + q * stride;
+      if (kDual && dwv[q] != 0) {
+        m[q] += rp_dual_delta(dj, cj[q], i, dwv[q], (double)yv[q]);
+        ym[i] = m[q];
+      }
+      if (kQ && ck[q] >= 0) {
+        const double tau = 1.0 / (1.0 + exp(m[q]));
+        rowq[i] = make_double2(-(double)yv[q] * tau, tau * (1.0 - tau));
+      }
+    }
+  }
+}
+
 // objective: out[0] += sum_i log(1 + exp(-ym_i))
 __global__ void __launch_bounds__(256)
 bcd_objective_kernel(const double* __restrict__ ym, int64_t n, double* __restrict__ out) {
@@ -542,15 +712,17 @@ void bcd_grad_chunked(const int32_t* col, const int32_t* row, const float* val,
                       const int64_t* chunks, int64_t nchunks, int64_t c0, int64_t ncols,
                       const double* ym, const float* y, int64_t nrows, const double* delta,
                       const uint8_t* active, double* rowq, double* G, double* U, bool zeroed,
-                      hipStream_t st) {
+                      bool rowq_ready, hipStream_t st) {
   if (!zeroed) {
     fill_async<double>(G, ncols, 0.0, st);
     fill_async<double>(U, ncols, 0.0, st);
   }
   if (nchunks <= 0) return;
   if (rowq) {
-    bcd_rowq_kernel<<<grid_for(nrows, 256, 4096), 256, 0, st>>>(ym, y, nrows, (double2*)rowq);
-    PSAMD_HIP_CHECK(hipGetLastError());
+    if (!rowq_ready) {  // (ready: a row pass wrote the block's examples' factors)
+      bcd_rowq_kernel<<<grid_for(nrows, 256, 4096), 256, 0, st>>>(ym, y, nrows, (double2*)rowq);
+      PSAMD_HIP_CHECK(hipGetLastError());
+    }
     bcd_grad_chunk_kernel<true><<<grid_for(nchunks, 4, 16384), 256, 0, st>>>(
         col, row, val, chunks, nchunks, c0, ncols, ym, y, nrows, delta, active,
         (const double2*)rowq, G, U);
@@ -614,6 +786,43 @@ void bcd_dual(const int32_t* col, const int32_t* row, const float* val, int64_t 
   else
     bcd_dual_kernel<false><<<grid_for(p1 - p0, 256, 4096), 256, 0, st>>>(
         col, row, val, p0, p1, c0, ncols, dw, y, ym, nrows);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+// Row pass (see bcd_rowpass_grad_kernel): pending dual of block j (jcol null: none), then
+// block k's gradient: narrow (part != null: LDS fixed point, W partials + reduce into G / U)
+// or rowq (wide; kcol null: the dense dual alone).
+void bcd_rowpass(int64_t n, double* ym, const float* y, const int32_t* jcol, const float* jval,
+                 const double* jdw, int64_t jncols, const int32_t* kcol, const float* kval,
+                 int64_t c0, int64_t ncols, const double* delta, const uint8_t* active, int k2,
+                 int W, long long* part, double* G, double* U, double* rowq, hipStream_t st) {
+  if (n <= 0) return;
+  const RowDual dj{jcol, jval, jdw, (int)jncols};
+  if (part) {  // narrow gradient of block k
+    if (ncols <= 0) return;
+    if (ncols > kRowCols) throw std::runtime_error("bcd_rowpass: narrow block ncols > 2048");
+    const int copies = std::max(1, std::min(8, kRowCols / (int)ncols));
+    if (jcol)
+      bcd_rowpass_grad_kernel<true><<<W, 512, 0, st>>>(n, ym, y, dj, kcol, kval, c0, (int)ncols,
+                                                       copies, delta, active, k2, part);
+    else
+      bcd_rowpass_grad_kernel<false><<<W, 512, 0, st>>>(n, ym, y, dj, kcol, kval, c0, (int)ncols,
+                                                        copies, delta, active, k2, part);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    bcd_rows_reduce_kernel<<<(unsigned)(2 * ncols), 256, 0, st>>>(part, W, (int)ncols, k2, G, U);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const unsigned grid = (unsigned)grid_for(n, 256 * 4, 4096);
+  auto q = reinterpret_cast<double2*>(rowq);
+  if (jcol && kcol)
+    bcd_rowpass_q_kernel<true, true><<<grid, 256, 0, st>>>(n, ym, y, dj, kcol, (int)ncols, q);
+  else if (kcol)
+    bcd_rowpass_q_kernel<false, true><<<grid, 256, 0, st>>>(n, ym, y, dj, kcol, (int)ncols, q);
+  else if (jcol)
+    bcd_rowpass_q_kernel<true, false><<<grid, 256, 0, st>>>(n, ym, y, dj, kcol, (int)ncols, q);
+  else
+    return;
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

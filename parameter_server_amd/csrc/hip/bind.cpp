@@ -165,7 +165,10 @@ void bcd_grad(const int32_t*, const int32_t*, const float*, int64_t, int64_t, in
               double*, hipStream_t);
 void bcd_grad_chunked(const int32_t*, const int32_t*, const float*, const int64_t*, int64_t,
                       int64_t, int64_t, const double*, const float*, int64_t, const double*,
-                      const uint8_t*, double*, double*, double*, bool, hipStream_t);
+                      const uint8_t*, double*, double*, double*, bool, bool, hipStream_t);
+void bcd_rowpass(int64_t, double*, const float*, const int32_t*, const float*, const double*,
+                 int64_t, const int32_t*, const float*, int64_t, int64_t, const double*,
+                 const uint8_t*, int, int, long long*, double*, double*, double*, hipStream_t);
 void bcd_update(int64_t, int64_t, double*, double*, double*, double*, uint8_t*, double*, double,
                 double, double, double, unsigned long long*, bool, bool, hipStream_t);
 void bcd_replica(int64_t, int64_t, int64_t, int64_t, double*, double*, double*, uint8_t*, double,
@@ -202,7 +205,7 @@ void wd_head(const void*, int64_t, int, const float*, const float*, const float*
 void colred_bf16(const void*, int64_t, int, const float*, float*, const float*, float*,
                  hipStream_t);
 void adam_update(float*, const float*, float*, float*, int64_t, float, float, float, float, float,
-                 float, float, void*, hipStream_t);
+                 float, float, void*, const int64_t*, hipStream_t);
 // spmv.hip
 void spmv(bool, const int64_t*, const void*, int, const void*, int, int64_t, int64_t, const void*,
           int64_t, double, double, void*, int64_t, hipStream_t);
@@ -1417,7 +1420,7 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("bcd_grad_chunked", [](Tensor col, Tensor row, optional<Tensor> val, Tensor chunks,
                                 int64_t c0, int64_t ncols, Tensor ym, Tensor y, Tensor delta,
                                 Tensor active, Tensor G, Tensor U, bool zeroed,
-                                optional<Tensor> rowq) {
+                                optional<Tensor> rowq, bool rowq_ready) {
     // chunks: [n + 1] int64 entry offsets (bit 62 = hot chunk), built and range-checked
     // on the host once per block (models/darlin.py build_chunks)
     chk(col, at::kInt, "col");
@@ -1442,7 +1445,54 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::bcd_grad_chunked(ptr<int32_t>(col), ptr<int32_t>(row), vp, ptr<int64_t>(chunks),
                             chunks.numel() - 1, c0, ncols, ptr<double>(ym), ptr<float>(y),
                             ym.numel(), ptr<double>(delta), ptr<uint8_t>(active), rq,
-                            ptr<double>(G), ptr<double>(U), zeroed, cur_stream());
+                            ptr<double>(G), ptr<double>(U), zeroed, rq != nullptr && rowq_ready,
+                            cur_stream());
+  });
+  // Darlin row pass over dense per-row block layouts (bcd.hip bcd_rowpass): the pending
+  // dual update of block j (jcol: [rows] int32 column relative to the block, -1 none)
+  // fused with block k's gradient (narrow: part/G/U; wide: rowq).
+  m.def("bcd_rowpass", [](Tensor ym, Tensor y, optional<Tensor> jcol, optional<Tensor> jval,
+                          optional<Tensor> jdw, int64_t jncols, optional<Tensor> kcol,
+                          optional<Tensor> kval, int64_t c0, int64_t ncols, Tensor delta,
+                          Tensor active, int k2, int W, optional<Tensor> part,
+                          optional<Tensor> G, optional<Tensor> U, optional<Tensor> rowq) {
+    chk(ym, at::kDouble, "ym");
+    chk(y, at::kFloat, "y");
+    chk(delta, at::kDouble, "delta");
+    chk(active, at::kByte, "active");
+    const int64_t n = ym.numel();
+    check(y.numel() == n, "y/ym size mismatch");
+    const int32_t* jc = optr<int32_t>(jcol, at::kInt, "jcol");
+    const float* jv = optr<float>(jval, at::kFloat, "jval");
+    const double* jd = optr<double>(jdw, at::kDouble, "jdw");
+    if (jc) {
+      check(jcol->numel() == n, "jcol: one int32 per example");
+      check(jd != nullptr && jncols >= 0 && jdw->numel() >= jncols, "jdw too small");
+      if (jv) check(jval->numel() == n, "jval: one float per example");
+    }
+    const int32_t* kc = optr<int32_t>(kcol, at::kInt, "kcol");
+    const float* kv = optr<float>(kval, at::kFloat, "kval");
+    if (kc) {
+      check(kcol->numel() == n, "kcol: one int32 per example");
+      if (kv) check(kval->numel() == n, "kval: one float per example");
+      check(c0 >= 0 && ncols >= 0 && c0 + ncols <= delta.numel(), "column block outside model");
+    }
+    long long* pp = optr<long long>(part, at::kLong, "part");
+    double* Gp = optr<double>(G, at::kDouble, "G");
+    double* Up = optr<double>(U, at::kDouble, "U");
+    double* rq = optr<double>(rowq, at::kDouble, "rowq");
+    if (pp) {
+      check(kc != nullptr, "narrow row pass needs kcol");
+      check(ncols <= psamd::bcd_rows_max_cols(), "bcd_rowpass: ncols <= 2048");
+      check(W >= 1 && part->numel() >= (int64_t)W * 2 * ncols, "part too small");
+      check(Gp && Up && G->numel() >= ncols && U->numel() >= ncols, "G/U too small");
+      check(k2 >= 0 && k2 <= 62, "fixed-point shift");
+    } else if (kc) {
+      check(rq != nullptr && rowq->numel() >= 2 * n, "rowq: 2 doubles per example");
+    }
+    psamd::bcd_rowpass(n, ptr<double>(ym), ptr<float>(y), jc, jv, jd, jncols, kc, kv, c0, ncols,
+                       ptr<double>(delta), ptr<uint8_t>(active), k2, W, pp, Gp, Up, rq,
+                       cur_stream());
   });
   m.def("bcd_grad", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                 int64_t p1, int64_t c0, int64_t ncols, Tensor ym, Tensor y,
@@ -1786,7 +1836,7 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("adam_update", [](Tensor p, Tensor g, Tensor m_, Tensor v, double lr, double b1,
                           double b2, double eps, int64_t step, double gscale,
-                          optional<Tensor> p16) {
+                          optional<Tensor> p16, optional<Tensor> step_dev) {
     chk(p, at::kFloat, "p");
     chk(g, at::kFloat, "g");
     chk(m_, at::kFloat, "m");
@@ -1799,11 +1849,18 @@ PYBIND11_MODULE(_hipops, m) {
       check(p16->numel() == n, "p16 mismatch");
       p16p = p16->data_ptr();
     }
-    check(step >= 1, "adam step >= 1");
-    const double bc1 = 1.0 - std::pow(b1, (double)step), bc2 = 1.0 - std::pow(b2, (double)step);
+    const int64_t* sd = nullptr;  // device step clock (graph-captured steps)
+    if (step_dev.has_value() && step_dev->defined()) {
+      chk(*step_dev, at::kLong, "step_dev");
+      sd = step_dev->data_ptr<int64_t>();
+    } else {
+      check(step >= 1, "adam step >= 1");
+    }
+    const double s1 = (double)(step >= 1 ? step : 1);
+    const double bc1 = 1.0 - std::pow(b1, s1), bc2 = 1.0 - std::pow(b2, s1);
     psamd::adam_update(ptr<float>(p), ptr<float>(g), ptr<float>(m_), ptr<float>(v), n, (float)lr,
                        (float)b1, (float)b2, (float)eps, (float)bc1, (float)bc2, (float)gscale,
-                       p16p, cur_stream());
+                       p16p, sd, cur_stream());
   });
   // SparseMatrix::times (utils/matrix.py): gather (row-reduce) or scatter (atomic) over the
   // compressed major dimension; y = alpha * A x + beta * y.

@@ -680,11 +680,19 @@ wd_head_db_kernel(double* __restrict__ metrics, int acc_stripes, float* __restri
   if (threadIdx.x == 0) db[0] += (float)d;
 }
 
-// Adam with fp32 master weights; writes the bf16 copy used by the GEMMs.
+// Adam with fp32 master weights; writes the bf16 copy used by the GEMMs. With a device
+// step clock (step_dev: steps completed so far, advanced later in the step by the AUC
+// epilogue) the bias corrections come from it, so a captured step replays correctly.
 __global__ void __launch_bounds__(256)
 adam_update_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                    float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
-                   float bc1, float bc2, float gscale, uint16_t* __restrict__ p16) {
+                   float bc1, float bc2, float gscale, uint16_t* __restrict__ p16,
+                   const int64_t* __restrict__ step_dev) {
+  if (step_dev) {
+    const float s = (float)(step_dev[0] + 1);
+    bc1 = 1.f - exp2f(s * log2f(b1));
+    bc2 = 1.f - exp2f(s * log2f(b2));
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const float gi = g[i] * gscale;
@@ -820,10 +828,11 @@ void colred_bf16(const void* x, int64_t B, int N, const float* s, float* out, co
 
 void adam_update(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                  float b2, float eps, float bc1, float bc2, float gscale, void* p16,
-                 hipStream_t st) {
+                 const int64_t* step_dev, hipStream_t st) {
   if (n <= 0) return;
   adam_update_kernel<<<grid_for(n, 256, 4096), 256, 0, st>>>(
-      p, g, m, v, n, lr, b1, b2, eps, bc1, bc2, gscale, reinterpret_cast<uint16_t*>(p16));
+      p, g, m, v, n, lr, b1, b2, eps, bc1, bc2, gscale, reinterpret_cast<uint16_t*>(p16),
+      step_dev);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -34,6 +34,7 @@ server leaves it NaN forever, darlin.h:228-231 + 223-246).
 from __future__ import annotations
 
 import math
+import os
 import random
 import sys
 import time
@@ -154,6 +155,8 @@ class Block:
     unique_rows: bool = False  # no example has two entries in the block (dual w/o atomics)
     row_mode: bool = False     # narrow block: row-order gradient (bcd.grad_rows)
     fx_k: int = 0              # its fixed-point scale 2^k
+    dcol: object = None        # dense per-example layout (bcd.dense_rows) for the row pass
+    dval: object = None
 
     @property
     def ncols(self):
@@ -479,6 +482,11 @@ class DarlinTrainer:
         # has ~1 entry per block, so its margin update walks ym sequentially
         # (coalesced, uncontended atomics) instead of gathering it in column order
         self.col_r, self.row_r, self.val_r = self.col, self.row, self.val
+        # fused row pass (bcd.rowpass): a block's dual update runs inside the next
+        # block's gradient pass over dense per-example layouts (PSAMD_DARLIN_FUSE=0: the
+        # separate kernels, for A/B)
+        self.fuse_rows = dev.type == "cuda" and os.environ.get("PSAMD_DARLIN_FUSE", "1") != "0"
+        self._pending_dual = None
         # workgroups of the row-order gradient (3 per CU) and its partial-sum buffer
         self.rows_W = 768
         rows_max = hipops().bcd_rows_max_cols() if dev.type == "cuda" else 0
@@ -507,6 +515,11 @@ class DarlinTrainer:
                     vmax = 1.0 if self.val is None else float(self.val[p0:p1].abs().max())
                     blk.row_mode = True
                     blk.fx_k = bcd.fixed_point_shift(p1 - p0, vmax)
+                # dense per-example layout (4 B per example) for the fused row pass:
+                # blocks with one entry per example covering >= 1/4 of the examples
+                if self.fuse_rows and blk.unique_rows and 4 * (p1 - p0) >= self.rows:
+                    blk.dcol, blk.dval = bcd.dense_rows(self.row_r, self.col_r, self.val_r,
+                                                        p0, p1, blk.c0, self.rows)
         # model state (replicated per rank) and margins
         f64 = torch.float64
         self.w = torch.full((base,), float(cfg.init_w), dtype=f64, device=dev)
@@ -527,9 +540,48 @@ class DarlinTrainer:
         return self.shard and (self.cfg.shard_server == "on"
                                or b.ncols >= self.cfg.shard_min_cols)
 
+    def _dual(self, b: Block, dw):
+        """Dual update of block b: deferred into the next gradient's row pass when b has a
+        dense layout (the next kernel touching the margins is always that gradient or a
+        flush), else now."""
+        self._flush_dual()
+        if b.dcol is not None:
+            self._pending_dual = (b, dw)
+            return
+        bcd.dual(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, dw, self.y,
+                 self.ym, b.unique_rows)
+
+    def _flush_dual(self):
+        """Apply a deferred dual update on its own (before anything else reads ym)."""
+        if self._pending_dual is None:
+            return
+        j, dw = self._pending_dual
+        self._pending_dual = None
+        bcd.rowpass(self.ym, self.y, self.delta, self.active, jcol=j.dcol, jval=j.dval,
+                    jdw=dw, jncols=j.ncols)
+
     def _grad(self, b: Block, G, U, zeroed: bool):
         """Block gradient into G / U: row order for narrow blocks, the load-balanced
-        column-order kernel otherwise."""
+        column-order kernel otherwise. With a dense layout the pending dual update of
+        the previous block runs in the same row pass."""
+        if b.dcol is not None and (b.row_mode or b.chunks is not None):
+            jd = {}
+            if self._pending_dual is not None:
+                j, dw = self._pending_dual
+                self._pending_dual = None
+                jd = dict(jcol=j.dcol, jval=j.dval, jdw=dw, jncols=j.ncols)
+            if b.row_mode:
+                bcd.rowpass(self.ym, self.y, self.delta, self.active, kcol=b.dcol, kval=b.dval,
+                            c0=b.c0, ncols=b.ncols, k2=b.fx_k, W=self.rows_W,
+                            part=self.rows_part, G=G, U=U, **jd)
+                return
+            bcd.rowpass(self.ym, self.y, self.delta, self.active, kcol=b.dcol, kval=b.dval,
+                        c0=b.c0, ncols=b.ncols, rowq=self.rowq, **jd)
+            bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
+                     self.delta, self.active, G, U, chunks=b.chunks, zeroed=zeroed,
+                     rowq=self.rowq, rowq_ready=True)
+            return
+        self._flush_dual()
         if b.row_mode:
             bcd.grad_rows(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, self.ym,
                           self.y, self.delta, self.active, G, U, self.rows_part, self.rows_W,
@@ -565,8 +617,7 @@ class DarlinTrainer:
                            c.delta_max, self.kkt_thr, vio=self.vio, consume=persistent)
         if persistent:
             b.busy = False
-        bcd.dual(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, dw, self.y,
-                 self.ym, b.unique_rows)
+        self._dual(b, dw)
 
     # ---- sharded server (G > 1): rank r owns the r-th even slice of every block
     def _own_slice(self, b: Block) -> tuple[int, int, int]:
@@ -608,8 +659,7 @@ class DarlinTrainer:
         dw = torch.empty(m * self.G, dtype=torch.float64, device=self.device)
         self.comm.all_gather_into_async(dw, dwo).wait()
         bcd.replica(b.c0, b.ncols, j0, j1, dw, self.w, self.delta, self.active, c.delta_max)
-        bcd.dual(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, dw, self.y,
-                 self.ym, b.unique_rows)
+        self._dual(b, dw)
 
     def run_pass(self, it: int, reset_kkt: bool = False) -> BCDProgress:
         cfg = self.cfg
@@ -645,6 +695,7 @@ class DarlinTrainer:
 
     def evaluate(self) -> BCDProgress:
         """Objective = sum_i log(1+exp(-ym_i)) + l1 * ||w||_1 (darlin.h:248-265, 504-511)."""
+        self._flush_dual()
         obj = bcd.objective(self.ym)
         st = bcd.server_stats(self.w, self.active, self.own[0], self.own[1])
         vio = self.vio.view(torch.float64)

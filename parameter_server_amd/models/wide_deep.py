@@ -155,6 +155,8 @@ class EmbeddingPS:
         if "param" in self._dense_state:
             self.param16.copy_(self.param.to(torch.bfloat16))
         self.step_count = int(sd.get("step", 0))
+        if hasattr(self, "step_dev"):  # the device step clock Adam reads
+            self.step_dev.fill_(self.step_count)
         self.examples = int(sd.get("examples", 0))
 
     def prefill(self, count: int, chunk: int = 1 << 23, seed: int = 12345) -> int:
@@ -461,8 +463,11 @@ class WideDeepTrainer(EmbeddingPS):
         if self.G > 1:
             self.comm.all_reduce_(self.grad)
         self.step_count += 1
+        # bias corrections from the device step clock (advanced by auc_from_hist below),
+        # so the whole step can replay from a HIP graph
         E.adam(self.param, self.grad, self.m, self.v, lr=cfg.mlp_lr, step=self.step_count,
-               gscale=1.0 / (B * self.G), p16=self.param16)
+               gscale=1.0 / (B * self.G), p16=self.param16,
+               step_dev=self.step_dev if self.gpu else None)
         auc_from_hist(self.hist, self.metrics, self.step_dev)
         self.examples += B
 

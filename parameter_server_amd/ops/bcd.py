@@ -61,12 +61,14 @@ def build_chunks(colptr, c0: int, c1: int, small: int = 64, hot: int = 4096) -> 
 
 
 def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, active,
-         G=None, U=None, chunks=None, zeroed: bool = False, rowq=None):
+         G=None, U=None, chunks=None, zeroed: bool = False, rowq=None, rowq_ready: bool = False):
     """Block gradient: returns (G, U) fp64[ncols] (inactive columns contribute 0).
     ``chunks`` (device int64 from ``build_chunks``) selects the load-balanced kernel;
     ``rowq`` (fp64 [2 * rows] scratch, with ``chunks``): the per-example factors are
     packed first so each entry gathers one 16-B record (wide blocks);
-    ``zeroed``: G / U already hold zeros (left by ``update(consume=True)``)."""
+    ``zeroed``: G / U already hold zeros (left by ``update(consume=True)``);
+    ``rowq_ready``: ``rowq`` already holds the factors of the block's examples (a
+    ``rowpass`` wrote them), so the packing pass is skipped."""
     dev = ym.device
     if G is None:
         G = torch.empty(ncols, dtype=torch.float64, device=dev)
@@ -75,7 +77,7 @@ def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, act
     if is_gpu(ym):
         if chunks is not None:
             hipops().bcd_grad_chunked(col, row, val, chunks, c0, ncols, ym, y, delta, active,
-                                      G, U, zeroed, rowq)
+                                      G, U, zeroed, rowq, bool(rowq_ready))
         else:
             hipops().bcd_grad(col, row, val, p0, p1, c0, ncols, ym, y, delta, active, G, U)
         return G, U
@@ -113,6 +115,34 @@ def grad_rows(col_r, row_r, val_r, p0: int, p1: int, c0: int, ncols: int, ym, y,
                                int(k2), int(W), part, G, U)
         return G, U
     return grad(col_r, row_r, val_r, p0, p1, c0, ncols, ym, y, delta, active, G, U)
+
+
+def dense_rows(row_r, col_r, val_r, p0: int, p1: int, c0: int, rows: int):
+    """Dense per-example layout of a block with at most one entry per example:
+    (dcol int32 [rows]: the entry's column relative to c0, -1 = none; dval float32
+    [rows] or None). 4 B per example, read in example order by ``rowpass``."""
+    dev = row_r.device
+    dcol = torch.full((rows,), -1, dtype=torch.int32, device=dev)
+    dval = None if val_r is None else torch.zeros(rows, dtype=torch.float32, device=dev)
+    if p1 > p0:
+        r = row_r[p0:p1].long()
+        dcol[r] = (col_r[p0:p1].long() - c0).to(torch.int32)
+        if dval is not None:
+            dval[r] = val_r[p0:p1]
+    return dcol, dval
+
+
+def rowpass(ym, y, delta, active, *, jcol=None, jval=None, jdw=None, jncols: int = 0,
+            kcol=None, kval=None, c0: int = 0, ncols: int = 0, k2: int = 0, W: int = 1,
+            part=None, G=None, U=None, rowq=None):
+    """GPU row pass over dense block layouts (``dense_rows``): first the pending dual
+    update of block j (``jcol`` / ``jval`` / its ``jdw``: ym_i += y_i dw_c x_ic), then on
+    the updated margins block k's gradient: narrow (``part`` given: fixed-point column
+    sums into ``G`` / ``U``, as ``grad_rows``) or the per-example factors of a wide block
+    into ``rowq`` (for ``grad(..., rowq_ready=True)``). Bitwise equal to ``dual``
+    followed by ``grad_rows`` / the rowq packing (tests/test_darlin_gpu.py)."""
+    hipops().bcd_rowpass(ym, y, jcol, jval, jdw, int(jncols), kcol, kval, int(c0), int(ncols),
+                         delta, active, int(k2), int(W), part, G, U, rowq)
 
 
 def fixed_point_shift(entries: int, max_abs_val: float) -> int:

@@ -206,9 +206,13 @@ def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = False):
     return out
 
 
-def adam(p, g, m, v, *, lr, step: int, b1=0.9, b2=0.999, eps=1e-8, gscale=1.0, p16=None):
+def adam(p, g, m, v, *, lr, step: int, b1=0.9, b2=0.999, eps=1e-8, gscale=1.0, p16=None,
+         step_dev=None):
+    """Adam on fp32 master weights (+ bf16 copy ``p16``). ``step_dev`` (GPU): int64 device
+    step clock holding the steps completed so far; the kernel takes its bias corrections
+    from it (step = step_dev + 1), so the update can be replayed from a HIP graph."""
     if is_gpu(p):
-        hipops().adam_update(p, g, m, v, lr, b1, b2, eps, step, gscale, p16)
+        hipops().adam_update(p, g, m, v, lr, b1, b2, eps, step, gscale, p16, step_dev)
         return
     gs = g * gscale
     m.mul_(b1).add_((1 - b1) * gs)

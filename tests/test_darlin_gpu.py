@@ -240,3 +240,33 @@ def test_grad_rows_matches_column_kernel(ncols, valued):
                   None if val is None else d(val[perm].contiguous()), 0, n, c0, ncols, d(ym), d(y),
                   d(delta), d(active), G2, U2, part, W, k2)
     assert torch.equal(G1, G2) and torch.equal(U1, U2)
+
+
+@pytest.mark.parametrize("tau,valued", [(1, False), (0, False), (2, True)])
+def test_fused_row_pass_bitwise_equal_to_separate_kernels(monkeypatch, tau, valued):
+    """The row pass (a block's dual update fused into the next block's gradient over dense
+    per-example layouts, bcd.rowpass) gives the same margins, weights and objectives as
+    the separate dual / gradient / rowq kernels (PSAMD_DARLIN_FUSE=0), to fp64 rounding."""
+    if valued:  # one valued entry per example and group (dense layouts with values)
+        sd = sparse_classification(30_000, groups=(1, 2, 3), keys_per_group=3000,
+                                   nnz_per_row=(1, 1, 1), binary=False, seed=5)
+    else:
+        sd = criteo_slots(120_000, seed=4, num_features=10 ** 6, device="cuda")
+    cfg = dict(l1=2.0, max_pass=3, tail_freq=2, tau=tau, seed=0, epsilon=1e-12)
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("PSAMD_DARLIN_FUSE", fuse)
+        tr = DarlinTrainer(sd, DarlinConfig(**cfg), device="cuda")
+        if fuse == "1":
+            assert any(b.dcol is not None for b in tr.blocks)
+            assert any(b.dcol is not None and b.row_mode for b in tr.blocks)
+        else:
+            assert all(b.dcol is None for b in tr.blocks)
+        prog = tr.train()
+        out[fuse] = ([p.objective for p in prog], tr.ym.cpu(), tr.w.cpu(), tr.active.cpu())
+    # (not bitwise: the wide blocks' hot columns and the objective add fp64 partial sums
+    # atomically, in a run-dependent order, on both paths)
+    np.testing.assert_allclose(out["1"][0], out["0"][0], rtol=1e-11)
+    torch.testing.assert_close(out["1"][1], out["0"][1], rtol=1e-9, atol=1e-9)
+    torch.testing.assert_close(out["1"][2], out["0"][2], rtol=1e-9, atol=1e-12)
+    assert (out["1"][3] != out["0"][3]).sum().item() <= 2
