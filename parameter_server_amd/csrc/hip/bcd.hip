@@ -249,6 +249,7 @@ bcd_dual_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row
 // for the random row gather (5.55, no change: the rows live in L2 / MALL) and
 // forcing 8 waves/SIMD with __launch_bounds__(256, 8) (6.33: 12 VGPRs spill).
 constexpr int64_t kHotBit = int64_t(1) << 62;
+constexpr int64_t kSkipBit = int64_t(1) << 61;
 
 __device__ __forceinline__ void bcd_gu(int64_t i, int64_t c, int64_t c0,
                                        const int32_t* __restrict__ row,
@@ -315,8 +316,9 @@ bcd_grad_chunk_kernel(const int32_t* __restrict__ col, const int32_t* __restrict
   for (int64_t k = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); k < nchunks;
        k += nw) {
     const int64_t e0 = chunks[k], e1 = chunks[k + 1];
+    if (e0 & kSkipBit) continue;  // a column summed by the row pass (hot in LDS)
     const bool hot = (e0 & kHotBit) != 0;
-    const int64_t a = e0 & ~kHotBit, b = e1 & ~kHotBit;
+    const int64_t a = e0 & ~(kHotBit | kSkipBit), b = e1 & ~(kHotBit | kSkipBit);
     if (hot) {
       const int64_t c = (int64_t)col[a] - c0;  // wave-uniform
       if (c < 0 || c >= ncols || !active[c0 + c]) continue;
@@ -471,7 +473,8 @@ bcd_grad_rows_kernel(const int32_t* __restrict__ col, const int32_t* __restrict_
 // order does not matter and the result is deterministic).
 __global__ void __launch_bounds__(256)
 bcd_rows_reduce_kernel(const long long* __restrict__ part, int W, int ncols, int k2,
-                       double* __restrict__ G, double* __restrict__ U) {
+                       double* __restrict__ G, double* __restrict__ U,
+                       const int32_t* __restrict__ cols = nullptr) {
   __shared__ long long ws[4];
   const int i = blockIdx.x;  // output 0 .. 2*ncols-1
   long long s = 0;
@@ -483,8 +486,10 @@ bcd_rows_reduce_kernel(const long long* __restrict__ part, int W, int ncols, int
   if (threadIdx.x == 0) {
     const long long tot = ws[0] + ws[1] + ws[2] + ws[3];
     const double v = (double)tot * ldexp(1.0, -k2);
-    if (i < ncols) G[i] = v;
-    else U[i - ncols] = v;
+    const int c = i < ncols ? i : i - ncols;
+    const int o = cols ? cols[c] : c;  // (hot-column sums of a wide block: their columns)
+    if (i < ncols) G[o] = v;
+    else U[o] = v;
   }
 }
 
@@ -501,6 +506,8 @@ bcd_rows_reduce_kernel(const long long* __restrict__ part, int W, int ncols, int
 //   bcd_rowpass_q_kernel: k wide: writes rowq[i] for the examples of block k (what
 //     bcd_rowq_kernel wrote for all of them) for the chunked column-order gradient;
 //     without a grad block it is the dense dual update alone.
+constexpr int kColdRow = 1 << 30;  // row pass: the example's entry is in a cold column
+
 struct RowDual {
   const int32_t* dcol;  // null: no pending dual update
   const float* dval;
@@ -514,12 +521,17 @@ __device__ __forceinline__ double rp_dual_delta(const RowDual& d, int c, int64_t
   return yr * dwc * x;  // the bcd_dual_kernel expression: (y * dw) * x
 }
 
-template <bool kDual>
+// kHot (wide block k): the LDS sums cover the block's hottest columns only, hcols[h] =
+// column of LDS slot h (ncols = their count); dcol[i] >= 0 marks a COLD entry (its
+// factors go to rowq[i] for the chunked column-order kernel over the cold columns),
+// dcol[i] <= -2 the hot slot -2 - dcol[i], -1 no entry.
+template <bool kDual, bool kHot>
 __global__ void __launch_bounds__(512)
 bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restrict__ y,
                         RowDual dj, const int32_t* __restrict__ dcol, const float* __restrict__ dval,
                         int64_t c0, int ncols, int copies, const double* __restrict__ delta,
-                        const uint8_t* __restrict__ active, int k2, long long* __restrict__ part) {
+                        const uint8_t* __restrict__ active, int k2, long long* __restrict__ part,
+                        const int32_t* __restrict__ hcols, double2* __restrict__ rowq) {
   __shared__ long long acc[2 * kRowCols];  // [copies][2][ncols] (G, U)
   __shared__ double cdl[kRowCols];
   __shared__ uint8_t cact[kRowCols];
@@ -527,9 +539,10 @@ bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restr
   const int stride = 2 * ncols;
   for (int i = t; i < copies * stride; i += blockDim.x) acc[i] = 0;
   for (int c = t; c < ncols; c += blockDim.x) {
-    const double dl = delta[c0 + c];
+    const int64_t k = c0 + (kHot ? hcols[c] : c);
+    const double dl = delta[k];
     cdl[c] = dval ? dl : exp(dl);
-    cact[c] = active[c0 + c];
+    cact[c] = active[k];
   }
   __syncthreads();
   const int64_t per = (n + gridDim.x - 1) / gridDim.x;
@@ -550,12 +563,13 @@ bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restr
       yv[q] = 0.f;
       if (i < b) {
         const int c = dcol[i];
-        ck[q] = (c >= 0 && c < ncols) ? c : -1;
+        if (kHot) ck[q] = c >= 0 ? kColdRow : (c <= -2 && -2 - c < ncols) ? -2 - c : -1;
+        else ck[q] = (c >= 0 && c < ncols) ? c : -1;
         if (kDual) {
           const int d = dj.dcol[i];
           cj[q] = (d >= 0 && d < dj.ncols) ? d : -1;
         }
-        if (ck[q] >= 0 || cj[q] >= 0) {
+        if (ck[q] != -1 || cj[q] >= 0) {
           m[q] = ym[i];
           yv[q] = y[i];
         }
@@ -576,6 +590,11 @@ bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restr
 #pragma unroll
     for (int q = 0; q < kR; ++q) {
       const int c = ck[q];
+      if (kHot && c == kColdRow) {  // cold entry: factors for the column-order kernel
+        const double tau = 1.0 / (1.0 + exp(m[q]));
+        rowq[i0 + (int64_t)q * blockDim.x] = make_double2(-(double)yv[q] * tau, tau * (1.0 - tau));
+        continue;
+      }
       if (c < 0 || !cact[c]) continue;
       const double tau = 1.0 / (1.0 + exp(m[q]));
       const double yr = (double)yv[q];
@@ -608,7 +627,7 @@ template <bool kDual, bool kQ>
 __global__ void __launch_bounds__(256)
 bcd_rowpass_q_kernel(int64_t n, double* __restrict__ ym, const float* __restrict__ y, RowDual dj,
                      const int32_t* __restrict__ dcol, int ncols, double2* __restrict__ rowq) {
-  constexpr int kR = 4;
+  constexpr int kR = 8;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n;
        i0 += (int64_t)kR * stride) {
@@ -635,13 +654,13 @@ bcd_rowpass_q_kernel(int64_t n, double* __restrict__ ym, const float* __restrict
     }
     double dwv[kR];
 #pragma unroll
-    for (int q = 0; q < kR; ++q) {
-      dwv[q] = kDual && cj[q] >= 0 ? dj.dw[cj[q]] : 0.0;
+    for (int q = 0; q < kR; ++q) {  // (margin loads beside the dw gather, not behind it)
       const int64_t i = i0 + q * stride;
-      if (ck[q] >= 0 || dwv[q] != 0) {
+      if (ck[q] >= 0 || cj[q] >= 0) {
         m[q] = ym[i];
         yv[q] = y[i];
       }
+      dwv[q] = kDual && cj[q] >= 0 ? dj.dw[cj[q]] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < kR; ++q) {
@@ -656,6 +675,48 @@ bcd_rowpass_q_kernel(int64_t n, double* __restrict__ ym, const float* __restrict
       }
     }
   }
+}
+
+// Coalesced two-stage sum of the row pass's W workgroup partials part[w][i] (i < n2 =
+// 2 x LDS columns): stage 1, one workgroup per 64 outputs x one of S segments of the
+// partials, every load a 512-B run of one partial row (a thread per output striding
+// over w read one 8-B word per 64-B line: ~35 us for 768 x 4096 partials); stage 2 adds
+// the S segment sums and stores G / U (through the hot-column map). Exact int64 sums:
+// deterministic in any order.
+constexpr int kPartSeg = 16;
+
+__global__ void __launch_bounds__(256)
+bcd_part_reduce1_kernel(const long long* __restrict__ part, int W, int n2,
+                        long long* __restrict__ part2) {
+  __shared__ long long ws[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  const int w0 = (int)((int64_t)blockIdx.y * W / kPartSeg);
+  const int w1 = (int)((int64_t)(blockIdx.y + 1) * W / kPartSeg);
+  long long s = 0;
+  if (i < n2)
+    for (int w = w0 + wv; w < w1; w += 4) s += part[(int64_t)w * n2 + i];
+  ws[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && i < n2)
+    part2[(int64_t)blockIdx.y * n2 + i] = ws[0][lane] + ws[1][lane] + ws[2][lane] + ws[3][lane];
+}
+
+__global__ void __launch_bounds__(256)
+bcd_part_reduce2_kernel(const long long* __restrict__ part2, int ncols, int k2,
+                        double* __restrict__ G, double* __restrict__ U,
+                        const int32_t* __restrict__ cols) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n2 = 2 * ncols;
+  if (i >= n2) return;
+  long long s = 0;
+#pragma unroll
+  for (int q = 0; q < kPartSeg; ++q) s += part2[(int64_t)q * n2 + i];
+  const double v = (double)s * ldexp(1.0, -k2);
+  const int c = i < ncols ? i : i - ncols;
+  const int o = cols ? cols[c] : c;
+  if (i < ncols) G[o] = v;
+  else U[o] = v;
 }
 
 // objective: out[0] += sum_i log(1 + exp(-ym_i))
@@ -734,6 +795,7 @@ void bcd_grad_chunked(const int32_t* col, const int32_t* row, const float* val,
 }
 
 int bcd_rows_max_cols() { return kRowCols; }
+int bcd_part_segments() { return kPartSeg; }
 
 void bcd_grad_rows(const int32_t* col, const int32_t* row, const float* val, int64_t p0,
                    int64_t p1, int64_t c0, int64_t ncols, const double* ym, const float* y,
@@ -795,25 +857,35 @@ void bcd_dual(const int32_t* col, const int32_t* row, const float* val, int64_t 
 void bcd_rowpass(int64_t n, double* ym, const float* y, const int32_t* jcol, const float* jval,
                  const double* jdw, int64_t jncols, const int32_t* kcol, const float* kval,
                  int64_t c0, int64_t ncols, const double* delta, const uint8_t* active, int k2,
-                 int W, long long* part, double* G, double* U, double* rowq, hipStream_t st) {
+                 int W, long long* part, double* G, double* U, double* rowq,
+                 const int32_t* hcols, int64_t nhot, hipStream_t st) {
   if (n <= 0) return;
   const RowDual dj{jcol, jval, jdw, (int)jncols};
-  if (part) {  // narrow gradient of block k
-    if (ncols <= 0) return;
-    if (ncols > kRowCols) throw std::runtime_error("bcd_rowpass: narrow block ncols > 2048");
-    const int copies = std::max(1, std::min(8, kRowCols / (int)ncols));
-    if (jcol)
-      bcd_rowpass_grad_kernel<true><<<W, 512, 0, st>>>(n, ym, y, dj, kcol, kval, c0, (int)ncols,
-                                                       copies, delta, active, k2, part);
-    else
-      bcd_rowpass_grad_kernel<false><<<W, 512, 0, st>>>(n, ym, y, dj, kcol, kval, c0, (int)ncols,
-                                                        copies, delta, active, k2, part);
+  if (part) {  // gradient of block k in LDS: narrow (all columns) or wide (hot columns)
+    const int nl = (int)(hcols ? nhot : ncols);  // LDS column slots
+    if (nl <= 0) return;
+    if (nl > kRowCols) throw std::runtime_error("bcd_rowpass: > 2048 LDS columns");
+    const int copies = std::max(1, std::min(8, kRowCols / nl));
+    auto q = reinterpret_cast<double2*>(rowq);
+#define PSAMD_RP(D, H)                                                                      \
+  bcd_rowpass_grad_kernel<D, H><<<W, 512, 0, st>>>(n, ym, y, dj, kcol, kval, c0, nl, copies, \
+                                                   delta, active, k2, part, hcols, q)
+    if (jcol && hcols) PSAMD_RP(true, true);
+    else if (jcol) PSAMD_RP(true, false);
+    else if (hcols) PSAMD_RP(false, true);
+    else PSAMD_RP(false, false);
+#undef PSAMD_RP
     PSAMD_HIP_CHECK(hipGetLastError());
-    bcd_rows_reduce_kernel<<<(unsigned)(2 * ncols), 256, 0, st>>>(part, W, (int)ncols, k2, G, U);
+    long long* part2 = part + (int64_t)W * 2 * nl;  // [kPartSeg][2 nl] after the partials
+    bcd_part_reduce1_kernel<<<dim3((unsigned)((2 * nl + 63) / 64), kPartSeg), 256, 0, st>>>(
+        part, W, 2 * nl, part2);
+    PSAMD_HIP_CHECK(hipGetLastError());
+    bcd_part_reduce2_kernel<<<(unsigned)((2 * nl + 255) / 256), 256, 0, st>>>(part2, nl, k2, G, U,
+                                                                            hcols);
     PSAMD_HIP_CHECK(hipGetLastError());
     return;
   }
-  const unsigned grid = (unsigned)grid_for(n, 256 * 4, 4096);
+  const unsigned grid = (unsigned)grid_for(n, 256 * 8, 4096);
   auto q = reinterpret_cast<double2*>(rowq);
   if (jcol && kcol)
     bcd_rowpass_q_kernel<true, true><<<grid, 256, 0, st>>>(n, ym, y, dj, kcol, (int)ncols, q);

@@ -168,7 +168,8 @@ void bcd_grad_chunked(const int32_t*, const int32_t*, const float*, const int64_
                       const uint8_t*, double*, double*, double*, bool, bool, hipStream_t);
 void bcd_rowpass(int64_t, double*, const float*, const int32_t*, const float*, const double*,
                  int64_t, const int32_t*, const float*, int64_t, int64_t, const double*,
-                 const uint8_t*, int, int, long long*, double*, double*, double*, hipStream_t);
+                 const uint8_t*, int, int, long long*, double*, double*, double*, const int32_t*,
+                 int64_t, hipStream_t);
 void bcd_update(int64_t, int64_t, double*, double*, double*, double*, uint8_t*, double*, double,
                 double, double, double, unsigned long long*, bool, bool, hipStream_t);
 void bcd_replica(int64_t, int64_t, int64_t, int64_t, double*, double*, double*, uint8_t*, double,
@@ -177,6 +178,7 @@ void bcd_dual(const int32_t*, const int32_t*, const float*, int64_t, int64_t, in
               const double*, const float*, double*, int64_t, bool, hipStream_t);
 void bcd_objective(const double*, int64_t, double*, hipStream_t);
 int bcd_rows_max_cols();
+int bcd_part_segments();
 void bcd_grad_rows(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
                    const double*, const float*, int64_t, const double*, const uint8_t*, int, int,
                    long long*, double*, double*, hipStream_t);
@@ -1455,7 +1457,8 @@ PYBIND11_MODULE(_hipops, m) {
                           optional<Tensor> jdw, int64_t jncols, optional<Tensor> kcol,
                           optional<Tensor> kval, int64_t c0, int64_t ncols, Tensor delta,
                           Tensor active, int k2, int W, optional<Tensor> part,
-                          optional<Tensor> G, optional<Tensor> U, optional<Tensor> rowq) {
+                          optional<Tensor> G, optional<Tensor> U, optional<Tensor> rowq,
+                          optional<Tensor> hcols) {
     chk(ym, at::kDouble, "ym");
     chk(y, at::kFloat, "y");
     chk(delta, at::kDouble, "delta");
@@ -1481,17 +1484,24 @@ PYBIND11_MODULE(_hipops, m) {
     double* Gp = optr<double>(G, at::kDouble, "G");
     double* Up = optr<double>(U, at::kDouble, "U");
     double* rq = optr<double>(rowq, at::kDouble, "rowq");
+    const int32_t* hc = optr<int32_t>(hcols, at::kInt, "hcols");
+    const int64_t nhot = hc ? hcols->numel() : 0;
     if (pp) {
-      check(kc != nullptr, "narrow row pass needs kcol");
-      check(ncols <= psamd::bcd_rows_max_cols(), "bcd_rowpass: ncols <= 2048");
-      check(W >= 1 && part->numel() >= (int64_t)W * 2 * ncols, "part too small");
+      check(kc != nullptr, "LDS row pass needs kcol");
+      const int64_t nl = hc ? nhot : ncols;
+      check(nl <= psamd::bcd_rows_max_cols(), "bcd_rowpass: <= 2048 LDS columns");
+      check(W >= 1 && part->numel() >= (int64_t)(W + psamd::bcd_part_segments()) * 2 * nl,
+            "part: (W + bcd_part_segments) x 2 x LDS columns int64");
       check(Gp && Up && G->numel() >= ncols && U->numel() >= ncols, "G/U too small");
       check(k2 >= 0 && k2 <= 62, "fixed-point shift");
+      // hot columns of a wide block (the reduce stores G[hcols[h]]): range-checked once
+      // where they are built (ops/bcd.py hot_layout), not per call (no host sync here)
+      if (hc) check(rq != nullptr && rowq->numel() >= 2 * n, "rowq: 2 doubles per example");
     } else if (kc) {
       check(rq != nullptr && rowq->numel() >= 2 * n, "rowq: 2 doubles per example");
     }
     psamd::bcd_rowpass(n, ptr<double>(ym), ptr<float>(y), jc, jv, jd, jncols, kc, kv, c0, ncols,
-                       ptr<double>(delta), ptr<uint8_t>(active), k2, W, pp, Gp, Up, rq,
+                       ptr<double>(delta), ptr<uint8_t>(active), k2, W, pp, Gp, Up, rq, hc, nhot,
                        cur_stream());
   });
   m.def("bcd_grad", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
@@ -1557,6 +1567,7 @@ PYBIND11_MODULE(_hipops, m) {
                     unique_rows, cur_stream());
   });
   m.def("bcd_rows_max_cols", []() { return psamd::bcd_rows_max_cols(); });
+  m.def("bcd_part_segments", []() { return psamd::bcd_part_segments(); });
   m.def("bcd_grad_rows", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                      int64_t p1, int64_t c0, int64_t ncols, Tensor ym, Tensor y,
                                      Tensor delta, Tensor active, int k2, int W, Tensor part,

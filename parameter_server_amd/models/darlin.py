@@ -157,6 +157,9 @@ class Block:
     fx_k: int = 0              # its fixed-point scale 2^k
     dcol: object = None        # dense per-example layout (bcd.dense_rows) for the row pass
     dval: object = None
+    kenc: object = None        # wide block: hot / cold encoded layout (bcd.hot_layout)
+    hcols: object = None       # ... its LDS hot slot -> column map
+    chunks_cold: object = None  # ... and the chunk list of its cold columns
 
     @property
     def ncols(self):
@@ -490,8 +493,14 @@ class DarlinTrainer:
         # workgroups of the row-order gradient (3 per CU) and its partial-sum buffer
         self.rows_W = 768
         rows_max = hipops().bcd_rows_max_cols() if dev.type == "cuda" else 0
-        self.rows_part = (torch.empty(self.rows_W * 2 * max(rows_max, 1), dtype=torch.int64,
-                                      device=dev) if dev.type == "cuda" else None)
+        # (+ the row pass's segment sums behind the partials; hot-column passes of wide
+        # blocks use fewer workgroups, rows_W_hot: their per-workgroup setup and partials
+        # cover 2048 columns)
+        self.rows_W_hot = 256
+        nseg = hipops().bcd_part_segments() if dev.type == "cuda" else 0
+        self.rows_part = (torch.empty((self.rows_W + nseg) * 2 * max(rows_max, 1),
+                                      dtype=torch.int64, device=dev)
+                          if dev.type == "cuda" else None)
         # wide blocks: packed per-example gradient factors (bcd.grad rowq)
         self.rowq = (torch.empty(2 * self.rows, dtype=torch.float64, device=dev)
                      if dev.type == "cuda" else None)
@@ -520,6 +529,16 @@ class DarlinTrainer:
                 if self.fuse_rows and blk.unique_rows and 4 * (p1 - p0) >= self.rows:
                     blk.dcol, blk.dval = bcd.dense_rows(self.row_r, self.col_r, self.val_r,
                                                         p0, p1, blk.c0, self.rows)
+                    # wide block: its hottest columns summed in LDS by the row pass, the
+                    # cold ones by the chunked kernel (random per-entry gathers only for
+                    # the cold share)
+                    if not blk.row_mode and blk.chunks is not None:
+                        hl = bcd.hot_layout(blk.dcol, colptr, blk.c0, blk.c1, nhot=rows_max)
+                        if hl is not None:
+                            blk.kenc, blk.hcols, cold, nh = hl
+                            blk.chunks_cold = torch.from_numpy(cold).to(dev)
+                            vmax = 1.0 if self.val is None else float(self.val[p0:p1].abs().max())
+                            blk.fx_k = bcd.fixed_point_shift(nh, vmax)
         # model state (replicated per rank) and margins
         f64 = torch.float64
         self.w = torch.full((base,), float(cfg.init_w), dtype=f64, device=dev)
@@ -574,6 +593,17 @@ class DarlinTrainer:
                 bcd.rowpass(self.ym, self.y, self.delta, self.active, kcol=b.dcol, kval=b.dval,
                             c0=b.c0, ncols=b.ncols, k2=b.fx_k, W=self.rows_W,
                             part=self.rows_part, G=G, U=U, **jd)
+                return
+            if b.hcols is not None:  # hot columns in LDS, cold ones column by column
+                if not zeroed:  # (the reduce stores the hot sums before the chunk pass)
+                    G.zero_()
+                    U.zero_()
+                bcd.rowpass(self.ym, self.y, self.delta, self.active, kcol=b.kenc, kval=b.dval,
+                            c0=b.c0, ncols=b.ncols, k2=b.fx_k, W=self.rows_W_hot,
+                            part=self.rows_part, G=G, U=U, rowq=self.rowq, hcols=b.hcols, **jd)
+                bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym,
+                         self.y, self.delta, self.active, G, U, chunks=b.chunks_cold,
+                         zeroed=True, rowq=self.rowq, rowq_ready=True)
                 return
             bcd.rowpass(self.ym, self.y, self.delta, self.active, kcol=b.dcol, kval=b.dval,
                         c0=b.c0, ncols=b.ncols, rowq=self.rowq, **jd)

@@ -29,17 +29,29 @@ from .native import hipops, is_gpu
 HOT_BIT = 1 << 62
 
 
-def build_chunks(colptr, c0: int, c1: int, small: int = 64, hot: int = 4096) -> np.ndarray:
+SKIP_BIT = 1 << 61
+
+
+def build_chunks(colptr, c0: int, c1: int, small: int = 64, hot: int = 4096,
+                 skip=None) -> np.ndarray:
     """Load-balanced work list of the CSC columns [c0, c1) for ``grad``'s chunked
     kernel: int64 entry offsets (+ end sentinel); columns of <= ``small`` entries
     are packed whole into chunks of <= ``small`` entries, longer ("hot") columns
-    are cut into pieces of <= ``hot`` entries flagged with HOT_BIT."""
+    are cut into pieces of <= ``hot`` entries flagged with HOT_BIT. ``skip`` (bool
+    per column of the block): columns another kernel sums (the row pass's LDS hot
+    columns) become one chunk each flagged with SKIP_BIT, which the kernel passes over."""
     cp = np.asarray(colptr, dtype=np.int64)
     n = np.diff(cp[c0:c1 + 1])
     out = []
     cur, cur_len = -1, 0
     for j in np.flatnonzero(n):
         a, m = int(cp[c0 + j]), int(n[j])
+        if skip is not None and skip[j]:
+            if cur >= 0:
+                out.append(cur)
+                cur = -1
+            out.append(a | SKIP_BIT)
+            continue
         if m > small:
             if cur >= 0:
                 out.append(cur)
@@ -55,7 +67,7 @@ def build_chunks(colptr, c0: int, c1: int, small: int = 64, hot: int = 4096) -> 
         out.append(cur)
     out.append(int(cp[c1]))
     ch = np.asarray(out, dtype=np.int64)
-    pos = ch & ~HOT_BIT
+    pos = ch & ~(HOT_BIT | SKIP_BIT)
     assert np.all(np.diff(pos) > 0) and pos[0] >= cp[c0] and pos[-1] == cp[c1]
     return ch
 
@@ -132,17 +144,49 @@ def dense_rows(row_r, col_r, val_r, p0: int, p1: int, c0: int, rows: int):
     return dcol, dval
 
 
+def hot_layout(dcol, colptr, c0: int, c1: int, nhot: int = 2048, min_share: float = 0.5):
+    """Hot / cold split of a WIDE block with a dense layout (``dense_rows``): its ``nhot``
+    most frequent columns are summed in LDS by the row pass and the rest by the chunked
+    column-order kernel. Returns None when the hot columns hold < ``min_share`` of the
+    entries, else (kenc int32 [rows]: -2 - hot slot / the column (cold) / -1 none,
+    hcols int32 [nhot] hot slot -> column, chunks of the cold columns (hot ones
+    SKIP_BIT-flagged), hot entry count)."""
+    cp = np.asarray(colptr, dtype=np.int64)
+    cnt = np.diff(cp[c0:c1 + 1])
+    ncols = c1 - c0
+    if ncols <= nhot or cnt.sum() == 0:
+        return None
+    top = np.argpartition(-cnt, nhot - 1)[:nhot]
+    hot_entries = int(cnt[top].sum())
+    if hot_entries < min_share * cnt.sum():
+        return None
+    hcols = np.sort(top).astype(np.int32)
+    assert hcols[0] >= 0 and hcols[-1] < ncols
+    slot = torch.full((ncols,), -1, dtype=torch.int32)
+    slot[torch.from_numpy(hcols).long()] = torch.arange(nhot, dtype=torch.int32)
+    slot = slot.to(dcol.device)
+    has = dcol >= 0
+    hs = torch.where(has, slot[dcol.clamp_min(0).long()], torch.full_like(dcol, -1))
+    kenc = torch.where(hs >= 0, -2 - hs, dcol)
+    skip = np.zeros(ncols, dtype=bool)
+    skip[hcols] = True
+    chunks = build_chunks(cp, c0, c1, skip=skip)
+    return kenc, torch.from_numpy(hcols).to(dcol.device), chunks, hot_entries
+
+
 def rowpass(ym, y, delta, active, *, jcol=None, jval=None, jdw=None, jncols: int = 0,
             kcol=None, kval=None, c0: int = 0, ncols: int = 0, k2: int = 0, W: int = 1,
-            part=None, G=None, U=None, rowq=None):
+            part=None, G=None, U=None, rowq=None, hcols=None):
     """GPU row pass over dense block layouts (``dense_rows``): first the pending dual
     update of block j (``jcol`` / ``jval`` / its ``jdw``: ym_i += y_i dw_c x_ic), then on
     the updated margins block k's gradient: narrow (``part`` given: fixed-point column
     sums into ``G`` / ``U``, as ``grad_rows``) or the per-example factors of a wide block
-    into ``rowq`` (for ``grad(..., rowq_ready=True)``). Bitwise equal to ``dual``
-    followed by ``grad_rows`` / the rowq packing (tests/test_darlin_gpu.py)."""
+    into ``rowq`` (for ``grad(..., rowq_ready=True)``); with ``hcols`` (``hot_layout``),
+    a wide block's hot columns in LDS and the cold entries' factors into ``rowq``.
+    Equal to ``dual`` followed by ``grad_rows`` / the rowq packing up to the fixed-point
+    quantisation (tests/test_darlin_gpu.py)."""
     hipops().bcd_rowpass(ym, y, jcol, jval, jdw, int(jncols), kcol, kval, int(c0), int(ncols),
-                         delta, active, int(k2), int(W), part, G, U, rowq)
+                         delta, active, int(k2), int(W), part, G, U, rowq, hcols)
 
 
 def fixed_point_shift(entries: int, max_abs_val: float) -> int:

@@ -260,6 +260,8 @@ def test_fused_row_pass_bitwise_equal_to_separate_kernels(monkeypatch, tau, valu
         if fuse == "1":
             assert any(b.dcol is not None for b in tr.blocks)
             assert any(b.dcol is not None and b.row_mode for b in tr.blocks)
+            if not valued:  # wide slots: hot columns in LDS, cold ones column-wise
+                assert any(b.hcols is not None for b in tr.blocks)
         else:
             assert all(b.dcol is None for b in tr.blocks)
         prog = tr.train()
