@@ -32,6 +32,8 @@ namespace psamd {
 
 namespace {
 
+constexpr int kPartSeg = 16;  // segments of the row pass's two-stage partial reduce
+
 __device__ __forceinline__ double softplus_neg(double m) {  // log(1 + exp(-m))
   return m > 0 ? log1p(exp(-m)) : -m + log1p(exp(m));
 }
@@ -119,14 +121,27 @@ bcd_update_kernel(int64_t c0, int64_t ncols, double* __restrict__ G, double* __r
                   double* __restrict__ w, double* __restrict__ delta,
                   uint8_t* __restrict__ active, double* __restrict__ dw, double eta, double lambda,
                   double delta_max, double kkt_thr, unsigned long long* __restrict__ vio_bits,
-                  int consume, int nan_filtered) {
+                  int consume, int nan_filtered, const long long* __restrict__ part2, int k2) {
   double vmax = 0;
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < ncols;
        j += (int64_t)gridDim.x * blockDim.x) {
     const int64_t k = c0 + j;
     double d = 0;
-    const double gj = G[j], uj = U[j];
-    if (consume) {  // leave G / U zeroed for the block's next gradient (no memsets)
+    double gj, uj;
+    if (part2) {  // a narrow row pass's segment sums (bcd_part_reduce2's arithmetic)
+      long long sg = 0, su = 0;
+#pragma unroll
+      for (int q = 0; q < kPartSeg; ++q) {
+        sg += part2[(int64_t)q * 2 * ncols + j];
+        su += part2[(int64_t)q * 2 * ncols + ncols + j];
+      }
+      gj = (double)sg * ldexp(1.0, -k2);
+      uj = (double)su * ldexp(1.0, -k2);
+    } else {
+      gj = G[j];
+      uj = U[j];
+    }
+    if (consume && !part2) {  // leave G / U zeroed for the block's next gradient (no memsets)
       G[j] = 0;
       U[j] = 0;
     }
@@ -683,8 +698,6 @@ bcd_rowpass_q_kernel(int64_t n, double* __restrict__ ym, const float* __restrict
 // over w read one 8-B word per 64-B line: ~35 us for 768 x 4096 partials); stage 2 adds
 // the S segment sums and stores G / U (through the hot-column map). Exact int64 sums:
 // deterministic in any order.
-constexpr int kPartSeg = 16;
-
 __global__ void __launch_bounds__(256)
 bcd_part_reduce1_kernel(const long long* __restrict__ part, int W, int n2,
                         long long* __restrict__ part2) {
@@ -822,11 +835,11 @@ void bcd_grad_rows(const int32_t* col, const int32_t* row, const float* val, int
 void bcd_update(int64_t c0, int64_t ncols, double* G, double* U, double* w, double* delta,
                 uint8_t* active, double* dw, double eta, double lambda, double delta_max,
                 double kkt_thr, unsigned long long* vio_bits, bool consume, bool nan_filtered,
-                hipStream_t st) {
+                const long long* part2, int k2, hipStream_t st) {
   if (ncols <= 0) return;
   bcd_update_kernel<<<grid_for(ncols, 256, 4096), 256, 0, st>>>(
       c0, ncols, G, U, w, delta, active, dw, eta, lambda, delta_max, kkt_thr, vio_bits,
-      consume ? 1 : 0, nan_filtered ? 1 : 0);
+      consume ? 1 : 0, nan_filtered ? 1 : 0, part2, k2);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
@@ -858,7 +871,7 @@ void bcd_rowpass(int64_t n, double* ym, const float* y, const int32_t* jcol, con
                  const double* jdw, int64_t jncols, const int32_t* kcol, const float* kval,
                  int64_t c0, int64_t ncols, const double* delta, const uint8_t* active, int k2,
                  int W, long long* part, double* G, double* U, double* rowq,
-                 const int32_t* hcols, int64_t nhot, hipStream_t st) {
+                 const int32_t* hcols, int64_t nhot, long long* part2_out, hipStream_t st) {
   if (n <= 0) return;
   const RowDual dj{jcol, jval, jdw, (int)jncols};
   if (part) {  // gradient of block k in LDS: narrow (all columns) or wide (hot columns)
@@ -876,10 +889,13 @@ void bcd_rowpass(int64_t n, double* ym, const float* y, const int32_t* jcol, con
     else PSAMD_RP(false, false);
 #undef PSAMD_RP
     PSAMD_HIP_CHECK(hipGetLastError());
-    long long* part2 = part + (int64_t)W * 2 * nl;  // [kPartSeg][2 nl] after the partials
+    // [kPartSeg][2 nl] segment sums: after the partials, or (part2_out) the block's own
+    // buffer that its coordinate update reads directly (no second stage)
+    long long* part2 = part2_out ? part2_out : part + (int64_t)W * 2 * nl;
     bcd_part_reduce1_kernel<<<dim3((unsigned)((2 * nl + 63) / 64), kPartSeg), 256, 0, st>>>(
         part, W, 2 * nl, part2);
     PSAMD_HIP_CHECK(hipGetLastError());
+    if (part2_out) return;
     bcd_part_reduce2_kernel<<<(unsigned)((2 * nl + 255) / 256), 256, 0, st>>>(part2, nl, k2, G, U,
                                                                             hcols);
     PSAMD_HIP_CHECK(hipGetLastError());

@@ -169,9 +169,10 @@ void bcd_grad_chunked(const int32_t*, const int32_t*, const float*, const int64_
 void bcd_rowpass(int64_t, double*, const float*, const int32_t*, const float*, const double*,
                  int64_t, const int32_t*, const float*, int64_t, int64_t, const double*,
                  const uint8_t*, int, int, long long*, double*, double*, double*, const int32_t*,
-                 int64_t, hipStream_t);
+                 int64_t, long long*, hipStream_t);
 void bcd_update(int64_t, int64_t, double*, double*, double*, double*, uint8_t*, double*, double,
-                double, double, double, unsigned long long*, bool, bool, hipStream_t);
+                double, double, double, unsigned long long*, bool, bool, const long long*, int,
+                hipStream_t);
 void bcd_replica(int64_t, int64_t, int64_t, int64_t, double*, double*, double*, uint8_t*, double,
                  hipStream_t);
 void bcd_dual(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
@@ -1458,7 +1459,7 @@ PYBIND11_MODULE(_hipops, m) {
                           optional<Tensor> kval, int64_t c0, int64_t ncols, Tensor delta,
                           Tensor active, int k2, int W, optional<Tensor> part,
                           optional<Tensor> G, optional<Tensor> U, optional<Tensor> rowq,
-                          optional<Tensor> hcols) {
+                          optional<Tensor> hcols, optional<Tensor> part2) {
     chk(ym, at::kDouble, "ym");
     chk(y, at::kFloat, "y");
     chk(delta, at::kDouble, "delta");
@@ -1497,12 +1498,15 @@ PYBIND11_MODULE(_hipops, m) {
       // hot columns of a wide block (the reduce stores G[hcols[h]]): range-checked once
       // where they are built (ops/bcd.py hot_layout), not per call (no host sync here)
       if (hc) check(rq != nullptr && rowq->numel() >= 2 * n, "rowq: 2 doubles per example");
+      if (part2.has_value() && part2->defined())
+        check(part2->numel() >= (int64_t)psamd::bcd_part_segments() * 2 * nl,
+              "part2: segments x 2 x LDS columns int64");
     } else if (kc) {
       check(rq != nullptr && rowq->numel() >= 2 * n, "rowq: 2 doubles per example");
     }
     psamd::bcd_rowpass(n, ptr<double>(ym), ptr<float>(y), jc, jv, jd, jncols, kc, kv, c0, ncols,
                        ptr<double>(delta), ptr<uint8_t>(active), k2, W, pp, Gp, Up, rq, hc, nhot,
-                       cur_stream());
+                       optr<long long>(part2, at::kLong, "part2"), cur_stream());
   });
   m.def("bcd_grad", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                 int64_t p1, int64_t c0, int64_t ncols, Tensor ym, Tensor y,
@@ -1524,7 +1528,8 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("bcd_update", [](int64_t c0, int64_t ncols, Tensor G, Tensor U, Tensor w, Tensor delta,
                          Tensor active, Tensor dw, double eta, double lambda, double delta_max,
-                         double kkt_thr, Tensor vio_bits, bool consume, bool nan_filtered) {
+                         double kkt_thr, Tensor vio_bits, bool consume, bool nan_filtered,
+                         optional<Tensor> part2, int k2) {
     chk(G, at::kDouble, "G");
     chk(U, at::kDouble, "U");
     chk(w, at::kDouble, "w");
@@ -1536,10 +1541,15 @@ PYBIND11_MODULE(_hipops, m) {
     check(c0 >= 0 && ncols >= 0 && c0 + ncols <= w.numel(), "column block outside model");
     check(G.numel() >= ncols && U.numel() >= ncols && dw.numel() >= ncols, "G/U/dw too small");
     check(eta > 0, "eta must be > 0");
+    const long long* p2 = optr<long long>(part2, at::kLong, "part2");
+    if (p2)
+      check(part2->numel() >= (int64_t)psamd::bcd_part_segments() * 2 * ncols && k2 >= 0 &&
+                k2 <= 62,
+            "part2: segments x 2 x ncols int64 (a narrow row pass's sums)");
     psamd::bcd_update(c0, ncols, ptr<double>(G), ptr<double>(U), ptr<double>(w),
                       ptr<double>(delta), ptr<uint8_t>(active), ptr<double>(dw), eta, lambda,
                       delta_max, kkt_thr, ptr<unsigned long long>(vio_bits), consume,
-                      nan_filtered, cur_stream());
+                      nan_filtered, p2, k2, cur_stream());
   });
   m.def("bcd_replica", [](int64_t c0, int64_t ncols, int64_t own0, int64_t own1, Tensor dw,
                           Tensor w, Tensor delta, Tensor active, double delta_max) {

@@ -160,6 +160,7 @@ class Block:
     kenc: object = None        # wide block: hot / cold encoded layout (bcd.hot_layout)
     hcols: object = None       # ... its LDS hot slot -> column map
     chunks_cold: object = None  # ... and the chunk list of its cold columns
+    part2: object = None       # narrow dense block: its row pass's segment sums (1 rank)
 
     @property
     def ncols(self):
@@ -490,15 +491,18 @@ class DarlinTrainer:
         # separate kernels, for A/B)
         self.fuse_rows = dev.type == "cuda" and os.environ.get("PSAMD_DARLIN_FUSE", "1") != "0"
         self._pending_dual = None
-        # workgroups of the row-order gradient (3 per CU) and its partial-sum buffer
-        self.rows_W = 768
+        # workgroups of the row-order gradient and row pass and their partial-sum buffer
+        self.rows_W = int(os.environ.get("PSAMD_BCD_W", "256"))
         rows_max = hipops().bcd_rows_max_cols() if dev.type == "cuda" else 0
         # (+ the row pass's segment sums behind the partials; hot-column passes of wide
         # blocks use fewer workgroups, rows_W_hot: their per-workgroup setup and partials
         # cover 2048 columns)
-        self.rows_W_hot = 256
+        # (256 = one workgroup per CU for both: 2.84 ms / pass vs 3.10 at 768 narrow,
+        # 3.06 / 3.36 at 192 / 320 hot; profiles/r3_darlin_rowpass.log)
+        self.rows_W_hot = int(os.environ.get("PSAMD_BCD_WHOT", "256"))
         nseg = hipops().bcd_part_segments() if dev.type == "cuda" else 0
-        self.rows_part = (torch.empty((self.rows_W + nseg) * 2 * max(rows_max, 1),
+        self.rows_part = (torch.empty((max(self.rows_W, self.rows_W_hot) + nseg) * 2 *
+                                      max(rows_max, 1),
                                       dtype=torch.int64, device=dev)
                           if dev.type == "cuda" else None)
         # wide blocks: packed per-example gradient factors (bcd.grad rowq)
@@ -570,6 +574,14 @@ class DarlinTrainer:
         bcd.dual(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, dw, self.y,
                  self.ym, b.unique_rows)
 
+    def _defer_sums(self, b: Block, persistent: bool) -> bool:
+        """Narrow dense block on one rank, launched into its persistent buffers: its row
+        pass leaves the segment sums in b.part2 and the coordinate update adds them (one
+        launch less per block; G / U never materialise). The same predicate is evaluated
+        at launch and at finish."""
+        return (persistent and self.G == 1 and b.row_mode and b.dcol is not None
+                and not self._sharded(b))
+
     def _flush_dual(self):
         """Apply a deferred dual update on its own (before anything else reads ym)."""
         if self._pending_dual is None:
@@ -590,9 +602,15 @@ class DarlinTrainer:
                 self._pending_dual = None
                 jd = dict(jcol=j.dcol, jval=j.dval, jdw=dw, jncols=j.ncols)
             if b.row_mode:
+                p2 = None
+                if self._defer_sums(b, zeroed):  # the update reads the segment sums itself
+                    if b.part2 is None:
+                        b.part2 = torch.empty(hipops().bcd_part_segments() * 2 * b.ncols,
+                                              dtype=torch.int64, device=self.device)
+                    p2 = b.part2
                 bcd.rowpass(self.ym, self.y, self.delta, self.active, kcol=b.dcol, kval=b.dval,
                             c0=b.c0, ncols=b.ncols, k2=b.fx_k, W=self.rows_W,
-                            part=self.rows_part, G=G, U=U, **jd)
+                            part=self.rows_part, G=G, U=U, part2=p2, **jd)
                 return
             if b.hcols is not None:  # hot columns in LDS, cold ones column by column
                 if not zeroed:  # (the reduce stores the hot sums before the chunk pass)
@@ -643,8 +661,10 @@ class DarlinTrainer:
             work.wait()
         G, U = GU[:b.ncols], GU[b.ncols:]
         c = self.cfg
+        p2 = b.part2 if self._defer_sums(b, persistent) else None
         dw, _ = bcd.update(b.c0, b.ncols, G, U, self.w, self.delta, self.active, c.eta, c.l1,
-                           c.delta_max, self.kkt_thr, vio=self.vio, consume=persistent)
+                           c.delta_max, self.kkt_thr, vio=self.vio, consume=persistent,
+                           part2=p2, k2=b.fx_k)
         if persistent:
             b.busy = False
         self._dual(b, dw)

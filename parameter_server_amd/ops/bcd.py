@@ -176,17 +176,19 @@ def hot_layout(dcol, colptr, c0: int, c1: int, nhot: int = 2048, min_share: floa
 
 def rowpass(ym, y, delta, active, *, jcol=None, jval=None, jdw=None, jncols: int = 0,
             kcol=None, kval=None, c0: int = 0, ncols: int = 0, k2: int = 0, W: int = 1,
-            part=None, G=None, U=None, rowq=None, hcols=None):
+            part=None, G=None, U=None, rowq=None, hcols=None, part2=None):
     """GPU row pass over dense block layouts (``dense_rows``): first the pending dual
     update of block j (``jcol`` / ``jval`` / its ``jdw``: ym_i += y_i dw_c x_ic), then on
     the updated margins block k's gradient: narrow (``part`` given: fixed-point column
     sums into ``G`` / ``U``, as ``grad_rows``) or the per-example factors of a wide block
     into ``rowq`` (for ``grad(..., rowq_ready=True)``); with ``hcols`` (``hot_layout``),
-    a wide block's hot columns in LDS and the cold entries' factors into ``rowq``.
+    a wide block's hot columns in LDS and the cold entries' factors into ``rowq``;
+    ``part2`` (narrow): leave the segment sums there for ``update(..., part2=)`` instead
+    of storing G / U.
     Equal to ``dual`` followed by ``grad_rows`` / the rowq packing up to the fixed-point
     quantisation (tests/test_darlin_gpu.py)."""
     hipops().bcd_rowpass(ym, y, jcol, jval, jdw, int(jncols), kcol, kval, int(c0), int(ncols),
-                         delta, active, int(k2), int(W), part, G, U, rowq, hcols)
+                         delta, active, int(k2), int(W), part, G, U, rowq, hcols, part2)
 
 
 def fixed_point_shift(entries: int, max_abs_val: float) -> int:
@@ -201,13 +203,14 @@ def fixed_point_shift(entries: int, max_abs_val: float) -> int:
 
 def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
            delta_max: float, kkt_thr: float, dw=None, vio=None, consume: bool = False,
-           nan_filtered: bool = False):
+           nan_filtered: bool = False, part2=None, k2: int = 0):
     """Coordinate update of block [c0, c0+ncols). Returns (dw fp64[ncols], vio) where
     ``vio`` is an int64[1] tensor holding the max KKT violation as fp64 bits
     (max-accumulated across calls; see ``violation``). ``consume`` zeroes G / U
     after reading them. ``nan_filtered``: a KKT-filtered column's dw is NaN instead of
     0 (the reference server's mark, src/app/linear_method/darlin.h:228-231), for
-    ``replica``."""
+    ``replica``. ``part2`` (GPU): G / U come from a narrow row pass's segment sums at
+    fixed-point scale 2^k2 (``rowpass(..., part2=)``) instead of G / U."""
     dev = w.device
     if dw is None:
         dw = torch.empty(ncols, dtype=torch.float64, device=dev)
@@ -215,7 +218,7 @@ def update(c0: int, ncols: int, G, U, w, delta, active, eta: float, lam: float,
         vio = torch.zeros(1, dtype=torch.int64, device=dev)
     if is_gpu(w):
         hipops().bcd_update(c0, ncols, G, U, w, delta, active, dw, eta, lam, delta_max, kkt_thr,
-                            vio, consume, nan_filtered)
+                            vio, consume, nan_filtered, part2, int(k2))
         return dw, vio
     sl = slice(c0, c0 + ncols)
     act = active[sl].bool()
