@@ -351,3 +351,44 @@ def test_build_chunks_partitions_columns():
                 assert cols.size == 1 and n[cols[0]] > small and b - a <= hot
             else:
                 assert b - a <= small and cp[cols[0]] == a and cp[cols[-1] + 1] == b
+
+
+def test_hot_layout_splits_wide_block():
+    """Wide-block hot / cold split of the row pass (ops/bcd.py hot_layout): the nhot most
+    frequent columns get LDS slots (kenc = -2 - slot), every other entry keeps its column,
+    and the cold chunk list skips exactly the hot columns, each as one SKIP_BIT chunk."""
+    import numpy as np
+    import torch
+
+    from parameter_server_amd.ops.bcd import HOT_BIT, SKIP_BIT, hot_layout
+
+    rng = np.random.default_rng(5)
+    ncols, rows, nhot = 600, 5000, 64
+    p = 1.0 / np.arange(1, ncols + 1) ** 1.3
+    col = rng.choice(ncols, size=rows, p=p / p.sum())
+    keep = rng.random(rows) < 0.9  # some examples without an entry in the block
+    dcol = torch.from_numpy(np.where(keep, col, -1).astype(np.int32))
+    c0 = 100  # block columns [c0, c0 + ncols) of a larger model
+    cnt = np.bincount(col[keep], minlength=ncols)
+    cp = np.zeros(c0 + ncols + 1, np.int64)
+    cp[c0 + 1:] = np.cumsum(cnt)
+    out = hot_layout(dcol, cp, c0, c0 + ncols, nhot=nhot)
+    assert out is not None
+    kenc, hcols, chunks, nh = out
+    hc = hcols.numpy()
+    assert hc.size == nhot and np.all(np.diff(hc) > 0)
+    assert nh == cnt[hc].sum() and cnt[hc].min() >= np.sort(cnt)[-nhot]
+    k = kenc.numpy()
+    d = dcol.numpy()
+    hot = k <= -2
+    assert np.array_equal(hc[-2 - k[hot]], d[hot])        # slot -> its column
+    assert np.array_equal(k[~hot], d[~hot])                # cold entries / no entry kept
+    assert not np.isin(d[~hot & (d >= 0)], hc).any()
+    skip = (chunks & SKIP_BIT) != 0
+    pos = chunks & ~(HOT_BIT | SKIP_BIT)
+    col_start = {int(cp[c0 + j]): j for j in range(ncols) if cnt[j]}
+    assert sorted(col_start[int(a)] for a in pos[:-1][skip[:-1]]) == sorted(
+        j for j in hc if cnt[j])
+    assert pos[-1] == cp[c0 + ncols] and np.all(np.diff(pos) > 0)
+    # no split when the hot columns hold too little of the block
+    assert hot_layout(dcol, cp, c0, c0 + ncols, nhot=nhot, min_share=0.999) is None
