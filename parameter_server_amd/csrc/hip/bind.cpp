@@ -207,8 +207,8 @@ void wd_head(const void*, int64_t, int, const float*, const float*, const float*
              uint32_t*, int, int, hipStream_t);
 void colred_bf16(const void*, int64_t, int, const float*, float*, const float*, float*,
                  hipStream_t);
-void adam_update(float*, const float*, float*, float*, int64_t, float, float, float, float, float,
-                 float, float, void*, const int64_t*, hipStream_t);
+void adam_update(float*, float*, float*, float*, int64_t, float, float, float, float, float,
+                 float, float, void*, const int64_t*, bool, hipStream_t);
 // spmv.hip
 void spmv(bool, const int64_t*, const void*, int, const void*, int, int64_t, int64_t, const void*,
           int64_t, double, double, void*, int64_t, hipStream_t);
@@ -1857,7 +1857,7 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("adam_update", [](Tensor p, Tensor g, Tensor m_, Tensor v, double lr, double b1,
                           double b2, double eps, int64_t step, double gscale,
-                          optional<Tensor> p16, optional<Tensor> step_dev) {
+                          optional<Tensor> p16, optional<Tensor> step_dev, bool zero_grad) {
     chk(p, at::kFloat, "p");
     chk(g, at::kFloat, "g");
     chk(m_, at::kFloat, "m");
@@ -1881,7 +1881,7 @@ PYBIND11_MODULE(_hipops, m) {
     const double bc1 = 1.0 - std::pow(b1, s1), bc2 = 1.0 - std::pow(b2, s1);
     psamd::adam_update(ptr<float>(p), ptr<float>(g), ptr<float>(m_), ptr<float>(v), n, (float)lr,
                        (float)b1, (float)b2, (float)eps, (float)bc1, (float)bc2, (float)gscale,
-                       p16p, sd, cur_stream());
+                       p16p, sd, zero_grad, cur_stream());
   });
   // SparseMatrix::times (utils/matrix.py): gather (row-reduce) or scatter (atomic) over the
   // compressed major dimension; y = alpha * A x + beta * y.

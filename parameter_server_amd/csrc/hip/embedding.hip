@@ -94,7 +94,12 @@ emb_gather_rows_kernel(const int64_t* __restrict__ slot, int64_t n_host,
   }
 }
 
-// X0[p, :] = src[idx ? idx[local_col[p]] : local_col[p], :]
+// X0[p, :] = src[idx ? idx[local_col[p]] : local_col[p], :]. Each 16-lane group moves
+// kExpR rows per round with every load of the round in flight (local_col -> idx -> row
+// is a three-deep dependent chain; one row per round ran at ~2.6 TB/s, 72 us for a
+// 16,384 x 39 x 128 minibatch).
+constexpr int kExpR = 4;
+
 __global__ void __launch_bounds__(256)
 emb_expand_kernel(const int32_t* __restrict__ local_col, int64_t nnz,
                   const int64_t* __restrict__ idx, int64_t idx_cap,
@@ -102,17 +107,31 @@ emb_expand_kernel(const int32_t* __restrict__ local_col, int64_t nnz,
                   uint16_t* __restrict__ X0) {
   const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
   const int vec = D / 8;
-  for (int64_t p = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; p < nnz;
-       p += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
-    int64_t r = local_col[p];
-    if (idx) r = in_range(r, idx_cap) ? idx[r] : -1;
-    uint4* o = reinterpret_cast<uint4*>(X0 + p * D);
-    if (!in_range(r, src_rows)) {
-      for (int v = l; v < vec; v += kGroup) o[v] = make_uint4(0, 0, 0, 0);
-      continue;
+  const int64_t ng = (int64_t)gridDim.x * (blockDim.x / kGroup);
+  for (int64_t p0 = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; p0 < nnz;
+       p0 += kExpR * ng) {
+    int64_t r[kExpR];
+#pragma unroll
+    for (int q = 0; q < kExpR; ++q) {
+      const int64_t p = p0 + q * ng;
+      r[q] = p < nnz ? (int64_t)local_col[p] : -1;
     }
-    const uint4* s = reinterpret_cast<const uint4*>(src + r * D);
-    for (int v = l; v < vec; v += kGroup) o[v] = s[v];
+    if (idx) {
+#pragma unroll
+      for (int q = 0; q < kExpR; ++q) r[q] = in_range(r[q], idx_cap) ? idx[r[q]] : -1;
+    }
+    for (int v = l; v < vec; v += kGroup) {
+      uint4 x[kExpR];
+#pragma unroll
+      for (int q = 0; q < kExpR; ++q)
+        x[q] = in_range(r[q], src_rows) ? reinterpret_cast<const uint4*>(src + r[q] * D)[v]
+                                        : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < kExpR; ++q) {
+        const int64_t p = p0 + q * ng;
+        if (p < nnz) reinterpret_cast<uint4*>(X0 + p * D)[v] = x[q];
+      }
+    }
   }
 }
 
@@ -684,10 +703,10 @@ wd_head_db_kernel(double* __restrict__ metrics, int acc_stripes, float* __restri
 // step clock (step_dev: steps completed so far, advanced later in the step by the AUC
 // epilogue) the bias corrections come from it, so a captured step replays correctly.
 __global__ void __launch_bounds__(256)
-adam_update_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+adam_update_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                    float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
                    float bc1, float bc2, float gscale, uint16_t* __restrict__ p16,
-                   const int64_t* __restrict__ step_dev) {
+                   const int64_t* __restrict__ step_dev, int zero_grad) {
   if (step_dev) {
     const float s = (float)(step_dev[0] + 1);
     bc1 = 1.f - exp2f(s * log2f(b1));
@@ -696,6 +715,7 @@ adam_update_kernel(float* __restrict__ p, const float* __restrict__ g, float* __
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const float gi = g[i] * gscale;
+    if (zero_grad) g[i] = 0.f;  // leave the next step's accumulators zeroed (no fill pass)
     const float mi = b1 * m[i] + (1.f - b1) * gi;
     const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
     m[i] = mi;
@@ -729,7 +749,7 @@ void emb_gather_rows(const int64_t* slot, int64_t n, const int32_t* n_dev, int64
 void emb_expand(const int32_t* local_col, int64_t nnz, const int64_t* idx, int64_t idx_cap,
                 const void* src, int64_t src_rows, int D, void* X0, hipStream_t st) {
   if (nnz <= 0) return;
-  emb_expand_kernel<<<grid_for(nnz, 16, 8192), 256, 0, st>>>(
+  emb_expand_kernel<<<grid_for(nnz, 16 * kExpR, 8192), 256, 0, st>>>(
       local_col, nnz, idx, idx_cap, reinterpret_cast<const uint16_t*>(src), src_rows, D,
       reinterpret_cast<uint16_t*>(X0));
   PSAMD_HIP_CHECK(hipGetLastError());
@@ -826,13 +846,13 @@ void colred_bf16(const void* x, int64_t B, int N, const float* s, float* out, co
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void adam_update(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
+void adam_update(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1,
                  float b2, float eps, float bc1, float bc2, float gscale, void* p16,
-                 const int64_t* step_dev, hipStream_t st) {
+                 const int64_t* step_dev, bool zero_grad, hipStream_t st) {
   if (n <= 0) return;
   adam_update_kernel<<<grid_for(n, 256, 4096), 256, 0, st>>>(
       p, g, m, v, n, lr, b1, b2, eps, bc1, bc2, gscale, reinterpret_cast<uint16_t*>(p16),
-      step_dev);
+      step_dev, zero_grad ? 1 : 0);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

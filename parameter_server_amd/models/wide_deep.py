@@ -418,7 +418,7 @@ class WideDeepTrainer(EmbeddingPS):
             acts.append(GM.linear_forward(acts[-1], self.W16[i], self.b[i], relu=True,
                                           backend=cfg.gemm, bias16=self.b16[i]))
         # ---------------- head (wide + deep), loss, metrics, head grads
-        self.grad.zero_()
+        # (the flat gradient is zero here: allocated zeroed, and Adam zeroes it once read)
         H = acts[-1]
         dH = torch.empty_like(H)
         L = len(cfg.hidden)
@@ -467,7 +467,7 @@ class WideDeepTrainer(EmbeddingPS):
         # so the whole step can replay from a HIP graph
         E.adam(self.param, self.grad, self.m, self.v, lr=cfg.mlp_lr, step=self.step_count,
                gscale=1.0 / (B * self.G), p16=self.param16,
-               step_dev=self.step_dev if self.gpu else None)
+               step_dev=self.step_dev if self.gpu else None, zero_grad=True)
         auc_from_hist(self.hist, self.metrics, self.step_dev)
         self.examples += B
 

@@ -207,12 +207,14 @@ def colsum(x: torch.Tensor, out: torch.Tensor, accumulate: bool = False):
 
 
 def adam(p, g, m, v, *, lr, step: int, b1=0.9, b2=0.999, eps=1e-8, gscale=1.0, p16=None,
-         step_dev=None):
+         step_dev=None, zero_grad: bool = False):
     """Adam on fp32 master weights (+ bf16 copy ``p16``). ``step_dev`` (GPU): int64 device
     step clock holding the steps completed so far; the kernel takes its bias corrections
-    from it (step = step_dev + 1), so the update can be replayed from a HIP graph."""
+    from it (step = step_dev + 1), so the update can be replayed from a HIP graph.
+    ``zero_grad``: g is zeroed once read (the next step accumulates into it)."""
     if is_gpu(p):
-        hipops().adam_update(p, g, m, v, lr, b1, b2, eps, step, gscale, p16, step_dev)
+        hipops().adam_update(p, g, m, v, lr, b1, b2, eps, step, gscale, p16, step_dev,
+                             bool(zero_grad))
         return
     gs = g * gscale
     m.mul_(b1).add_((1 - b1) * gs)
@@ -220,6 +222,8 @@ def adam(p, g, m, v, *, lr, step: int, b1=0.9, b2=0.999, eps=1e-8, gscale=1.0, p
     p.sub_(lr * (m / (1 - b1 ** step)) / (torch.sqrt(v / (1 - b2 ** step)) + eps))
     if p16 is not None:
         p16.copy_(p.to(torch.bfloat16))
+    if zero_grad:
+        g.zero_()
 
 
 def xavier(n_out: int, n_in: int, gen: torch.Generator) -> torch.Tensor:
