@@ -293,7 +293,10 @@ criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_
   __shared__ float spw[3][kGenRows];
   __shared__ float s_cm1[26];
   __shared__ uint32_t s_seed[40];  // per-slot streams + the label stream
-  if (row0_dev) row0 += (*row0_dev) * row_scale;
+  // (an L2-coherent vector load, not a scalar-cache load: the counter is advanced on the
+  // device between graph replays)
+  if (row0_dev)
+    row0 += __hip_atomic_load(row0_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * row_scale;
   const int t = threadIdx.x, lane = t & 63;
   const int g = __builtin_amdgcn_readfirstlane(t >> 6);
   const float oma = 1.f - alpha, inv_oma = 1.f / oma;
