@@ -407,7 +407,9 @@ def main():
     ap.add_argument("--num-features", type=float, default=1e9)
     ap.add_argument("--algo", default="ftrl")
     ap.add_argument("--consistency", default="ssp:4")
-    ap.add_argument("--graph", type=int, default=1, help="capture the 1-GPU step in a HIP graph")
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="replay the pipeline's pieces from HIP graphs: 1 / 0, -1 = auto (on with "
+                         "more than one rank or emulated peers, off on one GPU)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="generate + localise minibatch t+1 on a high-priority side stream "
                          "while step t trains (HIP graphs per stream / step segment)")
@@ -475,6 +477,14 @@ def main():
         comm = (nccl_loopback(args.emulate_peers, device) if eb == "nccl"
                 else LoopbackComm(args.emulate_peers, device))
     G, rank = comm.world, comm.rank
+    if args.graph < 0:
+        # auto: one GPU issues its kernels eagerly -- the HIP-graph replays of the same
+        # pipeline measured ~10 % slower there (0.119-0.120 vs 0.105-0.109 ms / step at
+        # B = 65,536, 0.0645 vs 0.0575 at B = 10,000, same box; profiles/r3_s2_graph_ab.log)
+        # while the host still issues a step in ~0.075 ms. With peers the step has many
+        # more launches plus the collectives and the eager host issue becomes the bound
+        # (8 emulated peers: 0.179 eager vs 0.147 graphs), so graphs stay on there.
+        args.graph = 1 if G > 1 else 0
     if G != args.gpus and rank == 0 and not args.emulate_peers:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {G}", file=sys.stderr)
     B = args.minibatch
