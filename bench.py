@@ -23,7 +23,14 @@ import os
 import sys
 import time
 
-import torch
+# HIP graph kernel nodes dispatched as ordinary packets instead of the runtime's
+# pre-captured packet batches: each graph replay costs ~2 us less GPU time on this ROCm
+# (benchmarks/probe_graph_overhead.py: 5 one-kernel graphs 50.4 -> 39.6 us; 8 emulated
+# peers 0.149-0.150 -> 0.140-0.144 ms / step, profiles/r3_s2_graph_ab.log). Set before
+# the HIP runtime initialises; inherited by the ranks bench.py spawns.
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
+import torch  # noqa: E402
 
 # thread-local capture: the RCCL watchdog thread of ProcessGroupNCCL keeps querying its
 # events while a rank captures its compute segments; global mode would invalidate
