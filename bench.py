@@ -23,14 +23,7 @@ import os
 import sys
 import time
 
-# HIP graph kernel nodes dispatched as ordinary packets instead of the runtime's
-# pre-captured packet batches: each graph replay costs ~2 us less GPU time on this ROCm
-# (benchmarks/probe_graph_overhead.py: 5 one-kernel graphs 50.4 -> 39.6 us; 8 emulated
-# peers 0.149-0.150 -> 0.140-0.144 ms / step, profiles/r3_s2_graph_ab.log). Set before
-# the HIP runtime initialises; inherited by the ranks bench.py spawns.
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
-
-import torch  # noqa: E402
+import torch
 
 # thread-local capture: the RCCL watchdog thread of ProcessGroupNCCL keeps querying its
 # events while a rank captures its compute segments; global mode would invalidate
@@ -93,15 +86,25 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     sides = [torch.cuda.Stream(device, priority=prio) for _ in range(nprep)]
     bufs = [(keys, labels)] + [(torch.empty_like(keys), torch.empty_like(labels))
                                for _ in range(NB - 1)]
+    # row counter of each preparation stream: on the host while preparations are issued
+    # eagerly (the rows go to the generator as a launch argument), on the device once
+    # they replay from graphs (a captured preparation reads and advances it)
+    hctr = [0] * nprep
     ctr = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(nprep)]
     locs = [None] * NB
+    mode = {"capture": False}
 
     def prep(b):  # buffer b belongs to prep stream b % nprep (rows (nprep*k + s) * B)
         sidx = b % nprep
         k, lab = bufs[b]
-        criteo_batch(B, seed=seed, row0=sidx * B, num_features=N, device=device, keys=k,
-                     labels=lab, row0_dev=ctr[sidx], row_scale=nprep * B)
-        ctr[sidx].add_(1)
+        if mode["capture"]:
+            criteo_batch(B, seed=seed, row0=sidx * B, num_features=N, device=device, keys=k,
+                         labels=lab, row0_dev=ctr[sidx], row_scale=nprep * B)
+            ctr[sidx].add_(1)
+        else:
+            criteo_batch(B, seed=seed, row0=(hctr[sidx] * nprep + sidx) * B, num_features=N,
+                         device=device, keys=k, labels=lab)
+            hctr[sidx] += 1
         locs[b] = tr.localize(k, buf=b)
 
     def segments(t):
@@ -291,6 +294,9 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
 
     iterate.release = release
     gp = []
+    for s_ in range(nprep):  # the replays continue the eager row counts on the device
+        ctr[s_].fill_(hctr[s_])
+    mode["capture"] = True
     for b in range(NB):  # t0 % NB == 0: buffer b <-> minibatch t0 + b
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
