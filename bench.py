@@ -378,6 +378,12 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
         if watch is not None:
             watch.beat("capture", j)
         xh, wh = halves(t0 + j)
+        if ccomm and asp_apply == "tail":
+            # the push apply replays at the tail of the exchange half anyway: move it
+            # behind all-to-all B before grouping, so A + resolve + B stay ONE captured
+            # graph (a graph replay costs ~6-8 us of GPU time and ~11 us of host time,
+            # profiles/r3_s2_graph_ab.log; ASP issued 6 graphs per step, now 5)
+            xh = [x for x in xh if x[0] != "async"] + [x for x in xh if x[0] == "async"]
         xplans[j] = capture(xh)
         wplans[j] = capture(wh)
     # capture ran nothing: the workspaces of the minibatches in flight still hold
