@@ -581,7 +581,10 @@ def main():
         scope.enter_context(torch.cuda.stream(torch.cuda.Stream(device, priority=int(mprio))))
     watch.beat("warmup")
     if gpu and args.pipeline and (G == 1 or tr.padded):
-        nprep = args.prep_streams or 3
+        # eager 1-GPU pipeline: 2 preparation streams (0.109-0.110 vs 0.112-0.116 ms / step
+        # with 3 over 300 steps on one box, equal over 20; 4 oversubscribes the hardware
+        # queues: 0.29-3.6 ms; profiles/r3_s2_graph_ab.log); graph replays / peers: 3
+        nprep = args.prep_streams or (2 if G == 1 and not args.graph else 3)
         args.prep_streams = nprep
         run, graph_used = pipeline(tr, B, N, seed, keys, labels, device, args, nprep=nprep,
                                    watch=watch)
