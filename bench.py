@@ -303,6 +303,16 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             prep(b)
         gp.append(g)
         held.append(g)
+    if args.graph == 2:
+        # preparations only: each replays as one graph on its side stream (one host
+        # launch instead of ~5, its graph-launch latency off the training stream), the
+        # training step is issued eagerly
+        preps[:] = [g.replay for g in gp]
+        torch.cuda.synchronize()
+        for _ in range(P):
+            iterate()
+        torch.cuda.synchronize()
+        return iterate, True
 
     # The all-to-alls are captured too (PSAMD_CAPTURE_COMM=0: eager between the graph
     # replays, as in round 2), so a step issues graph replays and event waits only.
@@ -427,8 +437,9 @@ def main():
     ap.add_argument("--algo", default="ftrl")
     ap.add_argument("--consistency", default="ssp:4")
     ap.add_argument("--graph", type=int, default=-1,
-                    help="replay the pipeline's pieces from HIP graphs: 1 / 0, -1 = auto (on with "
-                         "more than one rank or emulated peers, off on one GPU)")
+                    help="replay the pipeline's pieces from HIP graphs: 1 / 0, 2 = the data "
+                         "preparations only, -1 = auto (on with more than one rank or emulated "
+                         "peers, off on one GPU)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="generate + localise minibatch t+1 on a high-priority side stream "
                          "while step t trains (HIP graphs per stream / step segment)")
@@ -584,7 +595,7 @@ def main():
         # eager 1-GPU pipeline: 2 preparation streams (0.109-0.110 vs 0.112-0.116 ms / step
         # with 3 over 300 steps on one box, equal over 20; 4 oversubscribes the hardware
         # queues: 0.29-3.6 ms; profiles/r3_s2_graph_ab.log); graph replays / peers: 3
-        nprep = args.prep_streams or (2 if G == 1 and not args.graph else 3)
+        nprep = args.prep_streams or (2 if G == 1 and args.graph != 1 else 3)
         args.prep_streams = nprep
         run, graph_used = pipeline(tr, B, N, seed, keys, labels, device, args, nprep=nprep,
                                    watch=watch)
