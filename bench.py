@@ -76,6 +76,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     R = tr.R if tr.padded else 1
     P = NB * R // math.gcd(NB, R)  # graph phases: (buffer, ring position) pairs
     main = torch.cuda.current_stream(device)
+    set_stream = torch.cuda.set_stream
     # preparation streams at high priority, also with N > 1: ROCm maps streams of each
     # priority onto its own set of hardware queues, and normal-priority pool streams
     # share queues with the null stream and RCCL's streams, which serialises a
@@ -203,7 +204,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             xs.wait_event(chain[(t - 1) % E])
         if asp:  # ring entry of exchange t is free again once that apply is done
             aclock.wait_for(tr.sched.apply_gate(t), xs)
-        with torch.cuda.stream(xs):
+        set_stream(xs)  # (main is current here; see iterate)
+        try:
             if asp_apply == "tail" or post:
                 # the apply after the event the worker waits for (ssp post apply: the
                 # next exchange waits for it; asp: nothing waits for it)
@@ -236,6 +238,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             else:
                 run_plan(xplan(t), t, xs)
                 ev_x[t % E].record(xs)
+        finally:
+            set_stream(main)
 
     def iterate():
         t = state["t"]
@@ -254,13 +258,20 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
         # longer than the steady state behind the preparation's launch)
         run_plan(wplan(t), t, main)
         ev_buf[cur].record(main)
-        ev_w[t % E].record(main)
+        if split:  # (only the exchange halves wait for the worker half)
+            ev_w[t % E].record(main)
         nb = (t + nprep) % NB                 # minibatch t + nprep
         s = sides[nb % nprep]
         s.wait_event(ev_buf[nb])              # step(t + nprep - NB) done with bufs[nb]
-        with torch.cuda.stream(s):
+        # a plain set_stream there and back (main is current here): the torch.cuda.stream
+        # context re-queries the current stream and the lazy-init state on every use, ~10
+        # us of host time per step (cProfile, profiles/r3_s3_host_issue.log)
+        set_stream(s)
+        try:
             preps[nb]()
             ev_prep[nb].record(s)
+        finally:
+            set_stream(main)
         if xmode == "prep":
             issue_exchange(t + xd)
         state["t"] = t + 1

@@ -196,6 +196,10 @@ class SparseLRTrainer:
         self._xx = 0  # padded exchanges issued (exchange halves run)
         self.pending = None
         self._prefetch = None
+        # 1 GPU: entry scan + optimizer update fused (PSAMD_FUSED_UPDATE=0: scan, then
+        # kv_update); read once, not per step (host issue time)
+        self._fused_update = os.environ.get("PSAMD_FUSED_UPDATE", "1") != "0"
+        self._coef_views = {}  # B -> self.coef[:B]
         self.step_count = 0
         self.examples = 0
         self.comm_bytes = 0
@@ -293,13 +297,15 @@ class SparseLRTrainer:
             self._prefetch = None
         _cmp = trace_range("compute")
         _cmp.__enter__()
-        if push[0] == "local" and push[2] is not None and fused_update_ok(
-                loc, w_local, B=B, width=width or 0, row_ptr=row_ptr, rows=rows, vals=vals) and \
-                os.environ.get("PSAMD_FUSED_UPDATE", "1") != "0":
+        if push[0] == "local" and push[2] is not None and self._fused_update and fused_update_ok(
+                loc, w_local, B=B, width=width or 0, row_ptr=row_ptr, rows=rows, vals=vals):
             # 1 GPU: the entry scan applies the FTRL / AdaGrad / SGD update and the AUC
             # epilogue itself (tp_seg_update)
+            coef = self._coef_views.get(B)
+            if coef is None:
+                coef = self._coef_views[B] = self.coef[:B]
             linear_fwd_bwd(loc, w_local, labels, B=B, width=width, vals=vals, loss=self.cfg.loss,
-                           coef=self.coef[:B], metrics=self.metrics, hist=self.hist,
+                           coef=coef, metrics=self.metrics, hist=self.hist,
                            update=(self.table.slots, push[1], self.rule, self.stats,
                                    self.step_dev))
             _cmp.__exit__(None, None, None)

@@ -98,6 +98,7 @@ class Localizer:
         n = self.max_nnz
         dev = self.device
         self.gpu = dev.type == "cuda"
+        self._tp_views = None  # (n, n-sized workspace views) of the last "tp" call
         if mode not in ("sort", "part", "tp"):
             raise ValueError(f"unknown localisation mode {mode!r}")
         if mode == "part" and not (self.gpu and hipops().partloc_supported(n, self.bits)):
@@ -201,11 +202,16 @@ class Localizer:
                           None if self.lazy_cols else self.local_col,
                           self.n_uniq, self.t_nent, self.grad, self.t_pieces, self.err,
                           getattr(self, "tp_prof", None))
+            # unique keys <= n: expose n-sized views (the workspace is tile-rounded); the
+            # views of the last n are kept (4 slices are ~4 us of host time per call)
+            v = self._tp_views
+            if v is None or v[0] != n:
+                v = self._tp_views = (n, self.uniq[:n], self.local_col[:n], self.grad[:n],
+                                      self.t_pieces[:n])
             tile = TileInfo(self.t_rep, self.t_dcnt, self.t_nent, self.t_psum, self.t_ent_uid,
-                            not self.lazy_cols, self.t_pieces[:n])
-            # unique keys <= n: expose n-sized views (the workspace is tile-rounded)
-            return Localized(self.uniq[:n], self.seg_start, self.pos_s, self.segid,
-                             self.local_col[:n], self.n_uniq, self.grad[:n], None, n, tile=tile)
+                            not self.lazy_cols, v[4])
+            return Localized(v[1], self.seg_start, self.pos_s, self.segid, v[2], self.n_uniq,
+                             v[3], None, n, tile=tile)
         if self.mode == "part":
             H.localize_part(keys, self.bits, self.ptemp, self.pos_s, self.segid, self.uniq,
                             self.seg_start, self.local_col, self.n_uniq, self.grad, self.hess,
