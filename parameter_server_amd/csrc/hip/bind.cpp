@@ -7,8 +7,10 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <functional>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "common.cuh"
 
@@ -283,6 +285,119 @@ int64_t slot_capacity(const Tensor& slots) {
   return cap;
 }
 
+// ---- validate-once launchers (the single ops and LaunchList share them) ----
+using Launch = std::function<void(hipStream_t)>;
+struct LaunchList {
+  std::vector<Launch> ops;
+};
+
+Launch make_kv_resolve(Tensor slots, Tensor keys, optional<Tensor> n_dev, Tensor out_slot,
+                       optional<Tensor> out_w, bool insert, int init_type, double init_v,
+                       double init_s, uint64_t seed, optional<Tensor> err,
+                       optional<Tensor> inserted, uint64_t home_base, uint64_t home_m) {
+  const int64_t cap = slot_capacity(slots);
+  chk(keys, at::kLong, "keys");
+  chk(out_slot, at::kLong, "out_slot");
+  const int64_t n = keys.numel();
+  check(out_slot.numel() >= n, "out_slot too small");
+  float* w = optr<float>(out_w, at::kFloat, "out_w");
+  if (w) check(out_w->numel() >= n, "out_w too small");
+  int32_t* nd = optr<int32_t>(n_dev, at::kInt, "n_dev");
+  int32_t* ep = optr<int32_t>(err, at::kInt, "err");
+  int32_t* ip = optr<int32_t>(inserted, at::kInt, "inserted");
+  // (the lambda's tensor copies keep the buffers alive as long as the launcher)
+  return [=, keep = std::vector<optional<Tensor>>{slots, keys, n_dev, out_slot, out_w, err,
+                                                  inserted}](hipStream_t st) {
+    psamd::kv_resolve(slots.data_ptr(), cap, ptr<uint64_t>(keys), n, nd, ptr<int64_t>(out_slot), w,
+                      insert, init_type, (float)init_v, (float)init_s, seed, ep, ip, home_base,
+                      home_m, st);
+  };
+}
+
+Launch make_tp_seg_update(Tensor pos_s, Tensor segid, int64_t n, Tensor n_ent, Tensor psum,
+                          Tensor seg_start, Tensor n_uniq, Tensor pieces, Tensor slot_idx,
+                          Tensor slots, int algo, int lr_type, double alpha, double beta,
+                          double l1, double l2, double grad_scale, double max_delta,
+                          optional<Tensor> stats, optional<Tensor> hist, optional<Tensor> metrics,
+                          optional<Tensor> step_counter) {
+  chk(pos_s, at::kInt, "pos_s");
+  chk(segid, at::kInt, "segid");
+  chk(n_ent, at::kInt, "n_ent");
+  chk(psum, at::kFloat, "psum");
+  chk(seg_start, at::kInt, "seg_start");
+  chk(n_uniq, at::kInt, "n_uniq");
+  chk(pieces, at::kLong, "pieces");
+  chk(slot_idx, at::kLong, "slot_idx");
+  const int64_t cap = slot_capacity(slots);
+  check(n > 0, "tp_seg_update: n > 0");
+  check(alpha > 0, "learning rate alpha must be > 0");
+  const int64_t N = psamd::tploc_stride(n);
+  check(pos_s.numel() >= N && segid.numel() >= N && psum.numel() >= N &&
+            seg_start.numel() >= N + 1, "tp_seg_update: entry buffers < stride");
+  const int64_t ucap = std::min(pieces.numel(), slot_idx.numel());
+  uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
+  double* mp = optr<double>(metrics, at::kDouble, "metrics");
+  constexpr int kBins = 2048;
+  if (hp) check(mp && hist->numel() % (2 * kBins) == 0 && hist->numel() / (2 * kBins) <= 8,
+                "tp_seg_update: hist = stripes x 2 x 2048 (<= 8 stripes) with metrics");
+  double* sp = optr<double>(stats, at::kDouble, "stats");
+  const int sstripes = acc_stripes_of(stats);
+  const int hstripes = hp ? (int)(hist->numel() / (2 * kBins)) : 1;
+  int64_t* cp = optr<int64_t>(step_counter, at::kLong, "step_counter");
+  return [=, keep = std::vector<optional<Tensor>>{pos_s, segid, n_ent, psum, seg_start, n_uniq,
+                                                  pieces, slot_idx, slots, stats, hist, metrics,
+                                                  step_counter}](hipStream_t st) {
+    psamd::tp_seg_update(ptr<int32_t>(pos_s), ptr<int32_t>(segid), n, ptr<int32_t>(n_ent),
+                         ptr<float>(psum), ptr<int32_t>(seg_start), ptr<int32_t>(n_uniq),
+                         reinterpret_cast<unsigned long long*>(pieces.data_ptr()), ucap,
+                         ptr<int64_t>(slot_idx), slots.data_ptr(), cap, algo, lr_type, (float)alpha,
+                         (float)beta, (float)l1, (float)l2, (float)grad_scale, (float)max_delta,
+                         sp, sstripes, hp, kBins, hstripes, mp, cp, st);
+  };
+}
+
+Launch make_tp_fwd_bwd(Tensor rep, Tensor dcnt, Tensor ent_uid, int64_t n, int width,
+                       optional<Tensor> vals, Tensor w_local, Tensor labels, int64_t B,
+                       int loss_type, Tensor coef, optional<Tensor> metrics,
+                       optional<Tensor> hist, int nbins, Tensor psum, Tensor pos_s, Tensor segid,
+                       Tensor n_ent, Tensor grad, bool reduce) {
+  chk(rep, at::kShort, "rep");
+  chk(dcnt, at::kInt, "dcnt");
+  chk(ent_uid, at::kInt, "ent_uid");
+  chk(w_local, at::kFloat, "w_local");
+  chk(labels, at::kFloat, "labels");
+  chk(coef, at::kFloat, "coef");
+  chk(psum, at::kFloat, "psum");
+  chk(pos_s, at::kInt, "pos_s");
+  chk(segid, at::kInt, "segid");
+  chk(n_ent, at::kInt, "n_ent");
+  chk(grad, at::kFloat, "grad");
+  check(psamd::tp_fwd_bwd_supported(width) && n == B * (int64_t)width && n > 0,
+        "tp_fwd_bwd: fixed width 9..64 (tp_fwd_bwd_supported) and n == B * width");
+  const int64_t N = psamd::tploc_stride(n);
+  check(rep.numel() >= n && dcnt.numel() >= N / psamd::tploc_tile() && ent_uid.numel() >= N,
+        "tp_fwd_bwd: rep / dcnt / ent_uid");
+  check(psum.numel() >= N && pos_s.numel() >= N && segid.numel() >= N, "tp_fwd_bwd buffers");
+  check(labels.numel() >= B && coef.numel() >= B, "labels/coef too small");
+  const float* v = optr<float>(vals, at::kFloat, "vals");
+  if (v) check(vals->numel() >= n, "vals too small");
+  uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
+  if (hp) check(nbins > 0 && nbins <= 8192 && hist->numel() >= 2 * nbins, "hist size");
+  double* mp = optr<double>(metrics, at::kDouble, "metrics");
+  if (mp) check(metrics->numel() >= 5, "metrics needs >= 5 slots");
+  const int mstripes = acc_stripes_of(metrics);
+  const int hstripes = hp ? (int)std::max<int64_t>(1, hist->numel() / (2 * nbins)) : 1;
+  return [=, keep = std::vector<optional<Tensor>>{rep, dcnt, ent_uid, vals, w_local, labels, coef,
+                                                  metrics, hist, psum, pos_s, segid, n_ent,
+                                                  grad}](hipStream_t st) {
+    psamd::tp_fwd_bwd(ptr<uint16_t>(rep), ptr<int32_t>(dcnt), ptr<int32_t>(ent_uid), n, width, v,
+                      ptr<float>(w_local), w_local.numel(), ptr<float>(labels), B, loss_type,
+                      ptr<float>(coef), mp, hp, nbins, mstripes, hstripes, ptr<float>(psum),
+                      ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<int32_t>(n_ent),
+                      ptr<float>(grad), grad.numel(), reduce, st);
+  };
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_hipops, m) {
@@ -301,18 +416,8 @@ PYBIND11_MODULE(_hipops, m) {
                          optional<Tensor> out_w, bool insert, int init_type, double init_v,
                          double init_s, uint64_t seed, optional<Tensor> err,
                          optional<Tensor> inserted, uint64_t home_base, uint64_t home_m) {
-    const int64_t cap = slot_capacity(slots);
-    chk(keys, at::kLong, "keys");
-    chk(out_slot, at::kLong, "out_slot");
-    const int64_t n = keys.numel();
-    check(out_slot.numel() >= n, "out_slot too small");
-    float* w = optr<float>(out_w, at::kFloat, "out_w");
-    if (w) check(out_w->numel() >= n, "out_w too small");
-    psamd::kv_resolve(slots.data_ptr(), cap, ptr<uint64_t>(keys), n,
-                      optr<int32_t>(n_dev, at::kInt, "n_dev"), ptr<int64_t>(out_slot), w, insert,
-                      init_type, (float)init_v, (float)init_s, seed,
-                      optr<int32_t>(err, at::kInt, "err"),
-                      optr<int32_t>(inserted, at::kInt, "inserted"), home_base, home_m, cur_stream());
+    make_kv_resolve(slots, keys, n_dev, out_slot, out_w, insert, init_type, init_v, init_s, seed,
+                    err, inserted, home_base, home_m)(cur_stream());
   }, py::arg("slots"), py::arg("keys"), py::arg("n_dev"), py::arg("out_slot"),
      py::arg("out_w"), py::arg("insert"), py::arg("init_type"), py::arg("init_v"),
      py::arg("init_s"), py::arg("seed"), py::arg("err"), py::arg("inserted"),
@@ -525,35 +630,9 @@ PYBIND11_MODULE(_hipops, m) {
                             double beta, double l1, double l2, double grad_scale,
                             double max_delta, optional<Tensor> stats, optional<Tensor> hist,
                             optional<Tensor> metrics, optional<Tensor> step_counter) {
-    chk(pos_s, at::kInt, "pos_s");
-    chk(segid, at::kInt, "segid");
-    chk(n_ent, at::kInt, "n_ent");
-    chk(psum, at::kFloat, "psum");
-    chk(seg_start, at::kInt, "seg_start");
-    chk(n_uniq, at::kInt, "n_uniq");
-    chk(pieces, at::kLong, "pieces");
-    chk(slot_idx, at::kLong, "slot_idx");
-    const int64_t cap = slot_capacity(slots);
-    check(n > 0, "tp_seg_update: n > 0");
-    check(alpha > 0, "learning rate alpha must be > 0");
-    const int64_t N = psamd::tploc_stride(n);
-    check(pos_s.numel() >= N && segid.numel() >= N && psum.numel() >= N &&
-              seg_start.numel() >= N + 1, "tp_seg_update: entry buffers < stride");
-    const int64_t ucap = std::min(pieces.numel(), slot_idx.numel());
-    uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
-    double* mp = optr<double>(metrics, at::kDouble, "metrics");
-    constexpr int kBins = 2048;
-    if (hp) check(mp && hist->numel() % (2 * kBins) == 0 && hist->numel() / (2 * kBins) <= 8,
-                  "tp_seg_update: hist = stripes x 2 x 2048 (<= 8 stripes) with metrics");
-    psamd::tp_seg_update(ptr<int32_t>(pos_s), ptr<int32_t>(segid), n, ptr<int32_t>(n_ent),
-                         ptr<float>(psum), ptr<int32_t>(seg_start), ptr<int32_t>(n_uniq),
-                         reinterpret_cast<unsigned long long*>(pieces.data_ptr()), ucap,
-                         ptr<int64_t>(slot_idx),
-                         slots.data_ptr(), cap, algo, lr_type, (float)alpha, (float)beta,
-                         (float)l1, (float)l2, (float)grad_scale, (float)max_delta,
-                         optr<double>(stats, at::kDouble, "stats"), acc_stripes_of(stats), hp,
-                         kBins, hp ? (int)(hist->numel() / (2 * kBins)) : 1, mp,
-                         optr<int64_t>(step_counter, at::kLong, "step_counter"), cur_stream());
+    make_tp_seg_update(pos_s, segid, n, n_ent, psum, seg_start, n_uniq, pieces, slot_idx, slots,
+                       algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta, stats, hist,
+                       metrics, step_counter)(cur_stream());
   });
   m.def("tp_gather", [](Tensor rep, Tensor ent_uid, int64_t n, Tensor local_col) {
     chk(rep, at::kShort, "rep");
@@ -579,37 +658,51 @@ PYBIND11_MODULE(_hipops, m) {
                          int loss_type, Tensor coef, optional<Tensor> metrics,
                          optional<Tensor> hist, int nbins, Tensor psum, Tensor pos_s,
                          Tensor segid, Tensor n_ent, Tensor grad, bool reduce) {
-    chk(rep, at::kShort, "rep");
-    chk(dcnt, at::kInt, "dcnt");
-    chk(ent_uid, at::kInt, "ent_uid");
-    chk(w_local, at::kFloat, "w_local");
-    chk(labels, at::kFloat, "labels");
-    chk(coef, at::kFloat, "coef");
-    chk(psum, at::kFloat, "psum");
-    chk(pos_s, at::kInt, "pos_s");
-    chk(segid, at::kInt, "segid");
-    chk(n_ent, at::kInt, "n_ent");
-    chk(grad, at::kFloat, "grad");
-    check(psamd::tp_fwd_bwd_supported(width) && n == B * (int64_t)width && n > 0,
-          "tp_fwd_bwd: fixed width 9..64 (tp_fwd_bwd_supported) and n == B * width");
-    const int64_t N = psamd::tploc_stride(n);
-    check(rep.numel() >= n && dcnt.numel() >= N / psamd::tploc_tile() && ent_uid.numel() >= N,
-          "tp_fwd_bwd: rep / dcnt / ent_uid");
-    check(psum.numel() >= N && pos_s.numel() >= N && segid.numel() >= N, "tp_fwd_bwd buffers");
-    check(labels.numel() >= B && coef.numel() >= B, "labels/coef too small");
-    const float* v = optr<float>(vals, at::kFloat, "vals");
-    if (v) check(vals->numel() >= n, "vals too small");
-    uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
-    if (hp) check(nbins > 0 && nbins <= 8192 && hist->numel() >= 2 * nbins, "hist size");
-    double* mp = optr<double>(metrics, at::kDouble, "metrics");
-    if (mp) check(metrics->numel() >= 5, "metrics needs >= 5 slots");
-    psamd::tp_fwd_bwd(ptr<uint16_t>(rep), ptr<int32_t>(dcnt), ptr<int32_t>(ent_uid), n, width, v,
-                      ptr<float>(w_local), w_local.numel(), ptr<float>(labels), B, loss_type,
-                      ptr<float>(coef), mp, hp, nbins, acc_stripes_of(metrics),
-                      hp ? (int)std::max<int64_t>(1, hist->numel() / (2 * nbins)) : 1,
-                      ptr<float>(psum), ptr<int32_t>(pos_s), ptr<int32_t>(segid),
-                      ptr<int32_t>(n_ent), ptr<float>(grad), grad.numel(), reduce, cur_stream());
+    make_tp_fwd_bwd(rep, dcnt, ent_uid, n, width, vals, w_local, labels, B, loss_type, coef,
+                    metrics, hist, nbins, psum, pos_s, segid, n_ent, grad, reduce)(cur_stream());
   });
+  // A validate-once launch list: the add_* calls check their arguments exactly as the
+  // single ops above and keep the tensors alive; run() issues every launch in order on
+  // the current stream with no per-call argument conversion. The 1-GPU sparse-LR step
+  // (resolve, fused forward + backward, fused scan + update) runs from one per
+  // minibatch buffer: three pybind crossings with 60 tensor / scalar arguments cost
+  // ~10 us of host issue time per step (profiles/r3_s3_host_issue.log).
+  py::class_<LaunchList>(m, "LaunchList")
+      .def(py::init<>())
+      .def("add_kv_resolve", [](LaunchList& l, Tensor slots, Tensor keys, optional<Tensor> n_dev,
+                                Tensor out_slot, optional<Tensor> out_w, bool insert,
+                                int init_type, double init_v, double init_s, uint64_t seed,
+                                optional<Tensor> err, optional<Tensor> inserted,
+                                uint64_t home_base, uint64_t home_m) {
+        l.ops.push_back(make_kv_resolve(slots, keys, n_dev, out_slot, out_w, insert, init_type,
+                                        init_v, init_s, seed, err, inserted, home_base, home_m));
+      })
+      .def("add_tp_fwd_bwd", [](LaunchList& l, Tensor rep, Tensor dcnt, Tensor ent_uid, int64_t n,
+                                int width, optional<Tensor> vals, Tensor w_local, Tensor labels,
+                                int64_t B, int loss_type, Tensor coef, optional<Tensor> metrics,
+                                optional<Tensor> hist, int nbins, Tensor psum, Tensor pos_s,
+                                Tensor segid, Tensor n_ent, Tensor grad, bool reduce) {
+        l.ops.push_back(make_tp_fwd_bwd(rep, dcnt, ent_uid, n, width, vals, w_local, labels, B,
+                                        loss_type, coef, metrics, hist, nbins, psum, pos_s, segid,
+                                        n_ent, grad, reduce));
+      })
+      .def("add_tp_seg_update", [](LaunchList& l, Tensor pos_s, Tensor segid, int64_t n,
+                                   Tensor n_ent, Tensor psum, Tensor seg_start, Tensor n_uniq,
+                                   Tensor pieces, Tensor slot_idx, Tensor slots, int algo,
+                                   int lr_type, double alpha, double beta, double l1, double l2,
+                                   double grad_scale, double max_delta, optional<Tensor> stats,
+                                   optional<Tensor> hist, optional<Tensor> metrics,
+                                   optional<Tensor> step_counter) {
+        l.ops.push_back(make_tp_seg_update(pos_s, segid, n, n_ent, psum, seg_start, n_uniq, pieces,
+                                           slot_idx, slots, algo, lr_type, alpha, beta, l1, l2,
+                                           grad_scale, max_delta, stats, hist, metrics,
+                                           step_counter));
+      })
+      .def("__len__", [](const LaunchList& l) { return l.ops.size(); })
+      .def("run", [](const LaunchList& l) {
+        const hipStream_t st = cur_stream();
+        for (const auto& op : l.ops) op(st);
+      });
   // ---------------- fixed-capacity exchange (exchange.hip) ----------------
   // buffers: send/recv int32 [G * H]; row layout documented in exchange.hip
   m.def("kv_resolve_rows", [](Tensor slots, Tensor recv, int64_t H, int64_t C, int kw,

@@ -41,12 +41,13 @@ from ..ops.countmin import CountMinSketch
 from ..ops.keymix import key_bits_for, unmix
 from ..ops.kv_table import InitRule, KVTable, UpdateRule, next_pow2
 from ..ops.linear import (AUC_BINS, HIST_STRIPES, accum_total, auc_from_hist, fused_update_ok,
-                          linear_fwd_bwd, new_accum)
+                          linear_fwd_bwd, loss_id, new_accum)
 from ..ops.localize import Localizer
 from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.consistency import ExchangeSchedule, parse_consistency
 from ..parallel.partition import KeyPartition
+from ..utils.trace import enabled as trace_enabled
 from ..utils.trace import trace_range
 
 
@@ -200,6 +201,8 @@ class SparseLRTrainer:
         # kv_update); read once, not per step (host issue time)
         self._fused_update = os.environ.get("PSAMD_FUSED_UPDATE", "1") != "0"
         self._coef_views = {}  # B -> self.coef[:B]
+        self._plans = {}  # 1 GPU: native launch lists of the fused step (_step_plan)
+        self._use_plans = os.environ.get("PSAMD_STEP_PLAN", "1") != "0"
         self.step_count = 0
         self.examples = 0
         self.comm_bytes = 0
@@ -269,6 +272,17 @@ class SparseLRTrainer:
         B = labels.numel()
         if width is None and row_ptr is None:
             width = self.cfg.max_nnz_per_example
+        if (self.G == 1 and self.gpu and self.filter is None and self._fused_update
+                and self._use_plans and row_ptr is None and rows is None and vals is None and prefetch is None
+                and not trace_enabled()):
+            if loc is None:
+                loc = self.localizer(keys)
+            plan = self._step_plan(loc, labels, B, width)
+            if plan is not None:  # resolve + fused forward/backward + fused scan/update
+                plan.run()
+                self.step_count += 1
+                self.examples += B
+                return
         if row_ptr is not None and rows is None and self.gpu:
             rows = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
             hipops().csr_rows(row_ptr, rows)
@@ -330,6 +344,40 @@ class SparseLRTrainer:
             auc_from_hist(self.hist, self.metrics, self.step_dev)
         self.step_count += 1
         self.examples += B
+
+    def _step_plan(self, loc, labels, B: int, width: int):
+        """The 1-GPU fused step (kv_resolve, tp_fwd_bwd, tp_seg_update: the same launches
+        ``step`` issues one by one below) as a native ``LaunchList`` over the fixed
+        workspaces of one localisation buffer and one label buffer: arguments are
+        validated once, and a step is one host call (profiles/r3_s3_host_issue.log).
+        None when the fused tp path does not apply to this minibatch."""
+        t = loc.tile
+        if t is None:
+            return None
+        # (object ids: a cached plan holds its tensors, so no other tensor takes their id)
+        key = (id(t.rep), id(loc.uniq), id(labels), B, width, loc.nnz, id(self.rule),
+               id(self.table.init))
+        plan = self._plans.get(key)
+        if plan is None:
+            if not fused_update_ok(loc, self.w_buf, B=B, width=width):
+                return None
+            H, tb = hipops(), self.table
+            it, iv, isd, seed = tb.init.args()
+            plan = H.LaunchList()
+            plan.add_kv_resolve(tb.slots, loc.uniq, loc.n_uniq, self.slot_buf, self.w_buf, True,
+                                it, iv, isd, seed, tb._err, tb._inserted, tb.home_base, tb.home_m)
+            coef = self.coef[:B]
+            plan.add_tp_fwd_bwd(t.rep, t.dcnt, t.ent_uid, loc.nnz, width, None, self.w_buf, labels,
+                                B, loss_id(self.cfg.loss), coef, self.metrics, self.hist,
+                                AUC_BINS, t.psum, loc.pos_s, loc.segid, t.n_ent, loc.grad, False)
+            plan.add_tp_seg_update(loc.pos_s, loc.segid, loc.nnz, t.n_ent, t.psum, loc.seg_start,
+                                   loc.n_uniq, t.pieces, self.slot_buf, tb.slots,
+                                   *self.rule.args(), self.stats, self.hist, self.metrics,
+                                   self.step_dev)
+            if len(self._plans) >= 16:  # (callers passing fresh label tensors every step)
+                self._plans.clear()
+            self._plans[key] = plan
+        return plan
 
     # --------------------------------------------- padded exchange (G > 1, default)
     def step_segments(self, keys: torch.Tensor, labels: torch.Tensor, *, width=None,

@@ -132,11 +132,18 @@ def linear_backward(loc, coef, *, B: int, width: int = 0, rows=None, vals=None, 
     return loc.grad, loc.hess
 
 
+_FB_WIDTHS: dict[int, bool] = {}  # width -> tp_fwd_bwd has a kernel instance for it
+
+
 def _tp_fused(loc, w_local, B, width, row_ptr, rows) -> bool:
     t = getattr(loc, "tile", None)
-    return (t is not None and t.ent_uid is not None and row_ptr is None and rows is None
-            and bool(width) and loc.nnz == B * width and is_gpu(w_local)
-            and hipops().tp_fwd_bwd_supported(width))
+    if not (t is not None and t.ent_uid is not None and row_ptr is None and rows is None
+            and bool(width) and loc.nnz == B * width and is_gpu(w_local)):
+        return False
+    ok = _FB_WIDTHS.get(width)
+    if ok is None:  # (asked once per width: a native call per step is host issue time)
+        ok = _FB_WIDTHS[width] = bool(hipops().tp_fwd_bwd_supported(width))
+    return ok
 
 
 def linear_fwd_bwd(loc, w_local, labels, *, B: int, width: int = 0, row_ptr=None, rows=None,

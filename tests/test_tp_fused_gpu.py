@@ -174,3 +174,39 @@ def test_fused_seg_update_matches_scan_then_update(algo, monkeypatch):
     assert pa["loss"] == pytest.approx(pb["loss"], rel=1e-4)
     assert pa["auc"] == pytest.approx(pb["auc"], abs=1e-3)
     assert pa["nnz_w"] == pytest.approx(pb["nnz_w"], abs=3)
+
+
+def test_native_step_plan_matches_op_by_op():
+    """1 GPU: the step issued from the validate-once native LaunchList (_step_plan) runs
+    the launches the op-by-op path issues: the same keys, and weights / state / metrics
+    equal to float rounding (hot keys combine their chunk pieces through atomics, whose
+    order varies from run to run)."""
+    from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+
+    B = 16384
+    outs = []
+    for native in (True, False):
+        cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B, table_capacity=1 << 22)
+        tr = SparseLRTrainer(cfg, device=DEV)
+        if not native:
+            tr._step_plan = lambda *a, **k: None
+        keys = torch.empty(B * 39, dtype=torch.int64, device=DEV)
+        labels = torch.empty(B, dtype=torch.float32, device=DEV)
+        for t in range(5):
+            criteo_batch(B, seed=4, row0=t * B, num_features=cfg.num_features, device=DEV,
+                         keys=keys, labels=labels)
+            tr.step(keys, labels, width=39)
+        if native:
+            assert len(tr._plans) == 1  # one plan, replayed every step
+        p = tr.progress()
+        k, w, z, n = tr.table.occupied()
+        o = torch.argsort(k)
+        outs.append((p, k[o].cpu(), w[o].cpu(), z[o].cpu(), n[o].cpu()))
+    (pa, ka, wa, za, na), (pb, kb, wb, zb, nb) = outs
+    assert torch.equal(ka, kb)
+    torch.testing.assert_close(wa, wb, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(za, zb, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(na, nb, rtol=1e-4, atol=1e-4)
+    assert pa["examples"] == pb["examples"] == 5 * B
+    assert pa["loss"] == pytest.approx(pb["loss"], rel=1e-4)
+    assert pa["auc"] == pytest.approx(pb["auc"], abs=1e-3)
