@@ -94,10 +94,19 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     ctr = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(nprep)]
     locs = [None] * NB
     mode = {"capture": False}
+    # 1 GPU, flat layout: step t also pulls minibatch t+1 (in its update launch), and each
+    # preparation (generator + tile + flat bucket kernels) is ONE native launch-list call:
+    # buffer b holds minibatches b, b + NB, ... = rows (b + k * NB) * B
+    flat = getattr(tr, "localize_mode", "") == "tpf" and not tr.padded
+    fplans = ([tr.prep_plan(b, bufs[b][0], bufs[b][1], seed=seed, row0=b * B, row_step=NB * B,
+                            num_features=N) for b in range(NB)] if flat else None)
 
     def prep(b):  # buffer b belongs to prep stream b % nprep (rows (nprep*k + s) * B)
         sidx = b % nprep
         k, lab = bufs[b]
+        if fplans is not None:
+            locs[b] = fplans[b]()
+            return
         if mode["capture"]:
             criteo_batch(B, seed=seed, row0=sidx * B, num_features=N, device=device, keys=k,
                          labels=lab, row0_dev=ctr[sidx], row_scale=nprep * B)
@@ -111,7 +120,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     def segments(t):
         b = t % NB
         k, lab = bufs[b]
-        return tr.step_segments(k, lab, width=39, loc=locs[b], step=t)
+        return tr.step_segments(k, lab, width=39, loc=locs[b], step=t,
+                                next_loc=locs[(t + 1) % NB] if flat else None)
 
     split = tr.padded and tr.lag >= 1
     asp = tr.padded and tr.asp
@@ -253,6 +263,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             main.wait_event(ev_x[t % E])
         else:
             main.wait_event(ev_prep[cur])     # minibatch t is localised
+            if flat:                          # ... and t+1 (its pull runs in step t)
+                main.wait_event(ev_prep[(t + 1) % NB])
         # the training step is issued first: after an idle GPU (the first timed step)
         # its kernels start one graph launch earlier (short runs: step 0 took ~0.1 ms
         # longer than the steady state behind the preparation's launch)
@@ -291,7 +303,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     warm += (-warm) % P  # capture at a multiple of P: phase j <-> buffer j % NB, ring j % R
     for _ in range(warm):
         iterate()
-    if not args.graph:
+    if not args.graph or flat:  # (flat: eager launch lists; their row cursors live on the host)
         return iterate, False
     torch.cuda.synchronize()
     t0 = state["t"]

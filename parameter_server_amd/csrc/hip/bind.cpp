@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdint>
 #include <functional>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -53,6 +54,17 @@ void tp_seg_update(const int32_t*, const int32_t*, int64_t, const int32_t*, cons
                    const int32_t*, const int32_t*, unsigned long long*, int64_t, const int64_t*, void*,
                    int64_t, int, int, float, float, float, float, float, float, double*, int,
                    uint32_t*, int, int, double*, int64_t*, hipStream_t);
+int tpf_groups(int64_t, int);
+int tpf_key_region();
+int tpf_entry_region();
+size_t tpf_temp_bytes(int64_t, int);
+void localize_tpf(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint16_t*, uint64_t*,
+                  int32_t*, uint16_t*, int32_t*, int32_t*, hipStream_t);
+void tpf_step(int64_t, int, const int32_t*, const int32_t*, const uint16_t*, const uint32_t*,
+              const float*, int64_t, const int32_t*, const uint64_t*, const int32_t*,
+              const uint16_t*, uint32_t*, float*, int64_t, void*, int64_t, uint64_t, uint64_t, int,
+              float, float, uint64_t, int32_t*, int32_t*, int, int, float, float, float, float,
+              float, float, double*, int, uint32_t*, int, int, double*, int64_t*, hipStream_t);
 int64_t tploc_stride(int64_t);
 int tploc_tile();
 bool tploc_supported(int64_t, int);
@@ -356,28 +368,37 @@ Launch make_tp_seg_update(Tensor pos_s, Tensor segid, int64_t n, Tensor n_ent, T
   };
 }
 
-Launch make_tp_fwd_bwd(Tensor rep, Tensor dcnt, Tensor ent_uid, int64_t n, int width,
+// ent_uid = None: the flat layout (w_local = w_ent in tile-entry order, no entry CSC;
+// pos_s / segid / n_ent / grad unused and reduce must be false)
+Launch make_tp_fwd_bwd(Tensor rep, Tensor dcnt, optional<Tensor> ent_uid, int64_t n, int width,
                        optional<Tensor> vals, Tensor w_local, Tensor labels, int64_t B,
                        int loss_type, Tensor coef, optional<Tensor> metrics,
-                       optional<Tensor> hist, int nbins, Tensor psum, Tensor pos_s, Tensor segid,
-                       Tensor n_ent, Tensor grad, bool reduce) {
+                       optional<Tensor> hist, int nbins, Tensor psum, optional<Tensor> pos_s,
+                       optional<Tensor> segid, optional<Tensor> n_ent, optional<Tensor> grad,
+                       bool reduce) {
   chk(rep, at::kShort, "rep");
   chk(dcnt, at::kInt, "dcnt");
-  chk(ent_uid, at::kInt, "ent_uid");
+  const int32_t* eu = optr<int32_t>(ent_uid, at::kInt, "ent_uid");
   chk(w_local, at::kFloat, "w_local");
   chk(labels, at::kFloat, "labels");
   chk(coef, at::kFloat, "coef");
   chk(psum, at::kFloat, "psum");
-  chk(pos_s, at::kInt, "pos_s");
-  chk(segid, at::kInt, "segid");
-  chk(n_ent, at::kInt, "n_ent");
-  chk(grad, at::kFloat, "grad");
+  int32_t* ps = optr<int32_t>(pos_s, at::kInt, "pos_s");
+  int32_t* sg = optr<int32_t>(segid, at::kInt, "segid");
+  int32_t* ne = optr<int32_t>(n_ent, at::kInt, "n_ent");
+  float* gr = optr<float>(grad, at::kFloat, "grad");
   check(psamd::tp_fwd_bwd_supported(width) && n == B * (int64_t)width && n > 0,
         "tp_fwd_bwd: fixed width 9..64 (tp_fwd_bwd_supported) and n == B * width");
   const int64_t N = psamd::tploc_stride(n);
-  check(rep.numel() >= n && dcnt.numel() >= N / psamd::tploc_tile() && ent_uid.numel() >= N,
-        "tp_fwd_bwd: rep / dcnt / ent_uid");
-  check(psum.numel() >= N && pos_s.numel() >= N && segid.numel() >= N, "tp_fwd_bwd buffers");
+  check(rep.numel() >= n && dcnt.numel() >= N / psamd::tploc_tile(), "tp_fwd_bwd: rep / dcnt");
+  check(psum.numel() >= N, "tp_fwd_bwd: psum < stride");
+  if (eu) {
+    check(ent_uid->numel() >= N, "tp_fwd_bwd: ent_uid < stride");
+    check(ps && sg && ne && gr && pos_s->numel() >= N && segid->numel() >= N,
+          "tp_fwd_bwd: entry CSC buffers");
+  } else {
+    check(w_local.numel() >= N && !reduce, "tp_fwd_bwd flat: w_ent >= stride, no reduce");
+  }
   check(labels.numel() >= B && coef.numel() >= B, "labels/coef too small");
   const float* v = optr<float>(vals, at::kFloat, "vals");
   if (v) check(vals->numel() >= n, "vals too small");
@@ -387,15 +408,150 @@ Launch make_tp_fwd_bwd(Tensor rep, Tensor dcnt, Tensor ent_uid, int64_t n, int w
   if (mp) check(metrics->numel() >= 5, "metrics needs >= 5 slots");
   const int mstripes = acc_stripes_of(metrics);
   const int hstripes = hp ? (int)std::max<int64_t>(1, hist->numel() / (2 * nbins)) : 1;
+  const int64_t gcap = gr ? grad->numel() : 0;
   return [=, keep = std::vector<optional<Tensor>>{rep, dcnt, ent_uid, vals, w_local, labels, coef,
                                                   metrics, hist, psum, pos_s, segid, n_ent,
                                                   grad}](hipStream_t st) {
-    psamd::tp_fwd_bwd(ptr<uint16_t>(rep), ptr<int32_t>(dcnt), ptr<int32_t>(ent_uid), n, width, v,
+    psamd::tp_fwd_bwd(ptr<uint16_t>(rep), ptr<int32_t>(dcnt), eu, n, width, v,
                       ptr<float>(w_local), w_local.numel(), ptr<float>(labels), B, loss_type,
                       ptr<float>(coef), mp, hp, nbins, mstripes, hstripes, ptr<float>(psum),
-                      ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<int32_t>(n_ent),
-                      ptr<float>(grad), grad.numel(), reduce, st);
+                      ps, sg, ne, gr, gcap, reduce, st);
   };
+}
+
+// Flat-layout buffers of one localisation (Localizer mode "tpf"): checked against the
+// geometry of an n-key minibatch.
+struct TpfBufs {
+  Tensor cnt, uniqf, ent_pos, ent_j, slot_u;
+};
+void check_tpf(const TpfBufs& f, int64_t n, int bits, const char* what) {
+  chk(f.cnt, at::kInt, "cnt");
+  chk(f.uniqf, at::kLong, "uniqf");
+  chk(f.ent_pos, at::kInt, "ent_pos");
+  chk(f.ent_j, at::kShort, "ent_j");
+  chk(f.slot_u, at::kInt, "slot_u");
+  check(psamd::tploc_supported(n, bits), std::string(what) + ": tp geometry (2..34 key bits)");
+  const int64_t g = psamd::tpf_groups(n, bits);
+  check(f.cnt.numel() >= 4 * g && f.uniqf.numel() >= g * psamd::tpf_key_region() &&
+            f.slot_u.numel() >= g * psamd::tpf_key_region() &&
+            f.ent_pos.numel() >= g * psamd::tpf_entry_region() &&
+            f.ent_j.numel() >= g * psamd::tpf_entry_region(),
+        std::string(what) + ": flat regions smaller than the geometry");
+}
+
+Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor dcnt, Tensor rep,
+                         Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err) {
+  chk(keys, at::kLong, "keys");
+  chk(temp, at::kByte, "temp");
+  chk(dcnt, at::kInt, "dcnt");
+  chk(rep, at::kShort, "rep");
+  chk(err, at::kInt, "err");
+  check(n > 0 && keys.numel() >= n, "localize_tpf: n keys");
+  check_tpf(TpfBufs{cnt, uniqf, ent_pos, ent_j, ent_pos}, n, bits, "localize_tpf");
+  const int64_t T = psamd::tploc_stride(n) / psamd::tploc_tile();
+  check(dcnt.numel() >= T && rep.numel() >= n, "localize_tpf: dcnt / rep");
+  check((size_t)temp.numel() >= psamd::tpf_temp_bytes(n, bits), "localize_tpf: temp too small");
+  const psamd::KeyMix km = make_keymix(bits);
+  return [=, keep = std::vector<Tensor>{keys, temp, dcnt, rep, uniqf, ent_pos, ent_j, cnt,
+                                        err}](hipStream_t st) {
+    psamd::localize_tpf(ptr<uint64_t>(keys), n, km, temp.data_ptr(), (size_t)temp.numel(),
+                        ptr<int32_t>(dcnt), ptr<uint16_t>(rep), ptr<uint64_t>(uniqf),
+                        ptr<int32_t>(ent_pos), ptr<uint16_t>(ent_j), ptr<int32_t>(cnt),
+                        ptr<int32_t>(err), st);
+  };
+}
+
+// The flat step boundary: update A (optional) then pull B (optional), same n.
+Launch make_tpf_step(int64_t n, int bits, optional<TpfBufs> A, optional<Tensor> psum,
+                     optional<TpfBufs> B, optional<Tensor> w_ent, Tensor slots, int init_type,
+                     double init_v, double init_s, uint64_t seed, optional<Tensor> err,
+                     optional<Tensor> inserted, uint64_t home_base, uint64_t home_m, int algo,
+                     int lr_type, double alpha, double beta, double l1, double l2,
+                     double grad_scale, double max_delta, optional<Tensor> stats,
+                     optional<Tensor> hist, optional<Tensor> metrics,
+                     optional<Tensor> step_counter) {
+  const int64_t cap = slot_capacity(slots);
+  check(cap <= ((int64_t)1 << 32), "tpf_step: u32 slot ids need <= 2^32 slots");
+  check(A.has_value() || B.has_value(), "tpf_step: nothing to do");
+  check(alpha > 0, "learning rate alpha must be > 0");
+  const int64_t N = psamd::tploc_stride(n);
+  if (A) {
+    check_tpf(*A, n, bits, "tpf_step A");
+    check(psum.has_value(), "tpf_step: update needs psum");
+    chk(*psum, at::kFloat, "psum");
+    check(psum->numel() >= N, "tpf_step: psum < stride");
+  }
+  if (B) {
+    check_tpf(*B, n, bits, "tpf_step B");
+    check(w_ent.has_value(), "tpf_step: pull needs w_ent");
+    chk(*w_ent, at::kFloat, "w_ent");
+    check(w_ent->numel() >= N, "tpf_step: w_ent < stride");
+  }
+  uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
+  double* mp = optr<double>(metrics, at::kDouble, "metrics");
+  constexpr int kBins = 2048;
+  if (hp) check(mp && hist->numel() % (2 * kBins) == 0 && hist->numel() / (2 * kBins) <= 8,
+                "tpf_step: hist = stripes x 2 x 2048 (<= 8 stripes) with metrics");
+  double* sp = optr<double>(stats, at::kDouble, "stats");
+  const int sstripes = acc_stripes_of(stats);
+  const int hstripes = hp ? (int)(hist->numel() / (2 * kBins)) : 1;
+  int64_t* cp = optr<int64_t>(step_counter, at::kLong, "step_counter");
+  int32_t* ep = optr<int32_t>(err, at::kInt, "err");
+  int32_t* ip = optr<int32_t>(inserted, at::kInt, "inserted");
+  std::vector<optional<Tensor>> keep{psum, w_ent, slots, err, inserted, stats, hist, metrics,
+                                     step_counter};
+  for (const auto* f : {A ? &*A : nullptr, B ? &*B : nullptr})
+    if (f) keep.insert(keep.end(), {f->cnt, f->uniqf, f->ent_pos, f->ent_j, f->slot_u});
+  const TpfBufs* a = A ? &*A : nullptr;
+  const TpfBufs* b = B ? &*B : nullptr;
+  auto p32 = [](const TpfBufs* f, Tensor TpfBufs::*m) -> int32_t* {
+    return f ? reinterpret_cast<int32_t*>((f->*m).data_ptr()) : nullptr;
+  };
+  int32_t *ca = p32(a, &TpfBufs::cnt), *pa = p32(a, &TpfBufs::ent_pos);
+  uint16_t* ja = reinterpret_cast<uint16_t*>(p32(a, &TpfBufs::ent_j));
+  uint32_t* sa = reinterpret_cast<uint32_t*>(p32(a, &TpfBufs::slot_u));
+  int32_t *cb = p32(b, &TpfBufs::cnt), *pb = p32(b, &TpfBufs::ent_pos);
+  uint16_t* jb = reinterpret_cast<uint16_t*>(p32(b, &TpfBufs::ent_j));
+  uint32_t* sb = reinterpret_cast<uint32_t*>(p32(b, &TpfBufs::slot_u));
+  uint64_t* ub = reinterpret_cast<uint64_t*>(p32(b, &TpfBufs::uniqf));
+  float* ps = A ? ptr<float>(*psum) : nullptr;
+  float* we = B ? ptr<float>(*w_ent) : nullptr;
+  const int64_t pcap = A ? psum->numel() : 0, wcap = B ? w_ent->numel() : 0;
+  return [=](hipStream_t st) {
+    (void)keep;
+    psamd::tpf_step(n, bits, ca, pa, ja, sa, ps, pcap, cb, ub, pb, jb, sb, we, wcap,
+                    slots.data_ptr(), cap, home_base, home_m, init_type, (float)init_v,
+                    (float)init_s, seed, ep, ip, algo, lr_type, (float)alpha, (float)beta,
+                    (float)l1, (float)l2, (float)grad_scale, (float)max_delta, sp, sstripes, hp,
+                    kBins, hstripes, mp, cp, st);
+  };
+}
+
+// Synthetic minibatch generator with a row cursor kept in the launcher: run k uses rows
+// [row0 + k * row_step, + B) (a prepared-minibatch buffer is refilled every row_step / B
+// minibatches), so a launch list regenerates fresh data on every run with the row offset
+// as a plain launch argument (no device counter, no extra launch).
+Launch make_criteo_gen(uint64_t seed, int64_t row0, int64_t row_step, int64_t B,
+                       uint64_t num_features, double alpha, Tensor keys, Tensor labels) {
+  chk(keys, at::kLong, "keys");
+  chk(labels, at::kFloat, "labels");
+  check(keys.numel() >= B * 39 && labels.numel() >= B, "criteo_gen buffers too small");
+  check(alpha > 1.0, "power-law alpha must be > 1");
+  check(num_features > 0 && B > 0, "num_features > 0, B > 0");
+  auto cursor = std::make_shared<int64_t>(row0);
+  return [=, keep = std::vector<Tensor>{keys, labels}](hipStream_t st) {
+    psamd::criteo_gen(seed, *cursor, nullptr, 1, B, num_features, (float)alpha,
+                      ptr<uint64_t>(keys), ptr<float>(labels), st);
+    *cursor += row_step;
+  };
+}
+
+// (cnt, uniqf, ent_pos, ent_j, slot_u) from Python
+optional<TpfBufs> tpf_bufs(const optional<py::tuple>& t) {
+  if (!t.has_value() || t->is_none()) return c10::nullopt;
+  check(t->size() == 5, "flat buffers: (cnt, uniqf, ent_pos, ent_j, slot_u)");
+  return TpfBufs{(*t)[0].cast<Tensor>(), (*t)[1].cast<Tensor>(), (*t)[2].cast<Tensor>(),
+                 (*t)[3].cast<Tensor>(), (*t)[4].cast<Tensor>()};
 }
 
 }  // namespace
@@ -644,6 +800,28 @@ PYBIND11_MODULE(_hipops, m) {
                      cur_stream());
   });
   m.def("tp_fwd_bwd_supported", [](int width) { return psamd::tp_fwd_bwd_supported(width); });
+  // ---- flat 1-GPU layout (tploc.hip "tpf")
+  m.def("tpf_groups", [](int64_t n, int bits) { return psamd::tpf_groups(n, bits); });
+  m.def("tpf_key_region", []() { return psamd::tpf_key_region(); });
+  m.def("tpf_entry_region", []() { return psamd::tpf_entry_region(); });
+  m.def("tpf_temp_bytes", [](int64_t n, int bits) { return psamd::tpf_temp_bytes(n, bits); });
+  m.def("localize_tpf", [](Tensor keys, int bits, Tensor temp, Tensor dcnt, Tensor rep,
+                           Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err) {
+    make_localize_tpf(keys, keys.numel(), bits, temp, dcnt, rep, uniqf, ent_pos, ent_j, cnt,
+                      err)(cur_stream());
+  });
+  m.def("tpf_step", [](int64_t n, int bits, optional<py::tuple> A, optional<Tensor> psum,
+                       optional<py::tuple> B, optional<Tensor> w_ent, Tensor slots, int init_type,
+                       double init_v, double init_s, uint64_t seed, optional<Tensor> err,
+                       optional<Tensor> inserted, uint64_t home_base, uint64_t home_m, int algo,
+                       int lr_type, double alpha, double beta, double l1, double l2,
+                       double grad_scale, double max_delta, optional<Tensor> stats,
+                       optional<Tensor> hist, optional<Tensor> metrics,
+                       optional<Tensor> step_counter) {
+    make_tpf_step(n, bits, tpf_bufs(A), psum, tpf_bufs(B), w_ent, slots, init_type, init_v,
+                  init_s, seed, err, inserted, home_base, home_m, algo, lr_type, alpha, beta, l1,
+                  l2, grad_scale, max_delta, stats, hist, metrics, step_counter)(cur_stream());
+  });
   // phase marks of the fused kernel (tuning aid): 16 int64 per tile, or None to disable
   m.def("tp_fb_set_prof", [](optional<Tensor> prof) {
     uint64_t* p = nullptr;
@@ -653,11 +831,12 @@ PYBIND11_MODULE(_hipops, m) {
     }
     psamd::tp_fb_set_prof(p);
   });
-  m.def("tp_fwd_bwd", [](Tensor rep, Tensor dcnt, Tensor ent_uid, int64_t n, int width,
+  m.def("tp_fwd_bwd", [](Tensor rep, Tensor dcnt, optional<Tensor> ent_uid, int64_t n, int width,
                          optional<Tensor> vals, Tensor w_local, Tensor labels, int64_t B,
                          int loss_type, Tensor coef, optional<Tensor> metrics,
-                         optional<Tensor> hist, int nbins, Tensor psum, Tensor pos_s,
-                         Tensor segid, Tensor n_ent, Tensor grad, bool reduce) {
+                         optional<Tensor> hist, int nbins, Tensor psum, optional<Tensor> pos_s,
+                         optional<Tensor> segid, optional<Tensor> n_ent, optional<Tensor> grad,
+                         bool reduce) {
     make_tp_fwd_bwd(rep, dcnt, ent_uid, n, width, vals, w_local, labels, B, loss_type, coef,
                     metrics, hist, nbins, psum, pos_s, segid, n_ent, grad, reduce)(cur_stream());
   });
@@ -677,11 +856,12 @@ PYBIND11_MODULE(_hipops, m) {
         l.ops.push_back(make_kv_resolve(slots, keys, n_dev, out_slot, out_w, insert, init_type,
                                         init_v, init_s, seed, err, inserted, home_base, home_m));
       })
-      .def("add_tp_fwd_bwd", [](LaunchList& l, Tensor rep, Tensor dcnt, Tensor ent_uid, int64_t n,
-                                int width, optional<Tensor> vals, Tensor w_local, Tensor labels,
-                                int64_t B, int loss_type, Tensor coef, optional<Tensor> metrics,
-                                optional<Tensor> hist, int nbins, Tensor psum, Tensor pos_s,
-                                Tensor segid, Tensor n_ent, Tensor grad, bool reduce) {
+      .def("add_tp_fwd_bwd", [](LaunchList& l, Tensor rep, Tensor dcnt, optional<Tensor> ent_uid,
+                                int64_t n, int width, optional<Tensor> vals, Tensor w_local,
+                                Tensor labels, int64_t B, int loss_type, Tensor coef,
+                                optional<Tensor> metrics, optional<Tensor> hist, int nbins,
+                                Tensor psum, optional<Tensor> pos_s, optional<Tensor> segid,
+                                optional<Tensor> n_ent, optional<Tensor> grad, bool reduce) {
         l.ops.push_back(make_tp_fwd_bwd(rep, dcnt, ent_uid, n, width, vals, w_local, labels, B,
                                         loss_type, coef, metrics, hist, nbins, psum, pos_s, segid,
                                         n_ent, grad, reduce));
@@ -697,6 +877,32 @@ PYBIND11_MODULE(_hipops, m) {
                                            slot_idx, slots, algo, lr_type, alpha, beta, l1, l2,
                                            grad_scale, max_delta, stats, hist, metrics,
                                            step_counter));
+      })
+      .def("add_localize_tpf", [](LaunchList& l, Tensor keys, int64_t n, int bits, Tensor temp,
+                                  Tensor dcnt, Tensor rep, Tensor uniqf, Tensor ent_pos,
+                                  Tensor ent_j, Tensor cnt, Tensor err) {
+        l.ops.push_back(make_localize_tpf(keys, n, bits, temp, dcnt, rep, uniqf, ent_pos, ent_j,
+                                          cnt, err));
+      })
+      .def("add_tpf_step", [](LaunchList& l, int64_t n, int bits, optional<py::tuple> A,
+                              optional<Tensor> psum, optional<py::tuple> B,
+                              optional<Tensor> w_ent, Tensor slots, int init_type, double init_v,
+                              double init_s, uint64_t seed, optional<Tensor> err,
+                              optional<Tensor> inserted, uint64_t home_base, uint64_t home_m,
+                              int algo, int lr_type, double alpha, double beta, double l1,
+                              double l2, double grad_scale, double max_delta,
+                              optional<Tensor> stats, optional<Tensor> hist,
+                              optional<Tensor> metrics, optional<Tensor> step_counter) {
+        l.ops.push_back(make_tpf_step(n, bits, tpf_bufs(A), psum, tpf_bufs(B), w_ent, slots,
+                                      init_type, init_v, init_s, seed, err, inserted, home_base,
+                                      home_m, algo, lr_type, alpha, beta, l1, l2, grad_scale,
+                                      max_delta, stats, hist, metrics, step_counter));
+      })
+      .def("add_criteo_gen", [](LaunchList& l, uint64_t seed, int64_t row0, int64_t row_step,
+                                int64_t B, uint64_t num_features, double alpha, Tensor keys,
+                                Tensor labels) {
+        l.ops.push_back(make_criteo_gen(seed, row0, row_step, B, num_features, alpha, keys,
+                                        labels));
       })
       .def("__len__", [](const LaunchList& l) { return l.ops.size(); })
       .def("run", [](const LaunchList& l) {

@@ -1111,7 +1111,11 @@ __device__ uint64_t* g_fb_prof = nullptr;
 #define FB_MARK(k)                                                             \
   if (fbp && threadIdx.x == 0) fbp[(int64_t)blockIdx.x * 16 + (k)] = clock64()
 
-template <int PER, int NP>
+// kFlat (the flat 1-GPU path, tpf_step): w_local is already in tile-entry order
+// (w_ent[tile * 8192 + e], scattered there by the step boundary kernel), so the
+// prologue reads the tile's weights contiguously instead of the dependent
+// ent_uid -> w_local gather (19 k of 37 k cycles per workgroup, r3_tp_pair_phases.log).
+template <int PER, int NP, bool kFlat>
 __global__ void __launch_bounds__(tp::kThr)  // 68 KB LDS -> 2 workgroups per CU
 tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ dcnt,
                   const int32_t* __restrict__ ent_uid, int64_t n, int width,
@@ -1174,14 +1178,19 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
     for (int q = 0; q < PER; ++q)
       if (ce[p][q] == kFbExt) {
         const int64_t i = (r0 + ri) * width + sub + q * kFbLanes;
-        const int32_t u = ent_uid[(i / kTile) * kTile + __float_as_int(cv[p][q])];
+        const int64_t ge = (i / kTile) * kTile + __float_as_int(cv[p][q]);
+        const int64_t u = kFlat ? ge : (int64_t)ent_uid[ge];
         cv[p][q] = (in_range(u, w_cap) ? w_local[u] : 0.f) * (vals ? vals[i] : 1.f);
       }
   }
   for (int i = t; i < nr; i += kThr) crow[i] = r0 + i < B ? labels[r0 + i] : 0.f;
-  for (int i = t; i < cnt; i += kThr) {
-    const int32_t u = ent_uid[base + i];
-    wl[i] = in_range(u, w_cap) ? w_local[u] : 0.f;
+  if (kFlat) {
+    for (int i = t; i < cnt; i += kThr) wl[i] = w_local[base + i];  // (host: w_cap >= T * 8192)
+  } else {
+    for (int i = t; i < cnt; i += kThr) {
+      const int32_t u = ent_uid[base + i];
+      wl[i] = in_range(u, w_cap) ? w_local[u] : 0.f;
+    }
   }
   if (hist)
     for (int i = t; i < 2 * nbins; i += kThr) lhist[i] = 0u;
@@ -1270,6 +1279,364 @@ void tp_fb_set_prof(uint64_t* p) {
   PSAMD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_fb_prof), &p, sizeof(p)));
 }
 
+// ====================================================================== flat ("tpf")
+// The 1-GPU layout: the bucket stage writes FIXED per-workgroup output regions instead of
+// one compact sorted array, so no bucket waits for another (the compact layout's
+// decoupled look-back: 11 k of 47 k cycles per workgroup, r3_tp_pair_phases.log) and
+// nothing is rank-sorted or laid out as a CSC. Bucket workgroup b (a pair of fine
+// buckets, the tp_bucket geometry) owns
+//   keys     uniqf[b * kUC + s * kUnitK + j], j < D_s   (unit s = 0; units 0 and 1 when an
+//            overflowing pair falls back to its two fine buckets one after the other)
+//   entries  ent_pos / ent_j[b * kEC + e]: tile entry id (tile * 8192 + e) and the unit's
+//            key index j of every tile-distinct entry of the unit's keys (unit 1 after
+//            the E_0 entries of unit 0)
+//   counts   cnt[b * 4 + {D_0, E_0, D_1, E_1}]
+// The consumers run one workgroup per bucket workgroup and combine in LDS: tpf_step sums
+// each key's entry partials (fixed point) and applies the update, then pulls the next
+// minibatch's keys and scatters their weights into its tile-entry order (w_ent), which
+// the fused forward reads contiguously. Keys of one key-range bucket stay in the same
+// bucket workgroup for every minibatch of the same size, so a key's update and its next
+// pull run in the same workgroup, in that order.
+namespace tpf {
+constexpr int kUnitK = tp::kDH;  // keys of one unit (the bucket hash)
+constexpr int kUC = 2 * kUnitK;  // key region of a bucket workgroup (two units)
+constexpr int kEC = 8192;        // entry region of a bucket workgroup
+constexpr int kThr = 256;        // tpf_step workgroup (auc_hist_block runs in block 0)
+constexpr uint32_t kNoSlot = 0xffffffffu;
+}  // namespace tpf
+
+// Overflow unit (an overflowing pair's fine bucket f, or a lone bucket whose entries
+// exceed the LDS capacity): register-light like tp_bk_fine_light; entries are located
+// again from the per-tile runs for every pass, their key index found by probing the hash.
+// Writes D / E into co[0..1] and returns E (block-uniform, via lds).
+__device__ __forceinline__ uint32_t tpf_unit_light(
+    const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbf, int T,
+    int shift, int f, uint32_t hb, uint64_t key0, uint32_t* hkey, uint32_t* hmap,
+    uint16_t* ehraw, uint32_t* lds, uint64_t* __restrict__ uo, int32_t* __restrict__ po,
+    uint16_t* __restrict__ jo, uint32_t eoff, int32_t* __restrict__ co,
+    int32_t* __restrict__ err) {
+  using namespace tp;
+  const int t = threadIdx.x;
+  uint32_t* tpre = reinterpret_cast<uint32_t*>(ehraw);             // [kMaxT + 1]
+  uint16_t* tlo = reinterpret_cast<uint16_t*>(tpre + kMaxT + 1);  // [kMaxT]
+  for (int s = t; s < kDH; s += kBkThr) hkey[s] = kEmpty;
+  const int per = (T + kBkThr - 1) / kBkThr;
+  const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
+  uint32_t c = 0;
+  for (int q = q0; q < q1; ++q) {
+    const uint16_t* to = toff + (int64_t)q * (nbf + 1);
+    const uint32_t lo = to[f], hi = to[f + 1];
+    tlo[q] = (uint16_t)lo;
+    tpre[q] = hi - lo;
+    c += hi - lo;
+  }
+  uint32_t E;
+  uint32_t w = tp_block_scan<kBkThr>(c, lds, &E);
+  for (int q = q0; q < q1; ++q) {
+    const uint32_t len = tpre[q];
+    tpre[q] = w;
+    w += len;
+  }
+  if (t == 0) tpre[T] = E;
+  __syncthreads();
+  auto locate = [&](uint32_t g) -> int32_t {
+    int lo = 0, up = T - 1;  // last tile with tpre[q] <= g
+    while (lo < up) {
+      const int mid = (lo + up + 1) >> 1;
+      if (tpre[mid] <= g) lo = mid; else up = mid - 1;
+    }
+    return lo * kTile + tlo[lo] + (int32_t)(g - tpre[lo]);
+  };
+  // probe (insert = true: claim an empty slot); returns the slot or -1
+  auto probe = [&](uint32_t key, bool insert) -> int {
+    uint32_t h = tp_hash(key) & (kDH - 1);
+    for (int p = 0; p < kDH; ++p) {
+      const uint32_t cu = hkey[h];
+      if (cu == key) return (int)h;
+      if (cu == kEmpty) {
+        if (!insert) return -1;
+        const uint32_t prev = atomicCAS(&hkey[h], kEmpty, key);
+        if (prev == kEmpty || prev == key) return (int)h;
+      }
+      h = (h + 1) & (kDH - 1);
+    }
+    return -1;
+  };
+  bool bad = false;
+  for (uint32_t g = t; g < E; g += kBkThr)
+    bad |= probe(tkeys[locate(g)] | (hb << shift), true) < 0;
+  __syncthreads();
+  // key index j of every occupied slot (strided: conflict-free LDS reads)
+  constexpr int kPer = kDH / kBkThr;
+  uint32_t cc = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) cc += hkey[q * kBkThr + t] != kEmpty;
+  uint32_t D;
+  uint32_t wd = tp_block_scan<kBkThr>(cc, lds, &D);
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int s = q * kBkThr + t;
+    if (hkey[s] != kEmpty) {
+      hmap[s] = wd;
+      uo[wd++] = key0 | hkey[s];
+    }
+  }
+  __syncthreads();
+  const uint32_t room = eoff < (uint32_t)tpf::kEC ? tpf::kEC - eoff : 0u;
+  bad |= E > room;
+  for (uint32_t g = t; g < E && g < room; g += kBkThr) {
+    const int32_t id = locate(g);
+    const int h = probe(tkeys[id] | (hb << shift), false);
+    po[eoff + g] = id;
+    jo[eoff + g] = h >= 0 ? (uint16_t)hmap[h] : (uint16_t)0;
+  }
+  if (bad) atomicOr(err, 1);
+  if (t == 0) {
+    co[0] = (int32_t)D;
+    co[1] = (int32_t)(E < room ? E : room);
+  }
+  __syncthreads();
+  return E < room ? E : room;
+}
+
+// One workgroup per pair of fine buckets (pair = 0: per fine bucket), the tp_bucket
+// geometry and build; the occupied hash slots in compaction order are the keys' indices.
+__global__ void __launch_bounds__(tp::kBkThr, 8)
+tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbf,
+                  int pair, int T, int shift, uint64_t* __restrict__ uniqf,
+                  int32_t* __restrict__ ent_pos, uint16_t* __restrict__ ent_j,
+                  int32_t* __restrict__ cnt, int32_t* __restrict__ err) {
+  using namespace tp;
+  __shared__ uint16_t eh[kECapL];  // hash slot of every gathered entry
+  __shared__ uint64_t hs[kDH];     // hash (key u32 | count u32 -> key index)
+  __shared__ uint64_t dl[kDH];     // per-tile runs, then the compacted occupied slots
+  __shared__ uint32_t lds[kBkThr / 64 + 1];
+  __shared__ uint32_t flag;
+  uint32_t* hkey = reinterpret_cast<uint32_t*>(hs);
+  uint32_t* hcnt = hkey + kDH;
+  const int t = threadIdx.x, b = blockIdx.x;
+  const int f0 = pair ? 2 * b : b;
+  const uint64_t key0 = (uint64_t)f0 << shift;
+  uint64_t* uo = uniqf + (int64_t)b * tpf::kUC;
+  int32_t* po = ent_pos + (int64_t)b * tpf::kEC;
+  uint16_t* jo = ent_j + (int64_t)b * tpf::kEC;
+  int32_t* co = cnt + (int64_t)b * 4;
+  int32_t idx[kG];
+  uint32_t E, D;
+  const bool good = tp_bk_build(tkeys, toff, nbf, T, shift, f0, pair ? 2 : 1, 0u, hkey, hcnt, dl,
+                                eh, lds, &flag, idx, &E, &D, nullptr);
+  if (good) {
+    for (uint32_t j = t; j < D; j += kBkThr) {
+      const uint64_t v = dl[j];
+      uo[j] = key0 | (uint32_t)(v >> 32);
+      hcnt[(uint32_t)v & 0xffffu] = j;  // (the counts are dead after the compaction)
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kG; ++q) {
+      if (idx[q] < 0) continue;
+      const uint32_t g = q * kBkThr + t;
+      po[g] = idx[q];
+      jo[g] = (uint16_t)hcnt[eh[g]];
+    }
+    if (t == 0) {
+      co[0] = (int32_t)D;
+      co[1] = (int32_t)E;
+      co[2] = 0;
+      co[3] = 0;
+    }
+    return;
+  }
+  // the pair's entries overflow the LDS capacity (or its hash): its fine buckets one
+  // after the other, each a unit with its own key index space
+  const uint32_t e0 = tpf_unit_light(tkeys, toff, nbf, T, shift, f0, 0u, key0, hkey, hcnt, eh, lds,
+                                     uo, po, jo, 0u, co, err);
+  if (pair)
+    tpf_unit_light(tkeys, toff, nbf, T, shift, f0 + 1, 1u, key0, hkey, hcnt, eh, lds,
+                   uo + tpf::kUnitK, po, jo, e0, co + 2, err);
+  else if (t == 0) {
+    co[2] = 0;
+    co[3] = 0;
+  }
+}
+
+// Lookup-or-insert of one key with ONE 16-B load per probe (key and weight of the slot
+// together; resolve_key reads the weight after the key compare, a second round trip).
+__device__ __forceinline__ uint32_t tpf_resolve(Slot* __restrict__ slots, uint64_t mask,
+                                                uint64_t home_base, uint64_t home_m, int home_shr,
+                                                uint64_t h, int init_type, float init_v,
+                                                float init_s, uint64_t seed, float* w, int* ins) {
+  uint64_t idx = home_slot(h, mask, home_base, home_m, home_shr) & mask;
+  *w = 0.f;
+  for (uint64_t probe = 0; probe <= mask; ++probe) {
+    const uint4 v = *reinterpret_cast<const uint4*>(&slots[idx]);
+    const uint64_t k = ((uint64_t)v.y << 32) | v.x;
+    if (k == h) {
+      *w = __uint_as_float(v.z);
+      return (uint32_t)idx;
+    }
+    if (k == kEmptyKey) {
+      const unsigned long long prev = atomicCAS((unsigned long long*)&slots[idx].key,
+                                                (unsigned long long)kEmptyKey,
+                                                (unsigned long long)h);
+      if (prev == kEmptyKey) {
+        if (init_type != kInitZero) {
+          *w = init_value(h, init_type, init_v, init_s, seed);
+          slots[idx].w = *w;
+        }
+        ++*ins;
+        return (uint32_t)idx;
+      }
+      if (prev == h) {  // claimed by another lane meanwhile (its weight: re-read)
+        *w = __hip_atomic_load(&slots[idx].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return (uint32_t)idx;
+      }
+    }
+    idx = (idx + 1) & mask;
+  }
+  return tpf::kNoSlot;
+}
+
+// The step boundary of the flat 1-GPU path, one 256-thread workgroup per bucket
+// workgroup region (replaces tp_seg_update + kv_resolve: one launch, no global atomics):
+//   update A   every unit: the entries' partials psum[ent_pos] go into per-key LDS
+//              accumulators in 64-bit fixed point (scale 2^(48 - e) from the unit's
+//              largest |partial| < 2^e: <= 8192 addends stay below 2^61; exact,
+//              order-independent sums), then the optimizer update of each key at the
+//              slot its pull resolved (slotA), with the update statistics
+//   pull B     every unit: lookup-or-insert of B's keys -> slotB, weights into LDS, then
+//              scattered to B's tile-entry order: w_ent[ent_pos] = w[ent_j]
+// A and B must share the bucket geometry (same minibatch size); either half may be off
+// (the first pull, the last update). Block 0 also turns A's AUC histogram into metrics.
+// Within a workgroup the update's slot stores are visible to the pull's loads after the
+// barrier (workgroup scope: same CU, write-through L1).
+__global__ void __launch_bounds__(tpf::kThr)
+tpf_step_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __restrict__ posA,
+                const uint16_t* __restrict__ jA, const uint32_t* __restrict__ slotA,
+                const float* __restrict__ psum, int64_t p_cap, int do_res,
+                const int32_t* __restrict__ cntB, const uint64_t* __restrict__ uniqB,
+                const int32_t* __restrict__ posB, const uint16_t* __restrict__ jB,
+                uint32_t* __restrict__ slotB, float* __restrict__ w_ent, int64_t w_cap,
+                Slot* __restrict__ slots, uint64_t mask, uint64_t home_base, uint64_t home_m,
+                int home_shr, int init_type, float init_v, float init_s, uint64_t seed,
+                int32_t* __restrict__ err, int32_t* __restrict__ inserted, UpdateParams p,
+                double* __restrict__ stats, int acc_stripes, uint32_t* __restrict__ hist,
+                int nbins, int hist_stripes, double* __restrict__ metrics,
+                int64_t* __restrict__ step_counter) {
+  using namespace tpf;
+  __shared__ long long acc[kUnitK];  // fixed-point gradient sums of a unit's keys
+  __shared__ float wj[kUnitK];       // pulled weights of a unit's keys
+  __shared__ uint32_t smax;
+  const int t = threadIdx.x, b = blockIdx.x, lane = t & 63;
+  if (do_upd && hist && b == 0) auc_hist_block(hist, nbins, hist_stripes, metrics, step_counter);
+  double dnnz = 0, wsum = 0, dsum = 0;
+  if (do_upd) {
+    const int32_t* c = cntA + (int64_t)b * 4;
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s) {
+      // (counts clamped to the regions: a corrupted count never leaves them)
+      const int e0 = s ? min(max(c[1], 0), kEC) : 0;
+      const int D = min(c[2 * s], kUnitK), E = min(c[2 * s + 1], kEC - e0);
+      if (D <= 0) continue;
+      const int64_t eb = (int64_t)b * kEC + e0;
+      const int64_t kb = (int64_t)b * kUC + s * kUnitK;
+      for (int j = t; j < D; j += kThr) acc[j] = 0ll;
+      if (t == 0) smax = 0u;
+      constexpr int kR = 8;  // entries held in registers per thread (<= 2048 per unit)
+      float v[kR];
+      uint16_t jj[kR];
+      float vmax = 0.f;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const int g = r * kThr + t;
+        v[r] = 0.f;
+        jj[r] = 0;
+        if (g < E) {
+          const int32_t pos = posA[eb + g];
+          jj[r] = jA[eb + g];
+          v[r] = in_range(pos, p_cap) ? psum[pos] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kR; ++r) vmax = fmaxf(vmax, fabsf(v[r]));
+      for (int g = kR * kThr + t; g < E; g += kThr) {
+        const int32_t pos = posA[eb + g];
+        if (in_range(pos, p_cap)) vmax = fmaxf(vmax, fabsf(psum[pos]));
+      }
+      __syncthreads();  // acc / smax zeroed
+      fx_tile_max(vmax, &smax);
+      __syncthreads();
+      const int k2 = fx_shift(smax);
+      const double sc = ldexp(1.0, k2);
+#pragma unroll
+      for (int r = 0; r < kR; ++r)
+        if (v[r] != 0.f && jj[r] < kUnitK) fx_add(acc, jj[r], v[r], sc);
+      for (int g = kR * kThr + t; g < E; g += kThr) {
+        const int32_t pos = posA[eb + g];
+        const uint16_t j = jA[eb + g];
+        const float x = in_range(pos, p_cap) ? psum[pos] : 0.f;
+        if (x != 0.f && j < kUnitK) fx_add(acc, j, x, sc);
+      }
+      __syncthreads();
+      const double isc = ldexp(1.0, -k2);
+      for (int j = t; j < D; j += kThr) {
+        const uint32_t si = slotA[kb + j];
+        if (si == kNoSlot || si > mask) continue;
+        const float gs = (float)((double)acc[j] * isc) * p.grad_scale;
+        if (gs != gs) continue;
+        Slot sl = slots[si];
+        const float w_old = apply_update(sl, gs, p);
+        slots[si] = sl;
+        dnnz += (double)((sl.w != 0.f) - (w_old != 0.f));
+        wsum += (double)sl.w * sl.w;
+        const double d = (double)sl.w - w_old;
+        dsum += d * d;
+      }
+      __syncthreads();  // (acc of the next unit; the pull reads these slots)
+    }
+  }
+  int ins = 0;
+  if (do_res) {
+    const int32_t* c = cntB + (int64_t)b * 4;
+#pragma unroll 1
+    for (int s = 0; s < 2; ++s) {
+      const int e0 = s ? min(max(c[1], 0), kEC) : 0;
+      const int D = min(c[2 * s], kUnitK), E = min(c[2 * s + 1], kEC - e0);
+      if (D <= 0) continue;
+      const int64_t eb = (int64_t)b * kEC + e0;
+      const int64_t kb = (int64_t)b * kUC + s * kUnitK;
+      for (int j = t; j < D; j += kThr) {
+        float w;
+        const uint32_t si = tpf_resolve(slots, mask, home_base, home_m, home_shr, uniqB[kb + j],
+                                        init_type, init_v, init_s, seed, &w, &ins);
+        if (si == kNoSlot && err) atomicOr(err, 1);  // table full
+        slotB[kb + j] = si;
+        wj[j] = w;
+      }
+      __syncthreads();
+      for (int g = t; g < E; g += kThr) {
+        const int32_t pos = posB[eb + g];
+        const uint16_t j = jB[eb + g];
+        if (in_range(pos, w_cap) && j < kUnitK) w_ent[pos] = wj[j];
+      }
+      __syncthreads();  // (wj of the next unit)
+    }
+  }
+  if (do_upd && stats) {
+    const double a = wave_sum_dpp(dnnz), bb = wave_sum_dpp(wsum), cc = wave_sum_dpp(dsum);
+    if (lane == 63) {
+      double* st = acc_stripe(stats, acc_stripes);
+      if (a != 0) atomicAdd(&st[0], a);
+      if (bb != 0) atomicAdd(&st[1], bb);
+      if (cc != 0) atomicAdd(&st[2], cc);
+    }
+  }
+  if (inserted) {
+    const int tot = wave_sum(ins);
+    if (lane == 0 && tot) atomicAdd(inserted, tot);
+  }
+}
+
 // ---------------------------------------------------------------------------
 struct TpGeom {
   int nbk, shift;
@@ -1347,6 +1714,72 @@ void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t te
   }
 }
 
+// ---- flat (tpf) host side
+static int tpf_groups_of(const TpGeom& g) {
+  const bool pair = g.nbk >= 2 && g.shift <= 30;
+  return pair ? g.nbk / 2 : g.nbk;
+}
+int tpf_groups(int64_t n, int bits) { return tpf_groups_of(tp_geom(n, bits)); }
+int tpf_key_region() { return tpf::kUC; }
+int tpf_entry_region() { return tpf::kEC; }
+
+size_t tpf_temp_bytes(int64_t n, int bits) {
+  const TpGeom g = tp_geom(n, bits);
+  return al16((size_t)g.N * 4) + al16((size_t)g.T * (g.nbk + 1) * 2);  // tkeys, toff
+}
+
+// uniqf >= groups * kUC, ent_pos / ent_j >= groups * kEC, cnt >= groups * 4 (the host
+// checks; tpf_groups)
+void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
+                  int32_t* dcnt, uint16_t* rep, uint64_t* uniqf, int32_t* ent_pos, uint16_t* ent_j,
+                  int32_t* cnt, int32_t* err, hipStream_t st) {
+  if (n <= 0) return;
+  if (!tploc_supported(n, m.bits)) throw std::runtime_error("localize_tpf: unsupported size");
+  if (temp_bytes < tpf_temp_bytes(n, m.bits)) throw std::runtime_error("localize_tpf: temp");
+  const TpGeom g = tp_geom(n, m.bits);
+  char* p = (char*)temp;
+  auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
+  uint32_t* tkeys = (uint32_t*)take((size_t)g.N * 4);
+  uint16_t* toff = (uint16_t*)take((size_t)g.T * (g.nbk + 1) * 2);
+  if (m.bits > 31)
+    tp_tile_kernel<true><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
+                                                             dcnt, rep, err);
+  else
+    tp_tile_kernel<false><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
+                                                              dcnt, rep, err);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  const bool pair = g.nbk >= 2 && g.shift <= 30;
+  tpf_bucket_kernel<<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
+      tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+// One launch of tpf_step_kernel over the groups of an n-key minibatch (A and B: the
+// same n). A = null: pull only; B = null: update only.
+void tpf_step(int64_t n, int bits, const int32_t* cntA, const int32_t* posA, const uint16_t* jA,
+              const uint32_t* slotA, const float* psum, int64_t p_cap, const int32_t* cntB,
+              const uint64_t* uniqB, const int32_t* posB, const uint16_t* jB, uint32_t* slotB,
+              float* w_ent, int64_t w_cap, void* slots, int64_t cap, uint64_t home_base,
+              uint64_t home_m, int init_type, float init_v, float init_s, uint64_t seed,
+              int32_t* err, int32_t* inserted, int algo, int lr_type, float alpha, float beta,
+              float l1, float l2, float grad_scale, float max_delta, double* stats,
+              int acc_stripes, uint32_t* hist, int nbins, int hist_stripes, double* metrics,
+              int64_t* step_counter, hipStream_t st) {
+  if (n <= 0) return;
+  if (hist && nbins != 2048) throw std::runtime_error("tpf_step: the fused AUC needs 2048 bins");
+  if (cap > (int64_t)1 << 32) throw std::runtime_error("tpf_step: > 2^32 slots (u32 slot ids)");
+  int lg = 0;
+  while ((1ll << lg) < cap) ++lg;
+  UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
+  const int groups = tpf_groups(n, bits);
+  tpf_step_kernel<<<(unsigned)groups, tpf::kThr, 0, st>>>(
+      cntA != nullptr, cntA, posA, jA, slotA, psum, p_cap, cntB != nullptr, cntB, uniqB, posB, jB,
+      slotB, w_ent, w_cap, (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg,
+      init_type, init_v, init_s, seed, err, inserted, p, stats, acc_stripes,
+      cntA ? hist : nullptr, nbins, hist_stripes, metrics, step_counter);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
 void tp_backward(const uint16_t* rep, const int32_t* dcnt, int64_t n, const int32_t* rows,
                  int width, const float* vals, const float* coef, int64_t B, float* psum,
                  const int32_t* pos_s, const int32_t* segid, const int32_t* n_ent, float* grad,
@@ -1400,10 +1833,17 @@ void tp_fwd_bwd(const uint16_t* rep, const int32_t* dcnt, const int32_t* ent_uid
     throw std::runtime_error("tp_fwd_bwd: 1..2048 AUC bins (LDS histogram)");
   const size_t lds = 0;
   const int per = (width + kFbLanes - 1) / kFbLanes;
+  const bool flat = ent_uid == nullptr;  // w_local in tile-entry order (tpf)
+  if (flat && w_cap < g.N) throw std::runtime_error("tp_fwd_bwd: flat w_ent < tile stride");
 #define PSAMD_FB(PER, NP)                                                                     \
-  tp_fwd_bwd_kernel<PER, NP><<<(unsigned)g.T, tp::kThr, lds, st>>>(                          \
-      rep, dcnt, ent_uid, n, width, vals, w_local, w_cap, labels, B, loss_type, coef_out,     \
-      metrics, hist, nbins, acc_stripes, hist_stripes, psum)
+  if (flat)                                                                                   \
+    tp_fwd_bwd_kernel<PER, NP, true><<<(unsigned)g.T, tp::kThr, lds, st>>>(                  \
+        rep, dcnt, ent_uid, n, width, vals, w_local, w_cap, labels, B, loss_type, coef_out,   \
+        metrics, hist, nbins, acc_stripes, hist_stripes, psum);                               \
+  else                                                                                        \
+    tp_fwd_bwd_kernel<PER, NP, false><<<(unsigned)g.T, tp::kThr, lds, st>>>(                 \
+        rep, dcnt, ent_uid, n, width, vals, w_local, w_cap, labels, B, loss_type, coef_out,   \
+        metrics, hist, nbins, acc_stripes, hist_stripes, psum)
   switch (per) {  // NP = kFbNP[PER] row passes in registers (tp_fwd_bwd_supported)
     case 2: PSAMD_FB(2, 8); break;
     case 3: PSAMD_FB(3, 4); break;

@@ -147,9 +147,21 @@ class SparseLRTrainer:
                else self.part.range_of(self.rank))
         self.table = KVTable(cap, self.device, cfg.init, key_range=rng)
         self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
+        self.filter = (CountMinSketch(int(cfg.countmin_n), cfg.countmin_k, self.device)
+                       if cfg.tail_feature_freq > 0 else None)
+        # 1 GPU: entry scan + optimizer update fused (PSAMD_FUSED_UPDATE=0: scan, then
+        # kv_update); read once, not per step (host issue time)
+        self._fused_update = os.environ.get("PSAMD_FUSED_UPDATE", "1") != "0"
+        self._use_plans = os.environ.get("PSAMD_STEP_PLAN", "1") != "0"
         mode = cfg.localize
+        # 1 GPU: the flat layout (Localizer "tpf": fixed per-bucket regions, the step's
+        # pull fused into the previous step's update, tpf_step); PSAMD_FLAT=0 keeps "tp"
+        flat_ok = (self.G == 1 and self.gpu and self.filter is None and self._fused_update
+                   and self._use_plans and os.environ.get("PSAMD_FLAT", "1") != "0")
         if mode == "auto":  # tile dedup + key-range buckets (Localizer falls back to sort
-            mode = "tp"     # for > 34-bit keys or > 5.2 M keys per minibatch)
+            mode = "tpf" if flat_ok else "tp"  # for > 34-bit keys or > 5.2 M keys)
+        if mode == "tpf" and not flat_ok:
+            mode = "tp"
         if cfg.tail_feature_freq > 0 and mode == "tp":
             mode = "sort"  # the tail filter needs per-key nnz counts (seg_start over nnz)
         # local columns on demand: the fused tp forward/backward reads the entry map
@@ -157,8 +169,10 @@ class SparseLRTrainer:
                                    lazy_cols=True)
         self.localize_mode = self.localizer.mode  # after the Localizer's fallbacks
         self._localizers = [self.localizer]  # + a second buffer set for prefetching (G > 1)
-        self.filter = (CountMinSketch(int(cfg.countmin_n), cfg.countmin_k, self.device)
-                       if cfg.tail_feature_freq > 0 else None)
+        self._compact = None  # flat mode: a "tp" Localizer for steps the flat path cannot run
+        # flat mode: (id, generation) of the FlatLoc whose pull the previous step issued
+        # ahead (fused into its update launch); valid for the very next step only
+        self._pre = None
         dev = self.device
         self.metrics = new_accum(dev)  # [loss, correct, n, auc_sum, auc_n, ...] (striped)
         self.stats = new_accum(dev)    # [nnz delta, sum w^2, sum dw^2] (striped)
@@ -197,12 +211,8 @@ class SparseLRTrainer:
         self._xx = 0  # padded exchanges issued (exchange halves run)
         self.pending = None
         self._prefetch = None
-        # 1 GPU: entry scan + optimizer update fused (PSAMD_FUSED_UPDATE=0: scan, then
-        # kv_update); read once, not per step (host issue time)
-        self._fused_update = os.environ.get("PSAMD_FUSED_UPDATE", "1") != "0"
         self._coef_views = {}  # B -> self.coef[:B]
         self._plans = {}  # 1 GPU: native launch lists of the fused step (_step_plan)
-        self._use_plans = os.environ.get("PSAMD_STEP_PLAN", "1") != "0"
         self.step_count = 0
         self.examples = 0
         self.comm_bytes = 0
@@ -216,6 +226,7 @@ class SparseLRTrainer:
         new key, src/parameter/kv_store.h:37-57.)"""
         from ..ops.keymix import random_keys_in_range
 
+        self._pre = None  # (a pull issued ahead would miss nothing here, but stay strict)
         # the table's own key range (the loopback emulation's one rank owns all G ranges)
         lo, hi = self.table.key_range or self.part.range_of(self.rank)
         g = torch.Generator(device=self.device).manual_seed(seed + self.rank)
@@ -247,12 +258,34 @@ class SparseLRTrainer:
 
     def step(self, keys: torch.Tensor, labels: torch.Tensor, *, width: int | None = None,
              row_ptr: torch.Tensor | None = None, vals: torch.Tensor | None = None,
-             rows: torch.Tensor | None = None, loc=None, prefetch=None):
+             rows: torch.Tensor | None = None, loc=None, prefetch=None, next_loc=None):
         """One minibatch: pull, forward, backward, push. ``keys`` are raw feature ids
         in CSR order (fixed ``width`` per row, or ``row_ptr``). ``loc``: an already
         localised minibatch (``localize``); ``prefetch``: called once the step's
         exchange counts are in flight and before the step blocks on them (multi-GPU),
-        so the caller can enqueue the next minibatch's work on another stream."""
+        so the caller can enqueue the next minibatch's work on another stream.
+        ``next_loc`` (1 GPU, flat layout): the NEXT minibatch, already localised; its
+        pull runs in this step's update launch (after the update, in the same
+        workgroups), and the next ``step(loc=next_loc)`` skips its own pull. The table
+        is fully updated when this step's work completes either way."""
+        pre, self._pre = self._pre, None  # a pull issued ahead serves the next step only
+        if self.localize_mode == "tpf":
+            B = labels.numel()
+            width = width or (None if row_ptr is not None else self.cfg.max_nnz_per_example)
+            if (row_ptr is None and rows is None and vals is None and prefetch is None
+                    and (loc is None or getattr(loc, "flat", False))
+                    and self._flat_ok(B, width, keys.numel() if loc is None else loc.nnz)):
+                if loc is None:
+                    loc = self.localizer(keys)
+                self._flat_step(loc, labels, B, width, next_loc,
+                                pre == (id(loc), loc.gen))
+                return
+            # not expressible on the flat layout (valued / variable-width rows): the same
+            # keys through a compact "tp" localisation and the generic step below
+            if self._compact is None:
+                self._compact = Localizer(self.max_nnz, self.bits, self.device, mode="tp",
+                                          lazy_cols=True)
+            loc = self._compact(keys)
         if self.p2p:
             if loc is None:
                 loc = self.localizer(keys)
@@ -345,6 +378,86 @@ class SparseLRTrainer:
         self.step_count += 1
         self.examples += B
 
+    # ----------------------------------------------- flat 1-GPU step (Localizer "tpf")
+    _FLAT_WIDTHS: dict = {}
+
+    def _flat_ok(self, B: int, width, nnz: int) -> bool:
+        """Fixed width with a fused forward/backward instance, binary features, nnz =
+        B * width: the flat step applies (anything else takes the compact path)."""
+        if not width or nnz != B * width or B >= (1 << 25):
+            return False
+        ok = self._FLAT_WIDTHS.get(width)
+        if ok is None:
+            ok = self._FLAT_WIDTHS[width] = bool(hipops().tp_fwd_bwd_supported(width))
+        return ok
+
+    def _flat_step(self, loc, labels, B: int, width: int, next_loc, pre: bool):
+        """pull (unless issued ahead) -> fused forward + tile backward -> tpf_step: the
+        update of this minibatch, then the pull of ``next_loc`` (same size) in the same
+        launch. One native launch list per (buffers, labels, next buffers)."""
+        nxt = next_loc if (next_loc is not None and getattr(next_loc, "flat", False)
+                           and next_loc.nnz == loc.nnz and next_loc is not loc) else None
+        key = (id(loc), id(labels), B, width, loc.nnz, pre, id(nxt) if nxt is not None else 0,
+               id(self.rule), id(self.table.init))
+        plan = self._plans.get(key)
+        if plan is None:
+            H, tb = hipops(), self.table
+            it, iv, isd, seed = tb.init.args()
+            n, bits = loc.nnz, loc.bits
+            common = (tb.slots, it, iv, isd, seed, tb._err, tb._inserted, tb.home_base, tb.home_m,
+                      *self.rule.args(), self.stats)
+            plan = H.LaunchList()
+            if not pre:  # this minibatch's pull on its own
+                plan.add_tpf_step(n, bits, None, None, loc.bufs, loc.w_ent, *common, None, None,
+                                  None)
+            plan.add_tp_fwd_bwd(loc.rep, loc.dcnt, None, n, width, None, loc.w_ent, labels, B,
+                                loss_id(self.cfg.loss), self.coef[:B], self.metrics, self.hist,
+                                AUC_BINS, loc.psum, None, None, None, None, False)
+            plan.add_tpf_step(n, bits, loc.bufs, loc.psum,
+                              nxt.bufs if nxt is not None else None,
+                              nxt.w_ent if nxt is not None else None, *common, self.hist,
+                              self.metrics, self.step_dev)
+            if len(self._plans) >= 32:  # (callers passing fresh label tensors every step)
+                self._plans.clear()
+            self._plans[key] = plan
+        plan.run()
+        if nxt is not None:
+            self._pre = (id(nxt), nxt.gen)
+        self.step_count += 1
+        self.examples += B
+
+    def prep_plan(self, buf: int, keys: torch.Tensor, labels: torch.Tensor, *, seed: int,
+                  row0: int, row_step: int, num_features: int, alpha: float = 1.1):
+        """Flat mode: a native launch list that generates the next synthetic minibatch of
+        workspace ``buf`` (rows row0, row0 + row_step, ... on successive runs) and
+        localises it (tile + flat bucket kernels): ONE host call per data preparation.
+        Returns a callable -> the FlatLoc of ``buf``."""
+        from ..ops.synthetic import CRITEO_1TB_CARDS, _set_cards
+
+        if self.localize_mode != "tpf":
+            raise ValueError("prep_plan needs the flat (tpf) localisation")
+        while len(self._localizers) <= buf:
+            self._localizers.append(Localizer(self.max_nnz, self.bits, self.device,
+                                              mode=self.localize_mode, lazy_cols=True))
+        lz = self._localizers[buf]
+        f = lz.flat
+        B = labels.numel()
+        n = keys.numel()
+        _set_cards(self.device, CRITEO_1TB_CARDS)
+        H = hipops()
+        plan = H.LaunchList()
+        plan.add_criteo_gen(seed & ((1 << 64) - 1), row0, row_step, B, num_features, alpha, keys,
+                            labels)
+        plan.add_localize_tpf(keys, n, self.bits, lz.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos,
+                              f.ent_j, f.cnt, f.err)
+
+        def run():
+            plan.run()
+            f.nnz = n
+            f.gen += 1
+            return f
+        return run
+
     def _step_plan(self, loc, labels, B: int, width: int):
         """The 1-GPU fused step (kv_resolve, tp_fwd_bwd, tp_seg_update: the same launches
         ``step`` issues one by one below) as a native ``LaunchList`` over the fixed
@@ -381,7 +494,7 @@ class SparseLRTrainer:
 
     # --------------------------------------------- padded exchange (G > 1, default)
     def step_segments(self, keys: torch.Tensor, labels: torch.Tensor, *, width=None,
-                      row_ptr=None, vals=None, rows=None, loc=None, step=None):
+                      row_ptr=None, vals=None, rows=None, loc=None, step=None, next_loc=None):
         """The step as an ordered list of ``(kind, fn)``: ``"compute"`` segments are
         pure device work on fixed buffers (capturable in a HIP graph per localisation
         buffer and ring position), ``"comm"`` segments are the two equal-split RCCL
@@ -411,7 +524,8 @@ class SparseLRTrainer:
         """
         if not self.padded:
             return [("compute", lambda: self.step(keys, labels, width=width, row_ptr=row_ptr,
-                                                  vals=vals, rows=rows, loc=loc))]
+                                                  vals=vals, rows=rows, loc=loc,
+                                                  next_loc=next_loc))]
         if loc is None:
             loc = self.localizer(keys)
         B = labels.numel()
@@ -1123,6 +1237,7 @@ class SparseLRTrainer:
     def load_state_dict(self, sd: dict):
         from ..ops.keymix import mix
 
+        self._pre = None  # the table changes under any pull issued ahead
         keys = mix(sd["keys"].to(self.device), self.bits)
         own = self.part.owner_of(keys) == self.rank
         self.table.load(keys[own], sd["w"].to(self.device)[own], sd["z"].to(self.device)[own],

@@ -57,6 +57,52 @@ class TileInfo:
     pieces: torch.Tensor | None = None  # int64 [U] zeroed per localisation (tp_seg_update)
 
 
+@dataclass
+class FlatLoc:
+    """A minibatch localised into the flat per-bucket layout (``Localizer(mode="tpf")``,
+    csrc/hip/tploc.hip "tpf"; the 1-GPU fused step). Bucket workgroup b owns fixed
+    regions: keys ``uniqf[b * key_region + unit * key_region / 2 + j]``, entries
+    ``ent_pos`` (tile entry id) / ``ent_j`` (key index) at ``b * entry_region``, live
+    counts ``cnt[b] = (D0, E0, D1, E1)``; ``slot_u`` receives each key's table slot at
+    its pull and ``w_ent`` its weight in tile-entry order. There is no compact unique-key
+    array: consumers run one workgroup per bucket (``tpf_step``). One object per
+    workspace, refilled in place: ``gen`` counts its localisations (a pull issued ahead
+    of the step is valid only for the generation it was issued for)."""
+    rep: torch.Tensor       # int16 [nnz] tile entry of every position
+    dcnt: torch.Tensor      # int32 [tiles] entries per tile
+    psum: torch.Tensor      # float [tiles*TP_TILE] per-entry partial gradients
+    w_ent: torch.Tensor     # float [tiles*TP_TILE] pulled weights in tile-entry order
+    cnt: torch.Tensor
+    uniqf: torch.Tensor
+    ent_pos: torch.Tensor
+    ent_j: torch.Tensor
+    slot_u: torch.Tensor
+    err: torch.Tensor
+    bits: int
+    nnz: int = 0
+    gen: int = 0
+    flat = True
+
+    @property
+    def bufs(self):
+        """(cnt, uniqf, ent_pos, ent_j, slot_u): the tuple the native ops take."""
+        return (self.cnt, self.uniqf, self.ent_pos, self.ent_j, self.slot_u)
+
+    def unique_keys(self) -> torch.Tensor:
+        """Host sync: the distinct mixed keys in bucket order (key-range sorted across
+        buckets, unsorted inside one) -- for tests and diagnostics."""
+        H = hipops()
+        g = H.tpf_groups(self.nnz, self.bits)
+        kr = H.tpf_key_region()
+        c = self.cnt[:4 * g].view(g, 4).cpu()
+        u = self.uniqf[:g * kr].view(g, 2, kr // 2).cpu()
+        parts = []
+        for b in range(g):
+            for s in range(2):
+                parts.append(u[b, s, :int(c[b, 2 * s])])
+        return torch.cat(parts)
+
+
 def ensure_local_col(loc: "Localized") -> torch.Tensor:
     """local_col of a lazily localised "tp" minibatch (``Localizer(lazy_cols=True)``
     skips the per-occurrence gather: the fused forward/backward reads the tile entry
@@ -84,6 +130,9 @@ class Localizer:
     tile-distinct entries (a hot key is at most one entry per tile) and emits sorted
     unique keys, an entry-level CSC and local columns: 4 launches, no global atomics;
     the backward accumulates per tile in LDS and scans the entry CSC (``TileInfo``).
+    ``mode="tpf"`` (1 GPU, same limits as "tp"): the tile stage of "tp", then bucket
+    workgroups that write fixed per-bucket regions (``FlatLoc``): no look-back across
+    buckets, no sort, no CSC; only the fused 1-GPU step consumes it (``tpf_step``).
     (Measured and removed in round 3: a sort-free global scratch hash, a partition
     with per-bucket presence bitmaps and a 4096-key tile dedup + radix sort; none beat
     "tp" on the Criteo-shaped batch, profiles/r2_localize_tp_vs_sort.log.)"""
@@ -99,14 +148,31 @@ class Localizer:
         dev = self.device
         self.gpu = dev.type == "cuda"
         self._tp_views = None  # (n, n-sized workspace views) of the last "tp" call
-        if mode not in ("sort", "part", "tp"):
+        if mode not in ("sort", "part", "tp", "tpf"):
             raise ValueError(f"unknown localisation mode {mode!r}")
         if mode == "part" and not (self.gpu and hipops().partloc_supported(n, self.bits)):
             mode = "sort"
-        if mode == "tp" and (with_hess or not (self.gpu and hipops().tploc_supported(n, self.bits))):
+        if mode in ("tp", "tpf") and (with_hess or not (self.gpu and
+                                                        hipops().tploc_supported(n, self.bits))):
             mode = "sort"
         # (tp: up to 34-bit keys through its quotient-encoded tile hash)
-        self.mode = mode if (self.gpu and (self.bits <= 32 or mode == "tp")) else "sort"
+        self.mode = mode if (self.gpu and (self.bits <= 32 or mode in ("tp", "tpf"))) else "sort"
+        if self.gpu and self.mode == "tpf":
+            H = hipops()
+            N = H.tploc_stride(n)
+            g = H.tpf_groups(n, self.bits)  # the largest geometry (fewer keys: fewer groups)
+            kr, er = H.tpf_key_region(), H.tpf_entry_region()
+            self.ptemp = torch.empty(H.tpf_temp_bytes(n, self.bits), dtype=torch.uint8, device=dev)
+            i32 = lambda k: torch.zeros(k, dtype=torch.int32, device=dev)  # noqa: E731
+            self.flat = FlatLoc(
+                rep=torch.empty(n, dtype=torch.int16, device=dev), dcnt=i32(N // TP_TILE),
+                psum=torch.zeros(N, dtype=torch.float32, device=dev),
+                w_ent=torch.zeros(N, dtype=torch.float32, device=dev),
+                cnt=i32(4 * g), uniqf=torch.zeros(g * kr, dtype=torch.int64, device=dev),
+                ent_pos=i32(g * er), ent_j=torch.zeros(g * er, dtype=torch.int16, device=dev),
+                slot_u=i32(g * kr), err=i32(1), bits=self.bits)
+            self.err = self.flat.err
+            return
         if self.gpu and self.mode == "tp":
             H = hipops()
             N = H.tploc_stride(n)
@@ -180,7 +246,7 @@ class Localizer:
 
     def check(self):
         """Host sync: raise if a "part" localisation overflowed a bucket's LDS hash."""
-        if getattr(self, "err", None) is not None and self.mode in ("part", "tp") and \
+        if getattr(self, "err", None) is not None and self.mode in ("part", "tp", "tpf") and \
                 int(self.err.item()):
             raise RuntimeError(f"localize_{self.mode}: a bucket or tile overflowed its LDS capacity")
 
@@ -192,10 +258,19 @@ class Localizer:
             raise ValueError("empty minibatch")
         if self.gpu and is_gpu(keys):
             return self._gpu(keys.contiguous(), n)
+        if self.mode == "tpf":
+            raise ValueError("a flat (tpf) localiser takes GPU keys")
         return localize_torch(keys, self.bits, self.with_hess)
 
     def _gpu(self, keys, n) -> Localized:
         H = hipops()
+        if self.mode == "tpf":
+            f = self.flat
+            H.localize_tpf(keys, self.bits, self.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos,
+                           f.ent_j, f.cnt, f.err)
+            f.nnz = n
+            f.gen += 1
+            return f
         if self.mode == "tp":
             H.localize_tp(keys, self.bits, self.ptemp, self.t_dcnt, self.t_rep, self.pos_s,
                           self.segid, self.uniq, self.seg_start, self.t_ent_uid,

@@ -1,0 +1,287 @@
+"""Flat 1-GPU layout (Localizer mode "tpf", csrc/hip/tploc.hip tpf_*): the localisation
+covers every occurrence exactly, and the fused 1-GPU step built on it (pull issued in the
+previous step's update launch, fused forward + tile backward, per-bucket fixed-point
+gradient sums + optimizer update) trains the table a plain-PyTorch fp32 FTRL / AdaGrad /
+SGD loop trains (torch.unique, index_add, the reference's per-key update,
+src/app/linear_method/async_sgd.h:107-119)."""
+import math
+
+import pytest
+import torch
+
+from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+from parameter_server_amd.models.sparse_lr import algo_defaults
+from parameter_server_amd.ops.keymix import key_bits_for, mix, unmix
+from parameter_server_amd.ops.localize import TP_TILE, Localizer
+from parameter_server_amd.ops.native import hipops
+from parameter_server_amd.ops.synthetic import criteo_batch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _skewed_batch(step: int, bits: int = 20, B: int = 2048, width: int = 16):
+    """A minibatch whose first bucket pair overflows the bucket kernel's LDS capacity:
+    1500 distinct keys in each of the pair's two fine buckets, every one of them in the
+    first two 8192-occurrence tiles (6000 entries > 4064), so the pair falls back to its
+    two fine buckets as separate units. Raw keys (the trainer mixes them)."""
+    g = torch.Generator().manual_seed(100 + step)
+    n = B * width
+    shift = bits - 5  # n = 32768 -> 32 fine buckets
+    k0 = torch.randperm(1 << shift, generator=g)[:1500]
+    k1 = (1 << shift) + torch.randperm(1 << shift, generator=g)[:1500]
+    hot = torch.cat([k0, k1])
+    mixed = torch.randint(1 << (shift + 1), 1 << bits, (n,), generator=g)
+    for t in range(2):
+        pos = t * TP_TILE + torch.randperm(TP_TILE, generator=g)[:hot.numel()]
+        mixed[pos] = hot
+    keys = unmix(mixed.to(DEV), bits)
+    labels = torch.where(torch.rand(B, generator=g) < 0.3, 1.0, -1.0).to(DEV)
+    return keys, labels
+
+
+def _flat_entry_keys(f, n):
+    """tile entry id -> mixed key, from the flat regions (host side)."""
+    H = hipops()
+    G = H.tpf_groups(n, f.bits)
+    kr, er = H.tpf_key_region(), H.tpf_entry_region()
+    cnt = f.cnt[:4 * G].view(G, 4).cpu()
+    uq = f.uniqf[:G * kr].view(G, 2, kr // 2).cpu()
+    pos = f.ent_pos[:G * er].view(G, er).cpu()
+    jj = f.ent_j[:G * er].view(G, er).cpu().to(torch.int64) & 0xFFFF
+    ent_key = {}
+    for b in range(G):
+        e0 = int(cnt[b, 1])
+        for s in range(2):
+            D, E = int(cnt[b, 2 * s]), int(cnt[b, 2 * s + 1])
+            base = 0 if s == 0 else e0
+            p = pos[b, base:base + E]
+            j = jj[b, base:base + E]
+            assert int(j.max(initial=-1)) < max(D, 1)
+            ks = uq[b, s, j]
+            ent_key.update(zip(p.tolist(), ks.tolist()))
+    return ent_key, cnt
+
+
+@pytest.mark.parametrize("case", ["criteo", "criteo_small", "uniform", "skewed"])
+def test_tpf_localisation_covers_every_occurrence(case):
+    """Every occurrence's tile entry maps (ent_pos / ent_j / uniqf) to its own mixed key,
+    every distinct key appears once, and each tile's entry count is its distinct-key
+    count."""
+    if case == "criteo":
+        B, bits = 65536, 30
+        keys, _ = criteo_batch(B, seed=11, row0=0, num_features=10 ** 9, device=DEV)
+    elif case == "criteo_small":
+        B, bits = 3000, 30
+        keys, _ = criteo_batch(B, seed=12, row0=0, num_features=10 ** 9, device=DEV)
+    elif case == "uniform":  # nearly all distinct: the densest buckets
+        bits = 34
+        keys = torch.randint(0, 1 << 34, (400_000,), device=DEV)
+    else:
+        bits = 20
+        keys, _ = _skewed_batch(0, bits)
+    n = keys.numel()
+    lz = Localizer(n, bits, DEV, mode="tpf")
+    assert lz.mode == "tpf"
+    f = lz(keys)
+    torch.cuda.synchronize()
+    assert int(f.err.item()) == 0
+    mk = mix(keys, bits).cpu()
+    ent_key, cnt = _flat_entry_keys(f, n)
+    rep = f.rep[:n].cpu().to(torch.int64) & 0xFFFF
+    tile = torch.arange(n) // TP_TILE
+    eid = (tile * TP_TILE + rep).tolist()
+    got = torch.tensor([ent_key[e] for e in eid])
+    assert torch.equal(got, mk)
+    uq = f.unique_keys()
+    assert uq.numel() == torch.unique(mk).numel() == torch.unique(uq).numel()
+    T = (n + TP_TILE - 1) // TP_TILE
+    dc = f.dcnt[:T].cpu()
+    for t in range(T):
+        assert int(dc[t]) == torch.unique(mk[t * TP_TILE:(t + 1) * TP_TILE]).numel()
+    if case == "skewed":  # the overflowing pair ran as two fine units
+        assert cnt[0].tolist() == [1500, 3000, 1500, 3000]
+
+
+def _reference_train(batches, rule, bits):
+    """Plain PyTorch fp32 FTRL / AdaGrad / SGD over raw keys, one update per minibatch
+    (the per-key rules of kv_slot.cuh apply_update)."""
+    allk = torch.unique(torch.cat([k.cpu() for k, _ in batches]))
+    K = allk.numel()
+    W, Z, Nn, C = (torch.zeros(K) for _ in range(4))
+    for keys, labels in batches:
+        k, y = keys.cpu(), labels.cpu()
+        B = y.numel()
+        width = k.numel() // B
+        idx = torch.searchsorted(allk, k)
+        m = W[idx].view(B, width).double().sum(1).float()
+        yy = torch.where(y > 0, 1.0, -1.0)
+        coef = -yy * torch.sigmoid(-yy * m)
+        g = torch.zeros(K, dtype=torch.float64).index_add_(
+            0, idx, coef.double().repeat_interleave(width)).float() * rule.grad_scale
+        u = torch.unique(idx)
+        gu, w_old = g[u], W[u]
+        if rule.algo == "ftrl":
+            n_new = torch.sqrt(Nn[u] * Nn[u] + gu * gu)
+            sigma = (n_new - Nn[u]) / rule.alpha
+            Z[u] = Z[u] + gu - sigma * w_old
+            Nn[u] = n_new
+            eta = rule.alpha / (n_new + rule.beta)
+            zz = -Z[u] * eta
+        elif rule.algo == "adagrad":
+            Nn[u] = Nn[u] + gu * gu
+            eta = rule.alpha / (rule.beta + torch.sqrt(Nn[u]))
+            zz = w_old - eta * gu
+        else:
+            C[u] += 1
+            eta = rule.alpha / (rule.beta + torch.sqrt(C[u]))
+            zz = w_old - eta * gu
+        leta = rule.l1 * eta
+        W[u] = torch.where(zz.abs() <= leta, torch.zeros_like(zz),
+                           (zz - torch.sign(zz) * leta) / (1 + rule.l2 * eta))
+    return allk, W, Z, Nn
+
+
+def _table_by_raw_key(tr, allk):
+    keys, w, z, n = tr.table.occupied()
+    raw = unmix(keys, tr.bits).cpu()
+    o = torch.argsort(raw)
+    raw, w, z, n = raw[o], w.cpu()[o], z.cpu()[o], n.cpu()[o]
+    assert torch.equal(raw, allk)  # exactly the keys seen
+    return w, z, n
+
+
+@pytest.mark.parametrize("mode,algo", [("tpf", "ftrl"), ("tpf", "adagrad"), ("tpf", "sgd"),
+                                       ("tp", "ftrl")])
+def test_fused_1gpu_step_matches_fp32_reference(mode, algo, monkeypatch):
+    """5 fused 1-GPU steps (flat: pulls issued ahead via next_loc; tp: resolve + fused
+    forward/backward + fused scan/update) against the fp32 PyTorch loop on the same
+    keys: weights, z and n to rtol 1e-4."""
+    monkeypatch.setenv("PSAMD_FLAT", "1" if mode == "tpf" else "0")
+    B, steps = 16384, 5
+    cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B, table_capacity=1 << 22, algo=algo,
+                         **algo_defaults(algo))
+    tr = SparseLRTrainer(cfg, device=DEV)
+    assert tr.localize_mode == mode
+    batches = [criteo_batch(B, seed=31, row0=t * B, num_features=cfg.num_features, device=DEV)
+               for t in range(steps)]
+    if mode == "tpf":
+        loc = tr.localize(batches[0][0], buf=0)
+        for t in range(steps):
+            nxt = tr.localize(batches[t + 1][0], buf=(t + 1) % 2) if t + 1 < steps else None
+            tr.step(batches[t][0], batches[t][1], width=39, loc=loc, next_loc=nxt)
+            loc = nxt
+    else:
+        for k, lab in batches:
+            tr.step(k, lab, width=39)
+    torch.cuda.synchronize()
+    p = tr.progress()
+    assert p["examples"] == steps * B
+    allk, W, Z, Nn = _reference_train(batches, cfg.update_rule(), tr.bits)
+    w, z, n = _table_by_raw_key(tr, allk)
+    torch.testing.assert_close(w, W, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(z, Z, rtol=1e-4, atol=1e-4)
+    if algo != "sgd":
+        torch.testing.assert_close(n, Nn, rtol=1e-4, atol=1e-4)
+    assert (w != 0).sum() > 100  # the comparison covers trained weights, not only zeros
+
+
+def test_flat_step_overflow_units_match_reference(monkeypatch):
+    """Minibatches whose first bucket pair overflows (two fine units per workgroup, the
+    tpf_unit_light path) train like the fp32 reference."""
+    monkeypatch.setenv("PSAMD_FLAT", "1")
+    bits = 20
+    batches = [_skewed_batch(s, bits) for s in range(3)]
+    B = batches[0][1].numel()
+    cfg = SparseLRConfig(num_features=1 << bits, minibatch=B, max_nnz_per_example=16,
+                         table_capacity=1 << 22, l1=0.1, l2=0.1, alpha=0.1)
+    tr = SparseLRTrainer(cfg, device=DEV)
+    assert tr.localize_mode == "tpf" and tr.bits == bits
+    for k, lab in batches:
+        tr.step(k, lab, width=16)
+    torch.cuda.synchronize()
+    assert int(tr.localizer.err.item()) == 0
+    allk, W, Z, Nn = _reference_train(batches, cfg.update_rule(), bits)
+    w, z, n = _table_by_raw_key(tr, allk)
+    torch.testing.assert_close(w, W, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(z, Z, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(n, Nn, rtol=1e-4, atol=1e-4)
+
+
+def test_flat_pull_ahead_is_bitwise_the_plain_step(monkeypatch):
+    """A pull issued ahead inside the previous step's update launch (next_loc) gives the
+    same table, bitwise, as pulling at the step; a pull issued for a minibatch that is
+    then NOT the next step (or whose buffer was refilled) is not used."""
+    monkeypatch.setenv("PSAMD_FLAT", "1")
+    B = 8192
+    outs = []
+    batches = [criteo_batch(B, seed=41, row0=t * B, num_features=10 ** 9, device=DEV)
+               for t in range(6)]
+    for variant in ("ahead", "plain", "stale"):
+        cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, table_capacity=1 << 22)
+        tr = SparseLRTrainer(cfg, device=DEV)
+        if variant == "ahead":
+            loc = tr.localize(batches[0][0], buf=0)
+            for t in range(6):
+                nxt = tr.localize(batches[t + 1][0], buf=(t + 1) % 2) if t < 5 else None
+                tr.step(batches[t][0], batches[t][1], width=39, loc=loc, next_loc=nxt)
+                loc = nxt
+        elif variant == "plain":
+            for k, lab in batches:
+                tr.step(k, lab, width=39)
+        else:  # pulls issued ahead for a buffer that is refilled before its step
+            for t in range(6):
+                loc = tr.localize(batches[t][0], buf=0)
+                other = tr.localize(batches[(t + 3) % 6][0], buf=1)
+                tr.step(batches[t][0], batches[t][1], width=39, loc=loc, next_loc=other)
+        p = tr.progress()
+        k, w, z, n = tr.table.occupied()
+        o = torch.argsort(k)
+        outs.append((p, k[o].cpu(), w[o].cpu(), z[o].cpu(), n[o].cpu()))
+    for other in outs[1:]:
+        for a, b in zip(outs[0][1:], other[1:]):
+            assert torch.equal(a, b)
+        assert outs[0][0]["loss"] == pytest.approx(other[0]["loss"], rel=1e-12)
+
+
+def test_flat_gaussian_init_matches_compact(monkeypatch):
+    """Non-zero initial weights (inserted in the flat pull) train like the compact path."""
+    outs = []
+    B = 8192
+    from parameter_server_amd.ops.kv_table import InitRule
+
+    for flat in ("1", "0"):
+        monkeypatch.setenv("PSAMD_FLAT", flat)
+        cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B, table_capacity=1 << 22,
+                             init=InitRule("gaussian", 0.0, 0.01, 7))
+        tr = SparseLRTrainer(cfg, device=DEV)
+        for t in range(4):
+            k, lab = criteo_batch(B, seed=51, row0=t * B, num_features=cfg.num_features, device=DEV)
+            tr.step(k, lab, width=39)
+        k, w, z, n = tr.table.occupied()
+        o = torch.argsort(k)
+        outs.append((k[o].cpu(), w[o].cpu(), z[o].cpu(), n[o].cpu()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_prep_plan_generates_and_localises_like_the_ops():
+    """The native preparation launch list (generator with a row cursor + tile + flat
+    bucket) yields the rows and localisation of criteo_batch + Localizer."""
+    B = 4096
+    cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, table_capacity=1 << 20)
+    tr = SparseLRTrainer(cfg, device=DEV)
+    keys = torch.empty(B * 39, dtype=torch.int64, device=DEV)
+    labels = torch.empty(B, dtype=torch.float32, device=DEV)
+    run = tr.prep_plan(1, keys, labels, seed=77, row0=3 * B, row_step=5 * B,
+                       num_features=cfg.num_features)
+    for r in range(3):
+        f = run()
+        k2, l2 = criteo_batch(B, seed=77, row0=(3 + 5 * r) * B, num_features=cfg.num_features,
+                              device=DEV)
+        assert torch.equal(keys, k2) and torch.equal(labels, l2)
+        assert f.gen == r + 1 and f.nnz == B * 39
+        ref = Localizer(B * 39, tr.bits, DEV, mode="tpf")(k2)
+        assert torch.equal(f.rep, ref.rep) and torch.equal(f.cnt, ref.cnt)
+        assert torch.equal(f.unique_keys().sort().values, ref.unique_keys().sort().values)

@@ -223,7 +223,7 @@ def test_padded_exchange_matches_exact(model):
     # 2 steps: the second pulls rows the first pushed. (Over 6 steps the two runs drift
     # apart chaotically from the order of fp32 atomics in the wide / bias gradients: at
     # steps 1-2 the embedding rows are bitwise equal, at step 6 ~8 % of them differ by up
-    # to one AdaGrad step, benchmarks/wd_exchange_debug.py.)
+    # to one AdaGrad step, benchmarks/archive/wd_exchange_debug.py.)
     pad, ex = _run_rehearsal("padded", model, 2), _run_rehearsal("exact", model, 2)
     for rp, re_ in zip(pad, ex):
         assert rp[3] == re_[3]
