@@ -346,16 +346,17 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     # Every graph is released before the process group is destroyed: a live graph
     # holding RCCL work keeps the communicator's teardown waiting (the round-2 capture
     # experiment hung at exit that way, profiles/r2_capture_comm.log).
-    # PSAMD_CAPTURE_COMM: 1 = capture, 0 = eager, auto (default) = capture when the
-    # communicator is the 1-rank RCCL loopback of emulated peers (validated there,
-    # tests/test_bench_pipeline_gpu.py) and eager for a real multi-rank RCCL group,
-    # where graph-captured all-to-alls have not run on this project's hardware yet (a
-    # hang there would cost the whole scaling run; PSAMD_CAPTURE_COMM=1 opts in)
+    # PSAMD_CAPTURE_COMM: 1 / auto (default) = capture, 0 = eager. Captured all-to-alls
+    # are validated on the 1-rank RCCL loopback of emulated peers
+    # (tests/test_bench_pipeline_gpu.py) but have not run between real ranks on this
+    # project's hardware; a multi-rank job therefore runs under the rank supervisors of
+    # ``supervise`` below, which re-run the whole job in fresh processes with eager
+    # collectives if the captured attempt fails or stalls (its collective timeout is
+    # short, PSAMD_COMM_TIMEOUT of the first attempt).
     cchain = getattr(tr.comm, "chain", None)
     cmode = os.environ.get("PSAMD_CAPTURE_COMM", "auto")
-    multi = torch.distributed.is_initialized() and torch.distributed.get_world_size() > 1
     ccomm = (tr.padded and cchain is not None and getattr(tr.comm, "backend", "") != "gloo"
-             and (cmode == "1" or (cmode == "auto" and not multi)))
+             and cmode in ("1", "auto"))
     pipeline.captured_comm = ccomm
 
     def graph_of(fns):
@@ -450,6 +451,76 @@ def spawn_ranks(n: int, argv: list[str] | None = None, script: str | None = None
     return subprocess.call(cmd, env=env)
 
 
+def supervise(argv: list[str]) -> int:
+    """A torchrun rank of a multi-rank job, as a SUPERVISOR that never touches the GPU:
+    it runs this script as a child process (the real rank, on a rendezvous of its own),
+    and if the job's first attempt (collectives captured in the step graphs, short
+    collective timeout) fails on any rank, every supervisor re-runs it in a fresh child
+    with eager collectives (PSAMD_CAPTURE_COMM=0). The supervisors agree on ports,
+    exit codes and the retry over a host-only gloo group of their own. Rank 0's child
+    writes its JSON line to a file; rank 0's supervisor prints the one line, with
+    ``comm.captured_attempt`` / ``comm.fallback`` saying what happened."""
+    import datetime
+    import signal
+    import socket
+    import subprocess
+    import tempfile
+
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", timeout=datetime.timedelta(hours=2))
+    rank, world = dist.get_rank(), dist.get_world_size()
+    first_to = os.environ.get("PSAMD_FIRST_COMM_TIMEOUT", "60")
+    attempt_limit = float(os.environ.get("PSAMD_ATTEMPT_TIMEOUT", "900"))
+    attempts = [{"PSAMD_CAPTURE_COMM": os.environ.get("PSAMD_CAPTURE_COMM", "auto"),
+                 "PSAMD_COMM_TIMEOUT": os.environ.get("PSAMD_COMM_TIMEOUT", first_to)},
+                {"PSAMD_CAPTURE_COMM": "0"}]
+    if attempts[0]["PSAMD_CAPTURE_COMM"] == "0":
+        attempts = attempts[1:]
+    result_dir = tempfile.mkdtemp(prefix="psamd_bench_")
+    rc, first_rc, line = 1, None, None
+    for i, extra in enumerate(attempts):
+        port = [None]
+        if rank == 0:
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port[0] = sk.getsockname()[1]
+        dist.broadcast_object_list(port, src=0)
+        res = os.path.join(result_dir, f"attempt{i}.json")
+        env = dict(os.environ, MASTER_PORT=str(port[0]), PSAMD_SUPERVISED="1",
+                   PSAMD_RESULT_FILE=res, TORCHELASTIC_USE_AGENT_STORE="False", **extra)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if first_rc is not None:
+            env["PSAMD_FALLBACK_FROM"] = str(first_rc)
+        child = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                 start_new_session=True)
+        try:
+            rc = child.wait(timeout=attempt_limit)
+        except subprocess.TimeoutExpired:
+            os.killpg(child.pid, signal.SIGKILL)
+            child.wait()
+            rc = 124
+        rcs = [None] * world
+        dist.all_gather_object(rcs, rc)
+        if rank == 0 and os.path.exists(res):
+            with open(res) as f:
+                line = f.read().strip() or None
+        ok = [line is not None] if rank == 0 else [None]
+        dist.broadcast_object_list(ok, src=0)
+        if all(r == 0 for r in rcs) or ok[0]:
+            rc = 0
+            break
+        first_rc = max(r for r in rcs if r is not None)
+        if rank == 0 and i + 1 < len(attempts):
+            print(f"[psamd] attempt {i} ({extra}) failed on some rank (exit codes {rcs}); "
+                  f"re-running in fresh processes with eager collectives", file=sys.stderr,
+                  flush=True)
+    if rank == 0 and line is not None:
+        print(line, flush=True)
+    dist.destroy_process_group()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -510,6 +581,17 @@ def main():
         # touches the GPU, like the reference's launcher owns process fan-out
         # (script/local.sh:1-43); this process only waits and forwards the exit code.
         return spawn_ranks(args.gpus)
+    if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and "PSAMD_SUPERVISED" not in os.environ
+            and os.environ.get("PSAMD_SUPERVISE", "1") != "0"):
+        return supervise(sys.argv[1:])  # (before anything touches the GPU)
+    if os.environ.get("PSAMD_INJECT_CAPTURE_FAIL") == "1" and \
+            os.environ.get("PSAMD_CAPTURE_COMM", "auto") != "0":
+        # fault injection (tests/test_bench_spawn.py): the captured attempt dies like a
+        # rank the stall watchdog ended
+        from parameter_server_amd.utils.watchdog import EXIT_STALL
+
+        print("[psamd] injected failure of the captured-collective attempt", file=sys.stderr)
+        return EXIT_STALL
 
     from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
     from parameter_server_amd.ops.synthetic import criteo_batch
@@ -736,12 +818,23 @@ def main():
                                     and torch.distributed.get_backend() == "nccl" else 0),
                      "per_rank_ms": [dt_min * 1e3, dt * 1e3],
                      "collectives_rank0": comm.chain.n if comm.chain is not None else 0,
-                     "timeout_s": float(os.environ.get("PSAMD_COMM_TIMEOUT", "180"))},
+                     "timeout_s": float(os.environ.get("PSAMD_COMM_TIMEOUT", "180")),
+                     # multi-rank: the collectives rode the step graphs; fallback = the
+                     # exit code of a failed captured attempt this eager run replaced
+                     "captured": bool(getattr(pipeline, "captured_comm", False) and graph_used),
+                     "fallback": (int(os.environ["PSAMD_FALLBACK_FROM"])
+                                  if "PSAMD_FALLBACK_FROM" in os.environ else None)},
             "train": {"loss": prog["loss"], "auc": prog["auc"], "accuracy": prog["accuracy"],
                       "trains": bool(prog["loss"] < math.log(2)),
                       "table_occupied_rank0": occ, "nnz_w_rank0": nnz},
         }
-        print(json.dumps(out), flush=True)
+        res = os.environ.get("PSAMD_RESULT_FILE")
+        if res:  # (a supervised rank: the supervisor prints the one line)
+            with open(res + ".tmp", "w") as f:
+                f.write(json.dumps(out) + "\n")
+            os.replace(res + ".tmp", res)
+        else:
+            print(json.dumps(out), flush=True)
     scope.close()
     if args.trace:
         from parameter_server_amd.utils import trace

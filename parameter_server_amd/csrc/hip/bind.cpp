@@ -34,10 +34,12 @@ void kv_apply_part(void*, int64_t, const int64_t*, const uint64_t*, const float*
 // p2p.hip
 void p2p_lookup_rows(const void*, int, int, const int32_t*, int64_t, int64_t, int, float*, int64_t*,
                      int, float, float, uint64_t, int32_t*, int32_t*, hipStream_t);
-void p2p_post(const int32_t*, int64_t, int64_t, int, int, int, int32_t, int, void* const*,
-              void* const*, int32_t*, int32_t*, int64_t, hipStream_t);
-void p2p_gather(const int32_t*, const int32_t*, int, int, int, int64_t, int64_t, int, int32_t*,
-                int32_t*, hipStream_t);
+void p2p_post(const int32_t*, int64_t, int64_t, int, int, int, int, int32_t, int, void* const*,
+              void* const*, int32_t*, int32_t*, int32_t*, int64_t, hipStream_t);
+void p2p_gather(const int32_t*, const int32_t*, int, int, int, int64_t, int64_t, int, int,
+                int32_t*, int32_t*, hipStream_t);
+void* p2p_fine_alloc(size_t);
+void p2p_fine_free(void*);
 void p2p_commit(int32_t*, const int32_t*, int, int64_t*, hipStream_t);
 void ipc_export(const void*, uint8_t*);
 void* ipc_import(const uint8_t*);
@@ -680,33 +682,58 @@ PYBIND11_MODULE(_hipops, m) {
                            ptr<int32_t>(err), optr<int32_t>(inserted, at::kInt, "inserted"),
                            cur_stream());
   });
-  m.def("p2p_post", [](Tensor send, int64_t H, int64_t C, int kw, int G, int self, int64_t seq,
-                       int Q, Tensor rings, Tensor applied, Tensor ok, Tensor err, int64_t spin) {
+  // rings: per peer the base of its inbox = G x Q entries of H words + G x Q sequence words
+  m.def("p2p_post", [](Tensor send, int64_t H, int64_t C, int kw, int nb, int G, int self,
+                       int64_t seq, int Q, Tensor rings, Tensor applied, Tensor ok, Tensor err,
+                       optional<Tensor> err_host, int64_t spin) {
     chk(send, at::kInt, "send");
     chk(rings, at::kLong, "rings");
     chk(applied, at::kLong, "applied");
     chk(ok, at::kInt, "ok");
     chk(err, at::kInt, "err");
     check(G >= 1 && G <= 64 && self >= 0 && self < G, "p2p: 1..64 ranks");
+    check(nb >= 0 && nb <= 7, "p2p_post: FixingFloat 0..7 bytes");
     check(rings.numel() == G && applied.numel() == G && ok.numel() >= G, "p2p_post: G pointers");
-    check(send.numel() >= G * H && H >= 4 + C * kw + C, "p2p_post: send rows");
+    const int64_t gw = nb ? (C * nb + 3) / 4 : C;
+    check(send.numel() >= G * H && H >= 4 + C * kw + gw, "p2p_post: send rows");
     check(seq >= 1 && seq < (int64_t(1) << 31) && Q >= 1, "p2p_post: 1 <= seq < 2^31, Q >= 1");
-    psamd::p2p_post(ptr<int32_t>(send), H, C, kw, G, self, (int32_t)seq, Q,
+    int32_t* eh = nullptr;
+    if (err_host.has_value() && err_host->defined()) {
+      check(err_host->device().is_cpu() && err_host->is_pinned() &&
+                err_host->scalar_type() == at::kInt && err_host->numel() >= 1,
+            "err_host must be a pinned int32 host tensor");
+      void* dptr = nullptr;
+      PSAMD_HIP_CHECK(hipHostGetDevicePointer(&dptr, err_host->data_ptr(), 0));
+      eh = reinterpret_cast<int32_t*>(dptr);
+    }
+    psamd::p2p_post(ptr<int32_t>(send), H, C, kw, nb, G, self, (int32_t)seq, Q,
                     reinterpret_cast<void* const*>(rings.data_ptr()),
                     reinterpret_cast<void* const*>(applied.data_ptr()), ptr<int32_t>(ok),
-                    ptr<int32_t>(err), spin, cur_stream());
+                    ptr<int32_t>(err), eh, spin, cur_stream());
   });
   m.def("p2p_gather", [](Tensor inbox, Tensor applied, int G, int self, int Q, int64_t H, int64_t C,
-                         int kw, Tensor stage, Tensor ready) {
+                         int kw, int nb, Tensor stage, Tensor ready) {
     chk(inbox, at::kInt, "inbox");
     chk(applied, at::kInt, "applied");
     chk(stage, at::kInt, "stage");
     chk(ready, at::kInt, "ready");
     check(G >= 1 && G <= 64 && self >= 0 && self < G, "p2p: 1..64 ranks");
-    check(inbox.numel() >= (int64_t)G * Q * H && stage.numel() >= G * H, "p2p_gather: buffers");
+    check(nb >= 0 && nb <= 7, "p2p_gather: FixingFloat 0..7 bytes");
+    check(inbox.numel() >= (int64_t)G * Q * (H + 1) && stage.numel() >= G * H,
+          "p2p_gather: inbox = G x Q x (H + 1) words");
     check(applied.numel() >= G && ready.numel() >= G, "p2p_gather: counters");
-    psamd::p2p_gather(ptr<int32_t>(inbox), ptr<int32_t>(applied), G, self, Q, H, C, kw,
+    psamd::p2p_gather(ptr<int32_t>(inbox), ptr<int32_t>(applied), G, self, Q, H, C, kw, nb,
                       ptr<int32_t>(stage), ptr<int32_t>(ready), cur_stream());
+  });
+  // a zeroed FINE-GRAINED device buffer (cross-device coherent while kernels run; IPC
+  // exportable) as a uint8 tensor that frees itself
+  m.def("fine_empty", [](int64_t nbytes) {
+    check(nbytes > 0, "fine_empty: nbytes > 0");
+    int dev = 0;
+    PSAMD_HIP_CHECK(hipGetDevice(&dev));
+    void* p = psamd::p2p_fine_alloc((size_t)nbytes);
+    return torch::from_blob(p, {nbytes}, [](void* q) { psamd::p2p_fine_free(q); },
+                            torch::TensorOptions().dtype(at::kByte).device(at::kCUDA, dev));
   });
   m.def("p2p_commit", [](Tensor applied, Tensor ready, int G, optional<Tensor> total) {
     chk(applied, at::kInt, "applied");

@@ -58,6 +58,27 @@ __device__ __forceinline__ int key_part(uint64_t h, uint64_t base, uint64_t m, i
   return (int)(((h - base) * m) >> (64 - lgP));
 }
 
+// flags bit 1: the slot's non-zero initial weight is published. An inserter claims the
+// slot by CAS on the key and only then writes the weight, so a reader that finds the key
+// (another lane of the launch, or a peer's one-sided lookup over xGMI, p2p.hip) may run
+// ahead of that store: it takes the weight only once the flag is set (release / acquire
+// at system scope) and otherwise the init value itself, which is what the inserter
+// writes. Zero init needs no flag (the slot's weight starts at 0). (Bit 0: the
+// aggregated push's "touched" mark, kv_table.hip.)
+constexpr uint32_t kSlotInit = 2u;
+
+__device__ __forceinline__ float published_w(Slot* s, uint64_t h, int init_type, float init_v,
+                                             float init_s, uint64_t seed) {
+  if (init_type == kInitZero) return s->w;
+  const uint32_t f = __hip_atomic_load(&s->flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return (f & kSlotInit) ? s->w : init_value(h, init_type, init_v, init_s, seed);
+}
+
+__device__ __forceinline__ void publish_init(Slot* s, float w) {
+  s->w = w;
+  __hip_atomic_fetch_or(&s->flags, kSlotInit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Probe for one key; insert it if asked. Returns the slot index (-1: absent or
 // table full) and the weight through *w.
 __device__ __forceinline__ int64_t resolve_key(Slot* __restrict__ slots, uint64_t mask,
@@ -70,7 +91,7 @@ __device__ __forceinline__ int64_t resolve_key(Slot* __restrict__ slots, uint64_
   for (uint64_t probe = 0; probe <= mask; ++probe) {
     uint64_t k = slots[idx].key;
     if (k == h) {
-      *w = slots[idx].w;
+      *w = published_w(&slots[idx], h, init_type, init_v, init_s, seed);
       return (int64_t)idx;
     }
     if (k == kEmptyKey) {
@@ -80,13 +101,13 @@ __device__ __forceinline__ int64_t resolve_key(Slot* __restrict__ slots, uint64_
       if (prev == kEmptyKey) {
         if (init_type != kInitZero) {
           *w = init_value(h, init_type, init_v, init_s, seed);
-          slots[idx].w = *w;
+          publish_init(&slots[idx], *w);
         }
         ++*ins;
         return (int64_t)idx;
       }
       if (prev == h) {
-        *w = slots[idx].w;
+        *w = published_w(&slots[idx], h, init_type, init_v, init_s, seed);
         return (int64_t)idx;
       }
     }

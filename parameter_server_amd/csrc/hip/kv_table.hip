@@ -35,9 +35,9 @@ __global__ void kv_init_kernel(Slot* __restrict__ slots, int64_t cap) {
 }
 
 // Lookup (optionally insert) every key; write its slot index (-1 if absent or
-// table full) and optionally its weight. Fused gather is exact for zero init;
-// for non-zero init the caller uses a separate gather launch (the inserting
-// lane writes w after its CAS, a same-launch reader could see the old 0).
+// table full) and optionally its weight. The fused weight is exact for any init: a
+// lane that finds a key another lane of this launch has just claimed reads the weight
+// only once the inserter published it (kv_slot.cuh published_w), else the init value.
 __global__ void kv_resolve_kernel(Slot* __restrict__ slots, uint64_t mask, uint64_t home_base,
                                   uint64_t home_m, int home_shr,
                                   const uint64_t* __restrict__ keys, int64_t n_host,
@@ -114,22 +114,6 @@ __global__ void kv_resolve_rows_kernel(Slot* __restrict__ slots, uint64_t mask,
   }
 }
 
-// Re-read w of the rows' resolved slots after the resolve launch has completed
-// (non-zero init: a lane that lost the insert race to another row may have read w
-// before the inserting lane wrote it).
-__global__ void kv_gather_rows_kernel(const Slot* __restrict__ slots, int64_t cap,
-                                      const int32_t* __restrict__ recv, int64_t H, int64_t C,
-                                      const int64_t* __restrict__ slot_idx,
-                                      float* __restrict__ out_w) {
-  const int s = blockIdx.y;
-  const int64_t n = dev_len(recv + (int64_t)s * H, C);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t si = slot_idx[(int64_t)s * C + i];
-    out_w[(int64_t)s * C + i] = in_range(si, cap) ? slots[si].w : 0.f;
-  }
-}
-
 // out[i] = slot.w (0 for missing), gathered by cached slot index.
 __global__ void kv_gather_kernel(const Slot* __restrict__ slots, int64_t cap,
                                  const int64_t* __restrict__ slot_idx, int64_t n_host,
@@ -157,7 +141,7 @@ __global__ void kv_set_kernel(Slot* __restrict__ slots, int64_t cap,
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = slot_idx[i];
     if (!in_range(s, cap)) continue;
-    if (w) slots[s].w = w[i];
+    if (w) publish_init(&slots[s], w[i]);  // (an explicit weight counts as published)
     if (z) slots[s].z = z[i];
     if (nn) slots[s].n = nn[i];
   }
@@ -278,7 +262,7 @@ __global__ void kv_apply_accumulated_kernel(Slot* __restrict__ slots, int64_t ca
     Slot s = slots[si];
     const float g = s.acc * p.grad_scale;
     s.acc = 0.f;
-    s.flags = 0u;
+    s.flags &= ~1u;  // (bit 1, the published-init mark, stays)
     const float w_old = apply_update(s, g, p);
     slots[si] = s;
     dnnz += (double)((s.w != 0.f) - (w_old != 0.f));
@@ -575,19 +559,12 @@ void kv_resolve(void* slots, int64_t cap, const uint64_t* keys, int64_t n, const
                 int64_t* out_slot, float* out_w, bool insert, int init_type, float init_v,
                 float init_s, uint64_t seed, int32_t* err, int32_t* inserted, uint64_t home_base,
                 uint64_t home_m, hipStream_t st) {
-  const bool fused_w = out_w && init_type == kInitZero;
   int lg = 0;
   while ((1ll << lg) < cap) ++lg;
   kv_resolve_kernel<<<grid_for(n, 256), 256, 0, st>>>(
       (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg, keys, n, n_dev, out_slot,
-      fused_w ? out_w : nullptr,
-      insert ? 1 : 0, init_type, init_v, init_s, seed, err, inserted);
+      out_w, insert ? 1 : 0, init_type, init_v, init_s, seed, err, inserted);
   PSAMD_HIP_CHECK(hipGetLastError());
-  if (out_w && !fused_w) {
-    kv_gather_kernel<<<grid_for(n, 256), 256, 0, st>>>((const Slot*)slots, cap, out_slot, n,
-                                                       n_dev, out_w, 0);
-    PSAMD_HIP_CHECK(hipGetLastError());
-  }
 }
 
 void kv_resolve_rows(void* slots, int64_t cap, const int32_t* recv, int G, int64_t H, int64_t C,
@@ -603,11 +580,6 @@ void kv_resolve_rows(void* slots, int64_t cap, const int32_t* recv, int G, int64
       (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg, recv, H, C, kw, out_slot,
       out_w, insert ? 1 : 0, init_type, init_v, init_s, seed, err, inserted, out_key, bnd, lgP);
   PSAMD_HIP_CHECK(hipGetLastError());
-  if (init_type != kInitZero) {
-    kv_gather_rows_kernel<<<grid, 256, 0, st>>>((const Slot*)slots, cap, recv, H, C, out_slot,
-                                                out_w);
-    PSAMD_HIP_CHECK(hipGetLastError());
-  }
 }
 
 void kv_gather(const void* slots, int64_t cap, const int64_t* slot_idx, int64_t n,

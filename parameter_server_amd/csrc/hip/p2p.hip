@@ -11,19 +11,30 @@
 //          peer p's open-addressing table (read only; a key the owner has not inserted
 //          yet reads as its init value); the local row resolves with insert into the
 //          own shard. No message, no owner involvement.
-//   push   p2p_post: row p (keys + gradients of this step for owner p) is written into
-//          peer p's inbox ring entry [self][seq % Q]; a release fence at system scope,
-//          then the entry's sequence word. The ring has Q entries per source: a pusher
-//          waits (bounded spin on the owner's applied counter) only when it is Q steps
-//          ahead of what that owner has applied, the staleness bound of this mode.
+//   push   p2p_post: row p (keys + gradients of this step for owner p, in the padded
+//          exchange's row layout [nkeys, ngrads, min, max | keys | f32 gradients or
+//          FixingFloat nb-byte codes]) is written into peer p's inbox ring entry
+//          [self][seq % Q]; a release fence at system scope, then the entry's sequence
+//          word in the inbox's sequence area (after the G x Q entries). The ring has Q
+//          entries per source: a pusher waits (bounded spin on the owner's applied
+//          counter) only when it is Q steps ahead of what that owner has applied, the
+//          staleness bound of this mode.
 //   apply  p2p_gather: the owner snapshots, per source, whether the next entry's
 //          sequence word has arrived (system-scope acquire) and copies the ready
 //          entries into one G-row staging buffer; kv_resolve_rows + kv_update_rows
 //          (kv_table.hip) then apply them with per-push semantics (rank order per key);
 //          p2p_commit publishes the applied counters the pushers read.
 //
+// The inbox and the applied counters are written by one GPU and read by another inside
+// running kernels (a pusher spins on an owner's counter), so they live in FINE-GRAINED
+// device memory (hipExtMallocWithFlags(hipDeviceMallocFinegrained), exported through
+// the same IPC handles): coarse-grained memory is only coherent across devices at kernel
+// boundaries.
+//
 // Every kernel here is bounded: a wait gives up after `spin` microseconds (s_memrealtime)
-// and reports through err (bit 8) instead of hanging.
+// and reports through err (bit 8) instead of hanging; the post's last kernel publishes
+// err into pinned host memory, so the trainer fails at the first push that gave up
+// (its sequence number is consumed: the owner would wait for it forever).
 #include "kv_slot.cuh"
 
 #include <hip/hip_runtime.h>
@@ -109,11 +120,16 @@ __global__ void p2p_space_kernel(int32_t* const* __restrict__ applied, int G, in
   ok[p] = 1;
 }
 
-// push, step 2: grid (blocks, G). Copies the live words of row p (header words 0-2,
-// nkeys keys, ngrads gradient words) into peer p's ring entry; the entry's sequence
-// word (3) is written by p2p_flag_kernel after this launch completed.
+// gradient words of a row with ng gradients: f32, or nb-byte FixingFloat codes
+__device__ __forceinline__ int64_t p2p_grad_words(int64_t ng, int nb) {
+  return nb ? (ng * nb + 3) / 4 : ng;
+}
+
+// push, step 2: grid (blocks, G). Copies the live words of row p (the 4 header words,
+// nkeys keys, the gradient words) into peer p's ring entry; the entry's sequence word
+// is written by p2p_flag_kernel after this launch completed.
 __global__ void __launch_bounds__(256)
-p2p_copy_kernel(const int32_t* __restrict__ send, int64_t H, int64_t C, int kw,
+p2p_copy_kernel(const int32_t* __restrict__ send, int64_t H, int64_t C, int kw, int nb,
                 int32_t* const* __restrict__ rings, int self, int32_t seq, int Q,
                 const int32_t* __restrict__ ok) {
   const int p = blockIdx.y;
@@ -122,24 +138,32 @@ p2p_copy_kernel(const int32_t* __restrict__ send, int64_t H, int64_t C, int kw,
   int32_t* dst = rings[p] + ((int64_t)self * Q + (seq - 1) % Q) * H;
   const int64_t nk = dev_len(row, C), ng = dev_len(row + 1, C);
   const int64_t g0 = 4 + C * kw;
-  const int64_t tot = 3 + nk * kw + ng;
+  const int64_t tot = 4 + nk * kw + p2p_grad_words(ng, nb);
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot;
        e += (int64_t)gridDim.x * blockDim.x) {
     int64_t o;
-    if (e < 3) o = e;
-    else if (e < 3 + nk * kw) o = 4 + (e - 3);
-    else o = g0 + (e - 3 - nk * kw);
+    if (e < 4) o = e;
+    else if (e < 4 + nk * kw) o = e;
+    else o = g0 + (e - 4 - nk * kw);
     dst[o] = row[o];
   }
   __threadfence_system();
 }
 
+// the sequence word of ring entry [src][q] sits after the G x Q entries of H words
+__device__ __forceinline__ int64_t p2p_seq_word(int G, int Q, int64_t H, int src, int q) {
+  return (int64_t)G * Q * H + (int64_t)src * Q + q;
+}
+
 __global__ void p2p_flag_kernel(int32_t* const* __restrict__ rings, int64_t H, int G, int self,
-                                int32_t seq, int Q, const int32_t* __restrict__ ok) {
+                                int32_t seq, int Q, const int32_t* __restrict__ ok,
+                                const int32_t* __restrict__ err, int32_t* __restrict__ err_host) {
   const int p = threadIdx.x;
+  if (p == 0 && err_host)  // (the space kernel's give-up, for the host to raise on)
+    __hip_atomic_store(err_host, *err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (p >= G || !ok[p]) return;
   __threadfence_system();
-  p2p_store_release(rings[p] + ((int64_t)self * Q + (seq - 1) % Q) * H + 3, seq);
+  p2p_store_release(rings[p] + p2p_seq_word(G, Q, H, self, (seq - 1) % Q), seq);
 }
 
 // apply, step 1 (one block): which source has its next entry ready; stage row headers.
@@ -148,25 +172,23 @@ __global__ void p2p_ready_kernel(const int32_t* __restrict__ inbox, const int32_
                                  int32_t* __restrict__ ready) {
   const int s = threadIdx.x;
   if (s >= G) return;
-  int32_t r = 0, nk = 0, ng = 0;
+  int32_t r = 0, hd[4] = {0, 0, 0, 0};
   if (s != self) {
     const int32_t next = applied[s] + 1;
     const int32_t* e = inbox + ((int64_t)s * Q + (next - 1) % Q) * H;
-    if (p2p_load_acquire(e + 3) == next) {
+    if (p2p_load_acquire(inbox + p2p_seq_word(G, Q, H, s, (next - 1) % Q)) == next) {
       r = 1;
-      nk = e[0];
-      ng = e[1];
+      for (int k = 0; k < 4; ++k) hd[k] = e[k];
     }
   }
   ready[s] = r;
-  stage[(int64_t)s * H] = nk;
-  stage[(int64_t)s * H + 1] = ng;
+  for (int k = 0; k < 4; ++k) stage[(int64_t)s * H + k] = hd[k];
 }
 
 // apply, step 2: grid (blocks, G): the ready entries' keys and gradients -> staging rows.
 __global__ void __launch_bounds__(256)
 p2p_stage_kernel(const int32_t* __restrict__ inbox, const int32_t* __restrict__ applied, int Q,
-                 int64_t H, int64_t C, int kw, const int32_t* __restrict__ ready,
+                 int64_t H, int64_t C, int kw, int nb, const int32_t* __restrict__ ready,
                  int32_t* __restrict__ stage) {
   const int s = blockIdx.y;
   if (!ready[s]) return;
@@ -174,8 +196,8 @@ p2p_stage_kernel(const int32_t* __restrict__ inbox, const int32_t* __restrict__ 
   const int32_t* e = inbox + ((int64_t)s * Q + (next - 1) % Q) * H;
   int32_t* d = stage + (int64_t)s * H;
   const int64_t nk = dev_len(d, C), ng = dev_len(d + 1, C);
-  const int64_t g0 = 4 + C * kw;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nk * kw + ng;
+  const int64_t g0 = 4 + C * kw, gw = p2p_grad_words(ng, nb);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nk * kw + gw;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t o = i < nk * kw ? 4 + i : g0 + (i - nk * kw);
     d[o] = e[o];
@@ -209,29 +231,41 @@ void p2p_lookup_rows(const void* tabs, int G, int self, const int32_t* send, int
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void p2p_post(const int32_t* send, int64_t H, int64_t C, int kw, int G, int self, int32_t seq,
-              int Q, void* const* rings, void* const* applied, int32_t* ok, int32_t* err,
-              int64_t spin, hipStream_t st) {
+void p2p_post(const int32_t* send, int64_t H, int64_t C, int kw, int nb, int G, int self,
+              int32_t seq, int Q, void* const* rings, void* const* applied, int32_t* ok,
+              int32_t* err, int32_t* err_host, int64_t spin, hipStream_t st) {
   p2p_check_g(G, self);
   if (seq < 1 || Q < 1) throw std::runtime_error("p2p_post: seq >= 1, Q >= 1");
+  if (nb < 0 || nb > 7) throw std::runtime_error("p2p_post: FixingFloat 0..7 bytes");
   p2p_space_kernel<<<1, 64, 0, st>>>((int32_t* const*)applied, G, self, seq, Q, spin, ok, err);
   PSAMD_HIP_CHECK(hipGetLastError());
   dim3 grid(grid_for(2 * C, 256, 256), G);
-  p2p_copy_kernel<<<grid, 256, 0, st>>>(send, H, C, kw, (int32_t* const*)rings, self, seq, Q, ok);
+  p2p_copy_kernel<<<grid, 256, 0, st>>>(send, H, C, kw, nb, (int32_t* const*)rings, self, seq, Q,
+                                        ok);
   PSAMD_HIP_CHECK(hipGetLastError());
-  p2p_flag_kernel<<<1, 64, 0, st>>>((int32_t* const*)rings, H, G, self, seq, Q, ok);
+  p2p_flag_kernel<<<1, 64, 0, st>>>((int32_t* const*)rings, H, G, self, seq, Q, ok, err,
+                                    err_host);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
 void p2p_gather(const int32_t* inbox, const int32_t* applied, int G, int self, int Q, int64_t H,
-                int64_t C, int kw, int32_t* stage, int32_t* ready, hipStream_t st) {
+                int64_t C, int kw, int nb, int32_t* stage, int32_t* ready, hipStream_t st) {
   p2p_check_g(G, self);
   p2p_ready_kernel<<<1, 64, 0, st>>>(inbox, applied, G, self, Q, H, stage, ready);
   PSAMD_HIP_CHECK(hipGetLastError());
   dim3 grid(grid_for(2 * C, 256, 256), G);
-  p2p_stage_kernel<<<grid, 256, 0, st>>>(inbox, applied, Q, H, C, kw, ready, stage);
+  p2p_stage_kernel<<<grid, 256, 0, st>>>(inbox, applied, Q, H, C, kw, nb, ready, stage);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
+
+// Fine-grained device memory (coherent across devices while kernels run), zeroed.
+void* p2p_fine_alloc(size_t bytes) {
+  void* p = nullptr;
+  PSAMD_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained));
+  PSAMD_HIP_CHECK(hipMemset(p, 0, bytes));
+  return p;
+}
+void p2p_fine_free(void* p) { (void)hipFree(p); }
 
 void p2p_commit(int32_t* applied, const int32_t* ready, int G, int64_t* total, hipStream_t st) {
   p2p_commit_kernel<<<1, 64, 0, st>>>(applied, ready, G, total);

@@ -1471,8 +1471,9 @@ __device__ __forceinline__ uint32_t tpf_resolve(Slot* __restrict__ slots, uint64
   for (uint64_t probe = 0; probe <= mask; ++probe) {
     const uint4 v = *reinterpret_cast<const uint4*>(&slots[idx]);
     const uint64_t k = ((uint64_t)v.y << 32) | v.x;
-    if (k == h) {
-      *w = __uint_as_float(v.z);
+    if (k == h) {  // (non-zero init: the weight once its inserter published it)
+      *w = init_type == kInitZero ? __uint_as_float(v.z)
+                                  : published_w(&slots[idx], h, init_type, init_v, init_s, seed);
       return (uint32_t)idx;
     }
     if (k == kEmptyKey) {
@@ -1482,13 +1483,13 @@ __device__ __forceinline__ uint32_t tpf_resolve(Slot* __restrict__ slots, uint64
       if (prev == kEmptyKey) {
         if (init_type != kInitZero) {
           *w = init_value(h, init_type, init_v, init_s, seed);
-          slots[idx].w = *w;
+          publish_init(&slots[idx], *w);
         }
         ++*ins;
         return (uint32_t)idx;
       }
-      if (prev == h) {  // claimed by another lane meanwhile (its weight: re-read)
-        *w = __hip_atomic_load(&slots[idx].w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == h) {  // claimed by another lane meanwhile
+        *w = published_w(&slots[idx], h, init_type, init_v, init_s, seed);
         return (uint32_t)idx;
       }
     }

@@ -187,10 +187,10 @@ class SparseLRTrainer:
         if cfg.exchange not in ("padded", "exact", "p2p"):
             raise ValueError(f"exchange must be 'padded', 'exact' or 'p2p', not {cfg.exchange!r}")
         self.p2p = self.G > 1 and cfg.exchange == "p2p"
-        if self.p2p and (not self.gpu or self.filter is not None or cfg.fixing_float_bytes
+        if self.p2p and (not self.gpu or self.filter is not None
                          or cfg.push_mode == "aggregate" or not math.isinf(self.tau)):
             raise ValueError("exchange='p2p' is the asynchronous GPU data plane: consistency "
-                             "'asp', no tail filter / fixing-float, sequential pushes")
+                             "'asp', no tail filter, sequential pushes")
         self.px = None  # PeerExchange (p2p, set up on the first step)
         self.padded = self.G > 1 and cfg.exchange == "padded"
         self.fused = (self.G > 1 and self.filter is None and cfg.fixing_float_bytes == 0
@@ -935,10 +935,13 @@ class SparseLRTrainer:
             C = int(math.ceil(float(cnt.item()) * cfg.exchange_slack)) + 1024
         C = min(max(64, (C + 63) // 64 * 64), max(64, self.max_nnz))
         kw = 1 if self.bits <= 32 else 2
-        H = (4 + C * kw + C + 3) // 4 * 4
+        nb = int(cfg.fixing_float_bytes)  # FixingFloat pushes: nb-byte codes (padded layout)
+        gw = (C * nb + 3) // 4 if nb else C
+        H = (4 + C * kw + gw + 3) // 4 * 4
         i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)  # noqa: E731
         self.xc = SimpleNamespace(
-            C=C, kw=kw, H=H, off=off, send=i32(G * H),
+            C=C, kw=kw, H=H, nb=nb, off=off, send=i32(G * H),
+            gstage=torch.zeros(G * C, dtype=torch.float32, device=dev) if nb else None,
             wout=torch.zeros(G * C, dtype=torch.float32, device=dev),
             slot=torch.full((G * C,), -1, dtype=torch.int64, device=dev),
             w_local=torch.zeros(self.max_nnz, dtype=torch.float32, device=dev),
@@ -947,7 +950,7 @@ class SparseLRTrainer:
             link=torch.empty(next_pow2(2 * G * C), dtype=torch.int64, device=dev),
             nxt=torch.empty(G * C, dtype=torch.int32, device=dev), ovf=i32(1),
             ovf_host=torch.zeros(1, dtype=torch.int32, pin_memory=True))
-        self.px = PeerExchange(self.comm, self.table, C, kw, H, dev, Q=cfg.p2p_queue)
+        self.px = PeerExchange(self.comm, self.table, C, kw, H, dev, Q=cfg.p2p_queue, nb=nb)
 
     def _p2p_step(self, loc, labels, width, prefetch=None):
         """One asynchronous step: pack this minibatch's keys per owner, pull them
@@ -962,6 +965,8 @@ class SparseLRTrainer:
         width = width or self.cfg.max_nnz_per_example
         hh.owner_split(loc.uniq, loc.n_uniq, self.part.bounds_on(self.device), xc.off)
         hh.xchg_pack_keys(loc.uniq, loc.n_uniq, xc.off, C, kw, H, xc.send, xc.ovf)
+        if xc.nb:  # (FixingFloat: no pack_grads launch to publish the overflow flag)
+            hh.xchg_publish(xc.ovf, xc.ovf_host)
         self.px.lookup(xc.send, xc.wout, xc.slot)
         if prefetch is not None:  # the next minibatch's preparation overlaps this step
             prefetch()
@@ -970,13 +975,23 @@ class SparseLRTrainer:
         hh.xchg_unpack_w(xc.wout, None, loc.n_uniq, xc.off, C, w_local)
         _, grad = linear_fwd_bwd(loc, w_local, labels, B=B, width=width, loss=self.cfg.loss,
                                  coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
-        hh.xchg_pack_grads(grad[:U], None, loc.n_uniq, xc.off, C, kw, H, xc.send, hist=self.hist,
-                           metrics=self.metrics, step_counter=self.step_dev, ovf=xc.ovf,
-                           ovf_host=xc.ovf_host)
-        g_own = xc.send.view(torch.float32)[r * H + 4 + C * kw:r * H + 4 + C * kw + C]
+        if xc.nb:
+            # FixingFloat codes for the peers (reference async_sgd.h:273-277); the own row
+            # is applied from the unquantised staged gradients
+            seed = (self.cfg.seed * 7919 + 17) & ((1 << 64) - 1)
+            hh.xchg_ff_pack_grads(grad[:U], None, loc.n_uniq, xc.off, C, kw, H, xc.nb, seed,
+                                  self.step_dev, xc.send, xc.gstage)
+            g_own = xc.gstage[r * C:(r + 1) * C]
+            auc_from_hist(self.hist, self.metrics, self.step_dev)
+        else:
+            hh.xchg_pack_grads(grad[:U], None, loc.n_uniq, xc.off, C, kw, H, xc.send,
+                               hist=self.hist, metrics=self.metrics, step_counter=self.step_dev,
+                               ovf=xc.ovf, ovf_host=xc.ovf_host)
+            g_own = xc.send.view(torch.float32)[r * H + 4 + C * kw:r * H + 4 + C * kw + C]
         hh.kv_update(self.table.slots, xc.slot[r * C:(r + 1) * C], g_own,
                      xc.send[r * H + 1:r * H + 2], *self.rule.args(), self.stats)
         self.px.post(xc.send)
+        self.px.check_fatal()
         self.px.apply(self.rule, self.stats, xc.a_slot, xc.a_w, xc.link, xc.nxt,
                       rounds=self.cfg.p2p_rounds)
         self.step_count += 1

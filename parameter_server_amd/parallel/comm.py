@@ -219,6 +219,9 @@ class Comm:
     def all_gather_obj(self, obj):
         return [obj]
 
+    def host_gather_obj(self, obj):  # (host-only channel; see DistComm)
+        return self.all_gather_obj(obj)
+
     def barrier(self):
         pass
 
@@ -431,6 +434,19 @@ class DistComm(Comm):
     def all_gather_obj(self, obj):
         out = [None] * self.world
         self.chain.run("all_gather_obj", lambda: dist.all_gather_object(out, obj, group=self.group))
+        return out
+
+    def host_gather_obj(self, obj):
+        """All-gather of a small picklable object over a gloo group: host only, no device
+        synchronisation (an RCCL object collective stages through the device stream).
+        Collective; the first call creates the gloo group on every rank."""
+        if self.backend == "gloo":
+            return self.all_gather_obj(obj)
+        if getattr(self, "_hgroup", None) is None:
+            ranks = dist.get_process_group_ranks(self.group) if self.group is not None else None
+            self._hgroup = dist.new_group(ranks=ranks, backend="gloo")
+        out = [None] * self.world
+        dist.all_gather_object(out, obj, group=self._hgroup)
         return out
 
     def barrier(self):

@@ -21,6 +21,17 @@ A pusher waits (bounded device spin) only when it is ``Q`` steps ahead of what a
 owner has applied from it: the staleness bound of this mode. Between ranks there is
 no lock step, so a slow rank delays only the application of its own pushes.
 
+Rows use the padded exchange's layout, so FixingFloat pushes (nb-byte codes with the
+row's min / max in the header; reference fixing_float.h:44-95) travel as they do there
+and the owner decodes them before the update. The inbox (entries + a separate area of
+sequence words) and the applied counters are FINE-GRAINED device memory: another GPU
+writes / reads them while kernels run (``PSAMD_P2P_FINE=0``: ordinary coarse-grained
+allocations, for A/B). A push that gives up waiting for ring space is fatal at once:
+the post publishes the error word into pinned host memory and ``check_fatal`` raises
+(its sequence number is consumed, so that owner would otherwise wait for it forever).
+Host-side bookkeeping (handle exchange, drain counts) goes over a gloo group, never
+through a device-synchronising RCCL object collective.
+
 Validated on one MI355X with several processes sharing the GPU (real IPC mappings,
 the same kernels); the xGMI path itself needs a multi-GPU node.
 """
@@ -38,22 +49,36 @@ def _u64_to_i64(x: int) -> int:
     return x - (1 << 64) if x >= (1 << 63) else x
 
 
+def _fine_i32(n: int, dev, fine: bool):
+    """n zeroed int32 words: fine-grained device memory, or (fine=False) torch's."""
+    if fine:
+        return hipops().fine_empty(4 * n).view(torch.int32)
+    return torch.zeros(n, dtype=torch.int32, device=dev)
+
+
 class PeerExchange:
     def __init__(self, comm, table, C: int, kw: int, H: int, device, Q: int = 16,
-                 spin_us: int = 5_000_000):
+                 spin_us: int = 5_000_000, nb: int = 0):
+        import os
+
         self.comm, self.table = comm, table
         self.G, self.rank = comm.world, comm.rank
         self.C, self.kw, self.H, self.Q = int(C), int(kw), int(H), int(Q)
+        self.nb = int(nb)  # FixingFloat bytes per pushed gradient (0: f32)
         self.spin = int(spin_us)  # give-up time of a push waiting for inbox space
         self.device = dev = torch.device(device)
         G, H, Q = self.G, self.H, self.Q
         i32 = dict(dtype=torch.int32, device=dev)
-        self.inbox = torch.zeros(G * Q * H, **i32)   # [source][Q][H]; seq word 0 = empty
-        self.applied = torch.zeros(G, **i32)          # last sequence applied per source
+        self.fine = os.environ.get("PSAMD_P2P_FINE", "1") != "0"
+        # [source][Q][H] entries, then [source][Q] sequence words (0 = empty)
+        self.inbox = _fine_i32(G * Q * H + G * Q, dev, self.fine)
+        self.applied = _fine_i32(G, dev, self.fine)   # last sequence applied per source
         self.stage = torch.zeros(G * H, **i32)
+        self.gdec = torch.zeros(G * C, dtype=torch.float32, device=dev) if self.nb else None
         self.ready = torch.zeros(G, **i32)
         self.ok = torch.zeros(G, **i32)
         self.err = torch.zeros(1, **i32)
+        self.err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self.total = torch.zeros(1, dtype=torch.int64, device=dev)  # entries applied
         self.seq = 0                                  # pushes posted by this rank
         hh = hipops()
@@ -62,7 +87,7 @@ class PeerExchange:
         geom = [int(cap - 1), int(table.home_base), int(table.home_m), 64 - lg]
         mine = {"slots": hh.ipc_export(table.slots), "inbox": hh.ipc_export(self.inbox),
                 "applied": hh.ipc_export(self.applied), "geom": geom}
-        allh = comm.all_gather_obj(mine)
+        allh = comm.host_gather_obj(mine)
         self._opened = []
         tabs, rings, applieds = [], [], []
         for p, h in enumerate(allh):
@@ -96,8 +121,18 @@ class PeerExchange:
     def post(self, send):
         """Write the peer rows of ``send`` (keys + gradients) into the owners' inboxes."""
         self.seq += 1
-        hipops().p2p_post(send, self.H, self.C, self.kw, self.G, self.rank, self.seq, self.Q,
-                          self.rings, self.applieds, self.ok, self.err, self.spin)
+        hipops().p2p_post(send, self.H, self.C, self.kw, self.nb, self.G, self.rank, self.seq,
+                          self.Q, self.rings, self.applieds, self.ok, self.err, self.err_host,
+                          self.spin)
+
+    def check_fatal(self):
+        """No sync: raise if a completed post gave up waiting for ring space (published
+        into pinned host memory by the post's last kernel; seen at most the stream's
+        depth after it happened)."""
+        if int(self.err_host[0]):
+            raise RuntimeError(
+                f"p2p exchange: a push waited {self.spin / 1e6:g} s for an owner's inbox space "
+                f"and gave up (that owner stopped applying); its gradients are lost")
 
     def apply(self, rule, stats, slots_scratch, wscratch, link, nxt, rounds: int = 1):
         """Owner: apply up to ``rounds`` ready inbox entries per source."""
@@ -105,13 +140,17 @@ class PeerExchange:
         G, H, C = self.G, self.H, self.C
         it, iv, isd, seed = tb.init.args()
         for _ in range(rounds):
-            hh.p2p_gather(self.inbox, self.applied, G, self.rank, self.Q, H, C, self.kw,
+            hh.p2p_gather(self.inbox, self.applied, G, self.rank, self.Q, H, C, self.kw, self.nb,
                           self.stage, self.ready)
             hh.kv_resolve_rows(tb.slots, self.stage, H, C, self.kw, slots_scratch, wscratch, True,
                                it, iv, isd, seed, tb._err, tb._inserted, tb.home_base, tb.home_m,
                                None, None, 0)
-            g = self.stage.view(torch.float32)[4 + C * self.kw:]
-            hh.kv_update_rows(tb.slots, slots_scratch, g, H, self.stage, H, C, link, nxt,
+            if self.nb:  # FixingFloat codes -> f32 (rows not ready decode 0 gradients)
+                hh.xchg_ff_decode(self.stage, C, self.kw, H, self.nb, self.gdec)
+                g, gstride = self.gdec, C
+            else:
+                g, gstride = self.stage.view(torch.float32)[4 + C * self.kw:], H
+            hh.kv_update_rows(tb.slots, slots_scratch, g, gstride, self.stage, H, C, link, nxt,
                               *rule.args(), stats)
             hh.p2p_commit(self.applied, self.ready, G, self.total)
 
@@ -123,10 +162,12 @@ class PeerExchange:
                                "space (that owner stopped applying)")
 
     def drain(self, rule, stats, slots_scratch, wscratch, link, nxt, timeout: float = 120.0):
-        """Collective at the end of training: apply every push every rank posted. (No
-        device sync before the host all-gather: a post of this rank may be waiting for
-        ring space on a peer that only frees it while draining.)"""
-        posted = self.comm.all_gather_obj(self.seq)
+        """Collective at the end of training: apply every push every rank posted. The
+        posted counts go over the host (gloo) channel: an RCCL object all-gather would
+        synchronise this rank's stream first, and a post still waiting for ring space on a
+        peer that only frees it while draining would then stall both sides until the
+        spin gives up."""
+        posted = self.comm.host_gather_obj(self.seq)
         want = torch.tensor(posted, dtype=torch.int32)
         want[self.rank] = 0
         t0 = time.time()

@@ -61,3 +61,24 @@ def test_bench_stalled_rank_fails_fast():
     assert "[psamd] FAILED rank 0: phase timed" in out.stderr or \
         "[psamd] FAILED rank 2: phase timed" in out.stderr, out.stderr[-3000:]
     assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_failed_captured_attempt_reruns_eagerly():
+    """Multi-rank runs go through per-rank supervisors: when the first attempt (the
+    collectives captured in the step graphs) fails on the ranks, every supervisor re-runs
+    the job in fresh processes with eager collectives, and rank 0 still prints exactly
+    one JSON line, which records the fallback."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(PSAMD_INJECT_CAPTURE_FAIL="1")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "3",
+                          "--steps", "2", "--warmup", "1", "--minibatch", "1024",
+                          "--num-features", "1e6"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "re-running in fresh processes with eager collectives" in out.stderr
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 3 and r["comm"]["fallback"] == 3 and r["comm"]["captured"] is False

@@ -106,19 +106,21 @@ def test_p2p_transport_applies_every_push(tmp_path, world, steps, Q):
         assert r["total"] == steps * (world - 1)
 
 
-def _train_worker(rank, world, port, out_dir):
+def _train_worker(rank, world, port, out_dir, init="zero", nb=0):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+    from parameter_server_amd.ops.kv_table import InitRule
     from parameter_server_amd.ops.synthetic import criteo_batch
     from parameter_server_amd.parallel.comm import DistComm
 
     dev = torch.device("cuda", 0)
     B = 8192
     cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B, table_capacity=1 << 22,
-                         consistency="asp", exchange="p2p", seed=rank)
+                         consistency="asp", exchange="p2p", seed=rank, fixing_float_bytes=nb,
+                         init=InitRule(init, 0.0, 0.01 if init == "gaussian" else 0.0, 3))
     tr = SparseLRTrainer(cfg, DistComm(dev), dev)
     for t in range(40):
         k, lab = criteo_batch(B, seed=1000 + rank, row0=t * B, num_features=cfg.num_features,
@@ -128,17 +130,72 @@ def _train_worker(rank, world, port, out_dir):
             tr.progress(reset=True)
     p = tr.progress(reset=True)
     occ, nnz = tr.table.census()
-    torch.save({"p": p, "occ": occ, "desc": tr.consistency_desc()},
+    torch.save({"p": p, "occ": occ, "desc": tr.consistency_desc(), "fine": tr.px.fine},
                os.path.join(out_dir, f"p{rank}.pt"))
     tr.px.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_p2p_trainer_trains(tmp_path):
-    mp.spawn(_train_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
-    res = [torch.load(tmp_path / f"p{r}.pt", weights_only=False) for r in range(2)]
+@pytest.mark.parametrize("world,init,nb", [(2, "zero", 0), (2, "gaussian", 1), (3, "zero", 2)])
+def test_p2p_trainer_trains(tmp_path, world, init, nb):
+    """Asynchronous FTRL over the one-sided exchange trains, also with non-zero initial
+    weights (a peer's lookup may race the owner's insert: it must see the init value,
+    never an unpublished 0) and with FixingFloat pushes (1 or 2 bytes per gradient)."""
+    mp.spawn(_train_worker, args=(world, _port(), str(tmp_path), init, nb), nprocs=world,
+             join=True)
+    res = [torch.load(tmp_path / f"p{r}.pt", weights_only=False) for r in range(world)]
     for r in res:
         assert r["p"]["loss"] < math.log(2) and r["p"]["auc"] > 0.65, r["p"]
         assert r["occ"] > 0
         assert r["desc"].startswith("asp-p2p")
+        assert r["fine"]  # inbox / applied counters in fine-grained memory
+
+
+def _stall_worker(rank, world, port, out_dir):
+    """Rank 1 never applies; rank 0 keeps posting to it with a short give-up time and
+    must fail at the first post that gave up, not train on with lost pushes."""
+    import time
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from parameter_server_amd.ops.kv_table import KVTable
+    from parameter_server_amd.parallel.comm import DistComm
+    from parameter_server_amd.parallel.p2p import PeerExchange
+    from parameter_server_amd.parallel.partition import KeyPartition
+
+    dev = torch.device("cuda", 0)
+    comm = DistComm(dev)
+    part = KeyPartition(30, world)
+    table = KVTable(1 << 12, dev, key_range=part.range_of(rank))
+    C, kw, Q = 64, 1, 2
+    H = (4 + C * kw + C + 3) // 4 * 4
+    px = PeerExchange(comm, table, C, kw, H, dev, Q=Q, spin_us=200_000)
+    send = torch.zeros(world * H, dtype=torch.int32, device=dev)
+    send[1 * H] = 1  # one key for the owner, rank 1
+    send[1 * H + 1] = 1
+    send[1 * H + 4] = int(part.range_of(1)[0])
+    msg, t0 = "", time.time()
+    if rank == 0:
+        try:
+            for _ in range(Q + 3):
+                px.post(send)
+                torch.cuda.synchronize()
+                px.check_fatal()
+        except RuntimeError as e:
+            msg = str(e)
+    dt = time.time() - t0
+    with open(os.path.join(out_dir, f"s{rank}.txt"), "w") as f:
+        f.write(f"{dt}\n{msg}")
+    dist.barrier()
+    px.close()
+    dist.destroy_process_group()
+
+
+def test_p2p_push_timeout_is_fatal_at_once(tmp_path):
+    mp.spawn(_stall_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    dt, msg = (tmp_path / "s0.txt").read_text().split("\n", 1)
+    assert "gave up" in msg, msg
+    assert float(dt) < 10.0  # the first post past the ring (Q = 2) waits 0.2 s, then raises
