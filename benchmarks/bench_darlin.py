@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--tau", type=int, default=1)
     ap.add_argument("--l1", type=float, default=10.0)
     ap.add_argument("--tail-freq", type=int, default=4)
+    ap.add_argument("--data", default="criteo", choices=["criteo", "groups"],
+                    help="criteo: 39 one-hot slots (one block per slot; tau = 8 diverges on "
+                         "them, tests/test_darlin.py); groups: CTR-log-shaped, 120 groups with "
+                         "8 present per example x 2 keys (tau = 8 converges)")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--host-preprocess", action="store_true",
                     help="build the CSC with numpy (reference path) instead of on the GPU")
@@ -44,9 +48,14 @@ def main():
     comm, device = init_from_env("cpu" if args.cpu else "cuda")
     G, rank = comm.world, comm.rank
     t0 = time.time()
-    sd = criteo_slots(args.rows, seed=17, row0=rank * args.rows,
-                      num_features=int(args.num_features), device=device,
-                      on_device=args.device_data and not args.cpu)
+    if args.data == "groups":
+        from parameter_server_amd.data.synthetic import sparse_groups
+
+        sd = sparse_groups(args.rows, seed=17 + rank)
+    else:
+        sd = criteo_slots(args.rows, seed=17, row0=rank * args.rows,
+                          num_features=int(args.num_features), device=device,
+                          on_device=args.device_data and not args.cpu)
     cfg = DarlinConfig(l1=args.l1, tau=args.tau, tail_freq=args.tail_freq,
                        max_pass=args.passes + args.warmup, epsilon=0.0, seed=0,
                        host_preprocess=args.host_preprocess)
@@ -78,12 +87,13 @@ def main():
             "config": {"rows_per_gpu": args.rows, "num_features": int(args.num_features),
                        "kept_features": tr.num_cols, "nnz_per_gpu": tr.nnz,
                        "blocks": len(tr.blocks), "tau": args.tau, "l1": args.l1,
-                       "tail_freq": args.tail_freq},
+                       "tail_freq": args.tail_freq, "data": args.data},
             "preprocess_sec": prep,
             "trainer_preprocess_sec": tr.preprocess_time,
             "preprocess_breakdown_sec": tr.prep_times,
             "preprocess_path": "host numpy" if args.host_preprocess else "gpu",
             "train": {"objective": p.objective, "relative_obj": p.relative_obj,
+                      "objectives": [q.objective for q in tr.progress],
                       "nnz_w": p.nnz_w, "active_set": p.nnz_active_set},
         }), flush=True)
     if G > 1:
