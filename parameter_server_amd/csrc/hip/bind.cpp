@@ -61,7 +61,15 @@ int tpf_key_region();
 int tpf_entry_region();
 size_t tpf_temp_bytes(int64_t, int);
 void localize_tpf(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint16_t*, uint64_t*,
-                  int32_t*, uint16_t*, int32_t*, int32_t*, hipStream_t);
+                  int32_t*, uint16_t*, int32_t*, int32_t*, bool, hipStream_t);
+bool tpf_exchange_ok(int64_t, int, int);
+void tpf_pack_keys(int64_t, int, int, const int32_t*, const uint64_t*, int64_t, int, int64_t,
+                   int32_t*, int32_t*, hipStream_t);
+void tpf_unpack_w(int64_t, int, int, const int32_t*, const int32_t*, const uint16_t*, int64_t,
+                  const float*, float*, int64_t, hipStream_t);
+void tpf_pack_grads(int64_t, int, int, const int32_t*, const int32_t*, const uint16_t*, int64_t, int,
+                    int64_t, const float*, int64_t, int32_t*, bool, float*, uint32_t*, int, double*,
+                    int64_t*, const int32_t*, int32_t*, hipStream_t);
 void tpf_step(int64_t, int, const int32_t*, const int32_t*, const uint16_t*, const uint32_t*,
               const float*, int64_t, const int32_t*, const uint64_t*, const int32_t*,
               const uint16_t*, uint32_t*, float*, int64_t, void*, int64_t, uint64_t, uint64_t, int,
@@ -112,6 +120,9 @@ void xchg_ff_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, c
                         int64_t, int, int64_t, int, uint64_t, const int64_t*, int32_t*, float*,
                         hipStream_t);
 void xchg_ff_decode(const int32_t*, int, int64_t, int, int64_t, int, float*, hipStream_t);
+void xchg_ff_init(int32_t*, int, int64_t, hipStream_t);
+void xchg_ff_encode(const float*, int, int64_t, int, int64_t, int, uint64_t, const int64_t*,
+                    int32_t*, hipStream_t);
 void kv_gather(const void*, int64_t, const int64_t*, int64_t, const int32_t*, float*, int,
                hipStream_t);
 void kv_set(void*, int64_t, const int64_t*, int64_t, const float*, const float*, const float*,
@@ -426,23 +437,25 @@ Launch make_tp_fwd_bwd(Tensor rep, Tensor dcnt, optional<Tensor> ent_uid, int64_
 struct TpfBufs {
   Tensor cnt, uniqf, ent_pos, ent_j, slot_u;
 };
-void check_tpf(const TpfBufs& f, int64_t n, int bits, const char* what) {
-  chk(f.cnt, at::kInt, "cnt");
-  chk(f.uniqf, at::kLong, "uniqf");
-  chk(f.ent_pos, at::kInt, "ent_pos");
-  chk(f.ent_j, at::kShort, "ent_j");
-  chk(f.slot_u, at::kInt, "slot_u");
+// (partial = true: empty tensors are buffers the caller does not use)
+void check_tpf(const TpfBufs& f, int64_t n, int bits, const char* what, bool partial = false) {
   check(psamd::tploc_supported(n, bits), std::string(what) + ": tp geometry (2..34 key bits)");
   const int64_t g = psamd::tpf_groups(n, bits);
-  check(f.cnt.numel() >= 4 * g && f.uniqf.numel() >= g * psamd::tpf_key_region() &&
-            f.slot_u.numel() >= g * psamd::tpf_key_region() &&
-            f.ent_pos.numel() >= g * psamd::tpf_entry_region() &&
-            f.ent_j.numel() >= g * psamd::tpf_entry_region(),
-        std::string(what) + ": flat regions smaller than the geometry");
+  auto need = [&](const Tensor& t, at::ScalarType dt, const char* name, int64_t m) {
+    if (partial && t.numel() == 0) return;
+    chk(t, dt, name);
+    check(t.numel() >= m, std::string(what) + ": " + name + " smaller than the geometry");
+  };
+  need(f.cnt, at::kInt, "cnt", 4 * g);
+  need(f.uniqf, at::kLong, "uniqf", g * psamd::tpf_key_region());
+  need(f.ent_pos, at::kInt, "ent_pos", g * psamd::tpf_entry_region());
+  need(f.ent_j, at::kShort, "ent_j", g * psamd::tpf_entry_region());
+  need(f.slot_u, at::kInt, "slot_u", g * psamd::tpf_key_region());
 }
 
 Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor dcnt, Tensor rep,
-                         Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err) {
+                         Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err,
+                         bool sorted) {
   chk(keys, at::kLong, "keys");
   chk(temp, at::kByte, "temp");
   chk(dcnt, at::kInt, "dcnt");
@@ -459,7 +472,7 @@ Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor d
     psamd::localize_tpf(ptr<uint64_t>(keys), n, km, temp.data_ptr(), (size_t)temp.numel(),
                         ptr<int32_t>(dcnt), ptr<uint16_t>(rep), ptr<uint64_t>(uniqf),
                         ptr<int32_t>(ent_pos), ptr<uint16_t>(ent_j), ptr<int32_t>(cnt),
-                        ptr<int32_t>(err), st);
+                        ptr<int32_t>(err), sorted, st);
   };
 }
 
@@ -833,9 +846,75 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("tpf_entry_region", []() { return psamd::tpf_entry_region(); });
   m.def("tpf_temp_bytes", [](int64_t n, int bits) { return psamd::tpf_temp_bytes(n, bits); });
   m.def("localize_tpf", [](Tensor keys, int bits, Tensor temp, Tensor dcnt, Tensor rep,
-                           Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err) {
+                           Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err,
+                           bool sorted) {
     make_localize_tpf(keys, keys.numel(), bits, temp, dcnt, rep, uniqf, ent_pos, ent_j, cnt,
-                      err)(cur_stream());
+                      err, sorted)(cur_stream());
+  });
+  // ---- the padded multi-GPU exchange on the flat layout (rows as in exchange.hip)
+  m.def("tpf_exchange_ok", [](int64_t n, int bits, int G) {
+    return psamd::tpf_exchange_ok(n, bits, G);
+  });
+  m.def("tpf_pack_keys", [](int64_t n, int bits, int G, Tensor cnt, Tensor uniqf, int64_t C, int kw,
+                            int64_t H, Tensor send, optional<Tensor> ovf) {
+    check_tpf(TpfBufs{cnt, uniqf, cnt.new_empty({0}, at::kInt), cnt.new_empty({0}, at::kShort),
+                      cnt.new_empty({0}, at::kInt)}, n, bits, "tpf_pack_keys", true);
+    chk(send, at::kInt, "send");
+    check(psamd::tpf_exchange_ok(n, bits, G), "tpf_pack_keys: G a power of two dividing groups");
+    check((kw == 1 || kw == 2) && C > 0 && H >= 4 + C * kw + 1 && send.numel() >= G * H,
+          "tpf_pack_keys: row geometry");
+    psamd::tpf_pack_keys(n, bits, G, ptr<int32_t>(cnt), ptr<uint64_t>(uniqf), C, kw, H,
+                         ptr<int32_t>(send), optr<int32_t>(ovf, at::kInt, "ovf"), cur_stream());
+  });
+  m.def("tpf_unpack_w", [](int64_t n, int bits, int G, Tensor cnt, Tensor ent_pos, Tensor ent_j,
+                           int64_t C, Tensor wrecv, Tensor w_ent) {
+    check_tpf(TpfBufs{cnt, cnt.new_empty({0}, at::kLong), ent_pos, ent_j,
+                      cnt.new_empty({0}, at::kInt)}, n, bits, "tpf_unpack_w", true);
+    chk(wrecv, at::kFloat, "wrecv");
+    chk(w_ent, at::kFloat, "w_ent");
+    check(psamd::tpf_exchange_ok(n, bits, G), "tpf_unpack_w: G a power of two dividing groups");
+    check(C > 0 && wrecv.numel() >= G * C && w_ent.numel() >= psamd::tploc_stride(n),
+          "tpf_unpack_w: buffers");
+    psamd::tpf_unpack_w(n, bits, G, ptr<int32_t>(cnt), ptr<int32_t>(ent_pos),
+                        ptr<uint16_t>(ent_j), C, ptr<float>(wrecv), ptr<float>(w_ent),
+                        w_ent.numel(), cur_stream());
+  });
+  m.def("tpf_pack_grads", [](int64_t n, int bits, int G, Tensor cnt, Tensor ent_pos, Tensor ent_j,
+                             int64_t C, int kw, int64_t H, Tensor psum, Tensor send,
+                             optional<Tensor> gstage, optional<Tensor> hist,
+                             optional<Tensor> metrics, optional<Tensor> step_counter,
+                             optional<Tensor> ovf, optional<Tensor> ovf_host) {
+    check_tpf(TpfBufs{cnt, cnt.new_empty({0}, at::kLong), ent_pos, ent_j,
+                      cnt.new_empty({0}, at::kInt)}, n, bits, "tpf_pack_grads", true);
+    chk(psum, at::kFloat, "psum");
+    chk(send, at::kInt, "send");
+    check(psamd::tpf_exchange_ok(n, bits, G), "tpf_pack_grads: G a power of two dividing groups");
+    check((kw == 1 || kw == 2) && C > 0 && H >= 4 + C * kw + 1 && send.numel() >= G * H,
+          "tpf_pack_grads: row geometry");
+    check(psum.numel() >= psamd::tploc_stride(n), "tpf_pack_grads: psum < stride");
+    float* gs = optr<float>(gstage, at::kFloat, "gstage");
+    if (gs) check(gstage->numel() >= G * C, "tpf_pack_grads: gstage < G * C");
+    else check(H >= 4 + C * kw + C, "tpf_pack_grads: f32 gradient rows");
+    uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
+    double* mp = optr<double>(metrics, at::kDouble, "metrics");
+    if (hp) check(mp && hist->numel() % 4096 == 0 && hist->numel() / 4096 <= 8,
+                  "tpf_pack_grads: hist = stripes x 2 x 2048 with metrics");
+    int32_t* op = optr<int32_t>(ovf, at::kInt, "ovf");
+    int32_t* oh = nullptr;
+    if (ovf_host.has_value() && ovf_host->defined()) {
+      check(op && ovf_host->device().is_cpu() && ovf_host->is_pinned() &&
+                ovf_host->scalar_type() == at::kInt,
+            "ovf_host: pinned int32 host tensor (with ovf)");
+      void* dptr = nullptr;
+      PSAMD_HIP_CHECK(hipHostGetDevicePointer(&dptr, ovf_host->data_ptr(), 0));
+      oh = reinterpret_cast<int32_t*>(dptr);
+    }
+    psamd::tpf_pack_grads(n, bits, G, ptr<int32_t>(cnt), ptr<int32_t>(ent_pos),
+                          ptr<uint16_t>(ent_j), C, kw, H, ptr<float>(psum), psum.numel(),
+                          ptr<int32_t>(send), gs != nullptr, gs, hp,
+                          hp ? (int)(hist->numel() / 4096) : 1, mp,
+                          optr<int64_t>(step_counter, at::kLong, "step_counter"), op, oh,
+                          cur_stream());
   });
   m.def("tpf_step", [](int64_t n, int bits, optional<py::tuple> A, optional<Tensor> psum,
                        optional<py::tuple> B, optional<Tensor> w_ent, Tensor slots, int init_type,
@@ -907,9 +986,9 @@ PYBIND11_MODULE(_hipops, m) {
       })
       .def("add_localize_tpf", [](LaunchList& l, Tensor keys, int64_t n, int bits, Tensor temp,
                                   Tensor dcnt, Tensor rep, Tensor uniqf, Tensor ent_pos,
-                                  Tensor ent_j, Tensor cnt, Tensor err) {
+                                  Tensor ent_j, Tensor cnt, Tensor err, bool sorted) {
         l.ops.push_back(make_localize_tpf(keys, n, bits, temp, dcnt, rep, uniqf, ent_pos, ent_j,
-                                          cnt, err));
+                                          cnt, err, sorted));
       })
       .def("add_tpf_step", [](LaunchList& l, int64_t n, int bits, optional<py::tuple> A,
                               optional<Tensor> psum, optional<py::tuple> B,
@@ -1263,6 +1342,26 @@ PYBIND11_MODULE(_hipops, m) {
                               ptr<int64_t>(off), G, C, kw, H, nb, seed,
                               optr<int64_t>(step, at::kLong, "step"), ptr<int32_t>(send),
                               ptr<float>(gstage), cur_stream());
+  });
+  m.def("xchg_ff_init", [](Tensor send, int64_t H) {
+    chk(send, at::kInt, "send");
+    check(H > 4 && send.numel() % H == 0, "send is not a whole number of rows");
+    const int G = (int)(send.numel() / H);
+    check(G >= 1 && G <= 64, "1..64 peers");
+    psamd::xchg_ff_init(ptr<int32_t>(send), G, H, cur_stream());
+  });
+  m.def("xchg_ff_encode", [](Tensor gstage, int64_t C, int kw, int64_t H, int nb, uint64_t seed,
+                             optional<Tensor> step, Tensor send) {
+    chk(gstage, at::kFloat, "gstage");
+    chk(send, at::kInt, "send");
+    check(kw == 1 || kw == 2, "kw must be 1 or 2");
+    check(nb >= 1 && nb <= 7, "FixingFloat bytes in [1, 7]");
+    check(C > 0 && H >= 4 + C * kw + (C * nb + 3) / 4 && send.numel() % H == 0,
+          "bad exchange row geometry");
+    const int G = (int)(send.numel() / H);
+    check(G >= 1 && G <= 64 && gstage.numel() >= G * C, "gstage < G*C");
+    psamd::xchg_ff_encode(ptr<float>(gstage), G, C, kw, H, nb, seed,
+                          optr<int64_t>(step, at::kLong, "step"), ptr<int32_t>(send), cur_stream());
   });
   m.def("xchg_ff_decode", [](Tensor recv, int64_t C, int kw, int64_t H, int nb, Tensor gin) {
     chk(recv, at::kInt, "recv");

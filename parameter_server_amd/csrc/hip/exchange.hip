@@ -308,6 +308,19 @@ void xchg_ff_pack_grads(const float* grad, const int32_t* perm, const int32_t* n
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
+// the two halves of xchg_ff_pack_grads around a producer that stages the rows itself (the
+// flat layout's tpf_pack_grads writes gstage and the rows' min / max)
+void xchg_ff_init(int32_t* send, int G, int64_t H, hipStream_t st) {
+  xchg_ff_init_kernel<<<1, 64, 0, st>>>(send, G, H);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+void xchg_ff_encode(const float* gstage, int G, int64_t C, int kw, int64_t H, int nb, uint64_t seed,
+                    const int64_t* step, int32_t* send, hipStream_t st) {
+  dim3 grid(grid_for(C, 256, 512), G);
+  xchg_ff_encode_kernel<<<grid, 256, 0, st>>>(gstage, C, kw, H, nb, seed, step, send);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
 void xchg_ff_decode(const int32_t* recv, int G, int64_t C, int kw, int64_t H, int nb, float* gin,
                     hipStream_t st) {
   dim3 grid(grid_for(C, 256, 512), G);

@@ -1314,7 +1314,7 @@ __device__ __forceinline__ uint32_t tpf_unit_light(
     int shift, int f, uint32_t hb, uint64_t key0, uint32_t* hkey, uint32_t* hmap,
     uint16_t* ehraw, uint32_t* lds, uint64_t* __restrict__ uo, int32_t* __restrict__ po,
     uint16_t* __restrict__ jo, uint32_t eoff, int32_t* __restrict__ co,
-    int32_t* __restrict__ err) {
+    int32_t* __restrict__ err, bool sorted) {
   using namespace tp;
   const int t = threadIdx.x;
   uint32_t* tpre = reinterpret_cast<uint32_t*>(ehraw);             // [kMaxT + 1]
@@ -1366,7 +1366,9 @@ __device__ __forceinline__ uint32_t tpf_unit_light(
   for (uint32_t g = t; g < E; g += kBkThr)
     bad |= probe(tkeys[locate(g)] | (hb << shift), true) < 0;
   __syncthreads();
-  // key index j of every occupied slot (strided: conflict-free LDS reads)
+  // key index j of every occupied slot (strided: conflict-free LDS reads): compaction
+  // order, or (sorted) the key's rank = # smaller keys of the unit (the keys are
+  // distinct and below kEmpty)
   constexpr int kPer = kDH / kBkThr;
   uint32_t cc = 0;
 #pragma unroll
@@ -1376,9 +1378,15 @@ __device__ __forceinline__ uint32_t tpf_unit_light(
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     const int s = q * kBkThr + t;
-    if (hkey[s] != kEmpty) {
-      hmap[s] = wd;
-      uo[wd++] = key0 | hkey[s];
+    const uint32_t k = hkey[s];
+    if (k != kEmpty) {
+      uint32_t j = wd++;
+      if (sorted) {
+        j = 0;
+        for (int r = 0; r < kDH; ++r) j += hkey[r] < k;  // (kEmpty is never < k)
+      }
+      hmap[s] = j;
+      uo[j] = key0 | k;
     }
   }
   __syncthreads();
@@ -1405,7 +1413,7 @@ __global__ void __launch_bounds__(tp::kBkThr, 8)
 tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbf,
                   int pair, int T, int shift, uint64_t* __restrict__ uniqf,
                   int32_t* __restrict__ ent_pos, uint16_t* __restrict__ ent_j,
-                  int32_t* __restrict__ cnt, int32_t* __restrict__ err) {
+                  int32_t* __restrict__ cnt, int32_t* __restrict__ err, int sorted) {
   using namespace tp;
   __shared__ uint16_t eh[kECapL];  // hash slot of every gathered entry
   __shared__ uint64_t hs[kDH];     // hash (key u32 | count u32 -> key index)
@@ -1426,10 +1434,21 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
   const bool good = tp_bk_build(tkeys, toff, nbf, T, shift, f0, pair ? 2 : 1, 0u, hkey, hcnt, dl,
                                 eh, lds, &flag, idx, &E, &D, nullptr);
   if (good) {
+    // key index j: compaction order, or (sorted: the multi-GPU exchange rows must be
+    // key-ordered) the rank order of tp_bk_ranksort; slot -> j in LDS (the dead hash
+    // counts, or the dead compaction list once it is sorted into hs)
+    uint32_t* jmap = hcnt;
+    const uint64_t* lst = dl;
+    if (sorted) {
+      tp_bk_ranksort(dl, hs, D);
+      __syncthreads();
+      jmap = reinterpret_cast<uint32_t*>(dl);
+      lst = hs;
+    }
     for (uint32_t j = t; j < D; j += kBkThr) {
-      const uint64_t v = dl[j];
+      const uint64_t v = lst[j];
       uo[j] = key0 | (uint32_t)(v >> 32);
-      hcnt[(uint32_t)v & 0xffffu] = j;  // (the counts are dead after the compaction)
+      jmap[(uint32_t)v & 0xffffu] = j;
     }
     __syncthreads();
 #pragma unroll
@@ -1437,7 +1456,7 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
       if (idx[q] < 0) continue;
       const uint32_t g = q * kBkThr + t;
       po[g] = idx[q];
-      jo[g] = (uint16_t)hcnt[eh[g]];
+      jo[g] = (uint16_t)jmap[eh[g]];
     }
     if (t == 0) {
       co[0] = (int32_t)D;
@@ -1450,10 +1469,10 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
   // the pair's entries overflow the LDS capacity (or its hash): its fine buckets one
   // after the other, each a unit with its own key index space
   const uint32_t e0 = tpf_unit_light(tkeys, toff, nbf, T, shift, f0, 0u, key0, hkey, hcnt, eh, lds,
-                                     uo, po, jo, 0u, co, err);
+                                     uo, po, jo, 0u, co, err, sorted != 0);
   if (pair)
     tpf_unit_light(tkeys, toff, nbf, T, shift, f0 + 1, 1u, key0, hkey, hcnt, eh, lds,
-                   uo + tpf::kUnitK, po, jo, e0, co + 2, err);
+                   uo + tpf::kUnitK, po, jo, e0, co + 2, err, sorted != 0);
   else if (t == 0) {
     co[2] = 0;
     co[3] = 0;
@@ -1638,6 +1657,171 @@ tpf_step_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __r
   }
 }
 
+// ---- the padded multi-GPU exchange on the flat layout (G peers, G a power of two that
+// divides the bucket workgroups: owner p's key range is exactly the buckets
+// [p * B / G, (p + 1) * B / G), whose keys are rank-sorted (tpf_bucket sorted = 1), so
+// the rows stay key-ordered for the owner's partitioned apply). A bucket's keys sit in
+// its owner's row after those of the owner's earlier buckets: that offset is the sum of
+// < B / G earlier counts, read straight from cnt[] (the bucket kernel has completed),
+// so no bucket waits for another.
+__device__ __forceinline__ int tpf_row_base(const int32_t* __restrict__ cnt, int b, int per,
+                                            uint32_t* red /* LDS [kThr/64 + 1] */) {
+  const int b0 = (b / per) * per;
+  int s = 0;
+  for (int q = b0 + (int)threadIdx.x; q < b; q += blockDim.x) s += cnt[4 * q] + cnt[4 * q + 2];
+  uint32_t tot;
+  tp_block_scan<tpf::kThr>((uint32_t)s, red, &tot);
+  return (int)tot;
+}
+
+// keys of every bucket into its owner's row of `send` ([nkeys, ngrads, -, - | keys (C x kw
+// words) | grads]); the owner's last bucket writes the row's key count; keys past C
+// count as overflow (ovf, once per owner)
+__global__ void __launch_bounds__(tpf::kThr)
+tpf_pack_keys_kernel(const int32_t* __restrict__ cnt, const uint64_t* __restrict__ uniqf, int per,
+                     int64_t C, int kw, int64_t H, int32_t* __restrict__ send,
+                     int32_t* __restrict__ ovf) {
+  using namespace tpf;
+  __shared__ uint32_t red[kThr / 64 + 1];
+  const int b = blockIdx.x, p = b / per, t = threadIdx.x;
+  const int base = tpf_row_base(cnt, b, per, red);
+  const int D0 = min(cnt[4 * b], kUnitK), D1 = min(cnt[4 * b + 2], kUnitK);
+  int32_t* row = send + (int64_t)p * H;
+  for (int i = t; i < D0 + D1; i += kThr) {
+    const int64_t pos = (int64_t)base + i;
+    if (pos >= C) break;
+    const uint64_t k = i < D0 ? uniqf[(int64_t)b * kUC + i]
+                              : uniqf[(int64_t)b * kUC + kUnitK + (i - D0)];
+    if (kw == 1) row[4 + pos] = (int32_t)(uint32_t)k;
+    else reinterpret_cast<uint64_t*>(row + 4)[pos] = k;
+  }
+  if (t == 0 && b % per == per - 1) {
+    const int64_t tot = (int64_t)base + D0 + D1;
+    row[0] = (int32_t)(tot < C ? tot : C);
+    if (tot > C && ovf) atomicAdd(ovf, (int32_t)(tot - C));
+  }
+}
+
+// pulled weights (row order, wrecv[p * C + i]) -> LDS per unit key -> the bucket's
+// entries in tile-entry order (w_ent) for the flat fused forward
+__global__ void __launch_bounds__(tpf::kThr)
+tpf_unpack_w_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict__ ent_pos,
+                    const uint16_t* __restrict__ ent_j, int per, int64_t C,
+                    const float* __restrict__ wrecv, float* __restrict__ w_ent, int64_t w_cap) {
+  using namespace tpf;
+  __shared__ uint32_t red[kThr / 64 + 1];
+  __shared__ float wj[kUnitK];
+  const int b = blockIdx.x, p = b / per, t = threadIdx.x;
+  const int base = tpf_row_base(cnt, b, per, red);
+  const int32_t* c = cnt + 4 * b;
+  int off = base;
+#pragma unroll 1
+  for (int s = 0; s < 2; ++s) {
+    const int e0 = s ? min(max(c[1], 0), kEC) : 0;
+    const int D = min(c[2 * s], kUnitK), E = min(c[2 * s + 1], kEC - e0);
+    if (D <= 0) continue;
+    for (int j = t; j < D; j += kThr) {
+      const int64_t pos = (int64_t)off + j;
+      wj[j] = pos < C ? wrecv[(int64_t)p * C + pos] : 0.f;
+    }
+    __syncthreads();
+    const int64_t eb = (int64_t)b * kEC + e0;
+    for (int g = t; g < E; g += kThr) {
+      const int32_t pos = ent_pos[eb + g];
+      const uint16_t j = ent_j[eb + g];
+      if (in_range(pos, w_cap) && j < kUnitK) w_ent[pos] = wj[j];
+    }
+    __syncthreads();
+    off += D;
+  }
+}
+
+// every key's gradient (its entries' partials summed in LDS, 64-bit fixed point as in
+// tpf_step) into its owner's row; ff = 1: f32 into gstage[p * C + i] and the row's
+// FixingFloat min / max (header words 2 / 3, order-preserving ints; xchg_ff_init ran
+// first) for xchg_ff_encode. The owner's last bucket writes the row's gradient count.
+// Block 0: the step's AUC epilogue and the overflow flag to the host.
+__device__ __forceinline__ int tpf_ff_ord(float f) {
+  const int b = __float_as_int(f);
+  return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__global__ void __launch_bounds__(tpf::kThr)
+tpf_pack_grads_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict__ ent_pos,
+                      const uint16_t* __restrict__ ent_j, int per, int64_t C, int kw, int64_t H,
+                      const float* __restrict__ psum, int64_t p_cap, int32_t* __restrict__ send,
+                      int ff, float* __restrict__ gstage, uint32_t* __restrict__ hist,
+                      int hist_stripes, double* __restrict__ metrics,
+                      int64_t* __restrict__ step_counter, const int32_t* __restrict__ ovf,
+                      int32_t* __restrict__ ovf_host) {
+  using namespace tpf;
+  __shared__ uint32_t red[kThr / 64 + 1];
+  __shared__ long long acc[kUnitK];
+  __shared__ uint32_t smax;
+  const int b = blockIdx.x, p = b / per, t = threadIdx.x, lane = t & 63;
+  if (b == 0) {
+    if (ovf_host && t == 0) ovf_host[0] = ovf[0];
+    if (hist) auc_hist_block(hist, 2048, hist_stripes, metrics, step_counter);
+  }
+  const int base = tpf_row_base(cnt, b, per, red);
+  const int32_t* c = cnt + 4 * b;
+  int32_t* row = send + (int64_t)p * H;
+  float* grow = reinterpret_cast<float*>(row + 4 + C * kw);
+  float lo = 3.4e38f, hi = -3.4e38f;
+  int off = base;
+#pragma unroll 1
+  for (int s = 0; s < 2; ++s) {
+    const int e0 = s ? min(max(c[1], 0), kEC) : 0;
+    const int D = min(c[2 * s], kUnitK), E = min(c[2 * s + 1], kEC - e0);
+    if (D <= 0) continue;
+    const int64_t eb = (int64_t)b * kEC + e0;
+    for (int j = t; j < D; j += kThr) acc[j] = 0ll;
+    if (t == 0) smax = 0u;
+    float vmax = 0.f;
+    for (int g = t; g < E; g += kThr) {
+      const int32_t pos = ent_pos[eb + g];
+      if (in_range(pos, p_cap)) vmax = fmaxf(vmax, fabsf(psum[pos]));
+    }
+    __syncthreads();
+    fx_tile_max(vmax, &smax);
+    __syncthreads();
+    const int k2 = fx_shift(smax);
+    const double sc = ldexp(1.0, k2);
+    for (int g = t; g < E; g += kThr) {
+      const int32_t pos = ent_pos[eb + g];
+      const uint16_t j = ent_j[eb + g];
+      const float x = in_range(pos, p_cap) ? psum[pos] : 0.f;
+      if (x != 0.f && j < kUnitK) fx_add(acc, j, x, sc);
+    }
+    __syncthreads();
+    const double isc = ldexp(1.0, -k2);
+    for (int j = t; j < D; j += kThr) {
+      const int64_t pos = (int64_t)off + j;
+      if (pos >= C) break;
+      const float g = (float)((double)acc[j] * isc);
+      if (ff) {
+        gstage[(int64_t)p * C + pos] = g;
+        if (g == g) {
+          lo = fminf(lo, g);
+          hi = fmaxf(hi, g);
+        }
+      } else {
+        grow[pos] = g;
+      }
+    }
+    __syncthreads();  // (acc of the next unit)
+    off += D;
+  }
+  if (ff) {
+    lo = wave_min(lo);
+    hi = wave_max(hi);
+    if (lane == 0 && lo <= hi) {
+      atomicMin(&row[2], tpf_ff_ord(lo));
+      atomicMax(&row[3], tpf_ff_ord(hi));
+    }
+  }
+  if (t == 0 && b % per == per - 1) row[1] = (int32_t)(off < C ? off : C);
+}
+
 // ---------------------------------------------------------------------------
 struct TpGeom {
   int nbk, shift;
@@ -1733,7 +1917,7 @@ size_t tpf_temp_bytes(int64_t n, int bits) {
 // checks; tpf_groups)
 void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
                   int32_t* dcnt, uint16_t* rep, uint64_t* uniqf, int32_t* ent_pos, uint16_t* ent_j,
-                  int32_t* cnt, int32_t* err, hipStream_t st) {
+                  int32_t* cnt, int32_t* err, bool sorted, hipStream_t st) {
   if (n <= 0) return;
   if (!tploc_supported(n, m.bits)) throw std::runtime_error("localize_tpf: unsupported size");
   if (temp_bytes < tpf_temp_bytes(n, m.bits)) throw std::runtime_error("localize_tpf: temp");
@@ -1751,9 +1935,51 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
   PSAMD_HIP_CHECK(hipGetLastError());
   const bool pair = g.nbk >= 2 && g.shift <= 30;
   tpf_bucket_kernel<<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
-      tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err);
+      tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
+      sorted ? 1 : 0);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
+
+// multi-GPU flat exchange: the owner of bucket workgroup b is b / per, per = groups / G
+bool tpf_exchange_ok(int64_t n, int bits, int G) {
+  const int groups = tpf_groups(n, bits);
+  return G >= 1 && !(G & (G - 1)) && groups % G == 0;
+}
+static int tpf_per_owner(int64_t n, int bits, int G) {
+  if (!tpf_exchange_ok(n, bits, G))
+    throw std::runtime_error("tpf exchange: G must be a power of two dividing the bucket groups");
+  return tpf_groups(n, bits) / G;
+}
+
+void tpf_pack_keys(int64_t n, int bits, int G, const int32_t* cnt, const uint64_t* uniqf, int64_t C,
+                   int kw, int64_t H, int32_t* send, int32_t* ovf, hipStream_t st) {
+  const int per = tpf_per_owner(n, bits, G);
+  tpf_pack_keys_kernel<<<(unsigned)tpf_groups(n, bits), tpf::kThr, 0, st>>>(cnt, uniqf, per, C, kw,
+                                                                           H, send, ovf);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void tpf_unpack_w(int64_t n, int bits, int G, const int32_t* cnt, const int32_t* ent_pos,
+                  const uint16_t* ent_j, int64_t C, const float* wrecv, float* w_ent, int64_t w_cap,
+                  hipStream_t st) {
+  const int per = tpf_per_owner(n, bits, G);
+  tpf_unpack_w_kernel<<<(unsigned)tpf_groups(n, bits), tpf::kThr, 0, st>>>(cnt, ent_pos, ent_j, per,
+                                                                           C, wrecv, w_ent, w_cap);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void tpf_pack_grads(int64_t n, int bits, int G, const int32_t* cnt, const int32_t* ent_pos,
+                    const uint16_t* ent_j, int64_t C, int kw, int64_t H, const float* psum,
+                    int64_t p_cap, int32_t* send, bool ff, float* gstage, uint32_t* hist,
+                    int hist_stripes, double* metrics, int64_t* step_counter, const int32_t* ovf,
+                    int32_t* ovf_host, hipStream_t st) {
+  const int per = tpf_per_owner(n, bits, G);
+  tpf_pack_grads_kernel<<<(unsigned)tpf_groups(n, bits), tpf::kThr, 0, st>>>(
+      cnt, ent_pos, ent_j, per, C, kw, H, psum, p_cap, send, ff ? 1 : 0, gstage, hist,
+      hist_stripes, metrics, step_counter, ovf, ovf_host);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
 
 // One launch of tpf_step_kernel over the groups of an n-key minibatch (A and B: the
 // same n). A = null: pull only; B = null: update only.

@@ -154,19 +154,30 @@ class SparseLRTrainer:
         self._fused_update = os.environ.get("PSAMD_FUSED_UPDATE", "1") != "0"
         self._use_plans = os.environ.get("PSAMD_STEP_PLAN", "1") != "0"
         mode = cfg.localize
-        # 1 GPU: the flat layout (Localizer "tpf": fixed per-bucket regions, the step's
-        # pull fused into the previous step's update, tpf_step); PSAMD_FLAT=0 keeps "tp"
-        flat_ok = (self.G == 1 and self.gpu and self.filter is None and self._fused_update
-                   and self._use_plans and os.environ.get("PSAMD_FLAT", "1") != "0")
+        # the flat layout (Localizer "tpf": fixed per-bucket regions, ops/localize.FlatLoc):
+        # 1 GPU: the step's pull fused into the previous step's update (tpf_step); G > 1
+        # on the padded exchange: owner rows packed straight from the bucket regions (G a
+        # power of two dividing the bucket groups, tpf_exchange_ok). PSAMD_FLAT=0: "tp"
+        flat_env = os.environ.get("PSAMD_FLAT", "1") != "0"
+        self._flat_x = False  # G > 1: the padded exchange on the flat layout
+        if self.G == 1:
+            flat_ok = (self.gpu and self.filter is None and self._fused_update
+                       and self._use_plans and flat_env)
+        else:
+            flat_ok = self._flat_x = bool(
+                self.gpu and flat_env and self.filter is None and cfg.exchange == "padded"
+                and self.bits <= 34 and hipops().tploc_supported(self.max_nnz, self.bits)
+                and hipops().tpf_exchange_ok(self.max_nnz, self.bits, self.G))
         if mode == "auto":  # tile dedup + key-range buckets (Localizer falls back to sort
             mode = "tpf" if flat_ok else "tp"  # for > 34-bit keys or > 5.2 M keys)
         if mode == "tpf" and not flat_ok:
             mode = "tp"
+        self._flat_x = self._flat_x and mode == "tpf"
         if cfg.tail_feature_freq > 0 and mode == "tp":
             mode = "sort"  # the tail filter needs per-key nnz counts (seg_start over nnz)
         # local columns on demand: the fused tp forward/backward reads the entry map
         self.localizer = Localizer(self.max_nnz, self.bits, self.device, mode=mode,
-                                   lazy_cols=True)
+                                   lazy_cols=True, sorted_keys=self._flat_x)
         self.localize_mode = self.localizer.mode  # after the Localizer's fallbacks
         self._localizers = [self.localizer]  # + a second buffer set for prefetching (G > 1)
         self._compact = None  # flat mode: a "tp" Localizer for steps the flat path cannot run
@@ -253,7 +264,8 @@ class SparseLRTrainer:
         exchange (``step(..., loc=..., prefetch=...)``)."""
         while len(self._localizers) <= buf:
             self._localizers.append(Localizer(self.max_nnz, self.bits, self.device,
-                                              mode=self.localize_mode, lazy_cols=True))
+                                              mode=self.localize_mode, lazy_cols=True,
+                                              sorted_keys=self._flat_x))
         return self._localizers[buf](keys)
 
     def step(self, keys: torch.Tensor, labels: torch.Tensor, *, width: int | None = None,
@@ -269,7 +281,7 @@ class SparseLRTrainer:
         workgroups), and the next ``step(loc=next_loc)`` skips its own pull. The table
         is fully updated when this step's work completes either way."""
         pre, self._pre = self._pre, None  # a pull issued ahead serves the next step only
-        if self.localize_mode == "tpf":
+        if self.localize_mode == "tpf" and self.G == 1:
             B = labels.numel()
             width = width or (None if row_ptr is not None else self.cfg.max_nnz_per_example)
             if (row_ptr is None and rows is None and vals is None and prefetch is None
@@ -449,7 +461,7 @@ class SparseLRTrainer:
         plan.add_criteo_gen(seed & ((1 << 64) - 1), row0, row_step, B, num_features, alpha, keys,
                             labels)
         plan.add_localize_tpf(keys, n, self.bits, lz.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos,
-                              f.ent_j, f.cnt, f.err)
+                              f.ent_j, f.cnt, f.err, False)
 
         def run():
             plan.run()
@@ -531,6 +543,15 @@ class SparseLRTrainer:
         B = labels.numel()
         if width is None and row_ptr is None:
             width = self.cfg.max_nnz_per_example
+        flat = getattr(loc, "flat", False)
+        if flat and not (row_ptr is None and rows is None and vals is None
+                         and self._flat_ok(B, width, loc.nnz)
+                         and hipops().tpf_exchange_ok(loc.nnz, self.bits, self.G)):
+            # not expressible on the flat layout: the same keys, localised compactly
+            if self._compact is None:
+                self._compact = Localizer(self.max_nnz, self.bits, self.device, mode="tp",
+                                          lazy_cols=True)
+            loc, flat = self._compact(keys), False
         if row_ptr is not None and rows is None and self.gpu:
             rows = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
         if self.xc is None:
@@ -541,6 +562,8 @@ class SparseLRTrainer:
         gb = self.sched.grad_ring(t)  # grads(t-1-lag) live here; keys(t) join them
 
         def finish():
+            if flat:
+                return self._x_finish_flat(loc, labels, B, width, r)
             if row_ptr is not None and self.gpu:
                 hipops().csr_rows(row_ptr, rows)
             self._x_finish(loc, labels, B, width, row_ptr, vals, rows, r)
@@ -554,7 +577,9 @@ class SparseLRTrainer:
         def exchanged():
             self._xx += 1
 
-        segs = [("compute", lambda: self._x_pack_keys(loc, gb, r)),
+        pack = (lambda: self._x_pack_keys_flat(loc, gb, r)) if flat else \
+            (lambda: self._x_pack_keys(loc, gb, r))
+        segs = [("compute", pack),
                 ("comm", lambda: comm.all_to_all_fixed(xc.sends[gb], xc.recvs[r]))]
         if self.cfg.ssp_apply not in ("post", "pre"):
             raise ValueError(f"ssp_apply must be 'post' or 'pre', not {self.cfg.ssp_apply!r}")
@@ -603,7 +628,15 @@ class SparseLRTrainer:
 
         cfg, G, dev, R = self.cfg, self.G, self.device, self.R
         C = int(cfg.exchange_capacity)
-        if C <= 0:
+        if C <= 0 and getattr(loc, "flat", False):
+            # keys per owner: the owner's buckets' unit counts (buckets [p * B/G, ...))
+            g = hipops().tpf_groups(loc.nnz, loc.bits)
+            c = loc.cnt[:4 * g].view(G, g // G, 4).to(torch.float64)
+            cnt = (c[:, :, 0] + c[:, :, 2]).sum(1).max().reshape(1)
+            cnt = self.comm.all_reduce_(cnt.to(self.comm.device) if self.comm.backend == "nccl"
+                                        else cnt.cpu(), op="max")
+            C = int(math.ceil(float(cnt.item()) * cfg.exchange_slack)) + 1024
+        elif C <= 0:
             _, _, off, _ = self._owner_order(loc)
             cnt = (off[1:] - off[:-1]).max().to(torch.float64).reshape(1)
             cnt = self.comm.all_reduce_(cnt.to(self.comm.device) if self.comm.backend == "nccl"
@@ -726,6 +759,40 @@ class SparseLRTrainer:
             k = ukeys[a:a + c]
             k32 = k.to(torch.int32) if kw == 1 else k.contiguous().view(torch.int32)
             send[p * H + 4:p * H + 4 + c * kw] = k32
+
+    def _x_pack_keys_flat(self, loc, gb: int, r: int):
+        """Flat layout: every bucket's (rank-sorted) keys straight into its owner's row."""
+        xc = self.xc
+        xc.curs[r] = None
+        hh = hipops()
+        hh.tpf_pack_keys(loc.nnz, loc.bits, self.G, loc.cnt, loc.uniqf, xc.C, xc.kw, xc.H,
+                         xc.sends[gb], xc.ovf)
+        if xc.nb:  # (FixingFloat push: no pack_grads launch to carry the flag)
+            hh.xchg_publish(xc.ovf, xc.ovf_host)
+
+    def _x_finish_flat(self, loc, labels, B: int, width: int, r: int):
+        """Flat layout, worker half: the pulled weights into tile-entry order, the flat
+        fused forward + tile backward, every key's gradient (per-bucket fixed-point sums)
+        into its owner's row of the next exchange [+ FixingFloat codes], AUC epilogue."""
+        xc, hh = self.xc, hipops()
+        n, bits, G = loc.nnz, loc.bits, self.G
+        send = xc.sends[r]
+        hh.tpf_unpack_w(n, bits, G, loc.cnt, loc.ent_pos, loc.ent_j, xc.C, xc.wrecvs[r],
+                        loc.w_ent)
+        coef = self._coef_views.get(B)
+        if coef is None:
+            coef = self._coef_views[B] = self.coef[:B]
+        hh.tp_fwd_bwd(loc.rep, loc.dcnt, None, n, width, None, loc.w_ent, labels, B,
+                      loss_id(self.cfg.loss), coef, self.metrics, self.hist, AUC_BINS, loc.psum,
+                      None, None, None, None, False)
+        if xc.nb:
+            hh.xchg_ff_init(send, xc.H)
+        hh.tpf_pack_grads(n, bits, G, loc.cnt, loc.ent_pos, loc.ent_j, xc.C, xc.kw, xc.H,
+                          loc.psum, send, xc.gstage if xc.nb else None, self.hist, self.metrics,
+                          self.step_dev, xc.ovf, None if xc.nb else xc.ovf_host)
+        if xc.nb:
+            seed = (self.cfg.seed * 7919 + 17) & ((1 << 64) - 1)
+            hh.xchg_ff_encode(xc.gstage, xc.C, xc.kw, xc.H, xc.nb, seed, self.step_dev, send)
 
     def _x_poll_overflow(self):
         """Raise at the first step whose exchange dropped keys (the device counter is

@@ -138,8 +138,10 @@ class Localizer:
     "tp" on the Criteo-shaped batch, profiles/r2_localize_tp_vs_sort.log.)"""
 
     def __init__(self, max_nnz: int, bits: int, device="cpu", with_hess: bool = False,
-                 mode: str = "sort", lazy_cols: bool = False):
+                 mode: str = "sort", lazy_cols: bool = False, sorted_keys: bool = False):
         self.max_nnz = int(max_nnz)
+        # "tpf": rank-sort each bucket's keys (the multi-GPU exchange rows stay key-ordered)
+        self.sorted_keys = bool(sorted_keys)
         self.lazy_cols = bool(lazy_cols)  # "tp": local_col on demand (ensure_local_col)
         self.bits = int(bits)
         self.device = torch.device(device)
@@ -267,7 +269,7 @@ class Localizer:
         if self.mode == "tpf":
             f = self.flat
             H.localize_tpf(keys, self.bits, self.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos,
-                           f.ent_j, f.cnt, f.err)
+                           f.ent_j, f.cnt, f.err, self.sorted_keys)
             f.nnz = n
             f.gen += 1
             return f

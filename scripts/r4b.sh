@@ -2,7 +2,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/r4b
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
-timeout -k 10 600 python -u -m pytest tests/test_tpf_gpu.py tests/test_p2p_gpu.py tests/test_tp_fused_gpu.py -x -v --timeout 180 --timeout-method thread -p no:cacheprovider > gpurun_out/r4b/pytest_tpf.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_tpf_gpu.py tests/test_p2p_gpu.py tests/test_tp_fused_gpu.py tests/test_dist_gpu.py -x -v --timeout 180 --timeout-method thread -p no:cacheprovider > gpurun_out/r4b/pytest_tpf.log 2>&1
 rc=$?; tail -3 gpurun_out/r4b/pytest_tpf.log; [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
   for fl in 0 1; do

@@ -28,6 +28,7 @@ def _gpu_worker(rank, world, port, out_dir, cfg_kw, steps, pipelined=False):
     comm, dev = init_from_env("cuda")
     cfg = SparseLRConfig(**cfg_kw)
     tr = SparseLRTrainer(cfg, comm, dev)
+    assert tr.localize_mode == cfg.localize or cfg.localize == "auto", tr.localize_mode
     B = cfg.minibatch
     batches = [criteo_batch(B, seed=100 + rank, row0=s * B, num_features=cfg.num_features,
                             cards=[200] * 26) for s in range(steps)]
@@ -61,7 +62,9 @@ def _gpu_worker(rank, world, port, out_dir, cfg_kw, steps, pipelined=False):
                          [(0, False, "padded", "sort"), (0, False, "exact", "sort"),
                           (3, False, "padded", "sort"), (3, False, "exact", "sort"),
                           (0, True, "padded", "sort"),
-                          (0, True, "exact", "sort"), (0, False, "padded", "tp")])
+                          (0, True, "exact", "sort"), (0, False, "padded", "tp"),
+                          (0, False, "padded", "tpf"), (3, False, "padded", "tpf"),
+                          (0, True, "padded", "tpf")])
 def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes, pipelined, exchange,
                                                  localize):
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
