@@ -76,6 +76,7 @@ void tpf_step(int64_t, int, const int32_t*, const int32_t*, const uint16_t*, con
               float, float, uint64_t, int32_t*, int32_t*, int, int, float, float, float, float,
               float, float, double*, int, uint32_t*, int, int, double*, int64_t*, hipStream_t);
 int64_t tploc_stride(int64_t);
+int tploc_buckets(int64_t, int);
 int tploc_tile();
 bool tploc_supported(int64_t, int);
 size_t tploc_temp_bytes(int64_t, int);
@@ -757,6 +758,7 @@ PYBIND11_MODULE(_hipops, m) {
   });
   // ---------------- tile dedup + bucket partition localisation (tploc.hip) ----------------
   m.def("tploc_stride", [](int64_t n) { return psamd::tploc_stride(n); });
+  m.def("tploc_buckets", [](int64_t n, int bits) { return psamd::tploc_buckets(n, bits); });
   m.def("tploc_supported", [](int64_t n, int bits) { return psamd::tploc_supported(n, bits); });
   m.def("tploc_temp_bytes", [](int64_t n, int bits) { return (int64_t)psamd::tploc_temp_bytes(n, bits); });
   m.def("localize_tp", [](Tensor keys, int bits, Tensor temp, Tensor dcnt, Tensor rep, Tensor pos_s,

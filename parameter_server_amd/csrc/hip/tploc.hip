@@ -1844,6 +1844,7 @@ static TpGeom tp_geom(int64_t n, int bits) {
 }
 
 int64_t tploc_stride(int64_t n) { return tp_geom(n, 31).N; }
+int tploc_buckets(int64_t n, int bits) { return tp_geom(n, bits).nbk; }
 int tploc_tile() { return tp::kTile; }
 
 bool tploc_supported(int64_t n, int bits) {

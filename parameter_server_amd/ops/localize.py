@@ -119,7 +119,7 @@ class Localizer:
 
     ``mode="sort"``: radix sort + RLE (unique keys in sorted mixed order, CSC order
     for the segmented backward).
-    ``mode="part"``    ``mode="part"`` (csrc/hip/partloc.hip, GPU, key bits <= 32): one partition pass on
+    ``mode="part"`` (csrc/hip/partloc.hip, GPU, key bits <= 32): one partition pass on
     the top key bits, then one workgroup per bucket deduplicates its keys in an LDS
     hash and sorts only the DISTINCT keys; same outputs as "sort" except the order of
     positions inside a key's segment (5 launches instead of 16).
@@ -274,6 +274,14 @@ class Localizer:
             f.gen += 1
             return f
         if self.mode == "tp":
+            # the look-back's status words carry an 8-bit launch epoch: when the bucket
+            # count changes (another minibatch size), a bucket left unused for exactly
+            # 255 launches could accept a stale word -> zero them (and the epoch) then
+            nbk = H.tploc_buckets(n, self.bits)
+            if nbk != getattr(self, "_last_nbk", None):
+                if getattr(self, "_last_nbk", None) is not None:
+                    self.ptemp[:(max(nbk, self._last_nbk) * 8 + 16 + 15) // 16 * 16].zero_()
+                self._last_nbk = nbk
             H.localize_tp(keys, self.bits, self.ptemp, self.t_dcnt, self.t_rep, self.pos_s,
                           self.segid, self.uniq, self.seg_start, self.t_ent_uid,
                           None if self.lazy_cols else self.local_col,

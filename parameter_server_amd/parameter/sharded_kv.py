@@ -32,7 +32,9 @@ MI355X design (one process per GPU, every rank = worker + server shard):
   src/system/message.h:120-159; a fixed row of max_keys per peer would move G x the
   live payload over xGMI). A row that would overflow keeps its first C keys and the
   excess is counted on the device; the count is published to pinned host memory
-  (no stream sync) and the next call, ``wait``, ``flush`` or ``check`` raises on it
+  (no stream sync) and the next call, ``wait`` or ``check`` of THAT rank raises on it
+  (its peers then stop at their next collective, within the collective timeout
+  PSAMD_COMM_TIMEOUT); ``flush`` checks collectively, so every rank raises together
   (``peer_capacity=max_keys`` makes overflow impossible). The whole op runs on the
   worker's own HIP stream and ``push`` / ``pull`` return at once; ``wait(ts)``
   orders the caller's stream after the op (no host sync);
@@ -210,13 +212,17 @@ class KVWorker:
             self.ovf_host = self.ovf
 
     # ------------------------------------------------------------- helpers
-    def check(self, sync: bool = False) -> None:
+    def check(self, sync: bool = False, collective: bool = False) -> None:
         """Raise if a call dropped keys because a peer row was full. The pack kernels
         publish the device count to pinned host memory (seen once they completed);
-        ``sync=True`` waits for the worker's stream first."""
+        ``sync=True`` waits for the worker's stream first; ``collective=True`` (every
+        rank calls it) takes the largest count of all ranks over the host channel, so
+        all ranks raise together instead of the others waiting in their next collective."""
         if sync and self.gpu:
             self.stream.synchronize()
         n = int(self.ovf_host[0])
+        if collective and self.G > 1:
+            n = max(self.comm.host_gather_obj(n))
         if n:
             raise RuntimeError(
                 f"KVWorker exchange overflow: {n} keys exceeded the per-peer row capacity "
@@ -643,6 +649,7 @@ class KVWorker:
         out, ev = self._done.pop(ts)
         if ev is not None:
             torch.cuda.current_stream(self.device).wait_event(ev)
+        self.check()  # (an overflow published by a completed pack raises here)
         return out
 
     def flush(self):
@@ -651,7 +658,7 @@ class KVWorker:
             self._drain(keep=0)
 
         out = self.wait(self._run(op))
-        self.check(sync=True)
+        self.check(sync=True, collective=True)
         return out
 
     def barrier(self):
