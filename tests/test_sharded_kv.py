@@ -255,8 +255,8 @@ def test_skewed_keys_overflow_raises():
     np.testing.assert_allclose(kv.wait(kv.pull(ok)).numpy(), 1.0)
     bad = unmix(torch.arange(n, dtype=torch.int64), 64)   # all owned by shard 0
     assert int(kv.part.owner_of(torch.arange(n, dtype=torch.int64)).max()) == 0
-    kv.wait(kv.push(bad, torch.ones(n)))
-    with pytest.raises(RuntimeError, match="overflow"):
+    with pytest.raises(RuntimeError, match="overflow"):  # (wait() checks: CPU pack is done)
+        kv.wait(kv.push(bad, torch.ones(n)))
         kv.pull(ok)
 
 
@@ -305,6 +305,6 @@ def test_skewed_keys_overflow_raises_gpu():
     np.testing.assert_allclose(kv.wait(kv.pull(ok)).cpu().numpy(), 1.0)
     kv.flush()
     bad = unmix(torch.arange(n, dtype=torch.int64), 64).cuda()
-    kv.wait(kv.push(bad, torch.ones(n, device="cuda")))
-    with pytest.raises(RuntimeError, match="overflow"):
+    with pytest.raises(RuntimeError, match="overflow"):  # at wait() once the pack completed,
+        kv.wait(kv.push(bad, torch.ones(n, device="cuda")))  # else at the collective flush
         kv.flush()
