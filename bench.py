@@ -303,6 +303,41 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     warm += (-warm) % P  # capture at a multiple of P: phase j <-> buffer j % NB, ring j % R
     for _ in range(warm):
         iterate()
+    if flat and os.environ.get("PSAMD_NATIVE_ITER", "1") != "0":
+        # 1 GPU, flat: one iteration (both streams' event waits, the step's launches, the
+        # next preparation's launches, the records) is ONE native launch-list call; phase
+        # j = t % NB: step t on buffer j (its pull was issued by step t-1) pulling
+        # buffer j+1, and the preparation of buffer j + nprep on its stream. The lists
+        # share the launch objects of the eager path (the generators' row cursors).
+        from parameter_server_amd.ops.native import hipops
+
+        H = hipops()
+        phases = []
+        for j in range(NB):
+            cur, nxt, nb = j, (j + 1) % NB, (j + nprep) % NB
+            s = sides[nb % nprep]
+            splan, _ = tr.flat_plan(locs[cur], bufs[cur][1], B, 39, locs[nxt], True)
+            L = H.LaunchList()
+            L.add_stream(main.cuda_stream)
+            L.add_wait(ev_prep[cur].cuda_event)
+            L.add_wait(ev_prep[nxt].cuda_event)
+            L.extend(splan)
+            L.add_record(ev_buf[cur].cuda_event)
+            L.add_stream(s.cuda_stream)
+            L.add_wait(ev_buf[nb].cuda_event)
+            L.extend(fplans[nb].plan)
+            L.add_record(ev_prep[nb].cuda_event)
+            phases.append((L.run, locs[nxt], fplans[nb].done))
+
+        def iterate_native():
+            t = state["t"]
+            run, nxt_loc, prep_done = phases[t % NB]
+            run()
+            tr.flat_done(B, nxt_loc)
+            prep_done()
+            state["t"] = t + 1
+
+        return iterate_native, False
     if not args.graph or flat:  # (flat: eager launch lists; their row cursors live on the host)
         return iterate, False
     torch.cuda.synchronize()

@@ -313,8 +313,13 @@ int64_t slot_capacity(const Tensor& slots) {
 
 // ---- validate-once launchers (the single ops and LaunchList share them) ----
 using Launch = std::function<void(hipStream_t)>;
+// A launch list op gets the list's current stream by reference: kernel ops launch on
+// it, control ops switch it or order it against events (a multi-stream iteration of the
+// data pipeline as ONE host call, bench.py).
+using Op = std::function<void(hipStream_t&)>;
 struct LaunchList {
-  std::vector<Launch> ops;
+  std::vector<Op> ops;
+  void push(Launch l) { ops.push_back([l](hipStream_t& s) { l(s); }); }
 };
 
 Launch make_kv_resolve(Tensor slots, Tensor keys, optional<Tensor> n_dev, Tensor out_slot,
@@ -688,7 +693,7 @@ PYBIND11_MODULE(_hipops, m) {
     check(G >= 1 && G <= 64 && self >= 0 && self < G, "p2p: 1..64 ranks");
     check(tabs.numel() == 5 * G, "tabs: 5 int64 per rank");
     check(kw == 1 || kw == 2, "kw 1 or 2");
-    check(H >= 4 + C * kw + C, "row too short");
+    check(H >= 4 + C * kw, "row too short (header + C keys)");
     check(send.numel() >= G * H && wout.numel() >= G * C && slot_out.numel() >= G * C,
           "p2p_lookup_rows buffers too small");
     psamd::p2p_lookup_rows(tabs.data_ptr(), G, self, ptr<int32_t>(send), H, C, kw, ptr<float>(wout),
@@ -961,7 +966,7 @@ PYBIND11_MODULE(_hipops, m) {
                                 int init_type, double init_v, double init_s, uint64_t seed,
                                 optional<Tensor> err, optional<Tensor> inserted,
                                 uint64_t home_base, uint64_t home_m) {
-        l.ops.push_back(make_kv_resolve(slots, keys, n_dev, out_slot, out_w, insert, init_type,
+        l.push(make_kv_resolve(slots, keys, n_dev, out_slot, out_w, insert, init_type,
                                         init_v, init_s, seed, err, inserted, home_base, home_m));
       })
       .def("add_tp_fwd_bwd", [](LaunchList& l, Tensor rep, Tensor dcnt, optional<Tensor> ent_uid,
@@ -970,7 +975,7 @@ PYBIND11_MODULE(_hipops, m) {
                                 optional<Tensor> metrics, optional<Tensor> hist, int nbins,
                                 Tensor psum, optional<Tensor> pos_s, optional<Tensor> segid,
                                 optional<Tensor> n_ent, optional<Tensor> grad, bool reduce) {
-        l.ops.push_back(make_tp_fwd_bwd(rep, dcnt, ent_uid, n, width, vals, w_local, labels, B,
+        l.push(make_tp_fwd_bwd(rep, dcnt, ent_uid, n, width, vals, w_local, labels, B,
                                         loss_type, coef, metrics, hist, nbins, psum, pos_s, segid,
                                         n_ent, grad, reduce));
       })
@@ -981,7 +986,7 @@ PYBIND11_MODULE(_hipops, m) {
                                    double grad_scale, double max_delta, optional<Tensor> stats,
                                    optional<Tensor> hist, optional<Tensor> metrics,
                                    optional<Tensor> step_counter) {
-        l.ops.push_back(make_tp_seg_update(pos_s, segid, n, n_ent, psum, seg_start, n_uniq, pieces,
+        l.push(make_tp_seg_update(pos_s, segid, n, n_ent, psum, seg_start, n_uniq, pieces,
                                            slot_idx, slots, algo, lr_type, alpha, beta, l1, l2,
                                            grad_scale, max_delta, stats, hist, metrics,
                                            step_counter));
@@ -989,7 +994,7 @@ PYBIND11_MODULE(_hipops, m) {
       .def("add_localize_tpf", [](LaunchList& l, Tensor keys, int64_t n, int bits, Tensor temp,
                                   Tensor dcnt, Tensor rep, Tensor uniqf, Tensor ent_pos,
                                   Tensor ent_j, Tensor cnt, Tensor err, bool sorted) {
-        l.ops.push_back(make_localize_tpf(keys, n, bits, temp, dcnt, rep, uniqf, ent_pos, ent_j,
+        l.push(make_localize_tpf(keys, n, bits, temp, dcnt, rep, uniqf, ent_pos, ent_j,
                                           cnt, err, sorted));
       })
       .def("add_tpf_step", [](LaunchList& l, int64_t n, int bits, optional<py::tuple> A,
@@ -1001,7 +1006,7 @@ PYBIND11_MODULE(_hipops, m) {
                               double l2, double grad_scale, double max_delta,
                               optional<Tensor> stats, optional<Tensor> hist,
                               optional<Tensor> metrics, optional<Tensor> step_counter) {
-        l.ops.push_back(make_tpf_step(n, bits, tpf_bufs(A), psum, tpf_bufs(B), w_ent, slots,
+        l.push(make_tpf_step(n, bits, tpf_bufs(A), psum, tpf_bufs(B), w_ent, slots,
                                       init_type, init_v, init_s, seed, err, inserted, home_base,
                                       home_m, algo, lr_type, alpha, beta, l1, l2, grad_scale,
                                       max_delta, stats, hist, metrics, step_counter));
@@ -1009,12 +1014,32 @@ PYBIND11_MODULE(_hipops, m) {
       .def("add_criteo_gen", [](LaunchList& l, uint64_t seed, int64_t row0, int64_t row_step,
                                 int64_t B, uint64_t num_features, double alpha, Tensor keys,
                                 Tensor labels) {
-        l.ops.push_back(make_criteo_gen(seed, row0, row_step, B, num_features, alpha, keys,
+        l.push(make_criteo_gen(seed, row0, row_step, B, num_features, alpha, keys,
                                         labels));
+      })
+      // control ops: raw handles of torch.cuda.Stream.cuda_stream / Event.cuda_event (the
+      // caller keeps those objects alive and has created the events, e.g. by a record)
+      .def("add_stream", [](LaunchList& l, uint64_t stream) {
+        const hipStream_t h = reinterpret_cast<hipStream_t>(stream);
+        l.ops.push_back([h](hipStream_t& s) { s = h; });
+      })
+      .def("add_wait", [](LaunchList& l, uint64_t event) {
+        check(event != 0, "add_wait: event not created yet (record it once first)");
+        const hipEvent_t e = reinterpret_cast<hipEvent_t>(event);
+        l.ops.push_back([e](hipStream_t& s) { PSAMD_HIP_CHECK(hipStreamWaitEvent(s, e, 0)); });
+      })
+      .def("add_record", [](LaunchList& l, uint64_t event) {
+        check(event != 0, "add_record: event not created yet (record it once first)");
+        const hipEvent_t e = reinterpret_cast<hipEvent_t>(event);
+        l.ops.push_back([e](hipStream_t& s) { PSAMD_HIP_CHECK(hipEventRecord(e, s)); });
+      })
+      // the ops of another list, SHARED (a generator's row cursor advances for both)
+      .def("extend", [](LaunchList& l, const LaunchList& o) {
+        l.ops.insert(l.ops.end(), o.ops.begin(), o.ops.end());
       })
       .def("__len__", [](const LaunchList& l) { return l.ops.size(); })
       .def("run", [](const LaunchList& l) {
-        const hipStream_t st = cur_stream();
+        hipStream_t st = cur_stream();
         for (const auto& op : l.ops) op(st);
       });
   // ---------------- fixed-capacity exchange (exchange.hip) ----------------

@@ -407,6 +407,21 @@ class SparseLRTrainer:
         """pull (unless issued ahead) -> fused forward + tile backward -> tpf_step: the
         update of this minibatch, then the pull of ``next_loc`` (same size) in the same
         launch. One native launch list per (buffers, labels, next buffers)."""
+        plan, nxt = self.flat_plan(loc, labels, B, width, next_loc, pre)
+        plan.run()
+        self.flat_done(B, nxt)
+
+    def flat_done(self, B: int, nxt):
+        """Host bookkeeping of a flat step whose launches were issued (``flat_plan``)."""
+        if nxt is not None:
+            self._pre = (id(nxt), nxt.gen)
+        self.step_count += 1
+        self.examples += B
+
+    def flat_plan(self, loc, labels, B: int, width: int, next_loc, pre: bool):
+        """(LaunchList of one flat step, the next FlatLoc its update launch pulls or None);
+        cached per (buffers, labels, next buffers). bench.py splices it into its native
+        multi-stream iteration lists."""
         nxt = next_loc if (next_loc is not None and getattr(next_loc, "flat", False)
                            and next_loc.nnz == loc.nnz and next_loc is not loc) else None
         key = (id(loc), id(labels), B, width, loc.nnz, pre, id(nxt) if nxt is not None else 0,
@@ -432,11 +447,7 @@ class SparseLRTrainer:
             if len(self._plans) >= 32:  # (callers passing fresh label tensors every step)
                 self._plans.clear()
             self._plans[key] = plan
-        plan.run()
-        if nxt is not None:
-            self._pre = (id(nxt), nxt.gen)
-        self.step_count += 1
-        self.examples += B
+        return plan, nxt
 
     def prep_plan(self, buf: int, keys: torch.Tensor, labels: torch.Tensor, *, seed: int,
                   row0: int, row_step: int, num_features: int, alpha: float = 1.1):
@@ -465,9 +476,13 @@ class SparseLRTrainer:
 
         def run():
             plan.run()
+            return done()
+
+        def done():  # (host bookkeeping: also after the list ran inside another one)
             f.nnz = n
             f.gen += 1
             return f
+        run.plan, run.done = plan, done
         return run
 
     def _step_plan(self, loc, labels, B: int, width: int):

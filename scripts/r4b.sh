@@ -1,15 +1,20 @@
-# round 4: flat 1-GPU path tests + A/B bench (PSAMD_FLAT=0 baseline) + kernel trace
+# round 4: flat 1-GPU path tests + A/B bench (PSAMD_FLAT=0 baseline, native iteration on/off) + kernel trace
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/r4b
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest tests/test_tpf_gpu.py tests/test_p2p_gpu.py tests/test_tp_fused_gpu.py tests/test_dist_gpu.py -x -v --timeout 180 --timeout-method thread -p no:cacheprovider > gpurun_out/r4b/pytest_tpf.log 2>&1
 rc=$?; tail -3 gpurun_out/r4b/pytest_tpf.log; [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
-  for fl in 0 1; do
-    PSAMD_FLAT=$fl PSAMD_STEP_EVENTS=1 timeout -k 10 120 python bench.py --steps 20 --warmup 5 > gpurun_out/r4b/b20_f${fl}_$i.log 2>&1 || exit $?
+  for v in "PSAMD_FLAT=0" "PSAMD_FLAT=1 PSAMD_NATIVE_ITER=0" "PSAMD_FLAT=1"; do
+    tag=$(echo $v | tr ' =' '__')
+    env $v PSAMD_STEP_EVENTS=1 timeout -k 10 120 python bench.py --steps 20 --warmup 5 > gpurun_out/r4b/b20_${tag}_$i.log 2>&1 || exit $?
   done
 done
-for fl in 0 1; do
-  PSAMD_FLAT=$fl timeout -k 10 120 python bench.py --steps 300 --warmup 10 > gpurun_out/r4b/b300_f$fl.log 2>&1 || exit $?
+for v in "PSAMD_FLAT=0" "PSAMD_FLAT=1"; do
+  tag=$(echo $v | tr ' =' '__')
+  env $v timeout -k 10 120 python bench.py --steps 300 --warmup 10 > gpurun_out/r4b/b300_$tag.log 2>&1 || exit $?
 done
+timeout -k 10 120 python bench.py --steps 300 --warmup 10 --minibatch 10000 > gpurun_out/r4b/b300_b10k.log 2>&1 || exit $?
+timeout -k 10 200 python bench.py --steps 100 --warmup 10 --emulate-peers 8 > gpurun_out/r4b/e8.log 2>&1 || exit $?
+PSAMD_FLAT=0 timeout -k 10 200 python bench.py --steps 100 --warmup 10 --emulate-peers 8 > gpurun_out/r4b/e8_f0.log 2>&1 || exit $?
 cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/r4b/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 > "$GRAFT_REPO_ROOT/gpurun_out/r4b/prof.log" 2>&1
