@@ -40,7 +40,7 @@ for name, M, N, K in SHAPES:
     C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     ref = torch.relu(A[:512].float() @ B.float().t() + bias)
     errs = []
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3):
         C.fill_(float("nan"))
         H.gemm_nt256(A, B, M, N, K, bias, True, C, None, v)
         errs.append(((C[:512].float() - ref).abs() / (ref.abs() + 1)).max().item())
@@ -48,12 +48,14 @@ for name, M, N, K in SHAPES:
     us_new = t(lambda: H.gemm_nt256(A, B, M, N, K, bias, True, C, None, 0))
     us_pp = t(lambda: H.gemm_nt256(A, B, M, N, K, bias, True, C, None, 1))
     us_p8 = t(lambda: H.gemm_nt256(A, B, M, N, K, bias, True, C, None, 2))
+    us_fine = t(lambda: H.gemm_nt256(A, B, M, N, K, bias, True, C, None, 3))
     us_old = t(lambda: GM.gemm(A, True, B, True, M, N, K, bias=bias, relu=True))
     us_lib = t(lambda: torch.mm(A, B.t()))
     print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "max_rel_err_vs_fp32": errs,
                       "gemm256_us": us_new, "gemm256_tflops": fl / us_new / 1e6,
                       "gemm256pp_us": us_pp, "gemm256pp_tflops": fl / us_pp / 1e6,
                       "gemm256p8_us": us_p8, "gemm256p8_tflops": fl / us_p8 / 1e6,
+                      "gemm256fine_us": us_fine, "gemm256fine_tflops": fl / us_fine / 1e6,
                       "gemm128_tflops": fl / us_old / 1e6, "hipblaslt_tflops": fl / us_lib / 1e6}),
           flush=True)
 

@@ -66,6 +66,13 @@ __device__ __forceinline__ void g256_stage(const __bf16* __restrict__ p, int64_t
   }
 }
 
+// kFine: the fragment reads of a sub-step interleaved with its MFMAs (B fragments and
+// A fragment 0 first, then A fragment i+1 in flight while the 4 MFMAs of fragment i
+// issue, the next sub-step's B fragments during the last row), pinned by scheduling
+// group barriers: the compiler's own schedule waits for all 12 reads (lgkmcnt(0))
+// before the first of 32 MFMAs of every sub-step, and with 2 waves per SIMD that
+// wait is only covered when the other wave happens to be in its MFMA run.
+template <bool kFine>
 __global__ void __launch_bounds__(g256::TH)
 gemm_nt256_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B,
                   int64_t ldb, int M, int N, int K, const float* __restrict__ bias, int relu,
@@ -95,27 +102,70 @@ gemm_nt256_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
       g256_stage(A, lda, M, m0, (kt + 1) * BK, nxt, wave, lane);
       g256_stage(B, ldb, N, n0, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
     }
+    if (kFine) {
+      auto rd_b = [&](int ks, int j) {
+        const int c = ks * 4 + (lane >> 4), r = wc * 64 + j * 16 + (lane & 15);
+        return *reinterpret_cast<const bf16x8*>(cur + TILE_BYTES + r * 128 + g256_swz(r, c) * 16);
+      };
+      auto rd_a = [&](int ks, int i) {
+        const int c = ks * 4 + (lane >> 4), r = wr * 128 + i * 16 + (lane & 15);
+        return *reinterpret_cast<const bf16x8*>(cur + r * 128 + g256_swz(r, c) * 16);
+      };
+      bf16x8 b[2][4], a[2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c = ks * 4 + (lane >> 4);
-      bf16x8 a[8], b[4];
+      for (int j = 0; j < 4; ++j) b[0][j] = rd_b(0, j);
+      a[0] = rd_a(0, 0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = wc * 64 + j * 16 + (lane & 15);
-        b[j] = *reinterpret_cast<const bf16x8*>(cur + TILE_BYTES + r * 128 + g256_swz(r, c) * 16);
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          // in flight during the 4 MFMAs of row i: A fragment i+1 (or the next sub-step's
+          // first), and in the last row of sub-step 0 the next sub-step's B fragments
+          if (i < 7) a[(i + 1) & 1] = rd_a(ks, i + 1);
+          else if (ks == 0) a[(i + 1) & 1] = rd_a(1, 0);
+          if (ks == 0 && i == 7) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[1][j] = rd_b(1, j);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i & 1], b[ks][j], acc[i][j], 0,
+                                                                0, 0);
+        }
       }
+      // schedule: [B x4, A0] then per row {A next (+ B x4 of sub-step 1 at row 7), 4 MFMA}
+#define G256_SG(mask, n) __builtin_amdgcn_sched_group_barrier(mask, n, 0)
+#define G256_ROW(nr) G256_SG(0x100, nr); G256_SG(0x008, 4)
+      G256_SG(0x100, 5);
+      G256_ROW(1); G256_ROW(1); G256_ROW(1); G256_ROW(1);  // sub-step 0, rows 0-3
+      G256_ROW(1); G256_ROW(1); G256_ROW(1); G256_ROW(5);  // rows 4-7 (+ next B)
+      G256_ROW(1); G256_ROW(1); G256_ROW(1); G256_ROW(1);  // sub-step 1
+      G256_ROW(1); G256_ROW(1); G256_ROW(1); G256_SG(0x008, 4);
+#undef G256_ROW
+#undef G256_SG
+    } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int r = wr * 128 + i * 16 + (lane & 15);
-        a[i] = *reinterpret_cast<const bf16x8*>(cur + r * 128 + g256_swz(r, c) * 16);
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + (lane >> 4);
+        bf16x8 a[8], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = wc * 64 + j * 16 + (lane & 15);
+          b[j] = *reinterpret_cast<const bf16x8*>(cur + TILE_BYTES + r * 128 + g256_swz(r, c) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = wr * 128 + i * 16 + (lane & 15);
+          a[i] = *reinterpret_cast<const bf16x8*>(cur + r * 128 + g256_swz(r, c) * 16);
+        }
+        __builtin_amdgcn_s_setprio(1);  // MFMA cluster at raised priority (guide T5)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
       }
-      __builtin_amdgcn_s_setprio(1);  // MFMA cluster at raised priority (guide T5)
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next K-step has landed
     __syncthreads();                                   // ... and this one is read
@@ -796,10 +846,14 @@ void gemm_nt256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int 
     gemm_nt256pp_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
                                                                 relu ? 1 : 0, C, ldc, Cf, ldcf,
                                                                 tiles_n);
+  else if (variant == 3)
+    gemm_nt256_kernel<true><<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
+                                                                    relu ? 1 : 0, C, ldc, Cf, ldcf,
+                                                                    tiles_n);
   else
-    gemm_nt256_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
-                                                              relu ? 1 : 0, C, ldc, Cf, ldcf,
-                                                              tiles_n);
+    gemm_nt256_kernel<false><<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
+                                                                     relu ? 1 : 0, C, ldc, Cf,
+                                                                     ldcf, tiles_n);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

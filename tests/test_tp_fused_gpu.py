@@ -94,7 +94,9 @@ def test_tp_fused_fixed_point_partials_are_deterministic_and_exact():
         c_f, g_f = linear_fwd_bwd(L, w, labels, B=B, width=width, coef=torch.empty(B, device=DEV))
         outs.append(g_f[:U].clone())
         parts.append(L.tile.psum.clone())
-    assert all(torch.equal(parts[0], p) for p in parts[1:])
+    # bitwise (as int32: entries past a tile's count are never written, and uninitialised
+    # memory may hold NaN patterns, which torch.equal on floats reports as unequal)
+    assert all(torch.equal(parts[0].view(torch.int32), p.view(torch.int32)) for p in parts[1:])
     cols = ensure_local_col(L)[:n].long()
     m = w[cols].reshape(B, width).double().sum(1).float()
     _, c, _ = loss_terms_torch(m, labels, 2)
