@@ -153,6 +153,7 @@ def test_fused_seg_update_matches_scan_then_update(algo, monkeypatch):
 
     B = 16384
     outs = []
+    monkeypatch.setenv("PSAMD_FLAT", "0")  # the compact tp path (the flat one: test_tpf_gpu.py)
     for fused in ("1", "0"):
         monkeypatch.setenv("PSAMD_FUSED_UPDATE", fused)
         cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B, table_capacity=1 << 22, algo=algo,
@@ -178,7 +179,7 @@ def test_fused_seg_update_matches_scan_then_update(algo, monkeypatch):
     assert pa["nnz_w"] == pytest.approx(pb["nnz_w"], abs=3)
 
 
-def test_native_step_plan_matches_op_by_op():
+def test_native_step_plan_matches_op_by_op(monkeypatch):
     """1 GPU: the step issued from the validate-once native LaunchList (_step_plan) runs
     the launches the op-by-op path issues: the same keys, and weights / state / metrics
     equal to float rounding (hot keys combine their chunk pieces through atomics, whose
@@ -187,6 +188,7 @@ def test_native_step_plan_matches_op_by_op():
 
     B = 16384
     outs = []
+    monkeypatch.setenv("PSAMD_FLAT", "0")  # the compact tp path's launch list
     for native in (True, False):
         cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B, table_capacity=1 << 22)
         tr = SparseLRTrainer(cfg, device=DEV)
