@@ -34,6 +34,8 @@ def main():
                     help="criteo: 39 one-hot slots (one block per slot; tau = 8 diverges on "
                          "them, tests/test_darlin.py); groups: CTR-log-shaped, 120 groups with "
                          "8 present per example x 2 keys (tau = 8 converges)")
+    ap.add_argument("--tau32", type=int, default=1,
+                    help="1: row-pass tau_i in fp32 (G / U sums stay fp64 fixed point); 0: fp64 exp")
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--host-preprocess", action="store_true",
                     help="build the CSC with numpy (reference path) instead of on the GPU")
@@ -58,7 +60,7 @@ def main():
                           on_device=args.device_data and not args.cpu)
     cfg = DarlinConfig(l1=args.l1, tau=args.tau, tail_freq=args.tail_freq,
                        max_pass=args.passes + args.warmup, epsilon=0.0, seed=0,
-                       host_preprocess=args.host_preprocess)
+                       host_preprocess=args.host_preprocess, tau32=bool(args.tau32))
     tr = DarlinTrainer(sd, cfg, comm=comm, device=device)
     prep = time.time() - t0
     for it in range(args.warmup):
@@ -87,7 +89,8 @@ def main():
             "config": {"rows_per_gpu": args.rows, "num_features": int(args.num_features),
                        "kept_features": tr.num_cols, "nnz_per_gpu": tr.nnz,
                        "blocks": len(tr.blocks), "tau": args.tau, "l1": args.l1,
-                       "tail_freq": args.tail_freq, "data": args.data},
+                       "tail_freq": args.tail_freq, "data": args.data,
+                       "tau_fp32": bool(args.tau32)},
             "preprocess_sec": prep,
             "trainer_preprocess_sec": tr.preprocess_time,
             "preprocess_breakdown_sec": tr.prep_times,

@@ -530,6 +530,24 @@ struct RowDual {
   int ncols;
 };
 
+// tau_i = 1 / (1 + exp(ym_i)) in the row passes: kF32 computes it in fp32 (v_exp_f32 +
+// v_rcp_f32, ~1e-7 relative) instead of fp64 exp + divide (~50 VALU ops per example,
+// what made the narrow pass VALU-bound: profiles/r3_darlin_rowpass.log); the factors
+// -y tau, tau (1 - tau) and the G / U sums stay fp64 / 64-bit fixed point.
+template <bool kF32>
+__device__ __forceinline__ double rp_tau(double m) {
+  if (kF32) {
+    const float e = __expf(fminf((float)m, 80.f));  // exp(80) < FLT_MAX: no inf / NaN
+    return (double)__builtin_amdgcn_rcpf(1.f + e);
+  }
+  return 1.0 / (1.0 + exp(m));
+}
+
+template <bool kF32>
+__device__ __forceinline__ double rp_exp(double x) {
+  return kF32 ? (double)__expf(fminf((float)x, 80.f)) : exp(x);
+}
+
 __device__ __forceinline__ double rp_dual_delta(const RowDual& d, int c, int64_t i, double dwc,
                                                 double yr) {
   const double x = d.dval ? (double)d.dval[i] : 1.0;
@@ -540,7 +558,7 @@ __device__ __forceinline__ double rp_dual_delta(const RowDual& d, int c, int64_t
 // column of LDS slot h (ncols = their count); dcol[i] >= 0 marks a COLD entry (its
 // factors go to rowq[i] for the chunked column-order kernel over the cold columns),
 // dcol[i] <= -2 the hot slot -2 - dcol[i], -1 no entry.
-template <bool kDual, bool kHot>
+template <bool kDual, bool kHot, bool kF32>
 __global__ void __launch_bounds__(512)
 bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restrict__ y,
                         RowDual dj, const int32_t* __restrict__ dcol, const float* __restrict__ dval,
@@ -606,19 +624,19 @@ bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restr
     for (int q = 0; q < kR; ++q) {
       const int c = ck[q];
       if (kHot && c == kColdRow) {  // cold entry: factors for the column-order kernel
-        const double tau = 1.0 / (1.0 + exp(m[q]));
+        const double tau = rp_tau<kF32>(m[q]);
         rowq[i0 + (int64_t)q * blockDim.x] = make_double2(-(double)yv[q] * tau, tau * (1.0 - tau));
         continue;
       }
       if (c < 0 || !cact[c]) continue;
-      const double tau = 1.0 / (1.0 + exp(m[q]));
+      const double tau = rp_tau<kF32>(m[q]);
       const double yr = (double)yv[q];
       const double t2 = tau * (1.0 - tau);
       double g, u;
       if (dval) {
         const double v = (double)dval[i0 + (int64_t)q * blockDim.x];
         g = -yr * tau * v;
-        u = fmin(t2 * exp(fabs(v) * cdl[c]), 0.25) * v * v;
+        u = fmin(t2 * rp_exp<kF32>(fabs(v) * cdl[c]), 0.25) * v * v;
       } else {
         g = -yr * tau;
         u = fmin(t2 * cdl[c], 0.25);
@@ -638,7 +656,7 @@ bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restr
   }
 }
 
-template <bool kDual, bool kQ>
+template <bool kDual, bool kQ, bool kF32>
 __global__ void __launch_bounds__(256)
 bcd_rowpass_q_kernel(int64_t n, double* __restrict__ ym, const float* __restrict__ y, RowDual dj,
                      const int32_t* __restrict__ dcol, int ncols, double2* __restrict__ rowq) {
@@ -685,7 +703,7 @@ bcd_rowpass_q_kernel(int64_t n, double* __restrict__ ym, const float* __restrict
         ym[i] = m[q];
       }
       if (kQ && ck[q] >= 0) {
-        const double tau = 1.0 / (1.0 + exp(m[q]));
+        const double tau = rp_tau<kF32>(m[q]);
         rowq[i] = make_double2(-(double)yv[q] * tau, tau * (1.0 - tau));
       }
     }
@@ -871,7 +889,8 @@ void bcd_rowpass(int64_t n, double* ym, const float* y, const int32_t* jcol, con
                  const double* jdw, int64_t jncols, const int32_t* kcol, const float* kval,
                  int64_t c0, int64_t ncols, const double* delta, const uint8_t* active, int k2,
                  int W, long long* part, double* G, double* U, double* rowq,
-                 const int32_t* hcols, int64_t nhot, long long* part2_out, hipStream_t st) {
+                 const int32_t* hcols, int64_t nhot, long long* part2_out, bool tau32,
+                 hipStream_t st) {
   if (n <= 0) return;
   const RowDual dj{jcol, jval, jdw, (int)jncols};
   if (part) {  // gradient of block k in LDS: narrow (all columns) or wide (hot columns)
@@ -880,9 +899,17 @@ void bcd_rowpass(int64_t n, double* ym, const float* y, const int32_t* jcol, con
     if (nl > kRowCols) throw std::runtime_error("bcd_rowpass: > 2048 LDS columns");
     const int copies = std::max(1, std::min(8, kRowCols / nl));
     auto q = reinterpret_cast<double2*>(rowq);
-#define PSAMD_RP(D, H)                                                                      \
-  bcd_rowpass_grad_kernel<D, H><<<W, 512, 0, st>>>(n, ym, y, dj, kcol, kval, c0, nl, copies, \
-                                                   delta, active, k2, part, hcols, q)
+#define PSAMD_RP(D, H)                                                                       \
+  do {                                                                                        \
+    if (tau32)                                                                                \
+      bcd_rowpass_grad_kernel<D, H, true><<<W, 512, 0, st>>>(n, ym, y, dj, kcol, kval, c0, nl, \
+                                                             copies, delta, active, k2, part,  \
+                                                             hcols, q);                        \
+    else                                                                                      \
+      bcd_rowpass_grad_kernel<D, H, false><<<W, 512, 0, st>>>(n, ym, y, dj, kcol, kval, c0,    \
+                                                              nl, copies, delta, active, k2,   \
+                                                              part, hcols, q);                 \
+  } while (0)
     if (jcol && hcols) PSAMD_RP(true, true);
     else if (jcol) PSAMD_RP(true, false);
     else if (hcols) PSAMD_RP(false, true);
@@ -903,14 +930,19 @@ void bcd_rowpass(int64_t n, double* ym, const float* y, const int32_t* jcol, con
   }
   const unsigned grid = (unsigned)grid_for(n, 256 * 8, 4096);
   auto q = reinterpret_cast<double2*>(rowq);
-  if (jcol && kcol)
-    bcd_rowpass_q_kernel<true, true><<<grid, 256, 0, st>>>(n, ym, y, dj, kcol, (int)ncols, q);
-  else if (kcol)
-    bcd_rowpass_q_kernel<false, true><<<grid, 256, 0, st>>>(n, ym, y, dj, kcol, (int)ncols, q);
-  else if (jcol)
-    bcd_rowpass_q_kernel<true, false><<<grid, 256, 0, st>>>(n, ym, y, dj, kcol, (int)ncols, q);
-  else
-    return;
+#define PSAMD_RQ(D, K)                                                                      \
+  do {                                                                                       \
+    if (tau32)                                                                               \
+      bcd_rowpass_q_kernel<D, K, true><<<grid, 256, 0, st>>>(n, ym, y, dj, kcol, (int)ncols, q); \
+    else                                                                                     \
+      bcd_rowpass_q_kernel<D, K, false><<<grid, 256, 0, st>>>(n, ym, y, dj, kcol, (int)ncols,  \
+                                                              q);                            \
+  } while (0)
+  if (jcol && kcol) PSAMD_RQ(true, true);
+  else if (kcol) PSAMD_RQ(false, true);
+  else if (jcol) PSAMD_RQ(true, false);
+  else return;
+#undef PSAMD_RQ
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

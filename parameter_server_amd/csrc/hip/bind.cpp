@@ -197,7 +197,7 @@ void bcd_grad_chunked(const int32_t*, const int32_t*, const float*, const int64_
 void bcd_rowpass(int64_t, double*, const float*, const int32_t*, const float*, const double*,
                  int64_t, const int32_t*, const float*, int64_t, int64_t, const double*,
                  const uint8_t*, int, int, long long*, double*, double*, double*, const int32_t*,
-                 int64_t, long long*, hipStream_t);
+                 int64_t, long long*, bool, hipStream_t);
 void bcd_update(int64_t, int64_t, double*, double*, double*, double*, uint8_t*, double*, double,
                 double, double, double, unsigned long long*, bool, bool, const long long*, int,
                 hipStream_t);
@@ -1912,7 +1912,7 @@ PYBIND11_MODULE(_hipops, m) {
                           optional<Tensor> kval, int64_t c0, int64_t ncols, Tensor delta,
                           Tensor active, int k2, int W, optional<Tensor> part,
                           optional<Tensor> G, optional<Tensor> U, optional<Tensor> rowq,
-                          optional<Tensor> hcols, optional<Tensor> part2) {
+                          optional<Tensor> hcols, optional<Tensor> part2, bool tau32) {
     chk(ym, at::kDouble, "ym");
     chk(y, at::kFloat, "y");
     chk(delta, at::kDouble, "delta");
@@ -1959,8 +1959,12 @@ PYBIND11_MODULE(_hipops, m) {
     }
     psamd::bcd_rowpass(n, ptr<double>(ym), ptr<float>(y), jc, jv, jd, jncols, kc, kv, c0, ncols,
                        ptr<double>(delta), ptr<uint8_t>(active), k2, W, pp, Gp, Up, rq, hc, nhot,
-                       optr<long long>(part2, at::kLong, "part2"), cur_stream());
-  });
+                       optr<long long>(part2, at::kLong, "part2"), tau32, cur_stream());
+  }, py::arg("ym"), py::arg("y"), py::arg("jcol"), py::arg("jval"), py::arg("jdw"),
+     py::arg("jncols"), py::arg("kcol"), py::arg("kval"), py::arg("c0"), py::arg("ncols"),
+     py::arg("delta"), py::arg("active"), py::arg("k2"), py::arg("W"), py::arg("part"),
+     py::arg("G"), py::arg("U"), py::arg("rowq"), py::arg("hcols"), py::arg("part2"),
+     py::arg("tau32") = false);
   m.def("bcd_grad", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                 int64_t p1, int64_t c0, int64_t ncols, Tensor ym, Tensor y,
                                 Tensor delta, Tensor active, Tensor G, Tensor U) {

@@ -87,6 +87,9 @@ class DarlinConfig:
     # bound), all-reduce below (latency-bound)
     shard_server: str = "auto"
     shard_min_cols: int = 1 << 16
+    # fused row pass: tau_i = 1 / (1 + exp(ym_i)) in fp32 (bcd.hip rp_tau; the G / U sums
+    # stay fp64 / fixed point). Off = fp64 exp, the mode the CPU-parity tests pin.
+    tau32: bool = False
 
     @classmethod
     def from_lm(cls, lm, seed: int = 0) -> "DarlinConfig":
@@ -610,7 +613,7 @@ class DarlinTrainer:
                     p2 = b.part2
                 bcd.rowpass(self.ym, self.y, self.delta, self.active, kcol=b.dcol, kval=b.dval,
                             c0=b.c0, ncols=b.ncols, k2=b.fx_k, W=self.rows_W,
-                            part=self.rows_part, G=G, U=U, part2=p2, **jd)
+                            part=self.rows_part, G=G, U=U, part2=p2, tau32=self.cfg.tau32, **jd)
                 return
             if b.hcols is not None:  # hot columns in LDS, cold ones column by column
                 if not zeroed:  # (the reduce stores the hot sums before the chunk pass)
@@ -618,13 +621,13 @@ class DarlinTrainer:
                     U.zero_()
                 bcd.rowpass(self.ym, self.y, self.delta, self.active, kcol=b.kenc, kval=b.dval,
                             c0=b.c0, ncols=b.ncols, k2=b.fx_k, W=self.rows_W_hot,
-                            part=self.rows_part, G=G, U=U, rowq=self.rowq, hcols=b.hcols, **jd)
+                            part=self.rows_part, G=G, U=U, rowq=self.rowq, hcols=b.hcols, tau32=self.cfg.tau32, **jd)
                 bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym,
                          self.y, self.delta, self.active, G, U, chunks=b.chunks_cold,
                          zeroed=True, rowq=self.rowq, rowq_ready=True)
                 return
             bcd.rowpass(self.ym, self.y, self.delta, self.active, kcol=b.dcol, kval=b.dval,
-                        c0=b.c0, ncols=b.ncols, rowq=self.rowq, **jd)
+                        c0=b.c0, ncols=b.ncols, rowq=self.rowq, tau32=self.cfg.tau32, **jd)
             bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
                      self.delta, self.active, G, U, chunks=b.chunks, zeroed=zeroed,
                      rowq=self.rowq, rowq_ready=True)

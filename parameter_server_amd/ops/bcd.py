@@ -176,7 +176,7 @@ def hot_layout(dcol, colptr, c0: int, c1: int, nhot: int = 2048, min_share: floa
 
 def rowpass(ym, y, delta, active, *, jcol=None, jval=None, jdw=None, jncols: int = 0,
             kcol=None, kval=None, c0: int = 0, ncols: int = 0, k2: int = 0, W: int = 1,
-            part=None, G=None, U=None, rowq=None, hcols=None, part2=None):
+            part=None, G=None, U=None, rowq=None, hcols=None, part2=None, tau32: bool = False):
     """GPU row pass over dense block layouts (``dense_rows``): first the pending dual
     update of block j (``jcol`` / ``jval`` / its ``jdw``: ym_i += y_i dw_c x_ic), then on
     the updated margins block k's gradient: narrow (``part`` given: fixed-point column
@@ -184,11 +184,12 @@ def rowpass(ym, y, delta, active, *, jcol=None, jval=None, jdw=None, jncols: int
     into ``rowq`` (for ``grad(..., rowq_ready=True)``); with ``hcols`` (``hot_layout``),
     a wide block's hot columns in LDS and the cold entries' factors into ``rowq``;
     ``part2`` (narrow): leave the segment sums there for ``update(..., part2=)`` instead
-    of storing G / U.
+    of storing G / U. ``tau32``: tau_i = 1 / (1 + exp(ym_i)) in fp32 (the G / U sums
+    stay fp64 / fixed point; ~1e-7 relative per factor), the fast mode of the benchmark.
     Equal to ``dual`` followed by ``grad_rows`` / the rowq packing up to the fixed-point
     quantisation (tests/test_darlin_gpu.py)."""
     hipops().bcd_rowpass(ym, y, jcol, jval, jdw, int(jncols), kcol, kval, int(c0), int(ncols),
-                         delta, active, int(k2), int(W), part, G, U, rowq, hcols, part2)
+                         delta, active, int(k2), int(W), part, G, U, rowq, hcols, part2, bool(tau32))
 
 
 def fixed_point_shift(entries: int, max_abs_val: float) -> int:

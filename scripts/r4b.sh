@@ -19,5 +19,10 @@ timeout -k 10 120 python bench.py --steps 300 --warmup 10 --minibatch 10000 > gp
 timeout -k 10 200 python bench.py --steps 100 --warmup 10 --emulate-peers 8 > gpurun_out/r4b/e8.log 2>&1 || exit $?
 PSAMD_FLAT=0 timeout -k 10 200 python bench.py --steps 100 --warmup 10 --emulate-peers 8 > gpurun_out/r4b/e8_f0.log 2>&1 || exit $?
 timeout -k 10 300 python benchmarks/bench_gemm256.py > gpurun_out/r4b/gemm256.log 2>&1 || exit $?
+for t in 0 1; do
+  timeout -k 10 200 python benchmarks/bench_darlin.py --rows 4000000 --passes 5 --device-data --tau32 $t > gpurun_out/r4b/darlin_t32_$t.log 2>&1 || exit $?
+done
+timeout -k 10 300 python benchmarks/bench_darlin.py --rows 4000000 --passes 5 --data groups --tau 8 > gpurun_out/r4b/darlin_groups_tau8.log 2>&1 || exit $?
+timeout -k 10 300 python benchmarks/bench_darlin.py --rows 4000000 --passes 5 --data groups --tau 1 > gpurun_out/r4b/darlin_groups_tau1.log 2>&1 || exit $?
 cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/r4b/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 > "$GRAFT_REPO_ROOT/gpurun_out/r4b/prof.log" 2>&1 && \
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/r4b/prof_seq" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 40 --warmup 10 --pipeline 0 > "$GRAFT_REPO_ROOT/gpurun_out/r4b/prof_seq.log" 2>&1

@@ -272,3 +272,27 @@ def test_fused_row_pass_bitwise_equal_to_separate_kernels(monkeypatch, tau, valu
     torch.testing.assert_close(out["1"][1], out["0"][1], rtol=1e-9, atol=1e-9)
     torch.testing.assert_close(out["1"][2], out["0"][2], rtol=1e-9, atol=1e-12)
     assert (out["1"][3] != out["0"][3]).sum().item() <= 2
+
+
+@pytest.mark.parametrize("data,tau", [("criteo", 1), ("groups", 8)])
+def test_fp32_tau_row_pass_keeps_the_objective_trajectory(data, tau):
+    """tau32 (the benchmark's fast row pass: tau_i = 1 / (1 + exp(ym_i)) in fp32, G / U
+    sums still fp64 fixed point) follows the fp64 trainer's per-pass objective to 1e-5
+    relative, on the Criteo-shaped slots at tau = 1 and the converging groups data at
+    tau = 8."""
+    if data == "criteo":
+        sd = criteo_slots(200_000, seed=3, num_features=10 ** 6, device="cuda")
+    else:
+        from parameter_server_amd.data.synthetic import sparse_groups
+
+        sd = sparse_groups(60_000, seed=5)
+    objs = {}
+    for t32 in (False, True):
+        cfg = DarlinConfig(l1=4.0, max_pass=4, tail_freq=2, tau=tau, seed=0, epsilon=0.0,
+                           tau32=t32)
+        tr = DarlinTrainer(sd, cfg, device="cuda")
+        if data == "criteo":  # (the groups blocks are too sparse for the dense row layouts)
+            assert any(b.dcol is not None for b in tr.blocks)
+        objs[t32] = [p.objective for p in tr.train()]
+    np.testing.assert_allclose(objs[True], objs[False], rtol=1e-5)
+    assert objs[True][-1] < objs[True][0]
