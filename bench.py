@@ -337,6 +337,16 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             prep_done()
             state["t"] = t + 1
 
+        try:  # (untimed: a failing launch list falls back to the eager iteration, loudly)
+            for _ in range(NB):
+                iterate_native()
+            torch.cuda.synchronize()
+        except Exception as e:
+            print(f"[psamd] native iteration failed ({e}); eager launches", file=sys.stderr)
+            torch.cuda.synchronize()
+            args.native_iter = f"failed: {e}"
+            return iterate, False
+        args.native_iter = True
         return iterate_native, False
     if not args.graph or flat:  # (flat: eager launch lists; their row cursors live on the host)
         return iterate, False
@@ -840,6 +850,7 @@ def main():
                 "collectives_in_graphs": bool(getattr(pipeline, "captured_comm", False)
                                               and graph_used),
                 "prep_streams": args.prep_streams if (gpu and args.pipeline) else 1,
+                "native_iteration": getattr(args, "native_iter", False),
                 "localize": tr.localize_mode,
                 "emulated_peers": G if emulated else None,
                 "exchange": (f"{args.exchange} (capacity {tr.xc.C} keys/peer/step)"

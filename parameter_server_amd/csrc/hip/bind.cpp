@@ -319,7 +319,15 @@ using Launch = std::function<void(hipStream_t)>;
 using Op = std::function<void(hipStream_t&)>;
 struct LaunchList {
   std::vector<Op> ops;
-  void push(Launch l) { ops.push_back([l](hipStream_t& s) { l(s); }); }
+  std::vector<const char*> names;  // per op (a failing op is named in the error)
+  void push(Launch l, const char* name) {
+    ops.push_back([l](hipStream_t& s) { l(s); });
+    names.push_back(name);
+  }
+  void push_op(Op o, const char* name) {
+    ops.push_back(std::move(o));
+    names.push_back(name);
+  }
 };
 
 Launch make_kv_resolve(Tensor slots, Tensor keys, optional<Tensor> n_dev, Tensor out_slot,
@@ -967,7 +975,7 @@ PYBIND11_MODULE(_hipops, m) {
                                 optional<Tensor> err, optional<Tensor> inserted,
                                 uint64_t home_base, uint64_t home_m) {
         l.push(make_kv_resolve(slots, keys, n_dev, out_slot, out_w, insert, init_type,
-                                        init_v, init_s, seed, err, inserted, home_base, home_m));
+                                        init_v, init_s, seed, err, inserted, home_base, home_m), "kv_resolve");
       })
       .def("add_tp_fwd_bwd", [](LaunchList& l, Tensor rep, Tensor dcnt, optional<Tensor> ent_uid,
                                 int64_t n, int width, optional<Tensor> vals, Tensor w_local,
@@ -977,7 +985,7 @@ PYBIND11_MODULE(_hipops, m) {
                                 optional<Tensor> n_ent, optional<Tensor> grad, bool reduce) {
         l.push(make_tp_fwd_bwd(rep, dcnt, ent_uid, n, width, vals, w_local, labels, B,
                                         loss_type, coef, metrics, hist, nbins, psum, pos_s, segid,
-                                        n_ent, grad, reduce));
+                                        n_ent, grad, reduce), "tp_fwd_bwd");
       })
       .def("add_tp_seg_update", [](LaunchList& l, Tensor pos_s, Tensor segid, int64_t n,
                                    Tensor n_ent, Tensor psum, Tensor seg_start, Tensor n_uniq,
@@ -989,13 +997,13 @@ PYBIND11_MODULE(_hipops, m) {
         l.push(make_tp_seg_update(pos_s, segid, n, n_ent, psum, seg_start, n_uniq, pieces,
                                            slot_idx, slots, algo, lr_type, alpha, beta, l1, l2,
                                            grad_scale, max_delta, stats, hist, metrics,
-                                           step_counter));
+                                           step_counter), "tp_seg_update");
       })
       .def("add_localize_tpf", [](LaunchList& l, Tensor keys, int64_t n, int bits, Tensor temp,
                                   Tensor dcnt, Tensor rep, Tensor uniqf, Tensor ent_pos,
                                   Tensor ent_j, Tensor cnt, Tensor err, bool sorted) {
         l.push(make_localize_tpf(keys, n, bits, temp, dcnt, rep, uniqf, ent_pos, ent_j,
-                                          cnt, err, sorted));
+                                          cnt, err, sorted), "localize_tpf");
       })
       .def("add_tpf_step", [](LaunchList& l, int64_t n, int bits, optional<py::tuple> A,
                               optional<Tensor> psum, optional<py::tuple> B,
@@ -1009,38 +1017,46 @@ PYBIND11_MODULE(_hipops, m) {
         l.push(make_tpf_step(n, bits, tpf_bufs(A), psum, tpf_bufs(B), w_ent, slots,
                                       init_type, init_v, init_s, seed, err, inserted, home_base,
                                       home_m, algo, lr_type, alpha, beta, l1, l2, grad_scale,
-                                      max_delta, stats, hist, metrics, step_counter));
+                                      max_delta, stats, hist, metrics, step_counter), "tpf_step");
       })
       .def("add_criteo_gen", [](LaunchList& l, uint64_t seed, int64_t row0, int64_t row_step,
                                 int64_t B, uint64_t num_features, double alpha, Tensor keys,
                                 Tensor labels) {
         l.push(make_criteo_gen(seed, row0, row_step, B, num_features, alpha, keys,
-                                        labels));
+                                        labels), "criteo_gen");
       })
       // control ops: raw handles of torch.cuda.Stream.cuda_stream / Event.cuda_event (the
       // caller keeps those objects alive and has created the events, e.g. by a record)
       .def("add_stream", [](LaunchList& l, uint64_t stream) {
         const hipStream_t h = reinterpret_cast<hipStream_t>(stream);
-        l.ops.push_back([h](hipStream_t& s) { s = h; });
+        l.push_op([h](hipStream_t& s) { s = h; }, "stream");
       })
       .def("add_wait", [](LaunchList& l, uint64_t event) {
         check(event != 0, "add_wait: event not created yet (record it once first)");
         const hipEvent_t e = reinterpret_cast<hipEvent_t>(event);
-        l.ops.push_back([e](hipStream_t& s) { PSAMD_HIP_CHECK(hipStreamWaitEvent(s, e, 0)); });
+        l.push_op([e](hipStream_t& s) { PSAMD_HIP_CHECK(hipStreamWaitEvent(s, e, 0)); }, "wait");
       })
       .def("add_record", [](LaunchList& l, uint64_t event) {
         check(event != 0, "add_record: event not created yet (record it once first)");
         const hipEvent_t e = reinterpret_cast<hipEvent_t>(event);
-        l.ops.push_back([e](hipStream_t& s) { PSAMD_HIP_CHECK(hipEventRecord(e, s)); });
+        l.push_op([e](hipStream_t& s) { PSAMD_HIP_CHECK(hipEventRecord(e, s)); }, "record");
       })
       // the ops of another list, SHARED (a generator's row cursor advances for both)
       .def("extend", [](LaunchList& l, const LaunchList& o) {
         l.ops.insert(l.ops.end(), o.ops.begin(), o.ops.end());
+        l.names.insert(l.names.end(), o.names.begin(), o.names.end());
       })
       .def("__len__", [](const LaunchList& l) { return l.ops.size(); })
       .def("run", [](const LaunchList& l) {
         hipStream_t st = cur_stream();
-        for (const auto& op : l.ops) op(st);
+        size_t i = 0;
+        try {
+          for (; i < l.ops.size(); ++i) l.ops[i](st);
+        } catch (const std::exception& e) {
+          throw std::runtime_error("LaunchList op " + std::to_string(i) + " of " +
+                                   std::to_string(l.ops.size()) + " (" + l.names[i] +
+                                   "): " + e.what());
+        }
       });
   // ---------------- fixed-capacity exchange (exchange.hip) ----------------
   // buffers: send/recv int32 [G * H]; row layout documented in exchange.hip

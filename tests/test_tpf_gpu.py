@@ -293,3 +293,41 @@ def test_prep_plan_generates_and_localises_like_the_ops():
         assert torch.equal(torch.tensor([ek[e] for e in eid]), mix(k2, tr.bits).cpu())
         assert torch.equal(f.cnt[0::2], ref.cnt[0::2])  # distinct keys per unit
         assert torch.equal(f.unique_keys().sort().values, ref.unique_keys().sort().values)
+
+
+def test_launch_list_control_ops_order_two_streams():
+    """A native launch list switching streams and ordering them with event waits /
+    records (bench.py's one-call iteration): the generator on stream 1, then, ordered
+    behind its event, a second generator run on stream 2; both rows as criteo_batch.
+    A failing op is named in the error."""
+    B = 2048
+    H = hipops()
+    s1, s2 = torch.cuda.Stream(DEV), torch.cuda.Stream(DEV)
+    ev = torch.cuda.Event()
+    ev.record(s1)  # (created)
+    k1 = torch.empty(B * 39, dtype=torch.int64, device=DEV)
+    l1 = torch.empty(B, dtype=torch.float32, device=DEV)
+    k2, l2 = torch.empty_like(k1), torch.empty_like(l1)
+    from parameter_server_amd.ops.synthetic import CRITEO_1TB_CARDS, _set_cards
+
+    _set_cards(torch.device(DEV), CRITEO_1TB_CARDS)
+    g1, g2 = H.LaunchList(), H.LaunchList()
+    g1.add_criteo_gen(5, 0, 2 * B, B, 10 ** 9, 1.1, k1, l1)
+    g2.add_criteo_gen(5, B, 2 * B, B, 10 ** 9, 1.1, k2, l2)
+    L = H.LaunchList()
+    L.add_stream(s1.cuda_stream)
+    L.extend(g1)
+    L.add_record(ev.cuda_event)
+    L.add_stream(s2.cuda_stream)
+    L.add_wait(ev.cuda_event)
+    L.extend(g2)
+    L.add_record(ev.cuda_event)
+    L.add_stream(torch.cuda.current_stream(DEV).cuda_stream)
+    L.add_wait(ev.cuda_event)
+    assert len(L) == 9
+    for r in range(2):
+        L.run()
+        torch.cuda.current_stream(DEV).synchronize()
+        for row0, k, lab in ((2 * r * B, k1, l1), ((2 * r + 1) * B, k2, l2)):
+            kr, lr = criteo_batch(B, seed=5, row0=row0, num_features=10 ** 9, device=DEV)
+            assert torch.equal(k, kr) and torch.equal(lab, lr)
