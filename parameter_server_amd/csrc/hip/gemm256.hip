@@ -832,13 +832,192 @@ void transpose_bf16(const void* in, int R, int C, void* out, hipStream_t st) {
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------
+// Ring variant (variant 4): K-steps of 32 through a 4-slot LDS ring (4 x 32 KiB: A | B
+// of 256 rows x 64 B), the DMA of K-step p+3 issued while K-step p is read, so a
+// K-step has ~4-5 barrier intervals (2-3 MFMA segments of 512 cycles) between its
+// DMA and its first read. Per K-step a wave has a READ interval (its 8 A + 4 B
+// fragments, its 4 LDS-DMA instructions of K-step p+3, lgkmcnt(0)) and an MFMA
+// interval (the 32 MFMAs of its 128 x 64 output), each closed by a raw s_barrier; the
+// second wave row (waves 4-7, one beside each first-row wave on its SIMD) runs one
+// barrier behind, so every SIMD alternates the two waves' 512-cycle MFMA runs while
+// the other wave reads (twice the MFMA run of the 16-MFMA quadrant phases of
+// variants 1-2: half the barriers per FLOP). Ordering, by global barrier index
+// (row 0's K-step p: read interval 2p, MFMA interval 2p+1; row 1's one later):
+// * RAW: every wave waits for its share of K-step p+1 (vmcnt counting the younger
+//   DMAs of K-steps p+2, p+3) before barrier 2p+1, the barrier before its first read;
+// * WAR: slot (p+3) % 4 held K-step p-1, whose reads each row retired (lgkmcnt(0))
+//   before the barrier closing its read interval (2p-2, 2p-1); its DMA is issued after
+//   barrier 2p-1 (row 0 in interval 2p, row 1 in 2p+1).
+// LDS row image: 64-B rows, 16-B chunk c of row r at c ^ ((r >> 2) & 3) (a
+// ds_read_b128 lane group, rows r..r+15 of one chunk, covers all 64 banks); the
+// swizzle goes on the DMA's per-lane global source (the LDS-DMA writes lane-linear).
+namespace g256r {
+constexpr int BK = 32, NSLOT = 4;
+constexpr int OP_BYTES = 256 * BK * 2;   // 16 KiB per operand per K-step
+constexpr int SLOT_BYTES = 2 * OP_BYTES; // A | B
+}  // namespace g256r
+
+__device__ __forceinline__ int g256r_swz(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+// this wave's 4 DMA instructions of a K-step: wi = q*8 + wave, 0-15 A rows 16 wi.., 16-31 B
+__device__ __forceinline__ void g256r_stage(const __bf16* __restrict__ A, int64_t lda, int M,
+                                            const __bf16* __restrict__ B, int64_t ldb, int N,
+                                            int m0, int n0, int k0, char* slot, int wave,
+                                            int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int wi = q * 8 + wave;
+    const bool isb = wi >= 16;  // (q >= 2: wave-uniform)
+    const int rowb = (wi & 15) * 16;
+    const int row = rowb + (lane >> 2);
+    const int c = g256r_swz(row, lane & 3);
+    const __bf16* p = isb ? B : A;
+    const int64_t ld = isb ? ldb : lda;
+    const int lim = isb ? N : M;
+    int gr = (isb ? n0 : m0) + row;
+    gr = gr < lim ? gr : lim - 1;
+    __builtin_amdgcn_global_load_lds(
+        (const void*)(p + (int64_t)gr * ld + k0 + c * 8),
+        (__attribute__((address_space(3))) void*)(slot + (isb ? g256r::OP_BYTES : 0) + rowb * 64),
+        16, 0, 0);
+  }
+}
+
+#define G256R_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+// wait for this wave's DMA of K-step p+1 (younger: those of K-steps p+2 .. min(p+3, nk-1))
+#define G256R_WAIT_NEXT(p, nk)                    \
+  do {                                            \
+    const int y_ = min((p) + 3, (nk) - 1) - ((p) + 1); \
+    if (y_ >= 2) G256R_VMCNT(8);                  \
+    else if (y_ == 1) G256R_VMCNT(4);             \
+    else G256R_VMCNT(0);                          \
+  } while (0)
+
+__global__ void __launch_bounds__(g256::TH)
+gemm_nt256r_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B,
+                   int64_t ldb, int M, int N, int K, const float* __restrict__ bias, int relu,
+                   __bf16* __restrict__ C, int64_t ldc, float* __restrict__ Cf, int64_t ldcf,
+                   int tiles_n) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(16))) char smem[g256r::NSLOT * g256r::SLOT_BYTES];  // 128 KiB
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int id = g256_xcd(blockIdx.x, gridDim.x);
+  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = K / g256r::BK;
+  // prologue: K-steps 0..2 in flight, K-step 0 landed everywhere before barrier -1
+  for (int p = 0; p < 3 && p < nk; ++p)
+    g256r_stage(A, lda, M, B, ldb, N, m0, n0, p * g256r::BK, smem + p * g256r::SLOT_BYTES, wave,
+                lane);
+  if (nk >= 3) G256R_VMCNT(8);
+  else if (nk == 2) G256R_VMCNT(4);
+  else G256R_VMCNT(0);
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // the second wave row runs one barrier behind
+  const int c = lane >> 4;
+  for (int p = 0; p < nk; ++p) {
+    const char* cur = smem + (p & 3) * g256r::SLOT_BYTES;
+    // ---- READ interval
+    bf16x8 a[8], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = wc * 64 + j * 16 + (lane & 15);
+      b[j] = *reinterpret_cast<const bf16x8*>(cur + g256r::OP_BYTES + r * 64 + g256r_swz(r, c) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = wr * 128 + i * 16 + (lane & 15);
+      a[i] = *reinterpret_cast<const bf16x8*>(cur + r * 64 + g256r_swz(r, c) * 16);
+    }
+    if (p + 3 < nk)
+      g256r_stage(A, lda, M, B, ldb, N, m0, n0, (p + 3) * g256r::BK,
+                  smem + ((p + 3) & 3) * g256r::SLOT_BYTES, wave, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (wr == 1) G256R_WAIT_NEXT(p, nk);
+    __builtin_amdgcn_s_barrier();
+    // ---- MFMA interval
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (wr == 0) G256R_WAIT_NEXT(p, nk);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second row's extra barrier
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // epilogue (as gemm_nt256_kernel): m = m0 + wr*128 + i*16 + 4*(lane>>4) + r,
+  // n = n0 + wc*64 + j*16 + (lane&15)
+  if (C && !Cf && (ldc & 7) == 0 && m0 + BM <= M && n0 + BN <= N) {
+    __bf16* st = reinterpret_cast<__bf16*>(smem);  // [256][256] bf16 = 128 KiB
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nl = wc * 64 + j * 16 + (lane & 15);
+      const float bv = bias ? bias[n0 + nl] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ml = wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+          float v = acc[i][j][r] + bv;
+          if (relu) v = v > 0.f ? v : 0.f;
+          st[ml * BN + nl] = (__bf16)v;
+        }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int q = 0; q < BM * BN / 8 / TH; ++q) {
+      const int ch = q * TH + t;
+      const int ml = ch >> 5, nc = (ch & 31) * 8;
+      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + ml) * ldc + n0 + nc) =
+          *reinterpret_cast<const uint4*>(st + ml * BN + nc);
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
+    if (n >= N) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= M) continue;
+        float v = acc[i][j][r] + bv;
+        if (relu) v = v > 0.f ? v : 0.f;
+        if (C) C[(int64_t)m * ldc + n] = (__bf16)v;
+        if (Cf) Cf[(int64_t)m * ldcf + n] = v;
+      }
+    }
+  }
+}
+#undef G256R_WAIT_NEXT
+#undef G256R_VMCNT
+
 void gemm_nt256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
                 const float* bias, bool relu, __bf16* C, int64_t ldc, float* Cf, int64_t ldcf,
                 int variant, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   if (K % g256::BK != 0 || lda % 8 || ldb % 8) throw std::runtime_error("gemm_nt256: K % 64, ld % 8");
   const int tiles_m = (M + g256::BM - 1) / g256::BM, tiles_n = (N + g256::BN - 1) / g256::BN;
-  if (variant == 2)
+  if (variant == 4)
+    gemm_nt256r_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
+                                                               relu ? 1 : 0, C, ldc, Cf, ldcf,
+                                                               tiles_n);
+  else if (variant == 2)
     gemm_nt256p8_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
                                                                 relu ? 1 : 0, C, ldc, Cf, ldcf,
                                                                 tiles_n);

@@ -22,7 +22,7 @@ def _ref(A, B, bias, relu):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 128), (300, 1000, 192),
                                    (1024, 4992, 1024), (4097, 260, 640), (64, 64, 64)])
 @pytest.mark.parametrize("epi", ["none", "bias_relu"])
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_gemm256_matches_fp32(M, N, K, epi, variant):
     g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
     A = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
@@ -49,9 +49,10 @@ def test_gemm256_pingpong_repeatable_long_k():
     ref = torch.empty(M, N, device=DEV)
     hipops().gemm_nt256(A, B, M, N, K, None, False, None, ref, 0)
     out = torch.empty(M, N, device=DEV)
-    for _ in range(10):
-        hipops().gemm_nt256(A, B, M, N, K, None, False, None, out, 1)
-        assert torch.equal(out, ref)
+    for v in (1, 4):  # (4: the 4-slot ring's counted waits)
+        for _ in range(10):
+            hipops().gemm_nt256(A, B, M, N, K, None, False, None, out, v)
+            assert torch.equal(out, ref)
 
 
 def test_gemm256_rejects_bad_k():
