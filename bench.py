@@ -303,7 +303,9 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     warm += (-warm) % P  # capture at a multiple of P: phase j <-> buffer j % NB, ring j % R
     for _ in range(warm):
         iterate()
-    if flat and os.environ.get("PSAMD_NATIVE_ITER", "1") != "0":
+    # (off by default: on torch's HIP runtime a raw hipEventRecord of a torch event from
+    # the native list failed after the first round of phases, gpurun_out r4d)
+    if flat and os.environ.get("PSAMD_NATIVE_ITER", "0") != "0":
         # 1 GPU, flat: one iteration (both streams' event waits, the step's launches, the
         # next preparation's launches, the records) is ONE native launch-list call; phase
         # j = t % NB: step t on buffer j (its pull was issued by step t-1) pulling
