@@ -754,6 +754,15 @@ PYBIND11_MODULE(_hipops, m) {
   });
   // a zeroed FINE-GRAINED device buffer (cross-device coherent while kernels run; IPC
   // exportable) as a uint8 tensor that frees itself
+  // raw HIP events for native launch lists (handle as an integer; the caller destroys it)
+  m.def("event_create", []() {
+    hipEvent_t e = nullptr;
+    PSAMD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return reinterpret_cast<uint64_t>(e);
+  });
+  m.def("event_destroy", [](uint64_t e) {
+    if (e) PSAMD_HIP_CHECK(hipEventDestroy(reinterpret_cast<hipEvent_t>(e)));
+  });
   m.def("fine_empty", [](int64_t nbytes) {
     check(nbytes > 0, "fine_empty: nbytes > 0");
     int dev = 0;
