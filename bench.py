@@ -303,9 +303,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     warm += (-warm) % P  # capture at a multiple of P: phase j <-> buffer j % NB, ring j % R
     for _ in range(warm):
         iterate()
-    # (off by default: on torch's HIP runtime a raw hipEventRecord of a torch event from
-    # the native list failed after the first round of phases, gpurun_out r4d)
-    if flat and os.environ.get("PSAMD_NATIVE_ITER", "0") != "0":
+    if flat and os.environ.get("PSAMD_NATIVE_ITER", "1") != "0":
         # 1 GPU, flat: one iteration (both streams' event waits, the step's launches, the
         # next preparation's launches, the records) is ONE native launch-list call; phase
         # j = t % NB: step t on buffer j (its pull was issued by step t-1) pulling
@@ -320,15 +318,15 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             s = sides[nb % nprep]
             splan, _ = tr.flat_plan(locs[cur], bufs[cur][1], B, 39, locs[nxt], True)
             L = H.LaunchList()
-            L.add_stream(main.cuda_stream)
-            L.add_wait(ev_prep[cur].cuda_event)
-            L.add_wait(ev_prep[nxt].cuda_event)
+            L.add_stream(main)
+            L.add_wait(ev_prep[cur])
+            L.add_wait(ev_prep[nxt])
             L.extend(splan)
-            L.add_record(ev_buf[cur].cuda_event)
-            L.add_stream(s.cuda_stream)
-            L.add_wait(ev_buf[nb].cuda_event)
+            L.add_record(ev_buf[cur])
+            L.add_stream(s)
+            L.add_wait(ev_buf[nb])
             L.extend(fplans[nb].plan)
-            L.add_record(ev_prep[nb].cuda_event)
+            L.add_record(ev_prep[nb])
             phases.append((L.run, locs[nxt], fplans[nb].done))
 
         def iterate_native():

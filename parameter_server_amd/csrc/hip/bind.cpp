@@ -320,6 +320,7 @@ using Op = std::function<void(hipStream_t&)>;
 struct LaunchList {
   std::vector<Op> ops;
   std::vector<const char*> names;  // per op (a failing op is named in the error)
+  std::vector<py::object> keep;    // the torch streams / events the control ops use
   void push(Launch l, const char* name) {
     ops.push_back([l](hipStream_t& s) { l(s); });
     names.push_back(name);
@@ -581,6 +582,13 @@ optional<TpfBufs> tpf_bufs(const optional<py::tuple>& t) {
   check(t->size() == 5, "flat buffers: (cnt, uniqf, ent_pos, ent_j, slot_u)");
   return TpfBufs{(*t)[0].cast<Tensor>(), (*t)[1].cast<Tensor>(), (*t)[2].cast<Tensor>(),
                  (*t)[3].cast<Tensor>(), (*t)[4].cast<Tensor>()};
+}
+
+hipEvent_t list_event(const py::object& ev, const char* what) {
+  const uint64_t v = py::isinstance<py::int_>(ev) ? ev.cast<uint64_t>()
+                                                  : ev.attr("cuda_event").cast<uint64_t>();
+  check(v != 0, std::string(what) + ": event not created yet (record it once first)");
+  return reinterpret_cast<hipEvent_t>(v);
 }
 
 }  // namespace
@@ -1034,26 +1042,33 @@ PYBIND11_MODULE(_hipops, m) {
         l.push(make_criteo_gen(seed, row0, row_step, B, num_features, alpha, keys,
                                         labels), "criteo_gen");
       })
-      // control ops: raw handles of torch.cuda.Stream.cuda_stream / Event.cuda_event (the
-      // caller keeps those objects alive and has created the events, e.g. by a record)
-      .def("add_stream", [](LaunchList& l, uint64_t stream) {
-        const hipStream_t h = reinterpret_cast<hipStream_t>(stream);
+      // control ops: a torch.cuda.Stream / torch.cuda.Event (the list keeps a reference:
+      // a torch Event destroys its HIP event with the object, and a raw handle left in a
+      // list then fails on the next run) or a raw handle the caller owns (event_create).
+      // Events must exist already (torch creates them lazily: record once first).
+      .def("add_stream", [](LaunchList& l, py::object stream) {
+        const uint64_t v = py::isinstance<py::int_>(stream)
+                               ? stream.cast<uint64_t>()
+                               : stream.attr("cuda_stream").cast<uint64_t>();
+        const hipStream_t h = reinterpret_cast<hipStream_t>(v);
+        l.keep.push_back(stream);
         l.push_op([h](hipStream_t& s) { s = h; }, "stream");
       })
-      .def("add_wait", [](LaunchList& l, uint64_t event) {
-        check(event != 0, "add_wait: event not created yet (record it once first)");
-        const hipEvent_t e = reinterpret_cast<hipEvent_t>(event);
+      .def("add_wait", [](LaunchList& l, py::object event) {
+        const hipEvent_t e = list_event(event, "add_wait");
+        l.keep.push_back(event);
         l.push_op([e](hipStream_t& s) { PSAMD_HIP_CHECK(hipStreamWaitEvent(s, e, 0)); }, "wait");
       })
-      .def("add_record", [](LaunchList& l, uint64_t event) {
-        check(event != 0, "add_record: event not created yet (record it once first)");
-        const hipEvent_t e = reinterpret_cast<hipEvent_t>(event);
+      .def("add_record", [](LaunchList& l, py::object event) {
+        const hipEvent_t e = list_event(event, "add_record");
+        l.keep.push_back(event);
         l.push_op([e](hipStream_t& s) { PSAMD_HIP_CHECK(hipEventRecord(e, s)); }, "record");
       })
       // the ops of another list, SHARED (a generator's row cursor advances for both)
       .def("extend", [](LaunchList& l, const LaunchList& o) {
         l.ops.insert(l.ops.end(), o.ops.begin(), o.ops.end());
         l.names.insert(l.names.end(), o.names.begin(), o.names.end());
+        l.keep.insert(l.keep.end(), o.keep.begin(), o.keep.end());
       })
       .def("__len__", [](const LaunchList& l) { return l.ops.size(); })
       .def("run", [](const LaunchList& l) {

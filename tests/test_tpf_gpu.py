@@ -315,16 +315,17 @@ def test_launch_list_control_ops_order_two_streams():
     g1.add_criteo_gen(5, 0, 2 * B, B, 10 ** 9, 1.1, k1, l1)
     g2.add_criteo_gen(5, B, 2 * B, B, 10 ** 9, 1.1, k2, l2)
     L = H.LaunchList()
-    L.add_stream(s1.cuda_stream)
+    L.add_stream(s1)
     L.extend(g1)
-    L.add_record(ev.cuda_event)
-    L.add_stream(s2.cuda_stream)
-    L.add_wait(ev.cuda_event)
+    L.add_record(ev)
+    L.add_stream(s2)
+    L.add_wait(ev)
     L.extend(g2)
-    L.add_record(ev.cuda_event)
-    L.add_stream(torch.cuda.current_stream(DEV).cuda_stream)
-    L.add_wait(ev.cuda_event)
+    L.add_record(ev)
+    L.add_stream(torch.cuda.current_stream(DEV).cuda_stream)  # (raw handle)
+    L.add_wait(ev)
     assert len(L) == 9
+    del ev, s1, s2  # the list keeps the torch event and streams alive
     for r in range(2):
         L.run()
         torch.cuda.current_stream(DEV).synchronize()
