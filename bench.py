@@ -797,6 +797,11 @@ def main():
             print(f"step {i + 1}", file=sys.stderr)
     t_issue = time.perf_counter() - t0  # host time to enqueue the K steps (CPU-bound check)
     watch.beat("timed-drain")
+    if getattr(tr, "px", None) is not None:
+        # p2p: apply every push every rank posted (collective, host channel) before the
+        # device sync: a post still waiting for a peer's ring space completes only as the
+        # peer drains (part of the timed work)
+        tr.flush()
     if gpu:
         torch.cuda.synchronize()
     t_main = time.perf_counter() - t0

@@ -1045,6 +1045,7 @@ class SparseLRTrainer:
         C, kw, H = xc.C, xc.kw, xc.H
         B = labels.numel()
         width = width or self.cfg.max_nnz_per_example
+        self.px.wait_own()  # (the previous own-row update has read send / slot / gstage)
         hh.owner_split(loc.uniq, loc.n_uniq, self.part.bounds_on(self.device), xc.off)
         hh.xchg_pack_keys(loc.uniq, loc.n_uniq, xc.off, C, kw, H, xc.send, xc.ovf)
         if xc.nb:  # (FixingFloat: no pack_grads launch to publish the overflow flag)
@@ -1070,8 +1071,8 @@ class SparseLRTrainer:
                                hist=self.hist, metrics=self.metrics, step_counter=self.step_dev,
                                ovf=xc.ovf, ovf_host=xc.ovf_host)
             g_own = xc.send.view(torch.float32)[r * H + 4 + C * kw:r * H + 4 + C * kw + C]
-        hh.kv_update(self.table.slots, xc.slot[r * C:(r + 1) * C], g_own,
-                     xc.send[r * H + 1:r * H + 2], *self.rule.args(), self.stats)
+        self.px.own_update(xc.slot[r * C:(r + 1) * C], g_own, xc.send[r * H + 1:r * H + 2],
+                           self.rule, self.stats)
         self.px.post(xc.send)
         self.px.check_fatal()
         self.px.apply(self.rule, self.stats, xc.a_slot, xc.a_w, xc.link, xc.nxt,

@@ -30,7 +30,10 @@ allocations, for A/B). A push that gives up waiting for ring space is fatal at o
 the post publishes the error word into pinned host memory and ``check_fatal`` raises
 (its sequence number is consumed, so that owner would otherwise wait for it forever).
 Host-side bookkeeping (handle exchange, drain counts) goes over a gloo group, never
-through a device-synchronising RCCL object collective.
+through a device-synchronising RCCL object collective. The owner side (the own row's
+update and the inbox applies) runs on a stream of its own, so a rank whose post waits
+for a peer's ring space still applies that peer's posts: two ranks with full rings
+toward each other cannot block each other.
 
 Validated on one MI355X with several processes sharing the GPU (real IPC mappings,
 the same kernels); the xGMI path itself needs a multi-GPU node.
@@ -81,6 +84,11 @@ class PeerExchange:
         self.err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self.total = torch.zeros(1, dtype=torch.int64, device=dev)  # entries applied
         self.seq = 0                                  # pushes posted by this rank
+        # the owner side runs on its own stream: a post spinning for ring space on a peer
+        # never blocks this rank's applies (which free the peer's posts to it), so two
+        # ranks waiting on each other's rings always make progress
+        self.astream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self.ev_own = torch.cuda.Event() if dev.type == "cuda" else None
         hh = hipops()
         cap = table.capacity
         lg = (cap - 1).bit_length()
@@ -134,8 +142,32 @@ class PeerExchange:
                 f"p2p exchange: a push waited {self.spin / 1e6:g} s for an owner's inbox space "
                 f"and gave up (that owner stopped applying); its gradients are lost")
 
+    def own_update(self, slot, grad, count, rule, stats):
+        """This rank's own row of a step (resolved slots, gradients, live count) applied
+        on the owner stream, after the current stream's work so far; ``ev_own`` marks
+        its end (the next step's packs wait for it before reusing the buffers)."""
+        if self.astream is None:
+            hipops().kv_update(self.table.slots, slot, grad, count, *rule.args(), stats)
+            return
+        self.astream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.astream):
+            hipops().kv_update(self.table.slots, slot, grad, count, *rule.args(), stats)
+            self.ev_own.record(self.astream)
+
+    def wait_own(self):
+        """Order the current stream after the last ``own_update``."""
+        if self.ev_own is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.ev_own)
+
     def apply(self, rule, stats, slots_scratch, wscratch, link, nxt, rounds: int = 1):
-        """Owner: apply up to ``rounds`` ready inbox entries per source."""
+        """Owner: apply up to ``rounds`` ready inbox entries per source (on the owner
+        stream: independent of this rank's own posts)."""
+        if self.astream is None:
+            return self._apply(rule, stats, slots_scratch, wscratch, link, nxt, rounds)
+        with torch.cuda.stream(self.astream):
+            self._apply(rule, stats, slots_scratch, wscratch, link, nxt, rounds)
+
+    def _apply(self, rule, stats, slots_scratch, wscratch, link, nxt, rounds: int = 1):
         hh, tb = hipops(), self.table
         G, H, C = self.G, self.H, self.C
         it, iv, isd, seed = tb.init.args()
@@ -172,14 +204,19 @@ class PeerExchange:
         want[self.rank] = 0
         t0 = time.time()
         while True:
-            got = self.applied.cpu()
+            if self.astream is not None:  # (never behind this rank's own spinning posts)
+                self.astream.synchronize()
+                with torch.cuda.stream(self.astream):
+                    got = self.applied.cpu()
+            else:
+                got = self.applied.cpu()
             got[self.rank] = 0
             if bool((got >= want).all()):
                 break
             if time.time() - t0 > timeout:
                 raise RuntimeError(f"p2p drain: applied {got.tolist()} of {want.tolist()}")
             self.apply(rule, stats, slots_scratch, wscratch, link, nxt)
-            torch.cuda.synchronize(self.device)
+        torch.cuda.synchronize(self.device)
         self.check()
         self.comm.barrier()
 
