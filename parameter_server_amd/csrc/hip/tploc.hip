@@ -1657,6 +1657,237 @@ tpf_step_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __r
   }
 }
 
+// Overlapped form of tpf_step_kernel (the default): the dependent global-load chains of
+// the step run together instead of one after another. tpf_step_kernel walks unit 0's
+// update, unit 1's update, unit 0's pull, unit 1's pull, each a chain of dependent
+// loads (entry -> partial; key -> slot record; key -> hash probe) behind barriers: ~12
+// load latencies per workgroup, with ~114 keys and ~500 entries per unit too little
+// work to hide them (19 us per half, profiles/r4_flat_ab.log). Here both units are one
+// flat index space and, before the first barrier, every thread issues its A entries'
+// partial loads, its A keys' slot records and its B keys' hash probes (lookup-or-insert:
+// the slot a key resolves to does not depend on A's update), so the chain is about
+// four latencies: prefetch | LDS fixed-point sums | update + store | re-read of the
+// weights of B keys that existed (A may have updated them) | scatter. The pulled
+// weights reuse the accumulators' LDS. Same results as tpf_step_kernel (same
+// per-unit scales, same fixed-point sums, same per-key update).
+namespace tpf2 {
+constexpr int kRE = 8;   // A entries held in registers per thread (2048 per workgroup)
+constexpr int kRS = 2;   // A slot records held in registers per thread (512 keys)
+constexpr int kRP = 4;   // B probes held in registers per thread (1024 keys)
+constexpr int kRB = 8;   // B entries held in registers per thread
+}  // namespace tpf2
+
+__global__ void __launch_bounds__(tpf::kThr)
+tpf_step2_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __restrict__ posA,
+                 const uint16_t* __restrict__ jA, const uint32_t* __restrict__ slotA,
+                 const float* __restrict__ psum, int64_t p_cap, int do_res,
+                 const int32_t* __restrict__ cntB, const uint64_t* __restrict__ uniqB,
+                 const int32_t* __restrict__ posB, const uint16_t* __restrict__ jB,
+                 uint32_t* __restrict__ slotB, float* __restrict__ w_ent, int64_t w_cap,
+                 Slot* __restrict__ slots, uint64_t mask, uint64_t home_base, uint64_t home_m,
+                 int home_shr, int init_type, float init_v, float init_s, uint64_t seed,
+                 int32_t* __restrict__ err, int32_t* __restrict__ inserted, UpdateParams p,
+                 double* __restrict__ stats, int acc_stripes, uint32_t* __restrict__ hist,
+                 int nbins, int hist_stripes, double* __restrict__ metrics,
+                 int64_t* __restrict__ step_counter) {
+  using namespace tpf;
+  using namespace tpf2;
+  __shared__ long long acc[2 * kUnitK];  // fixed-point sums of both units; then B weights
+  __shared__ uint32_t smax[2];
+  float* wj = reinterpret_cast<float*>(acc);
+  const int t = threadIdx.x, b = blockIdx.x, lane = t & 63;
+  if (do_upd && hist && b == 0) auc_hist_block(hist, nbins, hist_stripes, metrics, step_counter);
+  // per-unit counts (clamped to the regions: a corrupted count never leaves them)
+  int DA0 = 0, DA1 = 0, EA0 = 0, EA = 0, DB0 = 0, DB1 = 0, EB0 = 0, EB = 0;
+  if (do_upd) {
+    const int32_t* c = cntA + (int64_t)b * 4;
+    EA0 = min(max(c[1], 0), kEC);
+    DA0 = max(min(c[0], kUnitK), 0);
+    DA1 = max(min(c[2], kUnitK), 0);
+    EA = EA0 + max(min(c[3], kEC - EA0), 0);
+  }
+  if (do_res) {
+    const int32_t* c = cntB + (int64_t)b * 4;
+    EB0 = min(max(c[1], 0), kEC);
+    DB0 = max(min(c[0], kUnitK), 0);
+    DB1 = max(min(c[2], kUnitK), 0);
+    EB = EB0 + max(min(c[3], kEC - EB0), 0);
+  }
+  const int DA = DA0 + DA1, DB = DB0 + DB1;
+  const int64_t ebase = (int64_t)b * kEC, kbase = (int64_t)b * kUC;
+  // key q of the flat index space -> its slot in the key region (unit 1 after unit 0)
+  auto kreg = [&](int q, int D0) -> int64_t {
+    return kbase + (q < D0 ? q : kUnitK + (q - D0));
+  };
+  auto kacc = [&](int q, int D0) -> int { return q < D0 ? q : kUnitK + (q - D0); };
+  // ---- prefetch: A entries' partials, A keys' slot records, B keys' probes, B entries
+  float v[kRE];
+  uint16_t ja[kRE];
+  float vmax0 = 0.f, vmax1 = 0.f;
+#pragma unroll
+  for (int r = 0; r < kRE; ++r) {
+    const int g = r * kThr + t;
+    v[r] = 0.f;
+    ja[r] = 0;
+    if (g < EA) {
+      const int32_t pos = posA[ebase + g];
+      ja[r] = jA[ebase + g];
+      v[r] = in_range(pos, p_cap) ? psum[pos] : 0.f;
+    }
+  }
+  uint32_t sa[kRS];
+  Slot sl[kRS];
+#pragma unroll
+  for (int i = 0; i < kRS; ++i) {
+    const int q = i * kThr + t;
+    sa[i] = kNoSlot;
+    if (q < DA) {
+      const uint32_t si = slotA[kreg(q, DA0)];
+      if (si != kNoSlot && si <= mask) {
+        sa[i] = si;
+        sl[i] = slots[si];
+      }
+    }
+  }
+  uint32_t sb[kRP];
+  float wb[kRP];
+  bool fresh[kRP];
+  int ins = 0;
+#pragma unroll
+  for (int i = 0; i < kRP; ++i) {
+    const int q = i * kThr + t;
+    sb[i] = kNoSlot;
+    wb[i] = 0.f;
+    fresh[i] = false;
+    if (q < DB) {
+      const int ins0 = ins;
+      sb[i] = tpf_resolve(slots, mask, home_base, home_m, home_shr, uniqB[kreg(q, DB0)],
+                          init_type, init_v, init_s, seed, &wb[i], &ins);
+      fresh[i] = ins != ins0;  // inserted now: not in A, its weight is final
+      if (sb[i] == kNoSlot && err) atomicOr(err, 1);  // table full
+      slotB[kreg(q, DB0)] = sb[i];
+    }
+  }
+  int32_t pb[kRB];
+  uint16_t jb[kRB];
+#pragma unroll
+  for (int r = 0; r < kRB; ++r) {
+    const int g = r * kThr + t;
+    pb[r] = -1;
+    jb[r] = 0;
+    if (g < EB) {
+      pb[r] = posB[ebase + g];
+      jb[r] = jB[ebase + g];
+    }
+  }
+  double dnnz = 0, wsum = 0, dsum = 0;
+  if (do_upd) {
+    for (int q = t; q < DA; q += kThr) acc[kacc(q, DA0)] = 0ll;
+    if (t < 2) smax[t] = 0u;
+#pragma unroll
+    for (int r = 0; r < kRE; ++r) {
+      const int g = r * kThr + t;
+      if (g < EA0) vmax0 = fmaxf(vmax0, fabsf(v[r]));
+      else vmax1 = fmaxf(vmax1, fabsf(v[r]));
+    }
+    for (int g = kRE * kThr + t; g < EA; g += kThr) {  // (rare: > 2048 entries)
+      const int32_t pos = posA[ebase + g];
+      const float x = in_range(pos, p_cap) ? fabsf(psum[pos]) : 0.f;
+      if (g < EA0) vmax0 = fmaxf(vmax0, x);
+      else vmax1 = fmaxf(vmax1, x);
+    }
+    __syncthreads();  // acc / smax zeroed
+    fx_tile_max(vmax0, &smax[0]);
+    fx_tile_max(vmax1, &smax[1]);
+    __syncthreads();
+    const int k20 = fx_shift(smax[0]), k21 = fx_shift(smax[1]);
+    const double sc0 = ldexp(1.0, k20), sc1 = ldexp(1.0, k21);
+#pragma unroll
+    for (int r = 0; r < kRE; ++r) {
+      const int g = r * kThr + t;
+      if (g < EA && v[r] != 0.f && ja[r] < kUnitK) {
+        const bool u1 = g >= EA0;
+        fx_add(acc, (u1 ? kUnitK : 0) + ja[r], v[r], u1 ? sc1 : sc0);
+      }
+    }
+    for (int g = kRE * kThr + t; g < EA; g += kThr) {
+      const int32_t pos = posA[ebase + g];
+      const uint16_t j = jA[ebase + g];
+      const float x = in_range(pos, p_cap) ? psum[pos] : 0.f;
+      const bool u1 = g >= EA0;
+      if (x != 0.f && j < kUnitK) fx_add(acc, (u1 ? kUnitK : 0) + j, x, u1 ? sc1 : sc0);
+    }
+    __syncthreads();
+    const double isc0 = ldexp(1.0, -k20), isc1 = ldexp(1.0, -k21);
+    auto upd = [&](int q, Slot& s_, uint32_t si) {
+      const double isc = q < DA0 ? isc0 : isc1;
+      const float gs = (float)((double)acc[kacc(q, DA0)] * isc) * p.grad_scale;
+      if (gs != gs) return;
+      const float w_old = apply_update(s_, gs, p);
+      slots[si] = s_;
+      dnnz += (double)((s_.w != 0.f) - (w_old != 0.f));
+      wsum += (double)s_.w * s_.w;
+      const double d = (double)s_.w - w_old;
+      dsum += d * d;
+    };
+#pragma unroll
+    for (int i = 0; i < kRS; ++i)
+      if (sa[i] != kNoSlot) upd(i * kThr + t, sl[i], sa[i]);
+    for (int q = kRS * kThr + t; q < DA; q += kThr) {  // (rare: > 512 keys)
+      const uint32_t si = slotA[kreg(q, DA0)];
+      if (si == kNoSlot || si > mask) continue;
+      Slot s_ = slots[si];
+      upd(q, s_, si);
+    }
+    __syncthreads();  // (the updated records are what B re-reads; acc is free for wj)
+  }
+  if (do_res) {
+#pragma unroll
+    for (int i = 0; i < kRP; ++i) {
+      const int q = i * kThr + t;
+      if (q >= DB) continue;
+      float w = wb[i];
+      // a key that existed may have been updated by A just now: its weight again
+      if (do_upd && !fresh[i] && sb[i] != kNoSlot) w = slots[sb[i]].w;
+      wj[kacc(q, DB0)] = w;
+    }
+    for (int q = kRP * kThr + t; q < DB; q += kThr) {  // (rare: > 1024 keys)
+      float w;
+      const uint32_t si = tpf_resolve(slots, mask, home_base, home_m, home_shr,
+                                      uniqB[kreg(q, DB0)], init_type, init_v, init_s, seed, &w,
+                                      &ins);
+      if (si == kNoSlot && err) atomicOr(err, 1);
+      slotB[kreg(q, DB0)] = si;
+      wj[kacc(q, DB0)] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRB; ++r) {
+      const int g = r * kThr + t;
+      if (g < EB && in_range(pb[r], w_cap) && jb[r] < kUnitK)
+        w_ent[pb[r]] = wj[(g >= EB0 ? kUnitK : 0) + jb[r]];
+    }
+    for (int g = kRB * kThr + t; g < EB; g += kThr) {
+      const int32_t pos = posB[ebase + g];
+      const uint16_t j = jB[ebase + g];
+      if (in_range(pos, w_cap) && j < kUnitK) w_ent[pos] = wj[(g >= EB0 ? kUnitK : 0) + j];
+    }
+  }
+  if (do_upd && stats) {
+    const double a = wave_sum_dpp(dnnz), bb = wave_sum_dpp(wsum), cc = wave_sum_dpp(dsum);
+    if (lane == 63) {
+      double* st = acc_stripe(stats, acc_stripes);
+      if (a != 0) atomicAdd(&st[0], a);
+      if (bb != 0) atomicAdd(&st[1], bb);
+      if (cc != 0) atomicAdd(&st[2], cc);
+    }
+  }
+  if (inserted) {
+    const int tot = wave_sum(ins);
+    if (lane == 0 && tot) atomicAdd(inserted, tot);
+  }
+}
+
 // ---- the padded multi-GPU exchange on the flat layout (G peers, G a power of two that
 // divides the bucket workgroups: owner p's key range is exactly the buckets
 // [p * B / G, (p + 1) * B / G), whose keys are rank-sorted (tpf_bucket sorted = 1), so
@@ -2000,11 +2231,19 @@ void tpf_step(int64_t n, int bits, const int32_t* cntA, const int32_t* posA, con
   while ((1ll << lg) < cap) ++lg;
   UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
   const int groups = tpf_groups(n, bits);
-  tpf_step_kernel<<<(unsigned)groups, tpf::kThr, 0, st>>>(
-      cntA != nullptr, cntA, posA, jA, slotA, psum, p_cap, cntB != nullptr, cntB, uniqB, posB, jB,
-      slotB, w_ent, w_cap, (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg,
-      init_type, init_v, init_s, seed, err, inserted, p, stats, acc_stripes,
-      cntA ? hist : nullptr, nbins, hist_stripes, metrics, step_counter);
+  const char* v1_env = getenv("PSAMD_TPF_STEP_V1");  // "1": the sequential form (A/B, tests)
+  if (v1_env && v1_env[0] == '1')
+    tpf_step_kernel<<<(unsigned)groups, tpf::kThr, 0, st>>>(
+        cntA != nullptr, cntA, posA, jA, slotA, psum, p_cap, cntB != nullptr, cntB, uniqB, posB,
+        jB, slotB, w_ent, w_cap, (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg,
+        init_type, init_v, init_s, seed, err, inserted, p, stats, acc_stripes,
+        cntA ? hist : nullptr, nbins, hist_stripes, metrics, step_counter);
+  else
+    tpf_step2_kernel<<<(unsigned)groups, tpf::kThr, 0, st>>>(
+        cntA != nullptr, cntA, posA, jA, slotA, psum, p_cap, cntB != nullptr, cntB, uniqB, posB,
+        jB, slotB, w_ent, w_cap, (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg,
+        init_type, init_v, init_s, seed, err, inserted, p, stats, acc_stripes,
+        cntA ? hist : nullptr, nbins, hist_stripes, metrics, step_counter);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -332,3 +332,48 @@ def test_launch_list_control_ops_order_two_streams():
         for row0, k, lab in ((2 * r * B, k1, l1), ((2 * r + 1) * B, k2, l2)):
             kr, lr = criteo_batch(B, seed=5, row0=row0, num_features=10 ** 9, device=DEV)
             assert torch.equal(k, kr) and torch.equal(lab, lr)
+
+
+@pytest.mark.parametrize("data,init", [("criteo", "zero"), ("uniform", "zero"),
+                                       ("uniform", "gaussian")])
+def test_overlapped_step_kernel_is_bitwise_the_sequential_one(monkeypatch, data, init):
+    """tpf_step2 (both units' load chains issued together, B's probes before A's update,
+    weights of existing B keys re-read after it) leaves the same table, bitwise, as the
+    sequential tpf_step kernel: Criteo-shaped batches, and uniform keys whose workgroups
+    hold > 1024 keys and > 2048 entries (the register batches' fallback loops), with
+    zero and gaussian initial weights."""
+    from parameter_server_amd.ops.kv_table import InitRule
+
+    monkeypatch.setenv("PSAMD_FLAT", "1")
+    B = 8192
+    g = torch.Generator(device=DEV).manual_seed(3)
+    if data == "criteo":
+        batches = [criteo_batch(B, seed=43, row0=t * B, num_features=10 ** 9, device=DEV)
+                   for t in range(5)]
+    else:  # every key of a batch drawn uniformly: mostly distinct, a quarter seen again
+        pool = torch.randint(0, 10 ** 9, (B * 39 * 3,), device=DEV, generator=g)
+        batches = [(pool[torch.randint(0, pool.numel(), (B * 39,), device=DEV, generator=g)],
+                    torch.where(torch.rand(B, device=DEV, generator=g) < 0.5, 1.0, -1.0))
+                   for _ in range(5)]
+    outs = []
+    for v1 in ("1", "0"):
+        monkeypatch.setenv("PSAMD_TPF_STEP_V1", v1)
+        cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, table_capacity=1 << 23,
+                             init=InitRule(init, 0.0, 0.01 if init == "gaussian" else 0.0, 5))
+        tr = SparseLRTrainer(cfg, device=DEV)
+        assert tr.localize_mode == "tpf"
+        loc = tr.localize(batches[0][0], buf=0)
+        for t in range(5):
+            nxt = tr.localize(batches[t + 1][0], buf=(t + 1) % 2) if t < 4 else None
+            tr.step(batches[t][0], batches[t][1], width=39, loc=loc, next_loc=nxt)
+            loc = nxt
+        if data == "uniform":  # the fallback loops ran
+            c = tr._localizers[0].flat.cnt.view(-1, 4)
+            assert int((c[:, 0] + c[:, 2]).max()) > 1024 and int((c[:, 1] + c[:, 3]).max()) > 2048
+        p = tr.progress()
+        k, w, z, n = tr.table.occupied()
+        o = torch.argsort(k)
+        outs.append((p, k[o].cpu(), w[o].cpu(), z[o].cpu(), n[o].cpu()))
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        assert torch.equal(a, b)
+    assert outs[0][0]["nnz_w"] == outs[1][0]["nnz_w"]
