@@ -22,6 +22,22 @@ H = hipops()
 B = 65536
 
 
+def timeit_list(add, it=30):
+    """Device time per op of ``it`` copies of one op in a native launch list (validated
+    once, issued from C++: the host issue cost of a Python binding call stays out)."""
+    L = H.LaunchList()
+    for _ in range(it):
+        add(L)
+    L.run()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    L.run()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it * 1e3
+
+
 def timeit(fn, it=30):
     for _ in range(3):
         fn()
@@ -52,16 +68,23 @@ for lg in (22, 26, 31):
     zero = tuple(torch.zeros_like(x) if i == 0 else x for i, x in enumerate(loc.bufs))
     row = {"table_log2": lg}
     for v1 in ("1", "0"):
-        os.environ["PSAMD_TPF_STEP_V1"] = v1
+        os.environ["PSAMD_TPF_STEP2"] = "0" if v1 == "1" else "1"
         tag = "v1" if v1 == "1" else "v2"
-        row[f"pull_{tag}"] = timeit(lambda: H.tpf_step(n, bits, None, None, loc.bufs, loc.w_ent,
-                                                       *common, None, None, None))
-        row[f"update_{tag}"] = timeit(lambda: H.tpf_step(n, bits, loc.bufs, loc.psum, None, None,
-                                                         *common, None, None, None))
-        row[f"both_{tag}"] = timeit(lambda: H.tpf_step(n, bits, loc.bufs, loc.psum, loc.bufs,
-                                                       loc.w_ent, *common, None, None, None))
-        row[f"empty_{tag}"] = timeit(lambda: H.tpf_step(n, bits, zero, loc.psum, zero, loc.w_ent,
-                                                        *common, None, None, None))
+        row[f"pull_{tag}"] = timeit_list(lambda L: L.add_tpf_step(
+            n, bits, None, None, loc.bufs, loc.w_ent, *common, None, None, None))
+        row[f"update_{tag}"] = timeit_list(lambda L: L.add_tpf_step(
+            n, bits, loc.bufs, loc.psum, None, None, *common, None, None, None))
+        row[f"both_{tag}"] = timeit_list(lambda L: L.add_tpf_step(
+            n, bits, loc.bufs, loc.psum, loc.bufs, loc.w_ent, *common, None, None, None))
+        row[f"empty_{tag}"] = timeit_list(lambda L: L.add_tpf_step(
+            n, bits, zero, loc.psum, zero, loc.w_ent, *common, None, None, None))
+    row["fwd_bwd"] = timeit_list(lambda L: L.add_tp_fwd_bwd(
+        loc.rep, loc.dcnt, None, n, 39, None, loc.w_ent, lab, B, 0, tr.coef[:B], tr.metrics,
+        tr.hist, 2048, loc.psum, None, None, None, None, False))
+    lz = tr._localizers[0]
+    f = lz.flat
+    row["localize_tpf"] = timeit_list(lambda L: L.add_localize_tpf(
+        k, n, bits, lz.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos, f.ent_j, f.cnt, f.err, False))
     uk = loc.unique_keys().to(dev)
     row["distinct_keys"] = int(uk.numel())
     row["kv_resolve_same_keys"] = timeit(lambda: tb.resolve(uk, insert=False, with_w=True))

@@ -1657,7 +1657,8 @@ tpf_step_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __r
   }
 }
 
-// Overlapped form of tpf_step_kernel (the default): the dependent global-load chains of
+// Overlapped form of tpf_step_kernel (opt-in, PSAMD_TPF_STEP2=1: measured SLOWER, see
+// tpf_step below; the chain-latency model that motivated it did not hold): the dependent global-load chains of
 // the step run together instead of one after another. tpf_step_kernel walks unit 0's
 // update, unit 1's update, unit 0's pull, unit 1's pull, each a chain of dependent
 // loads (entry -> partial; key -> slot record; key -> hash probe) behind barriers: ~12
@@ -2231,8 +2232,10 @@ void tpf_step(int64_t n, int bits, const int32_t* cntA, const int32_t* posA, con
   while ((1ll << lg) < cap) ++lg;
   UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
   const int groups = tpf_groups(n, bits);
-  const char* v1_env = getenv("PSAMD_TPF_STEP_V1");  // "1": the sequential form (A/B, tests)
-  if (v1_env && v1_env[0] == '1')
+  // PSAMD_TPF_STEP2=1: the overlapped form (measured slower: 28.7-30.2 vs 24.9-25.4 us per
+  // update + pull launch, profiles/r4_tpf_step_probe.log; kept for A/B and its test)
+  const char* v2_env = getenv("PSAMD_TPF_STEP2");
+  if (!(v2_env && v2_env[0] == '1'))
     tpf_step_kernel<<<(unsigned)groups, tpf::kThr, 0, st>>>(
         cntA != nullptr, cntA, posA, jA, slotA, psum, p_cap, cntB != nullptr, cntB, uniqB, posB,
         jB, slotB, w_ent, w_cap, (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg,

@@ -357,7 +357,7 @@ def test_overlapped_step_kernel_is_bitwise_the_sequential_one(monkeypatch, data,
                    for _ in range(5)]
     outs = []
     for v1 in ("1", "0"):
-        monkeypatch.setenv("PSAMD_TPF_STEP_V1", v1)
+        monkeypatch.setenv("PSAMD_TPF_STEP2", "0" if v1 == "1" else "1")
         cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, table_capacity=1 << 23,
                              init=InitRule(init, 0.0, 0.01 if init == "gaussian" else 0.0, 5))
         tr = SparseLRTrainer(cfg, device=DEV)
