@@ -303,7 +303,10 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     warm += (-warm) % P  # capture at a multiple of P: phase j <-> buffer j % NB, ring j % R
     for _ in range(warm):
         iterate()
-    if flat and os.environ.get("PSAMD_NATIVE_ITER", "1") != "0":
+    # auto: on for large minibatches (B = 65,536: 0.0966-0.1007 -> 0.0949-0.0957 ms); at
+    # B = 10,000 the GPU step took 0.050 vs 0.042 ms eagerly (profiles/r4_native_iter.log)
+    native = os.environ.get("PSAMD_NATIVE_ITER", "auto")
+    if flat and (native == "1" or (native == "auto" and B >= 32768)):
         # 1 GPU, flat: one iteration (both streams' event waits, the step's launches, the
         # next preparation's launches, the records) is ONE native launch-list call; phase
         # j = t % NB: step t on buffer j (its pull was issued by step t-1) pulling
