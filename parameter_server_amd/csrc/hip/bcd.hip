@@ -548,7 +548,7 @@ __device__ __forceinline__ double rp_exp(double x) {
   return kF32 ? (double)__expf(fminf((float)x, 80.f)) : exp(x);
 }
 
-__device__ __forceinline__ double rp_dual_delta(const RowDual& d, int c, int64_t i, double dwc,
+__device__ __forceinline__ double rp_dual_delta(const RowDual& d, int c, uint32_t i, double dwc,
                                                 double yr) {
   const double x = d.dval ? (double)d.dval[i] : 1.0;
   return yr * dwc * x;  // the bcd_dual_kernel expression: (y * dw) * x
@@ -578,18 +578,20 @@ bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restr
     cact[c] = active[k];
   }
   __syncthreads();
-  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-  const int64_t a = per * blockIdx.x, b = min(n, a + per);
+  // 32-bit example offsets (the host checks n < 2^31): zero-extended VGPR offsets from
+  // the arrays' SGPR bases, no 64-bit address arithmetic per access
+  const uint32_t per = (uint32_t)((n + gridDim.x - 1) / gridDim.x);
+  const uint32_t a = per * blockIdx.x, b = (uint32_t)min<int64_t>(n, (int64_t)a + per);
   long long* my = acc + (int64_t)((t >> 6) % copies) * stride;
   const double sc = ldexp(1.0, k2);
   constexpr int kR = 8;  // examples per thread per round, loads in flight together
-  for (int64_t i0 = a + t; i0 < b; i0 += (int64_t)kR * blockDim.x) {
+  for (uint32_t i0 = a + t; i0 < b; i0 += (uint32_t)kR * blockDim.x) {
     int ck[kR], cj[kR];
     double m[kR];
     float yv[kR];
 #pragma unroll
     for (int q = 0; q < kR; ++q) {
-      const int64_t i = i0 + (int64_t)q * blockDim.x;
+      const uint32_t i = i0 + (uint32_t)q * blockDim.x;
       ck[q] = -1;
       cj[q] = -1;
       m[q] = 0;
@@ -615,7 +617,7 @@ bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restr
 #pragma unroll
       for (int q = 0; q < kR; ++q) {
         if (dwv[q] == 0) continue;
-        const int64_t i = i0 + (int64_t)q * blockDim.x;
+        const uint32_t i = i0 + (uint32_t)q * blockDim.x;
         m[q] += rp_dual_delta(dj, cj[q], i, dwv[q], (double)yv[q]);
         ym[i] = m[q];
       }
@@ -625,7 +627,7 @@ bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restr
       const int c = ck[q];
       if (kHot && c == kColdRow) {  // cold entry: factors for the column-order kernel
         const double tau = rp_tau<kF32>(m[q]);
-        rowq[i0 + (int64_t)q * blockDim.x] = make_double2(-(double)yv[q] * tau, tau * (1.0 - tau));
+        rowq[i0 + (uint32_t)q * blockDim.x] = make_double2(-(double)yv[q] * tau, tau * (1.0 - tau));
         continue;
       }
       if (c < 0 || !cact[c]) continue;
@@ -634,7 +636,7 @@ bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restr
       const double t2 = tau * (1.0 - tau);
       double g, u;
       if (dval) {
-        const double v = (double)dval[i0 + (int64_t)q * blockDim.x];
+        const double v = (double)dval[i0 + (uint32_t)q * blockDim.x];
         g = -yr * tau * v;
         u = fmin(t2 * rp_exp<kF32>(fabs(v) * cdl[c]), 0.25) * v * v;
       } else {
@@ -661,15 +663,15 @@ __global__ void __launch_bounds__(256)
 bcd_rowpass_q_kernel(int64_t n, double* __restrict__ ym, const float* __restrict__ y, RowDual dj,
                      const int32_t* __restrict__ dcol, int ncols, double2* __restrict__ rowq) {
   constexpr int kR = 8;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n;
-       i0 += (int64_t)kR * stride) {
+  const uint32_t stride = gridDim.x * blockDim.x;  // (n < 2^31: 32-bit offsets)
+  for (uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < (uint64_t)n;
+       i0 += (uint32_t)kR * stride) {
     int ck[kR], cj[kR];
     double m[kR];
     float yv[kR];
 #pragma unroll
     for (int q = 0; q < kR; ++q) {
-      const int64_t i = i0 + q * stride;
+      const uint32_t i = i0 + q * stride;
       ck[q] = -1;
       cj[q] = -1;
       m[q] = 0;
@@ -688,7 +690,7 @@ bcd_rowpass_q_kernel(int64_t n, double* __restrict__ ym, const float* __restrict
     double dwv[kR];
 #pragma unroll
     for (int q = 0; q < kR; ++q) {  // (margin loads beside the dw gather, not behind it)
-      const int64_t i = i0 + q * stride;
+      const uint32_t i = i0 + q * stride;
       if (ck[q] >= 0 || cj[q] >= 0) {
         m[q] = ym[i];
         yv[q] = y[i];
@@ -697,7 +699,7 @@ bcd_rowpass_q_kernel(int64_t n, double* __restrict__ ym, const float* __restrict
     }
 #pragma unroll
     for (int q = 0; q < kR; ++q) {
-      const int64_t i = i0 + q * stride;
+      const uint32_t i = i0 + q * stride;
       if (kDual && dwv[q] != 0) {
         m[q] += rp_dual_delta(dj, cj[q], i, dwv[q], (double)yv[q]);
         ym[i] = m[q];
@@ -892,6 +894,7 @@ void bcd_rowpass(int64_t n, double* ym, const float* y, const int32_t* jcol, con
                  const int32_t* hcols, int64_t nhot, long long* part2_out, bool tau32,
                  hipStream_t st) {
   if (n <= 0) return;
+  if (n >= ((int64_t)1 << 31)) throw std::runtime_error("bcd_rowpass: >= 2^31 examples per rank");
   const RowDual dj{jcol, jval, jdw, (int)jncols};
   if (part) {  // gradient of block k in LDS: narrow (all columns) or wide (hot columns)
     const int nl = (int)(hcols ? nhot : ncols);  // LDS column slots
