@@ -67,16 +67,32 @@ def gemm(A, a_kmajor: bool, B, b_kmajor: bool, M: int, N: int, K: int, *, bias=N
 
 
 # Layer products on the GPU: "mfma" = the hand-written kernels (forward products with
-# K % 64 == 0 and N >= 256 on the 256x256 LDS-DMA kernel of gemm256.hip, the rest on
-# the 128x128 kernel above with fused epilogues); "hipblaslt" = the vendor library GEMM (torch.mm / addmm with its own
-# bias + ReLU epilogue) + separate elementwise kernels; "auto" = per product, the
-# faster of the two as measured on MI355X (benchmarks/bench_gemm.py --wd-backends,
-# B = 16384): the library for the plain long-K products (forward with K >= 1024:
-# 134 vs 250 us at 4992 -> 1024, 23 vs 31 us at 1024 -> 512; the unmasked input
-# gradient: 172 vs 270 us), the own kernel where its fused epilogue saves passes
-# (masked input gradient + bias-gradient column sums, short-K forward 14 vs 19 us)
-# and for every weight gradient (split-K: 285 vs 311, 53 vs 102, 42 vs 96 us).
+# K % 64 == 0 and N >= 256 on the 256x256 LDS-DMA kernels of gemm256.hip, the rest on
+# the 128x128 kernel above with fused epilogues); "hipblaslt" = the vendor library GEMM
+# (torch.mm / addmm with its own bias + ReLU epilogue) + separate elementwise kernels;
+# "auto" = per product, the faster of the two as measured on MI355X
+# (benchmarks/bench_gemm256.py, B = 16384, uniform random bf16,
+# profiles/r4_gemm256_ring.log): the library for the plain long-K products -- the
+# layer-0 forward (K = 4992: 1441 vs 1270 TFLOP/s for the best own variant) and the
+# unmasked input gradient (1125 vs 803) -- and the own kernels where their fused
+# epilogues save passes (masked input gradient + bias-gradient column sums, the short-K
+# forwards with their fused bias + ReLU: 1024 -> 512 604 own (128x128) vs 644 library,
+# 512 -> 256 312 vs 222) and for every weight gradient (TN 256x256 split-K: 668 vs 542,
+# 362 vs 167, 127 vs 45 TFLOP/s).
 BACKENDS = ("mfma", "hipblaslt", "auto")
+
+
+def _nt256_variant(K: int) -> int:
+    """gemm256.hip NT variant: the 4-slot LDS ring (4) on the wide & deep products (K up
+    to a few thousand: 1270 vs 1156 TFLOP/s at K = 4992, 803 vs 784 at K = 1024), the
+    one-barrier kernel (0) on very long K (8192^3: 1154 vs 937), profiles/r4_gemm256_ring.log;
+    PSAMD_GEMM_NT256 forces one."""
+    import os
+
+    v = os.environ.get("PSAMD_GEMM_NT256")
+    if v is not None:
+        return int(v)
+    return 4 if K <= 6144 else 0
 _addmm_act = getattr(torch, "_addmm_activation", None)
 
 
@@ -102,7 +118,7 @@ def linear_forward(X, W, bias=None, relu=False, backend: str = "mfma", bias16=No
         # 739 TFLOP/s for the 128x128 kernel on 16384 x 1024 x 4992; with fewer tiles
         # (16384 x 512) the 128x128 kernel wins (profiles/r2_gemm256.log)
         Z = torch.empty(Bn, N, dtype=torch.bfloat16, device=X.device)
-        hipops().gemm_nt256(X, W, Bn, N, K, bias, relu, Z, None)
+        hipops().gemm_nt256(X, W, Bn, N, K, bias, relu, Z, None, _nt256_variant(K))
         return Z
     return gemm(X, True, W, True, Bn, N, K, bias=bias, relu=relu)
 
@@ -132,7 +148,7 @@ def linear_input_grad(dZ, W, mask=None, backend: str = "mfma", colsum=None):
         else:
             Wt = W.t().contiguous()
         dX = torch.empty(Bn, K, dtype=torch.bfloat16, device=dZ.device)
-        hipops().gemm_nt256(dZ, Wt, Bn, K, N, None, False, dX, None)
+        hipops().gemm_nt256(dZ, Wt, Bn, K, N, None, False, dX, None, _nt256_variant(N))
         return dX
     return gemm(dZ, True, W, False, Bn, K, N, mask=mask, colsum=colsum)
 
