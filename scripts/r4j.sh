@@ -19,3 +19,6 @@ for g in auto mfma; do
   step timeout -k 10 300 python benchmarks/bench_wide_deep.py --gemm $g > $O/wd_$g.log 2>&1
   step env PSAMD_GEMM_NT256=0 timeout -k 10 300 python benchmarks/bench_wide_deep.py --gemm $g > $O/wd_${g}_v0.log 2>&1
 done
+step env PSAMD_NATIVE_ITER=1 timeout -k 10 120 python bench.py --steps 300 --warmup 10 --minibatch 10000 --prep-streams 1 > $O/b10k_native_p1.log 2>&1
+step env PSAMD_NATIVE_ITER=0 timeout -k 10 120 python bench.py --steps 300 --warmup 10 --minibatch 10000 --prep-streams 1 > $O/b10k_eager_p1.log 2>&1
+step timeout -k 10 120 python bench.py --steps 300 --warmup 10 --minibatch 10000 --pipeline 0 > $O/b10k_seq.log 2>&1
