@@ -278,19 +278,29 @@ __device__ __forceinline__ uint64_t gen_key(float u, int j, uint64_t num_feature
   return mod_barrett(fmix64(((uint64_t)(j + 1) << 48) ^ id), num_features, nf_m);
 }
 
-// 64 rows per block, one per lane; wave g of the 3 generates slots 13g .. 13g+12 of
-// every row (integer slots in wave 0, categorical in waves 1-2: no divergence), the
-// keys are staged in LDS and leave as one contiguous 64 x 39 x 8 B run, and wave 0
-// sums the three partial planted logits of its row and draws the label.
+// 64 rows per block, one per lane; 6 waves, wave w generating a fixed run of slots of
+// every row (integer slots 0-6 / 7-12 in waves 0-1, categorical 13-19 / 20-25 / 26-32 /
+// 33-38 in waves 2-5: the slot index is wave-uniform, so the integer and power-law
+// branches never diverge). (Round 3 used 3 waves of 13 slots: 12 waves per CU and 13
+// sequential samples per lane, 11 us per 65,536-row minibatch.) Keys and the planted
+// weight of every (row, slot) are staged in LDS; the keys leave as one contiguous
+// 64 x 39 x 8 B run, and lane r of wave 0 sums row r's planted weights in the
+// original order (three sequential 13-slot sums, then -1.2 + s0 + s1 + s2: bitwise the
+// labels of the 3-wave kernel) and draws the label.
 constexpr int kGenRows = 64;
-constexpr int kGenThreads = 192;
+constexpr int kGenThreads = 384;
+__device__ __forceinline__ void gen_slot_range(int w, int& j0, int& j1) {
+  // w = 0..5 -> [0, 7) [7, 13) [13, 20) [20, 26) [26, 33) [33, 39)
+  j0 = (w >> 1) * 13 + (w & 1) * 7;
+  j1 = (w & 1) ? ((w >> 1) + 1) * 13 : j0 + 7;
+}
 template <bool kWide>
 __global__ void __launch_bounds__(kGenThreads)
 criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_dev,
                   int64_t row_scale, int64_t B, uint64_t num_features, uint64_t nf_m,
                   float alpha, uint64_t* __restrict__ keys, float* __restrict__ labels) {
   __shared__ uint64_t sk[kGenRows * 39];
-  __shared__ float spw[3][kGenRows];
+  __shared__ float sp[kGenRows * 39];
   __shared__ float s_cm1[26];
   __shared__ uint32_t s_seed[40];  // per-slot streams + the label stream
   // (an L2-coherent vector load, not a scalar-cache load: the counter is advanced on the
@@ -299,6 +309,8 @@ criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_
     row0 += __hip_atomic_load(row0_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * row_scale;
   const int t = threadIdx.x, lane = t & 63;
   const int g = __builtin_amdgcn_readfirstlane(t >> 6);
+  int j0, j1;
+  gen_slot_range(g, j0, j1);
   const float oma = 1.f - alpha, inv_oma = 1.f / oma;
   if (t < 26) s_cm1[t] = powf((float)c_cards[t], oma) - 1.f;
   if (t < 40)
@@ -308,24 +320,27 @@ criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_
   for (int64_t rb = (int64_t)blockIdx.x * kGenRows; rb < B; rb += (int64_t)gridDim.x * kGenRows) {
     const int64_t r = rb + lane;
     const uint64_t gr = (uint64_t)(row0 + r);
-    float pw = 0.f;
     if (r < B) {
-#pragma unroll
-      for (int jj = 0; jj < 13; ++jj) {
-        const int j = g * 13 + jj;
+      for (int j = j0; j < j1; ++j) {
         const float u = gen_u01(gen_row_bits(gr, s_seed[j]));
         const uint64_t key = gen_key<kWide>(u, j, num_features, nf_m, inv_oma,
                                             j >= 13 ? s_cm1[j - 13] : 0.f);
         sk[lane * 39 + j] = key;
-        pw += gen_planted(key);
+        sp[lane * 39 + j] = gen_planted(key);
       }
     }
-    spw[g][lane] = pw;
     __syncthreads();
     const int nrow = (int)min<int64_t>(kGenRows, B - rb);
     for (int i = t; i < nrow * 39; i += kGenThreads) keys[rb * 39 + i] = sk[i];
     if (g == 0 && r < B) {
-      const float logit = -1.2f + spw[0][lane] + spw[1][lane] + spw[2][lane];
+      float spw[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        float pw = 0.f;
+        for (int jj = 0; jj < 13; ++jj) pw += sp[lane * 39 + q * 13 + jj];
+        spw[q] = pw;
+      }
+      const float logit = -1.2f + spw[0] + spw[1] + spw[2];
       const float p = 1.f / (1.f + __expf(-logit));
       labels[r] = gen_u01(gen_row_bits(gr, s_seed[39])) < p ? 1.f : -1.f;
     }
