@@ -4,7 +4,7 @@ O=gpurun_out/r4j
 mkdir -p $O
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 step() { "$@"; rc=$?; echo "rc=$rc: $*" >> $O/steps.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; }
-step timeout -k 10 400 python -u -m pytest tests/test_darlin_gpu.py -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest_darlin.log 2>&1
+step timeout -k 10 400 python -u -m pytest tests/test_darlin_gpu.py tests/test_gpu_ops.py tests/test_tpf_gpu.py -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest_darlin.log 2>&1
 for t in 1 0; do
   step timeout -k 10 200 python benchmarks/bench_darlin.py --rows 4000000 --passes 5 --device-data --tau32 $t > $O/darlin_t32_$t.log 2>&1
 done
