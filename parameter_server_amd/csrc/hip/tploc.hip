@@ -12,7 +12,7 @@
 //
 //   tile     one 512-thread workgroup per tile of 8192 occurrences: mix, LDS hash
 //            dedup, counting sort of the tile's distinct keys by bucket (top BB key
-//            bits) -> tkeys[tile][pos], per-tile bucket offsets toff[tile][b],
+//            bits) -> tkeys[tile][pos], per-tile bucket offsets toff[b][tile] (bucket-major),
 //            rep[i] = tile entry of occurrence i (u16)
 //   bucket   one workgroup per bucket: gather the bucket's entries from every tile
 //            (a key occurs at most once per tile, so a hot key is <= #tiles entries
@@ -198,18 +198,23 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
   }
   uint32_t D;
   uint32_t run = tp_block_scan<kThr>(s, lds, &D);
-  uint16_t* to = toff + (int64_t)blockIdx.x * (nbk + 1);
+  // toff is BUCKET-major, toff[d][tile] (T = gridDim.x tiles): a bucket workgroup reads
+  // its run offsets of all tiles as coalesced rows instead of one cache line per tile
+  // (~1 k scattered L2 requests per workgroup, issued by all 1024 bucket workgroups at
+  // once: about a third of the bucket kernel, profiles/r3_tp_pair_phases.log toff+scan)
+  const int64_t T = gridDim.x;
+  uint16_t* to = toff + blockIdx.x;
 #pragma unroll
   for (int e = 0; e < kDP; ++e) {
     const int d = t * kDP + e;
     if (d < nbk) {
       cnt[d] = run;
-      to[d] = (uint16_t)run;
+      to[d * T] = (uint16_t)run;
     }
     run += c[e];
   }
   if (t == 0) {
-    to[nbk] = (uint16_t)D;
+    to[nbk * T] = (uint16_t)D;
     dcnt[blockIdx.x] = (int32_t)D;
   }
   __syncthreads();
@@ -305,10 +310,10 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
   const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
   uint32_t c = 0;
   for (int q = q0; q < q1; ++q) {
-    const uint16_t* to = toff + (int64_t)q * (nbf + 1);
-    const uint32_t lo = to[f0], hi = to[f0 + nf];
+    const uint16_t* to = toff + q;  // bucket-major: to[d * T]
+    const uint32_t lo = to[(int64_t)f0 * T], hi = to[(int64_t)(f0 + nf) * T];
     tlo[q] = (uint16_t)lo;
-    tmid[q] = (uint16_t)((nf == 2 ? to[f0 + 1] : hi) - lo);
+    tmid[q] = (uint16_t)((nf == 2 ? to[(int64_t)(f0 + 1) * T] : hi) - lo);
     tpre[q] = hi - lo;
     c += hi - lo;
   }
@@ -588,8 +593,8 @@ __device__ __forceinline__ void tp_bk_fine_light(
   const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
   uint32_t c = 0;
   for (int q = q0; q < q1; ++q) {
-    const uint16_t* to = toff + (int64_t)q * (nbf + 1);
-    const uint32_t lo = to[f], hi = to[f + 1];
+    const uint16_t* to = toff + q;  // bucket-major: to[d * T]
+    const uint32_t lo = to[(int64_t)f * T], hi = to[(int64_t)(f + 1) * T];
     tlo[q] = (uint16_t)lo;
     tpre[q] = hi - lo;
     c += hi - lo;
@@ -1324,8 +1329,8 @@ __device__ __forceinline__ uint32_t tpf_unit_light(
   const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
   uint32_t c = 0;
   for (int q = q0; q < q1; ++q) {
-    const uint16_t* to = toff + (int64_t)q * (nbf + 1);
-    const uint32_t lo = to[f], hi = to[f + 1];
+    const uint16_t* to = toff + q;  // bucket-major: to[d * T]
+    const uint32_t lo = to[(int64_t)f * T], hi = to[(int64_t)(f + 1) * T];
     tlo[q] = (uint16_t)lo;
     tpre[q] = hi - lo;
     c += hi - lo;
