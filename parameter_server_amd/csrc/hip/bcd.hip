@@ -589,27 +589,35 @@ bcd_rowpass_grad_kernel(int64_t n, double* __restrict__ ym, const float* __restr
     int ck[kR], cj[kR];
     double m[kR];
     float yv[kR];
+    // two batches of unconditional loads at clamped in-range indices (a guarded load per
+    // example compiled to a branch + s_waitcnt each: ~kR serialised round trips), then
+    // selects: the column codes, then margins and labels
+    int cr[kR], dr[kR];
 #pragma unroll
     for (int q = 0; q < kR; ++q) {
       const uint32_t i = i0 + (uint32_t)q * blockDim.x;
-      ck[q] = -1;
-      cj[q] = -1;
-      m[q] = 0;
-      yv[q] = 0.f;
-      if (i < b) {
-        const int c = dcol[i];
-        if (kHot) ck[q] = c >= 0 ? kColdRow : (c <= -2 && -2 - c < ncols) ? -2 - c : -1;
-        else ck[q] = (c >= 0 && c < ncols) ? c : -1;
-        if (kDual) {
-          const int d = dj.dcol[i];
-          cj[q] = (d >= 0 && d < dj.ncols) ? d : -1;
-        }
-        if (ck[q] != -1 || cj[q] >= 0) {
-          m[q] = ym[i];
-          yv[q] = y[i];
-        }
-      }
+      const uint32_t ic = i < b ? i : a;
+      cr[q] = dcol[ic];
+      dr[q] = kDual ? dj.dcol[ic] : -1;
     }
+#pragma unroll
+    for (int q = 0; q < kR; ++q) {
+      const uint32_t i = i0 + (uint32_t)q * blockDim.x;
+      const bool in = i < b;
+      const int c = cr[q];
+      if (kHot) ck[q] = !in ? -1 : c >= 0 ? kColdRow : (c <= -2 && -2 - c < ncols) ? -2 - c : -1;
+      else ck[q] = (in && c >= 0 && c < ncols) ? c : -1;
+      cj[q] = (kDual && in && dr[q] >= 0 && dr[q] < dj.ncols) ? dr[q] : -1;
+      const uint32_t im = (ck[q] != -1 || cj[q] >= 0) ? i : a;
+      m[q] = ym[im];
+      yv[q] = y[im];
+    }
+#pragma unroll
+    for (int q = 0; q < kR; ++q)
+      if (!(ck[q] != -1 || cj[q] >= 0)) {
+        m[q] = 0;
+        yv[q] = 0.f;
+      }
     if (kDual) {
       double dwv[kR];
 #pragma unroll

@@ -1151,6 +1151,12 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
   FB_MARK(0);
   uint16_t ce[NP][PER];
   float cv[NP][PER];
+  // every load unconditional (a clamped in-range address, the value dropped by a select
+  // afterwards): a guarded load per element compiled to a branch + s_waitcnt vmcnt(0)
+  // each, i.e. NP * PER serialised global round trips (the prologue was ~half of the
+  // kernel's cycles, profiles/r3_tp_pair_phases.log)
+  bool ok[NP][PER];
+  int64_t ix[NP][PER];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     const int ri = p * kRowsPass + g;
@@ -1158,39 +1164,67 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int k = sub + q * kFbLanes;
-      ce[p][q] = kFbNone;
-      cv[p][q] = 0.f;
-      if (ri < nr && r < B && k < width) {
-        const int64_t i = r * width + k;
-        const int64_t o = i - base;
-        const bool in = o >= 0 && o < lim;
-        const uint16_t e = rep[i];  // outside the tile: the entry in the neighbour tile
-        ce[p][q] = in ? e : kFbExt;
-        cv[p][q] = in ? (vals ? vals[i] : 1.f) : __int_as_float((int)e);
-      }
+      ok[p][q] = ri < nr && r < B && k < width;
+      ix[p][q] = ok[p][q] ? r * width + k : base;
+      ce[p][q] = rep[ix[p][q]];  // outside the tile: the entry in the neighbour tile
+      cv[p][q] = vals ? vals[ix[p][q]] : 1.f;
     }
   }
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int64_t o = ix[p][q] - base;
+      const bool in = o >= 0 && o < lim;
+      const uint16_t e = ce[p][q];
+      ce[p][q] = !ok[p][q] ? kFbNone : in ? e : kFbExt;
+      cv[p][q] = !ok[p][q] ? 0.f : in ? cv[p][q] : __int_as_float((int)e);
+    }
   if (t < 4) sacc[t] = 0.f;
   if (t == 0) smax = 0u;
   // boundary rows: the outside part of row 0 / row nr-1 (only their lane groups) read
   // their weights through the neighbour tile's entry map; issued first, so the chain
   // rep -> ent_uid -> w_local overlaps the tile's own entry-weight loads
+  // (each stage's loads all issued before any of them is used: no per-element wait)
+  {
+    int64_t ue[NP][PER];
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int ri = p * kRowsPass + g;
-    if (ri != 0 && ri != nr - 1) continue;
+    for (int p = 0; p < NP; ++p)
 #pragma unroll
-    for (int q = 0; q < PER; ++q)
-      if (ce[p][q] == kFbExt) {
-        const int64_t i = (r0 + ri) * width + sub + q * kFbLanes;
-        const int64_t ge = (i / kTile) * kTile + __float_as_int(cv[p][q]);
-        const int64_t u = kFlat ? ge : (int64_t)ent_uid[ge];
-        cv[p][q] = (in_range(u, w_cap) ? w_local[u] : 0.f) * (vals ? vals[i] : 1.f);
-      }
+      for (int q = 0; q < PER; ++q)
+        ue[p][q] = ce[p][q] == kFbExt
+                       ? (ix[p][q] / kTile) * kTile + __float_as_int(cv[p][q]) : (int64_t)-1;
+    if (!kFlat) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int q = 0; q < PER; ++q)
+          if (ue[p][q] >= 0) ue[p][q] = (int64_t)ent_uid[ue[p][q]];
+    }
+    float wx[NP][PER];
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int q = 0; q < PER; ++q)
+        if (ce[p][q] == kFbExt && in_range(ue[p][q], w_cap)) wx[p][q] = w_local[ue[p][q]];
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int q = 0; q < PER; ++q)
+        if (ce[p][q] == kFbExt)
+          cv[p][q] = (in_range(ue[p][q], w_cap) ? wx[p][q] : 0.f) *
+                     (vals ? vals[ix[p][q]] : 1.f);
   }
   for (int i = t; i < nr; i += kThr) crow[i] = r0 + i < B ? labels[r0 + i] : 0.f;
-  if (kFlat) {
-    for (int i = t; i < cnt; i += kThr) wl[i] = w_local[base + i];  // (host: w_cap >= T * 8192)
+  if (kFlat) {  // (host: w_cap >= T * 8192) all loads first, then the LDS stores
+    constexpr int kW = kTile / kThr;
+    float wv[kW];
+#pragma unroll
+    for (int k = 0; k < kW; ++k)
+      if (t + k * kThr < cnt) wv[k] = w_local[base + t + k * kThr];
+#pragma unroll
+    for (int k = 0; k < kW; ++k)
+      if (t + k * kThr < cnt) wl[t + k * kThr] = wv[k];
   } else {
     for (int i = t; i < cnt; i += kThr) {
       const int32_t u = ent_uid[base + i];
@@ -1570,17 +1604,25 @@ tpf_step_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __r
       constexpr int kR = 8;  // entries held in registers per thread (<= 2048 per unit)
       float v[kR];
       uint16_t jj[kR];
+      int32_t pos[kR];
       float vmax = 0.f;
+      // two batches of unconditional loads at clamped in-region addresses (a guarded
+      // load per entry compiled to a branch + s_waitcnt each: 2 x kR serialised round
+      // trips), then selects
+      const int64_t rb = (int64_t)b * kEC;  // (always inside the entry region)
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
         const int g = r * kThr + t;
-        v[r] = 0.f;
-        jj[r] = 0;
-        if (g < E) {
-          const int32_t pos = posA[eb + g];
-          jj[r] = jA[eb + g];
-          v[r] = in_range(pos, p_cap) ? psum[pos] : 0.f;
-        }
+        const int64_t gi = g < E ? eb + g : rb;
+        pos[r] = posA[gi];
+        jj[r] = jA[gi];
+      }
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        const bool ok = r * kThr + t < E && in_range(pos[r], p_cap);
+        const float x = psum[ok ? pos[r] : 0];
+        v[r] = ok ? x : 0.f;
+        if (r * kThr + t >= E) jj[r] = 0;
       }
 #pragma unroll
       for (int r = 0; r < kR; ++r) vmax = fmaxf(vmax, fabsf(v[r]));
@@ -1639,10 +1681,21 @@ tpf_step_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __r
         wj[j] = w;
       }
       __syncthreads();
-      for (int g = t; g < E; g += kThr) {
-        const int32_t pos = posB[eb + g];
-        const uint16_t j = jB[eb + g];
-        if (in_range(pos, w_cap) && j < kUnitK) w_ent[pos] = wj[j];
+      const int64_t rb = (int64_t)b * kEC;
+      for (int g0 = 0; g0 < E; g0 += 8 * kThr) {  // (8 entries per thread: loads batched)
+        int32_t pp[8];
+        uint16_t jq[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int g = g0 + q * kThr + t;
+          const int64_t gi = g < E ? eb + g : rb;
+          pp[q] = posB[gi];
+          jq[q] = jB[gi];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (g0 + q * kThr + t < E && in_range(pp[q], w_cap) && jq[q] < kUnitK)
+            w_ent[pp[q]] = wj[jq[q]];
       }
       __syncthreads();  // (wj of the next unit)
     }
@@ -1730,15 +1783,23 @@ tpf_step2_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __
   float v[kRE];
   uint16_t ja[kRE];
   float vmax0 = 0.f, vmax1 = 0.f;
+  // (loads in batches at clamped in-region addresses, selects afterwards: a guarded load
+  // per element compiles to a branch + s_waitcnt each)
+  {
+    int32_t pa[kRE];
 #pragma unroll
-  for (int r = 0; r < kRE; ++r) {
-    const int g = r * kThr + t;
-    v[r] = 0.f;
-    ja[r] = 0;
-    if (g < EA) {
-      const int32_t pos = posA[ebase + g];
-      ja[r] = jA[ebase + g];
-      v[r] = in_range(pos, p_cap) ? psum[pos] : 0.f;
+    for (int r = 0; r < kRE; ++r) {
+      const int g = r * kThr + t;
+      const int64_t gi = ebase + (g < EA ? g : 0);
+      pa[r] = posA[gi];
+      ja[r] = jA[gi];
+    }
+#pragma unroll
+    for (int r = 0; r < kRE; ++r) {
+      const bool ok = r * kThr + t < EA && in_range(pa[r], p_cap);
+      const float x = psum[ok ? pa[r] : 0];
+      v[r] = ok ? x : 0.f;
+      if (r * kThr + t >= EA) ja[r] = 0;
     }
   }
   uint32_t sa[kRS];
@@ -1746,15 +1807,11 @@ tpf_step2_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __
 #pragma unroll
   for (int i = 0; i < kRS; ++i) {
     const int q = i * kThr + t;
-    sa[i] = kNoSlot;
-    if (q < DA) {
-      const uint32_t si = slotA[kreg(q, DA0)];
-      if (si != kNoSlot && si <= mask) {
-        sa[i] = si;
-        sl[i] = slots[si];
-      }
-    }
+    const uint32_t si = slotA[q < DA ? kreg(q, DA0) : kbase];
+    sa[i] = (q < DA && si != kNoSlot && si <= mask) ? si : kNoSlot;
   }
+#pragma unroll
+  for (int i = 0; i < kRS; ++i) sl[i] = slots[sa[i] != kNoSlot ? sa[i] : 0];
   uint32_t sb[kRP];
   float wb[kRP];
   bool fresh[kRP];
