@@ -12,7 +12,7 @@
 //
 //   tile     one 512-thread workgroup per tile of 8192 occurrences: mix, LDS hash
 //            dedup, counting sort of the tile's distinct keys by bucket (top BB key
-//            bits) -> tkeys[tile][pos], per-tile bucket offsets toff[b][tile] (bucket-major),
+//            bits) -> tkeys[tile][pos], per-tile bucket offsets toff[tile][b],
 //            rep[i] = tile entry of occurrence i (u16)
 //   bucket   one workgroup per bucket: gather the bucket's entries from every tile
 //            (a key occurs at most once per tile, so a hot key is <= #tiles entries
@@ -198,23 +198,18 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
   }
   uint32_t D;
   uint32_t run = tp_block_scan<kThr>(s, lds, &D);
-  // toff is BUCKET-major, toff[d][tile] (T = gridDim.x tiles): a bucket workgroup reads
-  // its run offsets of all tiles as coalesced rows instead of one cache line per tile
-  // (~1 k scattered L2 requests per workgroup, issued by all 1024 bucket workgroups at
-  // once: about a third of the bucket kernel, profiles/r3_tp_pair_phases.log toff+scan)
-  const int64_t T = gridDim.x;
-  uint16_t* to = toff + blockIdx.x;
+  uint16_t* to = toff + (int64_t)blockIdx.x * (nbk + 1);
 #pragma unroll
   for (int e = 0; e < kDP; ++e) {
     const int d = t * kDP + e;
     if (d < nbk) {
       cnt[d] = run;
-      to[d * T] = (uint16_t)run;
+      to[d] = (uint16_t)run;
     }
     run += c[e];
   }
   if (t == 0) {
-    to[nbk * T] = (uint16_t)D;
+    to[nbk] = (uint16_t)D;
     dcnt[blockIdx.x] = (int32_t)D;
   }
   __syncthreads();
@@ -310,10 +305,10 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
   const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
   uint32_t c = 0;
   for (int q = q0; q < q1; ++q) {
-    const uint16_t* to = toff + q;  // bucket-major: to[d * T]
-    const uint32_t lo = to[(int64_t)f0 * T], hi = to[(int64_t)(f0 + nf) * T];
+    const uint16_t* to = toff + (int64_t)q * (nbf + 1);
+    const uint32_t lo = to[f0], hi = to[f0 + nf];
     tlo[q] = (uint16_t)lo;
-    tmid[q] = (uint16_t)((nf == 2 ? to[(int64_t)(f0 + 1) * T] : hi) - lo);
+    tmid[q] = (uint16_t)((nf == 2 ? to[f0 + 1] : hi) - lo);
     tpre[q] = hi - lo;
     c += hi - lo;
   }
@@ -593,8 +588,8 @@ __device__ __forceinline__ void tp_bk_fine_light(
   const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
   uint32_t c = 0;
   for (int q = q0; q < q1; ++q) {
-    const uint16_t* to = toff + q;  // bucket-major: to[d * T]
-    const uint32_t lo = to[(int64_t)f * T], hi = to[(int64_t)(f + 1) * T];
+    const uint16_t* to = toff + (int64_t)q * (nbf + 1);
+    const uint32_t lo = to[f], hi = to[f + 1];
     tlo[q] = (uint16_t)lo;
     tpre[q] = hi - lo;
     c += hi - lo;
@@ -1363,8 +1358,8 @@ __device__ __forceinline__ uint32_t tpf_unit_light(
   const int q0 = t * per, q1 = q0 + per < T ? q0 + per : T;
   uint32_t c = 0;
   for (int q = q0; q < q1; ++q) {
-    const uint16_t* to = toff + q;  // bucket-major: to[d * T]
-    const uint32_t lo = to[(int64_t)f * T], hi = to[(int64_t)(f + 1) * T];
+    const uint16_t* to = toff + (int64_t)q * (nbf + 1);
+    const uint32_t lo = to[f], hi = to[f + 1];
     tlo[q] = (uint16_t)lo;
     tpre[q] = hi - lo;
     c += hi - lo;
@@ -1785,7 +1780,17 @@ tpf_step2_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __
   float vmax0 = 0.f, vmax1 = 0.f;
   // (loads in batches at clamped in-region addresses, selects afterwards: a guarded load
   // per element compiles to a branch + s_waitcnt each)
-  {
+  // (A's arrays are null on a pull-only launch: every A load is under do_upd)
+  uint32_t sa[kRS];
+  Slot sl[kRS];
+#pragma unroll
+  for (int r = 0; r < kRE; ++r) {
+    v[r] = 0.f;
+    ja[r] = 0;
+  }
+#pragma unroll
+  for (int i = 0; i < kRS; ++i) sa[i] = kNoSlot;
+  if (do_upd) {
     int32_t pa[kRE];
 #pragma unroll
     for (int r = 0; r < kRE; ++r) {
@@ -1801,17 +1806,15 @@ tpf_step2_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __
       v[r] = ok ? x : 0.f;
       if (r * kThr + t >= EA) ja[r] = 0;
     }
-  }
-  uint32_t sa[kRS];
-  Slot sl[kRS];
 #pragma unroll
-  for (int i = 0; i < kRS; ++i) {
-    const int q = i * kThr + t;
-    const uint32_t si = slotA[q < DA ? kreg(q, DA0) : kbase];
-    sa[i] = (q < DA && si != kNoSlot && si <= mask) ? si : kNoSlot;
-  }
+    for (int i = 0; i < kRS; ++i) {
+      const int q = i * kThr + t;
+      const uint32_t si = slotA[q < DA ? kreg(q, DA0) : kbase];
+      sa[i] = (q < DA && si != kNoSlot && si <= mask) ? si : kNoSlot;
+    }
 #pragma unroll
-  for (int i = 0; i < kRS; ++i) sl[i] = slots[sa[i] != kNoSlot ? sa[i] : 0];
+    for (int i = 0; i < kRS; ++i) sl[i] = slots[sa[i] != kNoSlot ? sa[i] : 0];
+  }
   uint32_t sb[kRP];
   float wb[kRP];
   bool fresh[kRP];
