@@ -83,16 +83,14 @@ BACKENDS = ("mfma", "hipblaslt", "auto")
 
 
 def _nt256_variant(K: int) -> int:
-    """gemm256.hip NT variant: the 4-slot LDS ring (4) on the wide & deep products (K up
-    to a few thousand: 1270 vs 1156 TFLOP/s at K = 4992, 803 vs 784 at K = 1024), the
-    one-barrier kernel (0) on very long K (8192^3: 1154 vs 937), profiles/r4_gemm256_ring.log;
-    PSAMD_GEMM_NT256 forces one."""
+    """gemm256.hip NT variant: the one-barrier kernel (0). The 4-slot LDS ring (4) is
+    faster in isolation (1270 vs 1156 TFLOP/s at K = 4992, profiles/r4_gemm256_ring.log)
+    but not inside the wide & deep step (gemm="mfma": 1.041 vs 1.029 ms, gpurun r4n),
+    where the other stream's kernels share the CUs; PSAMD_GEMM_NT256 selects one."""
     import os
 
     v = os.environ.get("PSAMD_GEMM_NT256")
-    if v is not None:
-        return int(v)
-    return 4 if K <= 6144 else 0
+    return int(v) if v is not None else 0
 _addmm_act = getattr(torch, "_addmm_activation", None)
 
 
