@@ -2022,11 +2022,21 @@ tpf_unpack_w_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict__
       wj[j] = pos < C ? wrecv[(int64_t)p * C + pos] : 0.f;
     }
     __syncthreads();
-    const int64_t eb = (int64_t)b * kEC + e0;
-    for (int g = t; g < E; g += kThr) {
-      const int32_t pos = ent_pos[eb + g];
-      const uint16_t j = ent_j[eb + g];
-      if (in_range(pos, w_cap) && j < kUnitK) w_ent[pos] = wj[j];
+    const int64_t eb = (int64_t)b * kEC + e0, rb = (int64_t)b * kEC;
+    for (int g0 = 0; g0 < E; g0 += 8 * kThr) {  // (8 entries per thread: loads batched)
+      int32_t pp[8];
+      uint16_t jq[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int g = g0 + q * kThr + t;
+        const int64_t gi = g < E ? eb + g : rb;
+        pp[q] = ent_pos[gi];
+        jq[q] = ent_j[gi];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (g0 + q * kThr + t < E && in_range(pp[q], w_cap) && jq[q] < kUnitK)
+          w_ent[pp[q]] = wj[jq[q]];
     }
     __syncthreads();
     off += D;
@@ -2074,7 +2084,29 @@ tpf_pack_grads_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict
     for (int j = t; j < D; j += kThr) acc[j] = 0ll;
     if (t == 0) smax = 0u;
     float vmax = 0.f;
-    for (int g = t; g < E; g += kThr) {
+    // the first 2048 entries' (pos, j) and partials in registers, loaded in two batches
+    // at clamped in-region addresses (a guarded dependent load pair per entry compiled
+    // to serialised round trips); the rest (rare) in a loop
+    constexpr int kR = 8;
+    const int64_t rb = (int64_t)b * kEC;
+    int32_t pr[kR];
+    uint16_t jr[kR];
+    float xr[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const int g = r * kThr + t;
+      const int64_t gi = g < E ? eb + g : rb;
+      pr[r] = ent_pos[gi];
+      jr[r] = ent_j[gi];
+    }
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const bool ok = r * kThr + t < E && in_range(pr[r], p_cap);
+      const float x = psum[ok ? pr[r] : 0];
+      xr[r] = ok ? x : 0.f;
+      vmax = fmaxf(vmax, fabsf(xr[r]));
+    }
+    for (int g = kR * kThr + t; g < E; g += kThr) {
       const int32_t pos = ent_pos[eb + g];
       if (in_range(pos, p_cap)) vmax = fmaxf(vmax, fabsf(psum[pos]));
     }
@@ -2083,7 +2115,10 @@ tpf_pack_grads_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict
     __syncthreads();
     const int k2 = fx_shift(smax);
     const double sc = ldexp(1.0, k2);
-    for (int g = t; g < E; g += kThr) {
+#pragma unroll
+    for (int r = 0; r < kR; ++r)
+      if (xr[r] != 0.f && jr[r] < kUnitK) fx_add(acc, jr[r], xr[r], sc);
+    for (int g = kR * kThr + t; g < E; g += kThr) {
       const int32_t pos = ent_pos[eb + g];
       const uint16_t j = ent_j[eb + g];
       const float x = in_range(pos, p_cap) ? psum[pos] : 0.f;
