@@ -1146,12 +1146,6 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
   FB_MARK(0);
   uint16_t ce[NP][PER];
   float cv[NP][PER];
-  // every load unconditional (a clamped in-range address, the value dropped by a select
-  // afterwards): a guarded load per element compiled to a branch + s_waitcnt vmcnt(0)
-  // each, i.e. NP * PER serialised global round trips (the prologue was ~half of the
-  // kernel's cycles, profiles/r3_tp_pair_phases.log)
-  bool ok[NP][PER];
-  int64_t ix[NP][PER];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     const int ri = p * kRowsPass + g;
@@ -1159,67 +1153,39 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int k = sub + q * kFbLanes;
-      ok[p][q] = ri < nr && r < B && k < width;
-      ix[p][q] = ok[p][q] ? r * width + k : base;
-      ce[p][q] = rep[ix[p][q]];  // outside the tile: the entry in the neighbour tile
-      cv[p][q] = vals ? vals[ix[p][q]] : 1.f;
+      ce[p][q] = kFbNone;
+      cv[p][q] = 0.f;
+      if (ri < nr && r < B && k < width) {
+        const int64_t i = r * width + k;
+        const int64_t o = i - base;
+        const bool in = o >= 0 && o < lim;
+        const uint16_t e = rep[i];  // outside the tile: the entry in the neighbour tile
+        ce[p][q] = in ? e : kFbExt;
+        cv[p][q] = in ? (vals ? vals[i] : 1.f) : __int_as_float((int)e);
+      }
     }
   }
-#pragma unroll
-  for (int p = 0; p < NP; ++p)
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int64_t o = ix[p][q] - base;
-      const bool in = o >= 0 && o < lim;
-      const uint16_t e = ce[p][q];
-      ce[p][q] = !ok[p][q] ? kFbNone : in ? e : kFbExt;
-      cv[p][q] = !ok[p][q] ? 0.f : in ? cv[p][q] : __int_as_float((int)e);
-    }
   if (t < 4) sacc[t] = 0.f;
   if (t == 0) smax = 0u;
   // boundary rows: the outside part of row 0 / row nr-1 (only their lane groups) read
   // their weights through the neighbour tile's entry map; issued first, so the chain
   // rep -> ent_uid -> w_local overlaps the tile's own entry-weight loads
-  // (each stage's loads all issued before any of them is used: no per-element wait)
-  {
-    int64_t ue[NP][PER];
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
+  for (int p = 0; p < NP; ++p) {
+    const int ri = p * kRowsPass + g;
+    if (ri != 0 && ri != nr - 1) continue;
 #pragma unroll
-      for (int q = 0; q < PER; ++q)
-        ue[p][q] = ce[p][q] == kFbExt
-                       ? (ix[p][q] / kTile) * kTile + __float_as_int(cv[p][q]) : (int64_t)-1;
-    if (!kFlat) {
-#pragma unroll
-      for (int p = 0; p < NP; ++p)
-#pragma unroll
-        for (int q = 0; q < PER; ++q)
-          if (ue[p][q] >= 0) ue[p][q] = (int64_t)ent_uid[ue[p][q]];
-    }
-    float wx[NP][PER];
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int q = 0; q < PER; ++q)
-        if (ce[p][q] == kFbExt && in_range(ue[p][q], w_cap)) wx[p][q] = w_local[ue[p][q]];
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int q = 0; q < PER; ++q)
-        if (ce[p][q] == kFbExt)
-          cv[p][q] = (in_range(ue[p][q], w_cap) ? wx[p][q] : 0.f) *
-                     (vals ? vals[ix[p][q]] : 1.f);
+    for (int q = 0; q < PER; ++q)
+      if (ce[p][q] == kFbExt) {
+        const int64_t i = (r0 + ri) * width + sub + q * kFbLanes;
+        const int64_t ge = (i / kTile) * kTile + __float_as_int(cv[p][q]);
+        const int64_t u = kFlat ? ge : (int64_t)ent_uid[ge];
+        cv[p][q] = (in_range(u, w_cap) ? w_local[u] : 0.f) * (vals ? vals[i] : 1.f);
+      }
   }
   for (int i = t; i < nr; i += kThr) crow[i] = r0 + i < B ? labels[r0 + i] : 0.f;
-  if (kFlat) {  // (host: w_cap >= T * 8192) all loads first, then the LDS stores
-    constexpr int kW = kTile / kThr;
-    float wv[kW];
-#pragma unroll
-    for (int k = 0; k < kW; ++k)
-      if (t + k * kThr < cnt) wv[k] = w_local[base + t + k * kThr];
-#pragma unroll
-    for (int k = 0; k < kW; ++k)
-      if (t + k * kThr < cnt) wl[t + k * kThr] = wv[k];
+  if (kFlat) {
+    for (int i = t; i < cnt; i += kThr) wl[i] = w_local[base + i];  // (host: w_cap >= T * 8192)
   } else {
     for (int i = t; i < cnt; i += kThr) {
       const int32_t u = ent_uid[base + i];
