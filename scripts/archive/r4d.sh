@@ -5,7 +5,7 @@ mkdir -p $O
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 # a python exception (rc 1) does not stop the script; a timeout / signal / abort does
 step() { "$@"; rc=$?; echo "rc=$rc: $*" >> $O/steps.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; }
-step timeout -k 10 120 python scripts/diag_launchlist.py > $O/diag.log 2>&1
+step timeout -k 10 120 python scripts/archive/diag_launchlist.py > $O/diag.log 2>&1
 step timeout -k 10 300 python -u -m pytest tests/test_gemm256_gpu.py -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest_gemm.log 2>&1
 for i in 1 2; do
   step timeout -k 10 120 python bench.py --steps 20 --warmup 5 > $O/b20_native_$i.log 2>&1

@@ -4,7 +4,7 @@ O=gpurun_out/r4e
 mkdir -p $O
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 step() { "$@"; rc=$?; echo "rc=$rc: $*" >> $O/steps.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi; }
-step timeout -k 10 120 python scripts/diag_launchlist.py > $O/diag.log 2>&1
+step timeout -k 10 120 python scripts/archive/diag_launchlist.py > $O/diag.log 2>&1
 step env PSAMD_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --exchange p2p --consistency asp --steps 50 --warmup 10 > $O/p2p_2.log 2>&1
 step env PSAMD_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 3 --exchange p2p --consistency asp --steps 50 --warmup 10 > $O/p2p_3.log 2>&1
 step env PSAMD_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --consistency asp --steps 50 --warmup 10 > $O/padded_gloo_2.log 2>&1
