@@ -33,7 +33,10 @@ Host-side bookkeeping (handle exchange, drain counts) goes over a gloo group, ne
 through a device-synchronising RCCL object collective. The owner side (the own row's
 update and the inbox applies) runs on a stream of its own, so a rank whose post waits
 for a peer's ring space still applies that peer's posts: two ranks with full rings
-toward each other cannot block each other.
+toward each other cannot block each other. Every update of this rank's table must
+therefore go through ``own_update`` (serialised with the applies on that stream; a
+``kv_update`` on another stream would race them on the same slots), and the next
+step's writes of the buffers it reads wait for ``wait_own``.
 
 Validated on one MI355X with several processes sharing the GPU (real IPC mappings,
 the same kernels); the xGMI path itself needs a multi-GPU node.

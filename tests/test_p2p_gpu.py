@@ -31,7 +31,6 @@ def _transport_worker(rank, world, port, out_dir, steps, Q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from parameter_server_amd.ops.kv_table import KVTable, UpdateRule, next_pow2
-    from parameter_server_amd.ops.native import hipops
     from parameter_server_amd.parallel.comm import DistComm
     from parameter_server_amd.parallel.p2p import PeerExchange
     from parameter_server_amd.parallel.partition import KeyPartition
@@ -70,11 +69,14 @@ def _transport_worker(rank, world, port, out_dir, steps, Q):
             sh.view(torch.float32)[p * H + 4 + C * kw:p * H + 4 + C * kw + n] = torch.from_numpy(gs)
             for k, g in zip(ks, gs):
                 sent[(p, k)] = sent.get((p, k), 0.0) + float(g)
+        px.wait_own()  # (the previous own-row update has read send / slot)
         send.copy_(sh.to(dev))
         px.lookup(send, wout, slot)
         g_own = send.view(torch.float32)[rank * H + 4 + C:rank * H + 4 + 2 * C]
-        hipops().kv_update(table.slots, slot[rank * C:(rank + 1) * C], g_own,
-                           send[rank * H + 1:rank * H + 2], *rule.args(), stats)
+        # the own row on the owner stream, serialised with the peer applies (a kv_update
+        # on this stream would race them on the same slots)
+        px.own_update(slot[rank * C:(rank + 1) * C], g_own, send[rank * H + 1:rank * H + 2],
+                      rule, stats)
         px.post(send)
         px.apply(rule, stats, a_slot, a_w, link, nxt, rounds=1)
     px.drain(rule, stats, a_slot, a_w, link, nxt)
