@@ -587,21 +587,27 @@ wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __
   double loss_acc = 0, corr = 0, cnt = 0, dbsum = 0;
   for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < B;
        r += (int64_t)gridDim.x * (blockDim.x >> 6)) {
-    float hv[8];
+    // loads at clamped in-range indices, issued together, then selects (a guarded load
+    // per element compiled to a branch + s_waitcnt each: serialised round trips)
+    float hv[8], wv[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int k = lane + 64 * q;
-      hv[q] = k < H ? bf2f(h[r * H + k]) : 0.f;
+      const int kc = k < H ? k : 0;
+      hv[q] = bf2f(h[r * H + kc]);
+      wv[q] = w[kc];
     }
     float m = 0.f;
-    if (lane < S) {
-      const int32_t c = local_col[r * S + lane];
-      if (in_range(c, wide_cap)) m = wide_w[c];
+    if (S > 0) {  // (S = 0: no wide part, local_col / wide_w may be null)
+      const int32_t c = local_col[r * S + (lane < S ? lane : 0)];
+      const float wc = wide_w[in_range(c, wide_cap) ? c : 0];
+      if (lane < S && in_range(c, wide_cap)) m = wc;
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int k = lane + 64 * q;
-      if (k < H) m += hv[q] * w[k];
+      if (k >= H) hv[q] = 0.f;
+      m += k < H ? hv[q] * wv[q] : 0.f;
     }
     m = wave_allsum(m) + b[0];
     const float y = labels[r] > 0.f ? 1.f : -1.f;
@@ -610,7 +616,7 @@ wd_head_kernel(const uint16_t* __restrict__ h, int64_t B, int H, const float* __
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int k = lane + 64 * q;
-      if (k < H) dh[r * H + k] = f2bf(hv[q] > 0.f ? coef * w[k] : 0.f);
+      if (k < H) dh[r * H + k] = f2bf(hv[q] > 0.f ? coef * wv[q] : 0.f);
     }
     if (lane == 0) {
       coef_out[r] = coef;
