@@ -133,7 +133,9 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
                int32_t* __restrict__ err) {
   using namespace tp;
   __shared__ uint32_t hk[kHash];    // quotient-encoded keys; after the bucket sort: entry position
-  __shared__ uint32_t cnt[kMaxBk];  // per-bucket counts, then offsets
+  // per-bucket counts, then offsets; [kMaxBk, kMaxBk + kThr): one dummy counter per
+  // thread, the target of the rank atomics of empty hash slots (branch-free atomics)
+  __shared__ uint32_t cnt[kMaxBk + kThr];
   __shared__ uint32_t lds[kThr / 64 + 1];
   const int t = threadIdx.x;
   for (int i = t; i < kHash; i += kThr) hk[i] = kEmpty;
@@ -180,12 +182,21 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
     if (!kQuot) return v;
     return ((uint64_t)(v >> kDispB) << kHB) | ((uint32_t)(s - (int)(v & kMaxDisp)) & (kHash - 1));
   };
-  uint32_t rr[kPer];
+  // all 16 slot reads first, then all 16 rank atomics (one LDS latency each batch: read
+  // -> atomic per slot compiled to a wait each, 16 serialised round trips); the slot
+  // values stay in registers for the scatter below
+  uint32_t rr[kPer], hv[kPer];
 #pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const uint32_t v = hk[q * kThr + t];
-    rr[q] = v != kEmpty ? atomicAdd(&cnt[decode(v, q * kThr + t) >> shift], 1u) : kEmpty;
+  for (int q = 0; q < kPer; ++q) hv[q] = hk[q * kThr + t];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {  // (unconditional: a guarded atomic waited per slot)
+    const bool occ = hv[q] != kEmpty;
+    const uint32_t d = occ ? (uint32_t)(decode(hv[q], q * kThr + t) >> shift) : kMaxBk + t;
+    rr[q] = atomicAdd(&cnt[d], 1u);
   }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q)
+    if (hv[q] == kEmpty) rr[q] = kEmpty;
   __syncthreads();
   // exclusive scan of the bucket counts (nbk <= kMaxBk: 2 per thread)
   constexpr int kDP = kMaxBk / kThr;
@@ -218,7 +229,7 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     if (rr[q] != kEmpty) {
-      const uint64_t k = decode(hk[q * kThr + t], q * kThr + t);
+      const uint64_t k = decode(hv[q], q * kThr + t);
       const uint32_t pos = cnt[k >> shift] + rr[q];
       tk[pos] = (uint32_t)(k & smask);
       rr[q] = pos;
