@@ -1213,11 +1213,15 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     float m = 0.f;
+    // every LDS weight read first (branch-free, entry 0 for the others), then the sum:
+    // a guarded read per occurrence compiled to a wait each
+    float wr[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) wr[q] = wl[ce[p][q] < kFbExt ? ce[p][q] : 0];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const uint16_t e = ce[p][q];
-      if (e == kFbExt) m += cv[p][q];
-      else if (e != kFbNone) m += wl[e] * cv[p][q];
+      m += e == kFbExt ? cv[p][q] : e != kFbNone ? wr[q] * cv[p][q] : 0.f;
     }
     m = group8_sum(m);
     const int ri = p * kRowsPass + g;
@@ -1277,7 +1281,15 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
   __syncthreads();
   FB_MARK(5);
   const double isc = ldexp(1.0, -k2);
-  for (int i = t; i < cnt; i += kThr) psum[base + i] = (float)((double)acc[i] * isc);
+  {  // (the tile's <= 8 partials per thread read from LDS together, then stored)
+    constexpr int kW = kTile / kThr;
+    long long av[kW];
+#pragma unroll
+    for (int k = 0; k < kW; ++k) av[k] = acc[t + k * kThr < cnt ? t + k * kThr : 0];
+#pragma unroll
+    for (int k = 0; k < kW; ++k)
+      if (t + k * kThr < cnt) psum[base + t + k * kThr] = (float)((double)av[k] * isc);
+  }
   FB_MARK(6);
   if (fbp && threadIdx.x == 0) {
     fbp[(int64_t)blockIdx.x * 16 + 9] = __builtin_amdgcn_s_memrealtime();
