@@ -133,9 +133,7 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
                int32_t* __restrict__ err) {
   using namespace tp;
   __shared__ uint32_t hk[kHash];    // quotient-encoded keys; after the bucket sort: entry position
-  // per-bucket counts, then offsets; [kMaxBk, kMaxBk + kThr): one dummy counter per
-  // thread, the target of the rank atomics of empty hash slots (branch-free atomics)
-  __shared__ uint32_t cnt[kMaxBk + kThr];
+  __shared__ uint32_t cnt[kMaxBk];  // per-bucket counts, then offsets
   __shared__ uint32_t lds[kThr / 64 + 1];
   const int t = threadIdx.x;
   for (int i = t; i < kHash; i += kThr) hk[i] = kEmpty;
@@ -182,21 +180,12 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
     if (!kQuot) return v;
     return ((uint64_t)(v >> kDispB) << kHB) | ((uint32_t)(s - (int)(v & kMaxDisp)) & (kHash - 1));
   };
-  // all 16 slot reads first, then all 16 rank atomics (one LDS latency each batch: read
-  // -> atomic per slot compiled to a wait each, 16 serialised round trips); the slot
-  // values stay in registers for the scatter below
-  uint32_t rr[kPer], hv[kPer];
+  uint32_t rr[kPer];
 #pragma unroll
-  for (int q = 0; q < kPer; ++q) hv[q] = hk[q * kThr + t];
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {  // (unconditional: a guarded atomic waited per slot)
-    const bool occ = hv[q] != kEmpty;
-    const uint32_t d = occ ? (uint32_t)(decode(hv[q], q * kThr + t) >> shift) : kMaxBk + t;
-    rr[q] = atomicAdd(&cnt[d], 1u);
+  for (int q = 0; q < kPer; ++q) {
+    const uint32_t v = hk[q * kThr + t];
+    rr[q] = v != kEmpty ? atomicAdd(&cnt[decode(v, q * kThr + t) >> shift], 1u) : kEmpty;
   }
-#pragma unroll
-  for (int q = 0; q < kPer; ++q)
-    if (hv[q] == kEmpty) rr[q] = kEmpty;
   __syncthreads();
   // exclusive scan of the bucket counts (nbk <= kMaxBk: 2 per thread)
   constexpr int kDP = kMaxBk / kThr;
@@ -229,7 +218,7 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
     if (rr[q] != kEmpty) {
-      const uint64_t k = decode(hv[q], q * kThr + t);
+      const uint64_t k = decode(hk[q * kThr + t], q * kThr + t);
       const uint32_t pos = cnt[k >> shift] + rr[q];
       tk[pos] = (uint32_t)(k & smask);
       rr[q] = pos;
@@ -1235,15 +1224,11 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     float m = 0.f;
-    // every LDS weight read first (branch-free, entry 0 for the others), then the sum:
-    // a guarded read per occurrence compiled to a wait each
-    float wr[PER];
-#pragma unroll
-    for (int q = 0; q < PER; ++q) wr[q] = wl[ce[p][q] < kFbExt ? ce[p][q] : 0];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const uint16_t e = ce[p][q];
-      m += e == kFbExt ? cv[p][q] : e != kFbNone ? wr[q] * cv[p][q] : 0.f;
+      if (e == kFbExt) m += cv[p][q];
+      else if (e != kFbNone) m += wl[e] * cv[p][q];
     }
     m = group8_sum(m);
     const int ri = p * kRowsPass + g;
@@ -1303,15 +1288,7 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
   __syncthreads();
   FB_MARK(5);
   const double isc = ldexp(1.0, -k2);
-  {  // (the tile's <= 8 partials per thread read from LDS together, then stored)
-    constexpr int kW = kTile / kThr;
-    long long av[kW];
-#pragma unroll
-    for (int k = 0; k < kW; ++k) av[k] = acc[t + k * kThr < cnt ? t + k * kThr : 0];
-#pragma unroll
-    for (int k = 0; k < kW; ++k)
-      if (t + k * kThr < cnt) psum[base + t + k * kThr] = (float)((double)av[k] * isc);
-  }
+  for (int i = t; i < cnt; i += kThr) psum[base + i] = (float)((double)acc[i] * isc);
   FB_MARK(6);
   if (fbp && threadIdx.x == 0) {
     fbp[(int64_t)blockIdx.x * 16 + 9] = __builtin_amdgcn_s_memrealtime();
