@@ -325,41 +325,19 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
   const uint32_t En = E < (uint32_t)kECapL ? E : (uint32_t)kECapL;
   bool bad = E > (uint32_t)kECapL;
   uint32_t hib = 0;  // bit q: entry q lies in the pair's second fine bucket
-  // each entry's tile: the last tile q with tpre[q] <= g. The kG searches run in lock
-  // step, branch-free (one batch of kG LDS reads per halving step; a data-dependent
-  // search per entry compiled to one wait per probe, ~kG x log2(T) serialised reads)
-  {
-    int lo[kG];
 #pragma unroll
-    for (int q = 0; q < kG; ++q) lo[q] = 0;
-    int top = 1;
-    while (2 * top <= T - 1) top *= 2;
-    for (int step = T > 1 ? top : 0; step > 0; step >>= 1) {
-      uint32_t v[kG];
-#pragma unroll
-      for (int q = 0; q < kG; ++q) v[q] = tpre[min(lo[q] + step, T - 1)];
-#pragma unroll
-      for (int q = 0; q < kG; ++q) {
-        const uint32_t g = q * kBkThr + t;
-        if (lo[q] + step <= T - 1 && v[q] <= g) lo[q] += step;
+  for (int q = 0; q < kG; ++q) {
+    const uint32_t g = q * kBkThr + t;
+    idx[q] = -1;
+    if (g < En) {
+      int lo = 0, up = T - 1;  // last tile with tpre[q] <= g
+      while (lo < up) {
+        const int mid = (lo + up + 1) >> 1;
+        if (tpre[mid] <= g) lo = mid; else up = mid - 1;
       }
-    }
-    uint32_t pv[kG], lv[kG], mv[kG];
-#pragma unroll
-    for (int q = 0; q < kG; ++q) {
-      pv[q] = tpre[lo[q]];
-      lv[q] = tlo[lo[q]];
-      mv[q] = tmid[lo[q]];
-    }
-#pragma unroll
-    for (int q = 0; q < kG; ++q) {
-      const uint32_t g = q * kBkThr + t;
-      idx[q] = -1;
-      if (g < En) {
-        const uint32_t off = g - pv[q];
-        idx[q] = lo[q] * kTile + (int32_t)lv[q] + (int32_t)off;
-        hib |= (off >= mv[q] ? 1u : 0u) << q;
-      }
+      const uint32_t off = g - tpre[lo];
+      idx[q] = lo * kTile + tlo[lo] + (int32_t)off;
+      hib |= (off >= tmid[lo] ? 1u : 0u) << q;
     }
   }
   uint32_t kv[kG];
