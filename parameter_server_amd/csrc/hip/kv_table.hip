@@ -457,43 +457,19 @@ __global__ __launch_bounds__(256) void kv_apply_part_kernel(
     const int tot = roff[G];
     if (tot == 0) break;
     const uint64_t th = thr;
-    // the window's entries (<= kApWin = 4 x 256): every thread's (key, slot, gradient)
-    // loads issued together at clamped addresses before any is used (a guarded load
-    // group per entry compiled to one s_waitcnt each: serialised round trips)
-    constexpr int kPer = kApWin / 256;
-    uint64_t kkey[kPer];
-    int64_t kslot[kPer];
-    float kgrad[kPer];
-    int64_t kent[kPer];
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int w = tid + u * (int)blockDim.x;
-      int64_t e = 0, gi = 0;
-      if (w < tot) {
-        int lo = 0, hi = G - 1;  // row of window entry w: last s with roff[s] <= w
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (roff[mid] <= w) lo = mid; else hi = mid - 1;
-        }
-        const int64_t i = ra[lo] + (w - roff[lo]);
-        e = (int64_t)lo * C + i;
-        gi = (int64_t)lo * gstride + i;
+    for (int w = tid; w < tot; w += blockDim.x) {
+      int lo = 0, hi = G - 1;  // row of window entry w: last s with roff[s] <= w
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (roff[mid] <= w) lo = mid; else hi = mid - 1;
       }
-      kent[u] = e;
-      kkey[u] = keys[e];
-      kslot[u] = slot_idx[e];
-      kgrad[u] = grad[gi];
-    }
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int w = tid + u * (int)blockDim.x;
-      if (w >= tot) continue;
-      const int64_t e = kent[u];
-      const int s = (int)(e / C);
+      const int s = lo;
+      const int64_t i = ra[s] + (w - roff[s]);
+      const int64_t e = (int64_t)s * C + i;
       int32_t ent = -1;
-      const uint64_t key = kkey[u];
-      const int64_t k = kslot[u];
-      const float g = kgrad[u];
+      const uint64_t key = keys[e];  // three independent loads in flight together
+      const int64_t k = slot_idx[e];
+      const float g = grad[(int64_t)s * gstride + i];
       if (key <= th) {
         atomicAdd(&rcnt[s], 1);
         if (in_range(k, cap) && g == g) {  // NaN mark = filtered entry
