@@ -321,7 +321,10 @@ criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_
     const int64_t r = rb + lane;
     const uint64_t gr = (uint64_t)(row0 + r);
     if (r < B) {
-      for (int j = j0; j < j1; ++j) {
+#pragma unroll
+      for (int jj = 0; jj < 7; ++jj) {  // (fixed trip count: the 6-7 samples interleave)
+        const int j = j0 + jj;
+        if (j >= j1) break;
         const float u = gen_u01(gen_row_bits(gr, s_seed[j]));
         const uint64_t key = gen_key<kWide>(u, j, num_features, nf_m, inv_oma,
                                             j >= 13 ? s_cm1[j - 13] : 0.f);
