@@ -149,6 +149,11 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     post = tr.padded and tr.sched.post
     xd_cap = int(os.environ.get("PSAMD_XD", "2"))  # exchanges issued ahead (A/B knob)
     xd = min(nprep, xd_cap, tr.lag if post else tr.lag + 1) if split else 0
+    # the key pack of exchange t runs before it waits for exchange t-1 (ssp post / asp
+    # tail apply; not with the tail filter: its CountMin and keep-mask scratch are shared
+    # by the key packs of consecutive exchanges). Otherwise the whole exchange half waits
+    # first and replays as ONE captured graph (pack + all-to-all A + owner work + B).
+    early = (post or asp_apply == "tail") and tr.filter is None
     E = 64  # event rings, indexed by step (every look-back here is < 64 steps)
     ev_buf = [torch.cuda.Event() for _ in range(NB)]   # worker done with buffer b
     ev_w = [torch.cuda.Event() for _ in range(E)]      # worker half of step t done
@@ -207,9 +212,6 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
         # the resolve needs that (it rewrites wsend and must see the apply), so the key
         # pack and all-to-all A of exchange t overlap the tail of exchange t-1
         chain = ev_post if post else ev_x
-        # (not with the tail filter: its CountMin and keep-mask scratch are shared by
-        # the key packs of consecutive exchanges)
-        early = (post or asp_apply == "tail") and tr.filter is None
         if t >= 1 and not early:
             xs.wait_event(chain[(t - 1) % E])
         if asp:  # ring entry of exchange t is free again once that apply is done
@@ -423,7 +425,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             cchain.mark(s, n)
         return f
 
-    def capture(plan):
+    def capture(plan, split=True):
         out = []
         if not ccomm:
             for kind, fn in plan:  # in order: a segment may bake in buffers the previous
@@ -450,7 +452,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
                 flush()
                 out.append((kind, graph_of([fn])))
             else:
-                if kind == "comm" and not any(k == "comm" for k, _ in grp):
+                if split and kind == "comm" and not any(k == "comm" for k, _ in grp):
                     flush()
                 grp.append((kind, fn))
         flush()
@@ -466,7 +468,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             # graph (a graph replay costs ~6-8 us of GPU time and ~11 us of host time,
             # profiles/r3_s2_graph_ab.log; ASP issued 6 graphs per step, now 5)
             xh = [x for x in xh if x[0] != "async"] + [x for x in xh if x[0] == "async"]
-        xplans[j] = capture(xh)
+        xplans[j] = capture(xh, split=early)
         wplans[j] = capture(wh)
     # capture ran nothing: the workspaces of the minibatches in flight still hold
     # their eager preparations (and the eager exchanges issued ahead), so the replays
@@ -598,6 +600,9 @@ def main():
                          "or one-sided peer-HBM pulls + inbox pushes (asp only, no collective "
                          "per step: parallel/p2p.py)")
     ap.add_argument("--fixing-float", type=int, default=0)
+    ap.add_argument("--ssp-apply", default="post", choices=["post", "pre"],
+                    help="N > 1, ssp: the owner applies the carried pushes after sending the "
+                         "pulled weights back (post) or before resolving the pulls (pre)")
     ap.add_argument("--push-mode", default="sequential", choices=["sequential", "aggregate"],
                     help="N > 1: one optimizer step per source row in rank order (per-push, "
                          "KVStore semantics), or the owner sums the G workers' gradients of a "
@@ -681,7 +686,7 @@ def main():
                          consistency=args.consistency,
                          fixing_float_bytes=args.fixing_float, exchange=args.exchange,
                          localize=args.localize, push_mode=args.push_mode,
-                         seed=rank)
+                         ssp_apply=args.ssp_apply, seed=rank)
     tr = SparseLRTrainer(cfg, comm, device)
     prefill_occ = None
     if args.prefill > 0:
@@ -853,6 +858,8 @@ def main():
                 "parallelism": f"dp{n_ranks}+kvshard{n_ranks}",
                 "consistency": tr.consistency_desc(),
                 "push": args.push_mode if G > 1 else None,
+                "ssp_apply": args.ssp_apply if G > 1 and tr.padded and tr.lag >= 1 and not tr.asp
+                else None,
                 "table_slots_per_gpu": tr.table.capacity,
                 "hip_graph": graph_used,
                 "collectives_in_graphs": bool(getattr(pipeline, "captured_comm", False)

@@ -51,6 +51,7 @@ def _weights(tr):
     ("prep", 3, 1, {"consistency": "bsp"}),
     ("prep", 2, 1, {"fixing_float_bytes": 2}), ("prep", 2, 1, {"push_mode": "aggregate"}),
     ("prep", 2, 1, {"algo": "adagrad"}),
+    ("prep", 2, 1, {"ssp_apply": "pre"}), ("prep", 3, 1, {"ssp_apply": "pre", "consistency": "ssp:1"}),
     ("prep", 2, 1, {"_env": {"PSAMD_CAPTURE_COMM": "0"}}),
     ("prep", 3, 1, {"consistency": "bsp", "_env": {"PSAMD_CAPTURE_COMM": "0"}})])
 def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
