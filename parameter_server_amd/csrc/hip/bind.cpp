@@ -227,9 +227,12 @@ void emb_unpack_records(const int32_t*, int64_t, int, const int64_t*, const int3
 void emb_pack_grads(const float*, const float*, const int64_t*, const int32_t*, int64_t, int64_t,
                     int, int, int32_t*, hipStream_t);
 void emb_grad_reduce(const int32_t*, const int32_t*, const int32_t*, const int32_t*, int64_t,
-                     int64_t, const void*, int, float*, float*, hipStream_t);
+                     int64_t, const void*, int, float*, float*, const float*, int, float*,
+                     hipStream_t);
+bool emb_grad_wide_ok(int);
 void emb_update(const int64_t*, int64_t, const int32_t*, int64_t, const float*, const void*, void*,
-                float*, int, float, float, hipStream_t);
+                float*, int, float, float, void*, const float*, const int*, const float*, double*,
+                int, hipStream_t);
 void wd_head(const void*, int64_t, int, const float*, const float*, const float*, int64_t,
              const int32_t*, int, const float*, float*, void*, float*, float*, float*, double*,
              uint32_t*, int, int, hipStream_t);
@@ -2271,8 +2274,10 @@ PYBIND11_MODULE(_hipops, m) {
                           ptr<int32_t>(n_uniq), dE.size(0), C, G, D, ptr<int32_t>(out),
                           cur_stream());
   });
+  m.def("emb_grad_wide_ok", [](int D) { return psamd::emb_grad_wide_ok(D); });
   m.def("emb_grad_reduce", [](Tensor pos_s, Tensor segid, Tensor seg_start, Tensor n_uniq,
-                              int64_t u_cap, int64_t nnz, Tensor dX0, int D, Tensor dE) {
+                              int64_t u_cap, int64_t nnz, Tensor dX0, int D, Tensor dE,
+                              optional<Tensor> coef, int width, optional<Tensor> g_wide) {
     chk(pos_s, at::kInt, "pos_s");
     chk(segid, at::kInt, "segid");
     check(segid.numel() >= nnz, "segid too small");
@@ -2287,13 +2292,29 @@ PYBIND11_MODULE(_hipops, m) {
     // caching allocator, so graph captures keep it in their pool)
     const int64_t pf = psamd::emb_grad_part_floats(nnz, D);
     Tensor part = pf ? at::empty({pf}, dE.options()) : Tensor();
+    // wide & deep: g_wide[u] = sum of coef[row] over u's occurrences (row = pos / width)
+    const bool wide = g_wide.has_value();
+    if (wide) {
+      check(coef.has_value() && width > 0 && nnz % width == 0, "g_wide needs coef and width");
+      chk(*coef, at::kFloat, "coef");
+      chk(*g_wide, at::kFloat, "g_wide");
+      check(coef->numel() >= nnz / width && g_wide->numel() >= u_cap, "coef / g_wide too small");
+      check(psamd::emb_grad_wide_ok(D), "g_wide rides along only with D = 128 / 256");
+    }
     psamd::emb_grad_reduce(ptr<int32_t>(pos_s), ptr<int32_t>(segid), ptr<int32_t>(seg_start),
                            ptr<int32_t>(n_uniq), u_cap, nnz, dX0.data_ptr(), D, ptr<float>(dE),
-                           pf ? ptr<float>(part) : nullptr, cur_stream());
-  });
+                           pf ? ptr<float>(part) : nullptr, wide ? ptr<float>(*coef) : nullptr,
+                           wide ? width : 0, wide ? ptr<float>(*g_wide) : nullptr, cur_stream());
+  }, py::arg("pos_s"), py::arg("segid"), py::arg("seg_start"), py::arg("n_uniq"),
+     py::arg("u_cap"), py::arg("nnz"), py::arg("dX0"), py::arg("D"), py::arg("dE"),
+     py::arg("coef") = py::none(), py::arg("width") = 0, py::arg("g_wide") = py::none());
+  // wide & deep: wide = (slots, g_wide, algo, lr_type, alpha, beta, l1, l2, grad_scale,
+  // max_delta) also applies the keys' wide gradients to their table slots (kv_update's
+  // update and stats) in the same pass
   m.def("emb_update", [rows_check](Tensor slot, optional<Tensor> n_dev, optional<Tensor> grad,
                                    optional<Tensor> grad16, Tensor rows, Tensor acc, double lr,
-                                   double eps) {
+                                   double eps, optional<Tensor> slots, optional<Tensor> g_wide,
+                                   std::vector<double> rule, optional<Tensor> stats) {
     chk(slot, at::kLong, "slot");
     chk(acc, at::kFloat, "acc");
     const int64_t cap = acc.numel();
@@ -2309,10 +2330,30 @@ PYBIND11_MODULE(_hipops, m) {
     } else {
       check(grad->numel() >= slot.numel() * D, "grad too small");
     }
+    void* sp = nullptr;
+    const float* gw = nullptr;
+    int wr[2] = {0, 0};
+    float wh[6] = {0, 0, 0, 0, 0, 0};
+    if (slots.has_value()) {
+      check(slot_capacity(*slots) == cap, "emb_update: slots and rows must be one table");
+      chk(*g_wide, at::kFloat, "g_wide");
+      check(g_wide->numel() >= slot.numel(), "g_wide too small");
+      check(rule.size() == 8, "wide rule = algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta");
+      check(rule[2] > 0, "learning rate alpha must be > 0");
+      sp = slots->data_ptr();
+      gw = ptr<float>(*g_wide);
+      wr[0] = (int)rule[0];
+      wr[1] = (int)rule[1];
+      for (int q = 0; q < 6; ++q) wh[q] = (float)rule[2 + q];
+    }
     psamd::emb_update(ptr<int64_t>(slot), slot.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"),
-                      cap, gp, g16, rows.data_ptr(), ptr<float>(acc), D, (float)lr, (float)eps,
+                      cap, gp, g16, rows.data_ptr(), ptr<float>(acc), D, (float)lr, (float)eps, sp,
+                      gw, wr, wh, optr<double>(stats, at::kDouble, "stats"), acc_stripes_of(stats),
                       cur_stream());
-  });
+  }, py::arg("slot"), py::arg("n_dev"), py::arg("grad"), py::arg("grad16"), py::arg("rows"),
+     py::arg("acc"), py::arg("lr"), py::arg("eps"), py::arg("slots") = py::none(),
+     py::arg("g_wide") = py::none(), py::arg("rule") = std::vector<double>{},
+     py::arg("stats") = py::none());
   m.def("wd_head", [](Tensor h, Tensor w, Tensor b, Tensor wide_w, Tensor local_col, int S,
                       Tensor labels, Tensor coef, Tensor dh, Tensor dw, Tensor db, Tensor metrics,
                       Tensor hist, int nbins, optional<Tensor> db_h) {

@@ -19,8 +19,10 @@
 //                    gradient, plain column sums (library-GEMM backend)
 //   adam_update      fp32 master weights + bf16 copy for the GEMMs
 #include "common.cuh"
+#include "kv_slot.cuh"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include <hip/hip_bf16.h>
 
@@ -228,12 +230,17 @@ emb_grad_reduce_long_kernel(const int32_t* __restrict__ pos_s, const int32_t* __
 // -> row): latency bound (55 + 147 us for 639 k x 128 on MI355X).
 constexpr int kSegRun = 64;
 
+// gw != null (wide & deep): the wide gradient of the same segments rides along,
+// gw[u] = sum of coef[row] over u's occurrences (row = position / width), summed in
+// entry order like the rows (partials in partw[run * 2 + 0 / 1], added by the cross
+// kernel): one pass for both, deterministic.
 template <int C>
 __global__ void __launch_bounds__(256)
 emb_grad_seg_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict__ segid,
                     const int32_t* __restrict__ seg_start, int64_t u_cap, int64_t nnz,
                     const uint32_t* __restrict__ dX0, float* __restrict__ dE,
-                    float* __restrict__ part) {
+                    float* __restrict__ part, const float* __restrict__ coef, int width,
+                    float* __restrict__ gw, float* __restrict__ partw) {
   constexpr int D = 128 * C;
   const int lane = threadIdx.x & 63;
   const int64_t run = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -255,6 +262,7 @@ emb_grad_seg_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict
   }
   const uint64_t take_m = __ballot(take);
   const uint64_t fl_m = __ballot(fl);
+  const float cw = gw && take ? coef[(uint32_t)p / (uint32_t)width] : 0.f;
   uint32_t v[kSegRun][C];
 #pragma unroll
   for (int j = 0; j < kSegRun; ++j) {
@@ -266,9 +274,11 @@ emb_grad_seg_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict
   float acc[2 * C];
 #pragma unroll
   for (int c = 0; c < 2 * C; ++c) acc[c] = 0.f;
+  float aw = 0.f;  // (wave-uniform)
 #pragma unroll
   for (int j = 0; j < kSegRun; ++j) {
     const bool tj = (take_m >> j) & 1;
+    aw += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cw), j));
 #pragma unroll
     for (int c = 0; c < C; ++c) {
       const uint32_t w = tj ? v[j][c] : 0u;
@@ -286,9 +296,14 @@ emb_grad_seg_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict
         for (int c = 0; c < C; ++c)
           *reinterpret_cast<float2*>(dst + c * 128 + 2 * lane) =
               make_float2(acc[2 * c], acc[2 * c + 1]);
+        if (gw && lane == 0) {
+          float* dw = kj == 1 ? gw + uj : partw + run * 2 + (kj == 3);
+          *dw = aw;
+        }
       }
 #pragma unroll
       for (int c = 0; c < 2 * C; ++c) acc[c] = 0.f;
+      aw = 0.f;
     }
   }
 }
@@ -296,11 +311,15 @@ emb_grad_seg_kernel(const int32_t* __restrict__ pos_s, const int32_t* __restrict
 // Segments crossing run boundaries: the run where segment u starts (its last
 // piece continues to the right) sums its slot-1 partial and the slot-0 partials
 // of the following runs up to the segment's end, in order.
-template <int C>
+// (A hot key's segment spans up to B / 64 runs: its partials are loaded kB at a time,
+// clamped in range and unconditionally, so one wave has kB loads in flight instead of
+// a round trip per run.)
+template <int C, int kB>
 __global__ void __launch_bounds__(256)
 emb_grad_cross_kernel(const int32_t* __restrict__ segid, const int32_t* __restrict__ seg_start,
                       int64_t u_cap, int64_t nnz, const float* __restrict__ part,
-                      float* __restrict__ dE) {
+                      float* __restrict__ dE, const float* __restrict__ partw,
+                      float* __restrict__ gw) {
   constexpr int D = 128 * C;
   const int lane = threadIdx.x & 63;
   const int64_t run = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -318,19 +337,46 @@ emb_grad_cross_kernel(const int32_t* __restrict__ segid, const int32_t* __restri
     acc[2 * c] = x.x;
     acc[2 * c + 1] = x.y;
   }
+  float aw = gw ? partw[run * 2 + 1] : 0.f;
+  if (kB == 1) {  // (one run per iteration, the compiler's unroll)
 #pragma unroll 8
-  for (int64_t r = run + 1; r <= re; ++r) {
+    for (int64_t r = run + 1; r <= re; ++r) {
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const float2 x = *reinterpret_cast<const float2*>(part + r * 2 * D + c * 128 + 2 * lane);
-      acc[2 * c] += x.x;
-      acc[2 * c + 1] += x.y;
+      for (int c = 0; c < C; ++c) {
+        const float2 x = *reinterpret_cast<const float2*>(part + r * 2 * D + c * 128 + 2 * lane);
+        acc[2 * c] += x.x;
+        acc[2 * c + 1] += x.y;
+      }
+      if (gw) aw += partw[r * 2];
+    }
+  } else
+  for (int64_t r0 = run + 1; r0 <= re; r0 += kB) {
+    float2 x[kB][C];
+    float xw[kB];
+#pragma unroll
+    for (int q = 0; q < kB; ++q) {
+      const int64_t r = r0 + q <= re ? r0 + q : re;
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        x[q][c] = *reinterpret_cast<const float2*>(part + r * 2 * D + c * 128 + 2 * lane);
+      xw[q] = gw ? partw[r * 2] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < kB; ++q) {
+      if (r0 + q > re) break;
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        acc[2 * c] += x[q][c].x;
+        acc[2 * c + 1] += x[q][c].y;
+      }
+      aw += xw[q];
     }
   }
 #pragma unroll
   for (int c = 0; c < C; ++c)
     *reinterpret_cast<float2*>(dE + (int64_t)u * D + c * 128 + 2 * lane) =
         make_float2(acc[2 * c], acc[2 * c + 1]);
+  if (gw && lane == 0) gw[u] = aw;
 }
 
 // Narrow rows (D = 8 .. 64, the FM factors): the same 64-entry runs, but lane =
@@ -523,13 +569,20 @@ emb_pack_grads_kernel(const float* __restrict__ dE, const float* __restrict__ g_
 }
 
 // Row-wise AdaGrad (one accumulator per row, DLRM-style) on bf16 rows, fp32 math.
+// kWide (wide & deep, one shard): the first lane of each key's group also applies the
+// key's wide gradient to its table slot (the same slot index: rows and slots are one
+// table), so the slot's optimizer update overlaps the row's loads instead of running
+// as a second pass over the keys (kv_update_kernel; same update, same stats).
+template <bool kWide>
 __global__ void __launch_bounds__(256)
 emb_update_kernel(const int64_t* __restrict__ slot, int64_t n, const int32_t* __restrict__ n_dev,
                   int64_t cap, const float* __restrict__ grad, const uint16_t* __restrict__ grad16,
                   uint16_t* __restrict__ rows, float* __restrict__ acc, int D, float lr,
-                  float eps) {
+                  float eps, Slot* __restrict__ slots, const float* __restrict__ gwide,
+                  UpdateParams up, double* __restrict__ stats, int acc_stripes) {
   const int64_t nn = dev_len(n_dev, n);
   const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
+  double dnnz = 0, wsum = 0, dsum = 0;
   for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; i < nn;
        i += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
     const int64_t s = slot[i];
@@ -552,8 +605,19 @@ emb_update_kernel(const int64_t* __restrict__ slot, int64_t n, const int32_t* __
 #pragma unroll
       for (int j = 0; j < 8; ++j) sq += gv[j] * gv[j];
     }
+    float gw = 0.f;
+    if (kWide && l == 0 && ok) gw = gwide[i] * up.grad_scale;
     sq = group_sum(sq);
     if (!ok) continue;
+    if (kWide && l == 0 && gw == gw) {  // (NaN mark = filtered entry)
+      Slot sl = slots[s];
+      const float w_old = apply_update(sl, gw, up);
+      slots[s] = sl;
+      dnnz += (double)((sl.w != 0.f) - (w_old != 0.f));
+      wsum += (double)sl.w * sl.w;
+      const double d = (double)sl.w - w_old;
+      dsum += d * d;
+    }
     float a = acc[s] + sq / D;
     if (l == 0) acc[s] = a;
     const float step = lr / (sqrtf(a) + eps);
@@ -564,6 +628,15 @@ emb_update_kernel(const int64_t* __restrict__ slot, int64_t n, const int32_t* __
 #pragma unroll
       for (int j = 0; j < 8; ++j) h[j] = f2bf(bf2f(h[j]) - step * gv[j]);
       *rp = v;
+    }
+  }
+  if (kWide && stats) {  // per-wave DPP sums, lane 63 adds (as kv_update_kernel)
+    const double a = wave_sum_dpp(dnnz), b = wave_sum_dpp(wsum), c = wave_sum_dpp(dsum);
+    if ((threadIdx.x & 63) == 63) {
+      double* st = acc_stripe(stats, acc_stripes);
+      if (a != 0) atomicAdd(&st[0], a);
+      if (b != 0) atomicAdd(&st[1], b);
+      if (c != 0) atomicAdd(&st[2], c);
     }
   }
 }
@@ -765,14 +838,28 @@ static bool seg_path(int D) {
   return D == 8 || D == 16 || D == 32 || D == 64 || D == 128 || D == 256;
 }
 
+// (+ 2 wide partials per run when the wide gradient rides along: wide_ok(D))
 int64_t emb_grad_part_floats(int64_t nnz, int D) {
-  return seg_path(D) ? ((nnz + kSegRun - 1) / kSegRun) * 2 * D : 0;
+  return seg_path(D) ? ((nnz + kSegRun - 1) / kSegRun) * 2 * (D + 1) : 0;
+}
+bool emb_grad_wide_ok(int D) { return D == 128 || D == 256; }
+// PSAMD_CROSS_BATCH=1: the cross kernel loads kB runs' partials per iteration (A/B)
+static bool cross_batched() {
+  static const bool on = [] {
+    const char* e = getenv("PSAMD_CROSS_BATCH");
+    return e && e[0] == '1';
+  }();
+  return on;
 }
 
 void emb_grad_reduce(const int32_t* pos_s, const int32_t* segid, const int32_t* seg_start,
                      const int32_t* n_uniq, int64_t u_cap, int64_t nnz, const void* dX0, int D,
-                     float* dE, float* part, hipStream_t st) {
+                     float* dE, float* part, const float* coef, int width, float* gw,
+                     hipStream_t st) {
   if (u_cap <= 0 || nnz <= 0) return;
+  if (gw && !(part && emb_grad_wide_ok(D) && coef && width > 0))
+    throw std::runtime_error("emb_grad_reduce: the wide gradient rides along only with D = 128 / 256");
+  float* partw = part ? part + ((nnz + kSegRun - 1) / kSegRun) * 2 * D : nullptr;
   if (part && seg_path(D)) {
     const int64_t runs = (nnz + kSegRun - 1) / kSegRun;
     const dim3 grid((unsigned)((runs + 3) / 4));
@@ -792,13 +879,25 @@ void emb_grad_reduce(const int32_t* pos_s, const int32_t* segid, const int32_t* 
     } else if (D == 64) {
       PSAMD_NARROW(64);
     } else if (D == 128) {
-      emb_grad_seg_kernel<1><<<grid, 256, 0, st>>>(pos_s, segid, seg_start, u_cap, nnz, x, dE, part);
+      emb_grad_seg_kernel<1><<<grid, 256, 0, st>>>(pos_s, segid, seg_start, u_cap, nnz, x, dE, part,
+                                                    coef, width, gw, partw);
       PSAMD_HIP_CHECK(hipGetLastError());
-      emb_grad_cross_kernel<1><<<grid, 256, 0, st>>>(segid, seg_start, u_cap, nnz, part, dE);
+      if (cross_batched())
+        emb_grad_cross_kernel<1, 16><<<grid, 256, 0, st>>>(segid, seg_start, u_cap, nnz, part, dE,
+                                                           partw, gw);
+      else
+        emb_grad_cross_kernel<1, 1><<<grid, 256, 0, st>>>(segid, seg_start, u_cap, nnz, part, dE,
+                                                          partw, gw);
     } else {
-      emb_grad_seg_kernel<2><<<grid, 256, 0, st>>>(pos_s, segid, seg_start, u_cap, nnz, x, dE, part);
+      emb_grad_seg_kernel<2><<<grid, 256, 0, st>>>(pos_s, segid, seg_start, u_cap, nnz, x, dE, part,
+                                                    coef, width, gw, partw);
       PSAMD_HIP_CHECK(hipGetLastError());
-      emb_grad_cross_kernel<2><<<grid, 256, 0, st>>>(segid, seg_start, u_cap, nnz, part, dE);
+      if (cross_batched())
+        emb_grad_cross_kernel<2, 8><<<grid, 256, 0, st>>>(segid, seg_start, u_cap, nnz, part, dE,
+                                                          partw, gw);
+      else
+        emb_grad_cross_kernel<2, 1><<<grid, 256, 0, st>>>(segid, seg_start, u_cap, nnz, part, dE,
+                                                          partw, gw);
     }
 #undef PSAMD_NARROW
     PSAMD_HIP_CHECK(hipGetLastError());
@@ -814,11 +913,22 @@ void emb_grad_reduce(const int32_t* pos_s, const int32_t* segid, const int32_t* 
 
 void emb_update(const int64_t* slot, int64_t n, const int32_t* n_dev, int64_t cap,
                 const float* grad, const void* grad16, void* rows, float* acc, int D, float lr,
-                float eps, hipStream_t st) {
+                float eps, void* slots, const float* gwide, const int* wide_rule,
+                const float* wide_hyper, double* stats, int acc_stripes, hipStream_t st) {
   if (n <= 0) return;
-  emb_update_kernel<<<grid_for(n, 16, 8192), 256, 0, st>>>(
-      slot, n, n_dev, cap, grad, reinterpret_cast<const uint16_t*>(grad16),
-      reinterpret_cast<uint16_t*>(rows), acc, D, lr, eps);
+  if (slots) {
+    const UpdateParams p{wide_rule[0], wide_rule[1], wide_hyper[0], wide_hyper[1], wide_hyper[2],
+                         wide_hyper[3], wide_hyper[4], wide_hyper[5]};
+    emb_update_kernel<true><<<grid_for(n, 16, 8192), 256, 0, st>>>(
+        slot, n, n_dev, cap, grad, reinterpret_cast<const uint16_t*>(grad16),
+        reinterpret_cast<uint16_t*>(rows), acc, D, lr, eps, (Slot*)slots, gwide, p, stats,
+        acc_stripes);
+  } else {
+    emb_update_kernel<false><<<grid_for(n, 16, 8192), 256, 0, st>>>(
+        slot, n, n_dev, cap, grad, reinterpret_cast<const uint16_t*>(grad16),
+        reinterpret_cast<uint16_t*>(rows), acc, D, lr, eps, nullptr, nullptr, UpdateParams{},
+        nullptr, 1);
+  }
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -25,6 +25,7 @@ Per rank (one process per GPU):
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -71,6 +72,10 @@ class EmbeddingPS:
     from their owners and push [row gradient | wide gradient] back, one packed
     all-to-all each way. Needs ``shard``, ``part``, ``comm``, ``G``, ``gpu``,
     ``stats`` and ``cfg.{embedding_dim, emb_lr, wide}`` on the host class."""
+
+    # one-shard GPU step: the wide gradient rides along the embedding gradient reduction
+    # and the wide slot update along the row update (PSAMD_WD_FUSE=0: separate passes)
+    _fuse = os.environ.get("PSAMD_WD_FUSE", "1") != "0"
 
     def localize(self, keys: torch.Tensor, buf: int = 0):
         """Localise a minibatch into workspace ``buf`` (buffer 0 = the step's own), so
@@ -290,10 +295,15 @@ class EmbeddingPS:
         if push[0] == "local":
             slot = push[1]
             n_dev = loc.n_uniq if self.gpu else None
-            if self.gpu:
+            if self.gpu and not self._fuse:
                 self.shard.update_rows(slot, grad=dE, lr=cfg.emb_lr, n_dev=n_dev)
                 hipops().kv_update(self.shard.table.slots, slot, g_wide, n_dev,
                                    *cfg.wide.args(), self.stats)
+            elif self.gpu:
+                # rows (AdaGrad) and wide slots (cfg.wide) of the same keys in ONE pass
+                hipops().emb_update(slot, n_dev, dE, None, self.shard.rows, self.shard.acc,
+                                    cfg.emb_lr, 1e-8, self.shard.table.slots, g_wide,
+                                    list(cfg.wide.args()), self.stats)
             else:
                 U = loc.num_unique()
                 self.shard.update_rows(slot[:U], grad=dE[:U], lr=cfg.emb_lr)
@@ -451,11 +461,17 @@ class WideDeepTrainer(EmbeddingPS):
         dX0 = dH  # [B, S*D]
         # ---------------- sparse gradients
         u_cap = nnz
-        if self.gpu:
-            dE = E.grad_reduce(loc, dX0, D, u_cap, out=self.dE)
+        if self.gpu and self._fuse and E.grad_wide_fused(D, True) and loc.grad is not None:
+            # the wide gradient (same segments) in the same pass over the CSC entries
+            dE = E.grad_reduce(loc, dX0, D, u_cap, out=self.dE, coef=self.coef[:B], width=S,
+                               g_wide=loc.grad)
+            g_wide = loc.grad
         else:
-            dE = E.grad_reduce(loc, dX0, D, loc.num_unique())
-        g_wide, _ = linear_backward(loc, self.coef[:B], B=B, width=S)
+            if self.gpu:
+                dE = E.grad_reduce(loc, dX0, D, u_cap, out=self.dE)
+            else:
+                dE = E.grad_reduce(loc, dX0, D, loc.num_unique())
+            g_wide, _ = linear_backward(loc, self.coef[:B], B=B, width=S)
         self._push(loc, push, dE, g_wide)
         if side is not None:
             main.wait_stream(side)

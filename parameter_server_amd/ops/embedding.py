@@ -145,14 +145,30 @@ def expand(local_col: torch.Tensor, nnz: int, src: torch.Tensor, idx=None, out=N
     return out
 
 
-def grad_reduce(loc, dX0: torch.Tensor, D: int, u_cap: int, out=None):
-    """dE[u] = sum of dX0 rows over u's occurrences (fp32 [u_cap, D])."""
+_WIDE_OK: dict[int, bool] = {}
+
+
+def grad_wide_fused(D: int, gpu: bool) -> bool:
+    """Whether ``grad_reduce`` can produce the wide gradient in the same pass."""
+    if not gpu:
+        return False
+    ok = _WIDE_OK.get(D)
+    if ok is None:  # (asked once per D: a native call per step is host issue time)
+        ok = _WIDE_OK[D] = bool(hipops().emb_grad_wide_ok(D))
+    return ok
+
+
+def grad_reduce(loc, dX0: torch.Tensor, D: int, u_cap: int, out=None, coef=None, width: int = 0,
+                g_wide=None):
+    """dE[u] = sum of dX0 rows over u's occurrences (fp32 [u_cap, D]). With ``g_wide``
+    (GPU, ``grad_wide_fused``): also g_wide[u] = sum of coef[row] over u's occurrences
+    (row = position // width, the wide part's gradient), in the same pass."""
     nnz = loc.nnz
     if out is None:
         out = torch.empty(u_cap, D, dtype=torch.float32, device=dX0.device)
     if is_gpu(dX0):
         hipops().emb_grad_reduce(loc.pos_s, loc.segid, loc.seg_start, loc.n_uniq, u_cap, nnz, dX0,
-                                 D, out)
+                                 D, out, coef, width, g_wide)
         return out
     out.zero_()
     seg = loc.segid[:nnz].long() - 1  # segid is 1-based in the localiser

@@ -129,7 +129,16 @@ def linear_input_grad(dZ, W, mask=None, backend: str = "mfma", colsum=None):
     if backend == "auto":
         backend = "hipblaslt" if mask is None and colsum is None and K >= 1024 else "mfma"
     if backend == "hipblaslt" and is_gpu(dZ):
-        dX = torch.mm(dZ, W)
+        import os
+
+        if os.environ.get("PSAMD_DX_WT", "0") == "1" and W.is_contiguous() and N % 64 == 0 \
+                and K % 64 == 0:
+            # both operands K-major (the forward's layout): a transposed weight copy
+            Wt = torch.empty(K, N, dtype=W.dtype, device=W.device)
+            hipops().transpose_bf16(W, Wt)
+            dX = torch.mm(dZ, Wt.t())
+        else:
+            dX = torch.mm(dZ, W)
         if mask is not None:
             dX.mul_(mask > 0)
         if colsum is not None:

@@ -73,6 +73,75 @@ def test_grad_reduce_segments_cross_runs(D, n, hot):
     assert torch.equal(again[:U], dE[:U]) or D == 24  # deterministic (no atomics)
 
 
+@pytest.mark.parametrize("D,B,S,hot", [(128, 3000, 39, 0), (128, 4000, 39, 60000), (256, 777, 13, 5000),
+                                       (128, 2, 39, 0), (128, 1, 1, 0)])
+def test_grad_reduce_fused_wide_gradient(D, B, S, hot):
+    """The wide gradient riding along the segmented reduction: g_wide[u] = sum of
+    coef[row] over u's occurrences (row = position // S), against an fp64 index_add;
+    dE unchanged by it; deterministic."""
+    n = B * S
+    g = torch.Generator().manual_seed(n + D)
+    k = torch.randint(0, 1 << 20, (n,), generator=g, dtype=torch.int64)
+    if hot:
+        k[torch.randperm(n, generator=g)[:min(hot, n)]] = 4242
+    loc = Localizer(n, 20, "cuda")(k.cuda())
+    U = loc.num_unique()
+    dX0 = torch.randn(n, D, generator=g).to(torch.bfloat16)
+    coef = torch.randn(B, generator=g)
+    col = loc.local_col.long().cpu()
+    ref = torch.zeros(U, dtype=torch.float64).index_add_(
+        0, col, coef.double().repeat_interleave(S))
+    gw = torch.full((n,), float("nan"), device="cuda")
+    assert E.grad_wide_fused(D, True)
+    dE = E.grad_reduce(loc, dX0.cuda(), D, n, coef=coef.cuda(), width=S, g_wide=gw)
+    torch.testing.assert_close(gw[:U].double().cpu(), ref, rtol=1e-5, atol=1e-4)
+    plain = E.grad_reduce(loc, dX0.cuda(), D, n)
+    assert torch.equal(plain[:U], dE[:U])
+    gw2 = torch.zeros_like(gw)
+    E.grad_reduce(loc, dX0.cuda(), D, n, coef=coef.cuda(), width=S, g_wide=gw2)
+    assert torch.equal(gw2[:U], gw[:U])
+
+
+@pytest.mark.parametrize("algo", ["ftrl", "adagrad", "sgd"])
+def test_fused_row_and_wide_update_is_the_two_pass_update(algo):
+    """emb_update with the wide slots (one pass) = emb_update then kv_update: rows,
+    AdaGrad accumulators and slots bitwise, stats to fp64 rounding; NaN-marked wide
+    gradients skip only the slot."""
+    from parameter_server_amd.ops.kv_table import UpdateRule
+    from parameter_server_amd.ops.native import hipops
+
+    H = hipops()
+    D, cap, n = 128, 1 << 14, 5000
+    g = torch.Generator().manual_seed(7)
+    keys = torch.randperm(1 << 30, generator=g)[:n].to(torch.int64)
+    dE = torch.randn(n, D, generator=g).cuda()
+    gw = torch.randn(n, generator=g).cuda()
+    gw[::97] = float("nan")
+    sh = E.EmbeddingShard(cap, D, "cuda", seed=3)
+    slot, _ = sh.resolve(keys.cuda())  # (one placement for both variants)
+    sh.table.slots.view(torch.float32).view(-1, 8)[:, 2:6] = 0.25  # (w, z, n, acc)
+    start = (sh.rows.clone(), sh.acc.clone(), sh.table.slots.clone())
+    runs = []
+    for fused in (False, True):
+        sh.rows.copy_(start[0])
+        sh.acc.copy_(start[1])
+        sh.table.slots.copy_(start[2])
+        rule = UpdateRule(algo=algo, alpha=0.05, beta=1.0, l1=0.01, l2=0.1)
+        stats = torch.zeros(8, dtype=torch.float64, device="cuda")
+        nd = torch.tensor([n - 3], dtype=torch.int32, device="cuda")
+        if fused:
+            H.emb_update(slot, nd, dE, None, sh.rows, sh.acc, 0.05, 1e-8, sh.table.slots, gw,
+                         list(rule.args()), stats)
+        else:
+            H.emb_update(slot, nd, dE, None, sh.rows, sh.acc, 0.05, 1e-8)
+            H.kv_update(sh.table.slots, slot, gw, nd, *rule.args(), stats)
+        torch.cuda.synchronize()
+        runs.append((sh.rows.clone(), sh.acc.clone(), sh.table.slots.clone(), stats.clone()))
+    (r0, a0, s0, st0), (r1, a1, s1, st1) = runs
+    assert torch.equal(r0, r1) and torch.equal(a0, a1) and torch.equal(s0, s1)
+    torch.testing.assert_close(st1[:3], st0[:3], rtol=1e-9, atol=1e-9)
+
+
 def test_head_colsum_adam_match_cpu():
     B, H, S = 1000, 256, 39
     torch.manual_seed(0)
