@@ -73,9 +73,12 @@ class EmbeddingPS:
     all-to-all each way. Needs ``shard``, ``part``, ``comm``, ``G``, ``gpu``,
     ``stats`` and ``cfg.{embedding_dim, emb_lr, wide}`` on the host class."""
 
-    # one-shard GPU step: the wide gradient rides along the embedding gradient reduction
-    # and the wide slot update along the row update (PSAMD_WD_FUSE=0: separate passes)
-    _fuse = os.environ.get("PSAMD_WD_FUSE", "1") != "0"
+    # one-shard GPU step, PSAMD_WD_FUSE=1: the wide gradient rides along the embedding
+    # gradient reduction and the wide slot update along the row update. Fewer kernels, but
+    # the step measured 0.963-0.971 vs 0.956-0.958 ms with separate passes on one box
+    # (the weight-gradient side stream sets the pace; profiles/r4_wide_deep_fusion_ab.log),
+    # so the separate passes stay the default
+    _fuse = os.environ.get("PSAMD_WD_FUSE", "0") == "1"
 
     def localize(self, keys: torch.Tensor, buf: int = 0):
         """Localise a minibatch into workspace ``buf`` (buffer 0 = the step's own), so

@@ -131,9 +131,12 @@ def linear_input_grad(dZ, W, mask=None, backend: str = "mfma", colsum=None):
     if backend == "hipblaslt" and is_gpu(dZ):
         import os
 
-        if os.environ.get("PSAMD_DX_WT", "0") == "1" and W.is_contiguous() and N % 64 == 0 \
+        if os.environ.get("PSAMD_DX_WT", "1") == "1" and W.is_contiguous() and N % 64 == 0 \
                 and K % 64 == 0:
-            # both operands K-major (the forward's layout): a transposed weight copy
+            # both operands K-major (the forward's layout) through a transposed weight copy
+            # (~5 us): the library's NT kernel beats its NN one on the layer-0 input
+            # gradient, wide & deep step 0.956-0.958 -> 0.939-0.948 ms
+            # (profiles/r4_wide_deep_fusion_ab.log); PSAMD_DX_WT=0: the plain product
             Wt = torch.empty(K, N, dtype=W.dtype, device=W.device)
             hipops().transpose_bf16(W, Wt)
             dX = torch.mm(dZ, Wt.t())
@@ -165,6 +168,10 @@ def linear_weight_grad(dZ, X, out=None, beta: float = 0.0, backend: str = "mfma"
     Bn, N = dZ.shape
     K = X.shape[1]
     out = torch.empty(N, K, dtype=torch.float32, device=dZ.device) if out is None else out
+    if backend == "auto":  # (PSAMD_DW_LIB=1: the library for the weight gradients, A/B)
+        import os
+
+        backend = "hipblaslt" if os.environ.get("PSAMD_DW_LIB", "0") == "1" else "mfma"
     if backend == "hipblaslt" and is_gpu(dZ):
         r = torch.mm(dZ.t(), X, out_dtype=torch.float32)
         if beta == 0.0:
