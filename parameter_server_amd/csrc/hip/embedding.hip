@@ -66,13 +66,26 @@ __global__ void __launch_bounds__(256)
 emb_init_rows_kernel(const int64_t* __restrict__ slot, const uint64_t* __restrict__ keys, int64_t n,
                      const int32_t* __restrict__ n_dev, int64_t cap, uint16_t* __restrict__ rows,
                      uint8_t* __restrict__ inited, int D, uint64_t seed, float scale) {
+  // kIR keys per group per round, their slot and flag loads issued together at clamped
+  // in-range addresses (one key per round was two dependent round trips per key)
+  constexpr int kIR = 4;
   const int64_t nn = dev_len(n_dev, n);
+  if (nn <= 0) return;
   const int g = threadIdx.x / kGroup, l = threadIdx.x % kGroup;
-  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; i < nn;
-       i += (int64_t)gridDim.x * (blockDim.x / kGroup)) {
-    const int64_t s = slot[i];
-    if (!in_range(s, cap) || inited[s]) continue;
-    init_row(rows, s, keys[i], D, seed, scale, l, inited);
+  const int64_t stride = (int64_t)gridDim.x * (blockDim.x / kGroup);
+  for (int64_t i0 = (int64_t)blockIdx.x * (blockDim.x / kGroup) + g; i0 < nn; i0 += kIR * stride) {
+    int64_t sv[kIR];
+#pragma unroll
+    for (int q = 0; q < kIR; ++q) sv[q] = slot[min(i0 + q * stride, nn - 1)];
+    uint8_t fv[kIR];
+#pragma unroll
+    for (int q = 0; q < kIR; ++q) fv[q] = inited[in_range(sv[q], cap) ? sv[q] : 0];
+#pragma unroll
+    for (int q = 0; q < kIR; ++q) {
+      const int64_t i = i0 + q * stride;
+      if (i < nn && in_range(sv[q], cap) && !fv[q])
+        init_row(rows, sv[q], keys[i], D, seed, scale, l, inited);
+    }
   }
 }
 
