@@ -776,16 +776,21 @@ gemm_splitk_reduce_kernel(const float4* __restrict__ P, int S, int64_t n4, float
   }
 }
 
+// phase: 0 = GEMM + split-K reduce, 1 = the GEMM into `part` only, 2 = the reduce only
+// (a caller can hold the reduce back so that a later GEMM is not queued behind it)
 void gemm_tn256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
-                int splits, float* part, float* out, float beta, hipStream_t st) {
+                int splits, float* part, float* out, float beta, int phase, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   if (splits < 1 || K % g256::BK != 0 || K / g256::BK < splits || M % 8 || N % 8 || lda % 8 ||
       ldb % 8)
     throw std::runtime_error("gemm_tn256: K % 64, K / 64 >= splits, M / N / ld % 8");
   const int tiles_m = (M + g256::BM - 1) / g256::BM, tiles_n = (N + g256::BN - 1) / g256::BN;
   dim3 grid(tiles_m * tiles_n, splits);
-  gemm_tn256_kernel<<<grid, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, part, tiles_n);
-  PSAMD_HIP_CHECK(hipGetLastError());
+  if (phase != 2) {
+    gemm_tn256_kernel<<<grid, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, part, tiles_n);
+    PSAMD_HIP_CHECK(hipGetLastError());
+  }
+  if (phase == 1) return;
   const int64_t n4 = (int64_t)M * N / 4;
   gemm_splitk_reduce_kernel<<<grid_for(n4, 256, 4096), 256, 0, st>>>(
       reinterpret_cast<const float4*>(part), splits, n4, reinterpret_cast<float4*>(out), beta);

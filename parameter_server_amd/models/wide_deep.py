@@ -79,6 +79,7 @@ class EmbeddingPS:
     # (the weight-gradient side stream sets the pace; profiles/r4_wide_deep_fusion_ab.log),
     # so the separate passes stay the default
     _fuse = os.environ.get("PSAMD_WD_FUSE", "0") == "1"
+    _defer_reduce = os.environ.get("PSAMD_WD_DEFER_REDUCE", "0") == "1"
 
     def localize(self, keys: torch.Tensor, buf: int = 0):
         """Localise a minibatch into workspace ``buf`` (buffer 0 = the step's own), so
@@ -448,12 +449,16 @@ class WideDeepTrainer(EmbeddingPS):
         # chip overlap); the side stream joins before the dense all-reduce / Adam.
         side = self._side if self.gpu and cfg.overlap_wgrad else None
         main = torch.cuda.current_stream(dev) if side is not None else None
+        # PSAMD_WD_DEFER_REDUCE=1: the split-K reduces of the weight gradients wait at the
+        # end of the side stream, so layer 0's weight-gradient GEMM follows layer 1's at once
+        # instead of queueing behind a memory-bound reduce that the input-gradient GEMM starves
+        deferred = [] if side is not None and self._defer_reduce else None
         for i in reversed(range(L)):
             if side is not None:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
                     GM.linear_weight_grad(dH, acts[i], out=self.dW[i], beta=1.0,
-                                          backend=cfg.gemm)
+                                          backend=cfg.gemm, deferred=deferred)
                 dH.record_stream(side)
                 acts[i].record_stream(side)
             else:
@@ -476,6 +481,10 @@ class WideDeepTrainer(EmbeddingPS):
                 dE = E.grad_reduce(loc, dX0, D, loc.num_unique())
             g_wide, _ = linear_backward(loc, self.coef[:B], B=B, width=S)
         self._push(loc, push, dE, g_wide)
+        if deferred:
+            with torch.cuda.stream(side):
+                for fn in deferred:
+                    fn()
         if side is not None:
             main.wait_stream(side)
         # ---------------- dense update: one all-reduce, fused Adam

@@ -163,8 +163,12 @@ def linear_input_grad(dZ, W, mask=None, backend: str = "mfma", colsum=None):
     return gemm(dZ, True, W, False, Bn, K, N, mask=mask, colsum=colsum)
 
 
-def linear_weight_grad(dZ, X, out=None, beta: float = 0.0, backend: str = "mfma"):
-    """dZ [B, N], X [B, K] -> dW = dZ^T X [N, K] fp32 (``out`` accumulates with ``beta``)."""
+def linear_weight_grad(dZ, X, out=None, beta: float = 0.0, backend: str = "mfma",
+                       deferred=None):
+    """dZ [B, N], X [B, K] -> dW = dZ^T X [N, K] fp32 (``out`` accumulates with ``beta``).
+    ``deferred`` (a list): where the 256x256 TN kernel runs, only its GEMM is issued and
+    the split-K reduce is appended to the list as a callable for the caller to issue
+    later (on the same stream), so the next layer's GEMM is not queued behind it."""
     Bn, N = dZ.shape
     K = X.shape[1]
     out = torch.empty(N, K, dtype=torch.float32, device=dZ.device) if out is None else out
@@ -187,6 +191,11 @@ def linear_weight_grad(dZ, X, out=None, beta: float = 0.0, backend: str = "mfma"
         # (gemm256.hip gemm_tn256), split-K partials summed in a fixed order
         S = tn256_splits(N, K, Bn)
         part = torch.empty(S * N * K, dtype=torch.float32, device=dZ.device)
+        if deferred is not None:
+            H = hipops()
+            H.gemm_tn256(dZ, X, N, K, Bn, S, part, out, float(beta), 1)
+            deferred.append(lambda: H.gemm_tn256(dZ, X, N, K, Bn, S, part, out, float(beta), 2))
+            return out
         hipops().gemm_tn256(dZ, X, N, K, Bn, S, part, out, float(beta))
         return out
     sk = auto_splitk(N, K, Bn) if beta in (0.0, 1.0) else 1
