@@ -461,7 +461,8 @@ class SparseLRTrainer:
             raise ValueError("prep_plan needs the flat (tpf) localisation")
         while len(self._localizers) <= buf:
             self._localizers.append(Localizer(self.max_nnz, self.bits, self.device,
-                                              mode=self.localize_mode, lazy_cols=True))
+                                              mode=self.localize_mode, lazy_cols=True,
+                                              sorted_keys=self._flat_x))
         lz = self._localizers[buf]
         f = lz.flat
         B = labels.numel()
@@ -472,7 +473,7 @@ class SparseLRTrainer:
         plan.add_criteo_gen(seed & ((1 << 64) - 1), row0, row_step, B, num_features, alpha, keys,
                             labels)
         plan.add_localize_tpf(keys, n, self.bits, lz.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos,
-                              f.ent_j, f.cnt, f.err, False)
+                              f.ent_j, f.cnt, f.err, self._flat_x)
 
         def run():
             plan.run()
@@ -1288,10 +1289,41 @@ class SparseLRTrainer:
         self.table.update(s, g, self.rule, self.stats)
 
     # ------------------------------------------------------------ reporting
+    def check_ok(self):
+        """Host sync: raise if any device-side capacity was exceeded since the start --
+        the table (full: a key could not be inserted), a localisation workspace (a tile
+        or bucket overflowed its LDS hash or its fixed entry region: the step kernels
+        would have dropped those occurrences' gradients and read stale weights) or the
+        padded exchange rows. All error words are sticky, so a check at any later point
+        still sees an overflow. Called by ``progress()`` and by bench.py after timing
+        (same fail-loudly rule as the exchange overflow, ``_x_poll_overflow``)."""
+        if not self.gpu:
+            return
+        lzs = list(self._localizers) + ([self._compact] if self._compact is not None else [])
+        words = [self.table._err] + [lz.err for lz in lzs if getattr(lz, "err", None) is not None]
+        if self.xc is not None and getattr(self.xc, "ovf", None) is not None:
+            words.append(self.xc.ovf)
+        v = torch.cat([w.reshape(-1)[:1] for w in words]).cpu().tolist()
+        if v[0]:
+            raise RuntimeError("KVTable full: increase table_capacity (keys were not inserted)")
+        for lz, e in zip([lz for lz in lzs if getattr(lz, "err", None) is not None], v[1:]):
+            if e:
+                raise RuntimeError(
+                    f"localize_{lz.mode} overflow (error bits {e:#x}): a tile or bucket "
+                    f"exceeded its LDS hash / entry region, so some occurrences were dropped "
+                    f"from the step; the minibatch is too skewed for the {lz.mode} layout "
+                    f"(PSAMD_FLAT=0 or localize='sort')")
+        if self.xc is not None and getattr(self.xc, "ovf", None) is not None and v[-1]:
+            raise RuntimeError(
+                f"exchange overflow: {v[-1]} keys exceeded the per-peer capacity {self.xc.C}; "
+                f"set exchange_capacity or exchange_slack higher, or exchange='exact'")
+
     def progress(self, reset: bool = True) -> dict:
         """Merged progress across ranks (reference ISGDScheduler::showProgress, sgd.h:45-80).
-        Collective when G > 1 (also applies deferred pushes)."""
+        Collective when G > 1 (also applies deferred pushes). Raises on a device-side
+        overflow (``check_ok``) instead of reporting a silently corrupted run."""
         self.flush()
+        self.check_ok()
         m = torch.cat([accum_total(self.metrics)[:8], accum_total(self.stats)[:3]])
         if self.G > 1:
             m = self.comm.all_reduce_(m.to(self.comm.device) if self.comm.backend == "nccl"

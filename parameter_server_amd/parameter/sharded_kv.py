@@ -646,18 +646,25 @@ class KVWorker:
 
     def wait(self, ts: int):
         """Order the caller's stream after op ``ts``; pulled values (or None)."""
-        out, ev = self._done.pop(ts)
-        if ev is not None:
-            torch.cuda.current_stream(self.device).wait_event(ev)
+        out = self._wait_nocheck(ts)
         self.check()  # (an overflow published by a completed pack raises here)
         return out
 
+    def _wait_nocheck(self, ts: int):
+        out, ev = self._done.pop(ts)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+        return out
+
     def flush(self):
-        """Apply every pending push (end of a training phase)."""
+        """Apply every pending push (end of a training phase). Collective: the overflow
+        check after the drain takes the largest count of all ranks, so every rank raises
+        together (a rank-local check first would let one rank raise while its peers wait
+        for it in the host gather)."""
         def op():
             self._drain(keep=0)
 
-        out = self.wait(self._run(op))
+        out = self._wait_nocheck(self._run(op))
         self.check(sync=True, collective=True)
         return out
 

@@ -85,3 +85,23 @@ def maybe_inject(rank: int, step: int) -> None:
         print(f"[psamd] injected stall: rank {rank} sleeps {sec} s at step {step}",
               file=sys.stderr, flush=True)
         time.sleep(float(sec))
+
+
+def maybe_inject_post(rank: int) -> None:
+    """Fault injection after the timed region (tests/test_bench_spawn.py):
+    ``PSAMD_INJECT_POST_EXIT=rank:code`` exits that rank with ``code`` right after the
+    report; ``PSAMD_INJECT_TEARDOWN_HANG=rank:sec`` sleeps there (a teardown hang)."""
+    spec = os.environ.get("PSAMD_INJECT_POST_EXIT")
+    if spec:
+        r, code = spec.split(":")
+        if int(r) == rank:
+            print(f"[psamd] injected post-timing exit {code} on rank {rank}", file=sys.stderr,
+                  flush=True)
+            os._exit(int(code))
+    spec = os.environ.get("PSAMD_INJECT_TEARDOWN_HANG")
+    if spec:
+        r, sec = spec.split(":")
+        if int(r) == rank:
+            print(f"[psamd] injected teardown hang: rank {rank} sleeps {sec} s", file=sys.stderr,
+                  flush=True)
+            time.sleep(float(sec))

@@ -142,3 +142,54 @@ def test_bench_captured_collectives_exit_cleanly(consistency):
     assert out["config"]["hip_graph"] and out["config"]["emulated_peers"] == 4
     assert out["config"]["collectives_in_graphs"]
     assert out["comm"]["rccl_world"] == 1
+
+
+@pytest.mark.parametrize("nprep,native", [(1, "0"), (2, "0"), (2, "1"), (3, "1")])
+def test_flat_pipeline_matches_sequential(monkeypatch, nprep, native):
+    """1 GPU, flat layout: step t pulls minibatch t+1 inside its update launch, so every
+    preparation must finish before the step that pulls it and must not refill a buffer a
+    pending step still reads (nprep = 1 is run with 2 streams). The pipeline -- eager
+    launch lists or the one-call native iteration -- must leave exactly the table that
+    plain sequential ``step()`` calls leave."""
+    from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+    from parameter_server_amd.ops.synthetic import criteo_batch
+
+    monkeypatch.setenv("PSAMD_FLAT", "1")
+    monkeypatch.setenv("PSAMD_NATIVE_ITER", native)
+    bench = _bench()
+    B, N, seed, extra = 4096, 10 ** 8, 91, 7
+    dev = torch.device("cuda")
+
+    def trainer():
+        cfg = SparseLRConfig(num_features=N, minibatch=B, table_capacity=1 << 22)
+        tr = SparseLRTrainer(cfg, device=dev)
+        assert tr.localize_mode == "tpf" and not tr.padded
+        return tr
+
+    tr = trainer()
+    keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
+    labels = torch.empty(B, dtype=torch.float32, device=dev)
+    args = argparse.Namespace(warmup=0, graph=0, prep_streams=nprep)
+    it, _ = bench.pipeline(tr, B, N, seed, keys, labels, dev, args, nprep=nprep)
+    assert args.prep_streams >= 2
+    assert (getattr(args, "native_iter", False) is True) == (native == "1")
+    for _ in range(extra):
+        it()
+    torch.cuda.synchronize()
+    T = tr.step_count
+    pk, pw = _weights(tr)
+    loss_p = tr.progress()["loss"]
+    ref = trainer()
+    for m in range(T):
+        k, lab = criteo_batch(B, seed=seed, row0=m * B, num_features=N, device=dev)
+        ref.step(k, lab, width=39)
+    torch.cuda.synchronize()
+    rk, rw = _weights(ref)
+    # the pipeline also pulled (inserted, w = 0) the minibatch after the last step
+    pos = torch.searchsorted(pk, rk)
+    assert torch.equal(pk[pos], rk)
+    assert torch.equal(pw[pos], rw)
+    extra_mask = torch.ones(pk.numel(), dtype=torch.bool)
+    extra_mask[pos] = False
+    assert torch.all(pw[extra_mask] == 0)
+    assert abs(loss_p - ref.progress()["loss"]) < 1e-5

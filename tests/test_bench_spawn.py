@@ -82,3 +82,47 @@ def test_bench_failed_captured_attempt_reruns_eagerly():
     assert len(lines) == 1, out.stdout
     r = json.loads(lines[0])
     assert r["n_gpus"] == 3 and r["comm"]["fallback"] == 3 and r["comm"]["captured"] is False
+
+
+def _spawn_env(**extra):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update(extra)
+    return env
+
+
+def test_bench_post_timing_rank_failure_is_reported():
+    """A rank that exits non-zero AFTER the timed region (rank 2, injected) does not void
+    the measurement, but the JSON line records which rank failed with what code."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "3",
+                          "--steps", "2", "--warmup", "1", "--minibatch", "1024",
+                          "--num-features", "1e6"],
+                         capture_output=True, text=True, timeout=300, cwd=ROOT,
+                         env=_spawn_env(PSAMD_INJECT_POST_EXIT="2:7"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["comm"]["post_timing_failures"] == [2]
+    assert r["comm"]["rank_exit_codes"][2] == 7
+    assert "re-running" not in out.stderr  # a complete measurement is not re-run
+
+
+def test_bench_teardown_hang_is_capped():
+    """A rank hanging after the timed region is killed PSAMD_TEARDOWN_TIMEOUT seconds
+    after it passed the timed region, not at the attempt limit."""
+    import time
+
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--gpus", "2",
+                          "--steps", "2", "--warmup", "1", "--minibatch", "1024",
+                          "--num-features", "1e6"],
+                         capture_output=True, text=True, timeout=300, cwd=ROOT,
+                         env=_spawn_env(PSAMD_INJECT_TEARDOWN_HANG="1:600",
+                                        PSAMD_TEARDOWN_TIMEOUT="5"))
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert time.time() - t0 < 150
+    r = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    assert r["comm"]["post_timing_failures"] == [1]
+    assert r["comm"]["rank_exit_codes"][1] == 125

@@ -290,6 +290,37 @@ def test_gloo_crossed_registration_gets_new_handle(tmp_path):
         np.testing.assert_allclose(r["got"], 3.0)
 
 
+def _ovf_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from parameter_server_amd.ops.keymix import unmix
+    from parameter_server_amd.parallel.comm import DistComm
+
+    n = 2048
+    kv = KVWorker(DistComm("cpu"), "cpu", capacity=1 << 14, max_keys=n, key_bits=64)
+    # rank 0 overflows its row to owner 0; rank 1 pushes keys that fit
+    keys = unmix(torch.arange(n if rank == 0 else 64, dtype=torch.int64), 64)
+    kv.push(keys, torch.ones(keys.numel()))
+    raised = False
+    try:
+        kv.flush()
+    except RuntimeError as e:
+        raised = "overflow" in str(e)
+    torch.save({"raised": raised}, os.path.join(out_dir, f"o{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_gloo_flush_overflow_raises_on_every_rank(tmp_path):
+    """flush() must not run a rank-local overflow check before its collective
+    one, or the overflowing rank raises alone and its peers hang in the host gather."""
+    port = _port()
+    mp.spawn(_ovf_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    res = [torch.load(tmp_path / f"o{r}.pt", weights_only=False) for r in range(2)]
+    assert all(r["raised"] for r in res), res
+
+
 @pytest.mark.gpu
 def test_skewed_keys_overflow_raises_gpu():
     """Device path: the pack kernel counts the dropped keys and publishes the count to

@@ -40,6 +40,42 @@ def _skewed_batch(step: int, bits: int = 20, B: int = 2048, width: int = 16):
     return keys, labels
 
 
+def _overflow_batch(B: int = 2048, width: int = 16, bits: int = 20):
+    """A minibatch that no flat bucket unit can hold: 2500 distinct keys of the first
+    fine bucket (> the 2048-key unit hash) in each of the 4 tiles (10,000 entries > the
+    8192-entry region)."""
+    g = torch.Generator().manual_seed(5)
+    n = B * width
+    shift = bits - 5
+    hot = torch.randperm(1 << shift, generator=g)[:2500]
+    mixed = torch.randint(1 << (shift + 1), 1 << bits, (n,), generator=g)
+    for t in range(n // TP_TILE):
+        pos = t * TP_TILE + torch.randperm(TP_TILE, generator=g)[:hot.numel()]
+        mixed[pos] = hot
+    keys = unmix(mixed.to(DEV), bits)
+    labels = torch.where(torch.rand(B, generator=g) < 0.3, 1.0, -1.0).to(DEV)
+    return keys, labels
+
+
+def test_flat_localizer_overflow_fails_loudly(monkeypatch):
+    """A localisation overflow (entries dropped from the flat regions) must not train
+    silently: progress() and check_ok() raise."""
+    monkeypatch.setenv("PSAMD_FLAT", "1")
+    keys, labels = _overflow_batch()
+    B = labels.numel()
+    cfg = SparseLRConfig(num_features=1 << 20, minibatch=B, max_nnz_per_example=16,
+                         table_capacity=1 << 22)
+    tr = SparseLRTrainer(cfg, device=DEV)
+    assert tr.localize_mode == "tpf"
+    tr.step(keys, labels, width=16)
+    torch.cuda.synchronize()
+    assert int(tr.localizer.err.item()) != 0
+    with pytest.raises(RuntimeError, match="localize_tpf overflow"):
+        tr.progress()
+    with pytest.raises(RuntimeError, match="overflow"):
+        tr.check_ok()
+
+
 def _flat_entry_keys(f, n):
     """tile entry id -> mixed key, from the flat regions (host side)."""
     H = hipops()
