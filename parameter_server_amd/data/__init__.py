@@ -138,8 +138,12 @@ class StreamReader:
 
     def __init__(self, files, fmt="LIBSVM", minibatch=1000, *, ignore_slot=False,
                  data_buf_mb=1000, hash_mod=0, passes=1, shuffle=False, seed=0, hadoop_home="",
-                 max_lines_per_file=-1, recordio=False):
+                 max_lines_per_file=-1, recordio=False, max_nnz=0, nthreads=4):
         self.files = list(files)
+        # a minibatch also ends before it exceeds max_nnz features (0 = no cap): a
+        # device consumer sizes its workspaces for minibatch rows x a per-row bound
+        self.max_nnz = int(max_nnz)
+        self.nthreads = int(nthreads)
         self.fmt = fmt
         self.minibatch = minibatch
         self.ignore_slot = ignore_slot
@@ -175,20 +179,38 @@ class StreamReader:
                     b = decode_examples(raw)
                 else:
                     b = parse_text(raw, self.fmt, ignore_slot=self.ignore_slot,
-                                   hash_mod=self.hash_mod, max_lines=self.max_lines)
+                                   hash_mod=self.hash_mod, max_lines=self.max_lines,
+                                   nthreads=self.nthreads)
                 pending.append(b)
                 have += b.rows
-                while have >= self.minibatch:
+                nnz = sum(x.nnz for x in pending)
+                while have >= self.minibatch or (self.max_nnz and nnz > self.max_nnz):
                     allb = ExampleBatch.concat(pending)
-                    self._put(allb.slice_rows(0, self.minibatch))
-                    rest = allb.slice_rows(self.minibatch, allb.rows)
+                    r = self._cut(allb)
+                    self._put(allb.slice_rows(0, r))
+                    rest = allb.slice_rows(r, allb.rows)
                     pending, have = ([rest], rest.rows) if rest.rows else ([], 0)
-            if have:
-                self._put(ExampleBatch.concat(pending))
+                    nnz = rest.nnz if rest.rows else 0
+            while have:
+                allb = ExampleBatch.concat(pending)
+                r = self._cut(allb)
+                self._put(allb.slice_rows(0, r))
+                rest = allb.slice_rows(r, allb.rows)
+                pending, have = ([rest], rest.rows) if rest.rows else ([], 0)
         except BaseException as e:  # noqa: BLE001  (re-raised by the consumer)
             self._error = e
         finally:
             self._q.push(None, 0, finished=True)
+
+    def _cut(self, b: ExampleBatch) -> int:
+        """Rows of the next minibatch: <= minibatch rows and <= max_nnz features."""
+        r = min(self.minibatch, b.rows)
+        if self.max_nnz and int(b.row_ptr[r]) > self.max_nnz:
+            r = int(np.searchsorted(b.row_ptr, self.max_nnz, side="right")) - 1
+            if r < 1:
+                raise ValueError(f"an example has {int(b.row_ptr[1])} features > the "
+                                 f"per-minibatch capacity {self.max_nnz}")
+        return r
 
     def _put(self, b):
         self._q.push(b, max(1, b.keys.nbytes + b.labels.nbytes + b.row_ptr.nbytes))

@@ -294,10 +294,7 @@ class SparseLRTrainer:
                 return
             # not expressible on the flat layout (valued / variable-width rows): the same
             # keys through a compact "tp" localisation and the generic step below
-            if self._compact is None:
-                self._compact = Localizer(self.max_nnz, self.bits, self.device, mode="tp",
-                                          lazy_cols=True)
-            loc = self._compact(keys)
+            loc = self._compact_localizer()(keys)
         if self.p2p:
             if loc is None:
                 loc = self.localizer(keys)
@@ -305,7 +302,11 @@ class SparseLRTrainer:
         if self.padded:
             if loc is None:
                 with trace_range("localize"):
-                    loc = self.localizer(keys)
+                    if self.localize_mode == "tpf" and (row_ptr is not None or rows is not None
+                                                        or vals is not None):
+                        loc = self._compact_localizer()(keys)  # (flat: fixed width only)
+                    else:
+                        loc = self.localizer(keys)
             segs = self.step_segments(keys, labels, width=width, row_ptr=row_ptr, vals=vals,
                                       rows=rows, loc=loc)
             for kind, fn in segs:
@@ -328,9 +329,8 @@ class SparseLRTrainer:
                 self.step_count += 1
                 self.examples += B
                 return
-        if row_ptr is not None and rows is None and self.gpu:
-            rows = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
-            hipops().csr_rows(row_ptr, rows)
+        if row_ptr is not None and rows is None:
+            rows = self._csr_rows(row_ptr, keys.numel())
         if loc is None:
             with trace_range("localize"):
                 loc = self.localizer(keys)
@@ -389,6 +389,24 @@ class SparseLRTrainer:
             auc_from_hist(self.hist, self.metrics, self.step_dev)
         self.step_count += 1
         self.examples += B
+
+    def _csr_rows(self, row_ptr: torch.Tensor, nnz: int) -> torch.Tensor:
+        """Row id of every CSR position (int32)."""
+        if self.gpu:
+            rows = torch.empty(nnz, dtype=torch.int32, device=row_ptr.device)
+            hipops().csr_rows(row_ptr, rows)
+            return rows
+        B = row_ptr.numel() - 1
+        return torch.repeat_interleave(torch.arange(B, dtype=torch.int32),
+                                       (row_ptr[1:] - row_ptr[:-1]).long())
+
+    def _compact_localizer(self) -> Localizer:
+        """Flat mode: the "tp" Localizer for minibatches the flat layout cannot express
+        (valued or variable-width rows)."""
+        if self._compact is None:
+            self._compact = Localizer(self.max_nnz, self.bits, self.device, mode="tp",
+                                      lazy_cols=True)
+        return self._compact
 
     # ----------------------------------------------- flat 1-GPU step (Localizer "tpf")
     _FLAT_WIDTHS: dict = {}
@@ -521,8 +539,22 @@ class SparseLRTrainer:
         return plan
 
     # --------------------------------------------- padded exchange (G > 1, default)
+    def idle_step(self):
+        """A key-less step (multi-rank file-fed runs, app/gpu.py): a rank whose data ran
+        out still joins the exchanges -- it owns a key range, so it resolves its peers'
+        pulls, applies their pushes and ships its own last pushes -- without pulling,
+        computing or pushing anything itself. Collective on the padded exchange; a no-op
+        on one rank."""
+        if self.G == 1:
+            return
+        if not self.padded:
+            raise NotImplementedError("key-less steps need the padded exchange")
+        for _, fn in self.step_segments(None, None, idle=True):
+            fn()
+
     def step_segments(self, keys: torch.Tensor, labels: torch.Tensor, *, width=None,
-                      row_ptr=None, vals=None, rows=None, loc=None, step=None, next_loc=None):
+                      row_ptr=None, vals=None, rows=None, loc=None, step=None, next_loc=None,
+                      idle: bool = False):
         """The step as an ordered list of ``(kind, fn)``: ``"compute"`` segments are
         pure device work on fixed buffers (capturable in a HIP graph per localisation
         buffer and ring position), ``"comm"`` segments are the two equal-split RCCL
@@ -554,6 +586,8 @@ class SparseLRTrainer:
             return [("compute", lambda: self.step(keys, labels, width=width, row_ptr=row_ptr,
                                                   vals=vals, rows=rows, loc=loc,
                                                   next_loc=next_loc))]
+        if idle:
+            return self._idle_segments()
         if loc is None:
             loc = self.localizer(keys)
         B = labels.numel()
@@ -564,12 +598,10 @@ class SparseLRTrainer:
                          and self._flat_ok(B, width, loc.nnz)
                          and hipops().tpf_exchange_ok(loc.nnz, self.bits, self.G)):
             # not expressible on the flat layout: the same keys, localised compactly
-            if self._compact is None:
-                self._compact = Localizer(self.max_nnz, self.bits, self.device, mode="tp",
-                                          lazy_cols=True)
-            loc, flat = self._compact(keys), False
-        if row_ptr is not None and rows is None and self.gpu:
-            rows = torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
+            loc, flat = self._compact_localizer()(keys), False
+        if row_ptr is not None and rows is None:
+            rows = (torch.empty(keys.numel(), dtype=torch.int32, device=keys.device) if self.gpu
+                    else self._csr_rows(row_ptr, keys.numel()))
         if self.xc is None:
             self._xc_setup(loc)
         comm, xc = self.comm, self.xc
@@ -614,6 +646,50 @@ class SparseLRTrainer:
                  ("host", host)]
         return segs
 
+    def _idle_segments(self):
+        """step_segments of a key-less step: the same exchange half with no keys packed
+        (the carried gradients still travel) and, for the worker half, no gradients of
+        this step (its row's gradient count is cleared)."""
+        if self.xc is None:
+            self._xc_setup(None)
+        comm, xc = self.comm, self.xc
+        t = self._xt
+        r, gb = self.sched.ring(t), self.sched.grad_ring(t)
+
+        def clear(buf, keys, grads):
+            if self.gpu:
+                hipops().xchg_clear_counts(buf, xc.H, keys, grads)
+                return
+            for p in range(self.G):
+                if keys:
+                    buf[p * xc.H] = 0
+                if grads:
+                    buf[p * xc.H + 1] = 0
+
+        def host():
+            self.step_count += 1
+            self._xt += 1
+            self._x_poll_overflow()
+
+        def exchanged():
+            self._xx += 1
+
+        segs = [("compute", lambda: clear(xc.sends[gb], True, False)),
+                ("comm", lambda: comm.all_to_all_fixed(xc.sends[gb], xc.recvs[r]))]
+        if self.asp:
+            segs += [("compute", lambda: self._x_resolve(r)),
+                     ("async", lambda: self._x_apply(r, gb))]
+        elif self.sched.post:
+            segs += [("compute", lambda: self._x_resolve(r))]
+        else:
+            segs += [("compute", lambda: (self._x_apply(r, gb), self._x_resolve(r)))]
+        segs += [("comm", lambda: comm.all_to_all_fixed(xc.wsend, xc.wrecvs[r])),
+                 ("host", exchanged)]
+        if self.sched.post:
+            segs += [("post", lambda: self._x_apply(r, gb))]
+        segs += [("compute", lambda: clear(xc.sends[r], False, True)), ("host", host)]
+        return segs
+
     @property
     def EXCHANGE_SEGMENTS(self) -> int:  # step_segments()[:n] = exchange half
         return 6 if self.asp or self.sched.post else 5
@@ -644,7 +720,12 @@ class SparseLRTrainer:
 
         cfg, G, dev, R = self.cfg, self.G, self.device, self.R
         C = int(cfg.exchange_capacity)
-        if C <= 0 and getattr(loc, "flat", False):
+        if C <= 0 and loc is None:  # a key-less first step (idle_step): join with count 0
+            cnt = torch.zeros(1, dtype=torch.float64)
+            cnt = self.comm.all_reduce_(cnt.to(self.comm.device) if self.comm.backend == "nccl"
+                                        else cnt, op="max")
+            C = int(math.ceil(float(cnt.item()) * cfg.exchange_slack)) + 1024
+        elif C <= 0 and getattr(loc, "flat", False):
             # keys per owner: the owner's buckets' unit counts (buckets [p * B/G, ...))
             g = hipops().tpf_groups(loc.nnz, loc.bits)
             c = loc.cnt[:4 * g].view(G, g // G, 4).to(torch.float64)
