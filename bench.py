@@ -72,6 +72,9 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     from parameter_server_amd.ops.synthetic import criteo_batch
     from parameter_server_amd.parallel.consistency import EventClock
 
+    if getattr(tr, "merged", False):  # one all-to-all per step (lag >= 1)
+        return pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=nprep,
+                               watch=watch)
     # 1 GPU, flat layout: step t also pulls minibatch t+1 (in its update launch), and each
     # preparation (generator + tile + flat bucket kernels) is ONE native launch-list call:
     # buffer b holds minibatches b, b + NB, ... = rows (b + k * NB) * B
@@ -491,6 +494,203 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     return iterate, True
 
 
+def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=None):
+    """The multi-GPU pipeline on the merged exchange (one all-to-all per step,
+    ``SparseLRTrainer.mx_exchange`` / ``mx_worker``, parallel/consistency.MergedSchedule).
+
+    Exchange s carries keys(s+1), the pushes of step s-d and the weights of keys(s); it
+    runs on the preparation stream of minibatch s+1 (right behind its localisation):
+
+      pack keys(s+1) -> [wait: resolve after exchange s-1, worker s-d] -> all-to-all
+      -> (event: worker s may start) -> [post: wait apply of exchange s-1]
+      -> owner resolve keys(s+1) -> (event) -> owner apply of step s-d -> (event)
+
+    and is issued ``xd`` iterations ahead of the worker half that needs it, so the
+    chain all-to-all -> resolve -> all-to-all runs while the main stream trains. The
+    worker half of step t waits only for the all-to-all of exchange t. Every piece
+    replays from a HIP graph per phase (t % lcm(buffers, ring)), the all-to-all graphs
+    ordered on the communicator's device chain. Returns (run, graph_used)."""
+    import math
+
+    from parameter_server_amd.ops.synthetic import criteo_batch
+
+    ms = tr.msched
+    R, d = ms.R, ms.d
+    NB = 2 * nprep
+    P = NB * R // math.gcd(NB, R)
+    main = torch.cuda.current_stream(device)
+    set_stream = torch.cuda.set_stream
+    prio = int(os.environ.get("PSAMD_PREP_PRIORITY", "-1"))
+    sides = [torch.cuda.Stream(device, priority=prio) for _ in range(nprep)]
+    bufs = [(keys, labels)] + [(torch.empty_like(keys), torch.empty_like(labels))
+                               for _ in range(NB - 1)]
+    hctr = [0] * nprep
+    ctr = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(nprep)]
+    locs = [None] * NB
+    mode = {"capture": False}
+    tr._mx_external = True  # progress() must not drain: the exchanges below are in flight
+
+    def prep(b):
+        sidx = b % nprep
+        k, lab = bufs[b]
+        if mode["capture"]:
+            criteo_batch(B, seed=seed, row0=sidx * B, num_features=N, device=device, keys=k,
+                         labels=lab, row0_dev=ctr[sidx], row_scale=nprep * B)
+            ctr[sidx].add_(1)
+        else:
+            criteo_batch(B, seed=seed, row0=(hctr[sidx] * nprep + sidx) * B, num_features=N,
+                         device=device, keys=k, labels=lab)
+            hctr[sidx] += 1
+        locs[b] = tr.localize(k, buf=b)
+
+    xd = max(1, min(d, nprep - 1, int(os.environ.get("PSAMD_XD", "2"))))
+    E = 64
+    ev = {k: [torch.cuda.Event() for _ in range(E)] for k in ("w", "M", "res", "app")}
+    ev_buf = [torch.cuda.Event() for _ in range(NB)]
+    ev_prep = [torch.cuda.Event() for _ in range(NB)]
+    graphs = {"on": False}
+    gx = {}   # phase -> dict of replays (pack, comm, resolve, apply)
+    gw = {}   # phase -> worker replay
+    cchain = getattr(tr.comm, "chain", None)
+
+    def xparts(s):
+        j = s % P
+        if graphs["on"] and j in gx:
+            return gx[j]
+        return tr.mx_exchange(s, locs[(s + 1) % NB])
+
+    def wpart(t):
+        j = t % P
+        if graphs["on"] and j in gw:
+            return gw[j]
+        b = t % NB
+        return tr.mx_worker(t, locs[b], bufs[b][1], width=39)
+
+    def issue_exchange(s):
+        xs = sides[((s + 1) % NB) % nprep]  # the stream that localised minibatch s+1
+        set_stream(xs)
+        try:
+            parts = xparts(s)
+            parts["pack"]()
+            if s - d >= 0:
+                xs.wait_event(ev["w"][(s - d) % E])     # grads(s-d) packed
+            if s >= 0:
+                xs.wait_event(ev["res"][(s - 1) % E])   # weights(s) in the send rows
+                xs.wait_event(ev["app"][(s - 1) % E])
+            parts["comm"]()
+            ev["M"][s % E].record(xs)
+            if parts["post"]:
+                parts["resolve"]()
+                ev["res"][s % E].record(xs)
+                parts["apply"]()
+            else:
+                parts["apply"]()
+                parts["resolve"]()
+                ev["res"][s % E].record(xs)
+            ev["app"][s % E].record(xs)
+        finally:
+            set_stream(main)
+
+    state = {"t": 0}
+
+    def iterate():
+        t = state["t"]
+        if watch is not None and not graphs["on"]:
+            watch.beat("pipeline-warmup", t)
+        cur = t % NB
+        main.wait_event(ev["M"][t % E])
+        wpart(t)()
+        tr.mx_done(B)
+        ev["w"][t % E].record(main)
+        ev_buf[cur].record(main)
+        nb = (t + nprep) % NB
+        s_ = sides[nb % nprep]
+        s_.wait_event(ev_buf[nb])
+        set_stream(s_)
+        try:
+            prep_fns[nb]()
+            ev_prep[nb].record(s_)
+        finally:
+            set_stream(main)
+        issue_exchange(t + xd)
+        state["t"] = t + 1
+
+    prep_fns = [(lambda b=b: prep(b)) for b in range(NB)]
+    for e in ev_buf:
+        e.record(main)
+    for b in range(nprep):
+        with torch.cuda.stream(sides[b]):
+            prep(b)
+            ev_prep[b].record(sides[b])
+    if tr.xc is None:
+        tr._xc_setup(locs[0])  # (collective: the row capacity from minibatch 0)
+    for s in range(-1, xd):  # exchanges -1 .. xd-1 carry keys(0) .. keys(xd)
+        issue_exchange(s)
+    warm = max(NB, args.warmup, d + 1)  # (captured exchanges all carry pushes: s - d >= 0)
+    warm += (-warm) % P
+    for _ in range(warm):
+        iterate()
+    if not args.graph:
+        return iterate, False
+    torch.cuda.synchronize()
+    t0 = state["t"]
+    held = []
+
+    def release():
+        torch.cuda.synchronize()
+        for g in held:
+            g.reset()
+        held.clear()
+
+    iterate.release = release
+    cmode = os.environ.get("PSAMD_CAPTURE_COMM", "auto")
+    ccomm = (cchain is not None and getattr(tr.comm, "backend", "") != "gloo"
+             and cmode in ("1", "auto"))
+    pipeline.captured_comm = ccomm
+
+    def graph_of(fn):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
+            fn()
+        held.append(g)
+        return g.replay
+
+    def chained(rep):
+        def f():
+            s_ = torch.cuda.current_stream(device)
+            cchain.wait(s_)
+            rep()
+            cchain.mark(s_, 1)
+        return f
+
+    gp = []
+    for s_ in range(nprep):
+        ctr[s_].fill_(hctr[s_])
+    mode["capture"] = True
+    for b in range(NB):
+        gp.append(graph_of(lambda b=b: prep(b)))
+    for j in range(P):
+        if watch is not None:
+            watch.beat("capture", j)
+        t = t0 + j
+        b = t % NB
+        gw[j] = graph_of(tr.mx_worker(t, locs[b], bufs[b][1], width=39))
+        # exchange s = t + xd is issued at iteration t: its phase is (t + xd) % P
+        s = t + xd
+        parts = tr.mx_exchange(s, locs[(s + 1) % NB])
+        gx[s % P] = {"pack": graph_of(parts["pack"]),
+                     "comm": chained(graph_of(parts["comm"])) if ccomm else parts["comm"],
+                     "resolve": graph_of(parts["resolve"]), "apply": graph_of(parts["apply"]),
+                     "post": parts["post"]}
+    prep_fns[:] = gp
+    graphs["on"] = True
+    torch.cuda.synchronize()
+    for _ in range(P):
+        iterate()
+    torch.cuda.synchronize()
+    return iterate, True
+
+
 def spawn_ranks(n: int, argv: list[str] | None = None, script: str | None = None) -> int:
     """Re-launch this script as ``n`` ranks through torch.distributed.run (rendezvous on
     127.0.0.1, a free port) as a CHILD process, and return its exit code. Called
@@ -636,6 +836,10 @@ def main():
                          "or one-sided peer-HBM pulls + inbox pushes (asp only, no collective "
                          "per step: parallel/p2p.py)")
     ap.add_argument("--fixing-float", type=int, default=0)
+    ap.add_argument("--exchange-merge", default="auto", choices=["auto", "on", "off"],
+                    help="N > 1, lag >= 1: one all-to-all per step carrying [keys(t+1) | "
+                         "pushes | weights of keys(t)] (auto: ssp:tau >= 2 and asp) or the "
+                         "two-collective exchange (off)")
     ap.add_argument("--ssp-apply", default="post", choices=["post", "pre"],
                     help="N > 1, ssp: the owner applies the carried pushes after sending the "
                          "pulled weights back (post) or before resolving the pulls (pre)")
@@ -723,7 +927,8 @@ def main():
                          consistency=args.consistency,
                          fixing_float_bytes=args.fixing_float, exchange=args.exchange,
                          localize=args.localize, push_mode=args.push_mode,
-                         ssp_apply=args.ssp_apply, seed=rank)
+                         ssp_apply=args.ssp_apply, exchange_merge=args.exchange_merge,
+                         seed=rank)
     tr = SparseLRTrainer(cfg, comm, device)
     prefill_occ = None
     if args.prefill > 0:
@@ -895,8 +1100,11 @@ def main():
                 "parallelism": f"dp{n_ranks}+kvshard{n_ranks}",
                 "consistency": tr.consistency_desc(),
                 "push": args.push_mode if G > 1 else None,
-                "ssp_apply": args.ssp_apply if G > 1 and tr.padded and tr.lag >= 1 and not tr.asp
-                else None,
+                "ssp_apply": ("merged" if getattr(tr, "merged", False) else
+                              args.ssp_apply if G > 1 and tr.padded and tr.lag >= 1
+                              and not tr.asp else None),
+                "collectives_per_step": (1 if getattr(tr, "merged", False) else
+                                         2 if G > 1 and tr.padded else None),
                 "table_slots_per_gpu": tr.table.capacity,
                 "hip_graph": graph_used,
                 "collectives_in_graphs": bool(getattr(pipeline, "captured_comm", False)

@@ -26,8 +26,8 @@ void kv_update_rows(void*, int64_t, const int64_t*, const float*, int64_t, const
                     int64_t, int64_t, unsigned long long*, int64_t, int32_t*, int, int, float, float,
                     float, float, float, float, double*, int, hipStream_t);
 void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int, int64_t*, float*,
-                     bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t, uint64_t,
-                     uint64_t*, int32_t*, int, hipStream_t);
+                     int64_t, bool, int, float, float, uint64_t, int32_t*, int32_t*, uint64_t,
+                     uint64_t, uint64_t*, int32_t*, int, hipStream_t);
 void kv_apply_part(void*, int64_t, const int64_t*, const uint64_t*, const float*, int64_t,
                    const int32_t*, int, int64_t, int64_t, const int32_t*, int, int, int, float, float,
                    float, float, float, float, double*, int, hipStream_t);
@@ -66,7 +66,7 @@ bool tpf_exchange_ok(int64_t, int, int);
 void tpf_pack_keys(int64_t, int, int, const int32_t*, const uint64_t*, int64_t, int, int64_t,
                    int32_t*, int32_t*, hipStream_t);
 void tpf_unpack_w(int64_t, int, int, const int32_t*, const int32_t*, const uint16_t*, int64_t,
-                  const float*, float*, int64_t, hipStream_t);
+                  const float*, int64_t, float*, int64_t, hipStream_t);
 void tpf_pack_grads(int64_t, int, int, const int32_t*, const int32_t*, const uint16_t*, int64_t, int,
                     int64_t, const float*, int64_t, int32_t*, bool, float*, uint32_t*, int, double*,
                     int64_t*, const int32_t*, int32_t*, hipStream_t);
@@ -116,7 +116,7 @@ void xchg_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, cons
 void xchg_clear_counts(int32_t*, int, int64_t, bool, bool, hipStream_t);
 void xchg_publish(const int32_t*, int32_t*, hipStream_t);
 void xchg_unpack_w(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
-                   int64_t, float*, hipStream_t);
+                   int64_t, int64_t, float*, hipStream_t);
 void xchg_ff_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
                         int64_t, int, int64_t, int, uint64_t, const int64_t*, int32_t*, float*,
                         hipStream_t);
@@ -902,18 +902,22 @@ PYBIND11_MODULE(_hipops, m) {
                          ptr<int32_t>(send), optr<int32_t>(ovf, at::kInt, "ovf"), cur_stream());
   });
   m.def("tpf_unpack_w", [](int64_t n, int bits, int G, Tensor cnt, Tensor ent_pos, Tensor ent_j,
-                           int64_t C, Tensor wrecv, Tensor w_ent) {
+                           int64_t C, Tensor wrecv, Tensor w_ent, int64_t wstride) {
+    // wstride: row stride of wrecv (0 = C; the merged exchange reads the weights in
+    // place from the received rows)
+    const int64_t ws = wstride > 0 ? wstride : C;
     check_tpf(TpfBufs{cnt, cnt.new_empty({0}, at::kLong), ent_pos, ent_j,
                       cnt.new_empty({0}, at::kInt)}, n, bits, "tpf_unpack_w", true);
     chk(wrecv, at::kFloat, "wrecv");
     chk(w_ent, at::kFloat, "w_ent");
     check(psamd::tpf_exchange_ok(n, bits, G), "tpf_unpack_w: G a power of two dividing groups");
-    check(C > 0 && wrecv.numel() >= G * C && w_ent.numel() >= psamd::tploc_stride(n),
-          "tpf_unpack_w: buffers");
+    check(C > 0 && ws >= C && wrecv.numel() >= (G - 1) * ws + C &&
+          w_ent.numel() >= psamd::tploc_stride(n), "tpf_unpack_w: buffers");
     psamd::tpf_unpack_w(n, bits, G, ptr<int32_t>(cnt), ptr<int32_t>(ent_pos),
-                        ptr<uint16_t>(ent_j), C, ptr<float>(wrecv), ptr<float>(w_ent),
+                        ptr<uint16_t>(ent_j), C, ptr<float>(wrecv), ws, ptr<float>(w_ent),
                         w_ent.numel(), cur_stream());
-  });
+  }, py::arg("n"), py::arg("bits"), py::arg("G"), py::arg("cnt"), py::arg("ent_pos"),
+     py::arg("ent_j"), py::arg("C"), py::arg("wrecv"), py::arg("w_ent"), py::arg("wstride") = 0);
   m.def("tpf_pack_grads", [](int64_t n, int bits, int G, Tensor cnt, Tensor ent_pos, Tensor ent_j,
                              int64_t C, int kw, int64_t H, Tensor psum, Tensor send,
                              optional<Tensor> gstage, optional<Tensor> hist,
@@ -1091,8 +1095,10 @@ PYBIND11_MODULE(_hipops, m) {
                               Tensor out_slot, Tensor out_w, bool insert, int init_type,
                               double init_v, double init_s, uint64_t seed, optional<Tensor> err,
                               optional<Tensor> inserted, uint64_t home_base, uint64_t home_m,
-                              optional<Tensor> out_key, optional<Tensor> bnd, int lgP) {
+                              optional<Tensor> out_key, optional<Tensor> bnd, int lgP,
+                              int64_t wstride) {
     const int64_t cap = slot_capacity(slots);
+    const int64_t ws = wstride > 0 ? wstride : C;
     chk(recv, at::kInt, "recv");
     chk(out_slot, at::kLong, "out_slot");
     chk(out_w, at::kFloat, "out_w");
@@ -1101,14 +1107,15 @@ PYBIND11_MODULE(_hipops, m) {
     check(recv.numel() % H == 0, "recv is not a whole number of rows");
     const int G = (int)(recv.numel() / H);
     check(G >= 1 && G <= 64, "1..64 peers");
-    check(out_slot.numel() >= G * C && out_w.numel() >= G * C, "out_slot/out_w < G*C");
+    check(ws >= C && out_slot.numel() >= G * C && out_w.numel() >= (G - 1) * ws + C,
+          "out_slot < G*C or out_w < (G-1)*wstride + C");
     int64_t* ok = optr<int64_t>(out_key, at::kLong, "out_key");
     if (ok) check(out_key->numel() >= G * C, "out_key < G*C");
     int32_t* bp = optr<int32_t>(bnd, at::kInt, "bnd");
     check(lgP >= 0 && lgP <= 20, "lgP in 0..20");
     if (bp) check(bnd->numel() >= G * ((1 << lgP) + 1), "bnd < G*(P+1)");
     psamd::kv_resolve_rows(slots.data_ptr(), cap, ptr<int32_t>(recv), G, H, C, kw,
-                           ptr<int64_t>(out_slot), ptr<float>(out_w), insert, init_type,
+                           ptr<int64_t>(out_slot), ptr<float>(out_w), ws, insert, init_type,
                            (float)init_v, (float)init_s, seed, optr<int32_t>(err, at::kInt, "err"),
                            optr<int32_t>(inserted, at::kInt, "inserted"), home_base, home_m,
                            reinterpret_cast<uint64_t*>(ok), bp, lgP, cur_stream());
@@ -1116,7 +1123,7 @@ PYBIND11_MODULE(_hipops, m) {
      py::arg("out_slot"), py::arg("out_w"), py::arg("insert"), py::arg("init_type"),
      py::arg("init_v"), py::arg("init_s"), py::arg("seed"), py::arg("err"), py::arg("inserted"),
      py::arg("home_base"), py::arg("home_m"), py::arg("out_key") = py::none(),
-     py::arg("bnd") = py::none(), py::arg("lgP") = 0);
+     py::arg("bnd") = py::none(), py::arg("lgP") = 0, py::arg("wstride") = 0);
   // per-push apply of every source row, partitioned by key range (see kv_apply_part_kernel)
   m.def("kv_apply_part", [](Tensor slots, Tensor slot_idx, Tensor keys, Tensor grad,
                             int64_t gstride, Tensor recv, int64_t H, int64_t C, Tensor bnd, int lgP,
@@ -1456,19 +1463,21 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::xchg_clear_counts(ptr<int32_t>(send), G, H, keys, grads, cur_stream());
   });
   m.def("xchg_unpack_w", [](Tensor recv_w, optional<Tensor> perm, Tensor n_uniq, Tensor off,
-                            int64_t C, Tensor w_local) {
+                            int64_t C, Tensor w_local, int64_t wstride) {
+    const int64_t ws = wstride > 0 ? wstride : C;
     chk(recv_w, at::kFloat, "recv_w");
     chk(n_uniq, at::kInt, "n_uniq");
     chk(off, at::kLong, "off");
     chk(w_local, at::kFloat, "w_local");
     const int G = (int)off.numel() - 1;
     check(G >= 1 && G <= 64, "1..64 peers");
-    check(recv_w.numel() >= G * C, "recv_w < G*C");
+    check(ws >= C && recv_w.numel() >= (G - 1) * ws + C, "recv_w < (G-1)*wstride + C");
     const int32_t* pp = optr<int32_t>(perm, at::kInt, "perm");
     if (pp) check(perm->numel() >= w_local.numel(), "perm shorter than w_local");
     psamd::xchg_unpack_w(ptr<float>(recv_w), pp, ptr<int32_t>(n_uniq), w_local.numel(),
-                         ptr<int64_t>(off), G, C, ptr<float>(w_local), cur_stream());
-  });
+                         ptr<int64_t>(off), G, C, ws, ptr<float>(w_local), cur_stream());
+  }, py::arg("recv_w"), py::arg("perm"), py::arg("n_uniq"), py::arg("off"), py::arg("C"),
+     py::arg("w_local"), py::arg("wstride") = 0);
   m.def("kv_gather", [](Tensor slots, Tensor slot_idx, optional<Tensor> n_dev, Tensor out,
                         int field) {
     const int64_t cap = slot_capacity(slots);

@@ -121,7 +121,7 @@ __global__ void xchg_unpack_w_kernel(const float* __restrict__ recv_w,
                                      const int32_t* __restrict__ perm,
                                      const int32_t* __restrict__ n_uniq, int64_t n_host,
                                      const int64_t* __restrict__ off, int G, int64_t C,
-                                     float* __restrict__ w_local) {
+                                     int64_t wstride, float* __restrict__ w_local) {
   __shared__ int64_t soff[kMaxPeers + 1];
   load_offsets(off, G, soff);
   const int64_t n = dev_len(n_uniq, n_host);
@@ -129,7 +129,7 @@ __global__ void xchg_unpack_w_kernel(const float* __restrict__ recv_w,
        j += (int64_t)gridDim.x * blockDim.x) {
     const int p = owner_of_pos(soff, G, j);
     const int64_t i = j - soff[p];
-    const float v = i < C ? recv_w[(int64_t)p * C + i] : 0.f;
+    const float v = i < C ? recv_w[(int64_t)p * wstride + i] : 0.f;
     const int64_t u = perm ? (int64_t)perm[j] : j;
     if (in_range(u, n_host)) w_local[u] = v;
   }
@@ -174,10 +174,10 @@ void xchg_clear_counts(int32_t* send, int G, int64_t H, bool keys, bool grads, h
 }
 
 void xchg_unpack_w(const float* recv_w, const int32_t* perm, const int32_t* n_uniq,
-                   int64_t n_host, const int64_t* off, int G, int64_t C, float* w_local,
-                   hipStream_t st) {
-  xchg_unpack_w_kernel<<<grid_for(n_host, 256), 256, 0, st>>>(recv_w, perm, n_uniq, n_host, off,
-                                                               G, C, w_local);
+                   int64_t n_host, const int64_t* off, int G, int64_t C, int64_t wstride,
+                   float* w_local, hipStream_t st) {
+  xchg_unpack_w_kernel<<<grid_for(n_host, 256), 256, 0, st>>>(
+      recv_w, perm, n_uniq, n_host, off, G, C, wstride > 0 ? wstride : C, w_local);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -71,7 +71,8 @@ __global__ void kv_resolve_rows_kernel(Slot* __restrict__ slots, uint64_t mask,
                                        uint64_t home_base, uint64_t home_m, int home_shr,
                                        const int32_t* __restrict__ recv, int64_t H, int64_t C,
                                        int kw, int64_t* __restrict__ out_slot,
-                                       float* __restrict__ out_w, int insert, int init_type,
+                                       float* __restrict__ out_w, int64_t wstride,
+                                       int insert, int init_type,
                                        float init_v, float init_s, uint64_t seed,
                                        int32_t* __restrict__ err, int32_t* __restrict__ inserted,
                                        uint64_t* __restrict__ out_key, int32_t* __restrict__ bnd,
@@ -93,7 +94,7 @@ __global__ void kv_resolve_rows_kernel(Slot* __restrict__ slots, uint64_t mask,
                                       init_type, init_v, init_s, seed, &w, &local_ins);
     if (found < 0 && insert && err) atomicOr(err, 1);
     out_slot[(int64_t)s * C + i] = found;
-    out_w[(int64_t)s * C + i] = w;
+    out_w[(int64_t)s * wstride + i] = w;
     if (out_key) out_key[(int64_t)s * C + i] = h;
     if (rb) {  // partition bounds of this (sorted) row: rb[q] = #keys of partition < q
       const int q = key_part(h, home_base, home_m, lgP);
@@ -568,17 +569,18 @@ void kv_resolve(void* slots, int64_t cap, const uint64_t* keys, int64_t n, const
 }
 
 void kv_resolve_rows(void* slots, int64_t cap, const int32_t* recv, int G, int64_t H, int64_t C,
-                     int kw, int64_t* out_slot, float* out_w, bool insert, int init_type,
-                     float init_v, float init_s, uint64_t seed, int32_t* err, int32_t* inserted,
-                     uint64_t home_base, uint64_t home_m, uint64_t* out_key, int32_t* bnd,
-                     int lgP, hipStream_t st) {
+                     int kw, int64_t* out_slot, float* out_w, int64_t wstride, bool insert,
+                     int init_type, float init_v, float init_s, uint64_t seed, int32_t* err,
+                     int32_t* inserted, uint64_t home_base, uint64_t home_m, uint64_t* out_key,
+                     int32_t* bnd, int lgP, hipStream_t st) {
   int lg = 0;
   while ((1ll << lg) < cap) ++lg;
   dim3 grid(grid_for(C, 256, 1024), G);
   if (bnd && !home_m) throw std::runtime_error("kv_resolve_rows: partition bounds need an ordered home");
   kv_resolve_rows_kernel<<<grid, 256, 0, st>>>(
       (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg, recv, H, C, kw, out_slot,
-      out_w, insert ? 1 : 0, init_type, init_v, init_s, seed, err, inserted, out_key, bnd, lgP);
+      out_w, wstride > 0 ? wstride : C, insert ? 1 : 0, init_type, init_v, init_s, seed, err,
+      inserted, out_key, bnd, lgP);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

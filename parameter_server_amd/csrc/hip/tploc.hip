@@ -1970,7 +1970,8 @@ tpf_pack_keys_kernel(const int32_t* __restrict__ cnt, const uint64_t* __restrict
 __global__ void __launch_bounds__(tpf::kThr)
 tpf_unpack_w_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict__ ent_pos,
                     const uint16_t* __restrict__ ent_j, int per, int64_t C,
-                    const float* __restrict__ wrecv, float* __restrict__ w_ent, int64_t w_cap) {
+                    const float* __restrict__ wrecv, int64_t wstride, float* __restrict__ w_ent,
+                    int64_t w_cap) {
   using namespace tpf;
   __shared__ uint32_t red[kThr / 64 + 1];
   __shared__ float wj[kUnitK];
@@ -1985,7 +1986,7 @@ tpf_unpack_w_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict__
     if (D <= 0) continue;
     for (int j = t; j < D; j += kThr) {
       const int64_t pos = (int64_t)off + j;
-      wj[j] = pos < C ? wrecv[(int64_t)p * C + pos] : 0.f;
+      wj[j] = pos < C ? wrecv[(int64_t)p * wstride + pos] : 0.f;
     }
     __syncthreads();
     const int64_t eb = (int64_t)b * kEC + e0, rb = (int64_t)b * kEC;
@@ -2259,11 +2260,11 @@ void tpf_pack_keys(int64_t n, int bits, int G, const int32_t* cnt, const uint64_
 }
 
 void tpf_unpack_w(int64_t n, int bits, int G, const int32_t* cnt, const int32_t* ent_pos,
-                  const uint16_t* ent_j, int64_t C, const float* wrecv, float* w_ent, int64_t w_cap,
-                  hipStream_t st) {
+                  const uint16_t* ent_j, int64_t C, const float* wrecv, int64_t wstride,
+                  float* w_ent, int64_t w_cap, hipStream_t st) {
   const int per = tpf_per_owner(n, bits, G);
-  tpf_unpack_w_kernel<<<(unsigned)tpf_groups(n, bits), tpf::kThr, 0, st>>>(cnt, ent_pos, ent_j, per,
-                                                                           C, wrecv, w_ent, w_cap);
+  tpf_unpack_w_kernel<<<(unsigned)tpf_groups(n, bits), tpf::kThr, 0, st>>>(
+      cnt, ent_pos, ent_j, per, C, wrecv, wstride > 0 ? wstride : C, w_ent, w_cap);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

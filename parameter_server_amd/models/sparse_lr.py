@@ -45,7 +45,7 @@ from ..ops.linear import (AUC_BINS, HIST_STRIPES, accum_total, auc_from_hist, fu
 from ..ops.localize import Localizer
 from ..ops.native import hipops
 from ..parallel.comm import Comm, LocalComm
-from ..parallel.consistency import ExchangeSchedule, parse_consistency
+from ..parallel.consistency import ExchangeSchedule, MergedSchedule, parse_consistency
 from ..parallel.partition import KeyPartition
 from ..utils.trace import enabled as trace_enabled
 from ..utils.trace import trace_range
@@ -96,6 +96,11 @@ class SparseLRConfig:
     # pushes. -1 = from `consistency` (bsp -> 0, ssp:tau -> tau, asp -> 1)
     exchange_lag: int = -1
     asp_depth: int = 4                   # asp: exchanges whose push applies may be in flight
+    # padded exchange with lag >= 1: ONE all-to-all per step carrying [keys(t+1) |
+    # grads(t-d) | weights of keys(t)] (parallel/consistency.MergedSchedule) instead of
+    # two (keys + grads, then weights). "auto": on for ssp:tau >= 2 and asp; "on" also
+    # for ssp:1 (worker and exchange then serialise); "off": two collectives
+    exchange_merge: str = "auto"
     seed: int = 0
 
     def update_rule(self) -> UpdateRule:
@@ -218,6 +223,20 @@ class SparseLRTrainer:
         # rings of R exchange buffers indexed by step (>= 2: the exchange of step t+1
         # runs while the worker half of step t still reads its weights)
         self.R = self.sched.R
+        if cfg.exchange_merge not in ("auto", "on", "off"):
+            raise ValueError(f"exchange_merge must be auto / on / off, not {cfg.exchange_merge!r}")
+        self.merged = bool(
+            self.padded and self.filter is None and cfg.exchange_merge != "off"
+            and self.tau > 0 and (cfg.exchange_merge == "on" or math.isinf(self.tau)
+                                  or self.tau >= 2))
+        self.msched = None
+        if self.merged:  # one collective per step (MergedSchedule)
+            self.msched = MergedSchedule(self.tau, cfg.exchange_lag)
+            self.lag, self.asp, self.async_depth = self.msched.lag, False, 0
+            self.R = self.msched.R
+        self._mx_pend = None      # sequential API: the minibatch whose worker half is due
+        self._mx_next = None      # index of the next merged exchange (None: bootstrap due)
+        self._mx_external = False  # exchanges issued by a caller's pipeline (bench.py)
         self._xt = 0  # padded steps computed (worker halves run)
         self._xx = 0  # padded exchanges issued (exchange halves run)
         self.pending = None
@@ -299,6 +318,9 @@ class SparseLRTrainer:
             if loc is None:
                 loc = self.localizer(keys)
             return self._p2p_step(loc, labels, width, prefetch)
+        if self.merged:
+            return self._mx_step(keys, labels, width=width, row_ptr=row_ptr, vals=vals,
+                                 rows=rows, loc=loc, prefetch=prefetch)
         if self.padded:
             if loc is None:
                 with trace_range("localize"):
@@ -400,13 +422,15 @@ class SparseLRTrainer:
         return torch.repeat_interleave(torch.arange(B, dtype=torch.int32),
                                        (row_ptr[1:] - row_ptr[:-1]).long())
 
-    def _compact_localizer(self) -> Localizer:
-        """Flat mode: the "tp" Localizer for minibatches the flat layout cannot express
-        (valued or variable-width rows)."""
+    def _compact_localizer(self, buf: int = 0) -> Localizer:
+        """Flat mode: the "tp" Localizer (workspace ``buf``) for minibatches the flat
+        layout cannot express (valued or variable-width rows)."""
         if self._compact is None:
-            self._compact = Localizer(self.max_nnz, self.bits, self.device, mode="tp",
-                                      lazy_cols=True)
-        return self._compact
+            self._compact = []
+        while len(self._compact) <= buf:
+            self._compact.append(Localizer(self.max_nnz, self.bits, self.device, mode="tp",
+                                           lazy_cols=True))
+        return self._compact[buf]
 
     # ----------------------------------------------- flat 1-GPU step (Localizer "tpf")
     _FLAT_WIDTHS: dict = {}
@@ -549,6 +573,8 @@ class SparseLRTrainer:
             return
         if not self.padded:
             raise NotImplementedError("key-less steps need the padded exchange")
+        if self.merged:
+            return self._mx_step(None, None, idle=True)
         for _, fn in self.step_segments(None, None, idle=True):
             fn()
 
@@ -690,6 +716,181 @@ class SparseLRTrainer:
         segs += [("compute", lambda: clear(xc.sends[r], False, True)), ("host", host)]
         return segs
 
+    # ------------------------------ merged exchange (one all-to-all per step, lag >= 1)
+    def mx_exchange(self, s: int, next_loc=None, *, prepare=True):
+        """The parts of merged exchange ``s`` (parallel/consistency.MergedSchedule) as a
+        dict of callables, for a caller that orders them against other streams
+        (bench.py) -- or run in order by ``_mx_step``:
+
+          pack     keys(s+1) of ``next_loc`` into the send rows of exchange s (None: no
+                   keys -- a drain or an idle rank)
+          comm     the all-to-all (send rows hold grads(s-d) packed by worker s-d and the
+                   weights resolved after exchange s-1)
+          resolve  owner: lookup-or-insert keys(s+1) -> slots of pull step s+1, their
+                   weights into the send rows of exchange s+1
+          apply    owner: the pushes of step s-d (``post``: after resolve, else before)
+
+        Everything is fixed device buffers (ring entries), so each part replays from a
+        HIP graph captured for ring position s % R. ``prepare``: allocate the exchange
+        rows on the first call (collective: agrees on the row capacity)."""
+        if self.xc is None and prepare:
+            self._xc_setup(next_loc)
+        xc, ms, comm = self.xc, self.msched, self.comm
+        R, d = ms.R, ms.d
+        b, bn = s % R, (s + 1) % R
+        send, recv = xc.sends[b], xc.recvs[b]
+        flat = next_loc is not None and getattr(next_loc, "flat", False)
+
+        def pack():
+            if next_loc is None:
+                self._mx_clear(send, keys=True)
+            elif flat:
+                self._x_pack_keys_flat(next_loc, b, bn)
+            else:
+                self._x_pack_keys(next_loc, b, bn)
+
+        def resolve():
+            self._x_resolve(b, bn, wout=self._mx_wview(xc.sends[bn]), wstride=xc.H)
+
+        def apply():
+            if s - d >= 0:
+                self._x_apply(b, (s - d) % R)
+
+        return {"pack": pack, "comm": lambda: comm.all_to_all_fixed(send, recv),
+                "resolve": resolve, "apply": apply, "post": ms.post}
+
+    def mx_worker(self, u: int, loc, labels, *, width=None, row_ptr=None, vals=None, rows=None):
+        """Worker half of step ``u`` on the merged exchange: weights read in place from
+        the rows of exchange u, forward + backward, gradients into the send rows of
+        exchange u+d (+ AUC epilogue). ``loc=None``: an idle step (no minibatch): only
+        clears its gradient rows."""
+        xc, ms = self.xc, self.msched
+        R = ms.R
+        b, bg = u % R, ms.grad_ring(u)
+        if loc is None:
+            return lambda: self._mx_clear(xc.sends[bg], grads=True)
+        B = labels.numel()
+        if width is None and row_ptr is None:
+            width = self.cfg.max_nnz_per_example
+        wsrc = self._mx_wview(xc.recvs[b])
+        if getattr(loc, "flat", False):
+            return lambda: self._x_finish_flat(loc, labels, B, width, b, send=xc.sends[bg],
+                                               wsrc=wsrc, wstride=xc.H)
+
+        def fin():
+            if row_ptr is not None and self.gpu:
+                hipops().csr_rows(row_ptr, rows)
+            self._x_finish(loc, labels, B, width, row_ptr, vals, rows, b, send=xc.sends[bg],
+                           wsrc=wsrc, wstride=xc.H)
+        return fin
+
+    def mx_done(self, B: int):
+        """Host bookkeeping of one merged worker step."""
+        self.step_count += 1
+        self._xt += 1
+        self.examples += B
+        self._x_poll_overflow()
+
+    def _mx_wview(self, buf: torch.Tensor) -> torch.Tensor:
+        """The weight words of a row buffer, as floats from row 0's weight offset (row
+        stride H)."""
+        return buf.view(torch.float32)[self.xc.w0:]
+
+    def _mx_clear(self, buf, keys: bool = False, grads: bool = False):
+        if self.gpu:
+            hipops().xchg_clear_counts(buf, self.xc.H, keys, grads)
+            return
+        for p in range(self.G):
+            if keys:
+                buf[p * self.xc.H] = 0
+            if grads:
+                buf[p * self.xc.H + 1] = 0
+
+    def _mx_run_exchange(self, s: int, next_loc):
+        parts = self.mx_exchange(s, next_loc)
+        parts["pack"]()
+        parts["comm"]()
+        if parts["post"]:
+            parts["resolve"]()
+            parts["apply"]()
+        else:
+            parts["apply"]()
+            parts["resolve"]()
+        self._mx_next = s + 1
+
+    def _mx_step(self, keys, labels, *, width=None, row_ptr=None, vals=None, rows=None,
+                 loc=None, prefetch=None, idle: bool = False):
+        """Sequential API on the merged exchange: step(u) issues exchange u-1, which
+        carries keys(u), and then runs the worker half of step u-1 (its weights came
+        with that exchange). So a call trains the PREVIOUS minibatch; ``flush()`` (and
+        ``progress()``) trains the last one and applies every outstanding push. The
+        minibatch tensors are captured (labels / row_ptr / vals copied)."""
+        if prefetch is not None:
+            prefetch()
+        cur = None
+        if not idle:
+            B = labels.numel()
+            if width is None and row_ptr is None:
+                width = self.cfg.max_nnz_per_example
+            buf = self._xt + (self._mx_pend is not None)  # step index of this minibatch
+            if loc is None:
+                flat_ok = (self.localize_mode == "tpf" and row_ptr is None and rows is None
+                           and vals is None and self._flat_ok(B, width, keys.numel())
+                           and hipops().tpf_exchange_ok(keys.numel(), self.bits, self.G))
+                loc = (self.localize(keys, buf=buf % 2) if flat_ok
+                       else self._compact_localizer(buf % 2)(keys))
+            if row_ptr is not None and rows is None:
+                rows = (torch.empty(keys.numel(), dtype=torch.int32, device=keys.device)
+                        if self.gpu else self._csr_rows(row_ptr, keys.numel()))
+            cur = dict(loc=loc, labels=labels.clone(), width=width,
+                       row_ptr=None if row_ptr is None else row_ptr.clone(),
+                       vals=None if vals is None else vals.clone(), rows=rows, B=B)
+        u = self._xt + (self._mx_pend is not None)
+        self._mx_run_exchange(u - 1, None if cur is None else cur["loc"])
+        self._mx_finish_pending()
+        self._mx_pend = cur if cur is not None else {"idle": True}
+
+    def _mx_finish_pending(self):
+        p, self._mx_pend = self._mx_pend, None
+        if p is None:
+            return
+        u = self._xt
+        if p.get("idle"):
+            self.mx_worker(u, None, None)()
+            self.step_count += 1
+            self._xt += 1
+            return
+        self.mx_worker(u, p["loc"], p["labels"], width=p["width"], row_ptr=p["row_ptr"],
+                       vals=p["vals"], rows=p["rows"])()
+        self.mx_done(p["B"])
+
+    def mx_drain(self):
+        """Apply every computed push that no issued exchange has carried yet: key-less
+        exchanges for the remaining ring entries (collective; synchronises the device).
+        Leaves the exchange ready for a fresh bootstrap."""
+        if self.xc is None:
+            return
+        ms = self.msched
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+        last = self._xt - 1  # last worker step whose gradients were packed
+        s = self._mx_next if self._mx_next is not None else last + 1
+        while s - ms.d <= last:
+            b = s % ms.R
+            send = self.xc.sends[b]
+            self._mx_clear(send, keys=True)
+            self.comm.all_to_all_fixed(send, self.xc.recvs[b])
+            if s - ms.d >= 0:
+                self._x_apply(b, (s - ms.d) % ms.R)
+            self._mx_clear(send, grads=True)
+            s += 1
+        # exchanges s' < s that a new bootstrap may reuse carry no gradients any more
+        for j in range(ms.R):
+            self._mx_clear(self.xc.sends[j], keys=True, grads=True)
+        self._mx_next = None
+        if self.gpu:
+            torch.cuda.synchronize(self.device)
+
     @property
     def EXCHANGE_SEGMENTS(self) -> int:  # step_segments()[:n] = exchange half
         return 6 if self.asp or self.sched.post else 5
@@ -702,6 +903,13 @@ class SparseLRTrainer:
             return (f"asp-p2p (one-sided pulls from the owners' HBM and inbox pushes, no "
                     f"collective per step; owners apply at their own pace, a pusher waits "
                     f"only {self.cfg.p2p_queue} steps ahead of an owner)")
+        if self.merged:
+            ms = self.msched
+            base = "asp (bounded here: " if ms.asp else f"ssp:{int(self.tau)} ("
+            return (f"{base}pull of step t sees exactly the pushes of steps <= t-1-{ms.lag}; "
+                    f"one all-to-all per step carrying keys(t+1), pushes(t-{ms.d}) and the "
+                    f"weights of keys(t), owner apply {'after' if ms.post else 'before'} "
+                    f"its resolve)")
         if not self.padded or self.lag == 0 and not self.asp:
             return "bsp (pull of step t sees every push of steps <= t-1)"
         if self.asp:
@@ -743,7 +951,10 @@ class SparseLRTrainer:
         kw = 1 if self.bits <= 32 else 2
         nb = int(cfg.fixing_float_bytes)  # FixingFloat: nb-byte codes instead of f32
         gw = (C * nb + 3) // 4 if nb else C
-        H = (4 + C * kw + gw + 3) // 4 * 4
+        # merged exchange: each row also carries the owner's weights answering the keys
+        # the row's receiver sent in the previous exchange, at word w0
+        w0 = 4 + C * kw + gw
+        H = (w0 + (C if self.merged else 0) + 3) // 4 * 4
         z32 = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
         # the partitioned apply needs rows sorted by key and an ordered home (key range
         # -> partition)
@@ -757,7 +968,7 @@ class SparseLRTrainer:
         if part_apply and os.environ.get("PSAMD_APPLY_LGP"):
             lgP = int(os.environ["PSAMD_APPLY_LGP"])
         self.xc = SimpleNamespace(
-            C=C, kw=kw, H=H, nb=nb,
+            C=C, kw=kw, H=H, nb=nb, w0=w0,
             gstage=z32(G * C, torch.float32) if nb else None,
             gins=[z32(G * C, torch.float32) for _ in range(R)] if nb else None,
             # rings of R entries indexed by step: sends[j] holds grads(j) then keys(j+1+lag);
@@ -867,15 +1078,18 @@ class SparseLRTrainer:
         if xc.nb:  # (FixingFloat push: no pack_grads launch to carry the flag)
             hh.xchg_publish(xc.ovf, xc.ovf_host)
 
-    def _x_finish_flat(self, loc, labels, B: int, width: int, r: int):
+    def _x_finish_flat(self, loc, labels, B: int, width: int, r: int, send=None, wsrc=None,
+                       wstride: int = 0):
         """Flat layout, worker half: the pulled weights into tile-entry order, the flat
         fused forward + tile backward, every key's gradient (per-bucket fixed-point sums)
-        into its owner's row of the next exchange [+ FixingFloat codes], AUC epilogue."""
+        into its owner's row of the next exchange [+ FixingFloat codes], AUC epilogue.
+        (merged exchange: weights read in place from the received rows ``wsrc`` with row
+        stride ``wstride``, gradients into ``send``.)"""
         xc, hh = self.xc, hipops()
         n, bits, G = loc.nnz, loc.bits, self.G
-        send = xc.sends[r]
-        hh.tpf_unpack_w(n, bits, G, loc.cnt, loc.ent_pos, loc.ent_j, xc.C, xc.wrecvs[r],
-                        loc.w_ent)
+        send = xc.sends[r] if send is None else send
+        hh.tpf_unpack_w(n, bits, G, loc.cnt, loc.ent_pos, loc.ent_j, xc.C,
+                        xc.wrecvs[r] if wsrc is None else wsrc, loc.w_ent, wstride)
         coef = self._coef_views.get(B)
         if coef is None:
             coef = self._coef_views[B] = self.coef[:B]
@@ -950,18 +1164,24 @@ class SparseLRTrainer:
                 parts.append((pslot[s * C:s * C + ng], grads[s][:ng]))
         self._apply_pushes(parts)
 
-    def _x_resolve(self, r: int):
-        """Owner: lookup-or-insert the keys pulled by exchange ``r`` -> slots[r], wsend."""
+    def _x_resolve(self, r: int, rs: int | None = None, wout=None, wstride: int = 0):
+        """Owner: lookup-or-insert the keys pulled by exchange ``r`` -> slots[rs] (default
+        rs = r) and their weights -> ``wout`` (default wsend; row stride ``wstride``, 0 =
+        C: the merged exchange writes them into the next send rows)."""
         xc, G, H, C, kw = self.xc, self.G, self.xc.H, self.xc.C, self.xc.kw
         recv = xc.recvs[r]
+        rs = r if rs is None else rs
+        wout = xc.wsend if wout is None else wout
+        ws = wstride or C
         if self.gpu:
             it, iv, isd, seed = self.table.init.args()
-            hipops().kv_resolve_rows(self.table.slots, recv, H, C, kw, xc.slots[r], xc.wsend,
+            hipops().kv_resolve_rows(self.table.slots, recv, H, C, kw, xc.slots[rs], wout,
                                      True, it, iv, isd, seed, self.table._err,
                                      self.table._inserted, self.table.home_base,
                                      self.table.home_m,
-                                     xc.pkeys[r] if xc.bnd is not None else None,
-                                     xc.bnd[r] if xc.bnd is not None else None, max(xc.lgP, 0))
+                                     xc.pkeys[rs] if xc.bnd is not None else None,
+                                     xc.bnd[rs] if xc.bnd is not None else None, max(xc.lgP, 0),
+                                     wstride=ws)
             return
         for s in range(G):
             row = recv[s * H:(s + 1) * H]
@@ -973,24 +1193,27 @@ class SparseLRTrainer:
             else:
                 req = row[4:4 + 2 * nk].contiguous().view(torch.int64)
             slot, w = self.table.resolve(req, insert=True)
-            xc.slots[r][s * C:s * C + nk] = slot
-            xc.wsend[s * C:s * C + nk] = w
+            xc.slots[rs][s * C:s * C + nk] = slot
+            wout[s * ws:s * ws + nk] = w
 
-    def _x_finish(self, loc, labels, B, width, row_ptr, vals, rows, r: int):
+    def _x_finish(self, loc, labels, B, width, row_ptr, vals, rows, r: int, send=None,
+                  wsrc=None, wstride: int = 0):
         xc = self.xc
         perm, off, n_uniq = xc.curs[r]
-        wrecv, send = xc.wrecvs[r], xc.sends[r]  # grads(t) -> sends[t % R]
+        wrecv = xc.wrecvs[r] if wsrc is None else wsrc
+        send = xc.sends[r] if send is None else send  # grads(t) -> sends[t % R]
+        ws = wstride or xc.C
         if self.gpu:
             w_local = xc.w_local[:loc.uniq.numel()]
             if self.filter is not None:
                 w_local.zero_()  # filtered keys: w = 0
-            hipops().xchg_unpack_w(wrecv, perm, n_uniq, off, xc.C, w_local)
+            hipops().xchg_unpack_w(wrecv, perm, n_uniq, off, xc.C, w_local, wstride=ws)
         else:
             w_local = torch.zeros(max(int(loc.n_uniq.reshape(-1)[0]), 1), dtype=torch.float32)
             for p in range(self.G):
                 a, c = int(off[p]), min(int(off[p + 1] - off[p]), xc.C)
                 dst = perm[a:a + c].long() if perm is not None else slice(a, a + c)
-                w_local[dst] = wrecv[p * xc.C:p * xc.C + c]
+                w_local[dst] = wrecv[p * ws:p * ws + c]
         coef, grad = linear_fwd_bwd(loc, w_local, labels, B=B, width=width or 0, row_ptr=row_ptr,
                                     rows=rows, vals=vals, loss=self.cfg.loss, coef=self.coef[:B],
                                     metrics=self.metrics, hist=self.hist)
@@ -1072,6 +1295,12 @@ class SparseLRTrainer:
                     send[p * xc.H + 1] = 0
         if self.gpu:
             torch.cuda.synchronize(self.device)
+        self._x_check_overflow()
+
+    def _x_check_overflow(self):
+        xc = self.xc
+        if xc is None:
+            return
         ovf = int(xc.ovf.item())
         if ovf:
             raise RuntimeError(
@@ -1104,7 +1333,7 @@ class SparseLRTrainer:
         H = (4 + C * kw + gw + 3) // 4 * 4
         i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)  # noqa: E731
         self.xc = SimpleNamespace(
-            C=C, kw=kw, H=H, nb=nb, off=off, send=i32(G * H),
+            C=C, kw=kw, H=H, nb=nb, w0=w0, off=off, send=i32(G * H),
             gstage=torch.zeros(G * C, dtype=torch.float32, device=dev) if nb else None,
             wout=torch.zeros(G * C, dtype=torch.float32, device=dev),
             slot=torch.full((G * C,), -1, dtype=torch.int64, device=dev),
@@ -1254,6 +1483,15 @@ class SparseLRTrainer:
                 xc = self.xc
                 self.px.drain(self.rule, self.stats, xc.a_slot, xc.a_w, xc.link, xc.nxt)
             return
+        if self.merged:
+            if self._mx_external:
+                return  # a caller's pipeline owns the in-flight exchanges (mx_drain)
+            if self._mx_pend is not None:  # the last minibatch: exchange without keys
+                self._mx_run_exchange(self._xt, None)
+                self._mx_finish_pending()
+            self.mx_drain()
+            self._x_check_overflow()
+            return
         if self.padded:
             if self.xc is not None:
                 self._x_flush()
@@ -1380,7 +1618,7 @@ class SparseLRTrainer:
         (same fail-loudly rule as the exchange overflow, ``_x_poll_overflow``)."""
         if not self.gpu:
             return
-        lzs = list(self._localizers) + ([self._compact] if self._compact is not None else [])
+        lzs = list(self._localizers) + list(self._compact or [])
         words = [self.table._err] + [lz.err for lz in lzs if getattr(lz, "err", None) is not None]
         if self.xc is not None and getattr(self.xc, "ovf", None) is not None:
             words.append(self.xc.ovf)

@@ -114,6 +114,63 @@ class ExchangeSchedule:
         return self.lag, (self.lag + self.depth if self.asp else self.lag)
 
 
+class MergedSchedule:
+    """One collective per step (padded exchange, lag >= 1): exchange s carries, per peer
+    row, ``[keys(s+1) | grads(s-d) | weights answering keys(s)]`` -- the keys of the NEXT
+    step, the pushes of step s-d, and the weights the owner resolved for the keys it
+    received in exchange s-1. After exchange s lands:
+
+    * the worker of step s unpacks its weights straight from the received rows;
+    * the owner resolves keys(s+1) (weights into the send rows of exchange s+1);
+    * the owner applies grads(s-d): ``post`` = after that resolve (off the path to the
+      next collective), ``pre`` = before it.
+
+    The pull of step u is resolved right after exchange u-1, so it sees the pushes
+    carried by exchanges <= u-2 (post) / <= u-1 (pre), i.e. exactly the pushes of steps
+    <= u-1-lag with lag = d+1 (post) or d (pre) -- the same bound as ExchangeSchedule
+    with half the collectives. The worker of step u-d must have packed its gradients
+    before exchange u is issued, so d >= 2 lets the exchange chain run while the worker
+    computes (d = 1 serialises them; kept for lag 1 / tests). Target lag: ssp tau ->
+    tau; asp -> 3 (an admissible asp schedule: staleness exactly 3).
+
+    Rings (send, recv, resolved slots) have R = d + 2 entries indexed by exchange / pull
+    step: the send row of exchange s is complete once worker s-d and the resolve after
+    exchange s-1 wrote it; the received rows of exchange s are read by worker s, the
+    resolve of s+1 and the apply of s-d; resolved slots of pull step u are read by the
+    apply in exchange u+d."""
+
+    def __init__(self, tau: float, lag: int = -1):
+        self.tau = float(tau)
+        self.asp = math.isinf(self.tau)
+        L = int(lag) if lag >= 0 else (3 if self.asp else int(self.tau))
+        if not self.asp and L > self.tau:
+            raise ValueError(f"exchange_lag {L} exceeds the staleness bound {self.tau}")
+        if L < 1:
+            raise ValueError("the merged exchange needs lag >= 1 (bsp: two collectives)")
+        self.lag = L
+        self.post = L >= 3
+        self.d = L - 1 if self.post else L
+        self.R = self.d + 2
+        self.depth = 0
+
+    def ring(self, i: int) -> int:
+        return i % self.R
+
+    def grads_in(self, s: int) -> int:
+        """Step whose gradients exchange s carries (negative: none)."""
+        return s - self.d
+
+    def grad_ring(self, u: int) -> int:
+        """Send ring entry that worker u packs its gradients into (exchange u + d)."""
+        return (u + self.d) % self.R
+
+    def visible_through(self, u: int) -> int:
+        return u - 1 - self.lag
+
+    def staleness_bounds(self) -> tuple[int, float]:
+        return self.lag, self.lag
+
+
 class EventClock:
     """Per-exchange HIP events of applied pushes (device-side vector clock)."""
 

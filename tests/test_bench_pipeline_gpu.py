@@ -53,7 +53,15 @@ def _weights(tr):
     ("prep", 2, 1, {"algo": "adagrad"}),
     ("prep", 2, 1, {"ssp_apply": "pre"}), ("prep", 3, 1, {"ssp_apply": "pre", "consistency": "ssp:1"}),
     ("prep", 2, 1, {"_env": {"PSAMD_CAPTURE_COMM": "0"}}),
-    ("prep", 3, 1, {"consistency": "bsp", "_env": {"PSAMD_CAPTURE_COMM": "0"}})])
+    ("prep", 3, 1, {"consistency": "bsp", "_env": {"PSAMD_CAPTURE_COMM": "0"}}),
+    # the merged one-collective exchange (auto for ssp >= 2 / asp), against the
+    # two-collective sequential trainer: same staleness, same table
+    ("prep", 3, 1, {"exchange_merge": "on"}), ("prep", 3, 0, {"exchange_merge": "on"}),
+    ("prep", 2, 1, {"exchange_merge": "on", "consistency": "ssp:2"}),
+    ("prep", 3, 1, {"exchange_merge": "on", "consistency": "ssp:3"}),
+    ("prep", 3, 1, {"exchange_merge": "on", "fixing_float_bytes": 2}),
+    ("prep", 3, 1, {"exchange_merge": "on", "push_mode": "aggregate"}),
+    ("prep", 3, 1, {"exchange_merge": "on", "_env": {"PSAMD_CAPTURE_COMM": "0"}})])
 def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     from parameter_server_amd.ops.synthetic import criteo_batch
 
@@ -65,6 +73,7 @@ def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     B, N, seed, extra = 4096, 10 ** 6, 77, 5
     dev = torch.device("cuda")
     tr = _trainer(B, N, **kw)
+    assert tr.merged == (kw.get("exchange_merge") == "on")
     keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
     labels = torch.empty(B, dtype=torch.float32, device=dev)
     args = argparse.Namespace(warmup=0, graph=graph)
@@ -73,15 +82,17 @@ def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
         it()
     torch.cuda.synchronize()
     T = tr._xt  # worker steps the pipeline ran
-    tr._x_flush()  # pushes no issued exchange carried yet (none in prep mode, nprep >= 2)
+    # pushes no issued exchange carried yet (none in prep mode, nprep >= 2)
+    tr.mx_drain() if tr.merged else tr._x_flush()
     pk, pw = _weights(tr)
     loss_p = tr.progress()["loss"]
 
-    ref = _trainer(B, N, **kw)
+    kw_ref = dict(kw, exchange_merge="off")  # the two-collective schedule, same bound
+    ref = _trainer(B, N, **kw_ref)
     for m in range(T):
         k, lab = criteo_batch(B, seed=seed, row0=m * B, num_features=N, device=dev)
         ref.step(k, lab, width=39)
-    ref._x_flush()
+    ref.flush()
     torch.cuda.synchronize()
     rk, rw = _weights(ref)
     # the pipeline also resolved (inserted) the keys of the minibatches prepared
@@ -193,3 +204,31 @@ def test_flat_pipeline_matches_sequential(monkeypatch, nprep, native):
     extra_mask[pos] = False
     assert torch.all(pw[extra_mask] == 0)
     assert abs(loss_p - ref.progress()["loss"]) < 1e-5
+
+
+@pytest.mark.parametrize("kw", [{"consistency": "ssp:4"}, {"consistency": "ssp:2"},
+                                {"consistency": "ssp:4", "fixing_float_bytes": 2}])
+def test_merged_sequential_matches_two_collective(kw):
+    """The sequential API on the merged exchange (step u trains minibatch u-1, flush the
+    last) leaves exactly the table the two-collective schedule leaves (same staleness
+    bound), on the GPU kernels (strided weight rows, in-place unpack)."""
+    from parameter_server_amd.ops.synthetic import criteo_batch
+
+    B, N = 4096, 10 ** 6
+    dev = torch.device("cuda")
+    outs = []
+    for merge in ("on", "off"):
+        tr = _trainer(B, N, exchange_merge=merge, **kw)
+        assert tr.merged == (merge == "on")
+        for m in range(7):
+            k, lab = criteo_batch(B, seed=5, row0=m * B, num_features=N, device=dev)
+            tr.step(k, lab, width=39)
+        p = tr.progress()
+        assert p["examples"] == 7 * B
+        outs.append((_weights(tr), p))
+    (k1, w1), p1 = outs[0]
+    (k2, w2), p2 = outs[1]
+    assert torch.equal(k1, k2)
+    atol = 2e-5 if kw.get("fixing_float_bytes") else 1e-6
+    assert torch.allclose(w1, w2, rtol=1e-4, atol=atol)
+    assert abs(p1["loss"] - p2["loss"]) < 1e-4

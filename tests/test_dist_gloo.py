@@ -157,19 +157,24 @@ def test_padded_exchange_overflow_is_loud(tmp_path):
         _run(tmp_path, cfg_kw, steps=2)
 
 
-@pytest.mark.parametrize("tau,world,ff,apply", [(1, 2, 0, "post"), (2, 2, 0, "post"),
-                                                 (4, 2, 0, "post"), (1, 3, 0, "post"),
-                                                 (2, 3, 0, "post"), (4, 3, 0, "post"),
-                                                 (4, 2, 3, "post"), (2, 2, 0, "pre"),
-                                                 (4, 3, 0, "pre")])
-def test_ssp_exchange_matches_stale_reference(tmp_path, tau, world, ff, apply):
+@pytest.mark.parametrize("tau,world,ff,apply,merge", [
+    (1, 2, 0, "post", "off"), (2, 2, 0, "post", "off"), (4, 2, 0, "post", "off"),
+    (1, 3, 0, "post", "off"), (2, 3, 0, "post", "off"), (4, 3, 0, "post", "off"),
+    (4, 2, 3, "post", "off"), (2, 2, 0, "pre", "off"), (4, 3, 0, "pre", "off"),
+    # one all-to-all per step (MergedSchedule): lag 1 / 2 apply before the resolve,
+    # lag >= 3 after it
+    (1, 2, 0, "post", "on"), (2, 2, 0, "post", "on"), (4, 2, 0, "post", "on"),
+    (1, 3, 0, "post", "on"), (2, 3, 0, "post", "on"), (3, 3, 0, "post", "on"),
+    (4, 3, 0, "post", "on"), (4, 2, 3, "post", "on"), (4, 3, 2, "post", "on")])
+def test_ssp_exchange_matches_stale_reference(tmp_path, tau, world, ff, apply, merge):
     """consistency ssp:tau -> the pull of step s sees exactly the pushes of steps
     <= s-1-tau (ring of tau+1 exchange buffers), with the owner applying the carried
     pushes after (post: exchange t carries step t-tau) or before (pre: step t-1-tau)
-    resolving the pulls."""
+    resolving the pulls; merge="on": the one-collective schedule, same bound."""
     steps = 7
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
-                  consistency=f"ssp:{tau}", fixing_float_bytes=ff, ssp_apply=apply)
+                  consistency=f"ssp:{tau}", fixing_float_bytes=ff, ssp_apply=apply,
+                  exchange_merge=merge)
     res = _run(tmp_path, cfg_kw, steps=steps, world=world)
     merged = {}
     for r in res:
@@ -193,21 +198,42 @@ def test_explicit_smaller_lag_within_bound(tmp_path):
                                                  r["state"]["w"].tolist())}
     ref = _reference(cfg_kw, 5, 2, lag=1)
     assert max(abs(merged[k] - ref[k]) for k in ref) < 1e-5
+    # (lag 1 is served by the two-collective schedule unless exchange_merge="on")
 
 
-def test_asp_differs_from_ssp1(tmp_path):
-    """asp: the owner applies the pushes an exchange carries AFTER resolving its pulls
-    (on the GPU on its own stream, which pulls never wait for). Run in program order
-    (CPU) that is one more step of staleness than ssp:1."""
+@pytest.mark.parametrize("merge,lag", [("off", 2), ("auto", 3)])
+def test_asp_differs_from_ssp1(tmp_path, merge, lag):
+    """asp, two collectives: the owner applies the pushes an exchange carries AFTER
+    resolving its pulls (on the GPU on its own stream, which pulls never wait for). Run
+    in program order (CPU) that is one more step of staleness than ssp:1. On the merged
+    one-collective schedule asp is served with staleness exactly 3 (an admissible asp
+    schedule)."""
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
-                  consistency="asp")
+                  consistency="asp", exchange_merge=merge)
     res = _run(tmp_path, cfg_kw, steps=6, world=2)
     merged = {k: w for r in res for k, w in zip(r["state"]["keys"].tolist(),
                                                  r["state"]["w"].tolist())}
-    ref = _reference(cfg_kw, 6, 2, lag=2)
+    ref = _reference(cfg_kw, 6, 2, lag=lag)
     assert max(abs(merged[k] - ref[k]) for k in ref) < 1e-5
     ssp1 = _reference(cfg_kw, 6, 2, lag=1)
     assert max(abs(merged[k] - ssp1[k]) for k in ref) > 1e-4
+
+
+def test_merged_schedule_rings():
+    from parameter_server_amd.parallel.consistency import MergedSchedule
+
+    m = MergedSchedule(4)  # post apply, d = 3
+    assert (m.lag, m.post, m.d, m.R) == (4, True, 3, 5)
+    assert m.grads_in(10) == 7 and m.grad_ring(7) == 10 % 5 and m.visible_through(10) == 5
+    m2 = MergedSchedule(2)  # pre apply, d = 2
+    assert (m2.lag, m2.post, m2.d, m2.R) == (2, False, 2, 4)
+    a = MergedSchedule(float("inf"))
+    assert a.asp and (a.lag, a.d, a.post) == (3, 2, True)
+    assert MergedSchedule(4, lag=1).d == 1
+    with pytest.raises(ValueError):
+        MergedSchedule(0)
+    with pytest.raises(ValueError):
+        MergedSchedule(2, lag=3)
 
 
 def test_exchange_schedule_rings():
