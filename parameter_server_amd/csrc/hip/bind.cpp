@@ -52,6 +52,10 @@ void tp_fwd_bwd(const uint16_t*, const int32_t*, const int32_t*, int64_t, int, c
                 const float*, int64_t, const float*, int64_t, int, float*, double*, uint32_t*, int,
                 int, int, float*, const int32_t*, const int32_t*, const int32_t*, float*, int64_t,
                 bool, hipStream_t);
+void tp_fwd_bwd_csr(const uint16_t*, const int32_t*, const int32_t*, int64_t, const int64_t*,
+                    const int32_t*, const float*, const float*, int64_t, const float*, int64_t, int,
+                    float*, double*, uint32_t*, int, int, int, float*, const int32_t*,
+                    const int32_t*, const int32_t*, float*, int64_t, bool, hipStream_t);
 void tp_seg_update(const int32_t*, const int32_t*, int64_t, const int32_t*, const float*,
                    const int32_t*, const int32_t*, unsigned long long*, int64_t, const int64_t*, void*,
                    int64_t, int, int, float, float, float, float, float, float, double*, int,
@@ -447,6 +451,60 @@ Launch make_tp_fwd_bwd(Tensor rep, Tensor dcnt, optional<Tensor> ent_uid, int64_
                       ptr<float>(w_local), w_local.numel(), ptr<float>(labels), B, loss_type,
                       ptr<float>(coef), mp, hp, nbins, mstripes, hstripes, ptr<float>(psum),
                       ps, sg, ne, gr, gcap, reduce, st);
+  };
+}
+
+// Variable-width / valued rows (CSR): row_ptr [B+1] int64, rows [n] int32 (row of every
+// occurrence, csr_rows), vals [n] or None. Same buffers / flat rule as make_tp_fwd_bwd.
+Launch make_tp_fwd_bwd_csr(Tensor rep, Tensor dcnt, optional<Tensor> ent_uid, int64_t n,
+                           Tensor row_ptr, Tensor rows, optional<Tensor> vals, Tensor w_local,
+                           Tensor labels, int64_t B, int loss_type, Tensor coef,
+                           optional<Tensor> metrics, optional<Tensor> hist, int nbins,
+                           Tensor psum, optional<Tensor> pos_s, optional<Tensor> segid,
+                           optional<Tensor> n_ent, optional<Tensor> grad, bool reduce) {
+  chk(rep, at::kShort, "rep");
+  chk(dcnt, at::kInt, "dcnt");
+  chk(row_ptr, at::kLong, "row_ptr");
+  chk(rows, at::kInt, "rows");
+  const int32_t* eu = optr<int32_t>(ent_uid, at::kInt, "ent_uid");
+  chk(w_local, at::kFloat, "w_local");
+  chk(labels, at::kFloat, "labels");
+  chk(coef, at::kFloat, "coef");
+  chk(psum, at::kFloat, "psum");
+  int32_t* ps = optr<int32_t>(pos_s, at::kInt, "pos_s");
+  int32_t* sg = optr<int32_t>(segid, at::kInt, "segid");
+  int32_t* ne = optr<int32_t>(n_ent, at::kInt, "n_ent");
+  float* gr = optr<float>(grad, at::kFloat, "grad");
+  check(n > 0 && B > 0 && row_ptr.numel() >= B + 1 && rows.numel() >= n,
+        "tp_fwd_bwd_csr: row_ptr [B+1], rows [n]");
+  check(psamd::tploc_stride(n) / psamd::tploc_tile() <= 640, "tp_fwd_bwd_csr: <= 5.2 M keys");
+  const int64_t N = psamd::tploc_stride(n);
+  check(rep.numel() >= n && dcnt.numel() >= N / psamd::tploc_tile(), "tp_fwd_bwd_csr: rep / dcnt");
+  check(psum.numel() >= N, "tp_fwd_bwd_csr: psum < stride");
+  if (eu) {
+    check(ent_uid->numel() >= N, "tp_fwd_bwd_csr: ent_uid < stride");
+    check(!reduce || (ps && sg && ne && gr && pos_s->numel() >= N && segid->numel() >= N),
+          "tp_fwd_bwd_csr: entry CSC buffers");
+  } else {
+    check(w_local.numel() >= N && !reduce, "tp_fwd_bwd_csr flat: w_ent >= stride, no reduce");
+  }
+  check(labels.numel() >= B && coef.numel() >= B, "labels/coef too small");
+  const float* v = optr<float>(vals, at::kFloat, "vals");
+  if (v) check(vals->numel() >= n, "vals too small");
+  uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
+  if (hp) check(nbins > 0 && nbins <= 8192 && hist->numel() >= 2 * nbins, "hist size");
+  double* mp = optr<double>(metrics, at::kDouble, "metrics");
+  if (mp) check(metrics->numel() >= 5, "metrics needs >= 5 slots");
+  const int mstripes = acc_stripes_of(metrics);
+  const int hstripes = hp ? (int)std::max<int64_t>(1, hist->numel() / (2 * nbins)) : 1;
+  const int64_t gcap = gr ? grad->numel() : 0;
+  return [=, keep = std::vector<optional<Tensor>>{rep, dcnt, ent_uid, row_ptr, rows, vals,
+                                                  w_local, labels, coef, metrics, hist, psum,
+                                                  pos_s, segid, n_ent, grad}](hipStream_t st) {
+    psamd::tp_fwd_bwd_csr(ptr<uint16_t>(rep), ptr<int32_t>(dcnt), eu, n, ptr<int64_t>(row_ptr),
+                          ptr<int32_t>(rows), v, ptr<float>(w_local), w_local.numel(),
+                          ptr<float>(labels), B, loss_type, ptr<float>(coef), mp, hp, nbins,
+                          mstripes, hstripes, ptr<float>(psum), ps, sg, ne, gr, gcap, reduce, st);
   };
 }
 
@@ -984,6 +1042,16 @@ PYBIND11_MODULE(_hipops, m) {
                          bool reduce) {
     make_tp_fwd_bwd(rep, dcnt, ent_uid, n, width, vals, w_local, labels, B, loss_type, coef,
                     metrics, hist, nbins, psum, pos_s, segid, n_ent, grad, reduce)(cur_stream());
+  });
+  m.def("tp_fwd_bwd_csr", [](Tensor rep, Tensor dcnt, optional<Tensor> ent_uid, int64_t n,
+                             Tensor row_ptr, Tensor rows, optional<Tensor> vals, Tensor w_local,
+                             Tensor labels, int64_t B, int loss_type, Tensor coef,
+                             optional<Tensor> metrics, optional<Tensor> hist, int nbins,
+                             Tensor psum, optional<Tensor> pos_s, optional<Tensor> segid,
+                             optional<Tensor> n_ent, optional<Tensor> grad, bool reduce) {
+    make_tp_fwd_bwd_csr(rep, dcnt, ent_uid, n, row_ptr, rows, vals, w_local, labels, B,
+                        loss_type, coef, metrics, hist, nbins, psum, pos_s, segid, n_ent, grad,
+                        reduce)(cur_stream());
   });
   // A validate-once launch list: the add_* calls check their arguments exactly as the
   // single ops above and keep the tensors alive; run() issues every launch in order on

@@ -1275,6 +1275,189 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
 }
 #undef FB_MARK
 
+// Variable-width / valued rows (CSR ``row_ptr`` + per-occurrence ``rows``, optional
+// ``vals``; reference SparseMatrix::rangeTimes, src/util/sparse_matrix.h:73-107): the
+// same fused forward + tile backward per 8192-occurrence tile as tp_fwd_bwd_kernel, for
+// rows of any width. Thread t holds the tile's occurrences [8t, 8t+8) in registers
+// (entry, value, row); a row's margin is summed in registers along the thread's run and
+// added into an LDS row array once per run (rows of the tile: <= kCsrRows per window,
+// windows repeat for tiles of very short rows). A row that starts before the tile or
+// ends after it (the boundary rows) gets its outside part from one wave each, through
+// the neighbour tiles' entry maps (flat: w_ent in tile-entry order). Every tile that
+// holds part of a row computes that row's margin in full, so each uses the row's coef
+// for its own entries; only the tile holding the row's first occurrence reports it
+// (coef_out, loss, accuracy, AUC bin). Backward: 64-bit fixed point per tile entry
+// (scale from the tile's largest |coef x val|), as the fixed-width kernel.
+constexpr int kCsrRows = 4080;  // LDS row slots of one window (80 KB of LDS in all: 2 per CU)
+// (~90 VGPRs: one workgroup per CU; a 64-VGPR bound spilled 100 B per lane. Real-data
+// minibatches of this path are 10-600 tiles, so the grid rarely fills 2 per CU anyway.)
+template <bool kFlat>
+__global__ void __launch_bounds__(tp::kThr)
+tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ dcnt,
+                      const int32_t* __restrict__ ent_uid, int64_t n,
+                      const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ rows,
+                      const float* __restrict__ vals, const float* __restrict__ w_local,
+                      int64_t w_cap, const float* __restrict__ labels, int64_t B, int loss_type,
+                      float* __restrict__ coef_out, double* __restrict__ metrics,
+                      uint32_t* __restrict__ hist, int nbins, int acc_stripes, int hist_stripes,
+                      float* __restrict__ psum) {
+  using namespace tp;
+  __shared__ unsigned long long region[kTile];  // fwd: entry weights + AUC bins; bwd: i64 acc
+  __shared__ float crow[kCsrRows];              // a window's row margins, then their coefs
+  __shared__ float sacc[4];
+  __shared__ float sc0;                         // coef of row r0 when an earlier tile owns it
+  __shared__ uint32_t smax;
+  float* const wl = reinterpret_cast<float*>(region);
+  uint32_t* const lhist = reinterpret_cast<uint32_t*>(region) + kTile;
+  long long* const acc = reinterpret_cast<long long*>(region);
+  constexpr int kPer = kTile / kThr;  // 8 occurrences per thread
+  constexpr uint32_t kNone = 0xffffffffu;
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int lim = (int)(n - base < kTile ? n - base : kTile);
+  const int cnt = min(kTile, max(0, dcnt[blockIdx.x]));
+  const int64_t r0 = rows[base], r1 = rows[base + lim - 1];  // (uniform loads)
+  // occurrence = (row - r0) << 16 | tile entry (rows of a tile < 2^14, entries < 2^13)
+  uint32_t er[kPer];
+  float v[kPer];
+  {  // 8 consecutive occurrences per thread: 16 / 32-byte loads, adjacent across lanes
+    const int64_t i0 = base + (int64_t)t * kPer;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const bool in = t * kPer + j < lim;
+      const int64_t i = in ? i0 + j : base;
+      const uint32_t ee = rep[i];
+      const int32_t rr = rows[i];
+      er[j] = in ? (uint32_t)(rr - r0) << 16 | ee : kNone;
+      v[j] = in ? (vals ? vals[i] : 1.f) : 0.f;
+    }
+  }
+  const bool own0 = row_ptr[r0] >= base;
+  if (t < 4) sacc[t] = 0.f;
+  if (t == 0) smax = 0u;
+  if (kFlat) {
+    for (int i = t; i < cnt; i += kThr) wl[i] = w_local[base + i];
+  } else {
+    for (int i = t; i < cnt; i += kThr) {
+      const int32_t u = ent_uid[base + i];
+      wl[i] = in_range(u, w_cap) ? w_local[u] : 0.f;
+    }
+  }
+  if (hist)
+    for (int i = t; i < 2 * nbins; i += kThr) lhist[i] = 0u;
+  const int wave = t / 64, lane = t % 64;
+  const int nr = (int)(r1 - r0 + 1);
+  float loss_acc = 0.f, corr_acc = 0.f, rows_acc = 0.f;
+  for (int wa = 0; wa < nr; wa += kCsrRows) {  // row windows (1 unless rows are tiny)
+    const int wb = min(nr, wa + kCsrRows);
+    for (int i = t; i < wb - wa; i += kThr) crow[i] = 0.f;
+    __syncthreads();
+    {  // this thread's runs of equal rows -> one LDS add per run
+      uint32_t cur = kNone;
+      float sum = 0.f;
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        if (er[j] == kNone) continue;
+        const uint32_t rr = er[j] >> 16;
+        if (rr != cur) {
+          if (cur != kNone && (int)cur >= wa && (int)cur < wb && sum != 0.f)
+            atomicAdd(&crow[cur - wa], sum);
+          cur = rr;
+          sum = 0.f;
+        }
+        sum += wl[er[j] & 0xffffu] * v[j];
+      }
+      if (cur != kNone && (int)cur >= wa && (int)cur < wb && sum != 0.f)
+        atomicAdd(&crow[cur - wa], sum);
+    }
+    // boundary rows: wave 0 sums the part of row r0 before the tile, wave 1 the part of
+    // row r1 after it (any length; a row longer than a tile has both)
+    if (wave < 2) {
+      const int rl = wave == 0 ? 0 : nr - 1;
+      if (rl >= wa && rl < wb) {
+        const int64_t r = r0 + rl;
+        const int64_t a = wave == 0 ? row_ptr[r] : base + lim;
+        const int64_t b = wave == 0 ? base : row_ptr[r + 1];
+        float sum = 0.f;
+        for (int64_t i = a + lane; i < b; i += 64) {
+          const int64_t ge = (i / kTile) * kTile + (int64_t)rep[i];
+          const int64_t u = kFlat ? ge : (int64_t)ent_uid[ge];
+          sum += (in_range(u, w_cap) ? w_local[u] : 0.f) * (vals ? vals[i] : 1.f);
+        }
+        sum = wave_sum(sum);
+        if (lane == 0 && sum != 0.f) atomicAdd(&crow[rl - wa], sum);
+      }
+    }
+    __syncthreads();
+    for (int i = t; i < wb - wa; i += kThr) {  // per row: loss terms -> coef
+      const int64_t r = r0 + wa + i;
+      float c = 0.f;
+      if (r < B) {
+        const float m = crow[i];
+        const float lab = labels[r];
+        float loss, c2;
+        loss_terms(m, lab, loss_type, loss, c, c2);
+        if (wa + i > 0 || own0) {  // the row's first occurrence is in this tile
+          coef_out[r] = c;
+          loss_acc += loss;
+          corr_acc += ((lab > 0.f) == (m > 0.f)) ? 1.f : 0.f;
+          rows_acc += 1.f;
+          if (hist) atomicAdd(&lhist[auc_bin(m, lab, nbins)], 1u);
+        } else {
+          sc0 = c;
+        }
+      }
+      crow[i] = c;
+    }
+    __syncthreads();
+  }
+  // coef of an occurrence's row: the window in LDS (one window), else the row's coef as
+  // this workgroup wrote it to coef_out (sc0 for a row an earlier tile owns)
+  const bool one = nr <= kCsrRows;
+  auto coef_of = [&](uint32_t rr) -> float {
+    if (one) return crow[rr];
+    if (rr == 0 && !own0) return sc0;
+    return coef_out[r0 + rr];
+  };
+  float vmax = 0.f;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if (er[j] != kNone) vmax = fmaxf(vmax, fabsf(coef_of(er[j] >> 16) * v[j]));
+  fx_tile_max(vmax, &smax);
+  if (metrics && rows_acc > 0.f) {
+    atomicAdd(&sacc[0], loss_acc);
+    atomicAdd(&sacc[1], corr_acc);
+    atomicAdd(&sacc[2], rows_acc);
+  }
+  __syncthreads();
+  if (hist) {
+    uint32_t* hs = hist + (int64_t)(blockIdx.x % hist_stripes) * 2 * nbins;
+    for (int i = t; i < 2 * nbins; i += kThr)
+      if (lhist[i]) atomicAdd(&hs[i], lhist[i]);
+  }
+  if (metrics && t == 0 && sacc[2] > 0.f) {
+    double* mt = acc_stripe(metrics, acc_stripes);
+    atomicAdd(&mt[0], (double)sacc[0]);
+    atomicAdd(&mt[1], (double)sacc[1]);
+    atomicAdd(&mt[2], (double)sacc[2]);
+  }
+  const uint32_t mb = smax;
+  __syncthreads();
+  for (int i = t; i < cnt; i += kThr) acc[i] = 0ll;
+  __syncthreads();
+  const int k2 = fx_shift(mb);
+  const double sc = ldexp(1.0, k2);
+#pragma unroll
+  for (int j = 0; j < kPer; ++j)
+    if (er[j] != kNone) {
+      const float c = coef_of(er[j] >> 16);
+      if (c != 0.f) fx_add(acc, er[j] & 0xffffu, c * v[j], sc);
+    }
+  __syncthreads();
+  const double isc = ldexp(1.0, -k2);
+  for (int i = t; i < cnt; i += kThr) psum[base + i] = (float)((double)acc[i] * isc);
+}
+
 void tp_fb_set_prof(uint64_t* p) {
   PSAMD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_fb_prof), &p, sizeof(p)));
 }
@@ -2393,6 +2576,34 @@ void tp_fwd_bwd(const uint16_t* rep, const int32_t* dcnt, const int32_t* ent_uid
 #undef PSAMD_FB
   PSAMD_HIP_CHECK(hipGetLastError());
   if (!reduce) return;  // (the caller runs tp_seg_update instead)
+  tp_seg_reduce_kernel<<<grid_for(g.N, 256, 2048), 256, 0, st>>>(pos_s, segid, g.N, n_ent, psum,
+                                                                 g.N, grad, grad_cap);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void tp_fwd_bwd_csr(const uint16_t* rep, const int32_t* dcnt, const int32_t* ent_uid, int64_t n,
+                    const int64_t* row_ptr, const int32_t* rows, const float* vals,
+                    const float* w_local, int64_t w_cap, const float* labels, int64_t B,
+                    int loss_type, float* coef_out, double* metrics, uint32_t* hist, int nbins,
+                    int acc_stripes, int hist_stripes, float* psum, const int32_t* pos_s,
+                    const int32_t* segid, const int32_t* n_ent, float* grad, int64_t grad_cap,
+                    bool reduce, hipStream_t st) {
+  if (n <= 0) return;
+  const TpGeom g = tp_geom(n, 31);
+  if (hist && (nbins <= 0 || nbins > kFbMaxBins))
+    throw std::runtime_error("tp_fwd_bwd_csr: 1..2048 AUC bins (LDS histogram)");
+  const bool flat = ent_uid == nullptr;
+  if (flat && w_cap < g.N) throw std::runtime_error("tp_fwd_bwd_csr: flat w_ent < tile stride");
+  if (flat)
+    tp_fwd_bwd_csr_kernel<true><<<(unsigned)g.T, tp::kThr, 0, st>>>(
+        rep, dcnt, ent_uid, n, row_ptr, rows, vals, w_local, w_cap, labels, B, loss_type,
+        coef_out, metrics, hist, nbins, acc_stripes, hist_stripes, psum);
+  else
+    tp_fwd_bwd_csr_kernel<false><<<(unsigned)g.T, tp::kThr, 0, st>>>(
+        rep, dcnt, ent_uid, n, row_ptr, rows, vals, w_local, w_cap, labels, B, loss_type,
+        coef_out, metrics, hist, nbins, acc_stripes, hist_stripes, psum);
+  PSAMD_HIP_CHECK(hipGetLastError());
+  if (!reduce) return;
   tp_seg_reduce_kernel<<<grid_for(g.N, 256, 2048), 256, 0, st>>>(pos_s, segid, g.N, n_ent, psum,
                                                                  g.N, grad, grad_cap);
   PSAMD_HIP_CHECK(hipGetLastError());

@@ -311,6 +311,16 @@ class SparseLRTrainer:
                 self._flat_step(loc, labels, B, width, next_loc,
                                 pre == (id(loc), loc.gen))
                 return
+            if (prefetch is None and B < (1 << 25) and (loc is None or getattr(loc, "flat", False))
+                    and (row_ptr is not None or vals is not None)):
+                # valued and / or variable-width rows: the same flat step with the CSR
+                # fused forward + tile backward (tp_fwd_bwd_csr)
+                if loc is None:
+                    loc = self.localizer(keys)
+                row_ptr, rows = self._csr_of(B, width, loc.nnz, row_ptr, rows, keys.device)
+                self._flat_step_csr(loc, labels, B, row_ptr, rows, vals, next_loc,
+                                    pre == (id(loc), loc.gen))
+                return
             # not expressible on the flat layout (valued / variable-width rows): the same
             # keys through a compact "tp" localisation and the generic step below
             loc = self._compact_localizer()(keys)
@@ -451,6 +461,54 @@ class SparseLRTrainer:
         launch. One native launch list per (buffers, labels, next buffers)."""
         plan, nxt = self.flat_plan(loc, labels, B, width, next_loc, pre)
         plan.run()
+        self.flat_done(B, nxt)
+
+    def _csr_of(self, B: int, width, nnz: int, row_ptr, rows, device):
+        """(row_ptr, rows) of a minibatch: given, or a fixed width's arithmetic row_ptr
+        (cached per shape); rows = the row of every occurrence (csr_rows)."""
+        if row_ptr is None:
+            key = ("rp", B, width)
+            row_ptr = self._coef_views.get(key)
+            if row_ptr is None:
+                row_ptr = self._coef_views[key] = torch.arange(
+                    0, (B + 1) * width, width, dtype=torch.int64, device=device)
+        if rows is None:
+            rows = self._rows_buf(nnz)
+            if self.gpu:
+                hipops().csr_rows(row_ptr, rows)
+            else:
+                rows.copy_(self._csr_rows(row_ptr, nnz))
+        return row_ptr, rows
+
+    def _rows_buf(self, nnz: int) -> torch.Tensor:
+        rb = getattr(self, "_rows", None)
+        if rb is None or rb.numel() < nnz:
+            rb = self._rows = torch.empty(max(nnz, self.max_nnz), dtype=torch.int32,
+                                          device=self.device)
+        return rb[:nnz]
+
+    def _flat_step_csr(self, loc, labels, B: int, row_ptr, rows, vals, next_loc, pre: bool):
+        """The flat 1-GPU step for valued / variable-width rows: pull (unless issued
+        ahead), the CSR fused forward + tile backward, then tpf_step (update of this
+        minibatch + pull of ``next_loc``). Issued op by op: minibatch shapes vary."""
+        nxt = next_loc if (next_loc is not None and getattr(next_loc, "flat", False)
+                           and next_loc.nnz == loc.nnz and next_loc is not loc) else None
+        H, tb = hipops(), self.table
+        it, iv, isd, seed = tb.init.args()
+        n, bits = loc.nnz, loc.bits
+        common = (tb.slots, it, iv, isd, seed, tb._err, tb._inserted, tb.home_base, tb.home_m,
+                  *self.rule.args(), self.stats)
+        if not pre:
+            H.tpf_step(n, bits, None, None, loc.bufs, loc.w_ent, *common, None, None, None)
+        coef = self._coef_views.get(B)
+        if coef is None:
+            coef = self._coef_views[B] = self.coef[:B]
+        H.tp_fwd_bwd_csr(loc.rep, loc.dcnt, None, n, row_ptr, rows, vals, loc.w_ent, labels, B,
+                         loss_id(self.cfg.loss), coef, self.metrics, self.hist, AUC_BINS,
+                         loc.psum, None, None, None, None, False)
+        H.tpf_step(n, bits, loc.bufs, loc.psum, nxt.bufs if nxt is not None else None,
+                   nxt.w_ent if nxt is not None else None, *common, self.hist, self.metrics,
+                   self.step_dev)
         self.flat_done(B, nxt)
 
     def flat_done(self, B: int, nxt):
@@ -620,12 +678,20 @@ class SparseLRTrainer:
         if width is None and row_ptr is None:
             width = self.cfg.max_nnz_per_example
         flat = getattr(loc, "flat", False)
-        if flat and not (row_ptr is None and rows is None and vals is None
-                         and self._flat_ok(B, width, loc.nnz)
+        csr = flat and (row_ptr is not None or vals is not None)  # CSR fused fwd/bwd
+        if flat and not ((csr or (row_ptr is None and rows is None and vals is None
+                                  and self._flat_ok(B, width, loc.nnz)))
                          and hipops().tpf_exchange_ok(loc.nnz, self.bits, self.G)):
             # not expressible on the flat layout: the same keys, localised compactly
             loc, flat = self._compact_localizer()(keys), False
-        if row_ptr is not None and rows is None:
+        csr_args = None
+        if flat and (row_ptr is not None or vals is not None):
+            rp = row_ptr if row_ptr is not None else torch.arange(
+                0, (B + 1) * width, width, dtype=torch.int64, device=loc.rep.device)
+            rw = rows if rows is not None else torch.empty(loc.nnz, dtype=torch.int32,
+                                                           device=loc.rep.device)
+            csr_args = (rp, rw, vals)
+        elif row_ptr is not None and rows is None:
             rows = (torch.empty(keys.numel(), dtype=torch.int32, device=keys.device) if self.gpu
                     else self._csr_rows(row_ptr, keys.numel()))
         if self.xc is None:
@@ -637,7 +703,9 @@ class SparseLRTrainer:
 
         def finish():
             if flat:
-                return self._x_finish_flat(loc, labels, B, width, r)
+                if csr_args is not None:  # the row of every occurrence, at replay time
+                    hipops().csr_rows(csr_args[0], csr_args[1])
+                return self._x_finish_flat(loc, labels, B, width, r, csr=csr_args)
             if row_ptr is not None and self.gpu:
                 hipops().csr_rows(row_ptr, rows)
             self._x_finish(loc, labels, B, width, row_ptr, vals, rows, r)
@@ -774,8 +842,22 @@ class SparseLRTrainer:
             width = self.cfg.max_nnz_per_example
         wsrc = self._mx_wview(xc.recvs[b])
         if getattr(loc, "flat", False):
-            return lambda: self._x_finish_flat(loc, labels, B, width, b, send=xc.sends[bg],
-                                               wsrc=wsrc, wstride=xc.H)
+            csr = None
+            if row_ptr is not None or vals is not None:
+                rw = rows if rows is not None else torch.empty(loc.nnz, dtype=torch.int32,
+                                                               device=self.device)
+                rp = row_ptr
+                if rp is None:
+                    rp = torch.arange(0, (B + 1) * width, width, dtype=torch.int64,
+                                      device=self.device)
+                csr = (rp, rw, vals)
+
+            def fin_flat():
+                if csr is not None:  # (rows: scratch, refilled from row_ptr)
+                    hipops().csr_rows(csr[0], csr[1])
+                self._x_finish_flat(loc, labels, B, width, b, send=xc.sends[bg], wsrc=wsrc,
+                                    wstride=xc.H, csr=csr)
+            return fin_flat
 
         def fin():
             if row_ptr is not None and self.gpu:
@@ -834,8 +916,9 @@ class SparseLRTrainer:
                 width = self.cfg.max_nnz_per_example
             buf = self._xt + (self._mx_pend is not None)  # step index of this minibatch
             if loc is None:
-                flat_ok = (self.localize_mode == "tpf" and row_ptr is None and rows is None
-                           and vals is None and self._flat_ok(B, width, keys.numel())
+                flat_ok = (self.localize_mode == "tpf"
+                           and (row_ptr is not None or vals is not None
+                                or (rows is None and self._flat_ok(B, width, keys.numel())))
                            and hipops().tpf_exchange_ok(keys.numel(), self.bits, self.G))
                 loc = (self.localize(keys, buf=buf % 2) if flat_ok
                        else self._compact_localizer(buf % 2)(keys))
@@ -1079,7 +1162,7 @@ class SparseLRTrainer:
             hh.xchg_publish(xc.ovf, xc.ovf_host)
 
     def _x_finish_flat(self, loc, labels, B: int, width: int, r: int, send=None, wsrc=None,
-                       wstride: int = 0):
+                       wstride: int = 0, csr=None):
         """Flat layout, worker half: the pulled weights into tile-entry order, the flat
         fused forward + tile backward, every key's gradient (per-bucket fixed-point sums)
         into its owner's row of the next exchange [+ FixingFloat codes], AUC epilogue.
@@ -1093,9 +1176,14 @@ class SparseLRTrainer:
         coef = self._coef_views.get(B)
         if coef is None:
             coef = self._coef_views[B] = self.coef[:B]
-        hh.tp_fwd_bwd(loc.rep, loc.dcnt, None, n, width, None, loc.w_ent, labels, B,
-                      loss_id(self.cfg.loss), coef, self.metrics, self.hist, AUC_BINS, loc.psum,
-                      None, None, None, None, False)
+        if csr is not None:  # (row_ptr, rows, vals): valued / variable-width rows
+            hh.tp_fwd_bwd_csr(loc.rep, loc.dcnt, None, n, csr[0], csr[1], csr[2], loc.w_ent,
+                              labels, B, loss_id(self.cfg.loss), coef, self.metrics, self.hist,
+                              AUC_BINS, loc.psum, None, None, None, None, False)
+        else:
+            hh.tp_fwd_bwd(loc.rep, loc.dcnt, None, n, width, None, loc.w_ent, labels, B,
+                          loss_id(self.cfg.loss), coef, self.metrics, self.hist, AUC_BINS,
+                          loc.psum, None, None, None, None, False)
         if xc.nb:
             hh.xchg_ff_init(send, xc.H)
         hh.tpf_pack_grads(n, bits, G, loc.cnt, loc.ent_pos, loc.ent_j, xc.C, xc.kw, xc.H,

@@ -413,3 +413,130 @@ def test_overlapped_step_kernel_is_bitwise_the_sequential_one(monkeypatch, data,
     for a, b in zip(outs[0][1:], outs[1][1:]):
         assert torch.equal(a, b)
     assert outs[0][0]["nnz_w"] == outs[1][0]["nnz_w"]
+
+
+# ---------------------------------------------- valued / variable-width rows (CSR)
+def _csr_batch(B: int, seed: int, lo: int = 5, hi: int = 145, valued: bool = True,
+               long_row: int = 0, N: int = 10 ** 8):
+    """rcv1-like minibatch: widths uniform in [lo, hi) (~75 on average), power-law keys
+    (a hot head shared across rows), tf-idf-like values in (0, 1]; optionally one row of
+    ``long_row`` features (longer than a tile: spans >= 2 tiles)."""
+    g = torch.Generator().manual_seed(seed)
+    w = torch.randint(lo, hi, (B,), generator=g)
+    if long_row:
+        w[B // 2] = long_row
+    row_ptr = torch.zeros(B + 1, dtype=torch.int64)
+    row_ptr[1:] = torch.cumsum(w, 0)
+    n = int(row_ptr[-1])
+    u = torch.rand(n, generator=g, dtype=torch.float64)
+    keys = (N * u ** 4).long().clamp(max=N - 1)  # power law: many repeats of small ids
+    vals = (torch.rand(n, generator=g) * 0.9 + 0.1) if valued else None
+    labels = torch.where(torch.rand(B, generator=g) < 0.35, 1.0, -1.0)
+    return (keys.to(DEV), labels.to(DEV), row_ptr.to(DEV),
+            None if vals is None else vals.to(DEV))
+
+
+def _reference_train_csr(batches, rule):
+    """Plain fp32 PyTorch loop over CSR minibatches (valued), one update per minibatch."""
+    allk = torch.unique(torch.cat([b[0].cpu() for b in batches]))
+    K = allk.numel()
+    W, Z, Nn = torch.zeros(K), torch.zeros(K), torch.zeros(K)
+    for keys, labels, row_ptr, vals in batches:
+        k, y, rp = keys.cpu(), labels.cpu(), row_ptr.cpu()
+        B = y.numel()
+        x = vals.cpu() if vals is not None else torch.ones(k.numel())
+        row = torch.repeat_interleave(torch.arange(B), rp[1:] - rp[:-1])
+        idx = torch.searchsorted(allk, k)
+        m = torch.zeros(B, dtype=torch.float64).index_add_(0, row, (W[idx] * x).double()).float()
+        yy = torch.where(y > 0, 1.0, -1.0)
+        coef = -yy * torch.sigmoid(-yy * m)
+        g = torch.zeros(K, dtype=torch.float64).index_add_(0, idx, (coef[row] * x).double()).float()
+        u = torch.unique(idx)
+        gu, w_old = g[u] * rule.grad_scale, W[u]
+        n_new = torch.sqrt(Nn[u] * Nn[u] + gu * gu)
+        sigma = (n_new - Nn[u]) / rule.alpha
+        Z[u] = Z[u] + gu - sigma * w_old
+        Nn[u] = n_new
+        eta = rule.alpha / (n_new + rule.beta)
+        zz = -Z[u] * eta
+        leta = rule.l1 * eta
+        W[u] = torch.where(zz.abs() <= leta, torch.zeros_like(zz),
+                           (zz - torch.sign(zz) * leta) / (1 + rule.l2 * eta))
+    return allk, W, Z, Nn
+
+
+@pytest.mark.parametrize("B,valued,long_row", [(1000, True, 0), (10000, True, 0),
+                                                (3000, False, 0), (2000, True, 20000)])
+def test_flat_csr_step_matches_fp32_reference(monkeypatch, B, valued, long_row):
+    """5 steps of valued / variable-width rows on the flat 1-GPU path (CSR fused forward +
+    tile backward, tpf_step) against the fp32 PyTorch loop: weights, z, n to rtol 1e-4.
+    Covers rows straddling tiles and a row longer than a tile."""
+    monkeypatch.setenv("PSAMD_FLAT", "1")
+    batches = [_csr_batch(B, 200 + s, valued=valued, long_row=long_row) for s in range(5)]
+    maxn = max(int(b[2][-1]) for b in batches)
+    cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B,
+                         max_nnz_per_example=(maxn + B - 1) // B, table_capacity=1 << 22,
+                         alpha=0.05, l1=1.0, l2=0.1)
+    tr = SparseLRTrainer(cfg, device=DEV)
+    assert tr.localize_mode == "tpf"
+    for k, lab, rp, v in batches:
+        tr.step(k, lab, row_ptr=rp, vals=v)
+    torch.cuda.synchronize()
+    assert tr._compact is None  # the flat path ran every step
+    p = tr.progress()
+    assert p["examples"] == 5 * B
+    allk, W, Z, Nn = _reference_train_csr(batches, cfg.update_rule())
+    w, z, n = _table_by_raw_key(tr, allk)
+    torch.testing.assert_close(w, W, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(z, Z, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(n, Nn, rtol=1e-4, atol=1e-4)
+    assert (w != 0).sum() > 50
+
+
+def test_flat_fixed_width_valued_rows_take_the_csr_kernel(monkeypatch):
+    """Fixed-width rows WITH values (no row_ptr): the flat step synthesises row_ptr."""
+    monkeypatch.setenv("PSAMD_FLAT", "1")
+    B = 4096
+    batches = []
+    for s in range(4):
+        k, lab = criteo_batch(B, seed=61, row0=s * B, num_features=10 ** 8, device=DEV)
+        v = torch.rand(k.numel(), device=DEV, generator=torch.Generator(device=DEV).manual_seed(s))
+        batches.append((k, lab, torch.arange(0, (B + 1) * 39, 39, device=DEV), v))
+    cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B, table_capacity=1 << 22)
+    tr = SparseLRTrainer(cfg, device=DEV)
+    for k, lab, _, v in batches:
+        tr.step(k, lab, width=39, vals=v)
+    torch.cuda.synchronize()
+    allk, W, Z, Nn = _reference_train_csr(batches, cfg.update_rule())
+    w, z, n = _table_by_raw_key(tr, allk)
+    torch.testing.assert_close(w, W, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(n, Nn, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("merge", ["on", "off"])
+def test_flat_csr_multi_peer_matches_compact(monkeypatch, merge):
+    """2 emulated peers, ssp:2: the flat exchange with the CSR fused kernel leaves the
+    same table as the compact layout with the generic kernels (PSAMD_FLAT=0)."""
+    from parameter_server_amd.parallel.comm import LoopbackComm
+
+    B = 3000
+    batches = [_csr_batch(B, 300 + s) for s in range(6)]
+    maxn = max(int(b[2][-1]) for b in batches)
+    outs = []
+    for flat in ("1", "0"):
+        monkeypatch.setenv("PSAMD_FLAT", flat)
+        cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B, consistency="ssp:2",
+                             max_nnz_per_example=(maxn + B - 1) // B, table_capacity=1 << 22,
+                             alpha=0.05, l1=1.0, l2=0.1, exchange_merge=merge)
+        tr = SparseLRTrainer(cfg, LoopbackComm(2, "cuda"), DEV)
+        assert (tr.localize_mode == "tpf") == (flat == "1")
+        for k, lab, rp, v in batches:
+            tr.step(k, lab, row_ptr=rp, vals=v)
+        p = tr.progress()
+        kk, w, z, n = tr.table.occupied()
+        o = torch.argsort(kk)
+        outs.append((kk[o].cpu(), w[o].cpu(), n[o].cpu(), p))
+    assert torch.equal(outs[0][0], outs[1][0])
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(outs[0][2], outs[1][2], rtol=1e-4, atol=1e-4)
+    assert abs(outs[0][3]["loss"] - outs[1][3]["loss"]) < 1e-4
