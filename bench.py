@@ -211,6 +211,12 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     preps = [(lambda b=b: prep(b)) for b in range(NB)]
     graphs = {"on": False}
     state = {"t": 0}
+    # 1 GPU, flat: the preparation of minibatch t + nprep also waits for step t-1
+    # (implies the buffer wait: steps complete in order); PSAMD_PREP_GATE=0: buffer only
+    # (auto: B >= 32,768, where a preparation is shorter than a step; at B = 10,000 the
+    # latency-bound preparation outlasts a step and needs the two-step window)
+    gate = os.environ.get("PSAMD_PREP_GATE", "auto")
+    prep_gate = flat and nprep >= 2 and (gate == "1" or (gate == "auto" and B >= 32768))
 
     def issue_exchange(t):
         xs = sides[(t % NB) % nprep] if xmode == "prep" else comm_s
@@ -288,7 +294,10 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             ev_w[t % E].record(main)
         nb = (t + nprep) % NB                 # minibatch t + nprep
         s = sides[nb % nprep]
-        s.wait_event(ev_buf[nb])              # step(t + nprep - NB) done with bufs[nb]
+        # step(t + nprep - NB) done with bufs[nb]; with prep_gate the preparation also
+        # waits for step t-1, so it runs beside step t and not in a burst with the other
+        # streams' preparations (the first timed steps after an idle GPU)
+        s.wait_event(ev_buf[(t - 1) % NB] if prep_gate else ev_buf[nb])
         # a plain set_stream there and back (main is current here): the torch.cuda.stream
         # context re-queries the current stream and the lazy-init state on every use, ~10
         # us of host time per step (cProfile, profiles/r3_s3_host_issue.log)
@@ -341,7 +350,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             L.extend(splan)
             L.add_record(ev_buf[cur])
             L.add_stream(s)
-            L.add_wait(ev_buf[nb])
+            L.add_wait(ev_buf[(j - 1) % NB] if prep_gate else ev_buf[nb])
             L.extend(fplans[nb].plan)
             L.add_record(ev_prep[nb])
             phases.append((L.run, locs[nxt], fplans[nb].done))

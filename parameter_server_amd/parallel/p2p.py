@@ -21,6 +21,17 @@ A pusher waits (bounded device spin) only when it is ``Q`` steps ahead of what a
 owner has applied from it: the staleness bound of this mode. Between ranks there is
 no lock step, so a slow rank delays only the application of its own pushes.
 
+A second, documented source of staleness: a peer's one-sided lookup reads the owner's
+table (ordinary coarse-grained HBM, mapped over xGMI) while the owner's apply kernels
+write it. A remote read returns the slot's weight as of some point during the owner's
+update stream -- before or after any given in-flight apply, and never torn (the
+weight is one aligned 32-bit word; a key being inserted reads as its init value until
+its weight is published, ``kv_slot.cuh publish_init`` / ``published_w``). So a pull
+sees every push the owner had finished applying when the lookup kernel ran, plus
+possibly some it was applying: asynchronous SGD semantics (the reference's servers
+answer pulls between pushes the same way, kv_store.h:37-57), not a bounded-delay
+guarantee -- use the padded exchange with ``ssp:tau`` for that.
+
 Rows use the padded exchange's layout, so FixingFloat pushes (nb-byte codes with the
 row's min / max in the header; reference fixing_float.h:44-95) travel as they do there
 and the owner decodes them before the update. The inbox (entries + a separate area of

@@ -69,11 +69,12 @@ def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     kw = dict(kw)
     for k, v in kw.pop("_env", {}).items():  # (default: collectives captured in the graphs)
         monkeypatch.setenv(k, v)
+    kw.setdefault("exchange_merge", "off")  # (the two-collective pipeline unless "on")
     bench = _bench()
     B, N, seed, extra = 4096, 10 ** 6, 77, 5
     dev = torch.device("cuda")
     tr = _trainer(B, N, **kw)
-    assert tr.merged == (kw.get("exchange_merge") == "on")
+    assert tr.merged == (kw["exchange_merge"] == "on")
     keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
     labels = torch.empty(B, dtype=torch.float32, device=dev)
     args = argparse.Namespace(warmup=0, graph=graph)
@@ -119,7 +120,7 @@ def test_asp_pipeline_trains(monkeypatch, apply):
     bench = _bench()
     B, N, seed = 4096, 10 ** 6, 78
     dev = torch.device("cuda")
-    tr = _trainer(B, N, consistency="asp")
+    tr = _trainer(B, N, consistency="asp", exchange_merge="off")
     assert tr.asp and tr.R == tr.lag + 1 + tr.async_depth
     keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
     labels = torch.empty(B, dtype=torch.float32, device=dev)

@@ -187,16 +187,19 @@ def _table_by_raw_key(tr, allk):
     return w, z, n
 
 
-@pytest.mark.parametrize("mode,algo", [("tpf", "ftrl"), ("tpf", "adagrad"), ("tpf", "sgd"),
-                                       ("tp", "ftrl")])
-def test_fused_1gpu_step_matches_fp32_reference(mode, algo, monkeypatch):
+@pytest.mark.parametrize("mode,algo,B,cap", [
+    ("tpf", "ftrl", 16384, 1 << 22), ("tpf", "adagrad", 16384, 1 << 22),
+    ("tpf", "sgd", 16384, 1 << 22), ("tp", "ftrl", 16384, 1 << 22),
+    # the driver's shape: B = 65,536 on the 2^31-slot (64 GiB) table of 10^9 features
+    ("tpf", "ftrl", 65536, 1 << 31)])
+def test_fused_1gpu_step_matches_fp32_reference(mode, algo, B, cap, monkeypatch):
     """5 fused 1-GPU steps (flat: pulls issued ahead via next_loc; tp: resolve + fused
     forward/backward + fused scan/update) against the fp32 PyTorch loop on the same
     keys: weights, z and n to rtol 1e-4."""
     monkeypatch.setenv("PSAMD_FLAT", "1" if mode == "tpf" else "0")
-    B, steps = 16384, 5
-    cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B, table_capacity=1 << 22, algo=algo,
-                         **algo_defaults(algo))
+    steps = 5
+    cfg = SparseLRConfig(num_features=10 ** 8 if cap < (1 << 31) else 10 ** 9, minibatch=B,
+                         table_capacity=cap, algo=algo, **algo_defaults(algo))
     tr = SparseLRTrainer(cfg, device=DEV)
     assert tr.localize_mode == mode
     batches = [criteo_batch(B, seed=31, row0=t * B, num_features=cfg.num_features, device=DEV)
