@@ -597,6 +597,7 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
                 parts["resolve"]()
                 ev["res"][s % E].record(xs)
             ev["app"][s % E].record(xs)
+            tr._mx_next = s + 1  # (mx_drain continues after the issued exchanges)
         finally:
             set_stream(main)
 
@@ -632,6 +633,7 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
             prep(b)
             ev_prep[b].record(sides[b])
     if tr.xc is None:
+        main.wait_event(ev_prep[0])
         tr._xc_setup(locs[0])  # (collective: the row capacity from minibatch 0)
     for s in range(-1, xd):  # exchanges -1 .. xd-1 carry keys(0) .. keys(xd)
         issue_exchange(s)

@@ -277,3 +277,63 @@ def test_tail_filter_padded_matches_exact(tmp_path, world, ff):
     # the filter is live: fewer keys than without it
     res_n = _run(tmp_path / "n", dict(base, tail_feature_freq=0), steps=5, world=world)
     assert sum(r["state"]["keys"].numel() for r in res_n) > len(wp)
+
+
+@pytest.mark.parametrize("tau,xd", [(4, 2), (2, 1), (3, 2), (4, 1)])
+def test_merged_pipeline_order_matches_two_collective(tau, xd):
+    """bench.py's merged pipeline issue order, in program order on the CPU (loopback
+    exchange, 2 emulated peers): exchanges -1 .. xd-1 first, then per iteration the
+    worker half of step t and exchange t+xd; mx_drain at the end. Leaves the table of
+    the two-collective sequential trainer (same staleness bound) on every trained key."""
+    from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+    from parameter_server_amd.ops.synthetic import criteo_batch
+    from parameter_server_amd.parallel.comm import LoopbackComm
+
+    B, N, T = 256, 1 << 20, 9
+    batches = [criteo_batch(B, seed=9, row0=m * B, num_features=N, cards=[200] * 26)
+               for m in range(T + xd + 2)]
+
+    def trainer(merge):
+        cfg = SparseLRConfig(num_features=N, minibatch=B, consistency=f"ssp:{tau}",
+                             table_capacity=1 << 16, l1=0.5, exchange_merge=merge)
+        return SparseLRTrainer(cfg, LoopbackComm(2), "cpu")
+
+    tr = trainer("on")
+    assert tr.merged and xd <= tr.msched.d
+    locs = {}
+
+    def loc(m):
+        if m not in locs:
+            locs[m] = tr.localize(batches[m][0], buf=m % 4)
+        return locs[m]
+
+    def issue(s):
+        parts = tr.mx_exchange(s, loc(s + 1))
+        parts["pack"]()
+        parts["comm"]()
+        if parts["post"]:
+            parts["resolve"]()
+            parts["apply"]()
+        else:
+            parts["apply"]()
+            parts["resolve"]()
+        tr._mx_next = s + 1
+
+    for s in range(-1, xd):
+        issue(s)
+    for t in range(T):
+        tr.mx_worker(t, loc(t), batches[t][1], width=39)()
+        tr.mx_done(B)
+        issue(t + xd)
+    tr.mx_drain()
+    ref = trainer("off")
+    for m in range(T):
+        ref.step(batches[m][0], batches[m][1], width=39)
+    ref.flush()
+    k1, w1, _, _ = tr.table.occupied()
+    k2, w2, _, _ = ref.table.occupied()
+    a = dict(zip(k1.tolist(), w1.tolist()))
+    b = dict(zip(k2.tolist(), w2.tolist()))
+    assert set(b) <= set(a)  # (the pipeline also pulled the minibatches issued ahead)
+    assert max(abs(a[k] - b[k]) for k in b) < 1e-6
+    assert all(a[k] == 0 for k in set(a) - set(b))
