@@ -152,12 +152,20 @@ class KVTable:
         if self.gpu and int(self._err.item()) != 0:
             raise RuntimeError("KVTable full: increase capacity")
 
-    def occupied(self):
-        """(mixed keys, w, z, n) of every occupied slot (device tensors)."""
-        keys = self.slots[:, 0]
-        mask = keys != EMPTY_KEY
-        vals = self.slots[:, 1:3].contiguous().view(torch.float32)  # w,z,n,acc
-        return keys[mask], vals[mask, 0], vals[mask, 1], vals[mask, 2]
+    def occupied(self, chunk: int = 1 << 27):
+        """(mixed keys, w, z, n) of every occupied slot (device tensors). Scanned in
+        chunks of slots: boolean-mask indexing over more than 2^31 elements overflows in
+        torch, and a whole-table copy of a 2^31-slot table would take 32 GiB."""
+        parts = []
+        for a in range(0, self.capacity, chunk):
+            sl = self.slots[a:a + chunk]
+            keys = sl[:, 0]
+            mask = keys != EMPTY_KEY
+            vals = sl[:, 1:3].contiguous().view(torch.float32)  # w,z,n,acc
+            parts.append((keys[mask], vals[mask, 0], vals[mask, 1], vals[mask, 2]))
+        if len(parts) == 1:
+            return parts[0]
+        return tuple(torch.cat([p[i] for p in parts]) for i in range(4))
 
     def load(self, keys_mixed: torch.Tensor, w, z=None, n=None):
         slot, _ = self.resolve(keys_mixed.to(self.device), insert=True, with_w=False)

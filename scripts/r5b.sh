@@ -2,7 +2,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/r5b
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 timeout -k 10 700 python -u -m pytest -x -v --timeout 150 --timeout-method thread -p no:cacheprovider \
-  tests/test_bench_pipeline_gpu.py tests/test_app_gpu.py tests/test_tpf_gpu.py > gpurun_out/r5b/pytest.log 2>&1
+  tests/test_tpf_gpu.py > gpurun_out/r5b/pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/r5b/pytest.log; [ $rc -eq 0 ] || exit $rc
 for m in on off; do
   for e in 8 2; do
