@@ -213,10 +213,9 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     state = {"t": 0}
     # 1 GPU, flat: the preparation of minibatch t + nprep also waits for step t-1
     # (implies the buffer wait: steps complete in order); PSAMD_PREP_GATE=0: buffer only
-    # (auto: B >= 32,768, where a preparation is shorter than a step; at B = 10,000 the
-    # latency-bound preparation outlasts a step and needs the two-step window)
-    gate = os.environ.get("PSAMD_PREP_GATE", "auto")
-    prep_gate = flat and nprep >= 2 and (gate == "1" or (gate == "auto" and B >= 32768))
+    # (measured slower at the driver shape, 0.0901-0.0906 vs 0.0870-0.0889 ms / step over
+    # 20 steps, profiles/r5_prep_gate_and_merge.log: off unless PSAMD_PREP_GATE=1)
+    prep_gate = flat and nprep >= 2 and os.environ.get("PSAMD_PREP_GATE", "0") == "1"
 
     def issue_exchange(t):
         xs = sides[(t % NB) % nprep] if xmode == "prep" else comm_s
@@ -585,9 +584,13 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
                 xs.wait_event(ev["w"][(s - d) % E])     # grads(s-d) packed
             if s >= 0:
                 xs.wait_event(ev["res"][(s - 1) % E])   # weights(s) in the send rows
-                xs.wait_event(ev["app"][(s - 1) % E])
             parts["comm"]()
             ev["M"][s % E].record(xs)
+            if s >= 0:
+                # owner updates in exchange order: the resolve of keys(s+1) (post) or
+                # this apply (pre) after the apply of exchange s-1, which so overlaps
+                # this all-to-all instead of delaying it
+                xs.wait_event(ev["app"][(s - 1) % E])
             if parts["post"]:
                 parts["resolve"]()
                 ev["res"][s % E].record(xs)

@@ -1641,6 +1641,8 @@ class SparseLRTrainer:
             return self._push(g, inner)
         if kind == "local":
             slot, n_dev = push[1], push[2]
+            if n_dev is not None:  # (the slot workspace is sized for the largest batch)
+                slot = slot[:grad.numel()]
             if n_dev is None:
                 self.table.update(slot, grad[:slot.numel()], self.rule, self.stats)
                 return False

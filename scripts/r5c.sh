@@ -9,3 +9,5 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -2 gpurun_out/r5c/smoke.log
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/r5c/prof_e8m" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 100 --warmup 10 --emulate-peers 8 > "$GRAFT_REPO_ROOT/gpurun_out/r5c/prof_e8m.log" 2>&1
 echo "prof rc=$?"
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/r5c/prof_csr" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/benchmarks/bench_csr.py" --minibatch 1000 10000 --steps 50 --warmup 10 > "$GRAFT_REPO_ROOT/gpurun_out/r5c/prof_csr.log" 2>&1
+echo "prof csr rc=$?"
