@@ -68,7 +68,7 @@ void localize_tpf(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uin
                   int32_t*, uint16_t*, int32_t*, int32_t*, bool, hipStream_t);
 bool tpf_exchange_ok(int64_t, int, int);
 void tpf_pack_keys(int64_t, int, int, const int32_t*, const uint64_t*, int64_t, int, int64_t,
-                   int32_t*, int32_t*, hipStream_t);
+                   int32_t*, int32_t*, const uint64_t*, int64_t, int, hipStream_t);
 void tpf_unpack_w(int64_t, int, int, const int32_t*, const int32_t*, const uint16_t*, int64_t,
                   const float*, int64_t, float*, int64_t, hipStream_t);
 void tpf_pack_grads(int64_t, int, int, const int32_t*, const int32_t*, const uint16_t*, int64_t, int,
@@ -114,7 +114,12 @@ void fm_l2(float*, const void*, const int64_t*, int64_t, const int32_t*, int64_t
            hipStream_t);
 // exchange.hip
 void xchg_pack_keys(const uint64_t*, const int32_t*, int64_t, const int64_t*, int, int64_t, int,
-                    int64_t, int32_t*, int32_t*, hipStream_t);
+                    int64_t, int32_t*, int32_t*, const uint64_t*, int64_t, int, hipStream_t);
+void kv_owner_part(void*, int64_t, uint64_t, uint64_t, const int32_t*, int, int64_t, int64_t, int,
+                   int64_t, int, int64_t*, uint64_t*, int32_t*, float*, int, float, float, uint64_t,
+                   int32_t*, int32_t*, const int64_t*, const uint64_t*, const float*, int64_t,
+                   const int32_t*, bool, bool, int, int, float, float, float, float, float, float,
+                   double*, int, hipStream_t);
 void xchg_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, const int64_t*, int,
                      int64_t, int, int64_t, int32_t*, uint32_t*, int, double*, int64_t*, const int32_t*, int32_t*, hipStream_t);
 void xchg_clear_counts(int32_t*, int, int64_t, bool, bool, hipStream_t);
@@ -506,6 +511,18 @@ Launch make_tp_fwd_bwd_csr(Tensor rep, Tensor dcnt, optional<Tensor> ent_uid, in
                           ptr<float>(labels), B, loss_type, ptr<float>(coef), mp, hp, nbins,
                           mstripes, hstripes, ptr<float>(psum), ps, sg, ne, gr, gcap, reduce, st);
   };
+}
+
+// Owner homes of the merged exchange's partition bounds: [G, 2] int64 (base, m) per owner;
+// the bounds (P + 1 words) go at word b0 of each H-word row, past the key words.
+const uint64_t* check_homes(const optional<Tensor>& homes, int G, int64_t H, int64_t b0, int lgP,
+                            int64_t key_end) {
+  if (!homes) return nullptr;
+  chk(*homes, at::kLong, "homes");
+  check(homes->numel() >= 2 * G, "homes: [G, 2] (base, m) per owner");
+  check(lgP >= 0 && lgP <= 20 && b0 >= key_end && b0 + (1 << lgP) + 1 <= H,
+        "partition bounds: b0 past the keys, P + 1 words inside the row");
+  return reinterpret_cast<const uint64_t*>(homes->data_ptr<int64_t>());
 }
 
 // Flat-layout buffers of one localisation (Localizer mode "tpf"): checked against the
@@ -949,16 +966,21 @@ PYBIND11_MODULE(_hipops, m) {
     return psamd::tpf_exchange_ok(n, bits, G);
   });
   m.def("tpf_pack_keys", [](int64_t n, int bits, int G, Tensor cnt, Tensor uniqf, int64_t C, int kw,
-                            int64_t H, Tensor send, optional<Tensor> ovf) {
+                            int64_t H, Tensor send, optional<Tensor> ovf, optional<Tensor> homes,
+                            int64_t b0, int lgP) {
     check_tpf(TpfBufs{cnt, uniqf, cnt.new_empty({0}, at::kInt), cnt.new_empty({0}, at::kShort),
                       cnt.new_empty({0}, at::kInt)}, n, bits, "tpf_pack_keys", true);
     chk(send, at::kInt, "send");
     check(psamd::tpf_exchange_ok(n, bits, G), "tpf_pack_keys: G a power of two dividing groups");
     check((kw == 1 || kw == 2) && C > 0 && H >= 4 + C * kw + 1 && send.numel() >= G * H,
           "tpf_pack_keys: row geometry");
+    const uint64_t* hp = check_homes(homes, G, H, b0, lgP, 4 + C * kw);
     psamd::tpf_pack_keys(n, bits, G, ptr<int32_t>(cnt), ptr<uint64_t>(uniqf), C, kw, H,
-                         ptr<int32_t>(send), optr<int32_t>(ovf, at::kInt, "ovf"), cur_stream());
-  });
+                         ptr<int32_t>(send), optr<int32_t>(ovf, at::kInt, "ovf"), hp, b0, lgP,
+                         cur_stream());
+  }, py::arg("n"), py::arg("bits"), py::arg("G"), py::arg("cnt"), py::arg("uniqf"), py::arg("C"),
+     py::arg("kw"), py::arg("H"), py::arg("send"), py::arg("ovf"),
+     py::arg("homes") = py::none(), py::arg("b0") = 0, py::arg("lgP") = 0);
   m.def("tpf_unpack_w", [](int64_t n, int bits, int G, Tensor cnt, Tensor ent_pos, Tensor ent_j,
                            int64_t C, Tensor wrecv, Tensor w_ent, int64_t wstride) {
     // wstride: row stride of wrecv (0 = C; the merged exchange reads the weights in
@@ -1426,7 +1448,8 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::xchg_publish(ptr<int32_t>(src), reinterpret_cast<int32_t*>(dptr), cur_stream());
   });
   m.def("xchg_pack_keys", [](Tensor ukeys, Tensor n_uniq, Tensor off, int64_t C, int kw,
-                             int64_t H, Tensor send, optional<Tensor> ovf) {
+                             int64_t H, Tensor send, optional<Tensor> ovf,
+                             optional<Tensor> homes, int64_t b0, int lgP) {
     chk(ukeys, at::kLong, "ukeys");
     chk(n_uniq, at::kInt, "n_uniq");
     chk(off, at::kLong, "off");
@@ -1436,9 +1459,62 @@ PYBIND11_MODULE(_hipops, m) {
     check(kw == 1 || kw == 2, "kw must be 1 or 2");
     check(C > 0 && H >= 4 + C * kw + 1 && H % 4 == 0, "bad exchange row geometry");
     check(send.numel() == G * H, "send must be [G * H]");
+    const uint64_t* hp = check_homes(homes, G, H, b0, lgP, 4 + C * kw);
     psamd::xchg_pack_keys(ptr<uint64_t>(ukeys), ptr<int32_t>(n_uniq), ukeys.numel(),
                           ptr<int64_t>(off), G, C, kw, H, ptr<int32_t>(send),
-                          optr<int32_t>(ovf, at::kInt, "ovf"), cur_stream());
+                          optr<int32_t>(ovf, at::kInt, "ovf"), hp, b0, lgP, cur_stream());
+  }, py::arg("ukeys"), py::arg("n_uniq"), py::arg("off"), py::arg("C"), py::arg("kw"),
+     py::arg("H"), py::arg("send"), py::arg("ovf"), py::arg("homes") = py::none(),
+     py::arg("b0") = 0, py::arg("lgP") = 0);
+  // The owner's half of a merged exchange in one launch (kv_table.hip kv_owner_part_kernel):
+  // resolve of the pulled keys (bounds from the rows, weights into the next send rows at
+  // word w0, stride H) and the per-source push apply of an earlier pull, per partition.
+  m.def("kv_owner_part", [](Tensor slots, Tensor recv, int64_t H, int64_t C, int kw, int64_t b0,
+                            int lgP, Tensor slot_out, Tensor key_out, Tensor bnd_out, Tensor wout,
+                            int init_type, double init_v, double init_s, uint64_t seed,
+                            optional<Tensor> err, optional<Tensor> inserted, uint64_t home_base,
+                            uint64_t home_m, optional<Tensor> slot_idx, optional<Tensor> keys,
+                            optional<Tensor> grad, int64_t gstride, optional<Tensor> bnd_in,
+                            bool post, int algo, int lr_type, double alpha, double beta,
+                            double l1, double l2, double grad_scale, double max_delta,
+                            optional<Tensor> stats) {
+    const int64_t cap = slot_capacity(slots);
+    chk(recv, at::kInt, "recv");
+    chk(slot_out, at::kLong, "slot_out");
+    chk(key_out, at::kLong, "key_out");
+    chk(bnd_out, at::kInt, "bnd_out");
+    chk(wout, at::kFloat, "wout");
+    check(kw == 1 || kw == 2, "kw must be 1 or 2");
+    check(recv.numel() % H == 0, "recv is not a whole number of rows");
+    const int G = (int)(recv.numel() / H);
+    const int P = 1 << lgP;
+    check(G >= 1 && G <= 64 && lgP >= 0 && lgP <= 20, "1..64 rows, lgP 0..20");
+    check(C > 0 && b0 >= 4 + C * kw && b0 + P + 1 <= H, "kv_owner_part: row geometry");
+    check(slot_out.numel() >= G * C && key_out.numel() >= G * C &&
+          bnd_out.numel() >= G * (P + 1) && wout.numel() >= (G - 1) * H + C,
+          "kv_owner_part: output sizes");
+    const bool apply = slot_idx.has_value();
+    if (apply) {
+      chk(*slot_idx, at::kLong, "slot_idx");
+      chk(*keys, at::kLong, "keys");
+      chk(*grad, at::kFloat, "grad");
+      chk(*bnd_in, at::kInt, "bnd_in");
+      check(slot_idx->numel() >= G * C && keys->numel() >= G * C &&
+            bnd_in->numel() >= G * (P + 1) && grad->numel() >= (G - 1) * gstride + C,
+            "kv_owner_part: apply inputs");
+      check(alpha > 0, "learning rate alpha must be > 0");
+    }
+    double* sp = optr<double>(stats, at::kDouble, "stats");
+    psamd::kv_owner_part(
+        slots.data_ptr(), cap, home_base, home_m, ptr<int32_t>(recv), G, H, C, kw, b0, lgP,
+        ptr<int64_t>(slot_out), reinterpret_cast<uint64_t*>(key_out.data_ptr<int64_t>()),
+        ptr<int32_t>(bnd_out), ptr<float>(wout), init_type, (float)init_v, (float)init_s, seed,
+        optr<int32_t>(err, at::kInt, "err"), optr<int32_t>(inserted, at::kInt, "inserted"),
+        apply ? ptr<int64_t>(*slot_idx) : nullptr,
+        apply ? reinterpret_cast<const uint64_t*>(keys->data_ptr<int64_t>()) : nullptr,
+        apply ? ptr<float>(*grad) : nullptr, gstride, apply ? ptr<int32_t>(*bnd_in) : nullptr,
+        apply, post, algo, lr_type, (float)alpha, (float)beta, (float)l1, (float)l2,
+        (float)grad_scale, (float)max_delta, sp, acc_stripes_of(stats), cur_stream());
   });
   m.def("xchg_pack_grads", [host_flag](Tensor grad, optional<Tensor> perm, Tensor n_uniq, Tensor off,
                               int64_t C, int kw, int64_t H, Tensor send, optional<Tensor> hist,

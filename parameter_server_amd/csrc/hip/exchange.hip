@@ -22,6 +22,7 @@
 // and counted in *ovf (the trainer raises on it; the capacity carries a large
 // statistical margin over the per-peer count of hashed keys).
 #include "common.cuh"
+#include "kv_slot.cuh"
 #include "loss.cuh"
 
 namespace psamd {
@@ -44,18 +45,24 @@ __device__ __forceinline__ void load_offsets(const int64_t* __restrict__ off, in
   __syncthreads();
 }
 
+// homes != null (the merged exchange): also the partition bounds of each row at word b0
+// (see tpf_pack_keys_kernel, tploc.hip)
 __global__ void xchg_pack_keys_kernel(const uint64_t* __restrict__ ukeys,
                                       const int32_t* __restrict__ n_uniq, int64_t n_host,
                                       const int64_t* __restrict__ off, int G, int64_t C, int kw,
                                       int64_t H, int32_t* __restrict__ send,
-                                      int32_t* __restrict__ ovf) {
+                                      int32_t* __restrict__ ovf, const uint64_t* __restrict__ homes,
+                                      int64_t b0, int lgP) {
   __shared__ int64_t soff[kMaxPeers + 1];
   load_offsets(off, G, soff);
+  const int P = 1 << lgP;
   if (blockIdx.x == 0 && threadIdx.x < G) {
     const int p = threadIdx.x;
     const int64_t cnt = soff[p + 1] - soff[p];
     send[(int64_t)p * H] = (int32_t)(cnt < C ? cnt : C);
     if (cnt > C && ovf) atomicAdd(ovf, (int32_t)(cnt - C));
+    if (homes && cnt == 0)
+      for (int j = 0; j <= P; ++j) send[(int64_t)p * H + b0 + j] = 0;
   }
   const int64_t n = dev_len(n_uniq, n_host);
   for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n;
@@ -67,6 +74,16 @@ __global__ void xchg_pack_keys_kernel(const uint64_t* __restrict__ ukeys,
     const uint64_t k = ukeys[j];
     if (kw == 1) row[i] = (int32_t)(uint32_t)k;
     else reinterpret_cast<uint64_t*>(row)[i] = k;
+    if (homes) {
+      const uint64_t hb = homes[2 * p], hm = homes[2 * p + 1];
+      int32_t* rb = send + (int64_t)p * H + b0;
+      const int q = key_part(k, hb, hm, lgP);
+      const int q0 = i > 0 ? key_part(ukeys[j - 1], hb, hm, lgP) + 1 : 0;
+      for (int jj = q0; jj <= q; ++jj) rb[jj] = (int32_t)i;
+      const int64_t nr = soff[p + 1] - soff[p];
+      if (i == (nr < C ? nr : C) - 1)  // the row's last key: the tail bounds
+        for (int jj = q + 1; jj <= P; ++jj) rb[jj] = (int32_t)(i + 1);
+    }
   }
 }
 
@@ -149,9 +166,9 @@ void xchg_publish(const int32_t* src, int32_t* host_mapped_dst, hipStream_t st) 
 
 void xchg_pack_keys(const uint64_t* ukeys, const int32_t* n_uniq, int64_t n_host,
                     const int64_t* off, int G, int64_t C, int kw, int64_t H, int32_t* send,
-                    int32_t* ovf, hipStream_t st) {
+                    int32_t* ovf, const uint64_t* homes, int64_t b0, int lgP, hipStream_t st) {
   xchg_pack_keys_kernel<<<grid_for(n_host, 256), 256, 0, st>>>(ukeys, n_uniq, n_host, off, G, C,
-                                                                kw, H, send, ovf);
+                                                                kw, H, send, ovf, homes, b0, lgP);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -413,7 +413,9 @@ __global__ void kv_apply_rows_kernel(Slot* __restrict__ slots, int64_t cap,
 constexpr int kApWin = 1024;   // entries per window
 constexpr int kApHash = 2048;  // LDS hash slots (power of two, >= 2 * kApWin)
 
-__global__ __launch_bounds__(256) void kv_apply_part_kernel(
+// The body of kv_apply_part_kernel for partition blockIdx.x (also the apply half of
+// kv_owner_part_kernel below).
+__device__ __forceinline__ void apply_part_block(
     Slot* __restrict__ slots, int64_t cap, const int64_t* __restrict__ slot_idx,
     const uint64_t* __restrict__ keys, const float* __restrict__ grad, int64_t gstride,
     const int32_t* __restrict__ recv, int64_t H, int64_t C, int G,
@@ -526,6 +528,93 @@ __global__ __launch_bounds__(256) void kv_apply_part_kernel(
       if (b != 0) atomicAdd(&st[1], b);
       if (c != 0) atomicAdd(&st[2], c);
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void kv_apply_part_kernel(
+    Slot* __restrict__ slots, int64_t cap, const int64_t* __restrict__ slot_idx,
+    const uint64_t* __restrict__ keys, const float* __restrict__ grad, int64_t gstride,
+    const int32_t* __restrict__ recv, int64_t H, int64_t C, int G,
+    const int32_t* __restrict__ bnd, int lgP, UpdateParams p, double* __restrict__ stats,
+    int acc_stripes) {
+  apply_part_block(slots, cap, slot_idx, keys, grad, gstride, recv, H, C, G, bnd, lgP, p, stats,
+                   acc_stripes);
+}
+
+// The owner's half of one merged exchange (models/sparse_lr.py mx_exchange) in ONE
+// launch, one workgroup per key-range partition q of the owner's ordered home:
+//   resolve  lookup-or-insert of the pulled keys of partition q from every source row
+//            (row word b0.. holds the row's partition bounds, written by the sender's
+//            key pack), their slots / keys / bounds for the later apply, and their
+//            weights into the next exchange's send rows (row stride H)
+//   apply    the pushes of partition q (kv_apply_part semantics: one optimizer step per
+//            source row, rank order) at the slots an earlier resolve recorded
+// post = resolve first (the pulls miss this exchange's pushes), else apply first. A
+// key's resolve and apply run in the same workgroup, ordered by a barrier (workgroup
+// scope: write-through L1), so no key is read and written by two workgroups.
+__global__ __launch_bounds__(256) void kv_owner_part_kernel(
+    Slot* __restrict__ slots, int64_t cap, uint64_t mask, uint64_t home_base, uint64_t home_m,
+    int home_shr, const int32_t* __restrict__ recv, int64_t H, int64_t C, int kw, int G,
+    int64_t b0, int lgP, int64_t* __restrict__ slot_out, uint64_t* __restrict__ key_out,
+    int32_t* __restrict__ bnd_out, float* __restrict__ wout, int init_type, float init_v,
+    float init_s, uint64_t seed, int32_t* __restrict__ err, int32_t* __restrict__ inserted,
+    const int64_t* __restrict__ slot_idx, const uint64_t* __restrict__ keys,
+    const float* __restrict__ grad, int64_t gstride, const int32_t* __restrict__ bnd_in,
+    int do_apply, int post, UpdateParams p, double* __restrict__ stats, int acc_stripes) {
+  __shared__ int32_t sa[kMaxChain], roff[kMaxChain + 1];
+  const int tid = threadIdx.x, P = 1 << lgP, q = blockIdx.x;
+  for (int phase = 0; phase < 2; ++phase) {
+    const bool resolve = (phase == 0) == (post != 0);
+    if (!resolve) {
+      if (do_apply)
+        apply_part_block(slots, cap, slot_idx, keys, grad, gstride, recv, H, C, G, bnd_in, lgP,
+                         p, stats, acc_stripes);
+      __syncthreads();
+      continue;
+    }
+    if (tid < G) {
+      const int32_t* row = recv + (int64_t)tid * H;
+      const int32_t n = (int32_t)dev_len(row, C);
+      const int32_t* rb = row + b0;
+      const int32_t a = min(max(rb[q], 0), n), b = min(max(rb[q + 1], a), n);
+      sa[tid] = a;
+      roff[tid + 1] = b - a;
+      int32_t* ob = bnd_out + (int64_t)tid * (P + 1);
+      ob[q] = a;
+      if (q == P - 1) ob[P] = n;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      roff[0] = 0;
+      for (int s = 0; s < G; ++s) roff[s + 1] += roff[s];
+    }
+    __syncthreads();
+    const int tot = roff[G];
+    int local_ins = 0;
+    for (int w = tid; w < tot; w += blockDim.x) {
+      int lo = 0, hi = G - 1;  // row of entry w: last s with roff[s] <= w
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (roff[mid] <= w) lo = mid; else hi = mid - 1;
+      }
+      const int s = lo;
+      const int64_t i = sa[s] + (w - roff[s]);
+      const int32_t* row = recv + (int64_t)s * H;
+      const uint64_t h = kw == 1 ? (uint64_t)(uint32_t)row[4 + i]
+                                 : reinterpret_cast<const uint64_t*>(row + 4)[i];
+      float wv;
+      const int64_t found = resolve_key(slots, mask, home_base, home_m, home_shr, h, 1,
+                                        init_type, init_v, init_s, seed, &wv, &local_ins);
+      if (found < 0 && err) atomicOr(err, 1);
+      slot_out[(int64_t)s * C + i] = found;
+      key_out[(int64_t)s * C + i] = h;
+      wout[(int64_t)s * H + i] = wv;
+    }
+    if (inserted) {
+      const int t = wave_sum(local_ins);
+      if ((threadIdx.x & 63) == 0 && t) atomicAdd(inserted, t);
+    }
+    __syncthreads();
   }
 }
 
@@ -672,6 +761,31 @@ void kv_apply_part(void* slots, int64_t cap, const int64_t* slot_idx, const uint
   UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
   kv_apply_part_kernel<<<1 << lgP, 256, 0, st>>>((Slot*)slots, cap, slot_idx, keys, grad, gstride,
                                                  recv, H, C, G, bnd, lgP, p, stats, acc_stripes);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+
+void kv_owner_part(void* slots, int64_t cap, uint64_t home_base, uint64_t home_m,
+                   const int32_t* recv, int G, int64_t H, int64_t C, int kw, int64_t b0, int lgP,
+                   int64_t* slot_out, uint64_t* key_out, int32_t* bnd_out, float* wout,
+                   int init_type, float init_v, float init_s, uint64_t seed, int32_t* err,
+                   int32_t* inserted, const int64_t* slot_idx, const uint64_t* keys,
+                   const float* grad, int64_t gstride, const int32_t* bnd_in, bool do_apply,
+                   bool post, int algo, int lr_type, float alpha, float beta, float l1, float l2,
+                   float grad_scale, float max_delta, double* stats, int acc_stripes,
+                   hipStream_t st) {
+  if (cap > (int64_t(1) << 32) - 1) throw std::runtime_error("kv_owner_part: capacity >= 2^32");
+  if ((int64_t)G * C >= (int64_t(1) << 31)) throw std::runtime_error("kv_owner_part: G*C >= 2^31");
+  if (G < 1 || G > kMaxChain) throw std::runtime_error("kv_owner_part: 1..64 source rows");
+  if (lgP < 0 || lgP > 20) throw std::runtime_error("kv_owner_part: lgP in 0..20");
+  if (!home_m) throw std::runtime_error("kv_owner_part: needs an ordered home");
+  int lg = 0;
+  while ((1ll << lg) < cap) ++lg;
+  UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
+  kv_owner_part_kernel<<<1 << lgP, 256, 0, st>>>(
+      (Slot*)slots, cap, (uint64_t)(cap - 1), home_base, home_m, 64 - lg, recv, H, C, kw, G, b0,
+      lgP, slot_out, key_out, bnd_out, wout, init_type, init_v, init_s, seed, err, inserted,
+      slot_idx, keys, grad, gstride, bnd_in, do_apply ? 1 : 0, post ? 1 : 0, p, stats,
+      acc_stripes);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -2123,28 +2123,79 @@ __device__ __forceinline__ int tpf_row_base(const int32_t* __restrict__ cnt, int
 // keys of every bucket into its owner's row of `send` ([nkeys, ngrads, -, - | keys (C x kw
 // words) | grads]); the owner's last bucket writes the row's key count; keys past C
 // count as overflow (ovf, once per owner)
+// (the key of unit-concatenated index i of bucket b)
+__device__ __forceinline__ uint64_t tpf_key_at(const uint64_t* __restrict__ uniqf, int b, int D0,
+                                               int i) {
+  return i < D0 ? uniqf[(int64_t)b * tpf::kUC + i]
+                : uniqf[(int64_t)b * tpf::kUC + tpf::kUnitK + (i - D0)];
+}
+
+// homes != null (the merged exchange): the row also carries, at word b0, the bounds of
+// the owner's 2^lgP key-range partitions over the row's sorted keys (bnd[q] = # keys of
+// partitions < q, bnd[P] = row count) -- what the owner's one-launch resolve + apply
+// (kv_owner_part) needs to find its partition's run in every row. homes[2p], [2p+1] =
+// owner p's ordered-home (base, m) (kv_slot.cuh key_part).
 __global__ void __launch_bounds__(tpf::kThr)
 tpf_pack_keys_kernel(const int32_t* __restrict__ cnt, const uint64_t* __restrict__ uniqf, int per,
                      int64_t C, int kw, int64_t H, int32_t* __restrict__ send,
-                     int32_t* __restrict__ ovf) {
+                     int32_t* __restrict__ ovf, const uint64_t* __restrict__ homes, int64_t b0,
+                     int lgP) {
   using namespace tpf;
   __shared__ uint32_t red[kThr / 64 + 1];
   const int b = blockIdx.x, p = b / per, t = threadIdx.x;
   const int base = tpf_row_base(cnt, b, per, red);
   const int D0 = min(cnt[4 * b], kUnitK), D1 = min(cnt[4 * b + 2], kUnitK);
   int32_t* row = send + (int64_t)p * H;
+  const int P = 1 << lgP;
+  const uint64_t hb = homes ? homes[2 * p] : 0, hm = homes ? homes[2 * p + 1] : 0;
+  int32_t* rb = row + b0;
+  // the key before this bucket's first one in the row: the last key of the nearest
+  // non-empty earlier bucket of the same owner (none: the row's first key)
+  int qprev = -1;
+  if (homes && base > 0 && t == 0) {
+    for (int c = b - 1; c >= (b / per) * per; --c) {
+      const int e0 = min(cnt[4 * c], kUnitK), e1 = min(cnt[4 * c + 2], kUnitK);
+      if (e0 + e1 > 0) {
+        qprev = key_part(tpf_key_at(uniqf, c, e0, e0 + e1 - 1), hb, hm, lgP);
+        break;
+      }
+    }
+  }
+  if (homes) {  // (broadcast qprev through the scan scratch)
+    __syncthreads();
+    if (t == 0) red[0] = (uint32_t)(qprev + 1);
+    __syncthreads();
+    qprev = (int)red[0] - 1;
+  }
   for (int i = t; i < D0 + D1; i += kThr) {
     const int64_t pos = (int64_t)base + i;
     if (pos >= C) break;
-    const uint64_t k = i < D0 ? uniqf[(int64_t)b * kUC + i]
-                              : uniqf[(int64_t)b * kUC + kUnitK + (i - D0)];
+    const uint64_t k = tpf_key_at(uniqf, b, D0, i);
     if (kw == 1) row[4 + pos] = (int32_t)(uint32_t)k;
     else reinterpret_cast<uint64_t*>(row + 4)[pos] = k;
+    if (homes) {
+      const int q = key_part(k, hb, hm, lgP);
+      const int q0 = (i > 0 ? key_part(tpf_key_at(uniqf, b, D0, i - 1), hb, hm, lgP) : qprev) + 1;
+      for (int j = q0; j <= q; ++j) rb[j] = (int32_t)pos;
+      if (pos == C - 1)  // a full row ends here
+        for (int j = q + 1; j <= P; ++j) rb[j] = (int32_t)C;
+    }
   }
   if (t == 0 && b % per == per - 1) {
     const int64_t tot = (int64_t)base + D0 + D1;
     row[0] = (int32_t)(tot < C ? tot : C);
     if (tot > C && ovf) atomicAdd(ovf, (int32_t)(tot - C));
+    if (homes && tot <= C) {  // the row's tail bounds after its last key
+      int qlast = -1;
+      for (int c = b; c >= (b / per) * per; --c) {
+        const int e0 = min(cnt[4 * c], kUnitK), e1 = min(cnt[4 * c + 2], kUnitK);
+        if (e0 + e1 > 0) {
+          qlast = key_part(tpf_key_at(uniqf, c, e0, e0 + e1 - 1), hb, hm, lgP);
+          break;
+        }
+      }
+      for (int j = qlast + 1; j <= P; ++j) rb[j] = (int32_t)tot;
+    }
   }
 }
 
@@ -2435,10 +2486,11 @@ static int tpf_per_owner(int64_t n, int bits, int G) {
 }
 
 void tpf_pack_keys(int64_t n, int bits, int G, const int32_t* cnt, const uint64_t* uniqf, int64_t C,
-                   int kw, int64_t H, int32_t* send, int32_t* ovf, hipStream_t st) {
+                   int kw, int64_t H, int32_t* send, int32_t* ovf, const uint64_t* homes,
+                   int64_t b0, int lgP, hipStream_t st) {
   const int per = tpf_per_owner(n, bits, G);
-  tpf_pack_keys_kernel<<<(unsigned)tpf_groups(n, bits), tpf::kThr, 0, st>>>(cnt, uniqf, per, C, kw,
-                                                                           H, send, ovf);
+  tpf_pack_keys_kernel<<<(unsigned)tpf_groups(n, bits), tpf::kThr, 0, st>>>(
+      cnt, uniqf, per, C, kw, H, send, ovf, homes, b0, lgP);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -824,6 +824,21 @@ class SparseLRTrainer:
             if s - d >= 0:
                 self._x_apply(b, (s - d) % R)
 
+        if xc.fused:  # resolve + apply of the owner in ONE launch (kv_owner_part)
+            def owner():
+                tb, ra = self.table, (s - d) % R
+                it, iv, isd, seed = tb.init.args()
+                gsrc, gstride = self._x_grads(b) if s - d >= 0 else (None, 0)
+                ap = s - d >= 0
+                hipops().kv_owner_part(
+                    tb.slots, recv, xc.H, xc.C, xc.kw, xc.b0, xc.lgP, xc.slots[bn],
+                    xc.pkeys[bn], xc.bnd[bn], self._mx_wview(xc.sends[bn]), it, iv, isd, seed,
+                    tb._err, tb._inserted, tb.home_base, tb.home_m,
+                    xc.slots[ra] if ap else None, xc.pkeys[ra] if ap else None, gsrc, gstride,
+                    xc.bnd[ra] if ap else None, ms.post, *self.rule.args(), self.stats)
+
+            return {"pack": pack, "comm": lambda: comm.all_to_all_fixed(send, recv),
+                    "resolve": owner, "apply": lambda: None, "post": ms.post}
         return {"pack": pack, "comm": lambda: comm.all_to_all_fixed(send, recv),
                 "resolve": resolve, "apply": apply, "post": ms.post}
 
@@ -1034,11 +1049,6 @@ class SparseLRTrainer:
         kw = 1 if self.bits <= 32 else 2
         nb = int(cfg.fixing_float_bytes)  # FixingFloat: nb-byte codes instead of f32
         gw = (C * nb + 3) // 4 if nb else C
-        # merged exchange: each row also carries the owner's weights answering the keys
-        # the row's receiver sent in the previous exchange, at word w0
-        w0 = 4 + C * kw + gw
-        H = (w0 + (C if self.merged else 0) + 3) // 4 * 4
-        z32 = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
         # the partitioned apply needs rows sorted by key and an ordered home (key range
         # -> partition)
         part_apply = (self.gpu and cfg.push_mode != "aggregate" and self.table.home_m != 0
@@ -1050,8 +1060,19 @@ class SparseLRTrainer:
         lgP = max(0, min(16, math.floor(math.log2(max(1, G * C // 512))))) if part_apply else -1
         if part_apply and os.environ.get("PSAMD_APPLY_LGP"):
             lgP = int(os.environ["PSAMD_APPLY_LGP"])
+        # merged exchange: each row also carries the owner's weights answering the keys
+        # the row's receiver sent in the previous exchange (word w0) and, for the owner's
+        # one-launch resolve + apply (kv_owner_part), the bounds of its 2^lgP key-range
+        # partitions over the row's keys (word b0, written by the sender's key pack)
+        fused = (self.merged and lgP >= 0
+                 and os.environ.get("PSAMD_OWNER_FUSED", "1") != "0")
+        w0 = 4 + C * kw + gw
+        b0 = w0 + (C if self.merged else 0)
+        H = (b0 + (((1 << lgP) + 1) if fused else 0) + 3) // 4 * 4
+        z32 = lambda n, dt: torch.zeros(n, dtype=dt, device=dev)  # noqa: E731
         self.xc = SimpleNamespace(
-            C=C, kw=kw, H=H, nb=nb, w0=w0,
+            C=C, kw=kw, H=H, nb=nb, w0=w0, b0=b0, fused=fused,
+            homes=self._owner_homes() if fused else None,
             gstage=z32(G * C, torch.float32) if nb else None,
             gins=[z32(G * C, torch.float32) for _ in range(R)] if nb else None,
             # rings of R entries indexed by step: sends[j] holds grads(j) then keys(j+1+lag);
@@ -1076,6 +1097,22 @@ class SparseLRTrainer:
             bnd=([torch.zeros(G * ((1 << lgP) + 1), dtype=torch.int32, device=dev)
                   for _ in range(R)] if lgP >= 0 else None),
             ovf_host=(torch.zeros(1, dtype=torch.int32, pin_memory=True) if self.gpu else None))
+
+    def _owner_homes(self) -> torch.Tensor:
+        """[G, 2] (base, m) of every owner's ordered home (KVTable key_range): the sender
+        computes the owner's key-range partitions of its rows with them (the loopback
+        emulation's one table owns every row)."""
+        M = (1 << 64) - 1
+        if self._loopback:
+            hs = [(self.table.home_base, self.table.home_m)] * self.G
+        else:
+            hs = []
+            for p in range(self.G):
+                lo, hi = self.part.range_of(p)
+                hs.append((lo, M // (hi - lo)) if hi > lo else (0, 0))
+        s64 = lambda x: x - (1 << 64) if x >= (1 << 63) else x  # noqa: E731
+        return torch.tensor([[s64(int(b)), s64(int(m))] for b, m in hs], dtype=torch.int64,
+                            device=self.device)
 
     def _tail_filter(self, loc, ring: int):
         """Tail-feature filter on the padded exchange (reference MinibatchReader::read,
@@ -1137,7 +1174,8 @@ class SparseLRTrainer:
         send = xc.sends[gb]
         if self.gpu:
             hh = hipops()
-            hh.xchg_pack_keys(ukeys, nkeys, off, xc.C, xc.kw, xc.H, send, xc.ovf)
+            hh.xchg_pack_keys(ukeys, nkeys, off, xc.C, xc.kw, xc.H, send, xc.ovf,
+                              homes=xc.homes, b0=xc.b0, lgP=max(xc.lgP, 0))
             if xc.nb:  # (FixingFloat push: no pack_grads launch to carry the flag)
                 hh.xchg_publish(xc.ovf, xc.ovf_host)
             return
@@ -1157,7 +1195,7 @@ class SparseLRTrainer:
         xc.curs[r] = None
         hh = hipops()
         hh.tpf_pack_keys(loc.nnz, loc.bits, self.G, loc.cnt, loc.uniqf, xc.C, xc.kw, xc.H,
-                         xc.sends[gb], xc.ovf)
+                         xc.sends[gb], xc.ovf, homes=xc.homes, b0=xc.b0, lgP=max(xc.lgP, 0))
         if xc.nb:  # (FixingFloat push: no pack_grads launch to carry the flag)
             hh.xchg_publish(xc.ovf, xc.ovf_host)
 
@@ -1421,7 +1459,8 @@ class SparseLRTrainer:
         H = (4 + C * kw + gw + 3) // 4 * 4
         i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)  # noqa: E731
         self.xc = SimpleNamespace(
-            C=C, kw=kw, H=H, nb=nb, w0=w0, off=off, send=i32(G * H),
+            C=C, kw=kw, H=H, nb=nb, w0=w0, b0=b0, fused=fused,
+            homes=self._owner_homes() if fused else None, off=off, send=i32(G * H),
             gstage=torch.zeros(G * C, dtype=torch.float32, device=dev) if nb else None,
             wout=torch.zeros(G * C, dtype=torch.float32, device=dev),
             slot=torch.full((G * C,), -1, dtype=torch.int64, device=dev),

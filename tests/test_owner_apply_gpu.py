@@ -109,3 +109,107 @@ def test_partitioned_apply_many_windows():
     hh.kv_apply_part(tabs[1].slots, slot, keys, gsrc, H, recv, H, C, bnd, 0, *rule.args(), None)
     torch.cuda.synchronize()
     assert torch.equal(tabs[0].slots, tabs[1].slots)
+
+
+@pytest.mark.parametrize("G,C,lgP,post", [(2, 4096, 5, True), (8, 2048, 9, True),
+                                          (8, 2048, 9, False), (3, 1024, 0, True)])
+def test_owner_part_matches_resolve_then_apply(G, C, lgP, post):
+    """kv_owner_part (one launch: resolve of the pulled keys with the SENDER's partition
+    bounds from xchg_pack_keys, then the per-source apply of an earlier pull) leaves the
+    table, slots, weights and bounds of kv_resolve_rows + kv_apply_part run separately
+    (post = resolve first; pre = apply first)."""
+    from parameter_server_amd.ops.kv_table import KVTable, UpdateRule
+    from parameter_server_amd.ops.native import hipops
+
+    dev = torch.device("cuda")
+    H = hipops()
+    P = 1 << lgP
+    kw = 2
+    gw = C
+    w0 = 4 + C * kw + gw
+    b0 = w0 + C
+    Hr = (b0 + P + 1 + 3) // 4 * 4
+    lo, hi = 1 << 40, 1 << 44
+    rule = UpdateRule("ftrl", "decay", 0.05, 1.0, 0.1, 0.1)
+    g = torch.Generator(device=dev).manual_seed(7)
+
+    def table():
+        return KVTable(1 << 16, dev, key_range=(lo, hi))
+
+    def sorted_keys(n):
+        return torch.unique(torch.randint(lo, hi, (n,), device=dev, generator=g))
+
+    # an earlier pull (the push's slots / keys / bounds) and this exchange's pulls
+    old_keys = [sorted_keys(int(C * 0.6)) for _ in range(G)]
+    new_keys = [torch.cat([old_keys[s][::3], sorted_keys(C // 3)]).unique()[:C - 8]
+                for s in range(G)]
+    outs = []
+    for fused in (True, False):
+        tb = table()
+        homes = torch.tensor([[tb.home_base - (1 << 64) if tb.home_base >= 1 << 63 else
+                               tb.home_base, tb.home_m - (1 << 64) if tb.home_m >= 1 << 63
+                               else tb.home_m]] * G, dtype=torch.int64, device=dev)
+        it, iv, isd, seed = tb.init.args()
+        # earlier pull: resolve old keys -> slots_old / keys_old / bnd_old
+        recv_old = torch.zeros(G * Hr, dtype=torch.int32, device=dev)
+        ukeys = torch.cat(old_keys)
+        off = torch.tensor([0] + torch.cumsum(torch.tensor([k.numel() for k in old_keys]), 0)
+                           .tolist(), dtype=torch.int64, device=dev)
+        n_u = torch.tensor([ukeys.numel()], dtype=torch.int32, device=dev)
+        # (the rows of one sender to G owners = one exchange's received rows here)
+        H.xchg_pack_keys(ukeys, n_u, off, C, kw, Hr, recv_old, None, homes=homes, b0=b0, lgP=lgP)
+        slots_old = torch.full((G * C,), -1, dtype=torch.int64, device=dev)
+        keys_old = torch.zeros(G * C, dtype=torch.int64, device=dev)
+        bnd_old = torch.zeros(G * (P + 1), dtype=torch.int32, device=dev)
+        wtmp = torch.zeros(G * C, dtype=torch.float32, device=dev)
+        H.kv_resolve_rows(tb.slots, recv_old, Hr, C, kw, slots_old, wtmp, True, it, iv, isd, seed,
+                          tb._err, None, tb.home_base, tb.home_m, keys_old, bnd_old, lgP)
+        # the rows' sender bounds equal the resolve's bounds
+        rb = torch.stack([recv_old[s * Hr + b0:s * Hr + b0 + P + 1] for s in range(G)])
+        assert torch.equal(rb.reshape(-1), bnd_old)
+        # this exchange: new keys + gradients of the old pull
+        recv = torch.zeros(G * Hr, dtype=torch.int32, device=dev)
+        ukeys = torch.cat(new_keys)
+        off = torch.tensor([0] + torch.cumsum(torch.tensor([k.numel() for k in new_keys]), 0)
+                           .tolist(), dtype=torch.int64, device=dev)
+        n_u = torch.tensor([ukeys.numel()], dtype=torch.int32, device=dev)
+        H.xchg_pack_keys(ukeys, n_u, off, C, kw, Hr, recv, None, homes=homes, b0=b0, lgP=lgP)
+        gr = torch.randn(G * C, device=dev, generator=g)
+        for s in range(G):
+            n = old_keys[s].numel()
+            recv[s * Hr + 1] = n
+            recv[s * Hr + 4 + C * kw:s * Hr + 4 + C * kw + n] = gr[s * C:s * C + n].view(torch.int32)
+        gsrc = recv.view(torch.float32)[4 + C * kw:]
+        slots_new = torch.full((G * C,), -1, dtype=torch.int64, device=dev)
+        keys_new = torch.zeros(G * C, dtype=torch.int64, device=dev)
+        bnd_new = torch.zeros(G * (P + 1), dtype=torch.int32, device=dev)
+        sendn = torch.zeros(G * Hr, dtype=torch.int32, device=dev)
+        wout = sendn.view(torch.float32)[w0:]
+        from parameter_server_amd.ops.linear import new_accum
+
+        stats = new_accum(dev)
+        if fused:
+            H.kv_owner_part(tb.slots, recv, Hr, C, kw, b0, lgP, slots_new, keys_new, bnd_new, wout,
+                            it, iv, isd, seed, tb._err, None, tb.home_base, tb.home_m, slots_old,
+                            keys_old, gsrc, Hr, bnd_old, post, *rule.args(), stats)
+        else:
+            def res():
+                H.kv_resolve_rows(tb.slots, recv, Hr, C, kw, slots_new, wout, True, it, iv, isd,
+                                  seed, tb._err, None, tb.home_base, tb.home_m, keys_new, bnd_new,
+                                  lgP, wstride=Hr)
+
+            def app():
+                H.kv_apply_part(tb.slots, slots_old, keys_old, gsrc, Hr, recv, Hr, C, bnd_old,
+                                lgP, *rule.args(), stats)
+            (res(), app()) if post else (app(), res())
+        torch.cuda.synchronize()
+        k, w, z, n = tb.occupied()
+        o = torch.argsort(k)
+        W = torch.stack([wout[s * Hr:s * Hr + new_keys[s].numel()] for s in range(G)], 0) \
+            if len({k_.numel() for k_ in new_keys}) == 1 else torch.cat(
+                [wout[s * Hr:s * Hr + new_keys[s].numel()] for s in range(G)])
+        outs.append((k[o].cpu(), w[o].cpu(), z[o].cpu(), n[o].cpu(), W.cpu(), bnd_new.cpu(),
+                     keys_new.cpu()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    assert int(tb._err.item()) == 0
