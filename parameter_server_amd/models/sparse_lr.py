@@ -1459,8 +1459,8 @@ class SparseLRTrainer:
         H = (4 + C * kw + gw + 3) // 4 * 4
         i32 = lambda n: torch.zeros(n, dtype=torch.int32, device=dev)  # noqa: E731
         self.xc = SimpleNamespace(
-            C=C, kw=kw, H=H, nb=nb, w0=w0, b0=b0, fused=fused,
-            homes=self._owner_homes() if fused else None, off=off, send=i32(G * H),
+            C=C, kw=kw, H=H, nb=nb, w0=None, b0=None, fused=False, homes=None, off=off,
+            send=i32(G * H),
             gstage=torch.zeros(G * C, dtype=torch.float32, device=dev) if nb else None,
             wout=torch.zeros(G * C, dtype=torch.float32, device=dev),
             slot=torch.full((G * C,), -1, dtype=torch.int64, device=dev),
