@@ -107,7 +107,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     # eagerly (the rows go to the generator as a launch argument), on the device once
     # they replay from graphs (a captured preparation reads and advances it)
     hctr = [0] * nprep
-    ctr = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(nprep)]
+    ctr = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(nprep)]
     locs = [None] * NB
     mode = {"capture": False}
     fplans = ([tr.prep_plan(b, bufs[b][0], bufs[b][1], seed=seed, row0=b * B, row_step=NB * B,
@@ -121,8 +121,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             return
         if mode["capture"]:
             criteo_batch(B, seed=seed, row0=sidx * B, num_features=N, device=device, keys=k,
-                         labels=lab, row0_dev=ctr[sidx], row_scale=nprep * B)
-            ctr[sidx].add_(1)
+                         labels=lab, row0_dev=ctr[sidx], row_scale=nprep * B, advance=True)
         else:
             criteo_batch(B, seed=seed, row0=(hctr[sidx] * nprep + sidx) * B, num_features=N,
                          device=device, keys=k, labels=lab)
@@ -388,7 +387,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     iterate.release = release
     gp = []
     for s_ in range(nprep):  # the replays continue the eager row counts on the device
-        ctr[s_].fill_(hctr[s_])
+        ctr[s_][0].fill_(hctr[s_])
     mode["capture"] = True
     for b in range(NB):  # t0 % NB == 0: buffer b <-> minibatch t0 + b
         g = torch.cuda.CUDAGraph()
@@ -533,7 +532,7 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
     bufs = [(keys, labels)] + [(torch.empty_like(keys), torch.empty_like(labels))
                                for _ in range(NB - 1)]
     hctr = [0] * nprep
-    ctr = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(nprep)]
+    ctr = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(nprep)]
     locs = [None] * NB
     mode = {"capture": False}
     tr._mx_external = True  # progress() must not drain: the exchanges below are in flight
@@ -543,8 +542,7 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         k, lab = bufs[b]
         if mode["capture"]:
             criteo_batch(B, seed=seed, row0=sidx * B, num_features=N, device=device, keys=k,
-                         labels=lab, row0_dev=ctr[sidx], row_scale=nprep * B)
-            ctr[sidx].add_(1)
+                         labels=lab, row0_dev=ctr[sidx], row_scale=nprep * B, advance=True)
         else:
             criteo_batch(B, seed=seed, row0=(hctr[sidx] * nprep + sidx) * B, num_features=N,
                          device=device, keys=k, labels=lab)
@@ -679,7 +677,7 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
 
     gp = []
     for s_ in range(nprep):
-        ctr[s_].fill_(hctr[s_])
+        ctr[s_][0].fill_(hctr[s_])
     mode["capture"] = True
     for b in range(NB):
         gp.append(graph_of(lambda b=b: prep(b)))

@@ -180,8 +180,8 @@ void linear_bwd(const int32_t*, const int32_t*, int64_t, const int32_t*, int, co
 void auc_from_hist(uint32_t*, int, int, double*, int64_t*, hipStream_t);
 void csr_rows(const int64_t*, int64_t, int32_t*, hipStream_t);
 void criteo_set_tables(const uint32_t*, const float*);
-void criteo_gen(uint64_t, int64_t, const int64_t*, int64_t, int64_t, uint64_t, float, uint64_t*,
-                float*, hipStream_t);
+void criteo_gen(uint64_t, int64_t, int64_t*, int64_t, int64_t, uint64_t, float, uint64_t*,
+                float*, bool, hipStream_t);
 void add_i64(int64_t*, int64_t, hipStream_t);
 // filters.hip
 void cm_insert(uint32_t*, uint64_t, int, uint32_t, const uint64_t*, const uint8_t*, int64_t,
@@ -649,7 +649,7 @@ Launch make_criteo_gen(uint64_t seed, int64_t row0, int64_t row_step, int64_t B,
   auto cursor = std::make_shared<int64_t>(row0);
   return [=, keep = std::vector<Tensor>{keys, labels}](hipStream_t st) {
     psamd::criteo_gen(seed, *cursor, nullptr, 1, B, num_features, (float)alpha,
-                      ptr<uint64_t>(keys), ptr<float>(labels), st);
+                      ptr<uint64_t>(keys), ptr<float>(labels), false, st);
     *cursor += row_step;
   };
 }
@@ -1961,7 +1961,10 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("criteo_gen", [](uint64_t seed, int64_t row0, int64_t B, uint64_t num_features,
                          double alpha, Tensor keys, Tensor labels, optional<Tensor> row0_dev,
-                         int64_t row_scale) {
+                         int64_t row_scale, bool advance) {
+    // advance: row0_dev = [cursor, done-count]; the kernel bumps the cursor by one at its
+    // end (a captured graph's next replay generates the next rows, no separate add)
+    if (advance) check(row0_dev && row0_dev->numel() >= 2, "advance needs row0_dev [2]");
     chk(keys, at::kLong, "keys");
     chk(labels, at::kFloat, "labels");
     check(keys.numel() >= B * 39 && labels.numel() >= B, "criteo_gen buffers too small");
@@ -1969,8 +1972,10 @@ PYBIND11_MODULE(_hipops, m) {
     check(num_features > 0, "num_features > 0");
     psamd::criteo_gen(seed, row0, optr<int64_t>(row0_dev, at::kLong, "row0_dev"), row_scale, B,
                       num_features, (float)alpha, ptr<uint64_t>(keys), ptr<float>(labels),
-                      cur_stream());
-  });
+                      advance, cur_stream());
+  }, py::arg("seed"), py::arg("row0"), py::arg("B"), py::arg("num_features"), py::arg("alpha"),
+     py::arg("keys"), py::arg("labels"), py::arg("row0_dev") = py::none(),
+     py::arg("row_scale") = 1, py::arg("advance") = false);
 
   // ---------------- filters ----------------
   m.def("cm_insert", [](Tensor table, int k, int vmax, Tensor keys, optional<Tensor> counts,

@@ -296,9 +296,10 @@ __device__ __forceinline__ void gen_slot_range(int w, int& j0, int& j1) {
 }
 template <bool kWide>
 __global__ void __launch_bounds__(kGenThreads)
-criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_dev,
+criteo_gen_kernel(uint64_t seed, int64_t row0, int64_t* __restrict__ row0_dev,
                   int64_t row_scale, int64_t B, uint64_t num_features, uint64_t nf_m,
-                  float alpha, uint64_t* __restrict__ keys, float* __restrict__ labels) {
+                  float alpha, uint64_t* __restrict__ keys, float* __restrict__ labels,
+                  int advance) {
   __shared__ uint64_t sk[kGenRows * 39];
   __shared__ float sp[kGenRows * 39];
   __shared__ float s_cm1[26];
@@ -349,6 +350,20 @@ criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_
     }
     __syncthreads();
   }
+  if (advance) {
+    // the row cursor advances on the device (a graph replay generates the next rows):
+    // the last block to finish bumps row0_dev[0] -- every block read it at its start,
+    // before counting itself done in row0_dev[1] (vector atomics only)
+    __syncthreads();
+    if (t == 0) {
+      __threadfence();
+      const unsigned long long d = atomicAdd(reinterpret_cast<unsigned long long*>(row0_dev + 1), 1ull);
+      if (d == (unsigned long long)gridDim.x - 1) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(row0_dev), 1ull);
+        atomicExch(reinterpret_cast<unsigned long long*>(row0_dev + 1), 0ull);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -397,18 +412,20 @@ void criteo_set_tables(const uint32_t* cards26, const float* gauss256) {
   PSAMD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_gauss), gauss256, 256 * sizeof(float)));
 }
 
-void criteo_gen(uint64_t seed, int64_t row0, const int64_t* row0_dev, int64_t row_scale,
+void criteo_gen(uint64_t seed, int64_t row0, int64_t* row0_dev, int64_t row_scale,
                 int64_t B, uint64_t num_features, float alpha, uint64_t* keys, float* labels,
-                hipStream_t st) {
+                bool advance, hipStream_t st) {
   const int64_t blocks = (B + kGenRows - 1) / kGenRows;
   const uint64_t nf_m = ~0ull / num_features;
   const unsigned grid = (unsigned)(blocks < 65535 ? blocks : 65535);
   if (num_features <= (1ull << 32))
     criteo_gen_kernel<false><<<grid, kGenThreads, 0, st>>>(seed, row0, row0_dev, row_scale, B,
-                                                           num_features, nf_m, alpha, keys, labels);
+                                                           num_features, nf_m, alpha, keys, labels,
+                                                           advance && row0_dev ? 1 : 0);
   else
     criteo_gen_kernel<true><<<grid, kGenThreads, 0, st>>>(seed, row0, row0_dev, row_scale, B,
-                                                          num_features, nf_m, alpha, keys, labels);
+                                                          num_features, nf_m, alpha, keys, labels,
+                                                          advance && row0_dev ? 1 : 0);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

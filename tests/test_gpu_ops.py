@@ -305,3 +305,20 @@ def test_criteo_gen_gpu_matches_cpu():
     assert float((kg.cpu() == kc).float().mean()) > 0.97
     assert float((lg.cpu() == lc).float().mean()) > 0.9
     assert int(kg.min()) >= 0 and int(kg.max()) < 10 ** 9
+
+
+@pytest.mark.gpu
+def test_criteo_gen_advances_its_device_cursor():
+    """criteo_batch(advance=True): the kernel's last block bumps row0_dev[0], so two
+    launches (or graph replays) generate rows row0 + k * scale for k = c, c + 1."""
+    from parameter_server_amd.ops.synthetic import criteo_batch
+
+    dev = torch.device("cuda")
+    B = 3000
+    ctr = torch.tensor([5, 0], dtype=torch.int64, device=dev)
+    for k in (5, 6, 7):
+        keys, labels = criteo_batch(B, seed=3, row0=11, num_features=10 ** 9, device=dev,
+                                    row0_dev=ctr, row_scale=B, advance=True)
+        rk, rl = criteo_batch(B, seed=3, row0=11 + k * B, num_features=10 ** 9, device=dev)
+        assert torch.equal(keys, rk) and torch.equal(labels, rl)
+    assert ctr.tolist() == [8, 0]
