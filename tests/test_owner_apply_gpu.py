@@ -143,6 +143,7 @@ def test_owner_part_matches_resolve_then_apply(G, C, lgP, post):
     old_keys = [sorted_keys(int(C * 0.6)) for _ in range(G)]
     new_keys = [torch.cat([old_keys[s][::3], sorted_keys(C // 3)]).unique()[:C - 8]
                 for s in range(G)]
+    gr = torch.randn(G * C, device=dev, generator=g)  # (the same pushes in both runs)
     outs = []
     for fused in (True, False):
         tb = table()
@@ -174,7 +175,6 @@ def test_owner_part_matches_resolve_then_apply(G, C, lgP, post):
                            .tolist(), dtype=torch.int64, device=dev)
         n_u = torch.tensor([ukeys.numel()], dtype=torch.int32, device=dev)
         H.xchg_pack_keys(ukeys, n_u, off, C, kw, Hr, recv, None, homes=homes, b0=b0, lgP=lgP)
-        gr = torch.randn(G * C, device=dev, generator=g)
         for s in range(G):
             n = old_keys[s].numel()
             recv[s * Hr + 1] = n
