@@ -850,7 +850,7 @@ def main():
     ap.add_argument("--fixing-float", type=int, default=0)
     ap.add_argument("--exchange-merge", default="auto", choices=["auto", "on", "off"],
                     help="N > 1, lag >= 1: one all-to-all per step carrying [keys(t+1) | "
-                         "pushes | weights of keys(t)] (auto: ssp:tau >= 2 and asp) or the "
+                         "pushes | weights of keys(t)] (auto: ssp:tau >= 2) or the "
                          "two-collective exchange (off)")
     ap.add_argument("--ssp-apply", default="post", choices=["post", "pre"],
                     help="N > 1, ssp: the owner applies the carried pushes after sending the "

@@ -98,8 +98,9 @@ class SparseLRConfig:
     asp_depth: int = 4                   # asp: exchanges whose push applies may be in flight
     # padded exchange with lag >= 1: ONE all-to-all per step carrying [keys(t+1) |
     # grads(t-d) | weights of keys(t)] (parallel/consistency.MergedSchedule) instead of
-    # two (keys + grads, then weights). "auto": on for ssp:tau >= 2 and asp; "on" also
-    # for ssp:1 (worker and exchange then serialise); "off": two collectives
+    # two (keys + grads, then weights). "auto": on for ssp:tau >= 2; "on" also for
+    # ssp:1 (worker and exchange then serialise) and asp (staleness exactly 3); "off":
+    # two collectives
     exchange_merge: str = "auto"
     seed: int = 0
 
@@ -225,10 +226,14 @@ class SparseLRTrainer:
         self.R = self.sched.R
         if cfg.exchange_merge not in ("auto", "on", "off"):
             raise ValueError(f"exchange_merge must be auto / on / off, not {cfg.exchange_merge!r}")
+        # (auto: ssp:tau >= 2. asp stays on the two-collective exchange, whose owner
+        # applies run beside the pulls: served on the merged one with staleness exactly
+        # 3, plain SGD at 8 emulated peers + fixing-float diverged, loss 1.03 after 50
+        # steps, tests/test_train_quality_gpu.py)
         self.merged = bool(
             self.padded and self.filter is None and cfg.exchange_merge != "off"
-            and self.tau > 0 and (cfg.exchange_merge == "on" or math.isinf(self.tau)
-                                  or self.tau >= 2))
+            and self.tau > 0 and (cfg.exchange_merge == "on"
+                                  or (not math.isinf(self.tau) and self.tau >= 2)))
         self.msched = None
         if self.merged:  # one collective per step (MergedSchedule)
             self.msched = MergedSchedule(self.tau, cfg.exchange_lag)

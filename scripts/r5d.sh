@@ -2,10 +2,8 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/r5d
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest -x -v --timeout 240 --timeout-method thread -p no:cacheprovider \
-  tests/test_owner_apply_gpu.py tests/test_bench_pipeline_gpu.py tests/test_p2p_gpu.py tests/test_partloc_gpu.py \
-  tests/test_rcv1_goldens.py tests/test_sharded_kv.py tests/test_tp_fused_gpu.py tests/test_tpf_gpu.py \
-  tests/test_tploc_gpu.py tests/test_train_quality_gpu.py tests/test_trainer_gpu.py tests/test_wide_deep_gpu.py \
-  tests/test_dist_gpu.py -m gpu > gpurun_out/r5d/pytest.log 2>&1
+  tests/test_train_quality_gpu.py tests/test_trainer_gpu.py tests/test_wide_deep_gpu.py \
+  tests/test_dist_gpu.py tests/test_gpu_ops.py -m gpu > gpurun_out/r5d/pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/r5d/pytest.log; [ $rc -eq 0 ] || exit $rc
 for f in 1 0; do
   for e in 8 2; do

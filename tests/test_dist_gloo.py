@@ -201,7 +201,7 @@ def test_explicit_smaller_lag_within_bound(tmp_path):
     # (lag 1 is served by the two-collective schedule unless exchange_merge="on")
 
 
-@pytest.mark.parametrize("merge,lag", [("off", 2), ("auto", 3)])
+@pytest.mark.parametrize("merge,lag", [("off", 2), ("auto", 2), ("on", 3)])
 def test_asp_differs_from_ssp1(tmp_path, merge, lag):
     """asp, two collectives: the owner applies the pushes an exchange carries AFTER
     resolving its pulls (on the GPU on its own stream, which pulls never wait for). Run
