@@ -1069,8 +1069,11 @@ class SparseLRTrainer:
         # the row's receiver sent in the previous exchange (word w0) and, for the owner's
         # one-launch resolve + apply (kv_owner_part), the bounds of its 2^lgP key-range
         # partitions over the row's keys (word b0, written by the sender's key pack)
+        # (off by default: one launch of both halves measured the SUM of their kernel
+        # times, 56.4 vs 22.3 + 34.4 us at 8 emulated peers, and it puts the apply on the
+        # path to the next collective: 0.175 vs 0.155 ms / step, profiles/r5_owner_fused.log)
         fused = (self.merged and lgP >= 0
-                 and os.environ.get("PSAMD_OWNER_FUSED", "1") != "0")
+                 and os.environ.get("PSAMD_OWNER_FUSED", "0") == "1")
         w0 = 4 + C * kw + gw
         b0 = w0 + (C if self.merged else 0)
         H = (b0 + (((1 << lgP) + 1) if fused else 0) + 3) // 4 * 4
