@@ -2365,11 +2365,14 @@ static TpGeom tp_geom(int64_t n, int bits) {
   TpGeom g;
   g.T = (n + tp::kTile - 1) / tp::kTile;
   g.N = g.T * tp::kTile;
-  // <= 1280 occurrences per bucket on average: even if every key is distinct a
-  // bucket's distinct keys stay under kDH / 2 (measured on Criteo-shaped batches:
-  // <= 1615 entries and 157 distinct keys per bucket at 2048 buckets)
+  // <= 1024 occurrences per bucket on average: even if every key is distinct a PAIR of
+  // buckets (the flat layout's unit) stays under the kDH-key hash (at 1280, nearly
+  // distinct minibatches -- e.g. 1000 rcv1-width rows over 10^8 ids -- overflowed every
+  // pair into the register-light fallback: ~20x slower bucket kernel). The 2048-bucket
+  // cap leaves the Criteo-shaped 65,536 x 39 batch as before (measured there: <= 1615
+  // entries and 157 distinct keys per bucket at 2048 buckets)
   int bb = 0;
-  while (bb < 11 && (n >> bb) > 1280) ++bb;
+  while (bb < 11 && (n >> bb) > 1024) ++bb;
   if (bb > bits) bb = bits;
   g.nbk = 1 << bb;
   g.shift = bits - bb;
