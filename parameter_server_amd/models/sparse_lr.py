@@ -1506,11 +1506,13 @@ class SparseLRTrainer:
                                  coef=self.coef[:B], metrics=self.metrics, hist=self.hist)
         if xc.nb:
             # FixingFloat codes for the peers (reference async_sgd.h:273-277); the own row
-            # is applied from the unquantised staged gradients
+            # is decoded from its codes too, as the padded exchange decodes every recv row
+            # (the reference quantises every push through its filter)
             seed = (self.cfg.seed * 7919 + 17) & ((1 << 64) - 1)
             hh.xchg_ff_pack_grads(grad[:U], None, loc.n_uniq, xc.off, C, kw, H, xc.nb, seed,
                                   self.step_dev, xc.send, xc.gstage)
             g_own = xc.gstage[r * C:(r + 1) * C]
+            hh.xchg_ff_decode(xc.send[r * H:(r + 1) * H], C, kw, H, xc.nb, g_own)
             auc_from_hist(self.hist, self.metrics, self.step_dev)
         else:
             hh.xchg_pack_grads(grad[:U], None, loc.n_uniq, xc.off, C, kw, H, xc.send,

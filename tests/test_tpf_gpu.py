@@ -384,7 +384,10 @@ def test_overlapped_step_kernel_is_bitwise_the_sequential_one(monkeypatch, data,
     from parameter_server_amd.ops.kv_table import InitRule
 
     monkeypatch.setenv("PSAMD_FLAT", "1")
-    B = 8192
+    # (uniform: the driver's B, where the unit geometry is capped at 1024 pairs of fine
+    # buckets, ~2,500 nearly distinct occurrences each; at smaller B the geometry keeps
+    # every unit <= 2,048 entries and the fallback loops never run)
+    B = 8192 if data == "criteo" else 65536
     g = torch.Generator(device=DEV).manual_seed(3)
     if data == "criteo":
         batches = [criteo_batch(B, seed=43, row0=t * B, num_features=10 ** 9, device=DEV)
@@ -397,7 +400,7 @@ def test_overlapped_step_kernel_is_bitwise_the_sequential_one(monkeypatch, data,
     outs = []
     for v1 in ("1", "0"):
         monkeypatch.setenv("PSAMD_TPF_STEP2", "0" if v1 == "1" else "1")
-        cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, table_capacity=1 << 23,
+        cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, table_capacity=1 << 25,
                              init=InitRule(init, 0.0, 0.01 if init == "gaussian" else 0.0, 5))
         tr = SparseLRTrainer(cfg, device=DEV)
         assert tr.localize_mode == "tpf"
