@@ -80,6 +80,9 @@ void tpf_step(int64_t, int, const int32_t*, const int32_t*, const uint16_t*, con
               float, float, uint64_t, int32_t*, int32_t*, int, int, float, float, float, float,
               float, float, double*, int, uint32_t*, int, int, double*, int64_t*, hipStream_t);
 int64_t tploc_stride(int64_t);
+int64_t tpf_stride(int64_t);
+int64_t tpf_stride_max(int64_t);
+int tpf_tile_log2(int64_t);
 int tploc_buckets(int64_t, int);
 int tploc_tile();
 bool tploc_supported(int64_t, int);
@@ -429,7 +432,7 @@ Launch make_tp_fwd_bwd(Tensor rep, Tensor dcnt, optional<Tensor> ent_uid, int64_
   float* gr = optr<float>(grad, at::kFloat, "grad");
   check(psamd::tp_fwd_bwd_supported(width) && n == B * (int64_t)width && n > 0,
         "tp_fwd_bwd: fixed width 9..64 (tp_fwd_bwd_supported) and n == B * width");
-  const int64_t N = psamd::tploc_stride(n);
+  const int64_t N = eu ? psamd::tploc_stride(n) : psamd::tpf_stride(n);
   check(rep.numel() >= n && dcnt.numel() >= N / psamd::tploc_tile(), "tp_fwd_bwd: rep / dcnt");
   check(psum.numel() >= N, "tp_fwd_bwd: psum < stride");
   if (eu) {
@@ -483,7 +486,7 @@ Launch make_tp_fwd_bwd_csr(Tensor rep, Tensor dcnt, optional<Tensor> ent_uid, in
   check(n > 0 && B > 0 && row_ptr.numel() >= B + 1 && rows.numel() >= n,
         "tp_fwd_bwd_csr: row_ptr [B+1], rows [n]");
   check(psamd::tploc_stride(n) / psamd::tploc_tile() <= 640, "tp_fwd_bwd_csr: <= 5.2 M keys");
-  const int64_t N = psamd::tploc_stride(n);
+  const int64_t N = eu ? psamd::tploc_stride(n) : psamd::tpf_stride(n);
   check(rep.numel() >= n && dcnt.numel() >= N / psamd::tploc_tile(), "tp_fwd_bwd_csr: rep / dcnt");
   check(psum.numel() >= N, "tp_fwd_bwd_csr: psum < stride");
   if (eu) {
@@ -556,7 +559,7 @@ Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor d
   chk(err, at::kInt, "err");
   check(n > 0 && keys.numel() >= n, "localize_tpf: n keys");
   check_tpf(TpfBufs{cnt, uniqf, ent_pos, ent_j, ent_pos}, n, bits, "localize_tpf");
-  const int64_t T = psamd::tploc_stride(n) / psamd::tploc_tile();
+  const int64_t T = psamd::tpf_stride(n) / psamd::tploc_tile();
   check(dcnt.numel() >= T && rep.numel() >= n, "localize_tpf: dcnt / rep");
   check((size_t)temp.numel() >= psamd::tpf_temp_bytes(n, bits), "localize_tpf: temp too small");
   const psamd::KeyMix km = make_keymix(bits);
@@ -582,7 +585,7 @@ Launch make_tpf_step(int64_t n, int bits, optional<TpfBufs> A, optional<Tensor> 
   check(cap <= ((int64_t)1 << 32), "tpf_step: u32 slot ids need <= 2^32 slots");
   check(A.has_value() || B.has_value(), "tpf_step: nothing to do");
   check(alpha > 0, "learning rate alpha must be > 0");
-  const int64_t N = psamd::tploc_stride(n);
+  const int64_t N = psamd::tpf_stride(n);
   if (A) {
     check_tpf(*A, n, bits, "tpf_step A");
     check(psum.has_value(), "tpf_step: update needs psum");
@@ -866,6 +869,10 @@ PYBIND11_MODULE(_hipops, m) {
   });
   // ---------------- tile dedup + bucket partition localisation (tploc.hip) ----------------
   m.def("tploc_stride", [](int64_t n) { return psamd::tploc_stride(n); });
+  // flat layout: entry stride of n keys / bound over minibatches of <= n keys / log2 tile
+  m.def("tpf_stride", [](int64_t n) { return psamd::tpf_stride(n); });
+  m.def("tpf_stride_max", [](int64_t n) { return psamd::tpf_stride_max(n); });
+  m.def("tpf_tile_log2", [](int64_t n) { return psamd::tpf_tile_log2(n); });
   m.def("tploc_buckets", [](int64_t n, int bits) { return psamd::tploc_buckets(n, bits); });
   m.def("tploc_supported", [](int64_t n, int bits) { return psamd::tploc_supported(n, bits); });
   m.def("tploc_temp_bytes", [](int64_t n, int bits) { return (int64_t)psamd::tploc_temp_bytes(n, bits); });
@@ -992,7 +999,7 @@ PYBIND11_MODULE(_hipops, m) {
     chk(w_ent, at::kFloat, "w_ent");
     check(psamd::tpf_exchange_ok(n, bits, G), "tpf_unpack_w: G a power of two dividing groups");
     check(C > 0 && ws >= C && wrecv.numel() >= (G - 1) * ws + C &&
-          w_ent.numel() >= psamd::tploc_stride(n), "tpf_unpack_w: buffers");
+          w_ent.numel() >= psamd::tpf_stride(n), "tpf_unpack_w: buffers");
     psamd::tpf_unpack_w(n, bits, G, ptr<int32_t>(cnt), ptr<int32_t>(ent_pos),
                         ptr<uint16_t>(ent_j), C, ptr<float>(wrecv), ws, ptr<float>(w_ent),
                         w_ent.numel(), cur_stream());
@@ -1010,7 +1017,7 @@ PYBIND11_MODULE(_hipops, m) {
     check(psamd::tpf_exchange_ok(n, bits, G), "tpf_pack_grads: G a power of two dividing groups");
     check((kw == 1 || kw == 2) && C > 0 && H >= 4 + C * kw + 1 && send.numel() >= G * H,
           "tpf_pack_grads: row geometry");
-    check(psum.numel() >= psamd::tploc_stride(n), "tpf_pack_grads: psum < stride");
+    check(psum.numel() >= psamd::tpf_stride(n), "tpf_pack_grads: psum < stride");
     float* gs = optr<float>(gstage, at::kFloat, "gstage");
     if (gs) check(gstage->numel() >= G * C, "tpf_pack_grads: gstage < G * C");
     else check(H >= 4 + C * kw + C, "tpf_pack_grads: f32 gradient rows");

@@ -426,6 +426,7 @@ __device__ __forceinline__ void apply_part_block(
   __shared__ int32_t went[kApWin], wnx[kApWin], whs[kApWin];
   __shared__ float wg[kApWin];
   __shared__ int32_t ra[kMaxChain], re[kMaxChain], roff[kMaxChain + 1], rcnt[kMaxChain];
+  __shared__ uint64_t thk[kMaxChain];
   __shared__ uint64_t thr;
   const int tid = threadIdx.x, P = 1 << lgP, part = blockIdx.x;
   const int CH = max(1, kApWin / G);
@@ -443,15 +444,21 @@ __device__ __forceinline__ void apply_part_block(
   double dnnz = 0, wsum = 0, dsum = 0;
   for (;;) {
     __syncthreads();
+    // the window's end keys of the rows that do not fit: one load per row, all rows in
+    // parallel (a serial loop over the rows was a chain of up to G dependent global loads)
+    if (tid < G) {
+      const int rem = re[tid] - ra[tid];
+      thk[tid] = rem > CH ? keys[(int64_t)tid * C + ra[tid] + CH - 1] : ~0ull;
+      rcnt[tid] = 0;
+    }
+    __syncthreads();
     if (tid == 0) {
       int off = 0;
       uint64_t t = ~0ull;
       for (int s = 0; s < G; ++s) {
-        const int rem = re[s] - ra[s];
         roff[s] = off;
-        off += min(rem, CH);
-        if (rem > CH) t = min(t, keys[(int64_t)s * C + ra[s] + CH - 1]);
-        rcnt[s] = 0;
+        off += min(re[s] - ra[s], CH);
+        t = min(t, thk[s]);
       }
       roff[G] = off;
       thr = t;

@@ -30,6 +30,7 @@
 #include "kv_slot.cuh"
 #include "loss.cuh"
 
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -130,7 +131,7 @@ __global__ void __launch_bounds__(tp::kThr, 8)
 tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift, int nbk,
                uint32_t* __restrict__ tkeys, uint16_t* __restrict__ toff,
                int32_t* __restrict__ dcnt, uint16_t* __restrict__ rep,
-               int32_t* __restrict__ err) {
+               int32_t* __restrict__ err, int lts) {
   using namespace tp;
   __shared__ uint32_t hk[kHash];    // quotient-encoded keys; after the bucket sort: entry position
   __shared__ uint32_t cnt[kMaxBk];  // per-bucket counts, then offsets
@@ -139,20 +140,22 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
   for (int i = t; i < kHash; i += kThr) hk[i] = kEmpty;
   for (int d = t; d < nbk; d += kThr) cnt[d] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kTile;
+  // occurrences [base, base + lim) (2^lts per tile, tp_geom); entry ids keep the
+  // kTile stride (tkeys, dcnt, the consumers' tile * kTile + entry)
+  const int64_t base = (int64_t)blockIdx.x << lts;
+  const int lim = (int)(n - base < (1 << lts) ? n - base : (1 << lts));
   uint64_t kr[kIt];
   uint16_t sl[kIt];
   bool bad = false;
 #pragma unroll
   for (int j = 0; j < kIt; ++j) {  // all loads in flight before the LDS insert chain
-    const int64_t i = base + j * kThr + t;
-    kr[j] = i < n ? raw[i] : 0ull;
+    const int o = j * kThr + t;
+    kr[j] = o < lim ? raw[base + o] : 0ull;
   }
 #pragma unroll
   for (int j = 0; j < kIt; ++j) {
-    const int64_t i = base + j * kThr + t;
     sl[j] = 0;
-    if (i < n) {
+    if (j * kThr + t < lim) {
       const uint64_t k = mix_key(kr[j], m);
       const uint32_t q = kQuot ? (uint32_t)(k >> kHB) << kDispB : (uint32_t)k;
       uint32_t h = (kQuot ? (uint32_t)k : tp_hash((uint32_t)k)) & (kHash - 1);
@@ -213,7 +216,7 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
     dcnt[blockIdx.x] = (int32_t)D;
   }
   __syncthreads();
-  uint32_t* tk = tkeys + base;
+  uint32_t* tk = tkeys + (int64_t)blockIdx.x * kTile;
   const uint64_t smask = (1ull << shift) - 1;
 #pragma unroll
   for (int q = 0; q < kPer; ++q) {
@@ -231,8 +234,8 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kIt; ++j) {
-    const int64_t i = base + j * kThr + t;
-    if (i < n) rep[i] = (uint16_t)hk[sl[j]];
+    const int o = j * kThr + t;
+    if (o < lim) rep[base + o] = (uint16_t)hk[sl[j]];
   }
 }
 
@@ -1123,7 +1126,7 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
                   const float* __restrict__ labels, int64_t B, int loss_type,
                   float* __restrict__ coef_out, double* __restrict__ metrics,
                   uint32_t* __restrict__ hist, int nbins, int acc_stripes, int hist_stripes,
-                  float* __restrict__ psum) {
+                  float* __restrict__ psum, int lts) {
   using namespace tp;
   // one 64 KB region: forward = entry weights (f32, [0, 32 KB)) + AUC histogram
   // ([32 KB, 48 KB)); backward = the entries' fixed-point accumulators (i64)
@@ -1136,8 +1139,9 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
   long long* const acc = reinterpret_cast<long long*>(region);
   constexpr int kRowsPass = kThr / kFbLanes;
   const int t = threadIdx.x, sub = t % kFbLanes, g = t / kFbLanes;
-  const int64_t base = (int64_t)blockIdx.x * kTile;
-  const int lim = (int)(n - base < kTile ? n - base : kTile);
+  // occurrences [base, base + lim) (2^lts per tile), entries [eb, eb + cnt)
+  const int64_t base = (int64_t)blockIdx.x << lts, eb = (int64_t)blockIdx.x * kTile;
+  const int lim = (int)(n - base < (1 << lts) ? n - base : (1 << lts));
   const int64_t r0 = base / width;
   const int nr = (int)((base + lim - 1) / width - r0 + 1);
   const int cnt = min(kTile, max(0, dcnt[blockIdx.x]));
@@ -1178,17 +1182,17 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
     for (int q = 0; q < PER; ++q)
       if (ce[p][q] == kFbExt) {
         const int64_t i = (r0 + ri) * width + sub + q * kFbLanes;
-        const int64_t ge = (i / kTile) * kTile + __float_as_int(cv[p][q]);
+        const int64_t ge = (i >> lts) * kTile + __float_as_int(cv[p][q]);
         const int64_t u = kFlat ? ge : (int64_t)ent_uid[ge];
         cv[p][q] = (in_range(u, w_cap) ? w_local[u] : 0.f) * (vals ? vals[i] : 1.f);
       }
   }
   for (int i = t; i < nr; i += kThr) crow[i] = r0 + i < B ? labels[r0 + i] : 0.f;
   if (kFlat) {
-    for (int i = t; i < cnt; i += kThr) wl[i] = w_local[base + i];  // (host: w_cap >= T * 8192)
+    for (int i = t; i < cnt; i += kThr) wl[i] = w_local[eb + i];  // (host: w_cap >= T * 8192)
   } else {
     for (int i = t; i < cnt; i += kThr) {
-      const int32_t u = ent_uid[base + i];
+      const int32_t u = ent_uid[eb + i];
       wl[i] = in_range(u, w_cap) ? w_local[u] : 0.f;
     }
   }
@@ -1266,7 +1270,7 @@ tp_fwd_bwd_kernel(const uint16_t* __restrict__ rep, const int32_t* __restrict__ 
   __syncthreads();
   FB_MARK(5);
   const double isc = ldexp(1.0, -k2);
-  for (int i = t; i < cnt; i += kThr) psum[base + i] = (float)((double)acc[i] * isc);
+  for (int i = t; i < cnt; i += kThr) psum[eb + i] = (float)((double)acc[i] * isc);
   FB_MARK(6);
   if (fbp && threadIdx.x == 0) {
     fbp[(int64_t)blockIdx.x * 16 + 9] = __builtin_amdgcn_s_memrealtime();
@@ -1300,7 +1304,7 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
                       int64_t w_cap, const float* __restrict__ labels, int64_t B, int loss_type,
                       float* __restrict__ coef_out, double* __restrict__ metrics,
                       uint32_t* __restrict__ hist, int nbins, int acc_stripes, int hist_stripes,
-                      float* __restrict__ psum) {
+                      float* __restrict__ psum, int lts) {
   using namespace tp;
   __shared__ unsigned long long region[kTile];  // fwd: entry weights + AUC bins; bwd: i64 acc
   __shared__ float crow[kCsrRows];              // a window's row margins, then their coefs
@@ -1313,8 +1317,9 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
   constexpr int kPer = kTile / kThr;  // 8 occurrences per thread
   constexpr uint32_t kNone = 0xffffffffu;
   const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kTile;
-  const int lim = (int)(n - base < kTile ? n - base : kTile);
+  // occurrences [base, base + lim) (2^lts per tile), entries [eb, eb + cnt)
+  const int64_t base = (int64_t)blockIdx.x << lts, eb = (int64_t)blockIdx.x * kTile;
+  const int lim = (int)(n - base < (1 << lts) ? n - base : (1 << lts));
   const int cnt = min(kTile, max(0, dcnt[blockIdx.x]));
   const int64_t r0 = rows[base], r1 = rows[base + lim - 1];  // (uniform loads)
   // occurrence = (row - r0) << 16 | tile entry (rows of a tile < 2^14, entries < 2^13)
@@ -1336,10 +1341,10 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
   if (t < 4) sacc[t] = 0.f;
   if (t == 0) smax = 0u;
   if (kFlat) {
-    for (int i = t; i < cnt; i += kThr) wl[i] = w_local[base + i];
+    for (int i = t; i < cnt; i += kThr) wl[i] = w_local[eb + i];
   } else {
     for (int i = t; i < cnt; i += kThr) {
-      const int32_t u = ent_uid[base + i];
+      const int32_t u = ent_uid[eb + i];
       wl[i] = in_range(u, w_cap) ? w_local[u] : 0.f;
     }
   }
@@ -1380,7 +1385,7 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
         const int64_t b = wave == 0 ? base : row_ptr[r + 1];
         float sum = 0.f;
         for (int64_t i = a + lane; i < b; i += 64) {
-          const int64_t ge = (i / kTile) * kTile + (int64_t)rep[i];
+          const int64_t ge = (i >> lts) * kTile + (int64_t)rep[i];
           const int64_t u = kFlat ? ge : (int64_t)ent_uid[ge];
           sum += (in_range(u, w_cap) ? w_local[u] : 0.f) * (vals ? vals[i] : 1.f);
         }
@@ -1455,7 +1460,7 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
     }
   __syncthreads();
   const double isc = ldexp(1.0, -k2);
-  for (int i = t; i < cnt; i += kThr) psum[base + i] = (float)((double)acc[i] * isc);
+  for (int i = t; i < cnt; i += kThr) psum[eb + i] = (float)((double)acc[i] * isc);
 }
 
 void tp_fb_set_prof(uint64_t* p) {
@@ -2358,12 +2363,40 @@ tpf_pack_grads_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict
 // ---------------------------------------------------------------------------
 struct TpGeom {
   int nbk, shift;
-  int64_t T, N;
+  int lts;      // log2 occurrences per tile
+  int64_t T, N;  // tiles, entry stride (T * kTile)
 };
 
-static TpGeom tp_geom(int64_t n, int bits) {
+// Occurrences per tile of the FLAT layout, 2^lts in [1024, 8192]: the largest that still
+// gives >= 128 tiles, so a small minibatch (B = 10,000 x 39: 48 tiles of 8192, i.e. 48
+// busy CUs, each tile's LDS insert chain ~15 us) spreads over the chip; large ones keep
+// 8192 (fewer tiles = fewer tile entries of the hot keys). Measured at B = 10,000
+// (profiles/r5_adaptive_tiles.log): 8192 -> 260.6 M ex/s, 4096 -> 304.3, 2048 -> 309.3,
+// 1024 -> 196.8 (the hot keys' extra entries). Entry ids keep the kTile stride whatever
+// the tile holds. The compact "tp" layout always uses 8192.
+// PSAMD_TILE_LTS=10..13 pins it (A/B), PSAMD_TILE_MIN the tile target.
+static int tp_flat_lts(int64_t n) {
+  // (read per call: host-side geometry only, a few calls per launch list build)
+  const char* pe = getenv("PSAMD_TILE_LTS");
+  const int pin = pe ? atoi(pe) : 0;
+  const char* te = getenv("PSAMD_TILE_MIN");
+  int tmin = te ? atoi(te) : 128;
+  tmin = tmin < 1 ? 1 : tmin > tp::kMaxT / 2 ? tp::kMaxT / 2 : tmin;
+  int lts = 13;
+  if (pin >= 10 && pin <= 13) {
+    lts = pin;
+  } else {
+    while (lts > 10 && ((n + (1ll << lts) - 1) >> lts) < tmin) --lts;
+  }
+  while (lts < 13 && ((n + (1ll << lts) - 1) >> lts) > tp::kMaxT) ++lts;  // (LDS tile runs)
+  return lts;
+}
+
+static TpGeom tp_geom(int64_t n, int bits, bool flat = false) {
   TpGeom g;
-  g.T = (n + tp::kTile - 1) / tp::kTile;
+  g.lts = flat ? tp_flat_lts(n) : 13;
+  static_assert(tp::kTile == 8192, "tile entry stride 2^13");
+  g.T = (n + (1ll << g.lts) - 1) >> g.lts;
   g.N = g.T * tp::kTile;
   // <= 1024 occurrences per bucket on average: even if every key is distinct a PAIR of
   // buckets (the flat layout's unit) stays under the kDH-key hash (at 1280, nearly
@@ -2380,6 +2413,15 @@ static TpGeom tp_geom(int64_t n, int bits) {
 }
 
 int64_t tploc_stride(int64_t n) { return tp_geom(n, 31).N; }
+// flat layout: the entry stride of an n-key minibatch, and a bound over every minibatch of
+// <= n keys (a workspace sized for n must take smaller minibatches, which may use more,
+// smaller tiles): <= kMaxT tiles, and tiles of 1024 at the least
+int64_t tpf_stride(int64_t n) { return tp_geom(n, 31, true).N; }
+int64_t tpf_stride_max(int64_t n) {
+  const int64_t t = std::min<int64_t>(tp::kMaxT, (n + 1023) / 1024);
+  return std::max<int64_t>(t, (n + tp::kTile - 1) / tp::kTile) * tp::kTile;
+}
+int tpf_tile_log2(int64_t n) { return tp_geom(n, 31, true).lts; }
 int tploc_buckets(int64_t n, int bits) { return tp_geom(n, bits).nbk; }
 int tploc_tile() { return tp::kTile; }
 
@@ -2418,10 +2460,10 @@ void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t te
   static const char* quot_env = getenv("PSAMD_TP_QUOT");  // "1": A/B the encoding at <= 31 bits
   if (m.bits > 31 || (quot_env && quot_env[0] == '1'))
     tp_tile_kernel<true><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
-                                                             dcnt, rep, err);
+                                                             dcnt, rep, err, g.lts);
   else
     tp_tile_kernel<false><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
-                                                              dcnt, rep, err);
+                                                              dcnt, rep, err, g.lts);
   PSAMD_HIP_CHECK(hipGetLastError());
   // buckets in pairs of fine buckets: one round of workgroups (the pair's key bit above
   // a <= 30-bit suffix keeps the LDS hash's empty word unreachable)
@@ -2445,9 +2487,9 @@ int tpf_groups(int64_t n, int bits) { return tpf_groups_of(tp_geom(n, bits)); }
 int tpf_key_region() { return tpf::kUC; }
 int tpf_entry_region() { return tpf::kEC; }
 
-size_t tpf_temp_bytes(int64_t n, int bits) {
-  const TpGeom g = tp_geom(n, bits);
-  return al16((size_t)g.N * 4) + al16((size_t)g.T * (g.nbk + 1) * 2);  // tkeys, toff
+size_t tpf_temp_bytes(int64_t n, int bits) {  // (any minibatch of <= n keys: tpf_stride_max)
+  const int64_t N = tpf_stride_max(n);
+  return al16((size_t)N * 4) + al16((size_t)(N / tp::kTile) * (tp::kMaxBk + 1) * 2);  // tkeys, toff
 }
 
 // uniqf >= groups * kUC, ent_pos / ent_j >= groups * kEC, cnt >= groups * 4 (the host
@@ -2458,17 +2500,17 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
   if (n <= 0) return;
   if (!tploc_supported(n, m.bits)) throw std::runtime_error("localize_tpf: unsupported size");
   if (temp_bytes < tpf_temp_bytes(n, m.bits)) throw std::runtime_error("localize_tpf: temp");
-  const TpGeom g = tp_geom(n, m.bits);
+  const TpGeom g = tp_geom(n, m.bits, true);
   char* p = (char*)temp;
   auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
   uint32_t* tkeys = (uint32_t*)take((size_t)g.N * 4);
   uint16_t* toff = (uint16_t*)take((size_t)g.T * (g.nbk + 1) * 2);
   if (m.bits > 31)
     tp_tile_kernel<true><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
-                                                             dcnt, rep, err);
+                                                             dcnt, rep, err, g.lts);
   else
     tp_tile_kernel<false><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
-                                                              dcnt, rep, err);
+                                                              dcnt, rep, err, g.lts);
   PSAMD_HIP_CHECK(hipGetLastError());
   const bool pair = g.nbk >= 2 && g.shift <= 30;
   tpf_bucket_kernel<<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
@@ -2603,30 +2645,44 @@ void tp_fwd_bwd(const uint16_t* rep, const int32_t* dcnt, const int32_t* ent_uid
   if (n <= 0) return;
   if (!tp_fwd_bwd_supported(width) || n != B * (int64_t)width)
     throw std::runtime_error("tp_fwd_bwd: unsupported width or n != B * width");
-  const TpGeom g = tp_geom(n, 31);
+  const bool flat = ent_uid == nullptr;  // w_local in tile-entry order (tpf)
+  const TpGeom g = tp_geom(n, 31, flat);
   if (hist && (nbins <= 0 || nbins > kFbMaxBins))
     throw std::runtime_error("tp_fwd_bwd: 1..2048 AUC bins (LDS histogram)");
   const size_t lds = 0;
   const int per = (width + kFbLanes - 1) / kFbLanes;
-  const bool flat = ent_uid == nullptr;  // w_local in tile-entry order (tpf)
   if (flat && w_cap < g.N) throw std::runtime_error("tp_fwd_bwd: flat w_ent < tile stride");
+  // rows of one tile fit one register pass (<= 128 rows: 2^lts / width + 2): NP = 1
+  const bool one = ((1 << g.lts) / width + 2) <= tp::kThr / kFbLanes;
 #define PSAMD_FB(PER, NP)                                                                     \
   if (flat)                                                                                   \
     tp_fwd_bwd_kernel<PER, NP, true><<<(unsigned)g.T, tp::kThr, lds, st>>>(                  \
         rep, dcnt, ent_uid, n, width, vals, w_local, w_cap, labels, B, loss_type, coef_out,   \
-        metrics, hist, nbins, acc_stripes, hist_stripes, psum);                               \
+        metrics, hist, nbins, acc_stripes, hist_stripes, psum, g.lts);                        \
   else                                                                                        \
     tp_fwd_bwd_kernel<PER, NP, false><<<(unsigned)g.T, tp::kThr, lds, st>>>(                 \
         rep, dcnt, ent_uid, n, width, vals, w_local, w_cap, labels, B, loss_type, coef_out,   \
-        metrics, hist, nbins, acc_stripes, hist_stripes, psum)
-  switch (per) {  // NP = kFbNP[PER] row passes in registers (tp_fwd_bwd_supported)
-    case 2: PSAMD_FB(2, 8); break;
-    case 3: PSAMD_FB(3, 4); break;
-    case 4: PSAMD_FB(4, 3); break;
-    case 5: PSAMD_FB(5, 2); break;
-    case 6: PSAMD_FB(6, 2); break;
-    case 7: PSAMD_FB(7, 2); break;
-    default: PSAMD_FB(8, 2); break;
+        metrics, hist, nbins, acc_stripes, hist_stripes, psum, g.lts)
+  if (one && flat) {
+    switch (per) {
+      case 2: PSAMD_FB(2, 1); break;
+      case 3: PSAMD_FB(3, 1); break;
+      case 4: PSAMD_FB(4, 1); break;
+      case 5: PSAMD_FB(5, 1); break;
+      case 6: PSAMD_FB(6, 1); break;
+      case 7: PSAMD_FB(7, 1); break;
+      default: PSAMD_FB(8, 1); break;
+    }
+  } else {
+    switch (per) {  // NP = kFbNP[PER] row passes in registers (tp_fwd_bwd_supported)
+      case 2: PSAMD_FB(2, 8); break;
+      case 3: PSAMD_FB(3, 4); break;
+      case 4: PSAMD_FB(4, 3); break;
+      case 5: PSAMD_FB(5, 2); break;
+      case 6: PSAMD_FB(6, 2); break;
+      case 7: PSAMD_FB(7, 2); break;
+      default: PSAMD_FB(8, 2); break;
+    }
   }
 #undef PSAMD_FB
   PSAMD_HIP_CHECK(hipGetLastError());
@@ -2644,19 +2700,19 @@ void tp_fwd_bwd_csr(const uint16_t* rep, const int32_t* dcnt, const int32_t* ent
                     const int32_t* segid, const int32_t* n_ent, float* grad, int64_t grad_cap,
                     bool reduce, hipStream_t st) {
   if (n <= 0) return;
-  const TpGeom g = tp_geom(n, 31);
+  const bool flat = ent_uid == nullptr;
+  const TpGeom g = tp_geom(n, 31, flat);
   if (hist && (nbins <= 0 || nbins > kFbMaxBins))
     throw std::runtime_error("tp_fwd_bwd_csr: 1..2048 AUC bins (LDS histogram)");
-  const bool flat = ent_uid == nullptr;
   if (flat && w_cap < g.N) throw std::runtime_error("tp_fwd_bwd_csr: flat w_ent < tile stride");
   if (flat)
     tp_fwd_bwd_csr_kernel<true><<<(unsigned)g.T, tp::kThr, 0, st>>>(
         rep, dcnt, ent_uid, n, row_ptr, rows, vals, w_local, w_cap, labels, B, loss_type,
-        coef_out, metrics, hist, nbins, acc_stripes, hist_stripes, psum);
+        coef_out, metrics, hist, nbins, acc_stripes, hist_stripes, psum, g.lts);
   else
     tp_fwd_bwd_csr_kernel<false><<<(unsigned)g.T, tp::kThr, 0, st>>>(
         rep, dcnt, ent_uid, n, row_ptr, rows, vals, w_local, w_cap, labels, B, loss_type,
-        coef_out, metrics, hist, nbins, acc_stripes, hist_stripes, psum);
+        coef_out, metrics, hist, nbins, acc_stripes, hist_stripes, psum, g.lts);
   PSAMD_HIP_CHECK(hipGetLastError());
   if (!reduce) return;
   tp_seg_reduce_kernel<<<grid_for(g.N, 256, 2048), 256, 0, st>>>(pos_s, segid, g.N, n_ent, psum,

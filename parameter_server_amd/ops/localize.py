@@ -132,7 +132,9 @@ class Localizer:
     the backward accumulates per tile in LDS and scans the entry CSC (``TileInfo``).
     ``mode="tpf"`` (1 GPU, same limits as "tp"): the tile stage of "tp", then bucket
     workgroups that write fixed per-bucket regions (``FlatLoc``): no look-back across
-    buckets, no sort, no CSC; only the fused 1-GPU step consumes it (``tpf_step``).
+    buckets, no sort, no CSC; only the fused 1-GPU step consumes it (``tpf_step``). Its
+    tiles hold 1024..8192 occurrences (``tpf_tile_log2``: >= ~128 tiles when the
+    minibatch allows, so B = 10,000 fills the chip); tile entry ids keep the 8192 stride.
     (Measured and removed in round 3: a sort-free global scratch hash, a partition
     with per-bucket presence bitmaps and a 4096-key tile dedup + radix sort; none beat
     "tp" on the Criteo-shaped batch, profiles/r2_localize_tp_vs_sort.log.)"""
@@ -161,7 +163,8 @@ class Localizer:
         self.mode = mode if (self.gpu and (self.bits <= 32 or mode in ("tp", "tpf"))) else "sort"
         if self.gpu and self.mode == "tpf":
             H = hipops()
-            N = H.tploc_stride(n)
+            # (smaller minibatches may use more, smaller tiles: the bound over n' <= n)
+            N = H.tpf_stride_max(n)
             g = H.tpf_groups(n, self.bits)  # the largest geometry (fewer keys: fewer groups)
             kr, er = H.tpf_key_region(), H.tpf_entry_region()
             self.ptemp = torch.empty(H.tpf_temp_bytes(n, self.bits), dtype=torch.uint8, device=dev)

@@ -57,10 +57,18 @@ def _overflow_batch(B: int = 2048, width: int = 16, bits: int = 20):
     return keys, labels
 
 
+def _tile(n: int) -> int:
+    """Occurrences per tile of the flat layout for an n-key minibatch (tp_flat_lts)."""
+    from parameter_server_amd.ops.native import hipops
+
+    return 1 << hipops().tpf_tile_log2(n)
+
+
 def test_flat_localizer_overflow_fails_loudly(monkeypatch):
     """A localisation overflow (entries dropped from the flat regions) must not train
     silently: progress() and check_ok() raise."""
     monkeypatch.setenv("PSAMD_FLAT", "1")
+    monkeypatch.setenv("PSAMD_TILE_LTS", "13")  # (the batch is built for 8192-key tiles)
     keys, labels = _overflow_batch()
     B = labels.numel()
     cfg = SparseLRConfig(num_features=1 << 20, minibatch=B, max_nnz_per_example=16,
@@ -99,25 +107,33 @@ def _flat_entry_keys(f, n):
     return ent_key, cnt
 
 
-@pytest.mark.parametrize("case", ["criteo", "criteo_small", "uniform", "skewed"])
-def test_tpf_localisation_covers_every_occurrence(case):
+@pytest.mark.parametrize("case", ["criteo", "criteo_small", "uniform", "skewed", "small_in_big"])
+def test_tpf_localisation_covers_every_occurrence(case, monkeypatch):
     """Every occurrence's tile entry maps (ent_pos / ent_j / uniqf) to its own mixed key,
     every distinct key appears once, and each tile's entry count is its distinct-key
-    count."""
+    count (tiles of 2^tpf_tile_log2(n) occurrences: 8192 at the driver's B, 1024 for
+    criteo_small, 2048 for the 400 k uniform keys)."""
     if case == "criteo":
         B, bits = 65536, 30
         keys, _ = criteo_batch(B, seed=11, row0=0, num_features=10 ** 9, device=DEV)
     elif case == "criteo_small":
         B, bits = 3000, 30
         keys, _ = criteo_batch(B, seed=12, row0=0, num_features=10 ** 9, device=DEV)
+    elif case == "small_in_big":  # a workspace sized for the driver's B takes B = 10,000,
+        B, bits = 10000, 30       # whose 2048-key tiles are 191 (vs 313 tiles of 8192)
+        keys, _ = criteo_batch(B, seed=13, row0=0, num_features=10 ** 9, device=DEV)
     elif case == "uniform":  # nearly all distinct: the densest buckets
         bits = 34
         keys = torch.randint(0, 1 << 34, (400_000,), device=DEV)
     else:
         bits = 20
+        monkeypatch.setenv("PSAMD_TILE_LTS", "13")  # (built for 8192-key tiles)
         keys, _ = _skewed_batch(0, bits)
     n = keys.numel()
-    lz = Localizer(n, bits, DEV, mode="tpf")
+    ts = _tile(n)
+    assert ts == {"criteo": 8192, "criteo_small": 1024, "uniform": 2048, "skewed": 8192,
+                  "small_in_big": 2048}[case]
+    lz = Localizer(65536 * 39 if case == "small_in_big" else n, bits, DEV, mode="tpf")
     assert lz.mode == "tpf"
     f = lz(keys)
     torch.cuda.synchronize()
@@ -125,16 +141,16 @@ def test_tpf_localisation_covers_every_occurrence(case):
     mk = mix(keys, bits).cpu()
     ent_key, cnt = _flat_entry_keys(f, n)
     rep = f.rep[:n].cpu().to(torch.int64) & 0xFFFF
-    tile = torch.arange(n) // TP_TILE
+    tile = torch.arange(n) // ts
     eid = (tile * TP_TILE + rep).tolist()
     got = torch.tensor([ent_key[e] for e in eid])
     assert torch.equal(got, mk)
     uq = f.unique_keys()
     assert uq.numel() == torch.unique(mk).numel() == torch.unique(uq).numel()
-    T = (n + TP_TILE - 1) // TP_TILE
+    T = (n + ts - 1) // ts
     dc = f.dcnt[:T].cpu()
     for t in range(T):
-        assert int(dc[t]) == torch.unique(mk[t * TP_TILE:(t + 1) * TP_TILE]).numel()
+        assert int(dc[t]) == torch.unique(mk[t * ts:(t + 1) * ts]).numel()
     if case == "skewed":  # the overflowing pair ran as two fine units
         assert cnt[0].tolist() == [1500, 3000, 1500, 3000]
 
@@ -190,6 +206,8 @@ def _table_by_raw_key(tr, allk):
 @pytest.mark.parametrize("mode,algo,B,cap", [
     ("tpf", "ftrl", 16384, 1 << 22), ("tpf", "adagrad", 16384, 1 << 22),
     ("tpf", "sgd", 16384, 1 << 22), ("tp", "ftrl", 16384, 1 << 22),
+    # the reference operating point (online_l1lr.conf minibatch: 10,000): 2048-key tiles
+    ("tpf", "ftrl", 10000, 1 << 22),
     # the driver's shape: B = 65,536 on the 2^31-slot (64 GiB) table of 10^9 features
     ("tpf", "ftrl", 65536, 1 << 31)])
 def test_fused_1gpu_step_matches_fp32_reference(mode, algo, B, cap, monkeypatch):
@@ -229,6 +247,7 @@ def test_flat_step_overflow_units_match_reference(monkeypatch):
     """Minibatches whose first bucket pair overflows (two fine units per workgroup, the
     tpf_unit_light path) train like the fp32 reference."""
     monkeypatch.setenv("PSAMD_FLAT", "1")
+    monkeypatch.setenv("PSAMD_TILE_LTS", "13")  # (the batches are built for 8192-key tiles)
     bits = 20
     batches = [_skewed_batch(s, bits) for s in range(3)]
     B = batches[0][1].numel()
@@ -328,7 +347,7 @@ def test_prep_plan_generates_and_localises_like_the_ops():
         n = B * 39
         ek, _ = _flat_entry_keys(f, n)
         rep = f.rep[:n].cpu().to(torch.int64) & 0xFFFF
-        eid = ((torch.arange(n) // TP_TILE) * TP_TILE + rep).tolist()
+        eid = ((torch.arange(n) // _tile(n)) * TP_TILE + rep).tolist()
         assert torch.equal(torch.tensor([ek[e] for e in eid]), mix(k2, tr.bits).cpu())
         assert torch.equal(f.cnt[0::2], ref.cnt[0::2])  # distinct keys per unit
         assert torch.equal(f.unique_keys().sort().values, ref.unique_keys().sort().values)
