@@ -48,6 +48,7 @@ void ipc_close(void*, int64_t);
 void tp_gather(const uint16_t*, const int32_t*, int64_t, int32_t*, hipStream_t);
 bool tp_fwd_bwd_supported(int);
 void tp_fb_set_prof(uint64_t*);
+void tp_tile_set_prof(uint64_t*);
 void tp_fwd_bwd(const uint16_t*, const int32_t*, const int32_t*, int64_t, int, const float*,
                 const float*, int64_t, const float*, int64_t, int, float*, double*, uint32_t*, int,
                 int, int, float*, const int32_t*, const int32_t*, const int32_t*, float*, int64_t,
@@ -1062,6 +1063,15 @@ PYBIND11_MODULE(_hipops, m) {
       p = reinterpret_cast<uint64_t*>(prof->data_ptr<int64_t>());
     }
     psamd::tp_fb_set_prof(p);
+  });
+  // phase marks of the tile kernel (tuning aid): 16 int64 per tile, or None to disable
+  m.def("tp_tile_set_prof", [](optional<Tensor> prof) {
+    uint64_t* p = nullptr;
+    if (prof) {
+      chk(*prof, at::kLong, "prof");
+      p = reinterpret_cast<uint64_t*>(prof->data_ptr<int64_t>());
+    }
+    psamd::tp_tile_set_prof(p);
   });
   m.def("tp_fwd_bwd", [](Tensor rep, Tensor dcnt, optional<Tensor> ent_uid, int64_t n, int width,
                          optional<Tensor> vals, Tensor w_local, Tensor labels, int64_t B,

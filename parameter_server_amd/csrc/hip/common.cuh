@@ -58,6 +58,17 @@ __host__ __device__ __forceinline__ uint64_t mix_key(uint64_t x, const KeyMix& m
   return x;
 }
 
+// mix_key for bits <= 32 in 32-bit arithmetic (the same value: products mod 2^bits only
+// see the factors' low bits)
+__host__ __device__ __forceinline__ uint32_t mix_key32(uint64_t x64, const KeyMix& m) {
+  const uint32_t mask = (uint32_t)m.mask;
+  uint32_t x = ((uint32_t)x64 * (uint32_t)m.a) & mask;
+  x ^= x >> m.s;
+  x = (x * (uint32_t)m.b) & mask;
+  x ^= x >> m.s;
+  return x;
+}
+
 __host__ __device__ __forceinline__ uint64_t unmix_key(uint64_t x, const KeyMix& m) {
   x ^= x >> m.s;
   x = (x * m.bi) & m.mask;

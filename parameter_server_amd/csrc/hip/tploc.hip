@@ -122,7 +122,13 @@ __device__ __forceinline__ uint64_t tp_match_any(uint32_t v, int nbits, uint64_t
 }
 
 // ------------------------------------------------------------------------ tile
-// kQuot = false (<= 31-bit keys): the slot keeps the key itself, home tp_hash(key);
+// Phase marks of the tile kernel (a tuning aid, benchmarks/prof_tile_phases.py): null
+// unless tp_tile_set_prof() installed a buffer of 16 u64 per workgroup.
+__device__ uint64_t* g_tile_prof = nullptr;
+#define TILE_MARK(k)                                                            \
+  if (tpp && threadIdx.x == 0) tpp[(int64_t)blockIdx.x * 16 + (k)] = clock64()
+
+// kQuot = false (<= 31-bit keys): the slot keeps the key itself, home = low kHB key bits;
 // kQuot = true (32..34 bits): quotient encoding, home = low kHB key bits.
 // (8 waves per SIMD = 2 workgroups per CU: <= 64 VGPRs. The quotient variant compiled to
 // 66 without the bound, i.e. 1 workgroup per CU: localise 90 vs 80 us.)
@@ -137,28 +143,46 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
   __shared__ uint32_t cnt[kMaxBk];  // per-bucket counts, then offsets
   __shared__ uint32_t lds[kThr / 64 + 1];
   const int t = threadIdx.x;
+  uint64_t* const tpp = g_tile_prof;
+  if (tpp && t == 0) tpp[(int64_t)blockIdx.x * 16 + 8] = __builtin_amdgcn_s_memrealtime();
+  TILE_MARK(0);
   for (int i = t; i < kHash; i += kThr) hk[i] = kEmpty;
   for (int d = t; d < nbk; d += kThr) cnt[d] = 0;
   __syncthreads();
+  TILE_MARK(1);
   // occurrences [base, base + lim) (2^lts per tile, tp_geom); entry ids keep the
   // kTile stride (tkeys, dcnt, the consumers' tile * kTile + entry)
   const int64_t base = (int64_t)blockIdx.x << lts;
   const int lim = (int)(n - base < (1 << lts) ? n - base : (1 << lts));
-  uint64_t kr[kIt];
-  uint16_t sl[kIt];
+  uint64_t kr[kIt];  // raw keys, then the mixed keys
+  uint16_t sl[kIt];  // hash slot of every key
+  uint32_t rr[kIt];  // a key this lane inserted (one lane per distinct key): rank in its
+                     // bucket, then its entry position; kEmpty otherwise
+  uint32_t won = 0;  // bit j: this lane inserted key j
   bool bad = false;
 #pragma unroll
   for (int j = 0; j < kIt; ++j) {  // all loads in flight before the LDS insert chain
     const int o = j * kThr + t;
     kr[j] = o < lim ? raw[base + o] : 0ull;
   }
+  if (tpp) {  // (profiling only: every load landed, workgroup-wide)
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    TILE_MARK(2);
+  }
+  // (<= 31 bits: the mix in 32-bit arithmetic -- the low bits of a product depend only
+  // on the low bits of its factors, so it equals mix_key -- and the mixed key's own low
+  // bits as the home slot: ~12 fewer VALU per key than the 64-bit mix + tp_hash. Measured
+  // and not kept: two keys per probe loop, both probes' LDS reads and CAS in flight
+  // together: insert phase 19.1 -> 22.2 k cycles per workgroup, benchmarks/prof_tile_phases.py)
 #pragma unroll
   for (int j = 0; j < kIt; ++j) {
     sl[j] = 0;
     if (j * kThr + t < lim) {
-      const uint64_t k = mix_key(kr[j], m);
+      const uint64_t k = kQuot ? mix_key(kr[j], m) : (uint64_t)mix_key32(kr[j], m);
+      kr[j] = k;
       const uint32_t q = kQuot ? (uint32_t)(k >> kHB) << kDispB : (uint32_t)k;
-      uint32_t h = (kQuot ? (uint32_t)k : tp_hash((uint32_t)k)) & (kHash - 1);
+      uint32_t h = (uint32_t)k & (kHash - 1);
       uint32_t d = 0;
       for (; d < kMaxDisp; ++d) {  // slot h holds key k iff it holds q | d (q: kQuot = false)
         const uint32_t want = kQuot ? q | d : q;
@@ -166,7 +190,11 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
         if (cur == want) break;
         if (cur == kEmpty) {
           const uint32_t prev = atomicCAS(&hk[h], kEmpty, want);
-          if (prev == kEmpty || prev == want) break;
+          if (prev == kEmpty) {
+            won |= 1u << j;
+            break;
+          }
+          if (prev == want) break;
         }
         h = (h + 1) & (kHash - 1);
       }
@@ -174,22 +202,16 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
       sl[j] = (uint16_t)h;
     }
   }
+  // counting sort of the distinct keys by bucket (top key bits), by the lanes that
+  // inserted them: their keys are in registers, so no pass over the (mostly empty) hash
+  // (the earlier form scanned all 16 K slots twice: ~3 K of them hold a key). The tile
+  // keys leave as their low `shift` bits (the bucket holds the rest).
+#pragma unroll
+  for (int j = 0; j < kIt; ++j)
+    rr[j] = (won >> j) & 1u ? atomicAdd(&cnt[kr[j] >> shift], 1u) : kEmpty;
   if (bad && err) atomicOr(err, 2);
   __syncthreads();
-  // counting sort of the distinct keys by bucket (top key bits); thread t owns slots
-  // q*kThr + t. The tile keys leave as their low `shift` bits (the bucket holds the rest).
-  constexpr int kPer = kHash / kThr;  // 16
-  auto decode = [](uint32_t v, int s) -> uint64_t {
-    if (!kQuot) return v;
-    return ((uint64_t)(v >> kDispB) << kHB) | ((uint32_t)(s - (int)(v & kMaxDisp)) & (kHash - 1));
-  };
-  uint32_t rr[kPer];
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const uint32_t v = hk[q * kThr + t];
-    rr[q] = v != kEmpty ? atomicAdd(&cnt[decode(v, q * kThr + t) >> shift], 1u) : kEmpty;
-  }
-  __syncthreads();
+  TILE_MARK(3);
   // exclusive scan of the bucket counts (nbk <= kMaxBk: 2 per thread)
   constexpr int kDP = kMaxBk / kThr;
   uint32_t c[kDP], s = 0;
@@ -216,27 +238,36 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
     dcnt[blockIdx.x] = (int32_t)D;
   }
   __syncthreads();
+  TILE_MARK(4);
+  // each inserted key -> its entry position: tile key out, and its hash slot now holds
+  // the position (no lane reads hk between the two barriers)
   uint32_t* tk = tkeys + (int64_t)blockIdx.x * kTile;
   const uint64_t smask = (1ull << shift) - 1;
 #pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    if (rr[q] != kEmpty) {
-      const uint64_t k = decode(hk[q * kThr + t], q * kThr + t);
-      const uint32_t pos = cnt[k >> shift] + rr[q];
-      tk[pos] = (uint32_t)(k & smask);
-      rr[q] = pos;
+  for (int j = 0; j < kIt; ++j) {
+    if (rr[j] != kEmpty) {
+      const uint32_t pos = cnt[kr[j] >> shift] + rr[j];
+      tk[pos] = (uint32_t)(kr[j] & smask);
+      hk[sl[j]] = pos;
     }
   }
-  __syncthreads();  // every hk read is done: reuse it as slot -> entry position
-#pragma unroll
-  for (int q = 0; q < kPer; ++q)
-    if (rr[q] != kEmpty) hk[q * kThr + t] = rr[q];
   __syncthreads();
+  TILE_MARK(5);
 #pragma unroll
   for (int j = 0; j < kIt; ++j) {
     const int o = j * kThr + t;
     if (o < lim) rep[base + o] = (uint16_t)hk[sl[j]];
   }
+  if (tpp && t == 0) {
+    TILE_MARK(6);
+    tpp[(int64_t)blockIdx.x * 16 + 9] = __builtin_amdgcn_s_memrealtime();
+    tpp[(int64_t)blockIdx.x * 16 + 10] = __smid();
+  }
+}
+#undef TILE_MARK
+
+void tp_tile_set_prof(uint64_t* p) {
+  PSAMD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_tile_prof), &p, sizeof(p)));
 }
 
 // ---------------------------------------------------------------------- bucket
