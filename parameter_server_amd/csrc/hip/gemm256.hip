@@ -1012,13 +1012,186 @@ gemm_nt256r_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __re
 #undef G256R_WAIT_NEXT
 #undef G256R_VMCNT
 
+// ---------------------------------------------------------------------------
+// Four-wave variant (variant 5): 256 threads = 4 waves as 2 (M) x 2 (N), ONE wave per
+// SIMD, each owning a 128 x 128 output = 8 x 8 v_mfma_f32_16x16x32_bf16 tiles (256
+// accumulator registers per lane: the unified VGPR/AGPR file of a 1-wave-per-SIMD
+// kernel). Per K-step of 64 a wave reads 8 A + 8 B fragments per sub-step of 32 (32
+// ds_read_b128 for 128 MFMAs: a third fewer LDS bytes per FLOP than the 8-wave 128 x 64
+// layout, 128 KiB of fragment reads + 64 KiB of DMA per CU per K-step against 2048
+// MFMA cycles per SIMD). Same LDS image / DMA / swizzle as gemm_nt256_kernel (two 64 KiB
+// buffers). A single wave per SIMD hides its own latency by software pipelining:
+//   K-step kt: DMA of kt+1 (into the buffer K-step kt-1 used: every wave retired its
+//   reads of it before barrier kt-1); sub-step 1 fragments of kt in flight during the
+//   64 MFMAs of sub-step 0; the first 32 MFMAs of sub-step 1; then vmcnt(0) (this wave's
+//   DMA of kt+1 landed) + barrier kt, and sub-step 0 fragments of kt+1 in flight during
+//   the last 32 MFMAs of kt.
+// Measured (profiles/r5_gemm_w4.log): correct but the slowest variant, 1000 vs 1306
+// (variant 4) vs 1438 (hipBLASLt) TFLOP/s on 16384 x 1024 x 4992: as compiled, the
+// 256 VGPRs hold the fragments plus every hoisted DMA / LDS address and the loop moves
+// 72 registers between the AGPR and VGPR halves per K-step. Kept for A/B.
+namespace g256w {
+constexpr int TH = 256, NW = 4;
+}
+
+// LDS-DMA of one 256 x 64 operand tile by 4 waves: wave-instruction wi = q*4 + wave
+// fills rows wi*8 .. wi*8+7 (bytes [wi*1024, +1024)), q = 0..7
+__device__ __forceinline__ void g256w_stage(const __bf16* __restrict__ p, int64_t ld, int rows,
+                                            int r0, int k0, char* dst, int wave, int lane) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int wi = q * g256w::NW + wave;
+    const int row = wi * 8 + (lane >> 3);
+    const int c = g256_swz(row, lane & 7);
+    int gr = r0 + row;
+    gr = gr < rows ? gr : rows - 1;
+    const __bf16* src = p + (int64_t)gr * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(dst + wi * 1024),
+                                     16, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(g256w::TH, 1)
+gemm_nt256w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B,
+                    int64_t ldb, int M, int N, int K, const float* __restrict__ bias, int relu,
+                    __bf16* __restrict__ C, int64_t ldc, float* __restrict__ Cf, int64_t ldcf,
+                    int tiles_n) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];  // 128 KiB
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int id = g256_xcd(blockIdx.x, gridDim.x);
+  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = K / BK;
+  auto rd_a = [&](const char* buf, int ks, int i) {
+    const int c = ks * 4 + (lane >> 4), r = wr * 128 + i * 16 + (lane & 15);
+    return *reinterpret_cast<const bf16x8*>(buf + r * 128 + g256_swz(r, c) * 16);
+  };
+  auto rd_b = [&](const char* buf, int ks, int j) {
+    const int c = ks * 4 + (lane >> 4), r = wc * 128 + j * 16 + (lane & 15);
+    return *reinterpret_cast<const bf16x8*>(buf + TILE_BYTES + r * 128 + g256_swz(r, c) * 16);
+  };
+  g256w_stage(A, lda, M, m0, 0, smem, wave, lane);
+  g256w_stage(B, ldb, N, n0, 0, smem + TILE_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a0[i] = rd_a(smem, 0, i);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b0[j] = rd_b(smem, 0, j);
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* cur = smem + (kt & 1) * BUF_BYTES;
+    char* nxt = smem + ((kt + 1) & 1) * BUF_BYTES;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      g256w_stage(A, lda, M, m0, (kt + 1) * BK, nxt, wave, lane);
+      g256w_stage(B, ldb, N, n0, (kt + 1) * BK, nxt + TILE_BYTES, wave, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a1[i] = rd_a(cur, 1, i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b1[j] = rd_b(cur, 1, j);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of kt+1 landed
+      __builtin_amdgcn_s_barrier();                     // ... every wave's
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a0[i] = rd_a(nxt, 0, i);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b0[j] = rd_b(nxt, 0, j);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // epilogue: C[m][n], m = m0 + wr*128 + i*16 + 4*(lane>>4) + r, n = n0 + wc*128 + j*16 + (lane&15)
+  if (C && !Cf && (ldc & 7) == 0 && m0 + BM <= M && n0 + BN <= N) {
+    __bf16* st = reinterpret_cast<__bf16*>(smem);  // [256][256] bf16 = 128 KiB
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int nl = wc * 128 + j * 16 + (lane & 15);
+      const float bv = bias ? bias[n0 + nl] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ml = wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+          float v = acc[i][j][r] + bv;
+          if (relu) v = v > 0.f ? v : 0.f;
+          st[ml * BN + nl] = (__bf16)v;
+        }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int q = 0; q < BM * BN / 8 / g256w::TH; ++q) {  // 32 chunks of 8 bf16 per thread
+      const int ch = q * g256w::TH + t;
+      const int ml = ch >> 5, nc = (ch & 31) * 8;
+      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + ml) * ldc + n0 + nc) =
+          *reinterpret_cast<const uint4*>(st + ml * BN + nc);
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = n0 + wc * 128 + j * 16 + (lane & 15);
+    if (n >= N) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= M) continue;
+        float v = acc[i][j][r] + bv;
+        if (relu) v = v > 0.f ? v : 0.f;
+        if (C) C[(int64_t)m * ldc + n] = (__bf16)v;
+        if (Cf) Cf[(int64_t)m * ldcf + n] = v;
+      }
+    }
+  }
+}
+
 void gemm_nt256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
                 const float* bias, bool relu, __bf16* C, int64_t ldc, float* Cf, int64_t ldcf,
                 int variant, hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   if (K % g256::BK != 0 || lda % 8 || ldb % 8) throw std::runtime_error("gemm_nt256: K % 64, ld % 8");
   const int tiles_m = (M + g256::BM - 1) / g256::BM, tiles_n = (N + g256::BN - 1) / g256::BN;
-  if (variant == 4)
+  if (variant == 5)
+    gemm_nt256w4_kernel<<<tiles_m * tiles_n, g256w::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
+                                                                 relu ? 1 : 0, C, ldc, Cf, ldcf,
+                                                                 tiles_n);
+  else if (variant == 4)
     gemm_nt256r_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
                                                                relu ? 1 : 0, C, ldc, Cf, ldcf,
                                                                tiles_n);
