@@ -84,28 +84,34 @@ def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes, pipelined, 
     assert max(abs(merged[k] - ref[k]) for k in ref) < tol
 
 
-@pytest.mark.parametrize("exchange,consistency", [("padded", "ssp:4"), ("exact", "ssp:4"),
-                                                  ("padded", "ssp:1"), ("padded", "asp")])
-def test_bench_two_rank_rehearsal_json(tmp_path, exchange, consistency):
+@pytest.mark.parametrize("exchange,consistency,world", [
+    ("padded", "ssp:4", 2), ("exact", "ssp:4", 2), ("padded", "ssp:1", 2), ("padded", "asp", 2),
+    ("padded", "ssp:4", 4)])
+def test_bench_two_rank_rehearsal_json(tmp_path, exchange, consistency, world):
     """bench.py's multi-GPU path (padded: graph-replayed compute segments around the
-    exchanges, post / tail owner applies; exact: pipelined count-sized exchange) under
-    torchrun, 2 ranks on one GPU over gloo (every rank must issue its collectives in
-    the same order, or the run hangs); checks the one-line JSON contract."""
+    exchanges, post / tail owner applies, ssp:4 the merged one-collective exchange;
+    exact: pipelined count-sized exchange) under torchrun, 2 (or 4) ranks on one GPU
+    over gloo (every rank must issue its collectives in the same order, or the run
+    hangs); checks the one-line JSON contract."""
     import json
     import subprocess
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, PSAMD_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus",
-           "2", "--steps", "4", "--warmup", "2", "--minibatch", "4096", "--num-features", "1e8",
-           "--exchange", exchange, "--consistency", consistency]
+           str(world), "--steps", "4", "--warmup", "2", "--minibatch", "4096", "--num-features",
+           "1e8", "--exchange", exchange, "--consistency", consistency]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["steps"] == 4 and out["config"]["global_batch"] == 8192
+    assert out["n_gpus"] == world and out["steps"] == 4
+    assert out["config"]["global_batch"] == 4096 * world
+    if exchange == "padded" and consistency == "ssp:4":  # exchange_merge "auto": one collective
+        assert out["config"]["ssp_apply"] == "merged"
+        assert out["config"]["collectives_per_step"] == 1
     assert out["value"] > 0 and 0.3 < out["train"]["loss"] < 1.0
     assert out["config"]["hip_graph"] == (exchange == "padded")
 
