@@ -120,8 +120,12 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             locs[b] = fplans[b]()
             return
         if mode["capture"]:
+            # buffer b reads cursor word (b // nprep) % 2 of its stream and writes the
+            # other: the stream's two buffers alternate, so each replay advances the cursor
+            kk = (b // nprep) % 2
             criteo_batch(B, seed=seed, row0=sidx * B, num_features=N, device=device, keys=k,
-                         labels=lab, row0_dev=ctr[sidx], row_scale=nprep * B, advance=True)
+                         labels=lab, row0_dev=ctr[sidx][kk:kk + 1], row_scale=nprep * B,
+                         row0_out=ctr[sidx][1 - kk:2 - kk])
         else:
             criteo_batch(B, seed=seed, row0=(hctr[sidx] * nprep + sidx) * B, num_features=N,
                          device=device, keys=k, labels=lab)
@@ -386,8 +390,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
 
     iterate.release = release
     gp = []
-    for s_ in range(nprep):  # the replays continue the eager row counts on the device
-        ctr[s_][0].fill_(hctr[s_])
+    seed_cursors(ctr, hctr, state["t"], nprep, NB)  # the replays continue the eager rows
     mode["capture"] = True
     for b in range(NB):  # t0 % NB == 0: buffer b <-> minibatch t0 + b
         g = torch.cuda.CUDAGraph()
@@ -501,6 +504,15 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     return iterate, True
 
 
+def seed_cursors(ctr, hctr, t, nprep, NB):
+    """Before the first graph replay: each preparation stream's row cursor (host count of
+    its eager preparations) into the word its first replayed buffer reads (prep of
+    buffer b reads word (b // nprep) % 2; iteration t prepares buffer (t + nprep) % NB)."""
+    for s in range(nprep):
+        b = next((t + nprep + i) % NB for i in range(NB) if (t + nprep + i) % NB % nprep == s)
+        ctr[s][(b // nprep) % 2].fill_(hctr[s])
+
+
 def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=None):
     """The multi-GPU pipeline on the merged exchange (one all-to-all per step,
     ``SparseLRTrainer.mx_exchange`` / ``mx_worker``, parallel/consistency.MergedSchedule).
@@ -541,8 +553,12 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         sidx = b % nprep
         k, lab = bufs[b]
         if mode["capture"]:
+            # buffer b reads cursor word (b // nprep) % 2 of its stream and writes the
+            # other: the stream's two buffers alternate, so each replay advances the cursor
+            kk = (b // nprep) % 2
             criteo_batch(B, seed=seed, row0=sidx * B, num_features=N, device=device, keys=k,
-                         labels=lab, row0_dev=ctr[sidx], row_scale=nprep * B, advance=True)
+                         labels=lab, row0_dev=ctr[sidx][kk:kk + 1], row_scale=nprep * B,
+                         row0_out=ctr[sidx][1 - kk:2 - kk])
         else:
             criteo_batch(B, seed=seed, row0=(hctr[sidx] * nprep + sidx) * B, num_features=N,
                          device=device, keys=k, labels=lab)
@@ -676,8 +692,7 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         return f
 
     gp = []
-    for s_ in range(nprep):
-        ctr[s_][0].fill_(hctr[s_])
+    seed_cursors(ctr, hctr, state["t"], nprep, NB)
     mode["capture"] = True
     for b in range(NB):
         gp.append(graph_of(lambda b=b: prep(b)))

@@ -184,8 +184,8 @@ void linear_bwd(const int32_t*, const int32_t*, int64_t, const int32_t*, int, co
 void auc_from_hist(uint32_t*, int, int, double*, int64_t*, hipStream_t);
 void csr_rows(const int64_t*, int64_t, int32_t*, hipStream_t);
 void criteo_set_tables(const uint32_t*, const float*);
-void criteo_gen(uint64_t, int64_t, int64_t*, int64_t, int64_t, uint64_t, float, uint64_t*,
-                float*, bool, hipStream_t);
+void criteo_gen(uint64_t, int64_t, const int64_t*, int64_t, int64_t, uint64_t, float, uint64_t*,
+                float*, int64_t*, hipStream_t);
 void add_i64(int64_t*, int64_t, hipStream_t);
 // filters.hip
 void cm_insert(uint32_t*, uint64_t, int, uint32_t, const uint64_t*, const uint8_t*, int64_t,
@@ -653,7 +653,7 @@ Launch make_criteo_gen(uint64_t seed, int64_t row0, int64_t row_step, int64_t B,
   auto cursor = std::make_shared<int64_t>(row0);
   return [=, keep = std::vector<Tensor>{keys, labels}](hipStream_t st) {
     psamd::criteo_gen(seed, *cursor, nullptr, 1, B, num_features, (float)alpha,
-                      ptr<uint64_t>(keys), ptr<float>(labels), false, st);
+                      ptr<uint64_t>(keys), ptr<float>(labels), nullptr, st);
     *cursor += row_step;
   };
 }
@@ -1979,10 +1979,14 @@ PYBIND11_MODULE(_hipops, m) {
   });
   m.def("criteo_gen", [](uint64_t seed, int64_t row0, int64_t B, uint64_t num_features,
                          double alpha, Tensor keys, Tensor labels, optional<Tensor> row0_dev,
-                         int64_t row_scale, bool advance) {
-    // advance: row0_dev = [cursor, done-count]; the kernel bumps the cursor by one at its
-    // end (a captured graph's next replay generates the next rows, no separate add)
-    if (advance) check(row0_dev && row0_dev->numel() >= 2, "advance needs row0_dev [2]");
+                         int64_t row_scale, optional<Tensor> row0_out) {
+    // row0_out: the kernel writes row0_dev + 1 there (the cursor of the next launch, which
+    // reads row0_out and writes row0_dev: a captured graph pair alternating the two
+    // words generates fresh rows on every replay, no separate add)
+    int64_t* op = optr<int64_t>(row0_out, at::kLong, "row0_out");
+    if (op) check(row0_dev.has_value() && row0_dev->defined() && row0_out->numel() >= 1 &&
+                      row0_dev->numel() >= 1 && op != row0_dev->data_ptr<int64_t>(),
+                  "row0_out: a word of its own next to row0_dev");
     chk(keys, at::kLong, "keys");
     chk(labels, at::kFloat, "labels");
     check(keys.numel() >= B * 39 && labels.numel() >= B, "criteo_gen buffers too small");
@@ -1990,10 +1994,10 @@ PYBIND11_MODULE(_hipops, m) {
     check(num_features > 0, "num_features > 0");
     psamd::criteo_gen(seed, row0, optr<int64_t>(row0_dev, at::kLong, "row0_dev"), row_scale, B,
                       num_features, (float)alpha, ptr<uint64_t>(keys), ptr<float>(labels),
-                      advance, cur_stream());
+                      op, cur_stream());
   }, py::arg("seed"), py::arg("row0"), py::arg("B"), py::arg("num_features"), py::arg("alpha"),
      py::arg("keys"), py::arg("labels"), py::arg("row0_dev") = py::none(),
-     py::arg("row_scale") = 1, py::arg("advance") = false);
+     py::arg("row_scale") = 1, py::arg("row0_out") = py::none());
 
   // ---------------- filters ----------------
   m.def("cm_insert", [](Tensor table, int k, int vmax, Tensor keys, optional<Tensor> counts,

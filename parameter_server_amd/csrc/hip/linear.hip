@@ -296,19 +296,28 @@ __device__ __forceinline__ void gen_slot_range(int w, int& j0, int& j1) {
 }
 template <bool kWide>
 __global__ void __launch_bounds__(kGenThreads)
-criteo_gen_kernel(uint64_t seed, int64_t row0, int64_t* __restrict__ row0_dev,
+criteo_gen_kernel(uint64_t seed, int64_t row0, const int64_t* __restrict__ row0_dev,
                   int64_t row_scale, int64_t B, uint64_t num_features, uint64_t nf_m,
                   float alpha, uint64_t* __restrict__ keys, float* __restrict__ labels,
-                  int advance) {
+                  int64_t* __restrict__ row0_out) {
   __shared__ uint64_t sk[kGenRows * 39];
   __shared__ float sp[kGenRows * 39];
   __shared__ float s_cm1[26];
   __shared__ uint32_t s_seed[40];  // per-slot streams + the label stream
   // (an L2-coherent vector load, not a scalar-cache load: the counter is advanced on the
   // device between graph replays)
-  if (row0_dev)
-    row0 += __hip_atomic_load(row0_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * row_scale;
+  int64_t cursor = 0;
+  if (row0_dev) {
+    cursor = __hip_atomic_load(row0_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    row0 += cursor * row_scale;
+  }
   const int t = threadIdx.x, lane = t & 63;
+  // row0_out: the cursor of the NEXT launch, in a second word (ping-pong: the launch
+  // after this one reads row0_out and writes this launch's row0_dev), written by one
+  // lane: no block reads what another writes within a launch, no atomics. (A completion
+  // counter on one address, bumped by each of the 1024 blocks, serialised them: 21 -> 55
+  // us per launch in the pipelined 8-peer step, profiles/r5_gen_cursor.log.)
+  if (row0_out && blockIdx.x == 0 && t == 0) row0_out[0] = cursor + 1;
   const int g = __builtin_amdgcn_readfirstlane(t >> 6);
   int j0, j1;
   gen_slot_range(g, j0, j1);
@@ -349,21 +358,6 @@ criteo_gen_kernel(uint64_t seed, int64_t row0, int64_t* __restrict__ row0_dev,
       labels[r] = gen_u01(gen_row_bits(gr, s_seed[39])) < p ? 1.f : -1.f;
     }
     __syncthreads();
-  }
-  if (advance) {
-    // the row cursor advances on the device (a graph replay generates the next rows):
-    // the last block to finish bumps row0_dev[0] -- every block read it at its start
-    // (the value fed all of its rows) before counting itself done in row0_dev[1], so no
-    // fence is needed (a device-scope __threadfence per block wrote back the XCD's L2:
-    // 11 -> 57 us per launch). Vector atomics only.
-    __syncthreads();
-    if (t == 0) {
-      const unsigned long long d = atomicAdd(reinterpret_cast<unsigned long long*>(row0_dev + 1), 1ull);
-      if (d == (unsigned long long)gridDim.x - 1) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(row0_dev), 1ull);
-        atomicExch(reinterpret_cast<unsigned long long*>(row0_dev + 1), 0ull);
-      }
-    }
   }
 }
 
@@ -413,20 +407,20 @@ void criteo_set_tables(const uint32_t* cards26, const float* gauss256) {
   PSAMD_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_gauss), gauss256, 256 * sizeof(float)));
 }
 
-void criteo_gen(uint64_t seed, int64_t row0, int64_t* row0_dev, int64_t row_scale,
+void criteo_gen(uint64_t seed, int64_t row0, const int64_t* row0_dev, int64_t row_scale,
                 int64_t B, uint64_t num_features, float alpha, uint64_t* keys, float* labels,
-                bool advance, hipStream_t st) {
+                int64_t* row0_out, hipStream_t st) {
   const int64_t blocks = (B + kGenRows - 1) / kGenRows;
   const uint64_t nf_m = ~0ull / num_features;
   const unsigned grid = (unsigned)(blocks < 65535 ? blocks : 65535);
   if (num_features <= (1ull << 32))
     criteo_gen_kernel<false><<<grid, kGenThreads, 0, st>>>(seed, row0, row0_dev, row_scale, B,
                                                            num_features, nf_m, alpha, keys, labels,
-                                                           advance && row0_dev ? 1 : 0);
+                                                           row0_dev ? row0_out : nullptr);
   else
     criteo_gen_kernel<true><<<grid, kGenThreads, 0, st>>>(seed, row0, row0_dev, row_scale, B,
                                                           num_features, nf_m, alpha, keys, labels,
-                                                          advance && row0_dev ? 1 : 0);
+                                                          row0_dev ? row0_out : nullptr);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

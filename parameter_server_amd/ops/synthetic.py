@@ -55,19 +55,20 @@ def _set_cards(device, cards):
 
 def criteo_batch(B: int, *, seed: int, row0: int, num_features: int, alpha: float = 1.1,
                  cards=CRITEO_1TB_CARDS, device="cpu", keys=None, labels=None, row0_dev=None,
-                 row_scale: int = 1, advance: bool = False):
+                 row_scale: int = 1, row0_out=None):
     """Returns (keys int64 [B*39] row-major, labels float32 [B] in {-1,+1}).
     GPU only: ``row0_dev`` (int64[1] device) adds ``row0_dev * row_scale`` to ``row0``
     at kernel time, so a captured graph generates fresh rows on every replay;
-    ``advance`` (row0_dev = int64[2]: cursor, done-count) also bumps the cursor by one
-    when the kernel finishes (no separate increment launch per replay)."""
+    ``row0_out`` (int64[1] device, another word) receives ``row0_dev + 1``: two captured
+    launches alternating the two words (A -> B, then B -> A) advance the cursor with no
+    separate increment launch per replay."""
     device = torch.device(device)
     keys = torch.empty(B * NUM_SLOTS, dtype=torch.int64, device=device) if keys is None else keys
     labels = torch.empty(B, dtype=torch.float32, device=device) if labels is None else labels
     if device.type == "cuda":
         _set_cards(device, cards)
         hipops().criteo_gen(seed & ((1 << 64) - 1), row0, B, num_features, alpha, keys, labels,
-                            row0_dev, row_scale, advance)
+                            row0_dev, row_scale, row0_out)
         return keys, labels
     k, l = _criteo_cpu(B, seed, row0, num_features, alpha, cards)
     keys.copy_(k)

@@ -309,16 +309,35 @@ def test_criteo_gen_gpu_matches_cpu():
 
 @pytest.mark.gpu
 def test_criteo_gen_advances_its_device_cursor():
-    """criteo_batch(advance=True): the kernel's last block bumps row0_dev[0], so two
-    launches (or graph replays) generate rows row0 + k * scale for k = c, c + 1."""
+    """criteo_batch(row0_dev=A, row0_out=B): the kernel generates rows row0 + A * scale
+    and writes A + 1 into B; alternating the two words (A -> B, B -> A: a captured graph
+    pair) generates rows row0 + k * scale for k = c, c + 1, c + 2, ..."""
     from parameter_server_amd.ops.synthetic import criteo_batch
 
     dev = torch.device("cuda")
     B = 3000
-    ctr = torch.tensor([5, 0], dtype=torch.int64, device=dev)
-    for k in (5, 6, 7):
+    ctr = torch.tensor([5, -1], dtype=torch.int64, device=dev)
+    for i, k in enumerate((5, 6, 7)):
+        a = i % 2
         keys, labels = criteo_batch(B, seed=3, row0=11, num_features=10 ** 9, device=dev,
-                                    row0_dev=ctr, row_scale=B, advance=True)
+                                    row0_dev=ctr[a:a + 1], row_scale=B,
+                                    row0_out=ctr[1 - a:2 - a])
         rk, rl = criteo_batch(B, seed=3, row0=11 + k * B, num_features=10 ** 9, device=dev)
         assert torch.equal(keys, rk) and torch.equal(labels, rl)
-    assert ctr.tolist() == [8, 0]
+    assert ctr.tolist() == [7, 8]
+    # the same through graph replays: two captured launches alternating the words
+    ctr = torch.tensor([2, -1], dtype=torch.int64, device=dev)
+    kb = [torch.empty(B * 39, dtype=torch.int64, device=dev) for _ in range(2)]
+    lb = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(2)]
+    gs = []
+    for a in range(2):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            criteo_batch(B, seed=3, row0=11, num_features=10 ** 9, device=dev, keys=kb[a],
+                         labels=lb[a], row0_dev=ctr[a:a + 1], row_scale=B,
+                         row0_out=ctr[1 - a:2 - a])
+        gs.append(g)
+    for i, k in enumerate((2, 3, 4, 5)):
+        gs[i % 2].replay()
+        rk, rl = criteo_batch(B, seed=3, row0=11 + k * B, num_features=10 ** 9, device=dev)
+        assert torch.equal(kb[i % 2], rk) and torch.equal(lb[i % 2], rl)
