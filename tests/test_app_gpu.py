@@ -255,3 +255,76 @@ def test_app_two_ranks_uneven_files(tmp_path):
     assert r[0]["steps"] == 6 and r[1]["steps"] == 3 and r[1]["idle"] == 3
     assert r[0]["progress"]["loss"] < 0.69
     assert sorted(os.listdir(model.parent)) == ["m_S0", "m_S1"]
+
+
+def _darlin_files(tmp_path):
+    """3 SPARSE_BINARY files of grouped rows and a reference batch_l1lr-style conf."""
+    from parameter_server_amd.data.slot_reader import SlotData
+    from parameter_server_amd.data.synthetic import sparse_classification, write_text
+
+    sd = sparse_classification(1800, groups=(1, 2, 3), keys_per_group=300,
+                               nnz_per_row=(1, 3, 5), seed=3)
+    data = tmp_path / "data"
+    data.mkdir()
+    n = sd.rows // 3
+    for p in range(3):
+        a, b = p * n, (p + 1) * n
+        part = SlotData(labels=sd.labels[a:b], groups={
+            g: (off[a:b + 1] - off[a], k[off[a]:off[b]], None)
+            for g, (off, k, v) in sd.groups.items()})
+        write_text(part, str(data / f"part-{p}"), "SPARSE_BINARY")
+    model = tmp_path / "model" / "m"
+    conf = tmp_path / "batch.conf"
+    conf.write_text(f"""linear_method {{
+training_data {{ format: TEXT text: SPARSE_BINARY file: "{data}/part.*" }}
+model_output {{ format: TEXT file: "{model}" }}
+loss {{ type: LOGIT }}
+penalty {{ type: L1 lambda: 1 }}
+learning_rate {{ type: CONSTANT alpha: 1 }}
+darlin {{ max_pass_of_data: 6 epsilon: 1e-9 feature_block_ratio: 2
+  random_feature_block_order: false max_block_delay: 1 }}
+}}""")
+    return data, model, conf
+
+
+def _app_darlin(tmp_path, device):
+    """The app's darlin path (DarlinConfig.from_lm, files read by SlotReader, text model
+    <file>_S0) against DarlinTrainer built directly on the same files and settings."""
+    from parameter_server_amd.app.gpu import run_darlin
+    from parameter_server_amd.data.slot_reader import SlotReader
+    from parameter_server_amd.models.darlin import DarlinConfig, DarlinTrainer
+    from parameter_server_amd.parallel.comm import LocalComm
+    from parameter_server_amd.utils.config import load_app_config
+
+    data, model, conf = _darlin_files(tmp_path)
+    lm = load_app_config(str(conf)).linear_method
+    dev = torch.device(device)
+    res = run_darlin(lm, LocalComm(dev), dev, _flags(device=device))
+    assert res["examples"] == 1800 and res["passes"] == 6
+    assert os.path.basename(res["model"]) == "m_S0"
+    cfg = DarlinConfig.from_lm(lm)
+    assert (cfg.l1, cfg.eta, cfg.tau, cfg.max_pass, cfg.block_ratio, cfg.random_order) == \
+        (1.0, 1.0, 1, 6, 2.0, False)
+    full = SlotReader(sorted(str(p) for p in data.iterdir()), "SPARSE_BINARY").read()
+    ref = DarlinTrainer(full, cfg, device=dev).train()
+    objs = [p.objective for p in res["trainer"].progress]
+    np.testing.assert_allclose(objs, [p.objective for p in ref], rtol=1e-6)
+    assert objs[-1] < objs[0]
+    keys, w = res["trainer"].model()
+    want = {int(k): float(v) for k, v in zip(keys, w) if v != 0}
+    saved = _read_models(model.parent)
+    assert set(saved) == set(want) and len(want) > 10
+    for k in want:
+        assert abs(saved[k] - want[k]) < 1e-4 * max(1.0, abs(want[k]))
+    return objs
+
+
+def test_app_darlin_cpu_matches_trainer(tmp_path):
+    _app_darlin(tmp_path, "cpu")
+
+
+@pytest.mark.gpu
+def test_app_darlin_gpu_matches_trainer_and_cpu(tmp_path):
+    g = _app_darlin(tmp_path / "g", "cuda")
+    c = _app_darlin(tmp_path / "c", "cpu")
+    np.testing.assert_allclose(g, c, rtol=1e-5)
