@@ -1054,6 +1054,11 @@ def main():
             run = one_step
     watch.beat("pre-timing")
     tr.progress(reset=True)
+    # two more untimed iterations after the metrics reset (its device reads idle the GPU
+    # for a few ms): the timed region then starts right behind busy work, as in steady
+    # state (PSAMD_PRE_TIMING_ITERS, default 2; the train block's loss / AUC include them)
+    for _ in range(int(os.environ.get("PSAMD_PRE_TIMING_ITERS", "2"))):
+        run()
 
     comm.barrier()
     if gpu:
