@@ -1019,9 +1019,10 @@ def main():
         scope.enter_context(torch.cuda.stream(torch.cuda.Stream(device, priority=int(mprio))))
     watch.beat("warmup")
     if gpu and args.pipeline and (G == 1 or tr.padded):
-        # 3 preparation streams. 1 GPU at the driver's 20 timed steps: 0.0849-0.0865 ms
-        # with 3 vs 0.0852-0.0903 with 2 (8 runs each, one box; over 300 steps 2 are
-        # ~1 % faster, 0.0813 vs 0.0823: profiles/r5_prep_streams.log). Rounds 3-4 kept 2
+        # 3 preparation streams. 1 GPU at the driver's 20 timed steps: 0.0849-0.0869 ms
+        # (mean 0.0860) with 3 vs 0.0852-0.0903 (mean 0.0873) with 2, 6 runs each on the
+        # same boxes; over 300 steps 2 are ~1 % faster, 0.0813 vs 0.0823
+        # (profiles/r5_prep_streams.log). Rounds 3-4 kept 2
         # on older kernels (0.109-0.110 vs 0.112-0.116 over 300 steps, r3_s2_graph_ab.log)
         nprep = args.prep_streams or 3
         args.prep_streams = nprep
