@@ -1626,6 +1626,59 @@ __device__ __forceinline__ uint32_t tpf_unit_light(
   return E < room ? E : room;
 }
 
+// Rank order of a unit's distinct keys by counting them into 256 bins of their top bits
+// (the mixed keys are uniform over the unit's range [0, 2^kbits)) and comparing each key
+// with the few others of its bin: O(D) work and 5 barriers instead of tp_bk_ranksort's
+// O(D^2) scan. In: dl[0..D) (key u32 << 32 | count | slot). Out: dl[0..D) in key order.
+// Scratch: sc = the dead hash region (>= kDH + 514 words: bin keys, counts, starts).
+__device__ __forceinline__ void tpf_rank_binned(uint64_t* dl, uint32_t* sc, uint32_t D, int kbits,
+                                                uint32_t* lds) {
+  using namespace tp;
+  constexpr int kPerT = kDH / kBkThr;  // <= 4 keys per thread
+  const int t = threadIdx.x;
+  const int bsh = kbits > 8 ? kbits - 8 : 0;
+  uint32_t* bkey = sc;              // [kDH] keys grouped by bin
+  uint32_t* bcnt = sc + kDH;        // [256]
+  uint32_t* bst = bcnt + 256;       // [256] bin starts
+  if (t < 256) bcnt[t] = 0u;
+  __syncthreads();
+  uint64_t e[kPerT];
+  uint32_t bs[kPerT];  // bin << 16 | slot in bin
+#pragma unroll
+  for (int q = 0; q < kPerT; ++q) {
+    const uint32_t i = q * kBkThr + t;
+    e[q] = i < D ? dl[i] : 0ull;
+    if (i < D) {
+      const uint32_t bin = ((uint32_t)(e[q] >> 32) >> bsh) & 255u;
+      bs[q] = bin << 16 | atomicAdd(&bcnt[bin], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t tot;
+  const uint32_t st = tp_block_scan<kBkThr>(t < 256 ? bcnt[t] : 0u, lds, &tot);
+  if (t < 256) bst[t] = st;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kPerT; ++q)
+    if (q * kBkThr + t < D) bkey[bst[bs[q] >> 16] + (bs[q] & 0xffffu)] = (uint32_t)(e[q] >> 32);
+  __syncthreads();
+  uint32_t rk[kPerT];
+#pragma unroll
+  for (int q = 0; q < kPerT; ++q) {
+    if (q * kBkThr + t >= D) continue;
+    const uint32_t bin = bs[q] >> 16, a = bst[bin], n = bcnt[bin];
+    const uint32_t k = (uint32_t)(e[q] >> 32);
+    uint32_t r = a;
+    for (uint32_t m = 0; m < n; ++m) r += bkey[a + m] < k;  // distinct keys
+    rk[q] = r;
+  }
+  __syncthreads();  // (every dl entry is in registers: dl takes the ordered list)
+#pragma unroll
+  for (int q = 0; q < kPerT; ++q)
+    if (q * kBkThr + t < D) dl[rk[q]] = e[q];
+  __syncthreads();
+}
+
 // One workgroup per pair of fine buckets (pair = 0: per fine bucket), the tp_bucket
 // geometry and build; the occupied hash slots in compaction order are the keys' indices.
 __global__ void __launch_bounds__(tp::kBkThr, 8)
@@ -1658,7 +1711,10 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
     // counts, or the dead compaction list once it is sorted into hs)
     uint32_t* jmap = hcnt;
     const uint64_t* lst = dl;
-    if (sorted) {
+    if (sorted && D > 64) {  // binned rank order into dl; the dead hash takes slot -> j
+      tpf_rank_binned(dl, hkey, D, pair ? shift + 1 : shift, lds);
+      jmap = hkey;
+    } else if (sorted) {
       tp_bk_ranksort(dl, hs, D);
       __syncthreads();
       jmap = reinterpret_cast<uint32_t*>(dl);

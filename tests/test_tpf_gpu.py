@@ -107,6 +107,44 @@ def _flat_entry_keys(f, n):
     return ent_key, cnt
 
 
+@pytest.mark.parametrize("case", ["criteo", "uniform", "few"])
+def test_tpf_sorted_units_are_key_ordered(case):
+    """sorted_keys=True (the multi-GPU exchange rows): every unit's keys strictly
+    increase (binned rank order for units of > 64 keys, the O(D^2) scan below), the
+    entry map still gives every occurrence its own key, and the key set equals the
+    unsorted localisation's."""
+    if case == "criteo":
+        keys, _ = criteo_batch(65536, seed=21, row0=0, num_features=10 ** 9, device=DEV)
+        bits = 30
+    elif case == "uniform":  # ~2000 distinct keys per unit: the densest bins
+        keys, bits = torch.randint(0, 1 << 34, (400_000,), device=DEV), 34
+    else:  # <= 64 keys in the one unit: the O(D^2) path
+        keys, bits = torch.randint(0, 1 << 30, (60,), device=DEV), 30
+    n = keys.numel()
+    fs = Localizer(n, bits, DEV, mode="tpf", sorted_keys=True)(keys)
+    torch.cuda.synchronize()
+    assert int(fs.err.item()) == 0
+    H = hipops()
+    G, kr = H.tpf_groups(n, bits), H.tpf_key_region()
+    cnt = fs.cnt[:4 * G].view(G, 4).cpu()
+    uq = fs.uniqf[:G * kr].view(G, 2, kr // 2).cpu()
+    big = 0
+    for b in range(G):
+        for s in range(2):
+            D = int(cnt[b, 2 * s])
+            u = uq[b, s, :D]
+            assert D < 2 or bool((u[1:] > u[:-1]).all()), (b, s)
+            big += D > 64
+    assert (big > 0) == (case != "few")
+    mk = mix(keys, bits).cpu()
+    ent_key, _ = _flat_entry_keys(fs, n)
+    rep = fs.rep[:n].cpu().to(torch.int64) & 0xFFFF
+    eid = ((torch.arange(n) // _tile(n)) * TP_TILE + rep).tolist()
+    assert torch.equal(torch.tensor([ent_key[e] for e in eid]), mk)
+    fu = Localizer(n, bits, DEV, mode="tpf")(keys)
+    assert torch.equal(fs.unique_keys().sort().values, fu.unique_keys().sort().values)
+
+
 @pytest.mark.parametrize("case", ["criteo", "criteo_small", "uniform", "skewed", "small_in_big"])
 def test_tpf_localisation_covers_every_occurrence(case, monkeypatch):
     """Every occurrence's tile entry maps (ent_pos / ent_j / uniqf) to its own mixed key,
