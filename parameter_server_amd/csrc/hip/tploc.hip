@@ -1520,7 +1520,7 @@ namespace tpf {
 constexpr int kUnitK = tp::kDH;  // keys of one unit (the bucket hash)
 constexpr int kUC = 2 * kUnitK;  // key region of a bucket workgroup (two units)
 constexpr int kEC = 8192;        // entry region of a bucket workgroup
-constexpr int kThr = 256;        // tpf_step workgroup (auc_hist_block runs in block 0)
+constexpr int kThr = 256;        // tpf_step workgroup (auc_hist_block: an extra last one)
 constexpr uint32_t kNoSlot = 0xffffffffu;
 }  // namespace tpf
 
@@ -1823,7 +1823,12 @@ tpf_step_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __r
   __shared__ float wj[kUnitK];       // pulled weights of a unit's keys
   __shared__ uint32_t smax;
   const int t = threadIdx.x, b = blockIdx.x, lane = t & 63;
-  if (do_upd && hist && b == 0) auc_hist_block(hist, nbins, hist_stripes, metrics, step_counter);
+  // the step's AUC epilogue in an extra last workgroup of its own (tpf_step launches
+  // groups + 1): in unit 0's workgroup its 8 dependent stripe loads delayed that unit
+  if (do_upd && hist && b == (int)gridDim.x - 1) {
+    auc_hist_block(hist, nbins, hist_stripes, metrics, step_counter);
+    return;
+  }
   double dnnz = 0, wsum = 0, dsum = 0;
   if (do_upd) {
     const int32_t* c = cntA + (int64_t)b * 4;
@@ -1991,7 +1996,10 @@ tpf_step2_kernel(int do_upd, const int32_t* __restrict__ cntA, const int32_t* __
   __shared__ uint32_t smax[2];
   float* wj = reinterpret_cast<float*>(acc);
   const int t = threadIdx.x, b = blockIdx.x, lane = t & 63;
-  if (do_upd && hist && b == 0) auc_hist_block(hist, nbins, hist_stripes, metrics, step_counter);
+  if (do_upd && hist && b == (int)gridDim.x - 1) {  // (an extra workgroup, as tpf_step_kernel)
+    auc_hist_block(hist, nbins, hist_stripes, metrics, step_counter);
+    return;
+  }
   // per-unit counts (clamped to the regions: a corrupted count never leaves them)
   int DA0 = 0, DA1 = 0, EA0 = 0, EA = 0, DB0 = 0, DB1 = 0, EB0 = 0, EB = 0;
   if (do_upd) {
@@ -2358,9 +2366,10 @@ tpf_pack_grads_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict
   __shared__ long long acc[kUnitK];
   __shared__ uint32_t smax;
   const int b = blockIdx.x, p = b / per, t = threadIdx.x, lane = t & 63;
-  if (b == 0) {
+  if ((hist || ovf_host) && b == (int)gridDim.x - 1) {  // extra workgroup (the launcher adds it)
     if (ovf_host && t == 0) ovf_host[0] = ovf[0];
     if (hist) auc_hist_block(hist, 2048, hist_stripes, metrics, step_counter);
+    return;
   }
   const int base = tpf_row_base(cnt, b, per, red);
   const int32_t* c = cnt + 4 * b;
@@ -2641,7 +2650,9 @@ void tpf_pack_grads(int64_t n, int bits, int G, const int32_t* cnt, const int32_
                     int hist_stripes, double* metrics, int64_t* step_counter, const int32_t* ovf,
                     int32_t* ovf_host, hipStream_t st) {
   const int per = tpf_per_owner(n, bits, G);
-  tpf_pack_grads_kernel<<<(unsigned)tpf_groups(n, bits), tpf::kThr, 0, st>>>(
+  // (+1 workgroup: the AUC epilogue / overflow publication, off unit 0's critical path)
+  tpf_pack_grads_kernel<<<(unsigned)tpf_groups(n, bits) + ((hist || ovf_host) ? 1u : 0u),
+                          tpf::kThr, 0, st>>>(
       cnt, ent_pos, ent_j, per, C, kw, H, psum, p_cap, send, ff ? 1 : 0, gstage, hist,
       hist_stripes, metrics, step_counter, ovf, ovf_host);
   PSAMD_HIP_CHECK(hipGetLastError());
@@ -2670,13 +2681,13 @@ void tpf_step(int64_t n, int bits, const int32_t* cntA, const int32_t* posA, con
   // update + pull launch, profiles/r4_tpf_step_probe.log; kept for A/B and its test)
   const char* v2_env = getenv("PSAMD_TPF_STEP2");
   if (!(v2_env && v2_env[0] == '1'))
-    tpf_step_kernel<<<(unsigned)groups, tpf::kThr, 0, st>>>(
+    tpf_step_kernel<<<(unsigned)groups + (cntA && hist ? 1u : 0u), tpf::kThr, 0, st>>>(
         cntA != nullptr, cntA, posA, jA, slotA, psum, p_cap, cntB != nullptr, cntB, uniqB, posB,
         jB, slotB, w_ent, w_cap, (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg,
         init_type, init_v, init_s, seed, err, inserted, p, stats, acc_stripes,
         cntA ? hist : nullptr, nbins, hist_stripes, metrics, step_counter);
   else
-    tpf_step2_kernel<<<(unsigned)groups, tpf::kThr, 0, st>>>(
+    tpf_step2_kernel<<<(unsigned)groups + (cntA && hist ? 1u : 0u), tpf::kThr, 0, st>>>(
         cntA != nullptr, cntA, posA, jA, slotA, psum, p_cap, cntB != nullptr, cntB, uniqB, posB,
         jB, slotB, w_ent, w_cap, (Slot*)slots, (uint64_t)(cap - 1), home_base, home_m, 64 - lg,
         init_type, init_v, init_s, seed, err, inserted, p, stats, acc_stripes,

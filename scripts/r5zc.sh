@@ -1,0 +1,11 @@
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R=$PWD; O=$R/gpurun_out/r5zc; mkdir -p $O
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+j() { python -c "import sys,json; d=json.loads([l for l in open('$1') if l.startswith('{')][-1]); print('$2', round(d['value']/1e6,1), round(d['ms_per_step'],4), round(d.get('host_issue_ms_per_step') or 0,4), round(d['train']['auc'],4))"; }
+timeout -k 10 800 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_tpf_gpu.py tests/test_bench_pipeline_gpu.py tests/test_dist_gpu.py tests/test_train_quality_gpu.py > $O/pytest.log 2>&1; rc=$?; tail -2 $O/pytest.log; [ $rc = 0 ] || exit $rc
+for i in 1 2 3; do timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/b1_$i.log 2>&1 || exit 3; j $O/b1_$i.log "1gpu-20"; done
+timeout -k 10 200 python bench.py --steps 300 --warmup 10 > $O/b300.log 2>&1 || exit 3; j $O/b300.log "1gpu-300"
+for i in 1 2; do timeout -k 10 200 python bench.py --steps 200 --warmup 10 --emulate-peers 8 --emulate-backend nccl > $O/e8_$i.log 2>&1 || exit 3; j $O/e8_$i.log "e8"; done
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/seq -o run -- python $R/bench.py --pipeline 0 --steps 60 --warmup 10 > $O/seq.log 2>&1 || exit 6
+python $R/scripts/kbusy_db.py $O/seq/run_results.db tp_fwd_bwd 20 60
