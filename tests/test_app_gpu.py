@@ -265,7 +265,7 @@ def _darlin_files(tmp_path):
     sd = sparse_classification(1800, groups=(1, 2, 3), keys_per_group=300,
                                nnz_per_row=(1, 3, 5), seed=3)
     data = tmp_path / "data"
-    data.mkdir()
+    data.mkdir(parents=True)
     n = sd.rows // 3
     for p in range(3):
         a, b = p * n, (p + 1) * n
