@@ -116,6 +116,48 @@ bcd_grad_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row
 // NaN with nan_filtered = the reference server's NaN mark, darlin.h:228-231, which
 // tells the replicas of a sharded server to drop the column from their active set).
 // Violation is max-reduced as the bit pattern of a non-negative double.
+// the coordinate step of one active column k (bcd_update_kernel, and the fused update at
+// the end of a small narrow block's row-order gradient)
+// (wk / dk: w[k] / delta[k], loaded by the caller)
+__device__ __forceinline__ double bcd_update_col(int64_t k, double gj, double uj, double wk,
+                                                 double dk, double* __restrict__ w,
+                                                 double* __restrict__ delta,
+                                                 uint8_t* __restrict__ active, double eta,
+                                                 double lambda, double delta_max, double kkt_thr,
+                                                 int nan_filtered, double& vmax) {
+  double d = 0;
+  const double g = gj, u = uj / eta + 1e-10;
+  const double gp = g + lambda, gn = g - lambda;
+  double vio = 0;
+  bool filtered = false;
+  if (wk == 0) {
+    if (gp < 0) vio = -gp;
+    else if (gn > 0) vio = gn;
+    else if (gp > kkt_thr && gn < -kkt_thr) filtered = true;
+  }
+  if (filtered) {
+    active[k] = 0;
+    if (nan_filtered) d = __builtin_nan("");
+  } else {
+    vmax = fmax(vmax, vio);
+    d = -wk;
+    if (gp <= u * wk) d = -gp / u;
+    else if (gn >= u * wk) d = -gn / u;
+    d = fmin(dk, fmax(-dk, d));
+    delta[k] = fmin(delta_max, 2 * fabs(d) + .1);
+    w[k] = wk + d;
+  }
+  return d;
+}
+
+// wave max -> one atomic per wave (violation as the bits of a non-negative double)
+__device__ __forceinline__ void bcd_vio_max(double vmax, unsigned long long* vio_bits) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, off, 64));
+  if ((threadIdx.x & 63) == 0 && vmax > 0)
+    atomicMax(vio_bits, (unsigned long long)__double_as_longlong(vmax));
+}
+
 __global__ void __launch_bounds__(256)
 bcd_update_kernel(int64_t c0, int64_t ncols, double* __restrict__ G, double* __restrict__ U,
                   double* __restrict__ w, double* __restrict__ delta,
@@ -145,38 +187,11 @@ bcd_update_kernel(int64_t c0, int64_t ncols, double* __restrict__ G, double* __r
       G[j] = 0;
       U[j] = 0;
     }
-    if (active[k]) {
-      const double g = gj, u = uj / eta + 1e-10;
-      const double gp = g + lambda, gn = g - lambda;
-      const double wk = w[k];
-      double vio = 0;
-      bool filtered = false;
-      if (wk == 0) {
-        if (gp < 0) vio = -gp;
-        else if (gn > 0) vio = gn;
-        else if (gp > kkt_thr && gn < -kkt_thr) filtered = true;
-      }
-      if (filtered) {
-        active[k] = 0;
-        if (nan_filtered) d = __builtin_nan("");
-      } else {
-        vmax = fmax(vmax, vio);
-        d = -wk;
-        if (gp <= u * wk) d = -gp / u;
-        else if (gn >= u * wk) d = -gn / u;
-        const double dk = delta[k];
-        d = fmin(dk, fmax(-dk, d));
-        delta[k] = fmin(delta_max, 2 * fabs(d) + .1);
-        w[k] = wk + d;
-      }
-    }
+    if (active[k]) d = bcd_update_col(k, gj, uj, w[k], delta[k], w, delta, active, eta, lambda,
+                                      delta_max, kkt_thr, nan_filtered, vmax);
     dw[j] = d;
   }
-  // wave max -> one atomic per wave
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) vmax = fmax(vmax, __shfl_xor(vmax, off, 64));
-  if ((threadIdx.x & 63) == 0 && vmax > 0)
-    atomicMax(vio_bits, (unsigned long long)__double_as_longlong(vmax));
+  bcd_vio_max(vmax, vio_bits);
 }
 
 // Sharded server, replica side: the owners' updates of a block arrive as one
@@ -290,11 +305,15 @@ __device__ __forceinline__ void bcd_gu(int64_t i, int64_t c, int64_t c0,
 // one 16-B record, recomputed per wide block (bcd_rowq_kernel, a 4 M-row stream), so the
 // random per-entry gather fetches ONE line instead of two (ym and y) and skips the
 // exp: the wide blocks' gradient is bound by these gathers.
+// rows (optional): the block's distinct examples (a block of the CTR-log group layout
+// touches ~1/15 of them: packing all 4 M rows per block cost 17.5 us, its list ~2 us).
 __global__ void __launch_bounds__(256)
 bcd_rowq_kernel(const double* __restrict__ ym, const float* __restrict__ y, int64_t n,
-                double2* __restrict__ rowq) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
+                const int32_t* __restrict__ rows, int64_t nrows, double2* __restrict__ rowq) {
+  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = rows ? rows[q] : q;
+    if (!in_range(i, nrows)) continue;
     const double tau = 1.0 / (1.0 + exp(ym[i]));
     rowq[i] = make_double2(-(double)y[i] * tau, tau * (1.0 - tau));
   }
@@ -401,14 +420,30 @@ bcd_grad_chunk_kernel(const int32_t* __restrict__ col, const int32_t* __restrict
 // sum are exact int64 sums).
 constexpr int kRowCols = 2048;
 
+// Fused coordinate update (upd.dw != null, one rank): the workgroups add their column
+// sums into the block's accumulator (part) and the last one to finish (a device counter,
+// reset by that workgroup) applies the update to every column, writing dw for the
+// block's later dual update, and zeroes the accumulator. The
+// block's columns are touched by no other block, so updating them when the gradient
+// lands instead of tau blocks later changes nothing (kkt_thr is fixed within a pass).
+struct RowsUpd {
+  double* w;
+  double* delta;   // (the kernel reads delta through its const view before the update)
+  uint8_t* active;
+  double* dw;
+  unsigned long long* vio_bits;
+  unsigned int* counter;
+  double eta, lambda, delta_max, kkt_thr;
+};
+
 template <bool kVal>
 __global__ void __launch_bounds__(512)
 bcd_grad_rows_kernel(const int32_t* __restrict__ col, const int32_t* __restrict__ row,
                      const float* __restrict__ val, int64_t p0, int64_t p1, int64_t c0,
                      int ncols, int copies, const double* __restrict__ ym,
-                     const float* __restrict__ y, int64_t nrows, const double* __restrict__ delta,
-                     const uint8_t* __restrict__ active, int k2,
-                     long long* __restrict__ part) {
+                     const float* __restrict__ y, int64_t nrows, const double* delta,
+                     const uint8_t* active, int k2,
+                     long long* __restrict__ part, RowsUpd upd) {
   __shared__ long long acc[2 * kRowCols];  // [copies][2][ncols] (G, U), copies*ncols <= 2048
   __shared__ double cdl[kRowCols];            // per column: exp(delta) (binary) or delta
   __shared__ uint8_t cact[kRowCols];
@@ -419,6 +454,18 @@ bcd_grad_rows_kernel(const int32_t* __restrict__ col, const int32_t* __restrict_
     const double dl = delta[c0 + c];
     cdl[c] = kVal ? dl : exp(dl);
     cact[c] = active[c0 + c];
+  }
+  // fused update: every workgroup holds w / delta of "its" update columns (j = t + 512 q)
+  // from the start, so the last one's update waits on no load but the sums
+  constexpr int kUq = kRowCols / 512;
+  double uw[kUq], ud[kUq];
+  if (upd.dw) {
+#pragma unroll
+    for (int q = 0; q < kUq; ++q) {
+      const int j = t + q * 512;
+      uw[q] = j < ncols ? upd.w[c0 + j] : 0.0;
+      ud[q] = j < ncols ? delta[c0 + j] : 0.0;
+    }
   }
   __syncthreads();
   const int64_t n = p1 - p0;
@@ -475,12 +522,54 @@ bcd_grad_rows_kernel(const int32_t* __restrict__ col, const int32_t* __restrict_
     }
   }
   __syncthreads();
-  long long* out = part + (int64_t)blockIdx.x * stride;
+  if (!upd.dw) {
+    long long* out = part + (int64_t)blockIdx.x * stride;
+    for (int i = t; i < stride; i += blockDim.x) {
+      long long s = 0;
+      for (int q = 0; q < copies; ++q) s += acc[q * stride + i];
+      out[i] = s;
+    }
+    return;
+  }
+  // fused update: part is the block's [G | U] fixed-point accumulator (2 x ncols int64,
+  // zero between uses); the nonzero workgroup sums go in by int64 atomics (exact: the
+  // result does not depend on their order)
   for (int i = t; i < stride; i += blockDim.x) {
     long long s = 0;
     for (int q = 0; q < copies; ++q) s += acc[q * stride + i];
-    out[i] = s;
+    if (s) atomicAdd(reinterpret_cast<unsigned long long*>(part + i), (unsigned long long)s);
   }
+  __shared__ unsigned int last;
+  __threadfence();  // this workgroup's sums visible device-wide before it counts
+  __syncthreads();
+  if (t == 0) {
+    const unsigned int prev = atomicAdd(upd.counter, 1u);
+    last = prev == gridDim.x - 1;
+    if (last) upd.counter[0] = 0;  // (every other workgroup has counted: reuse)
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const double isc = ldexp(1.0, -k2);
+  double vmax = 0;
+#pragma unroll
+  for (int q = 0; q < kUq; ++q) {
+    const int j = t + q * 512;
+    if (j >= ncols) break;
+    // (other workgroups' atomics: device-coherent loads), then zero for the next use
+    const long long sg = __hip_atomic_load(part + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long long su =
+        __hip_atomic_load(part + ncols + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    part[j] = 0;
+    part[ncols + j] = 0;
+    const int64_t k = c0 + j;
+    double d = 0;
+    if (cact[j])
+      d = bcd_update_col(k, (double)sg * isc, (double)su * isc, uw[q], ud[q], upd.w, upd.delta,
+                         upd.active, upd.eta, upd.lambda, upd.delta_max, upd.kkt_thr, 0, vmax);
+    upd.dw[j] = d;
+  }
+  bcd_vio_max(vmax, upd.vio_bits);
 }
 
 // G[c] / U[c] = sum over the W workgroup partials x 2^-k: one workgroup per output, its
@@ -814,7 +903,7 @@ void bcd_grad_chunked(const int32_t* col, const int32_t* row, const float* val,
                       const int64_t* chunks, int64_t nchunks, int64_t c0, int64_t ncols,
                       const double* ym, const float* y, int64_t nrows, const double* delta,
                       const uint8_t* active, double* rowq, double* G, double* U, bool zeroed,
-                      bool rowq_ready, hipStream_t st) {
+                      bool rowq_ready, const int32_t* urows, int64_t nurows, hipStream_t st) {
   if (!zeroed) {
     fill_async<double>(G, ncols, 0.0, st);
     fill_async<double>(U, ncols, 0.0, st);
@@ -822,7 +911,10 @@ void bcd_grad_chunked(const int32_t* col, const int32_t* row, const float* val,
   if (nchunks <= 0) return;
   if (rowq) {
     if (!rowq_ready) {  // (ready: a row pass wrote the block's examples' factors)
-      bcd_rowq_kernel<<<grid_for(nrows, 256, 4096), 256, 0, st>>>(ym, y, nrows, (double2*)rowq);
+      const int64_t n = urows ? nurows : nrows;
+      if (n > 0)
+        bcd_rowq_kernel<<<grid_for(n, 256, 4096), 256, 0, st>>>(ym, y, n, urows, nrows,
+                                                                 (double2*)rowq);
       PSAMD_HIP_CHECK(hipGetLastError());
     }
     bcd_grad_chunk_kernel<true><<<grid_for(nchunks, 4, 16384), 256, 0, st>>>(
@@ -840,22 +932,28 @@ int bcd_part_segments() { return kPartSeg; }
 
 void bcd_grad_rows(const int32_t* col, const int32_t* row, const float* val, int64_t p0,
                    int64_t p1, int64_t c0, int64_t ncols, const double* ym, const float* y,
-                   int64_t nrows, const double* delta, const uint8_t* active, int k2, int W,
-                   long long* part, double* G, double* U, hipStream_t st) {
+                   int64_t nrows, double* delta, uint8_t* active, int k2, int W,
+                   long long* part, double* G, double* U, double* w, double* dw,
+                   unsigned long long* vio_bits, unsigned int* counter, double eta, double lambda,
+                   double delta_max, double kkt_thr, hipStream_t st) {
   if (ncols <= 0) return;
   if (ncols > kRowCols) throw std::runtime_error("bcd_grad_rows: ncols > 2048");
   const int copies = std::max(1, std::min(8, kRowCols / (int)ncols));
-  if (p1 > p0) {
+  // dw given: part is the block's 2 x ncols accumulator and the coordinate update runs in
+  // the gradient's last workgroup (no reduce launch, no update launch)
+  const RowsUpd upd{w, delta, active, dw, vio_bits, counter, eta, lambda, delta_max, kkt_thr};
+  if (p1 > p0 || dw) {
     if (val)
       bcd_grad_rows_kernel<true><<<W, 512, 0, st>>>(col, row, val, p0, p1, c0, (int)ncols, copies,
-                                                    ym, y, nrows, delta, active, k2, part);
+                                                    ym, y, nrows, delta, active, k2, part, upd);
     else
       bcd_grad_rows_kernel<false><<<W, 512, 0, st>>>(col, row, val, p0, p1, c0, (int)ncols, copies,
-                                                     ym, y, nrows, delta, active, k2, part);
+                                                     ym, y, nrows, delta, active, k2, part, upd);
     PSAMD_HIP_CHECK(hipGetLastError());
   } else {
     fill_async<long long>(part, (int64_t)W * 2 * ncols, 0, st);
   }
+  if (dw) return;
   bcd_rows_reduce_kernel<<<(unsigned)(2 * ncols), 256, 0, st>>>(part, W, (int)ncols, k2, G, U);
   PSAMD_HIP_CHECK(hipGetLastError());
 }

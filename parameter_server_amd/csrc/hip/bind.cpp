@@ -206,7 +206,8 @@ void bcd_grad(const int32_t*, const int32_t*, const float*, int64_t, int64_t, in
               double*, hipStream_t);
 void bcd_grad_chunked(const int32_t*, const int32_t*, const float*, const int64_t*, int64_t,
                       int64_t, int64_t, const double*, const float*, int64_t, const double*,
-                      const uint8_t*, double*, double*, double*, bool, bool, hipStream_t);
+                      const uint8_t*, double*, double*, double*, bool, bool, const int32_t*,
+                      int64_t, hipStream_t);
 void bcd_rowpass(int64_t, double*, const float*, const int32_t*, const float*, const double*,
                  int64_t, const int32_t*, const float*, int64_t, int64_t, const double*,
                  const uint8_t*, int, int, long long*, double*, double*, double*, const int32_t*,
@@ -222,8 +223,9 @@ void bcd_objective(const double*, int64_t, double*, hipStream_t);
 int bcd_rows_max_cols();
 int bcd_part_segments();
 void bcd_grad_rows(const int32_t*, const int32_t*, const float*, int64_t, int64_t, int64_t, int64_t,
-                   const double*, const float*, int64_t, const double*, const uint8_t*, int, int,
-                   long long*, double*, double*, hipStream_t);
+                   const double*, const float*, int64_t, double*, uint8_t*, int, int,
+                   long long*, double*, double*, double*, double*, unsigned long long*,
+                   unsigned int*, double, double, double, double, hipStream_t);
 void bcd_server_stats(const double*, const uint8_t*, int64_t, int64_t, double*, hipStream_t);
 // embedding.hip
 void emb_init_rows(const int64_t*, const uint64_t*, int64_t, const int32_t*, int64_t, void*,
@@ -2101,7 +2103,8 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("bcd_grad_chunked", [](Tensor col, Tensor row, optional<Tensor> val, Tensor chunks,
                                 int64_t c0, int64_t ncols, Tensor ym, Tensor y, Tensor delta,
                                 Tensor active, Tensor G, Tensor U, bool zeroed,
-                                optional<Tensor> rowq, bool rowq_ready) {
+                                optional<Tensor> rowq, bool rowq_ready,
+                                optional<Tensor> urows) {
     // chunks: [n + 1] int64 entry offsets (bit 62 = hot chunk), built and range-checked
     // on the host once per block (models/darlin.py build_chunks)
     chk(col, at::kInt, "col");
@@ -2123,12 +2126,19 @@ PYBIND11_MODULE(_hipops, m) {
     check(G.numel() >= ncols && U.numel() >= ncols, "G/U too small");
     double* rq = optr<double>(rowq, at::kDouble, "rowq");
     if (rq) check(rowq->numel() >= 2 * ym.numel(), "rowq: 2 doubles per example");
+    // urows: the block's distinct examples (the rowq packing covers only them; entries
+    // outside the list would read stale factors: built from the block's rows, darlin.py)
+    const int32_t* ur = optr<int32_t>(urows, at::kInt, "urows");
+    if (ur) check(rq != nullptr, "urows needs rowq");
     psamd::bcd_grad_chunked(ptr<int32_t>(col), ptr<int32_t>(row), vp, ptr<int64_t>(chunks),
                             chunks.numel() - 1, c0, ncols, ptr<double>(ym), ptr<float>(y),
                             ym.numel(), ptr<double>(delta), ptr<uint8_t>(active), rq,
                             ptr<double>(G), ptr<double>(U), zeroed, rq != nullptr && rowq_ready,
-                            cur_stream());
-  });
+                            ur, ur ? urows->numel() : 0, cur_stream());
+  }, py::arg("col"), py::arg("row"), py::arg("val"), py::arg("chunks"), py::arg("c0"),
+     py::arg("ncols"), py::arg("ym"), py::arg("y"), py::arg("delta"), py::arg("active"),
+     py::arg("G"), py::arg("U"), py::arg("zeroed"), py::arg("rowq"), py::arg("rowq_ready"),
+     py::arg("urows") = py::none());
   // Darlin row pass over dense per-row block layouts (bcd.hip bcd_rowpass): the pending
   // dual update of block j (jcol: [rows] int32 column relative to the block, -1 none)
   // fused with block k's gradient (narrow: part/G/U; wide: rowq).
@@ -2263,7 +2273,10 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("bcd_grad_rows", [csc_check](Tensor col, Tensor row, optional<Tensor> val, int64_t p0,
                                      int64_t p1, int64_t c0, int64_t ncols, Tensor ym, Tensor y,
                                      Tensor delta, Tensor active, int k2, int W, Tensor part,
-                                     Tensor G, Tensor U) {
+                                     Tensor G, Tensor U, optional<Tensor> w,
+                                     optional<Tensor> dw, optional<Tensor> vio_bits,
+                                     optional<Tensor> counter, double eta, double lambda,
+                                     double delta_max, double kkt_thr) {
     csc_check(col, row, val, p0, p1);
     chk(ym, at::kDouble, "ym");
     chk(y, at::kFloat, "y");
@@ -2277,14 +2290,33 @@ PYBIND11_MODULE(_hipops, m) {
     check(c0 >= 0 && c0 + ncols <= delta.numel() && delta.numel() == active.numel(),
           "block columns out of range");
     check(G.numel() >= ncols && U.numel() >= ncols, "G/U too small");
-    check(W >= 1 && W <= 65535 && part.numel() >= (int64_t)W * 2 * ncols, "partials buffer");
+    check(W >= 1 && W <= 65535 &&
+              part.numel() >= (int64_t)(dw.has_value() && dw->defined() ? 1 : W) * 2 * ncols,
+          "partials buffer (fused update: the block's 2 x ncols accumulator)");
     check(k2 >= 0 && k2 <= 62, "fixed-point scale 2^0..2^62");
+    // fused update (dw given): the last workgroup applies the coordinate step of every
+    // column of the block (bcd_update's arithmetic) and writes dw
+    double* dwp = optr<double>(dw, at::kDouble, "dw");
+    double* wp = optr<double>(w, at::kDouble, "w");
+    auto* vp = reinterpret_cast<unsigned long long*>(optr<int64_t>(vio_bits, at::kLong, "vio_bits"));
+    auto* cp = reinterpret_cast<unsigned int*>(optr<int32_t>(counter, at::kInt, "counter"));
+    if (dwp) {
+      check(wp && vp && cp, "fused update needs w, vio_bits and counter");
+      check(w->numel() == delta.numel() && dw->numel() >= ncols, "w / dw size");
+      check(eta > 0, "eta must be > 0");
+    }
     psamd::bcd_grad_rows(ptr<int32_t>(col), ptr<int32_t>(row), optr<float>(val, at::kFloat, "val"),
                          p0, p1, c0, ncols, ptr<double>(ym), ptr<float>(y), ym.numel(),
                          ptr<double>(delta), ptr<uint8_t>(active), k2, W,
                          reinterpret_cast<long long*>(part.data_ptr()), ptr<double>(G),
-                         ptr<double>(U), cur_stream());
-  });
+                         ptr<double>(U), wp, dwp, vp, cp, eta, lambda, delta_max, kkt_thr,
+                         cur_stream());
+  }, py::arg("col"), py::arg("row"), py::arg("val"), py::arg("p0"), py::arg("p1"), py::arg("c0"),
+     py::arg("ncols"), py::arg("ym"), py::arg("y"), py::arg("delta"), py::arg("active"),
+     py::arg("k2"), py::arg("W"), py::arg("part"), py::arg("G"), py::arg("U"),
+     py::arg("w") = py::none(), py::arg("dw") = py::none(), py::arg("vio_bits") = py::none(),
+     py::arg("counter") = py::none(), py::arg("eta") = 1.0, py::arg("lam") = 0.0,
+     py::arg("delta_max") = 0.0, py::arg("kkt_thr") = 0.0);
   m.def("bcd_objective", [](Tensor ym, Tensor out) {
     chk(ym, at::kDouble, "ym");
     chk(out, at::kDouble, "out");

@@ -110,6 +110,21 @@ class DarlinConfig:
                    seed=seed)
 
 
+# narrow blocks of at most this many entries: gradient and coordinate update in one
+# launch of a few workgroups (one rank)
+_SMALL_ROWS_BLOCK = 1 << 18
+
+
+def _hot_piece(entries: int) -> int:
+    """Entries per piece of a hot column in the chunked gradient: ~2048 pieces per block
+    (256 .. 4096), so a block of a few 100 k entries is not a few dozen waves each
+    walking 4096 dependent gathers (CTR-log groups: 44.7 us per wide block at 4096)."""
+    if os.environ.get("PSAMD_BCD_HOT"):  # (A/B pin)
+        return int(os.environ["PSAMD_BCD_HOT"])
+    want = max(1, entries // 2048)
+    return int(min(4096, max(256, 1 << (want - 1).bit_length())))
+
+
 def divide_feature_blocks(info: dict, ratio: float) -> list[tuple[int, int, int]]:
     """[(group, key_begin, key_end)] — reference BCDScheduler::divideFeatureBlocks
     (src/learner/bcd.h:78-106): a group with nnz_per_row > 1 is split into
@@ -163,7 +178,9 @@ class Block:
     kenc: object = None        # wide block: hot / cold encoded layout (bcd.hot_layout)
     hcols: object = None       # ... its LDS hot slot -> column map
     chunks_cold: object = None  # ... and the chunk list of its cold columns
-    part2: object = None       # narrow dense block: its row pass's segment sums (1 rank)
+    part2: object = None       # narrow block: its gradient's segment sums (1 rank)
+    urows: object = None       # wide block w/o dense layout: its distinct examples (int32)
+    dw: object = None          # small narrow block: dw of its fused update (bcd.grad_rows)
 
     @property
     def ncols(self):
@@ -480,7 +497,8 @@ class DarlinTrainer:
             c1 = self.group_base[g] + int(np.searchsorted(gk, fb, side="right"))
             blk = Block(g, a, b, c0, c1, int(colptr[c0]), int(colptr[c1]))
             if dev.type == "cuda":
-                blk.chunks = torch.from_numpy(bcd.build_chunks(colptr, c0, c1)).to(dev)
+                blk.chunks = torch.from_numpy(bcd.build_chunks(
+                    colptr, c0, c1, hot=_hot_piece(blk.p1 - blk.p0))).to(dev)
                 # persistent [G | U], zeroed by the update that consumes it
                 blk.gu = torch.zeros(2 * (c1 - c0), dtype=torch.float64, device=dev)
             self.blocks.append(blk)
@@ -546,6 +564,12 @@ class DarlinTrainer:
                             blk.chunks_cold = torch.from_numpy(cold).to(dev)
                             vmax = 1.0 if self.val is None else float(self.val[p0:p1].abs().max())
                             blk.fx_k = bcd.fixed_point_shift(nh, vmax)
+                # wide block without a dense layout: its gradient packs the per-example
+                # factors (rowq) of its own examples only (CTR-log groups: ~1/15 of them)
+                if not blk.row_mode and blk.dcol is None:
+                    ur = torch.unique_consecutive(rs)
+                    if 2 * ur.numel() < self.rows:
+                        blk.urows = ur.to(torch.int32)
         # model state (replicated per rank) and margins
         f64 = torch.float64
         self.w = torch.full((base,), float(cfg.init_w), dtype=f64, device=dev)
@@ -555,6 +579,8 @@ class DarlinTrainer:
         if cfg.init_w != 0 and base:
             bcd.dual(self.col, self.row, self.val, 0, self.nnz, 0, base, self.w, self.y, self.ym)
         self.vio = torch.zeros(1, dtype=torch.int64, device=dev)
+        # last-workgroup counter of the fused gradient + update (reset by the kernel)
+        self._upd_ctr = torch.zeros(1, dtype=torch.int32, device=dev)
         # owned column share for the server-side statistics
         self.own = even_divide(0, base, self.G, self.rank)
         if self.verbose and self.rank == 0:
@@ -584,6 +610,15 @@ class DarlinTrainer:
         at launch and at finish."""
         return (persistent and self.G == 1 and b.row_mode and b.dcol is not None
                 and not self._sharded(b))
+
+    def _fused_update(self, b: Block, persistent: bool) -> bool:
+        """Small narrow block without a dense layout, one rank, persistent buffers: its
+        row-order gradient applies the coordinate update in its last workgroup (dw kept
+        in b.dw for the dual update at finish: the block's columns belong to no other
+        block, so the earlier update changes nothing). Same predicate at launch and
+        finish."""
+        return (persistent and self.G == 1 and b.row_mode and b.dcol is None
+                and not self._sharded(b) and b.p1 - b.p0 <= _SMALL_ROWS_BLOCK)
 
     def _flush_dual(self):
         """Apply a deferred dual update on its own (before anything else reads ym)."""
@@ -633,6 +668,20 @@ class DarlinTrainer:
                      rowq=self.rowq, rowq_ready=True)
             return
         self._flush_dual()
+        if self._fused_update(b, zeroed):
+            # small narrow block: gradient + coordinate update in one launch of a few
+            # workgroups (no 256-workgroup partials pass, no reduce, no update launch)
+            if b.part2 is None:
+                b.part2 = torch.zeros(2 * b.ncols, dtype=torch.int64, device=self.device)
+                b.dw = torch.empty(b.ncols, dtype=torch.float64, device=self.device)
+            c = self.cfg
+            W = max(4, min(64, -(-(b.p1 - b.p0) // 4096)))
+            bcd.grad_rows(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, self.ym,
+                          self.y, self.delta, self.active, G, U, b.part2, W, b.fx_k,
+                          upd=dict(w=self.w, dw=b.dw, vio=self.vio, counter=self._upd_ctr,
+                                   eta=c.eta, lam=c.l1, delta_max=c.delta_max,
+                                   kkt_thr=self.kkt_thr))
+            return
         if b.row_mode:
             bcd.grad_rows(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, self.ym,
                           self.y, self.delta, self.active, G, U, self.rows_part, self.rows_W,
@@ -640,7 +689,8 @@ class DarlinTrainer:
             return
         bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
                  self.delta, self.active, G, U, chunks=b.chunks, zeroed=zeroed,
-                 rowq=self.rowq if b.chunks is not None else None)
+                 rowq=self.rowq if b.chunks is not None else None,
+                 urows=b.urows if b.chunks is not None else None)
 
     def _launch(self, b: Block):
         if self._sharded(b):
@@ -664,6 +714,10 @@ class DarlinTrainer:
             work.wait()
         G, U = GU[:b.ncols], GU[b.ncols:]
         c = self.cfg
+        if self._fused_update(b, persistent):  # (updated by its gradient launch)
+            b.busy = False
+            self._dual(b, b.dw)
+            return
         p2 = b.part2 if self._defer_sums(b, persistent) else None
         dw, _ = bcd.update(b.c0, b.ncols, G, U, self.w, self.delta, self.active, c.eta, c.l1,
                            c.delta_max, self.kkt_thr, vio=self.vio, consume=persistent,

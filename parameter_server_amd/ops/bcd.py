@@ -73,14 +73,16 @@ def build_chunks(colptr, c0: int, c1: int, small: int = 64, hot: int = 4096,
 
 
 def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, active,
-         G=None, U=None, chunks=None, zeroed: bool = False, rowq=None, rowq_ready: bool = False):
+         G=None, U=None, chunks=None, zeroed: bool = False, rowq=None, rowq_ready: bool = False,
+         urows=None):
     """Block gradient: returns (G, U) fp64[ncols] (inactive columns contribute 0).
     ``chunks`` (device int64 from ``build_chunks``) selects the load-balanced kernel;
     ``rowq`` (fp64 [2 * rows] scratch, with ``chunks``): the per-example factors are
     packed first so each entry gathers one 16-B record (wide blocks);
     ``zeroed``: G / U already hold zeros (left by ``update(consume=True)``);
     ``rowq_ready``: ``rowq`` already holds the factors of the block's examples (a
-    ``rowpass`` wrote them), so the packing pass is skipped."""
+    ``rowpass`` wrote them), so the packing pass is skipped; ``urows`` (device int32, the
+    block's distinct examples): the packing covers only them instead of every example."""
     dev = ym.device
     if G is None:
         G = torch.empty(ncols, dtype=torch.float64, device=dev)
@@ -89,7 +91,7 @@ def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, act
     if is_gpu(ym):
         if chunks is not None:
             hipops().bcd_grad_chunked(col, row, val, chunks, c0, ncols, ym, y, delta, active,
-                                      G, U, zeroed, rowq, bool(rowq_ready))
+                                      G, U, zeroed, rowq, bool(rowq_ready), urows)
         else:
             hipops().bcd_grad(col, row, val, p0, p1, c0, ncols, ym, y, delta, active, G, U)
         return G, U
@@ -116,15 +118,23 @@ def grad(col, row, val, p0: int, p1: int, c0: int, ncols: int, ym, y, delta, act
 
 
 def grad_rows(col_r, row_r, val_r, p0: int, p1: int, c0: int, ncols: int, ym, y, delta,
-              active, G, U, part, W: int, k2: int):
+              active, G, U, part, W: int, k2: int, upd: dict | None = None):
     """Block gradient of a NARROW block (ncols <= ``hipops().bcd_rows_max_cols()``) from
     the row-sorted entries: sequential per-row reads, LDS fixed-point column sums at
     scale 2^k2 (``fixed_point_shift`` of the block's entry count), W workgroup partials
     in ``part`` reduced in a
-    fixed order (deterministic). Same result as ``grad`` up to the 2^-k2 quantisation."""
+    fixed order (deterministic). Same result as ``grad`` up to the 2^-k2 quantisation.
+    ``upd`` (GPU, one rank): ``dict(w, dw, vio, counter, eta, lam, delta_max, kkt_thr)``:
+    the coordinate update (``update``'s arithmetic) runs in the kernel's last workgroup and
+    writes ``dw``; ``part`` is then the block's zeroed 2 x ncols int64 accumulator and
+    G / U are not written."""
     if is_gpu(ym):
+        u = upd or {}
         hipops().bcd_grad_rows(col_r, row_r, val_r, p0, p1, c0, ncols, ym, y, delta, active,
-                               int(k2), int(W), part, G, U)
+                               int(k2), int(W), part, G, U, u.get("w"), u.get("dw"),
+                               u.get("vio"), u.get("counter"), float(u.get("eta", 1.0)),
+                               float(u.get("lam", 0.0)), float(u.get("delta_max", 0.0)),
+                               float(u.get("kkt_thr", 0.0)))
         return G, U
     return grad(col_r, row_r, val_r, p0, p1, c0, ncols, ym, y, delta, active, G, U)
 

@@ -55,6 +55,16 @@ def test_bcd_kernels_match_torch(valued):
                               D(delta), D(active), chunks=ch)
             torch.testing.assert_close(Gk.cpu(), Gc, rtol=1e-10, atol=1e-10)
             torch.testing.assert_close(Uk.cpu(), Uc, rtol=1e-10, atol=1e-10)
+        # per-example factors packed for the block's own examples only (urows): the
+        # other rows of rowq stay NaN and are never read
+        if p1 > p0:
+            ch = D(bcd.build_chunks(colptr, c0, c1, hot=256))
+            rq = torch.full((2 * rows,), float("nan"), dtype=torch.float64, device="cuda")
+            ur = torch.unique(D(row[p0:p1]))
+            Gq, Uq = bcd.grad(D(col), D(row), D(val), p0, p1, c0, c1 - c0, D(ym), D(y),
+                              D(delta), D(active), chunks=ch, rowq=rq, urows=ur)
+            torch.testing.assert_close(Gq.cpu(), Gc, rtol=1e-10, atol=1e-10)
+            torch.testing.assert_close(Uq.cpu(), Uc, rtol=1e-10, atol=1e-10)
         for thr in (1e20, 0.05):
             wc, dc, ac = T(w.copy()), T(delta.copy()), T(active.copy())
             wg, dg, ag = D(w.copy()), D(delta.copy()), D(active.copy())
@@ -85,6 +95,34 @@ def test_darlin_gpu_trainer_matches_cpu():
     np.testing.assert_allclose([p.objective for p in pg], [p.objective for p in pc], rtol=1e-8)
     assert [p.nnz_w for p in pg] == [p.nnz_w for p in pc]
     assert pg[-1].objective < pg[0].objective
+
+
+@pytest.mark.parametrize("tau", [0, 2])
+def test_darlin_gpu_groups_layout_matches_cpu(tau):
+    """CTR-log-shaped groups (2 keys per example and group, each group in 1/3 of the
+    examples): wide blocks without a dense layout pack rowq for their own examples only
+    (Block.urows), small narrow blocks run gradient + coordinate update in one launch
+    (the last workgroup updates), hot columns in pieces sized from the block; the
+    GPU trainer follows the CPU trainer's objectives and sparsity."""
+    from parameter_server_amd.data.synthetic import sparse_groups
+
+    sd = sparse_groups(60_000, groups=6, present=2, keys_per_group=100_000, seed=9, alpha=0.8)
+    cfg = DarlinConfig(l1=2.0, max_pass=4, epsilon=1e-12, tail_freq=1, tau=tau, seed=3)
+    tg = DarlinTrainer(sd, cfg, device="cuda")
+    assert any(b.urows is not None for b in tg.blocks)
+    assert any(b.row_mode and b.dcol is None and tg._fused_update(b, True) for b in tg.blocks)
+    pg = tg.train()
+    pc = DarlinTrainer(sd, cfg, device="cpu").train()
+    np.testing.assert_allclose([p.objective for p in pg], [p.objective for p in pc], rtol=1e-8)
+    assert [p.nnz_w for p in pg] == [p.nnz_w for p in pc]
+    assert pg[-1].objective < pg[0].objective
+
+
+def test_hot_piece_sizes():
+    from parameter_server_amd.models.darlin import _hot_piece
+
+    assert _hot_piece(10) == 256 and _hot_piece(400_000) == 256
+    assert _hot_piece(4_000_000) == 2048 and _hot_piece(10 ** 9) == 4096
 
 
 def test_darlin_gpu_criteo_shaped_with_delay():
