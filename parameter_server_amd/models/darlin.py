@@ -115,6 +115,9 @@ class DarlinConfig:
 _SMALL_ROWS_BLOCK = 1 << 18
 
 
+_FUSED_W = int(os.environ.get("PSAMD_BCD_FUSED_W", "0"))  # (A/B pin of the fused grid)
+
+
 def _hot_piece(entries: int) -> int:
     """Entries per piece of a hot column in the chunked gradient: ~2048 pieces per block
     (256 .. 4096), so a block of a few 100 k entries is not a few dozen waves each
@@ -179,7 +182,7 @@ class Block:
     hcols: object = None       # ... its LDS hot slot -> column map
     chunks_cold: object = None  # ... and the chunk list of its cold columns
     part2: object = None       # narrow block: its gradient's segment sums (1 rank)
-    urows: object = None       # wide block w/o dense layout: its distinct examples (int32)
+    few_rows: bool = False     # wide block w/o dense layout on < half of the examples
     dw: object = None          # small narrow block: dw of its fused update (bcd.grad_rows)
 
     @property
@@ -564,12 +567,13 @@ class DarlinTrainer:
                             blk.chunks_cold = torch.from_numpy(cold).to(dev)
                             vmax = 1.0 if self.val is None else float(self.val[p0:p1].abs().max())
                             blk.fx_k = bcd.fixed_point_shift(nh, vmax)
-                # wide block without a dense layout: its gradient packs the per-example
-                # factors (rowq) of its own examples only (CTR-log groups: ~1/15 of them)
+                # wide block without a dense layout on < half of the examples (CTR-log
+                # groups: ~1/15): its gradient gathers ym / y per entry instead of packing
+                # rowq first (4 M examples, 17.5 us; even packing its own examples only,
+                # bcd.grad urows=, 8.4 us, cost more than it saved: 19.1-19.6 vs 18.1 ms per
+                # pass, profiles/r5_darlin_groups.log)
                 if not blk.row_mode and blk.dcol is None:
-                    ur = torch.unique_consecutive(rs)
-                    if 2 * ur.numel() < self.rows:
-                        blk.urows = ur.to(torch.int32)
+                    blk.few_rows = 2 * torch.unique_consecutive(rs).numel() < self.rows
         # model state (replicated per rank) and margins
         f64 = torch.float64
         self.w = torch.full((base,), float(cfg.init_w), dtype=f64, device=dev)
@@ -675,7 +679,9 @@ class DarlinTrainer:
                 b.part2 = torch.zeros(2 * b.ncols, dtype=torch.int64, device=self.device)
                 b.dw = torch.empty(b.ncols, dtype=torch.float64, device=self.device)
             c = self.cfg
-            W = max(4, min(64, -(-(b.p1 - b.p0) // 4096)))
+            # (8 workgroups for a ~60 k-entry block: 17.3 ms per pass vs 18.1 at 4, 18.2 at
+            # ~15, 18.1 at 32, 20.6 at 64; profiles/r5_darlin_groups.log)
+            W = _FUSED_W or max(8, min(32, (b.p1 - b.p0) // 8192))
             bcd.grad_rows(self.col_r, self.row_r, self.val_r, b.p0, b.p1, b.c0, b.ncols, self.ym,
                           self.y, self.delta, self.active, G, U, b.part2, W, b.fx_k,
                           upd=dict(w=self.w, dw=b.dw, vio=self.vio, counter=self._upd_ctr,
@@ -689,8 +695,7 @@ class DarlinTrainer:
             return
         bcd.grad(self.col, self.row, self.val, b.p0, b.p1, b.c0, b.ncols, self.ym, self.y,
                  self.delta, self.active, G, U, chunks=b.chunks, zeroed=zeroed,
-                 rowq=self.rowq if b.chunks is not None else None,
-                 urows=b.urows if b.chunks is not None else None)
+                 rowq=self.rowq if b.chunks is not None and not b.few_rows else None)
 
     def _launch(self, b: Block):
         if self._sharded(b):

@@ -100,8 +100,8 @@ def test_darlin_gpu_trainer_matches_cpu():
 @pytest.mark.parametrize("tau", [0, 2])
 def test_darlin_gpu_groups_layout_matches_cpu(tau):
     """CTR-log-shaped groups (2 keys per example and group, each group in 1/3 of the
-    examples): wide blocks without a dense layout pack rowq for their own examples only
-    (Block.urows), small narrow blocks run gradient + coordinate update in one launch
+    examples): wide blocks without a dense layout gather ym / y per entry (Block.few_rows,
+    no rowq packing pass), small narrow blocks run gradient + coordinate update in one launch
     (the last workgroup updates), hot columns in pieces sized from the block; the
     GPU trainer follows the CPU trainer's objectives and sparsity."""
     from parameter_server_amd.data.synthetic import sparse_groups
@@ -109,7 +109,7 @@ def test_darlin_gpu_groups_layout_matches_cpu(tau):
     sd = sparse_groups(60_000, groups=6, present=2, keys_per_group=100_000, seed=9, alpha=0.8)
     cfg = DarlinConfig(l1=2.0, max_pass=4, epsilon=1e-12, tail_freq=1, tau=tau, seed=3)
     tg = DarlinTrainer(sd, cfg, device="cuda")
-    assert any(b.urows is not None for b in tg.blocks)
+    assert any(b.few_rows for b in tg.blocks)
     assert any(b.row_mode and b.dcol is None and tg._fused_update(b, True) for b in tg.blocks)
     pg = tg.train()
     pc = DarlinTrainer(sd, cfg, device="cpu").train()
