@@ -40,19 +40,19 @@ for name, M, N, K in SHAPES:
     C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     ref = torch.relu(A[:512].float() @ B.float().t() + bias)
     errs = []
-    VARS = (0, 1, 2, 3, 4, 5)
+    VARS = (0, 1, 2, 3, 4, 5, 6)
     for v in VARS:
         C.fill_(float("nan"))
         H.gemm_nt256(A, B, M, N, K, bias, True, C, None, v)
         errs.append(((C[:512].float() - ref).abs() / (ref.abs() + 1)).max().item())
     fl = 2.0 * M * N * K
-    # interleaved rounds in one process (variants 0-5), median per variant
+    # interleaved rounds in one process (variants 0-6), median per variant
     rounds = {v: [] for v in VARS}
     for _ in range(3):
         for v in VARS:
             rounds[v].append(t(lambda: H.gemm_nt256(A, B, M, N, K, bias, True, C, None, v)))
     med = {v: sorted(x)[1] for v, x in rounds.items()}
-    us_new, us_pp, us_p8, us_fine, us_ring, us_w4 = (med[v] for v in VARS)
+    us_new, us_pp, us_p8, us_fine, us_ring, us_w4, us_r32 = (med[v] for v in VARS)
     us_old = t(lambda: GM.gemm(A, True, B, True, M, N, K, bias=bias, relu=True))
     us_lib = t(lambda: torch.mm(A, B.t()))
     print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "max_rel_err_vs_fp32": errs,
@@ -62,6 +62,7 @@ for name, M, N, K in SHAPES:
                       "gemm256fine_us": us_fine, "gemm256fine_tflops": fl / us_fine / 1e6,
                       "gemm256ring_us": us_ring, "gemm256ring_tflops": fl / us_ring / 1e6,
                       "gemm256w4_us": us_w4, "gemm256w4_tflops": fl / us_w4 / 1e6,
+                      "gemm256r32_us": us_r32, "gemm256r32_tflops": fl / us_r32 / 1e6,
                       "gemm128_tflops": fl / us_old / 1e6, "hipblaslt_tflops": fl / us_lib / 1e6}),
           flush=True)
 

@@ -1322,10 +1322,10 @@ PYBIND11_MODULE(_hipops, m) {
     check(cp || fp, "gemm_nt256: need an output");
     if (cp) check(C->numel() >= M * N, "C too small");
     if (fp) check(Cf->numel() >= M * N, "Cf too small");
-    check(variant >= 0 && variant <= 5,
+    check(variant >= 0 && variant <= 6,
           "variant: 0 = one barrier per K-step, 1 = ping-pong, 2 = ping-pong with 2-step "
           "prefetch, 3 = 0 with fragment reads interleaved into the MFMA rows, 4 = 4-slot "
-          "LDS ring, 5 = 4 waves of 128 x 128");
+          "LDS ring, 5 = 4 waves of 128 x 128, 6 = 4 with 32x32x16 MFMAs");
     psamd::gemm_nt256(ptr<__bf16>(A), K, ptr<__bf16>(B), K, (int)M, (int)N, (int)K, bp, relu, cp, N,
                       fp, N, variant, cur_stream());
   }, py::arg("A"), py::arg("B"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bias"),

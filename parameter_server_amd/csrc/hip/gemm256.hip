@@ -35,6 +35,7 @@ namespace psamd {
 namespace g256 {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int BM = 256, BN = 256, BK = 64, TH = 512;
 constexpr int TILE_BYTES = BM * BK * 2;   // 32 KiB per operand tile
 constexpr int BUF_BYTES = 2 * TILE_BYTES; // A | B
@@ -1009,6 +1010,137 @@ gemm_nt256r_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __re
     }
   }
 }
+// ---------------------------------------------------------------------------
+// 32x32x16 ring variant (variant 6): variant 4's LDS ring, barriers and wave layout, the
+// 128 x 64 wave tile as 4 x 2 v_mfma_f32_32x32x16_bf16 tiles (lane l: A[row l&31][k 8(l>>5)
+// ..+7] of a 16-k sub-step, B likewise; C col l&31, rows (r&3) + 8(r>>2) + 4(l>>5)):
+// 16 MFMAs of 32 cycles per K-step instead of 32 of 16. The LDS traffic per K-step is
+// unchanged (the wave tile fixes it: 8 A + 4 B ds_read_b128), so the variant trades
+// issue slots only; the guide's bare-loop measurement puts 32x32x16 at ~0.87x the
+// FLOP/s of 16x16x32 (MI355X_MICROARCH.md, "bare bf16 MFMA loops").
+// Measured (profiles/r5_gemm_32x32.log): correct, slower than variant 4 on every W&D
+// shape (1199 vs 1306 TFLOP/s on 16384 x 1024 x 4992, 782 vs 819 on the dX product).
+// Kept for A/B.
+__global__ void __launch_bounds__(g256::TH)
+gemm_nt256r32_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B,
+                   int64_t ldb, int M, int N, int K, const float* __restrict__ bias, int relu,
+                   __bf16* __restrict__ C, int64_t ldc, float* __restrict__ Cf, int64_t ldcf,
+                   int tiles_n) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(16))) char smem[g256r::NSLOT * g256r::SLOT_BYTES];  // 128 KiB
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int id = g256_xcd(blockIdx.x, gridDim.x);
+  const int tm = id / tiles_n, tn = id - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = K / g256r::BK;
+  // prologue: K-steps 0..2 in flight, K-step 0 landed everywhere before barrier -1
+  for (int p = 0; p < 3 && p < nk; ++p)
+    g256r_stage(A, lda, M, B, ldb, N, m0, n0, p * g256r::BK, smem + p * g256r::SLOT_BYTES, wave,
+                lane);
+  if (nk >= 3) G256R_VMCNT(8);
+  else if (nk == 2) G256R_VMCNT(4);
+  else G256R_VMCNT(0);
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // the second wave row runs one barrier behind
+  const int h = lane >> 5;  // k half of a 16-k sub-step
+  for (int p = 0; p < nk; ++p) {
+    const char* cur = smem + (p & 3) * g256r::SLOT_BYTES;
+    // ---- READ interval: per 16-k sub-step ks, chunk 2 ks + h of rows (lane & 31)
+    bf16x8 a[4][2], b[2][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = 2 * ks + h;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wc * 64 + j * 32 + (lane & 31);
+        b[j][ks] = *reinterpret_cast<const bf16x8*>(cur + g256r::OP_BYTES + r * 64 +
+                                                    g256r_swz(r, c) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wr * 128 + i * 32 + (lane & 31);
+        a[i][ks] = *reinterpret_cast<const bf16x8*>(cur + r * 64 + g256r_swz(r, c) * 16);
+      }
+    }
+    if (p + 3 < nk)
+      g256r_stage(A, lda, M, B, ldb, N, m0, n0, (p + 3) * g256r::BK,
+                  smem + ((p + 3) & 3) * g256r::SLOT_BYTES, wave, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (wr == 1) G256R_WAIT_NEXT(p, nk);
+    __builtin_amdgcn_s_barrier();
+    // ---- MFMA interval
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][ks], b[j][ks], acc[i][j], 0, 0,
+                                                              0);
+    __builtin_amdgcn_s_setprio(0);
+    if (wr == 0) G256R_WAIT_NEXT(p, nk);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // match the second row's extra barrier
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // epilogue: m = m0 + wr*128 + i*32 + (r&3) + 8*(r>>2) + 4*(lane>>5),
+  // n = n0 + wc*64 + j*32 + (lane&31)
+  if (C && !Cf && (ldc & 7) == 0 && m0 + BM <= M && n0 + BN <= N) {
+    __bf16* st = reinterpret_cast<__bf16*>(smem);  // [256][256] bf16 = 128 KiB
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nl = wc * 64 + j * 32 + (lane & 31);
+      const float bv = bias ? bias[n0 + nl] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ml = wr * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          float v = acc[i][j][r] + bv;
+          if (relu) v = v > 0.f ? v : 0.f;
+          st[ml * BN + nl] = (__bf16)v;
+        }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int q = 0; q < BM * BN / 8 / TH; ++q) {
+      const int ch = q * TH + t;
+      const int ml = ch >> 5, nc = (ch & 31) * 8;
+      *reinterpret_cast<uint4*>(C + (int64_t)(m0 + ml) * ldc + n0 + nc) =
+          *reinterpret_cast<const uint4*>(st + ml * BN + nc);
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wc * 64 + j * 32 + (lane & 31);
+    if (n >= N) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wr * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m >= M) continue;
+        float v = acc[i][j][r] + bv;
+        if (relu) v = v > 0.f ? v : 0.f;
+        if (C) C[(int64_t)m * ldc + n] = (__bf16)v;
+        if (Cf) Cf[(int64_t)m * ldcf + n] = v;
+      }
+    }
+  }
+}
 #undef G256R_WAIT_NEXT
 #undef G256R_VMCNT
 
@@ -1187,7 +1319,11 @@ void gemm_nt256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int 
   if (M <= 0 || N <= 0) return;
   if (K % g256::BK != 0 || lda % 8 || ldb % 8) throw std::runtime_error("gemm_nt256: K % 64, ld % 8");
   const int tiles_m = (M + g256::BM - 1) / g256::BM, tiles_n = (N + g256::BN - 1) / g256::BN;
-  if (variant == 5)
+  if (variant == 6)
+    gemm_nt256r32_kernel<<<tiles_m * tiles_n, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
+                                                                 relu ? 1 : 0, C, ldc, Cf, ldcf,
+                                                                 tiles_n);
+  else if (variant == 5)
     gemm_nt256w4_kernel<<<tiles_m * tiles_n, g256w::TH, 0, st>>>(A, lda, B, ldb, M, N, K, bias,
                                                                  relu ? 1 : 0, C, ldc, Cf, ldcf,
                                                                  tiles_n);

@@ -22,7 +22,7 @@ def _ref(A, B, bias, relu):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 128), (300, 1000, 192),
                                    (1024, 4992, 1024), (4097, 260, 640), (64, 64, 64)])
 @pytest.mark.parametrize("epi", ["none", "bias_relu"])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6])
 def test_gemm256_matches_fp32(M, N, K, epi, variant):
     g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
     A = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).to(torch.bfloat16)
