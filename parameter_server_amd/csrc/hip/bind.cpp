@@ -96,7 +96,7 @@ void tp_backward(const uint16_t*, const int32_t*, int64_t, const int32_t*, int, 
                  float*, int64_t, hipStream_t);
 // gemm256.hip
 void gemm_tn256(const __bf16*, int64_t, const __bf16*, int64_t, int, int, int, int, float*, float*,
-                float, int, hipStream_t);
+                float, int, unsigned int*, hipStream_t);
 void transpose_bf16(const void*, int, int, void*, hipStream_t);
 void gemm_nt256(const __bf16*, int64_t, const __bf16*, int64_t, int, int, int, const float*, bool,
                 __bf16*, int64_t, float*, int64_t, int, hipStream_t);
@@ -1333,7 +1333,8 @@ PYBIND11_MODULE(_hipops, m) {
   // C [M, N] f32 = beta C + A^T B for MN-major A [K, M], B [K, N] (the weight gradient):
   // split-K partials into part [splits, M, N], then a fixed-order sum (gemm256.hip)
   m.def("gemm_tn256", [](Tensor A, Tensor B, int64_t M, int64_t N, int64_t K, int64_t splits,
-                         Tensor part, Tensor C, double beta, int phase) {
+                         Tensor part, Tensor C, double beta, int phase,
+                         optional<Tensor> tile_ctr) {
     chk(A, at::kBFloat16, "A");
     chk(B, at::kBFloat16, "B");
     chk(part, at::kFloat, "part");
@@ -1346,11 +1347,17 @@ PYBIND11_MODULE(_hipops, m) {
     check(((uintptr_t)A.data_ptr() % 16) == 0 && ((uintptr_t)B.data_ptr() % 16) == 0 &&
               ((uintptr_t)C.data_ptr() % 16) == 0 && ((uintptr_t)part.data_ptr() % 16) == 0,
           "gemm_tn256: 16-B aligned operands");
-    check(phase >= 0 && phase <= 2, "gemm_tn256: phase 0 (both) / 1 (GEMM) / 2 (reduce)");
+    check(phase >= 0 && phase <= 3,
+          "gemm_tn256: phase 0 (both) / 1 (GEMM) / 2 (reduce) / 3 (reduce in the GEMM)");
+    auto* tc = reinterpret_cast<unsigned int*>(optr<int32_t>(tile_ctr, at::kInt, "tile_ctr"));
+    if (phase == 3)
+      check(tc && tile_ctr->numel() >= ((M + 255) / 256) * ((N + 255) / 256),
+            "gemm_tn256 phase 3: tile_ctr, one zeroed int32 per 256 x 256 tile");
     psamd::gemm_tn256(ptr<__bf16>(A), M, ptr<__bf16>(B), N, (int)M, (int)N, (int)K, (int)splits,
-                      ptr<float>(part), ptr<float>(C), (float)beta, phase, cur_stream());
+                      ptr<float>(part), ptr<float>(C), (float)beta, phase, tc, cur_stream());
   }, py::arg("A"), py::arg("B"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("splits"),
-     py::arg("part"), py::arg("C"), py::arg("beta"), py::arg("phase") = 0);
+     py::arg("part"), py::arg("C"), py::arg("beta"), py::arg("phase") = 0,
+     py::arg("tile_ctr") = py::none());
   m.def("transpose_bf16", [](Tensor in, Tensor out) {
     chk(in, at::kBFloat16, "in");
     chk(out, at::kBFloat16, "out");

@@ -683,7 +683,8 @@ __device__ __forceinline__ gtn_s4 gtn_tr(const char* img, int kr, int cb, int la
 
 __global__ void __launch_bounds__(g256::TH)
 gemm_tn256_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B,
-                  int64_t ldb, int M, int N, int K, float* __restrict__ P, int tiles_n) {
+                  int64_t ldb, int M, int N, int K, float* P, int tiles_n,
+                  float* __restrict__ Out, float beta, unsigned int* tile_ctr) {
   using namespace g256;
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES];  // 128 KiB
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -756,6 +757,43 @@ gemm_tn256_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __res
         if (m < M) out[(int64_t)m * N + n] = acc[i][j][r];
       }
   }
+  if (!tile_ctr) return;
+  // in-kernel split-K reduce (tile_ctr given): the last of the tile's S splits to finish
+  // (a per-tile counter it resets) sums the S partials in split order -- its own from
+  // registers -- onto beta * Out: the arithmetic and order of gemm_splitk_reduce, so the
+  // result is bitwise that of the two-launch form, without the separate memory pass
+  __shared__ unsigned int last;
+  __threadfence();  // this split's partial visible device-wide before it counts
+  __syncthreads();
+  if (t == 0) {
+    const unsigned int prev = atomicAdd(tile_ctr + id, 1u);
+    last = prev == (unsigned)S - 1;
+    if (last) tile_ctr[id] = 0;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const int me = blockIdx.y;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
+    if (n >= N) continue;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 128 + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= M) continue;
+        const int64_t o = (int64_t)m * N + n;
+        float a = beta != 0.f ? Out[o] : 0.f;
+        if (beta != 0.f && beta != 1.f) a *= beta;
+        for (int q = 0; q < S; ++q)
+          a += q == me ? acc[i][j][r]
+                       : __hip_atomic_load(P + (int64_t)q * M * N + o, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        Out[o] = a;
+      }
+  }
 }
 
 // out[i] = beta * out[i] + sum over the S partials (fixed order: deterministic)
@@ -780,18 +818,24 @@ gemm_splitk_reduce_kernel(const float4* __restrict__ P, int S, int64_t n4, float
 // phase: 0 = GEMM + split-K reduce, 1 = the GEMM into `part` only, 2 = the reduce only
 // (a caller can hold the reduce back so that a later GEMM is not queued behind it)
 void gemm_tn256(const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
-                int splits, float* part, float* out, float beta, int phase, hipStream_t st) {
+                int splits, float* part, float* out, float beta, int phase, unsigned int* tile_ctr,
+                hipStream_t st) {
   if (M <= 0 || N <= 0) return;
   if (splits < 1 || K % g256::BK != 0 || K / g256::BK < splits || M % 8 || N % 8 || lda % 8 ||
       ldb % 8)
     throw std::runtime_error("gemm_tn256: K % 64, K / 64 >= splits, M / N / ld % 8");
   const int tiles_m = (M + g256::BM - 1) / g256::BM, tiles_n = (N + g256::BN - 1) / g256::BN;
   dim3 grid(tiles_m * tiles_n, splits);
+  // phase 3: the reduce inside the GEMM's last split per tile (tile_ctr: tiles_m x tiles_n
+  // zeroed counters, left zeroed)
+  if (phase == 3 && splits == 1) phase = 0;
   if (phase != 2) {
-    gemm_tn256_kernel<<<grid, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, part, tiles_n);
+    gemm_tn256_kernel<<<grid, g256::TH, 0, st>>>(A, lda, B, ldb, M, N, K, part, tiles_n,
+                                                 phase == 3 ? out : nullptr, beta,
+                                                 phase == 3 ? tile_ctr : nullptr);
     PSAMD_HIP_CHECK(hipGetLastError());
   }
-  if (phase == 1) return;
+  if (phase == 1 || phase == 3) return;
   const int64_t n4 = (int64_t)M * N / 4;
   gemm_splitk_reduce_kernel<<<grid_for(n4, 256, 4096), 256, 0, st>>>(
       reinterpret_cast<const float4*>(part), splits, n4, reinterpret_cast<float4*>(out), beta);

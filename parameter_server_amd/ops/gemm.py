@@ -196,11 +196,37 @@ def linear_weight_grad(dZ, X, out=None, beta: float = 0.0, backend: str = "mfma"
             H.gemm_tn256(dZ, X, N, K, Bn, S, part, out, float(beta), 1)
             deferred.append(lambda: H.gemm_tn256(dZ, X, N, K, Bn, S, part, out, float(beta), 2))
             return out
+        if S > 1 and _TN_FUSED_REDUCE:
+            # the split-K reduce inside the GEMM (the last split of each tile sums the
+            # partials in split order: bitwise the two-launch result, no separate pass)
+            hipops().gemm_tn256(dZ, X, N, K, Bn, S, part, out, float(beta), 3,
+                                _tile_counters(dZ.device, -(-N // 256) * -(-K // 256)))
+            return out
         hipops().gemm_tn256(dZ, X, N, K, Bn, S, part, out, float(beta))
         return out
     sk = auto_splitk(N, K, Bn) if beta in (0.0, 1.0) else 1
     gemm(dZ, False, X, False, N, K, Bn, out_bf16=False, out_f32=out, beta=beta, splitk=sk)
     return out
+
+
+# PSAMD_TN_FUSED_REDUCE=1 (A/B, off): the split-K reduce inside the TN GEMM's last split
+# per tile. Bitwise equal, but the W&D step measured 3.77 ms (all layers) / 1.14-1.16 ms
+# (S <= 4 only) vs 0.936-0.939 with the separate reduce pass: the reduce then runs on one
+# workgroup per 256 x 256 tile (profiles/r5_tn_fused_reduce_ab.log)
+_TN_FUSED_REDUCE = __import__("os").environ.get("PSAMD_TN_FUSED_REDUCE", "0") == "1"
+_TILE_CTRS: dict = {}
+
+
+def _tile_counters(dev, n: int):
+    """Zeroed int32 per-tile counters of gemm_tn256's in-kernel split-K reduce (each
+    launch leaves them zeroed; one buffer per device and stream ordering keeps launches
+    apart: a side-stream and a main-stream TN GEMM never run at once here)."""
+    key = (str(dev), torch.cuda.current_stream(dev).cuda_stream)
+    t = _TILE_CTRS.get(key)
+    if t is None or t.numel() < n:
+        t = torch.zeros(max(n, 1024), dtype=torch.int32, device=dev)
+        _TILE_CTRS[key] = t
+    return t
 
 
 def tn256_ok(M: int, N: int, K: int) -> bool:

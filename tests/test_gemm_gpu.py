@@ -98,8 +98,18 @@ def test_gemm_tn256_weight_grad(M, N, K, S, beta):
     C = torch.randn(M, N, device="cuda", generator=g)
     ref = A.float().t() @ B.float() + beta * C
     part = torch.full((S * M * N,), float("nan"), device="cuda")
+    C0 = C.clone()
     hipops().gemm_tn256(A, B, M, N, K, S, part, C, beta)
     torch.testing.assert_close(C, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
+    # the reduce inside the GEMM (phase 3: the last split of each tile sums the partials
+    # in split order): bitwise the two-launch result, and the tile counters end zeroed
+    ctr = torch.zeros(((M + 255) // 256) * ((N + 255) // 256), dtype=torch.int32, device="cuda")
+    for _ in range(3):
+        C3 = C0.clone()
+        part.fill_(float("nan"))
+        hipops().gemm_tn256(A, B, M, N, K, S, part, C3, beta, 3, ctr)
+        assert torch.equal(C3, C)
+        assert int(ctr.abs().sum()) == 0
 
 
 def test_linear_weight_grad_routes_to_tn256():
