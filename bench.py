@@ -566,7 +566,7 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         locs[b] = tr.localize(k, buf=b)
 
     xd = max(1, min(d, nprep - 1, int(os.environ.get("PSAMD_XD", "2"))))
-    E = 64
+    E = P * -(-64 // P)  # (a multiple of the phase count: one native plan per t % E)
     ev = {k: [torch.cuda.Event() for _ in range(E)] for k in ("w", "M", "res", "app")}
     ev_buf = [torch.cuda.Event() for _ in range(NB)]
     ev_prep = [torch.cuda.Event() for _ in range(NB)]
@@ -676,11 +676,14 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
              and cmode in ("1", "auto"))
     pipeline.captured_comm = ccomm
 
+    gobj = {}  # replay -> its CUDAGraph (the native plans launch the graphs themselves)
+
     def graph_of(fn):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
             fn()
         held.append(g)
+        gobj[g.replay] = g
         return g.replay
 
     def chained(rep):
@@ -705,8 +708,10 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         # exchange s = t + xd is issued at iteration t: its phase is (t + xd) % P
         s = t + xd
         parts = tr.mx_exchange(s, locs[(s + 1) % NB])
-        gx[s % P] = {"pack": graph_of(parts["pack"]),
-                     "comm": chained(graph_of(parts["comm"])) if ccomm else parts["comm"],
+        gpack = graph_of(parts["pack"])  # (captured in issue order: pack, all-to-all, ...)
+        gcomm = graph_of(parts["comm"]) if ccomm else None
+        gx[s % P] = {"pack": gpack,
+                     "comm": chained(gcomm) if ccomm else parts["comm"], "gcomm": gcomm,
                      "resolve": graph_of(parts["resolve"]), "apply": graph_of(parts["apply"]),
                      "post": parts["post"]}
     prep_fns[:] = gp
@@ -715,7 +720,72 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
     for _ in range(P):
         iterate()
     torch.cuda.synchronize()
-    return iterate, True
+    native = (os.environ.get("PSAMD_MX_NATIVE", "1") == "1" and ccomm and cchain.on
+              and cchain.ev is not None)
+    if not native:
+        return iterate, True
+    # one native LaunchList per t % E replays an iteration's graphs (worker, preparation,
+    # pack, all-to-all, resolve, apply) with its event waits and records in ONE host call
+    # instead of ~25 Python-level stream / event / replay calls (the HIP calls themselves
+    # remain: ~8 us per graph launch, ~2.5 per event op, cProfile r5hostprof). 2 peers
+    # 0.0963-0.0980 vs 0.0967-0.1123 ms, 8 peers 0.1004-0.1032 (one 0.133) vs 0.0989-0.1125
+    # (profiles/r5_mx_native_ab.log; PSAMD_MX_NATIVE=0: the Python iteration)
+    from parameter_server_amd.ops.native import hipops
+
+    H = hipops()
+    for e in [x for k in ev for x in ev[k]] + ev_buf + ev_prep:
+        e.record(main)  # (create every event; each wait still follows its real record)
+    torch.cuda.synchronize()
+    plans = []
+    for k in range(E):
+        t = state["t"] + ((k - state["t"]) % E)  # the next t with t % E == k
+        s = t + xd
+        cur, nb = t % NB, (t + nprep) % NB
+        L = H.LaunchList()
+        L.add_stream(main)
+        L.add_wait(ev["M"][t % E])
+        L.add_graph(gobj[gw[t % P]])
+        L.add_record(ev["w"][t % E])
+        L.add_record(ev_buf[cur])
+        L.add_stream(sides[nb % nprep])
+        L.add_wait(ev_buf[nb])
+        L.add_graph(gobj[gp[nb]])
+        L.add_record(ev_prep[nb])
+        xp = gx[s % P]
+        L.add_stream(sides[((s + 1) % NB) % nprep])
+        L.add_graph(gobj[xp["pack"]])
+        L.add_wait(ev["w"][(s - d) % E])
+        L.add_wait(ev["res"][(s - 1) % E])
+        L.add_wait(cchain.ev)
+        L.add_graph(gobj[xp["gcomm"]])
+        L.add_record(cchain.ev)
+        L.add_record(ev["M"][s % E])
+        L.add_wait(ev["app"][(s - 1) % E])
+        if xp["post"]:
+            L.add_graph(gobj[xp["resolve"]])
+            L.add_record(ev["res"][s % E])
+            L.add_graph(gobj[xp["apply"]])
+        else:
+            L.add_graph(gobj[xp["apply"]])
+            L.add_graph(gobj[xp["resolve"]])
+            L.add_record(ev["res"][s % E])
+        L.add_record(ev["app"][s % E])
+        L.add_stream(main)
+        plans.append(L)
+
+    def iterate_native():
+        t = state["t"]
+        plans[t % E].run()
+        tr.mx_done(B)
+        cchain.n += 1
+        tr._mx_next = t + xd + 1
+        state["t"] = t + 1
+
+    iterate_native.release = release
+    for _ in range(P):
+        iterate_native()
+    torch.cuda.synchronize()
+    return iterate_native, True
 
 
 def spawn_ranks(n: int, argv: list[str] | None = None, script: str | None = None) -> int:

@@ -1180,6 +1180,19 @@ PYBIND11_MODULE(_hipops, m) {
         l.keep.push_back(event);
         l.push_op([e](hipStream_t& s) { PSAMD_HIP_CHECK(hipEventRecord(e, s)); }, "record");
       })
+      // replay of a captured torch.cuda.CUDAGraph (the list keeps the graph alive):
+      // hipGraphLaunch of its executable graph on the list's current stream. Only for
+      // graphs whose kernels draw nothing from torch's RNG (torch's replay() also
+      // advances the captured generator offsets; ours use their own counters)
+      .def("add_graph", [](LaunchList& l, py::object graph) {
+        const py::object h = graph.attr("raw_cuda_graph_exec")();
+        if (!py::isinstance<py::int_>(h))
+          throw std::invalid_argument("add_graph: raw_cuda_graph_exec() is not an int handle");
+        const hipGraphExec_t ex = reinterpret_cast<hipGraphExec_t>(h.cast<uint64_t>());
+        if (!ex) throw std::invalid_argument("add_graph: graph not instantiated");
+        l.keep.push_back(graph);
+        l.push_op([ex](hipStream_t& s) { PSAMD_HIP_CHECK(hipGraphLaunch(ex, s)); }, "graph");
+      })
       // the ops of another list, SHARED (a generator's row cursor advances for both)
       .def("extend", [](LaunchList& l, const LaunchList& o) {
         l.ops.insert(l.ops.end(), o.ops.begin(), o.ops.end());

@@ -61,7 +61,11 @@ def _weights(tr):
     ("prep", 3, 1, {"exchange_merge": "on", "consistency": "ssp:3"}),
     ("prep", 3, 1, {"exchange_merge": "on", "fixing_float_bytes": 2}),
     ("prep", 3, 1, {"exchange_merge": "on", "push_mode": "aggregate"}),
-    ("prep", 3, 1, {"exchange_merge": "on", "_env": {"PSAMD_CAPTURE_COMM": "0"}})])
+    ("prep", 3, 1, {"exchange_merge": "on", "_env": {"PSAMD_CAPTURE_COMM": "0"}}),
+    # ... and its graphs replayed from one native launch list per iteration
+    ("prep", 3, 1, {"exchange_merge": "on", "_env": {"PSAMD_MX_NATIVE": "1"}}),
+    ("prep", 2, 1, {"exchange_merge": "on", "consistency": "ssp:2",
+                    "_env": {"PSAMD_MX_NATIVE": "1"}})])
 def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     from parameter_server_amd.ops.synthetic import criteo_batch
 
