@@ -740,17 +740,17 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
     for k in range(E):
         t = state["t"] + ((k - state["t"]) % E)  # the next t with t % E == k
         s = t + xd
-        cur, nb = t % NB, (t + nprep) % NB
+        nb = (t + nprep) % NB
         L = H.LaunchList()
         L.add_stream(main)
         L.add_wait(ev["M"][t % E])
         L.add_graph(gobj[gw[t % P]])
         L.add_record(ev["w"][t % E])
-        L.add_record(ev_buf[cur])
         L.add_stream(sides[nb % nprep])
-        L.add_wait(ev_buf[nb])
+        # (buffer nb was last trained at t + nprep - NB: its worker-done event is the
+        # buffer event; nothing waits for a preparation's own event after the setup)
+        L.add_wait(ev["w"][(t + nprep - NB) % E])
         L.add_graph(gobj[gp[nb]])
-        L.add_record(ev_prep[nb])
         xp = gx[s % P]
         L.add_stream(sides[((s + 1) % NB) % nprep])
         L.add_graph(gobj[xp["pack"]])
