@@ -785,6 +785,7 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
     for _ in range(P):
         iterate_native()
     torch.cuda.synchronize()
+    args.native_iter = True  # (reported as config.native_iteration)
     return iterate_native, True
 
 

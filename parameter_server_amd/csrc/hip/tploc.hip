@@ -1353,7 +1353,8 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
   const int lim = (int)(n - base < (1 << lts) ? n - base : (1 << lts));
   const int cnt = min(kTile, max(0, dcnt[blockIdx.x]));
   const int64_t r0 = rows[base], r1 = rows[base + lim - 1];  // (uniform loads)
-  // occurrence = (row - r0) << 16 | tile entry (rows of a tile < 2^14, entries < 2^13)
+  // occurrence = (row - r0) << 13 | tile entry (entries < 2^13; a tile's row span, empty
+  // rows included, < 2^19 - 1: the host routes B >= kCsrMaxRows elsewhere)
   uint32_t er[kPer];
   float v[kPer];
   {  // 8 consecutive occurrences per thread: 16 / 32-byte loads, adjacent across lanes
@@ -1364,7 +1365,7 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
       const int64_t i = in ? i0 + j : base;
       const uint32_t ee = rep[i];
       const int32_t rr = rows[i];
-      er[j] = in ? (uint32_t)(rr - r0) << 16 | ee : kNone;
+      er[j] = in ? (uint32_t)(rr - r0) << 13 | ee : kNone;
       v[j] = in ? (vals ? vals[i] : 1.f) : 0.f;
     }
   }
@@ -1394,14 +1395,14 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         if (er[j] == kNone) continue;
-        const uint32_t rr = er[j] >> 16;
+        const uint32_t rr = er[j] >> 13;
         if (rr != cur) {
           if (cur != kNone && (int)cur >= wa && (int)cur < wb && sum != 0.f)
             atomicAdd(&crow[cur - wa], sum);
           cur = rr;
           sum = 0.f;
         }
-        sum += wl[er[j] & 0xffffu] * v[j];
+        sum += wl[er[j] & 0x1fffu] * v[j];
       }
       if (cur != kNone && (int)cur >= wa && (int)cur < wb && sum != 0.f)
         atomicAdd(&crow[cur - wa], sum);
@@ -1447,6 +1448,24 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
     }
     __syncthreads();
   }
+  {  // empty rows (no occurrence) outside every tile's [first row, last row]: the gap
+     // between the previous tile's last row and this tile's first (tile 0: from row 0)
+     // and, in the last tile, the rows after its last one. Margin 0.
+    const int64_t g0 = blockIdx.x == 0 ? 0 : (int64_t)rows[base - 1] + 1;
+    const int64_t na = r0 > g0 ? r0 - g0 : 0;  // [g0, r0) (none when a row spans the cut)
+    const int64_t nb = base + lim >= n && B > r1 + 1 ? B - (r1 + 1) : 0;  // (r1, B)
+    for (int64_t i = t; i < na + nb; i += kThr) {
+      const int64_t rr = i < na ? g0 + i : r1 + 1 + (i - na);
+      const float lab = labels[rr];
+      float loss, c, c2;
+      loss_terms(0.f, lab, loss_type, loss, c, c2);
+      coef_out[rr] = c;
+      loss_acc += loss;
+      corr_acc += (lab > 0.f) == false ? 1.f : 0.f;
+      rows_acc += 1.f;
+      if (hist) atomicAdd(&lhist[auc_bin(0.f, lab, nbins)], 1u);
+    }
+  }
   // coef of an occurrence's row: the window in LDS (one window), else the row's coef as
   // this workgroup wrote it to coef_out (sc0 for a row an earlier tile owns)
   const bool one = nr <= kCsrRows;
@@ -1458,7 +1477,7 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
   float vmax = 0.f;
 #pragma unroll
   for (int j = 0; j < kPer; ++j)
-    if (er[j] != kNone) vmax = fmaxf(vmax, fabsf(coef_of(er[j] >> 16) * v[j]));
+    if (er[j] != kNone) vmax = fmaxf(vmax, fabsf(coef_of(er[j] >> 13) * v[j]));
   fx_tile_max(vmax, &smax);
   if (metrics && rows_acc > 0.f) {
     atomicAdd(&sacc[0], loss_acc);
@@ -1486,8 +1505,8 @@ tp_fwd_bwd_csr_kernel(const uint16_t* __restrict__ rep, const int32_t* __restric
 #pragma unroll
   for (int j = 0; j < kPer; ++j)
     if (er[j] != kNone) {
-      const float c = coef_of(er[j] >> 16);
-      if (c != 0.f) fx_add(acc, er[j] & 0xffffu, c * v[j], sc);
+      const float c = coef_of(er[j] >> 13);
+      if (c != 0.f) fx_add(acc, er[j] & 0x1fffu, c * v[j], sc);
     }
   __syncthreads();
   const double isc = ldexp(1.0, -k2);

@@ -51,6 +51,20 @@ from ..utils.trace import enabled as trace_enabled
 from ..utils.trace import trace_range
 
 
+# tp_fwd_bwd_csr encodes an occurrence's row as its offset from the tile's first row in 19
+# bits: minibatches of this many rows or more take the compact path
+_CSR_MAX_ROWS = (1 << 19) - 1
+
+
+def _same_workspace(a, b) -> bool:
+    """Two localisations share device workspaces (the same Localizer buffer set)."""
+    if a is b:
+        return True
+    ua, ub = getattr(a, "uniq", None), getattr(b, "uniq", None)
+    return (isinstance(ua, torch.Tensor) and isinstance(ub, torch.Tensor) and ua.numel() > 0
+            and ua.device == ub.device and ua.data_ptr() == ub.data_ptr())
+
+
 @dataclass
 class SparseLRConfig:
     num_features: int = 10 ** 9          # hashed feature space (keys in [0, N)); 0 = raw u64
@@ -316,7 +330,7 @@ class SparseLRTrainer:
                 self._flat_step(loc, labels, B, width, next_loc,
                                 pre == (id(loc), loc.gen))
                 return
-            if (prefetch is None and B < (1 << 25) and (loc is None or getattr(loc, "flat", False))
+            if (prefetch is None and B < _CSR_MAX_ROWS and (loc is None or getattr(loc, "flat", False))
                     and (row_ptr is not None or vals is not None)):
                 # valued and / or variable-width rows: the same flat step with the CSR
                 # fused forward + tile backward (tp_fwd_bwd_csr)
@@ -683,7 +697,7 @@ class SparseLRTrainer:
         if width is None and row_ptr is None:
             width = self.cfg.max_nnz_per_example
         flat = getattr(loc, "flat", False)
-        csr = flat and (row_ptr is not None or vals is not None)  # CSR fused fwd/bwd
+        csr = flat and (row_ptr is not None or vals is not None) and B < _CSR_MAX_ROWS
         if flat and not ((csr or (row_ptr is None and rows is None and vals is None
                                   and self._flat_ok(B, width, loc.nnz)))
                          and hipops().tpf_exchange_ok(loc.nnz, self.bits, self.G)):
@@ -926,20 +940,27 @@ class SparseLRTrainer:
         carries keys(u), and then runs the worker half of step u-1 (its weights came
         with that exchange). So a call trains the PREVIOUS minibatch; ``flush()`` (and
         ``progress()``) trains the last one and applies every outstanding push. The
-        minibatch tensors are captured (labels / row_ptr / vals copied)."""
-        if prefetch is not None:
-            prefetch()
+        minibatch tensors are captured (labels / row_ptr / vals copied).
+
+        A caller-supplied ``loc`` lives in a workspace the caller refills (``localize(k,
+        buf=...)``): the pending minibatch keeps a copy of its keys, and when the caller's
+        localisation of this minibatch reused the pending one's workspace, the pending
+        minibatch is localised again into a private workspace before its worker half.
+        ``prefetch`` runs after that worker half is enqueued (it may refill the pending
+        minibatch's workspace)."""
         cur = None
+        pend = self._mx_pend
         if not idle:
             B = labels.numel()
             if width is None and row_ptr is None:
                 width = self.cfg.max_nnz_per_example
-            buf = self._xt + (self._mx_pend is not None)  # step index of this minibatch
-            if loc is None:
-                flat_ok = (self.localize_mode == "tpf"
-                           and (row_ptr is not None or vals is not None
-                                or (rows is None and self._flat_ok(B, width, keys.numel())))
-                           and hipops().tpf_exchange_ok(keys.numel(), self.bits, self.G))
+            buf = self._xt + (pend is not None)  # step index of this minibatch
+            flat_ok = (self.localize_mode == "tpf"
+                       and ((row_ptr is not None or vals is not None) and B < _CSR_MAX_ROWS
+                            or (rows is None and self._flat_ok(B, width, keys.numel())))
+                       and hipops().tpf_exchange_ok(keys.numel(), self.bits, self.G))
+            own = loc is None
+            if own:
                 loc = (self.localize(keys, buf=buf % 2) if flat_ok
                        else self._compact_localizer(buf % 2)(keys))
             if row_ptr is not None and rows is None:
@@ -947,11 +968,33 @@ class SparseLRTrainer:
                         if self.gpu else self._csr_rows(row_ptr, keys.numel()))
             cur = dict(loc=loc, labels=labels.clone(), width=width,
                        row_ptr=None if row_ptr is None else row_ptr.clone(),
-                       vals=None if vals is None else vals.clone(), rows=rows, B=B)
-        u = self._xt + (self._mx_pend is not None)
+                       vals=None if vals is None else vals.clone(), rows=rows, B=B,
+                       keys=None if own else keys.clone(), flat=flat_ok)
+            if pend is not None and not pend.get("idle") and pend.get("keys") is not None \
+                    and _same_workspace(pend["loc"], loc):
+                # the caller localised this minibatch over the pending one's workspace:
+                # localise the pending keys again, into a workspace the caller never sees
+                pend["loc"] = self._mx_private_loc(pend["keys"], pend["flat"])
+        u = self._xt + (pend is not None)
         self._mx_run_exchange(u - 1, None if cur is None else cur["loc"])
         self._mx_finish_pending()
         self._mx_pend = cur if cur is not None else {"idle": True}
+        if prefetch is not None:
+            prefetch()
+
+    def _mx_private_loc(self, keys, flat: bool):
+        """Merged sequential API: a localisation in a workspace of the trainer's own (not
+        reachable through ``localize``), for a pending minibatch whose caller-supplied
+        workspace was refilled."""
+        own = self.__dict__.setdefault("_mx_own", {})
+        lz = own.get(flat)
+        if lz is None:
+            lz = own[flat] = (Localizer(self.max_nnz, self.bits, self.device,
+                                        mode=self.localize_mode, lazy_cols=True,
+                                        sorted_keys=self._flat_x) if flat
+                              else Localizer(self.max_nnz, self.bits, self.device, mode="tp",
+                                             lazy_cols=True))
+        return lz(keys)
 
     def _mx_finish_pending(self):
         p, self._mx_pend = self._mx_pend, None
@@ -1747,33 +1790,52 @@ class SparseLRTrainer:
         self.table.update(s, g, self.rule, self.stats)
 
     # ------------------------------------------------------------ reporting
-    def check_ok(self):
+    def check_ok(self, collective: bool | None = None):
         """Host sync: raise if any device-side capacity was exceeded since the start --
         the table (full: a key could not be inserted), a localisation workspace (a tile
         or bucket overflowed its LDS hash or its fixed entry region: the step kernels
         would have dropped those occurrences' gradients and read stale weights) or the
         padded exchange rows. All error words are sticky, so a check at any later point
         still sees an overflow. Called by ``progress()`` and by bench.py after timing
-        (same fail-loudly rule as the exchange overflow, ``_x_poll_overflow``)."""
+        (same fail-loudly rule as the exchange overflow, ``_x_poll_overflow``).
+
+        With G > 1 (``collective`` default) the three error classes are max-all-reduced
+        first, so every rank raises together: a rank-local raise would leave its peers
+        blocked in their next collective until the communicator timeout."""
         if not self.gpu:
             return
-        lzs = list(self._localizers) + list(self._compact or [])
-        words = [self.table._err] + [lz.err for lz in lzs if getattr(lz, "err", None) is not None]
+        lzs = [lz for lz in list(self._localizers) + list(self._compact or [])
+               + list(getattr(self, "_mx_own", {}).values())
+               if getattr(lz, "err", None) is not None]
+        words = [self.table._err] + [lz.err for lz in lzs]
         if self.xc is not None and getattr(self.xc, "ovf", None) is not None:
             words.append(self.xc.ovf)
-        v = torch.cat([w.reshape(-1)[:1] for w in words]).cpu().tolist()
-        if v[0]:
+        v = torch.cat([w.reshape(-1)[:1].to(torch.int64) for w in words])
+        nl = len(lzs)
+        # [table full, OR-ish (max) of the localisation error bits, exchange overflow]
+        summary = torch.stack([v[0], v[1:1 + nl].max() if nl else v[0] * 0,
+                               v[-1] if len(words) > 1 + nl else v[0] * 0])
+        if collective is None:
+            collective = self.G > 1
+        if collective:
+            summary = self.comm.all_reduce_(
+                summary.to(self.comm.device) if self.comm.backend == "nccl" else summary.cpu(),
+                op="max")
+        tab, loc_e, ovf = summary.cpu().tolist()
+        local = v.cpu().tolist()
+        if tab:
             raise RuntimeError("KVTable full: increase table_capacity (keys were not inserted)")
-        for lz, e in zip([lz for lz in lzs if getattr(lz, "err", None) is not None], v[1:]):
-            if e:
-                raise RuntimeError(
-                    f"localize_{lz.mode} overflow (error bits {e:#x}): a tile or bucket "
-                    f"exceeded its LDS hash / entry region, so some occurrences were dropped "
-                    f"from the step; the minibatch is too skewed for the {lz.mode} layout "
-                    f"(PSAMD_FLAT=0 or localize='sort')")
-        if self.xc is not None and getattr(self.xc, "ovf", None) is not None and v[-1]:
+        if loc_e:
+            bad = [lz.mode for lz, e in zip(lzs, local[1:1 + nl]) if e]
+            mode = bad[0] if bad else "tpf/tp (on a peer rank)"
             raise RuntimeError(
-                f"exchange overflow: {v[-1]} keys exceeded the per-peer capacity {self.xc.C}; "
+                f"localize_{mode} overflow (error bits {loc_e:#x}): a tile or bucket "
+                f"exceeded its LDS hash / entry region, so some occurrences were dropped "
+                f"from the step; the minibatch is too skewed for the {mode} layout "
+                f"(PSAMD_FLAT=0 or localize='sort')")
+        if ovf:
+            raise RuntimeError(
+                f"exchange overflow: {ovf} keys exceeded the per-peer capacity {self.xc.C}; "
                 f"set exchange_capacity or exchange_slack higher, or exchange='exact'")
 
     def progress(self, reset: bool = True) -> dict:

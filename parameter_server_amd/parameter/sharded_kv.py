@@ -309,7 +309,7 @@ class KVWorker:
         of the signature: a setup call, not a per-step one)."""
         from ..ops.fixing_float import key_signature
 
-        self.check()
+        self._local_check()
         keys = self._keys(keys)
         sig = key_signature(keys) if keys.numel() else 0
         old = next((h for h in self._handles
@@ -335,7 +335,9 @@ class KVWorker:
             self._register(keys, h)
 
         self.wait(self._run(op))
-        self.check(sync=True)  # (a setup call: a full row would break the handle for good)
+        # (a setup call: a full row would break the handle for good; collective like the
+        # registration itself, so every rank raises together)
+        self.check(sync=True, collective=True)
         return h
 
     def release(self, h: KeyHandle) -> None:
@@ -389,7 +391,7 @@ class KVWorker:
         """Values of ``keys`` (any order, duplicates allowed; or a ``KeyHandle`` from
         ``register_keys``) -> timestamp; ``wait`` returns ``[n]`` (dim 1) or ``[n, dim]``
         float32 values in request order."""
-        self.check()
+        self._local_check()
         if isinstance(keys, KeyHandle):
             self._check_handle(keys)
             if not self.clock.admissible(self._pushes):
@@ -491,7 +493,7 @@ class KVWorker:
         """Send ``vals`` (``[n]`` or ``[n, dim]``) for ``keys`` (or a ``KeyHandle``:
         key-less rows against the owners' cached slots); duplicates are summed before
         the server op. Returns the timestamp."""
-        self.check()
+        self._local_check()
         if isinstance(keys, KeyHandle):
             self._check_handle(keys)
             h = keys
@@ -645,10 +647,22 @@ class KVWorker:
                 srv.vals[slot[:n]] = torch.where(ok, v, srv.vals[slot[:n]])
 
     def wait(self, ts: int):
-        """Order the caller's stream after op ``ts``; pulled values (or None)."""
+        """Order the caller's stream after op ``ts``; pulled values (or None).
+
+        One process (G == 1 or the loopback emulation): an overflow published by a
+        completed pack raises here. With peer processes the check is deferred to the
+        next collective check (``flush()`` / ``barrier()``), where every rank raises
+        together: a rank-local raise here would leave the peers blocked in their next
+        all-to-all until the communicator timeout."""
         out = self._wait_nocheck(ts)
-        self.check()  # (an overflow published by a completed pack raises here)
+        self._local_check()
         return out
+
+    def _local_check(self):
+        """The non-collective overflow check of push / pull / wait: only where no peer
+        process waits in a collective (one rank, or the loopback emulation)."""
+        if self.G == 1 or getattr(self.comm, "backend", "") == "loopback":
+            self.check()
 
     def _wait_nocheck(self, ts: int):
         out, ev = self._done.pop(ts)
@@ -669,12 +683,15 @@ class KVWorker:
         return out
 
     def barrier(self):
+        """Collective: the caller's stream after every issued op, then the overflow
+        check of all ranks (every rank raises together)."""
         if self.gpu:
             cur = torch.cuda.current_stream(self.device)
             cur.wait_stream(self.stream)
             if self.apply_stream is not None:
                 cur.wait_stream(self.apply_stream)
         self.comm.barrier()
+        self.check(sync=True, collective=True)
 
     def staleness(self) -> int:
         """Pushes a pull issued now would miss (0 for bsp, <= tau for ssp)."""

@@ -36,6 +36,9 @@ def _gpu_worker(rank, world, port, out_dir, cfg_kw, steps, pipelined=False):
     if not pipelined:
         for k, l in batches:
             tr.step(k, l)
+    elif pipelined == "buf0":  # every minibatch localised into the default workspace
+        for k, l in batches:
+            tr.step(k, l, loc=tr.localize(k))
     else:  # bench.py's multi-GPU loop: localise t+1 on a side stream during step t
         side = torch.cuda.Stream(dev)
 
@@ -82,6 +85,29 @@ def test_two_rank_gpu_protocol_matches_reference(tmp_path, ff_bytes, pipelined, 
     assert merged.keys() == ref.keys()
     tol = 1e-5 if ff_bytes == 0 else 2e-3
     assert max(abs(merged[k] - ref[k]) for k in ref) < tol
+
+
+@pytest.mark.parametrize("pattern", ["side", "buf0"])
+@pytest.mark.parametrize("localize", ["tpf", "tp"])
+def test_merged_exchange_caller_localisations(tmp_path, pattern, localize):
+    """ssp:2 runs the merged one-collective exchange, whose sequential API trains the
+    PREVIOUS minibatch on each step() call. Caller-supplied localisations (the
+    prefetch-on-a-side-stream pattern over 2 workspaces, and every minibatch in the
+    default workspace) must not corrupt the pending minibatch: same weights as the
+    stale-pull protocol reference at lag 2."""
+    cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
+                  consistency="ssp:2", localize=localize)
+    port = _free_port()
+    mp.spawn(_gpu_worker, args=(2, port, str(tmp_path), cfg_kw, 6, pattern), nprocs=2,
+             join=True)
+    res = [torch.load(tmp_path / f"g{r}.pt", weights_only=False) for r in range(2)]
+    merged = {}
+    for r in res:
+        for k, w in zip(r["state"]["keys"].tolist(), r["state"]["w"].tolist()):
+            merged[k] = w
+    ref = _reference(cfg_kw, 6, 2, lag=2)
+    assert merged.keys() == ref.keys()
+    assert max(abs(merged[k] - ref[k]) for k in ref) < 1e-5
 
 
 @pytest.mark.parametrize("exchange,consistency,world", [

@@ -312,6 +312,42 @@ def _ovf_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+def _ovf_wait_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from parameter_server_amd.ops.keymix import unmix
+    from parameter_server_amd.parallel.comm import DistComm
+
+    n = 2048
+    kv = KVWorker(DistComm("cpu"), "cpu", capacity=1 << 14, max_keys=n, key_bits=64)
+    keys = unmix(torch.arange(n if rank == 0 else 64, dtype=torch.int64), 64)
+    waited = True
+    try:  # rank 0's push overflows; its wait() must not raise alone
+        kv.wait(kv.push(keys, torch.ones(keys.numel())))
+        kv.wait(kv.pull(keys[:64]))  # the peers' next collective still completes
+    except RuntimeError:
+        waited = False
+    raised = False
+    try:
+        kv.barrier()
+    except RuntimeError as e:
+        raised = "overflow" in str(e)
+    torch.save({"waited": waited, "raised": raised}, os.path.join(out_dir, f"w{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_gloo_wait_overflow_deferred_to_collective_check(tmp_path):
+    """with peer processes wait() defers the overflow check, and the next
+    collective check (barrier / flush) raises on EVERY rank."""
+    port = _port()
+    mp.spawn(_ovf_wait_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    res = [torch.load(tmp_path / f"w{r}.pt", weights_only=False) for r in range(2)]
+    assert all(r["waited"] for r in res), res
+    assert all(r["raised"] for r in res), res
+
+
 def test_gloo_flush_overflow_raises_on_every_rank(tmp_path):
     """flush() must not run a rank-local overflow check before its collective
     one, or the overflowing rank raises alone and its peers hang in the host gather."""

@@ -207,6 +207,8 @@ def _reference_train(batches, rule, bits):
         m = W[idx].view(B, width).double().sum(1).float()
         yy = torch.where(y > 0, 1.0, -1.0)
         coef = -yy * torch.sigmoid(-yy * m)
+        if losses is not None:
+            losses.append(float(torch.nn.functional.softplus(-yy * m).sum()))
         g = torch.zeros(K, dtype=torch.float64).index_add_(
             0, idx, coef.double().repeat_interleave(width)).float() * rule.grad_scale
         u = torch.unique(idx)
@@ -499,8 +501,9 @@ def _csr_batch(B: int, seed: int, lo: int = 5, hi: int = 145, valued: bool = Tru
             None if vals is None else vals.to(DEV))
 
 
-def _reference_train_csr(batches, rule):
-    """Plain fp32 PyTorch loop over CSR minibatches (valued), one update per minibatch."""
+def _reference_train_csr(batches, rule, losses=None):
+    """Plain fp32 PyTorch loop over CSR minibatches (valued), one update per minibatch.
+    ``losses``: a list that gets each minibatch's summed logistic loss."""
     allk = torch.unique(torch.cat([b[0].cpu() for b in batches]))
     K = allk.numel()
     W, Z, Nn = torch.zeros(K), torch.zeros(K), torch.zeros(K)
@@ -513,6 +516,8 @@ def _reference_train_csr(batches, rule):
         m = torch.zeros(B, dtype=torch.float64).index_add_(0, row, (W[idx] * x).double()).float()
         yy = torch.where(y > 0, 1.0, -1.0)
         coef = -yy * torch.sigmoid(-yy * m)
+        if losses is not None:
+            losses.append(float(torch.nn.functional.softplus(-yy * m).sum()))
         g = torch.zeros(K, dtype=torch.float64).index_add_(0, idx, (coef[row] * x).double()).float()
         u = torch.unique(idx)
         gu, w_old = g[u] * rule.grad_scale, W[u]
@@ -554,6 +559,48 @@ def test_flat_csr_step_matches_fp32_reference(monkeypatch, B, valued, long_row):
     torch.testing.assert_close(z, Z, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(n, Nn, rtol=1e-4, atol=1e-4)
     assert (w != 0).sum() > 50
+
+
+def test_flat_csr_empty_rows_are_counted(monkeypatch):
+    """rows with no features (label-only lines) before the first non-empty
+    row, after the last one, in long runs and at tile cuts are still examples: margin 0,
+    counted once in loss / examples. Weights still match the fp32 loop."""
+    monkeypatch.setenv("PSAMD_FLAT", "1")
+    B = 6000
+    batches = []
+    for s in range(4):
+        k, lab, rp, v = _csr_batch(B, 400 + s)
+        w = (rp[1:] - rp[:-1]).cpu()
+        g = torch.Generator().manual_seed(s)
+        w[torch.rand(B, generator=g) < 0.15] = 0  # scattered empties (some at tile cuts)
+        w[:7] = 0                                  # leading
+        w[-11:] = 0                                # trailing
+        w[2000:2900] = 0                           # a long run
+        rp2 = torch.zeros(B + 1, dtype=torch.int64)
+        rp2[1:] = torch.cumsum(w, 0)
+        # keep each row's first w[r] keys of the original row
+        old = rp.cpu()
+        idx = torch.cat([torch.arange(int(old[r]), int(old[r]) + int(w[r])) for r in range(B)])
+        batches.append((k[idx.to(DEV)].contiguous(), lab, rp2.to(DEV),
+                        v[idx.to(DEV)].contiguous()))
+    maxn = max(int(b[2][-1]) for b in batches)
+    cfg = SparseLRConfig(num_features=10 ** 8, minibatch=B,
+                         max_nnz_per_example=(maxn + B - 1) // B + 1, table_capacity=1 << 22,
+                         alpha=0.05, l1=1.0, l2=0.1)
+    tr = SparseLRTrainer(cfg, device=DEV)
+    assert tr.localize_mode == "tpf"
+    for k, lab, rp, v in batches:
+        tr.step(k, lab, row_ptr=rp, vals=v)
+    torch.cuda.synchronize()
+    assert tr._compact is None
+    p = tr.progress()
+    assert p["examples"] == 4 * B, p
+    losses = []
+    allk, W, Z, Nn = _reference_train_csr(batches, cfg.update_rule(), losses)
+    assert abs(p["loss"] - sum(losses) / (4 * B)) < 1e-4, (p, sum(losses) / (4 * B))
+    w, z, n = _table_by_raw_key(tr, allk)
+    torch.testing.assert_close(w, W, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(n, Nn, rtol=1e-4, atol=1e-4)
 
 
 def test_flat_fixed_width_valued_rows_take_the_csr_kernel(monkeypatch):
