@@ -168,7 +168,11 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     # tail apply; not with the tail filter: its CountMin and keep-mask scratch are shared
     # by the key packs of consecutive exchanges). Otherwise the whole exchange half waits
     # first and replays as ONE captured graph (pack + all-to-all A + owner work + B).
-    early = (post or asp_apply == "tail") and tr.filter is None
+    early = (post or asp_apply == "tail") and (tr.filter is None or tr._flat_x)
+    # tail filter: the CountMin inserts and queries of consecutive minibatches run in
+    # minibatch order (the reference's MinibatchReader::read sequence), so a preparation
+    # also waits for the previous minibatch's preparation (on another stream)
+    fchain = tr.filter is not None
     E = 64  # event rings, indexed by step (every look-back here is < 64 steps)
     ev_buf = [torch.cuda.Event() for _ in range(NB)]   # worker done with buffer b
     ev_w = [torch.cuda.Event() for _ in range(E)]      # worker half of step t done
@@ -300,6 +304,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
         # waits for step t-1, so it runs beside step t and not in a burst with the other
         # streams' preparations (the first timed steps after an idle GPU)
         s.wait_event(ev_buf[(t - 1) % NB] if prep_gate else ev_buf[nb])
+        if fchain:
+            s.wait_event(ev_prep[(nb - 1) % NB])
         # a plain set_stream there and back (main is current here): the torch.cuda.stream
         # context re-queries the current stream and the lazy-init state on every use, ~10
         # us of host time per step (cProfile, profiles/r3_s3_host_issue.log)
@@ -317,6 +323,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
         e.record(main)
     for b in range(nprep):  # minibatches 0 .. nprep-1
         with torch.cuda.stream(sides[b]):
+            if fchain and b:
+                sides[b].wait_event(ev_prep[b - 1])
             prep(b)
             ev_prep[b].record(sides[b])
     if xmode == "own":
@@ -353,6 +361,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
             L.add_record(ev_buf[cur])
             L.add_stream(s)
             L.add_wait(ev_buf[(j - 1) % NB] if prep_gate else ev_buf[nb])
+            if fchain:
+                L.add_wait(ev_prep[(nb - 1) % NB])
             L.extend(fplans[nb].plan)
             L.add_record(ev_prep[nb])
             phases.append((L.run, locs[nxt], fplans[nb].done))
@@ -619,6 +629,7 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
             set_stream(main)
 
     state = {"t": 0}
+    fchain = tr.filter is not None
 
     def iterate():
         t = state["t"]
@@ -633,6 +644,8 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         nb = (t + nprep) % NB
         s_ = sides[nb % nprep]
         s_.wait_event(ev_buf[nb])
+        if fchain:  # (tail filter: CountMin inserts / queries in minibatch order)
+            s_.wait_event(ev_prep[(nb - 1) % NB])
         set_stream(s_)
         try:
             prep_fns[nb]()
@@ -647,6 +660,8 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         e.record(main)
     for b in range(nprep):
         with torch.cuda.stream(sides[b]):
+            if fchain and b:
+                sides[b].wait_event(ev_prep[b - 1])
             prep(b)
             ev_prep[b].record(sides[b])
     if tr.xc is None:
@@ -750,7 +765,11 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         # (buffer nb was last trained at t + nprep - NB: its worker-done event is the
         # buffer event; nothing waits for a preparation's own event after the setup)
         L.add_wait(ev["w"][(t + nprep - NB) % E])
+        if fchain:
+            L.add_wait(ev_prep[(nb - 1) % NB])
         L.add_graph(gobj[gp[nb]])
+        if fchain:
+            L.add_record(ev_prep[nb])
         xp = gx[s % P]
         L.add_stream(sides[((s + 1) % NB) % nprep])
         L.add_graph(gobj[xp["pack"]])
@@ -938,6 +957,9 @@ def main():
                     help="N > 1, lag >= 1: one all-to-all per step carrying [keys(t+1) | "
                          "pushes | weights of keys(t)] (auto: ssp:tau >= 2) or the "
                          "two-collective exchange (off)")
+    ap.add_argument("--exchange-lag", type=int, default=-1,
+                    help="padded exchange lag (-1: from --consistency; asp on the merged "
+                         "exchange: the staleness, default 3)")
     ap.add_argument("--ssp-apply", default="post", choices=["post", "pre"],
                     help="N > 1, ssp: the owner applies the carried pushes after sending the "
                          "pulled weights back (post) or before resolving the pulls (pre)")
@@ -961,6 +983,10 @@ def main():
     ap.add_argument("--prefill", type=float, default=0,
                     help="insert this many random keys into each shard before timing (the "
                          "populated-table regime, e.g. 5e8 on 2^31 slots = 23%% load)")
+    ap.add_argument("--tail-freq", type=int, default=0,
+                    help="tail-feature filter: train only keys seen > this many times "
+                         "(CountMin, the reference CTR conf's tail_feature_freq: 1); 0 = off")
+    ap.add_argument("--countmin-n", type=float, default=1e8)
     ap.add_argument("--progress", action="store_true")
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check)")
     ap.add_argument("--trace", default="",
@@ -1026,6 +1052,8 @@ def main():
                          fixing_float_bytes=args.fixing_float, exchange=args.exchange,
                          localize=args.localize, push_mode=args.push_mode,
                          ssp_apply=args.ssp_apply, exchange_merge=args.exchange_merge,
+                         tail_feature_freq=args.tail_freq, countmin_n=args.countmin_n,
+                         exchange_lag=args.exchange_lag,
                          seed=rank)
     tr = SparseLRTrainer(cfg, comm, device)
     prefill_occ = None
@@ -1221,6 +1249,7 @@ def main():
                 "exchange": (f"{args.exchange} (capacity {tr.xc.C} keys/peer/step)"
                              if tr.xc is not None else (args.exchange if G > 1 else None)),
                 "prefill_keys_per_gpu": int(args.prefill) if args.prefill > 0 else None,
+                "tail_feature_freq": args.tail_freq or None,
             },
             "comm": {"backend": getattr(comm, "backend", "local"),
                      "world": comm.world,

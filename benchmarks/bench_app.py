@@ -6,7 +6,7 @@ the same minibatches already in HBM.
 
     python benchmarks/bench_app.py --rows 2000000 --files 8 --minibatch 10000 --kind criteo
 
-kind = criteo: 39 binary features per row (13 + 26 slots, power-law ids, "k:1" LIBSVM),
+kind = criteo: 39 binary features per row (power-law ids, "k:1" LIBSVM, zero-padded ids),
        rcv1:   5..145 features per row (~75), tf-idf-like values."""
 from __future__ import annotations
 
@@ -22,11 +22,40 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _write_criteo_fast(path, keys, y, N):
+    """Fixed-width binary rows as fixed-length text built by digit arithmetic (no per-token
+    Python): "+1 00001234:1 ...\n" (zero-padded ids parse as the same integers)."""
+    per, width = keys.shape
+    nd = len(str(N - 1))
+    tok = nd + 3  # digits ":1 "
+    L = 2 + width * tok  # "+1" then " ddd:1" per key, "\n" in the last token's space
+    buf = np.empty((per, L), dtype=np.uint8)
+    buf[:, 0] = np.where(y > 0, ord("+"), ord("-"))
+    buf[:, 1] = ord("1")
+    body = buf[:, 2:].reshape(per, width, tok)
+    body[:, :, 0] = ord(" ")
+    k = keys.copy()
+    for p in range(nd - 1, -1, -1):
+        body[:, :, 1 + p] = ord("0") + (k % 10)
+        k //= 10
+    body[:, :, 1 + nd] = ord(":")
+    body[:, :, 2 + nd] = ord("1")
+    out = np.empty((per, L + 1), dtype=np.uint8)
+    out[:, :L] = buf
+    out[:, L] = ord("\n")
+    out.tofile(path)
+
+
 def write_files(d, kind, rows, files, seed=0, N=10 ** 8):
     rng = np.random.default_rng(seed)
     per = rows // files
     for f in range(files):
         if kind == "criteo":
+            keys = np.sort((N * rng.random((per, 39)) ** 4).astype(np.int64), axis=1)
+            y = np.where(rng.random(per) < 0.3, 1, -1)
+            _write_criteo_fast(os.path.join(d, f"part-{f:03d}"), keys, y, N)
+            continue
+        if kind == "criteo_slow":
             w = np.full(per, 39)
         else:
             w = rng.integers(5, 145, per)
@@ -36,7 +65,7 @@ def write_files(d, kind, rows, files, seed=0, N=10 ** 8):
         order = np.lexsort((keys, row))  # LIBSVM wants non-decreasing ids per row
         keys = keys[order]
         y = np.where(rng.random(per) < 0.3, 1, -1)
-        if kind == "criteo":
+        if kind == "criteo_slow":
             toks = np.char.add(keys.astype(str), ":1")
         else:
             vals = rng.random(n) * 0.9 + 0.1
@@ -54,9 +83,13 @@ def main():
     ap.add_argument("--rows", type=int, default=2_000_000)
     ap.add_argument("--files", type=int, default=8)
     ap.add_argument("--minibatch", type=int, default=10000)
-    ap.add_argument("--kind", default="criteo", choices=["criteo", "rcv1"])
+    ap.add_argument("--kind", default="criteo", choices=["criteo", "criteo_slow", "rcv1"])
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default="")
+    ap.add_argument("--cache", type=int, default=1,
+                    help="1: run twice with a binary example cache (the first run parses the "
+                         "text and writes the cache, the second streams the cache)")
+    ap.add_argument("--io-threads", type=int, default=4)
     a = ap.parse_args()
     import torch
 
@@ -82,19 +115,28 @@ async_sgd {{ algo: FTRL minibatch: {a.minibatch} num_data_pass: 1 report_interva
     dev = torch.device("cuda")
     import types
 
-    flags = types.SimpleNamespace(num_features=1e8, max_nnz_per_example=160 if a.kind == "rcv1" else 39,
-                                  num_threads=a.threads, device="cuda", seed=0, table_capacity=1 << 26,
-                                  quiet=True)
-    res = run_async_sgd(lm, LocalComm(dev), dev, flags)
-    tr = res["trainer"]
-    out = {"bench": "app_file_fed", "kind": a.kind, "rows": res["examples"], "files": a.files,
-           "text_mb": round(mb, 1), "minibatch": a.minibatch, "parser_threads": a.threads,
-           "seconds": round(res["seconds"], 3),
-           "examples_per_s": res["examples"] / res["seconds"],
-           "text_mb_per_s": mb / res["seconds"], "steps": res["steps"],
-           "localize": tr.localize_mode, "flat_csr": tr._compact is None,
-           "loss": res["progress"]["loss"] if res["progress"] else None,
-           "file_gen_s": round(gen_s, 1)}
+    cache = os.path.join(d, "cache") if a.cache else "off"
+    runs = []
+    for r in range(2 if a.cache else 1):
+        flags = types.SimpleNamespace(
+            num_features=1e8, max_nnz_per_example=160 if a.kind == "rcv1" else 39,
+            num_threads=a.threads, device="cuda", seed=0, table_capacity=1 << 26, quiet=True,
+            data_cache=cache, io_threads=a.io_threads, report_steps=0)
+        res = run_async_sgd(lm, LocalComm(dev), dev, flags)
+        tr = res["trainer"]
+        runs.append({"source": "cache" if res["cached_passes"] else "text",
+                     "rows": res["examples"], "steps": res["steps"],
+                     "seconds": round(res["seconds"], 3),
+                     "examples_per_s": res["examples"] / res["seconds"],
+                     "h2d_gb_per_s": res["h2d_bytes"] / res["seconds"] / 1e9,
+                     "loss": res["progress"]["loss"] if res["progress"] else None,
+                     "localize": tr.localize_mode, "flat": tr._compact is None})
+        del tr, res
+        torch.cuda.empty_cache()
+    out = {"bench": "app_file_fed", "kind": a.kind, "files": a.files, "text_mb": round(mb, 1),
+           "minibatch": a.minibatch, "parser_threads": a.threads, "io_threads": a.io_threads,
+           "file_gen_s": round(gen_s, 1), "text_mb_per_s": mb / runs[0]["seconds"],
+           "runs": runs}
     print(json.dumps(out), flush=True)
 
 

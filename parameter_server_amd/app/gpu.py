@@ -51,6 +51,13 @@ def _flags(argv):
     ap.add_argument("-device", "--device", default="auto")
     ap.add_argument("-seed", "--seed", type=int, default=0)
     ap.add_argument("-table_capacity", "--table_capacity", type=int, default=0)
+    # binary example cache (data/bincache.py): "" = $PSAMD_DATA_CACHE, else a private
+    # temporary one when num_data_pass > 1; "off" = parse the text on every pass
+    ap.add_argument("-data_cache", "--data_cache", default="")
+    ap.add_argument("-io_threads", "--io_threads", type=int, default=4)
+    # progress lines every this many steps when the step count is agreed up front (a
+    # fully cached multi-rank run); 0 = 20 lines per run
+    ap.add_argument("-report_steps", "--report_steps", type=int, default=0)
     ap.add_argument("-quiet", "--quiet", action="store_true")
     return ap.parse_args(argv)
 
@@ -101,38 +108,59 @@ def run_async_sgd(lm, comm, device, flags, printer=None) -> dict:
     cfg = lm_to_sparse_lr(lm, **over)
     tr = SparseLRTrainer(cfg, comm, device)
     td = lm.training_data
+    cache_dir, tmp_cache = _cache_dir(flags, sgd.num_data_pass, rank)
     feeder = DeviceFeeder(rank_files(td, G, rank), td.text, cfg.minibatch, tr.max_nnz, device,
                           num_features=N, passes=sgd.num_data_pass, shuffle=sgd.num_data_pass > 1,
                           seed=flags.seed + rank, data_buf_mb=sgd.data_buf,
                           nthreads=flags.num_threads,
                           ignore_slot=True,
                           hadoop_home=td.hdfs.home if td.has("hdfs") else "",
-                          max_lines_per_file=td.max_num_lines_per_file)
+                          max_lines_per_file=td.max_num_lines_per_file,
+                          cache_dir=cache_dir, io_threads=getattr(flags, "io_threads", 4))
     interval = max(1, int(sgd.report_interval))
     printer = printer or (ProgressPrinter() if rank == 0 and not flags.quiet else None)
     t0 = last = time.time()
     it = iter(feeder)
     steps = idle = 0
     last_p = None
+    # a fully cached run knows its minibatch count: the ranks agree on the step count (and
+    # the report steps) ONCE; otherwise they agree every step over the host channel
+    planned = feeder.planned_batches()
+    total = None
+    if G > 1:
+        counts = comm.host_gather_obj(planned)
+        if all(c is not None for c in counts):
+            total = max(counts)
+    elif planned is not None:
+        total = planned
+    every = getattr(flags, "report_steps", 0) or (max(1, -(-total // 20)) if total else 0)
+    t = 0
     while True:
-        b = next(it, None)
-        report = time.time() - last >= interval
-        if G > 1:  # (host channel: every rank steps, reports and stops together)
-            st = comm.host_gather_obj((b is not None, report))
-            if not any(s[0] for s in st):
+        if total is not None:
+            if t >= total:
                 break
-            report = st[0][1]
-        elif b is None:
-            break
+            b = next(it, None)
+            report = (t + 1) % every == 0
+        else:
+            b = next(it, None)
+            report = time.time() - last >= interval
+            if G > 1:  # (host channel: every rank steps, reports and stops together)
+                st = comm.host_gather_obj((b is not None, report))
+                if not any(s[0] for s in st):
+                    break
+                report = st[0][1]
+            elif b is None:
+                break
+        t += 1
         if b is None:
             tr.idle_step()  # out of files: keep serving this shard and flushing pushes
             idle += 1
         else:
-            w = _uniform_width(b)
-            if w:  # one width, binary: the fused fixed-width path
-                tr.step(b.keys, b.labels, width=w)
+            if b.vals is None and b.width:  # one width, binary: the fused fixed-width path
+                tr.step(b.keys, b.labels, width=b.width)
             else:
-                tr.step(b.keys, b.labels, row_ptr=b.row_ptr, vals=b.vals)
+                tr.step(b.keys, b.labels, width=b.width or None, row_ptr=b.row_ptr,
+                        vals=b.vals)
             feeder.release(b)
             steps += 1
         if report:
@@ -148,7 +176,13 @@ def run_async_sgd(lm, comm, device, flags, printer=None) -> dict:
         torch.cuda.synchronize(device)
     dt = time.time() - t0
     out = {"examples": feeder.num_examples, "steps": steps, "idle_steps": idle, "seconds": dt,
-           "progress": p if p["examples"] else last_p, "trainer": tr, "h2d_bytes": feeder.bytes_h2d}
+           "progress": p if p["examples"] else last_p, "trainer": tr, "h2d_bytes": feeder.bytes_h2d,
+           "text_passes": feeder.text_passes, "cached_passes": feeder.cached_passes,
+           "agreed_steps": total}
+    if tmp_cache:
+        import shutil
+
+        shutil.rmtree(tmp_cache, ignore_errors=True)
     mo = lm.model_output
     if lm.has("model_output") and mo.has("file") and mo.format == "TEXT":
         d = os.path.dirname(mo.file[0])
@@ -158,10 +192,19 @@ def run_async_sgd(lm, comm, device, flags, printer=None) -> dict:
     return out
 
 
-def _uniform_width(b) -> int:
-    """Width when every row of the batch has the same number of binary features (the
-    feeder measured it on the host while staging the batch)."""
-    return b.width if b.vals is None else 0
+def _cache_dir(flags, passes: int, rank: int):
+    """(cache dir or None, temporary dir to delete at the end or None)."""
+    d = getattr(flags, "data_cache", "") or os.environ.get("PSAMD_DATA_CACHE", "")
+    if d == "off":
+        return None, None
+    if d:
+        return d, None
+    if passes > 1:  # later passes stream the binary cache of the first
+        import tempfile
+
+        t = tempfile.mkdtemp(prefix=f"psamd_cache_r{rank}_")
+        return t, t
+    return None, None
 
 
 def run_darlin(lm, comm, device, flags, printer=None) -> dict:

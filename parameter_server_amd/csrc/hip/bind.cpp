@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "common.cuh"
+#include "countmin.cuh"
 
 namespace psamd {
 // kv_table.hip
@@ -66,7 +67,8 @@ int tpf_key_region();
 int tpf_entry_region();
 size_t tpf_temp_bytes(int64_t, int);
 void localize_tpf(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint16_t*, uint64_t*,
-                  int32_t*, uint16_t*, int32_t*, int32_t*, bool, hipStream_t);
+                  int32_t*, uint16_t*, int32_t*, int32_t*, bool, hipStream_t, const CmArgs*,
+                  uint8_t*, float*, int64_t);
 bool tpf_exchange_ok(int64_t, int, int);
 void tpf_pack_keys(int64_t, int, int, const int32_t*, const uint64_t*, int64_t, int, int64_t,
                    int32_t*, int32_t*, const uint64_t*, int64_t, int, hipStream_t);
@@ -188,14 +190,14 @@ void criteo_gen(uint64_t, int64_t, const int64_t*, int64_t, int64_t, uint64_t, f
                 float*, int64_t*, hipStream_t);
 void add_i64(int64_t*, int64_t, hipStream_t);
 // filters.hip
-void cm_insert(uint32_t*, uint64_t, int, uint32_t, const uint64_t*, const uint8_t*, int64_t,
+void cm_insert(uint32_t*, uint64_t, int, int, uint32_t, const uint64_t*, const uint8_t*, int64_t,
                const int32_t*, hipStream_t);
-void cm_query(const uint32_t*, uint64_t, int, uint32_t, const uint64_t*, int64_t, const int32_t*,
-              int, int32_t*, uint8_t*, hipStream_t);
+void cm_query(const uint32_t*, uint64_t, int, int, uint32_t, const uint64_t*, int64_t,
+              const int32_t*, int, int32_t*, uint8_t*, hipStream_t);
 void compact_kept(const int32_t*, const int32_t*, int64_t, const int32_t*, int32_t*, int32_t*,
                   int32_t*, const uint64_t*, uint64_t*, hipStream_t);
-void cm_insert_seg(uint32_t*, uint64_t, int, uint32_t, const uint64_t*, const int32_t*, int64_t,
-                   const int32_t*, hipStream_t);
+void cm_insert_seg(uint32_t*, uint64_t, int, int, uint32_t, const uint64_t*, const int32_t*,
+                   int64_t, const int32_t*, hipStream_t);
 void ff_minmax(const float*, int64_t, float*, hipStream_t);
 void ff_encode(const float*, int64_t, const float*, int, uint64_t, uint8_t*, hipStream_t);
 void ff_decode(const uint8_t*, int64_t, const float*, int, float*, hipStream_t);
@@ -552,9 +554,12 @@ void check_tpf(const TpfBufs& f, int64_t n, int bits, const char* what, bool par
   need(f.slot_u, at::kInt, "slot_u", g * psamd::tpf_key_region());
 }
 
+// filt (the fused tail filter, tploc.hip tpf_filter_unit): (cells int32 [the sketch's
+// byte cells as words], rsize, rshift, k, vmax, freq, ecnt uint8 [>= tpf_stride_max(n)],
+// w_ent float32 [the FlatLoc's tile-entry weights])
 Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor dcnt, Tensor rep,
                          Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err,
-                         bool sorted) {
+                         bool sorted, optional<py::tuple> filt = {}) {
   chk(keys, at::kLong, "keys");
   chk(temp, at::kByte, "temp");
   chk(dcnt, at::kInt, "dcnt");
@@ -566,12 +571,46 @@ Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor d
   check(dcnt.numel() >= T && rep.numel() >= n, "localize_tpf: dcnt / rep");
   check((size_t)temp.numel() >= psamd::tpf_temp_bytes(n, bits), "localize_tpf: temp too small");
   const psamd::KeyMix km = make_keymix(bits);
-  return [=, keep = std::vector<Tensor>{keys, temp, dcnt, rep, uniqf, ent_pos, ent_j, cnt,
-                                        err}](hipStream_t st) {
+  std::vector<Tensor> keep{keys, temp, dcnt, rep, uniqf, ent_pos, ent_j, cnt, err};
+  bool has_f = false;
+  psamd::CmArgs ca{};
+  Tensor ecnt, w_ent;
+  if (filt && !filt->is_none()) {
+    const py::tuple& f = *filt;
+    check(f.size() == 8, "localize_tpf filt: (cells, rsize, rshift, k, vmax, freq, ecnt, w_ent)");
+    Tensor cells = f[0].cast<Tensor>();
+    ecnt = f[6].cast<Tensor>();
+    w_ent = f[7].cast<Tensor>();
+    chk(cells, at::kInt, "filt cells");
+    chk(ecnt, at::kByte, "filt ecnt");
+    chk(w_ent, at::kFloat, "filt w_ent");
+    ca.rsize = f[1].cast<uint64_t>();
+    ca.rshift = f[2].cast<int>();
+    ca.k = f[3].cast<int>();
+    ca.vmax = f[4].cast<uint32_t>();
+    ca.freq = f[5].cast<int>();
+    check(ca.k >= 1 && ca.k <= 30 && ca.vmax >= 1 && ca.vmax <= 255 && ca.freq >= 0 &&
+              ca.freq < 255,
+          "localize_tpf filt: k / vmax / freq");
+    check(ca.rsize > 0 && ca.rsize % 4 == 0 && ca.rshift >= 0 && ca.rshift <= bits &&
+              bits - ca.rshift <= 30 &&
+              (ca.rsize << (bits - ca.rshift)) <= (uint64_t)cells.numel() * 4,
+          "localize_tpf filt: sketch regions exceed the cells");
+    check(ecnt.numel() >= psamd::tpf_stride_max(n), "localize_tpf filt: ecnt too small");
+    check(w_ent.numel() >= psamd::tpf_stride(n), "localize_tpf filt: w_ent too small");
+    ca.cells = ptr<uint32_t>(cells);
+    keep.push_back(cells);
+    keep.push_back(ecnt);
+    keep.push_back(w_ent);
+    has_f = true;
+  }
+  return [=, keep = std::move(keep)](hipStream_t st) {
     psamd::localize_tpf(ptr<uint64_t>(keys), n, km, temp.data_ptr(), (size_t)temp.numel(),
                         ptr<int32_t>(dcnt), ptr<uint16_t>(rep), ptr<uint64_t>(uniqf),
                         ptr<int32_t>(ent_pos), ptr<uint16_t>(ent_j), ptr<int32_t>(cnt),
-                        ptr<int32_t>(err), sorted, st);
+                        ptr<int32_t>(err), sorted, st, has_f ? &ca : nullptr,
+                        has_f ? ptr<uint8_t>(ecnt) : nullptr, has_f ? ptr<float>(w_ent) : nullptr,
+                        has_f ? w_ent.numel() : 0);
   };
 }
 
@@ -679,6 +718,19 @@ hipEvent_t list_event(const py::object& ev, const char* what) {
 
 PYBIND11_MODULE(_hipops, m) {
   m.doc() = "parameter_server_amd HIP kernels (gfx950)";
+
+  // Event record / wait on the current stream with the EXTERNAL flags: inside a stream
+  // capture they become event record / wait nodes of the graph (cross-graph ordering
+  // between graphs replayed on different streams, no host-side event call per replay);
+  // outside a capture they act like hipEventRecord / hipStreamWaitEvent.
+  m.def("event_record_ext", [](py::object event) {
+    PSAMD_HIP_CHECK(hipEventRecordWithFlags(list_event(event, "event_record_ext"), cur_stream(),
+                                            hipEventRecordExternal));
+  });
+  m.def("event_wait_ext", [](py::object event) {
+    PSAMD_HIP_CHECK(hipStreamWaitEvent(cur_stream(), list_event(event, "event_wait_ext"),
+                                       hipEventWaitExternal));
+  });
 
   m.def("keymix_params", [](int bits) {
     auto k = make_keymix(bits);
@@ -967,10 +1019,12 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("tpf_temp_bytes", [](int64_t n, int bits) { return psamd::tpf_temp_bytes(n, bits); });
   m.def("localize_tpf", [](Tensor keys, int bits, Tensor temp, Tensor dcnt, Tensor rep,
                            Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err,
-                           bool sorted) {
+                           bool sorted, optional<py::tuple> filt) {
     make_localize_tpf(keys, keys.numel(), bits, temp, dcnt, rep, uniqf, ent_pos, ent_j, cnt,
-                      err, sorted)(cur_stream());
-  });
+                      err, sorted, filt)(cur_stream());
+  }, py::arg("keys"), py::arg("bits"), py::arg("temp"), py::arg("dcnt"), py::arg("rep"),
+     py::arg("uniqf"), py::arg("ent_pos"), py::arg("ent_j"), py::arg("cnt"), py::arg("err"),
+     py::arg("sorted"), py::arg("filt") = py::none());
   // ---- the padded multi-GPU exchange on the flat layout (rows as in exchange.hip)
   m.def("tpf_exchange_ok", [](int64_t n, int bits, int G) {
     return psamd::tpf_exchange_ok(n, bits, G);
@@ -1134,10 +1188,13 @@ PYBIND11_MODULE(_hipops, m) {
       })
       .def("add_localize_tpf", [](LaunchList& l, Tensor keys, int64_t n, int bits, Tensor temp,
                                   Tensor dcnt, Tensor rep, Tensor uniqf, Tensor ent_pos,
-                                  Tensor ent_j, Tensor cnt, Tensor err, bool sorted) {
+                                  Tensor ent_j, Tensor cnt, Tensor err, bool sorted,
+                                  optional<py::tuple> filt) {
         l.push(make_localize_tpf(keys, n, bits, temp, dcnt, rep, uniqf, ent_pos, ent_j,
-                                          cnt, err, sorted), "localize_tpf");
-      })
+                                          cnt, err, sorted, filt), "localize_tpf");
+      }, py::arg("keys"), py::arg("n"), py::arg("bits"), py::arg("temp"), py::arg("dcnt"),
+         py::arg("rep"), py::arg("uniqf"), py::arg("ent_pos"), py::arg("ent_j"), py::arg("cnt"),
+         py::arg("err"), py::arg("sorted"), py::arg("filt") = py::none())
       .def("add_tpf_step", [](LaunchList& l, int64_t n, int bits, optional<py::tuple> A,
                               optional<Tensor> psum, optional<py::tuple> B,
                               optional<Tensor> w_ent, Tensor slots, int init_type, double init_v,
@@ -2022,29 +2079,44 @@ PYBIND11_MODULE(_hipops, m) {
      py::arg("row_scale") = 1, py::arg("row0_out") = py::none());
 
   // ---------------- filters ----------------
-  m.def("cm_insert", [](Tensor table, int k, int vmax, Tensor keys, optional<Tensor> counts,
-                        optional<Tensor> n_dev) {
+  // CountMin over byte cells packed in int32 words: one region of all cells, or (rshift
+  // < 64) regions of rsize cells selected by key >> rshift (countmin.cuh)
+  auto cm_rsize = [](const Tensor& table, int64_t rsize, int rshift, int key_bits) {
+    const uint64_t n = (uint64_t)table.numel() * 4;
+    if (rshift >= 64) return rsize > 0 ? std::min<uint64_t>((uint64_t)rsize, n) : n;
+    check(rsize > 0 && rsize % 4 == 0, "countmin: region size must be a positive multiple of 4");
+    check(rshift >= 0 && key_bits >= rshift && key_bits - rshift <= 30 &&
+              ((uint64_t)rsize << (key_bits - rshift)) <= n,
+          "countmin: regions exceed the cell table");
+    return (uint64_t)rsize;
+  };
+  m.def("cm_insert", [cm_rsize](Tensor table, int k, int vmax, Tensor keys, optional<Tensor> counts,
+                                optional<Tensor> n_dev, int64_t rsize, int rshift, int key_bits) {
     chk(table, at::kInt, "table");
     chk(keys, at::kLong, "keys");
     check(k >= 1 && k <= 30 && vmax >= 1 && vmax <= 255, "countmin k/vmax");
     const uint8_t* c = optr<uint8_t>(counts, at::kByte, "counts");
     if (c) check(counts->numel() >= keys.numel(), "counts too small");
-    psamd::cm_insert(ptr<uint32_t>(table), (uint64_t)table.numel() * 4, k, (uint32_t)vmax,
-                     ptr<uint64_t>(keys), c, keys.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"),
-                     cur_stream());
-  });
-  m.def("cm_query", [](Tensor table, int k, int vmax, Tensor keys, optional<Tensor> n_dev,
-                       int freq, optional<Tensor> keep, optional<Tensor> out_count) {
+    psamd::cm_insert(ptr<uint32_t>(table), cm_rsize(table, rsize, rshift, key_bits), rshift, k,
+                     (uint32_t)vmax, ptr<uint64_t>(keys), c, keys.numel(),
+                     optr<int32_t>(n_dev, at::kInt, "n_dev"), cur_stream());
+  }, py::arg("table"), py::arg("k"), py::arg("vmax"), py::arg("keys"), py::arg("counts"),
+     py::arg("n_dev"), py::arg("rsize") = 0, py::arg("rshift") = 64, py::arg("key_bits") = 64);
+  m.def("cm_query", [cm_rsize](Tensor table, int k, int vmax, Tensor keys, optional<Tensor> n_dev,
+                               int freq, optional<Tensor> keep, optional<Tensor> out_count,
+                               int64_t rsize, int rshift, int key_bits) {
     chk(table, at::kInt, "table");
     chk(keys, at::kLong, "keys");
     int32_t* kp = optr<int32_t>(keep, at::kInt, "keep");
     uint8_t* cp = optr<uint8_t>(out_count, at::kByte, "out_count");
     if (kp) check(keep->numel() >= keys.numel(), "keep too small");
     if (cp) check(out_count->numel() >= keys.numel(), "out_count too small");
-    psamd::cm_query(ptr<uint32_t>(table), (uint64_t)table.numel() * 4, k, (uint32_t)vmax,
-                    ptr<uint64_t>(keys), keys.numel(), optr<int32_t>(n_dev, at::kInt, "n_dev"),
-                    freq, kp, cp, cur_stream());
-  });
+    psamd::cm_query(ptr<uint32_t>(table), cm_rsize(table, rsize, rshift, key_bits), rshift, k,
+                    (uint32_t)vmax, ptr<uint64_t>(keys), keys.numel(),
+                    optr<int32_t>(n_dev, at::kInt, "n_dev"), freq, kp, cp, cur_stream());
+  }, py::arg("table"), py::arg("k"), py::arg("vmax"), py::arg("keys"), py::arg("n_dev"),
+     py::arg("freq"), py::arg("keep"), py::arg("out_count"), py::arg("rsize") = 0,
+     py::arg("rshift") = 64, py::arg("key_bits") = 64);
   m.def("compact_kept", [](Tensor keep, Tensor incl, optional<Tensor> n_dev, Tensor kept_idx,
                            Tensor n_kept, optional<Tensor> remap, optional<Tensor> keys_in,
                            optional<Tensor> keys_out) {
@@ -2063,18 +2135,20 @@ PYBIND11_MODULE(_hipops, m) {
                         ptr<int32_t>(n_kept), optr<int32_t>(remap, at::kInt, "remap"), ki, ko,
                         cur_stream());
   });
-  m.def("cm_insert_seg", [](Tensor table, int k, int vmax, Tensor keys, Tensor seg_start,
-                            optional<Tensor> n_dev) {
+  m.def("cm_insert_seg", [cm_rsize](Tensor table, int k, int vmax, Tensor keys, Tensor seg_start,
+                                    optional<Tensor> n_dev, int64_t rsize, int rshift,
+                                    int key_bits) {
     chk(table, at::kInt, "table");
     chk(keys, at::kLong, "keys");
     chk(seg_start, at::kInt, "seg_start");
     check(k >= 1 && k <= 30 && vmax >= 1 && vmax <= 255, "countmin k/vmax");
     check(seg_start.numel() >= keys.numel() + 1 || n_dev.has_value(), "seg_start too small");
     const int64_t n = std::min<int64_t>(keys.numel(), seg_start.numel() - 1);
-    psamd::cm_insert_seg(ptr<uint32_t>(table), (uint64_t)table.numel() * 4, k, (uint32_t)vmax,
-                         ptr<uint64_t>(keys), ptr<int32_t>(seg_start), n,
+    psamd::cm_insert_seg(ptr<uint32_t>(table), cm_rsize(table, rsize, rshift, key_bits), rshift,
+                         k, (uint32_t)vmax, ptr<uint64_t>(keys), ptr<int32_t>(seg_start), n,
                          optr<int32_t>(n_dev, at::kInt, "n_dev"), cur_stream());
-  });
+  }, py::arg("table"), py::arg("k"), py::arg("vmax"), py::arg("keys"), py::arg("seg_start"),
+     py::arg("n_dev"), py::arg("rsize") = 0, py::arg("rshift") = 64, py::arg("key_bits") = 64);
   m.def("ff_minmax", [](Tensor x, Tensor mm) {
     chk(x, at::kFloat, "x");
     chk(mm, at::kFloat, "mm");

@@ -1,0 +1,87 @@
+// CountMin sketch cells shared by the filter kernels (filters.hip) and the flat
+// localiser's fused tail filter (tploc.hip).
+//
+// Reference CountMin<K, uint8> (src/util/countmin.h:8-48): k probes by double hashing of
+// the 64->32 sketch hash (src/util/sketch.h:20-33), saturating uint8 counters (v_max 254,
+// src/parameter/frequency_filter.h:17). Cells are bytes packed in 32-bit words and updated
+// by a CAS on the word, so concurrent inserts of keys sharing a word lose nothing.
+//
+// Partitioned layout (the GPU trainers'): the sketch is 2^lgR regions of `rsize` cells
+// (a multiple of 4: regions never share a word), and a key's k cells all lie in region
+// (mixed key >> rshift). The flat localiser's bucket workgroups own whole key ranges,
+// hence whole regions, so one workgroup can insert its keys and then query them after a
+// workgroup barrier: every insert that can touch a key's cells came from the same
+// workgroup (no grid-wide barrier between the reference's insertKeys and queryKeys).
+// rshift >= 64: one region (the reference's global layout; CPU runtime apps).
+#pragma once
+#include "common.cuh"
+
+namespace psamd {
+
+__host__ __device__ __forceinline__ uint32_t sketch_hash(uint64_t key) {
+  const uint32_t seed = 0xbc9f1d34u, m = 0xc6a4a793u;
+  uint32_t h = seed ^ (8u * m);
+  h += (uint32_t)key; h *= m; h ^= h >> 16;
+  h += (uint32_t)(key >> 32); h *= m; h ^= h >> 16;
+  return h;
+}
+
+struct CmArgs {
+  uint32_t* cells;   // byte cells, as words
+  uint64_t rsize;    // cells per region
+  int rshift;        // region = key >> rshift (>= 64: one region)
+  int k;             // probes
+  uint32_t vmax;     // saturation
+  int freq;          // keep keys whose estimate > freq
+};
+
+__host__ __device__ __forceinline__ uint64_t cm_base(uint64_t key, int rshift, uint64_t rsize) {
+  return rshift >= 64 ? 0ull : (key >> rshift) * rsize;
+}
+
+__device__ __forceinline__ uint32_t sat_add_byte(uint32_t* table, uint64_t cell, uint32_t cnt,
+                                                 uint32_t vmax) {
+  uint32_t* word = table + (cell >> 2);
+  const int sh = (int)(cell & 3) * 8;
+  uint32_t old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (true) {
+    const uint32_t b = (old >> sh) & 0xffu;
+    const uint32_t nb = (cnt > vmax - b) ? vmax : b + cnt;
+    if (nb == b) return b;
+    const uint32_t nw = (old & ~(0xffu << sh)) | (nb << sh);
+    const uint32_t prev = atomicCAS(word, old, nw);
+    if (prev == old) return nb;
+    old = prev;
+  }
+}
+
+__device__ __forceinline__ void cm_insert_key(const CmArgs& a, uint64_t key, uint32_t cnt) {
+  if (cnt == 0) return;
+  const uint64_t base = cm_base(key, a.rshift, a.rsize);
+  uint32_t h = sketch_hash(key);
+  const uint32_t delta = (h >> 17) | (h << 15);
+  for (int j = 0; j < a.k; ++j) {
+    sat_add_byte(a.cells, base + h % a.rsize, cnt, a.vmax);
+    h += delta;
+  }
+}
+
+// min over the key's cells (agent-scope loads: they see every insert that completed
+// before, whatever this CU's L1 holds)
+__device__ __forceinline__ uint32_t cm_query_key(const CmArgs& a, uint64_t key) {
+  const uint64_t base = cm_base(key, a.rshift, a.rsize);
+  uint32_t h = sketch_hash(key);
+  const uint32_t delta = (h >> 17) | (h << 15);
+  uint32_t res = a.vmax;
+  for (int j = 0; j < a.k; ++j) {
+    const uint64_t c = base + h % a.rsize;
+    const uint32_t w = __hip_atomic_load(a.cells + (c >> 2), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t v = (w >> ((c & 3) * 8)) & 0xffu;
+    res = v < res ? v : res;
+    h += delta;
+  }
+  return res;
+}
+
+}  // namespace psamd

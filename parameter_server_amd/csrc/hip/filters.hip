@@ -16,91 +16,44 @@
 // bytes, src/filter/key_caching.h:18,43): a whole-array, position-dependent
 // 64-bit hash computed on device so the key list never leaves HBM.
 #include "common.cuh"
+#include "countmin.cuh"
 #include <stdexcept>
 #include <string>
 
 namespace psamd {
 
-__host__ __device__ __forceinline__ uint32_t sketch_hash(uint64_t key) {
-  const uint32_t seed = 0xbc9f1d34u, m = 0xc6a4a793u;
-  uint32_t h = seed ^ (8u * m);
-  h += (uint32_t)key; h *= m; h ^= h >> 16;
-  h += (uint32_t)(key >> 32); h *= m; h ^= h >> 16;
-  return h;
-}
-
-__device__ __forceinline__ uint32_t sat_add_byte(uint32_t* table, uint64_t cell, uint32_t cnt,
-                                                 uint32_t vmax) {
-  uint32_t* word = table + (cell >> 2);
-  const int sh = (int)(cell & 3) * 8;
-  uint32_t old = *word;
-  while (true) {
-    const uint32_t b = (old >> sh) & 0xffu;
-    const uint32_t nb = (cnt > vmax - b) ? vmax : b + cnt;
-    if (nb == b) return b;
-    const uint32_t nw = (old & ~(0xffu << sh)) | (nb << sh);
-    const uint32_t prev = atomicCAS(word, old, nw);
-    if (prev == old) return nb;
-    old = prev;
-  }
-}
-
-__global__ void cm_insert_kernel(uint32_t* __restrict__ table, uint64_t n_cells, int k,
-                                 uint32_t vmax, const uint64_t* __restrict__ keys,
+__global__ void cm_insert_kernel(CmArgs a, const uint64_t* __restrict__ keys,
                                  const uint8_t* __restrict__ counts, int64_t n_host,
                                  const int32_t* __restrict__ n_dev) {
   const int64_t n = dev_len(n_dev, n_host);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t h = sketch_hash(keys[i]);
-    const uint32_t delta = (h >> 17) | (h << 15);
-    const uint32_t c = counts ? counts[i] : 1u;
-    for (int j = 0; j < k; ++j) {
-      sat_add_byte(table, h % n_cells, c, vmax);
-      h += delta;
-    }
-  }
+       i += (int64_t)gridDim.x * blockDim.x)
+    cm_insert_key(a, keys[i], counts ? counts[i] : 1u);
 }
 
 // Tail-filter insert of a localised minibatch (reference MinibatchReader::read,
 // src/learner/sgd.h:140-146): count of unique key i = its occurrences
 // seg_start[i+1] - seg_start[i], saturated to a byte; device unique count.
-__global__ void cm_insert_seg_kernel(uint32_t* __restrict__ table, uint64_t n_cells, int k,
-                                     uint32_t vmax, const uint64_t* __restrict__ keys,
+__global__ void cm_insert_seg_kernel(CmArgs a, const uint64_t* __restrict__ keys,
                                      const int32_t* __restrict__ seg_start, int64_t n_host,
                                      const int32_t* __restrict__ n_dev) {
   const int64_t n = dev_len(n_dev, n_host);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t h = sketch_hash(keys[i]);
-    const uint32_t delta = (h >> 17) | (h << 15);
     const int32_t occ = seg_start[i + 1] - seg_start[i];
-    const uint32_t c = occ <= 0 ? 0u : (occ > 255 ? 255u : (uint32_t)occ);
-    for (int j = 0; j < k; ++j) {
-      sat_add_byte(table, h % n_cells, c, vmax);
-      h += delta;
-    }
+    cm_insert_key(a, keys[i], occ <= 0 ? 0u : (occ > 255 ? 255u : (uint32_t)occ));
   }
 }
 
 // keep[i] = (min count > freq) ; also returns the min count.
-__global__ void cm_query_kernel(const uint32_t* __restrict__ table, uint64_t n_cells, int k,
-                                uint32_t vmax, const uint64_t* __restrict__ keys, int64_t n_host,
-                                const int32_t* __restrict__ n_dev, int freq,
-                                int32_t* __restrict__ keep, uint8_t* __restrict__ out_count) {
+__global__ void cm_query_kernel(CmArgs a, const uint64_t* __restrict__ keys, int64_t n_host,
+                                const int32_t* __restrict__ n_dev, int32_t* __restrict__ keep,
+                                uint8_t* __restrict__ out_count) {
   const int64_t n = dev_len(n_dev, n_host);
-  const uint8_t* bytes = (const uint8_t*)table;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t h = sketch_hash(keys[i]);
-    const uint32_t delta = (h >> 17) | (h << 15);
-    uint32_t res = vmax;
-    for (int j = 0; j < k; ++j) {
-      const uint32_t v = bytes[h % n_cells];
-      res = v < res ? v : res;
-      h += delta;
-    }
-    if (keep) keep[i] = (int)res > freq ? 1 : 0;
+    const uint32_t res = cm_query_key(a, keys[i]);
+    if (keep) keep[i] = (int)res > a.freq ? 1 : 0;
     if (out_count) out_count[i] = (uint8_t)res;
   }
 }
@@ -209,25 +162,28 @@ __global__ void key_signature_kernel(const uint64_t* __restrict__ keys, int64_t 
 }
 
 // ---------------------------------------------------------------------------
-void cm_insert(uint32_t* table, uint64_t n_cells, int k, uint32_t vmax, const uint64_t* keys,
-               const uint8_t* counts, int64_t n, const int32_t* n_dev, hipStream_t st) {
-  cm_insert_kernel<<<grid_for(n, 256), 256, 0, st>>>(table, n_cells, k, vmax, keys, counts, n,
-                                                     n_dev);
+// (rsize: cells per region; rshift >= 64: one region of rsize cells)
+void cm_insert(uint32_t* table, uint64_t rsize, int rshift, int k, uint32_t vmax,
+               const uint64_t* keys, const uint8_t* counts, int64_t n, const int32_t* n_dev,
+               hipStream_t st) {
+  const CmArgs a{table, rsize, rshift, k, vmax, 0};
+  cm_insert_kernel<<<grid_for(n, 256), 256, 0, st>>>(a, keys, counts, n, n_dev);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void cm_query(const uint32_t* table, uint64_t n_cells, int k, uint32_t vmax, const uint64_t* keys,
-              int64_t n, const int32_t* n_dev, int freq, int32_t* keep, uint8_t* out_count,
-              hipStream_t st) {
-  cm_query_kernel<<<grid_for(n, 256), 256, 0, st>>>(table, n_cells, k, vmax, keys, n, n_dev, freq,
-                                                    keep, out_count);
+void cm_query(const uint32_t* table, uint64_t rsize, int rshift, int k, uint32_t vmax,
+              const uint64_t* keys, int64_t n, const int32_t* n_dev, int freq, int32_t* keep,
+              uint8_t* out_count, hipStream_t st) {
+  const CmArgs a{const_cast<uint32_t*>(table), rsize, rshift, k, vmax, freq};
+  cm_query_kernel<<<grid_for(n, 256), 256, 0, st>>>(a, keys, n, n_dev, keep, out_count);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
-void cm_insert_seg(uint32_t* table, uint64_t n_cells, int k, uint32_t vmax, const uint64_t* keys,
-                   const int32_t* seg_start, int64_t n, const int32_t* n_dev, hipStream_t st) {
-  cm_insert_seg_kernel<<<grid_for(n, 256), 256, 0, st>>>(table, n_cells, k, vmax, keys, seg_start,
-                                                         n, n_dev);
+void cm_insert_seg(uint32_t* table, uint64_t rsize, int rshift, int k, uint32_t vmax,
+                   const uint64_t* keys, const int32_t* seg_start, int64_t n, const int32_t* n_dev,
+                   hipStream_t st) {
+  const CmArgs a{table, rsize, rshift, k, vmax, 0};
+  cm_insert_seg_kernel<<<grid_for(n, 256), 256, 0, st>>>(a, keys, seg_start, n, n_dev);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

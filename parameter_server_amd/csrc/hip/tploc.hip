@@ -27,6 +27,7 @@
 //
 // Buckets are ranges of the mixed key space, so the unique keys come out sorted
 // (the multi-GPU owner split and the ordered home slots of the KV table rely on it).
+#include "countmin.cuh"
 #include "kv_slot.cuh"
 #include "loss.cuh"
 
@@ -130,14 +131,17 @@ __device__ uint64_t* g_tile_prof = nullptr;
 
 // kQuot = false (<= 31-bit keys): the slot keeps the key itself, home = low kHB key bits;
 // kQuot = true (32..34 bits): quotient encoding, home = low kHB key bits.
+// kCnt (the tail filter's counts): ecnt[tile * kTile + e] = occurrences of entry e in the
+// tile, saturated to a byte (LDS u16 pairs in the dead hash, one integer LDS add per
+// occurrence).
 // (8 waves per SIMD = 2 workgroups per CU: <= 64 VGPRs. The quotient variant compiled to
 // 66 without the bound, i.e. 1 workgroup per CU: localise 90 vs 80 us.)
-template <bool kQuot>
+template <bool kQuot, bool kCnt = false>
 __global__ void __launch_bounds__(tp::kThr, 8)
 tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift, int nbk,
                uint32_t* __restrict__ tkeys, uint16_t* __restrict__ toff,
                int32_t* __restrict__ dcnt, uint16_t* __restrict__ rep,
-               int32_t* __restrict__ err, int lts) {
+               int32_t* __restrict__ err, int lts, uint8_t* __restrict__ ecnt = nullptr) {
   using namespace tp;
   __shared__ uint32_t hk[kHash];    // quotient-encoded keys; after the bucket sort: entry position
   __shared__ uint32_t cnt[kMaxBk];  // per-bucket counts, then offsets
@@ -256,7 +260,25 @@ tp_tile_kernel(const uint64_t* __restrict__ raw, int64_t n, KeyMix m, int shift,
 #pragma unroll
   for (int j = 0; j < kIt; ++j) {
     const int o = j * kThr + t;
-    if (o < lim) rep[base + o] = (uint16_t)hk[sl[j]];
+    if (o < lim) {
+      const uint16_t pos = (uint16_t)hk[sl[j]];
+      rep[base + o] = pos;
+      if (kCnt) sl[j] = pos;
+    }
+  }
+  if (kCnt) {  // occurrences per entry: u16 pairs in the dead hash
+    __syncthreads();
+    for (uint32_t i = t; i < (D + 1) / 2; i += kThr) hk[i] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kIt; ++j)
+      if (j * kThr + t < lim) atomicAdd(&hk[sl[j] >> 1], 1u << ((sl[j] & 1) * 16));
+    __syncthreads();
+    uint8_t* ec = ecnt + (int64_t)blockIdx.x * kTile;
+    for (uint32_t i = t; i < D; i += kThr) {
+      const uint32_t c = (hk[i >> 1] >> ((i & 1) * 16)) & 0xffffu;
+      ec[i] = (uint8_t)(c > 255u ? 255u : c);
+    }
   }
   if (tpp && t == 0) {
     TILE_MARK(6);
@@ -1698,13 +1720,107 @@ __device__ __forceinline__ void tpf_rank_binned(uint64_t* dl, uint32_t* sc, uint
   __syncthreads();
 }
 
+// Fused tail-feature filter of one unit of the flat layout (reference
+// MinibatchReader::read, src/learner/sgd.h:131-150: CountMin insertKeys of the minibatch's
+// per-key counts, then queryKeys > tail_feature_freq, src/parameter/frequency_filter.h:
+// 26-45). In: keys uo[0..D), entries po / jo[ein .. ein + E) (jo = key index), the tile
+// kernel's per-entry occurrence counts ecnt. Each key's count (its entries' counts,
+// saturated to a byte) goes into the partitioned sketch (countmin.cuh: this workgroup owns
+// every region its keys map to), then after a barrier every key is queried. Out: the kept
+// keys at uo[0..D') in their order (sorted stays sorted), the kept entries at
+// po / jo[eout .. eout + E') with the new key indices, and w_ent = 0 at the filtered
+// entries -- the minibatch as if the filtered keys were absent, so the step, pack and
+// owner kernels need no change. (D', E') -> res[0..1] (LDS).
+__device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32_t* __restrict__ po,
+                                                uint16_t* __restrict__ jo, uint32_t D, uint32_t E,
+                                                uint32_t ein, uint32_t eout,
+                                                const uint8_t* __restrict__ ecnt, const CmArgs& cm,
+                                                float* __restrict__ w_ent, int64_t w_cap,
+                                                uint32_t* occ, uint32_t* lds, uint32_t* res) {
+  using namespace tp;
+  constexpr int kKP = tpf::kUnitK / kBkThr;  // 4 keys per thread (contiguous)
+  constexpr int kEP = 4;                      // entries per thread per chunk
+  constexpr uint32_t kNone = 0xffffffffu;
+  const int t = threadIdx.x;
+  for (uint32_t j = t; j < D; j += kBkThr) occ[j] = 0u;
+  __syncthreads();
+  for (uint32_t g = t; g < E; g += kBkThr) {
+    const int32_t id = po[ein + g];
+    atomicAdd(&occ[jo[ein + g]], (uint32_t)ecnt[id]);
+  }
+  __syncthreads();
+  uint64_t key[kKP];
+#pragma unroll
+  for (int q = 0; q < kKP; ++q) {
+    const uint32_t j = t * kKP + q;
+    key[q] = j < D ? uo[j] : 0ull;
+    if (j < D) cm_insert_key(cm, key[q], occ[j] > 255u ? 255u : occ[j]);
+  }
+  __syncthreads();  // every insert of this minibatch that can reach these keys' cells is done
+  uint32_t keep = 0, kc = 0;
+#pragma unroll
+  for (int q = 0; q < kKP; ++q)
+    if (t * kKP + q < D && (int)cm_query_key(cm, key[q]) > cm.freq) {
+      keep |= 1u << q;
+      ++kc;
+    }
+  uint32_t Dn;
+  uint32_t off = tp_block_scan<kBkThr>(kc, lds, &Dn);  // (barriers: every uo read is done)
+#pragma unroll
+  for (int q = 0; q < kKP; ++q) {
+    const uint32_t j = t * kKP + q;
+    if (j < D) {
+      const bool k = (keep >> q) & 1u;
+      occ[j] = k ? off : kNone;
+      if (k) uo[off++] = key[q];
+    }
+  }
+  __syncthreads();
+  uint32_t eo = 0;
+  for (uint32_t c0 = 0; c0 < E; c0 += kBkThr * kEP) {
+    int32_t id[kEP];
+    uint32_t nj[kEP], ec = 0;
+#pragma unroll
+    for (int q = 0; q < kEP; ++q) {
+      const uint32_t g = c0 + t * kEP + q;
+      nj[q] = kNone;
+      id[q] = 0;
+      if (g < E) {
+        id[q] = po[ein + g];
+        nj[q] = occ[jo[ein + g]];
+        if (nj[q] != kNone) ++ec;
+        else if (in_range(id[q], w_cap)) w_ent[id[q]] = 0.f;
+      }
+    }
+    uint32_t tot;
+    uint32_t o = eout + eo + tp_block_scan<kBkThr>(ec, lds, &tot);  // (reads done: barrier)
+#pragma unroll
+    for (int q = 0; q < kEP; ++q)
+      if (nj[q] != kNone) {  // (output positions <= input ones: compaction)
+        po[o] = id[q];
+        jo[o] = (uint16_t)nj[q];
+        ++o;
+      }
+    eo += tot;
+  }
+  if (t == 0) {
+    res[0] = Dn;
+    res[1] = eo;
+  }
+  __syncthreads();
+}
+
 // One workgroup per pair of fine buckets (pair = 0: per fine bucket), the tp_bucket
 // geometry and build; the occupied hash slots in compaction order are the keys' indices.
+// kFilt: then the fused tail filter of each unit (tpf_filter_unit).
+template <bool kFilt>
 __global__ void __launch_bounds__(tp::kBkThr, 8)
 tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbf,
                   int pair, int T, int shift, uint64_t* __restrict__ uniqf,
                   int32_t* __restrict__ ent_pos, uint16_t* __restrict__ ent_j,
-                  int32_t* __restrict__ cnt, int32_t* __restrict__ err, int sorted) {
+                  int32_t* __restrict__ cnt, int32_t* __restrict__ err, int sorted,
+                  const uint8_t* __restrict__ ecnt, CmArgs cm, float* __restrict__ w_ent,
+                  int64_t w_cap) {
   using namespace tp;
   __shared__ uint16_t eh[kECapL];  // hash slot of every gathered entry
   __shared__ uint64_t hs[kDH];     // hash (key u32 | count u32 -> key index)
@@ -1758,18 +1874,44 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
       co[2] = 0;
       co[3] = 0;
     }
-    return;
+    if (!kFilt) return;
+  } else {
+    // the pair's entries overflow the LDS capacity (or its hash): its fine buckets one
+    // after the other, each a unit with its own key index space
+    const uint32_t e0 = tpf_unit_light(tkeys, toff, nbf, T, shift, f0, 0u, key0, hkey, hcnt, eh,
+                                       lds, uo, po, jo, 0u, co, err, sorted != 0);
+    if (pair)
+      tpf_unit_light(tkeys, toff, nbf, T, shift, f0 + 1, 1u, key0, hkey, hcnt, eh, lds,
+                     uo + tpf::kUnitK, po, jo, e0, co + 2, err, sorted != 0);
+    else if (t == 0) {
+      co[2] = 0;
+      co[3] = 0;
+    }
+    if (!kFilt) return;
   }
-  // the pair's entries overflow the LDS capacity (or its hash): its fine buckets one
-  // after the other, each a unit with its own key index space
-  const uint32_t e0 = tpf_unit_light(tkeys, toff, nbf, T, shift, f0, 0u, key0, hkey, hcnt, eh, lds,
-                                     uo, po, jo, 0u, co, err, sorted != 0);
-  if (pair)
-    tpf_unit_light(tkeys, toff, nbf, T, shift, f0 + 1, 1u, key0, hkey, hcnt, eh, lds,
-                   uo + tpf::kUnitK, po, jo, e0, co + 2, err, sorted != 0);
-  else if (t == 0) {
-    co[2] = 0;
-    co[3] = 0;
+  if (kFilt) {  // every unit's outputs are written (global, this workgroup): filter them
+    __syncthreads();
+    const uint32_t D0 = (uint32_t)co[0], E0 = (uint32_t)co[1];
+    const uint32_t D1 = (uint32_t)co[2], E1 = (uint32_t)co[3];
+    uint32_t* occ = reinterpret_cast<uint32_t*>(hs);  // (dead: kDH words of 2 kDH)
+    uint32_t* res = occ + tpf::kUnitK;
+    __syncthreads();
+    tpf_filter_unit(uo, po, jo, D0, E0, 0u, 0u, ecnt, cm, w_ent, w_cap, occ, lds, res);
+    const uint32_t D0k = res[0], E0k = res[1];
+    uint32_t D1k = 0, E1k = 0;
+    if (D1 | E1) {
+      __syncthreads();
+      tpf_filter_unit(uo + tpf::kUnitK, po, jo, D1, E1, E0, E0k, ecnt, cm, w_ent, w_cap, occ, lds,
+                      res);
+      D1k = res[0];
+      E1k = res[1];
+    }
+    if (t == 0) {
+      co[0] = (int32_t)D0k;
+      co[1] = (int32_t)E0k;
+      co[2] = (int32_t)D1k;
+      co[3] = (int32_t)E1k;
+    }
   }
 }
 
@@ -2609,18 +2751,31 @@ size_t tpf_temp_bytes(int64_t n, int bits) {  // (any minibatch of <= n keys: tp
 
 // uniqf >= groups * kUC, ent_pos / ent_j >= groups * kEC, cnt >= groups * 4 (the host
 // checks; tpf_groups)
+// Tail filter (filt != null): ecnt >= tpf_stride_max(n) bytes, w_ent >= w_cap floats, and
+// the sketch's regions no coarser than a fine bucket (region = key >> rshift, rshift <=
+// shift; the host checks).
 void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
                   int32_t* dcnt, uint16_t* rep, uint64_t* uniqf, int32_t* ent_pos, uint16_t* ent_j,
-                  int32_t* cnt, int32_t* err, bool sorted, hipStream_t st) {
+                  int32_t* cnt, int32_t* err, bool sorted, hipStream_t st, const CmArgs* filt,
+                  uint8_t* ecnt, float* w_ent, int64_t w_cap) {
   if (n <= 0) return;
   if (!tploc_supported(n, m.bits)) throw std::runtime_error("localize_tpf: unsupported size");
   if (temp_bytes < tpf_temp_bytes(n, m.bits)) throw std::runtime_error("localize_tpf: temp");
   const TpGeom g = tp_geom(n, m.bits, true);
+  if (filt && (filt->rshift > g.shift || !ecnt || !w_ent))
+    throw std::runtime_error("localize_tpf: tail filter regions coarser than a bucket");
   char* p = (char*)temp;
   auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
   uint32_t* tkeys = (uint32_t*)take((size_t)g.N * 4);
   uint16_t* toff = (uint16_t*)take((size_t)g.T * (g.nbk + 1) * 2);
-  if (m.bits > 31)
+  const bool q = m.bits > 31;
+  if (filt && q)
+    tp_tile_kernel<true, true><<<(unsigned)g.T, tp::kThr, 0, st>>>(
+        raw, n, m, g.shift, g.nbk, tkeys, toff, dcnt, rep, err, g.lts, ecnt);
+  else if (filt)
+    tp_tile_kernel<false, true><<<(unsigned)g.T, tp::kThr, 0, st>>>(
+        raw, n, m, g.shift, g.nbk, tkeys, toff, dcnt, rep, err, g.lts, ecnt);
+  else if (q)
     tp_tile_kernel<true><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
                                                              dcnt, rep, err, g.lts);
   else
@@ -2628,9 +2783,14 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
                                                               dcnt, rep, err, g.lts);
   PSAMD_HIP_CHECK(hipGetLastError());
   const bool pair = g.nbk >= 2 && g.shift <= 30;
-  tpf_bucket_kernel<<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
-      tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
-      sorted ? 1 : 0);
+  if (filt)
+    tpf_bucket_kernel<true><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
+        tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
+        sorted ? 1 : 0, ecnt, *filt, w_ent, w_cap);
+  else
+    tpf_bucket_kernel<false><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
+        tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
+        sorted ? 1 : 0, nullptr, CmArgs{}, nullptr, 0);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

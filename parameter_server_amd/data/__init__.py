@@ -138,8 +138,11 @@ class StreamReader:
 
     def __init__(self, files, fmt="LIBSVM", minibatch=1000, *, ignore_slot=False,
                  data_buf_mb=1000, hash_mod=0, passes=1, shuffle=False, seed=0, hadoop_home="",
-                 max_lines_per_file=-1, recordio=False, max_nnz=0, nthreads=4):
+                 max_lines_per_file=-1, recordio=False, max_nnz=0, nthreads=4,
+                 cache_dir: str | None = None):
         self.files = list(files)
+        # write every parsed text file as a binary cache there (data/bincache.py), once
+        self.cache_dir = cache_dir if (cache_dir and not recordio) else None
         # a minibatch also ends before it exceeds max_nnz features (0 = no cap): a
         # device consumer sizes its workspaces for minibatch rows x a per-row bound
         self.max_nnz = int(max_nnz)
@@ -181,6 +184,8 @@ class StreamReader:
                     b = parse_text(raw, self.fmt, ignore_slot=self.ignore_slot,
                                    hash_mod=self.hash_mod, max_lines=self.max_lines,
                                    nthreads=self.nthreads)
+                    if self.cache_dir:
+                        self._write_cache(f, b)
                 pending.append(b)
                 have += b.rows
                 nnz = sum(x.nnz for x in pending)
@@ -201,6 +206,19 @@ class StreamReader:
             self._error = e
         finally:
             self._q.push(None, 0, finished=True)
+
+    def _write_cache(self, f: str, b: ExampleBatch):
+        from . import bincache
+
+        fid = TEXT_FORMATS[self.fmt] if isinstance(self.fmt, str) else int(self.fmt)
+        cf = bincache.open_valid(f, self.cache_dir, self.fmt, fid, self.hash_mod,
+                                 self.ignore_slot)
+        if cf is not None:  # (another pass or run wrote it already)
+            cf.close()
+            return
+        bincache.write_cache(bincache.cache_path(self.cache_dir, f, self.fmt, self.hash_mod,
+                                                 self.ignore_slot), b, src=f, fmt_id=fid,
+                             hash_mod=self.hash_mod, ignore_slot=self.ignore_slot)
 
     def _cut(self, b: ExampleBatch) -> int:
         """Rows of the next minibatch: <= minibatch rows and <= max_nnz features."""

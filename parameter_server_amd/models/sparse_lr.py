@@ -167,7 +167,11 @@ class SparseLRTrainer:
                else self.part.range_of(self.rank))
         self.table = KVTable(cap, self.device, cfg.init, key_range=rng)
         self.max_nnz = cfg.minibatch * cfg.max_nnz_per_example
-        self.filter = (CountMinSketch(int(cfg.countmin_n), cfg.countmin_k, self.device)
+        # tail filter (reference MinibatchReader::read, sgd.h:131-150): a CountMin sketch
+        # partitioned by mixed-key range (ops/countmin.py), so the flat localiser's bucket
+        # workgroups insert and query it inside their own launch
+        self.filter = (CountMinSketch(int(cfg.countmin_n), cfg.countmin_k, self.device,
+                                      key_bits=self.bits)
                        if cfg.tail_feature_freq > 0 else None)
         # 1 GPU: entry scan + optimizer update fused (PSAMD_FUSED_UPDATE=0: scan, then
         # kv_update); read once, not per step (host issue time)
@@ -180,12 +184,12 @@ class SparseLRTrainer:
         # power of two dividing the bucket groups, tpf_exchange_ok). PSAMD_FLAT=0: "tp"
         flat_env = os.environ.get("PSAMD_FLAT", "1") != "0"
         self._flat_x = False  # G > 1: the padded exchange on the flat layout
+        # (the tail filter runs inside the flat bucket kernel: tpf_filter_unit)
         if self.G == 1:
-            flat_ok = (self.gpu and self.filter is None and self._fused_update
-                       and self._use_plans and flat_env)
+            flat_ok = self.gpu and self._fused_update and self._use_plans and flat_env
         else:
             flat_ok = self._flat_x = bool(
-                self.gpu and flat_env and self.filter is None and cfg.exchange == "padded"
+                self.gpu and flat_env and cfg.exchange == "padded"
                 and self.bits <= 34 and hipops().tploc_supported(self.max_nnz, self.bits)
                 and hipops().tpf_exchange_ok(self.max_nnz, self.bits, self.G))
         if mode == "auto":  # tile dedup + key-range buckets (Localizer falls back to sort
@@ -196,8 +200,7 @@ class SparseLRTrainer:
         if cfg.tail_feature_freq > 0 and mode == "tp":
             mode = "sort"  # the tail filter needs per-key nnz counts (seg_start over nnz)
         # local columns on demand: the fused tp forward/backward reads the entry map
-        self.localizer = Localizer(self.max_nnz, self.bits, self.device, mode=mode,
-                                   lazy_cols=True, sorted_keys=self._flat_x)
+        self.localizer = self._new_localizer(mode)
         self.localize_mode = self.localizer.mode  # after the Localizer's fallbacks
         self._localizers = [self.localizer]  # + a second buffer set for prefetching (G > 1)
         self._compact = None  # flat mode: a "tp" Localizer for steps the flat path cannot run
@@ -245,7 +248,7 @@ class SparseLRTrainer:
         # 3, plain SGD at 8 emulated peers + fixing-float diverged, loss 1.03 after 50
         # steps, tests/test_train_quality_gpu.py)
         self.merged = bool(
-            self.padded and self.filter is None and cfg.exchange_merge != "off"
+            self.padded and cfg.exchange_merge != "off"
             and self.tau > 0 and (cfg.exchange_merge == "on"
                                   or (not math.isinf(self.tau) and self.tau >= 2)))
         self.msched = None
@@ -301,10 +304,15 @@ class SparseLRTrainer:
         next minibatch on a side stream while the current step waits for its
         exchange (``step(..., loc=..., prefetch=...)``)."""
         while len(self._localizers) <= buf:
-            self._localizers.append(Localizer(self.max_nnz, self.bits, self.device,
-                                              mode=self.localize_mode, lazy_cols=True,
-                                              sorted_keys=self._flat_x))
+            self._localizers.append(self._new_localizer(self.localize_mode))
         return self._localizers[buf](keys)
+
+    def _new_localizer(self, mode: str) -> Localizer:
+        """A localisation workspace of this trainer (flat: with the fused tail filter)."""
+        tf = ((self.filter, self.cfg.tail_feature_freq)
+              if self.filter is not None and mode == "tpf" else None)
+        return Localizer(self.max_nnz, self.bits, self.device, mode=mode, lazy_cols=True,
+                         sorted_keys=self._flat_x if mode == "tpf" else False, tail_filter=tf)
 
     def step(self, keys: torch.Tensor, labels: torch.Tensor, *, width: int | None = None,
              row_ptr: torch.Tensor | None = None, vals: torch.Tensor | None = None,
@@ -457,8 +465,9 @@ class SparseLRTrainer:
         if self._compact is None:
             self._compact = []
         while len(self._compact) <= buf:
-            self._compact.append(Localizer(self.max_nnz, self.bits, self.device, mode="tp",
-                                           lazy_cols=True))
+            # (tail filter: "sort", whose segments count occurrences; tp's count entries)
+            self._compact.append(self._new_localizer("sort" if self.filter is not None
+                                                     else "tp"))
         return self._compact[buf]
 
     # ----------------------------------------------- flat 1-GPU step (Localizer "tpf")
@@ -579,9 +588,7 @@ class SparseLRTrainer:
         if self.localize_mode != "tpf":
             raise ValueError("prep_plan needs the flat (tpf) localisation")
         while len(self._localizers) <= buf:
-            self._localizers.append(Localizer(self.max_nnz, self.bits, self.device,
-                                              mode=self.localize_mode, lazy_cols=True,
-                                              sorted_keys=self._flat_x))
+            self._localizers.append(self._new_localizer(self.localize_mode))
         lz = self._localizers[buf]
         f = lz.flat
         B = labels.numel()
@@ -592,7 +599,7 @@ class SparseLRTrainer:
         plan.add_criteo_gen(seed & ((1 << 64) - 1), row0, row_step, B, num_features, alpha, keys,
                             labels)
         plan.add_localize_tpf(keys, n, self.bits, lz.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos,
-                              f.ent_j, f.cnt, f.err, self._flat_x)
+                              f.ent_j, f.cnt, f.err, self._flat_x, filt=lz.filt_args())
 
         def run():
             plan.run()
@@ -974,6 +981,11 @@ class SparseLRTrainer:
                     and _same_workspace(pend["loc"], loc):
                 # the caller localised this minibatch over the pending one's workspace:
                 # localise the pending keys again, into a workspace the caller never sees
+                if self.filter is not None:  # (a second localisation would count twice)
+                    raise ValueError(
+                        "merged exchange + tail filter: the caller's localisation of this "
+                        "minibatch reused the pending minibatch's workspace; use "
+                        "localize(keys, buf=t % 2) or pass keys without loc")
                 pend["loc"] = self._mx_private_loc(pend["keys"], pend["flat"])
         u = self._xt + (pend is not None)
         self._mx_run_exchange(u - 1, None if cur is None else cur["loc"])
@@ -989,11 +1001,9 @@ class SparseLRTrainer:
         own = self.__dict__.setdefault("_mx_own", {})
         lz = own.get(flat)
         if lz is None:
-            lz = own[flat] = (Localizer(self.max_nnz, self.bits, self.device,
-                                        mode=self.localize_mode, lazy_cols=True,
-                                        sorted_keys=self._flat_x) if flat
-                              else Localizer(self.max_nnz, self.bits, self.device, mode="tp",
-                                             lazy_cols=True))
+            lz = own[flat] = (self._new_localizer(self.localize_mode) if flat
+                              else self._new_localizer("sort" if self.filter is not None
+                                                       else "tp"))
         return lz(keys)
 
     def _mx_finish_pending(self):
@@ -1215,7 +1225,16 @@ class SparseLRTrainer:
             off = self.xc.offs[ring] if self.xc is not None else torch.empty(
                 self.G + 1, dtype=torch.int64, device=self.device)
             hipops().owner_split(loc.uniq, loc.n_uniq, self.part.bounds_on(self.device), off)
-            return loc.uniq, None, off, loc.n_uniq
+            if self.xc is None:
+                return loc.uniq, None, off, loc.n_uniq
+            # the count the worker half reads later lives in the ring, not in the
+            # localiser (a caller may refill that workspace before the worker half runs)
+            nkr = getattr(self.xc, "nkr", None)
+            if nkr is None or len(nkr) < self.R:
+                nkr = self.xc.nkr = [torch.zeros(1, dtype=torch.int32, device=self.device)
+                                     for _ in range(self.R)]
+            nkr[ring].copy_(loc.n_uniq.reshape(-1)[:1])
+            return loc.uniq, None, off, nkr[ring]
         return loc.uniq, None, self.part.split_sorted(loc.uniq, loc.n_uniq), loc.n_uniq
 
     def _x_pack_keys(self, loc, gb: int, r: int):
@@ -1707,26 +1726,55 @@ class SparseLRTrainer:
         return w_back, ("dist", slot, send_counts, recv_counts, U)
 
     def _pull_filtered(self, loc):
-        """Tail-feature filter (reference MinibatchReader::read, sgd.h:140-148):
-        insert per-key counts into the worker's CountMin, pull only keys whose
-        estimated count > tail_feature_freq; filtered keys get w = 0, no push."""
-        U = loc.num_unique()
-        uniq = loc.uniq[:U]
-        cnt = (loc.seg_start[1:U + 1] - loc.seg_start[:U]).clamp(max=255).to(torch.uint8)
-        self.filter.insert(uniq, cnt)
-        keep, _ = self.filter.query(uniq, self.cfg.tail_feature_freq)
-        kept_idx = torch.nonzero(keep, as_tuple=False).flatten()
-        w_kept, push = self._pull(uniq[kept_idx].contiguous(),
-                                  torch.tensor([kept_idx.numel()], dtype=torch.int32,
-                                               device=uniq.device))
-        w_local = torch.zeros(loc.grad.numel(), dtype=torch.float32, device=uniq.device)
-        w_local[kept_idx] = w_kept
-        return w_local, ("filtered", kept_idx, push)
+        """Tail-feature filter on the generic paths (reference MinibatchReader::read,
+        sgd.h:140-148): insert per-key counts into the worker's CountMin, pull only keys
+        whose estimated count > tail_feature_freq; filtered keys get w = 0, no push. (The
+        flat layout filters inside its bucket kernel instead, tpf_filter_unit.) GPU, one
+        shard: device-side compaction and counts, no host sync."""
+        if not (self.gpu and self.G == 1):
+            U = loc.num_unique()
+            uniq = loc.uniq[:U]
+            cnt = (loc.seg_start[1:U + 1] - loc.seg_start[:U]).clamp(max=255).to(torch.uint8)
+            self.filter.insert(uniq, cnt)
+            keep, _ = self.filter.query(uniq, self.cfg.tail_feature_freq)
+            kept_idx = torch.nonzero(keep, as_tuple=False).flatten()
+            w_kept, push = self._pull(uniq[kept_idx].contiguous(),
+                                      torch.tensor([kept_idx.numel()], dtype=torch.int32,
+                                                   device=uniq.device))
+            w_local = torch.zeros(loc.grad.numel(), dtype=torch.float32, device=uniq.device)
+            w_local[kept_idx] = w_kept
+            return w_local, ("filtered", kept_idx, push)
+        U = loc.uniq.numel()  # (workspace length; the live count stays on the device)
+        pf = getattr(self, "_pf", None)
+        if pf is None or pf["w"].numel() < U + 1:
+            pf = self._pf = {"w": torch.empty(U + 1, dtype=torch.float32, device=self.device),
+                             "wk": torch.empty(U, dtype=torch.float32, device=self.device)}
+        kk, ki, nk = self._tail_filter(loc, 0)  # kept keys, kept -> unique id, kept count
+        ki[:U].masked_fill_(torch.arange(U, device=self.device) >= nk.long(), U)  # tail -> dummy
+        slot, wk = self.slot_buf, pf["wk"][:U]
+        it, iv, isd, seed = self.table.init.args()
+        hipops().kv_resolve(self.table.slots, kk, nk, slot, wk, True, it, iv, isd, seed,
+                            self.table._err, self.table._inserted, self.table.home_base,
+                            self.table.home_m)
+        w_local = pf["w"][:U + 1]
+        w_local.zero_()
+        w_local.index_copy_(0, ki[:U].long(), wk)  # (kept tail past nk lands on the dummy U)
+        return w_local[:U], ("filtered_dev", ki[:U], slot, nk)
 
     def _push(self, grad: torch.Tensor, push, fold_auc: bool = False) -> bool:
         """Apply a push; True when the step's AUC epilogue rode along (``fold_auc``: the
         1-GPU KV update's block 0 turns the histogram into metrics, one launch less)."""
         kind = push[0]
+        if kind == "filtered_dev":  # gradients of the kept keys, in kept order (no host sync)
+            _, ki, slot, nk = push
+            g = torch.cat([grad[:ki.numel()], grad.new_zeros(1)])[ki.long()]
+            if fold_auc:
+                hipops().kv_update(self.table.slots, slot, g, nk, *self.rule.args(), self.stats,
+                                   hist=self.hist, metrics=self.metrics,
+                                   step_counter=self.step_dev)
+                return True
+            hipops().kv_update(self.table.slots, slot, g, nk, *self.rule.args(), self.stats)
+            return False
         if kind == "filtered":
             kept_idx, inner = push[1], push[2]
             g = grad[kept_idx].contiguous()

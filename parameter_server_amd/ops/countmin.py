@@ -3,6 +3,14 @@
 Reference: ``CountMin<K, uint8>`` (src/util/countmin.h:8-48) wrapped by
 ``FreqencyFilter`` (src/parameter/frequency_filter.h:9-45): insert per-key counts,
 keep keys whose estimated count > freq. Cells saturate at v_max = 254.
+
+``key_bits`` set (the GPU trainers): the sketch is partitioned into 2^lgR regions of
+``rsize`` cells and a key's k cells lie in region ``key >> (key_bits - lgR)``
+(csrc/hip/countmin.cuh). The flat localiser's bucket workgroups own whole key ranges and
+so whole regions: each inserts its keys and queries them behind a workgroup barrier, in
+the same launch. The cells per key and the collision rate are those of the reference's
+global layout (uniformly mixed keys); ``key_bits=None`` keeps that global layout (the CPU
+runtime apps on raw keys).
 """
 from __future__ import annotations
 
@@ -11,27 +19,95 @@ import torch
 from .native import core, hipops, is_gpu, ptr
 
 VMAX = 254
+LG_REGIONS = 11  # >= log2 of the flat localiser's largest fine-bucket count (2048)
+
+_M32 = 0xFFFFFFFF
+
+
+def sketch_hash_torch(keys: torch.Tensor) -> torch.Tensor:
+    """The 64->32 sketch hash (countmin.cuh sketch_hash) on an int64 tensor -> int64 in
+    [0, 2^32)."""
+    m = 0xC6A4A793
+    h = (0xBC9F1D34 ^ ((8 * m) & _M32)) & _M32
+    lo = keys & _M32
+    hi = (keys >> 32) & _M32
+    h = torch.full_like(keys, h)
+    for part in (lo, hi):
+        h = (h + part) & _M32
+        h = (h * m) & _M32
+        h = h ^ (h >> 16)
+    return h
 
 
 class CountMinSketch:
-    def __init__(self, n: int, k: int = 2, device="cpu", vmax: int = VMAX):
+    def __init__(self, n: int, k: int = 2, device="cpu", vmax: int = VMAX,
+                 key_bits: int | None = None, lg_regions: int = LG_REGIONS):
         n = max(64, int(n))
-        n = (n + 3) // 4 * 4  # whole 32-bit words on the device
-        self.n = n
         self.k = min(30, max(1, int(k)))
         self.vmax = int(vmax)
         self.device = torch.device(device)
+        self.key_bits = key_bits
+        if key_bits is None:
+            n = (n + 3) // 4 * 4  # whole 32-bit words on the device
+            self.lgR, self.rshift, self.rsize = 0, 64, n
+        else:
+            self.lgR = min(int(lg_regions), int(key_bits))
+            self.rshift = int(key_bits) - self.lgR
+            r = 1 << self.lgR
+            self.rsize = max(4, ((n + r - 1) // r + 3) // 4 * 4)  # regions never share a word
+            n = self.rsize << self.lgR
+        self.n = n
         self.cells = torch.zeros(n, dtype=torch.uint8, device=self.device)
+
+    @property
+    def partitioned(self) -> bool:
+        return self.rshift < 64
+
+    def args(self, freq: int = 0) -> tuple:
+        """(cells as int32 words, rsize, rshift, k, vmax, freq): what the fused localiser
+        filter takes."""
+        return (self.cells.view(torch.int32), self.rsize, self.rshift, self.k, self.vmax, int(freq))
 
     def clear(self):
         self.cells.zero_()
+
+    def _kw(self) -> dict:
+        return dict(rsize=self.rsize, rshift=self.rshift,
+                    key_bits=self.key_bits if self.key_bits is not None else 64)
+
+    def _cells_of(self, keys: torch.Tensor) -> torch.Tensor:
+        """[n, k] cell indices of keys (CPU reference of countmin.cuh)."""
+        keys = keys.to(torch.int64)
+        h = sketch_hash_torch(keys)
+        delta = ((h >> 17) | (h << 15)) & _M32
+        base = (torch.zeros_like(keys) if not self.partitioned
+                else (keys >> self.rshift) * self.rsize)
+        cols = []
+        for _ in range(self.k):
+            cols.append(base + h % self.rsize)
+            h = (h + delta) & _M32
+        return torch.stack(cols, 1)
 
     def insert(self, keys: torch.Tensor, counts: torch.Tensor | None = None, n_dev=None):
         keys = keys.contiguous()
         if counts is not None:
             counts = counts.contiguous()
         if is_gpu(keys):
-            hipops().cm_insert(self.cells.view(torch.int32), self.k, self.vmax, keys, counts, n_dev)
+            hipops().cm_insert(self.cells.view(torch.int32), self.k, self.vmax, keys, counts, n_dev,
+                               **self._kw())
+        elif self.partitioned:
+            if n_dev is not None:
+                n = int(n_dev.reshape(-1)[0])
+                keys = keys[:n]
+                counts = None if counts is None else counts[:n]
+            c = (torch.ones(keys.numel(), dtype=torch.int64) if counts is None
+                 else counts.to(torch.int64))
+            # a chain of saturating adds of non-negative counts = the clamped sum
+            cells = self._cells_of(keys)
+            acc = self.cells.to(torch.int64)
+            for j in range(self.k):
+                acc.index_add_(0, cells[:, j], c)
+            self.cells.copy_(acc.clamp(max=self.vmax).to(torch.uint8))
         else:
             core().cm_insert(ptr(self.cells), self.n, self.k, self.vmax, ptr(keys), ptr(counts),
                              keys.numel())
@@ -42,7 +118,7 @@ class CountMinSketch:
         (no host sync: graph-capturable)."""
         if is_gpu(keys):
             hipops().cm_insert_seg(self.cells.view(torch.int32), self.k, self.vmax,
-                                   keys.contiguous(), seg_start.contiguous(), n_dev)
+                                   keys.contiguous(), seg_start.contiguous(), n_dev, **self._kw())
             return
         n = keys.numel() if n_dev is None else int(n_dev.reshape(-1)[0])
         cnt = (seg_start[1:n + 1] - seg_start[:n]).clamp(max=255).to(torch.uint8)
@@ -55,7 +131,12 @@ class CountMinSketch:
         cnt = torch.empty(keys.numel(), dtype=torch.uint8, device=keys.device)
         if is_gpu(keys):
             hipops().cm_query(self.cells.view(torch.int32), self.k, self.vmax, keys, n_dev, freq,
-                              keep, cnt)
+                              keep, cnt, **self._kw())
+        elif self.partitioned:
+            v = self.cells[self._cells_of(keys)].to(torch.int32).min(1).values
+            v = v.clamp(max=self.vmax)
+            cnt.copy_(v.to(torch.uint8))
+            keep.copy_((v > freq).to(torch.int32))
         else:
             core().cm_query(ptr(self.cells), self.n, self.k, self.vmax, ptr(keys), keys.numel(),
                             freq, ptr(keep), ptr(cnt))

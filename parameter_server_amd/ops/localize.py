@@ -81,6 +81,7 @@ class FlatLoc:
     bits: int
     nnz: int = 0
     gen: int = 0
+    ecnt: torch.Tensor | None = None  # uint8 [tiles*TP_TILE] tail filter: entry occurrences
     flat = True
 
     @property
@@ -140,8 +141,12 @@ class Localizer:
     "tp" on the Criteo-shaped batch, profiles/r2_localize_tp_vs_sort.log.)"""
 
     def __init__(self, max_nnz: int, bits: int, device="cpu", with_hess: bool = False,
-                 mode: str = "sort", lazy_cols: bool = False, sorted_keys: bool = False):
+                 mode: str = "sort", lazy_cols: bool = False, sorted_keys: bool = False,
+                 tail_filter=None):
         self.max_nnz = int(max_nnz)
+        # "tpf": (CountMinSketch with key_bits = bits, freq) -> the fused tail filter of the
+        # bucket kernel (tploc.hip tpf_filter_unit): filtered keys leave the minibatch
+        self.tail_filter = tail_filter
         # "tpf": rank-sort each bucket's keys (the multi-GPU exchange rows stay key-ordered)
         self.sorted_keys = bool(sorted_keys)
         self.lazy_cols = bool(lazy_cols)  # "tp": local_col on demand (ensure_local_col)
@@ -175,7 +180,9 @@ class Localizer:
                 w_ent=torch.zeros(N, dtype=torch.float32, device=dev),
                 cnt=i32(4 * g), uniqf=torch.zeros(g * kr, dtype=torch.int64, device=dev),
                 ent_pos=i32(g * er), ent_j=torch.zeros(g * er, dtype=torch.int16, device=dev),
-                slot_u=i32(g * kr), err=i32(1), bits=self.bits)
+                slot_u=i32(g * kr), err=i32(1), bits=self.bits,
+                ecnt=(torch.zeros(N, dtype=torch.uint8, device=dev) if tail_filter is not None
+                      else None))
             self.err = self.flat.err
             return
         if self.gpu and self.mode == "tp":
@@ -249,6 +256,16 @@ class Localizer:
             self.scan_temp = torch.empty(max(1, H.scan_temp_bytes(n)), dtype=torch.uint8,
                                          device=dev)
 
+    def filt_args(self):
+        """The native fused tail filter's argument tuple ("tpf" with a tail filter) or None."""
+        if self.tail_filter is None or self.mode != "tpf":
+            return None
+        cm, freq = self.tail_filter
+        if cm.rshift >= 64 or cm.key_bits != self.bits:
+            raise ValueError("the fused tail filter needs a CountMinSketch partitioned over "
+                             "this localiser's key bits")
+        return (*cm.args(freq), self.flat.ecnt, self.flat.w_ent)
+
     def check(self):
         """Host sync: raise if a "part" localisation overflowed a bucket's LDS hash."""
         if getattr(self, "err", None) is not None and self.mode in ("part", "tp", "tpf") and \
@@ -272,7 +289,7 @@ class Localizer:
         if self.mode == "tpf":
             f = self.flat
             H.localize_tpf(keys, self.bits, self.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos,
-                           f.ent_j, f.cnt, f.err, self.sorted_keys)
+                           f.ent_j, f.cnt, f.err, self.sorted_keys, filt=self.filt_args())
             f.nnz = n
             f.gen += 1
             return f

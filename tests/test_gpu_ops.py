@@ -276,6 +276,23 @@ def test_countmin_gpu_equals_cpu():
     assert torch.equal(k0, k1.cpu()) and torch.equal(c0, c1.cpu())
 
 
+def test_countmin_partitioned_gpu_equals_cpu():
+    """The trainers' partitioned sketch (regions by mixed-key range): GPU kernels = the
+    CPU reference, cell for cell."""
+    torch.manual_seed(6)
+    bits = 30
+    keys = torch.randint(0, 1 << bits, (30000,), dtype=torch.int64)
+    counts = torch.randint(1, 200, (30000,), dtype=torch.int64).to(torch.uint8)
+    cms = [CountMinSketch(1 << 18, 2, d, key_bits=bits) for d in ("cpu", DEV)]
+    for cm in cms:
+        cm.insert(keys.to(cm.device), counts.to(cm.device))
+        cm.insert(keys[:7000].to(cm.device))
+    assert torch.equal(cms[0].cells, cms[1].cells.cpu())
+    k0, c0 = cms[0].query(keys, 3)
+    k1, c1 = cms[1].query(keys.to(DEV), 3)
+    assert torch.equal(k0, k1.cpu()) and torch.equal(c0, c1.cpu())
+
+
 @pytest.mark.parametrize("nbytes", [1, 2, 3])
 def test_fixing_float_roundtrip(nbytes):
     torch.manual_seed(5)

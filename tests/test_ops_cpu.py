@@ -86,6 +86,31 @@ def test_countmin_saturates_and_filters():
     assert keep.tolist() == [1, int(cnt[1]) > 2, 1]
 
 
+def test_countmin_partitioned_regions_and_saturation():
+    """Partitioned sketch (the trainers'): a key's cells stay inside its mixed-key region;
+    repeated inserts saturate at v_max exactly like the chain of saturating adds; the hash
+    is the C++ one."""
+    from parameter_server_amd.ops.countmin import sketch_hash_torch
+    from parameter_server_amd.ops.native import core
+
+    bits = 24
+    cm = CountMinSketch(1 << 16, 3, key_bits=bits)
+    assert cm.rsize % 4 == 0 and cm.rsize << cm.lgR == cm.n and cm.rshift == bits - 11
+    g = torch.Generator().manual_seed(3)
+    keys = torch.randint(0, 1 << bits, (5000,), dtype=torch.int64, generator=g)
+    cells = cm._cells_of(keys)
+    region = keys >> cm.rshift
+    assert bool(((cells // cm.rsize) == region[:, None]).all())
+    h = sketch_hash_torch(keys[:50])
+    assert h.tolist() == [core().sketch_hash(int(k)) for k in keys[:50]]
+    for _ in range(3):
+        cm.insert(keys[:10], torch.full((10,), 100, dtype=torch.uint8))
+    keep, cnt = cm.query(keys[:10], freq=253)
+    assert cnt.tolist() == [254] * 10 and keep.tolist() == [1] * 10
+    keep, cnt = cm.query(keys[10:20], freq=0)
+    assert bool((cnt < 254).all())
+
+
 def test_fixing_float_cpu_roundtrip():
     x = torch.randn(1000)
     code, mm = ff.encode(x, 2)

@@ -207,8 +207,6 @@ def _reference_train(batches, rule, bits):
         m = W[idx].view(B, width).double().sum(1).float()
         yy = torch.where(y > 0, 1.0, -1.0)
         coef = -yy * torch.sigmoid(-yy * m)
-        if losses is not None:
-            losses.append(float(torch.nn.functional.softplus(-yy * m).sum()))
         g = torch.zeros(K, dtype=torch.float64).index_add_(
             0, idx, coef.double().repeat_interleave(width)).float() * rule.grad_scale
         u = torch.unique(idx)
@@ -601,6 +599,108 @@ def test_flat_csr_empty_rows_are_counted(monkeypatch):
     w, z, n = _table_by_raw_key(tr, allk)
     torch.testing.assert_close(w, W, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(n, Nn, rtol=1e-4, atol=1e-4)
+
+
+def _reference_train_filtered(batches, rule, bits, freq, cm):
+    """The fp32 FTRL loop with the reference's tail filter (MinibatchReader::read,
+    sgd.h:131-150): per minibatch, CountMin insert of every distinct key's occurrence count
+    (a byte), then query; keys whose estimate <= freq are dropped from the minibatch (no
+    margin contribution, no update, never stored). ``cm``: a CPU CountMinSketch with the
+    trainer's hashes (partitioned by mixed-key range). Returns (ever-kept raw keys, W, Z, N,
+    filtered-occurrence count)."""
+    allk = torch.unique(torch.cat([b[0].cpu() for b in batches]))
+    K = allk.numel()
+    W, Z, Nn = torch.zeros(K), torch.zeros(K), torch.zeros(K)
+    ever = torch.zeros(K, dtype=torch.bool)
+    dropped = 0
+    for keys, labels, row_ptr, vals in batches:
+        k, y = keys.cpu(), labels.cpu()
+        B = y.numel()
+        rp = row_ptr.cpu() if row_ptr is not None else torch.arange(0, k.numel() + 1,
+                                                                    k.numel() // B)
+        x = vals.cpu() if vals is not None else torch.ones(k.numel())
+        mk = mix(k, bits)
+        um, inv, cnt = torch.unique(mk, return_inverse=True, return_counts=True)
+        cm.insert(um, cnt.clamp(max=255).to(torch.uint8))
+        keep, _ = cm.query(um, freq)
+        kocc = keep.bool()[inv]
+        dropped += int((~kocc).sum())
+        x = torch.where(kocc, x, torch.zeros_like(x))
+        row = torch.repeat_interleave(torch.arange(B), rp[1:] - rp[:-1])
+        idx = torch.searchsorted(allk, k)
+        m = torch.zeros(B, dtype=torch.float64).index_add_(0, row, (W[idx] * x).double()).float()
+        yy = torch.where(y > 0, 1.0, -1.0)
+        coef = -yy * torch.sigmoid(-yy * m)
+        g = torch.zeros(K, dtype=torch.float64).index_add_(0, idx, (coef[row] * x).double()).float()
+        u = torch.unique(idx[kocc])
+        ever[u] = True
+        gu, w_old = g[u] * rule.grad_scale, W[u]
+        n_new = torch.sqrt(Nn[u] * Nn[u] + gu * gu)
+        sigma = (n_new - Nn[u]) / rule.alpha
+        Z[u] = Z[u] + gu - sigma * w_old
+        Nn[u] = n_new
+        eta = rule.alpha / (n_new + rule.beta)
+        zz = -Z[u] * eta
+        leta = rule.l1 * eta
+        W[u] = torch.where(zz.abs() <= leta, torch.zeros_like(zz),
+                           (zz - torch.sign(zz) * leta) / (1 + rule.l2 * eta))
+    return allk[ever], W[ever], Z[ever], Nn[ever], dropped
+
+
+@pytest.mark.parametrize("kind", ["fixed", "fixed_pre", "csr", "skewed"])
+def test_flat_tail_filter_matches_fp32_reference(monkeypatch, kind):
+    """the tail filter on the flat fast path (CountMin insert + query fused into
+    the bucket kernel, filtered keys removed from the minibatch) against the fp32 loop with
+    a CPU CountMin of the same hashes, 5 steps, rtol 1e-4. tail_feature_freq 1 (the
+    reference CTR conf) and a small sketch, so collisions happen too."""
+    from parameter_server_amd.ops.countmin import CountMinSketch
+
+    monkeypatch.setenv("PSAMD_FLAT", "1")
+    steps, freq = 5, 1
+    if kind == "skewed":  # overflowing bucket pairs: the register-light units, filtered
+        monkeypatch.setenv("PSAMD_TILE_LTS", "13")
+        bits = 20
+        batches = [(k, lab, None, None) for k, lab in (_skewed_batch(s, bits) for s in range(3))]
+        B, width, N = batches[0][1].numel(), 16, 1 << bits
+        steps = 3
+    elif kind == "csr":
+        B, N = 3000, 10 ** 6
+        batches = [_csr_batch(B, 500 + s, N=N) for s in range(steps)]
+        width = None
+    else:
+        B, N, width = 8192, 10 ** 6, 39
+        batches = [(*criteo_batch(B, seed=77, row0=t * B, num_features=N, device=DEV), None, None)
+                   for t in range(steps)]
+    maxn = max(b[0].numel() for b in batches)
+    cfg = SparseLRConfig(num_features=N, minibatch=B, max_nnz_per_example=(maxn + B - 1) // B,
+                         table_capacity=1 << 22, alpha=0.05, l1=1.0, l2=0.1,
+                         tail_feature_freq=freq, countmin_n=1 << 16)
+    tr = SparseLRTrainer(cfg, device=DEV)
+    assert tr.localize_mode == "tpf" and tr.filter is not None
+    if kind == "fixed_pre":  # pulls issued ahead (the pipelined form), localised in order
+        loc = tr.localize(batches[0][0], buf=0)
+        for t in range(steps):
+            nxt = tr.localize(batches[t + 1][0], buf=(t + 1) % 2) if t + 1 < steps else None
+            tr.step(batches[t][0], batches[t][1], width=width, loc=loc, next_loc=nxt)
+            loc = nxt
+    else:
+        for k, lab, rp, v in batches:
+            tr.step(k, lab, width=width, row_ptr=rp, vals=v)
+    torch.cuda.synchronize()
+    assert tr._compact is None  # every step ran the flat path
+    tr.check_ok()
+    p = tr.progress()
+    assert p["examples"] == steps * B
+    cm = CountMinSketch(cfg.countmin_n, cfg.countmin_k, "cpu", key_bits=tr.bits)
+    allk, W, Z, Nn, dropped = _reference_train_filtered(batches, cfg.update_rule(), tr.bits,
+                                                        freq, cm)
+    assert dropped > 0  # the filter removed something
+    assert torch.equal(tr.filter.cells.cpu(), cm.cells)  # same sketch, cell for cell
+    w, z, n = _table_by_raw_key(tr, allk)  # only ever-kept keys were stored
+    torch.testing.assert_close(w, W, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(z, Z, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(n, Nn, rtol=1e-4, atol=1e-4)
+    assert (w != 0).sum() > 20
 
 
 def test_flat_fixed_width_valued_rows_take_the_csr_kernel(monkeypatch):

@@ -23,12 +23,15 @@ def _lr(algo, mode):
     from parameter_server_amd.parallel.comm import LoopbackComm
 
     dev = torch.device("cuda", 0)
-    emu = mode == "e8asp2"
+    emu = mode.startswith("e8asp2")
+    # e8asp2m: the merged one-collective exchange serving asp with staleness exactly 2
+    merged = dict(exchange_merge="on", exchange_lag=2) if mode == "e8asp2m" else {}
     cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, algo=algo,
                          consistency="asp" if emu else "bsp",
                          fixing_float_bytes=2 if emu else 0, table_capacity=1 << 26,
-                         **algo_defaults(algo))
+                         **merged, **algo_defaults(algo))
     tr = SparseLRTrainer(cfg, LoopbackComm(8, dev) if emu else None, dev)
+    assert tr.merged == bool(merged)
     keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
     labels = torch.empty(B, dtype=torch.float32, device=dev)
     for t in range(STEPS):
@@ -42,7 +45,7 @@ def _lr(algo, mode):
     return tr.progress(reset=True)
 
 
-@pytest.mark.parametrize("mode", ["1", "e8asp2"])
+@pytest.mark.parametrize("mode", ["1", "e8asp2", "e8asp2m"])
 @pytest.mark.parametrize("algo", ["ftrl", "adagrad", "sgd"])
 def test_sparse_lr_trains(algo, mode):
     p = _lr(algo, mode)
