@@ -110,8 +110,19 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     ctr = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(nprep)]
     locs = [None] * NB
     mode = {"capture": False}
+    # 1 GPU, native iteration: the localisation (tile kernel) of the minibatch prepared in
+    # iteration t waits for step t's fused forward/backward (PSAMD_TILE_GATE=1): the two
+    # LDS-heavy 1024-thread kernels otherwise share the CUs when the pipeline's phases
+    # line them up (10^10 features: fwd/bwd 26 -> 46 us, profiles/r6_1e10.log)
+    tile_gate = flat and os.environ.get("PSAMD_TILE_GATE", "0") == "1"
+    ev_fb = [torch.cuda.Event() for _ in range(NB)] if tile_gate else None
+    if tile_gate:
+        for e in ev_fb:
+            e.record(torch.cuda.current_stream(device))
     fplans = ([tr.prep_plan(b, bufs[b][0], bufs[b][1], seed=seed, row0=b * B, row_step=NB * B,
-                            num_features=N) for b in range(NB)] if flat else None)
+                            num_features=N,
+                            gate=ev_fb[(b - nprep) % NB] if tile_gate else None)
+               for b in range(NB)] if flat else None)
 
     def prep(b):  # buffer b belongs to prep stream b % nprep (rows (nprep*k + s) * B)
         sidx = b % nprep
@@ -352,7 +363,8 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
         for j in range(NB):
             cur, nxt, nb = j, (j + 1) % NB, (j + nprep) % NB
             s = sides[nb % nprep]
-            splan, _ = tr.flat_plan(locs[cur], bufs[cur][1], B, 39, locs[nxt], True)
+            splan, _ = tr.flat_plan(locs[cur], bufs[cur][1], B, 39, locs[nxt], True,
+                                    fb_record=ev_fb[j] if tile_gate else None)
             L = H.LaunchList()
             L.add_stream(main)
             L.add_wait(ev_prep[cur])
@@ -805,6 +817,82 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         iterate_native()
     torch.cuda.synchronize()
     args.native_iter = True  # (reported as config.native_iteration)
+    if os.environ.get("PSAMD_MX_G2", "0") == "1":
+        # TWO graph launches per iteration: the main stream's graph (wait for exchange t,
+        # worker t, record) and the preparation stream's graph (preparation, pack,
+        # all-to-all, owner resolve / apply) with every cross-stream event wait / record
+        # as an EXTERNAL event node inside the graphs (event_wait_ext / event_record_ext)
+        # instead of 6 graph launches + 11 host event calls (benchmarks/probe_graph_events.py)
+        Eg = P * -(-8 // P)
+        evg = {k: [torch.cuda.Event() for _ in range(Eg)] for k in ("w", "M", "res", "app")}
+        evp = [torch.cuda.Event() for _ in range(NB)]
+        for e in [x for k in evg for x in evg[k]] + evp:
+            e.record(main)
+        torch.cuda.synchronize()
+        g2 = []
+        for k in range(Eg):
+            if watch is not None:
+                watch.beat("capture2", k)
+            t = state["t"] + ((k - state["t"]) % Eg)
+            s = t + xd
+            nb = (t + nprep) % NB
+            b = t % NB
+            wfn = tr.mx_worker(t, locs[b], bufs[b][1], width=39)
+            gm = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gm, capture_error_mode=CAPTURE_MODE):
+                H.event_wait_ext(evg["M"][t % Eg])
+                wfn()
+                H.event_record_ext(evg["w"][t % Eg])
+            parts = tr.mx_exchange(s, locs[(s + 1) % NB])
+            gs = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gs, capture_error_mode=CAPTURE_MODE):
+                H.event_wait_ext(evg["w"][(t + nprep - NB) % Eg])
+                if fchain:
+                    H.event_wait_ext(evp[(nb - 1) % NB])
+                prep(nb)
+                if fchain:
+                    H.event_record_ext(evp[nb])
+                parts["pack"]()
+                H.event_wait_ext(evg["w"][(s - d) % Eg])
+                H.event_wait_ext(evg["res"][(s - 1) % Eg])
+                H.event_wait_ext(cchain.ev)
+                parts["comm"]()
+                H.event_record_ext(cchain.ev)
+                H.event_record_ext(evg["M"][s % Eg])
+                H.event_wait_ext(evg["app"][(s - 1) % Eg])
+                if parts["post"]:
+                    parts["resolve"]()
+                    H.event_record_ext(evg["res"][s % Eg])
+                    parts["apply"]()
+                else:
+                    parts["apply"]()
+                    parts["resolve"]()
+                    H.event_record_ext(evg["res"][s % Eg])
+                H.event_record_ext(evg["app"][s % Eg])
+            held.extend([gm, gs])
+            L = H.LaunchList()
+            L.add_stream(main)
+            L.add_graph(gm)
+            L.add_stream(sides[nb % nprep])
+            L.add_graph(gs)
+            L.add_stream(main)
+            g2.append(L)
+        torch.cuda.synchronize()
+
+        def iterate_g2():
+            t = state["t"]
+            g2[t % Eg].run()
+            tr.mx_done(B)
+            cchain.n += 1
+            tr._mx_next = t + xd + 1
+            state["t"] = t + 1
+
+        iterate_g2.release = release
+        for _ in range(P):
+            iterate_g2()
+        torch.cuda.synchronize()
+        args.native_iter = "graph2"
+        return iterate_g2, True
     return iterate_native, True
 
 

@@ -120,54 +120,60 @@ def run_async_sgd(lm, comm, device, flags, printer=None) -> dict:
     interval = max(1, int(sgd.report_interval))
     printer = printer or (ProgressPrinter() if rank == 0 and not flags.quiet else None)
     t0 = last = time.time()
-    it = iter(feeder)
     steps = idle = 0
     last_p = None
-    # a fully cached run knows its minibatch count: the ranks agree on the step count (and
-    # the report steps) ONCE; otherwise they agree every step over the host channel
-    planned = feeder.planned_batches()
-    total = None
-    if G > 1:
-        counts = comm.host_gather_obj(planned)
-        if all(c is not None for c in counts):
-            total = max(counts)
-    elif planned is not None:
-        total = planned
-    every = getattr(flags, "report_steps", 0) or (max(1, -(-total // 20)) if total else 0)
-    t = 0
-    while True:
-        if total is not None:
-            if t >= total:
-                break
-            b = next(it, None)
-            report = (t + 1) % every == 0
-        else:
-            b = next(it, None)
-            report = time.time() - last >= interval
-            if G > 1:  # (host channel: every rank steps, reports and stops together)
-                st = comm.host_gather_obj((b is not None, report))
-                if not any(s[0] for s in st):
+    agreed = []  # per pass: the agreed step count, or None (agreement every step)
+    for ps in range(feeder.passes):
+        # a pass that streams the binary cache knows its minibatch count: the ranks agree
+        # on the pass's step count (and its report steps) ONCE; a text pass agrees every
+        # step over the host channel
+        planned = feeder.planned_pass(ps)
+        total = None
+        if G > 1:
+            counts = comm.host_gather_obj(planned)
+            if all(c is not None for c in counts):
+                total = max(counts)
+        elif planned is not None:
+            total = planned
+        agreed.append(total)
+        every = getattr(flags, "report_steps", 0) or (max(1, -(-total // 10)) if total else 0)
+        it = feeder.iter_pass(ps)
+        t = 0
+        while True:
+            if total is not None:
+                if t >= total:
                     break
-                report = st[0][1]
-            elif b is None:
-                break
-        t += 1
-        if b is None:
-            tr.idle_step()  # out of files: keep serving this shard and flushing pushes
-            idle += 1
-        else:
-            if b.vals is None and b.width:  # one width, binary: the fused fixed-width path
-                tr.step(b.keys, b.labels, width=b.width)
+                b = next(it, None)
+                report = (t + 1) % every == 0
             else:
-                tr.step(b.keys, b.labels, width=b.width or None, row_ptr=b.row_ptr,
-                        vals=b.vals)
-            feeder.release(b)
-            steps += 1
-        if report:
-            last = time.time()
-            last_p = tr.progress()
-            if printer is not None:
-                printer(last_p)
+                b = next(it, None)
+                report = time.time() - last >= interval
+                if G > 1:  # (host channel: every rank steps, reports and stops together)
+                    st = comm.host_gather_obj((b is not None, report))
+                    if not any(s[0] for s in st):
+                        break
+                    report = st[0][1]
+                elif b is None:
+                    break
+            t += 1
+            if b is None:
+                tr.idle_step()  # out of files: keep serving this shard and flushing pushes
+                idle += 1
+            else:
+                if b.vals is None and b.width:  # one width, binary: the fused fixed-width path
+                    tr.step(b.keys, b.labels, width=b.width)
+                else:
+                    tr.step(b.keys, b.labels, width=b.width or None, row_ptr=b.row_ptr,
+                            vals=b.vals)
+                feeder.release(b)
+                steps += 1
+            if report:
+                last = time.time()
+                last_p = tr.progress()
+                if printer is not None:
+                    printer(last_p)
+        for _ in it:  # (a rank's pass ended early on the agreed count: none left)
+            raise RuntimeError("feeder yielded more minibatches than planned")
     p = tr.progress()
     if printer is not None and p["examples"]:
         printer(p)
@@ -178,7 +184,7 @@ def run_async_sgd(lm, comm, device, flags, printer=None) -> dict:
     out = {"examples": feeder.num_examples, "steps": steps, "idle_steps": idle, "seconds": dt,
            "progress": p if p["examples"] else last_p, "trainer": tr, "h2d_bytes": feeder.bytes_h2d,
            "text_passes": feeder.text_passes, "cached_passes": feeder.cached_passes,
-           "agreed_steps": total}
+           "agreed_steps": agreed}
     if tmp_cache:
         import shutil
 

@@ -179,9 +179,18 @@ class DeviceFeeder:
         before the first step), else None."""
         if self._caches is None:
             return None
-        if not hasattr(self, "_plans"):
-            self._plans = [self._plan_pass(o) for o in self._orders]
-        return sum(len(p) for p in self._plans)
+        return sum(self.planned_pass(p) for p in range(self.passes))
+
+    def planned_pass(self, p: int) -> int | None:
+        """Minibatches of pass ``p`` when it will stream from the cache (every file has a
+        valid cache now), else None."""
+        if self._caches is None:
+            return None
+        if getattr(self, "_plans", None) is None:
+            self._plans = [None] * self.passes
+        if self._plans[p] is None:
+            self._plans[p] = self._plan_pass(self._orders[p])
+        return len(self._plans[p])
 
     # ------------------------------------------------------------ text staging
     def _stage_text(self, order, out_q: queue.Queue):
@@ -388,22 +397,26 @@ class DeviceFeeder:
 
     # ------------------------------------------------------------ consumer
     def __iter__(self):
-        for p, order in enumerate(self._orders):
-            self._mode = "text" if self._caches is None else "cache"
-            if self._caches is None:
-                self.text_passes += 1
-                src = self._iter_text(order)
-                if self.cache_dir and p + 1 < self.passes:  # the caches exist after this pass
-                    src = self._then_open(src)
-            else:
-                self.cached_passes += 1
-                if not hasattr(self, "_plans"):
-                    self._plans = [None] * self.passes
-                plan = self._plans[p] if self._plans[p] is not None else self._plan_pass(order)
-                src = self._iter_cached(plan)
-            for b in src:
-                self.num_examples += b.rows
-                yield b
+        for p in range(self.passes):
+            yield from self.iter_pass(p)
+
+    def iter_pass(self, p: int):
+        """The minibatches of pass ``p`` (text, or the binary cache once every file has
+        one); passes run in order."""
+        order = self._orders[p]
+        self._mode = "text" if self._caches is None else "cache"
+        if self._caches is None:
+            self.text_passes += 1
+            src = self._iter_text(order)
+            if self.cache_dir:  # the caches exist after this pass
+                src = self._then_open(src)
+        else:
+            self.cached_passes += 1
+            self.planned_pass(p)
+            src = self._iter_cached(self._plans[p])
+        for b in src:
+            self.num_examples += b.rows
+            yield b
 
     def _then_open(self, src):
         yield from src

@@ -546,14 +546,15 @@ class SparseLRTrainer:
         self.step_count += 1
         self.examples += B
 
-    def flat_plan(self, loc, labels, B: int, width: int, next_loc, pre: bool):
+    def flat_plan(self, loc, labels, B: int, width: int, next_loc, pre: bool, fb_record=None):
         """(LaunchList of one flat step, the next FlatLoc its update launch pulls or None);
         cached per (buffers, labels, next buffers). bench.py splices it into its native
-        multi-stream iteration lists."""
+        multi-stream iteration lists. ``fb_record``: an event recorded between the fused
+        forward/backward and the step kernel (a preparation stream may wait for it)."""
         nxt = next_loc if (next_loc is not None and getattr(next_loc, "flat", False)
                            and next_loc.nnz == loc.nnz and next_loc is not loc) else None
         key = (id(loc), id(labels), B, width, loc.nnz, pre, id(nxt) if nxt is not None else 0,
-               id(self.rule), id(self.table.init))
+               id(self.rule), id(self.table.init), id(fb_record))
         plan = self._plans.get(key)
         if plan is None:
             H, tb = hipops(), self.table
@@ -568,6 +569,8 @@ class SparseLRTrainer:
             plan.add_tp_fwd_bwd(loc.rep, loc.dcnt, None, n, width, None, loc.w_ent, labels, B,
                                 loss_id(self.cfg.loss), self.coef[:B], self.metrics, self.hist,
                                 AUC_BINS, loc.psum, None, None, None, None, False)
+            if fb_record is not None:
+                plan.add_record(fb_record)
             plan.add_tpf_step(n, bits, loc.bufs, loc.psum,
                               nxt.bufs if nxt is not None else None,
                               nxt.w_ent if nxt is not None else None, *common, self.hist,
@@ -578,11 +581,13 @@ class SparseLRTrainer:
         return plan, nxt
 
     def prep_plan(self, buf: int, keys: torch.Tensor, labels: torch.Tensor, *, seed: int,
-                  row0: int, row_step: int, num_features: int, alpha: float = 1.1):
+                  row0: int, row_step: int, num_features: int, alpha: float = 1.1, gate=None):
         """Flat mode: a native launch list that generates the next synthetic minibatch of
         workspace ``buf`` (rows row0, row0 + row_step, ... on successive runs) and
         localises it (tile + flat bucket kernels): ONE host call per data preparation.
-        Returns a callable -> the FlatLoc of ``buf``."""
+        ``gate``: an event the localisation waits for after the generator (bench.py: the
+        training step's fused forward/backward, so the two LDS-heavy 1024-thread kernels
+        do not share the CUs). Returns a callable -> the FlatLoc of ``buf``."""
         from ..ops.synthetic import CRITEO_1TB_CARDS, _set_cards
 
         if self.localize_mode != "tpf":
@@ -598,6 +603,8 @@ class SparseLRTrainer:
         plan = H.LaunchList()
         plan.add_criteo_gen(seed & ((1 << 64) - 1), row0, row_step, B, num_features, alpha, keys,
                             labels)
+        if gate is not None:
+            plan.add_wait(gate)
         plan.add_localize_tpf(keys, n, self.bits, lz.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos,
                               f.ent_j, f.cnt, f.err, self._flat_x, filt=lz.filt_args())
 

@@ -65,7 +65,17 @@ def _weights(tr):
     # ... and its graphs replayed from one native launch list per iteration
     ("prep", 3, 1, {"exchange_merge": "on", "_env": {"PSAMD_MX_NATIVE": "1"}}),
     ("prep", 2, 1, {"exchange_merge": "on", "consistency": "ssp:2",
-                    "_env": {"PSAMD_MX_NATIVE": "1"}})])
+                    "_env": {"PSAMD_MX_NATIVE": "1"}}),
+    # ... and from two graphs per iteration with the event waits / records as external
+    # event nodes inside them
+    ("prep", 3, 1, {"exchange_merge": "on", "_env": {"PSAMD_MX_NATIVE": "1", "PSAMD_MX_G2": "1"}}),
+    ("prep", 2, 1, {"exchange_merge": "on", "consistency": "ssp:2",
+                    "_env": {"PSAMD_MX_NATIVE": "1", "PSAMD_MX_G2": "1"}}),
+    # the tail filter inside the flat localiser: preparations in minibatch order
+    ("prep", 3, 1, {"exchange_merge": "on", "tail_feature_freq": 1}),
+    ("prep", 3, 1, {"exchange_merge": "on", "tail_feature_freq": 1,
+                    "_env": {"PSAMD_MX_NATIVE": "1", "PSAMD_MX_G2": "1"}}),
+    ("prep", 2, 1, {"tail_feature_freq": 1})])
 def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     from parameter_server_amd.ops.synthetic import criteo_batch
 
@@ -160,8 +170,9 @@ def test_bench_captured_collectives_exit_cleanly(consistency):
     assert out["comm"]["rccl_world"] == 1
 
 
-@pytest.mark.parametrize("nprep,native", [(1, "0"), (2, "0"), (2, "1"), (3, "1")])
-def test_flat_pipeline_matches_sequential(monkeypatch, nprep, native):
+@pytest.mark.parametrize("nprep,native,tail", [(1, "0", 0), (2, "0", 0), (2, "1", 0), (3, "1", 0),
+                                               (3, "1", 1), (2, "0", 1)])
+def test_flat_pipeline_matches_sequential(monkeypatch, nprep, native, tail):
     """1 GPU, flat layout: step t pulls minibatch t+1 inside its update launch, so every
     preparation must finish before the step that pulls it and must not refill a buffer a
     pending step still reads (nprep = 1 is run with 2 streams). The pipeline -- eager
@@ -177,7 +188,8 @@ def test_flat_pipeline_matches_sequential(monkeypatch, nprep, native):
     dev = torch.device("cuda")
 
     def trainer():
-        cfg = SparseLRConfig(num_features=N, minibatch=B, table_capacity=1 << 22)
+        cfg = SparseLRConfig(num_features=N, minibatch=B, table_capacity=1 << 22,
+                             tail_feature_freq=tail, countmin_n=1 << 20)
         tr = SparseLRTrainer(cfg, device=dev)
         assert tr.localize_mode == "tpf" and not tr.padded
         return tr

@@ -145,12 +145,14 @@ def test_app_two_ranks_cached_agree_once(tmp_path):
 
     data, model = tmp_path / "data", tmp_path / "model" / "m"
     _write_libsvm(str(data))
-    conf = _conf(tmp_path, data, model, max_delay=2)
+    conf = _conf(tmp_path, data, model, max_delay=2, passes=2)
     cache = str(tmp_path / "cache")
-    for _ in range(2):  # the first run writes the caches, the second streams them
+    # the first run parses pass 1 (agreement every step) and streams pass 2 from the
+    # caches it wrote (agreed once); the second run streams both passes
+    for run, want in ((0, [None, 6]), (1, [6, 6])):
         mp.spawn(_mr_cached_worker, args=(2, _port(), str(conf), str(tmp_path), cache),
                  nprocs=2, join=True)
-    r = [torch.load(tmp_path / f"c{i}.pt") for i in range(2)]
-    assert r[0]["agreed"] == r[1]["agreed"] == 6
-    assert r[0]["examples"] == 1200 and r[1]["examples"] == 600
-    assert r[0]["steps"] == 6 and r[1]["steps"] == 3 and r[1]["idle"] == 3
+        r = [torch.load(tmp_path / f"c{i}.pt") for i in range(2)]
+        assert r[0]["agreed"] == r[1]["agreed"] == want
+        assert r[0]["examples"] == 2400 and r[1]["examples"] == 1200
+        assert r[0]["steps"] == 12 and r[1]["steps"] == 6 and r[1]["idle"] == 6
