@@ -820,9 +820,10 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
     if os.environ.get("PSAMD_MX_G2", "0") == "1":
         # TWO graph launches per iteration: the main stream's graph (wait for exchange t,
         # worker t, record) and the preparation stream's graph (preparation, pack,
-        # all-to-all, owner resolve / apply) with every cross-stream event wait / record
-        # as an EXTERNAL event node inside the graphs (event_wait_ext / event_record_ext)
-        # instead of 6 graph launches + 11 host event calls (benchmarks/probe_graph_events.py)
+        # all-to-all, owner resolve / apply), each a native GraphChain of the captured
+        # pieces with every cross-stream event wait / record as an event node between
+        # them, instead of 6 graph launches + 11 host event calls
+        # (benchmarks/probe_graph_events.py)
         Eg = P * -(-8 // P)
         evg = {k: [torch.cuda.Event() for _ in range(Eg)] for k in ("w", "M", "res", "app")}
         evp = [torch.cuda.Event() for _ in range(NB)]
@@ -830,6 +831,14 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
             e.record(main)
         torch.cuda.synchronize()
         g2 = []
+
+        def piece(fn):  # a captured piece kept as a graph (cloned into the chains)
+            g = torch.cuda.CUDAGraph(keep_graph=True)
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
+                fn()
+            held.append(g)
+            return g
+
         for k in range(Eg):
             if watch is not None:
                 watch.beat("capture2", k)
@@ -837,44 +846,44 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
             s = t + xd
             nb = (t + nprep) % NB
             b = t % NB
-            wfn = tr.mx_worker(t, locs[b], bufs[b][1], width=39)
-            gm = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gm, capture_error_mode=CAPTURE_MODE):
-                H.event_wait_ext(evg["M"][t % Eg])
-                wfn()
-                H.event_record_ext(evg["w"][t % Eg])
+            cm = H.GraphChain()
+            cm.add_wait(evg["M"][t % Eg])
+            cm.add_child(piece(tr.mx_worker(t, locs[b], bufs[b][1], width=39)))
+            cm.add_record(evg["w"][t % Eg])
+            cm.instantiate()
             parts = tr.mx_exchange(s, locs[(s + 1) % NB])
-            gs = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gs, capture_error_mode=CAPTURE_MODE):
-                H.event_wait_ext(evg["w"][(t + nprep - NB) % Eg])
-                if fchain:
-                    H.event_wait_ext(evp[(nb - 1) % NB])
-                prep(nb)
-                if fchain:
-                    H.event_record_ext(evp[nb])
-                parts["pack"]()
-                H.event_wait_ext(evg["w"][(s - d) % Eg])
-                H.event_wait_ext(evg["res"][(s - 1) % Eg])
-                H.event_wait_ext(cchain.ev)
-                parts["comm"]()
-                H.event_record_ext(cchain.ev)
-                H.event_record_ext(evg["M"][s % Eg])
-                H.event_wait_ext(evg["app"][(s - 1) % Eg])
-                if parts["post"]:
-                    parts["resolve"]()
-                    H.event_record_ext(evg["res"][s % Eg])
-                    parts["apply"]()
-                else:
-                    parts["apply"]()
-                    parts["resolve"]()
-                    H.event_record_ext(evg["res"][s % Eg])
-                H.event_record_ext(evg["app"][s % Eg])
-            held.extend([gm, gs])
+            cs = H.GraphChain()
+            cs.add_wait(evg["w"][(t + nprep - NB) % Eg])
+            if fchain:
+                cs.add_wait(evp[(nb - 1) % NB])
+                cs.add_child(piece(lambda nb=nb: prep(nb)))
+                cs.add_record(evp[nb])
+                cs.add_child(piece(parts["pack"]))
+            else:
+                cs.add_child(piece(lambda nb=nb, pk=parts["pack"]: (prep(nb), pk())))
+            cs.add_wait(evg["w"][(s - d) % Eg])
+            cs.add_wait(evg["res"][(s - 1) % Eg])
+            cs.add_wait(cchain.ev)
+            cs.add_child(piece(parts["comm"]))
+            cs.add_record(cchain.ev)
+            cs.add_record(evg["M"][s % Eg])
+            cs.add_wait(evg["app"][(s - 1) % Eg])
+            if parts["post"]:
+                cs.add_child(piece(parts["resolve"]))
+                cs.add_record(evg["res"][s % Eg])
+                cs.add_child(piece(parts["apply"]))
+            else:
+                cs.add_child(piece(parts["apply"]))
+                cs.add_child(piece(parts["resolve"]))
+                cs.add_record(evg["res"][s % Eg])
+            cs.add_record(evg["app"][s % Eg])
+            cs.instantiate()
+            held.extend([cm, cs])
             L = H.LaunchList()
             L.add_stream(main)
-            L.add_graph(gm)
+            L.add_chain(cm)
             L.add_stream(sides[nb % nprep])
-            L.add_graph(gs)
+            L.add_chain(cs)
             L.add_stream(main)
             g2.append(L)
         torch.cuda.synchronize()

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Probe: the merged-exchange iteration's host issue cost with its cross-stream event ops
 as host calls (a native LaunchList of 6 graph launches + 11 event ops, bench.py today)
-against 2 graph launches per iteration whose event waits / records are EXTERNAL event
-nodes inside the graphs (hipEventRecordWithFlags / hipStreamWaitEvent with the external
-flags during capture). Same dependency pattern as bench.py pipeline_merged (main stream
+against 2 graph launches per iteration whose event waits / records are event nodes inside
+the graphs (a native GraphChain: the captured pieces as child graphs, chained with
+hipGraphAddEventWaitNode / hipGraphAddEventRecordNode). Same dependency pattern as bench.py pipeline_merged (main stream
 worker, 3 preparation streams, exchange issued 2 iterations ahead), small kernels, plus
 an ordering check: the worker of step t must see exchange t done (a device counter).
 
@@ -114,32 +114,41 @@ def main():
                 L.add_record(ev["app"][s % E])
                 L.add_stream(main_s)
             else:
-                gm, gside = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gm):
-                    H.event_wait_ext(ev["M"][t % E])
-                    worker()
-                    H.event_record_ext(ev["w"][t % E])
-                with torch.cuda.graph(gside):
-                    H.event_wait_ext(ev["w"][(t + nprep - NB) % E])
-                    prep()
-                    pack()
-                    H.event_wait_ext(ev["w"][(s - 3) % E])
-                    H.event_wait_ext(ev["res"][(s - 1) % E])
-                    H.event_wait_ext(cev)
-                    comm()
-                    H.event_record_ext(cev)
-                    H.event_record_ext(ev["M"][s % E])
-                    H.event_wait_ext(ev["app"][(s - 1) % E])
-                    resolve()
-                    H.event_record_ext(ev["res"][s % E])
-                    apply()
-                    H.event_record_ext(ev["app"][s % E])
-                held += [gm, gside]
+                def cap(fn):
+                    g = torch.cuda.CUDAGraph(keep_graph=True)
+                    with torch.cuda.graph(g):
+                        fn()
+                    held.append(g)
+                    return g
+
+                gw, gpp = cap(worker), cap(lambda: (prep(), pack()))
+                gc, gr, ga = cap(comm), cap(resolve), cap(apply)
+                cm = H.GraphChain()
+                cm.add_wait(ev["M"][t % E])
+                cm.add_child(gw)
+                cm.add_record(ev["w"][t % E])
+                cm.instantiate()
+                cs = H.GraphChain()
+                cs.add_wait(ev["w"][(t + nprep - NB) % E])
+                cs.add_child(gpp)
+                cs.add_wait(ev["w"][(s - 3) % E])
+                cs.add_wait(ev["res"][(s - 1) % E])
+                cs.add_wait(cev)
+                cs.add_child(gc)
+                cs.add_record(cev)
+                cs.add_record(ev["M"][s % E])
+                cs.add_wait(ev["app"][(s - 1) % E])
+                cs.add_child(gr)
+                cs.add_record(ev["res"][s % E])
+                cs.add_child(ga)
+                cs.add_record(ev["app"][s % E])
+                cs.instantiate()
+                held += [cm, cs]
                 L = H.LaunchList()
                 L.add_stream(main_s)
-                L.add_graph(gm)
+                L.add_chain(cm)
                 L.add_stream(xs)
-                L.add_graph(gside)
+                L.add_chain(cs)
                 L.add_stream(main_s)
             plans.append(L)
         torch.cuda.synchronize()

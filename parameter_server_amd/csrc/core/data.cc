@@ -18,17 +18,33 @@ namespace pscore {
 
 namespace {
 
-inline bool is_sep(char c, const char* seps) { return std::strchr(seps, c) != nullptr && c; }
+// Separator sets as 256-entry tables (one load per character; strchr per character
+// was a third of the LIBSVM parse time).
+struct Seps {
+  bool t[256] = {};
+  explicit Seps(const char* s) {
+    for (; *s; ++s) t[(unsigned char)*s] = true;
+  }
+  bool operator()(char c) const { return t[(unsigned char)c]; }
+};
+const Seps kWs(" \t\r");
+const Seps kWsColon(" :\t\r");
+
+inline const Seps& seps_of(const char* s) { return s[1] == ':' ? kWsColon : kWs; }
 
 // Next token in [p, e) delimited by any char of seps; advances p.
-inline bool next_tok(const char*& p, const char* e, const char* seps, const char*& tb,
+inline bool next_tok(const char*& p, const char* e, const Seps& sep, const char*& tb,
                      const char*& te) {
-  while (p < e && is_sep(*p, seps)) ++p;
+  while (p < e && sep(*p)) ++p;
   if (p >= e) return false;
   tb = p;
-  while (p < e && !is_sep(*p, seps)) ++p;
+  while (p < e && !sep(*p)) ++p;
   te = p;
   return true;
+}
+inline bool next_tok(const char*& p, const char* e, const char* seps, const char*& tb,
+                     const char*& te) {
+  return next_tok(p, e, seps_of(seps), tb, te);
 }
 
 inline bool to_u64(const char* b, const char* e, uint64_t* v) {
@@ -55,29 +71,42 @@ struct Checkpoint {
   size_t labels, row_ptr, keys, vals, slots;
 };
 
+// Per-line example sink of one parse_range (reused for every line: no allocation per
+// line). Slot statistics go to a flat per-slot array (slot ids < kDenseSlots; a map
+// above), merged into the batch's info map once at the end.
 class LineSink {
  public:
-  explicit LineSink(ParsedBatch* b) : b_(b) {
-    cp_ = {b->labels.size(), b->row_ptr.size(), b->keys.size(), b->vals.size(), b->slots.size()};
+  static constexpr int kDenseSlots = 4096;
+  // mod: every key reduced mod it (the hashing trick, any format; 0 = raw keys)
+  explicit LineSink(ParsedBatch* b, uint64_t mod = 0) : b_(b), mod_(mod) {}
+  ~LineSink() { flush_info(); }
+  void begin() {
+    cp_ = {b_->labels.size(), b_->row_ptr.size(), b_->keys.size(), b_->vals.size(),
+           b_->slots.size()};
+    any_val_ = false;
+    nline_ = 0;
   }
   void label(float y) { b_->labels.push_back(y); }
   void add(int slot, uint64_t key, float val, bool has_val) {
+    if (mod_) key %= mod_;
     b_->keys.push_back(key);
     b_->vals.push_back(val);
     b_->slots.push_back(slot);
-    if (has_val) any_val_ = true;
-    auto& s = line_slots_[slot];
+    // (explicit values of exactly 1 -- one-hot "k:1" LIBSVM rows -- are binary features)
+    if (has_val && val != 1.f) any_val_ = true;
+    SlotStat& s = line_slot(slot);
     s.min_key = std::min(s.min_key, key);
     s.max_key = std::max(s.max_key, key);
     s.nnz_ele++;
     s.format = has_val ? (s.format == 1 ? 1 : 2) : 3;
   }
-  void dense_slot(int slot) { line_slots_[slot].format = 1; }
+  void dense_slot(int slot) { line_slot(slot).format = 1; }
   bool commit() {
     b_->row_ptr.push_back((int64_t)b_->keys.size());
     if (any_val_) b_->binary = false;
-    for (auto& [id, s] : line_slots_) {
-      auto& t = b_->info[id];
+    for (int i = 0; i < nline_; ++i) {
+      const SlotStat& s = lst_[i];
+      SlotStat& t = info_of(lid_[i]);
       t.min_key = std::min(t.min_key, s.min_key);
       t.max_key = std::max(t.max_key, s.max_key);
       t.nnz_ele += s.nnz_ele;
@@ -97,10 +126,52 @@ class LineSink {
   }
 
  private:
+  // this line's slots (few: a linear scan over the ids seen so far on the line)
+  SlotStat& line_slot(int slot) {
+    for (int i = nline_ - 1; i >= 0; --i)
+      if (lid_[i] == slot) return lst_[i];
+    if (nline_ == (int)lid_.size()) {
+      lid_.resize(lid_.size() * 2 + 8);
+      lst_.resize(lst_.size() * 2 + 8);
+    }
+    lid_[nline_] = slot;
+    lst_[nline_] = SlotStat{};
+    return lst_[nline_++];
+  }
+  SlotStat& info_of(int id) {
+    if (id >= 0 && id < kDenseSlots) {
+      if (dense_.empty()) {
+        dense_.resize(kDenseSlots);
+        dense_seen_.assign(kDenseSlots, 0);
+      }
+      dense_seen_[id] = 1;
+      return dense_[id];
+    }
+    return sparse_[id];
+  }
+  void flush_info() {
+    for (int id = 0; id < (int)dense_seen_.size(); ++id)
+      if (dense_seen_[id]) merge(b_->info[id], dense_[id]);
+    for (auto& [id, s] : sparse_) merge(b_->info[id], s);
+  }
+  static void merge(SlotStat& t, const SlotStat& s) {
+    t.min_key = std::min(t.min_key, s.min_key);
+    t.max_key = std::max(t.max_key, s.max_key);
+    t.nnz_ele += s.nnz_ele;
+    t.nnz_ex += s.nnz_ex;
+    if (s.format) t.format = s.format;
+  }
+
   ParsedBatch* b_;
-  Checkpoint cp_;
+  uint64_t mod_ = 0;
+  Checkpoint cp_{};
   bool any_val_ = false;
-  std::map<int, SlotStat> line_slots_;
+  int nline_ = 0;
+  std::vector<int> lid_;
+  std::vector<SlotStat> lst_;
+  std::vector<SlotStat> dense_;
+  std::vector<char> dense_seen_;
+  std::map<int, SlotStat> sparse_;
 };
 
 bool parse_libsvm(const char* p, const char* e, const ParseOptions&, LineSink& s) {
@@ -114,8 +185,9 @@ bool parse_libsvm(const char* p, const char* e, const ParseOptions&, LineSink& s
     const char* c = std::find(tb, te, ':');
     if (c == te) return false;
     uint64_t idx;
-    float v;
-    if (!to_u64(tb, c, &idx) || !to_f32(c + 1, te, &v)) return false;
+    float v = 1.f;
+    if (!to_u64(tb, c, &idx)) return false;
+    if (!(te - c == 2 && c[1] == '1') && !to_f32(c + 1, te, &v)) return false;  // ("k:1" fast)
     if (idx < last) return false;  // reference requires non-decreasing indices
     last = idx;
     s.add(1, idx, v, true);
@@ -238,8 +310,7 @@ bool parse_criteo(const char* p, const char* e, const ParseOptions& opt, LineSin
         if (r.ec != std::errc() || r.ptr != te) return false;
         id = v;
       }
-      uint64_t key = fmix(((uint64_t)(j + 1) << 48) ^ id);
-      if (opt.hash_mod) key %= opt.hash_mod;
+      const uint64_t key = fmix(((uint64_t)(j + 1) << 48) ^ id);  // (mod in the sink)
       s.add(opt.ignore_fea_slot ? 1 : j + 1, key, 1.f, false);
     }
     ++field;
@@ -270,9 +341,9 @@ void ParsedBatch::append(ParsedBatch&& o) {
   }
 }
 
-bool parse_line(const char* b, const char* e, const ParseOptions& opt, ParsedBatch* out) {
+static bool parse_line_into(const char* b, const char* e, const ParseOptions& opt, LineSink& s) {
   while (e > b && (e[-1] == '\n' || e[-1] == '\r')) --e;
-  LineSink s(out);
+  s.begin();
   bool ok;
   switch (opt.format) {
     case TextFormat::LIBSVM: ok = parse_libsvm(b, e, opt, s); break;
@@ -287,21 +358,34 @@ bool parse_line(const char* b, const char* e, const ParseOptions& opt, ParsedBat
   return ok ? s.commit() : s.rollback();
 }
 
+bool parse_line(const char* b, const char* e, const ParseOptions& opt, ParsedBatch* out) {
+  LineSink s(out, opt.hash_mod);
+  return parse_line_into(b, e, opt, s);
+}
+
 static ParsedBatch parse_range(const char* p, const char* e, const ParseOptions& opt,
                                int64_t max_lines) {
   ParsedBatch out;
-  int64_t n = 0;
-  while (p < e && (max_lines < 0 || n < max_lines)) {
-    const char* le = (const char*)std::memchr(p, '\n', e - p);
-    if (!le) le = e;
-    const char* q = p;
-    while (q < le && (*q == ' ' || *q == '\t' || *q == '\r')) ++q;
-    if (q < le && *q != '#') {
-      parse_line(p, le, opt, &out);
-      ++n;
+  // (reserve from the byte count: a binary feature is >= 4 bytes of text)
+  const size_t guess = (size_t)(e - p) / 8;
+  out.keys.reserve(guess);
+  out.vals.reserve(guess);
+  out.slots.reserve(guess);
+  {
+    LineSink s(&out, opt.hash_mod);
+    int64_t n = 0;
+    while (p < e && (max_lines < 0 || n < max_lines)) {
+      const char* le = (const char*)std::memchr(p, '\n', e - p);
+      if (!le) le = e;
+      const char* q = p;
+      while (q < le && (*q == ' ' || *q == '\t' || *q == '\r')) ++q;
+      if (q < le && *q != '#') {
+        parse_line_into(p, le, opt, s);
+        ++n;
+      }
+      p = le + 1;
     }
-    p = le + 1;
-  }
+  }  // (the sink merges its slot statistics into out.info here)
   return out;
 }
 
@@ -322,8 +406,43 @@ ParsedBatch parse_buffer(const char* data, size_t len, const ParseOptions& opt) 
   for (int t = 0; t < T; ++t)
     th.emplace_back([&, t] { parts[t] = parse_range(cuts[t], cuts[t + 1], opt, -1); });
   for (auto& x : th) x.join();
-  ParsedBatch out = std::move(parts[0]);
-  for (int t = 1; t < T; ++t) out.append(std::move(parts[t]));
+  // concatenate in parallel: every part copies itself into its slice of the output
+  std::vector<size_t> r0(T + 1, 0), k0(T + 1, 0);
+  for (int t = 0; t < T; ++t) {
+    r0[t + 1] = r0[t] + parts[t].labels.size();
+    k0[t + 1] = k0[t] + parts[t].keys.size();
+  }
+  ParsedBatch out;
+  out.labels.resize(r0[T]);
+  out.row_ptr.resize(r0[T] + 1);
+  out.row_ptr[0] = 0;
+  out.keys.resize(k0[T]);
+  out.vals.resize(k0[T]);
+  out.slots.resize(k0[T]);
+  th.clear();
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      const ParsedBatch& q = parts[t];
+      std::copy(q.labels.begin(), q.labels.end(), out.labels.begin() + r0[t]);
+      for (size_t i = 1; i < q.row_ptr.size(); ++i)
+        out.row_ptr[r0[t] + i] = q.row_ptr[i] + (int64_t)k0[t];
+      std::copy(q.keys.begin(), q.keys.end(), out.keys.begin() + k0[t]);
+      std::copy(q.vals.begin(), q.vals.end(), out.vals.begin() + k0[t]);
+      std::copy(q.slots.begin(), q.slots.end(), out.slots.begin() + k0[t]);
+    });
+  for (auto& x : th) x.join();
+  for (int t = 0; t < T; ++t) {
+    out.binary = out.binary && parts[t].binary;
+    out.bad_lines += parts[t].bad_lines;
+    for (auto& [id, st] : parts[t].info) {
+      auto& d = out.info[id];
+      d.min_key = std::min(d.min_key, st.min_key);
+      d.max_key = std::max(d.max_key, st.max_key);
+      d.nnz_ele += st.nnz_ele;
+      d.nnz_ex += st.nnz_ex;
+      if (st.format) d.format = st.format;
+    }
+  }
   return out;
 }
 

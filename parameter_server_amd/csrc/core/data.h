@@ -29,7 +29,7 @@ struct ParseOptions {
   TextFormat format = TextFormat::LIBSVM;
   bool ignore_fea_slot = false;
   bool shuffle_fea_id = false;  // TERAFEA: murmur3 shuffle (reference --shuffle_fea_id)
-  uint64_t hash_mod = 0;        // CRITEO: keys mod this (0 = none)
+  uint64_t hash_mod = 0;        // every key mod this (the hashing trick; 0 = none)
   int nthreads = 1;
   int64_t max_lines = -1;
 };
@@ -40,7 +40,7 @@ struct ParsedBatch {
   std::vector<uint64_t> keys;
   std::vector<float> vals;     // same length as keys, 1.0 for binary features
   std::vector<int32_t> slots;  // slot (feature group) id per nnz
-  bool binary = true;          // true if every value is an implicit 1
+  bool binary = true;          // true if every value is 1 (implicit, or an explicit "k:1")
   int64_t bad_lines = 0;
   std::map<int, SlotStat> info;
 

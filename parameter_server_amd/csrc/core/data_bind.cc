@@ -42,7 +42,10 @@ static py::dict batch_to_py(ParsedBatch&& b) {
 void register_data(py::module_& m) {
   m.def("parse_text", [](py::bytes data, int format, bool ignore_slot, bool shuffle_fea_id,
                          uint64_t hash_mod, int nthreads, int64_t max_lines) {
-    std::string s = data;
+    // (parsed in place: the bytes object is immutable and held by this call)
+    char* ptr = nullptr;
+    Py_ssize_t len = 0;
+    if (PyBytes_AsStringAndSize(data.ptr(), &ptr, &len) != 0) throw py::error_already_set();
     ParseOptions opt;
     opt.format = (TextFormat)format;
     opt.ignore_fea_slot = ignore_slot;
@@ -53,13 +56,37 @@ void register_data(py::module_& m) {
     ParsedBatch b;
     {
       py::gil_scoped_release rel;
-      b = parse_buffer(s.data(), s.size(), opt);
+      b = parse_buffer(ptr, (size_t)len, opt);
     }
     return batch_to_py(std::move(b));
   }, py::arg("data"), py::arg("format"), py::arg("ignore_slot") = false,
      py::arg("shuffle_fea_id") = false, py::arg("hash_mod") = 0, py::arg("nthreads") = 1,
      py::arg("max_lines") = -1);
   m.def("read_file", [](const std::string& path, const std::string& hadoop_home) {
+    // a plain local file goes straight into the bytes object (no second copy)
+    const bool plain = hadoop_home.empty() && path.rfind("hdfs://", 0) != 0 &&
+                       !(path.size() >= 3 && path.compare(path.size() - 3, 3, ".gz") == 0);
+    if (plain) {
+      FILE* f = fopen(path.c_str(), "rb");
+      if (!f) throw std::runtime_error("cannot open " + path);
+      fseek(f, 0, SEEK_END);
+      const long sz = ftell(f);
+      fseek(f, 0, SEEK_SET);
+      PyObject* o = PyBytes_FromStringAndSize(nullptr, sz < 0 ? 0 : sz);
+      if (!o) {
+        fclose(f);
+        throw py::error_already_set();
+      }
+      size_t got = 0;
+      {
+        py::gil_scoped_release rel;
+        got = fread(PyBytes_AS_STRING(o), 1, (size_t)(sz < 0 ? 0 : sz), f);
+      }
+      fclose(f);
+      py::bytes out = py::reinterpret_steal<py::bytes>(o);
+      if ((long)got != sz) throw std::runtime_error("short read of " + path);
+      return out;
+    }
     std::string s;
     {
       py::gil_scoped_release rel;

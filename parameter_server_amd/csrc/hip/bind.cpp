@@ -68,7 +68,7 @@ int tpf_entry_region();
 size_t tpf_temp_bytes(int64_t, int);
 void localize_tpf(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint16_t*, uint64_t*,
                   int32_t*, uint16_t*, int32_t*, int32_t*, bool, hipStream_t, const CmArgs*,
-                  uint8_t*, float*, int64_t);
+                  uint8_t*, float*, int64_t, int32_t*);
 bool tpf_exchange_ok(int64_t, int, int);
 void tpf_pack_keys(int64_t, int, int, const int32_t*, const uint64_t*, int64_t, int, int64_t,
                    int32_t*, int32_t*, const uint64_t*, int64_t, int, hipStream_t);
@@ -351,6 +351,27 @@ struct LaunchList {
   }
 };
 
+// A linear HIP graph composed natively: child graphs (torch CUDAGraphs captured with
+// keep_graph=True, cloned in) and event wait / record nodes, chained in order. One launch
+// replays a stream's whole iteration with its cross-stream event edges in the graph
+// (bench.py's merged pipeline, PSAMD_MX_G2; benchmarks/probe_graph_events.py).
+struct GraphChain {
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ex = nullptr;
+  hipGraphNode_t last = nullptr;
+  std::vector<py::object> keep;
+  GraphChain() { PSAMD_HIP_CHECK(hipGraphCreate(&g, 0)); }
+  ~GraphChain() {
+    if (ex) (void)hipGraphExecDestroy(ex);
+    if (g) (void)hipGraphDestroy(g);
+  }
+  GraphChain(const GraphChain&) = delete;
+  GraphChain& operator=(const GraphChain&) = delete;
+  void chain(hipGraphNode_t n) { last = n; }
+  const hipGraphNode_t* deps() const { return last ? &last : nullptr; }
+  size_t ndeps() const { return last ? 1 : 0; }
+};
+
 Launch make_kv_resolve(Tensor slots, Tensor keys, optional<Tensor> n_dev, Tensor out_slot,
                        optional<Tensor> out_w, bool insert, int init_type, double init_v,
                        double init_s, uint64_t seed, optional<Tensor> err,
@@ -556,7 +577,8 @@ void check_tpf(const TpfBufs& f, int64_t n, int bits, const char* what, bool par
 
 // filt (the fused tail filter, tploc.hip tpf_filter_unit): (cells int32 [the sketch's
 // byte cells as words], rsize, rshift, k, vmax, freq, ecnt uint8 [>= tpf_stride_max(n)],
-// w_ent float32 [the FlatLoc's tile-entry weights])
+// w_ent float32 [the FlatLoc's tile-entry weights][, cnt_pre int32 [like cnt]: the
+// unfiltered counts])
 Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor dcnt, Tensor rep,
                          Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err,
                          bool sorted, optional<py::tuple> filt = {}) {
@@ -574,10 +596,17 @@ Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor d
   std::vector<Tensor> keep{keys, temp, dcnt, rep, uniqf, ent_pos, ent_j, cnt, err};
   bool has_f = false;
   psamd::CmArgs ca{};
-  Tensor ecnt, w_ent;
+  Tensor ecnt, w_ent, cnt_pre;
   if (filt && !filt->is_none()) {
     const py::tuple& f = *filt;
-    check(f.size() == 8, "localize_tpf filt: (cells, rsize, rshift, k, vmax, freq, ecnt, w_ent)");
+    check(f.size() == 8 || f.size() == 9,
+          "localize_tpf filt: (cells, rsize, rshift, k, vmax, freq, ecnt, w_ent[, cnt_pre])");
+    if (f.size() == 9 && !f[8].is_none()) {
+      cnt_pre = f[8].cast<Tensor>();
+      chk(cnt_pre, at::kInt, "filt cnt_pre");
+      check(cnt_pre.numel() >= cnt.numel(), "localize_tpf filt: cnt_pre smaller than cnt");
+      keep.push_back(cnt_pre);
+    }
     Tensor cells = f[0].cast<Tensor>();
     ecnt = f[6].cast<Tensor>();
     w_ent = f[7].cast<Tensor>();
@@ -610,7 +639,8 @@ Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor d
                         ptr<int32_t>(ent_pos), ptr<uint16_t>(ent_j), ptr<int32_t>(cnt),
                         ptr<int32_t>(err), sorted, st, has_f ? &ca : nullptr,
                         has_f ? ptr<uint8_t>(ecnt) : nullptr, has_f ? ptr<float>(w_ent) : nullptr,
-                        has_f ? w_ent.numel() : 0);
+                        has_f ? w_ent.numel() : 0,
+                        cnt_pre.defined() ? ptr<int32_t>(cnt_pre) : nullptr);
   };
 }
 
@@ -1154,8 +1184,57 @@ PYBIND11_MODULE(_hipops, m) {
   // (resolve, fused forward + backward, fused scan + update) runs from one per
   // minibatch buffer: three pybind crossings with 60 tensor / scalar arguments cost
   // ~10 us of host issue time per step (profiles/r3_s3_host_issue.log).
+  py::class_<GraphChain>(m, "GraphChain")
+      .def(py::init<>())
+      .def("add_child", [](GraphChain& c, py::object torch_graph) {
+        check(c.ex == nullptr, "GraphChain: already instantiated");
+        const py::object h = torch_graph.attr("raw_cuda_graph")();
+        const hipGraph_t child = reinterpret_cast<hipGraph_t>(h.cast<uint64_t>());
+        check(child != nullptr, "GraphChain.add_child: capture with keep_graph=True");
+        hipGraphNode_t n;
+        PSAMD_HIP_CHECK(hipGraphAddChildGraphNode(&n, c.g, c.deps(), c.ndeps(), child));
+        c.chain(n);
+        c.keep.push_back(torch_graph);
+      })
+      .def("add_wait", [](GraphChain& c, py::object event) {
+        check(c.ex == nullptr, "GraphChain: already instantiated");
+        hipGraphNode_t n;
+        PSAMD_HIP_CHECK(hipGraphAddEventWaitNode(&n, c.g, c.deps(), c.ndeps(),
+                                                 list_event(event, "GraphChain.add_wait")));
+        c.chain(n);
+        c.keep.push_back(event);
+      })
+      .def("add_record", [](GraphChain& c, py::object event) {
+        check(c.ex == nullptr, "GraphChain: already instantiated");
+        hipGraphNode_t n;
+        PSAMD_HIP_CHECK(hipGraphAddEventRecordNode(&n, c.g, c.deps(), c.ndeps(),
+                                                   list_event(event, "GraphChain.add_record")));
+        c.chain(n);
+        c.keep.push_back(event);
+      })
+      .def("instantiate", [](GraphChain& c) {
+        if (!c.ex) PSAMD_HIP_CHECK(hipGraphInstantiate(&c.ex, c.g, nullptr, nullptr, 0));
+      })
+      .def("launch", [](GraphChain& c) {
+        check(c.ex != nullptr, "GraphChain: instantiate first");
+        PSAMD_HIP_CHECK(hipGraphLaunch(c.ex, cur_stream()));
+      })
+      // (like CUDAGraph.reset: frees the executable graph; the caller synchronised)
+      .def("reset", [](GraphChain& c) {
+        if (c.ex) PSAMD_HIP_CHECK(hipGraphExecDestroy(c.ex));
+        c.ex = nullptr;
+        c.keep.clear();
+      });
+
   py::class_<LaunchList>(m, "LaunchList")
       .def(py::init<>())
+      .def("add_chain", [](LaunchList& l, py::object chain) {
+        GraphChain& c = chain.cast<GraphChain&>();
+        check(c.ex != nullptr, "add_chain: instantiate the GraphChain first");
+        const hipGraphExec_t ex = c.ex;
+        l.keep.push_back(chain);
+        l.push_op([ex](hipStream_t& s) { PSAMD_HIP_CHECK(hipGraphLaunch(ex, s)); }, "chain");
+      })
       .def("add_kv_resolve", [](LaunchList& l, Tensor slots, Tensor keys, optional<Tensor> n_dev,
                                 Tensor out_slot, optional<Tensor> out_w, bool insert,
                                 int init_type, double init_v, double init_s, uint64_t seed,

@@ -1820,7 +1820,7 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
                   int32_t* __restrict__ ent_pos, uint16_t* __restrict__ ent_j,
                   int32_t* __restrict__ cnt, int32_t* __restrict__ err, int sorted,
                   const uint8_t* __restrict__ ecnt, CmArgs cm, float* __restrict__ w_ent,
-                  int64_t w_cap) {
+                  int64_t w_cap, int32_t* __restrict__ cnt_pre) {
   using namespace tp;
   __shared__ uint16_t eh[kECapL];  // hash slot of every gathered entry
   __shared__ uint64_t hs[kDH];     // hash (key u32 | count u32 -> key index)
@@ -1907,6 +1907,13 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
       E1k = res[1];
     }
     if (t == 0) {
+      if (cnt_pre) {  // the unfiltered counts (the exchange rows are sized from them)
+        int32_t* cp = cnt_pre + (int64_t)b * 4;
+        cp[0] = (int32_t)D0;
+        cp[1] = (int32_t)E0;
+        cp[2] = (int32_t)D1;
+        cp[3] = (int32_t)E1;
+      }
       co[0] = (int32_t)D0k;
       co[1] = (int32_t)E0k;
       co[2] = (int32_t)D1k;
@@ -2757,7 +2764,7 @@ size_t tpf_temp_bytes(int64_t n, int bits) {  // (any minibatch of <= n keys: tp
 void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
                   int32_t* dcnt, uint16_t* rep, uint64_t* uniqf, int32_t* ent_pos, uint16_t* ent_j,
                   int32_t* cnt, int32_t* err, bool sorted, hipStream_t st, const CmArgs* filt,
-                  uint8_t* ecnt, float* w_ent, int64_t w_cap) {
+                  uint8_t* ecnt, float* w_ent, int64_t w_cap, int32_t* cnt_pre) {
   if (n <= 0) return;
   if (!tploc_supported(n, m.bits)) throw std::runtime_error("localize_tpf: unsupported size");
   if (temp_bytes < tpf_temp_bytes(n, m.bits)) throw std::runtime_error("localize_tpf: temp");
@@ -2786,11 +2793,11 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
   if (filt)
     tpf_bucket_kernel<true><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
         tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
-        sorted ? 1 : 0, ecnt, *filt, w_ent, w_cap);
+        sorted ? 1 : 0, ecnt, *filt, w_ent, w_cap, cnt_pre);
   else
     tpf_bucket_kernel<false><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
         tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
-        sorted ? 1 : 0, nullptr, CmArgs{}, nullptr, 0);
+        sorted ? 1 : 0, nullptr, CmArgs{}, nullptr, 0, nullptr);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

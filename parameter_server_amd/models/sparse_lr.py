@@ -1099,7 +1099,9 @@ class SparseLRTrainer:
         elif C <= 0 and getattr(loc, "flat", False):
             # keys per owner: the owner's buckets' unit counts (buckets [p * B/G, ...))
             g = hipops().tpf_groups(loc.nnz, loc.bits)
-            c = loc.cnt[:4 * g].view(G, g // G, 4).to(torch.float64)
+            # (tail filter: the unfiltered counts -- later minibatches keep more keys)
+            cc = loc.cnt_pre if getattr(loc, "cnt_pre", None) is not None else loc.cnt
+            c = cc[:4 * g].view(G, g // G, 4).to(torch.float64)
             cnt = (c[:, :, 0] + c[:, :, 2]).sum(1).max().reshape(1)
             cnt = self.comm.all_reduce_(cnt.to(self.comm.device) if self.comm.backend == "nccl"
                                         else cnt.cpu(), op="max")

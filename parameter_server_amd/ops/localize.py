@@ -82,6 +82,7 @@ class FlatLoc:
     nnz: int = 0
     gen: int = 0
     ecnt: torch.Tensor | None = None  # uint8 [tiles*TP_TILE] tail filter: entry occurrences
+    cnt_pre: torch.Tensor | None = None  # tail filter: the counts before filtering
     flat = True
 
     @property
@@ -182,7 +183,8 @@ class Localizer:
                 ent_pos=i32(g * er), ent_j=torch.zeros(g * er, dtype=torch.int16, device=dev),
                 slot_u=i32(g * kr), err=i32(1), bits=self.bits,
                 ecnt=(torch.zeros(N, dtype=torch.uint8, device=dev) if tail_filter is not None
-                      else None))
+                      else None),
+                cnt_pre=i32(4 * g) if tail_filter is not None else None)
             self.err = self.flat.err
             return
         if self.gpu and self.mode == "tp":
@@ -264,7 +266,7 @@ class Localizer:
         if cm.rshift >= 64 or cm.key_bits != self.bits:
             raise ValueError("the fused tail filter needs a CountMinSketch partitioned over "
                              "this localiser's key bits")
-        return (*cm.args(freq), self.flat.ecnt, self.flat.w_ent)
+        return (*cm.args(freq), self.flat.ecnt, self.flat.w_ent, self.flat.cnt_pre)
 
     def check(self):
         """Host sync: raise if a "part" localisation overflowed a bucket's LDS hash."""

@@ -210,8 +210,13 @@ def test_app_matches_cpu_runtime_app(tmp_path):
     from parameter_server_amd.parallel.comm import LocalComm
     from parameter_server_amd.utils.config import load_app_config
 
-    lm = load_app_config(str(c_app)).linear_method
+    # (one progress window over the whole run: the app's time-based windows would make
+    # the comparison depend on how fast this host runs it)
+    c_one = tmp_path / "app_one.conf"
+    c_one.write_text(c_app.read_text().replace("report_interval: 1", "report_interval: 100000"))
+    lm = load_app_config(str(c_one)).linear_method
     res = run_async_sgd(lm, LocalComm("cpu"), torch.device("cpu"), _flags())
+    assert res["progress"]["examples"] == 3 * 600
     loss_rt, auc_rt = float(rt_lines[-1][2]), float(rt_lines[-1][3])
     assert abs(loss_rt - res["progress"]["loss"]) < 0.1, (loss_rt, res["progress"])
     assert abs(auc_rt - res["progress"]["auc"]) < 0.1, (auc_rt, res["progress"])

@@ -124,6 +124,67 @@ def test_pipeline_matches_sequential(monkeypatch, xmode, nprep, graph, kw):
     assert abs(loss_p - ref.progress()["loss"]) < 1e-4
 
 
+def _g2_parity_main(env: str):
+    """(run in a fresh process: a 1-rank RCCL group) the merged pipeline on the 2-peer
+    RCCL loopback -- native launch lists, or PSAMD_MX_G2 two graph chains per iteration --
+    against the two-collective sequential trainer; prints the max weight difference."""
+    import json
+
+    from parameter_server_amd.models import SparseLRConfig, SparseLRTrainer
+    from parameter_server_amd.ops.synthetic import criteo_batch
+    from parameter_server_amd.parallel.comm import LoopbackComm, nccl_loopback
+
+    os.environ.update(json.loads(env))
+    bench = _bench()
+    B, N, seed, extra = 4096, 10 ** 6, 77, 9
+    dev = torch.device("cuda")
+    kw = dict(num_features=N, minibatch=B, consistency="ssp:4", exchange_merge="on")
+    tr = SparseLRTrainer(SparseLRConfig(**kw), nccl_loopback(2, dev), dev)
+    assert tr.merged
+    keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
+    labels = torch.empty(B, dtype=torch.float32, device=dev)
+    args = argparse.Namespace(warmup=0, graph=1)
+    it, _ = bench.pipeline(tr, B, N, seed, keys, labels, dev, args, nprep=3)
+    for _ in range(extra):
+        it()
+    torch.cuda.synchronize()
+    T = tr._xt
+    tr.mx_drain()
+    pk, pw = _weights(tr)
+    ref = SparseLRTrainer(SparseLRConfig(**dict(kw, exchange_merge="off")),
+                          LoopbackComm(2, "cuda"), dev)
+    for m in range(T):
+        k, lab = criteo_batch(B, seed=seed, row0=m * B, num_features=N, device=dev)
+        ref.step(k, lab, width=39)
+    ref.flush()
+    torch.cuda.synchronize()
+    rk, rw = _weights(ref)
+    pos = torch.searchsorted(pk, rk)
+    assert torch.equal(pk[pos], rk)
+    print(json.dumps({"native": getattr(args, "native_iter", None), "steps": T,
+                      "maxdiff": float((pw[pos] - rw).abs().max())}), flush=True)
+
+
+@pytest.mark.parametrize("g2", ["0", "1"])
+def test_merged_native_rccl_pipeline_matches_sequential(g2):
+    """The merged pipeline's native iteration on a real (1-rank RCCL) communicator, with
+    the event ops as host calls (launch lists) or as event nodes inside two graph chains
+    per iteration (PSAMD_MX_G2=1): same table as the sequential trainer."""
+    import json
+    import subprocess
+    import sys
+
+    env = json.dumps({"PSAMD_MX_G2": g2, "PSAMD_MX_NATIVE": "1"})
+    code = ("import sys; sys.path.insert(0, 'tests'); import test_bench_pipeline_gpu as t; "
+            f"t._g2_parity_main({env!r})")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       timeout=240, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["native"] == ("graph2" if g2 == "1" else True), out
+    assert out["maxdiff"] < 1e-5, out
+
+
 @pytest.mark.parametrize("apply", ["stream", "tail"])
 def test_asp_pipeline_trains(monkeypatch, apply):
     """asp: the owner's push applies replay on their own stream (or at the tail of the
