@@ -119,9 +119,18 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     if tile_gate:
         for e in ev_fb:
             e.record(torch.cuda.current_stream(device))
+    # tail filter: the bucket kernels (CountMin insert + query) in minibatch order, the
+    # generators and tile kernels of the preparations still overlapping
+    fchain = tr.filter is not None
+    ev_bk = [torch.cuda.Event() for _ in range(NB)] if (flat and fchain) else None
+    if ev_bk is not None:
+        for e in ev_bk:
+            e.record(torch.cuda.current_stream(device))
     fplans = ([tr.prep_plan(b, bufs[b][0], bufs[b][1], seed=seed, row0=b * B, row_step=NB * B,
                             num_features=N,
-                            gate=ev_fb[(b - nprep) % NB] if tile_gate else None)
+                            gate=ev_fb[(b - nprep) % NB] if tile_gate else None,
+                            bucket_after=ev_bk[(b - 1) % NB] if ev_bk else None,
+                            bucket_done=ev_bk[b] if ev_bk else None)
                for b in range(NB)] if flat else None)
 
     def prep(b):  # buffer b belongs to prep stream b % nprep (rows (nprep*k + s) * B)
@@ -181,9 +190,10 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     # first and replays as ONE captured graph (pack + all-to-all A + owner work + B).
     early = (post or asp_apply == "tail") and (tr.filter is None or tr._flat_x)
     # tail filter: the CountMin inserts and queries of consecutive minibatches run in
-    # minibatch order (the reference's MinibatchReader::read sequence), so a preparation
-    # also waits for the previous minibatch's preparation (on another stream)
-    fchain = tr.filter is not None
+    # minibatch order (the reference's MinibatchReader::read sequence): a preparation
+    # waits for the previous minibatch's (on another stream); the flat launch lists order
+    # only their bucket kernels (ev_bk above)
+    fchain = tr.filter is not None and fplans is None
     E = 64  # event rings, indexed by step (every look-back here is < 64 steps)
     ev_buf = [torch.cuda.Event() for _ in range(NB)]   # worker done with buffer b
     ev_w = [torch.cuda.Event() for _ in range(E)]      # worker half of step t done

@@ -68,7 +68,7 @@ int tpf_entry_region();
 size_t tpf_temp_bytes(int64_t, int);
 void localize_tpf(const uint64_t*, int64_t, KeyMix, void*, size_t, int32_t*, uint16_t*, uint64_t*,
                   int32_t*, uint16_t*, int32_t*, int32_t*, bool, hipStream_t, const CmArgs*,
-                  uint8_t*, float*, int64_t, int32_t*);
+                  uint8_t*, float*, int64_t, int32_t*, int);
 bool tpf_exchange_ok(int64_t, int, int);
 void tpf_pack_keys(int64_t, int, int, const int32_t*, const uint64_t*, int64_t, int, int64_t,
                    int32_t*, int32_t*, const uint64_t*, int64_t, int, hipStream_t);
@@ -581,7 +581,8 @@ void check_tpf(const TpfBufs& f, int64_t n, int bits, const char* what, bool par
 // unfiltered counts])
 Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor dcnt, Tensor rep,
                          Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err,
-                         bool sorted, optional<py::tuple> filt = {}) {
+                         bool sorted, optional<py::tuple> filt = {}, int stage = 0) {
+  check(stage >= 0 && stage <= 2, "localize_tpf: stage 0 (both), 1 (tile), 2 (bucket)");
   chk(keys, at::kLong, "keys");
   chk(temp, at::kByte, "temp");
   chk(dcnt, at::kInt, "dcnt");
@@ -640,7 +641,7 @@ Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor d
                         ptr<int32_t>(err), sorted, st, has_f ? &ca : nullptr,
                         has_f ? ptr<uint8_t>(ecnt) : nullptr, has_f ? ptr<float>(w_ent) : nullptr,
                         has_f ? w_ent.numel() : 0,
-                        cnt_pre.defined() ? ptr<int32_t>(cnt_pre) : nullptr);
+                        cnt_pre.defined() ? ptr<int32_t>(cnt_pre) : nullptr, stage);
   };
 }
 
@@ -1268,12 +1269,12 @@ PYBIND11_MODULE(_hipops, m) {
       .def("add_localize_tpf", [](LaunchList& l, Tensor keys, int64_t n, int bits, Tensor temp,
                                   Tensor dcnt, Tensor rep, Tensor uniqf, Tensor ent_pos,
                                   Tensor ent_j, Tensor cnt, Tensor err, bool sorted,
-                                  optional<py::tuple> filt) {
+                                  optional<py::tuple> filt, int stage) {
         l.push(make_localize_tpf(keys, n, bits, temp, dcnt, rep, uniqf, ent_pos, ent_j,
-                                          cnt, err, sorted, filt), "localize_tpf");
+                                          cnt, err, sorted, filt, stage), "localize_tpf");
       }, py::arg("keys"), py::arg("n"), py::arg("bits"), py::arg("temp"), py::arg("dcnt"),
          py::arg("rep"), py::arg("uniqf"), py::arg("ent_pos"), py::arg("ent_j"), py::arg("cnt"),
-         py::arg("err"), py::arg("sorted"), py::arg("filt") = py::none())
+         py::arg("err"), py::arg("sorted"), py::arg("filt") = py::none(), py::arg("stage") = 0)
       .def("add_tpf_step", [](LaunchList& l, int64_t n, int bits, optional<py::tuple> A,
                               optional<Tensor> psum, optional<py::tuple> B,
                               optional<Tensor> w_ent, Tensor slots, int init_type, double init_v,

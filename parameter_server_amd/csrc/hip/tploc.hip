@@ -2764,7 +2764,7 @@ size_t tpf_temp_bytes(int64_t n, int bits) {  // (any minibatch of <= n keys: tp
 void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t temp_bytes,
                   int32_t* dcnt, uint16_t* rep, uint64_t* uniqf, int32_t* ent_pos, uint16_t* ent_j,
                   int32_t* cnt, int32_t* err, bool sorted, hipStream_t st, const CmArgs* filt,
-                  uint8_t* ecnt, float* w_ent, int64_t w_cap, int32_t* cnt_pre) {
+                  uint8_t* ecnt, float* w_ent, int64_t w_cap, int32_t* cnt_pre, int stage) {
   if (n <= 0) return;
   if (!tploc_supported(n, m.bits)) throw std::runtime_error("localize_tpf: unsupported size");
   if (temp_bytes < tpf_temp_bytes(n, m.bits)) throw std::runtime_error("localize_tpf: temp");
@@ -2775,7 +2775,10 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
   auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
   uint32_t* tkeys = (uint32_t*)take((size_t)g.N * 4);
   uint16_t* toff = (uint16_t*)take((size_t)g.T * (g.nbk + 1) * 2);
+  // stage 1: the tile kernel only, 2: the bucket kernel only (a caller orders something
+  // between them: the tail filter's bucket kernels run in minibatch order), 0: both
   const bool q = m.bits > 31;
+  if (stage == 2) goto bucket;
   if (filt && q)
     tp_tile_kernel<true, true><<<(unsigned)g.T, tp::kThr, 0, st>>>(
         raw, n, m, g.shift, g.nbk, tkeys, toff, dcnt, rep, err, g.lts, ecnt);
@@ -2789,6 +2792,8 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
     tp_tile_kernel<false><<<(unsigned)g.T, tp::kThr, 0, st>>>(raw, n, m, g.shift, g.nbk, tkeys, toff,
                                                               dcnt, rep, err, g.lts);
   PSAMD_HIP_CHECK(hipGetLastError());
+  if (stage == 1) return;
+bucket:
   const bool pair = g.nbk >= 2 && g.shift <= 30;
   if (filt)
     tpf_bucket_kernel<true><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(

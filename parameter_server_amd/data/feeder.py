@@ -93,6 +93,7 @@ class DeviceFeeder:
         self._caches = self._open_caches()
         self._error: BaseException | None = None
         self._mode = "text"
+        self._vcache = {}
         self._alloc_slots(self.depth)
 
     # ------------------------------------------------------------ setup
@@ -136,6 +137,21 @@ class DeviceFeeder:
             self._used = [False] * depth
         for s in range(depth):
             self._free.put(s)
+
+    def _views(self, s: int, B: int, n: int, rp: bool, vals: bool):
+        """Device-slot views of one minibatch shape, the SAME tensor objects whenever the
+        shape repeats: the trainer caches its native launch lists per tensor identity, so
+        fresh views every step would rebuild (and re-validate) them every step."""
+        key = (s, B, n, rp, vals)
+        v = self._vcache.get(key)
+        if v is None:
+            d = self._d[s]
+            if len(self._vcache) > 64:
+                self._vcache.clear()
+            v = self._vcache[key] = (d["keys"][:n], d["labels"][:B],
+                                     d["row_ptr"][:B + 1] if rp else None,
+                                     d["vals"][:n] if vals else None)
+        return v
 
     # ------------------------------------------------------------ planning (cache)
     def _plan_pass(self, order) -> list[list[tuple]]:
@@ -241,8 +257,8 @@ class DeviceFeeder:
                     self._h2d_done[s].record(cs)
                 self._used[s] = True
                 self.bytes_h2d += n * (8 + (4 if vals is not None else 0)) + B * 12 + 8
-                out_q.put(DeviceBatch(d["keys"][:n], d["labels"][:B], d["row_ptr"][:B + 1],
-                                      None if vals is None else d["vals"][:n], B, n, s, width))
+                v = self._views(s, B, n, True, vals is not None)
+                out_q.put(DeviceBatch(v[0], v[1], v[2], v[3], B, n, s, width))
         except BaseException as e:  # noqa: BLE001  (re-raised by the consumer)
             self._error = e
         finally:
@@ -387,9 +403,8 @@ class DeviceFeeder:
                 self.bytes_h2d += n * (kb + (4 if has_vals else 0)) + B * 4 + \
                     (0 if width else 8 * (B + 1))
                 torch.cuda.current_stream(self.device).wait_event(self._h2d_done[s])
-                yield DeviceBatch(d["keys"][:n], d["labels"][:B],
-                                  None if width else d["row_ptr"][:B + 1],
-                                  d["vals"][:n] if has_vals else None, B, n, s, width)
+                v = self._views(s, B, n, not width, has_vals)
+                yield DeviceBatch(v[0], v[1], v[2], v[3], B, n, s, width)
         finally:
             stop.set()
             for th in ths:

@@ -581,13 +581,18 @@ class SparseLRTrainer:
         return plan, nxt
 
     def prep_plan(self, buf: int, keys: torch.Tensor, labels: torch.Tensor, *, seed: int,
-                  row0: int, row_step: int, num_features: int, alpha: float = 1.1, gate=None):
+                  row0: int, row_step: int, num_features: int, alpha: float = 1.1, gate=None,
+                  bucket_after=None, bucket_done=None):
         """Flat mode: a native launch list that generates the next synthetic minibatch of
         workspace ``buf`` (rows row0, row0 + row_step, ... on successive runs) and
         localises it (tile + flat bucket kernels): ONE host call per data preparation.
         ``gate``: an event the localisation waits for after the generator (bench.py: the
         training step's fused forward/backward, so the two LDS-heavy 1024-thread kernels
-        do not share the CUs). Returns a callable -> the FlatLoc of ``buf``."""
+        do not share the CUs). ``bucket_after`` / ``bucket_done`` (tail filter): the
+        bucket kernel (CountMin insert + query) waits for the previous minibatch's bucket
+        kernel and records its own, so sketch updates run in minibatch order while the
+        generators and tile kernels of several preparations still overlap. Returns a
+        callable -> the FlatLoc of ``buf``."""
         from ..ops.synthetic import CRITEO_1TB_CARDS, _set_cards
 
         if self.localize_mode != "tpf":
@@ -605,8 +610,19 @@ class SparseLRTrainer:
                             labels)
         if gate is not None:
             plan.add_wait(gate)
-        plan.add_localize_tpf(keys, n, self.bits, lz.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos,
-                              f.ent_j, f.cnt, f.err, self._flat_x, filt=lz.filt_args())
+        if bucket_after is None and bucket_done is None:
+            plan.add_localize_tpf(keys, n, self.bits, lz.ptemp, f.dcnt, f.rep, f.uniqf,
+                                  f.ent_pos, f.ent_j, f.cnt, f.err, self._flat_x,
+                                  filt=lz.filt_args())
+        else:
+            for stage in (1, 2):
+                if stage == 2 and bucket_after is not None:
+                    plan.add_wait(bucket_after)
+                plan.add_localize_tpf(keys, n, self.bits, lz.ptemp, f.dcnt, f.rep, f.uniqf,
+                                      f.ent_pos, f.ent_j, f.cnt, f.err, self._flat_x,
+                                      filt=lz.filt_args(), stage=stage)
+            if bucket_done is not None:
+                plan.add_record(bucket_done)
 
         def run():
             plan.run()

@@ -137,7 +137,7 @@ def _g2_parity_main(env: str):
     os.environ.update(json.loads(env))
     bench = _bench()
     B, N, seed, extra = 4096, 10 ** 6, 77, 9
-    dev = torch.device("cuda")
+    dev = torch.device("cuda", 0)
     kw = dict(num_features=N, minibatch=B, consistency="ssp:4", exchange_merge="on")
     tr = SparseLRTrainer(SparseLRConfig(**kw), nccl_loopback(2, dev), dev)
     assert tr.merged
