@@ -111,10 +111,12 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     locs = [None] * NB
     mode = {"capture": False}
     # 1 GPU, native iteration: the localisation (tile kernel) of the minibatch prepared in
-    # iteration t waits for step t's fused forward/backward (PSAMD_TILE_GATE=1): the two
-    # LDS-heavy 1024-thread kernels otherwise share the CUs when the pipeline's phases
-    # line them up (10^10 features: fwd/bwd 26 -> 46 us, profiles/r6_1e10.log)
-    tile_gate = flat and os.environ.get("PSAMD_TILE_GATE", "0") == "1"
+    # iteration t waits for step t's fused forward/backward (PSAMD_TILE_GATE=0: off). The
+    # two LDS-heavy 1024-thread kernels otherwise share the CUs whenever the pipeline's
+    # phases line them up, and both run 1.3-1.7x longer: that was the 10^10-feature
+    # slowdown (fwd/bwd 26 -> 46 us pipelined; 300 steps 0.1052 -> 0.0815 ms with the
+    # gate, 10^9 0.0835 -> 0.0805, profiles/r6_1e10.log)
+    tile_gate = flat and os.environ.get("PSAMD_TILE_GATE", "1") == "1"
     ev_fb = [torch.cuda.Event() for _ in range(NB)] if tile_gate else None
     if tile_gate:
         for e in ev_fb:
