@@ -50,6 +50,7 @@ def write_files(d, kind, rows, files, seed=0, N=10 ** 8):
     rng = np.random.default_rng(seed)
     per = rows // files
     for f in range(files):
+        print(f"[bench_app] writing file {f + 1} / {files}", file=sys.stderr, flush=True)
         if kind == "criteo":
             keys = np.sort((N * rng.random((per, 39)) ** 4).astype(np.int64), axis=1)
             y = np.where(rng.random(per) < 0.3, 1, -1)
@@ -109,7 +110,7 @@ training_data {{ format: TEXT text: LIBSVM file: "{d}/part.*" }}
 loss {{ type: LOGIT }}
 penalty {{ type: L1 lambda: 10 lambda: 1 }}
 learning_rate {{ type: DECAY alpha: 0.01 beta: 10 }}
-async_sgd {{ algo: FTRL minibatch: {a.minibatch} num_data_pass: 1 report_interval: 1000 }}
+async_sgd {{ algo: FTRL minibatch: {a.minibatch} num_data_pass: 1 report_interval: 10 }}
 }}""")
     lm = load_app_config(conf).linear_method
     dev = torch.device("cuda")
@@ -117,13 +118,17 @@ async_sgd {{ algo: FTRL minibatch: {a.minibatch} num_data_pass: 1 report_interva
 
     cache = os.path.join(d, "cache") if a.cache else "off"
     runs = []
+    print(f"[bench_app] {a.rows} rows in {a.files} files ({mb:.0f} MB of text) in {gen_s:.1f} s",
+          file=sys.stderr, flush=True)
     for r in range(2 if a.cache else 1):
         flags = types.SimpleNamespace(
             num_features=1e8, max_nnz_per_example=160 if a.kind == "rcv1" else 39,
-            num_threads=a.threads, device="cuda", seed=0, table_capacity=1 << 26, quiet=True,
+            num_threads=a.threads, device="cuda", seed=0, table_capacity=1 << 27, quiet=False,
             data_cache=cache, io_threads=a.io_threads, report_steps=0)
         res = run_async_sgd(lm, LocalComm(dev), dev, flags)
         tr = res["trainer"]
+        print(f"[bench_app] run {r}: {res['examples'] / res['seconds'] / 1e6:.2f} M ex/s "
+              f"({'cache' if res['cached_passes'] else 'text'})", file=sys.stderr, flush=True)
         runs.append({"source": "cache" if res["cached_passes"] else "text",
                      "rows": res["examples"], "steps": res["steps"],
                      "seconds": round(res["seconds"], 3),

@@ -629,6 +629,7 @@ Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor d
     check(ecnt.numel() >= psamd::tpf_stride_max(n), "localize_tpf filt: ecnt too small");
     check(w_ent.numel() >= psamd::tpf_stride(n), "localize_tpf filt: w_ent too small");
     ca.cells = ptr<uint32_t>(cells);
+    ca.ncells32 = (uint64_t)cells.numel() * 4 <= ((uint64_t)1 << 32) ? 1 : 0;
     keep.push_back(cells);
     keep.push_back(ecnt);
     keep.push_back(w_ent);

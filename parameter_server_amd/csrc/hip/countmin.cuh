@@ -33,6 +33,7 @@ struct CmArgs {
   int k;             // probes
   uint32_t vmax;     // saturation
   int freq;          // keep keys whose estimate > freq
+  int ncells32;      // every cell index < 2^32 (the batched forms' 32-bit indices)
 };
 
 __host__ __device__ __forceinline__ uint64_t cm_base(uint64_t key, int rshift, uint64_t rsize) {
@@ -82,6 +83,90 @@ __device__ __forceinline__ uint32_t cm_query_key(const CmArgs& a, uint64_t key) 
     h += delta;
   }
   return res;
+}
+
+// Batched forms for a thread holding several keys (the flat localiser's fused filter):
+// every cell's word load, then every CAS, are issued before any result is used, so a
+// thread pays ~2 memory round trips for all its keys instead of 2 per probe (a dependent
+// chain of 16 for 4 keys x 2 probes). A CAS that lost a race (another key on the same
+// word) retries alone. Exactly kCmBatchK probes (the reference default k = 2; other k:
+// the one-key forms). Word indices and region sizes are 32-bit (the caller checks).
+constexpr int kCmBatchK = 2;
+
+template <int kN>
+__device__ __forceinline__ void cm_cells_batch(const CmArgs& a, const uint64_t (&key)[kN],
+                                               uint32_t (&cell)[kN][kCmBatchK]) {
+  const uint32_t rs = (uint32_t)a.rsize;  // (32-bit cell indices: the caller checks)
+#pragma unroll
+  for (int q = 0; q < kN; ++q) {
+    const uint32_t base = (uint32_t)cm_base(key[q], a.rshift, a.rsize);
+    uint32_t h = sketch_hash(key[q]);
+    const uint32_t delta = (h >> 17) | (h << 15);
+#pragma unroll
+    for (int j = 0; j < kCmBatchK; ++j) {
+      cell[q][j] = base + h % rs;
+      h += delta;
+    }
+  }
+}
+
+template <int kN>
+__device__ __forceinline__ void cm_insert_batch(const CmArgs& a, const uint64_t (&key)[kN],
+                                                const uint32_t (&cnt)[kN], uint32_t valid) {
+  uint32_t cell[kN][kCmBatchK], old[kN][kCmBatchK];
+  cm_cells_batch<kN>(a, key, cell);
+#pragma unroll
+  for (int q = 0; q < kN; ++q)
+#pragma unroll
+    for (int j = 0; j < kCmBatchK; ++j)
+      old[q][j] = ((valid >> q) & 1u) && cnt[q]
+                      ? __hip_atomic_load(a.cells + (cell[q][j] >> 2), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT)
+                      : 0u;
+  uint32_t lost = 0;  // bit q * K + j: that CAS lost a race
+#pragma unroll
+  for (int q = 0; q < kN; ++q)
+#pragma unroll
+    for (int j = 0; j < kCmBatchK; ++j)
+      if (((valid >> q) & 1u) && cnt[q]) {
+        const uint32_t sh = (cell[q][j] & 3u) * 8u;
+        const uint32_t b = (old[q][j] >> sh) & 0xffu;
+        const uint32_t nb = (cnt[q] > a.vmax - b) ? a.vmax : b + cnt[q];
+        if (nb != b && atomicCAS(a.cells + (cell[q][j] >> 2), old[q][j],
+                                 (old[q][j] & ~(0xffu << sh)) | (nb << sh)) != old[q][j])
+          lost |= 1u << (q * kCmBatchK + j);
+      }
+#pragma unroll
+  for (int q = 0; q < kN; ++q)
+#pragma unroll
+    for (int j = 0; j < kCmBatchK; ++j)
+      if ((lost >> (q * kCmBatchK + j)) & 1u)
+        sat_add_byte(a.cells, cell[q][j], cnt[q], a.vmax);  // (lost a race: retry alone)
+}
+
+// min over each key's cells, all loads in flight together
+template <int kN>
+__device__ __forceinline__ void cm_query_batch(const CmArgs& a, const uint64_t (&key)[kN],
+                                               uint32_t valid, uint32_t (&res)[kN]) {
+  uint32_t cell[kN][kCmBatchK], w[kN][kCmBatchK];
+  cm_cells_batch<kN>(a, key, cell);
+#pragma unroll
+  for (int q = 0; q < kN; ++q)
+#pragma unroll
+    for (int j = 0; j < kCmBatchK; ++j)
+      w[q][j] = (valid >> q) & 1u ? __hip_atomic_load(a.cells + (cell[q][j] >> 2),
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0u;
+#pragma unroll
+  for (int q = 0; q < kN; ++q) {
+    uint32_t r = a.vmax;
+#pragma unroll
+    for (int j = 0; j < kCmBatchK; ++j) {
+      const uint32_t v = (w[q][j] >> ((cell[q][j] & 3u) * 8u)) & 0xffu;
+      r = v < r ? v : r;
+    }
+    res[q] = r;
+  }
 }
 
 }  // namespace psamd

@@ -166,7 +166,7 @@ __global__ void key_signature_kernel(const uint64_t* __restrict__ keys, int64_t 
 void cm_insert(uint32_t* table, uint64_t rsize, int rshift, int k, uint32_t vmax,
                const uint64_t* keys, const uint8_t* counts, int64_t n, const int32_t* n_dev,
                hipStream_t st) {
-  const CmArgs a{table, rsize, rshift, k, vmax, 0};
+  const CmArgs a{table, rsize, rshift, k, vmax, 0, 0};
   cm_insert_kernel<<<grid_for(n, 256), 256, 0, st>>>(a, keys, counts, n, n_dev);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
@@ -174,7 +174,7 @@ void cm_insert(uint32_t* table, uint64_t rsize, int rshift, int k, uint32_t vmax
 void cm_query(const uint32_t* table, uint64_t rsize, int rshift, int k, uint32_t vmax,
               const uint64_t* keys, int64_t n, const int32_t* n_dev, int freq, int32_t* keep,
               uint8_t* out_count, hipStream_t st) {
-  const CmArgs a{const_cast<uint32_t*>(table), rsize, rshift, k, vmax, freq};
+  const CmArgs a{const_cast<uint32_t*>(table), rsize, rshift, k, vmax, freq, 0};
   cm_query_kernel<<<grid_for(n, 256), 256, 0, st>>>(a, keys, n, n_dev, keep, out_count);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
@@ -182,7 +182,7 @@ void cm_query(const uint32_t* table, uint64_t rsize, int rshift, int k, uint32_t
 void cm_insert_seg(uint32_t* table, uint64_t rsize, int rshift, int k, uint32_t vmax,
                    const uint64_t* keys, const int32_t* seg_start, int64_t n, const int32_t* n_dev,
                    hipStream_t st) {
-  const CmArgs a{table, rsize, rshift, k, vmax, 0};
+  const CmArgs a{table, rsize, rshift, k, vmax, 0, 0};
   cm_insert_seg_kernel<<<grid_for(n, 256), 256, 0, st>>>(a, keys, seg_start, n, n_dev);
   PSAMD_HIP_CHECK(hipGetLastError());
 }

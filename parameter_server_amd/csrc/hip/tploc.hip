@@ -1749,21 +1749,62 @@ __device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32
     atomicAdd(&occ[jo[ein + g]], (uint32_t)ecnt[id]);
   }
   __syncthreads();
+  // insert and query with the keys strided over the threads (key j = q * kBkThr + t: a
+  // typical unit of ~230 keys is one key per thread, one short memory chain each), two
+  // keys at a time (4 spill past 64 VGPRs); the keep flags go to occ[] for the
+  // order-preserving compaction below
   uint64_t key[kKP];
+  auto load2 = [&](int hq, uint64_t (&k2)[2], uint32_t (&c2)[2]) -> uint32_t {
+    uint32_t v = 0;
 #pragma unroll
-  for (int q = 0; q < kKP; ++q) {
-    const uint32_t j = t * kKP + q;
-    key[q] = j < D ? uo[j] : 0ull;
-    if (j < D) cm_insert_key(cm, key[q], occ[j] > 255u ? 255u : occ[j]);
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t j = (hq + i) * kBkThr + t;
+      k2[i] = j < D ? uo[j] : 0ull;
+      c2[i] = j < D ? (occ[j] > 255u ? 255u : occ[j]) : 0u;
+      v |= (j < D ? 1u : 0u) << i;
+    }
+    return v;
+  };
+#pragma unroll
+  for (int hq = 0; hq < kKP; hq += 2) {
+    uint64_t k2[2];
+    uint32_t c2[2];
+    const uint32_t v = load2(hq, k2, c2);
+    if (!v) continue;
+    if (cm.k == kCmBatchK && cm.ncells32) {
+      cm_insert_batch<2>(cm, k2, c2, v);
+    } else {
+      for (int i = 0; i < 2; ++i)
+        if ((v >> i) & 1u) cm_insert_key(cm, k2[i], c2[i]);
+    }
   }
   __syncthreads();  // every insert of this minibatch that can reach these keys' cells is done
+#pragma unroll
+  for (int hq = 0; hq < kKP; hq += 2) {
+    uint64_t k2[2];
+    uint32_t c2[2], e2[2] = {0u, 0u};
+    const uint32_t v = load2(hq, k2, c2);
+    if (!v) continue;
+    if (cm.k == kCmBatchK && cm.ncells32) {
+      cm_query_batch<2>(cm, k2, v, e2);
+    } else {
+      for (int i = 0; i < 2; ++i) e2[i] = (v >> i) & 1u ? cm_query_key(cm, k2[i]) : 0u;
+    }
+    // (each thread reads back only its own occ words: no barrier between the two)
+    for (int i = 0; i < 2; ++i)
+      if ((v >> i) & 1u) occ[(hq + i) * kBkThr + t] = (int)e2[i] > cm.freq ? 1u : 0u;
+  }
+  __syncthreads();
   uint32_t keep = 0, kc = 0;
 #pragma unroll
-  for (int q = 0; q < kKP; ++q)
-    if (t * kKP + q < D && (int)cm_query_key(cm, key[q]) > cm.freq) {
+  for (int q = 0; q < kKP; ++q) {  // contiguous keys per thread for the compaction
+    const uint32_t j = t * kKP + q;
+    key[q] = j < D ? uo[j] : 0ull;
+    if (j < D && occ[j]) {
       keep |= 1u << q;
       ++kc;
     }
+  }
   uint32_t Dn;
   uint32_t off = tp_block_scan<kBkThr>(kc, lds, &Dn);  // (barriers: every uo read is done)
 #pragma unroll
