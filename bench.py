@@ -829,7 +829,7 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         iterate_native()
     torch.cuda.synchronize()
     args.native_iter = True  # (reported as config.native_iteration)
-    if os.environ.get("PSAMD_MX_G2", "0") == "1":
+    if os.environ.get("PSAMD_MX_G2", "1") == "1":
         # TWO graph launches per iteration: the main stream's graph (wait for exchange t,
         # worker t, record) and the preparation stream's graph (preparation, pack,
         # all-to-all, owner resolve / apply), each a native GraphChain of the captured

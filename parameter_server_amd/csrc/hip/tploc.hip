@@ -339,13 +339,15 @@ __device__ __forceinline__ uint64_t tp_status(uint32_t ep, uint64_t flag, uint32
 // idx[] = tile entry ids (registers), hkey / hcnt = the hash, dl[0..D) = the compacted
 // occupied slots. Returns (block-uniform) whether every entry found a slot within the
 // LDS capacity; *E / *D = entries / distinct keys.
+template <bool kCnt = false>  // kCnt: hcnt sums ecnt (occurrences) instead of entries
 __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
                                             const uint16_t* __restrict__ toff, int nbf, int T,
                                             int shift, int f0, int nf, uint32_t hb,
                                             uint32_t* hkey, uint32_t* hcnt, uint64_t* dl,
                                             uint16_t* eh, uint32_t* lds, uint32_t* flag,
                                             int32_t (&idx)[tp::kG], uint32_t* E_out,
-                                            uint32_t* D_out, uint64_t* prof) {
+                                            uint32_t* D_out, uint64_t* prof,
+                                            const uint8_t* __restrict__ ecnt = nullptr) {
   using namespace tp;
   const int t = threadIdx.x;
   uint32_t* tpre = reinterpret_cast<uint32_t*>(dl);                // [kMaxT + 1]
@@ -417,9 +419,22 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
       }
       h = (h + 1) & (kDH - 1);
     }
-    if (ok) atomicAdd(&hcnt[h], 1u);
-    else bad = true;
+    if (ok) {
+      if (!kCnt) atomicAdd(&hcnt[h], 1u);
+    } else {
+      bad = true;
+    }
     eh[g] = ok ? (uint16_t)h : (uint16_t)0xffffu;
+  }
+  if (kCnt) {  // (tail filter) the key's occurrences: its entries' tile counts
+    uint32_t ec[kG];
+#pragma unroll
+    for (int q = 0; q < kG; ++q) ec[q] = idx[q] >= 0 ? (uint32_t)ecnt[idx[q]] : 0u;
+#pragma unroll
+    for (int q = 0; q < kG; ++q) {
+      const uint32_t g = q * kBkThr + t;
+      if (idx[q] >= 0 && eh[g] != 0xffffu) atomicAdd(&hcnt[eh[g]], ec[q]);
+    }
   }
   if (bad) atomicOr(flag, 1u);
   __syncthreads();
@@ -432,7 +447,8 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
   for (int q = 0; q < kPer; ++q) {
     const int s = q * kBkThr + t;
     ent[q] = hkey[s] != kEmpty
-                 ? (((uint64_t)hkey[s] << 32) | ((uint64_t)hcnt[s] << 16) | (uint64_t)s)
+                 ? (((uint64_t)hkey[s] << 32) |
+                    ((uint64_t)(kCnt ? min(hcnt[s], 0xffffu) : hcnt[s]) << 16) | (uint64_t)s)
                  : ~0ull;
     cc += ent[q] != ~0ull;
   }
@@ -1879,8 +1895,106 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
   int32_t* co = cnt + (int64_t)b * 4;
   int32_t idx[kG];
   uint32_t E, D;
-  const bool good = tp_bk_build(tkeys, toff, nbf, T, shift, f0, pair ? 2 : 1, 0u, hkey, hcnt, dl,
-                                eh, lds, &flag, idx, &E, &D, nullptr);
+  const bool good = tp_bk_build<kFilt>(tkeys, toff, nbf, T, shift, f0, pair ? 2 : 1, 0u, hkey,
+                                       hcnt, dl, eh, lds, &flag, idx, &E, &D, nullptr, ecnt);
+  uint32_t fkeep = ~0u, fbase = 0;  // (tail filter) kept entries of this thread, their base
+  if (good && kFilt) {
+    // the fused tail filter on the unit still in LDS (dl: key << 32 | occurrences << 16 |
+    // slot): insert every key's count, barrier, query (keys strided over the threads, two
+    // at a time); kept flag per hash slot in hcnt (dead: the counts are in dl); filtered
+    // entries leave the entry list (weight 0), kept keys keep their order in dl
+    if (t == 0 && cnt_pre) {
+      int32_t* cp = cnt_pre + (int64_t)b * 4;
+      cp[0] = (int32_t)D;
+      cp[1] = (int32_t)E;
+      cp[2] = 0;
+      cp[3] = 0;
+    }
+    constexpr int kKQ = tpf::kUnitK / kBkThr;  // 4
+    auto load2 = [&](int hq, uint64_t (&k2)[2], uint32_t (&c2)[2]) -> uint32_t {
+      uint32_t v = 0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t j = (hq + i) * kBkThr + t;
+        const uint64_t e = j < D ? dl[j] : 0ull;
+        k2[i] = key0 | (uint32_t)(e >> 32);
+        c2[i] = j < D ? min((uint32_t)(e >> 16) & 0xffffu, 255u) : 0u;
+        v |= (j < D ? 1u : 0u) << i;
+      }
+      return v;
+    };
+#pragma unroll
+    for (int hq = 0; hq < kKQ; hq += 2) {
+      uint64_t k2[2];
+      uint32_t c2[2];
+      const uint32_t v = load2(hq, k2, c2);
+      if (!v) continue;
+      if (cm.k == kCmBatchK && cm.ncells32) {
+        cm_insert_batch<2>(cm, k2, c2, v);
+      } else {
+        for (int i = 0; i < 2; ++i)
+          if ((v >> i) & 1u) cm_insert_key(cm, k2[i], c2[i]);
+      }
+    }
+    __syncthreads();  // every insert that can reach these keys' cells is done
+#pragma unroll
+    for (int hq = 0; hq < kKQ; hq += 2) {
+      uint64_t k2[2];
+      uint32_t c2[2], e2[2] = {0u, 0u};
+      const uint32_t v = load2(hq, k2, c2);
+      if (!v) continue;
+      if (cm.k == kCmBatchK && cm.ncells32) {
+        cm_query_batch<2>(cm, k2, v, e2);
+      } else {
+        for (int i = 0; i < 2; ++i) e2[i] = (v >> i) & 1u ? cm_query_key(cm, k2[i]) : 0u;
+      }
+      for (int i = 0; i < 2; ++i)
+        if ((v >> i) & 1u)
+          hcnt[(uint32_t)dl[(hq + i) * kBkThr + t] & 0xffffu] = (int)e2[i] > cm.freq ? 1u : 0u;
+    }
+    __syncthreads();
+    // entries: the kept ones numbered thread-major (any order within a unit is valid)
+    uint32_t ke = 0;
+    fkeep = 0;
+#pragma unroll
+    for (int q = 0; q < kG; ++q) {
+      if (idx[q] < 0) continue;
+      if (hcnt[eh[q * kBkThr + t]]) {
+        fkeep |= 1u << q;
+        ++ke;
+      } else if (in_range(idx[q], w_cap)) {
+        w_ent[idx[q]] = 0.f;  // (a filtered occurrence contributes nothing)
+      }
+    }
+    uint32_t En;
+    fbase = tp_block_scan<kBkThr>(ke, lds, &En);
+    // keys: compact dl, order kept (contiguous keys per thread for the scan), through the
+    // dead hash words (kept keys -> hkey, their slots -> hcnt once the flags are read)
+    uint32_t kc = 0, km = 0;
+#pragma unroll
+    for (int q = 0; q < kKQ; ++q) {
+      const uint32_t j = t * kKQ + q;
+      if (j < D && hcnt[(uint32_t)dl[j] & 0xffffu]) {
+        km |= 1u << q;
+        ++kc;
+      }
+    }
+    uint32_t Dn;
+    uint32_t kb = tp_block_scan<kBkThr>(kc, lds, &Dn);  // (barriers: every flag read is done)
+#pragma unroll
+    for (int q = 0; q < kKQ; ++q)
+      if ((km >> q) & 1u) {
+        const uint64_t v = dl[t * kKQ + q];
+        hkey[kb] = (uint32_t)(v >> 32);
+        hcnt[kb] = (uint32_t)v & 0xffffu;
+        ++kb;
+      }
+    __syncthreads();
+    for (uint32_t j = t; j < Dn; j += kBkThr) dl[j] = (uint64_t)hkey[j] << 32 | hcnt[j];
+    __syncthreads();
+    D = Dn;
+    E = En;
+  }
   if (good) {
     // key index j: compaction order, or (sorted: the multi-GPU exchange rows must be
     // key-ordered) the rank order of tp_bk_ranksort; slot -> j in LDS (the dead hash
@@ -1904,10 +2018,12 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kG; ++q) {
-      if (idx[q] < 0) continue;
+      if (idx[q] < 0 || !((fkeep >> q) & 1u)) continue;
       const uint32_t g = q * kBkThr + t;
-      po[g] = idx[q];
-      jo[g] = (uint16_t)jmap[eh[g]];
+      // (tail filter: the kept entries at their compacted positions)
+      const uint32_t o = kFilt ? fbase + __popc(fkeep & ((1u << q) - 1u)) : g;
+      po[o] = idx[q];
+      jo[o] = (uint16_t)jmap[eh[g]];
     }
     if (t == 0) {
       co[0] = (int32_t)D;
@@ -1915,7 +2031,7 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
       co[2] = 0;
       co[3] = 0;
     }
-    if (!kFilt) return;
+    return;
   } else {
     // the pair's entries overflow the LDS capacity (or its hash): its fine buckets one
     // after the other, each a unit with its own key index space

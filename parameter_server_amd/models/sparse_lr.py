@@ -243,13 +243,17 @@ class SparseLRTrainer:
         self.R = self.sched.R
         if cfg.exchange_merge not in ("auto", "on", "off"):
             raise ValueError(f"exchange_merge must be auto / on / off, not {cfg.exchange_merge!r}")
-        # (auto: ssp:tau >= 2. asp stays on the two-collective exchange, whose owner
-        # applies run beside the pulls: served on the merged one with staleness exactly
-        # 3, plain SGD at 8 emulated peers + fixing-float diverged, loss 1.03 after 50
-        # steps, tests/test_train_quality_gpu.py)
+        # (auto: ssp:tau >= 2, and asp for FTRL / AdaGrad, served on the merged exchange
+        # with staleness exactly 3 (an admissible asp schedule; both train there at 8
+        # emulated peers + fixing-float, tests/test_train_quality_gpu.py; config 4 FTRL FF 1 B
+        # 0.1299 -> 0.1205 ms, profiles/r6_asp_merged.log). Plain SGD diverged at
+        # staleness 3 (loss 1.03 after 50 steps) and at staleness 2 the merged exchange
+        # serialises with the worker (0.143 vs 0.130 ms): asp SGD keeps the two-collective
+        # exchange, whose owner applies run beside the pulls)
+        asp_merge = math.isinf(self.tau) and cfg.algo.lower() in ("ftrl", "adagrad")
         self.merged = bool(
             self.padded and cfg.exchange_merge != "off"
-            and self.tau > 0 and (cfg.exchange_merge == "on"
+            and self.tau > 0 and (cfg.exchange_merge == "on" or asp_merge
                                   or (not math.isinf(self.tau) and self.tau >= 2)))
         self.msched = None
         if self.merged:  # one collective per step (MergedSchedule)

@@ -14,6 +14,10 @@ for pc in 1 0; do for bs in 0 4 16 64; do for g2 in 0 1; do
   if [ $bs = 0 ]; then DEBUG_CLR_GRAPH_PACKET_CAPTURE=$pc PSAMD_MX_G2=$g2 run e8_pc${pc}_bs${bs}_g$g2 --steps 100 --warmup 10 --emulate-peers 8
   else DEBUG_CLR_GRAPH_PACKET_CAPTURE=$pc DEBUG_HIP_GRAPH_BATCH_SIZE=$bs PSAMD_MX_G2=$g2 run e8_pc${pc}_bs${bs}_g$g2 --steps 100 --warmup 10 --emulate-peers 8; fi
 done; done; done
+timeout -k 10 400 python -u -m pytest tests/test_train_quality_gpu.py -v --timeout 180 --timeout-method thread -p no:cacheprovider -k "e8asp2m3" > $O/pytest_tq.log 2>&1
+echo "pytest tq rc=$?"; grep -E "PASSED|FAILED|SKIPPED|^E " $O/pytest_tq.log | head -10
+run c4ftrl --steps 100 --warmup 10 --emulate-peers 8 --consistency asp --fixing-float 1
+run c4ftrlm3 --steps 100 --warmup 10 --emulate-peers 8 --consistency asp --fixing-float 1 --exchange-merge on --exchange-lag 3
 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run e2_pc0 --steps 100 --warmup 10 --emulate-peers 2
 run e2_pc1 --steps 100 --warmup 10 --emulate-peers 2
 timeout -k 10 600 python benchmarks/bench_app.py --rows 8000000 --files 8 --minibatch 65536 > $O/app8m.log 2>&1; echo "app rc=$?"; tail -1 $O/app8m.log

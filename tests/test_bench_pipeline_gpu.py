@@ -134,11 +134,14 @@ def _g2_parity_main(env: str):
     from parameter_server_amd.ops.synthetic import criteo_batch
     from parameter_server_amd.parallel.comm import LoopbackComm, nccl_loopback
 
-    os.environ.update(json.loads(env))
+    env = json.loads(env)
+    tail = int(env.pop("TAIL", "0"))
+    os.environ.update(env)
     bench = _bench()
     B, N, seed, extra = 4096, 10 ** 6, 77, 9
     dev = torch.device("cuda", 0)
-    kw = dict(num_features=N, minibatch=B, consistency="ssp:4", exchange_merge="on")
+    kw = dict(num_features=N, minibatch=B, consistency="ssp:4", exchange_merge="on",
+              tail_feature_freq=tail)
     tr = SparseLRTrainer(SparseLRConfig(**kw), nccl_loopback(2, dev), dev)
     assert tr.merged
     keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
@@ -165,8 +168,8 @@ def _g2_parity_main(env: str):
                       "maxdiff": float((pw[pos] - rw).abs().max())}), flush=True)
 
 
-@pytest.mark.parametrize("g2", ["0", "1"])
-def test_merged_native_rccl_pipeline_matches_sequential(g2):
+@pytest.mark.parametrize("g2,tail", [("0", "0"), ("1", "0"), ("1", "1")])
+def test_merged_native_rccl_pipeline_matches_sequential(g2, tail):
     """The merged pipeline's native iteration on a real (1-rank RCCL) communicator, with
     the event ops as host calls (launch lists) or as event nodes inside two graph chains
     per iteration (PSAMD_MX_G2=1): same table as the sequential trainer."""
@@ -174,7 +177,7 @@ def test_merged_native_rccl_pipeline_matches_sequential(g2):
     import subprocess
     import sys
 
-    env = json.dumps({"PSAMD_MX_G2": g2, "PSAMD_MX_NATIVE": "1"})
+    env = json.dumps({"PSAMD_MX_G2": g2, "PSAMD_MX_NATIVE": "1", "TAIL": tail})
     code = ("import sys; sys.path.insert(0, 'tests'); import test_bench_pipeline_gpu as t; "
             f"t._g2_parity_main({env!r})")
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,

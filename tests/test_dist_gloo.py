@@ -201,15 +201,19 @@ def test_explicit_smaller_lag_within_bound(tmp_path):
     # (lag 1 is served by the two-collective schedule unless exchange_merge="on")
 
 
-@pytest.mark.parametrize("merge,lag", [("off", 2), ("auto", 2), ("on", 3)])
-def test_asp_differs_from_ssp1(tmp_path, merge, lag):
+@pytest.mark.parametrize("merge,lag,algo", [("off", 2, "ftrl"), ("auto", 3, "ftrl"),
+                                            ("auto", 2, "sgd"), ("on", 3, "ftrl"),
+                                            ("on", 3, "sgd")])
+def test_asp_differs_from_ssp1(tmp_path, merge, lag, algo):
     """asp, two collectives: the owner applies the pushes an exchange carries AFTER
     resolving its pulls (on the GPU on its own stream, which pulls never wait for). Run
     in program order (CPU) that is one more step of staleness than ssp:1. On the merged
     one-collective schedule asp is served with staleness exactly 3 (an admissible asp
-    schedule)."""
+    schedule); "auto" takes it for FTRL / AdaGrad, plain SGD keeps two collectives."""
     cfg_kw = dict(num_features=1 << 20, minibatch=128, table_capacity=1 << 15, l1=0.5,
-                  consistency="asp", exchange_merge=merge)
+                  consistency="asp", exchange_merge=merge, algo=algo)
+    if algo == "sgd":
+        cfg_kw.update(alpha=0.05)
     res = _run(tmp_path, cfg_kw, steps=6, world=2)
     merged = {k: w for r in res for k, w in zip(r["state"]["keys"].tolist(),
                                                  r["state"]["w"].tolist())}

@@ -24,8 +24,10 @@ def _lr(algo, mode):
 
     dev = torch.device("cuda", 0)
     emu = mode.startswith("e8asp2")
-    # e8asp2m: the merged one-collective exchange serving asp with staleness exactly 2
-    merged = dict(exchange_merge="on", exchange_lag=2) if mode == "e8asp2m" else {}
+    # e8asp2m / e8asp2m3: the merged one-collective exchange serving asp with staleness
+    # exactly 2 / 3
+    merged = ({"exchange_merge": "on", "exchange_lag": 2} if mode == "e8asp2m" else
+              {"exchange_merge": "on", "exchange_lag": 3} if mode == "e8asp2m3" else {})
     cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, algo=algo,
                          consistency="asp" if emu else "bsp",
                          fixing_float_bytes=2 if emu else 0, table_capacity=1 << 26,
@@ -45,9 +47,11 @@ def _lr(algo, mode):
     return tr.progress(reset=True)
 
 
-@pytest.mark.parametrize("mode", ["1", "e8asp2", "e8asp2m"])
+@pytest.mark.parametrize("mode", ["1", "e8asp2", "e8asp2m", "e8asp2m3"])
 @pytest.mark.parametrize("algo", ["ftrl", "adagrad", "sgd"])
 def test_sparse_lr_trains(algo, mode):
+    if mode == "e8asp2m3" and algo == "sgd":
+        pytest.skip("plain SGD diverges at staleness 3 (asp keeps it on the lag-1 exchange)")
     p = _lr(algo, mode)
     assert p["loss"] < 0.65 and p["auc"] > 0.7, p
     assert p["loss"] < math.log(2)
