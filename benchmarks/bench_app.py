@@ -46,6 +46,45 @@ def _write_criteo_fast(path, keys, y, N):
     out.tofile(path)
 
 
+def _breakdown(tr, d, a, steps, cache):
+    """Where a cached run's time goes: the feeder alone (pread -> pinned -> HBM, no
+    training) and the trainer alone (the same step count on one HBM-resident minibatch)."""
+    import torch
+
+    from parameter_server_amd.data.feeder import DeviceFeeder
+
+    dev = torch.device("cuda")
+    files = sorted(os.path.join(d, f) for f in os.listdir(d) if f.startswith("part-"))
+    f = DeviceFeeder(files, "LIBSVM", a.minibatch, tr.max_nnz, dev, num_features=10 ** 8,
+                     cache_dir=cache, io_threads=a.io_threads)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    n = ex = 0
+    last = None
+    for b in f:
+        n += 1
+        ex += b.rows
+        last = (b.keys[:b.rows * 39].clone(), b.labels[:b.rows].clone()) if b.rows == a.minibatch \
+            else last
+        f.release(b)
+    torch.cuda.synchronize()
+    feed_s = time.time() - t0
+    out = {"source": "breakdown", "feeder_only_examples_per_s": ex / feed_s,
+           "feeder_only_h2d_gb_per_s": f.bytes_h2d / feed_s / 1e9, "feeder_batches": n}
+    if last is not None and a.kind == "criteo":
+        keys, labels = last
+        for _ in range(3):
+            tr.step(keys, labels, width=39)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        for _ in range(steps):
+            tr.step(keys, labels, width=39)
+        torch.cuda.synchronize()
+        out["trainer_only_examples_per_s"] = steps * a.minibatch / (time.time() - t0)
+    print(f"[bench_app] breakdown {out}", file=sys.stderr, flush=True)
+    return out
+
+
 def write_files(d, kind, rows, files, seed=0, N=10 ** 8):
     rng = np.random.default_rng(seed)
     per = rows // files
@@ -136,6 +175,8 @@ async_sgd {{ algo: FTRL minibatch: {a.minibatch} num_data_pass: 1 report_interva
                      "h2d_gb_per_s": res["h2d_bytes"] / res["seconds"] / 1e9,
                      "loss": res["progress"]["loss"] if res["progress"] else None,
                      "localize": tr.localize_mode, "flat": tr._compact is None})
+        if a.cache and r == 1:
+            runs.append(_breakdown(tr, d, a, res["steps"], cache))
         del tr, res
         torch.cuda.empty_cache()
     out = {"bench": "app_file_fed", "kind": a.kind, "files": a.files, "text_mb": round(mb, 1),

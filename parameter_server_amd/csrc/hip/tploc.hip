@@ -339,15 +339,13 @@ __device__ __forceinline__ uint64_t tp_status(uint32_t ep, uint64_t flag, uint32
 // idx[] = tile entry ids (registers), hkey / hcnt = the hash, dl[0..D) = the compacted
 // occupied slots. Returns (block-uniform) whether every entry found a slot within the
 // LDS capacity; *E / *D = entries / distinct keys.
-template <bool kCnt = false>  // kCnt: hcnt sums ecnt (occurrences) instead of entries
 __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
                                             const uint16_t* __restrict__ toff, int nbf, int T,
                                             int shift, int f0, int nf, uint32_t hb,
                                             uint32_t* hkey, uint32_t* hcnt, uint64_t* dl,
                                             uint16_t* eh, uint32_t* lds, uint32_t* flag,
                                             int32_t (&idx)[tp::kG], uint32_t* E_out,
-                                            uint32_t* D_out, uint64_t* prof,
-                                            const uint8_t* __restrict__ ecnt = nullptr) {
+                                            uint32_t* D_out, uint64_t* prof) {
   using namespace tp;
   const int t = threadIdx.x;
   uint32_t* tpre = reinterpret_cast<uint32_t*>(dl);                // [kMaxT + 1]
@@ -419,22 +417,9 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
       }
       h = (h + 1) & (kDH - 1);
     }
-    if (ok) {
-      if (!kCnt) atomicAdd(&hcnt[h], 1u);
-    } else {
-      bad = true;
-    }
+    if (ok) atomicAdd(&hcnt[h], 1u);
+    else bad = true;
     eh[g] = ok ? (uint16_t)h : (uint16_t)0xffffu;
-  }
-  if (kCnt) {  // (tail filter) the key's occurrences: its entries' tile counts
-    uint32_t ec[kG];
-#pragma unroll
-    for (int q = 0; q < kG; ++q) ec[q] = idx[q] >= 0 ? (uint32_t)ecnt[idx[q]] : 0u;
-#pragma unroll
-    for (int q = 0; q < kG; ++q) {
-      const uint32_t g = q * kBkThr + t;
-      if (idx[q] >= 0 && eh[g] != 0xffffu) atomicAdd(&hcnt[eh[g]], ec[q]);
-    }
   }
   if (bad) atomicOr(flag, 1u);
   __syncthreads();
@@ -447,8 +432,7 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
   for (int q = 0; q < kPer; ++q) {
     const int s = q * kBkThr + t;
     ent[q] = hkey[s] != kEmpty
-                 ? (((uint64_t)hkey[s] << 32) |
-                    ((uint64_t)(kCnt ? min(hcnt[s], 0xffffu) : hcnt[s]) << 16) | (uint64_t)s)
+                 ? (((uint64_t)hkey[s] << 32) | ((uint64_t)hcnt[s] << 16) | (uint64_t)s)
                  : ~0ull;
     cc += ent[q] != ~0ull;
   }
@@ -1736,40 +1720,14 @@ __device__ __forceinline__ void tpf_rank_binned(uint64_t* dl, uint32_t* sc, uint
   __syncthreads();
 }
 
-// Fused tail-feature filter of one unit of the flat layout (reference
-// MinibatchReader::read, src/learner/sgd.h:131-150: CountMin insertKeys of the minibatch's
-// per-key counts, then queryKeys > tail_feature_freq, src/parameter/frequency_filter.h:
-// 26-45). In: keys uo[0..D), entries po / jo[ein .. ein + E) (jo = key index), the tile
-// kernel's per-entry occurrence counts ecnt. Each key's count (its entries' counts,
-// saturated to a byte) goes into the partitioned sketch (countmin.cuh: this workgroup owns
-// every region its keys map to), then after a barrier every key is queried. Out: the kept
-// keys at uo[0..D') in their order (sorted stays sorted), the kept entries at
-// po / jo[eout .. eout + E') with the new key indices, and w_ent = 0 at the filtered
-// entries -- the minibatch as if the filtered keys were absent, so the step, pack and
-// owner kernels need no change. (D', E') -> res[0..1] (LDS).
-__device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32_t* __restrict__ po,
-                                                uint16_t* __restrict__ jo, uint32_t D, uint32_t E,
-                                                uint32_t ein, uint32_t eout,
-                                                const uint8_t* __restrict__ ecnt, const CmArgs& cm,
-                                                float* __restrict__ w_ent, int64_t w_cap,
-                                                uint32_t* occ, uint32_t* lds, uint32_t* res) {
+// The unit's sketch traffic with global atomics (units of more than kFlD keys, or k != 2):
+// insert and query with the keys strided over the threads (key j = q * kBkThr + t), two
+// keys at a time (4 spill past 64 VGPRs); keep flags -> occ[].
+__device__ __forceinline__ void tpf_filter_global(const uint64_t* __restrict__ uo, uint32_t D,
+                                                  const CmArgs& cm, uint32_t* occ) {
   using namespace tp;
-  constexpr int kKP = tpf::kUnitK / kBkThr;  // 4 keys per thread (contiguous)
-  constexpr int kEP = 4;                      // entries per thread per chunk
-  constexpr uint32_t kNone = 0xffffffffu;
+  constexpr int kKP = tpf::kUnitK / kBkThr;
   const int t = threadIdx.x;
-  for (uint32_t j = t; j < D; j += kBkThr) occ[j] = 0u;
-  __syncthreads();
-  for (uint32_t g = t; g < E; g += kBkThr) {
-    const int32_t id = po[ein + g];
-    atomicAdd(&occ[jo[ein + g]], (uint32_t)ecnt[id]);
-  }
-  __syncthreads();
-  // insert and query with the keys strided over the threads (key j = q * kBkThr + t: a
-  // typical unit of ~230 keys is one key per thread, one short memory chain each), two
-  // keys at a time (4 spill past 64 VGPRs); the keep flags go to occ[] for the
-  // order-preserving compaction below
-  uint64_t key[kKP];
   auto load2 = [&](int hq, uint64_t (&k2)[2], uint32_t (&c2)[2]) -> uint32_t {
     uint32_t v = 0;
 #pragma unroll
@@ -1810,7 +1768,166 @@ __device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32
     for (int i = 0; i < 2; ++i)
       if ((v >> i) & 1u) occ[(hq + i) * kBkThr + t] = (int)e2[i] > cm.freq ? 1u : 0u;
   }
+}
+
+// The unit's sketch traffic staged in LDS (units of <= kFlD keys, k = 2): the distinct
+// sketch words of the unit's cells go into an LDS table (word index -> value), each
+// loaded ONCE from HBM by the thread that claimed its slot; the saturating adds are LDS
+// CAS loops, the queries read the table, and the changed words are written back with
+// plain stores. Valid because this workgroup owns every region its keys map to
+// (countmin.cuh) and no other kernel touches the sketch meanwhile (the tail-filtered
+// pipelines order their bucket kernels): one memory round trip per key instead of the
+// global form's load -> CAS -> reload chain (a device-scope atomic drops the line from the
+// XCD's L2, MI355X_MICROARCH.md: the reload crosses the fabric again).
+constexpr int kFlD = 1024;    // keys of a staged unit (occ_small: the dead entry-hash LDS)
+constexpr int kFlTab = 4096;  // word table slots (load <= 0.5)
+
+__device__ __forceinline__ void lds_sat_add_byte(uint32_t* w, uint32_t sh, uint32_t cnt,
+                                                 uint32_t vmax) {
+  uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (true) {
+    const uint32_t b = (old >> sh) & 0xffu;
+    const uint32_t nb = (cnt > vmax - b) ? vmax : b + cnt;
+    if (nb == b) return;
+    const uint32_t prev = atomicCAS(w, old, (old & ~(0xffu << sh)) | (nb << sh));
+    if (prev == old) return;
+    old = prev;
+  }
+}
+
+__device__ __forceinline__ void tpf_filter_staged(const uint64_t* __restrict__ uo, uint32_t D,
+                                                  const CmArgs& cm, uint32_t* occ,
+                                                  uint32_t* wkey, uint32_t* wval) {
+  using namespace tp;
+  constexpr int kQ = kFlD / kBkThr;  // keys per thread (strided)
+  const int t = threadIdx.x;
+  uint64_t k[kQ];
+  uint32_t c[kQ], valid = 0;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    const uint32_t j = q * kBkThr + t;
+    k[q] = j < D ? uo[j] : 0ull;
+    c[q] = j < D ? (occ[j] > 255u ? 255u : occ[j]) : 0u;
+    valid |= (j < D ? 1u : 0u) << q;
+  }
+  uint32_t cell[kQ][kCmBatchK], sl[kQ][kCmBatchK], mine = 0;
+  cm_cells_batch<kQ>(cm, k, cell);
+#pragma unroll
+  for (int q = 0; q < kQ; ++q)
+#pragma unroll
+    for (int p = 0; p < kCmBatchK; ++p) {
+      sl[q][p] = 0;
+      if (!((valid >> q) & 1u)) continue;
+      const uint32_t w1 = (cell[q][p] >> 2) + 1u;  // (< 2^30 words: ncells32)
+      uint32_t h = (w1 * 0x9E3779B1u) >> (32 - 12);
+      static_assert(kFlTab == 1 << 12, "table hash width");
+      while (true) {
+        const uint32_t prev = atomicCAS(&wkey[h], 0u, w1);
+        if (prev == 0u) {
+          mine |= 1u << (q * kCmBatchK + p);
+          break;
+        }
+        if (prev == w1) break;
+        h = (h + 1) & (kFlTab - 1);
+      }
+      sl[q][p] = h;
+    }
+  uint32_t g[kQ][kCmBatchK];  // the claimed words as loaded (every load in flight)
+#pragma unroll
+  for (int q = 0; q < kQ; ++q)
+#pragma unroll
+    for (int p = 0; p < kCmBatchK; ++p)
+      g[q][p] = (mine >> (q * kCmBatchK + p)) & 1u
+                    ? __hip_atomic_load(cm.cells + (cell[q][p] >> 2), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT)
+                    : 0u;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q)
+#pragma unroll
+    for (int p = 0; p < kCmBatchK; ++p)
+      if ((mine >> (q * kCmBatchK + p)) & 1u) wval[sl[q][p]] = g[q][p];
   __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kQ; ++q)
+#pragma unroll
+    for (int p = 0; p < kCmBatchK; ++p)
+      if (((valid >> q) & 1u) && c[q])
+        lds_sat_add_byte(&wval[sl[q][p]], (cell[q][p] & 3u) * 8u, c[q], cm.vmax);
+  __syncthreads();  // every insert of the unit is in the table
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    if (!((valid >> q) & 1u)) continue;
+    uint32_t r = cm.vmax;
+#pragma unroll
+    for (int p = 0; p < kCmBatchK; ++p) {
+      const uint32_t v = (wval[sl[q][p]] >> ((cell[q][p] & 3u) * 8u)) & 0xffu;
+      r = v < r ? v : r;
+    }
+    occ[q * kBkThr + t] = (int)r > cm.freq ? 1u : 0u;  // (own occ words: read above)
+  }
+#pragma unroll
+  for (int q = 0; q < kQ; ++q)
+#pragma unroll
+    for (int p = 0; p < kCmBatchK; ++p)
+      if ((mine >> (q * kCmBatchK + p)) & 1u) {
+        const uint32_t v = wval[sl[q][p]];
+        if (v != g[q][p]) cm.cells[cell[q][p] >> 2] = v;
+      }
+}
+
+// Fused tail-feature filter of one unit of the flat layout (reference
+// MinibatchReader::read, src/learner/sgd.h:131-150: CountMin insertKeys of the minibatch's
+// per-key counts, then queryKeys > tail_feature_freq, src/parameter/frequency_filter.h:
+// 26-45). In: keys uo[0..D), entries po / jo[ein .. ein + E) (jo = key index), the tile
+// kernel's per-entry occurrence counts ecnt. Each key's count (its entries' counts,
+// saturated to a byte) goes into the partitioned sketch (countmin.cuh: this workgroup owns
+// every region its keys map to), then after a barrier every key is queried. Out: the kept
+// keys at uo[0..D') in their order (sorted stays sorted), the kept entries at
+// po / jo[eout .. eout + E') with the new key indices, and w_ent = 0 at the filtered
+// entries -- the minibatch as if the filtered keys were absent, so the step, pack and
+// owner kernels need no change. (D', E') -> res[0..1] (LDS).
+__device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32_t* __restrict__ po,
+                                                uint16_t* __restrict__ jo, uint32_t D, uint32_t E,
+                                                uint32_t ein, uint32_t eout,
+                                                const uint8_t* __restrict__ ecnt, const CmArgs& cm,
+                                                float* __restrict__ w_ent, int64_t w_cap,
+                                                uint32_t* occ_big, uint32_t* occ_small,
+                                                uint32_t* wkey, uint32_t* wval, uint32_t* lds,
+                                                uint32_t* res) {
+  using namespace tp;
+  constexpr int kKP = tpf::kUnitK / kBkThr;  // 4 keys per thread (contiguous)
+  constexpr int kEP = 4;                      // entries per thread per chunk
+  constexpr uint32_t kNone = 0xffffffffu;
+  const int t = threadIdx.x;
+  // the sketch words of the unit staged in LDS (block-uniform choice): <= kFlD keys
+  const bool staged = D <= (uint32_t)kFlD && cm.k == kCmBatchK && cm.ncells32;
+  uint32_t* occ = staged ? occ_small : occ_big;
+  if (staged)
+    for (uint32_t s = t; s < (uint32_t)kFlTab; s += kBkThr) wkey[s] = 0u;
+  for (uint32_t j = t; j < D; j += kBkThr) occ[j] = 0u;
+  __syncthreads();
+  for (uint32_t g = t; g < E; g += kBkThr) {
+    const int32_t id = po[ein + g];
+    atomicAdd(&occ[jo[ein + g]], (uint32_t)ecnt[id]);
+  }
+  __syncthreads();
+  if (cm.dbg & 2) {  // (measurement: the filter's fixed costs only, every key kept)
+    if (t == 0) {
+      res[0] = D;
+      res[1] = E;
+    }
+    __syncthreads();
+    return;
+  }
+  if (cm.dbg & 1) {
+    for (uint32_t j = t; j < D; j += kBkThr) occ[j] = 1u;
+  } else if (staged) {
+    tpf_filter_staged(uo, D, cm, occ, wkey, wval);
+  } else {
+    tpf_filter_global(uo, D, cm, occ);
+  }
+  __syncthreads();
+  uint64_t key[kKP];
   uint32_t keep = 0, kc = 0;
 #pragma unroll
   for (int q = 0; q < kKP; ++q) {  // contiguous keys per thread for the compaction
@@ -1879,10 +1996,10 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
                   const uint8_t* __restrict__ ecnt, CmArgs cm, float* __restrict__ w_ent,
                   int64_t w_cap, int32_t* __restrict__ cnt_pre) {
   using namespace tp;
-  __shared__ uint16_t eh[kECapL];  // hash slot of every gathered entry
+  __shared__ alignas(16) uint16_t eh[kECapL];  // hash slot of every gathered entry
   __shared__ uint64_t hs[kDH];     // hash (key u32 | count u32 -> key index)
   __shared__ uint64_t dl[kDH];     // per-tile runs, then the compacted occupied slots
-  __shared__ uint32_t lds[kBkThr / 64 + 1];
+  __shared__ uint32_t lds[kBkThr / 64 + 3];
   __shared__ uint32_t flag;
   uint32_t* hkey = reinterpret_cast<uint32_t*>(hs);
   uint32_t* hcnt = hkey + kDH;
@@ -1895,106 +2012,8 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
   int32_t* co = cnt + (int64_t)b * 4;
   int32_t idx[kG];
   uint32_t E, D;
-  const bool good = tp_bk_build<kFilt>(tkeys, toff, nbf, T, shift, f0, pair ? 2 : 1, 0u, hkey,
-                                       hcnt, dl, eh, lds, &flag, idx, &E, &D, nullptr, ecnt);
-  uint32_t fkeep = ~0u, fbase = 0;  // (tail filter) kept entries of this thread, their base
-  if (good && kFilt) {
-    // the fused tail filter on the unit still in LDS (dl: key << 32 | occurrences << 16 |
-    // slot): insert every key's count, barrier, query (keys strided over the threads, two
-    // at a time); kept flag per hash slot in hcnt (dead: the counts are in dl); filtered
-    // entries leave the entry list (weight 0), kept keys keep their order in dl
-    if (t == 0 && cnt_pre) {
-      int32_t* cp = cnt_pre + (int64_t)b * 4;
-      cp[0] = (int32_t)D;
-      cp[1] = (int32_t)E;
-      cp[2] = 0;
-      cp[3] = 0;
-    }
-    constexpr int kKQ = tpf::kUnitK / kBkThr;  // 4
-    auto load2 = [&](int hq, uint64_t (&k2)[2], uint32_t (&c2)[2]) -> uint32_t {
-      uint32_t v = 0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint32_t j = (hq + i) * kBkThr + t;
-        const uint64_t e = j < D ? dl[j] : 0ull;
-        k2[i] = key0 | (uint32_t)(e >> 32);
-        c2[i] = j < D ? min((uint32_t)(e >> 16) & 0xffffu, 255u) : 0u;
-        v |= (j < D ? 1u : 0u) << i;
-      }
-      return v;
-    };
-#pragma unroll
-    for (int hq = 0; hq < kKQ; hq += 2) {
-      uint64_t k2[2];
-      uint32_t c2[2];
-      const uint32_t v = load2(hq, k2, c2);
-      if (!v) continue;
-      if (cm.k == kCmBatchK && cm.ncells32) {
-        cm_insert_batch<2>(cm, k2, c2, v);
-      } else {
-        for (int i = 0; i < 2; ++i)
-          if ((v >> i) & 1u) cm_insert_key(cm, k2[i], c2[i]);
-      }
-    }
-    __syncthreads();  // every insert that can reach these keys' cells is done
-#pragma unroll
-    for (int hq = 0; hq < kKQ; hq += 2) {
-      uint64_t k2[2];
-      uint32_t c2[2], e2[2] = {0u, 0u};
-      const uint32_t v = load2(hq, k2, c2);
-      if (!v) continue;
-      if (cm.k == kCmBatchK && cm.ncells32) {
-        cm_query_batch<2>(cm, k2, v, e2);
-      } else {
-        for (int i = 0; i < 2; ++i) e2[i] = (v >> i) & 1u ? cm_query_key(cm, k2[i]) : 0u;
-      }
-      for (int i = 0; i < 2; ++i)
-        if ((v >> i) & 1u)
-          hcnt[(uint32_t)dl[(hq + i) * kBkThr + t] & 0xffffu] = (int)e2[i] > cm.freq ? 1u : 0u;
-    }
-    __syncthreads();
-    // entries: the kept ones numbered thread-major (any order within a unit is valid)
-    uint32_t ke = 0;
-    fkeep = 0;
-#pragma unroll
-    for (int q = 0; q < kG; ++q) {
-      if (idx[q] < 0) continue;
-      if (hcnt[eh[q * kBkThr + t]]) {
-        fkeep |= 1u << q;
-        ++ke;
-      } else if (in_range(idx[q], w_cap)) {
-        w_ent[idx[q]] = 0.f;  // (a filtered occurrence contributes nothing)
-      }
-    }
-    uint32_t En;
-    fbase = tp_block_scan<kBkThr>(ke, lds, &En);
-    // keys: compact dl, order kept (contiguous keys per thread for the scan), through the
-    // dead hash words (kept keys -> hkey, their slots -> hcnt once the flags are read)
-    uint32_t kc = 0, km = 0;
-#pragma unroll
-    for (int q = 0; q < kKQ; ++q) {
-      const uint32_t j = t * kKQ + q;
-      if (j < D && hcnt[(uint32_t)dl[j] & 0xffffu]) {
-        km |= 1u << q;
-        ++kc;
-      }
-    }
-    uint32_t Dn;
-    uint32_t kb = tp_block_scan<kBkThr>(kc, lds, &Dn);  // (barriers: every flag read is done)
-#pragma unroll
-    for (int q = 0; q < kKQ; ++q)
-      if ((km >> q) & 1u) {
-        const uint64_t v = dl[t * kKQ + q];
-        hkey[kb] = (uint32_t)(v >> 32);
-        hcnt[kb] = (uint32_t)v & 0xffffu;
-        ++kb;
-      }
-    __syncthreads();
-    for (uint32_t j = t; j < Dn; j += kBkThr) dl[j] = (uint64_t)hkey[j] << 32 | hcnt[j];
-    __syncthreads();
-    D = Dn;
-    E = En;
-  }
+  const bool good = tp_bk_build(tkeys, toff, nbf, T, shift, f0, pair ? 2 : 1, 0u, hkey, hcnt, dl,
+                                eh, lds, &flag, idx, &E, &D, nullptr);
   if (good) {
     // key index j: compaction order, or (sorted: the multi-GPU exchange rows must be
     // key-ordered) the rank order of tp_bk_ranksort; slot -> j in LDS (the dead hash
@@ -2018,12 +2037,10 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kG; ++q) {
-      if (idx[q] < 0 || !((fkeep >> q) & 1u)) continue;
+      if (idx[q] < 0) continue;
       const uint32_t g = q * kBkThr + t;
-      // (tail filter: the kept entries at their compacted positions)
-      const uint32_t o = kFilt ? fbase + __popc(fkeep & ((1u << q) - 1u)) : g;
-      po[o] = idx[q];
-      jo[o] = (uint16_t)jmap[eh[g]];
+      po[g] = idx[q];
+      jo[g] = (uint16_t)jmap[eh[g]];
     }
     if (t == 0) {
       co[0] = (int32_t)D;
@@ -2031,7 +2048,7 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
       co[2] = 0;
       co[3] = 0;
     }
-    return;
+    if (!kFilt) return;
   } else {
     // the pair's entries overflow the LDS capacity (or its hash): its fine buckets one
     // after the other, each a unit with its own key index space
@@ -2050,16 +2067,21 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
     __syncthreads();
     const uint32_t D0 = (uint32_t)co[0], E0 = (uint32_t)co[1];
     const uint32_t D1 = (uint32_t)co[2], E1 = (uint32_t)co[3];
-    uint32_t* occ = reinterpret_cast<uint32_t*>(hs);  // (dead: kDH words of 2 kDH)
-    uint32_t* res = occ + tpf::kUnitK;
+    // (dead LDS: occ_big / the table values in hs, the table keys in dl, occ_small in eh)
+    static_assert(kFlD * 4 <= kECapL * 2 && kFlTab * 4 <= kDH * 8, "filter LDS");
+    uint32_t* occ = reinterpret_cast<uint32_t*>(hs);
+    uint32_t* occs = reinterpret_cast<uint32_t*>(eh);
+    uint32_t* wkey = reinterpret_cast<uint32_t*>(dl);
+    uint32_t* res = lds + kBkThr / 64 + 1;
     __syncthreads();
-    tpf_filter_unit(uo, po, jo, D0, E0, 0u, 0u, ecnt, cm, w_ent, w_cap, occ, lds, res);
+    tpf_filter_unit(uo, po, jo, D0, E0, 0u, 0u, ecnt, cm, w_ent, w_cap, occ, occs, wkey, occ, lds,
+                    res);
     const uint32_t D0k = res[0], E0k = res[1];
     uint32_t D1k = 0, E1k = 0;
     if (D1 | E1) {
       __syncthreads();
-      tpf_filter_unit(uo + tpf::kUnitK, po, jo, D1, E1, E0, E0k, ecnt, cm, w_ent, w_cap, occ, lds,
-                      res);
+      tpf_filter_unit(uo + tpf::kUnitK, po, jo, D1, E1, E0, E0k, ecnt, cm, w_ent, w_cap, occ,
+                      occs, wkey, occ, lds, res);
       D1k = res[0];
       E1k = res[1];
     }
