@@ -620,7 +620,6 @@ Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor d
     ca.k = f[3].cast<int>();
     ca.vmax = f[4].cast<uint32_t>();
     ca.freq = f[5].cast<int>();
-    if (const char* e = std::getenv("PSAMD_CM_DEBUG")) ca.dbg = std::atoi(e);
     check(ca.k >= 1 && ca.k <= 30 && ca.vmax >= 1 && ca.vmax <= 255 && ca.freq >= 0 &&
               ca.freq < 255,
           "localize_tpf filt: k / vmax / freq");

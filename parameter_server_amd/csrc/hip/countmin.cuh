@@ -34,7 +34,6 @@ struct CmArgs {
   uint32_t vmax;     // saturation
   int freq;          // keep keys whose estimate > freq
   int ncells32;      // every cell index < 2^32 (the batched forms' 32-bit indices)
-  int dbg = 0;       // (measurement only, PSAMD_CM_DEBUG: 1 no sketch traffic, 2 no filter)
 };
 
 __host__ __device__ __forceinline__ uint64_t cm_base(uint64_t key, int rshift, uint64_t rsize) {

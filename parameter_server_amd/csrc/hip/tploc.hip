@@ -1795,72 +1795,91 @@ __device__ __forceinline__ void lds_sat_add_byte(uint32_t* w, uint32_t sh, uint3
   }
 }
 
-__device__ __forceinline__ void tpf_filter_staged(const uint64_t* __restrict__ uo, uint32_t D,
-                                                  const CmArgs& cm, uint32_t* occ,
-                                                  uint32_t* wkey, uint32_t* wval) {
+// (the staged form in two halves: claim + gathers in flight, issued before the unit's
+// occurrence counting so the two memory round trips overlap; then adds, query, write-back)
+struct CmStage {
+  static constexpr int kQ = kFlD / tp::kBkThr;  // keys per thread (strided)
+  uint32_t cell[kQ][kCmBatchK], g[kQ][kCmBatchK];
+  uint32_t sl[kQ];         // the two probes' table slots, 16 bits each
+  uint32_t mine, valid;    // (packed: registers are live across the occurrence counting)
+  __device__ __forceinline__ uint32_t slot(int q, int p) const {
+    return (sl[q] >> (16 * p)) & 0xffffu;
+  }
+};
+
+__device__ __forceinline__ void cm_stage_begin(const uint64_t* __restrict__ uo, uint32_t D,
+                                               const CmArgs& cm, uint32_t* wkey, CmStage& st) {
   using namespace tp;
-  constexpr int kQ = kFlD / kBkThr;  // keys per thread (strided)
+  constexpr int kQ = CmStage::kQ;
   const int t = threadIdx.x;
   uint64_t k[kQ];
-  uint32_t c[kQ], valid = 0;
+  st.valid = 0;
+  st.mine = 0;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     const uint32_t j = q * kBkThr + t;
-    k[q] = j < D ? uo[j] : 0ull;
-    c[q] = j < D ? (occ[j] > 255u ? 255u : occ[j]) : 0u;
-    valid |= (j < D ? 1u : 0u) << q;
+    k[q] = uo[j < D ? j : 0];  // (D >= 1 here; clamped, unconditional loads)
+    st.valid |= (j < D ? 1u : 0u) << q;
   }
-  uint32_t cell[kQ][kCmBatchK], sl[kQ][kCmBatchK], mine = 0;
-  cm_cells_batch<kQ>(cm, k, cell);
+  cm_cells_batch<kQ>(cm, k, st.cell);
 #pragma unroll
   for (int q = 0; q < kQ; ++q)
 #pragma unroll
     for (int p = 0; p < kCmBatchK; ++p) {
-      sl[q][p] = 0;
-      if (!((valid >> q) & 1u)) continue;
-      const uint32_t w1 = (cell[q][p] >> 2) + 1u;  // (< 2^30 words: ncells32)
+      if (p == 0) st.sl[q] = 0;
+      if (!((st.valid >> q) & 1u)) continue;
+      const uint32_t w1 = (st.cell[q][p] >> 2) + 1u;  // (< 2^30 words: ncells32)
       uint32_t h = (w1 * 0x9E3779B1u) >> (32 - 12);
       static_assert(kFlTab == 1 << 12, "table hash width");
       while (true) {
         const uint32_t prev = atomicCAS(&wkey[h], 0u, w1);
         if (prev == 0u) {
-          mine |= 1u << (q * kCmBatchK + p);
+          st.mine |= 1u << (q * kCmBatchK + p);
           break;
         }
         if (prev == w1) break;
         h = (h + 1) & (kFlTab - 1);
       }
-      sl[q][p] = h;
+      st.sl[q] |= h << (16 * p);
     }
-  uint32_t g[kQ][kCmBatchK];  // the claimed words as loaded (every load in flight)
+#pragma unroll
+  for (int q = 0; q < kQ; ++q)
+#pragma unroll
+    for (int p = 0; p < kCmBatchK; ++p)  // (every claimed word's load in flight)
+      st.g[q][p] = (st.mine >> (q * kCmBatchK + p)) & 1u
+                       ? __hip_atomic_load(cm.cells + (st.cell[q][p] >> 2), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT)
+                       : 0u;
+}
+
+__device__ __forceinline__ void cm_stage_end(const CmArgs& cm, uint32_t* occ, uint32_t* wval,
+                                             CmStage& st) {
+  using namespace tp;
+  constexpr int kQ = CmStage::kQ;
+  const int t = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < kQ; ++q)
 #pragma unroll
     for (int p = 0; p < kCmBatchK; ++p)
-      g[q][p] = (mine >> (q * kCmBatchK + p)) & 1u
-                    ? __hip_atomic_load(cm.cells + (cell[q][p] >> 2), __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT)
-                    : 0u;
-#pragma unroll
-  for (int q = 0; q < kQ; ++q)
-#pragma unroll
-    for (int p = 0; p < kCmBatchK; ++p)
-      if ((mine >> (q * kCmBatchK + p)) & 1u) wval[sl[q][p]] = g[q][p];
+      if ((st.mine >> (q * kCmBatchK + p)) & 1u) wval[st.slot(q, p)] = st.g[q][p];
   __syncthreads();
 #pragma unroll
-  for (int q = 0; q < kQ; ++q)
+  for (int q = 0; q < kQ; ++q) {
+    if (!((st.valid >> q) & 1u)) continue;
+    const uint32_t o = occ[q * kBkThr + t];
+    const uint32_t c = o > 255u ? 255u : o;
 #pragma unroll
     for (int p = 0; p < kCmBatchK; ++p)
-      if (((valid >> q) & 1u) && c[q])
-        lds_sat_add_byte(&wval[sl[q][p]], (cell[q][p] & 3u) * 8u, c[q], cm.vmax);
+      lds_sat_add_byte(&wval[st.slot(q, p)], (st.cell[q][p] & 3u) * 8u, c, cm.vmax);
+  }
   __syncthreads();  // every insert of the unit is in the table
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
-    if (!((valid >> q) & 1u)) continue;
+    if (!((st.valid >> q) & 1u)) continue;
     uint32_t r = cm.vmax;
 #pragma unroll
     for (int p = 0; p < kCmBatchK; ++p) {
-      const uint32_t v = (wval[sl[q][p]] >> ((cell[q][p] & 3u) * 8u)) & 0xffu;
+      const uint32_t v = (wval[st.slot(q, p)] >> ((st.cell[q][p] & 3u) * 8u)) & 0xffu;
       r = v < r ? v : r;
     }
     occ[q * kBkThr + t] = (int)r > cm.freq ? 1u : 0u;  // (own occ words: read above)
@@ -1869,9 +1888,9 @@ __device__ __forceinline__ void tpf_filter_staged(const uint64_t* __restrict__ u
   for (int q = 0; q < kQ; ++q)
 #pragma unroll
     for (int p = 0; p < kCmBatchK; ++p)
-      if ((mine >> (q * kCmBatchK + p)) & 1u) {
-        const uint32_t v = wval[sl[q][p]];
-        if (v != g[q][p]) cm.cells[cell[q][p] >> 2] = v;
+      if ((st.mine >> (q * kCmBatchK + p)) & 1u) {
+        const uint32_t v = wval[st.slot(q, p)];
+        if (v != st.g[q][p]) cm.cells[st.cell[q][p] >> 2] = v;
       }
 }
 
@@ -1906,24 +1925,31 @@ __device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32
     for (uint32_t s = t; s < (uint32_t)kFlTab; s += kBkThr) wkey[s] = 0u;
   for (uint32_t j = t; j < D; j += kBkThr) occ[j] = 0u;
   __syncthreads();
-  for (uint32_t g = t; g < E; g += kBkThr) {
-    const int32_t id = po[ein + g];
-    atomicAdd(&occ[jo[ein + g]], (uint32_t)ecnt[id]);
+  CmStage st;
+  const bool stage = staged && D > 0;
+  if (stage) cm_stage_begin(uo, D, cm, wkey, st);
+  // occurrences per key: 4 entries per thread per round, every load of a round in flight
+  // (clamped addresses, selects afterwards)
+  for (uint32_t c0 = 0; c0 < E; c0 += kBkThr * 4) {
+    uint32_t gi[4], jj[4], ec[4];
+    int32_t id[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t g = c0 + q * kBkThr + t;
+      gi[q] = ein + (g < E ? g : E - 1);
+      id[q] = po[gi[q]];
+      jj[q] = jo[gi[q]];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ec[q] = ecnt[id[q]];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (c0 + q * kBkThr + t < E) atomicAdd(&occ[jj[q]], ec[q]);
   }
   __syncthreads();
-  if (cm.dbg & 2) {  // (measurement: the filter's fixed costs only, every key kept)
-    if (t == 0) {
-      res[0] = D;
-      res[1] = E;
-    }
-    __syncthreads();
-    return;
-  }
-  if (cm.dbg & 1) {
-    for (uint32_t j = t; j < D; j += kBkThr) occ[j] = 1u;
-  } else if (staged) {
-    tpf_filter_staged(uo, D, cm, occ, wkey, wval);
-  } else {
+  if (stage) {
+    cm_stage_end(cm, occ, wval, st);
+  } else if (D > 0 && !staged) {
     tpf_filter_global(uo, D, cm, occ);
   }
   __syncthreads();
@@ -2922,10 +2948,15 @@ void localize_tp(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t te
 }
 
 // ---- flat (tpf) host side
-static int tpf_groups_of(const TpGeom& g) {
-  const bool pair = g.nbk >= 2 && g.shift <= 30;
-  return pair ? g.nbk / 2 : g.nbk;
+// (PSAMD_TPF_PAIR=0: one fine bucket per workgroup -- measurement of the pair layout)
+static bool tpf_pair(const TpGeom& g) {
+  static const int force = [] {
+    const char* e = std::getenv("PSAMD_TPF_PAIR");
+    return e ? std::atoi(e) : -1;
+  }();
+  return g.nbk >= 2 && g.shift <= 30 && force != 0;
 }
+static int tpf_groups_of(const TpGeom& g) { return tpf_pair(g) ? g.nbk / 2 : g.nbk; }
 int tpf_groups(int64_t n, int bits) { return tpf_groups_of(tp_geom(n, bits)); }
 int tpf_key_region() { return tpf::kUC; }
 int tpf_entry_region() { return tpf::kEC; }
@@ -2973,7 +3004,7 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
   PSAMD_HIP_CHECK(hipGetLastError());
   if (stage == 1) return;
 bucket:
-  const bool pair = g.nbk >= 2 && g.shift <= 30;
+  const bool pair = tpf_pair(g);
   if (filt)
     tpf_bucket_kernel<true><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
         tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
