@@ -62,6 +62,7 @@ constexpr int kECap = 4096;             // entries of one bucket (global stride)
 constexpr int kECapL = 4064;            // ... held in LDS (bucket kernel LDS <= 40 KB:
                                         // 4 workgroups per CU instead of 3)
 constexpr int kDH = 2048;               // distinct-key hash of one bucket
+constexpr int kBkProbe = 128;           // probe chain bound of the bucket hash build
 constexpr uint32_t kEmpty = 0xffffffffu;
 }  // namespace tp
 
@@ -406,7 +407,9 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
     const uint32_t key = kv[q] | ((hb + ((hib >> q) & 1u)) << shift);
     uint32_t h = tp_hash(key) & (kDH - 1);
     bool ok = false;
-    for (int p = 0; p < kDH / 2; ++p) {
+    // (bounded chain: a hash this full -- near-distinct keys -- is cheaper to give up on
+    // than to probe through: the overflow form takes the pair, profiles/r6_skew_layout.log)
+    for (int p = 0; p < kBkProbe && !bad; ++p) {
       const uint32_t cu = hkey[h];
       if (cu == kEmpty) {
         const uint32_t prev = atomicCAS(&hkey[h], kEmpty, key);
@@ -672,7 +675,9 @@ __device__ __forceinline__ void tp_bk_fine_light(
     const uint32_t key = tkeys[locate(g)] | (hb << shift);
     uint32_t h = tp_hash(key) & (kDH - 1);
     bool ok = false;
-    for (int p = 0; p < kDH / 2; ++p) {
+    // (bounded chain: a hash this full -- near-distinct keys -- is cheaper to give up on
+    // than to probe through: the overflow form takes the pair, profiles/r6_skew_layout.log)
+    for (int p = 0; p < kBkProbe && !bad; ++p) {
       const uint32_t cu = hkey[h];
       if (cu == kEmpty) {
         const uint32_t prev = atomicCAS(&hkey[h], kEmpty, key);
@@ -2010,10 +2015,64 @@ __device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32
   __syncthreads();
 }
 
+// One fine bucket f of an overflowing pair as unit u (keys at uo, entries from eoff, counts
+// at co): the LDS build when the bucket fits, the register-light form otherwise. Returns
+// the unit's entry count (block-uniform). Not inlined: a second inlined copy of the build
+// in the bucket kernel spilled its main path (100 B / lane); the call's register traffic
+// stays on this path.
+__device__ __noinline__ uint32_t tpf_unit_fine(const uint32_t* __restrict__ tkeys,
+                                               const uint16_t* __restrict__ toff, int nbf, int T,
+                                               int shift, int f, uint32_t u, uint64_t key0,
+                                               uint64_t* hs, uint64_t* dl, uint16_t* eh,
+                                               uint32_t* lds, uint32_t* flag, uint64_t* uo,
+                                               int32_t* po, uint16_t* jo, uint32_t eoff,
+                                               int32_t* co, int32_t* err, int sorted) {
+  using namespace tp;
+  const int t = threadIdx.x;
+  uint32_t* hkey = reinterpret_cast<uint32_t*>(hs);
+  uint32_t* hcnt = hkey + kDH;
+  int32_t idx[kG];
+  uint32_t E, D;
+  __syncthreads();  // (the LDS of the previous build)
+  if (!tp_bk_build(tkeys, toff, nbf, T, shift, f, 1, u, hkey, hcnt, dl, eh, lds, flag, idx, &E, &D,
+                   nullptr))
+    return tpf_unit_light(tkeys, toff, nbf, T, shift, f, u, key0, hkey, hcnt, eh, lds, uo, po, jo,
+                          eoff, co, err, sorted != 0);
+  uint32_t* jmap = hcnt;
+  const uint64_t* lst = dl;
+  if (sorted && D > 64) {
+    tpf_rank_binned(dl, hkey, D, shift + 1, lds);
+    jmap = hkey;
+  } else if (sorted) {
+    tp_bk_ranksort(dl, hs, D);
+    __syncthreads();
+    jmap = reinterpret_cast<uint32_t*>(dl);
+    lst = hs;
+  }
+  for (uint32_t j = t; j < D; j += kBkThr) {
+    const uint64_t v = lst[j];
+    uo[j] = key0 | (uint32_t)(v >> 32);
+    jmap[(uint32_t)v & 0xffffu] = j;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kG; ++q) {
+    if (idx[q] < 0) continue;
+    const uint32_t g = q * kBkThr + t;
+    po[eoff + g] = idx[q];
+    jo[eoff + g] = (uint16_t)jmap[eh[g]];
+  }
+  if (t == 0) {
+    co[0] = (int32_t)D;
+    co[1] = (int32_t)E;
+  }
+  return E;
+}
+
 // One workgroup per pair of fine buckets (pair = 0: per fine bucket), the tp_bucket
 // geometry and build; the occupied hash slots in compaction order are the keys' indices.
 // kFilt: then the fused tail filter of each unit (tpf_filter_unit).
-template <bool kFilt>
+template <bool kFilt, bool kFine = true>
 __global__ void __launch_bounds__(tp::kBkThr, 8)
 tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbf,
                   int pair, int T, int shift, uint64_t* __restrict__ uniqf,
@@ -2076,16 +2135,26 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
     }
     if (!kFilt) return;
   } else {
-    // the pair's entries overflow the LDS capacity (or its hash): its fine buckets one
-    // after the other, each a unit with its own key index space
-    const uint32_t e0 = tpf_unit_light(tkeys, toff, nbf, T, shift, f0, 0u, key0, hkey, hcnt, eh,
-                                       lds, uo, po, jo, 0u, co, err, sorted != 0);
-    if (pair)
-      tpf_unit_light(tkeys, toff, nbf, T, shift, f0 + 1, 1u, key0, hkey, hcnt, eh, lds,
-                     uo + tpf::kUnitK, po, jo, e0, co + 2, err, sorted != 0);
-    else if (t == 0) {
-      co[2] = 0;
-      co[3] = 0;
+    // the pair's entries overflow the LDS capacity or its hash (near-distinct keys): its
+    // fine buckets one after the other, each a unit with its own key index space, through
+    // the LDS build when the bucket fits. (The register-light form for every overflowing
+    // pair made localisation of near-distinct ids 1.1-1.7 ms against 0.09 ms for one fine
+    // bucket per workgroup, benchmarks/probe_skew_loc.py, profiles/r6_skew_layout.log.)
+    if (pair && kFine) {
+      const uint32_t e0 = tpf_unit_fine(tkeys, toff, nbf, T, shift, f0, 0u, key0, hs, dl, eh, lds,
+                                        &flag, uo, po, jo, 0u, co, err, sorted);
+      tpf_unit_fine(tkeys, toff, nbf, T, shift, f0 + 1, 1u, key0, hs, dl, eh, lds, &flag,
+                    uo + tpf::kUnitK, po, jo, e0, co + 2, err, sorted);
+    } else {
+      const uint32_t e0 = tpf_unit_light(tkeys, toff, nbf, T, shift, f0, 0u, key0, hkey, hcnt, eh,
+                                         lds, uo, po, jo, 0u, co, err, sorted != 0);
+      if (pair)
+        tpf_unit_light(tkeys, toff, nbf, T, shift, f0 + 1, 1u, key0, hkey, hcnt, eh, lds,
+                       uo + tpf::kUnitK, po, jo, e0, co + 2, err, sorted != 0);
+      else if (t == 0) {
+        co[2] = 0;
+        co[3] = 0;
+      }
     }
     if (!kFilt) return;
   }
@@ -3005,14 +3074,20 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
   if (stage == 1) return;
 bucket:
   const bool pair = tpf_pair(g);
+  static const bool fine = [] {  // (PSAMD_TPF_FINE=0: the register-light overflow form)
+    const char* e = std::getenv("PSAMD_TPF_FINE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  auto launch = [&](auto kern) {
+    kern<<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
+        tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
+        sorted ? 1 : 0, filt ? ecnt : nullptr, filt ? *filt : CmArgs{}, filt ? w_ent : nullptr,
+        filt ? w_cap : 0, filt ? cnt_pre : nullptr);
+  };
   if (filt)
-    tpf_bucket_kernel<true><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
-        tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
-        sorted ? 1 : 0, ecnt, *filt, w_ent, w_cap, cnt_pre);
+    fine ? launch(tpf_bucket_kernel<true, true>) : launch(tpf_bucket_kernel<true, false>);
   else
-    tpf_bucket_kernel<false><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
-        tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
-        sorted ? 1 : 0, nullptr, CmArgs{}, nullptr, 0, nullptr);
+    fine ? launch(tpf_bucket_kernel<false, true>) : launch(tpf_bucket_kernel<false, false>);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

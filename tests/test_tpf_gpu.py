@@ -304,6 +304,41 @@ def test_flat_step_overflow_units_match_reference(monkeypatch):
     torch.testing.assert_close(n, Nn, rtol=1e-4, atol=1e-4)
 
 
+def test_flat_near_distinct_pairs_match_reference(monkeypatch):
+    """Near-distinct keys (uniform over 10^8, ~1024 occurrences per fine bucket): the bucket
+    pairs overflow their 2048-key hash, and each runs as two fine units (the LDS build per
+    fine bucket); 3 steps train like the fp32 reference."""
+    monkeypatch.setenv("PSAMD_FLAT", "1")
+    B = (1 << 20) // 39  # n just under 2^20: 1024 buckets of ~1024 occurrences
+    N = 10 ** 8
+    g = torch.Generator(device=DEV)
+    g.manual_seed(5)
+    batches = [(torch.randint(0, N, (B * 39,), device=DEV, generator=g),
+                torch.where(torch.rand(B, device=DEV, generator=g) < 0.3, 1.0, -1.0))
+               for _ in range(3)]
+    cfg = SparseLRConfig(num_features=N, minibatch=B, table_capacity=1 << 23)
+    tr = SparseLRTrainer(cfg, device=DEV)
+    assert tr.localize_mode == "tpf"
+    f = tr.localizer(batches[0][0])
+    torch.cuda.synchronize()
+    assert int(f.err.item()) == 0
+    H = hipops()
+    G = H.tpf_groups(f.nnz, f.bits)
+    c = f.cnt[:4 * G].view(G, 4).cpu()
+    assert int((c[:, 2] > 0).sum()) > G // 2  # most pairs ran as two units
+    uq = f.unique_keys()
+    assert uq.numel() == torch.unique(mix(batches[0][0], tr.bits)).numel()
+    for k, lab in batches:
+        tr.step(k, lab, width=39)
+    torch.cuda.synchronize()
+    tr.check_ok()
+    allk, W, Z, Nn = _reference_train(batches, cfg.update_rule(), tr.bits)
+    w, z, n = _table_by_raw_key(tr, allk)
+    torch.testing.assert_close(w, W, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(z, Z, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(n, Nn, rtol=1e-4, atol=1e-4)
+
+
 def test_flat_pull_ahead_is_bitwise_the_plain_step(monkeypatch):
     """A pull issued ahead inside the previous step's update launch (next_loc) gives the
     same table, bitwise, as pulling at the step; a pull issued for a minibatch that is
