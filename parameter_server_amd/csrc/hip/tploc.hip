@@ -340,13 +340,15 @@ __device__ __forceinline__ uint64_t tp_status(uint32_t ep, uint64_t flag, uint32
 // idx[] = tile entry ids (registers), hkey / hcnt = the hash, dl[0..D) = the compacted
 // occupied slots. Returns (block-uniform) whether every entry found a slot within the
 // LDS capacity; *E / *D = entries / distinct keys.
+template <bool kCnt = false>  // kCnt: hcnt sums the entries' occurrence counts (ecnt)
 __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
                                             const uint16_t* __restrict__ toff, int nbf, int T,
                                             int shift, int f0, int nf, uint32_t hb,
                                             uint32_t* hkey, uint32_t* hcnt, uint64_t* dl,
                                             uint16_t* eh, uint32_t* lds, uint32_t* flag,
                                             int32_t (&idx)[tp::kG], uint32_t* E_out,
-                                            uint32_t* D_out, uint64_t* prof) {
+                                            uint32_t* D_out, uint64_t* prof,
+                                            const uint8_t* __restrict__ ecnt = nullptr) {
   using namespace tp;
   const int t = threadIdx.x;
   uint32_t* tpre = reinterpret_cast<uint32_t*>(dl);                // [kMaxT + 1]
@@ -398,8 +400,16 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
     }
   }
   uint32_t kv[kG];
+  uint32_t ecp[(kG + 3) / 4];  // (kCnt: the entries' occurrence counts, 4 bytes a word)
 #pragma unroll
   for (int q = 0; q < kG; ++q) kv[q] = idx[q] >= 0 ? tkeys[idx[q]] : 0u;
+  if (kCnt) {
+#pragma unroll
+    for (int w = 0; w < (kG + 3) / 4; ++w) ecp[w] = 0u;
+#pragma unroll
+    for (int q = 0; q < kG; ++q)
+      if (idx[q] >= 0) ecp[q >> 2] |= (uint32_t)ecnt[idx[q]] << ((q & 3) * 8);
+  }
 #pragma unroll
   for (int q = 0; q < kG; ++q) {
     if (idx[q] < 0) continue;
@@ -407,6 +417,8 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
     const uint32_t key = kv[q] | ((hb + ((hib >> q) & 1u)) << shift);
     uint32_t h = tp_hash(key) & (kDH - 1);
     bool ok = false;
+    // (another lane gave up: the build is lost anyway)
+    bad |= __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u;
     // (bounded chain: a hash this full -- near-distinct keys -- is cheaper to give up on
     // than to probe through: the overflow form takes the pair, profiles/r6_skew_layout.log)
     for (int p = 0; p < kBkProbe && !bad; ++p) {
@@ -420,8 +432,12 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
       }
       h = (h + 1) & (kDH - 1);
     }
-    if (ok) atomicAdd(&hcnt[h], 1u);
-    else bad = true;
+    if (ok) {
+      atomicAdd(&hcnt[h], kCnt ? (ecp[q >> 2] >> ((q & 3) * 8)) & 0xffu : 1u);
+    } else if (!bad) {
+      bad = true;
+      atomicOr(flag, 1u);
+    }
     eh[g] = ok ? (uint16_t)h : (uint16_t)0xffffu;
   }
   if (bad) atomicOr(flag, 1u);
@@ -435,7 +451,8 @@ __device__ __forceinline__ bool tp_bk_build(const uint32_t* __restrict__ tkeys,
   for (int q = 0; q < kPer; ++q) {
     const int s = q * kBkThr + t;
     ent[q] = hkey[s] != kEmpty
-                 ? (((uint64_t)hkey[s] << 32) | ((uint64_t)hcnt[s] << 16) | (uint64_t)s)
+                 ? (((uint64_t)hkey[s] << 32) |
+                    ((uint64_t)(kCnt ? min(hcnt[s], 0xffffu) : hcnt[s]) << 16) | (uint64_t)s)
                  : ~0ull;
     cc += ent[q] != ~0ull;
   }
@@ -1628,8 +1645,23 @@ __device__ __forceinline__ uint32_t tpf_unit_light(
     return -1;
   };
   bool bad = false;
-  for (uint32_t g = t; g < E; g += kBkThr)
-    bad |= probe(tkeys[locate(g)] | (hb << shift), true) < 0;
+  // 4 entries per thread per round: every locate, then every key load in flight, then the
+  // probes (one memory round trip per round instead of one per entry)
+  constexpr int kLB = 4;
+  for (uint32_t c0 = 0; c0 < E; c0 += kBkThr * kLB) {
+    int32_t id[kLB];
+    uint32_t kk[kLB];
+#pragma unroll
+    for (int q = 0; q < kLB; ++q) {
+      const uint32_t g = c0 + q * kBkThr + t;
+      id[q] = locate(g < E ? g : E - 1);
+    }
+#pragma unroll
+    for (int q = 0; q < kLB; ++q) kk[q] = tkeys[id[q]];
+#pragma unroll
+    for (int q = 0; q < kLB; ++q)
+      if (c0 + q * kBkThr + t < E) bad |= probe(kk[q] | (hb << shift), true) < 0;
+  }
   __syncthreads();
   // key index j of every occupied slot (strided: conflict-free LDS reads): compaction
   // order, or (sorted) the key's rank = # smaller keys of the unit (the keys are
@@ -1657,11 +1689,25 @@ __device__ __forceinline__ uint32_t tpf_unit_light(
   __syncthreads();
   const uint32_t room = eoff < (uint32_t)tpf::kEC ? tpf::kEC - eoff : 0u;
   bad |= E > room;
-  for (uint32_t g = t; g < E && g < room; g += kBkThr) {
-    const int32_t id = locate(g);
-    const int h = probe(tkeys[id] | (hb << shift), false);
-    po[eoff + g] = id;
-    jo[eoff + g] = h >= 0 ? (uint16_t)hmap[h] : (uint16_t)0;
+  const uint32_t Er = E < room ? E : room;
+  for (uint32_t c0 = 0; c0 < Er; c0 += kBkThr * kLB) {
+    int32_t id[kLB];
+    uint32_t kk[kLB];
+#pragma unroll
+    for (int q = 0; q < kLB; ++q) {
+      const uint32_t g = c0 + q * kBkThr + t;
+      id[q] = locate(g < Er ? g : Er - 1);
+    }
+#pragma unroll
+    for (int q = 0; q < kLB; ++q) kk[q] = tkeys[id[q]];
+#pragma unroll
+    for (int q = 0; q < kLB; ++q) {
+      const uint32_t g = c0 + q * kBkThr + t;
+      if (g >= Er) continue;
+      const int h = probe(kk[q] | (hb << shift), false);
+      po[eoff + g] = id[q];
+      jo[eoff + g] = h >= 0 ? (uint16_t)hmap[h] : (uint16_t)0;
+    }
   }
   if (bad) atomicOr(err, 1);
   if (t == 0) {
@@ -1725,6 +1771,10 @@ __device__ __forceinline__ void tpf_rank_binned(uint64_t* dl, uint32_t* sc, uint
   __syncthreads();
 }
 
+// a unit key's bits (the bucket build's units carry the key's occurrences in the top byte
+// until the tail filter rewrites them)
+constexpr uint64_t kUoKey = (1ull << 56) - 1;
+
 // The unit's sketch traffic with global atomics (units of more than kFlD keys, or k != 2):
 // insert and query with the keys strided over the threads (key j = q * kBkThr + t), two
 // keys at a time (4 spill past 64 VGPRs); keep flags -> occ[].
@@ -1738,7 +1788,7 @@ __device__ __forceinline__ void tpf_filter_global(const uint64_t* __restrict__ u
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const uint32_t j = (hq + i) * kBkThr + t;
-      k2[i] = j < D ? uo[j] : 0ull;
+      k2[i] = j < D ? uo[j] & kUoKey : 0ull;
       c2[i] = j < D ? (occ[j] > 255u ? 255u : occ[j]) : 0u;
       v |= (j < D ? 1u : 0u) << i;
     }
@@ -1823,7 +1873,7 @@ __device__ __forceinline__ void cm_stage_begin(const uint64_t* __restrict__ uo, 
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     const uint32_t j = q * kBkThr + t;
-    k[q] = uo[j < D ? j : 0];  // (D >= 1 here; clamped, unconditional loads)
+    k[q] = uo[j < D ? j : 0] & kUoKey;  // (D >= 1 here; clamped, unconditional loads)
     st.valid |= (j < D ? 1u : 0u) << q;
   }
   cm_cells_batch<kQ>(cm, k, st.cell);
@@ -1917,7 +1967,7 @@ __device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32
                                                 float* __restrict__ w_ent, int64_t w_cap,
                                                 uint32_t* occ_big, uint32_t* occ_small,
                                                 uint32_t* wkey, uint32_t* wval, uint32_t* lds,
-                                                uint32_t* res) {
+                                                uint32_t* res, bool packed) {
   using namespace tp;
   constexpr int kKP = tpf::kUnitK / kBkThr;  // 4 keys per thread (contiguous)
   constexpr int kEP = 4;                      // entries per thread per chunk
@@ -1928,14 +1978,19 @@ __device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32
   uint32_t* occ = staged ? occ_small : occ_big;
   if (staged)
     for (uint32_t s = t; s < (uint32_t)kFlTab; s += kBkThr) wkey[s] = 0u;
-  for (uint32_t j = t; j < D; j += kBkThr) occ[j] = 0u;
+  if (!packed)
+    for (uint32_t j = t; j < D; j += kBkThr) occ[j] = 0u;
   __syncthreads();
   CmStage st;
   const bool stage = staged && D > 0;
   if (stage) cm_stage_begin(uo, D, cm, wkey, st);
-  // occurrences per key: 4 entries per thread per round, every load of a round in flight
-  // (clamped addresses, selects afterwards)
-  for (uint32_t c0 = 0; c0 < E; c0 += kBkThr * 4) {
+  // occurrences per key: from the keys' top byte (packed: the LDS build summed them), or
+  // 4 entries per thread per round, every load of a round in flight (clamped addresses,
+  // selects afterwards)
+  if (packed) {
+    for (uint32_t j = t; j < D; j += kBkThr) occ[j] = (uint32_t)(uo[j] >> 56);
+  }
+  for (uint32_t c0 = 0; c0 < (packed ? 0u : E); c0 += kBkThr * 4) {
     uint32_t gi[4], jj[4], ec[4];
     int32_t id[4];
 #pragma unroll
@@ -1963,7 +2018,7 @@ __device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32
 #pragma unroll
   for (int q = 0; q < kKP; ++q) {  // contiguous keys per thread for the compaction
     const uint32_t j = t * kKP + q;
-    key[q] = j < D ? uo[j] : 0ull;
+    key[q] = j < D ? uo[j] & kUoKey : 0ull;
     if (j < D && occ[j]) {
       keep |= 1u << q;
       ++kc;
@@ -2015,64 +2070,10 @@ __device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32
   __syncthreads();
 }
 
-// One fine bucket f of an overflowing pair as unit u (keys at uo, entries from eoff, counts
-// at co): the LDS build when the bucket fits, the register-light form otherwise. Returns
-// the unit's entry count (block-uniform). Not inlined: a second inlined copy of the build
-// in the bucket kernel spilled its main path (100 B / lane); the call's register traffic
-// stays on this path.
-__device__ __noinline__ uint32_t tpf_unit_fine(const uint32_t* __restrict__ tkeys,
-                                               const uint16_t* __restrict__ toff, int nbf, int T,
-                                               int shift, int f, uint32_t u, uint64_t key0,
-                                               uint64_t* hs, uint64_t* dl, uint16_t* eh,
-                                               uint32_t* lds, uint32_t* flag, uint64_t* uo,
-                                               int32_t* po, uint16_t* jo, uint32_t eoff,
-                                               int32_t* co, int32_t* err, int sorted) {
-  using namespace tp;
-  const int t = threadIdx.x;
-  uint32_t* hkey = reinterpret_cast<uint32_t*>(hs);
-  uint32_t* hcnt = hkey + kDH;
-  int32_t idx[kG];
-  uint32_t E, D;
-  __syncthreads();  // (the LDS of the previous build)
-  if (!tp_bk_build(tkeys, toff, nbf, T, shift, f, 1, u, hkey, hcnt, dl, eh, lds, flag, idx, &E, &D,
-                   nullptr))
-    return tpf_unit_light(tkeys, toff, nbf, T, shift, f, u, key0, hkey, hcnt, eh, lds, uo, po, jo,
-                          eoff, co, err, sorted != 0);
-  uint32_t* jmap = hcnt;
-  const uint64_t* lst = dl;
-  if (sorted && D > 64) {
-    tpf_rank_binned(dl, hkey, D, shift + 1, lds);
-    jmap = hkey;
-  } else if (sorted) {
-    tp_bk_ranksort(dl, hs, D);
-    __syncthreads();
-    jmap = reinterpret_cast<uint32_t*>(dl);
-    lst = hs;
-  }
-  for (uint32_t j = t; j < D; j += kBkThr) {
-    const uint64_t v = lst[j];
-    uo[j] = key0 | (uint32_t)(v >> 32);
-    jmap[(uint32_t)v & 0xffffu] = j;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < kG; ++q) {
-    if (idx[q] < 0) continue;
-    const uint32_t g = q * kBkThr + t;
-    po[eoff + g] = idx[q];
-    jo[eoff + g] = (uint16_t)jmap[eh[g]];
-  }
-  if (t == 0) {
-    co[0] = (int32_t)D;
-    co[1] = (int32_t)E;
-  }
-  return E;
-}
-
 // One workgroup per pair of fine buckets (pair = 0: per fine bucket), the tp_bucket
 // geometry and build; the occupied hash slots in compaction order are the keys' indices.
 // kFilt: then the fused tail filter of each unit (tpf_filter_unit).
-template <bool kFilt, bool kFine = true>
+template <bool kFilt>
 __global__ void __launch_bounds__(tp::kBkThr, 8)
 tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbf,
                   int pair, int T, int shift, uint64_t* __restrict__ uniqf,
@@ -2097,8 +2098,8 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
   int32_t* co = cnt + (int64_t)b * 4;
   int32_t idx[kG];
   uint32_t E, D;
-  const bool good = tp_bk_build(tkeys, toff, nbf, T, shift, f0, pair ? 2 : 1, 0u, hkey, hcnt, dl,
-                                eh, lds, &flag, idx, &E, &D, nullptr);
+  const bool good = tp_bk_build<kFilt>(tkeys, toff, nbf, T, shift, f0, pair ? 2 : 1, 0u, hkey,
+                                       hcnt, dl, eh, lds, &flag, idx, &E, &D, nullptr, ecnt);
   if (good) {
     // key index j: compaction order, or (sorted: the multi-GPU exchange rows must be
     // key-ordered) the rank order of tp_bk_ranksort; slot -> j in LDS (the dead hash
@@ -2116,7 +2117,10 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
     }
     for (uint32_t j = t; j < D; j += kBkThr) {
       const uint64_t v = lst[j];
-      uo[j] = key0 | (uint32_t)(v >> 32);
+      // (tail filter: the key's occurrences, saturated to a byte, ride in the top byte
+      // until the filter rewrites the unit's keys)
+      uo[j] = key0 | (uint32_t)(v >> 32) |
+              (kFilt ? (uint64_t)min((uint32_t)(v >> 16) & 0xffffu, 255u) << 56 : 0ull);
       jmap[(uint32_t)v & 0xffffu] = j;
     }
     __syncthreads();
@@ -2135,17 +2139,13 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
     }
     if (!kFilt) return;
   } else {
-    // the pair's entries overflow the LDS capacity or its hash (near-distinct keys): its
-    // fine buckets one after the other, each a unit with its own key index space, through
-    // the LDS build when the bucket fits. (The register-light form for every overflowing
-    // pair made localisation of near-distinct ids 1.1-1.7 ms against 0.09 ms for one fine
-    // bucket per workgroup, benchmarks/probe_skew_loc.py, profiles/r6_skew_layout.log.)
-    if (pair && kFine) {
-      const uint32_t e0 = tpf_unit_fine(tkeys, toff, nbf, T, shift, f0, 0u, key0, hs, dl, eh, lds,
-                                        &flag, uo, po, jo, 0u, co, err, sorted);
-      tpf_unit_fine(tkeys, toff, nbf, T, shift, f0 + 1, 1u, key0, hs, dl, eh, lds, &flag,
-                    uo + tpf::kUnitK, po, jo, e0, co + 2, err, sorted);
-    } else {
+    // the pair's entries overflow the LDS capacity or its hash (near-distinct keys; the
+    // hash build gives up after kBkProbe probes): its fine buckets one after the other,
+    // each a unit with its own key index space. (Measured and not kept: the LDS build per
+    // fine bucket here -- as a second inlined build it spilled the main path, as a
+    // non-inlined call (308 B of scratch) it slowed the headline step 0.082 -> 0.105 ms,
+    // profiles/r6_skew_layout.log.)
+    {
       const uint32_t e0 = tpf_unit_light(tkeys, toff, nbf, T, shift, f0, 0u, key0, hkey, hcnt, eh,
                                          lds, uo, po, jo, 0u, co, err, sorted != 0);
       if (pair)
@@ -2170,13 +2170,13 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
     uint32_t* res = lds + kBkThr / 64 + 1;
     __syncthreads();
     tpf_filter_unit(uo, po, jo, D0, E0, 0u, 0u, ecnt, cm, w_ent, w_cap, occ, occs, wkey, occ, lds,
-                    res);
+                    res, good);
     const uint32_t D0k = res[0], E0k = res[1];
     uint32_t D1k = 0, E1k = 0;
     if (D1 | E1) {
       __syncthreads();
       tpf_filter_unit(uo + tpf::kUnitK, po, jo, D1, E1, E0, E0k, ecnt, cm, w_ent, w_cap, occ,
-                      occs, wkey, occ, lds, res);
+                      occs, wkey, occ, lds, res, false);
       D1k = res[0];
       E1k = res[1];
     }
@@ -3074,20 +3074,14 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
   if (stage == 1) return;
 bucket:
   const bool pair = tpf_pair(g);
-  static const bool fine = [] {  // (PSAMD_TPF_FINE=0: the register-light overflow form)
-    const char* e = std::getenv("PSAMD_TPF_FINE");
-    return !(e && std::atoi(e) == 0);
-  }();
-  auto launch = [&](auto kern) {
-    kern<<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
-        tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
-        sorted ? 1 : 0, filt ? ecnt : nullptr, filt ? *filt : CmArgs{}, filt ? w_ent : nullptr,
-        filt ? w_cap : 0, filt ? cnt_pre : nullptr);
-  };
   if (filt)
-    fine ? launch(tpf_bucket_kernel<true, true>) : launch(tpf_bucket_kernel<true, false>);
+    tpf_bucket_kernel<true><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
+        tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
+        sorted ? 1 : 0, ecnt, *filt, w_ent, w_cap, cnt_pre);
   else
-    fine ? launch(tpf_bucket_kernel<false, true>) : launch(tpf_bucket_kernel<false, false>);
+    tpf_bucket_kernel<false><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
+        tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
+        sorted ? 1 : 0, nullptr, CmArgs{}, nullptr, 0, nullptr);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
