@@ -124,7 +124,9 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     # tail filter: the bucket kernels (CountMin insert + query) in minibatch order, the
     # generators and tile kernels of the preparations still overlapping
     fchain = tr.filter is not None
-    ev_bk = [torch.cuda.Event() for _ in range(NB)] if (flat and fchain) else None
+    ev_bk = ([torch.cuda.Event() for _ in range(NB)]
+             if (flat and fchain and os.environ.get("PSAMD_TAIL_ORDER_MEASURE", "1") == "1")
+             else None)  # (=0: measurement only -- unordered sketch updates race)
     if ev_bk is not None:
         for e in ev_bk:
             e.record(torch.cuda.current_stream(device))

@@ -623,7 +623,7 @@ Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor d
     check(ca.k >= 1 && ca.k <= 30 && ca.vmax >= 1 && ca.vmax <= 255 && ca.freq >= 0 &&
               ca.freq < 255,
           "localize_tpf filt: k / vmax / freq");
-    check(ca.rsize > 0 && ca.rsize % 4 == 0 && ca.rshift >= 0 && ca.rshift <= bits &&
+    check(ca.rsize > 0 && ca.rsize % 64 == 0 && ca.rshift >= 0 && ca.rshift <= bits &&
               bits - ca.rshift <= 30 &&
               (ca.rsize << (bits - ca.rshift)) <= (uint64_t)cells.numel() * 4,
           "localize_tpf filt: sketch regions exceed the cells");
@@ -2166,7 +2166,8 @@ PYBIND11_MODULE(_hipops, m) {
   auto cm_rsize = [](const Tensor& table, int64_t rsize, int rshift, int key_bits) {
     const uint64_t n = (uint64_t)table.numel() * 4;
     if (rshift >= 64) return rsize > 0 ? std::min<uint64_t>((uint64_t)rsize, n) : n;
-    check(rsize > 0 && rsize % 4 == 0, "countmin: region size must be a positive multiple of 4");
+    check(rsize > 0 && rsize % 64 == 0,
+          "countmin: region size must be a positive multiple of 64 (one block)");
     check(rshift >= 0 && key_bits >= rshift && key_bits - rshift <= 30 &&
               ((uint64_t)rsize << (key_bits - rshift)) <= n,
           "countmin: regions exceed the cell table");

@@ -7,8 +7,10 @@
 // by a CAS on the word, so concurrent inserts of keys sharing a word lose nothing.
 //
 // Partitioned layout (the GPU trainers'): the sketch is 2^lgR regions of `rsize` cells
-// (a multiple of 4: regions never share a word), and a key's k cells all lie in region
-// (mixed key >> rshift). The flat localiser's bucket workgroups own whole key ranges,
+// (a multiple of 64: regions never share a line), and a key's k cells all lie in region
+// (mixed key >> rshift), inside ONE 64-cell block of it (blocked CountMin: block h mod
+// (rsize / 64), offsets o_j = (h2 + j * d2) mod 64 with d2 odd, from the double-hash step):
+// a key touches one cache line of the 100 MB-class sketch instead of k. The flat localiser's bucket workgroups own whole key ranges,
 // hence whole regions, so one workgroup can insert its keys and then query them after a
 // workgroup barrier: every insert that can touch a key's cells came from the same
 // workgroup (no grid-wide barrier between the reference's insertKeys and queryKeys).
@@ -40,6 +42,35 @@ __host__ __device__ __forceinline__ uint64_t cm_base(uint64_t key, int rshift, u
   return rshift >= 64 ? 0ull : (key >> rshift) * rsize;
 }
 
+constexpr int kCmBlock = 64;  // cells of a block (partitioned layout)
+
+// cell j of a key: the reference's double hashing over the whole table (rshift >= 64), or
+// inside the key's block of its region (partitioned)
+struct CmProbe {
+  uint64_t base;  // first cell of the key's block (partitioned) or 0
+  uint32_t h, delta, o, d2;
+  __host__ __device__ __forceinline__ CmProbe(uint64_t key, int rshift, uint64_t rsize) {
+    h = sketch_hash(key);
+    delta = (h >> 17) | (h << 15);
+    base = cm_base(key, rshift, rsize);
+    o = delta & (kCmBlock - 1);
+    d2 = ((delta >> 6) & (kCmBlock - 1)) | 1u;
+    if (rshift < 64) base += (uint64_t)(h % (uint32_t)(rsize / kCmBlock)) * kCmBlock;
+  }
+  // the next cell (call k times)
+  __host__ __device__ __forceinline__ uint64_t next(int rshift, uint64_t rsize) {
+    uint64_t c;
+    if (rshift >= 64) {
+      c = h % rsize;
+      h += delta;
+    } else {
+      c = base + o;
+      o = (o + d2) & (kCmBlock - 1);
+    }
+    return c;
+  }
+};
+
 __device__ __forceinline__ uint32_t sat_add_byte(uint32_t* table, uint64_t cell, uint32_t cnt,
                                                  uint32_t vmax) {
   uint32_t* word = table + (cell >> 2);
@@ -58,29 +89,21 @@ __device__ __forceinline__ uint32_t sat_add_byte(uint32_t* table, uint64_t cell,
 
 __device__ __forceinline__ void cm_insert_key(const CmArgs& a, uint64_t key, uint32_t cnt) {
   if (cnt == 0) return;
-  const uint64_t base = cm_base(key, a.rshift, a.rsize);
-  uint32_t h = sketch_hash(key);
-  const uint32_t delta = (h >> 17) | (h << 15);
-  for (int j = 0; j < a.k; ++j) {
-    sat_add_byte(a.cells, base + h % a.rsize, cnt, a.vmax);
-    h += delta;
-  }
+  CmProbe p(key, a.rshift, a.rsize);
+  for (int j = 0; j < a.k; ++j) sat_add_byte(a.cells, p.next(a.rshift, a.rsize), cnt, a.vmax);
 }
 
 // min over the key's cells (agent-scope loads: they see every insert that completed
 // before, whatever this CU's L1 holds)
 __device__ __forceinline__ uint32_t cm_query_key(const CmArgs& a, uint64_t key) {
-  const uint64_t base = cm_base(key, a.rshift, a.rsize);
-  uint32_t h = sketch_hash(key);
-  const uint32_t delta = (h >> 17) | (h << 15);
+  CmProbe p(key, a.rshift, a.rsize);
   uint32_t res = a.vmax;
   for (int j = 0; j < a.k; ++j) {
-    const uint64_t c = base + h % a.rsize;
+    const uint64_t c = p.next(a.rshift, a.rsize);
     const uint32_t w = __hip_atomic_load(a.cells + (c >> 2), __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t v = (w >> ((c & 3) * 8)) & 0xffu;
     res = v < res ? v : res;
-    h += delta;
   }
   return res;
 }
@@ -97,15 +120,27 @@ template <int kN>
 __device__ __forceinline__ void cm_cells_batch(const CmArgs& a, const uint64_t (&key)[kN],
                                                uint32_t (&cell)[kN][kCmBatchK]) {
   const uint32_t rs = (uint32_t)a.rsize;  // (32-bit cell indices: the caller checks)
+  const bool part = a.rshift < 64;
 #pragma unroll
   for (int q = 0; q < kN; ++q) {
-    const uint32_t base = (uint32_t)cm_base(key[q], a.rshift, a.rsize);
+    uint32_t base = (uint32_t)cm_base(key[q], a.rshift, a.rsize);
     uint32_t h = sketch_hash(key[q]);
     const uint32_t delta = (h >> 17) | (h << 15);
+    if (part) {  // (CmProbe, 32-bit)
+      base += (h % (rs / kCmBlock)) * kCmBlock;
+      const uint32_t d2 = ((delta >> 6) & (kCmBlock - 1)) | 1u;
+      uint32_t o = delta & (kCmBlock - 1);
 #pragma unroll
-    for (int j = 0; j < kCmBatchK; ++j) {
-      cell[q][j] = base + h % rs;
-      h += delta;
+      for (int j = 0; j < kCmBatchK; ++j) {
+        cell[q][j] = base + o;
+        o = (o + d2) & (kCmBlock - 1);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kCmBatchK; ++j) {
+        cell[q][j] = base + h % rs;
+        h += delta;
+      }
     }
   }
 }

@@ -6,11 +6,12 @@ keep keys whose estimated count > freq. Cells saturate at v_max = 254.
 
 ``key_bits`` set (the GPU trainers): the sketch is partitioned into 2^lgR regions of
 ``rsize`` cells and a key's k cells lie in region ``key >> (key_bits - lgR)``
-(csrc/hip/countmin.cuh). The flat localiser's bucket workgroups own whole key ranges and
-so whole regions: each inserts its keys and queries them behind a workgroup barrier, in
-the same launch. The cells per key and the collision rate are those of the reference's
-global layout (uniformly mixed keys); ``key_bits=None`` keeps that global layout (the CPU
-runtime apps on raw keys).
+(csrc/hip/countmin.cuh), inside one 64-cell block of it (blocked CountMin: a key's cells
+share one cache line). The flat localiser's bucket workgroups own whole key ranges and so
+whole regions: each inserts its keys and queries them behind a workgroup barrier, in the
+same launch. The cells per key are the reference's k; the collision rate is that of a
+blocked sketch of the same size (slightly above the global layout's for the same n);
+``key_bits=None`` keeps the reference's global layout (the CPU runtime apps on raw keys).
 """
 from __future__ import annotations
 
@@ -54,7 +55,8 @@ class CountMinSketch:
             self.lgR = min(int(lg_regions), int(key_bits))
             self.rshift = int(key_bits) - self.lgR
             r = 1 << self.lgR
-            self.rsize = max(4, ((n + r - 1) // r + 3) // 4 * 4)  # regions never share a word
+            # whole 64-cell blocks: regions never share a cache line
+            self.rsize = max(64, ((n + r - 1) // r + 63) // 64 * 64)
             n = self.rsize << self.lgR
         self.n = n
         self.cells = torch.zeros(n, dtype=torch.uint8, device=self.device)
@@ -80,12 +82,19 @@ class CountMinSketch:
         keys = keys.to(torch.int64)
         h = sketch_hash_torch(keys)
         delta = ((h >> 17) | (h << 15)) & _M32
-        base = (torch.zeros_like(keys) if not self.partitioned
-                else (keys >> self.rshift) * self.rsize)
         cols = []
+        if not self.partitioned:
+            for _ in range(self.k):
+                cols.append(h % self.rsize)
+                h = (h + delta) & _M32
+            return torch.stack(cols, 1)
+        # blocked: the key's block of its region, offsets o_j = (h2 + j * d2) mod 64
+        base = (keys >> self.rshift) * self.rsize + (h % (self.rsize // 64)) * 64
+        o = delta & 63
+        d2 = ((delta >> 6) & 63) | 1
         for _ in range(self.k):
-            cols.append(base + h % self.rsize)
-            h = (h + delta) & _M32
+            cols.append(base + o)
+            o = (o + d2) & 63
         return torch.stack(cols, 1)
 
     def insert(self, keys: torch.Tensor, counts: torch.Tensor | None = None, n_dev=None):

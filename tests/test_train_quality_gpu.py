@@ -24,14 +24,16 @@ def _lr(algo, mode):
 
     dev = torch.device("cuda", 0)
     emu = mode.startswith("e8asp2")
-    # e8asp2m / e8asp2m3: the merged one-collective exchange serving asp with staleness
-    # exactly 2 / 3
+    # e8asp2: the two-collective asp exchange (exchange_merge off: auto puts FTRL / AdaGrad
+    # asp on the merged exchange); e8asp2m / e8asp2m3: the merged one-collective exchange
+    # serving asp with staleness exactly 2 / 3 (3 = what auto picks)
     merged = ({"exchange_merge": "on", "exchange_lag": 2} if mode == "e8asp2m" else
               {"exchange_merge": "on", "exchange_lag": 3} if mode == "e8asp2m3" else {})
+    off = {"exchange_merge": "off"} if mode == "e8asp2" else {}
     cfg = SparseLRConfig(num_features=10 ** 9, minibatch=B, algo=algo,
                          consistency="asp" if emu else "bsp",
                          fixing_float_bytes=2 if emu else 0, table_capacity=1 << 26,
-                         **merged, **algo_defaults(algo))
+                         **merged, **off, **algo_defaults(algo))
     tr = SparseLRTrainer(cfg, LoopbackComm(8, dev) if emu else None, dev)
     assert tr.merged == bool(merged)
     keys = torch.empty(B * 39, dtype=torch.int64, device=dev)
