@@ -130,6 +130,8 @@ def main():
                     help="1: run twice with a binary example cache (the first run parses the "
                          "text and writes the cache, the second streams the cache)")
     ap.add_argument("--io-threads", type=int, default=4)
+    ap.add_argument("--report-steps", type=int, default=0,
+                    help="progress line every this many steps on cached passes (0: 10 per pass)")
     a = ap.parse_args()
     import torch
 
@@ -163,7 +165,7 @@ async_sgd {{ algo: FTRL minibatch: {a.minibatch} num_data_pass: 1 report_interva
         flags = types.SimpleNamespace(
             num_features=1e8, max_nnz_per_example=160 if a.kind == "rcv1" else 39,
             num_threads=a.threads, device="cuda", seed=0, table_capacity=1 << 27, quiet=False,
-            data_cache=cache, io_threads=a.io_threads, report_steps=0)
+            data_cache=cache, io_threads=a.io_threads, report_steps=a.report_steps)
         res = run_async_sgd(lm, LocalComm(dev), dev, flags)
         tr = res["trainer"]
         print(f"[bench_app] run {r}: {res['examples'] / res['seconds'] / 1e6:.2f} M ex/s "

@@ -167,6 +167,12 @@ def main():
             "config": {"num_features": N, "embedding_dim": args.dim, "slots": 39,
                        "hidden": list(cfg.hidden), "global_batch": NG * B, "gemm": args.gemm,
                        "table_slots_per_gpu": tr.shard.capacity,
+                       "table_slots_total": NG * tr.shard.capacity,
+                       "table_note": ("ids hashed over num_features; rows are created on first "
+                                      "touch, so a run needs slots only for the ids it touches. "
+                                      "The default 2^27 slots per GPU is the per-GPU shard of "
+                                      "the 8-GPU config: a 1e9-row table needs 8 GPUs at "
+                                      "128 x bf16 (256 GB of rows alone)"),
                        "shard_gb": tr.shard.nbytes() / 2 ** 30, "mlp_params": tr.num_params},
             "train": {**p, "rows_rank0": occ},
         }), flush=True)
