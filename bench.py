@@ -121,12 +121,10 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     if tile_gate:
         for e in ev_fb:
             e.record(torch.cuda.current_stream(device))
-    # tail filter: the bucket kernels (CountMin insert + query) in minibatch order, the
-    # generators and tile kernels of the preparations still overlapping
+    # tail filter: the filter kernels (CountMin insert + query + compaction) in minibatch
+    # order, the generators, tile and bucket kernels of the preparations still overlapping
     fchain = tr.filter is not None
-    ev_bk = ([torch.cuda.Event() for _ in range(NB)]
-             if (flat and fchain and os.environ.get("PSAMD_TAIL_ORDER_MEASURE", "1") == "1")
-             else None)  # (=0: measurement only -- unordered sketch updates race)
+    ev_bk = [torch.cuda.Event() for _ in range(NB)] if (flat and fchain) else None
     if ev_bk is not None:
         for e in ev_bk:
             e.record(torch.cuda.current_stream(device))
@@ -196,7 +194,7 @@ def pipeline(tr, B, N, seed, keys, labels, device, args, nprep=1, watch=None):
     # tail filter: the CountMin inserts and queries of consecutive minibatches run in
     # minibatch order (the reference's MinibatchReader::read sequence): a preparation
     # waits for the previous minibatch's (on another stream); the flat launch lists order
-    # only their bucket kernels (ev_bk above)
+    # only their tail-filter kernels (ev_bk above)
     fchain = tr.filter is not None and fplans is None
     E = 64  # event rings, indexed by step (every look-back here is < 64 steps)
     ev_buf = [torch.cuda.Event() for _ in range(NB)]   # worker done with buffer b
@@ -585,9 +583,14 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
     mode = {"capture": False}
     tr._mx_external = True  # progress() must not drain: the exchanges below are in flight
 
-    def prep(b):
+    def prep(b, part=0):
+        """part 0: generate + localise; (tail filter) 1: generate + tile + bucket, 2: the
+        filter kernel (ordered across minibatches by the caller)"""
         sidx = b % nprep
         k, lab = bufs[b]
+        if part == 2:
+            locs[b] = tr.localize(k, buf=b, stage=3)
+            return
         if mode["capture"]:
             # buffer b reads cursor word (b // nprep) % 2 of its stream and writes the
             # other: the stream's two buffers alternate, so each replay advances the cursor
@@ -599,7 +602,10 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
             criteo_batch(B, seed=seed, row0=(hctr[sidx] * nprep + sidx) * B, num_features=N,
                          device=device, keys=k, labels=lab)
             hctr[sidx] += 1
-        locs[b] = tr.localize(k, buf=b)
+        if part == 1:
+            tr.localize(k, buf=b, stage=4)
+        else:
+            locs[b] = tr.localize(k, buf=b)
 
     xd = max(1, min(d, nprep - 1, int(os.environ.get("PSAMD_XD", "2"))))
     E = P * -(-64 // P)  # (a multiple of the phase count: one native plan per t % E)
@@ -655,7 +661,9 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
             set_stream(main)
 
     state = {"t": 0}
-    fchain = tr.filter is not None
+    # (tail filter on the flat layout: the filter kernels of consecutive minibatches in
+    # minibatch order; elsewhere the sketch is updated by the worker, on the main stream)
+    fchain = tr.filter is not None and tr.localize_mode == "tpf"
 
     def iterate():
         t = state["t"]
@@ -670,25 +678,33 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         nb = (t + nprep) % NB
         s_ = sides[nb % nprep]
         s_.wait_event(ev_buf[nb])
-        if fchain:  # (tail filter: CountMin inserts / queries in minibatch order)
-            s_.wait_event(ev_prep[(nb - 1) % NB])
         set_stream(s_)
         try:
-            prep_fns[nb]()
+            if fchain:  # (tail filter: the CountMin filters in minibatch order)
+                prep_fns[nb][0]()
+                s_.wait_event(ev_prep[(nb - 1) % NB])
+                prep_fns[nb][1]()
+            else:
+                prep_fns[nb]()
             ev_prep[nb].record(s_)
         finally:
             set_stream(main)
         issue_exchange(t + xd)
         state["t"] = t + 1
 
-    prep_fns = [(lambda b=b: prep(b)) for b in range(NB)]
+    prep_fns = [((lambda b=b: prep(b, 1)), (lambda b=b: prep(b, 2))) if fchain
+                else (lambda b=b: prep(b)) for b in range(NB)]
     for e in ev_buf:
         e.record(main)
     for b in range(nprep):
         with torch.cuda.stream(sides[b]):
-            if fchain and b:
-                sides[b].wait_event(ev_prep[b - 1])
-            prep(b)
+            if fchain:
+                prep(b, 1)
+                if b:
+                    sides[b].wait_event(ev_prep[b - 1])
+                prep(b, 2)
+            else:
+                prep(b)
             ev_prep[b].record(sides[b])
     if tr.xc is None:
         main.wait_event(ev_prep[0])
@@ -739,7 +755,8 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
     seed_cursors(ctr, hctr, state["t"], nprep, NB)
     mode["capture"] = True
     for b in range(NB):
-        gp.append(graph_of(lambda b=b: prep(b)))
+        gp.append((graph_of(lambda b=b: prep(b, 1)), graph_of(lambda b=b: prep(b, 2)))
+                  if fchain else graph_of(lambda b=b: prep(b)))
     for j in range(P):
         if watch is not None:
             watch.beat("capture", j)
@@ -791,11 +808,13 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         # (buffer nb was last trained at t + nprep - NB: its worker-done event is the
         # buffer event; nothing waits for a preparation's own event after the setup)
         L.add_wait(ev["w"][(t + nprep - NB) % E])
-        if fchain:
+        if fchain:  # (the filters in minibatch order)
+            L.add_graph(gobj[gp[nb][0]])
             L.add_wait(ev_prep[(nb - 1) % NB])
-        L.add_graph(gobj[gp[nb]])
-        if fchain:
+            L.add_graph(gobj[gp[nb][1]])
             L.add_record(ev_prep[nb])
+        else:
+            L.add_graph(gobj[gp[nb]])
         xp = gx[s % P]
         L.add_stream(sides[((s + 1) % NB) % nprep])
         L.add_graph(gobj[xp["pack"]])
@@ -868,9 +887,10 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
             parts = tr.mx_exchange(s, locs[(s + 1) % NB])
             cs = H.GraphChain()
             cs.add_wait(evg["w"][(t + nprep - NB) % Eg])
-            if fchain:
+            if fchain:  # (the filters in minibatch order)
+                cs.add_child(piece(lambda nb=nb: prep(nb, 1)))
                 cs.add_wait(evp[(nb - 1) % NB])
-                cs.add_child(piece(lambda nb=nb: prep(nb)))
+                cs.add_child(piece(lambda nb=nb: prep(nb, 2)))
                 cs.add_record(evp[nb])
                 cs.add_child(piece(parts["pack"]))
             else:

@@ -583,7 +583,8 @@ void check_tpf(const TpfBufs& f, int64_t n, int bits, const char* what, bool par
 Launch make_localize_tpf(Tensor keys, int64_t n, int bits, Tensor temp, Tensor dcnt, Tensor rep,
                          Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err,
                          bool sorted, optional<py::tuple> filt = {}, int stage = 0) {
-  check(stage >= 0 && stage <= 2, "localize_tpf: stage 0 (both), 1 (tile), 2 (bucket)");
+  check(stage >= 0 && stage <= 4,
+        "localize_tpf: stage 0 (all), 1 (tile), 2 (bucket), 3 (tail filter), 4 (tile + bucket)");
   chk(keys, at::kLong, "keys");
   chk(temp, at::kByte, "temp");
   chk(dcnt, at::kInt, "dcnt");

@@ -2072,20 +2072,22 @@ __device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32
 
 // One workgroup per pair of fine buckets (pair = 0: per fine bucket), the tp_bucket
 // geometry and build; the occupied hash slots in compaction order are the keys' indices.
-// kFilt: then the fused tail filter of each unit (tpf_filter_unit).
+// kFilt (tail filter, count mode): the LDS build sums the tile kernel's per-entry
+// occurrence counts, and each key of a built unit carries its count (a byte) in the top
+// byte of uniqf for tpf_filter_kernel, which runs as its own launch so that only IT has to
+// run in minibatch order.
 template <bool kFilt>
 __global__ void __launch_bounds__(tp::kBkThr, 8)
 tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict__ toff, int nbf,
                   int pair, int T, int shift, uint64_t* __restrict__ uniqf,
                   int32_t* __restrict__ ent_pos, uint16_t* __restrict__ ent_j,
                   int32_t* __restrict__ cnt, int32_t* __restrict__ err, int sorted,
-                  const uint8_t* __restrict__ ecnt, CmArgs cm, float* __restrict__ w_ent,
-                  int64_t w_cap, int32_t* __restrict__ cnt_pre) {
+                  const uint8_t* __restrict__ ecnt) {
   using namespace tp;
   __shared__ alignas(16) uint16_t eh[kECapL];  // hash slot of every gathered entry
   __shared__ uint64_t hs[kDH];     // hash (key u32 | count u32 -> key index)
   __shared__ uint64_t dl[kDH];     // per-tile runs, then the compacted occupied slots
-  __shared__ uint32_t lds[kBkThr / 64 + 3];
+  __shared__ uint32_t lds[kBkThr / 64 + 1];
   __shared__ uint32_t flag;
   uint32_t* hkey = reinterpret_cast<uint32_t*>(hs);
   uint32_t* hcnt = hkey + kDH;
@@ -2137,7 +2139,6 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
       co[2] = 0;
       co[3] = 0;
     }
-    if (!kFilt) return;
   } else {
     // the pair's entries overflow the LDS capacity or its hash (near-distinct keys; the
     // hash build gives up after kBkProbe probes): its fine buckets one after the other,
@@ -2156,43 +2157,63 @@ tpf_bucket_kernel(const uint32_t* __restrict__ tkeys, const uint16_t* __restrict
         co[3] = 0;
       }
     }
-    if (!kFilt) return;
   }
-  if (kFilt) {  // every unit's outputs are written (global, this workgroup): filter them
+}
+
+// The fused tail filter of every bucket workgroup's units (tpf_filter_unit), one
+// workgroup per bucket group, after tpf_bucket_kernel<true>: the partitioned CountMin
+// insert + query of the minibatch's keys and the compaction of the filtered ones. A launch
+// of its own so that only the sketch traffic runs in minibatch order (the callers chain
+// these launches across their preparation streams; the bucket builds overlap freely):
+// ordering the whole bucket kernel cost the pipelined step ~6.5 us
+// (profiles/r6_tail_filter.log). cnt_pre <- the unfiltered counts, cnt <- the kept ones.
+__global__ void __launch_bounds__(tp::kBkThr, 8)
+tpf_filter_kernel(uint64_t* __restrict__ uniqf, int32_t* __restrict__ ent_pos,
+                  uint16_t* __restrict__ ent_j, int32_t* __restrict__ cnt,
+                  const uint8_t* __restrict__ ecnt, CmArgs cm, float* __restrict__ w_ent,
+                  int64_t w_cap, int32_t* __restrict__ cnt_pre) {
+  using namespace tp;
+  __shared__ uint64_t hs[kDH];          // occ_big / the sketch table's values
+  __shared__ uint64_t dl[kDH];          // the sketch table's word ids
+  __shared__ uint32_t occs[kFlD];       // occ_small
+  __shared__ uint32_t lds[kBkThr / 64 + 3];
+  static_assert(kFlTab * 4 <= kDH * 8, "filter LDS");
+  const int t = threadIdx.x, b = blockIdx.x;
+  uint64_t* uo = uniqf + (int64_t)b * tpf::kUC;
+  int32_t* po = ent_pos + (int64_t)b * tpf::kEC;
+  uint16_t* jo = ent_j + (int64_t)b * tpf::kEC;
+  int32_t* co = cnt + (int64_t)b * 4;
+  const uint32_t D0 = (uint32_t)co[0], E0 = (uint32_t)co[1];
+  const uint32_t D1 = (uint32_t)co[2], E1 = (uint32_t)co[3];
+  // a unit the LDS build wrote carries its keys' counts in the top byte (every count >= 1);
+  // the register-light units do not (their counts come from the entries)
+  const bool packed = D0 > 0 && (uo[0] >> 56) != 0;
+  uint32_t* occ = reinterpret_cast<uint32_t*>(hs);
+  uint32_t* wkey = reinterpret_cast<uint32_t*>(dl);
+  uint32_t* res = lds + kBkThr / 64 + 1;
+  tpf_filter_unit(uo, po, jo, D0, E0, 0u, 0u, ecnt, cm, w_ent, w_cap, occ, occs, wkey, occ, lds,
+                  res, packed);
+  const uint32_t D0k = res[0], E0k = res[1];
+  uint32_t D1k = 0, E1k = 0;
+  if (D1 | E1) {
     __syncthreads();
-    const uint32_t D0 = (uint32_t)co[0], E0 = (uint32_t)co[1];
-    const uint32_t D1 = (uint32_t)co[2], E1 = (uint32_t)co[3];
-    // (dead LDS: occ_big / the table values in hs, the table keys in dl, occ_small in eh)
-    static_assert(kFlD * 4 <= kECapL * 2 && kFlTab * 4 <= kDH * 8, "filter LDS");
-    uint32_t* occ = reinterpret_cast<uint32_t*>(hs);
-    uint32_t* occs = reinterpret_cast<uint32_t*>(eh);
-    uint32_t* wkey = reinterpret_cast<uint32_t*>(dl);
-    uint32_t* res = lds + kBkThr / 64 + 1;
-    __syncthreads();
-    tpf_filter_unit(uo, po, jo, D0, E0, 0u, 0u, ecnt, cm, w_ent, w_cap, occ, occs, wkey, occ, lds,
-                    res, good);
-    const uint32_t D0k = res[0], E0k = res[1];
-    uint32_t D1k = 0, E1k = 0;
-    if (D1 | E1) {
-      __syncthreads();
-      tpf_filter_unit(uo + tpf::kUnitK, po, jo, D1, E1, E0, E0k, ecnt, cm, w_ent, w_cap, occ,
-                      occs, wkey, occ, lds, res, false);
-      D1k = res[0];
-      E1k = res[1];
+    tpf_filter_unit(uo + tpf::kUnitK, po, jo, D1, E1, E0, E0k, ecnt, cm, w_ent, w_cap, occ, occs,
+                    wkey, occ, lds, res, false);
+    D1k = res[0];
+    E1k = res[1];
+  }
+  if (t == 0) {
+    if (cnt_pre) {  // the unfiltered counts (the exchange rows are sized from them)
+      int32_t* cp = cnt_pre + (int64_t)b * 4;
+      cp[0] = (int32_t)D0;
+      cp[1] = (int32_t)E0;
+      cp[2] = (int32_t)D1;
+      cp[3] = (int32_t)E1;
     }
-    if (t == 0) {
-      if (cnt_pre) {  // the unfiltered counts (the exchange rows are sized from them)
-        int32_t* cp = cnt_pre + (int64_t)b * 4;
-        cp[0] = (int32_t)D0;
-        cp[1] = (int32_t)E0;
-        cp[2] = (int32_t)D1;
-        cp[3] = (int32_t)E1;
-      }
-      co[0] = (int32_t)D0k;
-      co[1] = (int32_t)E0k;
-      co[2] = (int32_t)D1k;
-      co[3] = (int32_t)E1k;
-    }
+    co[0] = (int32_t)D0k;
+    co[1] = (int32_t)E0k;
+    co[2] = (int32_t)D1k;
+    co[3] = (int32_t)E1k;
   }
 }
 
@@ -3054,10 +3075,12 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
   auto take = [&](size_t bytes) { char* r = p; p += al16(bytes); return r; };
   uint32_t* tkeys = (uint32_t*)take((size_t)g.N * 4);
   uint16_t* toff = (uint16_t*)take((size_t)g.T * (g.nbk + 1) * 2);
-  // stage 1: the tile kernel only, 2: the bucket kernel only (a caller orders something
-  // between them: the tail filter's bucket kernels run in minibatch order), 0: both
+  // stage 1: the tile kernel only, 2: the bucket kernel only, 3: (tail filter) the filter
+  // kernel only, 4: tile + bucket -- a caller orders something between them (the tail
+  // filter's filter kernels run in minibatch order); 0: all
   const bool q = m.bits > 31;
   if (stage == 2) goto bucket;
+  if (stage == 3) goto filter;
   if (filt && q)
     tp_tile_kernel<true, true><<<(unsigned)g.T, tp::kThr, 0, st>>>(
         raw, n, m, g.shift, g.nbk, tkeys, toff, dcnt, rep, err, g.lts, ecnt);
@@ -3072,16 +3095,23 @@ void localize_tpf(const uint64_t* raw, int64_t n, KeyMix m, void* temp, size_t t
                                                               dcnt, rep, err, g.lts);
   PSAMD_HIP_CHECK(hipGetLastError());
   if (stage == 1) return;
-bucket:
-  const bool pair = tpf_pair(g);
+bucket : {
+  const int pair = tpf_pair(g) ? 1 : 0;
   if (filt)
     tpf_bucket_kernel<true><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
-        tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
-        sorted ? 1 : 0, ecnt, *filt, w_ent, w_cap, cnt_pre);
+        tkeys, toff, g.nbk, pair, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
+        sorted ? 1 : 0, ecnt);
   else
     tpf_bucket_kernel<false><<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
-        tkeys, toff, g.nbk, pair ? 1 : 0, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
-        sorted ? 1 : 0, nullptr, CmArgs{}, nullptr, 0, nullptr);
+        tkeys, toff, g.nbk, pair, (int)g.T, g.shift, uniqf, ent_pos, ent_j, cnt, err,
+        sorted ? 1 : 0, nullptr);
+  PSAMD_HIP_CHECK(hipGetLastError());
+}
+  if (stage == 2 || stage == 4 || !filt) return;
+filter:
+  if (!filt) return;
+  tpf_filter_kernel<<<(unsigned)tpf_groups_of(g), tp::kBkThr, 0, st>>>(
+      uniqf, ent_pos, ent_j, cnt, ecnt, *filt, w_ent, w_cap, cnt_pre);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

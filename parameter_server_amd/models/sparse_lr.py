@@ -303,13 +303,14 @@ class SparseLRTrainer:
         return max(1024, min(want, cap_max))
 
     # ------------------------------------------------------------------ step
-    def localize(self, keys: torch.Tensor, buf: int = 0):
+    def localize(self, keys: torch.Tensor, buf: int = 0, stage: int = 0):
         """Localise a minibatch into buffer set ``buf`` (0 or 1). Used to prefetch the
         next minibatch on a side stream while the current step waits for its
-        exchange (``step(..., loc=..., prefetch=...)``)."""
+        exchange (``step(..., loc=..., prefetch=...)``). ``stage`` (flat layout + tail
+        filter): 4 = tile + bucket, 3 = the filter (``Localizer``)."""
         while len(self._localizers) <= buf:
             self._localizers.append(self._new_localizer(self.localize_mode))
-        return self._localizers[buf](keys)
+        return self._localizers[buf](keys, stage) if stage else self._localizers[buf](keys)
 
     def _new_localizer(self, mode: str) -> Localizer:
         """A localisation workspace of this trainer (flat: with the fused tail filter)."""
@@ -593,10 +594,11 @@ class SparseLRTrainer:
         ``gate``: an event the localisation waits for after the generator (bench.py: the
         training step's fused forward/backward, so the two LDS-heavy 1024-thread kernels
         do not share the CUs). ``bucket_after`` / ``bucket_done`` (tail filter): the
-        bucket kernel (CountMin insert + query) waits for the previous minibatch's bucket
-        kernel and records its own, so sketch updates run in minibatch order while the
-        generators and tile kernels of several preparations still overlap. Returns a
-        callable -> the FlatLoc of ``buf``."""
+        filter kernel (CountMin insert + query + compaction, after the bucket kernel)
+        waits for the previous minibatch's filter kernel and records its own, so sketch
+        updates run in minibatch order while the generators, tile and bucket kernels of
+        several preparations still overlap. Returns a callable -> the FlatLoc of
+        ``buf``."""
         from ..ops.synthetic import CRITEO_1TB_CARDS, _set_cards
 
         if self.localize_mode != "tpf":
@@ -619,8 +621,8 @@ class SparseLRTrainer:
                                   f.ent_pos, f.ent_j, f.cnt, f.err, self._flat_x,
                                   filt=lz.filt_args())
         else:
-            for stage in (1, 2):
-                if stage == 2 and bucket_after is not None:
+            for stage in ((1, 2, 3) if lz.filt_args() is not None else (1, 2)):
+                if stage == 3 and bucket_after is not None:
                     plan.add_wait(bucket_after)
                 plan.add_localize_tpf(keys, n, self.bits, lz.ptemp, f.dcnt, f.rep, f.uniqf,
                                       f.ent_pos, f.ent_j, f.cnt, f.err, self._flat_x,

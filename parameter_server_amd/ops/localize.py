@@ -274,26 +274,33 @@ class Localizer:
                 int(self.err.item()):
             raise RuntimeError(f"localize_{self.mode}: a bucket or tile overflowed its LDS capacity")
 
-    def __call__(self, keys: torch.Tensor) -> Localized:
+    def __call__(self, keys: torch.Tensor, stage: int = 0) -> Localized:
+        """``stage`` (flat layout with a tail filter): 4 = tile + bucket kernels, 3 = the
+        filter kernel (a caller orders the filters of consecutive minibatches between
+        the two calls); 0 = all."""
         n = keys.numel()
         if n > self.max_nnz:
             raise ValueError(f"minibatch has {n} keys > workspace {self.max_nnz}")
         if n == 0:
             raise ValueError("empty minibatch")
+        if stage and (self.mode != "tpf" or self.tail_filter is None or stage not in (3, 4)):
+            raise ValueError("staged localisation: the flat layout with a tail filter, 4 / 3")
         if self.gpu and is_gpu(keys):
-            return self._gpu(keys.contiguous(), n)
+            return self._gpu(keys.contiguous(), n, stage)
         if self.mode == "tpf":
             raise ValueError("a flat (tpf) localiser takes GPU keys")
         return localize_torch(keys, self.bits, self.with_hess)
 
-    def _gpu(self, keys, n) -> Localized:
+    def _gpu(self, keys, n, stage=0) -> Localized:
         H = hipops()
         if self.mode == "tpf":
             f = self.flat
             H.localize_tpf(keys, self.bits, self.ptemp, f.dcnt, f.rep, f.uniqf, f.ent_pos,
-                           f.ent_j, f.cnt, f.err, self.sorted_keys, filt=self.filt_args())
-            f.nnz = n
-            f.gen += 1
+                           f.ent_j, f.cnt, f.err, self.sorted_keys, filt=self.filt_args(),
+                           stage=stage)
+            if stage != 4:  # (a new generation once the minibatch is complete)
+                f.nnz = n
+                f.gen += 1
             return f
         if self.mode == "tp":
             # the look-back's status words carry an 8-bit launch epoch: when the bucket
