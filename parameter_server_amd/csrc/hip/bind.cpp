@@ -1053,12 +1053,12 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("tpf_temp_bytes", [](int64_t n, int bits) { return psamd::tpf_temp_bytes(n, bits); });
   m.def("localize_tpf", [](Tensor keys, int bits, Tensor temp, Tensor dcnt, Tensor rep,
                            Tensor uniqf, Tensor ent_pos, Tensor ent_j, Tensor cnt, Tensor err,
-                           bool sorted, optional<py::tuple> filt) {
+                           bool sorted, optional<py::tuple> filt, int stage) {
     make_localize_tpf(keys, keys.numel(), bits, temp, dcnt, rep, uniqf, ent_pos, ent_j, cnt,
-                      err, sorted, filt)(cur_stream());
+                      err, sorted, filt, stage)(cur_stream());
   }, py::arg("keys"), py::arg("bits"), py::arg("temp"), py::arg("dcnt"), py::arg("rep"),
      py::arg("uniqf"), py::arg("ent_pos"), py::arg("ent_j"), py::arg("cnt"), py::arg("err"),
-     py::arg("sorted"), py::arg("filt") = py::none());
+     py::arg("sorted"), py::arg("filt") = py::none(), py::arg("stage") = 0);
   // ---- the padded multi-GPU exchange on the flat layout (rows as in exchange.hip)
   m.def("tpf_exchange_ok", [](int64_t n, int bits, int G) {
     return psamd::tpf_exchange_ok(n, bits, G);
