@@ -13,3 +13,5 @@ run e8tail --steps 100 --warmup 10 --emulate-peers 8 --tail-freq 1 || exit 1
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/p_tail -o run -- python $R/bench.py --steps 100 --warmup 10 --tail-freq 1 > $O/p_tail.log 2>&1 || exit 6
 python $R/scripts/kdist_db.py $O/p_tail/run_results.db 6
+cd $R
+timeout -k 10 600 python benchmarks/bench_app.py --rows 8000000 --files 8 --minibatch 65536 --io-threads 8 --report-steps 100000 > $O/app8m_norep.log 2>&1; echo "app rc=$?"; tail -1 $O/app8m_norep.log
