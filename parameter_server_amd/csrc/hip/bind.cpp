@@ -32,7 +32,7 @@ void kv_resolve_rows(void*, int64_t, const int32_t*, int, int64_t, int64_t, int,
                      uint64_t, uint64_t*, int32_t*, int, hipStream_t);
 void kv_apply_part(void*, int64_t, const int64_t*, const uint64_t*, const float*, int64_t,
                    const int32_t*, int, int64_t, int64_t, const int32_t*, int, int, int, float, float,
-                   float, float, float, float, double*, int, hipStream_t);
+                   float, float, float, float, double*, int, int, int, hipStream_t);
 // p2p.hip
 void p2p_lookup_rows(const void*, int, int, const int32_t*, int64_t, int64_t, int, float*, int64_t*,
                      int, float, float, uint64_t, int32_t*, int32_t*, hipStream_t);
@@ -139,7 +139,7 @@ void xchg_ff_pack_grads(const float*, const int32_t*, const int32_t*, int64_t, c
 void xchg_ff_decode(const int32_t*, int, int64_t, int, int64_t, int, float*, hipStream_t);
 void xchg_ff_init(int32_t*, int, int64_t, hipStream_t);
 void xchg_ff_encode(const float*, int, int64_t, int, int64_t, int, uint64_t, const int64_t*,
-                    int32_t*, hipStream_t);
+                    int32_t*, int, hipStream_t);
 void kv_gather(const void*, int64_t, const int64_t*, int64_t, const int32_t*, float*, int,
                hipStream_t);
 void kv_set(void*, int64_t, const int64_t*, int64_t, const float*, const float*, const float*,
@@ -1110,7 +1110,9 @@ PYBIND11_MODULE(_hipops, m) {
           "tpf_pack_grads: row geometry");
     check(psum.numel() >= psamd::tpf_stride(n), "tpf_pack_grads: psum < stride");
     float* gs = optr<float>(gstage, at::kFloat, "gstage");
-    if (gs) check(gstage->numel() >= G * C, "tpf_pack_grads: gstage < G * C");
+    if (gs)  // (+ 2 floats per bucket group: the workgroups' min / max partials)
+      check(gstage->numel() >= G * C + 2 * (int64_t)psamd::tpf_groups(n, bits),
+            "tpf_pack_grads: gstage < G * C + 2 * groups");
     else check(H >= 4 + C * kw + C, "tpf_pack_grads: f32 gradient rows");
     uint32_t* hp = optr<uint32_t>(hist, at::kInt, "hist");
     double* mp = optr<double>(metrics, at::kDouble, "metrics");
@@ -1390,7 +1392,8 @@ PYBIND11_MODULE(_hipops, m) {
   m.def("kv_apply_part", [](Tensor slots, Tensor slot_idx, Tensor keys, Tensor grad,
                             int64_t gstride, Tensor recv, int64_t H, int64_t C, Tensor bnd, int lgP,
                             int algo, int lr_type, double alpha, double beta, double l1, double l2,
-                            double grad_scale, double max_delta, optional<Tensor> stats) {
+                            double grad_scale, double max_delta, optional<Tensor> stats,
+                            int ff_nb, int kw) {
     const int64_t cap = slot_capacity(slots);
     chk(slot_idx, at::kLong, "slot_idx");
     chk(keys, at::kLong, "keys");
@@ -1400,7 +1403,10 @@ PYBIND11_MODULE(_hipops, m) {
     check(C > 0 && H > 4 && recv.numel() % H == 0, "bad exchange row geometry");
     const int G = (int)(recv.numel() / H);
     check(G >= 1 && G <= 64, "1..64 peers");
-    check(gstride >= C && grad.numel() >= (G - 1) * gstride + C, "grad rows out of bounds");
+    // ff_nb > 0: the gradients are the rows' FixingFloat codes (grad unused)
+    check(ff_nb >= 0 && ff_nb <= 7 && (kw == 1 || kw == 2), "kv_apply_part: ff_nb / kw");
+    if (ff_nb) check(H >= 4 + C * kw + (C * ff_nb + 3) / 4, "kv_apply_part: FixingFloat rows");
+    else check(gstride >= C && grad.numel() >= (G - 1) * gstride + C, "grad rows out of bounds");
     check(slot_idx.numel() >= G * C && keys.numel() >= G * C, "slot_idx/keys < G*C");
     check(lgP >= 0 && lgP <= 20, "lgP in 0..20");
     check(bnd.numel() >= G * ((1 << lgP) + 1), "bnd < G*(P+1)");
@@ -1410,8 +1416,13 @@ PYBIND11_MODULE(_hipops, m) {
                          reinterpret_cast<const uint64_t*>(keys.data_ptr<int64_t>()),
                          ptr<float>(grad), gstride, ptr<int32_t>(recv), G, H, C, ptr<int32_t>(bnd),
                          lgP, algo, lr_type, (float)alpha, (float)beta, (float)l1, (float)l2,
-                         (float)grad_scale, (float)max_delta, st, stripes, cur_stream());
-  });
+                         (float)grad_scale, (float)max_delta, st, stripes, ff_nb, kw,
+                         cur_stream());
+  }, py::arg("slots"), py::arg("slot_idx"), py::arg("keys"), py::arg("grad"), py::arg("gstride"),
+     py::arg("recv"), py::arg("H"), py::arg("C"), py::arg("bnd"), py::arg("lgP"), py::arg("algo"),
+     py::arg("lr_type"), py::arg("alpha"), py::arg("beta"), py::arg("l1"), py::arg("l2"),
+     py::arg("grad_scale"), py::arg("max_delta"), py::arg("stats"), py::arg("ff_nb") = 0,
+     py::arg("kw") = 1);
   // aggregated pushes of every source row in one launch; grad row s at grad[s*gstride]
   m.def("kv_accumulate_rows", [](Tensor slots, Tensor slot_idx, Tensor grad, int64_t gstride,
                                  Tensor recv, int64_t H, int64_t C, Tensor touched,
@@ -1755,7 +1766,7 @@ PYBIND11_MODULE(_hipops, m) {
     psamd::xchg_ff_init(ptr<int32_t>(send), G, H, cur_stream());
   });
   m.def("xchg_ff_encode", [](Tensor gstage, int64_t C, int kw, int64_t H, int nb, uint64_t seed,
-                             optional<Tensor> step, Tensor send) {
+                             optional<Tensor> step, Tensor send, int per) {
     chk(gstage, at::kFloat, "gstage");
     chk(send, at::kInt, "send");
     check(kw == 1 || kw == 2, "kw must be 1 or 2");
@@ -1764,9 +1775,13 @@ PYBIND11_MODULE(_hipops, m) {
           "bad exchange row geometry");
     const int G = (int)(send.numel() / H);
     check(G >= 1 && G <= 64 && gstage.numel() >= G * C, "gstage < G*C");
+    check(per >= 0 && gstage.numel() >= G * C + 2 * (int64_t)G * per,
+          "xchg_ff_encode: gstage < G*C + the producers' partials");
     psamd::xchg_ff_encode(ptr<float>(gstage), G, C, kw, H, nb, seed,
-                          optr<int64_t>(step, at::kLong, "step"), ptr<int32_t>(send), cur_stream());
-  });
+                          optr<int64_t>(step, at::kLong, "step"), ptr<int32_t>(send), per,
+                          cur_stream());
+  }, py::arg("gstage"), py::arg("C"), py::arg("kw"), py::arg("H"), py::arg("nb"), py::arg("seed"),
+     py::arg("step"), py::arg("send"), py::arg("per") = 0);
   m.def("xchg_ff_decode", [](Tensor recv, int64_t C, int kw, int64_t H, int nb, Tensor gin) {
     chk(recv, at::kInt, "recv");
     chk(gin, at::kFloat, "gin");

@@ -268,14 +268,45 @@ __global__ void xchg_ff_stage_kernel(const float* __restrict__ grad,
   }
 }
 
+// per > 0 (the flat layout's tpf_pack_grads): the row's min / max from its producer
+// workgroups' partials at gstage[G * C + 2 w] (w in [p per, (p + 1) per)), reduced by every
+// block of the row (a few hundred floats from L2), the header written by block 0; per = 0:
+// the header words as reduced by the producer's atomics (xchg_ff_stage_kernel).
 __global__ void xchg_ff_encode_kernel(const float* __restrict__ gstage, int64_t C, int kw,
                                       int64_t H, int nb, uint64_t seed,
                                       const int64_t* __restrict__ step,
-                                      int32_t* __restrict__ send) {
+                                      int32_t* __restrict__ send, int per) {
   const int p = blockIdx.y;
   int32_t* row = send + (int64_t)p * H;
   const int64_t n = dev_len(row + 1, C);
-  const float lo = ff_unord(row[2]), hi = ff_unord(row[3]) + 1e-6f;
+  float lo, hi;
+  if (per > 0) {
+    __shared__ float sl[4], sh[4];
+    const float* part = gstage + (int64_t)gridDim.y * C + 2 * (int64_t)p * per;
+    float a = 3.4e38f, z = -3.4e38f;
+    for (int w = threadIdx.x; w < per; w += blockDim.x) {
+      a = fminf(a, part[2 * w]);
+      z = fmaxf(z, part[2 * w + 1]);
+    }
+    a = wave_min(a);
+    z = wave_max(z);
+    if ((threadIdx.x & 63) == 0) {
+      sl[threadIdx.x >> 6] = a;
+      sh[threadIdx.x >> 6] = z;
+    }
+    __syncthreads();
+    a = fminf(fminf(sl[0], sl[1]), fminf(sl[2], sl[3]));
+    z = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      row[2] = ff_ord(a);
+      row[3] = ff_ord(z);
+    }
+    lo = ff_unord(ff_ord(a));
+    hi = ff_unord(ff_ord(z)) + 1e-6f;
+  } else {
+    lo = ff_unord(row[2]);
+    hi = ff_unord(row[3]) + 1e-6f;
+  }
   const double bin = (double)hi - (double)lo;
   const double ratio = (double)((1ull << (8 * nb)) - 2ull);
   const uint64_t sd = fmix64(seed ^ fmix64((step ? (uint64_t)*step : 0ull) * 0x9e3779b97f4a7c15ull +
@@ -321,7 +352,7 @@ void xchg_ff_pack_grads(const float* grad, const int32_t* perm, const int32_t* n
                                                                C, H, send, gstage);
   PSAMD_HIP_CHECK(hipGetLastError());
   dim3 grid(grid_for(C, 256, 512), G);
-  xchg_ff_encode_kernel<<<grid, 256, 0, st>>>(gstage, C, kw, H, nb, seed, step, send);
+  xchg_ff_encode_kernel<<<grid, 256, 0, st>>>(gstage, C, kw, H, nb, seed, step, send, 0);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 
@@ -332,9 +363,9 @@ void xchg_ff_init(int32_t* send, int G, int64_t H, hipStream_t st) {
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 void xchg_ff_encode(const float* gstage, int G, int64_t C, int kw, int64_t H, int nb, uint64_t seed,
-                    const int64_t* step, int32_t* send, hipStream_t st) {
+                    const int64_t* step, int32_t* send, int per, hipStream_t st) {
   dim3 grid(grid_for(C, 256, 512), G);
-  xchg_ff_encode_kernel<<<grid, 256, 0, st>>>(gstage, C, kw, H, nb, seed, step, send);
+  xchg_ff_encode_kernel<<<grid, 256, 0, st>>>(gstage, C, kw, H, nb, seed, step, send, per);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

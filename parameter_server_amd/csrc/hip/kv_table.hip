@@ -410,6 +410,10 @@ __global__ void kv_apply_rows_kernel(Slot* __restrict__ slots, int64_t cap,
 // entries of equal slot through an LDS hash, and the head of each chain applies
 // its gradients in increasing entry order (= source-rank order) to a register
 // copy of the slot: bitwise the weights of kv_apply_rows.
+// (exchange.hip ff_unord: the order-preserving int of a FixingFloat row header -> float)
+__device__ __forceinline__ float ff_unord_kv(int b) {
+  return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff);
+}
 constexpr int kApWin = 1024;   // entries per window
 constexpr int kApHash = 2048;  // LDS hash slots (power of two, >= 2 * kApWin)
 
@@ -420,7 +424,7 @@ __device__ __forceinline__ void apply_part_block(
     const uint64_t* __restrict__ keys, const float* __restrict__ grad, int64_t gstride,
     const int32_t* __restrict__ recv, int64_t H, int64_t C, int G,
     const int32_t* __restrict__ bnd, int lgP, UpdateParams p, double* __restrict__ stats,
-    int acc_stripes) {
+    int acc_stripes, int ffnb = 0, int kw = 1) {
   __shared__ uint32_t hk[kApHash];
   __shared__ int32_t hh[kApHash];
   __shared__ int32_t went[kApWin], wnx[kApWin], whs[kApWin];
@@ -430,6 +434,16 @@ __device__ __forceinline__ void apply_part_block(
   __shared__ uint64_t thr;
   const int tid = threadIdx.x, P = 1 << lgP, part = blockIdx.x;
   const int CH = max(1, kApWin / G);
+  // ffnb > 0: the pushes are FixingFloat codes in the received rows, decoded here (the
+  // math of xchg_ff_decode_kernel, bit for bit) instead of by a separate launch
+  __shared__ double flo[kMaxChain], fbin[kMaxChain];
+  const double fratio = ffnb ? (double)((1ull << (8 * ffnb)) - 2ull) : 1.0;
+  if (ffnb && tid < G) {
+    const int32_t* row = recv + (int64_t)tid * H;
+    const float lo = ff_unord_kv(row[2]), hi = ff_unord_kv(row[3]) + 1e-6f;
+    flo[tid] = lo;
+    fbin[tid] = (double)hi - (double)lo;
+  }
   if (tid < G) {
     const int32_t n = (int32_t)dev_len(recv + (int64_t)tid * H + 1, C);
     const int32_t* rb = bnd + (int64_t)tid * (P + 1);
@@ -479,7 +493,16 @@ __device__ __forceinline__ void apply_part_block(
       int32_t ent = -1;
       const uint64_t key = keys[e];  // three independent loads in flight together
       const int64_t k = slot_idx[e];
-      const float g = grad[(int64_t)s * gstride + i];
+      float g;
+      if (ffnb) {
+        const uint8_t* code =
+            reinterpret_cast<const uint8_t*>(recv + (int64_t)s * H + 4 + C * kw) + i * ffnb;
+        uint64_t r = 0;
+        for (int b = 0; b < ffnb; ++b) r |= (uint64_t)code[b] << (8 * b);
+        g = (float)((double)r / fratio * fbin[s] + flo[s]);
+      } else {
+        g = grad[(int64_t)s * gstride + i];
+      }
       if (key <= th) {
         atomicAdd(&rcnt[s], 1);
         if (in_range(k, cap) && g == g) {  // NaN mark = filtered entry
@@ -543,9 +566,9 @@ __global__ __launch_bounds__(256) void kv_apply_part_kernel(
     const uint64_t* __restrict__ keys, const float* __restrict__ grad, int64_t gstride,
     const int32_t* __restrict__ recv, int64_t H, int64_t C, int G,
     const int32_t* __restrict__ bnd, int lgP, UpdateParams p, double* __restrict__ stats,
-    int acc_stripes) {
+    int acc_stripes, int ffnb, int kw) {
   apply_part_block(slots, cap, slot_idx, keys, grad, gstride, recv, H, C, G, bnd, lgP, p, stats,
-                   acc_stripes);
+                   acc_stripes, ffnb, kw);
 }
 
 // The owner's half of one merged exchange (models/sparse_lr.py mx_exchange) in ONE
@@ -760,14 +783,15 @@ void kv_apply_part(void* slots, int64_t cap, const int64_t* slot_idx, const uint
                    const float* grad, int64_t gstride, const int32_t* recv, int G, int64_t H,
                    int64_t C, const int32_t* bnd, int lgP, int algo, int lr_type, float alpha,
                    float beta, float l1, float l2, float grad_scale, float max_delta,
-                   double* stats, int acc_stripes, hipStream_t st) {
+                   double* stats, int acc_stripes, int ffnb, int kw, hipStream_t st) {
   if (cap > (int64_t(1) << 32) - 1) throw std::runtime_error("kv_apply_part: capacity >= 2^32");
   if ((int64_t)G * C >= (int64_t(1) << 31)) throw std::runtime_error("kv_apply_part: G*C >= 2^31");
   if (G < 1 || G > kMaxChain) throw std::runtime_error("kv_apply_part: 1..64 source rows");
   if (lgP < 0 || lgP > 20) throw std::runtime_error("kv_apply_part: lgP in 0..20");
   UpdateParams p{algo, lr_type, alpha, beta, l1, l2, grad_scale, max_delta};
   kv_apply_part_kernel<<<1 << lgP, 256, 0, st>>>((Slot*)slots, cap, slot_idx, keys, grad, gstride,
-                                                 recv, H, C, G, bnd, lgP, p, stats, acc_stripes);
+                                                 recv, H, C, G, bnd, lgP, p, stats, acc_stripes,
+                                                 ffnb, kw);
   PSAMD_HIP_CHECK(hipGetLastError());
 }
 

@@ -2909,11 +2909,26 @@ tpf_pack_grads_kernel(const int32_t* __restrict__ cnt, const int32_t* __restrict
     off += D;
   }
   if (ff) {
+    // the workgroup's min / max -> its partial at gstage[G * C + 2 b] (xchg_ff_encode
+    // reduces a row's partials): per-wave atomics on the row header's two words were
+    // ~8 k device-scope atomics on 16 addresses per step, serialised across the XCDs
+    // (pack 16 -> 32 us with fixing-float at 8 emulated peers, gpurun r6u)
     lo = wave_min(lo);
     hi = wave_max(hi);
-    if (lane == 0 && lo <= hi) {
-      atomicMin(&row[2], tpf_ff_ord(lo));
-      atomicMax(&row[3], tpf_ff_ord(hi));
+    __shared__ float sl[kThr / 64], sh[kThr / 64];
+    if (lane == 0) {
+      sl[t >> 6] = lo;
+      sh[t >> 6] = hi;
+    }
+    __syncthreads();
+    if (t == 0) {
+      for (int w = 1; w < kThr / 64; ++w) {
+        lo = fminf(lo, sl[w]);
+        hi = fmaxf(hi, sh[w]);
+      }
+      float* part = gstage + (int64_t)(gridDim.x - ((hist || ovf_host) ? 1 : 0)) / per * C;
+      part[2 * b] = lo;
+      part[2 * b + 1] = hi;
     }
   }
   if (t == 0 && b % per == per - 1) row[1] = (int32_t)(off < C ? off : C);

@@ -1165,7 +1165,8 @@ class SparseLRTrainer:
         self.xc = SimpleNamespace(
             C=C, kw=kw, H=H, nb=nb, w0=w0, b0=b0, fused=fused,
             homes=self._owner_homes() if fused else None,
-            gstage=z32(G * C, torch.float32) if nb else None,
+            # (+ the flat pack's per-workgroup min / max partials: 2 per bucket group)
+            gstage=z32(G * C + 2 * 2048, torch.float32) if nb else None,
             gins=[z32(G * C, torch.float32) for _ in range(R)] if nb else None,
             # rings of R entries indexed by step: sends[j] holds grads(j) then keys(j+1+lag);
             # recvs[j] what exchange j received; slots[j] the owner's resolved slots of
@@ -1297,8 +1298,8 @@ class SparseLRTrainer:
         hh = hipops()
         hh.tpf_pack_keys(loc.nnz, loc.bits, self.G, loc.cnt, loc.uniqf, xc.C, xc.kw, xc.H,
                          xc.sends[gb], xc.ovf, homes=xc.homes, b0=xc.b0, lgP=max(xc.lgP, 0))
-        if xc.nb:  # (FixingFloat push: no pack_grads launch to carry the flag)
-            hh.xchg_publish(xc.ovf, xc.ovf_host)
+        # (the overflow flag reaches the host through tpf_pack_grads' extra workgroup,
+        # fixing-float or not)
 
     def _x_finish_flat(self, loc, labels, B: int, width: int, r: int, send=None, wsrc=None,
                        wstride: int = 0, csr=None):
@@ -1323,14 +1324,13 @@ class SparseLRTrainer:
             hh.tp_fwd_bwd(loc.rep, loc.dcnt, None, n, width, None, loc.w_ent, labels, B,
                           loss_id(self.cfg.loss), coef, self.metrics, self.hist, AUC_BINS,
                           loc.psum, None, None, None, None, False)
-        if xc.nb:
-            hh.xchg_ff_init(send, xc.H)
         hh.tpf_pack_grads(n, bits, G, loc.cnt, loc.ent_pos, loc.ent_j, xc.C, xc.kw, xc.H,
                           loc.psum, send, xc.gstage if xc.nb else None, self.hist, self.metrics,
-                          self.step_dev, xc.ovf, None if xc.nb else xc.ovf_host)
+                          self.step_dev, xc.ovf, xc.ovf_host)
         if xc.nb:
             seed = (self.cfg.seed * 7919 + 17) & ((1 << 64) - 1)
-            hh.xchg_ff_encode(xc.gstage, xc.C, xc.kw, xc.H, xc.nb, seed, self.step_dev, send)
+            hh.xchg_ff_encode(xc.gstage, xc.C, xc.kw, xc.H, xc.nb, seed, self.step_dev, send,
+                              per=hh.tpf_groups(n, bits) // G)  # (the pack's partials)
 
     def _x_poll_overflow(self):
         """Raise at the first step whose exchange dropped keys (the device counter is
@@ -1362,8 +1362,14 @@ class SparseLRTrainer:
         xc, G, H, C = self.xc, self.G, self.xc.H, self.xc.C
         pslot, recv = xc.slots[gb], xc.recvs[r]
         if self.gpu:
-            gsrc, gstride = self._x_grads(r)
             hh = hipops()
+            if xc.nb and self.cfg.push_mode != "aggregate" and xc.bnd is not None:
+                # FixingFloat codes decoded inside the apply (no decode launch)
+                hh.kv_apply_part(self.table.slots, pslot, xc.pkeys[gb], xc.gins[r], C, recv, H,
+                                 C, xc.bnd[gb], xc.lgP, *self.rule.args(), self.stats,
+                                 ff_nb=xc.nb, kw=xc.kw)
+                return
+            gsrc, gstride = self._x_grads(r)
             if self.cfg.push_mode == "aggregate":
                 xc.n_touched.zero_()
                 hh.kv_accumulate_rows(self.table.slots, pslot, gsrc, gstride, recv, H, C,
