@@ -415,6 +415,7 @@ __device__ __forceinline__ float ff_unord_kv(int b) {
   return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff);
 }
 constexpr int kApWin = 1024;   // entries per window
+constexpr int kApRun = 16;     // a chain up to this long is ordered in LDS
 constexpr int kApHash = 2048;  // LDS hash slots (power of two, >= 2 * kApWin)
 
 // The body of kv_apply_part_kernel for partition blockIdx.x (also the apply half of
@@ -429,6 +430,7 @@ __device__ __forceinline__ void apply_part_block(
   __shared__ int32_t hh[kApHash];
   __shared__ int32_t went[kApWin], wnx[kApWin], whs[kApWin];
   __shared__ float wg[kApWin];
+  __shared__ int32_t wrun[256 * kApRun];  // per-thread chain runs (blockDim 256)
   __shared__ int32_t ra[kMaxChain], re[kMaxChain], roff[kMaxChain + 1], rcnt[kMaxChain];
   __shared__ uint64_t thk[kMaxChain];
   __shared__ uint64_t thr;
@@ -524,22 +526,46 @@ __device__ __forceinline__ void apply_part_block(
     __syncthreads();
     for (int w = tid; w < tot; w += blockDim.x) {
       if (went[w] < 0 || hh[whs[w]] != w) continue;  // not the head of its chain
-      int len = 0;
-      for (int c = w; c >= 0 && len < kMaxChain; c = wnx[c]) ++len;
       const int64_t k = (int64_t)hk[whs[w]];
-      Slot sl = slots[k];
-      int32_t last = -1;
-      for (int it = 0; it < len; ++it) {  // next entry in increasing (source) order
-        int32_t best = INT32_MAX, bw = -1, walked = 0;
-        for (int c = w; c >= 0 && walked < len; c = wnx[c], ++walked)
-          if (went[c] > last && went[c] < best) { best = went[c]; bw = c; }
-        if (bw < 0) break;
-        const float w_old = apply_update(sl, wg[bw] * p.grad_scale, p);
-        dnnz += (double)((sl.w != 0.f) - (w_old != 0.f));
-        wsum += (double)sl.w * sl.w;
-        const double d = (double)sl.w - w_old;
-        dsum += d * d;
-        last = best;
+      Slot sl = slots[k];  // (the slot's load in flight while the chain is ordered)
+      // the chain (keys shared by several source rows: hot features) into this thread's
+      // LDS run, insertion-sorted by entry (= source-rank) order: one pointer chase and
+      // ~len^2 / 4 compares, instead of a full chain walk per applied entry (len^2
+      // dependent LDS reads: 64 for a key in all 8 rows of an 8-peer exchange)
+      int32_t* run = wrun + tid * kApRun;
+      int len = 0;
+      int c = w;
+      for (; c >= 0 && len < kApRun; c = wnx[c]) {
+        const int32_t e = went[c];
+        int q = len++;
+        for (; q > 0 && went[run[q - 1]] > e; --q) run[q] = run[q - 1];
+        run[q] = c;
+      }
+      if (c < 0) {
+        for (int it = 0; it < len; ++it) {
+          const int bw = run[it];
+          const float w_old = apply_update(sl, wg[bw] * p.grad_scale, p);
+          dnnz += (double)((sl.w != 0.f) - (w_old != 0.f));
+          wsum += (double)sl.w * sl.w;
+          const double d = (double)sl.w - w_old;
+          dsum += d * d;
+        }
+      } else {  // (a longer chain: the selection walk)
+        len = 0;
+        for (int cc = w; cc >= 0 && len < kMaxChain; cc = wnx[cc]) ++len;
+        int32_t last = -1;
+        for (int it = 0; it < len; ++it) {  // next entry in increasing (source) order
+          int32_t best = INT32_MAX, bw = -1, walked = 0;
+          for (int cc = w; cc >= 0 && walked < len; cc = wnx[cc], ++walked)
+            if (went[cc] > last && went[cc] < best) { best = went[cc]; bw = cc; }
+          if (bw < 0) break;
+          const float w_old = apply_update(sl, wg[bw] * p.grad_scale, p);
+          dnnz += (double)((sl.w != 0.f) - (w_old != 0.f));
+          wsum += (double)sl.w * sl.w;
+          const double d = (double)sl.w - w_old;
+          dsum += d * d;
+          last = best;
+        }
       }
       slots[k] = sl;
     }
