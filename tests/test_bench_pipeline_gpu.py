@@ -168,7 +168,7 @@ def _g2_parity_main(env: str):
                       "maxdiff": float((pw[pos] - rw).abs().max())}), flush=True)
 
 
-@pytest.mark.parametrize("g2,tail", [("0", "0"), ("1", "0"), ("1", "1")])
+@pytest.mark.parametrize("g2,tail", [("0", "0"), ("1", "0"), ("0", "1"), ("1", "1")])
 def test_merged_native_rccl_pipeline_matches_sequential(g2, tail):
     """The merged pipeline's native iteration on a real (1-rank RCCL) communicator, with
     the event ops as host calls (launch lists) or as event nodes inside two graph chains
