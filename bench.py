@@ -585,11 +585,18 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
 
     def prep(b, part=0):
         """part 0: generate + localise; (tail filter) 1: generate + tile + bucket, 2: the
-        filter kernel (ordered across minibatches by the caller)"""
+        filter kernel (ordered across minibatches by the caller); 3: generate only, 4: the
+        localisation only (tile + bucket with the tail filter, else all of it)"""
         sidx = b % nprep
         k, lab = bufs[b]
         if part == 2:
             locs[b] = tr.localize(k, buf=b, stage=3)
+            return
+        if part == 4:
+            if fchain:
+                tr.localize(k, buf=b, stage=4)
+            else:
+                locs[b] = tr.localize(k, buf=b)
             return
         if mode["capture"]:
             # buffer b reads cursor word (b // nprep) % 2 of its stream and writes the
@@ -602,6 +609,8 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
             criteo_batch(B, seed=seed, row0=(hctr[sidx] * nprep + sidx) * B, num_features=N,
                          device=device, keys=k, labels=lab)
             hctr[sidx] += 1
+        if part == 3:
+            return
         if part == 1:
             tr.localize(k, buf=b, stage=4)
         else:
@@ -858,6 +867,10 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
         # them, instead of 6 graph launches + 11 host event calls
         # (benchmarks/probe_graph_events.py)
         Eg = P * -(-8 // P)
+        # (PSAMD_MX_TILE_GATE=1: the 1-GPU tile gate here too -- measured SLOWER at 8 emulated
+        # peers, 0.1196 vs 0.1011-0.1021 ms, config 4 0.1245 vs 0.1020: the merged
+        # iteration's preparation has no slack to wait for the worker, gpurun r6y)
+        tgate = os.environ.get("PSAMD_MX_TILE_GATE", "0") == "1"
         evg = {k: [torch.cuda.Event() for _ in range(Eg)] for k in ("w", "M", "res", "app")}
         evp = [torch.cuda.Event() for _ in range(NB)]
         for e in [x for k in evg for x in evg[k]] + evp:
@@ -887,7 +900,19 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
             parts = tr.mx_exchange(s, locs[(s + 1) % NB])
             cs = H.GraphChain()
             cs.add_wait(evg["w"][(t + nprep - NB) % Eg])
-            if fchain:  # (the filters in minibatch order)
+            if tgate:
+                # the localisation of minibatch t + nprep waits for worker t (its fused
+                # forward / backward): the 1024-thread tile kernel and the forward /
+                # backward then do not split the CUs (the 1-GPU pipeline's tile gate)
+                cs.add_child(piece(lambda nb=nb: prep(nb, 3)))
+                cs.add_wait(evg["w"][t % Eg])
+                cs.add_child(piece(lambda nb=nb: prep(nb, 4)))
+                if fchain:
+                    cs.add_wait(evp[(nb - 1) % NB])
+                    cs.add_child(piece(lambda nb=nb: prep(nb, 2)))
+                    cs.add_record(evp[nb])
+                cs.add_child(piece(parts["pack"]))
+            elif fchain:  # (the filters in minibatch order)
                 cs.add_child(piece(lambda nb=nb: prep(nb, 1)))
                 cs.add_wait(evp[(nb - 1) % NB])
                 cs.add_child(piece(lambda nb=nb: prep(nb, 2)))
