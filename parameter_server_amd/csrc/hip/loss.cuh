@@ -50,6 +50,9 @@ __device__ __forceinline__ int auc_bin(float m, float label, int nbins) {
 // Resets the histogram (so the next step starts clean inside a captured graph).
 // Run by ONE whole 256-thread block (auc_from_hist_kernel, or block 0 of the KV update
 // that follows the fused forward: one launch less per step).
+// kBatch: stripes loaded per round (2 halves the dependent round trips for +16 VGPRs in
+// this block; measured neutral in tpf_step / tpf_pack_grads, gpurun r6z: 1 everywhere)
+template <int kBatch = 1>
 __device__ __forceinline__ void auc_hist_block(uint32_t* __restrict__ hist, int nbins,
                                                int hist_stripes, double* __restrict__ metrics,
                                                int64_t* __restrict__ step_counter) {
@@ -65,7 +68,6 @@ __device__ __forceinline__ void auc_hist_block(uint32_t* __restrict__ hist, int 
   // ms, within run-to-run noise): the update is bound by its random slot lines.
   constexpr int kPer = 8;  // nbins == 256 * kPer (AUC_BINS = 2048), checked on the host
   constexpr int kMaxStripes = 8;
-  constexpr int kBatch = 1;
   __shared__ unsigned long long s_w[3][4];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;  // blockDim.x == 256
   const int lo = t * kPer;
