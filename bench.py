@@ -671,7 +671,10 @@ def pipeline_merged(tr, B, N, seed, keys, labels, device, args, nprep=3, watch=N
 
     state = {"t": 0}
     # (tail filter on the flat layout: the filter kernels of consecutive minibatches in
-    # minibatch order; elsewhere the sketch is updated by the worker, on the main stream)
+    # minibatch order. On the compact layout the sketch is updated by the key pack of
+    # each exchange (sparse_lr._tail_filter, global CountMin atomics): those packs run on
+    # the preparation streams unordered here, so a query may already see the next
+    # minibatch's inserts -- the trainer's sequential step() keeps the exact order)
     fchain = tr.filter is not None and tr.localize_mode == "tpf"
 
     def iterate():
