@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 6: final-tree GPU suite + smoke + driver-shape bench x3
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/r6x; mkdir -p $O
+O=gpurun_out/${RUN_TAG:-r6x}; mkdir -p $O
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 $O/pytest_gpu.log; grep FAILED $O/pytest_gpu.log | head -5; [ $rc -eq 0 ] || exit $rc
