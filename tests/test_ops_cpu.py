@@ -95,12 +95,15 @@ def test_countmin_partitioned_regions_and_saturation():
 
     bits = 24
     cm = CountMinSketch(1 << 16, 3, key_bits=bits)
-    assert cm.rsize % 4 == 0 and cm.rsize << cm.lgR == cm.n and cm.rshift == bits - 11
+    assert cm.rsize % 64 == 0 and cm.rsize << cm.lgR == cm.n and cm.rshift == bits - 11
     g = torch.Generator().manual_seed(3)
     keys = torch.randint(0, 1 << bits, (5000,), dtype=torch.int64, generator=g)
     cells = cm._cells_of(keys)
     region = keys >> cm.rshift
     assert bool(((cells // cm.rsize) == region[:, None]).all())
+    # blocked: a key's k cells are distinct and share one 64-cell block (one cache line)
+    assert bool((cells // 64 == cells[:, :1] // 64).all())
+    assert bool((cells[:, 0] != cells[:, 1]).all() & (cells[:, 1] != cells[:, 2]).all())
     h = sketch_hash_torch(keys[:50])
     assert h.tolist() == [core().sketch_hash(int(k)) for k in keys[:50]]
     for _ in range(3):
@@ -153,3 +156,16 @@ def test_exact_auc():
     s = torch.tensor([0.1, 0.4, 0.35, 0.8])
     y = torch.tensor([-1.0, -1.0, 1.0, 1.0])
     assert abs(exact_auc(s, y) - 0.75) < 1e-9
+
+
+def test_staged_localisation_needs_the_flat_tail_filter():
+    """Localizer(keys, stage): the tile + bucket / filter split exists only for the flat
+    layout with a tail filter; anything else is refused loudly."""
+    from parameter_server_amd.ops.localize import Localizer
+
+    lz = Localizer(1000, 20, "cpu", mode="sort")
+    keys = torch.randint(0, 1 << 20, (500,), dtype=torch.int64)
+    lz(keys)  # (stage 0: fine)
+    for stage in (3, 4):
+        with pytest.raises(ValueError, match="staged localisation"):
+            lz(keys, stage)
