@@ -176,7 +176,9 @@ async_sgd {{ algo: FTRL minibatch: {a.minibatch} num_data_pass: 1 report_interva
                      "examples_per_s": res["examples"] / res["seconds"],
                      "h2d_gb_per_s": res["h2d_bytes"] / res["seconds"] / 1e9,
                      "loss": res["progress"]["loss"] if res["progress"] else None,
-                     "localize": tr.localize_mode, "flat": tr._compact is None})
+                     "localize": tr.localize_mode, "flat": tr._compact is None,
+                     "host_feed_wait_s": round(res.get("host_feed_wait_s", 0.0), 4),
+                     "host_step_issue_s": round(res.get("host_step_issue_s", 0.0), 4)})
         if a.cache and r == 1:
             runs.append(_breakdown(tr, d, a, res["steps"], cache))
         del tr, res

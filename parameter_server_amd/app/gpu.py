@@ -121,6 +121,7 @@ def run_async_sgd(lm, comm, device, flags, printer=None) -> dict:
     printer = printer or (ProgressPrinter() if rank == 0 and not flags.quiet else None)
     t0 = last = time.time()
     steps = idle = 0
+    t_feed = t_step = 0.0  # host seconds waiting for minibatches / issuing steps
     last_p = None
     agreed = []  # per pass: the agreed step count, or None (agreement every step)
     for ps in range(feeder.passes):
@@ -143,10 +144,14 @@ def run_async_sgd(lm, comm, device, flags, printer=None) -> dict:
             if total is not None:
                 if t >= total:
                     break
+                tf = time.perf_counter()
                 b = next(it, None)
+                t_feed += time.perf_counter() - tf
                 report = (t + 1) % every == 0
             else:
+                tf = time.perf_counter()
                 b = next(it, None)
+                t_feed += time.perf_counter() - tf
                 report = time.time() - last >= interval
                 if G > 1:  # (host channel: every rank steps, reports and stops together)
                     st = comm.host_gather_obj((b is not None, report))
@@ -160,12 +165,14 @@ def run_async_sgd(lm, comm, device, flags, printer=None) -> dict:
                 tr.idle_step()  # out of files: keep serving this shard and flushing pushes
                 idle += 1
             else:
+                ts = time.perf_counter()
                 if b.vals is None and b.width:  # one width, binary: the fused fixed-width path
                     tr.step(b.keys, b.labels, width=b.width)
                 else:
                     tr.step(b.keys, b.labels, width=b.width or None, row_ptr=b.row_ptr,
                             vals=b.vals)
                 feeder.release(b)
+                t_step += time.perf_counter() - ts
                 steps += 1
             if report:
                 last = time.time()
@@ -184,7 +191,7 @@ def run_async_sgd(lm, comm, device, flags, printer=None) -> dict:
     out = {"examples": feeder.num_examples, "steps": steps, "idle_steps": idle, "seconds": dt,
            "progress": p if p["examples"] else last_p, "trainer": tr, "h2d_bytes": feeder.bytes_h2d,
            "text_passes": feeder.text_passes, "cached_passes": feeder.cached_passes,
-           "agreed_steps": agreed}
+           "agreed_steps": agreed, "host_feed_wait_s": t_feed, "host_step_issue_s": t_step}
     if tmp_cache:
         import shutil
 
