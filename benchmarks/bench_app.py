@@ -129,7 +129,7 @@ def main():
     ap.add_argument("--cache", type=int, default=1,
                     help="1: run twice with a binary example cache (the first run parses the "
                          "text and writes the cache, the second streams the cache)")
-    ap.add_argument("--io-threads", type=int, default=4)
+    ap.add_argument("--io-threads", type=int, default=16)
     ap.add_argument("--report-steps", type=int, default=0,
                     help="progress line every this many steps on cached passes (0: 10 per pass)")
     a = ap.parse_args()

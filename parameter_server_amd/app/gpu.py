@@ -54,7 +54,10 @@ def _flags(argv):
     # binary example cache (data/bincache.py): "" = $PSAMD_DATA_CACHE, else a private
     # temporary one when num_data_pass > 1; "off" = parse the text on every pass
     ap.add_argument("-data_cache", "--data_cache", default="")
-    ap.add_argument("-io_threads", "--io_threads", type=int, default=4)
+    # cached-pass reader threads (pread -> pinned slots): the cached pass waits on them
+    # (Criteo-shaped 8 M rows, B = 65,536: 8 threads 52-64 M ex/s, 16 threads 86 M,
+    # profiles/r6_app_cache.log)
+    ap.add_argument("-io_threads", "--io_threads", type=int, default=16)
     # progress lines every this many steps when the step count is agreed up front (a
     # fully cached multi-rank run); 0 = 20 lines per run
     ap.add_argument("-report_steps", "--report_steps", type=int, default=0)
@@ -116,7 +119,7 @@ def run_async_sgd(lm, comm, device, flags, printer=None) -> dict:
                           ignore_slot=True,
                           hadoop_home=td.hdfs.home if td.has("hdfs") else "",
                           max_lines_per_file=td.max_num_lines_per_file,
-                          cache_dir=cache_dir, io_threads=getattr(flags, "io_threads", 4))
+                          cache_dir=cache_dir, io_threads=getattr(flags, "io_threads", 16))
     interval = max(1, int(sgd.report_interval))
     printer = printer or (ProgressPrinter() if rank == 0 and not flags.quiet else None)
     t0 = last = time.time()
