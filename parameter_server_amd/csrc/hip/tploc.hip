@@ -1863,7 +1863,8 @@ struct CmStage {
 };
 
 __device__ __forceinline__ void cm_stage_begin(const uint64_t* __restrict__ uo, uint32_t D,
-                                               const CmArgs& cm, uint32_t* wkey, CmStage& st) {
+                                               const CmArgs& cm, uint32_t* wkey, CmStage& st,
+                                               uint32_t* occ_packed) {
   using namespace tp;
   constexpr int kQ = CmStage::kQ;
   const int t = threadIdx.x;
@@ -1873,7 +1874,10 @@ __device__ __forceinline__ void cm_stage_begin(const uint64_t* __restrict__ uo, 
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     const uint32_t j = q * kBkThr + t;
-    k[q] = uo[j < D ? j : 0] & kUoKey;  // (D >= 1 here; clamped, unconditional loads)
+    const uint64_t raw = uo[j < D ? j : 0];  // (D >= 1 here; clamped, unconditional loads)
+    k[q] = raw & kUoKey;
+    // (packed unit: the key's occurrence count rides in the top byte -- no second pass)
+    if (occ_packed && j < D) occ_packed[j] = (uint32_t)(raw >> 56);
     st.valid |= (j < D ? 1u : 0u) << q;
   }
   cm_cells_batch<kQ>(cm, k, st.cell);
@@ -1983,11 +1987,11 @@ __device__ __forceinline__ void tpf_filter_unit(uint64_t* __restrict__ uo, int32
   __syncthreads();
   CmStage st;
   const bool stage = staged && D > 0;
-  if (stage) cm_stage_begin(uo, D, cm, wkey, st);
+  if (stage) cm_stage_begin(uo, D, cm, wkey, st, packed ? occ : nullptr);
   // occurrences per key: from the keys' top byte (packed: the LDS build summed them), or
   // 4 entries per thread per round, every load of a round in flight (clamped addresses,
   // selects afterwards)
-  if (packed) {
+  if (packed && !stage) {
     for (uint32_t j = t; j < D; j += kBkThr) occ[j] = (uint32_t)(uo[j] >> 56);
   }
   for (uint32_t c0 = 0; c0 < (packed ? 0u : E); c0 += kBkThr * 4) {
