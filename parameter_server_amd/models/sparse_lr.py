@@ -1338,7 +1338,15 @@ class SparseLRTrainer:
         GPU the check sees a pack that has completed, at most the pipeline depth
         behind). Dropped keys would have been pulled as 0 and their pushes lost."""
         xc = self.xc
-        ovf = int(xc.ovf_host[0]) if xc.ovf_host is not None else int(xc.ovf.item())
+        if xc.ovf_host is not None:
+            # (a cached numpy view of the pinned word: ~0.1 us, vs a few us for a tensor
+            # index, on the per-step host path of the merged pipelines)
+            npv = getattr(xc, "ovf_np", None)
+            if npv is None:
+                npv = xc.ovf_np = xc.ovf_host.numpy()
+            ovf = int(npv[0])
+        else:
+            ovf = int(xc.ovf.item())
         if ovf:
             raise RuntimeError(
                 f"padded exchange overflow at step {self.step_count}: {ovf} keys exceeded the "
